@@ -1,0 +1,125 @@
+/* ksg.h — C ABI of the MI355X scheduling-cycle engine (drop-in boundary).
+ *
+ * This is the surface a cgo package behind the simulator's debuggable scheduler
+ * binds.  It replaces, for the hot-path plugins
+ * (NodeResourcesFit, NodeResourcesBalancedAllocation, TaintToleration,
+ * NodeAffinity, PodTopologySpread, InterPodAffinity), the per-(pod, node)
+ * plugin calls the framework makes through the simulator's wrapper:
+ *
+ *   PreFilter        simulator/scheduler/plugin/wrappedplugin.go:504
+ *   Filter           wrappedplugin.go:535   (interface pinned: plugin/mock/framework.go:114)
+ *   PreScore         wrappedplugin.go:472   (mock :233)
+ *   Score            wrappedplugin.go:433   (mock :285)
+ *   NormalizeScore   wrappedplugin.go:400   (mock :338, ScoreExtensions :300)
+ *   Reserve          wrappedplugin.go:631   (mock :597)  -> assume delta on the device
+ *   selectHost       upstream schedule_one.go (seeded deterministic tie-break)
+ * and renders the result store's annotations (resultstore/store.go:133-198) for
+ * the evaluated pod, so filter-result / score-result / finalscore-result /
+ * selected-node are byte-identical to what the wrapper records.
+ *
+ * Objects cross the boundary as Kubernetes JSON (what json.Marshal of a *v1.Pod /
+ * *v1.Node produces); the library interns them into the device SoA snapshot.
+ * Conventions: every function returns 0 on success and a negative KSG_E* code on
+ * failure (message in ksg_last_error); no exceptions or aborts cross the ABI;
+ * output buffers are caller-owned; one context per scheduler profile and GPU;
+ * calls on one context must be serialised by the caller.
+ */
+#ifndef KSG_H_
+#define KSG_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KSG_ABI_VERSION 1
+
+#define KSG_OK 0
+#define KSG_E_INVALID (-1)   /* bad argument / JSON */
+#define KSG_E_DEVICE (-2)    /* HIP error */
+#define KSG_E_STATE (-3)     /* call out of order */
+#define KSG_E_RANGE (-4)     /* index out of range */
+#define KSG_E_NOBUF (-5)     /* output buffer too small (*len holds the size) */
+
+/* plugin ids (profile positions are reported in this order of the profile) */
+#define KSG_PLUGIN_NODE_RESOURCES_FIT 0
+#define KSG_PLUGIN_NODE_RESOURCES_BALANCED_ALLOCATION 1
+#define KSG_PLUGIN_TAINT_TOLERATION 2
+#define KSG_PLUGIN_NODE_AFFINITY 3
+#define KSG_PLUGIN_POD_TOPOLOGY_SPREAD 4
+#define KSG_PLUGIN_INTER_POD_AFFINITY 5
+
+/* ksg_pod_result.status */
+#define KSG_SCHEDULED 0
+#define KSG_UNSCHEDULABLE 1
+#define KSG_ERROR 2
+
+/* filter code per (pod, node): see ksg_filter_codes */
+#define KSG_FILTER_PASSED 0xFFFFFFFFu
+#define KSG_FILTER_NOT_EVALUATED 0xFFFFFFFEu
+
+typedef struct ksg_ctx ksg_ctx;
+
+typedef struct ksg_opts {
+  int32_t device;        /* HIP device ordinal */
+  void* stream;          /* hipStream_t to run on; NULL = library-owned stream */
+  uint32_t shard_rank;   /* node sharding across GPUs: this context owns nodes   */
+  uint32_t shard_count;  /* [rank*N/count, (rank+1)*N/count) of the cluster      */
+  uint32_t flags;        /* reserved, 0 */
+} ksg_opts;
+
+typedef struct ksg_pod_result {
+  int32_t selected;      /* global node index, -1 when none */
+  int32_t feasible;      /* nodes that passed every filter plugin */
+  int32_t status;        /* KSG_SCHEDULED / KSG_UNSCHEDULABLE / KSG_ERROR */
+  uint32_t skip_filter;  /* bit i: plugin id i returned Skip from PreFilter */
+  uint32_t skip_score;   /* bit i: plugin id i returned Skip from PreScore */
+  int32_t total;         /* weighted score of the selected node */
+} ksg_pod_result;
+
+/* Profile JSON: {"plugins": [names in MultiPoint order], "weights": {name: w},
+ * "storeWeights": {name: w}, "pluginConfig": {name: args}, "seed": n}
+ * (the shape of KubeSchedulerConfiguration.profiles[0] restricted to the hot path;
+ * storeWeights is the result store's map, plugins.go:289-304). */
+int ksg_create(const char* profile_json, size_t len, const ksg_opts* opts, ksg_ctx** out);
+void ksg_destroy(ksg_ctx* ctx);
+const char* ksg_last_error(const ksg_ctx* ctx);
+int ksg_abi_version(void);
+
+/* Snapshot: {"nodes": [v1.Node], "pods": [bound v1.Pod], "queue": [v1.Pod]} .
+ * Replaces the device snapshot (UpdateSnapshot) and the queue. */
+int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len);
+int ksg_num_nodes(const ksg_ctx* ctx);     /* global node count */
+int ksg_queue_len(const ksg_ctx* ctx);
+
+/* Queue mode: schedule queue pods [first, first+count) back to back on the
+ * device; every selection is assumed on the device before the next pod
+ * (no host round trip per pod).  Asynchronous: ksg_wait() completes it. */
+int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count);
+int ksg_wait(ksg_ctx* ctx, float* device_ms);
+int ksg_pod_results(ksg_ctx* ctx, uint32_t first, uint32_t count, ksg_pod_result* out);
+
+/* Keep per-(pod, node) outputs for queue pods [first, first+count) (tests,
+ * annotation rendering).  Must precede ksg_schedule_queue. */
+int ksg_keep_outputs(ksg_ctx* ctx, uint32_t first, uint32_t count);
+/* Filter code per local node: KSG_FILTER_PASSED, KSG_FILTER_NOT_EVALUATED or
+ * (profile position << 24) | detail. */
+int ksg_filter_codes(ksg_ctx* ctx, uint32_t q, uint32_t* out, uint32_t n);
+/* Raw Score of profile position pos per local node (valid where the filter passed). */
+int ksg_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* out, uint32_t n);
+/* Store.GetStoredResult for queue pod q as a JSON object {annotation key: value}. */
+int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len);
+
+/* Drop-in cycle: schedule one more pod (appended to the queue) and, when
+ * commit != 0, assume it on the selected node (Reserve). */
+int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_pod_result* out);
+
+/* Device node rows (assume parity): requested [n_res][n], pod count [n]. */
+int ksg_node_requested(ksg_ctx* ctx, int64_t* requested, int32_t* pod_count, uint32_t n_res, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KSG_H_ */

@@ -1,0 +1,114 @@
+// Engine: device-resident node snapshot + existing-pod table + the per-pod
+// scheduling-cycle kernels.  Host-side C++ (host.cpp) owns the object model,
+// interning and rendering; it talks to the engine only through this class.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "ksg_types.h"
+
+namespace ksg {
+
+struct EngineConfig {
+  int device = 0;
+  void* stream = nullptr;  // hipStream_t (nullptr: engine creates its own)
+  int n_plugins = 0;
+  int plugins[KSG_MAX_PLUGINS] = {};         // KP_* in MultiPoint (profile) order
+  int64_t weight[KSG_MAX_PLUGINS] = {};      // framework score weights per profile position
+  int fit_strategy = 0;                      // 0 LeastAllocated 1 MostAllocated 2 RequestedToCapacityRatio
+  int fit_n = 2;
+  int fit_res[KSG_MAX_SCORE_RES] = {0, 1};
+  int64_t fit_w[KSG_MAX_SCORE_RES] = {1, 1};
+  int rtc_n = 0;
+  int64_t rtc_util[KSG_MAX_RTC] = {};
+  int64_t rtc_score[KSG_MAX_RTC] = {};
+  int ba_n = 2;
+  int ba_res[KSG_MAX_SCORE_RES] = {0, 1};
+  int64_t ipa_hard_weight = 1;
+  int ipa_ignore_existing_pref = 0;
+  uint64_t seed = 0;
+  uint32_t global_node_offset = 0;  // shard: global index of local node 0
+};
+
+// Host-side SoA image of the node snapshot (one shard).
+struct NodeSoA {
+  uint32_t n = 0, n_res = 3, n_keys = 0;
+  uint32_t global_offset = 0;             // global index of local node 0 (sharding)
+  std::vector<int64_t> alloc, requested;  // [n_res][n]
+  std::vector<int64_t> nz_cpu, nz_mem;    // [n]
+  std::vector<int32_t> allowed_pods, pod_count;
+  std::vector<int32_t> label_vid;         // [n_keys][n]
+  std::vector<uint32_t> taint_off;        // [n+1]
+  std::vector<int32_t> taint_id;
+  std::vector<uint8_t> has_labels;        // [n]
+  // node-label vocabulary numeric view (Gt/Lt): per key offset into value tables
+  std::vector<uint32_t> key_val_off;      // [n_keys+1]
+  std::vector<int64_t> val_num;
+  std::vector<uint8_t> val_num_ok;
+  // topology slots: node label key per slot and value count
+  std::vector<int32_t> topo_key;
+  std::vector<uint32_t> topo_base, topo_count;
+  uint32_t topo_pairs = 0;
+};
+
+// Existing pods (bound) on this shard's nodes, and their (anti)affinity terms.
+struct PodTableSoA {
+  uint32_t n = 0, n_keys = 0;
+  std::vector<int32_t> node, ns;
+  std::vector<uint32_t> flags;     // KEF_*
+  std::vector<int32_t> label_vid;  // [n_keys][cap] (cap == n on upload)
+  std::vector<ksg_exist_term> terms;
+  std::vector<int32_t> term_pod;
+  std::vector<ksg_req> reqs;
+  std::vector<int32_t> vals;
+};
+
+struct PodOutputs {  // per-pair outputs of one pod, host copies
+  std::vector<uint32_t> filter;  // [n]
+  std::vector<int32_t> score;    // [n_plugins][n]
+  std::vector<int32_t> total;    // [n]
+  ksg_pod_summary summary;
+};
+
+class Engine {
+ public:
+  Engine();
+  ~Engine();
+  bool init(const EngineConfig& cfg, std::string& err);
+  // capacities: pods/terms/reqs/vals of the existing-pod table (device appends on assume)
+  bool upload(const NodeSoA& nodes, const PodTableSoA& pods, uint32_t pod_cap, uint32_t term_cap,
+              uint32_t req_cap, uint32_t val_cap, std::string& err);
+  // Queue programs: blobs laid out by the host encoder (ksg_prog + pools).
+  bool set_programs(const std::vector<std::vector<uint8_t>>& progs, std::string& err);
+  // Run pods [first, first+count) of the program list back to back on the device
+  // (device-side assume).  keep: store per-pair outputs for pods [keep_first, keep_first+keep_n).
+  bool run_queue(uint32_t first, uint32_t count, bool commit, std::string& err);
+  bool keep_outputs(uint32_t keep_first, uint32_t keep_n, std::string& err);
+  bool summaries(uint32_t first, uint32_t count, ksg_pod_summary* out, std::string& err);
+  bool outputs(uint32_t prog_idx, PodOutputs& out, std::string& err);
+  bool sync(std::string& err);
+  // Read back the node resource rows (parity tests of the assume delta).
+  bool read_requested(std::vector<int64_t>& requested, std::vector<int32_t>& pod_count, std::string& err);
+  uint32_t n_nodes() const;
+  void* stream() const;
+  // timing of the last run_queue (device events), ms
+  float last_ms() const;
+  // per-kernel launch records for roofline accounting
+  struct KernelStat {
+    const char* name;
+    double bytes;   // algorithmic bytes per launch
+    uint32_t launches;
+  };
+  std::vector<KernelStat> kernel_stats() const;
+
+  struct Impl;
+  Impl* impl() { return p_; }
+
+ private:
+  Impl* p_;
+};
+
+}  // namespace ksg

@@ -1,0 +1,1295 @@
+// HIP engine for the scheduling-cycle hot path (gfx950 / MI355X).
+//
+// One scheduling cycle of one pod = the reference's schedulePod
+// (findNodesThatFitPod -> prioritizeNodes -> selectHost) plus the assume of
+// scheduleOne, restated as a short chain of kernels over the device-resident
+// node snapshot (SoA, one thread per node, coalesced columns):
+//
+//   k_begin        zero the per-pod topology histograms            (PTS/IPA only)
+//   k_scan_pods    existing pods  x incoming selectors/terms       (PTS/IPA only)
+//   k_scan_terms   existing terms x incoming pod                   (IPA only)
+//   k_pts_prep     per-node eligibility -> domain histograms       (PTS only)
+//   k_pts_reduce   minMatchNum / domain counts per topology key     (PTS only)
+//   k_filter_score Filter chain (first failure stops) + raw Score + per-plugin
+//                  max/min + feasible count  [+ total & argmax when no plugin
+//                  of the profile has ScoreExtensions]
+//   k_pts_weights  topologyNormalizingWeight (Go math.Log restated) (PTS only)
+//   k_pts_score    PodTopologySpread raw score + min/max            (PTS only)
+//   k_finalize     NormalizeScore, [0,100] check, x weight, packed-key argmax
+//   k_commit       assume: NodeInfo.AddPod delta on the selected node, append the
+//                  pod (and its affinity terms) to the existing-pod table
+//
+// Reference call sites replaced: wrappedplugin.go:504 (PreFilter), :535
+// (Filter), :472 (PreScore), :433 (Score), :400 (NormalizeScore), :631
+// (Reserve); upstream algorithms restated in oracle/ksg_oracle.cpp (the
+// checker).  Float64 arithmetic is compiled with -ffp-contract=off and follows
+// the reference operation order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+
+namespace ksg {
+
+#define HIPCHK(x)                                                                 \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) {                                                       \
+      err = std::string(#x) + ": " + hipGetErrorString(e_);                       \
+      return false;                                                               \
+    }                                                                             \
+  } while (0)
+
+static constexpr int kBlock = 256;
+
+// ----------------------------------------------------------------- kernel args
+struct DevCluster {
+  uint32_t N, R, K, goff;
+  const int64_t* alloc;
+  int64_t* req;
+  int64_t* nzc;
+  int64_t* nzm;
+  const int32_t* allowed;
+  int32_t* podcnt;
+  const int32_t* label;
+  const uint32_t* toff;
+  const int32_t* tid;
+  const uint8_t* haslab;
+  const uint32_t* kvo;
+  const int64_t* vnum;
+  const uint8_t* vok;
+  uint32_t n_topo, pairs;
+  int32_t topo_key[KSG_MAX_TOPO];
+  uint32_t topo_base[KSG_MAX_TOPO];
+  uint32_t topo_count[KSG_MAX_TOPO];
+  // existing-pod table
+  uint32_t pcap, pkeys, tcap, rcap, vcap;
+  int32_t* ptnode;
+  int32_t* ptns;
+  uint32_t* ptflags;
+  int32_t* ptlab;
+  ksg_exist_term* terms;
+  int32_t* tpod;
+  ksg_req* treq;
+  int32_t* tval;
+  uint32_t* tcounts;  // [0] pods [1] terms [2] reqs [3] vals [4] overflow flag
+};
+
+struct DevProfile {
+  int n;
+  int plugins[KSG_MAX_PLUGINS];
+  int64_t weight[KSG_MAX_PLUGINS];
+  int has_ext;  // any plugin with ScoreExtensions (or PTS)
+  int fit_strategy, fit_n, ba_n, rtc_n;
+  int fit_res[KSG_MAX_SCORE_RES];
+  int64_t fit_w[KSG_MAX_SCORE_RES];
+  int ba_res[KSG_MAX_SCORE_RES];
+  int64_t rtc_util[KSG_MAX_RTC], rtc_score[KSG_MAX_RTC];
+  int64_t ipa_hard_weight;
+  int ipa_ignore_existing_pref;
+  uint64_t seed;
+};
+
+struct DevScratch {
+  int32_t* cnt;        // [KSG_MAX_TSC][N]
+  int32_t* hist_f;     // [pairs] PTS filter TpPairToMatchNum
+  uint8_t* present_f;  // [pairs] pair registered
+  int32_t* hist_s;     // [pairs] PTS score TopologyPairToPodCounts
+  uint8_t* reg;        // [pairs] pair registered by a filtered node
+  int32_t* ipa_aff;    // [pairs]
+  int32_t* ipa_anti;   // [pairs]
+  int32_t* ipa_exist;  // [pairs]
+  int64_t* ipa_score;  // [pairs]
+  int32_t* pts_min;    // [KSG_MAX_TOPO]
+  int32_t* pts_dom;    // [KSG_MAX_TOPO]
+  uint32_t* exist_any; // [1] bitmask over topology slots with existing anti counts
+};
+
+struct DevOut {
+  uint32_t* filter;  // [N]
+  int32_t* score;    // [n_plugins][N]
+  int32_t* total;    // [N]
+  ksg_pod_summary* sum;
+};
+
+struct ProgView {
+  const ksg_prog* h;
+  const int32_t* i32;
+  const uint32_t* u32;
+  const ksg_req* req;
+  const ksg_sel* sel;
+  const ksg_aterm* at;
+  const ksg_exist_term* et;
+};
+
+__device__ __forceinline__ ProgView view(const uint8_t* p) {
+  ProgView v;
+  v.h = reinterpret_cast<const ksg_prog*>(p);
+  v.i32 = reinterpret_cast<const int32_t*>(p + v.h->off_i32);
+  v.u32 = reinterpret_cast<const uint32_t*>(p + v.h->off_u32);
+  v.req = reinterpret_cast<const ksg_req*>(p + v.h->off_req);
+  v.sel = reinterpret_cast<const ksg_sel*>(p + v.h->off_sel);
+  v.at = reinterpret_cast<const ksg_aterm*>(p + v.h->off_aterm);
+  v.et = reinterpret_cast<const ksg_exist_term*>(p + v.h->off_eterm);
+  return v;
+}
+
+// ----------------------------------------------------------------- helpers
+__device__ __forceinline__ bool in_list(int32_t v, const int32_t* vals, int cnt) {
+  for (int i = 0; i < cnt; ++i)
+    if (vals[i] == v) return true;
+  return false;
+}
+
+// labels.Requirement.Matches over an interned label set (vid < 0: key absent).
+template <class VidF>
+__device__ __forceinline__ bool sel_eval(const ksg_sel& s, const ksg_req* reqs, const int32_t* vals, VidF vid_of) {
+  if (s.kind == 0) return false;
+  for (int i = 0; i < s.req_cnt; ++i) {
+    const ksg_req& r = reqs[s.req_off + i];
+    int32_t v = vid_of(r.key);
+    bool ok;
+    switch (r.op) {
+      case KR_IN: ok = v >= 0 && in_list(v, vals + r.val_off, r.nvals); break;
+      case KR_NOT_IN: ok = v < 0 || !in_list(v, vals + r.val_off, r.nvals); break;
+      case KR_EXISTS: ok = v >= 0; break;
+      case KR_NOT_EXISTS: ok = v < 0; break;
+      default: ok = false;
+    }
+    if (!ok) return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ int32_t node_vid(const DevCluster& C, int32_t key, uint32_t n) {
+  return (key >= 0 && (uint32_t)key < C.K) ? C.label[(size_t)key * C.N + n] : -1;
+}
+
+// node selector requirement incl. Gt/Lt (numeric view of the value) and
+// matchFields metadata.name (KR_NAME_EQ / KR_NAME_NE on the global node index).
+__device__ bool node_req(const DevCluster& C, const ksg_req& r, const int32_t* vals, uint32_t n) {
+  if (r.op == KR_NAME_EQ) return (int64_t)(C.goff + n) == r.num;
+  if (r.op == KR_NAME_NE) return (int64_t)(C.goff + n) != r.num;
+  int32_t v = node_vid(C, r.key, n);
+  switch (r.op) {
+    case KR_IN: return v >= 0 && in_list(v, vals + r.val_off, r.nvals);
+    case KR_NOT_IN: return v < 0 || !in_list(v, vals + r.val_off, r.nvals);
+    case KR_EXISTS: return v >= 0;
+    case KR_NOT_EXISTS: return v < 0;
+    case KR_GT:
+    case KR_LT: {
+      if (v < 0) return false;
+      uint32_t o = C.kvo[r.key] + (uint32_t)v;
+      if (!C.vok[o]) return false;
+      return r.op == KR_GT ? C.vnum[o] > r.num : C.vnum[o] < r.num;
+    }
+    default: return false;
+  }
+}
+
+__device__ bool node_sel(const DevCluster& C, const ProgView& V, const ksg_sel& s, uint32_t n) {
+  if (s.kind == 0) return false;
+  for (int i = 0; i < s.req_cnt; ++i)
+    if (!node_req(C, V.req[s.req_off + i], V.i32, n)) return false;
+  return true;
+}
+
+// nodeaffinity.RequiredNodeAffinity.Match
+__device__ bool required_na(const DevCluster& C, const ProgView& V, uint32_t n) {
+  uint32_t f = V.h->flags;
+  if ((f & KPF_HAS_NODE_SEL) && !node_sel(C, V, V.h->node_sel, n)) return false;
+  if (f & KPF_HAS_REQ_NA) {
+    for (int t = 0; t < V.h->n_req_terms; ++t)
+      if (node_sel(C, V, V.sel[V.h->req_terms_off + t], n)) return true;
+    return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ bool bit(const uint32_t* w, int nw, int32_t i) {
+  return i >= 0 && (i >> 5) < nw && ((w[i >> 5] >> (i & 31)) & 1u);
+}
+
+// first untolerated NoSchedule/NoExecute taint in node.spec.taints order, or -1
+__device__ __forceinline__ int32_t untolerated_taint(const DevCluster& C, const ProgView& V, uint32_t n) {
+  const uint32_t* hard = V.u32 + V.h->taint_hard_off;
+  for (uint32_t i = C.toff[n]; i < C.toff[n + 1]; ++i) {
+    int32_t t = C.tid[i];
+    if (bit(hard, V.h->taint_words, t)) return t;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// highest total, then smallest h20, then largest node index.
+__device__ __forceinline__ uint64_t pack_key(int64_t total, uint64_t seed, int32_t qidx, uint32_t gnode) {
+  uint64_t h20 = splitmix64(seed ^ ((uint64_t)(uint32_t)qidx * 0x9E3779B97F4A7C15ull) ^ (uint64_t)gnode) >> 44;
+  return ((uint64_t)total << 40) | ((0xFFFFFull - h20) << 20) | (uint64_t)gnode;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_max(T v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    T u = __shfl_xor(v, o, 64);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+template <class T>
+__device__ __forceinline__ T wave_min(T v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    T u = __shfl_xor(v, o, 64);
+    v = u < v ? u : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int64_t wave_sum(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ bool lane0() { return (threadIdx.x & 63) == 0; }
+
+// Go math.Log restated (oracle/ksg_oracle.cpp go_log); no contraction.
+__device__ double go_log(double x) {
+#pragma clang fp contract(off)
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10,
+               L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01,
+               L3 = 2.857142874366239149e-01, L4 = 2.222219843214978396e-01,
+               L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (!(x > 0)) return x == 0 ? -INFINITY : NAN;
+  if (isinf(x)) return x;
+  int ki;
+  double f1 = frexp(x, &ki);
+  if (f1 < 0.70710678118654752440) {  // Sqrt2/2
+    f1 = __dmul_rn(f1, 2.0);
+    ki--;
+  }
+  double f = __dsub_rn(f1, 1.0);
+  double k = (double)ki;
+  double s = __ddiv_rn(f, __dadd_rn(2.0, f));
+  double s2 = __dmul_rn(s, s);
+  double s4 = __dmul_rn(s2, s2);
+  double t1 = __dmul_rn(s2, __dadd_rn(L1, __dmul_rn(s4, __dadd_rn(L3, __dmul_rn(s4, __dadd_rn(L5, __dmul_rn(s4, L7)))))));
+  double t2 = __dmul_rn(s4, __dadd_rn(L2, __dmul_rn(s4, __dadd_rn(L4, __dmul_rn(s4, L6)))));
+  double R = __dadd_rn(t1, t2);
+  double hfsq = __dmul_rn(__dmul_rn(0.5, f), f);
+  return __dsub_rn(__dmul_rn(k, Ln2Hi),
+                   __dsub_rn(__dsub_rn(hfsq, __dadd_rn(__dmul_rn(s, __dadd_rn(hfsq, R)), __dmul_rn(k, Ln2Lo))), f));
+}
+
+// ----------------------------------------------------------------- plugins (per node)
+// NodeResourcesFit Filter (fit.go fitsRequest): reason bits, 0 = fits.
+__device__ __forceinline__ uint32_t fit_filter(const DevCluster& C, const ProgView& V, uint32_t n) {
+  uint32_t bits = 0;
+  if (C.podcnt[n] + 1 > C.allowed[n]) bits |= KSG_FIT_TOO_MANY_PODS;
+  if (V.h->flags & KPF_ZERO_REQUEST) return bits;
+  for (uint32_t r = 0; r < C.R; ++r) {
+    int64_t q = V.h->req[r];
+    if (q <= 0) continue;  // cpu/mem/eph: "> 0" guard; scalars: zero skipped
+    if (q > C.alloc[(size_t)r * C.N + n] - C.req[(size_t)r * C.N + n]) bits |= 1u << (1 + r);
+  }
+  return bits;
+}
+
+// resourceAllocationScorer.calculateResourceAllocatableRequest
+__device__ __forceinline__ void alloc_req(const DevCluster& C, uint32_t n, int res, int64_t pod_req, bool use_requested,
+                                          int64_t& a, int64_t& q) {
+  if (res < 0 || (res >= KSG_RES_EPH + 1 && pod_req == 0)) { a = 0; q = 0; return; }  // unknown / scalar not requested
+  a = C.alloc[(size_t)res * C.N + n];
+  if (res == KSG_RES_CPU) q = (use_requested ? C.req[n] : C.nzc[n]) + pod_req;
+  else if (res == KSG_RES_MEM) q = (use_requested ? C.req[(size_t)C.N + n] : C.nzm[n]) + pod_req;
+  else q = C.req[(size_t)res * C.N + n] + pod_req;
+}
+
+__device__ int64_t rtc_fn(const DevProfile& F, int64_t p) {
+  for (int i = 0; i < F.rtc_n; ++i) {
+    if (p <= F.rtc_util[i]) {
+      if (i == 0) return F.rtc_score[0];
+      return F.rtc_score[i - 1] + (F.rtc_score[i] - F.rtc_score[i - 1]) * (p - F.rtc_util[i - 1]) /
+                                      (F.rtc_util[i] - F.rtc_util[i - 1]);
+    }
+  }
+  return F.rtc_score[F.rtc_n - 1];
+}
+
+__device__ int64_t fit_score(const DevCluster& C, const DevProfile& F, const ProgView& V, uint32_t n) {
+#pragma clang fp contract(off)
+  int64_t ns = 0, ws = 0;
+  for (int i = 0; i < F.fit_n; ++i) {
+    int64_t a, q;
+    alloc_req(C, n, F.fit_res[i], V.h->fit_score_req[i], false, a, q);
+    if (a == 0) continue;
+    int64_t s;
+    if (F.fit_strategy == 2) {
+      s = q > a ? rtc_fn(F, 100) : rtc_fn(F, q * 100 / a);
+      if (s <= 0) continue;
+    } else if (F.fit_strategy == 1) {
+      s = (q > a ? a : q) * 100 / a;
+    } else {
+      s = q > a ? 0 : (a - q) * 100 / a;
+    }
+    ns += s * F.fit_w[i];
+    ws += F.fit_w[i];
+  }
+  if (ws == 0) return 0;
+  if (F.fit_strategy == 2) return (int64_t)round(__ddiv_rn((double)ns, (double)ws));
+  return ns / ws;
+}
+
+__device__ int64_t ba_score(const DevCluster& C, const DevProfile& F, const ProgView& V, uint32_t n) {
+#pragma clang fp contract(off)
+  double fr[KSG_MAX_SCORE_RES];
+  int m = 0;
+  double total = 0;
+  for (int i = 0; i < F.ba_n; ++i) {
+    int64_t a, q;
+    alloc_req(C, n, F.ba_res[i], V.h->ba_req[i], true, a, q);
+    if (a == 0) continue;
+    double f = __ddiv_rn((double)q, (double)a);
+    if (f > 1) f = 1;
+    total = __dadd_rn(total, f);
+    fr[m++] = f;
+  }
+  double sd = 0.0;
+  if (m == 2) {
+    sd = fabs(__ddiv_rn(__dsub_rn(fr[0], fr[1]), 2.0));
+  } else if (m > 2) {
+    double mean = __ddiv_rn(total, (double)m);
+    double sum = 0;
+    for (int i = 0; i < m; ++i) {
+      double d = __dsub_rn(fr[i], mean);
+      sum = __dadd_rn(sum, __dmul_rn(d, d));
+    }
+    sd = __dsqrt_rn(__ddiv_rn(sum, (double)m));
+  }
+  return (int64_t)__dmul_rn(__dsub_rn(1.0, sd), 100.0);
+}
+
+__device__ __forceinline__ int64_t taint_score(const DevCluster& C, const ProgView& V, uint32_t n) {
+  const uint32_t* pref = V.u32 + V.h->taint_pref_off;
+  int64_t c = 0;
+  for (uint32_t i = C.toff[n]; i < C.toff[n + 1]; ++i)
+    if (bit(pref, V.h->taint_words, C.tid[i])) c++;
+  return c;
+}
+
+__device__ __forceinline__ int64_t na_score(const DevCluster& C, const ProgView& V, uint32_t n) {
+  int64_t s = 0;
+  for (int t = 0; t < V.h->n_pref_terms; ++t)
+    if (node_sel(C, V, V.sel[V.h->pref_terms_off + t], n)) s += V.i32[V.h->pref_w_off + t];
+  return s;
+}
+
+__device__ __forceinline__ bool pts_has_keys(const DevCluster& C, const ProgView& V, int c0, int c1, uint32_t n) {
+  for (int c = c0; c < c1; ++c)
+    if (node_vid(C, V.h->tsc[c].topo_key, n) < 0) return false;
+  return true;
+}
+
+// PodTopologySpread Filter
+__device__ __forceinline__ int pts_filter(const DevCluster& C, const DevScratch& S, const ProgView& V, uint32_t n,
+                                          bool& error) {
+  for (int c = 0; c < V.h->n_tsc_filter; ++c) {
+    const ksg_tsc& t = V.h->tsc[c];
+    int32_t v = node_vid(C, t.topo_key, n);
+    if (v < 0) return 1 + KSG_PTS_MISSING_LABEL;
+    int32_t dom = S.pts_dom[t.topo];
+    if (dom == 0) { error = true; return 0; }  // minMatchNum: no domains for key -> Error status
+    int64_t mn = dom < t.min_domains ? 0 : S.pts_min[t.topo];
+    int64_t match = S.hist_f[C.topo_base[t.topo] + v];
+    if (match + t.self_match - mn > t.max_skew) return 1 + KSG_PTS_SKEW;
+  }
+  return 0;
+}
+
+// InterPodAffinity Filter
+__device__ __forceinline__ int ipa_filter(const DevCluster& C, const DevScratch& S, const ProgView& V, uint32_t n,
+                                          uint32_t ipa_flags, uint32_t exist_any) {
+  const ksg_prog* h = V.h;
+  const ksg_aterm* aff = V.at + h->aterm_off;
+  const ksg_aterm* anti = aff + h->n_req_aff;
+  bool pods_exist = true;
+  for (int i = 0; i < h->n_req_aff; ++i) {
+    int32_t v = node_vid(C, aff[i].topo_key, n);
+    if (v < 0) return 1 + KSG_IPA_AFFINITY;
+    if (S.ipa_aff[C.topo_base[aff[i].topo] + v] <= 0) pods_exist = false;
+  }
+  if (!pods_exist && !(!(ipa_flags & 1u) && h->self_matches_all)) return 1 + KSG_IPA_AFFINITY;
+  if (ipa_flags & 2u)
+    for (int i = 0; i < h->n_req_anti; ++i) {
+      int32_t v = node_vid(C, anti[i].topo_key, n);
+      if (v >= 0 && S.ipa_anti[C.topo_base[anti[i].topo] + v] > 0) return 1 + KSG_IPA_ANTI_AFFINITY;
+    }
+  if (exist_any)
+    for (uint32_t s = 0; s < C.n_topo; ++s) {
+      if (!((exist_any >> s) & 1u)) continue;
+      int32_t v = node_vid(C, C.topo_key[s], n);
+      if (v >= 0 && S.ipa_exist[C.topo_base[s] + v] > 0) return 1 + KSG_IPA_EXISTING_ANTI;
+    }
+  return 0;
+}
+
+__device__ __forceinline__ int64_t ipa_score(const DevCluster& C, const DevScratch& S, uint32_t n) {
+  int64_t s = 0;
+  for (uint32_t t = 0; t < C.n_topo; ++t) {
+    int32_t v = node_vid(C, C.topo_key[t], n);
+    if (v >= 0) s += S.ipa_score[C.topo_base[t] + v];
+  }
+  return s;
+}
+
+// ----------------------------------------------------------------- kernels
+__global__ void k_init_summaries(ksg_pod_summary* sum, uint32_t count, DevProfile F) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  ksg_pod_summary s = {};
+  s.selected = -1;
+  for (int p = 0; p < KSG_MAX_PLUGINS; ++p) {
+    s.max_score[p] = (p < F.n && F.plugins[p] == KP_IPA) ? INT64_MIN : 0;
+    s.min_score[p] = INT64_MAX;
+  }
+  sum[i] = s;
+}
+
+__global__ void k_begin(DevCluster C, DevScratch S, const uint8_t* prog) {
+  ProgView V = view(prog);
+  uint32_t ntsc = (uint32_t)(V.h->n_tsc_filter + V.h->n_tsc_score);
+  size_t cnt_n = (size_t)ntsc * C.N;
+  size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt_n || i < C.pairs; i += stride) {
+    if (i < cnt_n) S.cnt[i] = 0;
+    if (i < C.pairs) {
+      S.hist_f[i] = 0; S.present_f[i] = 0; S.hist_s[i] = 0; S.reg[i] = 0;
+      S.ipa_aff[i] = 0; S.ipa_anti[i] = 0; S.ipa_exist[i] = 0; S.ipa_score[i] = 0;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < KSG_MAX_TOPO) {
+    S.pts_min[threadIdx.x] = 0x7FFFFFFF;
+    S.pts_dom[threadIdx.x] = 0;
+    if (threadIdx.x == 0) S.exist_any[0] = 0;
+  }
+}
+
+// existing pods x (PTS selectors, IPA incoming required terms, IPA incoming preferred terms)
+__global__ void k_scan_pods(DevCluster C, DevProfile F, DevScratch S, DevOut O, const uint8_t* prog) {
+  ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  uint32_t np = C.tcounts[0];
+  uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t aff_hit = 0;
+  if (p < np) {
+    int32_t node = C.ptnode[p];
+    int32_t ns = C.ptns[p];
+    uint32_t fl = C.ptflags[p];
+    auto vid = [&](int32_t k) -> int32_t {
+      return (k >= 0 && (uint32_t)k < C.pkeys) ? C.ptlab[(size_t)k * C.pcap + p] : -1;
+    };
+    // PTS countPodsMatchSelector (Empty() selector counts nothing)
+    int ntsc = h->n_tsc_filter + h->n_tsc_score;
+    if (!(fl & KEF_TERMINATING) && ns == h->ns_id)
+      for (int c = 0; c < ntsc; ++c) {
+        const ksg_sel& s = h->tsc[c].sel;
+        if (s.kind == 1 && s.req_cnt > 0 && sel_eval(s, V.req, V.i32, vid)) atomicAdd(&S.cnt[(size_t)c * C.N + node], 1);
+      }
+    const ksg_aterm* aff = V.at + h->aterm_off;
+    const ksg_aterm* anti = aff + h->n_req_aff;
+    const ksg_aterm* paff = anti + h->n_req_anti;  // preferred affinity, then preferred anti
+    auto term_ok = [&](const ksg_aterm& t) {
+      return (t.ns_all || in_list(ns, V.i32 + t.ns_off, t.ns_cnt)) && sel_eval(t.sel, V.req, V.i32, vid);
+    };
+    if (h->n_req_aff > 0) {
+      bool all = true;
+      for (int i = 0; i < h->n_req_aff && all; ++i) all = term_ok(aff[i]);
+      if (all)
+        for (int i = 0; i < h->n_req_aff; ++i) {
+          int32_t v = node_vid(C, aff[i].topo_key, node);
+          if (v >= 0) { atomicAdd(&S.ipa_aff[C.topo_base[aff[i].topo] + v], 1); aff_hit |= 1u; }
+        }
+    }
+    for (int i = 0; i < h->n_req_anti; ++i)
+      if (term_ok(anti[i])) {
+        int32_t v = node_vid(C, anti[i].topo_key, node);
+        if (v >= 0) { atomicAdd(&S.ipa_anti[C.topo_base[anti[i].topo] + v], 1); aff_hit |= 2u; }
+      }
+    if ((h->flags & KPF_IPA_HAS_CONSTRAINTS) && C.haslab[node]) {
+      for (int i = 0; i < h->n_pref_aff + h->n_pref_anti; ++i) {
+        const ksg_aterm& t = paff[i];
+        if (!term_ok(t)) continue;
+        int32_t v = node_vid(C, t.topo_key, node);
+        if (v < 0) continue;
+        int64_t w = i < h->n_pref_aff ? (int64_t)t.weight : -(int64_t)t.weight;
+        atomicAdd((unsigned long long*)&S.ipa_score[C.topo_base[t.topo] + v], (unsigned long long)w);
+        aff_hit |= 8u;
+      }
+    }
+  }
+    uint32_t m = aff_hit;
+  for (int o = 32; o > 0; o >>= 1) m |= __shfl_xor(m, o, 64);
+  if (lane0() && m) atomicOr(&O.sum->ipa_flags, m);
+}
+
+// existing pods' terms x incoming pod (existing anti-affinity counts, IPA score terms)
+__global__ void k_scan_terms(DevCluster C, DevProfile F, DevScratch S, DevOut O, const uint8_t* prog) {
+  ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  uint32_t nt = C.tcounts[1];
+  uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t hit = 0, slots = 0;
+  if (t < nt) {
+    const ksg_exist_term& e = C.terms[t];
+    int32_t p = C.tpod[t];
+    int32_t node = C.ptnode[p];
+    auto vid = [&](int32_t k) -> int32_t {
+      return (k >= 0 && k < h->n_pod_label_keys) ? V.i32[h->labels_off + k] : -1;
+    };
+    bool ns_ok = e.ns_all || in_list(h->ns_id, C.tval + e.ns_off, e.ns_cnt);
+    bool score_on = !(F.ipa_ignore_existing_pref && !(h->flags & KPF_IPA_HAS_CONSTRAINTS));
+    if (ns_ok && sel_eval(e.sel, C.treq, C.tval, vid)) {
+      int32_t v = node_vid(C, e.topo_key, node);
+      if (v >= 0) {
+        uint32_t pair = C.topo_base[e.topo] + v;
+        if (e.kind == 1) {
+          atomicAdd(&S.ipa_exist[pair], 1);
+          slots |= 1u << e.topo;
+        } else if (score_on && C.haslab[node]) {
+          int64_t w = e.kind == 0 ? (F.ipa_hard_weight > 0 ? F.ipa_hard_weight : 0)
+                                  : (e.kind == 2 ? (int64_t)e.weight : -(int64_t)e.weight);
+          if (e.kind != 0 || F.ipa_hard_weight > 0) {
+            atomicAdd((unsigned long long*)&S.ipa_score[pair], (unsigned long long)w);
+            hit |= 8u;
+          }
+        }
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    hit |= __shfl_xor(hit, o, 64);
+    slots |= __shfl_xor(slots, o, 64);
+  }
+  if (lane0()) {
+    if (hit) atomicOr(&O.sum->ipa_flags, hit);
+    if (slots) { atomicOr(S.exist_any, slots); atomicOr(&O.sum->ipa_flags, 4u); }
+  }
+}
+
+// PodTopologySpread PreFilter / PreScore per-node aggregation
+__global__ void k_pts_prep(DevCluster C, DevScratch S, const uint8_t* prog) {
+  ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= C.N) return;
+  int nf = h->n_tsc_filter, ns = h->n_tsc_score;
+  bool na_ok = true, taint_ok = true;
+  bool need_na = false, need_taint = false;
+  for (int c = 0; c < nf + ns; ++c) {
+    need_na |= h->tsc[c].honor_affinity != 0;
+    need_taint |= h->tsc[c].honor_taints != 0;
+  }
+  if (need_na) na_ok = required_na(C, V, n);
+  if (need_taint) taint_ok = untolerated_taint(C, V, n) < 0;
+  if (nf > 0 && pts_has_keys(C, V, 0, nf, n)) {
+    uint32_t done = 0;
+    for (int c = nf - 1; c >= 0; --c) {  // last passing constraint per key wins (tpCounts[pair] = count)
+      const ksg_tsc& t = h->tsc[c];
+      if ((done >> t.topo) & 1u) continue;
+      if ((t.honor_affinity && !na_ok) || (t.honor_taints && !taint_ok)) continue;
+      done |= 1u << t.topo;
+      uint32_t pair = C.topo_base[t.topo] + node_vid(C, t.topo_key, n);
+      int32_t cnt = S.cnt[(size_t)c * C.N + n];
+      if (cnt) atomicAdd(&S.hist_f[pair], cnt);
+      S.present_f[pair] = 1;
+    }
+  }
+  if (ns > 0 && !(h->flags & KPF_SKIP_PTS_SCORE) && pts_has_keys(C, V, nf, nf + ns, n)) {
+    for (int c = nf; c < nf + ns; ++c) {
+      const ksg_tsc& t = h->tsc[c];
+      if (t.is_hostname) continue;
+      if ((t.honor_affinity && !na_ok) || (t.honor_taints && !taint_ok)) continue;
+      uint32_t pair = C.topo_base[t.topo] + node_vid(C, t.topo_key, n);
+      int32_t cnt = S.cnt[(size_t)c * C.N + n];
+      if (cnt) atomicAdd(&S.hist_s[pair], cnt);
+    }
+  }
+}
+
+// minMatchNum / TpKeyToDomainsNum per filter topology key
+__global__ void k_pts_reduce(DevCluster C, DevScratch S, const uint8_t* prog) {
+  ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  uint32_t seen = 0;
+  for (int c = 0; c < h->n_tsc_filter; ++c) {
+    int slot = h->tsc[c].topo;
+    if ((seen >> slot) & 1u) continue;
+    seen |= 1u << slot;
+    uint32_t base = C.topo_base[slot], cnt = C.topo_count[slot];
+    int32_t mn = 0x7FFFFFFF;
+    int32_t dom = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+      if (S.present_f[base + i]) {
+        dom++;
+        int32_t x = S.hist_f[base + i];
+        mn = x < mn ? x : mn;
+      }
+    }
+    mn = wave_min(mn);
+    dom = (int32_t)wave_sum(dom);
+    if (lane0()) {
+      if (mn != 0x7FFFFFFF) atomicMin(&S.pts_min[slot], mn);
+      if (dom) atomicAdd(&S.pts_dom[slot], dom);
+    }
+  }
+}
+
+// Filter chain + raw scores (+ total/argmax when the profile has no ScoreExtensions)
+__global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfile F, DevScratch S, DevOut O,
+                                                         const uint8_t* prog) {
+  ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+  bool active = n < C.N;
+  uint32_t code = KSG_FILTER_NOT_EVALUATED;
+  bool err = false;
+  int64_t raw[KSG_MAX_PLUGINS];
+  uint32_t ipa_flags = O.sum->ipa_flags;
+  uint32_t exist_any = S.exist_any ? S.exist_any[0] : 0;
+  if (active && !(h->flags & KPF_PREFILTER_REJECT) &&
+      !((h->flags & KPF_RESTRICT) && !bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n))) {
+    code = KSG_FILTER_PASS;
+    for (int pos = 0; pos < F.n && code == KSG_FILTER_PASS; ++pos) {
+      uint32_t detail = 0;
+      bool fail = false;
+      switch (F.plugins[pos]) {
+        case KP_FIT: {
+          uint32_t b = fit_filter(C, V, n);
+          if (b) { fail = true; detail = b; }
+          break;
+        }
+        case KP_TAINT: {
+          int32_t t = untolerated_taint(C, V, n);
+          if (t >= 0) { fail = true; detail = (uint32_t)t; }
+          break;
+        }
+        case KP_NA:
+          if (!(h->flags & KPF_SKIP_NA_FILTER) && !required_na(C, V, n)) fail = true;
+          break;
+        case KP_PTS:
+          if (!(h->flags & KPF_SKIP_PTS_FILTER)) {
+            int r = pts_filter(C, S, V, n, err);
+            if (r) { fail = true; detail = (uint32_t)(r - 1); }
+          }
+          break;
+        case KP_IPA: {
+          int r = ipa_filter(C, S, V, n, ipa_flags, exist_any);
+          if (r) { fail = true; detail = (uint32_t)(r - 1); }
+          break;
+        }
+        default: break;
+      }
+      if (fail) code = ((uint32_t)pos << 24) | (detail & 0xFFFFFFu);
+    }
+  }
+  bool feasible = active && code == KSG_FILTER_PASS;
+  uint64_t best = 0;
+  int32_t total = 0;
+  bool range_err = false;
+  for (int pos = 0; pos < F.n; ++pos) raw[pos] = 0;
+  if (feasible) {
+    for (int pos = 0; pos < F.n; ++pos) {
+      int64_t s = 0;
+      switch (F.plugins[pos]) {
+        case KP_FIT: s = fit_score(C, F, V, n); break;
+        case KP_BA: s = ba_score(C, F, V, n); break;
+        case KP_TAINT: s = taint_score(C, V, n); break;
+        case KP_NA: s = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n); break;
+        case KP_IPA: s = ipa_score(C, S, n); break;
+        default: break;
+      }
+      raw[pos] = s;
+    }
+    // PodTopologySpread PreScore registration (initPreScoreState)
+    int nf = h->n_tsc_filter, ns = h->n_tsc_score;
+    if (ns > 0 && !(h->flags & KPF_SKIP_PTS_SCORE)) {
+      if (!pts_has_keys(C, V, nf, nf + ns, n)) {
+        atomicAdd(&O.sum->ignored, 1);
+      } else {
+        for (int c = nf; c < nf + ns; ++c)
+          if (!h->tsc[c].is_hostname) S.reg[C.topo_base[h->tsc[c].topo] + node_vid(C, h->tsc[c].topo_key, n)] = 1;
+      }
+    }
+    if (!F.has_ext) {
+      int64_t tot = 0;
+      for (int pos = 0; pos < F.n; ++pos) {
+        if (raw[pos] < 0 || raw[pos] > 100) range_err = true;
+        tot += raw[pos] * F.weight[pos];
+      }
+      total = (int32_t)tot;
+      best = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
+    }
+  }
+  if (active) {
+    O.filter[n] = code;
+    if (feasible) {
+      for (int pos = 0; pos < F.n; ++pos) O.score[(size_t)pos * C.N + n] = (int32_t)raw[pos];
+      if (!F.has_ext) O.total[n] = total;
+    }
+  }
+  // ---- reductions: feasible count, per-plugin max/min, argmax
+  unsigned long long bal = __ballot(feasible);
+  if (lane0() && bal) atomicAdd(&O.sum->feasible, (int)__popcll(bal));
+  if (__any(err) && lane0()) atomicOr((uint32_t*)&O.sum->status, 2u);
+  if (__any(range_err) && lane0()) atomicOr((uint32_t*)&O.sum->status, 2u);
+  if (bal) {
+    for (int pos = 0; pos < F.n; ++pos) {
+      int p = F.plugins[pos];
+      if (p == KP_TAINT || p == KP_NA || p == KP_IPA) {
+        int64_t mx = wave_max(feasible ? raw[pos] : INT64_MIN);
+        int64_t mn = wave_min(feasible ? raw[pos] : INT64_MAX);
+        if (lane0()) {
+          atomicMax((long long*)&O.sum->max_score[pos], (long long)mx);
+          atomicMin((long long*)&O.sum->min_score[pos], (long long)mn);
+        }
+      }
+    }
+    if (!F.has_ext) {
+      uint64_t b = wave_max(best);
+      if (lane0()) atomicMax((unsigned long long*)&O.sum->best_key, (unsigned long long)b);
+    }
+  }
+}
+
+// topologyNormalizingWeight per score constraint
+__global__ void k_pts_weights(DevCluster C, DevScratch S, DevOut O, const uint8_t* prog) {
+  ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  __shared__ int32_t red[kBlock / 64];
+  int nf = h->n_tsc_filter, ns = h->n_tsc_score;
+  for (int c = nf; c < nf + ns; ++c) {
+    const ksg_tsc& t = h->tsc[c];
+    int64_t size = 0;
+    if (t.is_hostname) {
+      size = (int64_t)O.sum->feasible - O.sum->ignored;
+    } else if (t.first_of_key) {
+      uint32_t base = C.topo_base[t.topo], cnt = C.topo_count[t.topo];
+      int32_t x = 0;
+      for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) x += S.reg[base + i];
+      x = (int32_t)wave_sum(x);
+      if (lane0()) red[threadIdx.x >> 6] = x;
+      __syncthreads();
+      if (threadIdx.x == 0)
+        for (int w = 0; w < kBlock / 64; ++w) size += red[w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) O.sum->pts_weight[c - nf] = go_log((double)(size + 2));
+  }
+}
+
+__global__ void k_pts_score(DevCluster C, DevScratch S, DevOut O, const uint8_t* prog, int pos) {
+  ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+  bool feasible = n < C.N && O.filter[n] == KSG_FILTER_PASS;
+  bool counted = false;
+  int64_t s = 0;
+  int nf = h->n_tsc_filter, ns = h->n_tsc_score;
+  if (feasible && !(h->flags & KPF_SKIP_PTS_SCORE) && pts_has_keys(C, V, nf, nf + ns, n)) {
+#pragma clang fp contract(off)
+    counted = true;
+    double score = 0;
+    for (int c = nf; c < nf + ns; ++c) {
+      const ksg_tsc& t = h->tsc[c];
+      int32_t v = node_vid(C, t.topo_key, n);
+      if (v < 0) continue;
+      int64_t cnt = t.is_hostname ? S.cnt[(size_t)c * C.N + n] : S.hist_s[C.topo_base[t.topo] + v];
+      score = __dadd_rn(score, __dadd_rn(__dmul_rn((double)cnt, O.sum->pts_weight[c - nf]), (double)(t.max_skew - 1)));
+    }
+    s = (int64_t)round(score);
+  }
+  if (feasible) O.score[(size_t)pos * C.N + n] = (int32_t)s;
+  int64_t mx = wave_max(counted ? s : INT64_MIN);
+  int64_t mn = wave_min(counted ? s : INT64_MAX);
+  if (lane0() && __any(counted)) {
+    atomicMax((long long*)&O.sum->max_score[pos], (long long)mx);
+    atomicMin((long long*)&O.sum->min_score[pos], (long long)mn);
+  }
+}
+
+// NormalizeScore + [0,100] check + weights + packed-key argmax
+__global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, const uint8_t* prog) {
+  ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+  bool feasible = n < C.N && O.filter[n] == KSG_FILTER_PASS;
+  uint64_t best = 0;
+  bool range_err = false;
+  if (feasible) {
+    int nf = h->n_tsc_filter, ns = h->n_tsc_score;
+    int64_t tot = 0;
+    uint32_t ipa_flags = O.sum->ipa_flags;
+    for (int pos = 0; pos < F.n; ++pos) {
+      int64_t s = O.score[(size_t)pos * C.N + n];
+      int64_t mx = O.sum->max_score[pos], mn = O.sum->min_score[pos];
+      switch (F.plugins[pos]) {
+        case KP_TAINT:  // DefaultNormalizeScore(100, reverse)
+          s = mx == 0 ? 100 : 100 - 100 * s / mx;
+          break;
+        case KP_NA:
+          if (h->flags & KPF_SKIP_NA_SCORE) { s = 0; continue; }
+          s = mx == 0 ? s : 100 * s / mx;
+          break;
+        case KP_PTS:
+          if (h->flags & KPF_SKIP_PTS_SCORE) continue;
+          if (!pts_has_keys(C, V, nf, nf + ns, n)) s = 0;
+          else if (mx == 0) s = 100;
+          else s = 100 * (mx + mn - s) / mx;
+          break;
+        case KP_IPA:
+          if (!(ipa_flags & 8u)) continue;  // PreScore Skip (empty topology score map)
+          {
+#pragma clang fp contract(off)
+            int64_t diff = mx - mn;
+            double f = 0;
+            if (diff > 0) f = __dmul_rn(100.0, __ddiv_rn((double)(s - mn), (double)diff));
+            s = (int64_t)f;
+          }
+          break;
+        default: break;
+      }
+      if (s < 0 || s > 100) range_err = true;
+      tot += s * F.weight[pos];
+    }
+    if (O.sum->feasible == 1) tot = 0;  // single feasible node: no scoring
+    O.total[n] = (int32_t)tot;
+    best = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
+  }
+  if (O.sum->feasible > 1 && __any(range_err) && lane0()) atomicOr((uint32_t*)&O.sum->status, 2u);
+  uint64_t b = wave_max(best);
+  if (lane0() && b) atomicMax((unsigned long long*)&O.sum->best_key, (unsigned long long)b);
+}
+
+// assume (scheduleOne -> assume -> NodeInfo.AddPod) + existing-pod table append
+__global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* prog, int append) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  ksg_pod_summary* s = O.sum;
+  if (h->flags & KPF_PREFILTER_ERROR) s->status |= 2;
+  if (s->status & 2) { s->status = 2; s->selected = -1; return; }
+  if (s->feasible == 0) { s->status = 1; s->selected = -1; return; }
+  uint32_t g = (uint32_t)(s->best_key & 0xFFFFFull);
+  s->selected = (int32_t)g;
+  s->status = 0;
+  uint32_t n = g - C.goff;
+  if (g < C.goff || n >= C.N) return;  // another shard owns the node
+  for (uint32_t r = 0; r < C.R; ++r) C.req[(size_t)r * C.N + n] += h->req[r];
+  C.nzc[n] += h->nz_cpu;
+  C.nzm[n] += h->nz_mem;
+  C.podcnt[n] += 1;
+  if (!append) return;
+  uint32_t row = C.tcounts[0];
+  uint32_t tb = C.tcounts[1], rb = C.tcounts[2], vb = C.tcounts[3];
+  int ne = h->n_exist_terms;
+  uint32_t need_r = 0, need_v = 0;
+  for (int i = 0; i < ne; ++i) {
+    const ksg_exist_term& e = V.et[h->exist_terms_off + i];
+    need_r += e.sel.req_cnt;
+    need_v += e.ns_cnt;
+    for (int k = 0; k < e.sel.req_cnt; ++k) need_v += V.req[e.sel.req_off + k].nvals;
+  }
+  if (row >= C.pcap || tb + ne > C.tcap || rb + need_r > C.rcap || vb + need_v > C.vcap) {
+    C.tcounts[4] = 1;  // overflow: host re-uploads the table from its mirror
+    return;
+  }
+  C.ptnode[row] = (int32_t)n;
+  C.ptns[row] = h->ns_id;
+  C.ptflags[row] = h->exist_flags;
+  for (uint32_t k = 0; k < C.pkeys; ++k)
+    C.ptlab[(size_t)k * C.pcap + row] = (int32_t)k < h->n_pod_label_keys ? V.i32[h->labels_off + k] : -1;
+  for (int i = 0; i < ne; ++i) {
+    ksg_exist_term e = V.et[h->exist_terms_off + i];
+    for (int k = 0; k < e.ns_cnt; ++k) C.tval[vb + k] = V.i32[e.ns_off + k];
+    e.ns_off = (int32_t)vb;
+    vb += e.ns_cnt;
+    int r0 = e.sel.req_off;
+    e.sel.req_off = (int32_t)rb;
+    for (int k = 0; k < e.sel.req_cnt; ++k) {
+      ksg_req q = V.req[r0 + k];
+      for (int j = 0; j < q.nvals; ++j) C.tval[vb + j] = V.i32[q.val_off + j];
+      q.val_off = (int32_t)vb;
+      vb += q.nvals;
+      C.treq[rb++] = q;
+    }
+    C.terms[tb] = e;
+    C.tpod[tb] = (int32_t)row;
+    tb++;
+  }
+  C.tcounts[0] = row + 1;
+  C.tcounts[1] = tb;
+  C.tcounts[2] = rb;
+  C.tcounts[3] = vb;
+}
+
+// ----------------------------------------------------------------- host side
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  bool alloc(size_t count, std::string& err) {
+    if (count <= n && p) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+    hipError_t e = hipMalloc((void**)&p, bytes);
+    if (e != hipSuccess) {
+      err = std::string("hipMalloc: ") + hipGetErrorString(e);
+      return false;
+    }
+    n = std::max<size_t>(count, 1);
+    return true;
+  }
+  bool upload(const std::vector<T>& v, hipStream_t s, std::string& err) {
+    if (!alloc(v.size(), err)) return false;
+    if (!v.empty()) {
+      hipError_t e = hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+      if (e != hipSuccess) { err = hipGetErrorString(e); return false; }
+    }
+    return true;
+  }
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+struct Engine::Impl {
+  EngineConfig cfg;
+  DevProfile F{};
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  uint32_t N = 0, R = 3, K = 0, goff = 0;
+  // nodes
+  DBuf<int64_t> alloc, req, nzc, nzm, vnum;
+  DBuf<int32_t> allowed, podcnt, label, tid;
+  DBuf<uint32_t> toff, kvo;
+  DBuf<uint8_t> haslab, vok;
+  NodeSoA topo;  // topology tables (host copy)
+  // pod table
+  DBuf<int32_t> ptnode, ptns, ptlab, tpod, tval;
+  DBuf<uint32_t> ptflags, tcounts;
+  DBuf<ksg_exist_term> terms;
+  DBuf<ksg_req> treq;
+  uint32_t pcap = 0, pkeys = 0, tcap = 0, rcap = 0, vcap = 0;
+  // scratch
+  DBuf<int32_t> cnt, hist_f, hist_s, ipa_aff, ipa_anti, ipa_exist, pts_min, pts_dom;
+  DBuf<uint8_t> present_f, reg;
+  DBuf<int64_t> ipa_score;
+  DBuf<uint32_t> exist_any;
+  // outputs
+  DBuf<uint32_t> filter;
+  DBuf<int32_t> score, total;
+  DBuf<ksg_pod_summary> sums;
+  // kept per-pair outputs
+  uint32_t keep_first = 0, keep_n = 0;
+  DBuf<uint32_t> kfilter;
+  DBuf<int32_t> kscore, ktotal;
+  // programs
+  DBuf<uint8_t> progs;
+  std::vector<size_t> prog_off;
+  std::vector<uint32_t> prog_need;  // bit0 pts, bit1 ipa
+  bool has_pts = false, has_ipa = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  float last_ms = 0;
+  std::vector<Engine::KernelStat> stats;
+
+  DevCluster cluster() const {
+    DevCluster C{};
+    C.N = N; C.R = R; C.K = K; C.goff = goff;
+    C.alloc = alloc.p; C.req = req.p; C.nzc = nzc.p; C.nzm = nzm.p;
+    C.allowed = allowed.p; C.podcnt = podcnt.p; C.label = label.p; C.toff = toff.p; C.tid = tid.p;
+    C.haslab = haslab.p; C.kvo = kvo.p; C.vnum = vnum.p; C.vok = vok.p;
+    C.n_topo = (uint32_t)topo.topo_key.size();
+    C.pairs = topo.topo_pairs;
+    for (uint32_t i = 0; i < C.n_topo && i < KSG_MAX_TOPO; ++i) {
+      C.topo_key[i] = topo.topo_key[i];
+      C.topo_base[i] = topo.topo_base[i];
+      C.topo_count[i] = topo.topo_count[i];
+    }
+    C.pcap = pcap; C.pkeys = pkeys; C.tcap = tcap; C.rcap = rcap; C.vcap = vcap;
+    C.ptnode = ptnode.p; C.ptns = ptns.p; C.ptflags = ptflags.p; C.ptlab = ptlab.p;
+    C.terms = terms.p; C.tpod = tpod.p; C.treq = treq.p; C.tval = tval.p; C.tcounts = tcounts.p;
+    return C;
+  }
+  DevScratch scratch() const {
+    DevScratch S{};
+    S.cnt = cnt.p; S.hist_f = hist_f.p; S.present_f = present_f.p; S.hist_s = hist_s.p; S.reg = reg.p;
+    S.ipa_aff = ipa_aff.p; S.ipa_anti = ipa_anti.p; S.ipa_exist = ipa_exist.p; S.ipa_score = ipa_score.p;
+    S.pts_min = pts_min.p; S.pts_dom = pts_dom.p; S.exist_any = exist_any.p;
+    return S;
+  }
+};
+
+Engine::Engine() : p_(new Impl()) {}
+Engine::~Engine() {
+  if (p_->ev0) (void)hipEventDestroy(p_->ev0);
+  if (p_->ev1) (void)hipEventDestroy(p_->ev1);
+  if (p_->own_stream && p_->stream) (void)hipStreamDestroy(p_->stream);
+  delete p_;
+}
+
+bool Engine::init(const EngineConfig& cfg, std::string& err) {
+  Impl& I = *p_;
+  I.cfg = cfg;
+  HIPCHK(hipSetDevice(cfg.device));
+  if (cfg.stream) {
+    I.stream = (hipStream_t)cfg.stream;
+  } else {
+    HIPCHK(hipStreamCreateWithFlags(&I.stream, hipStreamNonBlocking));
+    I.own_stream = true;
+  }
+  HIPCHK(hipEventCreate(&I.ev0));
+  HIPCHK(hipEventCreate(&I.ev1));
+  DevProfile& F = I.F;
+  F.n = cfg.n_plugins;
+  F.has_ext = 0;
+  for (int i = 0; i < cfg.n_plugins; ++i) {
+    F.plugins[i] = cfg.plugins[i];
+    F.weight[i] = cfg.weight[i];
+    int p = cfg.plugins[i];
+    if (p == KP_TAINT || p == KP_NA || p == KP_PTS || p == KP_IPA) F.has_ext = 1;
+    if (p == KP_PTS) I.has_pts = true;
+    if (p == KP_IPA) I.has_ipa = true;
+  }
+  F.fit_strategy = cfg.fit_strategy;
+  F.fit_n = cfg.fit_n;
+  F.ba_n = cfg.ba_n;
+  F.rtc_n = cfg.rtc_n;
+  for (int i = 0; i < KSG_MAX_SCORE_RES; ++i) {
+    F.fit_res[i] = cfg.fit_res[i];
+    F.fit_w[i] = cfg.fit_w[i];
+    F.ba_res[i] = cfg.ba_res[i];
+  }
+  for (int i = 0; i < KSG_MAX_RTC; ++i) {
+    F.rtc_util[i] = cfg.rtc_util[i];
+    F.rtc_score[i] = cfg.rtc_score[i];
+  }
+  F.ipa_hard_weight = cfg.ipa_hard_weight;
+  F.ipa_ignore_existing_pref = cfg.ipa_ignore_existing_pref;
+  F.seed = cfg.seed;
+  return true;
+}
+
+bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, uint32_t term_cap, uint32_t req_cap,
+                    uint32_t val_cap, std::string& err) {
+  Impl& I = *p_;
+  hipStream_t s = I.stream;
+  if (ns.topo_key.size() > KSG_MAX_TOPO) { err = "too many topology keys"; return false; }
+  if (ns.n_res > KSG_MAX_RES) { err = "too many resources"; return false; }
+  I.N = ns.n;
+  I.goff = ns.global_offset;
+  I.R = ns.n_res;
+  I.K = ns.n_keys;
+  if (!I.alloc.upload(ns.alloc, s, err) || !I.req.upload(ns.requested, s, err) || !I.nzc.upload(ns.nz_cpu, s, err) ||
+      !I.nzm.upload(ns.nz_mem, s, err) || !I.allowed.upload(ns.allowed_pods, s, err) ||
+      !I.podcnt.upload(ns.pod_count, s, err) || !I.label.upload(ns.label_vid, s, err) ||
+      !I.toff.upload(ns.taint_off, s, err) || !I.tid.upload(ns.taint_id, s, err) ||
+      !I.haslab.upload(ns.has_labels, s, err) || !I.kvo.upload(ns.key_val_off, s, err) ||
+      !I.vnum.upload(ns.val_num, s, err) || !I.vok.upload(ns.val_num_ok, s, err))
+    return false;
+  I.topo = NodeSoA();
+  I.topo.topo_key = ns.topo_key;
+  I.topo.topo_base = ns.topo_base;
+  I.topo.topo_count = ns.topo_count;
+  I.topo.topo_pairs = ns.topo_pairs;
+  // existing-pod table (capacity for device-side appends)
+  I.pcap = std::max<uint32_t>(pod_cap, pt.n);
+  I.pkeys = pt.n_keys;
+  I.tcap = std::max<uint32_t>(term_cap, (uint32_t)pt.terms.size());
+  I.rcap = std::max<uint32_t>(req_cap, (uint32_t)pt.reqs.size());
+  I.vcap = std::max<uint32_t>(val_cap, (uint32_t)pt.vals.size());
+  if (!I.ptnode.alloc(I.pcap, err) || !I.ptns.alloc(I.pcap, err) || !I.ptflags.alloc(I.pcap, err) ||
+      !I.ptlab.alloc((size_t)I.pcap * std::max<uint32_t>(I.pkeys, 1), err) || !I.terms.alloc(I.tcap, err) ||
+      !I.tpod.alloc(I.tcap, err) || !I.treq.alloc(I.rcap, err) || !I.tval.alloc(I.vcap, err) ||
+      !I.tcounts.alloc(8, err))
+    return false;
+  if (pt.n) {
+    HIPCHK(hipMemcpyAsync(I.ptnode.p, pt.node.data(), pt.n * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(I.ptns.p, pt.ns.data(), pt.n * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(I.ptflags.p, pt.flags.data(), pt.n * 4, hipMemcpyHostToDevice, s));
+    for (uint32_t k = 0; k < pt.n_keys; ++k)
+      HIPCHK(hipMemcpyAsync(I.ptlab.p + (size_t)k * I.pcap, pt.label_vid.data() + (size_t)k * pt.n, pt.n * 4,
+                            hipMemcpyHostToDevice, s));
+  }
+  if (!pt.terms.empty()) {
+    HIPCHK(hipMemcpyAsync(I.terms.p, pt.terms.data(), pt.terms.size() * sizeof(ksg_exist_term), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(I.tpod.p, pt.term_pod.data(), pt.term_pod.size() * 4, hipMemcpyHostToDevice, s));
+  }
+  if (!pt.reqs.empty())
+    HIPCHK(hipMemcpyAsync(I.treq.p, pt.reqs.data(), pt.reqs.size() * sizeof(ksg_req), hipMemcpyHostToDevice, s));
+  if (!pt.vals.empty())
+    HIPCHK(hipMemcpyAsync(I.tval.p, pt.vals.data(), pt.vals.size() * 4, hipMemcpyHostToDevice, s));
+  uint32_t counts[8] = {pt.n, (uint32_t)pt.terms.size(), (uint32_t)pt.reqs.size(), (uint32_t)pt.vals.size(), 0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(I.tcounts.p, counts, sizeof(counts), hipMemcpyHostToDevice, s));
+  // scratch + outputs
+  size_t pairs = std::max<uint32_t>(ns.topo_pairs, 1);
+  if (!I.cnt.alloc((size_t)KSG_MAX_TSC * std::max<uint32_t>(I.N, 1), err) || !I.hist_f.alloc(pairs, err) ||
+      !I.hist_s.alloc(pairs, err) || !I.present_f.alloc(pairs, err) || !I.reg.alloc(pairs, err) ||
+      !I.ipa_aff.alloc(pairs, err) || !I.ipa_anti.alloc(pairs, err) || !I.ipa_exist.alloc(pairs, err) ||
+      !I.ipa_score.alloc(pairs, err) || !I.pts_min.alloc(KSG_MAX_TOPO, err) || !I.pts_dom.alloc(KSG_MAX_TOPO, err) ||
+      !I.exist_any.alloc(1, err) || !I.filter.alloc(std::max<uint32_t>(I.N, 1), err) ||
+      !I.score.alloc((size_t)KSG_MAX_PLUGINS * std::max<uint32_t>(I.N, 1), err) ||
+      !I.total.alloc(std::max<uint32_t>(I.N, 1), err))
+    return false;
+  HIPCHK(hipMemsetAsync(I.exist_any.p, 0, 4, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return true;
+}
+
+bool Engine::set_programs(const std::vector<std::vector<uint8_t>>& progs, std::string& err) {
+  Impl& I = *p_;
+  std::vector<uint8_t> blob;
+  I.prog_off.clear();
+  I.prog_need.clear();
+  for (auto& p : progs) {
+    size_t off = (blob.size() + 255) & ~(size_t)255;  // 256-B aligned programs
+    blob.resize(off);
+    I.prog_off.push_back(off);
+    blob.insert(blob.end(), p.begin(), p.end());
+    const ksg_prog* h = reinterpret_cast<const ksg_prog*>(p.data());
+    uint32_t need = 0;
+    if (h->n_tsc_filter + h->n_tsc_score > 0) need |= 1;
+    need |= 2;  // IPA: existing pods' terms may apply to any pod
+    I.prog_need.push_back(need);
+  }
+  if (!I.progs.upload(blob, I.stream, err)) return false;
+  if (!I.sums.alloc(std::max<size_t>(progs.size(), 1), err)) return false;
+  uint32_t cnt = (uint32_t)progs.size();
+  if (cnt) {
+    hipLaunchKernelGGL(k_init_summaries, dim3((cnt + 255) / 256), dim3(256), 0, I.stream, I.sums.p, cnt, I.F);
+    HIPCHK(hipGetLastError());
+  }
+  return true;
+}
+
+bool Engine::keep_outputs(uint32_t keep_first, uint32_t keep_n, std::string& err) {
+  Impl& I = *p_;
+  I.keep_first = keep_first;
+  I.keep_n = keep_n;
+  if (!keep_n) return true;
+  size_t N = std::max<uint32_t>(I.N, 1);
+  return I.kfilter.alloc(N * keep_n, err) && I.kscore.alloc(N * keep_n * KSG_MAX_PLUGINS, err) &&
+         I.ktotal.alloc(N * keep_n, err);
+}
+
+bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string& err) {
+  Impl& I = *p_;
+  if (first + count > I.prog_off.size()) { err = "program index out of range"; return false; }
+  hipStream_t s = I.stream;
+  DevCluster C = I.cluster();
+  DevScratch S = I.scratch();
+  const DevProfile& F = I.F;
+  uint32_t N = I.N;
+  dim3 gN((N + kBlock - 1) / kBlock), b(kBlock);
+  int pts_pos = -1;
+  for (int i = 0; i < F.n; ++i)
+    if (F.plugins[i] == KP_PTS) pts_pos = i;
+  HIPCHK(hipEventRecord(I.ev0, s));
+  for (uint32_t j = first; j < first + count; ++j) {
+    const uint8_t* prog = I.progs.p + I.prog_off[j];
+    DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j};
+    bool kept = I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n;
+    if (kept) {
+      size_t k = j - I.keep_first;
+      O.filter = I.kfilter.p + k * N;
+      O.score = I.kscore.p + k * N * KSG_MAX_PLUGINS;
+      O.total = I.ktotal.p + k * N;
+    }
+    bool pts = I.has_pts && (I.prog_need[j] & 1);
+    bool ipa = I.has_ipa;
+    if (pts || ipa) {
+      uint32_t work = std::max<uint32_t>(KSG_MAX_TSC * N, I.topo.topo_pairs);
+      uint32_t gb = std::min<uint32_t>((work + kBlock - 1) / kBlock, 2048);
+      hipLaunchKernelGGL(k_begin, dim3(std::max<uint32_t>(gb, 1)), b, 0, s, C, S, prog);
+      uint32_t pc = I.pcap;  // grid covers capacity; kernel reads the live count
+      hipLaunchKernelGGL(k_scan_pods, dim3((pc + kBlock - 1) / kBlock), b, 0, s, C, F, S, O, prog);
+      if (ipa)
+        hipLaunchKernelGGL(k_scan_terms, dim3((I.tcap + kBlock - 1) / kBlock), b, 0, s, C, F, S, O, prog);
+      if (pts) {
+        hipLaunchKernelGGL(k_pts_prep, gN, b, 0, s, C, S, prog);
+        hipLaunchKernelGGL(k_pts_reduce, dim3(std::max<uint32_t>(std::min<uint32_t>(gN.x, 256), 1)), b, 0, s, C, S, prog);
+      }
+    }
+    hipLaunchKernelGGL(k_filter_score, gN, b, 0, s, C, F, S, O, prog);
+    if (F.has_ext) {
+      if (pts_pos >= 0 && pts) {
+        hipLaunchKernelGGL(k_pts_weights, dim3(1), b, 0, s, C, S, O, prog);
+        hipLaunchKernelGGL(k_pts_score, gN, b, 0, s, C, S, O, prog, pts_pos);
+      }
+      hipLaunchKernelGGL(k_finalize, gN, b, 0, s, C, F, S, O, prog);
+    }
+    hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, s, C, F, O, prog, (commit && (I.has_pts || I.has_ipa)) ? 1 : 0);
+    if (!commit) {
+      // what-if: the commit kernel still resolves the selection; undo is not needed
+      // because k_commit only mutates when commit is requested (see below)
+    }
+  }
+  HIPCHK(hipEventRecord(I.ev1, s));
+  HIPCHK(hipGetLastError());
+  return true;
+}
+
+bool Engine::sync(std::string& err) {
+  Impl& I = *p_;
+  HIPCHK(hipStreamSynchronize(I.stream));
+  HIPCHK(hipEventElapsedTime(&I.last_ms, I.ev0, I.ev1));
+  return true;
+}
+
+bool Engine::summaries(uint32_t first, uint32_t count, ksg_pod_summary* out, std::string& err) {
+  Impl& I = *p_;
+  HIPCHK(hipMemcpyAsync(out, I.sums.p + first, count * sizeof(ksg_pod_summary), hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
+bool Engine::outputs(uint32_t j, PodOutputs& out, std::string& err) {
+  Impl& I = *p_;
+  if (!(I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n)) { err = "outputs not kept for this pod"; return false; }
+  size_t N = I.N, k = j - I.keep_first;
+  out.filter.resize(N);
+  out.score.resize(N * KSG_MAX_PLUGINS);
+  out.total.resize(N);
+  HIPCHK(hipMemcpyAsync(out.filter.data(), I.kfilter.p + k * N, N * 4, hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipMemcpyAsync(out.score.data(), I.kscore.p + k * N * KSG_MAX_PLUGINS, N * KSG_MAX_PLUGINS * 4,
+                        hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipMemcpyAsync(out.total.data(), I.ktotal.p + k * N, N * 4, hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipMemcpyAsync(&out.summary, I.sums.p + j, sizeof(ksg_pod_summary), hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
+bool Engine::read_requested(std::vector<int64_t>& requested, std::vector<int32_t>& pod_count, std::string& err) {
+  Impl& I = *p_;
+  requested.resize((size_t)I.R * I.N);
+  pod_count.resize(I.N);
+  HIPCHK(hipMemcpyAsync(requested.data(), I.req.p, requested.size() * 8, hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipMemcpyAsync(pod_count.data(), I.podcnt.p, pod_count.size() * 4, hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
+uint32_t Engine::n_nodes() const { return p_->N; }
+void* Engine::stream() const { return p_->stream; }
+float Engine::last_ms() const { return p_->last_ms; }
+std::vector<Engine::KernelStat> Engine::kernel_stats() const { return p_->stats; }
+
+}  // namespace ksg

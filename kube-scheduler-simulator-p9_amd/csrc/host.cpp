@@ -1,0 +1,1468 @@
+// Host side of the drop-in: Kubernetes objects (JSON) -> interned device
+// snapshot + per-pod programs, result-store rendering, and the C ABI (ksg.h).
+//
+// What the Go cgo package would do natively lives here in C++ (no Go toolchain
+// in this image):  the plugin-facing semantics that are host-known per pod
+// (PreFilter Skip rules, PreFilterResult, PodRequests, toleration sets,
+// selector compilation) are decided here; everything per (pod, node) runs on
+// the GPU (engine.hip).  Recording follows the simulator's wrapper
+// (simulator/scheduler/plugin/wrappedplugin.go:388-548, 616-645) and store
+// (resultstore/store.go:133-507): filter[node][plugin] = "passed" | message
+// up to the first failure, score = raw, finalscore = normalized x store weight
+// (raw x weight for plugins without ScoreExtensions), selected node on Reserve.
+#include <algorithm>
+#include <cctype>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ksg.h"
+#include "engine.h"
+#include "json.hpp"
+
+namespace ksg {
+namespace host {
+
+using std::map;
+using std::set;
+using std::string;
+using std::unordered_map;
+using std::vector;
+typedef long long i64;
+typedef __int128 i128;
+typedef json::Node J;
+
+static const char* kHostname = "kubernetes.io/hostname";
+
+// ---------------------------------------------------------------- small helpers
+static string str_of(const J* n) { return n ? n->text() : string(); }
+static map<string, string> smap(const J* n) {
+  map<string, string> m;
+  if (n && n->t == J::OBJ)
+    for (size_t i = 0; i < n->keys.size(); ++i) m[n->keys[i]] = n->items[i].text();
+  return m;
+}
+static vector<string> slist(const J* n) {
+  vector<string> v;
+  if (n && n->t == J::ARR)
+    for (auto& x : n->items) v.push_back(x.text());
+  return v;
+}
+
+// strconv.ParseInt(s, 10, 64)
+static bool parse_i64(const string& s, i64& out) {
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    if (s.size() == 1) return false;
+    i = 1;
+  }
+  unsigned __int128 v = 0;
+  for (; i < s.size(); ++i) {
+    if (!std::isdigit((unsigned char)s[i])) return false;
+    v = v * 10 + (unsigned)(s[i] - '0');
+    if (v > ((unsigned __int128)1 << 63)) return false;
+  }
+  if (!neg && v > (unsigned __int128)INT64_MAX) return false;
+  out = neg ? (i64)(-(i128)v) : (i64)v;
+  return true;
+}
+
+// resource.Quantity -> exact nano units; Value()/MilliValue() round up.
+static bool quantity(const string& s, i128& nano) {
+  size_t i = 0;
+  bool neg = false;
+  if (i < s.size() && (s[i] == '+' || s[i] == '-')) neg = s[i++] == '-';
+  i128 m = 0;
+  int frac = 0;
+  bool digits = false, dot = false;
+  for (; i < s.size(); ++i) {
+    char c = s[i];
+    if (std::isdigit((unsigned char)c)) {
+      m = m * 10 + (c - '0');
+      digits = true;
+      if (dot) ++frac;
+    } else if (c == '.' && !dot) {
+      dot = true;
+    } else {
+      break;
+    }
+  }
+  if (!digits) return false;
+  string suf = s.substr(i);
+  i128 num = m * 1000000000, den = 1;
+  for (int k = 0; k < frac; ++k) den *= 10;
+  static const char* dec[] = {"n", "u", "m", "", "k", "M", "G", "T", "P", "E"};
+  static const int dexp[] = {-9, -6, -3, 0, 3, 6, 9, 12, 15, 18};
+  static const char* bin[] = {"Ki", "Mi", "Gi", "Ti", "Pi", "Ei"};
+  bool ok = false;
+  for (int k = 0; k < 10 && !ok; ++k)
+    if (suf == dec[k]) {
+      int e = dexp[k];
+      for (; e > 0; --e) num *= 10;
+      for (; e < 0; ++e) den *= 10;
+      ok = true;
+    }
+  for (int k = 0; k < 6 && !ok; ++k)
+    if (suf == bin[k]) {
+      num <<= 10 * (k + 1);
+      ok = true;
+    }
+  if (!ok && !suf.empty() && (suf[0] == 'e' || suf[0] == 'E')) {
+    i64 e;
+    if (!parse_i64(suf.substr(1), e)) return false;
+    for (; e > 0; --e) num *= 10;
+    for (; e < 0; ++e) den *= 10;
+    ok = true;
+  }
+  if (!ok) return false;
+  i128 q = num / den;
+  if (q * den != num) q += 1;
+  nano = neg ? -q : q;
+  return true;
+}
+static i64 up_div(i128 a, i64 b) {
+  i128 q = a / b;
+  if (q * b != a && a > 0) ++q;
+  return (i64)q;
+}
+static i64 as_value(i128 nano) { return up_div(nano, 1000000000LL); }
+static i64 as_milli(i128 nano) { return up_div(nano, 1000000LL); }
+
+typedef map<string, i128> RList;
+static RList rlist(const J* n) {
+  RList r;
+  if (n && n->t == J::OBJ)
+    for (size_t i = 0; i < n->keys.size(); ++i) {
+      i128 q;
+      if (quantity(n->items[i].text(), q)) r[n->keys[i]] = q;
+    }
+  return r;
+}
+static bool scalar_name(const string& n) { return n.find('/') != string::npos || n.rfind("hugepages-", 0) == 0; }
+
+// ---------------------------------------------------------------- API objects
+struct Taint { string key, value, effect; };
+struct Tol {
+  string key, op, value, effect;
+  bool tolerates(const Taint& t) const {
+    if (!effect.empty() && effect != t.effect) return false;
+    if (!key.empty() && key != t.key) return false;
+    if (op.empty() || op == "Equal") return value == t.value;
+    return op == "Exists";
+  }
+};
+static bool tolerated(const vector<Tol>& ts, const Taint& t) {
+  for (auto& x : ts)
+    if (x.tolerates(t)) return true;
+  return false;
+}
+
+struct SelReq { string key, op; vector<string> vals; };
+struct LSel {             // metav1.LabelSelector after LabelSelectorAsSelector
+  bool nothing = true;    // nil selector
+  bool err = false;
+  vector<SelReq> reqs;    // matchLabels as In, then matchExpressions
+  bool matches(const map<string, string>& l) const {
+    if (nothing || err) return false;
+    for (auto& r : reqs) {
+      auto it = l.find(r.key);
+      bool has = it != l.end();
+      bool in = has && std::find(r.vals.begin(), r.vals.end(), it->second) != r.vals.end();
+      bool ok = r.op == "In" ? in : r.op == "NotIn" ? !in : r.op == "Exists" ? has : !has;
+      if (!ok) return false;
+    }
+    return true;
+  }
+};
+static LSel lsel(const J* n) {
+  LSel s;
+  if (!n || n->null()) return s;
+  s.nothing = false;
+  for (auto& kv : smap((*n)["matchLabels"])) s.reqs.push_back({kv.first, "In", {kv.second}});
+  if (auto* ex = (*n)["matchExpressions"])
+    for (auto& e : ex->items) {
+      SelReq r{str_of(e["key"]), str_of(e["operator"]), slist(e["values"])};
+      bool setop = r.op == "In" || r.op == "NotIn";
+      bool exop = r.op == "Exists" || r.op == "DoesNotExist";
+      if (r.key.empty() || (!setop && !exop) || (setop && r.vals.empty()) || (exop && !r.vals.empty())) s.err = true;
+      s.reqs.push_back(r);
+    }
+  return s;
+}
+
+struct ATerm {  // framework.AffinityTerm
+  LSel sel;
+  set<string> namespaces;
+  bool ns_all = false;  // namespaceSelector matches the (label-less) namespaces
+  string topo;
+  int32_t weight = 0;
+};
+static ATerm aterm(const J& t, const string& owner_ns) {
+  ATerm a;
+  a.sel = lsel(t["labelSelector"]);
+  vector<string> nss = slist(t["namespaces"]);
+  const J* nsSel = t["namespaceSelector"];
+  if (nss.empty() && (!nsSel || nsSel->null())) a.namespaces.insert(owner_ns);
+  else a.namespaces.insert(nss.begin(), nss.end());
+  LSel ns = lsel(nsSel);
+  a.ns_all = ns.matches({});  // namespaces carry no labels in this model
+  a.topo = str_of(t["topologyKey"]);
+  return a;
+}
+
+struct TSC {
+  int32_t max_skew = 0;
+  string key, when;
+  const J* sel = nullptr;
+  int32_t min_domains = 1;
+  string aff_policy, taint_policy;
+  vector<string> match_label_keys;
+};
+
+struct Pod {
+  string name, ns;
+  map<string, string> labels;
+  string node;
+  bool terminating = false;
+  RList req, req_nz;  // PodRequests without / with NonMissingContainerRequests
+  bool has_node_sel = false;
+  map<string, string> node_sel;
+  vector<Tol> tols;
+  bool has_req_na = false, has_pref_na = false;
+  vector<const J*> req_terms, pref_terms;
+  bool pod_aff = false, pod_anti = false, pref_aff_present = false, pref_anti_present = false;
+  vector<ATerm> req_aff, req_anti, pref_aff, pref_anti;
+  vector<TSC> tsc;
+};
+
+static RList pod_requests(const J* spec, bool nonzero) {
+  auto fill = [&](RList r) {
+    if (nonzero) {
+      if (!r.count("cpu")) r["cpu"] = (i128)100 * 1000000;                      // DefaultMilliCPURequest
+      if (!r.count("memory")) r["memory"] = (i128)(200LL << 20) * 1000000000;  // DefaultMemoryRequest
+    }
+    return r;
+  };
+  auto add = [](RList& a, const RList& b) {
+    for (auto& kv : b) a[kv.first] += kv.second;
+  };
+  auto mx = [](RList& a, const RList& b) {
+    for (auto& kv : b) {
+      auto it = a.find(kv.first);
+      if (it == a.end() || kv.second > it->second) a[kv.first] = kv.second;
+    }
+  };
+  RList reqs, restartable, init;
+  if (!spec) return reqs;
+  if (auto* cs = (*spec)["containers"])
+    for (auto& c : cs->items) {
+      const J* res = c["resources"];
+      add(reqs, fill(rlist(res ? (*res)["requests"] : nullptr)));
+    }
+  if (auto* cs = (*spec)["initContainers"])
+    for (auto& c : cs->items) {
+      const J* res = c["resources"];
+      RList cr = fill(rlist(res ? (*res)["requests"] : nullptr));
+      if (str_of(c["restartPolicy"]) == "Always") {
+        add(reqs, cr);
+        add(restartable, cr);
+        cr = restartable;
+      } else {
+        RList t;
+        add(t, cr);
+        add(t, restartable);
+        cr = t;
+      }
+      mx(init, cr);
+    }
+  mx(reqs, init);
+  add(reqs, rlist((*spec)["overhead"]));
+  return reqs;
+}
+
+static Pod parse_pod(const J& v) {
+  Pod p;
+  const J* md = v["metadata"];
+  const J* sp = v["spec"];
+  p.name = md ? str_of((*md)["name"]) : "";
+  p.ns = md ? str_of((*md)["namespace"]) : "";
+  if (p.ns.empty()) p.ns = "default";
+  p.labels = smap(md ? (*md)["labels"] : nullptr);
+  p.terminating = md && (*md)["deletionTimestamp"] && !(*md)["deletionTimestamp"]->null();
+  p.req = pod_requests(sp, false);
+  p.req_nz = pod_requests(sp, true);
+  if (!sp) return p;
+  p.node = str_of((*sp)["nodeName"]);
+  if (auto* ns = (*sp)["nodeSelector"]; ns && !ns->null()) {
+    p.has_node_sel = true;
+    p.node_sel = smap(ns);
+  }
+  if (auto* ts = (*sp)["tolerations"])
+    for (auto& t : ts->items) p.tols.push_back({str_of(t["key"]), str_of(t["operator"]), str_of(t["value"]), str_of(t["effect"])});
+  if (auto* aff = (*sp)["affinity"]; aff && !aff->null()) {
+    if (auto* na = (*aff)["nodeAffinity"]; na && !na->null()) {
+      if (auto* rq = (*na)["requiredDuringSchedulingIgnoredDuringExecution"]; rq && !rq->null()) {
+        p.has_req_na = true;
+        if (auto* ts = (*rq)["nodeSelectorTerms"])
+          for (auto& t : ts->items) p.req_terms.push_back(&t);
+      }
+      if (auto* pf = (*na)["preferredDuringSchedulingIgnoredDuringExecution"]; pf && !pf->null()) {
+        p.has_pref_na = true;
+        for (auto& t : pf->items) p.pref_terms.push_back(&t);
+      }
+    }
+    auto pa = [&](const char* k, bool& present, vector<ATerm>& rq, vector<ATerm>& pf, bool& pf_present) {
+      const J* x = (*aff)[k];
+      if (!x || x->null()) return;
+      present = true;
+      if (auto* r = (*x)["requiredDuringSchedulingIgnoredDuringExecution"])
+        for (auto& t : r->items) rq.push_back(aterm(t, p.ns));
+      if (auto* f = (*x)["preferredDuringSchedulingIgnoredDuringExecution"]; f && !f->null()) {
+        pf_present = f->size() > 0;
+        for (auto& t : f->items) {
+          const J* pt = t["podAffinityTerm"];
+          ATerm a = pt ? aterm(*pt, p.ns) : ATerm();
+          a.weight = (int32_t)(t["weight"] ? t["weight"]->num() : 0);
+          pf.push_back(a);
+        }
+      }
+    };
+    pa("podAffinity", p.pod_aff, p.req_aff, p.pref_aff, p.pref_aff_present);
+    pa("podAntiAffinity", p.pod_anti, p.req_anti, p.pref_anti, p.pref_anti_present);
+  }
+  if (auto* ts = (*sp)["topologySpreadConstraints"])
+    for (auto& c : ts->items) {
+      TSC t;
+      t.max_skew = (int32_t)(c["maxSkew"] ? c["maxSkew"]->num() : 0);
+      t.key = str_of(c["topologyKey"]);
+      t.when = str_of(c["whenUnsatisfiable"]);
+      t.sel = c["labelSelector"];
+      if (c["minDomains"] && !c["minDomains"]->null()) t.min_domains = (int32_t)c["minDomains"]->num();
+      t.aff_policy = str_of(c["nodeAffinityPolicy"]);
+      t.taint_policy = str_of(c["nodeTaintsPolicy"]);
+      t.match_label_keys = slist(c["matchLabelKeys"]);
+      p.tsc.push_back(t);
+    }
+  return p;
+}
+
+struct Node {
+  string name;
+  map<string, string> labels;
+  vector<Taint> taints;
+  RList alloc;
+};
+static Node parse_node(const J& v) {
+  Node n;
+  const J* md = v["metadata"];
+  n.name = md ? str_of((*md)["name"]) : "";
+  n.labels = smap(md ? (*md)["labels"] : nullptr);
+  if (auto* sp = v["spec"])
+    if (auto* ts = (*sp)["taints"])
+      for (auto& t : ts->items) n.taints.push_back({str_of(t["key"]), str_of(t["value"]), str_of(t["effect"])});
+  const J* st = v["status"];
+  n.alloc = rlist(st ? (*st)["allocatable"] : nullptr);
+  return n;
+}
+
+// ---------------------------------------------------------------- interning
+struct Dict {
+  unordered_map<string, int32_t> id;
+  vector<string> names;
+  int32_t get(const string& s) const {
+    auto it = id.find(s);
+    return it == id.end() ? -1 : it->second;
+  }
+  int32_t add(const string& s) {
+    auto it = id.find(s);
+    if (it != id.end()) return it->second;
+    id.emplace(s, (int32_t)names.size());
+    names.push_back(s);
+    return (int32_t)names.size() - 1;
+  }
+};
+
+enum { P_FIT = KP_FIT, P_BA = KP_BA, P_TAINT = KP_TAINT, P_NA = KP_NA, P_PTS = KP_PTS, P_IPA = KP_IPA };
+static const char* kPluginNames[] = {"NodeResourcesFit", "NodeResourcesBalancedAllocation", "TaintToleration",
+                                     "NodeAffinity", "PodTopologySpread", "InterPodAffinity"};
+static int plugin_id(const string& n) {
+  for (int i = 0; i < 6; ++i)
+    if (n == kPluginNames[i]) return i;
+  return -1;
+}
+static bool has_prefilter(int p) { return p == P_FIT || p == P_NA || p == P_PTS || p == P_IPA; }
+static bool has_filter(int p) { return p != P_BA; }
+static bool has_ext(int p) { return p == P_TAINT || p == P_NA || p == P_PTS || p == P_IPA; }
+
+// Per-pod host-known facts the renderer needs besides the device outputs.
+struct PodMeta {
+  uint32_t flags = 0;
+  string prefilter_fail_msg;  // PreFilter rejection (NodeAffinity conflict)
+  int prefilter_fail_pos = -1;
+  bool prefilter_error = false;
+  bool restricted = false;
+  vector<string> prefilter_names;  // NodeAffinity PreFilterResult
+  bool ipa_no_req_terms = true;
+  bool ipa_prescore_skip_static = false;
+  bool na_prescore_error = false;
+};
+
+struct Cluster {
+  // profile
+  int n_plugins = 0;
+  int plugins[KSG_MAX_PLUGINS] = {};
+  string names[KSG_MAX_PLUGINS];
+  i64 fw_w[KSG_MAX_PLUGINS] = {}, store_w[KSG_MAX_PLUGINS] = {};
+  EngineConfig ecfg;
+  vector<string> fit_res_names{"cpu", "memory"}, ba_res_names{"cpu", "memory"};
+  i64 ipa_hard = 1;
+  bool ipa_ignore = false;
+  // objects
+  vector<Node> nodes;
+  Dict node_names;
+  vector<Pod> bound;
+  vector<Pod> queue;
+  // vocabularies
+  Dict res;  // resource columns
+  Dict nkeys;
+  vector<Dict> nvals;
+  Dict pkeys;
+  vector<Dict> pvals;
+  Dict nss;
+  std::map<std::tuple<string, string, string>, int32_t> taint_id;
+  vector<Taint> taints;
+  Dict topo;  // topology key name -> slot
+  // shard
+  uint32_t rank = 0, shards = 1, lo = 0, hi = 0;
+  // device
+  std::unique_ptr<Engine> eng;
+  vector<PodMeta> meta;
+  bool compiled = false;
+  uint32_t keep_first = 0, keep_n = 0;
+  string err;
+
+  // ------------------------------------------------------------ profile
+  bool load_profile(const J& pr) {
+    const J* pl = pr["plugins"];
+    if (!pl) { err = "profile.plugins missing"; return false; }
+    for (auto& x : pl->items) {
+      int id = plugin_id(x.text());
+      if (id < 0) { err = "unsupported plugin " + x.text(); return false; }
+      if (n_plugins >= KSG_MAX_PLUGINS) { err = "too many plugins"; return false; }
+      names[n_plugins] = x.text();
+      plugins[n_plugins++] = id;
+    }
+    auto weights = smap(pr["weights"]), sw = smap(pr["storeWeights"]);
+    for (int i = 0; i < n_plugins; ++i) {
+      i64 w = 0, s = 0;
+      if (weights.count(names[i])) parse_i64(weights[names[i]], w);
+      if (sw.count(names[i])) parse_i64(sw[names[i]], s);
+      fw_w[i] = w == 0 ? 1 : w;
+      store_w[i] = sw.count(names[i]) ? (s == 0 ? 1 : s) : 0;
+    }
+    if (const J* s = pr["seed"]) ecfg.seed = std::strtoull(s->text().c_str(), nullptr, 10);
+    if (const J* pc = pr["pluginConfig"]) {
+      if (const J* fit = (*pc)["NodeResourcesFit"])
+        if (const J* ss = (*fit)["scoringStrategy"]) {
+          string t = str_of((*ss)["type"]);
+          ecfg.fit_strategy = t == "MostAllocated" ? 1 : t == "RequestedToCapacityRatio" ? 2 : 0;
+          if (const J* rs = (*ss)["resources"]) {
+            fit_res_names.clear();
+            ecfg.fit_n = 0;
+            for (auto& r : rs->items) {
+              if (ecfg.fit_n >= KSG_MAX_SCORE_RES) break;
+              fit_res_names.push_back(str_of(r["name"]));
+              ecfg.fit_w[ecfg.fit_n++] = r["weight"] ? r["weight"]->num() : 1;
+            }
+          }
+          if (const J* rtc = (*ss)["requestedToCapacityRatio"])
+            if (const J* sh = (*rtc)["shape"])
+              for (auto& pt : sh->items) {
+                if (ecfg.rtc_n >= KSG_MAX_RTC) break;
+                ecfg.rtc_util[ecfg.rtc_n] = pt["utilization"]->num();
+                ecfg.rtc_score[ecfg.rtc_n++] = pt["score"]->num() * (100 / 10);  // MaxNodeScore / MaxCustomPriorityScore
+              }
+        }
+      if (const J* ba = (*pc)["NodeResourcesBalancedAllocation"])
+        if (const J* rs = (*ba)["resources"]) {
+          ba_res_names.clear();
+          for (auto& r : rs->items)
+            if (ba_res_names.size() < KSG_MAX_SCORE_RES) ba_res_names.push_back(str_of(r["name"]));
+        }
+      if (const J* ipa = (*pc)["InterPodAffinity"]) {
+        if (const J* h = (*ipa)["hardPodAffinityWeight"]) ipa_hard = h->num();
+        if (const J* ig = (*ipa)["ignorePreferredTermsOfExistingPods"]) ipa_ignore = ig->b;
+      }
+    }
+    ecfg.n_plugins = n_plugins;
+    for (int i = 0; i < n_plugins; ++i) {
+      ecfg.plugins[i] = plugins[i];
+      ecfg.weight[i] = fw_w[i];
+    }
+    ecfg.ba_n = (int)ba_res_names.size();
+    ecfg.ipa_hard_weight = ipa_hard;
+    ecfg.ipa_ignore_existing_pref = ipa_ignore;
+    return true;
+  }
+
+  int pos_of(int plugin) const {
+    for (int i = 0; i < n_plugins; ++i)
+      if (plugins[i] == plugin) return i;
+    return -1;
+  }
+
+  // ------------------------------------------------------------ vocabularies
+  void intern_pod_labels(const Pod& p) {
+    nss.add(p.ns);
+    for (auto& kv : p.labels) {
+      int32_t k = pkeys.add(kv.first);
+      if ((int32_t)pvals.size() <= k) pvals.resize(k + 1);
+      pvals[k].add(kv.second);
+    }
+    auto topo_of = [&](const string& key) { topo.add(key); nkeys.add(key); };
+    for (auto* v : {&p.req_aff, &p.req_anti, &p.pref_aff, &p.pref_anti})
+      for (auto& t : *v) topo_of(t.topo);
+    for (auto& c : p.tsc) topo_of(c.key);
+  }
+
+  bool build_vocab() {
+    res = Dict();
+    res.add("cpu");
+    res.add("memory");
+    res.add("ephemeral-storage");
+    set<string> scal;
+    for (auto& n : nodes)
+      for (auto& kv : n.alloc)
+        if (scalar_name(kv.first)) scal.insert(kv.first);
+    for (auto* v : {&bound, &queue})
+      for (auto& p : *v)
+        for (auto& kv : p.req)
+          if (scalar_name(kv.first)) scal.insert(kv.first);
+    for (auto& s : scal) res.add(s);  // sorted: Fit reasons come out in name order
+    if (res.names.size() > KSG_MAX_RES) { err = "too many scalar resources"; return false; }
+    for (auto& n : nodes)
+      for (auto& kv : n.labels) {
+        int32_t k = nkeys.add(kv.first);
+        if ((int32_t)nvals.size() <= k) nvals.resize(k + 1);
+        nvals[k].add(kv.second);
+      }
+    for (auto& n : nodes)
+      for (auto& t : n.taints) {
+        auto key = std::make_tuple(t.key, t.value, t.effect);
+        if (!taint_id.count(key)) {
+          taint_id[key] = (int32_t)taints.size();
+          taints.push_back(t);
+        }
+      }
+    for (auto* v : {&bound, &queue})
+      for (auto& p : *v) intern_pod_labels(p);
+    if (nvals.size() < nkeys.names.size()) nvals.resize(nkeys.names.size());
+    if (topo.names.size() > KSG_MAX_TOPO) { err = "too many topology keys"; return false; }
+    if (fit_res_names.size() > KSG_MAX_SCORE_RES || ba_res_names.size() > KSG_MAX_SCORE_RES) {
+      err = "too many scoring resources";
+      return false;
+    }
+    for (size_t i = 0; i < fit_res_names.size(); ++i) ecfg.fit_res[i] = res.get(fit_res_names[i]);
+    for (size_t i = 0; i < ba_res_names.size(); ++i) ecfg.ba_res[i] = res.get(ba_res_names[i]);
+    return true;
+  }
+
+  // ------------------------------------------------------------ snapshot encode
+  void add_requests(const Pod& p, vector<i64>& out_req, i64& nzc, i64& nzm) {
+    out_req.assign(res.names.size(), 0);
+    for (auto& kv : p.req) {
+      int32_t r = res.get(kv.first);
+      if (r < 0) continue;
+      out_req[r] += r == 0 ? as_milli(kv.second) : as_value(kv.second);
+    }
+    auto c = p.req_nz.find("cpu");
+    auto m = p.req_nz.find("memory");
+    nzc = c == p.req_nz.end() ? 0 : as_milli(c->second);
+    nzm = m == p.req_nz.end() ? 0 : as_value(m->second);
+  }
+
+  int32_t pkey_vid(int32_t key, const string& v) const {
+    if (key < 0 || key >= (int32_t)pvals.size()) return -2;
+    int32_t x = pvals[key].get(v);
+    return x < 0 ? -2 : x;
+  }
+
+  // label selector -> reqs over pod-label space into (reqs, vals)
+  void compile_lsel(const LSel& s, ksg_sel& out, vector<ksg_req>& reqs, vector<int32_t>& vals) {
+    out.kind = s.nothing ? 0 : 1;
+    out.req_off = (int32_t)reqs.size();
+    out.req_cnt = 0;
+    out.pad = 0;
+    if (s.nothing) return;
+    if (s.err) {  // unparsable selector never matches
+      out.kind = 0;
+      return;
+    }
+    for (auto& r : s.reqs) {
+      ksg_req q{};
+      q.key = pkeys.get(r.key);
+      q.op = r.op == "In" ? KR_IN : r.op == "NotIn" ? KR_NOT_IN : r.op == "Exists" ? KR_EXISTS : KR_NOT_EXISTS;
+      q.val_off = (int32_t)vals.size();
+      for (auto& v : r.vals) vals.push_back(pkey_vid(q.key, v));
+      q.nvals = (int32_t)r.vals.size();
+      if (q.key < 0) q.key = -1;
+      reqs.push_back(q);
+      out.req_cnt++;
+    }
+  }
+
+  bool encode_snapshot(NodeSoA& S, PodTableSoA& T) {
+    uint32_t G = (uint32_t)nodes.size();
+    lo = (uint32_t)((uint64_t)G * rank / shards);
+    hi = (uint32_t)((uint64_t)G * (rank + 1) / shards);
+    uint32_t n = hi - lo, R = (uint32_t)res.names.size(), K = (uint32_t)nkeys.names.size();
+    S = NodeSoA();
+    S.n = n;
+    S.global_offset = lo;
+    S.n_res = R;
+    S.n_keys = K;
+    S.alloc.assign((size_t)R * n, 0);
+    S.requested.assign((size_t)R * n, 0);
+    S.nz_cpu.assign(n, 0);
+    S.nz_mem.assign(n, 0);
+    S.allowed_pods.assign(n, 0);
+    S.pod_count.assign(n, 0);
+    S.label_vid.assign((size_t)K * n, -1);
+    S.has_labels.assign(n, 0);
+    S.taint_off.assign(n + 1, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+      const Node& nd = nodes[lo + i];
+      for (auto& kv : nd.alloc) {
+        if (kv.first == "pods") S.allowed_pods[i] = (int32_t)as_value(kv.second);
+        int32_t r = res.get(kv.first);
+        if (r >= 0) S.alloc[(size_t)r * n + i] = r == 0 ? as_milli(kv.second) : as_value(kv.second);
+      }
+      for (auto& kv : nd.labels) S.label_vid[(size_t)nkeys.get(kv.first) * n + i] = nvals[nkeys.get(kv.first)].get(kv.second);
+      S.has_labels[i] = !nd.labels.empty();
+      for (auto& t : nd.taints) S.taint_id.push_back(taint_id[std::make_tuple(t.key, t.value, t.effect)]);
+      S.taint_off[i + 1] = (uint32_t)S.taint_id.size();
+    }
+    S.key_val_off.assign(K + 1, 0);
+    for (uint32_t k = 0; k < K; ++k) {
+      S.key_val_off[k + 1] = S.key_val_off[k] + (uint32_t)nvals[k].names.size();
+      for (auto& v : nvals[k].names) {
+        i64 x = 0;
+        bool ok = parse_i64(v, x);
+        S.val_num.push_back(ok ? x : 0);
+        S.val_num_ok.push_back(ok ? 1 : 0);
+      }
+    }
+    uint32_t pairs = 0;
+    for (auto& tk : topo.names) {
+      int32_t k = nkeys.get(tk);
+      S.topo_key.push_back(k);
+      S.topo_base.push_back(pairs);
+      uint32_t c = k < 0 ? 0 : (uint32_t)nvals[k].names.size();
+      S.topo_count.push_back(c);
+      pairs += c;
+    }
+    S.topo_pairs = pairs;
+    // bound pods: NodeInfo aggregates + existing-pod table (this shard's nodes)
+    T = PodTableSoA();
+    T.n_keys = (uint32_t)pkeys.names.size();
+    vector<i64> rq;
+    vector<vector<int32_t>> lab;
+    for (auto& p : bound) {
+      int32_t g = node_names.get(p.node);
+      if (g < 0 || (uint32_t)g < lo || (uint32_t)g >= hi) continue;
+      uint32_t i = (uint32_t)g - lo;
+      i64 nzc, nzm;
+      add_requests(p, rq, nzc, nzm);
+      for (uint32_t r = 0; r < R; ++r) S.requested[(size_t)r * n + i] += rq[r];
+      S.nz_cpu[i] += nzc;
+      S.nz_mem[i] += nzm;
+      S.pod_count[i] += 1;
+      T.node.push_back((int32_t)i);
+      T.ns.push_back(nss.get(p.ns));
+      T.flags.push_back(exist_flags(p));
+      vector<int32_t> l(T.n_keys, -1);
+      for (auto& kv : p.labels) l[pkeys.get(kv.first)] = pvals[pkeys.get(kv.first)].get(kv.second);
+      lab.push_back(l);
+      append_terms(p, (int32_t)T.n, T.terms, T.term_pod, T.reqs, T.vals);
+      T.n++;
+    }
+    T.label_vid.assign((size_t)T.n_keys * T.n, -1);
+    for (uint32_t r = 0; r < T.n; ++r)
+      for (uint32_t k = 0; k < T.n_keys; ++k) T.label_vid[(size_t)k * T.n + r] = lab[r][k];
+    return true;
+  }
+
+  static uint32_t exist_flags(const Pod& p) {
+    uint32_t f = 0;
+    if (p.terminating) f |= KEF_TERMINATING;
+    if (p.pod_aff || p.pod_anti) f |= KEF_WITH_AFFINITY;
+    if (!p.req_anti.empty()) f |= KEF_REQ_ANTI;
+    return f;
+  }
+
+  // existing pod's terms (PodInfo.RequiredAffinityTerms etc., not namespace-merged)
+  void append_terms(const Pod& p, int32_t row, vector<ksg_exist_term>& terms, vector<int32_t>* term_pod_v,
+                    vector<ksg_req>& reqs, vector<int32_t>& vals) {
+    auto add = [&](const ATerm& a, int kind) {
+      ksg_exist_term e{};
+      e.kind = kind;
+      e.weight = a.weight;
+      e.topo = topo.get(a.topo);
+      e.topo_key = nkeys.get(a.topo);
+      compile_lsel(a.sel, e.sel, reqs, vals);
+      e.ns_all = a.ns_all ? 1 : 0;
+      e.ns_off = (int32_t)vals.size();
+      for (auto& ns : a.namespaces) vals.push_back(nss.get(ns) < 0 ? -2 : nss.get(ns));
+      e.ns_cnt = (int32_t)a.namespaces.size();
+      terms.push_back(e);
+      if (term_pod_v) term_pod_v->push_back(row);
+    };
+    for (auto& t : p.req_aff) add(t, 0);
+    for (auto& t : p.req_anti) add(t, 1);
+    for (auto& t : p.pref_aff) add(t, 2);
+    for (auto& t : p.pref_anti) add(t, 3);
+  }
+  void append_terms(const Pod& p, int32_t row, vector<ksg_exist_term>& terms, vector<int32_t>& term_pod,
+                    vector<ksg_req>& reqs, vector<int32_t>& vals) {
+    append_terms(p, row, terms, &term_pod, reqs, vals);
+  }
+
+  // ------------------------------------------------------------ pod program
+  struct Prog {
+    ksg_prog h{};
+    vector<int32_t> i32;
+    vector<uint32_t> u32;
+    vector<ksg_req> req;
+    vector<ksg_sel> sel;
+    vector<ksg_aterm> at;
+    vector<ksg_exist_term> et;
+  };
+
+  int32_t nval(int32_t key, const string& v) const {
+    if (key < 0 || key >= (int32_t)nvals.size()) return -2;
+    int32_t x = nvals[key].get(v);
+    return x < 0 ? -2 : x;
+  }
+
+  // node selector term (component-helpers nodeSelectorTerm); false on parse error
+  bool compile_node_term(const J& t, Prog& P, ksg_sel& out) {
+    out = ksg_sel{1, (int32_t)P.req.size(), 0, 0};
+    vector<ksg_req> rs;
+    if (const J* me = t["matchExpressions"])
+      for (auto& e : me->items) {
+        string op = str_of(e["operator"]), key = str_of(e["key"]);
+        vector<string> vals = slist(e["values"]);
+        ksg_req q{};
+        q.key = nkeys.get(key);
+        if (op == "In" || op == "NotIn") {
+          if (vals.empty()) return false;
+          q.op = op == "In" ? KR_IN : KR_NOT_IN;
+          q.val_off = (int32_t)P.i32.size();
+          for (auto& v : vals) P.i32.push_back(nval(q.key, v));
+          q.nvals = (int32_t)vals.size();
+        } else if (op == "Exists" || op == "DoesNotExist") {
+          if (!vals.empty()) return false;
+          q.op = op == "Exists" ? KR_EXISTS : KR_NOT_EXISTS;
+        } else if (op == "Gt" || op == "Lt") {
+          i64 thr = 0;
+          if (vals.size() != 1 || !parse_i64(vals[0], thr)) return false;
+          q.num = thr;
+          q.op = op == "Gt" ? KR_GT : KR_LT;
+        } else {
+          return false;
+        }
+        if (key.empty()) return false;
+        rs.push_back(q);
+      }
+    if (const J* mf = t["matchFields"])
+      for (auto& e : mf->items) {
+        string op = str_of(e["operator"]), key = str_of(e["key"]);
+        vector<string> vals = slist(e["values"]);
+        if ((op != "In" && op != "NotIn") || vals.size() != 1) return false;
+        ksg_req q{};
+        q.key = -1;
+        if (key == "metadata.name") {
+          q.op = op == "In" ? KR_NAME_EQ : KR_NAME_NE;
+          q.num = node_names.get(vals[0]);  // -1: no such node
+        } else {  // other fields read "" on a node
+          bool eq = vals[0].empty();
+          bool match = op == "In" ? eq : !eq;
+          q.op = match ? KR_NAME_NE : KR_FALSE;
+          q.num = -1;
+        }
+        rs.push_back(q);
+      }
+    for (auto& q : rs) P.req.push_back(q);
+    out.req_cnt = (int32_t)rs.size();
+    return true;
+  }
+
+  static bool term_empty(const J& t) {
+    const J* me = t["matchExpressions"];
+    const J* mf = t["matchFields"];
+    return (!me || me->size() == 0) && (!mf || mf->size() == 0);
+  }
+
+  void fill_aterm(const ATerm& a, Prog& P, ksg_aterm& t) {
+    t = ksg_aterm{};
+    compile_lsel(a.sel, t.sel, P.req, P.i32);
+    t.topo = topo.get(a.topo);
+    t.topo_key = nkeys.get(a.topo);
+    t.ns_all = a.ns_all ? 1 : 0;
+    t.ns_off = (int32_t)P.i32.size();
+    for (auto& ns : a.namespaces) P.i32.push_back(nss.get(ns) < 0 ? -2 : nss.get(ns));
+    t.ns_cnt = (int32_t)a.namespaces.size();
+    t.weight = a.weight;
+  }
+
+  bool compile(const Pod& p, int32_t qidx, vector<uint8_t>& blob, PodMeta& m) {
+    Prog P;
+    ksg_prog& h = P.h;
+    h.queue_idx = qidx;
+    h.ns_id = nss.get(p.ns);
+    uint32_t R = (uint32_t)res.names.size();
+    // incoming pod labels (pod-label space)
+    h.n_pod_label_keys = (int32_t)pkeys.names.size();
+    h.labels_off = 0;
+    P.i32.assign(pkeys.names.size(), -1);
+    for (auto& kv : p.labels) P.i32[pkeys.get(kv.first)] = pvals[pkeys.get(kv.first)].get(kv.second);
+    // ---- resources
+    vector<i64> rq;
+    i64 nzc = 0, nzm = 0;
+    add_requests(p, rq, nzc, nzm);
+    h.nz_cpu = nzc;
+    h.nz_mem = nzm;
+    bool any_scalar = false;
+    for (auto& kv : p.req)
+      if (scalar_name(kv.first)) any_scalar = true;
+    bool zero = !any_scalar;
+    for (uint32_t r = 0; r < R && r < 3; ++r) zero &= rq[r] == 0;
+    for (uint32_t r = 0; r < R; ++r) h.req[r] = rq[r];
+    if (zero) h.flags |= KPF_ZERO_REQUEST;
+    auto res_req = [&](const string& name, bool nonzero) -> i64 {
+      const RList& l = nonzero ? p.req_nz : p.req;
+      auto it = l.find(name);
+      if (it == l.end()) return 0;
+      return name == "cpu" ? as_milli(it->second) : as_value(it->second);
+    };
+    for (size_t i = 0; i < fit_res_names.size(); ++i) h.fit_score_req[i] = res_req(fit_res_names[i], true);
+    for (size_t i = 0; i < ba_res_names.size(); ++i) h.ba_req[i] = res_req(ba_res_names[i], false);
+    // ---- TaintToleration
+    uint32_t words = ((uint32_t)taints.size() + 31) / 32;
+    h.taint_words = (int32_t)words;
+    h.taint_hard_off = (int32_t)P.u32.size();
+    P.u32.resize(P.u32.size() + words, 0);
+    h.taint_pref_off = (int32_t)P.u32.size();
+    P.u32.resize(P.u32.size() + words, 0);
+    vector<Tol> pref_tols;
+    for (auto& t : p.tols)
+      if (t.effect.empty() || t.effect == "PreferNoSchedule") pref_tols.push_back(t);
+    for (size_t t = 0; t < taints.size(); ++t) {
+      const Taint& tt = taints[t];
+      if ((tt.effect == "NoSchedule" || tt.effect == "NoExecute") && !tolerated(p.tols, tt))
+        P.u32[h.taint_hard_off + t / 32] |= 1u << (t % 32);
+      if (tt.effect == "PreferNoSchedule" && !tolerated(pref_tols, tt))
+        P.u32[h.taint_pref_off + t / 32] |= 1u << (t % 32);
+    }
+    // ---- NodeAffinity
+    if (!p.has_req_na && !p.has_node_sel) h.flags |= KPF_SKIP_NA_FILTER;
+    if (!p.node_sel.empty()) {
+      h.flags |= KPF_HAS_NODE_SEL;
+      h.node_sel = ksg_sel{1, (int32_t)P.req.size(), 0, 0};
+      for (auto& kv : p.node_sel) {
+        ksg_req q{};
+        q.key = nkeys.get(kv.first);
+        q.op = KR_IN;
+        q.val_off = (int32_t)P.i32.size();
+        P.i32.push_back(nval(q.key, kv.second));
+        q.nvals = 1;
+        P.req.push_back(q);
+        h.node_sel.req_cnt++;
+      }
+    }
+    if (p.has_req_na) {
+      h.flags |= KPF_HAS_REQ_NA;
+      vector<ksg_sel> terms;
+      for (auto* t : p.req_terms) {
+        if (term_empty(*t)) continue;
+        ksg_sel s;
+        size_t r0 = P.req.size(), v0 = P.i32.size();
+        if (compile_node_term(*t, P, s)) terms.push_back(s);
+        else { P.req.resize(r0); P.i32.resize(v0); }  // parse error: term never matches
+      }
+      h.req_terms_off = (int32_t)P.sel.size();
+      h.n_req_terms = (int32_t)terms.size();
+      for (auto& s : terms) P.sel.push_back(s);
+      // PreFilterResult from matchFields metadata.name In (node_affinity.go PreFilter)
+      if (!p.req_terms.empty()) {
+        bool names_nil = true, all_named = true;
+        set<string> names;
+        for (auto* t : p.req_terms) {
+          bool tnil = true;
+          set<string> tn;
+          if (const J* mf = (*t)["matchFields"])
+            for (auto& r : mf->items)
+              if (str_of(r["key"]) == "metadata.name" && str_of(r["operator"]) == "In") {
+                vector<string> v = slist(r["values"]);
+                set<string> s(v.begin(), v.end());
+                if (tnil) { tn = s; tnil = false; }
+                else {
+                  set<string> x;
+                  for (auto& a : tn)
+                    if (s.count(a)) x.insert(a);
+                  tn = x;
+                }
+              }
+          if (tnil) { all_named = false; break; }
+          names_nil = false;
+          names.insert(tn.begin(), tn.end());
+        }
+        if (all_named && !names_nil) {
+          if (names.empty()) {
+            m.prefilter_fail_pos = pos_of(P_NA);
+            m.prefilter_fail_msg = "pod affinity terms conflict";
+            h.flags |= KPF_PREFILTER_REJECT;
+          } else {
+            m.restricted = true;
+            m.prefilter_names.assign(names.begin(), names.end());
+            h.flags |= KPF_RESTRICT;
+            uint32_t n = hi - lo, w = (n + 31) / 32;
+            h.restrict_words = (int32_t)w;
+            h.restrict_off = (int32_t)P.u32.size();
+            P.u32.resize(P.u32.size() + w, 0);
+            for (auto& nm : names) {
+              int32_t g = node_names.get(nm);
+              if (g >= (int32_t)lo && g < (int32_t)hi) P.u32[h.restrict_off + (g - lo) / 32] |= 1u << ((g - lo) % 32);
+            }
+          }
+        }
+      }
+    }
+    if (!p.has_pref_na) h.flags |= KPF_SKIP_NA_SCORE;
+    else {
+      h.pref_terms_off = (int32_t)P.sel.size();
+      vector<std::pair<ksg_sel, int32_t>> pts;
+      bool bad = false;
+      for (auto* t : p.pref_terms) {
+        i64 w = (*t)["weight"] ? (*t)["weight"]->num() : 0;
+        const J* pref = (*t)["preference"];
+        if (w == 0 || !pref || term_empty(*pref)) continue;
+        ksg_sel s;
+        if (!compile_node_term(*pref, P, s)) { bad = true; continue; }
+        pts.push_back({s, (int32_t)w});
+      }
+      if (bad) { m.na_prescore_error = true; h.flags |= KPF_NA_PREF_ERROR; }
+      h.n_pref_terms = (int32_t)pts.size();
+      h.pref_w_off = (int32_t)P.i32.size();
+      for (auto& x : pts) { P.sel.push_back(x.first); P.i32.push_back(x.second); }
+    }
+    // ---- PodTopologySpread
+    auto build_tsc = [&](const string& when, int& count) -> bool {
+      count = 0;
+      for (auto& c : p.tsc) {
+        if (c.when != when) continue;
+        int idx = h.n_tsc_filter + h.n_tsc_score + count;
+        if (idx >= KSG_MAX_TSC) { err = "too many topology spread constraints"; return false; }
+        ksg_tsc& t = h.tsc[idx];
+        t = ksg_tsc{};
+        LSel s = lsel(c.sel);
+        if (!c.match_label_keys.empty() && !s.nothing) {
+          for (auto& k : c.match_label_keys) {
+            auto it = p.labels.find(k);
+            if (it != p.labels.end()) s.reqs.push_back({k, "In", {it->second}});
+          }
+        }
+        if (s.err) m.prefilter_error = true;
+        compile_lsel(s, t.sel, P.req, P.i32);
+        t.topo = topo.get(c.key);
+        t.topo_key = nkeys.get(c.key);
+        t.max_skew = c.max_skew;
+        t.min_domains = c.min_domains;
+        t.honor_affinity = c.aff_policy.empty() || c.aff_policy == "Honor";
+        t.honor_taints = c.taint_policy == "Honor";
+        t.self_match = s.matches(p.labels) ? 1 : 0;
+        t.is_hostname = c.key == kHostname;
+        count++;
+      }
+      return true;
+    };
+    int nf = 0, ns = 0;
+    if (!build_tsc("DoNotSchedule", nf)) return false;
+    h.n_tsc_filter = nf;
+    if (!build_tsc("ScheduleAnyway", ns)) return false;
+    h.n_tsc_score = ns;
+    for (int i = nf; i < nf + ns; ++i) {
+      ksg_tsc& t = h.tsc[i];
+      t.first_of_key = 1;
+      for (int j = nf; j < i; ++j)
+        if (h.tsc[j].topo_key == t.topo_key && !h.tsc[j].is_hostname) t.first_of_key = 0;
+    }
+    if (nf == 0) h.flags |= KPF_SKIP_PTS_FILTER;
+    if (ns == 0) h.flags |= KPF_SKIP_PTS_SCORE;
+    // ---- InterPodAffinity (incoming terms; namespaceSelector merged)
+    h.aterm_off = (int32_t)P.at.size();
+    for (auto* v : {&p.req_aff, &p.req_anti, &p.pref_aff, &p.pref_anti})
+      for (auto& a : *v) {
+        ksg_aterm t;
+        fill_aterm(a, P, t);
+        P.at.push_back(t);
+        if (a.sel.err) m.prefilter_error = true;
+      }
+    h.n_req_aff = (int32_t)p.req_aff.size();
+    h.n_req_anti = (int32_t)p.req_anti.size();
+    h.n_pref_aff = (int32_t)p.pref_aff.size();
+    h.n_pref_anti = (int32_t)p.pref_anti.size();
+    bool self_all = !p.req_aff.empty();
+    for (auto& a : p.req_aff)
+      self_all = self_all && (a.namespaces.count(p.ns) || a.ns_all) && a.sel.matches(p.labels);
+    h.self_matches_all = self_all ? 1 : 0;
+    if (p.pref_aff_present || p.pref_anti_present) h.flags |= KPF_IPA_HAS_CONSTRAINTS;
+    m.ipa_no_req_terms = p.req_aff.empty() && p.req_anti.empty();
+    m.ipa_prescore_skip_static = ipa_ignore && !(p.pref_aff_present || p.pref_anti_present);
+    if (m.prefilter_error) h.flags |= KPF_PREFILTER_ERROR;
+    // ---- as-existing record
+    h.exist_flags = exist_flags(p);
+    h.exist_terms_off = (int32_t)P.et.size();
+    vector<int32_t>* none = nullptr;
+    append_terms(p, 0, P.et, none, P.req, P.i32);
+    h.n_exist_terms = (int32_t)P.et.size();
+    m.flags = h.flags;
+    // ---- lay out the blob
+    auto align = [](uint32_t x) { return (x + 15u) & ~15u; };
+    uint32_t off = align(sizeof(ksg_prog));
+    h.off_i32 = off; h.n_i32 = (uint32_t)P.i32.size(); off = align(off + h.n_i32 * 4);
+    h.off_u32 = off; h.n_u32 = (uint32_t)P.u32.size(); off = align(off + h.n_u32 * 4);
+    h.off_req = off; h.n_req = (uint32_t)P.req.size(); off = align(off + h.n_req * sizeof(ksg_req));
+    h.off_sel = off; h.n_sel = (uint32_t)P.sel.size(); off = align(off + h.n_sel * sizeof(ksg_sel));
+    h.off_aterm = off; h.n_aterm = (uint32_t)P.at.size(); off = align(off + h.n_aterm * sizeof(ksg_aterm));
+    h.off_eterm = off; h.n_eterm = (uint32_t)P.et.size(); off = align(off + h.n_eterm * sizeof(ksg_exist_term));
+    h.total_bytes = off;
+    blob.assign(off, 0);
+    std::memcpy(blob.data(), &h, sizeof(h));
+    if (h.n_i32) std::memcpy(blob.data() + h.off_i32, P.i32.data(), h.n_i32 * 4);
+    if (h.n_u32) std::memcpy(blob.data() + h.off_u32, P.u32.data(), h.n_u32 * 4);
+    if (h.n_req) std::memcpy(blob.data() + h.off_req, P.req.data(), h.n_req * sizeof(ksg_req));
+    if (h.n_sel) std::memcpy(blob.data() + h.off_sel, P.sel.data(), h.n_sel * sizeof(ksg_sel));
+    if (h.n_aterm) std::memcpy(blob.data() + h.off_aterm, P.at.data(), h.n_aterm * sizeof(ksg_aterm));
+    if (h.n_eterm) std::memcpy(blob.data() + h.off_eterm, P.et.data(), h.n_eterm * sizeof(ksg_exist_term));
+    return true;
+  }
+
+  // ------------------------------------------------------------ load / run
+  bool load(const char* js, size_t len) {
+    J doc;
+    try {
+      doc = json::parse(js, len);
+    } catch (std::exception& e) {
+      err = e.what();
+      return false;
+    }
+    docs.emplace_back(new J(std::move(doc)));
+    const J& d = *docs.back();
+    nodes.clear();
+    node_names = Dict();
+    bound.clear();
+    queue.clear();
+    nkeys = Dict(); nvals.clear(); pkeys = Dict(); pvals.clear(); nss = Dict();
+    taint_id.clear(); taints.clear(); topo = Dict();
+    if (const J* ns = d["nodes"])
+      for (auto& n : ns->items) {
+        nodes.push_back(parse_node(n));
+        node_names.add(nodes.back().name);
+      }
+    if (const J* ps = d["pods"])
+      for (auto& p : ps->items) bound.push_back(parse_pod(p));
+    if (const J* q = d["queue"])
+      for (auto& p : q->items) queue.push_back(parse_pod(p));
+    if (!build_vocab()) return false;
+    NodeSoA S;
+    PodTableSoA T;
+    if (!encode_snapshot(S, T)) return false;
+    // capacity for device-side appends of the whole queue
+    uint32_t qn = (uint32_t)queue.size();
+    size_t qterms = 0, qreqs = 0, qvals = 0;
+    for (auto& p : queue) {
+      vector<ksg_exist_term> et;
+      vector<ksg_req> rq;
+      vector<int32_t> vl, tp;
+      append_terms(p, 0, et, tp, rq, vl);
+      qterms += et.size();
+      qreqs += rq.size();
+      qvals += vl.size();
+    }
+    if (!eng->upload(S, T, T.n + qn + 16, (uint32_t)(T.terms.size() + qterms + 16),
+                     (uint32_t)(T.reqs.size() + qreqs + 16), (uint32_t)(T.vals.size() + qvals + 16), err))
+      return false;
+    compiled = false;
+    progs.clear();
+    meta.clear();
+    return true;
+  }
+
+  vector<std::unique_ptr<J>> docs;
+  vector<vector<uint8_t>> progs;
+
+  bool compile_queue() {
+    if (compiled) return true;
+    progs.assign(queue.size(), {});
+    meta.assign(queue.size(), PodMeta());
+    for (size_t q = 0; q < queue.size(); ++q)
+      if (!compile(queue[q], (int32_t)q, progs[q], meta[q])) return false;
+    if (!eng->set_programs(progs, err)) return false;
+    compiled = true;
+    return true;
+  }
+
+  // ------------------------------------------------------------ rendering
+  static void jstr(string& o, const string& s) {
+    static const char* hx = "0123456789abcdef";
+    o += '"';
+    for (size_t i = 0; i < s.size(); ++i) {
+      unsigned char c = (unsigned char)s[i];
+      switch (c) {
+        case '"': o += "\\\""; break;
+        case '\\': o += "\\\\"; break;
+        case '\n': o += "\\n"; break;
+        case '\r': o += "\\r"; break;
+        case '\t': o += "\\t"; break;
+        default:
+          if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+            o += "\\u00";
+            o += hx[c >> 4];
+            o += hx[c & 15];
+          } else if (c == 0xE2 && i + 2 < s.size() && (unsigned char)s[i + 1] == 0x80 &&
+                     ((unsigned char)s[i + 2] & 0xFE) == 0xA8) {
+            o += ((unsigned char)s[i + 2] == 0xA8) ? "\\u2028" : "\\u2029";
+            i += 2;
+          } else {
+            o += (char)c;
+          }
+      }
+    }
+    o += '"';
+  }
+  static string jmap(const map<string, string>& m) {
+    string o = "{";
+    for (auto it = m.begin(); it != m.end(); ++it) {
+      if (it != m.begin()) o += ',';
+      jstr(o, it->first);
+      o += ':';
+      jstr(o, it->second);
+    }
+    return o + "}";
+  }
+
+  string filter_message(int pos, uint32_t detail) const {
+    switch (plugins[pos]) {
+      case P_FIT: {
+        string m;
+        auto add = [&](const string& s) { m += (m.empty() ? "" : ", ") + s; };
+        if (detail & KSG_FIT_TOO_MANY_PODS) add("Too many pods");
+        for (size_t r = 0; r < res.names.size(); ++r)
+          if (detail & (1u << (1 + r))) add("Insufficient " + res.names[r]);
+        return m;
+      }
+      case P_TAINT: {
+        const Taint& t = taints[detail];
+        return "node(s) had untolerated taint {" + t.key + ": " + t.value + "}";
+      }
+      case P_NA: return "node(s) didn't match Pod's node affinity/selector";
+      case P_PTS:
+        return detail == KSG_PTS_MISSING_LABEL ? "node(s) didn't match pod topology spread constraints (missing required label)"
+                                               : "node(s) didn't match pod topology spread constraints";
+      case P_IPA:
+        return detail == KSG_IPA_AFFINITY ? "node(s) didn't match pod affinity rules"
+               : detail == KSG_IPA_ANTI_AFFINITY ? "node(s) didn't match pod anti-affinity rules"
+                                                 : "node(s) didn't satisfy existing pods anti-affinity rules";
+    }
+    return "";
+  }
+
+  // normalized score of one node (host restatement of k_finalize, for finalscore-result)
+  i64 normalize(int pos, i64 s, const ksg_pod_summary& S, bool ignored) const {
+    i64 mx = S.max_score[pos], mn = S.min_score[pos];
+    switch (plugins[pos]) {
+      case P_TAINT: return mx == 0 ? 100 : 100 - 100 * s / mx;
+      case P_NA: return mx == 0 ? s : 100 * s / mx;
+      case P_PTS:
+        if (ignored) return 0;
+        if (mx == 0) return 100;
+        return 100 * (mx + mn - s) / mx;
+      case P_IPA: {
+        if (!(S.ipa_flags & 8u)) return s;
+        i64 diff = mx - mn;
+        double f = 0;
+        if (diff > 0) f = 100.0 * ((double)(s - mn) / (double)diff);
+        return (i64)f;
+      }
+    }
+    return s;
+  }
+
+  bool render(uint32_t q, string& out) {
+    PodOutputs o;
+    if (!eng->outputs(q, o, err)) return false;
+    const ksg_pod_summary& S = o.summary;
+    const PodMeta& m = meta[q];
+    uint32_t n = hi - lo;
+    map<string, string> pre_status, pre_score;
+    map<string, vector<string>> pre_result;
+    map<string, map<string, string>> filt, score, fin;
+    // skip sets
+    uint32_t skip_f = 0, skip_s = 0;
+    if (m.flags & KPF_SKIP_NA_FILTER) skip_f |= 1u << P_NA;
+    if (m.flags & KPF_SKIP_PTS_FILTER) skip_f |= 1u << P_PTS;
+    if (m.ipa_no_req_terms && !(S.ipa_flags & 4u)) skip_f |= 1u << P_IPA;
+    bool aborted = false;
+    for (int pos = 0; pos < n_plugins && !aborted; ++pos) {
+      int id = plugins[pos];
+      if (!has_prefilter(id)) continue;
+      string msg = "success";
+      if (skip_f & (1u << id)) msg = "";
+      if (pos == m.prefilter_fail_pos) {
+        msg = m.prefilter_fail_msg;
+        aborted = true;
+      }
+      pre_status[names[pos]] = msg;
+      if (id == P_NA && m.restricted) pre_result[names[pos]] = m.prefilter_names;
+    }
+    if (!aborted) {
+      for (uint32_t i = 0; i < n; ++i) {
+        uint32_t code = o.filter[i];
+        if (code == KSG_FILTER_NOT_EVALUATED) continue;
+        int fail_pos = code == KSG_FILTER_PASS ? n_plugins : (int)(code >> 24);
+        auto& row = filt[nodes[lo + i].name];
+        for (int pos = 0; pos < n_plugins; ++pos) {
+          int id = plugins[pos];
+          if (!has_filter(id) || (skip_f & (1u << id))) continue;
+          if (pos < fail_pos) row[names[pos]] = "passed";
+          else if (pos == fail_pos) { row[names[pos]] = filter_message(pos, code & 0xFFFFFFu); break; }
+        }
+      }
+      if (S.feasible > 1 && S.status != 2) {
+        if (m.flags & KPF_SKIP_NA_SCORE) skip_s |= 1u << P_NA;
+        if (m.flags & KPF_SKIP_PTS_SCORE) skip_s |= 1u << P_PTS;
+        if (m.ipa_prescore_skip_static || !(S.ipa_flags & 8u)) skip_s |= 1u << P_IPA;
+        for (int pos = 0; pos < n_plugins; ++pos) pre_score[names[pos]] = (skip_s & (1u << plugins[pos])) ? "" : "success";
+        int pts = pos_of(P_PTS);
+        for (uint32_t i = 0; i < n; ++i) {
+          if (o.filter[i] != KSG_FILTER_PASS) continue;
+          const string& nm = nodes[lo + i].name;
+          bool ignored = false;
+          if (pts >= 0) ignored = pts_ignored(q, i);
+          for (int pos = 0; pos < n_plugins; ++pos) {
+            int id = plugins[pos];
+            if (skip_s & (1u << id)) continue;
+            i64 raw = o.score[(size_t)pos * n + i];
+            score[nm][names[pos]] = std::to_string(raw);
+            i64 v = has_ext(id) ? normalize(pos, raw, S, ignored) : raw;
+            fin[nm][names[pos]] = std::to_string(v * store_w[pos]);
+          }
+        }
+      }
+    }
+    string sel = S.status == 0 && S.selected >= 0 ? nodes[S.selected].name : "";
+    auto j2 = [&](const map<string, map<string, string>>& mm) {
+      string s = "{";
+      for (auto it = mm.begin(); it != mm.end(); ++it) {
+        if (it != mm.begin()) s += ',';
+        jstr(s, it->first);
+        s += ':';
+        s += jmap(it->second);
+      }
+      return s + "}";
+    };
+    string pr = "{";
+    for (auto it = pre_result.begin(); it != pre_result.end(); ++it) {
+      if (it != pre_result.begin()) pr += ',';
+      jstr(pr, it->first);
+      pr += ":[";
+      for (size_t k = 0; k < it->second.size(); ++k) {
+        if (k) pr += ',';
+        jstr(pr, it->second[k]);
+      }
+      pr += ']';
+    }
+    pr += "}";
+    const string P = "kube-scheduler-simulator.sigs.k8s.io/";
+    map<string, string> ann{{P + "prefilter-result", pr},          {P + "prefilter-result-status", jmap(pre_status)},
+                            {P + "filter-result", j2(filt)},       {P + "postfilter-result", "{}"},
+                            {P + "prescore-result", jmap(pre_score)}, {P + "score-result", j2(score)},
+                            {P + "finalscore-result", j2(fin)},    {P + "reserve-result", "{}"},
+                            {P + "permit-result", "{}"},           {P + "permit-result-timeout", "{}"},
+                            {P + "prebind-result", "{}"},          {P + "bind-result", "{}"},
+                            {P + "selected-node", sel}};
+    out = jmap(ann);
+    return true;
+  }
+
+  // PodTopologySpread IgnoredNodes: feasible node missing a score-constraint key
+  bool pts_ignored(uint32_t q, uint32_t i) const {
+    const Pod& p = queue[q];
+    const Node& nd = nodes[lo + i];
+    for (auto& c : p.tsc)
+      if (c.when == "ScheduleAnyway" && !nd.labels.count(c.key)) return true;
+    return false;
+  }
+};
+
+}  // namespace host
+}  // namespace ksg
+
+// ================================================================== C ABI
+using ksg::host::Cluster;
+
+struct ksg_ctx {
+  Cluster c;
+  std::string last_error;
+  int fail(const std::string& m, int code) {
+    last_error = m;
+    return code;
+  }
+};
+
+extern "C" {
+
+int ksg_abi_version(void) { return KSG_ABI_VERSION; }
+
+int ksg_create(const char* profile_json, size_t len, const ksg_opts* opts, ksg_ctx** out) {
+  if (!out || !profile_json) return KSG_E_INVALID;
+  *out = nullptr;
+  std::unique_ptr<ksg_ctx> ctx(new ksg_ctx());
+  try {
+    ksg::json::Node pr = ksg::json::parse(profile_json, len);
+    const ksg::json::Node* p = pr["profile"] ? pr["profile"] : &pr;
+    if (!ctx->c.load_profile(*p)) return KSG_E_INVALID;
+  } catch (std::exception& e) {
+    return KSG_E_INVALID;
+  }
+  if (opts) {
+    ctx->c.ecfg.device = opts->device;
+    ctx->c.ecfg.stream = opts->stream;
+    ctx->c.rank = opts->shard_rank;
+    ctx->c.shards = opts->shard_count ? opts->shard_count : 1;
+    if (ctx->c.rank >= ctx->c.shards) return KSG_E_INVALID;
+  }
+  ctx->c.eng.reset(new ksg::Engine());
+  std::string err;
+  if (!ctx->c.eng->init(ctx->c.ecfg, err)) return KSG_E_DEVICE;
+  *out = ctx.release();
+  return KSG_OK;
+}
+
+void ksg_destroy(ksg_ctx* ctx) { delete ctx; }
+
+const char* ksg_last_error(const ksg_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len) {
+  if (!ctx || !json) return KSG_E_INVALID;
+  try {
+    Cluster& c = ctx->c;
+    // fix the engine's global node offset for this shard before upload
+    if (!c.load(json, len)) return ctx->fail(c.err, KSG_E_INVALID);
+  } catch (std::exception& e) {
+    return ctx->fail(e.what(), KSG_E_INVALID);
+  }
+  return KSG_OK;
+}
+
+int ksg_num_nodes(const ksg_ctx* ctx) { return ctx ? (int)ctx->c.nodes.size() : KSG_E_INVALID; }
+int ksg_queue_len(const ksg_ctx* ctx) { return ctx ? (int)ctx->c.queue.size() : KSG_E_INVALID; }
+
+int ksg_keep_outputs(ksg_ctx* ctx, uint32_t first, uint32_t count) {
+  if (!ctx) return KSG_E_INVALID;
+  if (!ctx->c.eng->keep_outputs(first, count, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
+  return KSG_OK;
+}
+
+int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
+  if (!ctx) return KSG_E_INVALID;
+  Cluster& c = ctx->c;
+  if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
+  if (c.shards != 1) return ctx->fail("queue mode on a sharded context needs ksg_whatif/exchange", KSG_E_STATE);
+  if (!c.compile_queue()) return ctx->fail(c.err, KSG_E_INVALID);
+  if (!c.eng->run_queue(first, count, true, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
+  return KSG_OK;
+}
+
+int ksg_wait(ksg_ctx* ctx, float* ms) {
+  if (!ctx) return KSG_E_INVALID;
+  if (!ctx->c.eng->sync(ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
+  if (ms) *ms = ctx->c.eng->last_ms();
+  return KSG_OK;
+}
+
+int ksg_pod_results(ksg_ctx* ctx, uint32_t first, uint32_t count, ksg_pod_result* out) {
+  if (!ctx || !out) return KSG_E_INVALID;
+  Cluster& c = ctx->c;
+  if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
+  std::vector<ksg_pod_summary> s(count);
+  if (count && !c.eng->summaries(first, count, s.data(), c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
+  for (uint32_t i = 0; i < count; ++i) {
+    out[i].selected = s[i].selected;
+    out[i].feasible = s[i].feasible;
+    out[i].status = s[i].status;
+    out[i].skip_filter = s[i].skip_filter;
+    out[i].skip_score = s[i].skip_score;
+    out[i].total = (int32_t)(s[i].best_key >> 40);
+  }
+  return KSG_OK;
+}
+
+int ksg_filter_codes(ksg_ctx* ctx, uint32_t q, uint32_t* out, uint32_t n) {
+  if (!ctx || !out) return KSG_E_INVALID;
+  ksg::PodOutputs o;
+  if (!ctx->c.eng->outputs(q, o, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_STATE);
+  if (n < o.filter.size()) return KSG_E_NOBUF;
+  std::copy(o.filter.begin(), o.filter.end(), out);
+  return KSG_OK;
+}
+
+int ksg_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* out, uint32_t n) {
+  if (!ctx || !out) return KSG_E_INVALID;
+  ksg::PodOutputs o;
+  if (!ctx->c.eng->outputs(q, o, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_STATE);
+  size_t N = o.filter.size();
+  if (n < N || pos >= KSG_MAX_PLUGINS) return KSG_E_NOBUF;
+  std::copy(o.score.begin() + pos * N, o.score.begin() + (pos + 1) * N, out);
+  return KSG_OK;
+}
+
+int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len) {
+  if (!ctx || !len) return KSG_E_INVALID;
+  std::string s;
+  if (q >= ctx->c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
+  if (!ctx->c.render(q, s)) return ctx->fail(ctx->c.err, KSG_E_STATE);
+  *len = s.size();
+  if (!buf || cap < s.size()) return KSG_E_NOBUF;
+  std::memcpy(buf, s.data(), s.size());
+  return KSG_OK;
+}
+
+int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_pod_result* out) {
+  (void)ctx; (void)pod_json; (void)len; (void)commit; (void)out;
+  return KSG_E_STATE;  // implemented by the cycle API (next step)
+}
+
+int ksg_node_requested(ksg_ctx* ctx, int64_t* requested, int32_t* pod_count, uint32_t n_res, uint32_t n) {
+  if (!ctx) return KSG_E_INVALID;
+  std::vector<int64_t> r;
+  std::vector<int32_t> pc;
+  if (!ctx->c.eng->read_requested(r, pc, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
+  uint32_t N = (uint32_t)pc.size(), R = N ? (uint32_t)(r.size() / N) : 0;
+  if (n < N || n_res < R) return KSG_E_NOBUF;
+  for (uint32_t k = 0; k < R; ++k)
+    for (uint32_t i = 0; i < N; ++i) requested[(size_t)k * n + i] = r[(size_t)k * N + i];
+  for (uint32_t i = 0; i < N; ++i) pod_count[i] = pc[i];
+  return KSG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,199 @@
+// Device-visible data layout shared by the host encoder and the HIP kernels.
+//
+// Everything the kernels read about the cluster is interned to integers by the
+// host (label keys, per-key label values, taints, namespaces, pod-label keys and
+// values) and stored structure-of-arrays in HBM, one column per field, so a
+// wavefront reading 64 consecutive nodes touches 64 consecutive elements.
+// See DESIGN.md "Data layout in HBM" for sizes per config.
+#pragma once
+#include <stdint.h>
+
+#define KSG_MAX_RES 8        // resource columns: 0 cpu(milli) 1 memory 2 ephemeral-storage 3.. scalar
+#define KSG_MAX_PLUGINS 8    // hot-path plugins in one profile
+#define KSG_MAX_SCORE_RES 8  // resources in a Fit/BA scoring config
+#define KSG_MAX_TSC 8        // topology spread constraints per pod (filter + score)
+#define KSG_MAX_TOPO 16      // distinct topology keys in one cluster
+#define KSG_MAX_RTC 16       // RequestedToCapacityRatio shape points
+
+#define KSG_RES_CPU 0
+#define KSG_RES_MEM 1
+#define KSG_RES_EPH 2
+
+// plugin ids (ksg.h KSG_PLUGIN_*)
+#define KP_FIT 0
+#define KP_BA 1
+#define KP_TAINT 2
+#define KP_NA 3
+#define KP_PTS 4
+#define KP_IPA 5
+
+// filter result code per (pod,node): 0xFFFFFFFF passed every filter plugin,
+// 0xFFFFFFFE not evaluated (outside the NodeAffinity PreFilterResult), else
+// (profile position << 24) | detail  (detail: Fit reason bits, taint id, PTS/IPA reason).
+#define KSG_FILTER_PASS 0xFFFFFFFFu
+#define KSG_FILTER_NOT_EVALUATED 0xFFFFFFFEu
+#define KSG_FIT_TOO_MANY_PODS 1u   // Fit detail bit 0; bit (1 + r) = insufficient resource column r
+#define KSG_PTS_MISSING_LABEL 0u
+#define KSG_PTS_SKEW 1u
+#define KSG_IPA_AFFINITY 0u
+#define KSG_IPA_ANTI_AFFINITY 1u
+#define KSG_IPA_EXISTING_ANTI 2u
+
+// requirement operators (labels.Requirement / node selector requirement)
+#define KR_IN 0          // present && value in vals
+#define KR_NOT_IN 1      // !present || value not in vals
+#define KR_EXISTS 2
+#define KR_NOT_EXISTS 3
+#define KR_GT 4          // present && numeric(value) > num
+#define KR_LT 5
+#define KR_FALSE 6       // parse error: never matches
+#define KR_NAME_EQ 7     // matchFields metadata.name In: global node index == num
+#define KR_NAME_NE 8     // matchFields metadata.name NotIn
+
+typedef struct ksg_req {
+  int32_t key;      // label key id (node-label space or pod-label space)
+  int32_t op;       // KR_*
+  int32_t nvals;    // values in the program's value pool
+  int32_t val_off;
+  int64_t num;      // KR_GT / KR_LT threshold
+} ksg_req;          // 24 B
+
+// A selector = AND of reqs. kind 0: labels.Nothing (matches nothing, Empty()==false);
+// kind 1: requirement list (zero reqs = labels.Everything, Empty()==true).
+typedef struct ksg_sel {
+  int32_t kind;
+  int32_t req_off;
+  int32_t req_cnt;
+  int32_t pad;
+} ksg_sel;
+
+// one pod (anti-)affinity term of the incoming pod (framework.AffinityTerm)
+typedef struct ksg_aterm {
+  ksg_sel sel;
+  int32_t topo;      // topology slot (index into pair_base)
+  int32_t topo_key;  // node label key id
+  int32_t ns_all;    // namespaceSelector matches every namespace
+  int32_t ns_cnt;    // namespaces (ids) in the program's value pool
+  int32_t ns_off;
+  int32_t weight;    // preferred terms
+} ksg_aterm;
+
+typedef struct ksg_tsc {
+  ksg_sel sel;
+  int32_t topo;          // topology slot of the key
+  int32_t topo_key;      // node label key id
+  int32_t max_skew;
+  int32_t min_domains;
+  int32_t honor_affinity;
+  int32_t honor_taints;
+  int32_t self_match;    // selector matches the incoming pod's own labels
+  int32_t is_hostname;
+  int32_t first_of_key;  // first score constraint with this key (topoSize owner)
+  int32_t pad;
+} ksg_tsc;
+
+// Existing-pod record appended at assume time (Reserve -> NodeInfo.AddPod).
+typedef struct ksg_exist_term {
+  int32_t kind;      // 0 required affinity, 1 required anti, 2 preferred affinity, 3 preferred anti
+  int32_t weight;
+  int32_t topo;      // topology slot
+  int32_t topo_key;  // node label key id
+  ksg_sel sel;       // offsets into the TABLE's req pool once appended
+  int32_t ns_all;
+  int32_t ns_cnt;
+  int32_t ns_off;    // into the table's value pool
+  int32_t pad;
+} ksg_exist_term;
+
+// Pod program: everything the kernels need about one incoming pod.  The
+// program is a flat blob: this header followed by pools addressed by offsets
+// (all offsets are element indices into the named pool, which start at the
+// byte offsets given in the header).
+typedef struct ksg_prog {
+  int32_t queue_idx;        // scheduling-queue position (tie-break hash input)
+  int32_t ns_id;
+  uint32_t flags;           // KPF_*
+  int32_t n_pod_label_keys; // incoming pod's label values: pool_i32[labels_off .. + n)
+  int32_t labels_off;
+
+  // ---- NodeResourcesFit / BalancedAllocation
+  int64_t req[KSG_MAX_RES];               // PodRequests (Fit filter, Requested delta)
+  int64_t fit_score_req[KSG_MAX_SCORE_RES];  // nonzero requests per Fit scoring resource
+  int64_t ba_req[KSG_MAX_SCORE_RES];      // requests per BA resource
+  int64_t nz_cpu, nz_mem;                 // NonZeroRequested delta
+
+  // ---- TaintToleration: bitsets over the taint vocabulary in pool_u32
+  int32_t taint_words;
+  int32_t taint_hard_off;   // bit t: taint t is NoSchedule/NoExecute and NOT tolerated
+  int32_t taint_pref_off;   // bit t: taint t is PreferNoSchedule and NOT tolerated by prefer-tolerations
+
+  // ---- NodeAffinity (RequiredNodeAffinity + PreferredSchedulingTerms)
+  ksg_sel node_sel;         // pod.spec.nodeSelector (kind 1 with reqs) when present
+  int32_t n_req_terms;      // required terms (OR); terms with parse errors are dropped
+  int32_t req_terms_off;    // pool_sel
+  int32_t n_pref_terms;
+  int32_t pref_terms_off;   // pool_sel; weight in pool_i32[pref_w_off + i]
+  int32_t pref_w_off;
+  int32_t restrict_words;   // PreFilterResult node bitmask (local nodes) in pool_u32
+  int32_t restrict_off;
+
+  // ---- PodTopologySpread
+  int32_t n_tsc_filter, n_tsc_score;
+  ksg_tsc tsc[KSG_MAX_TSC];  // filter constraints first, then score constraints
+
+  // ---- InterPodAffinity (incoming terms, namespaces merged)
+  int32_t n_req_aff, n_req_anti, n_pref_aff, n_pref_anti;
+  int32_t aterm_off;        // pool_aterm: req_aff, req_anti, pref_aff, pref_anti
+  int32_t self_matches_all; // podMatchesAllAffinityTerms(required affinity, pod)
+
+  // ---- as-existing record (committed on assume)
+  uint32_t exist_flags;     // KEF_*
+  int32_t n_exist_terms;
+  int32_t exist_terms_off;  // pool_eterm (sel/ns offsets relative to this program's pools)
+
+  // ---- pools (byte offsets from the start of the blob)
+  uint32_t off_i32, n_i32;
+  uint32_t off_u32, n_u32;
+  uint32_t off_req, n_req;
+  uint32_t off_sel, n_sel;
+  uint32_t off_aterm, n_aterm;
+  uint32_t off_eterm, n_eterm;
+  uint32_t total_bytes;
+  uint32_t pad;
+} ksg_prog;
+
+// KPF_* pod flags
+#define KPF_ZERO_REQUEST (1u << 0)    // PodRequests all zero incl. scalars (fitsRequest early return)
+#define KPF_HAS_NODE_SEL (1u << 1)    // RequiredNodeAffinity.labelSelector != nil
+#define KPF_HAS_REQ_NA (1u << 2)      // RequiredNodeAffinity.nodeSelector != nil
+#define KPF_RESTRICT (1u << 3)        // PreFilterResult restricts evaluated nodes
+#define KPF_SKIP_NA_FILTER (1u << 4)  // PreFilter Skip (host-known)
+#define KPF_SKIP_PTS_FILTER (1u << 5)
+#define KPF_SKIP_NA_SCORE (1u << 6)   // PreScore Skip (host-known)
+#define KPF_SKIP_PTS_SCORE (1u << 7)
+#define KPF_IPA_HAS_CONSTRAINTS (1u << 8)  // incoming preferred (anti)affinity terms present
+#define KPF_NA_PREF_ERROR (1u << 9)   // preferred terms failed to parse: PreScore error
+#define KPF_HAS_SCALAR_REQ (1u << 10)
+#define KPF_PREFILTER_REJECT (1u << 11)  // PreFilter Unschedulable (host-known): no node evaluated
+#define KPF_PREFILTER_ERROR (1u << 12)   // PreFilter error status: cycle aborts
+
+// KEF_* existing-pod flags
+#define KEF_TERMINATING (1u << 0)
+#define KEF_WITH_AFFINITY (1u << 1)
+#define KEF_REQ_ANTI (1u << 2)
+
+// per-pod cycle summary written by the device (read back by the host)
+typedef struct ksg_pod_summary {
+  uint64_t best_key;        // (total << 40) | ((0xFFFFF - h20) << 20) | global node index
+  int32_t selected;         // global node index, -1 none
+  int32_t feasible;
+  int32_t status;           // 0 scheduled, 1 unschedulable, 2 error
+  uint32_t skip_filter;     // bit = plugin id, PreFilter returned Skip
+  uint32_t skip_score;      // bit = plugin id, PreScore returned Skip
+  int32_t ignored;          // PodTopologySpread ignored nodes (feasible, missing keys)
+  int64_t max_score[KSG_MAX_PLUGINS];  // per profile position, over feasible nodes
+  int64_t min_score[KSG_MAX_PLUGINS];
+  double pts_weight[KSG_MAX_TSC];
+  uint32_t ipa_flags;       // bit0 affinity counts non-empty, bit1 anti counts, bit2 existing anti, bit3 topo score non-empty
+  int32_t pad;
+} ksg_pod_summary;

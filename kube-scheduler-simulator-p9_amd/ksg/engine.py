@@ -1,0 +1,155 @@
+"""ctypes binding of libksg.so (include/ksg.h).  No fallback path."""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+from dataclasses import dataclass
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+_lib = None
+
+FILTER_PASSED = 0xFFFFFFFF
+FILTER_NOT_EVALUATED = 0xFFFFFFFE
+
+
+def lib_path() -> str:
+    return os.path.join(_PKG, "libksg.so")
+
+
+class _PodResult(ctypes.Structure):
+    _fields_ = [("selected", ctypes.c_int32), ("feasible", ctypes.c_int32), ("status", ctypes.c_int32),
+                ("skip_filter", ctypes.c_uint32), ("skip_score", ctypes.c_uint32), ("total", ctypes.c_int32)]
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("stream", ctypes.c_void_p), ("shard_rank", ctypes.c_uint32),
+                ("shard_count", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+@dataclass
+class PodResult:
+    selected: int
+    feasible: int
+    status: int
+    total: int
+
+
+def load_library():
+    """Load libksg.so; raises OSError when the HIP build is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = lib_path()
+    if not os.path.exists(p):
+        raise OSError(f"libksg.so not built at {p}: run __graft_entry__.build() (hipcc gfx950)")
+    L = ctypes.CDLL(p)
+    vp, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int32
+    L.ksg_create.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(_Opts), ctypes.POINTER(vp)]
+    L.ksg_destroy.argtypes = [vp]
+    L.ksg_last_error.restype = ctypes.c_char_p
+    L.ksg_last_error.argtypes = [vp]
+    L.ksg_load_cluster.argtypes = [vp, ctypes.c_char_p, sz]
+    L.ksg_num_nodes.argtypes = [vp]
+    L.ksg_queue_len.argtypes = [vp]
+    L.ksg_schedule_queue.argtypes = [vp, u32, u32]
+    L.ksg_wait.argtypes = [vp, ctypes.POINTER(ctypes.c_float)]
+    L.ksg_pod_results.argtypes = [vp, u32, u32, ctypes.POINTER(_PodResult)]
+    L.ksg_keep_outputs.argtypes = [vp, u32, u32]
+    L.ksg_filter_codes.argtypes = [vp, u32, ctypes.POINTER(u32), u32]
+    L.ksg_scores.argtypes = [vp, u32, u32, ctypes.POINTER(i32), u32]
+    L.ksg_annotations.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.ksg_node_requested.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i32), u32, u32]
+    _lib = L
+    return L
+
+
+class KsgError(RuntimeError):
+    pass
+
+
+class Scheduler:
+    """One engine context (one profile, one GPU, optionally one node shard)."""
+
+    def __init__(self, profile: dict, device: int = 0, stream: int | None = None, shard_rank=0, shard_count=1):
+        self.L = load_library()
+        self.h = ctypes.c_void_p()
+        prof = json.dumps(profile).encode()
+        opts = _Opts(device, stream, shard_rank, shard_count, 0)
+        rc = self.L.ksg_create(prof, len(prof), ctypes.byref(opts), ctypes.byref(self.h))
+        if rc != 0:
+            raise KsgError(f"ksg_create failed ({rc})")
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            raise KsgError(f"{what}: {rc} {self.L.ksg_last_error(self.h).decode()}")
+
+    def close(self):
+        if self.h:
+            self.L.ksg_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_cluster(self, doc):
+        s = doc if isinstance(doc, (bytes, str)) else json.dumps(doc)
+        b = s.encode() if isinstance(s, str) else s
+        self._chk(self.L.ksg_load_cluster(self.h, b, len(b)), "ksg_load_cluster")
+
+    @property
+    def n_nodes(self):
+        return self.L.ksg_num_nodes(self.h)
+
+    @property
+    def queue_len(self):
+        return self.L.ksg_queue_len(self.h)
+
+    def keep_outputs(self, first, count):
+        self._chk(self.L.ksg_keep_outputs(self.h, first, count), "ksg_keep_outputs")
+
+    def schedule(self, first=0, count=None, wait=True):
+        count = self.queue_len - first if count is None else count
+        self._chk(self.L.ksg_schedule_queue(self.h, first, count), "ksg_schedule_queue")
+        return self.wait() if wait else None
+
+    def wait(self):
+        ms = ctypes.c_float()
+        self._chk(self.L.ksg_wait(self.h, ctypes.byref(ms)), "ksg_wait")
+        return ms.value
+
+    def results(self, first=0, count=None):
+        count = self.queue_len - first if count is None else count
+        arr = (_PodResult * max(count, 1))()
+        self._chk(self.L.ksg_pod_results(self.h, first, count, arr), "ksg_pod_results")
+        return [PodResult(a.selected, a.feasible, a.status, a.total) for a in arr[:count]]
+
+    def filter_codes(self, q):
+        n = self.n_nodes
+        arr = (ctypes.c_uint32 * n)()
+        self._chk(self.L.ksg_filter_codes(self.h, q, arr, n), "ksg_filter_codes")
+        return list(arr)
+
+    def scores(self, q, pos):
+        n = self.n_nodes
+        arr = (ctypes.c_int32 * n)()
+        self._chk(self.L.ksg_scores(self.h, q, pos, arr, n), "ksg_scores")
+        return list(arr)
+
+    def annotations(self, q) -> dict:
+        n = ctypes.c_size_t()
+        self.L.ksg_annotations(self.h, q, None, 0, ctypes.byref(n))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._chk(self.L.ksg_annotations(self.h, q, buf, n.value + 1, ctypes.byref(n)), "ksg_annotations")
+        return json.loads(buf.raw[:n.value].decode())
+
+    def node_requested(self, n_res=8):
+        n = self.n_nodes
+        req = (ctypes.c_int64 * (n_res * n))()
+        pc = (ctypes.c_int32 * n)()
+        self._chk(self.L.ksg_node_requested(self.h, req, pc, n_res, n), "ksg_node_requested")
+        return [list(req[r * n:(r + 1) * n]) for r in range(n_res)], list(pc)

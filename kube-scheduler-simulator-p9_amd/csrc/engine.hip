@@ -818,7 +818,8 @@ __global__ void k_pts_score(DevCluster C, DevScratch S, DevOut O, const uint8_t*
   if (feasible) O.score[(size_t)pos * C.N + n] = (int32_t)s;
   int64_t mx = wave_max(counted ? s : INT64_MIN);
   int64_t mn = wave_min(counted ? s : INT64_MAX);
-  if (lane0() && __any(counted)) {
+  bool any = __any(counted);  // every lane votes (no short-circuit around the wave op)
+  if (any && lane0()) {
     atomicMax((long long*)&O.sum->max_score[pos], (long long)mx);
     atomicMin((long long*)&O.sum->min_score[pos], (long long)mn);
   }

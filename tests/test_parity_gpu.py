@@ -39,7 +39,11 @@ def test_selected_and_annotations(name, c, sizes):
         sel, feas, st = o.result(q)
         if (r.selected, r.feasible, r.status) != (sel, feas, st):
             mismatches.append((q, (r.selected, r.feasible, r.status), (sel, feas, st)))
-    assert not mismatches, f"{name}: {len(mismatches)} pods differ, first {mismatches[:5]}"
+    if mismatches:
+        q = mismatches[0][0]
+        a, b = s.annotations(q), o.annotations(q)
+        diff = {k: (a.get(k, "")[:600], b[k][:600]) for k in b if a.get(k) != b[k]}
+        raise AssertionError(f"{name}: {len(mismatches)} pods differ, first {mismatches[:5]}; pod {q} diff {diff}")
     for q in range(s.queue_len):
         a, b = s.annotations(q), o.annotations(q)
         for k in b:

@@ -101,6 +101,14 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count);
 int ksg_wait(ksg_ctx* ctx, float* device_ms);
 int ksg_pod_results(ksg_ctx* ctx, uint32_t first, uint32_t count, ksg_pod_result* out);
 
+/* Restore node rows and the existing-pod table to the loaded snapshot
+ * (benchmark steps replay the same queue). */
+int ksg_reset(ksg_ctx* ctx);
+/* Time the dominant Filter/Score kernel with HIP events on the context stream
+ * for every `every`-th pod of the following ksg_schedule_queue (0 = off). */
+int ksg_sample_kernel(ksg_ctx* ctx, uint32_t every);
+int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples);
+
 /* Keep per-(pod, node) outputs for queue pods [first, first+count) (tests,
  * annotation rendering).  Must precede ksg_schedule_queue. */
 int ksg_keep_outputs(ksg_ctx* ctx, uint32_t first, uint32_t count);

@@ -90,6 +90,13 @@ class Engine {
   bool summaries(uint32_t first, uint32_t count, ksg_pod_summary* out, std::string& err);
   bool outputs(uint32_t prog_idx, PodOutputs& out, std::string& err);
   bool sync(std::string& err);
+  // Restore the node rows / pod table to the state of the last upload (device copy).
+  bool reset(std::string& err);
+  // Sample the dominant kernel (k_filter_score) every `every` pods inside run_queue
+  // with HIP events on the engine stream; 0 disables.
+  void sample_kernel(uint32_t every);
+  // Average duration (ms) and count of the sampled launches of the last run.
+  bool kernel_time(float& avg_ms, uint32_t& samples, std::string& err);
   // Read back the node resource rows (parity tests of the assume delta).
   bool read_requested(std::vector<int64_t>& requested, std::vector<int32_t>& pod_count, std::string& err);
   uint32_t n_nodes() const;

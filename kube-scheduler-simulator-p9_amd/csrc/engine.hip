@@ -1010,6 +1010,14 @@ struct Engine::Impl {
   bool has_pts = false, has_ipa = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0;
+  // pristine copies for reset()
+  DBuf<int64_t> req0, nzc0, nzm0;
+  DBuf<int32_t> podcnt0;
+  uint32_t counts0[8] = {};
+  // sampled kernel timing
+  uint32_t sample_every = 0;
+  std::vector<hipEvent_t> sev;
+  uint32_t n_samples = 0;
   std::vector<Engine::KernelStat> stats;
 
   DevCluster cluster() const {
@@ -1140,6 +1148,15 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     HIPCHK(hipMemcpyAsync(I.tval.p, pt.vals.data(), pt.vals.size() * 4, hipMemcpyHostToDevice, s));
   uint32_t counts[8] = {pt.n, (uint32_t)pt.terms.size(), (uint32_t)pt.reqs.size(), (uint32_t)pt.vals.size(), 0, 0, 0, 0};
   HIPCHK(hipMemcpyAsync(I.tcounts.p, counts, sizeof(counts), hipMemcpyHostToDevice, s));
+  std::memcpy(I.counts0, counts, sizeof(counts));
+  size_t RN = (size_t)I.R * std::max<uint32_t>(I.N, 1);
+  if (!I.req0.alloc(RN, err) || !I.nzc0.alloc(std::max<uint32_t>(I.N, 1), err) ||
+      !I.nzm0.alloc(std::max<uint32_t>(I.N, 1), err) || !I.podcnt0.alloc(std::max<uint32_t>(I.N, 1), err))
+    return false;
+  HIPCHK(hipMemcpyAsync(I.req0.p, I.req.p, (size_t)I.R * I.N * 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.nzc0.p, I.nzc.p, (size_t)I.N * 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.nzm0.p, I.nzm.p, (size_t)I.N * 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.podcnt0.p, I.podcnt.p, (size_t)I.N * 4, hipMemcpyDeviceToDevice, s));
   // scratch + outputs
   size_t pairs = std::max<uint32_t>(ns.topo_pairs, 1);
   if (!I.cnt.alloc((size_t)KSG_MAX_TSC * std::max<uint32_t>(I.N, 1), err) || !I.hist_f.alloc(pairs, err) ||
@@ -1203,6 +1220,15 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   int pts_pos = -1;
   for (int i = 0; i < F.n; ++i)
     if (F.plugins[i] == KP_PTS) pts_pos = i;
+  if (I.sample_every) {
+    size_t need = 2 * ((count + I.sample_every - 1) / I.sample_every + 1);
+    while (I.sev.size() < need) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      I.sev.push_back(e);
+    }
+  }
+  I.n_samples = 0;
   HIPCHK(hipEventRecord(I.ev0, s));
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
@@ -1229,7 +1255,13 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         hipLaunchKernelGGL(k_pts_reduce, dim3(std::max<uint32_t>(std::min<uint32_t>(gN.x, 256), 1)), b, 0, s, C, S, prog);
       }
     }
+    bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
+    if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
     hipLaunchKernelGGL(k_filter_score, gN, b, 0, s, C, F, S, O, prog);
+    if (sampled) {
+      HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
+      I.n_samples++;
+    }
     if (F.has_ext) {
       if (pts_pos >= 0 && pts) {
         hipLaunchKernelGGL(k_pts_weights, dim3(1), b, 0, s, C, S, O, prog);
@@ -1285,6 +1317,35 @@ bool Engine::read_requested(std::vector<int64_t>& requested, std::vector<int32_t
   HIPCHK(hipMemcpyAsync(requested.data(), I.req.p, requested.size() * 8, hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipMemcpyAsync(pod_count.data(), I.podcnt.p, pod_count.size() * 4, hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
+bool Engine::reset(std::string& err) {
+  Impl& I = *p_;
+  hipStream_t s = I.stream;
+  HIPCHK(hipMemcpyAsync(I.req.p, I.req0.p, (size_t)I.R * I.N * 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.nzc.p, I.nzc0.p, (size_t)I.N * 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.nzm.p, I.nzm0.p, (size_t)I.N * 8, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.podcnt.p, I.podcnt0.p, (size_t)I.N * 4, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.tcounts.p, I.counts0, sizeof(I.counts0), hipMemcpyHostToDevice, s));
+  uint32_t cnt = (uint32_t)I.prog_off.size();
+  if (cnt) hipLaunchKernelGGL(k_init_summaries, dim3((cnt + 255) / 256), dim3(256), 0, s, I.sums.p, cnt, I.F);
+  HIPCHK(hipGetLastError());
+  return true;
+}
+
+void Engine::sample_kernel(uint32_t every) { p_->sample_every = every; }
+
+bool Engine::kernel_time(float& avg_ms, uint32_t& samples, std::string& err) {
+  Impl& I = *p_;
+  double tot = 0;
+  for (uint32_t i = 0; i < I.n_samples; ++i) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, I.sev[2 * i], I.sev[2 * i + 1]));
+    tot += ms;
+  }
+  samples = I.n_samples;
+  avg_ms = I.n_samples ? (float)(tot / I.n_samples) : 0.f;
   return true;
 }
 

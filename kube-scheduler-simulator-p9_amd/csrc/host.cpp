@@ -1447,6 +1447,25 @@ int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len
   return KSG_OK;
 }
 
+int ksg_reset(ksg_ctx* ctx) {
+  if (!ctx) return KSG_E_INVALID;
+  if (!ctx->c.compile_queue()) return ctx->fail(ctx->c.err, KSG_E_INVALID);
+  if (!ctx->c.eng->reset(ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
+  return KSG_OK;
+}
+
+int ksg_sample_kernel(ksg_ctx* ctx, uint32_t every) {
+  if (!ctx) return KSG_E_INVALID;
+  ctx->c.eng->sample_kernel(every);
+  return KSG_OK;
+}
+
+int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples) {
+  if (!ctx || !avg_ms || !samples) return KSG_E_INVALID;
+  if (!ctx->c.eng->kernel_time(*avg_ms, *samples, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
+  return KSG_OK;
+}
+
 int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_pod_result* out) {
   (void)ctx; (void)pod_json; (void)len; (void)commit; (void)out;
   return KSG_E_STATE;  // implemented by the cycle API (next step)

@@ -60,6 +60,9 @@ def load_library():
     L.ksg_filter_codes.argtypes = [vp, u32, ctypes.POINTER(u32), u32]
     L.ksg_scores.argtypes = [vp, u32, u32, ctypes.POINTER(i32), u32]
     L.ksg_annotations.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.ksg_reset.argtypes = [vp]
+    L.ksg_sample_kernel.argtypes = [vp, u32]
+    L.ksg_kernel_time.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32)]
     L.ksg_node_requested.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i32), u32, u32]
     _lib = L
     return L
@@ -146,6 +149,17 @@ class Scheduler:
         buf = ctypes.create_string_buffer(n.value + 1)
         self._chk(self.L.ksg_annotations(self.h, q, buf, n.value + 1, ctypes.byref(n)), "ksg_annotations")
         return json.loads(buf.raw[:n.value].decode())
+
+    def reset(self):
+        self._chk(self.L.ksg_reset(self.h), "ksg_reset")
+
+    def sample_kernel(self, every):
+        self._chk(self.L.ksg_sample_kernel(self.h, every), "ksg_sample_kernel")
+
+    def kernel_time(self):
+        ms, n = ctypes.c_float(), ctypes.c_uint32()
+        self._chk(self.L.ksg_kernel_time(self.h, ctypes.byref(ms), ctypes.byref(n)), "ksg_kernel_time")
+        return ms.value, n.value
 
     def node_requested(self, n_res=8):
         n = self.n_nodes

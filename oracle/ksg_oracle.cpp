@@ -642,31 +642,74 @@ static ResourceList pod_requests(const Pod& p, bool nonzero) {
 }
 
 // ============================================================ parallelize.Until
+// Persistent worker pool (goroutines are cheap in Go; spawning OS threads per
+// call would penalise the CPU baseline).  chunk = max(1, min(sqrt(n), n/workers+1))
+// (framework/parallelize/parallelism.go chunkSizeFor).
 struct Pool {
   int workers;
-  explicit Pool(int w) : workers(w < 1 ? 1 : w) {}
-  // chunk = max(1, min(sqrt(n), n/workers + 1))  (framework/parallelize/parallelism.go chunkSizeFor)
-  void until(int n, const std::function<void(int)>& fn) {
-    if (n <= 0) return;
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  const std::function<void(int)>* fn = nullptr;
+  int n = 0, chunk = 1;
+  std::atomic<int> next{0};
+  int active = 0;
+  unsigned long long gen = 0;
+  bool stop = false;
+  explicit Pool(int w) : workers(w < 1 ? 1 : w) {
+    for (int t = 1; t < workers; ++t) th.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+  void work() {
+    for (;;) {
+      int s = next.fetch_add(chunk);
+      if (s >= n) return;
+      int e = std::min(n, s + chunk);
+      for (int i = s; i < e; ++i) (*fn)(i);
+    }
+  }
+  void loop() {
+    unsigned long long seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+      }
+      work();
+      {
+        std::lock_guard<std::mutex> g(mu);
+        if (--active == 0) done_cv.notify_one();
+      }
+    }
+  }
+  void until(int count, const std::function<void(int)>& f) {
+    if (count <= 0) return;
     if (workers == 1) {
-      for (int i = 0; i < n; ++i) fn(i);
+      for (int i = 0; i < count; ++i) f(i);
       return;
     }
-    int chunk = std::max(1, std::min((int)std::sqrt((double)n), n / workers + 1));
-    std::atomic<int> next{0};
-    auto body = [&]() {
-      for (;;) {
-        int s = next.fetch_add(chunk);
-        if (s >= n) return;
-        int e = std::min(n, s + chunk);
-        for (int i = s; i < e; ++i) fn(i);
-      }
-    };
-    int nt = std::min(workers, (n + chunk - 1) / chunk);
-    vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(body);
-    body();
-    for (auto& t : th) t.join();
+    {
+      std::lock_guard<std::mutex> g(mu);
+      fn = &f;
+      n = count;
+      chunk = std::max(1, std::min((int)std::sqrt((double)count), count / workers + 1));
+      next = 0;
+      active = workers - 1;
+      ++gen;
+    }
+    cv.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(mu);
+    done_cv.wait(g, [&] { return active == 0; });
   }
 };
 
@@ -725,7 +768,7 @@ struct PodResult {
   // store maps (resultstore/store.go result)
   map<string, string> pre_filter_status, pre_score;
   map<string, vector<string>> pre_filter_result;
-  map<string, map<string, string>> filter, score, final_score;
+  std::unordered_map<string, std::unordered_map<string, string>> filter, score, final_score;
 };
 
 // ============================================================ JSON rendering (Go encoding/json)
@@ -763,7 +806,9 @@ static string json_map(const map<string, string>& m) {
   }
   return o + "}";
 }
-static string json_map2(const map<string, map<string, string>>& m) {
+static string json_map2(const std::unordered_map<string, std::unordered_map<string, string>>& um) {
+  map<string, map<string, string>> m;  // encoding/json sorts map keys
+  for (auto& kv : um) m[kv.first] = map<string, string>(kv.second.begin(), kv.second.end());
   string o = "{";
   bool first = true;
   for (auto& kv : m) {
@@ -1751,6 +1796,7 @@ struct ksg_oracle {
   oracle::Cluster c;
   std::string err;
   int next = 0;
+  std::unique_ptr<oracle::Pool> pool;
 };
 
 ksg_oracle* ksg_oracle_load(const char* json, size_t len, char* err, size_t errlen) {
@@ -1774,11 +1820,11 @@ int ksg_oracle_num_queue(ksg_oracle* h) { return (int)h->c.queue.size(); }
 // scheduler does), 2 = also digest the rendered annotations, 3 = also keep them.
 // Returns pods processed.
 int ksg_oracle_schedule(ksg_oracle* h, int n, int workers, int record) {
-  oracle::Pool pool(workers);
+  if (!h->pool || h->pool->workers != (workers < 1 ? 1 : workers)) h->pool.reset(new oracle::Pool(workers));
   int done = 0;
   while (done < n && h->next < (int)h->c.queue.size()) {
     int q = h->next++;
-    h->c.schedule_one(q, h->c.queue[q], pool, record);
+    h->c.schedule_one(q, h->c.queue[q], *h->pool, record);
     ++done;
   }
   return done;

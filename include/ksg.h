@@ -108,6 +108,11 @@ int ksg_reset(ksg_ctx* ctx);
  * for every `every`-th pod of the following ksg_schedule_queue (0 = off). */
 int ksg_sample_kernel(ksg_ctx* ctx, uint32_t every);
 int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples);
+/* Execution path: profiles made only of NodeResourcesFit / BalancedAllocation
+ * run as exact speculative batches (k_batch_eval / merge / fixup); every other
+ * profile runs the per-pod kernel chain.  per_pod != 0 forces the chain. */
+int ksg_set_path(ksg_ctx* ctx, int per_pod);
+int ksg_batch_path(const ksg_ctx* ctx);  /* 1 when the batch path is active */
 
 /* Keep per-(pod, node) outputs for queue pods [first, first+count) (tests,
  * annotation rendering).  Must precede ksg_schedule_queue. */

@@ -95,6 +95,9 @@ class Engine {
   // Sample the dominant kernel (k_filter_score) every `every` pods inside run_queue
   // with HIP events on the engine stream; 0 disables.
   void sample_kernel(uint32_t every);
+  // 1: force the per-pod kernel chain even when the speculative batch path applies
+  void set_path(int per_pod);
+  bool batch_path() const;
   // Average duration (ms) and count of the sampled launches of the last run.
   bool kernel_time(float& avg_ms, uint32_t& samples, std::string& err);
   // Read back the node resource rows (parity tests of the assume delta).

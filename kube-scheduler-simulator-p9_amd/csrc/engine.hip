@@ -940,6 +940,381 @@ __global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* pr
   C.tcounts[3] = vb;
 }
 
+// ----------------------------------------------------------------- speculative batch path
+// For profiles whose plugins are all NodeResourcesFit / BalancedAllocation (no
+// ScoreExtensions, no cross-node state) a pod's result on node n depends only on
+// node n's row.  B pods are evaluated against one snapshot in one wide launch
+// (k_batch_eval); each keeps its top-64 nodes by packed key (k_batch_merge); a
+// one-wave fixup (k_batch_fixup) then replays the B pods in queue order,
+// re-evaluating only the nodes already modified inside the batch (at most B-1 <
+// 64, so one unmodified candidate always survives).  The result is exactly the
+// sequential schedule: same selections, same per-pair outputs (patched for the
+// modified nodes), same assume deltas.
+#define KSG_BATCH 32
+#define KSG_TOPK 64
+
+struct RowV {  // one node row (resource columns 0..3)
+  int64_t alloc[4], req[4];
+  int64_t nzc, nzm;
+  int32_t podcnt, allowed;
+};
+struct CandRow {  // top-K candidate with its snapshot row (96 B)
+  uint64_t key;
+  int64_t alloc[4], req[4];
+  int64_t nzc, nzm;
+  int32_t podcnt, allowed;
+};
+
+struct BatchOut {
+  uint32_t* filter;   // per pod base = filter + slot*N
+  int32_t* score;     // per pod base = score + slot*N*KSG_MAX_PLUGINS
+  int32_t* total;
+  uint32_t slot0;     // slot of the batch's first pod (kept window) or 0 (scratch)
+  int kept;           // 1: slot = pod - keep_first ; 0: slot = pod - first (scratch ring)
+};
+
+__device__ __forceinline__ uint32_t fit_filter_row(const RowV& r, const ksg_prog* h, uint32_t R) {
+  uint32_t bits = 0;
+  if (r.podcnt + 1 > r.allowed) bits |= KSG_FIT_TOO_MANY_PODS;
+  if (h->flags & KPF_ZERO_REQUEST) return bits;
+  for (uint32_t c = 0; c < R; ++c) {
+    int64_t q = h->req[c];
+    if (q > 0 && q > r.alloc[c] - r.req[c]) bits |= 1u << (1 + c);
+  }
+  return bits;
+}
+__device__ __forceinline__ void alloc_req_row(const RowV& r, int res, int64_t pod_req, bool use_requested, int64_t& a,
+                                              int64_t& q) {
+  if (res < 0 || (res >= KSG_RES_EPH + 1 && pod_req == 0)) { a = 0; q = 0; return; }
+  a = r.alloc[res];
+  if (res == KSG_RES_CPU) q = (use_requested ? r.req[0] : r.nzc) + pod_req;
+  else if (res == KSG_RES_MEM) q = (use_requested ? r.req[1] : r.nzm) + pod_req;
+  else q = r.req[res] + pod_req;
+}
+// exact floor(x / a) for 0 <= x < 2^53, a > 0, via f64 then integer correction
+__device__ __forceinline__ int64_t div_small(int64_t x, int64_t a) {
+  int64_t q = (int64_t)__ddiv_rn((double)x, (double)a);
+  if (q * a > x) q--;
+  else if ((q + 1) * a <= x) q++;
+  return q;
+}
+__device__ int64_t fit_score_row(const RowV& r, const DevProfile& F, const ksg_prog* h) {
+  int64_t ns = 0, ws = 0;
+  for (int i = 0; i < F.fit_n; ++i) {
+    int64_t a, q;
+    alloc_req_row(r, F.fit_res[i], h->fit_score_req[i], false, a, q);
+    if (a == 0) continue;
+    int64_t s;
+    if (F.fit_strategy == 2) {
+      s = q > a ? rtc_fn(F, 100) : rtc_fn(F, q * 100 / a);
+      if (s <= 0) continue;
+    } else if (F.fit_strategy == 1) {
+      int64_t m = q > a ? a : q;
+      s = (m < ((int64_t)1 << 46)) ? div_small(m * 100, a) : m * 100 / a;
+    } else {
+      s = q > a ? 0 : ((a - q) < ((int64_t)1 << 46) ? div_small((a - q) * 100, a) : (a - q) * 100 / a);
+    }
+    ns += s * F.fit_w[i];
+    ws += F.fit_w[i];
+  }
+  if (ws == 0) return 0;
+  if (F.fit_strategy == 2) return (int64_t)round(__ddiv_rn((double)ns, (double)ws));
+  return ns / ws;
+}
+__device__ int64_t ba_score_row(const RowV& r, const DevProfile& F, const ksg_prog* h) {
+#pragma clang fp contract(off)
+  double fr[KSG_MAX_SCORE_RES];
+  int m = 0;
+  double total = 0;
+  for (int i = 0; i < F.ba_n; ++i) {
+    int64_t a, q;
+    alloc_req_row(r, F.ba_res[i], h->ba_req[i], true, a, q);
+    if (a == 0) continue;
+    double f = __ddiv_rn((double)q, (double)a);
+    if (f > 1) f = 1;
+    total = __dadd_rn(total, f);
+    fr[m++] = f;
+  }
+  double sd = 0.0;
+  if (m == 2) {
+    sd = fabs(__ddiv_rn(__dsub_rn(fr[0], fr[1]), 2.0));
+  } else if (m > 2) {
+    double mean = __ddiv_rn(total, (double)m);
+    double sum = 0;
+    for (int i = 0; i < m; ++i) {
+      double d = __dsub_rn(fr[i], mean);
+      sum = __dadd_rn(sum, __dmul_rn(d, d));
+    }
+    sd = __dsqrt_rn(__ddiv_rn(sum, (double)m));
+  }
+  return (int64_t)__dmul_rn(__dsub_rn(1.0, sd), 100.0);
+}
+
+// Evaluate one (pod, node row): filter code, raw scores per profile position, total.
+__device__ __forceinline__ uint32_t eval_row(const RowV& r, const DevProfile& F, const ksg_prog* h, uint32_t R,
+                                             int32_t* raw, int64_t& total) {
+  uint32_t code = KSG_FILTER_PASS;
+  for (int pos = 0; pos < F.n; ++pos)
+    if (F.plugins[pos] == KP_FIT) {
+      uint32_t b = fit_filter_row(r, h, R);
+      if (b) { code = ((uint32_t)pos << 24) | b; break; }
+    }
+  total = 0;
+  if (code != KSG_FILTER_PASS) return code;
+#pragma unroll
+  for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+    if (pos >= F.n) break;
+    int64_t s = F.plugins[pos] == KP_FIT ? fit_score_row(r, F, h) : ba_score_row(r, F, h);
+    raw[pos] = (int32_t)s;
+    total += s * F.weight[pos];
+  }
+  return code;
+}
+
+__device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v) {
+  int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      uint64_t o = __shfl_xor(v, j, 64);
+      bool desc = (lane & k) == 0 || k == 64;
+      bool low = (lane & j) == 0;
+      v = (low == desc) ? (v > o ? v : o) : (v < o ? v : o);
+    }
+  return v;
+}
+// v: descending list, o_rev: the other descending list read in reverse lane order
+__device__ __forceinline__ uint64_t wave_merge_top(uint64_t v, uint64_t o_rev) {
+  int lane = threadIdx.x & 63;
+  v = v > o_rev ? v : o_rev;
+#pragma unroll
+  for (int j = 32; j > 0; j >>= 1) {
+    uint64_t o = __shfl_xor(v, j, 64);
+    bool low = (lane & j) == 0;
+    v = low ? (v > o ? v : o) : (v < o ? v : o);
+  }
+  return v;
+}
+
+__device__ __forceinline__ void out_ptrs(const BatchOut& BO, uint32_t b, uint32_t N, uint32_t*& f, int32_t*& s,
+                                         int32_t*& t) {
+  size_t slot = BO.slot0 + b;
+  f = BO.filter + slot * N;
+  s = BO.score + slot * N * KSG_MAX_PLUGINS;
+  t = BO.total + slot * N;
+}
+
+// grid (tiles, pods): one node per thread, one pod per block
+__global__ __launch_bounds__(kBlock) void k_batch_eval(DevCluster C, DevProfile F, BatchOut BO, const uint8_t* progs,
+                                                       const uint64_t* prog_off, uint32_t j0, uint64_t* tile_top,
+                                                       int32_t* feas, uint32_t n_tiles, uint32_t need_eph) {
+  __shared__ uint64_t lists[kBlock];
+  uint32_t b = blockIdx.y;
+  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[j0 + b]);
+  uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+  uint64_t key = 0;
+  bool feasible = false;
+  if (n < C.N) {
+    RowV r;
+    r.alloc[0] = C.alloc[n];
+    r.alloc[1] = C.alloc[(size_t)C.N + n];
+    r.req[0] = C.req[n];
+    r.req[1] = C.req[(size_t)C.N + n];
+    r.alloc[2] = r.req[2] = r.alloc[3] = r.req[3] = 0;
+    if (need_eph)
+      for (uint32_t c = 2; c < C.R && c < 4; ++c) {
+        r.alloc[c] = C.alloc[(size_t)c * C.N + n];
+        r.req[c] = C.req[(size_t)c * C.N + n];
+      }
+    r.nzc = C.nzc[n];
+    r.nzm = C.nzm[n];
+    r.podcnt = C.podcnt[n];
+    r.allowed = C.allowed[n];
+    int32_t raw[KSG_MAX_PLUGINS];
+    int64_t total;
+    uint32_t code = eval_row(r, F, h, C.R < 4 ? C.R : 4, raw, total);
+    uint32_t* of;
+    int32_t *os, *ot;
+    out_ptrs(BO, b, C.N, of, os, ot);
+    of[n] = code;
+    if (code == KSG_FILTER_PASS) {
+      feasible = true;
+      for (int pos = 0; pos < F.n; ++pos) os[(size_t)pos * C.N + n] = raw[pos];
+      ot[n] = (int32_t)total;
+      key = pack_key(total, F.seed, h->queue_idx, C.goff + n);
+    }
+  }
+  unsigned long long bal = __ballot(feasible);
+  if (lane0() && bal) atomicAdd(&feas[b], (int)__popcll(bal));
+  key = wave_sort_desc(key);
+  int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  lists[w * 64 + lane] = key;
+  __syncthreads();
+  if (w == 0) {
+    uint64_t v = lists[lane];
+    for (int k = 1; k < kBlock / 64; ++k) v = wave_merge_top(v, lists[k * 64 + 63 - lane]);
+    tile_top[((size_t)b * n_tiles + blockIdx.x) * KSG_TOPK + lane] = v;
+  }
+}
+
+// one wave per pod: merge the tile lists into the pod's top-64 and gather rows
+__global__ __launch_bounds__(64) void k_batch_merge(DevCluster C, const uint64_t* tile_top, uint32_t n_tiles,
+                                                    CandRow* cand) {
+  uint32_t b = blockIdx.x;
+  int lane = threadIdx.x;
+  const uint64_t* L = tile_top + (size_t)b * n_tiles * KSG_TOPK;
+  uint64_t v = L[lane];
+  uint32_t t = 1;
+  for (; t + 4 <= n_tiles; t += 4) {
+    uint64_t o0 = L[(size_t)t * 64 + 63 - lane], o1 = L[(size_t)(t + 1) * 64 + 63 - lane];
+    uint64_t o2 = L[(size_t)(t + 2) * 64 + 63 - lane], o3 = L[(size_t)(t + 3) * 64 + 63 - lane];
+    v = wave_merge_top(v, o0);
+    v = wave_merge_top(v, o1);
+    v = wave_merge_top(v, o2);
+    v = wave_merge_top(v, o3);
+  }
+  for (; t < n_tiles; ++t) v = wave_merge_top(v, L[(size_t)t * 64 + 63 - lane]);
+  CandRow c;
+  c.key = v;
+  for (int k = 0; k < 4; ++k) c.alloc[k] = c.req[k] = 0;
+  c.nzc = c.nzm = 0;
+  c.podcnt = c.allowed = 0;
+  if (v) {
+    uint32_t n = (uint32_t)(v & 0xFFFFFull) - C.goff;
+    for (uint32_t k = 0; k < C.R && k < 4; ++k) {
+      c.alloc[k] = C.alloc[(size_t)k * C.N + n];
+      c.req[k] = C.req[(size_t)k * C.N + n];
+    }
+    c.nzc = C.nzc[n];
+    c.nzm = C.nzm[n];
+    c.podcnt = C.podcnt[n];
+    c.allowed = C.allowed[n];
+  }
+  cand[(size_t)b * KSG_TOPK + lane] = c;
+}
+
+// one wave: replay the batch in queue order
+__global__ __launch_bounds__(64) void k_batch_fixup(DevCluster C, DevProfile F, BatchOut BO, const uint8_t* progs,
+                                                    const uint64_t* prog_off, uint32_t j0, uint32_t nb,
+                                                    const CandRow* cand, int32_t* feas, ksg_pod_summary* sums) {
+  __shared__ int32_t hset[512];  // open-addressing set of modified global node ids
+  int lane = threadIdx.x;
+  for (int i = lane; i < 512; i += 64) hset[i] = -1;
+  __syncthreads();
+  uint32_t R = C.R < 4 ? C.R : 4;
+  // modified-node state: lane j holds entry j
+  int32_t m_id = -1;
+  RowV cur, snap;
+  for (int k = 0; k < 4; ++k) cur.alloc[k] = cur.req[k] = snap.alloc[k] = snap.req[k] = 0;
+  cur.nzc = cur.nzm = snap.nzc = snap.nzm = 0;
+  cur.podcnt = cur.allowed = snap.podcnt = snap.allowed = 0;
+  int nm = 0;
+  CandRow nxt = cand[lane];
+  for (uint32_t b = 0; b < nb; ++b) {
+    CandRow cr = nxt;
+    if (b + 1 < nb) nxt = cand[(size_t)(b + 1) * KSG_TOPK + lane];
+    const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[j0 + b]);
+    // 1. candidates not modified in this batch
+    uint32_t cnode = (uint32_t)(cr.key & 0xFFFFFull);
+    bool valid = cr.key != 0;
+    if (valid) {
+      uint32_t slot = (cnode * 2654435761u) >> 23;
+      for (;;) {
+        int32_t x = hset[slot];
+        if (x < 0) break;
+        if (x == (int32_t)cnode) { valid = false; break; }
+        slot = (slot + 1) & 511;
+      }
+    }
+    uint64_t best = valid ? cr.key : 0;
+    // 2. modified nodes: exact evaluation on the current row
+    int dfeas = 0;
+    if (lane < nm) {
+      int32_t raw[KSG_MAX_PLUGINS];
+      int64_t tot, tot0;
+      int32_t raw0[KSG_MAX_PLUGINS];
+      uint32_t code = eval_row(cur, F, h, R, raw, tot);
+      uint32_t code0 = eval_row(snap, F, h, R, raw0, tot0);
+      dfeas = (code == KSG_FILTER_PASS ? 1 : 0) - (code0 == KSG_FILTER_PASS ? 1 : 0);
+      uint32_t n = (uint32_t)m_id - C.goff;
+      if ((uint32_t)m_id >= C.goff && n < C.N) {  // patch this pod's per-pair outputs
+        uint32_t* of;
+        int32_t *os, *ot;
+        out_ptrs(BO, b, C.N, of, os, ot);
+        of[n] = code;
+        if (code == KSG_FILTER_PASS) {
+          for (int pos = 0; pos < F.n; ++pos) os[(size_t)pos * C.N + n] = raw[pos];
+          ot[n] = (int32_t)tot;
+        }
+      }
+      if (code == KSG_FILTER_PASS) {
+        uint64_t k = pack_key(tot, F.seed, h->queue_idx, (uint32_t)m_id);
+        best = k > best ? k : best;
+      }
+    }
+    best = wave_max(best);
+    int feasible = feas[b] + (int)wave_sum(dfeas);
+    int32_t sel = (feasible > 0 && best) ? (int32_t)(best & 0xFFFFFull) : -1;
+    if (sel >= 0) {
+      unsigned long long inm = __ballot(lane < nm && m_id == sel);
+      int holder;
+      if (!inm) {  // new modified node: row from the candidate that carries it
+        unsigned long long cl = __ballot(valid && cnode == (uint32_t)sel);
+        int src = __ffsll((long long)cl) - 1;
+        RowV nr;
+        for (int k = 0; k < 4; ++k) {
+          nr.alloc[k] = __shfl(cr.alloc[k], src, 64);
+          nr.req[k] = __shfl(cr.req[k], src, 64);
+        }
+        nr.nzc = __shfl(cr.nzc, src, 64);
+        nr.nzm = __shfl(cr.nzm, src, 64);
+        nr.podcnt = __shfl(cr.podcnt, src, 64);
+        nr.allowed = __shfl(cr.allowed, src, 64);
+        if (lane == nm) {
+          m_id = sel;
+          cur = nr;
+          snap = nr;
+        }
+        if (lane == 0) {
+          uint32_t slot = ((uint32_t)sel * 2654435761u) >> 23;
+          while (hset[slot] >= 0) slot = (slot + 1) & 511;
+          hset[slot] = sel;
+        }
+        holder = nm;
+        nm++;
+        __syncthreads();
+      } else {
+        holder = __ffsll((long long)inm) - 1;
+      }
+      if (lane == holder) {  // assume: NodeInfo.AddPod
+        for (uint32_t k = 0; k < R; ++k) cur.req[k] += h->req[k];
+        cur.nzc += h->nz_cpu;
+        cur.nzm += h->nz_mem;
+        cur.podcnt += 1;
+      }
+    }
+    if (lane == 0) {
+      ksg_pod_summary& s = sums[j0 + b];
+      s.best_key = sel >= 0 ? (feasible == 1 ? (best & 0xFFFFFFFFFFull) : best) : 0;
+      s.selected = sel;
+      s.feasible = feasible;
+      s.status = sel >= 0 ? 0 : 1;
+      feas[b] = 0;  // ready for the next batch
+    }
+  }
+  // write back the modified rows (this shard's nodes)
+  if (lane < nm) {
+    uint32_t n = (uint32_t)m_id - C.goff;
+    if ((uint32_t)m_id >= C.goff && n < C.N) {
+      for (uint32_t k = 0; k < R; ++k) C.req[(size_t)k * C.N + n] = cur.req[k];
+      C.nzc[n] = cur.nzc;
+      C.nzm[n] = cur.nzm;
+      C.podcnt[n] = cur.podcnt;
+    }
+  }
+}
+
 // ----------------------------------------------------------------- host side
 template <class T>
 struct DBuf {
@@ -1005,9 +1380,19 @@ struct Engine::Impl {
   DBuf<int32_t> kscore, ktotal;
   // programs
   DBuf<uint8_t> progs;
+  DBuf<uint64_t> prog_off_d;
+  bool any_eph_req = false;
+  // speculative batch path
+  bool batch_ok = false;
+  DBuf<uint64_t> tile_top;
+  DBuf<int32_t> bfeas;
+  DBuf<CandRow> cand;
+  DBuf<uint32_t> bfilter;
+  DBuf<int32_t> bscore, btotal;
   std::vector<size_t> prog_off;
   std::vector<uint32_t> prog_need;  // bit0 pts, bit1 ipa
   bool has_pts = false, has_ipa = false;
+  bool force_per_pod = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0;
   // pristine copies for reset()
@@ -1094,6 +1479,8 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   F.ipa_hard_weight = cfg.ipa_hard_weight;
   F.ipa_ignore_existing_pref = cfg.ipa_ignore_existing_pref;
   F.seed = cfg.seed;
+  I.batch_ok = F.n > 0;
+  for (int i = 0; i < F.n; ++i) I.batch_ok &= (F.plugins[i] == KP_FIT || F.plugins[i] == KP_BA);
   return true;
 }
 
@@ -1168,7 +1555,66 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
       !I.total.alloc(std::max<uint32_t>(I.N, 1), err))
     return false;
   HIPCHK(hipMemsetAsync(I.exist_any.p, 0, 4, s));
+  if (I.batch_ok && I.R <= 4) {
+    uint32_t T = (I.N + kBlock - 1) / kBlock;
+    size_t Nn = std::max<uint32_t>(I.N, 1);
+    if (!I.tile_top.alloc((size_t)KSG_BATCH * std::max<uint32_t>(T, 1) * KSG_TOPK, err) ||
+        !I.bfeas.alloc(KSG_BATCH, err) || !I.cand.alloc((size_t)KSG_BATCH * KSG_TOPK, err) ||
+        !I.bfilter.alloc(Nn * KSG_BATCH, err) || !I.bscore.alloc(Nn * KSG_BATCH * KSG_MAX_PLUGINS, err) ||
+        !I.btotal.alloc(Nn * KSG_BATCH, err))
+      return false;
+    HIPCHK(hipMemsetAsync(I.bfeas.p, 0, KSG_BATCH * 4, s));
+  }
   HIPCHK(hipStreamSynchronize(s));
+  return true;
+}
+
+// Speculative batches of KSG_BATCH pods (see k_batch_eval); batches never
+// straddle the kept-output window so each batch writes one output region.
+static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::string& err) {
+  if (I.R > 4) { err = "batch path supports at most 4 resource columns"; return false; }
+  hipStream_t s = I.stream;
+  DevCluster C = I.cluster();
+  uint32_t T = (I.N + kBlock - 1) / kBlock;
+  if (I.sample_every) {
+    size_t need = 2 * ((count + KSG_BATCH - 1) / KSG_BATCH + 2);
+    while (I.sev.size() < need) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      I.sev.push_back(e);
+    }
+  }
+  I.n_samples = 0;
+  HIPCHK(hipEventRecord(I.ev0, s));
+  uint32_t end = first + count, j0 = first;
+  while (j0 < end) {
+    uint32_t j1 = std::min(end, j0 + KSG_BATCH);
+    uint32_t kf = I.keep_first, ke = I.keep_first + I.keep_n;
+    bool kept = I.keep_n && j0 >= kf && j0 < ke;
+    if (kept) j1 = std::min(j1, ke);
+    else if (I.keep_n && j0 < kf && j1 > kf) j1 = kf;
+    uint32_t nb = j1 - j0;
+    BatchOut BO;
+    if (kept) {
+      BO.filter = I.kfilter.p; BO.score = I.kscore.p; BO.total = I.ktotal.p; BO.slot0 = j0 - kf; BO.kept = 1;
+    } else {
+      BO.filter = I.bfilter.p; BO.score = I.bscore.p; BO.total = I.btotal.p; BO.slot0 = 0; BO.kept = 0;
+    }
+    bool sampled = I.sample_every && I.n_samples * 2 + 2 <= I.sev.size();
+    if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
+    hipLaunchKernelGGL(k_batch_eval, dim3(T, nb), dim3(kBlock), 0, s, C, I.F, BO, I.progs.p, I.prog_off_d.p, j0,
+                       I.tile_top.p, I.bfeas.p, T, I.any_eph_req ? 1u : 0u);
+    if (sampled) {
+      HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
+      I.n_samples++;
+    }
+    hipLaunchKernelGGL(k_batch_merge, dim3(nb), dim3(64), 0, s, C, I.tile_top.p, T, I.cand.p);
+    hipLaunchKernelGGL(k_batch_fixup, dim3(1), dim3(64), 0, s, C, I.F, BO, I.progs.p, I.prog_off_d.p, j0, nb,
+                       I.cand.p, I.bfeas.p, I.sums.p);
+    j0 = j1;
+  }
+  HIPCHK(hipEventRecord(I.ev1, s));
+  HIPCHK(hipGetLastError());
   return true;
 }
 
@@ -1189,6 +1635,15 @@ bool Engine::set_programs(const std::vector<std::vector<uint8_t>>& progs, std::s
     I.prog_need.push_back(need);
   }
   if (!I.progs.upload(blob, I.stream, err)) return false;
+  std::vector<uint64_t> offs(I.prog_off.begin(), I.prog_off.end());
+  if (!I.prog_off_d.upload(offs, I.stream, err)) return false;
+  I.any_eph_req = false;
+  for (auto& p : progs) {
+    const ksg_prog* h = reinterpret_cast<const ksg_prog*>(p.data());
+    for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
+  }
+  for (int i = 0; i < I.F.fit_n; ++i) I.any_eph_req |= I.F.fit_res[i] >= 2;
+  for (int i = 0; i < I.F.ba_n; ++i) I.any_eph_req |= I.F.ba_res[i] >= 2;
   if (!I.sums.alloc(std::max<size_t>(progs.size(), 1), err)) return false;
   uint32_t cnt = (uint32_t)progs.size();
   if (cnt) {
@@ -1208,9 +1663,12 @@ bool Engine::keep_outputs(uint32_t keep_first, uint32_t keep_n, std::string& err
          I.ktotal.alloc(N * keep_n, err);
 }
 
+static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::string& err);
+
 bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string& err) {
   Impl& I = *p_;
   if (first + count > I.prog_off.size()) { err = "program index out of range"; return false; }
+  if (I.batch_ok && commit && !I.force_per_pod) return run_batches(I, first, count, err);
   hipStream_t s = I.stream;
   DevCluster C = I.cluster();
   DevScratch S = I.scratch();
@@ -1335,6 +1793,8 @@ bool Engine::reset(std::string& err) {
 }
 
 void Engine::sample_kernel(uint32_t every) { p_->sample_every = every; }
+void Engine::set_path(int per_pod) { p_->force_per_pod = per_pod != 0; }
+bool Engine::batch_path() const { return p_->batch_ok && !p_->force_per_pod && p_->R <= 4; }
 
 bool Engine::kernel_time(float& avg_ms, uint32_t& samples, std::string& err) {
   Impl& I = *p_;

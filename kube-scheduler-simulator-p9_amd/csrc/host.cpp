@@ -1460,6 +1460,14 @@ int ksg_sample_kernel(ksg_ctx* ctx, uint32_t every) {
   return KSG_OK;
 }
 
+int ksg_set_path(ksg_ctx* ctx, int per_pod) {
+  if (!ctx) return KSG_E_INVALID;
+  ctx->c.eng->set_path(per_pod);
+  return KSG_OK;
+}
+
+int ksg_batch_path(const ksg_ctx* ctx) { return ctx ? (ctx->c.eng->batch_path() ? 1 : 0) : KSG_E_INVALID; }
+
 int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples) {
   if (!ctx || !avg_ms || !samples) return KSG_E_INVALID;
   if (!ctx->c.eng->kernel_time(*avg_ms, *samples, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);

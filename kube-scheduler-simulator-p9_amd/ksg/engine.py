@@ -62,6 +62,8 @@ def load_library():
     L.ksg_annotations.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.ksg_reset.argtypes = [vp]
     L.ksg_sample_kernel.argtypes = [vp, u32]
+    L.ksg_set_path.argtypes = [vp, ctypes.c_int]
+    L.ksg_batch_path.argtypes = [vp]
     L.ksg_kernel_time.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32)]
     L.ksg_node_requested.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i32), u32, u32]
     _lib = L
@@ -155,6 +157,13 @@ class Scheduler:
 
     def sample_kernel(self, every):
         self._chk(self.L.ksg_sample_kernel(self.h, every), "ksg_sample_kernel")
+
+    def set_path(self, per_pod: bool):
+        self._chk(self.L.ksg_set_path(self.h, 1 if per_pod else 0), "ksg_set_path")
+
+    @property
+    def batch_path(self) -> bool:
+        return self.L.ksg_batch_path(self.h) == 1
 
     def kernel_time(self):
         ms, n = ctypes.c_float(), ctypes.c_uint32()

@@ -77,3 +77,54 @@ def test_known_answer_readme_example():
         assert fin[node]["NodeResourcesFit"] == "73"
         assert fin[node]["NodeResourcesBalancedAllocation"] == "76"
         assert fin[node]["TaintToleration"] == "300"
+
+
+def _tight_cluster(n_nodes=24, n_pods=700, seed=7):
+    """Few small nodes, many pods: nodes fill up (Too many pods / Insufficient cpu|memory),
+    so the speculative batches must re-evaluate modified nodes and drop feasibility."""
+    r = g.Rng(seed)
+    nodes = [g.node_obj(f"node-{i:07d}", 2000 + 1000 * r.below(4), (4 + 4 * r.below(4)) * g.Gi, pods=10 + r.below(30))
+             for i in range(n_nodes)]
+    queue = []
+    for j in range(n_pods):
+        if r.pct() < 15:
+            queue.append(g.pod_obj(f"pod-{j:07d}", [{}]))
+        else:
+            queue.append(g.pod_obj(f"pod-{j:07d}", [g.req(50 * (1 + r.below(8)), 64 * g.Mi * (1 + r.below(8)))]))
+    prof = g.make_profile([("NodeResourcesFit", 1), ("NodeResourcesBalancedAllocation", 1)], seed)
+    return {"profile": prof, "nodes": nodes, "pods": [], "queue": queue}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("per_pod", [False, True], ids=["batch", "per-pod"])
+def test_tight_cluster_both_paths(per_pod):
+    doc = _tight_cluster()
+    o = Oracle(doc)
+    o.schedule(record=3)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    s.set_path(per_pod)
+    assert s.batch_path == (not per_pod)
+    s.keep_outputs(0, s.queue_len)
+    s.schedule()
+    res = s.results()
+    got = [(r.selected, r.feasible, r.status) for r in res]
+    want = [o.result(q) for q in range(len(res))]
+    assert sum(1 for w in want if w[2] == 1) > 20, "cluster should saturate"
+    assert got == want
+    for q in range(0, s.queue_len, 7):
+        assert s.annotations(q) == o.annotations(q), q
+
+
+@pytest.mark.gpu
+def test_cfg2_large_batch_path_selected_nodes():
+    """Full-width cfg2 node count, a queue of 1,000 pods: every selection equals the oracle's."""
+    doc = g.generate(2, n_nodes=5000, n_pods=1000)
+    o = Oracle(doc)
+    o.schedule(workers=8, record=0)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    assert s.batch_path
+    s.schedule()
+    got = [(r.selected, r.feasible, r.status) for r in s.results()]
+    assert got == [o.result(q) for q in range(len(got))]

@@ -64,9 +64,9 @@ struct DevCluster {
   const int64_t* vnum;
   const uint8_t* vok;
   uint32_t n_topo, pairs;
-  int32_t topo_key[KSG_MAX_TOPO];
-  uint32_t topo_base[KSG_MAX_TOPO];
-  uint32_t topo_count[KSG_MAX_TOPO];
+  const int32_t* tkey;     // [n_topo] node label key of each topology slot (device memory:
+  const uint32_t* tbase;   // runtime-indexed kernel-argument arrays would spill to scratch)
+  const uint32_t* tcount;
   // existing-pod table
   uint32_t pcap, pkeys, tcap, rcap, vcap;
   int32_t* ptnode;
@@ -93,6 +93,8 @@ struct DevProfile {
   int64_t ipa_hard_weight;
   int ipa_ignore_existing_pref;
   uint64_t seed;
+  int pos_fit, pos_ba;  // profile positions (-1 absent)
+  int64_t w_fit, w_ba;
 };
 
 struct DevScratch {
@@ -323,54 +325,80 @@ __device__ int64_t rtc_fn(const DevProfile& F, int64_t p) {
   return F.rtc_score[F.rtc_n - 1];
 }
 
-__device__ int64_t fit_score(const DevCluster& C, const DevProfile& F, const ProgView& V, uint32_t n) {
-#pragma clang fp contract(off)
+__device__ __forceinline__ int64_t fit_score(const DevCluster& C, const DevProfile& F, const ProgView& V, uint32_t n) {
   int64_t ns = 0, ws = 0;
-  for (int i = 0; i < F.fit_n; ++i) {
-    int64_t a, q;
-    alloc_req(C, n, F.fit_res[i], V.h->fit_score_req[i], false, a, q);
-    if (a == 0) continue;
-    int64_t s;
-    if (F.fit_strategy == 2) {
-      s = q > a ? rtc_fn(F, 100) : rtc_fn(F, q * 100 / a);
-      if (s <= 0) continue;
-    } else if (F.fit_strategy == 1) {
-      s = (q > a ? a : q) * 100 / a;
-    } else {
-      s = q > a ? 0 : (a - q) * 100 / a;
+#pragma unroll
+  for (int i = 0; i < KSG_MAX_SCORE_RES; ++i) {
+    if (i < F.fit_n) {
+      int64_t a, q;
+      alloc_req(C, n, F.fit_res[i], V.h->fit_score_req[i], false, a, q);
+      if (a != 0) {
+        int64_t s;
+        bool use = true;
+        if (F.fit_strategy == 2) {
+          s = q > a ? rtc_fn(F, 100) : rtc_fn(F, q * 100 / a);
+          use = s > 0;
+        } else if (F.fit_strategy == 1) {
+          s = (q > a ? a : q) * 100 / a;
+        } else {
+          s = q > a ? 0 : (a - q) * 100 / a;
+        }
+        if (use) {
+          ns += s * F.fit_w[i];
+          ws += F.fit_w[i];
+        }
+      }
     }
-    ns += s * F.fit_w[i];
-    ws += F.fit_w[i];
   }
   if (ws == 0) return 0;
   if (F.fit_strategy == 2) return (int64_t)round(__ddiv_rn((double)ns, (double)ws));
   return ns / ws;
 }
 
-__device__ int64_t ba_score(const DevCluster& C, const DevProfile& F, const ProgView& V, uint32_t n) {
+__device__ __forceinline__ int64_t ba_score(const DevCluster& C, const DevProfile& F, const ProgView& V, uint32_t n) {
 #pragma clang fp contract(off)
   double fr[KSG_MAX_SCORE_RES];
+  bool ok[KSG_MAX_SCORE_RES];
   int m = 0;
   double total = 0;
-  for (int i = 0; i < F.ba_n; ++i) {
-    int64_t a, q;
-    alloc_req(C, n, F.ba_res[i], V.h->ba_req[i], true, a, q);
-    if (a == 0) continue;
-    double f = __ddiv_rn((double)q, (double)a);
-    if (f > 1) f = 1;
-    total = __dadd_rn(total, f);
-    fr[m++] = f;
+#pragma unroll
+  for (int i = 0; i < KSG_MAX_SCORE_RES; ++i) {
+    ok[i] = false;
+    fr[i] = 0;
+    if (i < F.ba_n) {
+      int64_t a, q;
+      alloc_req(C, n, F.ba_res[i], V.h->ba_req[i], true, a, q);
+      if (a != 0) {
+        double f = __ddiv_rn((double)q, (double)a);
+        if (f > 1) f = 1;
+        total = __dadd_rn(total, f);
+        fr[i] = f;
+        ok[i] = true;
+        m++;
+      }
+    }
   }
   double sd = 0.0;
   if (m == 2) {
-    sd = fabs(__ddiv_rn(__dsub_rn(fr[0], fr[1]), 2.0));
+    double f0 = 0, f1 = 0;
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < KSG_MAX_SCORE_RES; ++i)
+      if (ok[i]) {
+        if (c == 0) f0 = fr[i];
+        else if (c == 1) f1 = fr[i];
+        c++;
+      }
+    sd = fabs(__ddiv_rn(__dsub_rn(f0, f1), 2.0));
   } else if (m > 2) {
     double mean = __ddiv_rn(total, (double)m);
     double sum = 0;
-    for (int i = 0; i < m; ++i) {
-      double d = __dsub_rn(fr[i], mean);
-      sum = __dadd_rn(sum, __dmul_rn(d, d));
-    }
+#pragma unroll
+    for (int i = 0; i < KSG_MAX_SCORE_RES; ++i)
+      if (ok[i]) {
+        double d = __dsub_rn(fr[i], mean);
+        sum = __dadd_rn(sum, __dmul_rn(d, d));
+      }
     sd = __dsqrt_rn(__ddiv_rn(sum, (double)m));
   }
   return (int64_t)__dmul_rn(__dsub_rn(1.0, sd), 100.0);
@@ -407,7 +435,7 @@ __device__ __forceinline__ int pts_filter(const DevCluster& C, const DevScratch&
     int32_t dom = S.pts_dom[t.topo];
     if (dom == 0) { error = true; return 0; }  // minMatchNum: no domains for key -> Error status
     int64_t mn = dom < t.min_domains ? 0 : S.pts_min[t.topo];
-    int64_t match = S.hist_f[C.topo_base[t.topo] + v];
+    int64_t match = S.hist_f[C.tbase[t.topo] + v];
     if (match + t.self_match - mn > t.max_skew) return 1 + KSG_PTS_SKEW;
   }
   return 0;
@@ -423,19 +451,19 @@ __device__ __forceinline__ int ipa_filter(const DevCluster& C, const DevScratch&
   for (int i = 0; i < h->n_req_aff; ++i) {
     int32_t v = node_vid(C, aff[i].topo_key, n);
     if (v < 0) return 1 + KSG_IPA_AFFINITY;
-    if (S.ipa_aff[C.topo_base[aff[i].topo] + v] <= 0) pods_exist = false;
+    if (S.ipa_aff[C.tbase[aff[i].topo] + v] <= 0) pods_exist = false;
   }
   if (!pods_exist && !(!(ipa_flags & 1u) && h->self_matches_all)) return 1 + KSG_IPA_AFFINITY;
   if (ipa_flags & 2u)
     for (int i = 0; i < h->n_req_anti; ++i) {
       int32_t v = node_vid(C, anti[i].topo_key, n);
-      if (v >= 0 && S.ipa_anti[C.topo_base[anti[i].topo] + v] > 0) return 1 + KSG_IPA_ANTI_AFFINITY;
+      if (v >= 0 && S.ipa_anti[C.tbase[anti[i].topo] + v] > 0) return 1 + KSG_IPA_ANTI_AFFINITY;
     }
   if (exist_any)
     for (uint32_t s = 0; s < C.n_topo; ++s) {
       if (!((exist_any >> s) & 1u)) continue;
-      int32_t v = node_vid(C, C.topo_key[s], n);
-      if (v >= 0 && S.ipa_exist[C.topo_base[s] + v] > 0) return 1 + KSG_IPA_EXISTING_ANTI;
+      int32_t v = node_vid(C, C.tkey[s], n);
+      if (v >= 0 && S.ipa_exist[C.tbase[s] + v] > 0) return 1 + KSG_IPA_EXISTING_ANTI;
     }
   return 0;
 }
@@ -443,8 +471,8 @@ __device__ __forceinline__ int ipa_filter(const DevCluster& C, const DevScratch&
 __device__ __forceinline__ int64_t ipa_score(const DevCluster& C, const DevScratch& S, uint32_t n) {
   int64_t s = 0;
   for (uint32_t t = 0; t < C.n_topo; ++t) {
-    int32_t v = node_vid(C, C.topo_key[t], n);
-    if (v >= 0) s += S.ipa_score[C.topo_base[t] + v];
+    int32_t v = node_vid(C, C.tkey[t], n);
+    if (v >= 0) s += S.ipa_score[C.tbase[t] + v];
   }
   return s;
 }
@@ -514,13 +542,13 @@ __global__ void k_scan_pods(DevCluster C, DevProfile F, DevScratch S, DevOut O, 
       if (all)
         for (int i = 0; i < h->n_req_aff; ++i) {
           int32_t v = node_vid(C, aff[i].topo_key, node);
-          if (v >= 0) { atomicAdd(&S.ipa_aff[C.topo_base[aff[i].topo] + v], 1); aff_hit |= 1u; }
+          if (v >= 0) { atomicAdd(&S.ipa_aff[C.tbase[aff[i].topo] + v], 1); aff_hit |= 1u; }
         }
     }
     for (int i = 0; i < h->n_req_anti; ++i)
       if (term_ok(anti[i])) {
         int32_t v = node_vid(C, anti[i].topo_key, node);
-        if (v >= 0) { atomicAdd(&S.ipa_anti[C.topo_base[anti[i].topo] + v], 1); aff_hit |= 2u; }
+        if (v >= 0) { atomicAdd(&S.ipa_anti[C.tbase[anti[i].topo] + v], 1); aff_hit |= 2u; }
       }
     if ((h->flags & KPF_IPA_HAS_CONSTRAINTS) && C.haslab[node]) {
       for (int i = 0; i < h->n_pref_aff + h->n_pref_anti; ++i) {
@@ -529,7 +557,7 @@ __global__ void k_scan_pods(DevCluster C, DevProfile F, DevScratch S, DevOut O, 
         int32_t v = node_vid(C, t.topo_key, node);
         if (v < 0) continue;
         int64_t w = i < h->n_pref_aff ? (int64_t)t.weight : -(int64_t)t.weight;
-        atomicAdd((unsigned long long*)&S.ipa_score[C.topo_base[t.topo] + v], (unsigned long long)w);
+        atomicAdd((unsigned long long*)&S.ipa_score[C.tbase[t.topo] + v], (unsigned long long)w);
         aff_hit |= 8u;
       }
     }
@@ -558,7 +586,7 @@ __global__ void k_scan_terms(DevCluster C, DevProfile F, DevScratch S, DevOut O,
     if (ns_ok && sel_eval(e.sel, C.treq, C.tval, vid)) {
       int32_t v = node_vid(C, e.topo_key, node);
       if (v >= 0) {
-        uint32_t pair = C.topo_base[e.topo] + v;
+        uint32_t pair = C.tbase[e.topo] + v;
         if (e.kind == 1) {
           atomicAdd(&S.ipa_exist[pair], 1);
           slots |= 1u << e.topo;
@@ -605,7 +633,7 @@ __global__ void k_pts_prep(DevCluster C, DevScratch S, const uint8_t* prog) {
       if ((done >> t.topo) & 1u) continue;
       if ((t.honor_affinity && !na_ok) || (t.honor_taints && !taint_ok)) continue;
       done |= 1u << t.topo;
-      uint32_t pair = C.topo_base[t.topo] + node_vid(C, t.topo_key, n);
+      uint32_t pair = C.tbase[t.topo] + node_vid(C, t.topo_key, n);
       int32_t cnt = S.cnt[(size_t)c * C.N + n];
       if (cnt) atomicAdd(&S.hist_f[pair], cnt);
       S.present_f[pair] = 1;
@@ -616,7 +644,7 @@ __global__ void k_pts_prep(DevCluster C, DevScratch S, const uint8_t* prog) {
       const ksg_tsc& t = h->tsc[c];
       if (t.is_hostname) continue;
       if ((t.honor_affinity && !na_ok) || (t.honor_taints && !taint_ok)) continue;
-      uint32_t pair = C.topo_base[t.topo] + node_vid(C, t.topo_key, n);
+      uint32_t pair = C.tbase[t.topo] + node_vid(C, t.topo_key, n);
       int32_t cnt = S.cnt[(size_t)c * C.N + n];
       if (cnt) atomicAdd(&S.hist_s[pair], cnt);
     }
@@ -632,7 +660,7 @@ __global__ void k_pts_reduce(DevCluster C, DevScratch S, const uint8_t* prog) {
     int slot = h->tsc[c].topo;
     if ((seen >> slot) & 1u) continue;
     seen |= 1u << slot;
-    uint32_t base = C.topo_base[slot], cnt = C.topo_count[slot];
+    uint32_t base = C.tbase[slot], cnt = C.tcount[slot];
     int32_t mn = 0x7FFFFFFF;
     int32_t dom = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
@@ -666,7 +694,9 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
   if (active && !(h->flags & KPF_PREFILTER_REJECT) &&
       !((h->flags & KPF_RESTRICT) && !bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n))) {
     code = KSG_FILTER_PASS;
-    for (int pos = 0; pos < F.n && code == KSG_FILTER_PASS; ++pos) {
+#pragma unroll
+    for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+      if (pos >= F.n || code != KSG_FILTER_PASS) continue;
       uint32_t detail = 0;
       bool fail = false;
       switch (F.plugins[pos]) {
@@ -703,9 +733,12 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
   uint64_t best = 0;
   int32_t total = 0;
   bool range_err = false;
-  for (int pos = 0; pos < F.n; ++pos) raw[pos] = 0;
+#pragma unroll
+  for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) raw[pos] = 0;
   if (feasible) {
-    for (int pos = 0; pos < F.n; ++pos) {
+#pragma unroll
+    for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+      if (pos >= F.n) continue;
       int64_t s = 0;
       switch (F.plugins[pos]) {
         case KP_FIT: s = fit_score(C, F, V, n); break;
@@ -724,12 +757,14 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
         atomicAdd(&O.sum->ignored, 1);
       } else {
         for (int c = nf; c < nf + ns; ++c)
-          if (!h->tsc[c].is_hostname) S.reg[C.topo_base[h->tsc[c].topo] + node_vid(C, h->tsc[c].topo_key, n)] = 1;
+          if (!h->tsc[c].is_hostname) S.reg[C.tbase[h->tsc[c].topo] + node_vid(C, h->tsc[c].topo_key, n)] = 1;
       }
     }
     if (!F.has_ext) {
       int64_t tot = 0;
-      for (int pos = 0; pos < F.n; ++pos) {
+#pragma unroll
+      for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+        if (pos >= F.n) continue;
         if (raw[pos] < 0 || raw[pos] > 100) range_err = true;
         tot += raw[pos] * F.weight[pos];
       }
@@ -740,7 +775,9 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
   if (active) {
     O.filter[n] = code;
     if (feasible) {
-      for (int pos = 0; pos < F.n; ++pos) O.score[(size_t)pos * C.N + n] = (int32_t)raw[pos];
+#pragma unroll
+      for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos)
+        if (pos < F.n) O.score[(size_t)pos * C.N + n] = (int32_t)raw[pos];
       if (!F.has_ext) O.total[n] = total;
     }
   }
@@ -750,7 +787,9 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
   if (__any(err) && lane0()) atomicOr((uint32_t*)&O.sum->status, 2u);
   if (__any(range_err) && lane0()) atomicOr((uint32_t*)&O.sum->status, 2u);
   if (bal) {
-    for (int pos = 0; pos < F.n; ++pos) {
+#pragma unroll
+    for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+      if (pos >= F.n) continue;
       int p = F.plugins[pos];
       if (p == KP_TAINT || p == KP_NA || p == KP_IPA) {
         int64_t mx = wave_max(feasible ? raw[pos] : INT64_MIN);
@@ -780,7 +819,7 @@ __global__ void k_pts_weights(DevCluster C, DevScratch S, DevOut O, const uint8_
     if (t.is_hostname) {
       size = (int64_t)O.sum->feasible - O.sum->ignored;
     } else if (t.first_of_key) {
-      uint32_t base = C.topo_base[t.topo], cnt = C.topo_count[t.topo];
+      uint32_t base = C.tbase[t.topo], cnt = C.tcount[t.topo];
       int32_t x = 0;
       for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) x += S.reg[base + i];
       x = (int32_t)wave_sum(x);
@@ -810,7 +849,7 @@ __global__ void k_pts_score(DevCluster C, DevScratch S, DevOut O, const uint8_t*
       const ksg_tsc& t = h->tsc[c];
       int32_t v = node_vid(C, t.topo_key, n);
       if (v < 0) continue;
-      int64_t cnt = t.is_hostname ? S.cnt[(size_t)c * C.N + n] : S.hist_s[C.topo_base[t.topo] + v];
+      int64_t cnt = t.is_hostname ? S.cnt[(size_t)c * C.N + n] : S.hist_s[C.tbase[t.topo] + v];
       score = __dadd_rn(score, __dadd_rn(__dmul_rn((double)cnt, O.sum->pts_weight[c - nf]), (double)(t.max_skew - 1)));
     }
     s = (int64_t)round(score);
@@ -952,6 +991,7 @@ __global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* pr
 // modified nodes), same assume deltas.
 #define KSG_BATCH 32
 #define KSG_TOPK 64
+#define KSG_CAND 32  // candidates kept per pod (>= KSG_BATCH guarantees a surviving one)
 
 struct RowV {  // one node row (resource columns 0..3)
   int64_t alloc[4], req[4];
@@ -965,6 +1005,15 @@ struct CandRow {  // top-K candidate with its snapshot row (96 B)
   int32_t podcnt, allowed;
 };
 
+struct PodLite {  // the fields of ksg_prog the Fit/BA evaluation reads (LDS-staged)
+  int64_t req[4];
+  int64_t fit_score_req[KSG_MAX_SCORE_RES];
+  int64_t ba_req[KSG_MAX_SCORE_RES];
+  int64_t nz_cpu, nz_mem;
+  int32_t queue_idx;
+  uint32_t flags;
+};
+
 struct BatchOut {
   uint32_t* filter;   // per pod base = filter + slot*N
   int32_t* score;     // per pod base = score + slot*N*KSG_MAX_PLUGINS
@@ -973,23 +1022,32 @@ struct BatchOut {
   int kept;           // 1: slot = pod - keep_first ; 0: slot = pod - first (scratch ring)
 };
 
-__device__ __forceinline__ uint32_t fit_filter_row(const RowV& r, const ksg_prog* h, uint32_t R) {
+// Register-resident row evaluation: every loop has a compile-time trip count and
+// a runtime guard so no local array is indexed dynamically (no scratch).
+__device__ __forceinline__ int64_t sel4(const int64_t (&v)[4], int i) {
+  return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3];
+}
+template <class P>
+__device__ __forceinline__ uint32_t fit_filter_row(const RowV& r, const P* h, uint32_t R) {
   uint32_t bits = 0;
   if (r.podcnt + 1 > r.allowed) bits |= KSG_FIT_TOO_MANY_PODS;
   if (h->flags & KPF_ZERO_REQUEST) return bits;
-  for (uint32_t c = 0; c < R; ++c) {
-    int64_t q = h->req[c];
-    if (q > 0 && q > r.alloc[c] - r.req[c]) bits |= 1u << (1 + c);
+#pragma unroll
+  for (uint32_t c = 0; c < 4; ++c) {
+    if (c < R) {
+      int64_t q = h->req[c];
+      if (q > 0 && q > r.alloc[c] - r.req[c]) bits |= 1u << (1 + c);
+    }
   }
   return bits;
 }
 __device__ __forceinline__ void alloc_req_row(const RowV& r, int res, int64_t pod_req, bool use_requested, int64_t& a,
                                               int64_t& q) {
-  if (res < 0 || (res >= KSG_RES_EPH + 1 && pod_req == 0)) { a = 0; q = 0; return; }
-  a = r.alloc[res];
+  if (res < 0 || res > 3 || (res >= KSG_RES_EPH + 1 && pod_req == 0)) { a = 0; q = 0; return; }
+  a = sel4(r.alloc, res);
   if (res == KSG_RES_CPU) q = (use_requested ? r.req[0] : r.nzc) + pod_req;
   else if (res == KSG_RES_MEM) q = (use_requested ? r.req[1] : r.nzm) + pod_req;
-  else q = r.req[res] + pod_req;
+  else q = sel4(r.req, res) + pod_req;
 }
 // exact floor(x / a) for 0 <= x < 2^53, a > 0, via f64 then integer correction
 __device__ __forceinline__ int64_t div_small(int64_t x, int64_t a) {
@@ -998,77 +1056,113 @@ __device__ __forceinline__ int64_t div_small(int64_t x, int64_t a) {
   else if ((q + 1) * a <= x) q++;
   return q;
 }
-__device__ int64_t fit_score_row(const RowV& r, const DevProfile& F, const ksg_prog* h) {
+template <class P>
+__device__ __forceinline__ int64_t fit_score_row(const RowV& r, const DevProfile& F, const P* h) {
   int64_t ns = 0, ws = 0;
-  for (int i = 0; i < F.fit_n; ++i) {
-    int64_t a, q;
-    alloc_req_row(r, F.fit_res[i], h->fit_score_req[i], false, a, q);
-    if (a == 0) continue;
-    int64_t s;
-    if (F.fit_strategy == 2) {
-      s = q > a ? rtc_fn(F, 100) : rtc_fn(F, q * 100 / a);
-      if (s <= 0) continue;
-    } else if (F.fit_strategy == 1) {
-      int64_t m = q > a ? a : q;
-      s = (m < ((int64_t)1 << 46)) ? div_small(m * 100, a) : m * 100 / a;
-    } else {
-      s = q > a ? 0 : ((a - q) < ((int64_t)1 << 46) ? div_small((a - q) * 100, a) : (a - q) * 100 / a);
+#pragma unroll
+  for (int i = 0; i < KSG_MAX_SCORE_RES; ++i) {
+    if (i < F.fit_n) {
+      int64_t a, q;
+      alloc_req_row(r, F.fit_res[i], h->fit_score_req[i], false, a, q);
+      if (a != 0) {
+        int64_t s;
+        bool use = true;
+        if (F.fit_strategy == 2) {
+          s = q > a ? rtc_fn(F, 100) : rtc_fn(F, q * 100 / a);
+          use = s > 0;
+        } else if (F.fit_strategy == 1) {
+          int64_t m = q > a ? a : q;
+          s = (m < ((int64_t)1 << 46)) ? div_small(m * 100, a) : m * 100 / a;
+        } else {
+          s = q > a ? 0 : ((a - q) < ((int64_t)1 << 46) ? div_small((a - q) * 100, a) : (a - q) * 100 / a);
+        }
+        if (use) {
+          ns += s * F.fit_w[i];
+          ws += F.fit_w[i];
+        }
+      }
     }
-    ns += s * F.fit_w[i];
-    ws += F.fit_w[i];
   }
   if (ws == 0) return 0;
   if (F.fit_strategy == 2) return (int64_t)round(__ddiv_rn((double)ns, (double)ws));
   return ns / ws;
 }
-__device__ int64_t ba_score_row(const RowV& r, const DevProfile& F, const ksg_prog* h) {
+template <class P>
+__device__ __forceinline__ int64_t ba_score_row(const RowV& r, const DevProfile& F, const P* h) {
 #pragma clang fp contract(off)
   double fr[KSG_MAX_SCORE_RES];
+  bool ok[KSG_MAX_SCORE_RES];
   int m = 0;
   double total = 0;
-  for (int i = 0; i < F.ba_n; ++i) {
-    int64_t a, q;
-    alloc_req_row(r, F.ba_res[i], h->ba_req[i], true, a, q);
-    if (a == 0) continue;
-    double f = __ddiv_rn((double)q, (double)a);
-    if (f > 1) f = 1;
-    total = __dadd_rn(total, f);
-    fr[m++] = f;
+#pragma unroll
+  for (int i = 0; i < KSG_MAX_SCORE_RES; ++i) {
+    ok[i] = false;
+    fr[i] = 0;
+    if (i < F.ba_n) {
+      int64_t a, q;
+      alloc_req_row(r, F.ba_res[i], h->ba_req[i], true, a, q);
+      if (a != 0) {
+        double f = __ddiv_rn((double)q, (double)a);
+        if (f > 1) f = 1;
+        total = __dadd_rn(total, f);
+        fr[i] = f;
+        ok[i] = true;
+        m++;
+      }
+    }
   }
   double sd = 0.0;
   if (m == 2) {
-    sd = fabs(__ddiv_rn(__dsub_rn(fr[0], fr[1]), 2.0));
+    double f0 = 0, f1 = 0;
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < KSG_MAX_SCORE_RES; ++i)
+      if (ok[i]) {
+        if (c == 0) f0 = fr[i];
+        else if (c == 1) f1 = fr[i];
+        c++;
+      }
+    sd = fabs(__ddiv_rn(__dsub_rn(f0, f1), 2.0));
   } else if (m > 2) {
     double mean = __ddiv_rn(total, (double)m);
     double sum = 0;
-    for (int i = 0; i < m; ++i) {
-      double d = __dsub_rn(fr[i], mean);
-      sum = __dadd_rn(sum, __dmul_rn(d, d));
-    }
+#pragma unroll
+    for (int i = 0; i < KSG_MAX_SCORE_RES; ++i)
+      if (ok[i]) {
+        double d = __dsub_rn(fr[i], mean);
+        sum = __dadd_rn(sum, __dmul_rn(d, d));
+      }
     sd = __dsqrt_rn(__ddiv_rn(sum, (double)m));
   }
   return (int64_t)__dmul_rn(__dsub_rn(1.0, sd), 100.0);
 }
 
-// Evaluate one (pod, node row): filter code, raw scores per profile position, total.
-__device__ __forceinline__ uint32_t eval_row(const RowV& r, const DevProfile& F, const ksg_prog* h, uint32_t R,
-                                             int32_t* raw, int64_t& total) {
-  uint32_t code = KSG_FILTER_PASS;
-  for (int pos = 0; pos < F.n; ++pos)
-    if (F.plugins[pos] == KP_FIT) {
-      uint32_t b = fit_filter_row(r, h, R);
-      if (b) { code = ((uint32_t)pos << 24) | b; break; }
-    }
+// Evaluate one (pod, node row) for a Fit/BA profile: filter code, raw Fit and BA, total.
+template <class P>
+__device__ __forceinline__ uint32_t eval_row(const RowV& r, const DevProfile& F, const P* h, uint32_t R,
+                                             int32_t& fit_s, int32_t& ba_s, int64_t& total) {
   total = 0;
-  if (code != KSG_FILTER_PASS) return code;
-#pragma unroll
-  for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
-    if (pos >= F.n) break;
-    int64_t s = F.plugins[pos] == KP_FIT ? fit_score_row(r, F, h) : ba_score_row(r, F, h);
-    raw[pos] = (int32_t)s;
-    total += s * F.weight[pos];
+  fit_s = ba_s = 0;
+  if (F.pos_fit >= 0) {
+    uint32_t b = fit_filter_row(r, h, R);
+    if (b) return ((uint32_t)F.pos_fit << 24) | b;
+    fit_s = (int32_t)fit_score_row(r, F, h);
+    total += (int64_t)fit_s * F.w_fit;
   }
-  return code;
+  if (F.pos_ba >= 0) {
+    ba_s = (int32_t)ba_score_row(r, F, h);
+    total += (int64_t)ba_s * F.w_ba;
+  }
+  return KSG_FILTER_PASS;
+}
+__device__ __forceinline__ void write_pair(const DevProfile& F, uint32_t* of, int32_t* os, int32_t* ot, uint32_t N,
+                                           uint32_t n, uint32_t code, int32_t fit_s, int32_t ba_s, int64_t tot) {
+  of[n] = code;
+  if (code == KSG_FILTER_PASS) {
+    if (F.pos_fit >= 0) os[(size_t)F.pos_fit * N + n] = fit_s;
+    if (F.pos_ba >= 0) os[(size_t)F.pos_ba * N + n] = ba_s;
+    ot[n] = (int32_t)tot;
+  }
 }
 
 __device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v) {
@@ -1122,26 +1216,27 @@ __global__ __launch_bounds__(kBlock) void k_batch_eval(DevCluster C, DevProfile 
     r.req[0] = C.req[n];
     r.req[1] = C.req[(size_t)C.N + n];
     r.alloc[2] = r.req[2] = r.alloc[3] = r.req[3] = 0;
-    if (need_eph)
-      for (uint32_t c = 2; c < C.R && c < 4; ++c) {
-        r.alloc[c] = C.alloc[(size_t)c * C.N + n];
-        r.req[c] = C.req[(size_t)c * C.N + n];
-      }
+    if (need_eph) {
+#pragma unroll
+      for (uint32_t c = 2; c < 4; ++c)
+        if (c < C.R) {
+          r.alloc[c] = C.alloc[(size_t)c * C.N + n];
+          r.req[c] = C.req[(size_t)c * C.N + n];
+        }
+    }
     r.nzc = C.nzc[n];
     r.nzm = C.nzm[n];
     r.podcnt = C.podcnt[n];
     r.allowed = C.allowed[n];
-    int32_t raw[KSG_MAX_PLUGINS];
+    int32_t fit_s, ba_s;
     int64_t total;
-    uint32_t code = eval_row(r, F, h, C.R < 4 ? C.R : 4, raw, total);
+    uint32_t code = eval_row(r, F, h, C.R < 4 ? C.R : 4, fit_s, ba_s, total);
     uint32_t* of;
     int32_t *os, *ot;
     out_ptrs(BO, b, C.N, of, os, ot);
-    of[n] = code;
+    write_pair(F, of, os, ot, C.N, n, code, fit_s, ba_s, total);
     if (code == KSG_FILTER_PASS) {
       feasible = true;
-      for (int pos = 0; pos < F.n; ++pos) os[(size_t)pos * C.N + n] = raw[pos];
-      ot[n] = (int32_t)total;
       key = pack_key(total, F.seed, h->queue_idx, C.goff + n);
     }
   }
@@ -1177,137 +1272,202 @@ __global__ __launch_bounds__(64) void k_batch_merge(DevCluster C, const uint64_t
   for (; t < n_tiles; ++t) v = wave_merge_top(v, L[(size_t)t * 64 + 63 - lane]);
   CandRow c;
   c.key = v;
+#pragma unroll
   for (int k = 0; k < 4; ++k) c.alloc[k] = c.req[k] = 0;
   c.nzc = c.nzm = 0;
   c.podcnt = c.allowed = 0;
   if (v) {
     uint32_t n = (uint32_t)(v & 0xFFFFFull) - C.goff;
-    for (uint32_t k = 0; k < C.R && k < 4; ++k) {
-      c.alloc[k] = C.alloc[(size_t)k * C.N + n];
-      c.req[k] = C.req[(size_t)k * C.N + n];
-    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+      if (k < C.R) {
+        c.alloc[k] = C.alloc[(size_t)k * C.N + n];
+        c.req[k] = C.req[(size_t)k * C.N + n];
+      }
     c.nzc = C.nzc[n];
     c.nzm = C.nzm[n];
     c.podcnt = C.podcnt[n];
     c.allowed = C.allowed[n];
   }
-  cand[(size_t)b * KSG_TOPK + lane] = c;
+  if (lane < KSG_CAND) cand[(size_t)b * KSG_CAND + lane] = c;
 }
 
-// one wave: replay the batch in queue order
-__global__ __launch_bounds__(64) void k_batch_fixup(DevCluster C, DevProfile F, BatchOut BO, const uint8_t* progs,
-                                                    const uint64_t* prog_off, uint32_t j0, uint32_t nb,
-                                                    const CandRow* cand, int32_t* feas, ksg_pod_summary* sums) {
-  __shared__ int32_t hset[512];  // open-addressing set of modified global node ids
-  int lane = threadIdx.x;
-  for (int i = lane; i < 512; i += 64) hset[i] = -1;
-  __syncthreads();
-  uint32_t R = C.R < 4 ? C.R : 4;
-  // modified-node state: lane j holds entry j
-  int32_t m_id = -1;
-  RowV cur, snap;
-  for (int k = 0; k < 4; ++k) cur.alloc[k] = cur.req[k] = snap.alloc[k] = snap.req[k] = 0;
-  cur.nzc = cur.nzm = snap.nzc = snap.nzm = 0;
-  cur.podcnt = cur.allowed = snap.podcnt = snap.allowed = 0;
-  int nm = 0;
-  CandRow nxt = cand[lane];
-  for (uint32_t b = 0; b < nb; ++b) {
-    CandRow cr = nxt;
-    if (b + 1 < nb) nxt = cand[(size_t)(b + 1) * KSG_TOPK + lane];
-    const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[j0 + b]);
-    // 1. candidates not modified in this batch
-    uint32_t cnode = (uint32_t)(cr.key & 0xFFFFFull);
-    bool valid = cr.key != 0;
-    if (valid) {
-      uint32_t slot = (cnode * 2654435761u) >> 23;
-      for (;;) {
-        int32_t x = hset[slot];
-        if (x < 0) break;
-        if (x == (int32_t)cnode) { valid = false; break; }
-        slot = (slot + 1) & 511;
+// Replay the batch in queue order.  All 256 threads stage the batch's
+// candidates / pod records / snapshot feasible counts in LDS; wave 0 then runs
+// the sequential loop out of LDS and registers only (no global memory op in the
+// loop: on CDNA vmcnt also counts stores, so a store in the loop would stall the
+// next load), buffering patches and summaries in LDS; all threads flush them.
+struct Patch {
+  int32_t node;  // local node index, -1 none
+  uint32_t code;
+  int32_t fit, ba, total;
+};
+struct FixupLDS {
+  CandRow cand[KSG_BATCH * KSG_CAND];   // 96 KiB
+  PodLite pod[KSG_BATCH];
+  Patch patch[KSG_BATCH * KSG_CAND];
+  ksg_pod_summary sum[KSG_BATCH];
+  int32_t feas[KSG_BATCH];
+  int32_t npatch[KSG_BATCH];
+  int32_t hset[512];
+};
+
+__global__ __launch_bounds__(256) void k_batch_fixup(DevCluster C, DevProfile F, BatchOut BO, const uint8_t* progs,
+                                                     const uint64_t* prog_off, uint32_t j0, uint32_t nb,
+                                                     const CandRow* cand, int32_t* feas, ksg_pod_summary* sums) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  FixupLDS& L = *reinterpret_cast<FixupLDS*>(lds_raw);
+  int tid = threadIdx.x;
+  {  // stage: candidates (16 B per thread per step), pods, counts
+    const uint4* src = reinterpret_cast<const uint4*>(cand);
+    uint4* dst = reinterpret_cast<uint4*>(L.cand);
+    uint32_t n16 = nb * KSG_CAND * (uint32_t)(sizeof(CandRow) / 16);
+    for (uint32_t i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
+    for (uint32_t b = tid; b < nb; b += blockDim.x) {
+      const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[j0 + b]);
+      PodLite& p = L.pod[b];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) p.req[k] = h->req[k];
+#pragma unroll
+      for (int k = 0; k < KSG_MAX_SCORE_RES; ++k) {
+        p.fit_score_req[k] = h->fit_score_req[k];
+        p.ba_req[k] = h->ba_req[k];
       }
-    }
-    uint64_t best = valid ? cr.key : 0;
-    // 2. modified nodes: exact evaluation on the current row
-    int dfeas = 0;
-    if (lane < nm) {
-      int32_t raw[KSG_MAX_PLUGINS];
-      int64_t tot, tot0;
-      int32_t raw0[KSG_MAX_PLUGINS];
-      uint32_t code = eval_row(cur, F, h, R, raw, tot);
-      uint32_t code0 = eval_row(snap, F, h, R, raw0, tot0);
-      dfeas = (code == KSG_FILTER_PASS ? 1 : 0) - (code0 == KSG_FILTER_PASS ? 1 : 0);
-      uint32_t n = (uint32_t)m_id - C.goff;
-      if ((uint32_t)m_id >= C.goff && n < C.N) {  // patch this pod's per-pair outputs
-        uint32_t* of;
-        int32_t *os, *ot;
-        out_ptrs(BO, b, C.N, of, os, ot);
-        of[n] = code;
-        if (code == KSG_FILTER_PASS) {
-          for (int pos = 0; pos < F.n; ++pos) os[(size_t)pos * C.N + n] = raw[pos];
-          ot[n] = (int32_t)tot;
-        }
-      }
-      if (code == KSG_FILTER_PASS) {
-        uint64_t k = pack_key(tot, F.seed, h->queue_idx, (uint32_t)m_id);
-        best = k > best ? k : best;
-      }
-    }
-    best = wave_max(best);
-    int feasible = feas[b] + (int)wave_sum(dfeas);
-    int32_t sel = (feasible > 0 && best) ? (int32_t)(best & 0xFFFFFull) : -1;
-    if (sel >= 0) {
-      unsigned long long inm = __ballot(lane < nm && m_id == sel);
-      int holder;
-      if (!inm) {  // new modified node: row from the candidate that carries it
-        unsigned long long cl = __ballot(valid && cnode == (uint32_t)sel);
-        int src = __ffsll((long long)cl) - 1;
-        RowV nr;
-        for (int k = 0; k < 4; ++k) {
-          nr.alloc[k] = __shfl(cr.alloc[k], src, 64);
-          nr.req[k] = __shfl(cr.req[k], src, 64);
-        }
-        nr.nzc = __shfl(cr.nzc, src, 64);
-        nr.nzm = __shfl(cr.nzm, src, 64);
-        nr.podcnt = __shfl(cr.podcnt, src, 64);
-        nr.allowed = __shfl(cr.allowed, src, 64);
-        if (lane == nm) {
-          m_id = sel;
-          cur = nr;
-          snap = nr;
-        }
-        if (lane == 0) {
-          uint32_t slot = ((uint32_t)sel * 2654435761u) >> 23;
-          while (hset[slot] >= 0) slot = (slot + 1) & 511;
-          hset[slot] = sel;
-        }
-        holder = nm;
-        nm++;
-        __syncthreads();
-      } else {
-        holder = __ffsll((long long)inm) - 1;
-      }
-      if (lane == holder) {  // assume: NodeInfo.AddPod
-        for (uint32_t k = 0; k < R; ++k) cur.req[k] += h->req[k];
-        cur.nzc += h->nz_cpu;
-        cur.nzm += h->nz_mem;
-        cur.podcnt += 1;
-      }
-    }
-    if (lane == 0) {
-      ksg_pod_summary& s = sums[j0 + b];
-      s.best_key = sel >= 0 ? (feasible == 1 ? (best & 0xFFFFFFFFFFull) : best) : 0;
-      s.selected = sel;
-      s.feasible = feasible;
-      s.status = sel >= 0 ? 0 : 1;
+      p.nz_cpu = h->nz_cpu;
+      p.nz_mem = h->nz_mem;
+      p.queue_idx = h->queue_idx;
+      p.flags = h->flags;
+      L.feas[b] = feas[b];
       feas[b] = 0;  // ready for the next batch
     }
+    for (int i = tid; i < 512; i += blockDim.x) L.hset[i] = -1;
   }
-  // write back the modified rows (this shard's nodes)
-  if (lane < nm) {
+  __syncthreads();
+  uint32_t R = C.R < 4 ? C.R : 4;
+  int lane = tid & 63;
+  int32_t m_id = -1;
+  RowV cur, snap;
+  int nm = 0;
+  if (tid < 64) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cur.alloc[k] = cur.req[k] = snap.alloc[k] = snap.req[k] = 0;
+    cur.nzc = cur.nzm = snap.nzc = snap.nzm = 0;
+    cur.podcnt = cur.allowed = snap.podcnt = snap.allowed = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+      const PodLite* h = &L.pod[b];
+      // 1. candidates not modified in this batch (lanes < KSG_CAND)
+      uint64_t ckey = 0;
+      uint32_t cnode = 0;
+      if (lane < KSG_CAND) {
+        ckey = L.cand[b * KSG_CAND + lane].key;
+        cnode = (uint32_t)(ckey & 0xFFFFFull);
+      }
+      bool valid = ckey != 0;
+      if (valid) {
+        uint32_t slot = (cnode * 2654435761u) >> 23;
+        for (;;) {
+          int32_t x = L.hset[slot];
+          if (x < 0) break;
+          if (x == (int32_t)cnode) { valid = false; break; }
+          slot = (slot + 1) & 511;
+        }
+      }
+      uint64_t best = valid ? ckey : 0;
+      // 2. modified nodes: exact evaluation on the current row
+      int dfeas = 0;
+      if (lane < nm) {
+        int32_t fit_s, ba_s;
+        int64_t tot;
+        uint32_t code = eval_row(cur, F, h, R, fit_s, ba_s, tot);
+        bool snap_ok = F.pos_fit < 0 || fit_filter_row(snap, h, R) == 0;
+        dfeas = (code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0);
+        uint32_t n = (uint32_t)m_id - C.goff;
+        Patch& pt = L.patch[b * KSG_CAND + lane];
+        pt.node = ((uint32_t)m_id >= C.goff && n < C.N) ? (int32_t)n : -1;
+        pt.code = code;
+        pt.fit = fit_s;
+        pt.ba = ba_s;
+        pt.total = (int32_t)tot;
+        if (code == KSG_FILTER_PASS) {
+          uint64_t k = pack_key(tot, F.seed, h->queue_idx, (uint32_t)m_id);
+          best = k > best ? k : best;
+        }
+      }
+      best = wave_max(best);
+      int feasible = L.feas[b] + (int)wave_sum(dfeas);
+      int32_t sel = (feasible > 0 && best) ? (int32_t)(best & 0xFFFFFull) : -1;
+      if (lane == 0) L.npatch[b] = nm;
+      if (sel >= 0) {
+        unsigned long long inm = __ballot(lane < nm && m_id == sel);
+        int holder;
+        if (!inm) {  // new modified node: snapshot row from the candidate carrying it
+          unsigned long long cl = __ballot(valid && cnode == (uint32_t)sel);
+          int src = __ffsll((long long)cl) - 1;
+          if (lane == nm) {
+            const CandRow& cr = L.cand[b * KSG_CAND + src];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              cur.alloc[k] = cr.alloc[k];
+              cur.req[k] = cr.req[k];
+            }
+            cur.nzc = cr.nzc;
+            cur.nzm = cr.nzm;
+            cur.podcnt = cr.podcnt;
+            cur.allowed = cr.allowed;
+            snap = cur;
+            m_id = sel;
+            uint32_t slot = ((uint32_t)sel * 2654435761u) >> 23;
+            while (L.hset[slot] >= 0) slot = (slot + 1) & 511;
+            L.hset[slot] = sel;
+          }
+          holder = nm;
+          nm++;
+        } else {
+          holder = __ffsll((long long)inm) - 1;
+        }
+        if (lane == holder) {  // assume: NodeInfo.AddPod
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k)
+            if (k < R) cur.req[k] += h->req[k];
+          cur.nzc += h->nz_cpu;
+          cur.nzm += h->nz_mem;
+          cur.podcnt += 1;
+        }
+      }
+      if (lane == 0) {
+        ksg_pod_summary& sm = L.sum[b];
+        sm.best_key = sel >= 0 ? (feasible == 1 ? (best & 0xFFFFFFFFFFull) : best) : 0;
+        sm.selected = sel;
+        sm.feasible = feasible;
+        sm.status = sel >= 0 ? 0 : 1;
+      }
+    }
+  }
+  __syncthreads();
+  // flush: summaries, patches, modified rows
+  for (uint32_t b = tid; b < nb; b += blockDim.x) {
+    ksg_pod_summary& d = sums[j0 + b];
+    d.best_key = L.sum[b].best_key;
+    d.selected = L.sum[b].selected;
+    d.feasible = L.sum[b].feasible;
+    d.status = L.sum[b].status;
+  }
+  for (uint32_t i = tid; i < nb * KSG_CAND; i += blockDim.x) {
+    uint32_t b = i / KSG_CAND, j = i % KSG_CAND;
+    if ((int)j >= L.npatch[b]) continue;
+    const Patch& pt = L.patch[i];
+    if (pt.node < 0) continue;
+    uint32_t* of;
+    int32_t *os, *ot;
+    out_ptrs(BO, b, C.N, of, os, ot);
+    write_pair(F, of, os, ot, C.N, (uint32_t)pt.node, pt.code, pt.fit, pt.ba, pt.total);
+  }
+  if (tid < 64 && lane < nm) {
     uint32_t n = (uint32_t)m_id - C.goff;
     if ((uint32_t)m_id >= C.goff && n < C.N) {
-      for (uint32_t k = 0; k < R; ++k) C.req[(size_t)k * C.N + n] = cur.req[k];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k)
+        if (k < R) C.req[(size_t)k * C.N + n] = cur.req[k];
       C.nzc[n] = cur.nzc;
       C.nzm[n] = cur.nzm;
       C.podcnt[n] = cur.podcnt;
@@ -1359,6 +1519,8 @@ struct Engine::Impl {
   DBuf<uint32_t> toff, kvo;
   DBuf<uint8_t> haslab, vok;
   NodeSoA topo;  // topology tables (host copy)
+  DBuf<int32_t> topo_key_d;
+  DBuf<uint32_t> topo_base_d, topo_count_d;
   // pod table
   DBuf<int32_t> ptnode, ptns, ptlab, tpod, tval;
   DBuf<uint32_t> ptflags, tcounts;
@@ -1413,11 +1575,9 @@ struct Engine::Impl {
     C.haslab = haslab.p; C.kvo = kvo.p; C.vnum = vnum.p; C.vok = vok.p;
     C.n_topo = (uint32_t)topo.topo_key.size();
     C.pairs = topo.topo_pairs;
-    for (uint32_t i = 0; i < C.n_topo && i < KSG_MAX_TOPO; ++i) {
-      C.topo_key[i] = topo.topo_key[i];
-      C.topo_base[i] = topo.topo_base[i];
-      C.topo_count[i] = topo.topo_count[i];
-    }
+    C.tkey = topo_key_d.p;
+    C.tbase = topo_base_d.p;
+    C.tcount = topo_count_d.p;
     C.pcap = pcap; C.pkeys = pkeys; C.tcap = tcap; C.rcap = rcap; C.vcap = vcap;
     C.ptnode = ptnode.p; C.ptns = ptns.p; C.ptflags = ptflags.p; C.ptlab = ptlab.p;
     C.terms = terms.p; C.tpod = tpod.p; C.treq = treq.p; C.tval = tval.p; C.tcounts = tcounts.p;
@@ -1479,6 +1639,12 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   F.ipa_hard_weight = cfg.ipa_hard_weight;
   F.ipa_ignore_existing_pref = cfg.ipa_ignore_existing_pref;
   F.seed = cfg.seed;
+  F.pos_fit = F.pos_ba = -1;
+  F.w_fit = F.w_ba = 0;
+  for (int i = 0; i < F.n; ++i) {
+    if (F.plugins[i] == KP_FIT) { F.pos_fit = i; F.w_fit = F.weight[i]; }
+    if (F.plugins[i] == KP_BA) { F.pos_ba = i; F.w_ba = F.weight[i]; }
+  }
   I.batch_ok = F.n > 0;
   for (int i = 0; i < F.n; ++i) I.batch_ok &= (F.plugins[i] == KP_FIT || F.plugins[i] == KP_BA);
   return true;
@@ -1506,6 +1672,9 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   I.topo.topo_base = ns.topo_base;
   I.topo.topo_count = ns.topo_count;
   I.topo.topo_pairs = ns.topo_pairs;
+  if (!I.topo_key_d.upload(ns.topo_key, s, err) || !I.topo_base_d.upload(ns.topo_base, s, err) ||
+      !I.topo_count_d.upload(ns.topo_count, s, err))
+    return false;
   // existing-pod table (capacity for device-side appends)
   I.pcap = std::max<uint32_t>(pod_cap, pt.n);
   I.pkeys = pt.n_keys;
@@ -1559,7 +1728,7 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     uint32_t T = (I.N + kBlock - 1) / kBlock;
     size_t Nn = std::max<uint32_t>(I.N, 1);
     if (!I.tile_top.alloc((size_t)KSG_BATCH * std::max<uint32_t>(T, 1) * KSG_TOPK, err) ||
-        !I.bfeas.alloc(KSG_BATCH, err) || !I.cand.alloc((size_t)KSG_BATCH * KSG_TOPK, err) ||
+        !I.bfeas.alloc(KSG_BATCH, err) || !I.cand.alloc((size_t)KSG_BATCH * KSG_CAND, err) ||
         !I.bfilter.alloc(Nn * KSG_BATCH, err) || !I.bscore.alloc(Nn * KSG_BATCH * KSG_MAX_PLUGINS, err) ||
         !I.btotal.alloc(Nn * KSG_BATCH, err))
       return false;
@@ -1585,6 +1754,12 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     }
   }
   I.n_samples = 0;
+  static bool attr = false;
+  if (!attr) {
+    HIPCHK(hipFuncSetAttribute((const void*)k_batch_fixup, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)sizeof(FixupLDS)));
+    attr = true;
+  }
   HIPCHK(hipEventRecord(I.ev0, s));
   uint32_t end = first + count, j0 = first;
   while (j0 < end) {
@@ -1609,8 +1784,8 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
       I.n_samples++;
     }
     hipLaunchKernelGGL(k_batch_merge, dim3(nb), dim3(64), 0, s, C, I.tile_top.p, T, I.cand.p);
-    hipLaunchKernelGGL(k_batch_fixup, dim3(1), dim3(64), 0, s, C, I.F, BO, I.progs.p, I.prog_off_d.p, j0, nb,
-                       I.cand.p, I.bfeas.p, I.sums.p);
+    hipLaunchKernelGGL(k_batch_fixup, dim3(1), dim3(256), sizeof(FixupLDS), s, C, I.F, BO, I.progs.p, I.prog_off_d.p,
+                       j0, nb, I.cand.p, I.bfeas.p, I.sums.p);
     j0 = j1;
   }
   HIPCHK(hipEventRecord(I.ev1, s));

@@ -1,0 +1,87 @@
+"""Regenerate the golden fixtures under tests/golden/ from the CPU oracle.
+
+Fixtures are data: a small cluster (inputs) and the expected per-pod results
+(selected node, feasible count, status, and the result-store annotations the
+reference's debuggable scheduler would write).  Run:
+
+    python tests/golden/make_golden.py
+
+Cases pinned to the reference's own known answers are listed in KNOWN (README.md:63-80,
+simulator/docs/debuggable-scheduler.md:13-31, resultstore/store_test.go:284-833);
+the config families are pinned to the restatement itself ("parity unpinned"
+against the Go code).
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
+sys.path.insert(0, os.path.dirname(HERE))
+
+from ksg import generator as g  # noqa: E402
+from _oracle import Oracle  # noqa: E402
+
+
+def readme_example():
+    """README.md:63-80: pod {100m, 16Gi} on two empty {4, 32Gi} nodes (web templates node.yaml/pod.yaml)."""
+    prof = g.make_profile(g.DEFAULT_HOT_PROFILE, 1)
+    return {"profile": prof,
+            "nodes": [g.node_obj("node-282x7", 4000, 32 * g.Gi), g.node_obj("node-gp9t4", 4000, 32 * g.Gi)],
+            "pods": [], "queue": [g.pod_obj("hoge-pod", [g.req(100, 16 * g.Gi)])]}
+
+
+def store_weight_example():
+    """resultstore/store_test.go:284-446: finalscore = score x weight (score 10, weight 2 -> "20");
+    plugins.go:289-304: a weight of 0 in the store map becomes 1."""
+    prof = g.make_profile([("NodeResourcesFit", 2), ("NodeResourcesBalancedAllocation", 1)], 1)
+    prof["storeWeights"]["NodeResourcesBalancedAllocation"] = 0
+    nodes = [g.node_obj(f"node-{i}", 10000, 10 * g.Gi) for i in range(2)]
+    return {"profile": prof, "nodes": nodes, "pods": [],
+            "queue": [g.pod_obj("pod1", [g.req(9000, 9 * g.Gi)])]}
+
+
+def empty_maps_example():
+    """resultstore/store_test.go:584-833: maps with no entries render as "{}" — a single
+    feasible node is selected without PreScore/Score (schedule_one.go), so the score maps are empty."""
+    prof = g.make_profile(g.DEFAULT_HOT_PROFILE, 1)
+    nodes = [g.node_obj("node-a", 1000, 1 * g.Gi), g.node_obj("node-b", 8000, 8 * g.Gi)]
+    return {"profile": prof, "nodes": nodes, "pods": [],
+            "queue": [g.pod_obj("big", [g.req(4000, 2 * g.Gi)])]}
+
+
+KNOWN = {"readme_example": readme_example, "store_weight_example": store_weight_example,
+         "empty_maps_example": empty_maps_example}
+FAMILIES = {
+    "cfg1_small": (1, dict(n_nodes=12, n_pods=24)),
+    "cfg2_small": (2, dict(n_nodes=30, n_pods=30)),
+    "cfg3_small": (3, dict(n_nodes=40, n_pods=25)),
+    "cfg4_small": (4, dict(n_nodes=40, n_existing=120, n_pods=25, n_zones=4)),
+}
+
+
+def expected(doc):
+    o = Oracle(doc)
+    o.schedule(record=3)
+    pods = []
+    for q in range(o.n_queue):
+        sel, feas, st = o.result(q)
+        pods.append({"selected": sel, "feasible": feas, "status": st, "annotations": o.annotations(q)})
+    return pods
+
+
+def main():
+    for name, fn in KNOWN.items():
+        doc = fn()
+        with open(os.path.join(HERE, name + ".json"), "w") as f:
+            json.dump({"cluster": doc, "expected": expected(doc)}, f, indent=1, sort_keys=True)
+    for name, (c, kw) in FAMILIES.items():
+        doc = g.generate(c, **kw)
+        with open(os.path.join(HERE, name + ".json"), "w") as f:
+            json.dump({"config": c, "sizes": kw, "cluster": doc, "expected": expected(doc)}, f, sort_keys=True)
+    print("wrote", len(KNOWN) + len(FAMILIES), "fixtures")
+
+
+if __name__ == "__main__":
+    main()

@@ -128,3 +128,24 @@ def test_cfg2_large_batch_path_selected_nodes():
     s.schedule()
     got = [(r.selected, r.feasible, r.status) for r in s.results()]
     assert got == [o.result(q) for q in range(len(got))]
+
+
+import glob as _glob
+import json as _json
+import os as _os
+
+_GOLD = sorted(_glob.glob(_os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "golden", "*.json")))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", _GOLD, ids=lambda p: _os.path.basename(p)[:-5])
+def test_engine_matches_golden_fixture(path):
+    d = _json.load(open(path))
+    doc = d["cluster"]
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    s.keep_outputs(0, s.queue_len)
+    s.schedule()
+    for q, (r, e) in enumerate(zip(s.results(), d["expected"])):
+        assert (r.selected, r.feasible, r.status) == (e["selected"], e["feasible"], e["status"]), q
+        assert s.annotations(q) == e["annotations"], q

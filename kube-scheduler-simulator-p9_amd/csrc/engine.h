@@ -98,6 +98,9 @@ class Engine {
   // 1: force the per-pod kernel chain even when the speculative batch path applies
   void set_path(int per_pod);
   bool batch_path() const;
+  // diagnostic: enable (out == nullptr, count pods) / read back s_memtime stamps of the fixup loop
+  bool fixup_stamps(uint32_t count, std::vector<uint64_t>* out, std::string& err);
+  bool eval_stamps(bool on, std::vector<uint64_t>* out, std::string& err);
   // Average duration (ms) and count of the sampled launches of the last run.
   bool kernel_time(float& avg_ms, uint32_t& samples, std::string& err);
   // Read back the node resource rows (parity tests of the assume delta).

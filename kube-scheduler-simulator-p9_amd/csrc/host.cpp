@@ -1466,6 +1466,24 @@ int ksg_set_path(ksg_ctx* ctx, int per_pod) {
   return KSG_OK;
 }
 
+// diagnostic (not in ksg.h): fixup-loop s_memtime stamps, 8 per pod
+extern "C" int ksg_debug_fixup_stamps(ksg_ctx* ctx, uint32_t count, uint64_t* out) {
+  if (!ctx) return KSG_E_INVALID;
+  std::vector<uint64_t> v;
+  if (!ctx->c.eng->fixup_stamps(count, out ? &v : nullptr, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
+  if (out) std::copy(v.begin(), v.end(), out);
+  return KSG_OK;
+}
+
+extern "C" int ksg_debug_eval_stamps(ksg_ctx* ctx, int on, uint64_t* out, size_t* n) {
+  if (!ctx) return KSG_E_INVALID;
+  std::vector<uint64_t> v;
+  if (!ctx->c.eng->eval_stamps(on != 0, out ? &v : nullptr, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
+  if (out) std::copy(v.begin(), v.end(), out);
+  if (n) *n = v.size();
+  return KSG_OK;
+}
+
 int ksg_batch_path(const ksg_ctx* ctx) { return ctx ? (ctx->c.eng->batch_path() ? 1 : 0) : KSG_E_INVALID; }
 
 int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples) {

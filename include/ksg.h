@@ -114,6 +114,18 @@ int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples);
 int ksg_set_path(ksg_ctx* ctx, int per_pod);
 int ksg_batch_path(const ksg_ctx* ctx);  /* 1 when the batch path is active */
 
+/* Node sharding across GPUs (ksg_opts.shard_rank / shard_count): per batch of
+ * 32 pods every rank all-gathers its per-pod top-32 candidates (with their node
+ * rows) and local feasible counts, merges them, and runs the same deterministic
+ * replay, applying only its own nodes' assume deltas.
+ *   mode 1: RCCL all-gather on the context stream; nccl_id = 128 bytes from
+ *           ksg_nccl_unique_id() on one rank, broadcast by the caller.
+ *   mode 2: host callback fn(user, send, recv, bytes_per_rank) that all-gathers
+ *           host buffers (recv = ranks x bytes, rank order); returns 0.        */
+typedef int (*ksg_exchange_fn)(void* user, const void* send, void* recv, size_t bytes_per_rank);
+int ksg_nccl_unique_id(uint8_t* out128);
+int ksg_set_exchange(ksg_ctx* ctx, int mode, const uint8_t* nccl_id, ksg_exchange_fn fn, void* user);
+
 /* Keep per-(pod, node) outputs for queue pods [first, first+count) (tests,
  * annotation rendering).  Must precede ksg_schedule_queue. */
 int ksg_keep_outputs(ksg_ctx* ctx, uint32_t first, uint32_t count);

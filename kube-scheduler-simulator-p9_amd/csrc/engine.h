@@ -98,6 +98,14 @@ class Engine {
   // 1: force the per-pod kernel chain even when the speculative batch path applies
   void set_path(int per_pod);
   bool batch_path() const;
+  // Node-shard exchange for the batch path: mode 1 = RCCL all-gather on the engine
+  // stream (nccl_id from nccl_unique_id on one rank), mode 2 = host callback
+  // fn(user, send, recv, bytes_per_rank) returning 0 (tests: gloo).
+  typedef int (*ExchangeFn)(void* user, const void* send, void* recv, size_t bytes_per_rank);
+  bool set_exchange(int mode, const void* nccl_id, uint32_t rank, uint32_t ranks, ExchangeFn fn, void* user,
+                    std::string& err);
+  uint32_t exchange_ranks() const;
+  static bool nccl_unique_id(void* out128, std::string& err);
   // diagnostic: enable (out == nullptr, count pods) / read back s_memtime stamps of the fixup loop
   bool fixup_stamps(uint32_t count, std::vector<uint64_t>* out, std::string& err);
   bool eval_stamps(bool on, std::vector<uint64_t>* out, std::string& err);

@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "engine.h"
+#include <rccl/rccl.h>
 
 namespace ksg {
 
@@ -1249,7 +1250,7 @@ __global__ __launch_bounds__(kBlock) void k_batch_eval(DevCluster C, DevProfile 
 
 // one wave per pod: merge the tile lists into the pod's top-64 and gather rows
 __global__ __launch_bounds__(64) void k_batch_merge(DevCluster C, const uint64_t* tile_top, uint32_t n_tiles,
-                                                    CandRow* cand) {
+                                                    CandRow* cand, int32_t* feas, int32_t* feas_out) {
   uint32_t b = blockIdx.x;
   int lane = threadIdx.x;
   const uint64_t* L = tile_top + (size_t)b * n_tiles * KSG_TOPK;
@@ -1284,7 +1285,58 @@ __global__ __launch_bounds__(64) void k_batch_merge(DevCluster C, const uint64_t
     c.allowed = C.allowed[n];
   }
   if (lane < KSG_CAND) cand[(size_t)b * KSG_CAND + lane] = c;
+  if (feas_out && lane == 0) {  // sharded: ship the local feasible count, reset the accumulator
+    feas_out[b] = feas[b];
+    feas[b] = 0;
+  }
 }
+
+// Sharded batches: every rank's exchange record = [feasible counts (KSG_BATCH
+// ints, 128 B)] [top-KSG_CAND CandRow per pod].  One wave per pod merges the R
+// sorted lists into the global top-KSG_CAND and sums the feasible counts.
+#define KSG_XHDR 128
+__global__ __launch_bounds__(64) void k_batch_gmerge(const uint8_t* recv, size_t rec_bytes, uint32_t ranks,
+                                                     CandRow* cand, int32_t* gfeas) {
+  __shared__ uint64_t keys[8 * KSG_CAND];
+  uint32_t b = blockIdx.x;
+  int lane = threadIdx.x;
+  for (uint32_t i = lane; i < ranks * KSG_CAND; i += 64) {
+    uint32_t r = i / KSG_CAND, j = i % KSG_CAND;
+    const CandRow* L = reinterpret_cast<const CandRow*>(recv + r * rec_bytes + KSG_XHDR);
+    keys[i] = L[(size_t)b * KSG_CAND + j].key;
+  }
+  __syncthreads();
+  uint64_t v = lane < KSG_CAND ? keys[lane] : 0;
+  for (uint32_t r = 1; r < ranks; ++r) {
+    int j = 63 - lane;
+    uint64_t o = j < KSG_CAND ? keys[r * KSG_CAND + j] : 0;
+    v = wave_merge_top(v, o);
+  }
+  int32_t f = 0;
+  for (uint32_t r = 0; r < ranks; ++r) f += reinterpret_cast<const int32_t*>(recv + r * rec_bytes)[b];
+  if (lane < KSG_CAND) {
+    CandRow c;
+    memset(&c, 0, sizeof(c));
+    if (v) {  // find the source entry: each rank's list is sorted descending
+      for (uint32_t r = 0; r < ranks; ++r) {
+        int lo = 0, hi = KSG_CAND - 1, at = -1;
+        while (lo <= hi) {
+          int mid = (lo + hi) >> 1;
+          uint64_t k = keys[r * KSG_CAND + mid];
+          if (k == v) { at = mid; break; }
+          if (k > v) lo = mid + 1; else hi = mid - 1;
+        }
+        if (at >= 0) {
+          c = reinterpret_cast<const CandRow*>(recv + r * rec_bytes + KSG_XHDR)[(size_t)b * KSG_CAND + at];
+          break;
+        }
+      }
+    }
+    cand[(size_t)b * KSG_CAND + lane] = c;
+  }
+  if (lane == 0) gfeas[b] = f;
+}
+
 
 // Replay the batch in queue order.  All 256 threads stage the batch's
 // candidates / pod records / snapshot feasible counts in LDS; wave 0 then runs
@@ -1530,6 +1582,15 @@ struct DBuf {
 
 struct Engine::Impl {
   EngineConfig cfg;
+  // node-shard exchange (sharded batch path)
+  int xmode = 0;  // 0 none, 1 RCCL all-gather on the engine stream, 2 host callback
+  uint32_t xrank = 0, xranks = 1;
+  ncclComm_t comm = nullptr;
+  Engine::ExchangeFn xfn = nullptr;
+  void* xuser = nullptr;
+  DBuf<uint8_t> xsend, xrecv;
+  std::vector<uint8_t> hsend, hrecv;
+  DBuf<int32_t> gfeas;
   DevProfile F{};
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -1622,6 +1683,7 @@ struct Engine::Impl {
 
 Engine::Engine() : p_(new Impl()) {}
 Engine::~Engine() {
+  if (p_->comm) (void)ncclCommDestroy(p_->comm);
   if (p_->ev0) (void)hipEventDestroy(p_->ev0);
   if (p_->ev1) (void)hipEventDestroy(p_->ev1);
   if (p_->own_stream && p_->stream) (void)hipStreamDestroy(p_->stream);
@@ -1831,14 +1893,34 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
       HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
       I.n_samples++;
     }
-    hipLaunchKernelGGL(k_batch_merge, dim3(nb), dim3(64), 0, s, C, I.tile_top.p, T, I.cand.p);
+    int32_t* fx = I.bfeas.p;
+    if (I.xranks > 1) {
+      const size_t rec = KSG_XHDR + (size_t)KSG_BATCH * KSG_CAND * sizeof(CandRow);
+      hipLaunchKernelGGL(k_batch_merge, dim3(nb), dim3(64), 0, s, C, I.tile_top.p, T,
+                         reinterpret_cast<CandRow*>(I.xsend.p + KSG_XHDR), I.bfeas.p,
+                         reinterpret_cast<int32_t*>(I.xsend.p));
+      if (I.xmode == 1) {
+        ncclResult_t nr = ncclAllGather(I.xsend.p, I.xrecv.p, rec, ncclUint8, I.comm, s);
+        if (nr != ncclSuccess) { err = std::string("ncclAllGather: ") + ncclGetErrorString(nr); return false; }
+      } else {
+        HIPCHK(hipMemcpyAsync(I.hsend.data(), I.xsend.p, rec, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (I.xfn(I.xuser, I.hsend.data(), I.hrecv.data(), rec) != 0) { err = "exchange callback failed"; return false; }
+        HIPCHK(hipMemcpyAsync(I.xrecv.p, I.hrecv.data(), rec * I.xranks, hipMemcpyHostToDevice, s));
+      }
+      hipLaunchKernelGGL(k_batch_gmerge, dim3(nb), dim3(64), 0, s, I.xrecv.p, rec, I.xranks, I.cand.p, I.gfeas.p);
+      fx = I.gfeas.p;
+    } else {
+      hipLaunchKernelGGL(k_batch_merge, dim3(nb), dim3(64), 0, s, C, I.tile_top.p, T, I.cand.p, I.bfeas.p,
+                         (int32_t*)nullptr);
+    }
     uint64_t* fst = I.stamps_on ? I.stamps.p + (size_t)(j0 - first) * 8 : nullptr;
     if (I.eval_mode == 1)
       hipLaunchKernelGGL(k_batch_fixup<1>, dim3(1), dim3(KSG_FIXUP_THREADS), sizeof(FixupLDS), s, C, I.F, BO, I.progs.p,
-                         I.prog_off_d.p, j0, nb, I.cand.p, I.bfeas.p, I.sums.p, fst);
+                         I.prog_off_d.p, j0, nb, I.cand.p, fx, I.sums.p, fst);
     else
       hipLaunchKernelGGL(k_batch_fixup<0>, dim3(1), dim3(KSG_FIXUP_THREADS), sizeof(FixupLDS), s, C, I.F, BO, I.progs.p,
-                         I.prog_off_d.p, j0, nb, I.cand.p, I.bfeas.p, I.sums.p, fst);
+                         I.prog_off_d.p, j0, nb, I.cand.p, fx, I.sums.p, fst);
     j0 = j1;
   }
   HIPCHK(hipEventRecord(I.ev1, s));
@@ -2021,6 +2103,47 @@ bool Engine::reset(std::string& err) {
 }
 
 void Engine::sample_kernel(uint32_t every) { p_->sample_every = every; }
+
+bool Engine::set_exchange(int mode, const void* nccl_id, uint32_t rank, uint32_t ranks, ExchangeFn fn, void* user,
+                          std::string& err) {
+  Impl& I = *p_;
+  if (ranks < 1 || rank >= ranks || ranks > 8) { err = "exchange: 1 <= ranks <= 8, rank < ranks"; return false; }
+  if (I.comm) { (void)ncclCommDestroy(I.comm); I.comm = nullptr; }
+  I.xmode = mode;
+  I.xrank = rank;
+  I.xranks = ranks;
+  I.xfn = fn;
+  I.xuser = user;
+  if (ranks == 1) { I.xmode = 0; return true; }
+  const size_t rec = KSG_XHDR + (size_t)KSG_BATCH * KSG_CAND * sizeof(CandRow);
+  if (!I.xsend.alloc(rec, err) || !I.xrecv.alloc(rec * ranks, err) || !I.gfeas.alloc(KSG_BATCH, err)) return false;
+  HIPCHK(hipMemset(I.xsend.p, 0, rec));
+  if (mode == 1) {
+    ncclUniqueId id;
+    std::memcpy(&id, nccl_id, sizeof(id));
+    HIPCHK(hipSetDevice(I.cfg.device));
+    ncclResult_t nr = ncclCommInitRank(&I.comm, (int)ranks, id, (int)rank);
+    if (nr != ncclSuccess) { err = std::string("ncclCommInitRank: ") + ncclGetErrorString(nr); return false; }
+  } else if (mode == 2) {
+    if (!fn) { err = "exchange: host mode needs a callback"; return false; }
+    I.hsend.assign(rec, 0);
+    I.hrecv.assign(rec * ranks, 0);
+  } else {
+    err = "exchange: unknown mode";
+    return false;
+  }
+  return true;
+}
+
+uint32_t Engine::exchange_ranks() const { return p_->xranks; }
+
+bool Engine::nccl_unique_id(void* out128, std::string& err) {
+  ncclUniqueId id;
+  ncclResult_t nr = ncclGetUniqueId(&id);
+  if (nr != ncclSuccess) { err = std::string("ncclGetUniqueId: ") + ncclGetErrorString(nr); return false; }
+  std::memcpy(out128, &id, sizeof(id));
+  return true;
+}
 void Engine::set_path(int per_pod) { p_->force_per_pod = per_pod != 0; }
 bool Engine::eval_stamps(bool on, std::vector<uint64_t>* out, std::string& err) {
   Impl& I = *p_;

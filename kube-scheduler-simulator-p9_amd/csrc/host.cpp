@@ -1387,7 +1387,10 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   if (!ctx) return KSG_E_INVALID;
   Cluster& c = ctx->c;
   if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
-  if (c.shards != 1) return ctx->fail("queue mode on a sharded context needs ksg_whatif/exchange", KSG_E_STATE);
+  if (c.shards != 1) {
+    if (!c.eng->batch_path()) return ctx->fail("sharded contexts support Fit/BalancedAllocation profiles (batch path)", KSG_E_STATE);
+    if (c.eng->exchange_ranks() != c.shards) return ctx->fail("sharded context: call ksg_set_exchange first", KSG_E_STATE);
+  }
   if (!c.compile_queue()) return ctx->fail(c.err, KSG_E_INVALID);
   if (!c.eng->run_queue(first, count, true, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
   return KSG_OK;
@@ -1481,6 +1484,19 @@ extern "C" int ksg_debug_eval_stamps(ksg_ctx* ctx, int on, uint64_t* out, size_t
   if (!ctx->c.eng->eval_stamps(on != 0, out ? &v : nullptr, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
   if (out) std::copy(v.begin(), v.end(), out);
   if (n) *n = v.size();
+  return KSG_OK;
+}
+
+int ksg_nccl_unique_id(uint8_t* out128) {
+  std::string err;
+  if (!out128) return KSG_E_INVALID;
+  return ksg::Engine::nccl_unique_id(out128, err) ? KSG_OK : KSG_E_DEVICE;
+}
+
+int ksg_set_exchange(ksg_ctx* ctx, int mode, const uint8_t* nccl_id, ksg_exchange_fn fn, void* user) {
+  if (!ctx) return KSG_E_INVALID;
+  Cluster& c = ctx->c;
+  if (!c.eng->set_exchange(mode, nccl_id, c.rank, c.shards, fn, user, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
   return KSG_OK;
 }
 

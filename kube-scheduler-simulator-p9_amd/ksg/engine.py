@@ -62,6 +62,8 @@ def load_library():
     L.ksg_annotations.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.ksg_reset.argtypes = [vp]
     L.ksg_sample_kernel.argtypes = [vp, u32]
+    L.ksg_nccl_unique_id.argtypes = [ctypes.c_void_p]
+    L.ksg_set_exchange.argtypes = [vp, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     L.ksg_set_path.argtypes = [vp, ctypes.c_int]
     L.ksg_batch_path.argtypes = [vp]
     L.ksg_kernel_time.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32)]
@@ -157,6 +159,16 @@ class Scheduler:
 
     def sample_kernel(self, every):
         self._chk(self.L.ksg_sample_kernel(self.h, every), "ksg_sample_kernel")
+
+    def set_exchange_rccl(self, unique_id: bytes):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._chk(self.L.ksg_set_exchange(self.h, 1, buf, None, None), "ksg_set_exchange")
+
+    def set_exchange_host(self, world: int):
+        from .distributed import make_host_exchange
+        self._xfn = make_host_exchange(world)  # keep alive
+        self._chk(self.L.ksg_set_exchange(self.h, 2, None, ctypes.cast(self._xfn, ctypes.c_void_p), None),
+                  "ksg_set_exchange")
 
     def set_path(self, per_pod: bool):
         self._chk(self.L.ksg_set_path(self.h, 1 if per_pod else 0), "ksg_set_path")

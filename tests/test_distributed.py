@@ -1,0 +1,89 @@
+"""Multi-rank (node-shard) paths.
+
+CPU: world_size-2 gloo run of the host exchange used by sharded contexts.
+GPU: two sharded ranks on one MI355X (host exchange over gloo) schedule a
+cluster; every pod's selection must equal the single-rank oracle's.
+"""
+import ctypes
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _exchange_worker(rank, world, port, out):
+    sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
+    dist = _init(rank, world, port)
+    from ksg.distributed import make_host_exchange, shard_bounds
+    fn = make_host_exchange(world)
+    n = 4096 + 128
+    send = (ctypes.c_uint8 * n)(*([rank + 1] * n))
+    recv = (ctypes.c_uint8 * (n * world))()
+    rc = fn(None, ctypes.addressof(send), ctypes.addressof(recv), n)
+    ok = rc == 0 and all(recv[r * n] == r + 1 and recv[r * n + n - 1] == r + 1 for r in range(world))
+    lo, hi = shard_bounds(5003, rank, world)
+    out[rank] = int(ok) * 10 + int(hi - lo in (2501, 2502))
+    dist.destroy_process_group()
+
+
+def test_host_exchange_gloo_world2():
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_exchange_worker, args=(2, port, out), nprocs=2, join=True)
+        assert dict(out) == {0: 11, 1: 11}
+
+
+def _sharded_worker(rank, world, port, doc_json, out):
+    sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
+    dist = _init(rank, world, port)
+    import json
+    from ksg import Scheduler
+    doc = json.loads(doc_json)
+    s = Scheduler(doc["profile"], device=0, shard_rank=rank, shard_count=world)
+    s.set_exchange_host(world)
+    s.load_cluster(doc)
+    assert s.batch_path
+    s.schedule()
+    out[rank] = [(r.selected, r.feasible, r.status) for r in s.results()]
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_batch_path_matches_oracle(world):
+    import json
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _oracle import Oracle
+    from ksg import generator as g
+    doc = g.generate(2, n_nodes=600, n_pods=300)
+    o = Oracle(doc)
+    o.schedule(record=0)
+    want = [o.result(q) for q in range(o.n_queue)]
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_sharded_worker, args=(world, port, json.dumps(doc), out), nprocs=world, join=True)
+        for r in range(world):
+            assert out[r] == want, f"rank {r} differs"

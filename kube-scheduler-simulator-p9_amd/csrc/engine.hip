@@ -262,6 +262,21 @@ __device__ __forceinline__ int64_t wave_max(int64_t v) {  // order-preserving ma
 __device__ __forceinline__ int64_t wave_min(int64_t v) { return ~wave_max((int64_t)~v); }
 __device__ __forceinline__ int32_t wave_min(int32_t v) { return __ockl_wfred_min_i32(v); }
 __device__ __forceinline__ int32_t wave_sum(int32_t v) { return __ockl_wfred_add_i32(v); }
+__device__ __noinline__ int64_t div_i64_slow(int64_t x, int64_t a) { return x / a; }
+// floor(x / a) for 0 <= x, a > 0 — exact.  32-bit operands use the hardware
+// 32-bit divide; otherwise an estimate from one v_rcp_f64 (relative error
+// ~2^-50, so |estimate - quotient| < 1 for x < 2^52 with small quotients) is
+// corrected with exact 64-bit products.  Only BalancedAllocation's fractions
+// need an IEEE-rounded f64 division; integer quotients never do.
+__device__ __forceinline__ int64_t div_small(int64_t x, int64_t a) {
+  if ((uint64_t)x <= 0xFFFFFFFFull && (uint64_t)a <= 0xFFFFFFFFull) return (int64_t)((uint32_t)x / (uint32_t)a);
+  if (x >= ((int64_t)1 << 52)) return div_i64_slow(x, a);
+  int64_t q = (int64_t)((double)x * __builtin_amdgcn_rcp((double)a));
+  if (q < 0) q = 0;
+  if (q * a > x) q--;
+  else if ((q + 1) * a <= x) q++;
+  return q;
+}
 __device__ __forceinline__ bool lane0() { return (threadIdx.x & 63) == 0; }
 
 // Go math.Log restated (oracle/ksg_oracle.cpp go_log); no contraction.
@@ -340,16 +355,16 @@ __device__ int64_t fit_score(const DevCluster& C, const DevProfile& F, const Pro
       s = q > a ? rtc_fn(F, 100) : rtc_fn(F, q * 100 / a);
       if (s <= 0) continue;
     } else if (F.fit_strategy == 1) {
-      s = (q > a ? a : q) * 100 / a;
+      s = div_small((q > a ? a : q) * 100, a);
     } else {
-      s = q > a ? 0 : (a - q) * 100 / a;
+      s = q > a ? 0 : div_small((a - q) * 100, a);
     }
     ns += s * F.fit_w[i];
     ws += F.fit_w[i];
   }
   if (ws == 0) return 0;
   if (F.fit_strategy == 2) return (int64_t)round((double)ns / (double)ws);
-  return ns / ws;
+  return div_small(ns, ws);
 }
 
 __device__ int64_t ba_score(const DevCluster& C, const DevProfile& F, const ProgView& V, uint32_t n) {
@@ -1022,15 +1037,6 @@ __device__ __forceinline__ void alloc_req_row(const RowV& r, int res, int64_t po
   if (res == KSG_RES_CPU) q = (use_requested ? r.req[0] : r.nzc) + pod_req;
   else if (res == KSG_RES_MEM) q = (use_requested ? r.req[1] : r.nzm) + pod_req;
   else q = sel4(r.req, res) + pod_req;
-}
-__device__ __noinline__ int64_t div_i64_slow(int64_t x, int64_t a) { return x / a; }
-// floor(x / a), x >= 0, a > 0: exact via f64 + integer correction when x < 2^53
-__device__ __forceinline__ int64_t div_small(int64_t x, int64_t a) {
-  if (x >= ((int64_t)1 << 52)) return div_i64_slow(x, a);
-  int64_t q = (int64_t)((double)x / (double)a);
-  if (q * a > x) q--;
-  else if ((q + 1) * a <= x) q++;
-  return q;
 }
 __device__ __noinline__ int64_t rtc_fn_ool(const DevProfile& F, int64_t p) { return rtc_fn(F, p); }
 __device__ __forceinline__ int64_t least_req(int64_t a, int64_t q) {  // leastRequestedScore

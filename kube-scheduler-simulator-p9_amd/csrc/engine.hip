@@ -1238,17 +1238,27 @@ __global__ __launch_bounds__(kBlock) void k_batch_eval(DevCluster C, DevProfile 
     }
   }
   ESTAMP(3);
+  // Feasible count per (pod, tile) with a plain store: device atomics from every
+  // wave onto the 128-B line of per-pod counters serialise across XCDs.
+  __shared__ int32_t wcount[kBlock / 64];
   unsigned long long bal = __ballot(feasible);
-  if (lane0() && bal) atomicAdd(&feas[b], (int)__popcll(bal));
   key = wave_sort_desc(key);
   ESTAMP(4);
   int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   lists[w * 64 + lane] = key;
-  __syncthreads();
+  if (lane == 0) wcount[w] = (int32_t)__popcll(bal);
+  // LDS-only barrier: __syncthreads() would also wait (vmcnt(0)) for this
+  // wave's per-pair output stores, which nothing below depends on.
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (w == 0) {
     uint64_t v = lists[lane];
     for (int k = 1; k < kBlock / 64; ++k) v = wave_merge_top(v, lists[k * 64 + 63 - lane]);
     tile_top[((size_t)b * n_tiles + blockIdx.x) * KSG_TOPK + lane] = v;
+    if (lane == 0) {
+      int32_t c = 0;
+      for (int k = 0; k < kBlock / 64; ++k) c += wcount[k];
+      feas[(size_t)b * n_tiles + blockIdx.x] = c;
+    }
   }
   ESTAMP(5);
 #undef ESTAMP
@@ -1256,9 +1266,12 @@ __global__ __launch_bounds__(kBlock) void k_batch_eval(DevCluster C, DevProfile 
 
 // one wave per pod: merge the tile lists into the pod's top-64 and gather rows
 __global__ __launch_bounds__(64) void k_batch_merge(DevCluster C, const uint64_t* tile_top, uint32_t n_tiles,
-                                                    CandRow* cand, int32_t* feas, int32_t* feas_out) {
+                                                    CandRow* cand, const int32_t* tile_feas, int32_t* feas) {
   uint32_t b = blockIdx.x;
   int lane = threadIdx.x;
+  int32_t fc = 0;
+  for (uint32_t t = lane; t < n_tiles; t += 64) fc += tile_feas[(size_t)b * n_tiles + t];
+  fc = wave_sum(fc);
   const uint64_t* L = tile_top + (size_t)b * n_tiles * KSG_TOPK;
   uint64_t v = L[lane];
   uint32_t t = 1;
@@ -1291,10 +1304,7 @@ __global__ __launch_bounds__(64) void k_batch_merge(DevCluster C, const uint64_t
     c.allowed = C.allowed[n];
   }
   if (lane < KSG_CAND) cand[(size_t)b * KSG_CAND + lane] = c;
-  if (feas_out && lane == 0) {  // sharded: ship the local feasible count, reset the accumulator
-    feas_out[b] = feas[b];
-    feas[b] = 0;
-  }
+  if (lane == 0) feas[b] = fc;  // this shard's feasible count for pod b
 }
 
 // Sharded batches: every rank's exchange record = [feasible counts (KSG_BATCH
@@ -1344,41 +1354,106 @@ __global__ __launch_bounds__(64) void k_batch_gmerge(const uint8_t* recv, size_t
 }
 
 
-// Replay the batch in queue order.  All 256 threads stage the batch's
-// candidates / pod records / snapshot feasible counts in LDS; wave 0 then runs
-// the sequential loop out of LDS and registers only (no global memory op in the
-// loop: on CDNA vmcnt also counts stores, so a store in the loop would stall the
-// next load), buffering patches and summaries in LDS; all threads flush them.
+// Replay the batch in queue order, exactly, as a fixed-point iteration.
+//
+// Pod b's outcome is a function of the selections of pods < b only:
+// S_b = f_b(S_0..S_{b-1}) (its surviving candidates plus the nodes modified by
+// earlier pods, re-evaluated on their current rows).  A vector S with
+// S_b == f_b(S_<b) for every b IS the sequential schedule (induction on b), so
+// the kernel iterates S <- f(S) over all pods at once until nothing changes.
+// Pods below a stable prefix are final: if pods < p were right and the first
+// changed selection of an iteration is d >= p, pods <= d are right after it, so
+// the prefix grows by at least one per iteration (<= nb iterations) and the
+// loop ends when it covers the batch.  The starting guess is the greedy
+// "first candidate no earlier pod took"; on cfg2 it converges in 1.5 iterations
+// on average (vs 32 sequential steps; tools/jacobi_sim notes in DESIGN.md).
+//
+// Layout: 16 waves, wave w evaluates pods w and w+16; lanes 0..31 re-evaluate
+// the nodes modified by pods a < b (lane a = the last pod before b that
+// selected node S_a: one lane per distinct node), lanes 32..63 test pod b's 32
+// candidates for having been modified.  Everything lives in LDS; all global
+// stores happen in the final flush.
 struct Patch {
   int32_t node;  // local node index, -1 none
   uint32_t code;
   int32_t fit, ba, total;
 };
+struct Delta {  // requests of the pods assumed on one node inside the batch
+  int64_t req[4];
+  int64_t nzc, nzm;
+  int32_t pods, pad;
+};
+struct SumLite {
+  uint64_t best_key;
+  int32_t selected, feasible, status, pad;
+};
 struct FixupLDS {
   CandRow cand[KSG_BATCH * KSG_CAND];   // 96 KiB
   PodLite pod[KSG_BATCH];
-  Patch patch[KSG_BATCH * KSG_CAND];
-  ksg_pod_summary sum[KSG_BATCH];
+  Patch patch[KSG_BATCH * KSG_CAND];    // [pod][lane a]
+  SumLite sum[KSG_BATCH];
+  Delta cum[2][KSG_BATCH];              // sum over pods <= a selecting sel[a]
+  int32_t sel[2][KSG_BATCH];            // selected global node, -1 none (iteration parity)
+  int32_t srow[2][KSG_BATCH];           // index into cand[] of a row of that node
+  int32_t nxt[2][KSG_BATCH];            // next pod selecting the same node, KSG_BATCH none
+  int32_t prv[KSG_BATCH];
   int32_t feas[KSG_BATCH];
-  int32_t npatch[KSG_BATCH];
-  int32_t hset[512];
+  uint32_t taken[128];                  // initial guess: hashed bitmap of taken nodes
+  int32_t stable;
 };
 
+// Chains of pods per selected node for parity p (one wave; lanes 0..31 = pods).
+__device__ __forceinline__ void fixup_prep(FixupLDS& L, int p, uint32_t nb, uint32_t R, int lane) {
+  int a = lane & (KSG_BATCH - 1);
+  int32_t s = (a < (int)nb) ? L.sel[p][a] : -1;
+  int prv = -1;
+#pragma unroll
+  for (int j = 0; j < KSG_BATCH; ++j) {
+    int32_t sj = __builtin_amdgcn_readlane(s, j);
+    prv = (j < a && sj == s) ? j : prv;
+  }
+  if (s < 0) prv = -1;
+  if (lane < KSG_BATCH) {
+    L.prv[a] = prv;
+    L.nxt[p][a] = KSG_BATCH;
+  }
+  if (lane < KSG_BATCH && prv >= 0) L.nxt[p][prv] = a;  // after the init: LDS ops of a wave are in order
+  if (lane < KSG_BATCH) {
+    Delta d;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d.req[k] = 0;
+    d.nzc = d.nzm = 0;
+    d.pods = d.pad = 0;
+    for (int j = s >= 0 ? a : -1; j >= 0; j = L.prv[j]) {
+      const PodLite& q = L.pod[j];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k)
+        if (k < R) d.req[k] += q.req[k];
+      d.nzc += q.nz_cpu;
+      d.nzm += q.nz_mem;
+      d.pods += 1;
+    }
+    L.cum[p][a] = d;
+  }
+}
+
 #define KSG_FIXUP_THREADS 1024
+#define KSG_FIXUP_WAVES (KSG_FIXUP_THREADS / 64)
 template <int MODE>
 __global__ __launch_bounds__(KSG_FIXUP_THREADS) void k_batch_fixup(DevCluster C, DevProfile F, BatchOut BO, const uint8_t* progs,
                                                      const uint64_t* prog_off, uint32_t j0, uint32_t nb,
                                                      const CandRow* cand, int32_t* feas, ksg_pod_summary* sums,
                                                      uint64_t* stamps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-#define STAMP(k)                                                              \
-  if (stamps && lane == 0) {                                                  \
-    __builtin_amdgcn_sched_barrier(0);                                        \
-    stamps[b * 8 + (k)] = __builtin_amdgcn_s_memtime();                       \
-    __builtin_amdgcn_sched_barrier(0);                                        \
-  }
   FixupLDS& L = *reinterpret_cast<FixupLDS*>(lds_raw);
-  int tid = threadIdx.x;
+  int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#define STAMP(k)                                        \
+  if (stamps && tid == 0) {                             \
+    __builtin_amdgcn_sched_barrier(0);                  \
+    stamps[k] = __builtin_amdgcn_s_memtime();           \
+    __builtin_amdgcn_sched_barrier(0);                  \
+  }
+  STAMP(0);
   {  // stage: candidates (6 independent 16-B loads in flight per thread), pods, counts
     const uint4* src = reinterpret_cast<const uint4*>(cand);
     uint4* dst = reinterpret_cast<uint4*>(L.cand);
@@ -1386,9 +1461,9 @@ __global__ __launch_bounds__(KSG_FIXUP_THREADS) void k_batch_fixup(DevCluster C,
     uint32_t n16 = nb * KSG_CAND * kRow16;
     uint4 v[kRow16];
 #pragma unroll
-    for (uint32_t k = 0; k < kRow16; ++k) {
+    for (uint32_t k = 0; k < kRow16; ++k) {  // clamped, unconditional loads: v stays in registers
       uint32_t i = tid + k * KSG_FIXUP_THREADS;
-      if (i < n16) v[k] = src[i];
+      v[k] = src[i < n16 ? i : 0];
     }
 #pragma unroll
     for (uint32_t k = 0; k < kRow16; ++k) {
@@ -1397,133 +1472,141 @@ __global__ __launch_bounds__(KSG_FIXUP_THREADS) void k_batch_fixup(DevCluster C,
     }
     for (uint32_t b = tid; b < nb; b += blockDim.x) {
       const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[j0 + b]);
-      PodLite& p = L.pod[b];
+      PodLite& q = L.pod[b];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) p.req[k] = h->req[k];
+      for (int k = 0; k < 4; ++k) q.req[k] = h->req[k];
 #pragma unroll
       for (int k = 0; k < KSG_MAX_SCORE_RES; ++k) {
-        p.fit_score_req[k] = h->fit_score_req[k];
-        p.ba_req[k] = h->ba_req[k];
+        q.fit_score_req[k] = h->fit_score_req[k];
+        q.ba_req[k] = h->ba_req[k];
       }
-      p.nz_cpu = h->nz_cpu;
-      p.nz_mem = h->nz_mem;
-      p.queue_idx = h->queue_idx;
-      p.flags = h->flags;
+      q.nz_cpu = h->nz_cpu;
+      q.nz_mem = h->nz_mem;
+      q.queue_idx = h->queue_idx;
+      q.flags = h->flags;
       L.feas[b] = feas[b];
-      feas[b] = 0;  // ready for the next batch
     }
-    for (int i = tid; i < 512; i += blockDim.x) L.hset[i] = -1;
+    if (tid < 128) L.taken[tid] = 0;
+    if (tid == 0) L.stable = 0;
   }
   __syncthreads();
+  STAMP(1);
   uint32_t R = C.R < 4 ? C.R : 4;
-  int lane = tid & 63;
-  int32_t m_id = -1;
-  RowV cur, snap;
-  int nm = 0;
-  if (tid < 64) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) cur.alloc[k] = cur.req[k] = snap.alloc[k] = snap.req[k] = 0;
-    cur.nzc = cur.nzm = snap.nzc = snap.nzm = 0;
-    cur.podcnt = cur.allowed = snap.podcnt = snap.allowed = 0;
+  if (wave == 0) {  // initial guess: each pod takes its best candidate no earlier pod took
     for (uint32_t b = 0; b < nb; ++b) {
-      STAMP(0);
+      uint64_t k = lane < KSG_CAND ? L.cand[b * KSG_CAND + lane].key : 0;
+      uint32_t node = (uint32_t)(k & 0xFFFFFull);
+      uint32_t hb = (node * 2654435761u) >> 20;
+      bool ok = k != 0 && !((L.taken[hb >> 5] >> (hb & 31)) & 1u);
+      unsigned long long m = __ballot(ok), v = __ballot(k != 0);
+      int g = m ? __ffsll((long long)m) - 1 : (v ? 0 : -1);
+      if (lane == g) {
+        L.sel[0][b] = (int32_t)node;
+        L.srow[0][b] = (int32_t)(b * KSG_CAND + g);
+        atomicOr(&L.taken[hb >> 5], 1u << (hb & 31));
+      }
+      if (g < 0 && lane == 0) {
+        L.sel[0][b] = -1;
+        L.srow[0][b] = 0;
+      }
+    }
+    if (lane >= (int)nb && lane < KSG_BATCH) L.sel[0][lane] = L.sel[1][lane] = -1;
+    fixup_prep(L, 0, nb, R, lane);
+  }
+  __syncthreads();
+  STAMP(2);
+  int p = 0;
+  uint32_t iters = 0;
+  for (;;) {
+    int stable = L.stable;
+    for (uint32_t b = wave; b < nb; b += KSG_FIXUP_WAVES) {
+      if ((int)b < stable) {  // final: carry the selection over
+        if (lane == 0) {
+          L.sel[p ^ 1][b] = L.sel[p][b];
+          L.srow[p ^ 1][b] = L.srow[p][b];
+        }
+        continue;
+      }
       const PodLite* h = &L.pod[b];
-      // 1. candidates not modified in this batch (lanes < KSG_CAND)
-      uint64_t ckey = 0;
-      uint32_t cnode = 0;
-      if (lane < KSG_CAND) {
-        ckey = L.cand[b * KSG_CAND + lane].key;
-        cnode = (uint32_t)(ckey & 0xFFFFFull);
-      }
-      bool valid = ckey != 0;
-      if (valid) {
-        uint32_t slot = (cnode * 2654435761u) >> 23;
-        for (;;) {
-          int32_t x = L.hset[slot];
-          if (x < 0) break;
-          if (x == (int32_t)cnode) { valid = false; break; }
-          slot = (slot + 1) & 511;
-        }
-      }
-      uint64_t best = valid ? ckey : 0;
-      STAMP(1);
-      // 2. modified nodes: exact evaluation on the current row
+      int a = lane & (KSG_BATCH - 1);
+      int32_t sv = L.sel[p][a];
+      int32_t rowidx = lane < KSG_BATCH ? L.srow[p][a] : (int32_t)(b * KSG_CAND + a);
+      // candidate lanes: node taken by a pod < b?
+      uint64_t ck = lane >= KSG_BATCH ? L.cand[b * KSG_CAND + a].key : 0;
+      uint32_t cnode = (uint32_t)(ck & 0xFFFFFull);
+      bool modified = false;
+#pragma unroll 1
+      for (uint32_t j = 0; j < b; ++j) modified |= (uint32_t)__builtin_amdgcn_readlane(sv, j) == cnode;
+      uint64_t key = (ck != 0 && !modified) ? ck : 0;
       int dfeas = 0;
-      if (lane < nm) {
-        int32_t fit_s, ba_s;
-        int64_t tot;
-        uint32_t code = eval_row<MODE>(cur, F, h, R, fit_s, ba_s, tot);
-        bool snap_ok = F.pos_fit < 0 || fit_filter_row(snap, h, R) == 0;
-        dfeas = (code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0);
-        uint32_t n = (uint32_t)m_id - C.goff;
-        Patch& pt = L.patch[b * KSG_CAND + lane];
-        pt.node = ((uint32_t)m_id >= C.goff && n < C.N) ? (int32_t)n : -1;
-        pt.code = code;
-        pt.fit = fit_s;
-        pt.ba = ba_s;
-        pt.total = (int32_t)tot;
-        if (code == KSG_FILTER_PASS) {
-          uint64_t k = pack_key(tot, F.seed, h->queue_idx, (uint32_t)m_id);
-          best = k > best ? k : best;
-        }
-      }
-      STAMP(2);
-      best = wave_max(best);
-      int feasible = L.feas[b] + wave_sum(dfeas);
-      STAMP(3);
-      int32_t sel = (feasible > 0 && best) ? (int32_t)(best & 0xFFFFFull) : -1;
-      if (lane == 0) L.npatch[b] = nm;
-      if (sel >= 0) {
-        unsigned long long inm = __ballot(lane < nm && m_id == sel);
-        int holder;
-        if (!inm) {  // new modified node: snapshot row from the candidate carrying it
-          unsigned long long cl = __ballot(valid && cnode == (uint32_t)sel);
-          int src = __ffsll((long long)cl) - 1;
-          if (lane == nm) {
-            const CandRow& cr = L.cand[b * KSG_CAND + src];
+      if (lane < KSG_BATCH) {
+        Patch pt;
+        pt.node = -1;
+        pt.code = 0;
+        pt.fit = pt.ba = pt.total = 0;
+        if (a < (int)b && sv >= 0 && L.nxt[p][a] >= (int)b) {
+          const CandRow& cr = L.cand[rowidx];
+          const Delta& d = L.cum[p][a];
+          RowV snap, cur;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              cur.alloc[k] = cr.alloc[k];
-              cur.req[k] = cr.req[k];
-            }
-            cur.nzc = cr.nzc;
-            cur.nzm = cr.nzm;
-            cur.podcnt = cr.podcnt;
-            cur.allowed = cr.allowed;
-            snap = cur;
-            m_id = sel;
-            uint32_t slot = ((uint32_t)sel * 2654435761u) >> 23;
-            while (L.hset[slot] >= 0) slot = (slot + 1) & 511;
-            L.hset[slot] = sel;
+          for (int k = 0; k < 4; ++k) {
+            snap.alloc[k] = cur.alloc[k] = cr.alloc[k];
+            snap.req[k] = cr.req[k];
+            cur.req[k] = cr.req[k] + d.req[k];
           }
-          holder = nm;
-          nm++;
-        } else {
-          holder = __ffsll((long long)inm) - 1;
+          snap.nzc = cr.nzc;
+          snap.nzm = cr.nzm;
+          snap.podcnt = cr.podcnt;
+          snap.allowed = cur.allowed = cr.allowed;
+          cur.nzc = cr.nzc + d.nzc;
+          cur.nzm = cr.nzm + d.nzm;
+          cur.podcnt = cr.podcnt + d.pods;
+          int32_t fit_s, ba_s;
+          int64_t tot;
+          uint32_t code = eval_row<MODE>(cur, F, h, R, fit_s, ba_s, tot);
+          bool snap_ok = F.pos_fit < 0 || fit_filter_row(snap, h, R) == 0;
+          dfeas = (code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0);
+          uint32_t n = (uint32_t)sv - C.goff;
+          pt.node = ((uint32_t)sv >= C.goff && n < C.N) ? (int32_t)n : -1;
+          pt.code = code;
+          pt.fit = fit_s;
+          pt.ba = ba_s;
+          pt.total = (int32_t)tot;
+          if (code == KSG_FILTER_PASS) key = pack_key(tot, F.seed, h->queue_idx, (uint32_t)sv);
         }
-        if (lane == holder) {  // assume: NodeInfo.AddPod
-#pragma unroll
-          for (uint32_t k = 0; k < 4; ++k)
-            if (k < R) cur.req[k] += h->req[k];
-          cur.nzc += h->nz_cpu;
-          cur.nzm += h->nz_mem;
-          cur.podcnt += 1;
-        }
+        L.patch[b * KSG_CAND + a] = pt;
       }
-      STAMP(4);
+      uint64_t best = wave_max(key);
+      int feasible = L.feas[b] + wave_sum(dfeas);
+      int32_t sel = (feasible > 0 && best) ? (int32_t)(best & 0xFFFFFull) : -1;
+      unsigned long long wm = __ballot(best != 0 && key == best);
+      int32_t srow_new = wm ? __builtin_amdgcn_readlane(rowidx, __ffsll((long long)wm) - 1) : 0;
       if (lane == 0) {
-        ksg_pod_summary& sm = L.sum[b];
+        L.sel[p ^ 1][b] = sel;
+        L.srow[p ^ 1][b] = srow_new;
+        SumLite& sm = L.sum[b];
         sm.best_key = sel >= 0 ? (feasible == 1 ? (best & 0xFFFFFFFFFFull) : best) : 0;
         sm.selected = sel;
         sm.feasible = feasible;
         sm.status = sel >= 0 ? 0 : 1;
       }
-      STAMP(5);
     }
+    __syncthreads();
+    if (wave == 0) {
+      int a = lane & (KSG_BATCH - 1);
+      bool changed = lane < (int)nb && lane >= stable && L.sel[p ^ 1][a] != L.sel[p][a];
+      unsigned long long m = __ballot(changed);
+      fixup_prep(L, p ^ 1, nb, R, lane);
+      if (lane == 0) L.stable = m ? (int)min((uint32_t)(__ffsll((long long)m)), nb) : (int)nb;
+    }
+    __syncthreads();
+    p ^= 1;
+    ++iters;
+    if (L.stable >= (int)nb) break;
   }
-#undef STAMP
-  __syncthreads();
-  // flush: summaries, patches, modified rows
+  STAMP(3);
+  if (stamps && tid == 0) stamps[4] = iters;
+  // flush: summaries, patches, final node rows
   for (uint32_t b = tid; b < nb; b += blockDim.x) {
     ksg_pod_summary& d = sums[j0 + b];
     d.best_key = L.sum[b].best_key;
@@ -1532,26 +1615,29 @@ __global__ __launch_bounds__(KSG_FIXUP_THREADS) void k_batch_fixup(DevCluster C,
     d.status = L.sum[b].status;
   }
   for (uint32_t i = tid; i < nb * KSG_CAND; i += blockDim.x) {
-    uint32_t b = i / KSG_CAND, j = i % KSG_CAND;
-    if ((int)j >= L.npatch[b]) continue;
     const Patch& pt = L.patch[i];
     if (pt.node < 0) continue;
     uint32_t* of;
     int32_t *os, *ot;
-    out_ptrs(BO, b, C.N, of, os, ot);
+    out_ptrs(BO, i / KSG_CAND, C.N, of, os, ot);
     write_pair(F, of, os, ot, C.N, (uint32_t)pt.node, pt.code, pt.fit, pt.ba, pt.total);
   }
-  if (tid < 64 && lane < nm) {
-    uint32_t n = (uint32_t)m_id - C.goff;
-    if ((uint32_t)m_id >= C.goff && n < C.N) {
+  if (tid < (int)nb) {
+    int32_t s = L.sel[p][tid];
+    uint32_t n = (uint32_t)s - C.goff;
+    if (s >= 0 && L.nxt[p][tid] == KSG_BATCH && (uint32_t)s >= C.goff && n < C.N) {
+      const CandRow& cr = L.cand[L.srow[p][tid]];
+      const Delta& d = L.cum[p][tid];
 #pragma unroll
       for (uint32_t k = 0; k < 4; ++k)
-        if (k < R) C.req[(size_t)k * C.N + n] = cur.req[k];
-      C.nzc[n] = cur.nzc;
-      C.nzm[n] = cur.nzm;
-      C.podcnt[n] = cur.podcnt;
+        if (k < R) C.req[(size_t)k * C.N + n] = cr.req[k] + d.req[k];
+      C.nzc[n] = cr.nzc + d.nzc;
+      C.nzm[n] = cr.nzm + d.nzm;
+      C.podcnt[n] = cr.podcnt + d.pods;
     }
   }
+  STAMP(5);
+#undef STAMP
 }
 
 // ----------------------------------------------------------------- host side
@@ -1635,7 +1721,7 @@ struct Engine::Impl {
   // speculative batch path
   bool batch_ok = false;
   DBuf<uint64_t> tile_top;
-  DBuf<int32_t> bfeas;
+  DBuf<int32_t> bfeas, tfeas;
   DBuf<CandRow> cand;
   DBuf<uint32_t> bfilter;
   DBuf<int32_t> bscore, btotal;
@@ -1838,7 +1924,8 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     uint32_t T = (I.N + kBlock - 1) / kBlock;
     size_t Nn = std::max<uint32_t>(I.N, 1);
     if (!I.tile_top.alloc((size_t)KSG_BATCH * std::max<uint32_t>(T, 1) * KSG_TOPK, err) ||
-        !I.bfeas.alloc(KSG_BATCH, err) || !I.cand.alloc((size_t)KSG_BATCH * KSG_CAND, err) ||
+        !I.bfeas.alloc(KSG_BATCH, err) || !I.tfeas.alloc((size_t)KSG_BATCH * std::max<uint32_t>(T, 1), err) ||
+        !I.cand.alloc((size_t)KSG_BATCH * KSG_CAND, err) ||
         !I.bfilter.alloc(Nn * KSG_BATCH, err) || !I.bscore.alloc(Nn * KSG_BATCH * KSG_MAX_PLUGINS, err) ||
         !I.btotal.alloc(Nn * KSG_BATCH, err))
       return false;
@@ -1891,10 +1978,10 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
     if (I.eval_mode == 1)
       hipLaunchKernelGGL(k_batch_eval<1>, dim3(T, nb), dim3(kBlock), 0, s, C, I.F, BO, I.progs.p, I.prog_off_d.p, j0,
-                         I.tile_top.p, I.bfeas.p, T, I.any_eph_req ? 1u : 0u, I.estamps_on ? I.estamps.p : nullptr);
+                         I.tile_top.p, I.tfeas.p, T, I.any_eph_req ? 1u : 0u, I.estamps_on ? I.estamps.p : nullptr);
     else
       hipLaunchKernelGGL(k_batch_eval<0>, dim3(T, nb), dim3(kBlock), 0, s, C, I.F, BO, I.progs.p, I.prog_off_d.p, j0,
-                         I.tile_top.p, I.bfeas.p, T, I.any_eph_req ? 1u : 0u, I.estamps_on ? I.estamps.p : nullptr);
+                         I.tile_top.p, I.tfeas.p, T, I.any_eph_req ? 1u : 0u, I.estamps_on ? I.estamps.p : nullptr);
     if (sampled) {
       HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
       I.n_samples++;
@@ -1903,7 +1990,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     if (I.xranks > 1) {
       const size_t rec = KSG_XHDR + (size_t)KSG_BATCH * KSG_CAND * sizeof(CandRow);
       hipLaunchKernelGGL(k_batch_merge, dim3(nb), dim3(64), 0, s, C, I.tile_top.p, T,
-                         reinterpret_cast<CandRow*>(I.xsend.p + KSG_XHDR), I.bfeas.p,
+                         reinterpret_cast<CandRow*>(I.xsend.p + KSG_XHDR), I.tfeas.p,
                          reinterpret_cast<int32_t*>(I.xsend.p));
       if (I.xmode == 1) {
         ncclResult_t nr = ncclAllGather(I.xsend.p, I.xrecv.p, rec, ncclUint8, I.comm, s);
@@ -1917,10 +2004,9 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
       hipLaunchKernelGGL(k_batch_gmerge, dim3(nb), dim3(64), 0, s, I.xrecv.p, rec, I.xranks, I.cand.p, I.gfeas.p);
       fx = I.gfeas.p;
     } else {
-      hipLaunchKernelGGL(k_batch_merge, dim3(nb), dim3(64), 0, s, C, I.tile_top.p, T, I.cand.p, I.bfeas.p,
-                         (int32_t*)nullptr);
+      hipLaunchKernelGGL(k_batch_merge, dim3(nb), dim3(64), 0, s, C, I.tile_top.p, T, I.cand.p, I.tfeas.p, I.bfeas.p);
     }
-    uint64_t* fst = I.stamps_on ? I.stamps.p + (size_t)(j0 - first) * 8 : nullptr;
+    uint64_t* fst = I.stamps_on ? I.stamps.p + (size_t)(j0 - first) * 8 : nullptr;  // per batch: 8 stamps at its first pod
     if (I.eval_mode == 1)
       hipLaunchKernelGGL(k_batch_fixup<1>, dim3(1), dim3(KSG_FIXUP_THREADS), sizeof(FixupLDS), s, C, I.F, BO, I.progs.p,
                          I.prog_off_d.p, j0, nb, I.cand.p, fx, I.sums.p, fst);

@@ -19,17 +19,16 @@ L.ksg_debug_fixup_stamps(s.h, n, None)
 s.schedule()
 buf = (ctypes.c_uint64 * (8 * n))()
 L.ksg_debug_fixup_stamps(s.h, n, buf)
-ph = [[] for _ in range(5)]
-for b in range(32, n):
-    st = buf[b * 8:(b + 1) * 8]
-    for k in range(5):
-        ph[k].append(st[k + 1] - st[k])
-names = ["cand+hset", "eval M", "reductions", "select/update", "summary"]
-for k in range(5):
-    v = sorted(ph[k])
-    print(f"{names[k]:14s} median {v[len(v)//2]:6d} mean {sum(v)/len(v):8.1f} cycles")
-tot = [buf[b * 8 + 5] - buf[b * 8] for b in range(32, n)]
-print("per pod total median", sorted(tot)[len(tot) // 2])
+# per batch: [0] start [1] staged [2] guess+prep [3] converged [4] iterations [5] flushed
+bs = [buf[j * 8:(j + 1) * 8] for j in range(32, n, 32)]
+names = ["stage", "guess+prep", "iterations", "flush"]
+for k, (i0, i1) in enumerate([(0, 1), (1, 2), (2, 3), (3, 5)]):
+    v = sorted(x[i1] - x[i0] for x in bs)
+    print(f"fixup {names[k]:12s} median {v[len(v)//2]:6d} mean {sum(v)/len(v):8.1f} cycles")
+it = [x[4] for x in bs]
+print("fixup iterations: mean", sum(it) / len(it), "max", max(it), "hist", {k: it.count(k) for k in sorted(set(it))})
+tot = sorted(x[5] - x[0] for x in bs)
+print("per batch total median", tot[len(tot) // 2], "cycles")
 
 # k_batch_eval per-wave phases (last batch of a run)
 L.ksg_debug_eval_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]

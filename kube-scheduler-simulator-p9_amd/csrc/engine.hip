@@ -961,31 +961,51 @@ __global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* pr
   C.tcounts[3] = vb;
 }
 
-// ----------------------------------------------------------------- speculative batch path
+// ----------------------------------------------------------------- speculative window path
 // For profiles whose plugins are all NodeResourcesFit / BalancedAllocation (no
 // ScoreExtensions, no cross-node state) a pod's result on node n depends only on
-// node n's row.  B pods are evaluated against one snapshot in one wide launch
-// (k_batch_eval); each keeps its top-64 nodes by packed key (k_batch_merge); a
-// one-wave fixup (k_batch_fixup) then replays the B pods in queue order,
-// re-evaluating only the nodes already modified inside the batch (at most B-1 <
-// 64, so one unmodified candidate always survives).  The result is exactly the
-// sequential schedule: same selections, same per-pair outputs (patched for the
-// modified nodes), same assume deltas.
+// node n's row, so the queue runs as windows of KSG_BATCH pods, pipelined two
+// deep: ONE launch of k_window per window j
+//
+//   block 0      replays window j exactly (k_window's fixup: Jacobi iteration
+//                over the window's picks, see win_fixup), appends the window's
+//                assume deltas to the pending list P_j and writes P_{j-1} back
+//                into the node rows;
+//   blocks 1..   evaluate window j+1 against the rows as of the end of window
+//                j-1 (rows of P_{j-1} taken from the list, since block 0 is
+//                rewriting them), write every per-pair output, keep each tile's
+//                top-64 keys; the last tile block of each pod (arrival counter)
+//                merges them into the pod's 64 candidates with their rows.
+//
+// The candidates of window j+1 are thus taken on a snapshot two windows old:
+// at most 32 (window j) + 31 (earlier pods of window j+1) nodes can have
+// changed since, so of 64 candidates at least one is unmodified, and the best
+// unmodified node of a pod is always in its list.  Modified nodes are
+// re-evaluated exactly on their current rows.  The result is the sequential
+// schedule: same selections, same per-pair outputs, same assume deltas.
 #define KSG_BATCH 32
+#define KSG_CAND 64        // candidates per pod: >= 2*KSG_BATCH (see above)
 #define KSG_TOPK 64
-#define KSG_CAND 32  // candidates kept per pod (>= KSG_BATCH guarantees a surviving one)
+#define KSG_WIN_THREADS 1024
+#define KSG_TILE KSG_WIN_THREADS  // nodes per eval block
+#define KSG_STAGE 16       // candidate ranks whose rows are staged in LDS (deeper ranks: global)
+#define KSG_XHDR 128       // record header: feasible count per pod (KSG_BATCH ints)
+#define KSG_NOT_PATCHED 0xFFFFFFFDu
 
 struct RowV {  // one node row (resource columns 0..3)
   int64_t alloc[4], req[4];
   int64_t nzc, nzm;
   int32_t podcnt, allowed;
 };
-struct CandRow {  // top-K candidate with its snapshot row (96 B)
+struct CandRow {  // candidate key with the row the key was computed on (96 B)
   uint64_t key;
-  int64_t alloc[4], req[4];
-  int64_t nzc, nzm;
-  int32_t podcnt, allowed;
+  RowV r;
 };
+struct Pend {  // a node modified by a window: row before (base) and after it
+  int32_t node, pad;  // global node index
+  RowV base, after;
+};
+static constexpr size_t kRecBytes = KSG_XHDR + (size_t)KSG_BATCH * KSG_CAND * sizeof(CandRow);
 
 struct PodLite {  // the fields of ksg_prog the Fit/BA evaluation reads (LDS-staged)
   int64_t req[4];
@@ -996,19 +1016,29 @@ struct PodLite {  // the fields of ksg_prog the Fit/BA evaluation reads (LDS-sta
   uint32_t flags;
 };
 
-struct BatchOut {
-  uint32_t* filter;   // per pod base = filter + slot*N
-  int32_t* score;     // per pod base = score + slot*N*KSG_MAX_PLUGINS
-  int32_t* total;
-  uint32_t slot0;     // slot of the batch's first pod (kept window) or 0 (scratch)
-  int kept;           // 1: slot = pod - keep_first ; 0: slot = pod - first (scratch ring)
+struct WinArgs {
+  const uint8_t* progs;
+  const uint64_t* prog_off;
+  uint32_t first, keep_first, keep_n, need_eph;
+  uint32_t *kfilter, *sfilter;  // kept outputs / scratch ring of 2*KSG_BATCH pods
+  int32_t *kscore, *sscore, *ktotal, *stotal;
+  // eval part: window E = queue pods [e0, e0 + ne)
+  uint32_t e0, ne, T;
+  uint64_t* tile_top;    // [KSG_BATCH][T][KSG_TOPK]
+  int32_t* tile_feas;    // [KSG_BATCH][T]
+  uint32_t* arrive;      // [KSG_BATCH] tile arrivals (reset by the last block)
+  uint8_t* erec;         // candidate record of window E (kRecBytes)
+  // fixup part: window W = queue pods [w0, w0 + nw)
+  uint32_t w0, nw;
+  const uint8_t* wrec;   // candidate record of window W
+  const Pend* pprev;     // P_{W-1} (also the eval part's row overrides)
+  const int32_t* pprev_n;
+  Pend* pnext;           // P_W
+  int32_t* pnext_n;
+  ksg_pod_summary* sums;
+  uint64_t* stamps;      // diagnostic stamps of window W's fixup (16 slots), or null
+  uint64_t* estamps;     // diagnostic stamps of window E's eval blocks (16 slots), or null
 };
-
-// Register-resident row evaluation.  No local array is indexed at run time (no
-// scratch) and nothing is unrolled beyond what the profile needs: instruction
-// cache footprint matters more than loop overhead here.  MODE 1 is the compiled
-// specialisation for the default arguments (Fit LeastAllocated over cpu+memory,
-// BalancedAllocation over cpu+memory); MODE 0 walks the configured resources.
 __device__ __forceinline__ int64_t sel4(const int64_t (&v)[4], int i) {
   return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3];
 }
@@ -1176,303 +1206,338 @@ __device__ __forceinline__ uint64_t wave_merge_top(uint64_t v, uint64_t o_rev) {
   return v;
 }
 
-__device__ __forceinline__ void out_ptrs(const BatchOut& BO, uint32_t b, uint32_t N, uint32_t*& f, int32_t*& s,
+// Per-pair output rows of queue pod q: the kept window, or a scratch ring of
+// two windows (window j+1 is evaluated while window j is being patched).
+__device__ __forceinline__ void out_ptrs(const WinArgs& A, uint32_t q, uint32_t N, uint32_t*& f, int32_t*& s,
                                          int32_t*& t) {
-  size_t slot = BO.slot0 + b;
-  f = BO.filter + slot * N;
-  s = BO.score + slot * N * KSG_MAX_PLUGINS;
-  t = BO.total + slot * N;
+  if (A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n) {
+    size_t slot = q - A.keep_first;
+    f = A.kfilter + slot * N;
+    s = A.kscore + slot * N * KSG_MAX_PLUGINS;
+    t = A.ktotal + slot * N;
+  } else {
+    size_t slot = (q - A.first) % (2 * KSG_BATCH);
+    f = A.sfilter + slot * N;
+    s = A.sscore + slot * N * KSG_MAX_PLUGINS;
+    t = A.stotal + slot * N;
+  }
+}
+__device__ __forceinline__ void load_row(const DevCluster& C, uint32_t n, uint32_t need_eph, RowV& r) {
+  r.alloc[0] = C.alloc[n];
+  r.alloc[1] = C.alloc[(size_t)C.N + n];
+  r.req[0] = C.req[n];
+  r.req[1] = C.req[(size_t)C.N + n];
+  r.alloc[2] = r.req[2] = r.alloc[3] = r.req[3] = 0;
+  if (need_eph) {
+#pragma unroll
+    for (uint32_t c = 2; c < 4; ++c)
+      if (c < C.R) {
+        r.alloc[c] = C.alloc[(size_t)c * C.N + n];
+        r.req[c] = C.req[(size_t)c * C.N + n];
+      }
+  }
+  r.nzc = C.nzc[n];
+  r.nzm = C.nzm[n];
+  r.podcnt = C.podcnt[n];
+  r.allowed = C.allowed[n];
+}
+__device__ __forceinline__ void store_row(const DevCluster& C, uint32_t n, const RowV& r) {
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k)
+    if (k < C.R) C.req[(size_t)k * C.N + n] = r.req[k];
+  C.nzc[n] = r.nzc;
+  C.nzm[n] = r.nzm;
+  C.podcnt[n] = r.podcnt;
+}
+// Index of global node gid in P_{W-1} (lane e of pn holds entry e's node), or -1.
+__device__ __forceinline__ int pend_index(int32_t gid, int32_t pn, int np) {
+  int hit = -1;
+  for (int e = 0; e < np; ++e) hit = __builtin_amdgcn_readlane(pn, e) == gid ? e : hit;
+  return hit;
+}
+// LDS-only barrier: __syncthreads() would also wait (vmcnt(0)) for this
+// wave's per-pair output stores, which nothing after it depends on.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// grid (tiles, pods): one node per thread, one pod per block
+// Blocks 1.. of k_window: one pod x KSG_TILE nodes per block.  Tile lists are
+// handed to the pod's last-arriving block with sc1 stores/loads and an agent
+// counter (MI355X_MICROARCH.md, hand-off table row 1).
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void k_batch_eval(DevCluster C, DevProfile F, BatchOut BO, const uint8_t* progs,
-                                                       const uint64_t* prog_off, uint32_t j0, uint64_t* tile_top,
-                                                       int32_t* feas, uint32_t n_tiles, uint32_t need_eph,
-                                                       uint64_t* stamps) {
-  __shared__ uint64_t lists[kBlock];
-  uint32_t b = blockIdx.y;
-  uint64_t* st = stamps ? stamps + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)) * 8 : nullptr;
-#define ESTAMP(k)                                               \
-  if (st && (threadIdx.x & 63) == 0) {                          \
-    __builtin_amdgcn_sched_barrier(0);                          \
-    st[k] = __builtin_amdgcn_s_memtime();                       \
-    __builtin_amdgcn_sched_barrier(0);                          \
-  }
-  ESTAMP(0);
-  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[j0 + b]);
-  uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+__device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& F, const WinArgs& A, uint32_t blk, uint64_t* L) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t* wcount = reinterpret_cast<uint32_t*>(L + 16 * 64);
+  const uint32_t b = blk / A.T, tile = blk - b * A.T, q = A.e0 + b;
+  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[q]);
+  const int np = *A.pprev_n;
+  const int32_t pn = lane < np ? A.pprev[lane].node : -1;
+  const uint32_t n = tile * KSG_TILE + tid;
+  const int hit = pend_index((int32_t)(C.goff + n), pn, np);
+  if (A.estamps && tid == 0) atomicMax((unsigned long long*)&A.estamps[8], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
   uint64_t key = 0;
   bool feasible = false;
   if (n < C.N) {
     RowV r;
-    r.alloc[0] = C.alloc[n];
-    r.alloc[1] = C.alloc[(size_t)C.N + n];
-    r.req[0] = C.req[n];
-    r.req[1] = C.req[(size_t)C.N + n];
-    r.alloc[2] = r.req[2] = r.alloc[3] = r.req[3] = 0;
-    if (need_eph) {
-#pragma unroll
-      for (uint32_t c = 2; c < 4; ++c)
-        if (c < C.R) {
-          r.alloc[c] = C.alloc[(size_t)c * C.N + n];
-          r.req[c] = C.req[(size_t)c * C.N + n];
-        }
-    }
-    r.nzc = C.nzc[n];
-    r.nzm = C.nzm[n];
-    r.podcnt = C.podcnt[n];
-    r.allowed = C.allowed[n];
+    if (hit >= 0) r = A.pprev[hit].after;
+    else load_row(C, n, A.need_eph, r);
     int32_t fit_s, ba_s;
     int64_t total;
-    ESTAMP(1);
     uint32_t code = eval_row<MODE>(r, F, h, C.R < 4 ? C.R : 4, fit_s, ba_s, total);
-    ESTAMP(2);
     uint32_t* of;
     int32_t *os, *ot;
-    out_ptrs(BO, b, C.N, of, os, ot);
+    out_ptrs(A, q, C.N, of, os, ot);
     write_pair(F, of, os, ot, C.N, n, code, fit_s, ba_s, total);
     if (code == KSG_FILTER_PASS) {
       feasible = true;
       key = pack_key(total, F.seed, h->queue_idx, C.goff + n);
     }
   }
-  ESTAMP(3);
-  // Feasible count per (pod, tile) with a plain store: device atomics from every
-  // wave onto the 128-B line of per-pod counters serialise across XCDs.
-  __shared__ int32_t wcount[kBlock / 64];
   unsigned long long bal = __ballot(feasible);
   key = wave_sort_desc(key);
-  ESTAMP(4);
-  int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  lists[w * 64 + lane] = key;
-  if (lane == 0) wcount[w] = (int32_t)__popcll(bal);
-  // LDS-only barrier: __syncthreads() would also wait (vmcnt(0)) for this
-  // wave's per-pair output stores, which nothing below depends on.
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  L[w * 64 + lane] = key;
+  if (lane == 0) wcount[w] = (uint32_t)__popcll(bal);
+  lds_barrier();
+#pragma unroll 1
+  for (int s = 8; s >= 1; s >>= 1) {
+    if (w < s) L[w * 64 + lane] = wave_merge_top(L[w * 64 + lane], L[(w + s) * 64 + 63 - lane]);
+    lds_barrier();
+  }
   if (w == 0) {
-    uint64_t v = lists[lane];
-    for (int k = 1; k < kBlock / 64; ++k) v = wave_merge_top(v, lists[k * 64 + 63 - lane]);
-    tile_top[((size_t)b * n_tiles + blockIdx.x) * KSG_TOPK + lane] = v;
+    uint64_t* dst = A.tile_top + ((size_t)b * A.T + tile) * KSG_TOPK;
+    __hip_atomic_store(dst + lane, L[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (lane == 0) {
       int32_t c = 0;
-      for (int k = 0; k < kBlock / 64; ++k) c += wcount[k];
-      feas[(size_t)b * n_tiles + blockIdx.x] = c;
+      for (int k = 0; k < 16; ++k) c += (int32_t)wcount[k];
+      __hip_atomic_store(A.tile_feas + (size_t)b * A.T + tile, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(A.arrive + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (lane == 0) wcount[16] = old == A.T - 1 ? 1u : 0u;
   }
-  ESTAMP(5);
-#undef ESTAMP
-}
-
-// one wave per pod: merge the tile lists into the pod's top-64 and gather rows
-__global__ __launch_bounds__(64) void k_batch_merge(DevCluster C, const uint64_t* tile_top, uint32_t n_tiles,
-                                                    CandRow* cand, const int32_t* tile_feas, int32_t* feas) {
-  uint32_t b = blockIdx.x;
-  int lane = threadIdx.x;
-  int32_t fc = 0;
-  for (uint32_t t = lane; t < n_tiles; t += 64) fc += tile_feas[(size_t)b * n_tiles + t];
-  fc = wave_sum(fc);
-  const uint64_t* L = tile_top + (size_t)b * n_tiles * KSG_TOPK;
-  uint64_t v = L[lane];
-  uint32_t t = 1;
-  for (; t + 4 <= n_tiles; t += 4) {
-    uint64_t o0 = L[(size_t)t * 64 + 63 - lane], o1 = L[(size_t)(t + 1) * 64 + 63 - lane];
-    uint64_t o2 = L[(size_t)(t + 2) * 64 + 63 - lane], o3 = L[(size_t)(t + 3) * 64 + 63 - lane];
-    v = wave_merge_top(v, o0);
-    v = wave_merge_top(v, o1);
-    v = wave_merge_top(v, o2);
-    v = wave_merge_top(v, o3);
+  lds_barrier();
+  if (A.estamps && tid == 0) atomicMax((unsigned long long*)&A.estamps[9], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  if (!wcount[16]) return;
+  // last tile block of pod b: merge the T tile lists (wave w takes tiles w, w+16, ...)
+  {
+    const uint64_t* src = A.tile_top + (size_t)b * A.T * KSG_TOPK;
+    uint64_t v = 0;
+    if ((uint32_t)w < A.T) v = ld_agent(src + (size_t)w * KSG_TOPK + lane);
+#pragma unroll 1
+    for (uint32_t t = w + 16; t < A.T; t += 16) v = wave_merge_top(v, ld_agent(src + (size_t)t * KSG_TOPK + 63 - lane));
+    L[w * 64 + lane] = v;
   }
-  for (; t < n_tiles; ++t) v = wave_merge_top(v, L[(size_t)t * 64 + 63 - lane]);
-  CandRow c;
-  c.key = v;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) c.alloc[k] = c.req[k] = 0;
-  c.nzc = c.nzm = 0;
-  c.podcnt = c.allowed = 0;
-  if (v) {
-    uint32_t n = (uint32_t)(v & 0xFFFFFull) - C.goff;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
-      if (k < C.R) {
-        c.alloc[k] = C.alloc[(size_t)k * C.N + n];
-        c.req[k] = C.req[(size_t)k * C.N + n];
-      }
-    c.nzc = C.nzc[n];
-    c.nzm = C.nzm[n];
-    c.podcnt = C.podcnt[n];
-    c.allowed = C.allowed[n];
+  lds_barrier();
+#pragma unroll 1
+  for (int s = 8; s >= 1; s >>= 1) {
+    if (w < s) L[w * 64 + lane] = wave_merge_top(L[w * 64 + lane], L[(w + s) * 64 + 63 - lane]);
+    lds_barrier();
   }
-  if (lane < KSG_CAND) cand[(size_t)b * KSG_CAND + lane] = c;
-  if (lane == 0) feas[b] = fc;  // this shard's feasible count for pod b
-}
-
-// Sharded batches: every rank's exchange record = [feasible counts (KSG_BATCH
-// ints, 128 B)] [top-KSG_CAND CandRow per pod].  One wave per pod merges the R
-// sorted lists into the global top-KSG_CAND and sums the feasible counts.
-#define KSG_XHDR 128
-__global__ __launch_bounds__(64) void k_batch_gmerge(const uint8_t* recv, size_t rec_bytes, uint32_t ranks,
-                                                     CandRow* cand, int32_t* gfeas) {
-  __shared__ uint64_t keys[8 * KSG_CAND];
-  uint32_t b = blockIdx.x;
-  int lane = threadIdx.x;
-  for (uint32_t i = lane; i < ranks * KSG_CAND; i += 64) {
-    uint32_t r = i / KSG_CAND, j = i % KSG_CAND;
-    const CandRow* L = reinterpret_cast<const CandRow*>(recv + r * rec_bytes + KSG_XHDR);
-    keys[i] = L[(size_t)b * KSG_CAND + j].key;
-  }
-  __syncthreads();
-  uint64_t v = lane < KSG_CAND ? keys[lane] : 0;
-  for (uint32_t r = 1; r < ranks; ++r) {
-    int j = 63 - lane;
-    uint64_t o = j < KSG_CAND ? keys[r * KSG_CAND + j] : 0;
-    v = wave_merge_top(v, o);
-  }
-  int32_t f = 0;
-  for (uint32_t r = 0; r < ranks; ++r) f += reinterpret_cast<const int32_t*>(recv + r * rec_bytes)[b];
-  if (lane < KSG_CAND) {
+  if (w == 0) {
+    uint64_t v = L[lane];
     CandRow c;
     memset(&c, 0, sizeof(c));
-    if (v) {  // find the source entry: each rank's list is sorted descending
-      for (uint32_t r = 0; r < ranks; ++r) {
-        int lo = 0, hi = KSG_CAND - 1, at = -1;
-        while (lo <= hi) {
-          int mid = (lo + hi) >> 1;
-          uint64_t k = keys[r * KSG_CAND + mid];
-          if (k == v) { at = mid; break; }
-          if (k > v) lo = mid + 1; else hi = mid - 1;
-        }
-        if (at >= 0) {
-          c = reinterpret_cast<const CandRow*>(recv + r * rec_bytes + KSG_XHDR)[(size_t)b * KSG_CAND + at];
-          break;
-        }
-      }
+    c.key = v;
+    int32_t gid = (int32_t)(v & 0xFFFFFull);
+    int hh = pend_index(gid, pn, np);
+    if (v) {
+      if (hh >= 0) c.r = A.pprev[hh].after;
+      else load_row(C, (uint32_t)gid - C.goff, A.need_eph, c.r);
     }
-    cand[(size_t)b * KSG_CAND + lane] = c;
+    reinterpret_cast<CandRow*>(A.erec + KSG_XHDR)[(size_t)b * KSG_CAND + lane] = c;
+    int32_t f = 0;
+    for (uint32_t t = lane; t < A.T; t += 64)
+      f += __hip_atomic_load(A.tile_feas + (size_t)b * A.T + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    f = wave_sum(f);
+    if (lane == 0) {
+      reinterpret_cast<int32_t*>(A.erec)[b] = f;
+      A.arrive[b] = 0;
+      if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
   }
-  if (lane == 0) gfeas[b] = f;
 }
 
-
-// Replay the batch in queue order, exactly, as a fixed-point iteration.
+// ---- block 0: exact replay of window W as a fixed-point (Jacobi) iteration.
 //
-// Pod b's outcome is a function of the selections of pods < b only:
-// S_b = f_b(S_0..S_{b-1}) (its surviving candidates plus the nodes modified by
-// earlier pods, re-evaluated on their current rows).  A vector S with
-// S_b == f_b(S_<b) for every b IS the sequential schedule (induction on b), so
-// the kernel iterates S <- f(S) over all pods at once until nothing changes.
-// Pods below a stable prefix are final: if pods < p were right and the first
-// changed selection of an iteration is d >= p, pods <= d are right after it, so
-// the prefix grows by at least one per iteration (<= nb iterations) and the
-// loop ends when it covers the batch.  The starting guess is the greedy
-// "first candidate no earlier pod took"; on cfg2 it converges in 1.5 iterations
-// on average (vs 32 sequential steps; tools/jacobi_sim notes in DESIGN.md).
+// Pod b's outcome is a function of the picks of pods < b only: S_b =
+// f_b(S_0..S_{b-1}) = the best of (its candidates no earlier pick and no
+// node of P_{W-1} touched; the nodes of P_{W-1} and the earlier picks,
+// re-evaluated on their current rows).  A vector S with S_b == f_b(S_<b) for
+// every b IS the sequential schedule (induction on b), so all pods iterate
+// S <- f(S) at once until nothing changes; if pods < p were right and the first
+// change of an iteration is at d >= p, pods <= d are right after it, so the
+// stable prefix grows every iteration.  The starting guess is the greedy
+// "best candidate or P_{W-1} node no earlier pod took" (serial dictatorship,
+// computed in parallel rounds); on cfg2 it is right in ~2/3 of the windows.
 //
-// Layout: 16 waves, wave w evaluates pods w and w+16; lanes 0..31 re-evaluate
-// the nodes modified by pods a < b (lane a = the last pod before b that
-// selected node S_a: one lane per distinct node), lanes 32..63 test pod b's 32
-// candidates for having been modified.  Everything lives in LDS; all global
-// stores happen in the final flush.
-struct Patch {
-  int32_t node;  // local node index, -1 none
+// Lanes: wave w owns pods w and w+16.  Evaluations of modified nodes pack both
+// pods in one wave instruction stream (lanes 0..31: pod w, 32..63: pod w+16,
+// lane&31 = the earlier pick a it re-evaluates); the per-pod reduction then
+// covers 64 candidate lanes + 32 P_{W-1} lanes + its 32 pick lanes.
+struct PatchV {
   uint32_t code;
   int32_t fit, ba, total;
-};
-struct Delta {  // requests of the pods assumed on one node inside the batch
-  int64_t req[4];
-  int64_t nzc, nzm;
-  int32_t pods, pad;
 };
 struct SumLite {
   uint64_t best_key;
   int32_t selected, feasible, status, pad;
 };
-struct FixupLDS {
-  CandRow cand[KSG_BATCH * KSG_CAND];   // 96 KiB
+struct Delta {
+  int64_t req[4];
+  int64_t nzc, nzm;
+  int32_t pods;
+};
+#define KSG_HSLOTS 128  // LDS hash tables: node -> prior entry / picks (<= 32 keys each)
+struct PickTab {        // nodes picked by the window's pods under one iteration's S
+  int32_t node[KSG_HSLOTS];  // -1 empty
+  int32_t first[KSG_HSLOTS], last[KSG_HSLOTS], cnt[KSG_HSLOTS];
+};
+struct WinLDS {
+  uint64_t key[KSG_BATCH][KSG_CAND];    // candidate keys (sorted, 0 = none)
+  RowV row[KSG_BATCH][KSG_STAGE];       // rows of candidate ranks < KSG_STAGE
+  Pend prior[KSG_BATCH];                // P_{W-1}
   PodLite pod[KSG_BATCH];
-  Patch patch[KSG_BATCH * KSG_CAND];    // [pod][lane a]
+  PatchV patch[KSG_BATCH][KSG_CAND];    // [pod][prior e | 32 + pick a]
+  uint64_t pkey[KSG_BATCH][KSG_BATCH];  // key of pod b on prior node e as of the window start
+  int8_t pdf[KSG_BATCH][KSG_BATCH];     // its feasible-count change vs the snapshot
+  uint64_t pmask[KSG_BATCH];            // bit i: candidate i of pod b is a prior node
+  uint64_t pbest[KSG_BATCH];
+  int32_t pbest_e[KSG_BATCH];
+  int32_t S[3][KSG_BATCH];              // picks (global node, -1 none), rotating buffers
+  int32_t O[3][KSG_BATCH];              // pick origins: prior e (< 32) or 64 + pod*64 + rank
+  int32_t feas[KSG_BATCH];              // snapshot feasible counts
   SumLite sum[KSG_BATCH];
-  Delta cum[2][KSG_BATCH];              // sum over pods <= a selecting sel[a]
-  int32_t sel[2][KSG_BATCH];            // selected global node, -1 none (iteration parity)
-  int32_t srow[2][KSG_BATCH];           // index into cand[] of a row of that node
-  int32_t nxt[2][KSG_BATCH];            // next pod selecting the same node, KSG_BATCH none
-  int32_t prv[KSG_BATCH];
-  int32_t feas[KSG_BATCH];
-  uint32_t taken[128];                  // initial guess: hashed bitmap of taken nodes
-  int32_t stable;
+  int32_t ptn[KSG_HSLOTS], pte[KSG_HSLOTS];  // prior node -> entry
+  int32_t gtn[KSG_HSLOTS], gtf[KSG_HSLOTS];  // guess rounds: node -> smallest proposer
+  PickTab pick[3];                      // per S buffer
 };
 
-// Chains of pods per selected node for parity p (one wave; lanes 0..31 = pods).
-__device__ __forceinline__ void fixup_prep(FixupLDS& L, int p, uint32_t nb, uint32_t R, int lane) {
-  int a = lane & (KSG_BATCH - 1);
-  int32_t s = (a < (int)nb) ? L.sel[p][a] : -1;
-  int prv = -1;
-#pragma unroll
-  for (int j = 0; j < KSG_BATCH; ++j) {
-    int32_t sj = __builtin_amdgcn_readlane(s, j);
-    prv = (j < a && sj == s) ? j : prv;
+__device__ __forceinline__ uint32_t hslot(int32_t node) { return ((uint32_t)node * 2654435761u) >> 25; }
+__device__ __forceinline__ int prior_of(const WinLDS& L, int32_t x) {
+  uint32_t h = hslot(x);
+  for (int k = 0; k < KSG_HSLOTS; ++k) {
+    int32_t v = L.ptn[h];
+    if (v == x) return L.pte[h];
+    if (v == -1) return -1;
+    h = (h + 1) & (KSG_HSLOTS - 1);
   }
-  if (s < 0) prv = -1;
-  if (lane < KSG_BATCH) {
-    L.prv[a] = prv;
-    L.nxt[p][a] = KSG_BATCH;
+  return -1;
+}
+// slot of node x in an open-addressing table (inserting it when absent)
+__device__ __forceinline__ uint32_t tab_claim(int32_t* nodes, int32_t x) {
+  uint32_t h = hslot(x);
+  for (int k = 0; k < KSG_HSLOTS; ++k) {
+    int32_t old = atomicCAS(&nodes[h], -1, x);
+    if (old == -1 || old == x) return h;
+    h = (h + 1) & (KSG_HSLOTS - 1);
   }
-  if (lane < KSG_BATCH && prv >= 0) L.nxt[p][prv] = a;  // after the init: LDS ops of a wave are in order
-  if (lane < KSG_BATCH) {
-    Delta d;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) d.req[k] = 0;
-    d.nzc = d.nzm = 0;
-    d.pods = d.pad = 0;
-    for (int j = s >= 0 ? a : -1; j >= 0; j = L.prv[j]) {
-      const PodLite& q = L.pod[j];
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k)
-        if (k < R) d.req[k] += q.req[k];
-      d.nzc += q.nz_cpu;
-      d.nzm += q.nz_mem;
-      d.pods += 1;
-    }
-    L.cum[p][a] = d;
+  return 0;  // unreachable: <= 64 keys in 128 slots
+}
+__device__ __forceinline__ int tab_find(const int32_t* nodes, int32_t x) {
+  uint32_t h = hslot(x);
+  for (int k = 0; k < KSG_HSLOTS; ++k) {
+    int32_t v = nodes[h];
+    if (v == x) return (int)h;
+    if (v == -1) return -1;
+    h = (h + 1) & (KSG_HSLOTS - 1);
   }
+  return -1;
+}
+__device__ __forceinline__ void pick_insert(PickTab& T, int32_t x, int b) {
+  uint32_t h = tab_claim(T.node, x);
+  atomicMin(&T.first[h], b);
+  atomicMax(&T.last[h], b);
+  atomicAdd(&T.cnt[h], 1);
+}
+__device__ __forceinline__ void pick_clear(PickTab& T, int i) {  // i < KSG_HSLOTS
+  T.node[i] = -1;
+  T.first[i] = KSG_BATCH;
+  T.last[i] = -1;
+  T.cnt[i] = 0;
+}
+// first pod picking node x under T (KSG_BATCH: none)
+__device__ __forceinline__ int first_pick(const PickTab& T, int32_t x) {
+  int h = x >= 0 ? tab_find(T.node, x) : -1;
+  return h >= 0 ? T.first[h] : KSG_BATCH;
 }
 
-#define KSG_FIXUP_THREADS 1024
-#define KSG_FIXUP_WAVES (KSG_FIXUP_THREADS / 64)
+__device__ __forceinline__ void origin_rows(const WinLDS& L, const WinArgs& A, int32_t o, RowV& start, RowV& snap) {
+  if (o < KSG_BATCH) {
+    start = L.prior[o].after;
+    snap = L.prior[o].base;
+  } else {
+    int p = (o - 64) >> 6, i = (o - 64) & 63;
+    if (i < KSG_STAGE) start = L.row[p][i];
+    else start = reinterpret_cast<const CandRow*>(A.wrec + KSG_XHDR)[p * KSG_CAND + i].r;
+    snap = start;
+  }
+}
+__device__ __forceinline__ void delta_of(const PodLite& p, Delta& d) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d.req[k] = p.req[k];
+  d.nzc = p.nz_cpu;
+  d.nzm = p.nz_mem;
+  d.pods = 1;
+}
+__device__ __forceinline__ void delta_add(Delta& d, const PodLite& p) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d.req[k] += p.req[k];
+  d.nzc += p.nz_cpu;
+  d.nzm += p.nz_mem;
+  d.pods += 1;
+}
+__device__ __forceinline__ void apply_delta(RowV& r, const Delta& d, uint32_t R) {
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k)
+    if (k < R) r.req[k] += d.req[k];
+  r.nzc += d.nzc;
+  r.nzm += d.nzm;
+  r.podcnt += d.pods;
+}
+// Requests of the picks of node S[a] by pods <= a, and the next pod after a picking it.
+__device__ __forceinline__ void pick_chain(const WinLDS& L, const int32_t* S, int a, int32_t x, Delta& cum, int& nx) {
+  cum = Delta{};
+  nx = KSG_BATCH;
+  for (int j = 0; j < KSG_BATCH; ++j)
+    if (S[j] == x) {
+      if (j <= a) delta_add(cum, L.pod[j]);
+      else if (nx == KSG_BATCH) nx = j;
+    }
+}
+__device__ __forceinline__ uint64_t max3u(uint64_t a, uint64_t b, uint64_t c) {
+  uint64_t m = a > b ? a : b;
+  return m > c ? m : c;
+}
+
 template <int MODE>
-__global__ __launch_bounds__(KSG_FIXUP_THREADS) void k_batch_fixup(DevCluster C, DevProfile F, BatchOut BO, const uint8_t* progs,
-                                                     const uint64_t* prog_off, uint32_t j0, uint32_t nb,
-                                                     const CandRow* cand, int32_t* feas, ksg_pod_summary* sums,
-                                                     uint64_t* stamps) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-  FixupLDS& L = *reinterpret_cast<FixupLDS*>(lds_raw);
-  int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+__device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile& F, const WinArgs& A, WinLDS& L) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = (int)A.nw;
+  const uint32_t R = C.R < 4 ? C.R : 4;
 #define STAMP(k)                                        \
-  if (stamps && tid == 0) {                             \
+  if (A.stamps && tid == 0) {                           \
     __builtin_amdgcn_sched_barrier(0);                  \
-    stamps[k] = __builtin_amdgcn_s_memtime();           \
+    A.stamps[k] = __builtin_amdgcn_s_memtime();         \
     __builtin_amdgcn_sched_barrier(0);                  \
   }
   STAMP(0);
-  {  // stage: candidates (6 independent 16-B loads in flight per thread), pods, counts
-    const uint4* src = reinterpret_cast<const uint4*>(cand);
-    uint4* dst = reinterpret_cast<uint4*>(L.cand);
-    constexpr uint32_t kRow16 = (uint32_t)(sizeof(CandRow) / 16);
-    uint32_t n16 = nb * KSG_CAND * kRow16;
-    uint4 v[kRow16];
-#pragma unroll
-    for (uint32_t k = 0; k < kRow16; ++k) {  // clamped, unconditional loads: v stays in registers
-      uint32_t i = tid + k * KSG_FIXUP_THREADS;
-      v[k] = src[i < n16 ? i : 0];
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kRow16; ++k) {
-      uint32_t i = tid + k * KSG_FIXUP_THREADS;
-      if (i < n16) dst[i] = v[k];
-    }
-    for (uint32_t b = tid; b < nb; b += blockDim.x) {
-      const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[j0 + b]);
-      PodLite& q = L.pod[b];
+  if (A.stamps && tid == 0) A.stamps[11] = __builtin_amdgcn_s_memrealtime();
+  const int np = *A.pprev_n;
+  // ---- stage.  The small inputs (P_{W-1}, pods, counts) are loaded first and
+  // stored at once; the candidate keys and rows stay in flight in registers
+  // across the prior-node evaluations (vmcnt is in order) and land after them.
+  constexpr int kRowW = (int)(sizeof(RowV) / 8), kCandW = (int)(sizeof(CandRow) / 8), kPendW = (int)(sizeof(Pend) / 8);
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(A.wrec + KSG_XHDR);
+  const int nk = nb * KSG_CAND, nr = nb * KSG_STAGE * kRowW;
+  uint64_t kv[2], rv[6];
+  {
+    const uint64_t pv = tid < np * kPendW ? reinterpret_cast<const uint64_t*>(A.pprev)[tid] : 0;
+    if (tid < nb) {
+      const ksg_prog* h = reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[A.w0 + tid]);
+      PodLite& q = L.pod[tid];
 #pragma unroll
       for (int k = 0; k < 4; ++k) q.req[k] = h->req[k];
 #pragma unroll
@@ -1484,106 +1549,227 @@ __global__ __launch_bounds__(KSG_FIXUP_THREADS) void k_batch_fixup(DevCluster C,
       q.nz_mem = h->nz_mem;
       q.queue_idx = h->queue_idx;
       q.flags = h->flags;
-      L.feas[b] = feas[b];
+      L.feas[tid] = reinterpret_cast<const int32_t*>(A.wrec)[tid];
     }
-    if (tid < 128) L.taken[tid] = 0;
-    if (tid == 0) L.stable = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      int i = tid + k * KSG_WIN_THREADS;
+      kv[k] = i < nk ? src[(size_t)i * kCandW] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      int i = tid + k * KSG_WIN_THREADS;
+      int row = i / kRowW, wd = i - row * kRowW;
+      int p = row / KSG_STAGE, r = row - p * KSG_STAGE;
+      rv[k] = i < nr ? src[(size_t)(p * KSG_CAND + r) * kCandW + 1 + wd] : 0;
+    }
+    if (tid < np * kPendW) reinterpret_cast<uint64_t*>(L.prior)[tid] = pv;
+    if (tid < 3 * KSG_BATCH) {
+      (&L.S[0][0])[tid] = -1;
+      (&L.O[0][0])[tid] = -1;
+    }
+    if (tid < KSG_HSLOTS) {
+      L.ptn[tid] = -1;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) pick_clear(L.pick[t], tid);
+    }
   }
-  __syncthreads();
+  lds_barrier();
   STAMP(1);
-  uint32_t R = C.R < 4 ? C.R : 4;
-  if (wave == 0) {  // initial guess: each pod takes its best candidate no earlier pod took
-    for (uint32_t b = 0; b < nb; ++b) {
-      uint64_t k = lane < KSG_CAND ? L.cand[b * KSG_CAND + lane].key : 0;
-      uint32_t node = (uint32_t)(k & 0xFFFFFull);
-      uint32_t hb = (node * 2654435761u) >> 20;
-      bool ok = k != 0 && !((L.taken[hb >> 5] >> (hb & 31)) & 1u);
-      unsigned long long m = __ballot(ok), v = __ballot(k != 0);
-      int g = m ? __ffsll((long long)m) - 1 : (v ? 0 : -1);
-      if (lane == g) {
-        L.sel[0][b] = (int32_t)node;
-        L.srow[0][b] = (int32_t)(b * KSG_CAND + g);
-        atomicOr(&L.taken[hb >> 5], 1u << (hb & 31));
+  if (tid < np) {  // P_{W-1}: index it, write it back (the eval blocks read those rows from the list)
+    const Pend& pe = L.prior[tid];
+    uint32_t h = tab_claim(L.ptn, pe.node);
+    L.pte[h] = tid;
+    uint32_t nl = (uint32_t)pe.node - C.goff;
+    if ((uint32_t)pe.node >= C.goff && nl < C.N) store_row(C, nl, pe.after);
+  }
+  {  // pods on the P_{W-1} nodes as of the window start (independent of the picks)
+    const int pb = 2 * wave + (lane >> 5), e = lane & 31;
+    uint64_t k = 0;
+    if (pb < nb && e < np) {
+      const Pend& pe = L.prior[e];
+      const PodLite* h = &L.pod[pb];
+      int32_t fs, bs;
+      int64_t tot;
+      uint32_t code = eval_row<MODE>(pe.after, F, h, R, fs, bs, tot);
+      bool snap_ok = F.pos_fit < 0 || fit_filter_row(pe.base, h, R) == 0;
+      PatchV pt;
+      pt.code = code;
+      pt.fit = fs;
+      pt.ba = bs;
+      pt.total = (int32_t)tot;
+      L.patch[pb][e] = pt;
+      k = code == KSG_FILTER_PASS ? pack_key(tot, F.seed, h->queue_idx, (uint32_t)pe.node) : 0;
+      L.pkey[pb][e] = k;
+      L.pdf[pb][e] = (int8_t)((code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0));
+    }
+    STAMP(16);
+    // best prior node per pod: reduce within each half (DPP row ops stay inside 32 lanes
+    // only up to 16; finish with one cross-half step)
+    uint64_t k0 = wave_max(lane < 32 ? k : (uint64_t)0), k1 = wave_max(lane >= 32 ? k : (uint64_t)0);
+    unsigned long long m0 = __ballot(k0 && lane < 32 && k == k0), m1 = __ballot(k1 && lane >= 32 && k == k1);
+    if (lane == 0) {
+      if (2 * wave < nb) {
+        L.pbest[2 * wave] = k0;
+        L.pbest_e[2 * wave] = m0 ? __ffsll((long long)m0) - 1 : -1;
       }
-      if (g < 0 && lane == 0) {
-        L.sel[0][b] = -1;
-        L.srow[0][b] = 0;
+      if (2 * wave + 1 < nb) {
+        L.pbest[2 * wave + 1] = k1;
+        L.pbest_e[2 * wave + 1] = m1 ? __ffsll((long long)m1) - 1 - 32 : -1;
       }
     }
-    if (lane >= (int)nb && lane < KSG_BATCH) L.sel[0][lane] = L.sel[1][lane] = -1;
-    fixup_prep(L, 0, nb, R, lane);
   }
-  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    int i = tid + k * KSG_WIN_THREADS;
+    if (i < nk) (&L.key[0][0])[i] = kv[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    int i = tid + k * KSG_WIN_THREADS;
+    if (i < nr) reinterpret_cast<uint64_t*>(&L.row[0][0])[i] = rv[k];
+  }
+  lds_barrier();
+  STAMP(17);
+#pragma unroll 1
+  for (int hh = 0; hh < 2; ++hh) {  // candidates that are P_{W-1} nodes
+    int b = 2 * wave + hh;
+    if (b >= nb) break;
+    uint64_t ck = L.key[b][lane];
+    bool m = ck != 0 && np > 0 && prior_of(L, (int32_t)(ck & 0xFFFFFull)) >= 0;
+    unsigned long long mask = __ballot(m);
+    if (lane == 0) L.pmask[b] = mask;
+  }
+  lds_barrier();
   STAMP(2);
-  int p = 0;
+  if (wave == 0) {  // starting guess: serial dictatorship over (candidates, P_{W-1} nodes), parallel rounds
+    const int b = lane;
+    const bool valid = b < nb;
+    const uint64_t pm = valid ? L.pmask[b] : 0;
+    const uint64_t pbk = valid ? L.pbest[b] : 0;
+    int r = 0;
+    bool pok = pbk != 0;
+    int32_t node = -1, org = -1;
+#pragma unroll 1
+    for (int round = 0; round < 64; ++round) {
+      uint64_t ck = 0;
+      if (valid) {
+        uint64_t free_ = ~pm & (r < 64 ? (~0ull << r) : 0ull);
+        r = free_ ? __ffsll((long long)free_) - 1 : KSG_CAND;
+        ck = r < KSG_CAND ? L.key[b][r] : 0;
+      }
+      uint64_t pk = pok ? pbk : 0;
+      uint64_t best = ck > pk ? ck : pk;
+      bool from_c = best != 0 && best == ck;
+      node = best ? (int32_t)(best & 0xFFFFFull) : -1;
+      org = !best ? -1 : from_c ? 64 + b * 64 + r : L.pbest_e[b];
+      // smallest proposer per node
+      L.gtn[lane] = -1;
+      L.gtn[lane + 64] = -1;
+      uint32_t h = 0;
+      if (node >= 0) {
+        h = tab_claim(L.gtn, node);
+        L.gtf[h] = KSG_BATCH;
+      }
+      if (node >= 0) atomicMin(&L.gtf[h], b);
+      bool lose = node >= 0 && L.gtf[h] < b;
+      if (__ballot(lose) == 0) break;
+      if (lose) {
+        if (from_c) ++r;
+        else pok = false;
+      }
+    }
+    if (valid) {
+      L.S[0][b] = node;
+      L.O[0][b] = org;
+      if (node >= 0) pick_insert(L.pick[0], node, b);
+    }
+  }
+  lds_barrier();
+  STAMP(3);
+  int cur = 0, stable = 0;
   uint32_t iters = 0;
+#pragma unroll 1
   for (;;) {
-    int stable = L.stable;
-    for (uint32_t b = wave; b < nb; b += KSG_FIXUP_WAVES) {
-      if ((int)b < stable) {  // final: carry the selection over
+    const int nxt = cur == 2 ? 0 : cur + 1;
+    if (tid < KSG_HSLOTS) pick_clear(L.pick[nxt == 2 ? 0 : nxt + 1], tid);
+    const PickTab& T = L.pick[cur];
+    const int a = lane & 31;
+    const int32_t Sv = L.S[cur][a], Ov = L.O[cur][a];
+    const int p0 = 2 * wave;
+    // pods p0 (lanes 0..31) and p0 + 1 (lanes 32..63) re-evaluate the picks a < pod
+    const int pb = p0 + (lane >> 5);
+    const bool live = pb < nb && pb >= stable;
+    uint64_t ke = 0;
+    int dfe = 0;
+    if (__ballot(live)) {
+      int nx = KSG_BATCH;
+      Delta cum;
+      delta_of(L.pod[a], cum);
+      if (Sv >= 0) {
+        int h = tab_find(T.node, Sv);
+        if (T.cnt[h] > 1) pick_chain(L, L.S[cur], a, Sv, cum, nx);  // node picked twice (rare)
+      }
+      if (live) {
+        PatchV pt;
+        pt.code = KSG_NOT_PATCHED;
+        pt.fit = pt.ba = pt.total = 0;
+        if (Sv >= 0 && a < pb && nx >= pb) {
+          RowV cur_r, snap;
+          origin_rows(L, A, Ov, cur_r, snap);
+          apply_delta(cur_r, cum, R);
+          const PodLite* h = &L.pod[pb];
+          int32_t fs, bs;
+          int64_t tot;
+          uint32_t code = eval_row<MODE>(cur_r, F, h, R, fs, bs, tot);
+          bool snap_ok = F.pos_fit < 0 || fit_filter_row(snap, h, R) == 0;
+          dfe = (code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0);
+          if (code == KSG_FILTER_PASS) ke = pack_key(tot, F.seed, h->queue_idx, (uint32_t)Sv);
+          pt.code = code;
+          pt.fit = fs;
+          pt.ba = bs;
+          pt.total = (int32_t)tot;
+        }
+        L.patch[pb][32 + a] = pt;
+      }
+    }
+    // first pick of each P_{W-1} node under S (lanes < np), shared by both pods
+    const int pf = lane < np ? first_pick(T, L.prior[lane].node) : -1;
+#pragma unroll 1
+    for (int hh = 0; hh < 2; ++hh) {
+      const int b = p0 + hh;
+      if (b >= nb) break;
+      if (b < stable) {
         if (lane == 0) {
-          L.sel[p ^ 1][b] = L.sel[p][b];
-          L.srow[p ^ 1][b] = L.srow[p][b];
+          int32_t s = L.S[cur][b];
+          L.S[nxt][b] = s;
+          L.O[nxt][b] = L.O[cur][b];
+          if (s >= 0) pick_insert(L.pick[nxt], s, b);
         }
         continue;
       }
-      const PodLite* h = &L.pod[b];
-      int a = lane & (KSG_BATCH - 1);
-      int32_t sv = L.sel[p][a];
-      int32_t rowidx = lane < KSG_BATCH ? L.srow[p][a] : (int32_t)(b * KSG_CAND + a);
-      // candidate lanes: node taken by a pod < b?
-      uint64_t ck = lane >= KSG_BATCH ? L.cand[b * KSG_CAND + a].key : 0;
-      uint32_t cnode = (uint32_t)(ck & 0xFFFFFull);
-      bool modified = false;
-#pragma unroll 1
-      for (uint32_t j = 0; j < b; ++j) modified |= (uint32_t)__builtin_amdgcn_readlane(sv, j) == cnode;
-      uint64_t key = (ck != 0 && !modified) ? ck : 0;
-      int dfeas = 0;
-      if (lane < KSG_BATCH) {
-        Patch pt;
-        pt.node = -1;
-        pt.code = 0;
-        pt.fit = pt.ba = pt.total = 0;
-        if (a < (int)b && sv >= 0 && L.nxt[p][a] >= (int)b) {
-          const CandRow& cr = L.cand[rowidx];
-          const Delta& d = L.cum[p][a];
-          RowV snap, cur;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            snap.alloc[k] = cur.alloc[k] = cr.alloc[k];
-            snap.req[k] = cr.req[k];
-            cur.req[k] = cr.req[k] + d.req[k];
-          }
-          snap.nzc = cr.nzc;
-          snap.nzm = cr.nzm;
-          snap.podcnt = cr.podcnt;
-          snap.allowed = cur.allowed = cr.allowed;
-          cur.nzc = cr.nzc + d.nzc;
-          cur.nzm = cr.nzm + d.nzm;
-          cur.podcnt = cr.podcnt + d.pods;
-          int32_t fit_s, ba_s;
-          int64_t tot;
-          uint32_t code = eval_row<MODE>(cur, F, h, R, fit_s, ba_s, tot);
-          bool snap_ok = F.pos_fit < 0 || fit_filter_row(snap, h, R) == 0;
-          dfeas = (code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0);
-          uint32_t n = (uint32_t)sv - C.goff;
-          pt.node = ((uint32_t)sv >= C.goff && n < C.N) ? (int32_t)n : -1;
-          pt.code = code;
-          pt.fit = fit_s;
-          pt.ba = ba_s;
-          pt.total = (int32_t)tot;
-          if (code == KSG_FILTER_PASS) key = pack_key(tot, F.seed, h->queue_idx, (uint32_t)sv);
-        }
-        L.patch[b * KSG_CAND + a] = pt;
-      }
-      uint64_t best = wave_max(key);
-      int feasible = L.feas[b] + wave_sum(dfeas);
-      int32_t sel = (feasible > 0 && best) ? (int32_t)(best & 0xFFFFFull) : -1;
-      unsigned long long wm = __ballot(best != 0 && key == best);
-      int32_t srow_new = wm ? __builtin_amdgcn_readlane(rowidx, __ffsll((long long)wm) - 1) : 0;
+      const uint64_t ck = L.key[b][lane];
+      const bool mod = ((L.pmask[b] >> lane) & 1) || (ck != 0 && first_pick(T, (int32_t)(ck & 0xFFFFFull)) < b);
+      const bool pact = lane < np && pf >= b;
+      const uint64_t kc = (ck != 0 && !mod) ? ck : 0;
+      const uint64_t kp = pact ? L.pkey[b][lane] : 0;
+      const int dfp = pact ? (int)L.pdf[b][lane] : 0;
+      const bool mine = (lane >> 5) == hh;
+      const uint64_t kr = mine ? ke : 0;
+      const int dfr = mine ? dfe : 0;
+      const uint64_t best = wave_max(max3u(kc, kp, kr));
+      const int feasible = L.feas[b] + wave_sum(dfp + dfr);
+      const int32_t sel = (feasible > 0 && best) ? (int32_t)(best & 0xFFFFFull) : -1;
+      const unsigned long long mc = __ballot(best && kc == best), mp = __ballot(best && kp == best),
+                               mr = __ballot(best && kr == best);
+      int32_t org = -1;
+      if (mc) org = 64 + b * 64 + (__ffsll((long long)mc) - 1);
+      else if (mp) org = __ffsll((long long)mp) - 1;
+      else if (mr) org = __builtin_amdgcn_readlane(Ov, __ffsll((long long)mr) - 1);
       if (lane == 0) {
-        L.sel[p ^ 1][b] = sel;
-        L.srow[p ^ 1][b] = srow_new;
+        L.S[nxt][b] = sel;
+        L.O[nxt][b] = sel >= 0 ? org : -1;
+        if (sel >= 0) pick_insert(L.pick[nxt], sel, b);
         SumLite& sm = L.sum[b];
         sm.best_key = sel >= 0 ? (feasible == 1 ? (best & 0xFFFFFFFFFFull) : best) : 0;
         sm.selected = sel;
@@ -1591,53 +1777,129 @@ __global__ __launch_bounds__(KSG_FIXUP_THREADS) void k_batch_fixup(DevCluster C,
         sm.status = sel >= 0 ? 0 : 1;
       }
     }
-    __syncthreads();
-    if (wave == 0) {
-      int a = lane & (KSG_BATCH - 1);
-      bool changed = lane < (int)nb && lane >= stable && L.sel[p ^ 1][a] != L.sel[p][a];
-      unsigned long long m = __ballot(changed);
-      fixup_prep(L, p ^ 1, nb, R, lane);
-      if (lane == 0) L.stable = m ? (int)min((uint32_t)(__ffsll((long long)m)), nb) : (int)nb;
-    }
-    __syncthreads();
-    p ^= 1;
+    lds_barrier();
+    if (iters < 2) STAMP(19 + iters);
     ++iters;
-    if (L.stable >= (int)nb) break;
-  }
-  STAMP(3);
-  if (stamps && tid == 0) stamps[4] = iters;
-  // flush: summaries, patches, final node rows
-  for (uint32_t b = tid; b < nb; b += blockDim.x) {
-    ksg_pod_summary& d = sums[j0 + b];
-    d.best_key = L.sum[b].best_key;
-    d.selected = L.sum[b].selected;
-    d.feasible = L.sum[b].feasible;
-    d.status = L.sum[b].status;
-  }
-  for (uint32_t i = tid; i < nb * KSG_CAND; i += blockDim.x) {
-    const Patch& pt = L.patch[i];
-    if (pt.node < 0) continue;
-    uint32_t* of;
-    int32_t *os, *ot;
-    out_ptrs(BO, i / KSG_CAND, C.N, of, os, ot);
-    write_pair(F, of, os, ot, C.N, (uint32_t)pt.node, pt.code, pt.fit, pt.ba, pt.total);
-  }
-  if (tid < (int)nb) {
-    int32_t s = L.sel[p][tid];
-    uint32_t n = (uint32_t)s - C.goff;
-    if (s >= 0 && L.nxt[p][tid] == KSG_BATCH && (uint32_t)s >= C.goff && n < C.N) {
-      const CandRow& cr = L.cand[L.srow[p][tid]];
-      const Delta& d = L.cum[p][tid];
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k)
-        if (k < R) C.req[(size_t)k * C.N + n] = cr.req[k] + d.req[k];
-      C.nzc[n] = cr.nzc + d.nzc;
-      C.nzm[n] = cr.nzm + d.nzm;
-      C.podcnt[n] = cr.podcnt + d.pods;
+    {  // every wave derives the same stable prefix
+      const int32_t so = L.S[cur][lane & 31], sn = L.S[nxt][lane & 31];
+      unsigned long long m = __ballot(lane < nb && lane >= stable && sn != so);
+      stable = m ? min(__ffsll((long long)m), nb) : nb;
     }
+    cur = nxt;
+    if (stable >= nb) break;
+  }
+  STAMP(4);
+  if (A.stamps && tid == 0) A.stamps[7] = iters;
+  // ---- flush: summaries, per-pair patches, P_W
+  const PickTab& T = L.pick[cur];
+  if (tid < nb) {
+    ksg_pod_summary& d = A.sums[A.w0 + tid];
+    d.best_key = L.sum[tid].best_key;
+    d.selected = L.sum[tid].selected;
+    d.feasible = L.sum[tid].feasible;
+    d.status = L.sum[tid].status;
+  }
+  {
+    const int32_t Sv = L.S[cur][lane & 31];
+    const int32_t pn = lane < np ? L.prior[lane].node : -1;
+    const int pf = lane < np ? first_pick(T, pn) : -1;
+#pragma unroll 1
+    for (int hh = 0; hh < 2; ++hh) {
+      const int b = 2 * wave + hh;
+      if (b >= nb) break;
+      const PatchV pt = L.patch[b][lane];
+      const bool wr = lane < 32 ? (lane < np && pf >= b) : pt.code != KSG_NOT_PATCHED;
+      const int32_t node = lane < 32 ? pn : Sv;
+      const uint32_t nl = (uint32_t)node - C.goff;
+      if (wr && node >= 0 && (uint32_t)node >= C.goff && nl < C.N) {
+        uint32_t* of;
+        int32_t *os, *ot;
+        out_ptrs(A, A.w0 + b, C.N, of, os, ot);
+        write_pair(F, of, os, ot, C.N, nl, pt.code, pt.fit, pt.ba, pt.total);
+      }
+    }
+  }
+  if (wave == 0) {  // P_W: each node picked in the window, by its last pick
+    const int a = lane;
+    const int32_t Sv = a < nb ? L.S[cur][a] : -1;
+    int h = Sv >= 0 ? tab_find(T.node, Sv) : -1;
+    const bool last = h >= 0 && T.last[h] == a;
+    unsigned long long m = __ballot(last);
+    if (last) {
+      Delta cum;
+      delta_of(L.pod[a], cum);
+      int nx;
+      if (T.cnt[h] > 1) pick_chain(L, L.S[cur], a, Sv, cum, nx);
+      RowV st, snap;
+      origin_rows(L, A, L.O[cur][a], st, snap);
+      Pend p;
+      p.node = Sv;
+      p.pad = 0;
+      p.base = st;
+      apply_delta(st, cum, R);
+      p.after = st;
+      A.pnext[__popcll(m & ((1ull << a) - 1))] = p;
+    }
+    if (lane == 0) *A.pnext_n = __popcll(m);
   }
   STAMP(5);
+  if (A.stamps && tid == 0) A.stamps[12] = __builtin_amdgcn_s_memrealtime();
 #undef STAMP
+}
+
+template <int MODE>
+__global__ __launch_bounds__(KSG_WIN_THREADS) void k_window(DevCluster C, DevProfile F, WinArgs A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  if (blockIdx.x == 0) {
+    if (A.nw) win_fixup<MODE>(C, F, A, *reinterpret_cast<WinLDS*>(lds_raw));
+    return;
+  }
+  win_eval<MODE>(C, F, A, blockIdx.x - 1, reinterpret_cast<uint64_t*>(lds_raw));
+}
+
+// After the last window: write its pending rows back.
+__global__ void k_apply_pend(DevCluster C, const Pend* p, const int32_t* pn) {
+  int e = threadIdx.x;
+  if (e >= *pn) return;
+  uint32_t nl = (uint32_t)p[e].node - C.goff;
+  if ((uint32_t)p[e].node >= C.goff && nl < C.N) store_row(C, nl, p[e].after);
+}
+
+// Sharded windows: every rank's record (feasible counts + its top-KSG_CAND
+// candidates per pod, rows included) is all-gathered; one wave per pod merges
+// the R sorted lists into the global top-KSG_CAND and sums the counts.
+__global__ __launch_bounds__(64) void k_window_gmerge(const uint8_t* recv, uint32_t ranks, uint8_t* out) {
+  __shared__ uint64_t keys[8 * KSG_CAND];
+  const uint32_t b = blockIdx.x;
+  const int lane = threadIdx.x;
+  for (uint32_t r = 0; r < ranks; ++r)
+    keys[r * KSG_CAND + lane] =
+        reinterpret_cast<const CandRow*>(recv + r * kRecBytes + KSG_XHDR)[(size_t)b * KSG_CAND + lane].key;
+  __syncthreads();
+  uint64_t v = keys[lane];
+  for (uint32_t r = 1; r < ranks; ++r) v = wave_merge_top(v, keys[r * KSG_CAND + 63 - lane]);
+  int32_t f = 0;
+  for (uint32_t r = 0; r < ranks; ++r) f += reinterpret_cast<const int32_t*>(recv + r * kRecBytes)[b];
+  CandRow c;
+  memset(&c, 0, sizeof(c));
+  if (v) {  // find the source entry: each rank's list is sorted descending
+    for (uint32_t r = 0; r < ranks; ++r) {
+      int lo = 0, hi = KSG_CAND - 1, at = -1;
+      while (lo <= hi) {
+        int mid = (lo + hi) >> 1;
+        uint64_t k = keys[r * KSG_CAND + mid];
+        if (k == v) { at = mid; break; }
+        if (k > v) lo = mid + 1;
+        else hi = mid - 1;
+      }
+      if (at >= 0) {
+        c = reinterpret_cast<const CandRow*>(recv + r * kRecBytes + KSG_XHDR)[(size_t)b * KSG_CAND + at];
+        break;
+      }
+    }
+  }
+  reinterpret_cast<CandRow*>(out + KSG_XHDR)[(size_t)b * KSG_CAND + lane] = c;
+  if (lane == 0) reinterpret_cast<int32_t*>(out)[b] = f;
 }
 
 // ----------------------------------------------------------------- host side
@@ -1682,7 +1944,6 @@ struct Engine::Impl {
   void* xuser = nullptr;
   DBuf<uint8_t> xsend, xrecv;
   std::vector<uint8_t> hsend, hrecv;
-  DBuf<int32_t> gfeas;
   DevProfile F{};
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -1721,8 +1982,10 @@ struct Engine::Impl {
   // speculative batch path
   bool batch_ok = false;
   DBuf<uint64_t> tile_top;
-  DBuf<int32_t> bfeas, tfeas;
-  DBuf<CandRow> cand;
+  DBuf<int32_t> tfeas, pend_n;
+  DBuf<uint32_t> arrive;
+  DBuf<uint8_t> wrec;     // candidate records of two windows (kRecBytes each)
+  DBuf<Pend> pend;        // pending rows P_j of two windows
   DBuf<uint32_t> bfilter;
   DBuf<int32_t> bscore, btotal;
   std::vector<size_t> prog_off;
@@ -1733,8 +1996,6 @@ struct Engine::Impl {
   DBuf<int32_t> fit_res_d, ba_res_d;
   DBuf<int64_t> fit_w_d;
   bool stamps_on = false;  // diagnostic: s_memtime stamps in the fixup loop
-  bool estamps_on = false; // diagnostic: stamps per wave of k_batch_eval (last batch wins)
-  DBuf<uint64_t> estamps;
   DBuf<uint64_t> stamps;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0;
@@ -1921,29 +2182,32 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     return false;
   HIPCHK(hipMemsetAsync(I.exist_any.p, 0, 4, s));
   if (I.batch_ok && I.R <= 4) {
-    uint32_t T = (I.N + kBlock - 1) / kBlock;
+    uint32_t T = std::max<uint32_t>((I.N + KSG_TILE - 1) / KSG_TILE, 1);
     size_t Nn = std::max<uint32_t>(I.N, 1);
-    if (!I.tile_top.alloc((size_t)KSG_BATCH * std::max<uint32_t>(T, 1) * KSG_TOPK, err) ||
-        !I.bfeas.alloc(KSG_BATCH, err) || !I.tfeas.alloc((size_t)KSG_BATCH * std::max<uint32_t>(T, 1), err) ||
-        !I.cand.alloc((size_t)KSG_BATCH * KSG_CAND, err) ||
-        !I.bfilter.alloc(Nn * KSG_BATCH, err) || !I.bscore.alloc(Nn * KSG_BATCH * KSG_MAX_PLUGINS, err) ||
-        !I.btotal.alloc(Nn * KSG_BATCH, err))
+    if (!I.tile_top.alloc((size_t)KSG_BATCH * T * KSG_TOPK, err) || !I.tfeas.alloc((size_t)KSG_BATCH * T, err) ||
+        !I.arrive.alloc(KSG_BATCH, err) || !I.pend_n.alloc(2, err) || !I.wrec.alloc(2 * kRecBytes, err) ||
+        !I.pend.alloc(2 * KSG_BATCH, err) || !I.bfilter.alloc(Nn * 2 * KSG_BATCH, err) ||
+        !I.bscore.alloc(Nn * 2 * KSG_BATCH * KSG_MAX_PLUGINS, err) || !I.btotal.alloc(Nn * 2 * KSG_BATCH, err))
       return false;
-    HIPCHK(hipMemsetAsync(I.bfeas.p, 0, KSG_BATCH * 4, s));
+    HIPCHK(hipMemsetAsync(I.arrive.p, 0, KSG_BATCH * 4, s));
+    HIPCHK(hipMemsetAsync(I.pend_n.p, 0, 2 * 4, s));
+    HIPCHK(hipMemsetAsync(I.wrec.p, 0, 2 * kRecBytes, s));
   }
   HIPCHK(hipStreamSynchronize(s));
   return true;
 }
 
-// Speculative batches of KSG_BATCH pods (see k_batch_eval); batches never
-// straddle the kept-output window so each batch writes one output region.
+// Windows of KSG_BATCH pods, one k_window launch each (see the kernel): launch
+// j evaluates window j+1 and replays window j; the sharded path all-gathers
+// each window's candidate records between launches.
 static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::string& err) {
   if (I.R > 4) { err = "batch path supports at most 4 resource columns"; return false; }
   hipStream_t s = I.stream;
   DevCluster C = I.cluster();
-  uint32_t T = (I.N + kBlock - 1) / kBlock;
+  const uint32_t T = std::max<uint32_t>((I.N + KSG_TILE - 1) / KSG_TILE, 1);
+  const uint32_t nwin = (count + KSG_BATCH - 1) / KSG_BATCH;
   if (I.sample_every) {
-    size_t need = 2 * ((count + KSG_BATCH - 1) / KSG_BATCH + 2);
+    size_t need = 2 * (nwin + 2);
     while (I.sev.size() < need) {
       hipEvent_t e;
       HIPCHK(hipEventCreate(&e));
@@ -1953,67 +2217,76 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   I.n_samples = 0;
   static bool attr = false;
   if (!attr) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_batch_fixup<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)sizeof(FixupLDS)));
-    HIPCHK(hipFuncSetAttribute((const void*)k_batch_fixup<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)sizeof(FixupLDS)));
+    HIPCHK(hipFuncSetAttribute((const void*)k_window<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLDS)));
+    HIPCHK(hipFuncSetAttribute((const void*)k_window<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLDS)));
     attr = true;
   }
   HIPCHK(hipEventRecord(I.ev0, s));
-  uint32_t end = first + count, j0 = first;
-  while (j0 < end) {
-    uint32_t j1 = std::min(end, j0 + KSG_BATCH);
-    uint32_t kf = I.keep_first, ke = I.keep_first + I.keep_n;
-    bool kept = I.keep_n && j0 >= kf && j0 < ke;
-    if (kept) j1 = std::min(j1, ke);
-    else if (I.keep_n && j0 < kf && j1 > kf) j1 = kf;
-    uint32_t nb = j1 - j0;
-    BatchOut BO;
-    if (kept) {
-      BO.filter = I.kfilter.p; BO.score = I.kscore.p; BO.total = I.ktotal.p; BO.slot0 = j0 - kf; BO.kept = 1;
-    } else {
-      BO.filter = I.bfilter.p; BO.score = I.bscore.p; BO.total = I.btotal.p; BO.slot0 = 0; BO.kept = 0;
+  HIPCHK(hipMemsetAsync(I.pend_n.p, 0, 2 * sizeof(int32_t), s));
+  WinArgs A{};
+  A.progs = I.progs.p;
+  A.prog_off = I.prog_off_d.p;
+  A.first = first;
+  A.keep_first = I.keep_first;
+  A.keep_n = I.keep_n;
+  A.need_eph = I.any_eph_req ? 1u : 0u;
+  A.kfilter = I.kfilter.p; A.kscore = I.kscore.p; A.ktotal = I.ktotal.p;
+  A.sfilter = I.bfilter.p; A.sscore = I.bscore.p; A.stotal = I.btotal.p;
+  A.T = T;
+  A.tile_top = I.tile_top.p;
+  A.tile_feas = I.tfeas.p;
+  A.arrive = I.arrive.p;
+  A.sums = I.sums.p;
+  const bool sharded = I.xranks > 1;
+  for (int64_t j = -1; j < (int64_t)nwin; ++j) {
+    const int64_t E = j + 1, W = j;
+    A.ne = 0;
+    A.nw = 0;
+    A.stamps = A.estamps = nullptr;
+    if (E < (int64_t)nwin) {
+      A.estamps = I.stamps_on ? I.stamps.p + (size_t)E * 24 : nullptr;
+      A.e0 = first + (uint32_t)E * KSG_BATCH;
+      A.ne = std::min<uint32_t>(KSG_BATCH, first + count - A.e0);
+      A.erec = sharded ? I.xsend.p : I.wrec.p + (size_t)(E & 1) * kRecBytes;
     }
-    bool sampled = I.sample_every && I.n_samples * 2 + 2 <= I.sev.size();
+    if (W >= 0) {
+      A.w0 = first + (uint32_t)W * KSG_BATCH;
+      A.nw = std::min<uint32_t>(KSG_BATCH, first + count - A.w0);
+      A.wrec = I.wrec.p + (size_t)(W & 1) * kRecBytes;
+      A.pnext = I.pend.p + (size_t)(W & 1) * KSG_BATCH;
+      A.pnext_n = I.pend_n.p + (W & 1);
+      A.stamps = I.stamps_on ? I.stamps.p + (size_t)W * 24 : nullptr;
+    }
+    const int64_t P = W - 1;  // P_{W-1}: the list the eval part overrides rows from, too
+    A.pprev = I.pend.p + (size_t)(P & 1) * KSG_BATCH;
+    A.pprev_n = I.pend_n.p + (P & 1);
+    bool sampled = I.sample_every && A.ne && A.nw && I.n_samples * 2 + 2 <= I.sev.size();
     if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
-    if (I.eval_mode == 1)
-      hipLaunchKernelGGL(k_batch_eval<1>, dim3(T, nb), dim3(kBlock), 0, s, C, I.F, BO, I.progs.p, I.prog_off_d.p, j0,
-                         I.tile_top.p, I.tfeas.p, T, I.any_eph_req ? 1u : 0u, I.estamps_on ? I.estamps.p : nullptr);
-    else
-      hipLaunchKernelGGL(k_batch_eval<0>, dim3(T, nb), dim3(kBlock), 0, s, C, I.F, BO, I.progs.p, I.prog_off_d.p, j0,
-                         I.tile_top.p, I.tfeas.p, T, I.any_eph_req ? 1u : 0u, I.estamps_on ? I.estamps.p : nullptr);
+    dim3 grid(1 + A.ne * T);
+    if (I.eval_mode == 1) hipLaunchKernelGGL(k_window<1>, grid, dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, A);
+    else hipLaunchKernelGGL(k_window<0>, grid, dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, A);
     if (sampled) {
       HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
       I.n_samples++;
     }
-    int32_t* fx = I.bfeas.p;
-    if (I.xranks > 1) {
-      const size_t rec = KSG_XHDR + (size_t)KSG_BATCH * KSG_CAND * sizeof(CandRow);
-      hipLaunchKernelGGL(k_batch_merge, dim3(nb), dim3(64), 0, s, C, I.tile_top.p, T,
-                         reinterpret_cast<CandRow*>(I.xsend.p + KSG_XHDR), I.tfeas.p,
-                         reinterpret_cast<int32_t*>(I.xsend.p));
+    if (sharded && A.ne) {
       if (I.xmode == 1) {
-        ncclResult_t nr = ncclAllGather(I.xsend.p, I.xrecv.p, rec, ncclUint8, I.comm, s);
+        ncclResult_t nr = ncclAllGather(I.xsend.p, I.xrecv.p, kRecBytes, ncclUint8, I.comm, s);
         if (nr != ncclSuccess) { err = std::string("ncclAllGather: ") + ncclGetErrorString(nr); return false; }
       } else {
-        HIPCHK(hipMemcpyAsync(I.hsend.data(), I.xsend.p, rec, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(I.hsend.data(), I.xsend.p, kRecBytes, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        if (I.xfn(I.xuser, I.hsend.data(), I.hrecv.data(), rec) != 0) { err = "exchange callback failed"; return false; }
-        HIPCHK(hipMemcpyAsync(I.xrecv.p, I.hrecv.data(), rec * I.xranks, hipMemcpyHostToDevice, s));
+        if (I.xfn(I.xuser, I.hsend.data(), I.hrecv.data(), kRecBytes) != 0) { err = "exchange callback failed"; return false; }
+        HIPCHK(hipMemcpyAsync(I.xrecv.p, I.hrecv.data(), kRecBytes * I.xranks, hipMemcpyHostToDevice, s));
       }
-      hipLaunchKernelGGL(k_batch_gmerge, dim3(nb), dim3(64), 0, s, I.xrecv.p, rec, I.xranks, I.cand.p, I.gfeas.p);
-      fx = I.gfeas.p;
-    } else {
-      hipLaunchKernelGGL(k_batch_merge, dim3(nb), dim3(64), 0, s, C, I.tile_top.p, T, I.cand.p, I.tfeas.p, I.bfeas.p);
+      hipLaunchKernelGGL(k_window_gmerge, dim3(A.ne), dim3(64), 0, s, I.xrecv.p, I.xranks,
+                         I.wrec.p + (size_t)(E & 1) * kRecBytes);
     }
-    uint64_t* fst = I.stamps_on ? I.stamps.p + (size_t)(j0 - first) * 8 : nullptr;  // per batch: 8 stamps at its first pod
-    if (I.eval_mode == 1)
-      hipLaunchKernelGGL(k_batch_fixup<1>, dim3(1), dim3(KSG_FIXUP_THREADS), sizeof(FixupLDS), s, C, I.F, BO, I.progs.p,
-                         I.prog_off_d.p, j0, nb, I.cand.p, fx, I.sums.p, fst);
-    else
-      hipLaunchKernelGGL(k_batch_fixup<0>, dim3(1), dim3(KSG_FIXUP_THREADS), sizeof(FixupLDS), s, C, I.F, BO, I.progs.p,
-                         I.prog_off_d.p, j0, nb, I.cand.p, fx, I.sums.p, fst);
-    j0 = j1;
+  }
+  if (nwin) {
+    const int64_t L = nwin - 1;
+    hipLaunchKernelGGL(k_apply_pend, dim3(1), dim3(KSG_BATCH), 0, s, C, I.pend.p + (size_t)(L & 1) * KSG_BATCH,
+                       I.pend_n.p + (L & 1));
   }
   HIPCHK(hipEventRecord(I.ev1, s));
   HIPCHK(hipGetLastError());
@@ -2207,8 +2480,8 @@ bool Engine::set_exchange(int mode, const void* nccl_id, uint32_t rank, uint32_t
   I.xfn = fn;
   I.xuser = user;
   if (ranks == 1) { I.xmode = 0; return true; }
-  const size_t rec = KSG_XHDR + (size_t)KSG_BATCH * KSG_CAND * sizeof(CandRow);
-  if (!I.xsend.alloc(rec, err) || !I.xrecv.alloc(rec * ranks, err) || !I.gfeas.alloc(KSG_BATCH, err)) return false;
+  const size_t rec = kRecBytes;
+  if (!I.xsend.alloc(rec, err) || !I.xrecv.alloc(rec * ranks, err)) return false;
   HIPCHK(hipMemset(I.xsend.p, 0, rec));
   if (mode == 1) {
     ncclUniqueId id;
@@ -2238,19 +2511,9 @@ bool Engine::nccl_unique_id(void* out128, std::string& err) {
 }
 void Engine::set_path(int per_pod) { p_->force_per_pod = per_pod != 0; }
 bool Engine::eval_stamps(bool on, std::vector<uint64_t>* out, std::string& err) {
-  Impl& I = *p_;
-  uint32_t T = (I.N + kBlock - 1) / kBlock;
-  size_t n = (size_t)T * KSG_BATCH * 4 * 8;
-  if (!out) {
-    I.estamps_on = on;
-    if (on) {
-      if (!I.estamps.alloc(n, err)) return false;
-      HIPCHK(hipMemset(I.estamps.p, 0, n * 8));
-    }
-    return true;
-  }
-  out->resize(n);
-  HIPCHK(hipMemcpy(out->data(), I.estamps.p, n * 8, hipMemcpyDeviceToHost));
+  (void)on;
+  (void)err;
+  if (out) out->clear();  // the window kernel's eval blocks carry no stamps
   return true;
 }
 

@@ -1,4 +1,11 @@
-"""Diagnostic: per-phase cycle breakdown of the batch fixup loop (s_memtime stamps)."""
+"""Diagnostic: timeline of k_window per window (s_memtime / s_memrealtime stamps).
+
+Per window W, 24 slots at [W*24]: fixup block (shader clock) 0 start, 1 staged,
+2 prior-node evaluations, 3 starting guess, 4 Jacobi converged, 5 flushed,
+7 Jacobi iterations; realtime (100 MHz): 8 ~first eval-block start of window W
+(evaluated one launch earlier), 9 last tile eval done, 10 last merge done,
+11 fixup start, 12 fixup end.
+"""
 import ctypes
 import os
 import sys
@@ -7,46 +14,49 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
 from ksg import Scheduler, generator as g  # noqa: E402
 
-doc = g.generate(2, n_nodes=5000, n_pods=640)
+n_nodes = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
+n_pods = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+doc = g.generate(2, n_nodes=n_nodes, n_pods=n_pods)
 s = Scheduler(doc["profile"])
 s.load_cluster(doc)
 L = s.L
 L.ksg_debug_fixup_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
 n = s.queue_len
+nw = (n + 31) // 32
 s.schedule()  # warm
 s.reset()
 L.ksg_debug_fixup_stamps(s.h, n, None)
 s.schedule()
 buf = (ctypes.c_uint64 * (8 * n))()
 L.ksg_debug_fixup_stamps(s.h, n, buf)
-# per batch: [0] start [1] staged [2] guess+prep [3] converged [4] iterations [5] flushed
-bs = [buf[j * 8:(j + 1) * 8] for j in range(32, n, 32)]
-names = ["stage", "guess+prep", "iterations", "flush"]
-for k, (i0, i1) in enumerate([(0, 1), (1, 2), (2, 3), (3, 5)]):
-    v = sorted(x[i1] - x[i0] for x in bs)
-    print(f"fixup {names[k]:12s} median {v[len(v)//2]:6d} mean {sum(v)/len(v):8.1f} cycles")
-it = [x[4] for x in bs]
-print("fixup iterations: mean", sum(it) / len(it), "max", max(it), "hist", {k: it.count(k) for k in sorted(set(it))})
-tot = sorted(x[5] - x[0] for x in bs)
-print("per batch total median", tot[len(tot) // 2], "cycles")
+bs = [buf[j * 24:(j + 1) * 24] for j in range(nw)]
 
-# k_batch_eval per-wave phases (last batch of a run)
-L.ksg_debug_eval_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
-s.reset()
-L.ksg_debug_eval_stamps(s.h, 1, None, None)
-s.schedule()
-T = (s.n_nodes + 255) // 256
-m = T * 32 * 4 * 8
-eb = (ctypes.c_uint64 * m)()
-L.ksg_debug_eval_stamps(s.h, 1, eb, None)
-waves = [eb[i * 8:(i + 1) * 8] for i in range(T * 32 * 4)]
-waves = [w for w in waves if w[0] and w[5]]
-names = ["load row", "eval", "store+key", "sort", "merge+write"]
+
+def med(v):
+    v = sorted(v)
+    return v[len(v) // 2]
+
+
+names = ["stage", "prior eval", "guess", "jacobi", "flush"]
 for k in range(5):
-    v = sorted(w[k + 1] - w[k] for w in waves)
-    print(f"eval {names[k]:12s} median {v[len(v)//2]:6d} cycles")
-t0 = min(w[0] for w in waves)
-t1 = max(w[5] for w in waves)
-print("eval kernel span (s_memtime ticks)", t1 - t0, "waves", len(waves))
-starts = sorted(w[0] - t0 for w in waves)
-print("wave start spread: median", starts[len(starts)//2], "max", starts[-1])
+    v = [x[k + 1] - x[k] for x in bs[1:]]
+    print(f"fixup {names[k]:12s} median {med(v):6d} mean {sum(v)/len(v):8.1f} cycles")
+it = [x[7] for x in bs[1:]]
+print("jacobi iterations: mean", sum(it) / len(it), "max", max(it), "hist", {k: it.count(k) for k in sorted(set(it))})
+print("fixup block total median", med([x[5] - x[0] for x in bs[1:]]), "cycles")
+ns = 10.0  # s_memrealtime: 100 MHz
+ev = [((~x[8]) & 0xFFFFFFFFFFFFFFFF) for x in bs]
+print("realtime (us): eval start->last tile eval", med([(bs[j][9] - ev[j]) / 100 for j in range(1, nw)]))
+print("realtime (us): eval start->last merge", med([(bs[j][10] - ev[j]) / 100 for j in range(1, nw)]))
+# window j's eval runs in the same launch as window j-1's fixup
+print("realtime (us): fixup W-1 start -> eval W start", med([(ev[j] - bs[j - 1][11]) / 100 for j in range(2, nw)]))
+print("realtime (us): fixup duration", med([(x[12] - x[11]) / 100 for x in bs[1:]]))
+print("realtime (us): fixup W-1 end -> fixup W start", med([(bs[j][11] - bs[j - 1][12]) / 100 for j in range(2, nw)]))
+print("realtime (us): last merge of W -> fixup W start", med([(bs[j][11] - bs[j][10]) / 100 for j in range(2, nw)]))
+print("realtime (us): window period", med([(bs[j][11] - bs[j - 1][11]) / 100 for j in range(2, nw)]))
+for lab, i0, i1 in [("store_row", 1, 16), ("prior eval_row", 16, 17), ("wave_max", 17, 18), ("pmask+sync", 18, 2),
+                     ("iteration 1", 3, 19)]:
+    print(f"fixup {lab:14s} median {med([x[i1] - x[i0] for x in bs[1:]]):6d}")
+two = [x for x in bs[1:] if x[7] >= 2]
+if two:
+    print("iteration 2 median", med([x[20] - x[19] for x in two]), "windows", len(two))

@@ -1007,6 +1007,7 @@ struct Pend {  // a node modified by a window: row before (base) and after it
 };
 static constexpr size_t kRecBytes = KSG_XHDR + (size_t)KSG_BATCH * KSG_CAND * sizeof(CandRow);
 
+
 struct PodLite {  // the fields of ksg_prog the Fit/BA evaluation reads (LDS-staged)
   int64_t req[4];
   int64_t fit_score_req[KSG_MAX_SCORE_RES];
@@ -1017,8 +1018,7 @@ struct PodLite {  // the fields of ksg_prog the Fit/BA evaluation reads (LDS-sta
 };
 
 struct WinArgs {
-  const uint8_t* progs;
-  const uint64_t* prog_off;
+  const PodLite* plite;  // Fit/BA fields of every queue pod (flat copy of the programs)
   uint32_t first, keep_first, keep_n, need_eph;
   uint32_t *kfilter, *sfilter;  // kept outputs / scratch ring of 2*KSG_BATCH pods
   int32_t *kscore, *sscore, *ktotal, *stotal;
@@ -1072,13 +1072,26 @@ __device__ __noinline__ int64_t rtc_fn_ool(const DevProfile& F, int64_t p) { ret
 __device__ __forceinline__ int64_t least_req(int64_t a, int64_t q) {  // leastRequestedScore
   return q > a ? 0 : div_small((a - q) * 100, a);
 }
+// leastRequestedScore for the compiled default arguments: floor((a-q)*100/a)
+// from one f64 reciprocal estimate (relative error ~2^-50, quotient <= 100, so
+// the truncated estimate is the quotient or one below it) and one exact
+// integer correction; branch-free unless (a-q)*100 >= 2^52.
+__device__ __forceinline__ int64_t least_req_q(int64_t a, int64_t q) {
+  if (q > a || a <= 0) return 0;
+  int64_t x = (a - q) * 100;
+  if (__builtin_expect(x >= ((int64_t)1 << 52), 0)) return div_i64_slow(x, a);
+  int64_t d = (int64_t)((double)x * __builtin_amdgcn_rcp((double)a));
+  int64_t rem = x - d * a;
+  return rem >= a ? d + 1 : (rem < 0 ? d - 1 : d);
+}
 template <int MODE, class P>
 __device__ __forceinline__ int64_t fit_score_row(const RowV& r, const DevProfile& F, const P* h) {
-  if (MODE == 1) {
-    int64_t ns = 0, ws = 0;
-    if (r.alloc[0] != 0) { ns += least_req(r.alloc[0], r.nzc + h->fit_score_req[0]) * F.fit_w[0]; ws += F.fit_w[0]; }
-    if (r.alloc[1] != 0) { ns += least_req(r.alloc[1], r.nzm + h->fit_score_req[1]) * F.fit_w[1]; ws += F.fit_w[1]; }
-    return ws == 0 ? 0 : div_small(ns, ws);
+  if (MODE == 1) {  // LeastAllocated, cpu:1 memory:1 (the defaults): (s_cpu + s_mem) / 2
+    bool ok0 = r.alloc[0] != 0, ok1 = r.alloc[1] != 0;
+    int64_t s0 = ok0 ? least_req_q(r.alloc[0], r.nzc + h->fit_score_req[0]) : 0;
+    int64_t s1 = ok1 ? least_req_q(r.alloc[1], r.nzm + h->fit_score_req[1]) : 0;
+    int64_t ns = s0 + s1;
+    return ok0 && ok1 ? ns >> 1 : ns;
   }
   int64_t ns = 0, ws = 0;
 #pragma unroll 1
@@ -1270,7 +1283,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t* wcount = reinterpret_cast<uint32_t*>(L + 16 * 64);
   const uint32_t b = blk / A.T, tile = blk - b * A.T, q = A.e0 + b;
-  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[q]);
+  const PodLite* h = A.plite + q;
   const int np = *A.pprev_n;
   const int32_t pn = lane < np ? A.pprev[lane].node : -1;
   const uint32_t n = tile * KSG_TILE + tid;
@@ -1413,8 +1426,13 @@ struct WinLDS {
   int32_t ptn[KSG_HSLOTS], pte[KSG_HSLOTS];  // prior node -> entry
   int32_t gtn[KSG_HSLOTS], gtf[KSG_HSLOTS];  // guess rounds: node -> smallest proposer
   PickTab pick[3];                      // per S buffer
+  uint64_t kc[KSG_BATCH][KSG_CAND];     // per iteration: candidate keys, 0 where the node was touched
+  uint64_t rk[KSG_BATCH][KSG_BATCH];    // per iteration: key of pod b on the node pod a < b picked
+  int8_t rdf[KSG_BATCH][KSG_BATCH];     // its feasible-count change vs the snapshot
+  int32_t pf[KSG_BATCH];                // per iteration: first pick of P_{W-1} node e
 };
 
+static_assert(sizeof(WinLDS) <= 160 * 1024, "window LDS exceeds the CU's 160 KiB");
 __device__ __forceinline__ uint32_t hslot(int32_t node) { return ((uint32_t)node * 2654435761u) >> 25; }
 __device__ __forceinline__ int prior_of(const WinLDS& L, int32_t x) {
   uint32_t h = hslot(x);
@@ -1534,23 +1552,10 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   const int nk = nb * KSG_CAND, nr = nb * KSG_STAGE * kRowW;
   uint64_t kv[2], rv[6];
   {
-    const uint64_t pv = tid < np * kPendW ? reinterpret_cast<const uint64_t*>(A.pprev)[tid] : 0;
-    if (tid < nb) {
-      const ksg_prog* h = reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[A.w0 + tid]);
-      PodLite& q = L.pod[tid];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) q.req[k] = h->req[k];
-#pragma unroll
-      for (int k = 0; k < KSG_MAX_SCORE_RES; ++k) {
-        q.fit_score_req[k] = h->fit_score_req[k];
-        q.ba_req[k] = h->ba_req[k];
-      }
-      q.nz_cpu = h->nz_cpu;
-      q.nz_mem = h->nz_mem;
-      q.queue_idx = h->queue_idx;
-      q.flags = h->flags;
-      L.feas[tid] = reinterpret_cast<const int32_t*>(A.wrec)[tid];
-    }
+    const uint64_t pv = tid < KSG_BATCH * kPendW ? reinterpret_cast<const uint64_t*>(A.pprev)[tid] : 0;
+    constexpr int kPodW = (int)(sizeof(PodLite) / 8);
+    const uint64_t qv = tid < nb * kPodW ? reinterpret_cast<const uint64_t*>(A.plite + A.w0)[tid] : 0;
+    const int32_t fv = tid < nb ? reinterpret_cast<const int32_t*>(A.wrec)[tid] : 0;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       int i = tid + k * KSG_WIN_THREADS;
@@ -1564,22 +1569,27 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       rv[k] = i < nr ? src[(size_t)(p * KSG_CAND + r) * kCandW + 1 + wd] : 0;
     }
     if (tid < np * kPendW) reinterpret_cast<uint64_t*>(L.prior)[tid] = pv;
+    if (tid < nb * kPodW) reinterpret_cast<uint64_t*>(L.pod)[tid] = qv;
+    if (tid < nb) L.feas[tid] = fv;
     if (tid < 3 * KSG_BATCH) {
       (&L.S[0][0])[tid] = -1;
       (&L.O[0][0])[tid] = -1;
     }
     if (tid < KSG_HSLOTS) {
-      L.ptn[tid] = -1;
 #pragma unroll
       for (int t = 0; t < 3; ++t) pick_clear(L.pick[t], tid);
+    }
+    if (wave == 0) {  // index P_{W-1} (one wave: its LDS operations stay in order)
+      const int32_t pnode = lane < np ? A.pprev[lane].node : -1;
+      L.ptn[lane] = -1;
+      L.ptn[lane + 64] = -1;
+      if (lane < np) L.pte[tab_claim(L.ptn, pnode)] = lane;
     }
   }
   lds_barrier();
   STAMP(1);
-  if (tid < np) {  // P_{W-1}: index it, write it back (the eval blocks read those rows from the list)
+  if (tid < np) {  // write P_{W-1} back (the eval blocks read those rows from the list)
     const Pend& pe = L.prior[tid];
-    uint32_t h = tab_claim(L.ptn, pe.node);
-    L.pte[h] = tid;
     uint32_t nl = (uint32_t)pe.node - C.goff;
     if ((uint32_t)pe.node >= C.goff && nl < C.N) store_row(C, nl, pe.after);
   }
@@ -1620,9 +1630,13 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     }
   }
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < 2; ++k) {  // kv[k] = key of pod wave + 16k, rank lane
     int i = tid + k * KSG_WIN_THREADS;
     if (i < nk) (&L.key[0][0])[i] = kv[k];
+    const int b = wave + 16 * k;
+    bool m = kv[k] != 0 && np > 0 && prior_of(L, (int32_t)(kv[k] & 0xFFFFFull)) >= 0;
+    unsigned long long mask = __ballot(m);
+    if (lane == 0 && b < nb) L.pmask[b] = mask;
   }
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
@@ -1631,16 +1645,6 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   }
   lds_barrier();
   STAMP(17);
-#pragma unroll 1
-  for (int hh = 0; hh < 2; ++hh) {  // candidates that are P_{W-1} nodes
-    int b = 2 * wave + hh;
-    if (b >= nb) break;
-    uint64_t ck = L.key[b][lane];
-    bool m = ck != 0 && np > 0 && prior_of(L, (int32_t)(ck & 0xFFFFFull)) >= 0;
-    unsigned long long mask = __ballot(m);
-    if (lane == 0) L.pmask[b] = mask;
-  }
-  lds_barrier();
   STAMP(2);
   if (wave == 0) {  // starting guess: serial dictatorship over (candidates, P_{W-1} nodes), parallel rounds
     const int b = lane;
@@ -1653,7 +1657,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
 #pragma unroll 1
     for (int round = 0; round < 64; ++round) {
       uint64_t ck = 0;
-      if (valid) {
+      if (valid) {  // next candidate that is not a P_{W-1} node
         uint64_t free_ = ~pm & (r < 64 ? (~0ull << r) : 0ull);
         r = free_ ? __ffsll((long long)free_) - 1 : KSG_CAND;
         ck = r < KSG_CAND ? L.key[b][r] : 0;
@@ -1694,50 +1698,73 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     const int nxt = cur == 2 ? 0 : cur + 1;
     if (tid < KSG_HSLOTS) pick_clear(L.pick[nxt == 2 ? 0 : nxt + 1], tid);
     const PickTab& T = L.pick[cur];
-    const int a = lane & 31;
-    const int32_t Sv = L.S[cur][a], Ov = L.O[cur][a];
-    const int p0 = 2 * wave;
-    // pods p0 (lanes 0..31) and p0 + 1 (lanes 32..63) re-evaluate the picks a < pod
-    const int pb = p0 + (lane >> 5);
-    const bool live = pb < nb && pb >= stable;
-    uint64_t ke = 0;
-    int dfe = 0;
-    if (__ballot(live)) {
-      int nx = KSG_BATCH;
-      Delta cum;
-      delta_of(L.pod[a], cum);
-      if (Sv >= 0) {
-        int h = tab_find(T.node, Sv);
-        if (T.cnt[h] > 1) pick_chain(L, L.S[cur], a, Sv, cum, nx);  // node picked twice (rare)
-      }
-      if (live) {
-        PatchV pt;
-        pt.code = KSG_NOT_PATCHED;
-        pt.fit = pt.ba = pt.total = 0;
-        if (Sv >= 0 && a < pb && nx >= pb) {
-          RowV cur_r, snap;
-          origin_rows(L, A, Ov, cur_r, snap);
-          apply_delta(cur_r, cum, R);
-          const PodLite* h = &L.pod[pb];
-          int32_t fs, bs;
-          int64_t tot;
-          uint32_t code = eval_row<MODE>(cur_r, F, h, R, fs, bs, tot);
-          bool snap_ok = F.pos_fit < 0 || fit_filter_row(snap, h, R) == 0;
-          dfe = (code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0);
-          if (code == KSG_FILTER_PASS) ke = pack_key(tot, F.seed, h->queue_idx, (uint32_t)Sv);
-          pt.code = code;
-          pt.fit = fs;
-          pt.ba = bs;
-          pt.total = (int32_t)tot;
+    // phase A.  Waves 0..7 re-evaluate, for every pod b >= stable, the nodes the
+    // pods a < b picked (pairs packed triangularly, p = b(b-1)/2 + a, so only
+    // the live pairs occupy lanes); waves 8..15 mask each live pod's candidates
+    // that an earlier pick touched.
+    if (wave < 8) {
+      const int p_hi = nb * (nb - 1) / 2;
+#pragma unroll 1
+      for (int base = stable * (stable - 1) / 2 + wave * 64; base < p_hi; base += 8 * 64) {
+        const int p = base + lane;
+        if (p < p_hi) {
+          int b = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)p)) * 0.5f);
+          b = b * (b - 1) / 2 > p ? b - 1 : ((b + 1) * b / 2 <= p ? b + 1 : b);
+          const int a = p - b * (b - 1) / 2;
+          const int32_t Sv = L.S[cur][a];
+          uint64_t k = 0;
+          int df = 0;
+          PatchV pt;
+          pt.code = KSG_NOT_PATCHED;
+          pt.fit = pt.ba = pt.total = 0;
+          if (Sv >= 0) {
+            int nx = KSG_BATCH;
+            Delta cum;
+            delta_of(L.pod[a], cum);
+            if (iters == 0) STAMP(24);
+            if (T.cnt[tab_find(T.node, Sv)] > 1) pick_chain(L, L.S[cur], a, Sv, cum, nx);  // picked twice (rare)
+            if (iters == 0) STAMP(25);
+            if (nx >= b) {  // a is the last pick of the node before b
+              RowV cur_r, snap;
+              origin_rows(L, A, L.O[cur][a], cur_r, snap);
+              apply_delta(cur_r, cum, R);
+              const PodLite* h = &L.pod[b];
+              int32_t fs, bs;
+              int64_t tot;
+              if (iters == 0) STAMP(26);
+              uint32_t code = eval_row<MODE>(cur_r, F, h, R, fs, bs, tot);
+              if (iters == 0) STAMP(27);
+              bool snap_ok = F.pos_fit < 0 || fit_filter_row(snap, h, R) == 0;
+              df = (code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0);
+              if (code == KSG_FILTER_PASS) k = pack_key(tot, F.seed, h->queue_idx, (uint32_t)Sv);
+              pt.code = code;
+              pt.fit = fs;
+              pt.ba = bs;
+              pt.total = (int32_t)tot;
+            }
+          }
+          L.rk[b][a] = k;
+          L.rdf[b][a] = (int8_t)df;
+          L.patch[b][32 + a] = pt;
         }
-        L.patch[pb][32 + a] = pt;
+      }
+    } else {
+      if (wave == 8 && lane < np) L.pf[lane] = first_pick(T, L.prior[lane].node);
+#pragma unroll 1
+      for (int b = stable + (wave - 8); b < nb; b += 8) {
+        const uint64_t ck = L.key[b][lane];
+        const bool mod = ((L.pmask[b] >> lane) & 1) || (ck != 0 && first_pick(T, (int32_t)(ck & 0xFFFFFull)) < b);
+        L.kc[b][lane] = mod ? 0 : ck;
       }
     }
-    // first pick of each P_{W-1} node under S (lanes < np), shared by both pods
-    const int pf = lane < np ? first_pick(T, L.prior[lane].node) : -1;
+    if (iters == 0) STAMP(21);
+    lds_barrier();
+    if (iters == 0) STAMP(22);
+    // phase B: per pod, the best of (untouched candidates, P_{W-1} nodes no
+    // earlier pick touched, re-evaluated picks); waves own pods 2w and 2w+1.
 #pragma unroll 1
     for (int hh = 0; hh < 2; ++hh) {
-      const int b = p0 + hh;
+      const int b = 2 * wave + hh;
       if (b >= nb) break;
       if (b < stable) {
         if (lane == 0) {
@@ -1748,25 +1775,21 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
         }
         continue;
       }
-      const uint64_t ck = L.key[b][lane];
-      const bool mod = ((L.pmask[b] >> lane) & 1) || (ck != 0 && first_pick(T, (int32_t)(ck & 0xFFFFFull)) < b);
-      const bool pact = lane < np && pf >= b;
-      const uint64_t kc = (ck != 0 && !mod) ? ck : 0;
-      const uint64_t kp = pact ? L.pkey[b][lane] : 0;
-      const int dfp = pact ? (int)L.pdf[b][lane] : 0;
-      const bool mine = (lane >> 5) == hh;
-      const uint64_t kr = mine ? ke : 0;
-      const int dfr = mine ? dfe : 0;
+      const bool pact = lane < np && L.pf[lane & 31] >= b;
+      const uint64_t kc = L.kc[b][lane];
+      const uint64_t kp = pact ? L.pkey[b][lane & 31] : 0;
+      const uint64_t kr = lane < b ? L.rk[b][lane & 31] : 0;
+      const int df = (pact ? (int)L.pdf[b][lane & 31] : 0) + (lane < b ? (int)L.rdf[b][lane & 31] : 0);
       const uint64_t best = wave_max(max3u(kc, kp, kr));
-      const int feasible = L.feas[b] + wave_sum(dfp + dfr);
+      const int feasible = L.feas[b] + wave_sum(df);
       const int32_t sel = (feasible > 0 && best) ? (int32_t)(best & 0xFFFFFull) : -1;
       const unsigned long long mc = __ballot(best && kc == best), mp = __ballot(best && kp == best),
                                mr = __ballot(best && kr == best);
-      int32_t org = -1;
-      if (mc) org = 64 + b * 64 + (__ffsll((long long)mc) - 1);
-      else if (mp) org = __ffsll((long long)mp) - 1;
-      else if (mr) org = __builtin_amdgcn_readlane(Ov, __ffsll((long long)mr) - 1);
       if (lane == 0) {
+        int32_t org = -1;
+        if (mc) org = 64 + b * 64 + (__ffsll((long long)mc) - 1);
+        else if (mp) org = __ffsll((long long)mp) - 1;
+        else if (mr) org = L.O[cur][__ffsll((long long)mr) - 1];
         L.S[nxt][b] = sel;
         L.O[nxt][b] = sel >= 0 ? org : -1;
         if (sel >= 0) pick_insert(L.pick[nxt], sel, b);
@@ -1777,6 +1800,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
         sm.status = sel >= 0 ? 0 : 1;
       }
     }
+    if (iters == 0) STAMP(23);
     lds_barrier();
     if (iters < 2) STAMP(19 + iters);
     ++iters;
@@ -1808,7 +1832,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       const int b = 2 * wave + hh;
       if (b >= nb) break;
       const PatchV pt = L.patch[b][lane];
-      const bool wr = lane < 32 ? (lane < np && pf >= b) : pt.code != KSG_NOT_PATCHED;
+      const bool wr = lane < 32 ? (lane < np && pf >= b) : (lane - 32 < b && pt.code != KSG_NOT_PATCHED);
       const int32_t node = lane < 32 ? pn : Sv;
       const uint32_t nl = (uint32_t)node - C.goff;
       if (wr && node >= 0 && (uint32_t)node >= C.goff && nl < C.N) {
@@ -1977,6 +2001,7 @@ struct Engine::Impl {
   DBuf<int32_t> kscore, ktotal;
   // programs
   DBuf<uint8_t> progs;
+  DBuf<PodLite> plite;  // Fit/BA fields of the programs (window path)
   DBuf<uint64_t> prog_off_d;
   bool any_eph_req = false;
   // speculative batch path
@@ -2097,8 +2122,8 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
     F.fit_res_d = I.fit_res_d.p;
     F.fit_w_d = I.fit_w_d.p;
     F.ba_res_d = I.ba_res_d.p;
-    I.eval_mode = (F.fit_strategy == 0 && F.fit_n == 2 && F.fit_res[0] == 0 && F.fit_res[1] == 1 && F.ba_n == 2 &&
-                   F.ba_res[0] == 0 && F.ba_res[1] == 1)
+    I.eval_mode = (F.fit_strategy == 0 && F.fit_n == 2 && F.fit_res[0] == 0 && F.fit_res[1] == 1 && F.fit_w[0] == 1 &&
+                   F.fit_w[1] == 1 && F.ba_n == 2 && F.ba_res[0] == 0 && F.ba_res[1] == 1)
                       ? 1
                       : 0;
   }
@@ -2224,8 +2249,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   HIPCHK(hipEventRecord(I.ev0, s));
   HIPCHK(hipMemsetAsync(I.pend_n.p, 0, 2 * sizeof(int32_t), s));
   WinArgs A{};
-  A.progs = I.progs.p;
-  A.prog_off = I.prog_off_d.p;
+  A.plite = I.plite.p;
   A.first = first;
   A.keep_first = I.keep_first;
   A.keep_n = I.keep_n;
@@ -2244,7 +2268,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     A.nw = 0;
     A.stamps = A.estamps = nullptr;
     if (E < (int64_t)nwin) {
-      A.estamps = I.stamps_on ? I.stamps.p + (size_t)E * 24 : nullptr;
+      A.estamps = I.stamps_on ? I.stamps.p + (size_t)E * 32 : nullptr;
       A.e0 = first + (uint32_t)E * KSG_BATCH;
       A.ne = std::min<uint32_t>(KSG_BATCH, first + count - A.e0);
       A.erec = sharded ? I.xsend.p : I.wrec.p + (size_t)(E & 1) * kRecBytes;
@@ -2255,7 +2279,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
       A.wrec = I.wrec.p + (size_t)(W & 1) * kRecBytes;
       A.pnext = I.pend.p + (size_t)(W & 1) * KSG_BATCH;
       A.pnext_n = I.pend_n.p + (W & 1);
-      A.stamps = I.stamps_on ? I.stamps.p + (size_t)W * 24 : nullptr;
+      A.stamps = I.stamps_on ? I.stamps.p + (size_t)W * 32 : nullptr;
     }
     const int64_t P = W - 1;  // P_{W-1}: the list the eval part overrides rows from, too
     A.pprev = I.pend.p + (size_t)(P & 1) * KSG_BATCH;
@@ -2310,6 +2334,23 @@ bool Engine::set_programs(const std::vector<std::vector<uint8_t>>& progs, std::s
     I.prog_need.push_back(need);
   }
   if (!I.progs.upload(blob, I.stream, err)) return false;
+  {
+    std::vector<PodLite> pl(progs.size());
+    for (size_t i = 0; i < progs.size(); ++i) {
+      const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs[i].data());
+      PodLite& q = pl[i];
+      for (int k = 0; k < 4; ++k) q.req[k] = h->req[k];
+      for (int k = 0; k < KSG_MAX_SCORE_RES; ++k) {
+        q.fit_score_req[k] = h->fit_score_req[k];
+        q.ba_req[k] = h->ba_req[k];
+      }
+      q.nz_cpu = h->nz_cpu;
+      q.nz_mem = h->nz_mem;
+      q.queue_idx = h->queue_idx;
+      q.flags = h->flags;
+    }
+    if (!I.plite.upload(pl, I.stream, err)) return false;
+  }
   std::vector<uint64_t> offs(I.prog_off.begin(), I.prog_off.end());
   if (!I.prog_off_d.upload(offs, I.stream, err)) return false;
   I.any_eph_req = false;

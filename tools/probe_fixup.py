@@ -29,7 +29,7 @@ L.ksg_debug_fixup_stamps(s.h, n, None)
 s.schedule()
 buf = (ctypes.c_uint64 * (8 * n))()
 L.ksg_debug_fixup_stamps(s.h, n, buf)
-bs = [buf[j * 24:(j + 1) * 24] for j in range(nw)]
+bs = [buf[j * 32:(j + 1) * 32] for j in range(nw)]
 
 
 def med(v):
@@ -54,8 +54,10 @@ print("realtime (us): fixup duration", med([(x[12] - x[11]) / 100 for x in bs[1:
 print("realtime (us): fixup W-1 end -> fixup W start", med([(bs[j][11] - bs[j - 1][12]) / 100 for j in range(2, nw)]))
 print("realtime (us): last merge of W -> fixup W start", med([(bs[j][11] - bs[j][10]) / 100 for j in range(2, nw)]))
 print("realtime (us): window period", med([(bs[j][11] - bs[j - 1][11]) / 100 for j in range(2, nw)]))
-for lab, i0, i1 in [("store_row", 1, 16), ("prior eval_row", 16, 17), ("wave_max", 17, 18), ("pmask+sync", 18, 2),
-                     ("iteration 1", 3, 19)]:
+for lab, i0, i1 in [("prior eval", 1, 16), ("keys->LDS+sync", 16, 17), ("pmask+sync", 17, 2),
+                     ("iteration 1", 3, 19), ("it1 phase A", 3, 21), ("it1 barrier A", 21, 22), ("it1 phase B", 22, 23),
+                     ("it1 barrier B", 23, 19), ("A: start->find", 3, 24), ("A: find/chain", 24, 25),
+                     ("A: origin rows", 25, 26), ("A: eval_row", 26, 27), ("A: rest", 27, 21)]:
     print(f"fixup {lab:14s} median {med([x[i1] - x[i0] for x in bs[1:]]):6d}")
 two = [x for x in bs[1:] if x[7] >= 2]
 if two:

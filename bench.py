@@ -39,25 +39,54 @@ def parse():
 
 
 def algorithmic_bytes_per_node_fit_ba(n_res=3):
-    """k_filter_score, Fit+BA profile (DESIGN.md roofline table):
+    """Per (pod, node) pair, Fit+BA profile (DESIGN.md roofline table):
     reads  alloc cpu/mem 16 + allowed pods 4 + requested cpu/mem 16 + nonzero cpu/mem 16 + pod count 4 = 56 B
     writes filter code 4 + raw Fit 4 + raw BA 4 + total 4 = 16 B."""
     return 56 + 16
+
+
+WINDOW = 32          # pods per k_window launch (KSG_BATCH)
+TILE = 1024          # nodes per eval block (KSG_TILE)
+REC_BYTES = 128 + WINDOW * 64 * 96  # candidate record of one window (KSG_XHDR + 32 x 64 CandRow)
+
+
+def window_bytes_per_launch(shard):
+    """k_window, one launch = eval of one window (WINDOW pods x shard nodes) + the
+    replay of the previous one: per-pair row reads and outputs, the tile top-64
+    lists (written and read back), the candidate record (written by the eval
+    part, read by the next launch's replay)."""
+    tiles = (shard + TILE - 1) // TILE
+    return WINDOW * shard * algorithmic_bytes_per_node_fit_ba() + 2 * tiles * WINDOW * 64 * 8 + 2 * REC_BYTES
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per dispatch of `kernel` from the committed PMC pass
+    (profiles/*pmc_traffic.json, tools/pmc_pass.sh): FETCH_SIZE x 2 (gfx950
+    tallies 128-B requests at 64 B, MI355X_MICROARCH.md HBM section) + WRITE_SIZE,
+    both in KB per dispatch.  None when no pass is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    return None if k is None else k["hbm_bytes_per_dispatch"]
 
 
 def cpu_baseline(doc, n_pods, workers):
     """Time the oracle (the CPU restatement, test infrastructure) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _oracle import Oracle
-    res = {}
+    res, secs = {}, 0.0
     for w in sorted({1, workers}):
         o = Oracle(doc)
         t = time.perf_counter()
         done = o.schedule(n=n_pods, workers=w, record=0)
         dt = time.perf_counter() - t
+        secs += dt
         res[w] = done * len(doc["nodes"]) / dt
     best_w = max(res, key=res.get)
-    return best_w, res
+    return best_w, res, secs
 
 
 def main():
@@ -118,10 +147,9 @@ def main():
     ms_per_step = elapsed * 1e3 / a.steps
     kernel_ms = ksum / max(kcount, 1)
     shard = n_nodes // world
-    if s.batch_path:  # k_batch_eval: 32 pods x shard nodes per launch + tile top-64 lists
-        kname = "k_batch_eval"
-        tiles = (shard + 255) // 256
-        bytes_per_launch = 32 * shard * algorithmic_bytes_per_node_fit_ba() + tiles * 32 * 64 * 8
+    if s.batch_path:
+        kname = "k_window"
+        bytes_per_launch = window_bytes_per_launch(shard)
     else:
         kname = "k_filter_score"
         bytes_per_launch = shard * algorithmic_bytes_per_node_fit_ba()
@@ -145,16 +173,17 @@ def main():
                    "nodes_per_gpu": shard, "nodes_total": n_nodes, "pods": n_pods, "parallelism": f"node-shard x{world} (RCCL all-gather per 32-pod batch)" if world > 1 else "1 GPU"},
         "scheduled_pods_per_s": scheduled * a.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(kname),
                      "kernel": kname, "kernel_avg_us": kernel_ms * 1e3, "kernel_samples": kcount,
                      "bytes_per_launch": bytes_per_launch},
     }
     if a.cpu_baseline and world == 1:
-        n_cpu = a.cpu_pods or 400
-        w, rates = cpu_baseline(doc, n_cpu, a.cpu_workers)
+        n_cpu = a.cpu_pods or n_pods
+        w, rates, secs = cpu_baseline(doc, n_cpu, a.cpu_workers)
         out["cpu_baseline"] = {"value": rates[w], "unit": "pairs/s", "cores": w, "kind": "port",
                                "sample": f"first {n_cpu} of {n_pods} pods x {n_nodes} nodes (same cfg2 cluster), "
-                                         f"oracle plugin-only path; rates by workers: "
+                                         f"oracle plugin-only path (parallelize.Until chunking), "
+                                         f"{secs:.1f} s of CPU runs; rates by workers: "
                                          + ", ".join(f"{k}: {v:.3g}" for k, v in sorted(rates.items()))}
     print(json.dumps(out))
 

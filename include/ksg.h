@@ -109,13 +109,14 @@ int ksg_reset(ksg_ctx* ctx);
 int ksg_sample_kernel(ksg_ctx* ctx, uint32_t every);
 int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples);
 /* Execution path: profiles made only of NodeResourcesFit / BalancedAllocation
- * run as exact speculative batches (k_batch_eval / merge / fixup); every other
- * profile runs the per-pod kernel chain.  per_pod != 0 forces the chain. */
+ * run as exact speculative 32-pod windows (k_window: evaluation of window j+1
+ * beside the exact replay of window j); every other profile runs the per-pod
+ * kernel chain.  per_pod != 0 forces the chain. */
 int ksg_set_path(ksg_ctx* ctx, int per_pod);
 int ksg_batch_path(const ksg_ctx* ctx);  /* 1 when the batch path is active */
 
-/* Node sharding across GPUs (ksg_opts.shard_rank / shard_count): per batch of
- * 32 pods every rank all-gathers its per-pod top-32 candidates (with their node
+/* Node sharding across GPUs (ksg_opts.shard_rank / shard_count): per window of
+ * 32 pods every rank all-gathers its per-pod top-64 candidates (with their node
  * rows) and local feasible counts, merges them, and runs the same deterministic
  * replay, applying only its own nodes' assume deltas.
  *   mode 1: RCCL all-gather on the context stream; nccl_id = 128 bytes from
@@ -137,9 +138,21 @@ int ksg_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* out, uint32_t n)
 /* Store.GetStoredResult for queue pod q as a JSON object {annotation key: value}. */
 int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len);
 
-/* Drop-in cycle: schedule one more pod (appended to the queue) and, when
- * commit != 0, assume it on the selected node (Reserve). */
+/* Drop-in cycle (one pod, the framework's scheduleOne): PreFilter..Score..
+ * NormalizeScore for a new pod (v1.Pod JSON, appended to the queue: its index
+ * is ksg_queue_len() - 1), its per-node outputs kept for ksg_filter_codes /
+ * ksg_scores / ksg_annotations.  commit != 0 also assumes it on the engine's
+ * selectHost choice (harness mode); commit == 0 leaves the assume to
+ * ksg_reserve with the framework's own choice (plugin mode).  A pod bringing
+ * labels, namespaces, topology keys or scalar resources the snapshot has not
+ * seen triggers a re-encode of the snapshot (placements kept). */
 int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_pod_result* out);
+/* ReservePlugin.Reserve (wrappedplugin.go:631 -> scheduler cache assume):
+ * assume queue pod q (run with commit == 0) on global node `node`. */
+int ksg_reserve(ksg_ctx* ctx, uint32_t q, int32_t node);
+/* ReservePlugin.Unreserve (mock framework.go:611): undo the assume of queue
+ * pod q (cycle or queue mode): node rows, and its existing-pod table entry. */
+int ksg_unreserve(ksg_ctx* ctx, uint32_t q);
 
 /* Device node rows (assume parity): requested [n_res][n], pod count [n]. */
 int ksg_node_requested(ksg_ctx* ctx, int64_t* requested, int32_t* pod_count, uint32_t n_res, uint32_t n);

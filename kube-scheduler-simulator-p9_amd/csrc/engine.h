@@ -83,6 +83,13 @@ class Engine {
               uint32_t req_cap, uint32_t val_cap, std::string& err);
   // Queue programs: blobs laid out by the host encoder (ksg_prog + pools).
   bool set_programs(const std::vector<std::vector<uint8_t>>& progs, std::string& err);
+  // Append one program (drop-in cycle API); its index is the previous count.
+  bool append_program(const std::vector<uint8_t>& prog, std::string& err);
+  // Reserve (sign +1) / Unreserve (sign -1) program q on global node gnode.
+  bool assume(uint32_t q, int32_t gnode, int sign, std::string& err);
+  bool set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err);
+  // An assume found the existing-pod table full (the pod was not appended).
+  bool table_overflow(bool& overflow, std::string& err);
   // Run pods [first, first+count) of the program list back to back on the device
   // (device-side assume).  keep: store per-pair outputs for pods [keep_first, keep_first+keep_n).
   bool run_queue(uint32_t first, uint32_t count, bool commit, std::string& err);

@@ -514,7 +514,7 @@ __global__ void k_scan_pods(DevCluster C, DevProfile F, DevScratch S, DevOut O, 
   uint32_t np = C.tcounts[0];
   uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t aff_hit = 0;
-  if (p < np) {
+  if (p < np && !(C.ptflags[p] & KEF_DELETED)) {
     int32_t node = C.ptnode[p];
     int32_t ns = C.ptns[p];
     uint32_t fl = C.ptflags[p];
@@ -572,7 +572,7 @@ __global__ void k_scan_terms(DevCluster C, DevProfile F, DevScratch S, DevOut O,
   uint32_t nt = C.tcounts[1];
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t hit = 0, slots = 0;
-  if (t < nt) {
+  if (t < nt && !(C.ptflags[C.tpod[t]] & KEF_DELETED)) {
     const ksg_exist_term& e = C.terms[t];
     int32_t p = C.tpod[t];
     int32_t node = C.ptnode[p];
@@ -899,25 +899,23 @@ __global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, c
   if (lane0() && b) atomicMax((unsigned long long*)&O.sum->best_key, (unsigned long long)b);
 }
 
-// assume (scheduleOne -> assume -> NodeInfo.AddPod) + existing-pod table append
-__global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* prog, int append) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  ProgView V = view(prog);
+// assume (scheduleOne -> assume -> NodeInfo.AddPod, or its reversal for
+// Unreserve) of program V on local node n: resource rows, and for PTS/IPA
+// profiles the existing-pod table (append; reversal marks the row deleted).
+__device__ void assume_pod(DevCluster& C, const ProgView& V, uint32_t n, int sign, bool table, int32_t* prow) {
   const ksg_prog* h = V.h;
-  ksg_pod_summary* s = O.sum;
-  if (h->flags & KPF_PREFILTER_ERROR) s->status |= 2;
-  if (s->status & 2) { s->status = 2; s->selected = -1; return; }
-  if (s->feasible == 0) { s->status = 1; s->selected = -1; return; }
-  uint32_t g = (uint32_t)(s->best_key & 0xFFFFFull);
-  s->selected = (int32_t)g;
-  s->status = 0;
-  uint32_t n = g - C.goff;
-  if (g < C.goff || n >= C.N) return;  // another shard owns the node
-  for (uint32_t r = 0; r < C.R; ++r) C.req[(size_t)r * C.N + n] += h->req[r];
-  C.nzc[n] += h->nz_cpu;
-  C.nzm[n] += h->nz_mem;
-  C.podcnt[n] += 1;
-  if (!append) return;
+  for (uint32_t r = 0; r < C.R; ++r) C.req[(size_t)r * C.N + n] += sign * h->req[r];
+  C.nzc[n] += sign * h->nz_cpu;
+  C.nzm[n] += sign * h->nz_mem;
+  C.podcnt[n] += sign;
+  if (sign < 0) {
+    if (prow && *prow >= 0) {
+      C.ptflags[*prow] |= KEF_DELETED;
+      *prow = -1;
+    }
+    return;
+  }
+  if (!table) return;
   uint32_t row = C.tcounts[0];
   uint32_t tb = C.tcounts[1], rb = C.tcounts[2], vb = C.tcounts[3];
   int ne = h->n_exist_terms;
@@ -959,6 +957,35 @@ __global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* pr
   C.tcounts[1] = tb;
   C.tcounts[2] = rb;
   C.tcounts[3] = vb;
+  if (prow) *prow = (int32_t)row;
+}
+
+// selectHost result of the cycle; mode bit 0: assume on the selected node,
+// bit 1: also append the pod to the existing-pod table.
+__global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* prog, int mode, int32_t* prow) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  ksg_pod_summary* s = O.sum;
+  *prow = -1;
+  if (h->flags & KPF_PREFILTER_ERROR) s->status |= 2;
+  if (s->status & 2) { s->status = 2; s->selected = -1; return; }
+  if (s->feasible == 0) { s->status = 1; s->selected = -1; return; }
+  uint32_t g = (uint32_t)(s->best_key & 0xFFFFFull);
+  s->selected = (int32_t)g;
+  s->status = 0;
+  uint32_t n = g - C.goff;
+  if (!(mode & 1) || g < C.goff || n >= C.N) return;  // what-if, or another shard owns the node
+  assume_pod(C, V, n, +1, (mode & 2) != 0, prow);
+}
+
+// Reserve / Unreserve on an explicit node (the framework's selectHost choice).
+__global__ void k_assume(DevCluster C, const uint8_t* prog, int32_t gnode, int sign, int table, int32_t* prow) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ProgView V = view(prog);
+  uint32_t n = (uint32_t)gnode - C.goff;
+  if (gnode < 0 || (uint32_t)gnode < C.goff || n >= C.N) return;
+  assume_pod(C, V, n, sign, table != 0, prow);
 }
 
 // ----------------------------------------------------------------- speculative window path
@@ -1945,6 +1972,28 @@ struct DBuf {
     n = std::max<size_t>(count, 1);
     return true;
   }
+  // capacity >= count, keeping the first `used` elements (doubling growth)
+  bool grow(size_t count, size_t used, hipStream_t s, std::string& err) {
+    if (count <= n && p) return true;
+    size_t cap = std::max<size_t>(std::max<size_t>(count, 2 * n), 1);
+    T* q = nullptr;
+    hipError_t e = hipMalloc((void**)&q, cap * sizeof(T));
+    if (e != hipSuccess) {
+      err = std::string("hipMalloc: ") + hipGetErrorString(e);
+      return false;
+    }
+    if (p && used) e = hipMemcpyAsync(q, p, std::min(used, n) * sizeof(T), hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+      err = hipGetErrorString(e);
+      (void)hipFree(q);
+      return false;
+    }
+    if (p) (void)hipFree(p);
+    p = q;
+    n = cap;
+    return true;
+  }
   bool upload(const std::vector<T>& v, hipStream_t s, std::string& err) {
     if (!alloc(v.size(), err)) return false;
     if (!v.empty()) {
@@ -1995,6 +2044,8 @@ struct Engine::Impl {
   DBuf<uint32_t> filter;
   DBuf<int32_t> score, total;
   DBuf<ksg_pod_summary> sums;
+  DBuf<int32_t> prow;     // existing-pod table row of each assumed queue pod (-1 none)
+  size_t prog_bytes = 0;  // used bytes of the program blob
   // kept per-pair outputs
   uint32_t keep_first = 0, keep_n = 0;
   DBuf<uint32_t> kfilter;
@@ -2317,6 +2368,77 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   return true;
 }
 
+static PodLite pod_lite(const std::vector<uint8_t>& prog) {
+  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
+  PodLite q;
+  for (int k = 0; k < 4; ++k) q.req[k] = h->req[k];
+  for (int k = 0; k < KSG_MAX_SCORE_RES; ++k) {
+    q.fit_score_req[k] = h->fit_score_req[k];
+    q.ba_req[k] = h->ba_req[k];
+  }
+  q.nz_cpu = h->nz_cpu;
+  q.nz_mem = h->nz_mem;
+  q.queue_idx = h->queue_idx;
+  q.flags = h->flags;
+  return q;
+}
+
+bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) {
+  Impl& I = *p_;
+  hipStream_t s = I.stream;
+  const size_t q = I.prog_off.size();
+  const size_t off = (I.prog_bytes + 255) & ~(size_t)255;
+  if (!I.progs.grow(off + prog.size(), I.prog_bytes, s, err) || !I.prog_off_d.grow(q + 1, q, s, err) ||
+      !I.plite.grow(q + 1, q, s, err) || !I.sums.grow(q + 1, q, s, err) || !I.prow.grow(q + 1, q, s, err))
+    return false;
+  const uint64_t off64 = off;
+  const PodLite pl = pod_lite(prog);
+  const int32_t none = -1;
+  HIPCHK(hipMemcpyAsync(I.progs.p + off, prog.data(), prog.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.prog_off_d.p + q, &off64, sizeof(off64), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.plite.p + q, &pl, sizeof(pl), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.prow.p + q, &none, sizeof(none), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_init_summaries, dim3(1), dim3(256), 0, s, I.sums.p + q, 1u, I.F);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));  // the host sources above are stack / caller buffers
+  I.prog_bytes = off + prog.size();
+  I.prog_off.push_back(off);
+  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
+  I.prog_need.push_back((h->n_tsc_filter + h->n_tsc_score > 0 ? 1u : 0u) | 2u);
+  for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
+  return true;
+}
+
+bool Engine::assume(uint32_t q, int32_t gnode, int sign, std::string& err) {
+  Impl& I = *p_;
+  if (q >= I.prog_off.size()) { err = "program index out of range"; return false; }
+  DevCluster C = I.cluster();
+  hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, I.stream, C, I.progs.p + I.prog_off[q], gnode, sign,
+                     (I.has_pts || I.has_ipa) ? 1 : 0, I.prow.p + q);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
+bool Engine::table_overflow(bool& overflow, std::string& err) {
+  Impl& I = *p_;
+  uint32_t f = 0;
+  overflow = false;
+  if (!I.tcounts.p) return true;
+  HIPCHK(hipMemcpyAsync(&f, I.tcounts.p + 4, sizeof(f), hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipStreamSynchronize(I.stream));
+  overflow = f != 0;
+  return true;
+}
+
+bool Engine::set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err) {
+  Impl& I = *p_;
+  if (first + count > I.prog_off.size()) { err = "program index out of range"; return false; }
+  HIPCHK(hipMemcpyAsync(I.sums.p + first, in, count * sizeof(ksg_pod_summary), hipMemcpyHostToDevice, I.stream));
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
 bool Engine::set_programs(const std::vector<std::vector<uint8_t>>& progs, std::string& err) {
   Impl& I = *p_;
   std::vector<uint8_t> blob;
@@ -2334,21 +2456,10 @@ bool Engine::set_programs(const std::vector<std::vector<uint8_t>>& progs, std::s
     I.prog_need.push_back(need);
   }
   if (!I.progs.upload(blob, I.stream, err)) return false;
+  I.prog_bytes = blob.size();
   {
     std::vector<PodLite> pl(progs.size());
-    for (size_t i = 0; i < progs.size(); ++i) {
-      const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs[i].data());
-      PodLite& q = pl[i];
-      for (int k = 0; k < 4; ++k) q.req[k] = h->req[k];
-      for (int k = 0; k < KSG_MAX_SCORE_RES; ++k) {
-        q.fit_score_req[k] = h->fit_score_req[k];
-        q.ba_req[k] = h->ba_req[k];
-      }
-      q.nz_cpu = h->nz_cpu;
-      q.nz_mem = h->nz_mem;
-      q.queue_idx = h->queue_idx;
-      q.flags = h->flags;
-    }
+    for (size_t i = 0; i < progs.size(); ++i) pl[i] = pod_lite(progs[i]);
     if (!I.plite.upload(pl, I.stream, err)) return false;
   }
   std::vector<uint64_t> offs(I.prog_off.begin(), I.prog_off.end());
@@ -2360,7 +2471,9 @@ bool Engine::set_programs(const std::vector<std::vector<uint8_t>>& progs, std::s
   }
   for (int i = 0; i < I.F.fit_n; ++i) I.any_eph_req |= I.F.fit_res[i] >= 2;
   for (int i = 0; i < I.F.ba_n; ++i) I.any_eph_req |= I.F.ba_res[i] >= 2;
-  if (!I.sums.alloc(std::max<size_t>(progs.size(), 1), err)) return false;
+  if (!I.sums.alloc(std::max<size_t>(progs.size(), 1), err) || !I.prow.alloc(std::max<size_t>(progs.size(), 1), err))
+    return false;
+  HIPCHK(hipMemsetAsync(I.prow.p, 0xFF, I.prow.n * sizeof(int32_t), I.stream));
   uint32_t cnt = (uint32_t)progs.size();
   if (cnt) {
     hipLaunchKernelGGL(k_init_summaries, dim3((cnt + 255) / 256), dim3(256), 0, I.stream, I.sums.p, cnt, I.F);
@@ -2443,11 +2556,8 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
       }
       hipLaunchKernelGGL(k_finalize, gN, b, 0, s, C, F, S, O, prog);
     }
-    hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, s, C, F, O, prog, (commit && (I.has_pts || I.has_ipa)) ? 1 : 0);
-    if (!commit) {
-      // what-if: the commit kernel still resolves the selection; undo is not needed
-      // because k_commit only mutates when commit is requested (see below)
-    }
+    const int mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
+    hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, s, C, F, O, prog, mode, I.prow.p + j);
   }
   HIPCHK(hipEventRecord(I.ev1, s));
   HIPCHK(hipGetLastError());

@@ -1098,17 +1098,173 @@ struct Cluster {
       qreqs += rq.size();
       qvals += vl.size();
     }
-    if (!eng->upload(S, T, T.n + qn + 16, (uint32_t)(T.terms.size() + qterms + 16),
-                     (uint32_t)(T.reqs.size() + qreqs + 16), (uint32_t)(T.vals.size() + qvals + 16), err))
+    const uint32_t slack = 1024;  // room for drop-in cycle pods (ksg_cycle) before a re-encode
+    if (!eng->upload(S, T, T.n + qn + slack, (uint32_t)(T.terms.size() + qterms + 4 * slack),
+                     (uint32_t)(T.reqs.size() + qreqs + 8 * slack), (uint32_t)(T.vals.size() + qvals + 16 * slack),
+                     err))
       return false;
     compiled = false;
     progs.clear();
     meta.clear();
+    qmode.clear();
+    placed.clear();
+    assumed_in.clear();
+    epoch = 0;
     return true;
   }
 
   vector<std::unique_ptr<J>> docs;
   vector<vector<uint8_t>> progs;
+
+  // ------------------------------------------------------------ drop-in cycles
+  // Host mirror of what the device has assumed, so the snapshot can be rebuilt
+  // (a pod bringing new vocabulary, an Unreserve the device cannot undo).
+  vector<int8_t> qmode;         // per queue pod: 0 not run, 1 queue mode (placement = summary), 2 cycle mode
+  vector<int32_t> placed;       // cycle mode: node the pod is assumed on (-1 none)
+  vector<uint32_t> assumed_in;  // rebuild epoch in which the device assumed the pod
+  uint32_t epoch = 0;
+
+  void track_queue() {
+    qmode.resize(queue.size(), 0);
+    placed.resize(queue.size(), -1);
+    assumed_in.resize(queue.size(), 0);
+  }
+  void mark_run(uint32_t first, uint32_t count) {
+    track_queue();
+    for (uint32_t q = first; q < first + count; ++q) {
+      qmode[q] = 1;
+      assumed_in[q] = epoch;
+    }
+  }
+  // Current placement of queue pod q (-1 none), from the mirror or the device summary.
+  int32_t placement(uint32_t q, const ksg_pod_summary* sum) const {
+    if (qmode[q] == 2) return placed[q];
+    if (qmode[q] == 1 && sum) return sum->status == 0 ? sum->selected : -1;
+    return -1;
+  }
+  bool vocab_grows(const Pod& p) const {
+    if (nss.get(p.ns) < 0) return true;
+    for (auto& kv : p.labels) {
+      int32_t k = pkeys.get(kv.first);
+      if (k < 0 || k >= (int32_t)pvals.size() || pvals[k].get(kv.second) < 0) return true;
+    }
+    for (auto* v : {&p.req_aff, &p.req_anti, &p.pref_aff, &p.pref_anti})
+      for (auto& t : *v)
+        if (topo.get(t.topo) < 0) return true;
+    for (auto& c : p.tsc)
+      if (topo.get(c.key) < 0) return true;
+    for (auto& kv : p.req)
+      if (scalar_name(kv.first) && res.get(kv.first) < 0) return true;
+    return false;
+  }
+  // Re-encode and re-upload the snapshot with every assumed queue pod as a bound
+  // pod, recompile the queue, and restore the per-pod summaries.
+  bool rebuild() {
+    track_queue();
+    size_t nq = queue.size();
+    const size_t ns = compiled ? progs.size() : 0;  // pods with programs (and summaries) on the device
+    vector<ksg_pod_summary> sum(nq);
+    if (ns && !eng->summaries(0, (uint32_t)ns, sum.data(), err)) return false;
+    vector<Pod> saved = bound;
+    for (size_t q = 0; q < nq; ++q) {
+      int32_t at = placement((uint32_t)q, q < ns ? &sum[q] : nullptr);
+      if (at < 0 || at >= (int32_t)nodes.size()) continue;
+      Pod x = queue[q];
+      x.node = nodes[at].name;
+      bound.push_back(x);
+    }
+    nkeys = Dict(); nvals.clear(); pkeys = Dict(); pvals.clear(); nss = Dict();
+    taint_id.clear(); taints.clear(); topo = Dict();
+    bool ok = build_vocab();
+    NodeSoA S;
+    PodTableSoA T;
+    ok = ok && encode_snapshot(S, T);
+    if (ok) {
+      size_t qterms = 0, qreqs = 0, qvals = 0;
+      for (auto& p : queue) {
+        vector<ksg_exist_term> et;
+        vector<ksg_req> rq;
+        vector<int32_t> vl, tp;
+        append_terms(p, 0, et, tp, rq, vl);
+        qterms += et.size();
+        qreqs += rq.size();
+        qvals += vl.size();
+      }
+      const uint32_t slack = 1024;  // room for cycle pods assumed before the next rebuild
+      ok = eng->upload(S, T, T.n + (uint32_t)nq + slack, (uint32_t)(T.terms.size() + qterms + 4 * slack),
+                       (uint32_t)(T.reqs.size() + qreqs + 8 * slack), (uint32_t)(T.vals.size() + qvals + 16 * slack), err);
+    }
+    bound.swap(saved);
+    if (!ok) return false;
+    compiled = false;
+    if (!compile_queue()) return false;
+    if (ns && !eng->set_summaries(0, (uint32_t)ns, sum.data(), err)) return false;
+    ++epoch;
+    return true;
+  }
+  // One scheduling cycle of a new pod (appended to the queue).
+  bool cycle(const char* js, size_t len, bool commit, ksg_pod_summary& out) {
+    if (shards != 1) { err = "the cycle API needs an unsharded context"; return false; }
+    if (!compile_queue()) return false;
+    try {
+      docs.emplace_back(new J(json::parse(js, len)));
+    } catch (std::exception& e) {
+      err = e.what();
+      return false;
+    }
+    const J& d = *docs.back();
+    queue.push_back(parse_pod(d["pod"] ? *d["pod"] : d));
+    track_queue();
+    uint32_t q = (uint32_t)queue.size() - 1;
+    qmode[q] = 2;
+    if (vocab_grows(queue[q])) {
+      if (!rebuild()) return false;
+    } else {
+      vector<uint8_t> blob;
+      PodMeta m;
+      if (!compile(queue[q], (int32_t)q, blob, m)) return false;
+      if (!eng->append_program(blob, err)) return false;
+      progs.push_back(std::move(blob));
+      meta.push_back(std::move(m));
+    }
+    if (!eng->keep_outputs(q, 1, err) || !eng->run_queue(q, 1, commit, err) || !eng->sync(err) ||
+        !eng->summaries(q, 1, &out, err))
+      return false;
+    if (commit && out.status == 0) {
+      placed[q] = out.selected;
+      assumed_in[q] = epoch;
+      if (!check_table()) return false;
+    }
+    return true;
+  }
+  // The device appends assumed pods to its existing-pod table; when that is full
+  // the snapshot is re-encoded from the mirror (with fresh slack).
+  bool check_table() {
+    bool full = false;
+    if (!eng->table_overflow(full, err)) return false;
+    return full ? rebuild() : true;
+  }
+  bool reserve(uint32_t q, int32_t node) {
+    track_queue();
+    if (q >= queue.size() || qmode[q] != 2 || placed[q] >= 0) { err = "reserve: pod not in an uncommitted cycle"; return false; }
+    if (node < 0 || node >= (int32_t)nodes.size()) { err = "reserve: node out of range"; return false; }
+    if (!eng->assume(q, node, +1, err)) return false;
+    placed[q] = node;
+    assumed_in[q] = epoch;
+    return check_table();
+  }
+  bool unreserve(uint32_t q) {
+    track_queue();
+    if (q >= queue.size()) { err = "unreserve: pod out of range"; return false; }
+    ksg_pod_summary sm;
+    if (qmode[q] == 1 && !eng->summaries(q, 1, &sm, err)) return false;
+    int32_t at = placement(q, qmode[q] == 1 ? &sm : nullptr);
+    if (at < 0) { err = "unreserve: pod is not assumed"; return false; }
+    qmode[q] = 2;
+    placed[q] = -1;
+    if (assumed_in[q] == epoch) return eng->assume(q, at, -1, err);
+    return rebuild();  // assumed before the last rebuild: it is a bound pod of the snapshot now
+  }
 
   bool compile_queue() {
     if (compiled) return true;
@@ -1393,6 +1549,7 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   }
   if (!c.compile_queue()) return ctx->fail(c.err, KSG_E_INVALID);
   if (!c.eng->run_queue(first, count, true, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
+  c.mark_run(first, count);
   return KSG_OK;
 }
 
@@ -1509,8 +1666,34 @@ int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples) {
 }
 
 int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_pod_result* out) {
-  (void)ctx; (void)pod_json; (void)len; (void)commit; (void)out;
-  return KSG_E_STATE;  // implemented by the cycle API (next step)
+  if (!ctx || !pod_json) return KSG_E_INVALID;
+  ksg_pod_summary s;
+  try {
+    if (!ctx->c.cycle(pod_json, len, commit != 0, s)) return ctx->fail(ctx->c.err, KSG_E_STATE);
+  } catch (std::exception& e) {
+    return ctx->fail(e.what(), KSG_E_INVALID);
+  }
+  if (out) {
+    out->selected = s.selected;
+    out->feasible = s.feasible;
+    out->status = s.status;
+    out->skip_filter = s.skip_filter;
+    out->skip_score = s.skip_score;
+    out->total = (int32_t)(s.best_key >> 40);
+  }
+  return KSG_OK;
+}
+
+int ksg_reserve(ksg_ctx* ctx, uint32_t q, int32_t node) {
+  if (!ctx) return KSG_E_INVALID;
+  if (!ctx->c.reserve(q, node)) return ctx->fail(ctx->c.err, KSG_E_STATE);
+  return KSG_OK;
+}
+
+int ksg_unreserve(ksg_ctx* ctx, uint32_t q) {
+  if (!ctx) return KSG_E_INVALID;
+  if (!ctx->c.unreserve(q)) return ctx->fail(ctx->c.err, KSG_E_STATE);
+  return KSG_OK;
 }
 
 int ksg_node_requested(ksg_ctx* ctx, int64_t* requested, int32_t* pod_count, uint32_t n_res, uint32_t n) {

@@ -181,6 +181,7 @@ typedef struct ksg_prog {
 #define KEF_TERMINATING (1u << 0)
 #define KEF_WITH_AFFINITY (1u << 1)
 #define KEF_REQ_ANTI (1u << 2)
+#define KEF_DELETED (1u << 3)      // unreserved: ignored by every scan
 
 // per-pod cycle summary written by the device (read back by the host)
 typedef struct ksg_pod_summary {

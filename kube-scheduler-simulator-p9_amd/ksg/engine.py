@@ -68,6 +68,9 @@ def load_library():
     L.ksg_batch_path.argtypes = [vp]
     L.ksg_kernel_time.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32)]
     L.ksg_node_requested.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i32), u32, u32]
+    L.ksg_cycle.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_int, ctypes.c_void_p]
+    L.ksg_reserve.argtypes = [vp, u32, i32]
+    L.ksg_unreserve.argtypes = [vp, u32]
     _lib = L
     return L
 
@@ -156,6 +159,21 @@ class Scheduler:
 
     def reset(self):
         self._chk(self.L.ksg_reset(self.h), "ksg_reset")
+
+    def cycle(self, pod, commit=True):
+        """One drop-in scheduling cycle for a new pod (v1.Pod dict); returns
+        (queue index, PodResult).  commit=False leaves the assume to reserve()."""
+        b = (pod if isinstance(pod, (bytes, str)) else json.dumps(pod))
+        b = b.encode() if isinstance(b, str) else b
+        r = _PodResult()
+        self._chk(self.L.ksg_cycle(self.h, b, len(b), 1 if commit else 0, ctypes.byref(r)), "ksg_cycle")
+        return self.queue_len - 1, PodResult(r.selected, r.feasible, r.status, r.total)
+
+    def reserve(self, q, node):
+        self._chk(self.L.ksg_reserve(self.h, q, node), "ksg_reserve")
+
+    def unreserve(self, q):
+        self._chk(self.L.ksg_unreserve(self.h, q), "ksg_unreserve")
 
     def sample_kernel(self, every):
         self._chk(self.L.ksg_sample_kernel(self.h, every), "ksg_sample_kernel")

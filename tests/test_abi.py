@@ -17,7 +17,8 @@ def declared():
 def test_header_declares_entry_points():
     names = declared()
     for must in ("ksg_create", "ksg_load_cluster", "ksg_schedule_queue", "ksg_pod_results",
-                 "ksg_annotations", "ksg_filter_codes", "ksg_scores", "ksg_cycle"):
+                 "ksg_annotations", "ksg_filter_codes", "ksg_scores", "ksg_cycle", "ksg_reserve",
+                 "ksg_unreserve"):
         assert must in names
 
 

@@ -1,0 +1,117 @@
+"""GPU parity of the drop-in cycle API (ksg_cycle / ksg_reserve / ksg_unreserve).
+
+The per-pod path a Go plugin would take (PreFilter..NormalizeScore per pod,
+Reserve with the framework's choice, Unreserve on a failed binding) must give
+exactly the queue-mode / oracle results: same selection, feasible count and
+annotations for every pod.
+"""
+import copy
+
+import pytest
+
+from _oracle import Oracle
+from ksg import Scheduler, generator as g
+
+CASES = [
+    ("cfg2", 2, dict(n_nodes=200, n_pods=120)),
+    ("cfg3", 3, dict(n_nodes=200, n_pods=80)),
+    ("cfg4", 4, dict(n_nodes=160, n_existing=600, n_pods=60, n_zones=6)),
+]
+
+
+def _empty_queue(doc):
+    d = dict(doc)
+    d["queue"] = []
+    return d
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
+def test_cycle_matches_oracle(name, c, sizes):
+    doc = g.generate(c, **sizes)
+    o = Oracle(doc)
+    o.schedule(record=3)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(_empty_queue(doc))
+    for i, pod in enumerate(doc["queue"]):
+        q, r = s.cycle(pod, commit=True)
+        assert q == i
+        assert (r.selected, r.feasible, r.status) == o.result(i), (name, i)
+        if i % 7 == 0:
+            a, b = s.annotations(q), o.annotations(i)
+            for k in b:
+                assert a.get(k) == b[k], (name, i, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
+def test_reserve_with_framework_choice(name, c, sizes):
+    """commit=0 then Reserve on the engine's own choice == commit=1."""
+    doc = g.generate(c, **sizes)
+    o = Oracle(doc)
+    o.schedule(record=0)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(_empty_queue(doc))
+    for i, pod in enumerate(doc["queue"]):
+        q, r = s.cycle(pod, commit=False)
+        assert (r.selected, r.feasible, r.status) == o.result(i), (name, i)
+        if r.selected >= 0:
+            s.reserve(q, r.selected)
+
+
+def _blocker(pod):
+    """A copy of `pod` no node can hold: its cycle assumes nothing in the oracle."""
+    p = copy.deepcopy(pod)
+    p["metadata"]["name"] = p["metadata"]["name"] + "-blocked"
+    p["spec"]["containers"] = [{"name": "c0", "image": "registry.k8s.io/pause:3.5",
+                                "resources": {"requests": {"cpu": "100000", "memory": "1Gi"}}}]
+    return p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
+def test_unreserve_restores_state(name, c, sizes):
+    """Every 5th pod is assumed then unreserved; the others must match an oracle
+    run in which those pods were unschedulable (same queue indices)."""
+    doc = g.generate(c, **sizes)
+    ref = copy.deepcopy(doc)
+    ref["queue"] = [(_blocker(p) if i % 5 == 2 else p) for i, p in enumerate(doc["queue"])]
+    o = Oracle(ref)
+    o.schedule(record=0)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(_empty_queue(doc))
+    for i, pod in enumerate(doc["queue"]):
+        q, r = s.cycle(pod, commit=True)
+        if i % 5 == 2:
+            if r.selected >= 0:
+                s.unreserve(q)
+            continue
+        assert (r.selected, r.feasible, r.status) == o.result(i), (name, i)
+
+
+@pytest.mark.gpu
+def test_cycle_new_vocabulary_rebuilds():
+    """Pods bringing label keys/values and namespaces the snapshot never saw force a
+    re-encode (placements kept): results stay equal to the oracle's.  An Unreserve of
+    a pod assumed before those rebuilds then takes exactly its requests off its node."""
+    doc = g.generate(4, n_nodes=120, n_existing=400, n_pods=40, n_zones=4)
+    for i, p in enumerate(doc["queue"]):
+        if i % 6 == 3:
+            p["metadata"]["labels"] = dict(p["metadata"]["labels"], **{f"fresh-{i}": f"v{i}"})
+        if i % 11 == 5:
+            p["metadata"]["namespace"] = f"ns-new-{i}"
+    o = Oracle(doc)
+    o.schedule(record=0)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(_empty_queue(doc))
+    for i, pod in enumerate(doc["queue"]):
+        q, r = s.cycle(pod, commit=True)
+        assert (r.selected, r.feasible, r.status) == o.result(i), i
+    sel1 = s.results(1, 1)[0].selected
+    assert sel1 >= 0
+    req0, pc0 = s.node_requested()
+    s.unreserve(1)
+    req1, pc1 = s.node_requested()
+    assert pc0[sel1] - pc1[sel1] == 1
+    assert sum(pc0) - sum(pc1) == 1
+    assert req0[0][sel1] - req1[0][sel1] > 0 or req0[1][sel1] - req1[1][sel1] > 0

@@ -99,6 +99,14 @@ int ksg_queue_len(const ksg_ctx* ctx);
  * (no host round trip per pod).  Asynchronous: ksg_wait() completes it. */
 int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count);
 int ksg_wait(ksg_ctx* ctx, float* device_ms);
+/* What-if step (BASELINE cfg5): queue pods [first, first+count) are each
+ * scheduled against the SAME snapshot (no assume between them: the question
+ * "where would each of these pods go now?"), then all their placements are
+ * bound together.  Profiles of NodeResourcesFit, BalancedAllocation,
+ * TaintToleration and NodeAffinity; sharded contexts reduce the per-pod
+ * feasible counts, normaliser max/min and argmax keys across ranks.
+ * Asynchronous like ksg_schedule_queue; results via ksg_pod_results. */
+int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count);
 int ksg_pod_results(ksg_ctx* ctx, uint32_t first, uint32_t count, ksg_pod_result* out);
 
 /* Restore node rows and the existing-pod table to the loaded snapshot

@@ -93,6 +93,9 @@ class Engine {
   // Run pods [first, first+count) of the program list back to back on the device
   // (device-side assume).  keep: store per-pair outputs for pods [keep_first, keep_first+keep_n).
   bool run_queue(uint32_t first, uint32_t count, bool commit, std::string& err);
+  // What-if step: pods [first, first+count) each against the current snapshot,
+  // then all their placements bound (Fit/BA/Taint/NodeAffinity profiles).
+  bool run_whatif(uint32_t first, uint32_t count, std::string& err);
   bool keep_outputs(uint32_t keep_first, uint32_t keep_n, std::string& err);
   bool summaries(uint32_t first, uint32_t count, ksg_pod_summary* out, std::string& err);
   bool outputs(uint32_t prog_idx, PodOutputs& out, std::string& err);

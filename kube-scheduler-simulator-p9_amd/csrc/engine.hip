@@ -988,6 +988,192 @@ __global__ void k_assume(DevCluster C, const uint8_t* prog, int32_t gnode, int s
   assume_pod(C, V, n, sign, table != 0, prow);
 }
 
+// ----------------------------------------------------------------- what-if batches (cfg5)
+// A step of `count` queue pods is scheduled against ONE frozen snapshot (no
+// assume between them), then all placements are bound together
+// (BASELINE.json cfg5; oracle: ksg_oracle_whatif).  Profiles of NodeResourcesFit,
+// BalancedAllocation, TaintToleration and NodeAffinity.  Two passes over the
+// (pod tile x node tile) grid:
+//   k_whatif<1>  filter chain + the raw scores of the normalised plugins:
+//                per-pod feasible count and max/min (DefaultNormalizeScore input)
+//   k_whatif<2>  filter chain + all scores, NormalizeScore, weights, packed key:
+//                per-pod argmax (atomicMax of the 64-bit key)
+// A block holds KSG_WI_PODS pods (program headers through the scalar cache) x
+// KSG_WI_NPT * 256 nodes; every node row is read from HBM once per pod tile and
+// served from L1/L2 for the tile's pods.  Per-pod reductions: wave DPP, then one
+// atomic per wave.  Per-pair outputs are written only for the kept pods (the
+// sampled parity subset).
+#define KSG_WI_PODS 32
+#define KSG_WI_NPT 4
+struct WiArgs {
+  const uint8_t* progs;
+  const uint64_t* prog_off;
+  uint32_t q0, count;
+  ksg_pod_summary* sums;
+  uint32_t keep_first, keep_n;
+  uint32_t* kfilter;
+  int32_t *kscore, *ktotal;
+};
+
+template <int PASS>
+__global__ __launch_bounds__(256) void k_whatif(DevCluster C, DevProfile F, WiArgs A) {
+  const uint32_t base = blockIdx.x * (256 * KSG_WI_NPT) + threadIdx.x;
+#pragma unroll 1
+  for (uint32_t pi = 0; pi < KSG_WI_PODS; ++pi) {
+    const uint32_t j = blockIdx.y * KSG_WI_PODS + pi;
+    if (j >= A.count) break;
+    const uint32_t q = A.q0 + j;
+    const ProgView V = view(A.progs + A.prog_off[q]);
+    const ksg_prog* h = V.h;
+    ksg_pod_summary* sm = A.sums + q;
+    const bool kept = A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n;
+    const size_t slot = kept ? q - A.keep_first : 0;
+    int32_t feas_all = 0;
+    if (PASS == 2) feas_all = sm->feasible;
+    int cnt = 0;
+    uint64_t best = 0;
+    bool range_err = false;
+    int64_t mx[KSG_MAX_PLUGINS], mn[KSG_MAX_PLUGINS];
+#pragma unroll
+    for (int p = 0; p < KSG_MAX_PLUGINS; ++p) {
+      mx[p] = INT64_MIN;
+      mn[p] = INT64_MAX;
+    }
+#pragma unroll 1
+    for (int k = 0; k < KSG_WI_NPT; ++k) {
+      const uint32_t n = base + k * 256;
+      if (n >= C.N || (h->flags & KPF_PREFILTER_REJECT) ||
+          ((h->flags & KPF_RESTRICT) && !bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n))) {
+        if (PASS == 2 && kept && n < C.N) A.kfilter[slot * C.N + n] = KSG_FILTER_NOT_EVALUATED;
+        continue;
+      }
+      uint32_t code = KSG_FILTER_PASS;
+#pragma unroll 1
+      for (int pos = 0; pos < F.n && code == KSG_FILTER_PASS; ++pos) {
+        switch (F.plugins[pos]) {
+          case KP_FIT: {
+            uint32_t b = fit_filter(C, V, n);
+            if (b) code = ((uint32_t)pos << 24) | b;
+            break;
+          }
+          case KP_TAINT: {
+            int32_t t = untolerated_taint(C, V, n);
+            if (t >= 0) code = ((uint32_t)pos << 24) | ((uint32_t)t & 0xFFFFFFu);
+            break;
+          }
+          case KP_NA:
+            if (!(h->flags & KPF_SKIP_NA_FILTER) && !required_na(C, V, n)) code = (uint32_t)pos << 24;
+            break;
+          default: break;
+        }
+      }
+      if (PASS == 2 && kept) A.kfilter[slot * C.N + n] = code;
+      if (code != KSG_FILTER_PASS) continue;
+      ++cnt;
+      int64_t tot = 0;
+#pragma unroll 1
+      for (int pos = 0; pos < F.n; ++pos) {
+        const int p = F.plugins[pos];
+        int64_t s = 0;
+        if (PASS == 1 && p != KP_TAINT && p != KP_NA) continue;
+        switch (p) {
+          case KP_FIT: s = fit_score(C, F, V, n); break;
+          case KP_BA: s = ba_score(C, F, V, n); break;
+          case KP_TAINT: s = taint_score(C, V, n); break;
+          case KP_NA: s = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n); break;
+          default: break;
+        }
+        if (PASS == 1) {
+          mx[pos] = s > mx[pos] ? s : mx[pos];
+          mn[pos] = s < mn[pos] ? s : mn[pos];
+          continue;
+        }
+        if (kept) A.kscore[(slot * KSG_MAX_PLUGINS + pos) * C.N + n] = (int32_t)s;
+        const int64_t M = sm->max_score[pos];
+        if (p == KP_TAINT) s = M == 0 ? 100 : 100 - 100 * s / M;  // DefaultNormalizeScore(reverse)
+        else if (p == KP_NA) s = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : (M == 0 ? s : 100 * s / M);
+        if (s < 0 || s > 100) range_err = true;
+        tot += s * F.weight[pos];
+      }
+      if (PASS == 2) {
+        if (feas_all == 1) tot = 0;  // single feasible node: no scoring
+        if (kept) A.ktotal[slot * C.N + n] = (int32_t)tot;
+        uint64_t key = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
+        best = key > best ? key : best;
+      }
+    }
+    if (PASS == 1) {
+      int c = wave_sum(cnt);
+      if (lane0() && c) atomicAdd(&sm->feasible, c);
+#pragma unroll 1
+      for (int pos = 0; pos < F.n; ++pos) {
+        if (F.plugins[pos] != KP_TAINT && F.plugins[pos] != KP_NA) continue;
+        int64_t a = wave_max(mx[pos]), b = wave_min(mn[pos]);
+        if (lane0() && c) {
+          atomicMax((long long*)&sm->max_score[pos], (long long)a);
+          atomicMin((long long*)&sm->min_score[pos], (long long)b);
+        }
+      }
+    } else {
+      uint64_t b = wave_max(best);
+      if (lane0() && b) atomicMax((unsigned long long*)&sm->best_key, (unsigned long long)b);
+      if (feas_all > 1 && __any(range_err) && lane0()) atomicOr((uint32_t*)&sm->status, 2u);
+    }
+  }
+}
+
+// selectHost result per pod of the step (no assume yet)
+__global__ void k_whatif_select(WiArgs A) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= A.count) return;
+  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[A.q0 + j]);
+  ksg_pod_summary* s = A.sums + A.q0 + j;
+  if (h->flags & KPF_PREFILTER_ERROR) s->status |= 2;
+  if (s->status & 2) { s->status = 2; s->selected = -1; return; }
+  if (s->feasible == 0) { s->status = 1; s->selected = -1; return; }
+  s->selected = (int32_t)(s->best_key & 0xFFFFFull);
+  s->status = 0;
+}
+
+// Bind the step's placements (resource rows; sums commute, so in parallel).
+__global__ void k_whatif_bind(DevCluster C, WiArgs A) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= A.count) return;
+  const ksg_pod_summary* s = A.sums + A.q0 + j;
+  if (s->status != 0) return;
+  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[A.q0 + j]);
+  uint32_t g = (uint32_t)s->selected, n = g - C.goff;
+  if (g < C.goff || n >= C.N) return;  // another shard owns the node
+  for (uint32_t r = 0; r < C.R; ++r)
+    atomicAdd((unsigned long long*)&C.req[(size_t)r * C.N + n], (unsigned long long)h->req[r]);
+  atomicAdd((unsigned long long*)&C.nzc[n], (unsigned long long)h->nz_cpu);
+  atomicAdd((unsigned long long*)&C.nzm[n], (unsigned long long)h->nz_mem);
+  atomicAdd(&C.podcnt[n], 1);
+}
+
+// Sharded steps: merge the ranks' summaries of the step's pods
+// (phase 1: feasible counts and score max/min; phase 2: argmax key, status bits).
+__global__ void k_whatif_merge(const ksg_pod_summary* recv, uint32_t ranks, uint32_t count, ksg_pod_summary* sums,
+                               int phase) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= count) return;
+  ksg_pod_summary m = recv[j];
+  for (uint32_t r = 1; r < ranks; ++r) {
+    const ksg_pod_summary& o = recv[(size_t)r * count + j];
+    if (phase == 1) {
+      m.feasible += o.feasible;
+      for (int p = 0; p < KSG_MAX_PLUGINS; ++p) {
+        m.max_score[p] = o.max_score[p] > m.max_score[p] ? o.max_score[p] : m.max_score[p];
+        m.min_score[p] = o.min_score[p] < m.min_score[p] ? o.min_score[p] : m.min_score[p];
+      }
+    } else {
+      m.best_key = o.best_key > m.best_key ? o.best_key : m.best_key;
+      m.status |= o.status;
+    }
+  }
+  sums[j] = m;
+}
+
 // ----------------------------------------------------------------- speculative window path
 // For profiles whose plugins are all NodeResourcesFit / BalancedAllocation (no
 // ScoreExtensions, no cross-node state) a pod's result on node n depends only on
@@ -2381,6 +2567,86 @@ static PodLite pod_lite(const std::vector<uint8_t>& prog) {
   q.queue_idx = h->queue_idx;
   q.flags = h->flags;
   return q;
+}
+
+static bool exchange(Engine::Impl& I, const void* src, size_t bytes, std::string& err);
+
+bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
+  Impl& I = *p_;
+  if (I.has_pts || I.has_ipa) {
+    err = "what-if steps support NodeResourcesFit / BalancedAllocation / TaintToleration / NodeAffinity profiles";
+    return false;
+  }
+  if (first + count > I.prog_off.size()) { err = "program index out of range"; return false; }
+  hipStream_t s = I.stream;
+  DevCluster C = I.cluster();
+  WiArgs A{};
+  A.progs = I.progs.p;
+  A.prog_off = I.prog_off_d.p;
+  A.q0 = first;
+  A.count = count;
+  A.sums = I.sums.p;
+  A.keep_first = I.keep_first;
+  A.keep_n = I.keep_n;
+  A.kfilter = I.kfilter.p;
+  A.kscore = I.kscore.p;
+  A.ktotal = I.ktotal.p;
+  if (I.sample_every) {
+    while (I.sev.size() < 4) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      I.sev.push_back(e);
+    }
+  }
+  I.n_samples = 0;
+  HIPCHK(hipEventRecord(I.ev0, s));
+  if (count) {
+    const dim3 grid(std::max<uint32_t>((I.N + 256 * KSG_WI_NPT - 1) / (256 * KSG_WI_NPT), 1),
+                    (count + KSG_WI_PODS - 1) / KSG_WI_PODS);
+    const dim3 pods((count + 255) / 256);
+    const size_t xb = (size_t)count * sizeof(ksg_pod_summary);
+    hipLaunchKernelGGL(k_init_summaries, pods, dim3(256), 0, s, I.sums.p + first, count, I.F);
+    for (int pass = 1; pass <= 2; ++pass) {
+      const bool sampled = I.sample_every != 0;
+      if (sampled) HIPCHK(hipEventRecord(I.sev[2 * (pass - 1)], s));
+      if (pass == 1) hipLaunchKernelGGL(k_whatif<1>, grid, dim3(256), 0, s, C, I.F, A);
+      else hipLaunchKernelGGL(k_whatif<2>, grid, dim3(256), 0, s, C, I.F, A);
+      if (sampled) {
+        HIPCHK(hipEventRecord(I.sev[2 * (pass - 1) + 1], s));
+        I.n_samples++;
+      }
+      if (I.xranks > 1) {  // per-pod partials of every shard -> global values on every rank
+        if (!exchange(I, I.sums.p + first, xb, err)) return false;
+        hipLaunchKernelGGL(k_whatif_merge, pods, dim3(256), 0, s, reinterpret_cast<const ksg_pod_summary*>(I.xrecv.p),
+                           I.xranks, count, I.sums.p + first, pass);
+      }
+    }
+    hipLaunchKernelGGL(k_whatif_select, pods, dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_whatif_bind, pods, dim3(256), 0, s, C, A);
+  }
+  HIPCHK(hipEventRecord(I.ev1, s));
+  HIPCHK(hipGetLastError());
+  return true;
+}
+
+// All-gather `bytes` from every rank into I.xrecv (rank order), on the engine stream.
+static bool exchange(Engine::Impl& I, const void* src, size_t bytes, std::string& err) {
+  hipStream_t s = I.stream;
+  if (!I.xsend.grow(bytes, 0, s, err) || !I.xrecv.grow(bytes * I.xranks, 0, s, err)) return false;
+  HIPCHK(hipMemcpyAsync(I.xsend.p, src, bytes, hipMemcpyDeviceToDevice, s));
+  if (I.xmode == 1) {
+    ncclResult_t nr = ncclAllGather(I.xsend.p, I.xrecv.p, bytes, ncclUint8, I.comm, s);
+    if (nr != ncclSuccess) { err = std::string("ncclAllGather: ") + ncclGetErrorString(nr); return false; }
+    return true;
+  }
+  if (I.hsend.size() < bytes) I.hsend.resize(bytes);
+  if (I.hrecv.size() < bytes * I.xranks) I.hrecv.resize(bytes * I.xranks);
+  HIPCHK(hipMemcpyAsync(I.hsend.data(), I.xsend.p, bytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (I.xfn(I.xuser, I.hsend.data(), I.hrecv.data(), bytes) != 0) { err = "exchange callback failed"; return false; }
+  HIPCHK(hipMemcpyAsync(I.xrecv.p, I.hrecv.data(), bytes * I.xranks, hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));  // the host buffers are reused by the next exchange
+  return true;
 }
 
 bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) {

@@ -1553,6 +1553,18 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   return KSG_OK;
 }
 
+int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count) {
+  if (!ctx) return KSG_E_INVALID;
+  Cluster& c = ctx->c;
+  if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
+  if (c.shards != 1 && c.eng->exchange_ranks() != c.shards)
+    return ctx->fail("sharded context: call ksg_set_exchange first", KSG_E_STATE);
+  if (!c.compile_queue()) return ctx->fail(c.err, KSG_E_INVALID);
+  if (!c.eng->run_whatif(first, count, c.err)) return ctx->fail(c.err, KSG_E_STATE);
+  c.mark_run(first, count);
+  return KSG_OK;
+}
+
 int ksg_wait(ksg_ctx* ctx, float* ms) {
   if (!ctx) return KSG_E_INVALID;
   if (!ctx->c.eng->sync(ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);

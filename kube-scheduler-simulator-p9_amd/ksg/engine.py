@@ -68,6 +68,7 @@ def load_library():
     L.ksg_batch_path.argtypes = [vp]
     L.ksg_kernel_time.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32)]
     L.ksg_node_requested.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i32), u32, u32]
+    L.ksg_whatif.argtypes = [vp, u32, u32]
     L.ksg_cycle.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_int, ctypes.c_void_p]
     L.ksg_reserve.argtypes = [vp, u32, i32]
     L.ksg_unreserve.argtypes = [vp, u32]
@@ -125,6 +126,12 @@ class Scheduler:
     def schedule(self, first=0, count=None, wait=True):
         count = self.queue_len - first if count is None else count
         self._chk(self.L.ksg_schedule_queue(self.h, first, count), "ksg_schedule_queue")
+        return self.wait() if wait else None
+
+    def whatif(self, first=0, count=None, wait=True):
+        """What-if step: pods [first, first+count) against one snapshot, then bound."""
+        count = self.queue_len - first if count is None else count
+        self._chk(self.L.ksg_whatif(self.h, first, count), "ksg_whatif")
         return self.wait() if wait else None
 
     def wait(self):

@@ -924,6 +924,10 @@ struct Cluster {
   std::mutex store_mu;
 
   // ---------------------------------------------------------------- assume
+  // What-if batches (BASELINE cfg5): every pod of a step is scheduled against the
+  // same snapshot; the step's placements are bound together afterwards.
+  bool defer_assume = false;
+  vector<std::pair<int, int>> deferred;
   void add_pod(int pi, int ni) {  // framework.NodeInfo.AddPod (+ calculateResource)
     NodeInfo& n = infos[ni];
     PodRecord& r = pods[pi];
@@ -1668,7 +1672,8 @@ struct Cluster {
     }
     r.selected = nodes[chosen].name;
     r.selected_idx = chosen;
-    add_pod(pi, chosen);  // assume
+    if (defer_assume) deferred.emplace_back(pi, chosen);  // what-if batch: bound after the step
+    else add_pod(pi, chosen);  // assume
     finish(qidx, pi, r, record);
   }
   unsigned long long pack_key(i64 total, int qidx, int ni) const {
@@ -1827,6 +1832,19 @@ int ksg_oracle_schedule(ksg_oracle* h, int n, int workers, int record) {
     h->c.schedule_one(q, h->c.queue[q], *h->pool, record);
     ++done;
   }
+  return done;
+}
+
+// What-if step: the next n queue pods each scheduled against the current
+// snapshot (no assume between them), then all their placements bound in queue
+// order.  Returns pods processed.
+int ksg_oracle_whatif(ksg_oracle* h, int n, int workers, int record) {
+  h->c.defer_assume = true;
+  h->c.deferred.clear();
+  int done = ksg_oracle_schedule(h, n, workers, record);
+  h->c.defer_assume = false;
+  for (auto& pn : h->c.deferred) h->c.add_pod(pn.first, pn.second);
+  h->c.deferred.clear();
   return done;
 }
 

@@ -25,6 +25,7 @@ def lib():
         L.ksg_oracle_num_nodes.argtypes = [ctypes.c_void_p]
         L.ksg_oracle_num_queue.argtypes = [ctypes.c_void_p]
         L.ksg_oracle_schedule.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.ksg_oracle_whatif.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.ksg_oracle_result.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.POINTER(ctypes.c_int)] * 3
         L.ksg_oracle_digest.restype = ctypes.c_ulonglong
         L.ksg_oracle_digest.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -59,6 +60,10 @@ class Oracle:
     def schedule(self, n=None, workers=1, record=3):
         n = self.n_queue if n is None else n
         return lib().ksg_oracle_schedule(self.h, n, workers, record)
+
+    def whatif(self, n, workers=1, record=0):
+        """What-if step: n pods against one snapshot, placements bound afterwards."""
+        return lib().ksg_oracle_whatif(self.h, n, workers, record)
 
     def result(self, q):
         s, f, st = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

@@ -1,0 +1,88 @@
+"""GPU parity of what-if steps (BASELINE.json cfg5: a step of pods scored against
+one frozen snapshot, placements bound between steps) against the oracle's
+ksg_oracle_whatif, single context and node-sharded (host exchange over gloo)."""
+import json
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+from _oracle import Oracle
+from ksg import Scheduler, generator as g
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STEP = 96
+
+
+def _oracle_steps(doc, steps, record=0, keep=0):
+    o = Oracle(doc)
+    for _ in range(steps):
+        o.whatif(STEP, record=record)
+    return o
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,sizes", [(5, dict(n_nodes=1500, n_pods=3 * STEP)), (2, dict(n_nodes=800, n_pods=2 * STEP))],
+                         ids=["cfg5", "cfg2"])
+def test_whatif_steps_match_oracle(c, sizes):
+    doc = g.generate(c, **sizes)
+    steps = len(doc["queue"]) // STEP
+    o = _oracle_steps(doc, steps, record=3)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    s.keep_outputs(STEP, 6)  # sampled parity subset: per-pair outputs / annotations of 6 pods of step 2
+    for k in range(steps):
+        s.whatif(k * STEP, STEP)
+    res = s.results()
+    bad = [(q, (r.selected, r.feasible, r.status), o.result(q)) for q, r in enumerate(res)
+           if (r.selected, r.feasible, r.status) != o.result(q)]
+    assert not bad, bad[:5]
+    for q in range(STEP, STEP + 6):
+        a, b = s.annotations(q), o.annotations(q)
+        for k in b:
+            assert a.get(k) == b[k], (q, k)
+    # bound placements: every scheduled pod's requests landed on its node
+    _, pc = s.node_requested()
+    assert sum(pc) == len(doc["pods"]) + sum(1 for r in res if r.status == 0)
+
+
+def _free_port():
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    p = sk.getsockname()[1]
+    sk.close()
+    return p
+
+
+def _sharded_worker(rank, world, port, doc_json, out):
+    sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ksg import Scheduler as S
+    doc = json.loads(doc_json)
+    s = S(doc["profile"], device=0, shard_rank=rank, shard_count=world)
+    s.set_exchange_host(world)
+    s.load_cluster(doc)
+    for k in range(len(doc["queue"]) // STEP):
+        s.whatif(k * STEP, STEP)
+    out[rank] = [(r.selected, r.feasible, r.status) for r in s.results()]
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_whatif_matches_oracle(world):
+    doc = g.generate(5, n_nodes=1200, n_pods=2 * STEP)
+    o = _oracle_steps(doc, 2)
+    want = [o.result(q) for q in range(o.n_queue)]
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_sharded_worker, args=(world, port, json.dumps(doc), out), nprocs=world, join=True)
+        for r in range(world):
+            assert out[r] == want, f"rank {r} differs"

@@ -95,6 +95,7 @@ struct DevProfile {
   int ipa_ignore_existing_pref;
   uint64_t seed;
   int pos_fit, pos_ba;  // profile positions (-1 absent)
+  int pos_taint, pos_na;
   int64_t w_fit, w_ba;
   // copies in device memory for run-time indexed loops (kernel-argument arrays
   // indexed at run time would be copied to scratch)
@@ -123,6 +124,9 @@ struct DevOut {
   int32_t* score;    // [n_plugins][N]
   int32_t* total;    // [N]
   ksg_pod_summary* sum;
+  uint32_t* arrive;  // block arrivals of the cycle's last kernel (its last block commits), or null
+  int mode;          // commit mode (k_commit)
+  int32_t* prow;     // existing-pod table row of the assumed pod
 };
 
 struct ProgView {
@@ -180,10 +184,13 @@ __device__ __forceinline__ int32_t node_vid(const DevCluster& C, int32_t key, ui
 
 // node selector requirement incl. Gt/Lt (numeric view of the value) and
 // matchFields metadata.name (KR_NAME_EQ / KR_NAME_NE on the global node index).
-__device__ bool node_req(const DevCluster& C, const ksg_req& r, const int32_t* vals, uint32_t n) {
+// v: the node's value id for r.key (loaded by the caller, so that the label
+// loads of a whole selector are in flight together instead of one per
+// requirement behind the previous one's compare).
+__device__ __forceinline__ bool node_req_v(const DevCluster& C, const ksg_req& r, const int32_t* vals, uint32_t n,
+                                           int32_t v) {
   if (r.op == KR_NAME_EQ) return (int64_t)(C.goff + n) == r.num;
   if (r.op == KR_NAME_NE) return (int64_t)(C.goff + n) != r.num;
-  int32_t v = node_vid(C, r.key, n);
   switch (r.op) {
     case KR_IN: return v >= 0 && in_list(v, vals + r.val_off, r.nvals);
     case KR_NOT_IN: return v < 0 || !in_list(v, vals + r.val_off, r.nvals);
@@ -198,6 +205,10 @@ __device__ bool node_req(const DevCluster& C, const ksg_req& r, const int32_t* v
     }
     default: return false;
   }
+}
+
+__device__ __forceinline__ bool node_req(const DevCluster& C, const ksg_req& r, const int32_t* vals, uint32_t n) {
+  return node_req_v(C, r, vals, n, node_vid(C, r.key, n));
 }
 
 __device__ bool node_sel(const DevCluster& C, const ProgView& V, const ksg_sel& s, uint32_t n) {
@@ -677,6 +688,25 @@ __global__ void k_pts_reduce(DevCluster C, DevScratch S, const uint8_t* prog) {
   }
 }
 
+__device__ void commit_cycle(DevCluster& C, const ProgView& V, ksg_pod_summary* s, int mode, int32_t* prow,
+                             bool fresh);
+// The cycle's last kernel: its last-arriving block resolves selectHost and the
+// assume (what k_commit does as a launch of its own).  Every wave's atomics on
+// the summary have completed (vmcnt(0) at the barrier) before its block
+// arrives; the last block re-reads them with atomic RMWs (coherence point).
+__device__ __forceinline__ void last_block_commit(DevCluster& C, const ProgView& V, const DevOut& O) {
+  __shared__ uint32_t last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t old = __hip_atomic_fetch_add(O.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __hip_atomic_store(O.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  commit_cycle(C, V, O.sum, O.mode, O.prow, true);
+}
+
 // Filter chain + raw scores (+ total/argmax when the profile has no ScoreExtensions).
 // Position loops are run-time loops (one copy of each plugin's code: the
 // instruction cache, not the loop overhead, is what limits this kernel); raw
@@ -736,7 +766,10 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
   unsigned long long bal = __ballot(feasible);
   if (lane0() && bal) atomicAdd(&O.sum->feasible, (int)__popcll(bal));
   if (__any(err) && lane0()) atomicOr((uint32_t*)&O.sum->status, 2u);
-  if (!bal) return;  // wave-uniform: no feasible node in this wave
+  if (!bal) {  // wave-uniform: no feasible node in this wave
+    if (O.arrive && !F.has_ext) last_block_commit(C, V, O);
+    return;
+  }
   int64_t tot = 0;
   bool range_err = false;
 #pragma unroll 1
@@ -787,6 +820,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
     if (lane0()) atomicMax((unsigned long long*)&O.sum->best_key, (unsigned long long)b);
     if (__any(range_err) && lane0()) atomicOr((uint32_t*)&O.sum->status, 2u);
   }
+  if (O.arrive && !F.has_ext) last_block_commit(C, V, O);
 }
 
 // topologyNormalizingWeight per score constraint
@@ -897,6 +931,7 @@ __global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, c
   if (O.sum->feasible > 1 && __any(range_err) && lane0()) atomicOr((uint32_t*)&O.sum->status, 2u);
   uint64_t b = wave_max(best);
   if (lane0() && b) atomicMax((unsigned long long*)&O.sum->best_key, (unsigned long long)b);
+  if (O.arrive) last_block_commit(C, V, O);
 }
 
 // assume (scheduleOne -> assume -> NodeInfo.AddPod, or its reversal for
@@ -962,21 +997,30 @@ __device__ void assume_pod(DevCluster& C, const ProgView& V, uint32_t n, int sig
 
 // selectHost result of the cycle; mode bit 0: assume on the selected node,
 // bit 1: also append the pod to the existing-pod table.
-__global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* prog, int mode, int32_t* prow) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  ProgView V = view(prog);
+// fresh: the summary was updated by atomics of other blocks of the running
+// kernel — read it back through atomic RMWs (performed at the coherence point).
+__device__ void commit_cycle(DevCluster& C, const ProgView& V, ksg_pod_summary* s, int mode, int32_t* prow,
+                             bool fresh) {
   const ksg_prog* h = V.h;
-  ksg_pod_summary* s = O.sum;
   *prow = -1;
-  if (h->flags & KPF_PREFILTER_ERROR) s->status |= 2;
-  if (s->status & 2) { s->status = 2; s->selected = -1; return; }
-  if (s->feasible == 0) { s->status = 1; s->selected = -1; return; }
-  uint32_t g = (uint32_t)(s->best_key & 0xFFFFFull);
+  int32_t status = fresh ? (int32_t)atomicOr((uint32_t*)&s->status, 0u) : s->status;
+  int32_t feasible = fresh ? atomicAdd(&s->feasible, 0) : s->feasible;
+  uint64_t best = fresh ? atomicMax((unsigned long long*)&s->best_key, 0ull) : s->best_key;
+  if (h->flags & KPF_PREFILTER_ERROR) status |= 2;
+  if (status & 2) { s->status = 2; s->selected = -1; return; }
+  if (feasible == 0) { s->status = 1; s->selected = -1; return; }
+  uint32_t g = (uint32_t)(best & 0xFFFFFull);
   s->selected = (int32_t)g;
   s->status = 0;
   uint32_t n = g - C.goff;
   if (!(mode & 1) || g < C.goff || n >= C.N) return;  // what-if, or another shard owns the node
   assume_pod(C, V, n, +1, (mode & 2) != 0, prow);
+}
+
+__global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* prog, int mode, int32_t* prow) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ProgView V = view(prog);
+  commit_cycle(C, V, O.sum, mode, prow, false);
 }
 
 // Reserve / Unreserve on an explicit node (the framework's selectHost choice).
@@ -1172,6 +1216,236 @@ __global__ void k_whatif_merge(const ksg_pod_summary* recv, uint32_t ranks, uint
     }
   }
   sums[j] = m;
+}
+
+
+// ----------------------------------------------------------------- static pre-pass (per-pod chain, Taint/NA profiles)
+// TaintToleration's and NodeAffinity's Filter and raw Score of a (pod, node)
+// pair depend only on the node's taints and labels, never on the pods assumed on
+// it.  So a chunk of queue pods gets them in one wide pass (k_static, same tiling
+// as the what-if kernels) and each pod's cycle is then ONE kernel (k_fs_static)
+// that reads an 8-B record per node instead of walking taints and label columns
+// through dependent loads.  NormalizeScore's max is taken over feasible nodes;
+// k_static provides the max over the statically feasible nodes (M), which is
+// the true max whenever one node reaching it is also Fit-feasible — counted per
+// cycle; otherwise the cycle's last block recomputes it (exact fallback).
+struct StaticRec {
+  uint32_t code;  // KSG_FILTER_PASS, KSG_FILTER_NOT_EVALUATED, or (pos << 24) | detail of the first failing static filter
+  uint32_t raw;   // raw TaintToleration score << 20 | raw NodeAffinity score
+};
+#define KSG_RAW_NA_MASK 0xFFFFFu
+
+__global__ __launch_bounds__(256) void k_static(DevCluster C, DevProfile F, const uint8_t* progs, const uint64_t* prog_off,
+                                                uint32_t q0, uint32_t count, StaticRec* out, int64_t* mpred) {
+  const uint32_t base = blockIdx.x * (256 * KSG_WI_NPT) + threadIdx.x;
+#pragma unroll 1
+  for (uint32_t pi = 0; pi < KSG_WI_PODS; ++pi) {
+    const uint32_t j = blockIdx.y * KSG_WI_PODS + pi;
+    if (j >= count) break;
+    const ProgView V = view(progs + prog_off[q0 + j]);
+    const ksg_prog* h = V.h;
+    const bool skip_na_score = (h->flags & KPF_SKIP_NA_SCORE) != 0;
+    int64_t mt = -1, ma = -1;
+#pragma unroll 1
+    for (int k = 0; k < KSG_WI_NPT; ++k) {
+      const uint32_t n = base + k * 256;
+      if (n >= C.N) continue;
+      uint32_t code = KSG_FILTER_PASS, raw = 0;
+      if ((h->flags & KPF_PREFILTER_REJECT) ||
+          ((h->flags & KPF_RESTRICT) && !bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n))) {
+        code = KSG_FILTER_NOT_EVALUATED;
+      } else {
+#pragma unroll 1
+        for (int pos = 0; pos < F.n && code == KSG_FILTER_PASS; ++pos) {
+          if (F.plugins[pos] == KP_TAINT) {
+            int32_t t = untolerated_taint(C, V, n);
+            if (t >= 0) code = ((uint32_t)pos << 24) | ((uint32_t)t & 0xFFFFFFu);
+          } else if (F.plugins[pos] == KP_NA) {
+            if (!(h->flags & KPF_SKIP_NA_FILTER) && !required_na(C, V, n)) code = (uint32_t)pos << 24;
+          }
+        }
+        if (code == KSG_FILTER_PASS) {
+          int64_t t = F.pos_taint >= 0 ? taint_score(C, V, n) : 0;
+          int64_t a = (F.pos_na >= 0 && !skip_na_score) ? na_score(C, V, n) : 0;
+          raw = ((uint32_t)t << 20) | ((uint32_t)a & KSG_RAW_NA_MASK);
+          mt = t > mt ? t : mt;
+          ma = a > ma ? a : ma;
+        }
+      }
+      out[(size_t)j * C.N + n] = StaticRec{code, raw};
+    }
+    int64_t a0 = wave_max(mt), a1 = wave_max(ma);
+    if (lane0()) {
+      if (a0 >= 0) atomicMax((long long*)&mpred[2 * j], (long long)a0);
+      if (a1 >= 0) atomicMax((long long*)&mpred[2 * j + 1], (long long)a1);
+    }
+  }
+}
+
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_sc1(int32_t* p, int32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ int32_t ld_sc1(const int32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// DefaultNormalizeScore of the two static plugins, weighted; raw Fit/BA scores given.
+__device__ __forceinline__ int64_t static_total(const DevProfile& F, bool skip_na_score, int64_t fit, int64_t ba,
+                                                int64_t t, int64_t a, int64_t MT, int64_t MA, bool& range_err) {
+  int64_t tot = 0;
+  for (int pos = 0; pos < F.n; ++pos) {
+    int64_t s = 0;
+    switch (F.plugins[pos]) {
+      case KP_FIT: s = fit; break;
+      case KP_BA: s = ba; break;
+      case KP_TAINT: s = MT == 0 ? 100 : 100 - 100 * t / MT; break;  // reverse
+      case KP_NA:
+        if (skip_na_score) continue;
+        s = MA == 0 ? a : 100 * a / MA;
+        break;
+      default: break;
+    }
+    if (s < 0 || s > 100) range_err = true;
+    tot += s * F.weight[pos];
+  }
+  return tot;
+}
+
+// One scheduling cycle of one pod for a profile of Fit/BA/Taint/NA (any order):
+// Filter chain in profile order, raw scores, NormalizeScore with the static max,
+// weighted total, packed-key argmax; the last block checks the max, falls back
+// to the exact max when no Fit-feasible node reaches it, and commits.
+// Per-pair outputs are stored sc1 (the fallback re-reads them in this kernel).
+__global__ __launch_bounds__(kBlock) void k_fs_static(DevCluster C, DevProfile F, DevOut O, const uint8_t* prog,
+                                                     const StaticRec* st, const int64_t* mp, int32_t* aux) {
+  // aux: [0] a feasible node reaches the static Taint max, [1] NodeAffinity, [2] a score out of range, [3] arrivals
+  __shared__ uint64_t red64[kBlock / 64];
+  __shared__ int64_t redm[2][kBlock / 64];
+  __shared__ uint32_t last;
+  const ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  const bool skip_na_score = (h->flags & KPF_SKIP_NA_SCORE) != 0;
+  const int64_t MT = mp[0] < 0 ? 0 : mp[0], MA = mp[1] < 0 ? 0 : mp[1];
+  const uint32_t N = C.N;
+  // one node: Filter chain in profile order (static part from the record), raw scores, total with (mt, ma)
+  auto eval = [&](uint32_t n, int64_t mt, int64_t ma, uint32_t& code, int64_t (&raw)[4], int64_t& tot, bool& re) {
+    const StaticRec r = st[n];
+    code = r.code;
+    if (code != KSG_FILTER_NOT_EVALUATED && F.pos_fit >= 0) {
+      const uint32_t spos = code == KSG_FILTER_PASS ? 0xFFu : code >> 24;
+      if ((uint32_t)F.pos_fit < spos) {
+        const uint32_t fb = fit_filter(C, V, n);
+        if (fb) code = ((uint32_t)F.pos_fit << 24) | fb;
+      }
+    }
+    if (code != KSG_FILTER_PASS) return;
+    raw[0] = F.pos_fit >= 0 ? fit_score(C, F, V, n) : 0;
+    raw[1] = F.pos_ba >= 0 ? ba_score(C, F, V, n) : 0;
+    raw[2] = r.raw >> 20;
+    raw[3] = skip_na_score ? 0 : (int64_t)(r.raw & KSG_RAW_NA_MASK);
+    tot = static_total(F, skip_na_score, raw[0], raw[1], raw[2], raw[3], mt, ma, re);
+  };
+  auto store = [&](uint32_t n, uint32_t code, const int64_t (&raw)[4], int64_t tot) {
+    O.filter[n] = code;
+    if (code != KSG_FILTER_PASS) return;
+    if (F.pos_fit >= 0) O.score[(size_t)F.pos_fit * N + n] = (int32_t)raw[0];
+    if (F.pos_ba >= 0) O.score[(size_t)F.pos_ba * N + n] = (int32_t)raw[1];
+    if (F.pos_taint >= 0) O.score[(size_t)F.pos_taint * N + n] = (int32_t)raw[2];
+    if (F.pos_na >= 0) O.score[(size_t)F.pos_na * N + n] = (int32_t)raw[3];
+    O.total[n] = (int32_t)tot;
+  };
+  const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t code = KSG_FILTER_NOT_EVALUATED;
+  int64_t raw[4] = {0, 0, 0, 0}, tot = 0;
+  bool range_err = false;
+  if (n < N) eval(n, MT, MA, code, raw, tot, range_err);
+  const bool feasible = n < N && code == KSG_FILTER_PASS;
+  const uint64_t best = feasible ? pack_key(tot, F.seed, h->queue_idx, C.goff + n) : 0;
+  // aggregates first (completed before this block arrives); the per-pair stores drain afterwards
+  const unsigned long long bal = __ballot(feasible);
+  const uint64_t bk = wave_max(best);
+  const bool at = __any(feasible && raw[2] == MT), aa = __any(feasible && raw[3] == MA), re = __any(range_err);
+  if (lane0()) {
+    if (bal) atomicAdd(&O.sum->feasible, (int)__popcll(bal));
+    if (bk) atomicMax((unsigned long long*)&O.sum->best_key, (unsigned long long)bk);
+    if (at) atomicOr(&aux[0], 1);
+    if (aa) atomicOr(&aux[1], 1);
+    if (re) atomicOr(&aux[2], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add((uint32_t*)&aux[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  if (n < N) store(n, code, raw, tot);
+  __syncthreads();
+  if (!last) return;
+  // ---- last block: the cycle's aggregates, read back in one round of atomic RMWs
+  __shared__ int64_t agg[8];
+  if (threadIdx.x < 6) {
+    int64_t v = 0;
+    switch (threadIdx.x) {
+      case 0: v = atomicAdd(&O.sum->feasible, 0); break;
+      case 1: v = atomicOr(&aux[0], 0); break;
+      case 2: v = atomicOr(&aux[1], 0); break;
+      case 3: v = atomicOr(&aux[2], 0); break;
+      case 4: v = (int64_t)atomicOr((uint32_t*)&O.sum->status, 0u); break;
+      case 5: v = (int64_t)atomicMax((unsigned long long*)&O.sum->best_key, 0ull); break;
+    }
+    agg[threadIdx.x] = v;
+  }
+  __syncthreads();
+  const int32_t feas_all = (int32_t)agg[0];
+  bool any_range = agg[3] != 0;
+  uint64_t best_all = (uint64_t)agg[5];
+  const bool need_t = F.pos_taint >= 0 && agg[1] == 0, need_a = F.pos_na >= 0 && !skip_na_score && agg[2] == 0;
+  int64_t mt = MT, ma = MA;
+  if (feas_all > 0 && (need_t || need_a)) {
+    // exact fallback (no Fit-feasible node reaches the static max): recompute the
+    // max over the feasible nodes, then every total and the argmax, from the rows
+    int64_t lt = 0, la = 0;
+    for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+      uint32_t c;
+      int64_t rw[4] = {0, 0, 0, 0}, t2 = 0;
+      bool e2 = false;
+      eval(i, MT, MA, c, rw, t2, e2);
+      if (c == KSG_FILTER_PASS) { lt = max(lt, rw[2]); la = max(la, rw[3]); }
+    }
+    lt = wave_max(lt);
+    la = wave_max(la);
+    if (lane0()) { redm[0][threadIdx.x >> 6] = lt; redm[1][threadIdx.x >> 6] = la; }
+    __syncthreads();
+    mt = ma = 0;
+    for (int w = 0; w < kBlock / 64; ++w) { mt = max(mt, redm[0][w]); ma = max(ma, redm[1][w]); }
+    uint64_t lb = 0;
+    bool lre = false;
+    for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+      uint32_t c;
+      int64_t rw[4] = {0, 0, 0, 0}, t2 = 0;
+      eval(i, mt, ma, c, rw, t2, lre);
+      if (c == KSG_FILTER_PASS) {
+        uint64_t key = pack_key(t2, F.seed, h->queue_idx, C.goff + i);
+        lb = key > lb ? key : lb;
+      }
+    }
+    lb = wave_max(lb);
+    lre = __any(lre);
+    if (lane0()) red64[threadIdx.x >> 6] = lb | (lre ? 0x8000000000000000ull : 0ull);
+    __syncthreads();
+    best_all = 0;
+    any_range = false;
+    for (int w = 0; w < kBlock / 64; ++w) {
+      uint64_t x = red64[w] & 0x7FFFFFFFFFFFFFFFull;
+      best_all = x > best_all ? x : best_all;
+      any_range |= (red64[w] >> 63) != 0;
+    }
+  }
+  if (threadIdx.x != 0) return;
+  if (F.pos_taint >= 0) O.sum->max_score[F.pos_taint] = mt;
+  if (F.pos_na >= 0) O.sum->max_score[F.pos_na] = skip_na_score ? 0 : ma;
+  int32_t status = (int32_t)agg[4];
+  if (feas_all > 1 && any_range) status |= 2;
+  O.sum->best_key = feas_all == 1 ? (best_all & 0xFFFFFFFFFFull) : best_all;  // one feasible node: not scored
+  O.sum->status = status;
+  O.sum->feasible = feas_all;
+  for (int i = 0; i < 4; ++i) aux[i] = 0;  // the next cycle's counters (ordered by the kernel boundary)
+  commit_cycle(C, V, O.sum, O.mode, O.prow, false);
 }
 
 // ----------------------------------------------------------------- speculative window path
@@ -2231,6 +2505,12 @@ struct Engine::Impl {
   DBuf<int32_t> score, total;
   DBuf<ksg_pod_summary> sums;
   DBuf<int32_t> prow;     // existing-pod table row of each assumed queue pod (-1 none)
+  DBuf<uint32_t> arrive1; // block arrivals of the per-pod chain's last kernel
+  bool static_ok = false; // per-pod cycles of Fit/BA/Taint/NA profiles: k_static + k_fs_static
+  bool static_fits = true; // raw scores fit the record (taints per node < 4096, NodeAffinity weights < 2^20)
+  DBuf<StaticRec> stat;   // static records of a chunk of pods [chunk][N]
+  DBuf<int64_t> mpred;    // [chunk][2] static max of the Taint / NodeAffinity raw scores
+  DBuf<int32_t> saux;     // k_fs_static counters
   size_t prog_bytes = 0;  // used bytes of the program blob
   // kept per-pair outputs
   uint32_t keep_first = 0, keep_n = 0;
@@ -2317,6 +2597,8 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   }
   HIPCHK(hipEventCreate(&I.ev0));
   HIPCHK(hipEventCreate(&I.ev1));
+  if (!I.arrive1.alloc(1, err)) return false;
+  HIPCHK(hipMemsetAsync(I.arrive1.p, 0, sizeof(uint32_t), I.stream));
   DevProfile& F = I.F;
   F.n = cfg.n_plugins;
   F.has_ext = 0;
@@ -2344,9 +2626,11 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   F.ipa_hard_weight = cfg.ipa_hard_weight;
   F.ipa_ignore_existing_pref = cfg.ipa_ignore_existing_pref;
   F.seed = cfg.seed;
-  F.pos_fit = F.pos_ba = -1;
+  F.pos_fit = F.pos_ba = F.pos_taint = F.pos_na = -1;
   F.w_fit = F.w_ba = 0;
   for (int i = 0; i < F.n; ++i) {
+    if (F.plugins[i] == KP_TAINT) F.pos_taint = i;
+    if (F.plugins[i] == KP_NA) F.pos_na = i;
     if (F.plugins[i] == KP_FIT) { F.pos_fit = i; F.w_fit = F.weight[i]; }
     if (F.plugins[i] == KP_BA) { F.pos_ba = i; F.w_ba = F.weight[i]; }
   }
@@ -2364,6 +2648,11 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
                       ? 1
                       : 0;
   }
+  I.static_ok = F.n > 0 && (F.pos_taint >= 0 || F.pos_na >= 0);
+  for (int i = 0; i < F.n; ++i)
+    I.static_ok &= (F.plugins[i] == KP_FIT || F.plugins[i] == KP_BA || F.plugins[i] == KP_TAINT || F.plugins[i] == KP_NA);
+  if (!I.saux.alloc(4, err)) return false;
+  HIPCHK(hipMemsetAsync(I.saux.p, 0, 4 * sizeof(int32_t), I.stream));
   I.batch_ok = F.n > 0;
   for (int i = 0; i < F.n; ++i) I.batch_ok &= (F.plugins[i] == KP_FIT || F.plugins[i] == KP_BA);
   return true;
@@ -2377,6 +2666,9 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   if (ns.n_res > KSG_MAX_RES) { err = "too many resources"; return false; }
   I.N = ns.n;
   I.goff = ns.global_offset;
+  I.static_fits = true;
+  for (uint32_t i = 0; i < ns.n; ++i)
+    if (ns.taint_off[i + 1] - ns.taint_off[i] >= 4096) I.static_fits = false;
   I.R = ns.n_res;
   I.K = ns.n_keys;
   if (!I.alloc.upload(ns.alloc, s, err) || !I.req.upload(ns.requested, s, err) || !I.nzc.upload(ns.nz_cpu, s, err) ||
@@ -2554,6 +2846,15 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   return true;
 }
 
+// The static record keeps the raw NodeAffinity score in 20 bits.
+static bool na_weights_fit(const std::vector<uint8_t>& prog) {
+  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
+  const int32_t* i32 = reinterpret_cast<const int32_t*>(prog.data() + h->off_i32);
+  int64_t sum = 0;
+  for (int t = 0; t < h->n_pref_terms; ++t) sum += i32[h->pref_w_off + t] > 0 ? i32[h->pref_w_off + t] : 0;
+  return sum <= (int64_t)KSG_RAW_NA_MASK;
+}
+
 static PodLite pod_lite(const std::vector<uint8_t>& prog) {
   const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
   PodLite q;
@@ -2669,6 +2970,7 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
   HIPCHK(hipStreamSynchronize(s));  // the host sources above are stack / caller buffers
   I.prog_bytes = off + prog.size();
   I.prog_off.push_back(off);
+  if (!na_weights_fit(prog)) I.static_fits = false;
   const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
   I.prog_need.push_back((h->n_tsc_filter + h->n_tsc_score > 0 ? 1u : 0u) | 2u);
   for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
@@ -2734,6 +3036,7 @@ bool Engine::set_programs(const std::vector<std::vector<uint8_t>>& progs, std::s
   for (auto& p : progs) {
     const ksg_prog* h = reinterpret_cast<const ksg_prog*>(p.data());
     for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
+    if (!na_weights_fit(p)) I.static_fits = false;
   }
   for (int i = 0; i < I.F.fit_n; ++i) I.any_eph_req |= I.F.fit_res[i] >= 2;
   for (int i = 0; i < I.F.ba_n; ++i) I.any_eph_req |= I.F.ba_res[i] >= 2;
@@ -2783,9 +3086,44 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   }
   I.n_samples = 0;
   HIPCHK(hipEventRecord(I.ev0, s));
+  if (I.static_ok && I.static_fits) {
+    const size_t Nn = std::max<uint32_t>(N, 1);
+    const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, ((size_t)64 << 20) / (Nn * sizeof(StaticRec))));
+    if (!I.stat.alloc((size_t)chunk * Nn, err) || !I.mpred.alloc(2 * (size_t)chunk, err)) return false;
+    for (uint32_t c0 = first; c0 < first + count; c0 += chunk) {
+      const uint32_t cn = std::min(chunk, first + count - c0);
+      HIPCHK(hipMemsetAsync(I.mpred.p, 0xFF, 2 * (size_t)cn * sizeof(int64_t), s));  // -1: no statically feasible node
+      const dim3 grid(std::max<uint32_t>((N + 256 * KSG_WI_NPT - 1) / (256 * KSG_WI_NPT), 1),
+                      (cn + KSG_WI_PODS - 1) / KSG_WI_PODS);
+      hipLaunchKernelGGL(k_static, grid, dim3(256), 0, s, C, F, I.progs.p, I.prog_off_d.p, c0, cn, I.stat.p, I.mpred.p);
+      for (uint32_t j = c0; j < c0 + cn; ++j) {
+        const uint8_t* prog = I.progs.p + I.prog_off[j];
+        const int mode = commit ? 1 : 0;
+        DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j, nullptr, mode, I.prow.p + j};
+        if (I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n) {
+          size_t k = j - I.keep_first;
+          O.filter = I.kfilter.p + k * N;
+          O.score = I.kscore.p + k * N * KSG_MAX_PLUGINS;
+          O.total = I.ktotal.p + k * N;
+        }
+        bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
+        if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
+        hipLaunchKernelGGL(k_fs_static, gN, b, 0, s, C, F, O, prog, I.stat.p + (size_t)(j - c0) * Nn,
+                           I.mpred.p + 2 * (size_t)(j - c0), I.saux.p);
+        if (sampled) {
+          HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
+          I.n_samples++;
+        }
+      }
+    }
+    HIPCHK(hipEventRecord(I.ev1, s));
+    HIPCHK(hipGetLastError());
+    return true;
+  }
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
-    DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j};
+    const int mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
+    DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j, I.arrive1.p, mode, I.prow.p + j};
     bool kept = I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n;
     if (kept) {
       size_t k = j - I.keep_first;
@@ -2822,8 +3160,7 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
       }
       hipLaunchKernelGGL(k_finalize, gN, b, 0, s, C, F, S, O, prog);
     }
-    const int mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
-    hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, s, C, F, O, prog, mode, I.prow.p + j);
+    // selectHost + assume: folded into the last block of the cycle's last kernel
   }
   HIPCHK(hipEventRecord(I.ev1, s));
   HIPCHK(hipGetLastError());

@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -1296,10 +1297,10 @@ __device__ __forceinline__ int64_t static_total(const DevProfile& F, bool skip_n
     switch (F.plugins[pos]) {
       case KP_FIT: s = fit; break;
       case KP_BA: s = ba; break;
-      case KP_TAINT: s = MT == 0 ? 100 : 100 - 100 * t / MT; break;  // reverse
+      case KP_TAINT: s = MT == 0 ? 100 : 100 - div_small(100 * t, MT); break;  // reverse; 0 <= t <= MT
       case KP_NA:
         if (skip_na_score) continue;
-        s = MA == 0 ? a : 100 * a / MA;
+        s = MA == 0 ? a : div_small(100 * a, MA);
         break;
       default: break;
     }
@@ -1476,7 +1477,7 @@ __global__ __launch_bounds__(kBlock) void k_fs_static(DevCluster C, DevProfile F
 #define KSG_WIN_THREADS 1024
 #define KSG_TILE KSG_WIN_THREADS  // nodes per eval block
 #define KSG_STAGE 16       // candidate ranks whose rows are staged in LDS (deeper ranks: global)
-#define KSG_XHDR 128       // record header: feasible count per pod (KSG_BATCH ints)
+#define KSG_XHDR 512       // record header: per pod feasible count, static-max achievers (Taint, NodeAffinity): 3 x KSG_BATCH ints
 #define KSG_NOT_PATCHED 0xFFFFFFFDu
 
 struct RowV {  // one node row (resource columns 0..3)
@@ -1525,7 +1526,15 @@ struct WinArgs {
   ksg_pod_summary* sums;
   uint64_t* stamps;      // diagnostic stamps of window W's fixup (16 slots), or null
   uint64_t* estamps;     // diagnostic stamps of window E's eval blocks (16 slots), or null
+  // profiles with TaintToleration / NodeAffinity: static records of a ring of
+  // stat_ring queue pods (pod q at slot (q - first) % stat_ring) and their static maxima
+  const StaticRec* stat;
+  uint32_t stat_ring;
+  const int64_t* mpred;  // [2 * (q - first)]: Taint, NodeAffinity (-1: no statically feasible node)
 };
+__device__ __forceinline__ const StaticRec* srec_row(const WinArgs& A, uint32_t q, uint32_t N) {
+  return A.stat + (size_t)((q - A.first) % A.stat_ring) * N;
+}
 __device__ __forceinline__ int64_t sel4(const int64_t (&v)[4], int i) {
   return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3];
 }
@@ -1670,12 +1679,42 @@ __device__ __forceinline__ uint32_t eval_row(const RowV& r, const DevProfile& F,
   }
   return KSG_FILTER_PASS;
 }
+// Fit/BA/Taint/NodeAffinity profiles: the static record of (pod, node) supplies
+// the Taint/NodeAffinity filter verdicts and raw scores; the Fit filter runs in
+// its profile position; NormalizeScore uses the pod's normaliser (MT, MA).
+template <int MODE, class P>
+__device__ __forceinline__ uint32_t eval_row_s(const RowV& r, const DevProfile& F, const P* h, uint32_t R, StaticRec s,
+                                               int64_t MT, int64_t MA, int32_t& fit_s, int32_t& ba_s, int64_t& total) {
+  total = 0;
+  fit_s = ba_s = 0;
+  const uint32_t code = s.code;
+  if (code == KSG_FILTER_NOT_EVALUATED) return code;
+  if (F.pos_fit >= 0 && (code == KSG_FILTER_PASS || (uint32_t)F.pos_fit < (code >> 24))) {
+    uint32_t b = fit_filter_row(r, h, R);
+    if (b) return ((uint32_t)F.pos_fit << 24) | b;
+  }
+  if (code != KSG_FILTER_PASS) return code;
+  if (F.pos_fit >= 0) fit_s = (int32_t)fit_score_row<MODE>(r, F, h);
+  if (F.pos_ba >= 0) ba_s = (int32_t)ba_score_row<MODE>(r, F, h);
+  bool re = false;
+  const bool skip_na = (h->flags & KPF_SKIP_NA_SCORE) != 0;
+  total = static_total(F, skip_na, fit_s, ba_s, s.raw >> 20, (int64_t)(s.raw & KSG_RAW_NA_MASK), MT < 0 ? 0 : MT,
+                       MA < 0 ? 0 : MA, re);
+  return code;
+}
+// raw: the static record's raw Taint/NodeAffinity scores (STAT profiles)
+template <bool STAT>
 __device__ __forceinline__ void write_pair(const DevProfile& F, uint32_t* of, int32_t* os, int32_t* ot, uint32_t N,
-                                           uint32_t n, uint32_t code, int32_t fit_s, int32_t ba_s, int64_t tot) {
+                                           uint32_t n, uint32_t code, int32_t fit_s, int32_t ba_s, int64_t tot,
+                                           uint32_t raw) {
   of[n] = code;
   if (code == KSG_FILTER_PASS) {
     if (F.pos_fit >= 0) os[(size_t)F.pos_fit * N + n] = fit_s;
     if (F.pos_ba >= 0) os[(size_t)F.pos_ba * N + n] = ba_s;
+    if (STAT) {
+      if (F.pos_taint >= 0) os[(size_t)F.pos_taint * N + n] = (int32_t)(raw >> 20);
+      if (F.pos_na >= 0) os[(size_t)F.pos_na * N + n] = (int32_t)(raw & KSG_RAW_NA_MASK);
+    }
     ot[n] = (int32_t)tot;
   }
 }
@@ -1765,7 +1804,7 @@ __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
 // Blocks 1.. of k_window: one pod x KSG_TILE nodes per block.  Tile lists are
 // handed to the pod's last-arriving block with sc1 stores/loads and an agent
 // counter (MI355X_MICROARCH.md, hand-off table row 1).
-template <int MODE>
+template <int MODE, bool STAT>
 __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& F, const WinArgs& A, uint32_t blk, uint64_t* L) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t* wcount = reinterpret_cast<uint32_t*>(L + 16 * 64);
@@ -1777,27 +1816,42 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   const int hit = pend_index((int32_t)(C.goff + n), pn, np);
   if (A.estamps && tid == 0) atomicMax((unsigned long long*)&A.estamps[8], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
   uint64_t key = 0;
-  bool feasible = false;
+  bool feasible = false, achT = false, achA = false;
   if (n < C.N) {
     RowV r;
     if (hit >= 0) r = A.pprev[hit].after;
     else load_row(C, n, A.need_eph, r);
     int32_t fit_s, ba_s;
     int64_t total;
-    uint32_t code = eval_row<MODE>(r, F, h, C.R < 4 ? C.R : 4, fit_s, ba_s, total);
+    uint32_t code, raw = 0;
+    if (STAT) {
+      const StaticRec sr = srec_row(A, q, C.N)[n];
+      const int64_t MT = A.mpred[2 * (q - A.first)], MA = A.mpred[2 * (q - A.first) + 1];
+      code = eval_row_s<MODE>(r, F, h, C.R < 4 ? C.R : 4, sr, MT, MA, fit_s, ba_s, total);
+      raw = sr.raw;
+      achT = F.pos_taint >= 0 && (int64_t)(raw >> 20) == MT;
+      achA = F.pos_na >= 0 && !(h->flags & KPF_SKIP_NA_SCORE) && (int64_t)(raw & KSG_RAW_NA_MASK) == MA;
+    } else {
+      code = eval_row<MODE>(r, F, h, C.R < 4 ? C.R : 4, fit_s, ba_s, total);
+    }
     uint32_t* of;
     int32_t *os, *ot;
     out_ptrs(A, q, C.N, of, os, ot);
-    write_pair(F, of, os, ot, C.N, n, code, fit_s, ba_s, total);
+    write_pair<STAT>(F, of, os, ot, C.N, n, code, fit_s, ba_s, total, raw);
     if (code == KSG_FILTER_PASS) {
       feasible = true;
       key = pack_key(total, F.seed, h->queue_idx, C.goff + n);
     }
   }
   unsigned long long bal = __ballot(feasible);
+  unsigned long long balT = STAT ? __ballot(feasible && achT) : 0ull, balA = STAT ? __ballot(feasible && achA) : 0ull;
   key = wave_sort_desc(key);
   L[w * 64 + lane] = key;
-  if (lane == 0) wcount[w] = (uint32_t)__popcll(bal);
+  if (lane == 0) {
+    wcount[w] = (uint32_t)__popcll(bal);
+    wcount[32 + w] = (uint32_t)__popcll(balT);
+    wcount[48 + w] = (uint32_t)__popcll(balA);
+  }
   lds_barrier();
 #pragma unroll 1
   for (int s = 8; s >= 1; s >>= 1) {
@@ -1807,16 +1861,18 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   if (w == 0) {
     uint64_t* dst = A.tile_top + ((size_t)b * A.T + tile) * KSG_TOPK;
     __hip_atomic_store(dst + lane, L[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lane == 0) {
+    if (lane < 3) {  // feasible nodes, Taint / NodeAffinity static-max achievers among them
+      const int off = lane == 0 ? 0 : 16 + 16 * lane;
       int32_t c = 0;
-      for (int k = 0; k < 16; ++k) c += (int32_t)wcount[k];
-      __hip_atomic_store(A.tile_feas + (size_t)b * A.T + tile, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < 16; ++k) c += (int32_t)wcount[off + k];
+      __hip_atomic_store(A.tile_feas + ((size_t)b * A.T + tile) * 3 + lane, c, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t old = 0;
     if (lane == 0) old = __hip_atomic_fetch_add(A.arrive + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __builtin_amdgcn_readfirstlane(old);
-    if (lane == 0) wcount[16] = old == A.T - 1 ? 1u : 0u;
+    if (lane == 0) wcount[16] = old == A.T - 1 ? 1u : 0u;  // (slots 17..31 unused)
   }
   lds_barrier();
   if (A.estamps && tid == 0) atomicMax((unsigned long long*)&A.estamps[9], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1848,12 +1904,16 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
       else load_row(C, (uint32_t)gid - C.goff, A.need_eph, c.r);
     }
     reinterpret_cast<CandRow*>(A.erec + KSG_XHDR)[(size_t)b * KSG_CAND + lane] = c;
-    int32_t f = 0;
+    int32_t f[3] = {0, 0, 0};
     for (uint32_t t = lane; t < A.T; t += 64)
-      f += __hip_atomic_load(A.tile_feas + (size_t)b * A.T + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    f = wave_sum(f);
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        f[k] += __hip_atomic_load(A.tile_feas + ((size_t)b * A.T + t) * 3 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) f[k] = wave_sum(f[k]);
     if (lane == 0) {
-      reinterpret_cast<int32_t*>(A.erec)[b] = f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) reinterpret_cast<int32_t*>(A.erec)[k * KSG_BATCH + b] = f[k];
       A.arrive[b] = 0;
       if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
@@ -1879,7 +1939,9 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
 // covers 64 candidate lanes + 32 P_{W-1} lanes + its 32 pick lanes.
 struct PatchV {
   uint32_t code;
-  int32_t fit, ba, total;
+  int32_t fitba;  // raw Fit | raw BalancedAllocation << 16 (both in [0, 100])
+  int32_t total;
+  uint32_t raw;   // static record's raw Taint / NodeAffinity scores
 };
 struct SumLite {
   uint64_t best_key;
@@ -1917,6 +1979,15 @@ struct WinLDS {
   uint64_t rk[KSG_BATCH][KSG_BATCH];    // per iteration: key of pod b on the node pod a < b picked
   int8_t rdf[KSG_BATCH][KSG_BATCH];     // its feasible-count change vs the snapshot
   int32_t pf[KSG_BATCH];                // per iteration: first pick of P_{W-1} node e
+  // Taint / NodeAffinity profiles (STAT): NormalizeScore's max is the static max
+  // (mt, ma) while a feasible node reaches it; achiever counts track that
+  int32_t achT[KSG_BATCH], achA[KSG_BATCH];  // snapshot achievers
+  int64_t mt[KSG_BATCH], ma[KSG_BATCH];      // static maxima (-1: no statically feasible node)
+  int64_t xmt[KSG_BATCH], xma[KSG_BATCH];    // normaliser of the pod's result (exact on fallback)
+  int8_t pdfT[KSG_BATCH][KSG_BATCH], pdfA[KSG_BATCH][KSG_BATCH];  // achiever changes: prior nodes
+  int8_t rdfT[KSG_BATCH][KSG_BATCH], rdfA[KSG_BATCH][KSG_BATCH];  // and picks
+  int32_t fbf[KSG_BATCH];                    // pod needs the exact full re-evaluation (no achiever left)
+  uint64_t red[16][4];                       // block reductions of the fallback
 };
 
 static_assert(sizeof(WinLDS) <= 160 * 1024, "window LDS exceeds the CU's 160 KiB");
@@ -1969,8 +2040,13 @@ __device__ __forceinline__ int first_pick(const PickTab& T, int32_t x) {
   return h >= 0 ? T.first[h] : KSG_BATCH;
 }
 
-__device__ __forceinline__ void origin_rows(const WinLDS& L, const WinArgs& A, int32_t o, RowV& start, RowV& snap) {
-  if (o < KSG_BATCH) {
+#define KSG_ORG_NODE 0x40000000  // pick origin: node (o & 0xFFFFF) read from the node rows (fallback picks)
+__device__ __forceinline__ void origin_rows(const DevCluster& C, const WinLDS& L, const WinArgs& A, int32_t o,
+                                            RowV& start, RowV& snap) {
+  if (o & KSG_ORG_NODE) {
+    load_row(C, (uint32_t)(o & 0xFFFFF) - C.goff, A.need_eph, start);
+    snap = start;
+  } else if (o < KSG_BATCH) {
     start = L.prior[o].after;
     snap = L.prior[o].base;
   } else {
@@ -2017,7 +2093,122 @@ __device__ __forceinline__ uint64_t max3u(uint64_t a, uint64_t b, uint64_t c) {
   return m > c ? m : c;
 }
 
+// Pod b's row of local node i under the picks S of the pods < b.
+__device__ __forceinline__ void row_under(const DevCluster& C, const WinLDS& L, const WinArgs& A, const int32_t* S,
+                                          const PickTab& T, int b, uint32_t i, uint32_t R, RowV& r) {
+  const int32_t g = (int32_t)(C.goff + i);
+  const int e = prior_of(L, g);
+  if (e >= 0) r = L.prior[e].after;
+  else load_row(C, i, A.need_eph, r);
+  const int hs = tab_find(T.node, g);
+  if (hs >= 0 && T.first[hs] < b) {
+    Delta cum{};
+    for (int j = 0; j < b; ++j)
+      if (S[j] == g) delta_add(cum, L.pod[j]);
+    apply_delta(r, cum, R);
+  }
+}
+// STAT profiles, no feasible node of pod b left at the static max (rare): its
+// exact result under S = L.S[cur] from two block-wide passes over all nodes —
+// the normaliser over the feasible nodes, then the argmax — into L.S[nxt][b].
 template <int MODE>
+__device__ __forceinline__ void win_exact_select(const DevCluster& C, const DevProfile& F, const WinArgs& A, WinLDS& L,
+                                              int b, int cur, int nxt, uint32_t R) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const PodLite* h = &L.pod[b];
+  const StaticRec* st = srec_row(A, A.w0 + b, C.N);
+  const int32_t* S = L.S[cur];
+  const PickTab& T = L.pick[cur];
+  int32_t feas = 0;
+  int64_t lt = 0, la = 0;
+#pragma unroll 1
+  for (uint32_t i = tid; i < C.N; i += KSG_WIN_THREADS) {
+    RowV r;
+    row_under(C, L, A, S, T, b, i, R, r);
+    const StaticRec sr = st[i];
+    int32_t fs, bs;
+    int64_t tot;
+    if (eval_row_s<MODE>(r, F, h, R, sr, 0, 0, fs, bs, tot) == KSG_FILTER_PASS) {
+      ++feas;
+      lt = max(lt, (int64_t)(sr.raw >> 20));
+      la = max(la, (int64_t)(sr.raw & KSG_RAW_NA_MASK));
+    }
+  }
+  feas = wave_sum(feas);
+  lt = wave_max(lt);
+  la = wave_max(la);
+  if (lane == 0) {
+    L.red[wave][0] = (uint64_t)feas;
+    L.red[wave][1] = (uint64_t)lt;
+    L.red[wave][2] = (uint64_t)la;
+  }
+  lds_barrier();
+  int32_t fa = 0;
+  int64_t mt = 0, ma = 0;
+  for (int w = 0; w < KSG_WIN_THREADS / 64; ++w) {
+    fa += (int32_t)L.red[w][0];
+    mt = max(mt, (int64_t)L.red[w][1]);
+    ma = max(ma, (int64_t)L.red[w][2]);
+  }
+  uint64_t best = 0;
+#pragma unroll 1
+  for (uint32_t i = tid; i < C.N; i += KSG_WIN_THREADS) {
+    RowV r;
+    row_under(C, L, A, S, T, b, i, R, r);
+    int32_t fs, bs;
+    int64_t tot;
+    if (eval_row_s<MODE>(r, F, h, R, st[i], mt, ma, fs, bs, tot) == KSG_FILTER_PASS) {
+      const uint64_t k = pack_key(tot, F.seed, h->queue_idx, C.goff + i);
+      best = k > best ? k : best;
+    }
+  }
+  best = wave_max(best);
+  if (lane == 0) L.red[wave][3] = best;
+  lds_barrier();
+  if (tid == 0) {
+    uint64_t bk = 0;
+    for (int w = 0; w < KSG_WIN_THREADS / 64; ++w) bk = L.red[w][3] > bk ? L.red[w][3] : bk;
+    const int32_t sel = (fa > 0 && bk) ? (int32_t)(bk & 0xFFFFFull) : -1;
+    int32_t org = -1;
+    if (sel >= 0) {
+      const int e = prior_of(L, sel);
+      org = e >= 0 ? e : (KSG_ORG_NODE | sel);
+      pick_insert(L.pick[nxt], sel, b);
+    }
+    L.S[nxt][b] = sel;
+    L.O[nxt][b] = org;
+    SumLite& sm = L.sum[b];
+    sm.best_key = sel >= 0 ? (fa == 1 ? (bk & 0xFFFFFFFFFFull) : bk) : 0;
+    sm.selected = sel;
+    sm.feasible = fa;
+    sm.status = sel >= 0 ? 0 : 1;
+    L.xmt[b] = mt;
+    L.xma[b] = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : ma;
+  }
+}
+// ... and, once S is final, every per-pair output of such a pod.
+template <int MODE>
+__device__ __forceinline__ void win_exact_write(const DevCluster& C, const DevProfile& F, const WinArgs& A, WinLDS& L,
+                                             int b, int cur, uint32_t R) {
+  const PodLite* h = &L.pod[b];
+  const StaticRec* st = srec_row(A, A.w0 + b, C.N);
+  uint32_t* of;
+  int32_t *os, *ot;
+  out_ptrs(A, A.w0 + b, C.N, of, os, ot);
+  const int64_t mt = L.xmt[b], ma = L.xma[b];
+#pragma unroll 1
+  for (uint32_t i = threadIdx.x; i < C.N; i += KSG_WIN_THREADS) {
+    RowV r;
+    row_under(C, L, A, L.S[cur], L.pick[cur], b, i, R, r);
+    const StaticRec sr = st[i];
+    int32_t fs, bs;
+    int64_t tot;
+    const uint32_t code = eval_row_s<MODE>(r, F, h, R, sr, mt, ma, fs, bs, tot);
+    write_pair<true>(F, of, os, ot, C.N, i, code, fs, bs, tot, sr.raw);
+  }
+}
+
+template <int MODE, bool STAT>
 __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile& F, const WinArgs& A, WinLDS& L) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nb = (int)A.nw;
@@ -2043,6 +2234,14 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     constexpr int kPodW = (int)(sizeof(PodLite) / 8);
     const uint64_t qv = tid < nb * kPodW ? reinterpret_cast<const uint64_t*>(A.plite + A.w0)[tid] : 0;
     const int32_t fv = tid < nb ? reinterpret_cast<const int32_t*>(A.wrec)[tid] : 0;
+    int32_t aT = 0, aA = 0;
+    int64_t m0 = -1, m1 = -1;
+    if (STAT && tid < nb) {
+      aT = reinterpret_cast<const int32_t*>(A.wrec)[KSG_BATCH + tid];
+      aA = reinterpret_cast<const int32_t*>(A.wrec)[2 * KSG_BATCH + tid];
+      m0 = A.mpred[2 * (A.w0 - A.first + tid)];
+      m1 = A.mpred[2 * (A.w0 - A.first + tid) + 1];
+    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       int i = tid + k * KSG_WIN_THREADS;
@@ -2058,6 +2257,13 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     if (tid < np * kPendW) reinterpret_cast<uint64_t*>(L.prior)[tid] = pv;
     if (tid < nb * kPodW) reinterpret_cast<uint64_t*>(L.pod)[tid] = qv;
     if (tid < nb) L.feas[tid] = fv;
+    if (STAT && tid < nb) {
+      L.achT[tid] = aT;
+      L.achA[tid] = aA;
+      L.mt[tid] = m0;
+      L.ma[tid] = m1;
+      L.fbf[tid] = 0;
+    }
     if (tid < 3 * KSG_BATCH) {
       (&L.S[0][0])[tid] = -1;
       (&L.O[0][0])[tid] = -1;
@@ -2088,17 +2294,30 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       const PodLite* h = &L.pod[pb];
       int32_t fs, bs;
       int64_t tot;
-      uint32_t code = eval_row<MODE>(pe.after, F, h, R, fs, bs, tot);
-      bool snap_ok = F.pos_fit < 0 || fit_filter_row(pe.base, h, R) == 0;
+      StaticRec sr{KSG_FILTER_PASS, 0};
+      uint32_t code;
+      if (STAT) {
+        sr = srec_row(A, A.w0 + pb, C.N)[(uint32_t)pe.node - C.goff];
+        code = eval_row_s<MODE>(pe.after, F, h, R, sr, L.mt[pb], L.ma[pb], fs, bs, tot);
+      } else {
+        code = eval_row<MODE>(pe.after, F, h, R, fs, bs, tot);
+      }
+      bool snap_ok = sr.code == KSG_FILTER_PASS && (F.pos_fit < 0 || fit_filter_row(pe.base, h, R) == 0);
       PatchV pt;
       pt.code = code;
-      pt.fit = fs;
-      pt.ba = bs;
+      pt.fitba = fs | (bs << 16);
       pt.total = (int32_t)tot;
+      pt.raw = sr.raw;
       L.patch[pb][e] = pt;
       k = code == KSG_FILTER_PASS ? pack_key(tot, F.seed, h->queue_idx, (uint32_t)pe.node) : 0;
       L.pkey[pb][e] = k;
-      L.pdf[pb][e] = (int8_t)((code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0));
+      const int df = (code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0);
+      L.pdf[pb][e] = (int8_t)df;
+      if (STAT) {
+        const bool na_on = F.pos_na >= 0 && !(h->flags & KPF_SKIP_NA_SCORE);
+        L.pdfT[pb][e] = (int8_t)(F.pos_taint >= 0 && (int64_t)(sr.raw >> 20) == L.mt[pb] ? df : 0);
+        L.pdfA[pb][e] = (int8_t)(na_on && (int64_t)(sr.raw & KSG_RAW_NA_MASK) == L.ma[pb] ? df : 0);
+      }
     }
     STAMP(16);
     // best prior node per pod: reduce within each half (DPP row ops stay inside 32 lanes
@@ -2200,10 +2419,11 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
           const int a = p - b * (b - 1) / 2;
           const int32_t Sv = L.S[cur][a];
           uint64_t k = 0;
-          int df = 0;
+          int df = 0, dT = 0, dA = 0;
           PatchV pt;
           pt.code = KSG_NOT_PATCHED;
-          pt.fit = pt.ba = pt.total = 0;
+          pt.fitba = pt.total = 0;
+          pt.raw = 0;
           if (Sv >= 0) {
             int nx = KSG_BATCH;
             Delta cum;
@@ -2213,25 +2433,41 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
             if (iters == 0) STAMP(25);
             if (nx >= b) {  // a is the last pick of the node before b
               RowV cur_r, snap;
-              origin_rows(L, A, L.O[cur][a], cur_r, snap);
+              origin_rows(C, L, A, L.O[cur][a], cur_r, snap);
               apply_delta(cur_r, cum, R);
               const PodLite* h = &L.pod[b];
               int32_t fs, bs;
               int64_t tot;
               if (iters == 0) STAMP(26);
-              uint32_t code = eval_row<MODE>(cur_r, F, h, R, fs, bs, tot);
+              StaticRec sr{KSG_FILTER_PASS, 0};
+              uint32_t code;
+              if (STAT) {
+                sr = srec_row(A, A.w0 + b, C.N)[(uint32_t)Sv - C.goff];
+                code = eval_row_s<MODE>(cur_r, F, h, R, sr, L.mt[b], L.ma[b], fs, bs, tot);
+              } else {
+                code = eval_row<MODE>(cur_r, F, h, R, fs, bs, tot);
+              }
               if (iters == 0) STAMP(27);
-              bool snap_ok = F.pos_fit < 0 || fit_filter_row(snap, h, R) == 0;
+              bool snap_ok = sr.code == KSG_FILTER_PASS && (F.pos_fit < 0 || fit_filter_row(snap, h, R) == 0);
               df = (code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0);
+              if (STAT) {
+                const bool na_on = F.pos_na >= 0 && !(h->flags & KPF_SKIP_NA_SCORE);
+                dT = F.pos_taint >= 0 && (int64_t)(sr.raw >> 20) == L.mt[b] ? df : 0;
+                dA = na_on && (int64_t)(sr.raw & KSG_RAW_NA_MASK) == L.ma[b] ? df : 0;
+              }
               if (code == KSG_FILTER_PASS) k = pack_key(tot, F.seed, h->queue_idx, (uint32_t)Sv);
               pt.code = code;
-              pt.fit = fs;
-              pt.ba = bs;
+              pt.fitba = fs | (bs << 16);
               pt.total = (int32_t)tot;
+              pt.raw = sr.raw;
             }
           }
           L.rk[b][a] = k;
           L.rdf[b][a] = (int8_t)df;
+          if (STAT) {
+            L.rdfT[b][a] = (int8_t)dT;
+            L.rdfA[b][a] = (int8_t)dA;
+          }
           L.patch[b][32 + a] = pt;
         }
       }
@@ -2268,11 +2504,31 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       const uint64_t kr = lane < b ? L.rk[b][lane & 31] : 0;
       const int df = (pact ? (int)L.pdf[b][lane & 31] : 0) + (lane < b ? (int)L.rdf[b][lane & 31] : 0);
       const uint64_t best = wave_max(max3u(kc, kp, kr));
-      const int feasible = L.feas[b] + wave_sum(df);
-      const int32_t sel = (feasible > 0 && best) ? (int32_t)(best & 0xFFFFFull) : -1;
+      int feasible;
+      bool fb = false;
+      if (STAT) {  // feasible and achiever counts in one reduction (per lane each change is in [-2, 2])
+        const int dT = (pact ? (int)L.pdfT[b][lane & 31] : 0) + (lane < b ? (int)L.rdfT[b][lane & 31] : 0);
+        const int dA = (pact ? (int)L.pdfA[b][lane & 31] : 0) + (lane < b ? (int)L.rdfA[b][lane & 31] : 0);
+        const int sum = wave_sum((df + 2) | ((dT + 2) << 10) | ((dA + 2) << 20));
+        feasible = L.feas[b] + (sum & 1023) - 128;
+        const int achT = L.achT[b] + ((sum >> 10) & 1023) - 128, achA = L.achA[b] + ((sum >> 20) & 1023) - 128;
+        const bool na_on = F.pos_na >= 0 && !(L.pod[b].flags & KPF_SKIP_NA_SCORE);
+        fb = !(L.pod[b].flags & KPF_PREFILTER_ERROR) && feasible > 0 &&
+             ((F.pos_taint >= 0 && achT <= 0) || (na_on && achA <= 0));
+      } else {
+        feasible = L.feas[b] + wave_sum(df);
+      }
+      const bool perr = (L.pod[b].flags & KPF_PREFILTER_ERROR) != 0;
+      const int32_t sel = (feasible > 0 && best && !perr) ? (int32_t)(best & 0xFFFFFull) : -1;
       const unsigned long long mc = __ballot(best && kc == best), mp = __ballot(best && kp == best),
                                mr = __ballot(best && kr == best);
+      if (STAT && lane == 0) L.fbf[b] = fb ? 1 : 0;
+      if (fb) continue;  // win_exact_select below
       if (lane == 0) {
+        if (STAT) {
+          L.xmt[b] = L.mt[b] < 0 ? 0 : L.mt[b];
+          L.xma[b] = (F.pos_na < 0 || (L.pod[b].flags & KPF_SKIP_NA_SCORE) || L.ma[b] < 0) ? 0 : L.ma[b];
+        }
         int32_t org = -1;
         if (mc) org = 64 + b * 64 + (__ffsll((long long)mc) - 1);
         else if (mp) org = __ffsll((long long)mp) - 1;
@@ -2284,11 +2540,22 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
         sm.best_key = sel >= 0 ? (feasible == 1 ? (best & 0xFFFFFFFFFFull) : best) : 0;
         sm.selected = sel;
         sm.feasible = feasible;
-        sm.status = sel >= 0 ? 0 : 1;
+        sm.status = perr ? 2 : (sel >= 0 ? 0 : 1);
       }
     }
     if (iters == 0) STAMP(23);
     lds_barrier();
+    if (STAT) {  // pods with no feasible node left at the static max: exact re-evaluation
+      unsigned long long fm = __ballot(lane < nb && lane >= stable && L.fbf[lane & 31] != 0);
+      if (fm) {
+        while (fm) {
+          const int b = __ffsll((long long)fm) - 1;
+          fm &= fm - 1;
+          win_exact_select<MODE>(C, F, A, L, b, cur, nxt, R);
+        }
+        lds_barrier();
+      }
+    }
     if (iters < 2) STAMP(19 + iters);
     ++iters;
     {  // every wave derives the same stable prefix
@@ -2309,6 +2576,10 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     d.selected = L.sum[tid].selected;
     d.feasible = L.sum[tid].feasible;
     d.status = L.sum[tid].status;
+    if (STAT) {
+      if (F.pos_taint >= 0) d.max_score[F.pos_taint] = L.xmt[tid];
+      if (F.pos_na >= 0) d.max_score[F.pos_na] = L.xma[tid];
+    }
   }
   {
     const int32_t Sv = L.S[cur][lane & 31];
@@ -2318,6 +2589,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     for (int hh = 0; hh < 2; ++hh) {
       const int b = 2 * wave + hh;
       if (b >= nb) break;
+      if (STAT && L.fbf[b]) continue;  // rewritten whole below
       const PatchV pt = L.patch[b][lane];
       const bool wr = lane < 32 ? (lane < np && pf >= b) : (lane - 32 < b && pt.code != KSG_NOT_PATCHED);
       const int32_t node = lane < 32 ? pn : Sv;
@@ -2326,8 +2598,16 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
         uint32_t* of;
         int32_t *os, *ot;
         out_ptrs(A, A.w0 + b, C.N, of, os, ot);
-        write_pair(F, of, os, ot, C.N, nl, pt.code, pt.fit, pt.ba, pt.total);
+        write_pair<STAT>(F, of, os, ot, C.N, nl, pt.code, pt.fitba & 0xFFFF, pt.fitba >> 16, pt.total, pt.raw);
       }
+    }
+  }
+  if (STAT) {
+    unsigned long long fm = __ballot(lane < nb && L.fbf[lane & 31] != 0);
+    while (fm) {
+      const int b = __ffsll((long long)fm) - 1;
+      fm &= fm - 1;
+      win_exact_write<MODE>(C, F, A, L, b, cur, R);
     }
   }
   if (wave == 0) {  // P_W: each node picked in the window, by its last pick
@@ -2342,7 +2622,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       int nx;
       if (T.cnt[h] > 1) pick_chain(L, L.S[cur], a, Sv, cum, nx);
       RowV st, snap;
-      origin_rows(L, A, L.O[cur][a], st, snap);
+      origin_rows(C, L, A, L.O[cur][a], st, snap);
       Pend p;
       p.node = Sv;
       p.pad = 0;
@@ -2358,14 +2638,14 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
 #undef STAMP
 }
 
-template <int MODE>
+template <int MODE, bool STAT>
 __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window(DevCluster C, DevProfile F, WinArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   if (blockIdx.x == 0) {
-    if (A.nw) win_fixup<MODE>(C, F, A, *reinterpret_cast<WinLDS*>(lds_raw));
+    if (A.nw) win_fixup<MODE, STAT>(C, F, A, *reinterpret_cast<WinLDS*>(lds_raw));
     return;
   }
-  win_eval<MODE>(C, F, A, blockIdx.x - 1, reinterpret_cast<uint64_t*>(lds_raw));
+  win_eval<MODE, STAT>(C, F, A, blockIdx.x - 1, reinterpret_cast<uint64_t*>(lds_raw));
 }
 
 // After the last window: write its pending rows back.
@@ -2389,8 +2669,9 @@ __global__ __launch_bounds__(64) void k_window_gmerge(const uint8_t* recv, uint3
   __syncthreads();
   uint64_t v = keys[lane];
   for (uint32_t r = 1; r < ranks; ++r) v = wave_merge_top(v, keys[r * KSG_CAND + 63 - lane]);
-  int32_t f = 0;
-  for (uint32_t r = 0; r < ranks; ++r) f += reinterpret_cast<const int32_t*>(recv + r * kRecBytes)[b];
+  int32_t f[3] = {0, 0, 0};
+  for (uint32_t r = 0; r < ranks; ++r)
+    for (int k = 0; k < 3; ++k) f[k] += reinterpret_cast<const int32_t*>(recv + r * kRecBytes)[k * KSG_BATCH + b];
   CandRow c;
   memset(&c, 0, sizeof(c));
   if (v) {  // find the source entry: each rank's list is sorted descending
@@ -2410,7 +2691,7 @@ __global__ __launch_bounds__(64) void k_window_gmerge(const uint8_t* recv, uint3
     }
   }
   reinterpret_cast<CandRow*>(out + KSG_XHDR)[(size_t)b * KSG_CAND + lane] = c;
-  if (lane == 0) reinterpret_cast<int32_t*>(out)[b] = f;
+  if (lane < 3) reinterpret_cast<int32_t*>(out)[lane * KSG_BATCH + b] = f[lane];
 }
 
 // ----------------------------------------------------------------- host side
@@ -2522,7 +2803,9 @@ struct Engine::Impl {
   DBuf<uint64_t> prog_off_d;
   bool any_eph_req = false;
   // speculative batch path
-  bool batch_ok = false;
+  bool batch_ok = false;     // profile of Fit / BA (/ Taint / NodeAffinity) plugins only
+  bool batch_static = false;
+  uint32_t stat_chunk_cap = 0;  // diagnostic: cap on the static chunk (pods, multiple of KSG_BATCH)  // ... with Taint / NodeAffinity: static records per pod (k_static)
   DBuf<uint64_t> tile_top;
   DBuf<int32_t> tfeas, pend_n;
   DBuf<uint32_t> arrive;
@@ -2654,7 +2937,13 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (!I.saux.alloc(4, err)) return false;
   HIPCHK(hipMemsetAsync(I.saux.p, 0, 4 * sizeof(int32_t), I.stream));
   I.batch_ok = F.n > 0;
-  for (int i = 0; i < F.n; ++i) I.batch_ok &= (F.plugins[i] == KP_FIT || F.plugins[i] == KP_BA);
+  for (int i = 0; i < F.n; ++i)
+    I.batch_ok &= (F.plugins[i] == KP_FIT || F.plugins[i] == KP_BA || F.plugins[i] == KP_TAINT || F.plugins[i] == KP_NA);
+  I.batch_static = I.batch_ok && I.static_ok;
+  if (const char* e = std::getenv("KSG_STATIC_CHUNK")) {  // diagnostic (tests): smaller static chunks
+    long v = std::strtol(e, nullptr, 10);
+    I.stat_chunk_cap = v > 0 ? (uint32_t)std::max<long>(KSG_BATCH, v / KSG_BATCH * KSG_BATCH) : 0;
+  }
   return true;
 }
 
@@ -2738,7 +3027,7 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   if (I.batch_ok && I.R <= 4) {
     uint32_t T = std::max<uint32_t>((I.N + KSG_TILE - 1) / KSG_TILE, 1);
     size_t Nn = std::max<uint32_t>(I.N, 1);
-    if (!I.tile_top.alloc((size_t)KSG_BATCH * T * KSG_TOPK, err) || !I.tfeas.alloc((size_t)KSG_BATCH * T, err) ||
+    if (!I.tile_top.alloc((size_t)KSG_BATCH * T * KSG_TOPK, err) || !I.tfeas.alloc((size_t)KSG_BATCH * T * 3, err) ||
         !I.arrive.alloc(KSG_BATCH, err) || !I.pend_n.alloc(2, err) || !I.wrec.alloc(2 * kRecBytes, err) ||
         !I.pend.alloc(2 * KSG_BATCH, err) || !I.bfilter.alloc(Nn * 2 * KSG_BATCH, err) ||
         !I.bscore.alloc(Nn * 2 * KSG_BATCH * KSG_MAX_PLUGINS, err) || !I.btotal.alloc(Nn * 2 * KSG_BATCH, err))
@@ -2771,8 +3060,9 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   I.n_samples = 0;
   static bool attr = false;
   if (!attr) {
-    HIPCHK(hipFuncSetAttribute((const void*)k_window<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLDS)));
-    HIPCHK(hipFuncSetAttribute((const void*)k_window<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLDS)));
+    const void* fns[4] = {(const void*)k_window<0, false>, (const void*)k_window<1, false>,
+                          (const void*)k_window<0, true>, (const void*)k_window<1, true>};
+    for (const void* f : fns) HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLDS)));
     attr = true;
   }
   HIPCHK(hipEventRecord(I.ev0, s));
@@ -2791,6 +3081,22 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   A.arrive = I.arrive.p;
   A.sums = I.sums.p;
   const bool sharded = I.xranks > 1;
+  // static records: a ring of two chunks of whole windows (window j+1's eval and
+  // window j's replay may sit in consecutive chunks); chunk c computed by k_static
+  // just before the launch that evaluates its first window
+  const bool stat = I.batch_static;
+  uint32_t chunk = 0;
+  if (stat) {
+    const size_t Nn = std::max<uint32_t>(I.N, 1);
+    chunk = (uint32_t)std::max<size_t>(KSG_BATCH, (((size_t)64 << 20) / (Nn * sizeof(StaticRec))) / KSG_BATCH * KSG_BATCH);
+    chunk = std::min<uint32_t>(chunk, (count + KSG_BATCH - 1) / KSG_BATCH * KSG_BATCH);
+    if (I.stat_chunk_cap) chunk = std::min<uint32_t>(chunk, I.stat_chunk_cap);  // tests: force ring roll-over
+    if (!I.stat.alloc((size_t)2 * chunk * Nn, err) || !I.mpred.alloc(2 * (size_t)std::max<uint32_t>(count, 1), err))
+      return false;
+    A.stat = I.stat.p;
+    A.stat_ring = 2 * chunk;
+    A.mpred = I.mpred.p;
+  }
   for (int64_t j = -1; j < (int64_t)nwin; ++j) {
     const int64_t E = j + 1, W = j;
     A.ne = 0;
@@ -2813,11 +3119,25 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     const int64_t P = W - 1;  // P_{W-1}: the list the eval part overrides rows from, too
     A.pprev = I.pend.p + (size_t)(P & 1) * KSG_BATCH;
     A.pprev_n = I.pend_n.p + (P & 1);
+    if (stat && A.ne && (A.e0 - first) % chunk == 0) {
+      const uint32_t q0 = A.e0, cn = std::min(chunk, first + count - q0);
+      HIPCHK(hipMemsetAsync(I.mpred.p + 2 * (size_t)(q0 - first), 0xFF, 2 * (size_t)cn * sizeof(int64_t), s));
+      const dim3 sgrid(std::max<uint32_t>((I.N + 256 * KSG_WI_NPT - 1) / (256 * KSG_WI_NPT), 1),
+                       (cn + KSG_WI_PODS - 1) / KSG_WI_PODS);
+      hipLaunchKernelGGL(k_static, sgrid, dim3(256), 0, s, C, I.F, I.progs.p, I.prog_off_d.p, q0, cn,
+                         I.stat.p + (size_t)((q0 - first) % (2 * chunk)) * I.N, I.mpred.p + 2 * (size_t)(q0 - first));
+    }
     bool sampled = I.sample_every && A.ne && A.nw && I.n_samples * 2 + 2 <= I.sev.size();
     if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
     dim3 grid(1 + A.ne * T);
-    if (I.eval_mode == 1) hipLaunchKernelGGL(k_window<1>, grid, dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, A);
-    else hipLaunchKernelGGL(k_window<0>, grid, dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, A);
+    const dim3 blk(KSG_WIN_THREADS);
+    if (stat) {
+      if (I.eval_mode == 1) hipLaunchKernelGGL((k_window<1, true>), grid, blk, sizeof(WinLDS), s, C, I.F, A);
+      else hipLaunchKernelGGL((k_window<0, true>), grid, blk, sizeof(WinLDS), s, C, I.F, A);
+    } else {
+      if (I.eval_mode == 1) hipLaunchKernelGGL((k_window<1, false>), grid, blk, sizeof(WinLDS), s, C, I.F, A);
+      else hipLaunchKernelGGL((k_window<0, false>), grid, blk, sizeof(WinLDS), s, C, I.F, A);
+    }
     if (sampled) {
       HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
       I.n_samples++;
@@ -3066,7 +3386,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
 bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string& err) {
   Impl& I = *p_;
   if (first + count > I.prog_off.size()) { err = "program index out of range"; return false; }
-  if (I.batch_ok && commit && !I.force_per_pod) return run_batches(I, first, count, err);
+  if (commit && batch_path()) return run_batches(I, first, count, err);
   hipStream_t s = I.stream;
   DevCluster C = I.cluster();
   DevScratch S = I.scratch();
@@ -3285,7 +3605,11 @@ bool Engine::fixup_stamps(uint32_t count, std::vector<uint64_t>* out, std::strin
   HIPCHK(hipMemcpy(out->data(), I.stamps.p, out->size() * 8, hipMemcpyDeviceToHost));
   return true;
 }
-bool Engine::batch_path() const { return p_->batch_ok && !p_->force_per_pod && p_->R <= 4; }
+bool Engine::batch_path() const {
+  const Impl& I = *p_;
+  if (!I.batch_ok || I.force_per_pod || I.R > 4) return false;
+  return !I.batch_static || (I.static_fits && I.xranks <= 1);  // static maxima: single shard for now
+}
 
 bool Engine::kernel_time(float& avg_ms, uint32_t& samples, std::string& err) {
   Impl& I = *p_;

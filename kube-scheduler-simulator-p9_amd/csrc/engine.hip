@@ -1236,19 +1236,24 @@ struct StaticRec {
 };
 #define KSG_RAW_NA_MASK 0xFFFFFu
 
+// Grid: node tiles of 256 x KSG_ST_NPT nodes x pod tiles of KSG_ST_PODS pods —
+// small tiles, so that a chunk of pods gives every SIMD several waves to hide
+// the label loads' latency behind (the work per pair is a few dependent loads).
+#define KSG_ST_PODS 4
+#define KSG_ST_NPT 1
 __global__ __launch_bounds__(256) void k_static(DevCluster C, DevProfile F, const uint8_t* progs, const uint64_t* prog_off,
                                                 uint32_t q0, uint32_t count, StaticRec* out, int64_t* mpred) {
-  const uint32_t base = blockIdx.x * (256 * KSG_WI_NPT) + threadIdx.x;
+  const uint32_t base = blockIdx.x * (256 * KSG_ST_NPT) + threadIdx.x;
 #pragma unroll 1
-  for (uint32_t pi = 0; pi < KSG_WI_PODS; ++pi) {
-    const uint32_t j = blockIdx.y * KSG_WI_PODS + pi;
+  for (uint32_t pi = 0; pi < KSG_ST_PODS; ++pi) {
+    const uint32_t j = blockIdx.y * KSG_ST_PODS + pi;
     if (j >= count) break;
     const ProgView V = view(progs + prog_off[q0 + j]);
     const ksg_prog* h = V.h;
     const bool skip_na_score = (h->flags & KPF_SKIP_NA_SCORE) != 0;
     int64_t mt = -1, ma = -1;
 #pragma unroll 1
-    for (int k = 0; k < KSG_WI_NPT; ++k) {
+    for (int k = 0; k < KSG_ST_NPT; ++k) {
       const uint32_t n = base + k * 256;
       if (n >= C.N) continue;
       uint32_t code = KSG_FILTER_PASS, raw = 0;
@@ -1476,6 +1481,7 @@ __global__ __launch_bounds__(kBlock) void k_fs_static(DevCluster C, DevProfile F
 #define KSG_TOPK 64
 #define KSG_WIN_THREADS 1024
 #define KSG_TILE KSG_WIN_THREADS  // nodes per eval block
+#define KSG_STASH_NPT 8    // eval tiles of up to this many nodes per thread hold their outputs in LDS
 #define KSG_STAGE 16       // candidate ranks whose rows are staged in LDS (deeper ranks: global)
 #define KSG_XHDR 512       // record header: per pod feasible count, static-max achievers (Taint, NodeAffinity): 3 x KSG_BATCH ints
 #define KSG_NOT_PATCHED 0xFFFFFFFDu
@@ -1511,7 +1517,7 @@ struct WinArgs {
   uint32_t *kfilter, *sfilter;  // kept outputs / scratch ring of 2*KSG_BATCH pods
   int32_t *kscore, *sscore, *ktotal, *stotal;
   // eval part: window E = queue pods [e0, e0 + ne)
-  uint32_t e0, ne, T;
+  uint32_t e0, ne, T, npt;  // T tiles of KSG_TILE * npt nodes per pod
   uint64_t* tile_top;    // [KSG_BATCH][T][KSG_TOPK]
   int32_t* tile_feas;    // [KSG_BATCH][T]
   uint32_t* arrive;      // [KSG_BATCH] tile arrivals (reset by the last block)
@@ -1719,30 +1725,89 @@ __device__ __forceinline__ void write_pair(const DevProfile& F, uint32_t* of, in
   }
 }
 
+// Lane exchange v[lane ^ J] on the VALU (no LDS crossbar round trip as with
+// ds_bpermute): DPP quad_perm for 1 and 2, DPP row rotations for 4 and 8,
+// gfx950's v_permlane16_swap / v_permlane32_swap for 16 and 32.
+// (dpp row_ror:N — lane i of a 16-lane row reads lane (i - N) mod 16.)
+template <int J>
+__device__ __forceinline__ uint32_t xor_lanes32(uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (J == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  if (J == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  if (J == 4) {
+    const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x12C, 0xF, 0xF, false);  // row_ror:12
+    return (lane & 4) ? a : b;
+  }
+  if (J == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  if (J == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane & 16) ? r[0] : r[1];
+  }
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (lane & 32) ? r[0] : r[1];
+}
+template <int J>
+__device__ __forceinline__ uint64_t xor_lanes(uint64_t v) {
+  return ((uint64_t)xor_lanes32<J>((uint32_t)(v >> 32)) << 32) | xor_lanes32<J>((uint32_t)v);
+}
+template <int J>
+__device__ __forceinline__ uint64_t bitonic_step(uint64_t v, bool desc) {
+  const uint64_t o = xor_lanes<J>(v);
+  const bool low = (threadIdx.x & J) == 0;
+  return (low == desc) ? (v > o ? v : o) : (v < o ? v : o);
+}
+template <int K>
+__device__ __forceinline__ uint64_t bitonic_stage(uint64_t v) {  // merge step of block size K
+  const bool desc = K == 64 || (threadIdx.x & K) == 0;
+  if (K >= 64) v = bitonic_step<32>(v, desc);
+  if (K >= 32) v = bitonic_step<16>(v, desc);
+  if (K >= 16) v = bitonic_step<8>(v, desc);
+  if (K >= 8) v = bitonic_step<4>(v, desc);
+  if (K >= 4) v = bitonic_step<2>(v, desc);
+  return bitonic_step<1>(v, desc);
+}
 __device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v) {
-  int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int k = 2; k <= 64; k <<= 1)
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      uint64_t o = __shfl_xor(v, j, 64);
-      bool desc = (lane & k) == 0 || k == 64;
-      bool low = (lane & j) == 0;
-      v = (low == desc) ? (v > o ? v : o) : (v < o ? v : o);
-    }
-  return v;
+  v = bitonic_stage<2>(v);
+  v = bitonic_stage<4>(v);
+  v = bitonic_stage<8>(v);
+  v = bitonic_stage<16>(v);
+  v = bitonic_stage<32>(v);
+  return bitonic_stage<64>(v);
 }
 // v: descending list, o_rev: the other descending list read in reverse lane order
 __device__ __forceinline__ uint64_t wave_merge_top(uint64_t v, uint64_t o_rev) {
-  int lane = threadIdx.x & 63;
-  v = v > o_rev ? v : o_rev;
-#pragma unroll
-  for (int j = 32; j > 0; j >>= 1) {
-    uint64_t o = __shfl_xor(v, j, 64);
-    bool low = (lane & j) == 0;
-    v = low ? (v > o ? v : o) : (v < o ? v : o);
+  v = v > o_rev ? v : o_rev;  // bitonic; its top half holds the 64 largest
+  return bitonic_stage<64>(v);
+}
+// v read in reverse lane order (lane ^ 63)
+__device__ __forceinline__ uint64_t wave_reverse(uint64_t v) {
+  return xor_lanes<32>(xor_lanes<16>(xor_lanes<8>(xor_lanes<4>(xor_lanes<2>(xor_lanes<1>(v))))));
+}
+// Self-test of the lane exchanges against ds_bpermute shuffles (diagnostic ABI).
+__global__ void k_selftest_lanes(const uint64_t* in, int32_t* bad) {
+  const uint64_t v = in[threadIdx.x + blockIdx.x * 64];
+  int e = 0;
+  e += xor_lanes<1>(v) != __shfl_xor(v, 1, 64);
+  e += xor_lanes<2>(v) != __shfl_xor(v, 2, 64);
+  e += xor_lanes<4>(v) != __shfl_xor(v, 4, 64);
+  e += xor_lanes<8>(v) != __shfl_xor(v, 8, 64);
+  e += xor_lanes<16>(v) != __shfl_xor(v, 16, 64);
+  e += xor_lanes<32>(v) != __shfl_xor(v, 32, 64);
+  e += wave_reverse(v) != __shfl(v, 63 - (int)(threadIdx.x & 63), 64);
+  const uint64_t srt = wave_sort_desc(v);  // descending, and a permutation (sum and xor kept)
+  const uint64_t nxt = __shfl_down(srt, 1, 64);
+  e += (threadIdx.x & 63) < 63 && nxt > srt;
+  const uint64_t m = wave_merge_top(srt, wave_reverse(wave_sort_desc(~v)));
+  const uint64_t nm = __shfl_down(m, 1, 64);
+  e += (threadIdx.x & 63) < 63 && nm > m;
+  int c_sorted = 0, c_in = 0;  // multiset check: occurrences of v in the input and in the sorted list
+  for (int j = 0; j < 64; ++j) {
+    c_sorted += __shfl(srt, j, 64) == v;
+    c_in += __shfl(v, j, 64) == v;
   }
-  return v;
+  e += c_sorted != c_in;
+  atomicAdd(bad, e);
 }
 
 // Per-pair output rows of queue pod q: the kept window, or a scratch ring of
@@ -1801,6 +1866,13 @@ __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// per-pair outputs of one (pod, node) held back in LDS
+struct PatchV {
+  uint32_t code;
+  int32_t fitba;  // raw Fit | raw BalancedAllocation << 16 (both in [0, 100])
+  int32_t total;
+  uint32_t raw;   // static record's raw Taint / NodeAffinity scores
+};
 // Blocks 1.. of k_window: one pod x KSG_TILE nodes per block.  Tile lists are
 // handed to the pod's last-arriving block with sc1 stores/loads and an agent
 // counter (MI355X_MICROARCH.md, hand-off table row 1).
@@ -1809,24 +1881,80 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t* wcount = reinterpret_cast<uint32_t*>(L + 16 * 64);
   const uint32_t b = blk / A.T, tile = blk - b * A.T, q = A.e0 + b;
-  const PodLite* h = A.plite + q;
+  // LDS: keys [16][64] u64 | wcount u32[64] | P_{W-1} nodes i32[32] | pod record, normaliser | wave 0's outputs
+  // (the pod's fields come from LDS: as vector loads behind the output stores
+  // every one of them waited for all outstanding stores)
+  PodLite* h = reinterpret_cast<PodLite*>(wcount + 96);
+  int64_t* mlds = reinterpret_cast<int64_t*>(wcount + 96 + sizeof(PodLite) / 4);
+  {
+    constexpr int kPodW = (int)(sizeof(PodLite) / 8);
+    if (tid < kPodW) reinterpret_cast<uint64_t*>(h)[tid] = reinterpret_cast<const uint64_t*>(A.plite + q)[tid];
+    if (STAT && tid < 2) mlds[tid] = A.mpred[2 * (q - A.first) + tid];
+  }
   const int np = *A.pprev_n;
-  const int32_t pn = lane < np ? A.pprev[lane].node : -1;
-  const uint32_t n = tile * KSG_TILE + tid;
-  const int hit = pend_index((int32_t)(C.goff + n), pn, np);
-  if (A.estamps && tid == 0) atomicMax((unsigned long long*)&A.estamps[8], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+  // P_{W-1}'s nodes in LDS (a lookup through LDS: a VGPR loaded from memory and
+  // read lane by lane in a loop made the compiler wait for every outstanding
+  // load and store, vmcnt(0), at each lookup)
+  int32_t* pnl = reinterpret_cast<int32_t*>(wcount + 64);
+  if (tid < np) pnl[tid] = A.pprev[tid].node;
+  lds_barrier();
+  auto pend_lds = [&](int32_t gid) {
+    int hit = -1;
+    for (int e = 0; e < np; ++e) hit = pnl[e] == gid ? e : hit;
+    return hit;
+  };
+  const uint64_t t_start = A.estamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  if (A.estamps && tid == 0) {
+    atomicMax((unsigned long long*)&A.estamps[8], ~(unsigned long long)t_start);
+    atomicMax((unsigned long long*)&A.estamps[30], (unsigned long long)t_start);
+  }
+  // a tile is KSG_TILE * A.npt nodes: each wave keeps the top 64 of its npt x 64 keys
+  uint64_t top = 0;
+  uint32_t cF = 0, cT = 0, cA = 0;
+  const bool est = A.estamps && tid == 960;  // wave 15: writes its outputs directly
+  uint64_t t_eval = 0, t_sort = 0, t_wait = 0;
+#define ETIME(v)                             \
+  __builtin_amdgcn_sched_barrier(0);         \
+  const uint64_t v = __builtin_amdgcn_s_memtime(); \
+  __builtin_amdgcn_sched_barrier(0);
+  // per-pair outputs wait in LDS and are written once the tile list is handed
+  // over: wave 0's arrival waits (vmcnt) for all of its stores, and every
+  // wave's next-node loads would wait behind its previous node's stores.
+  // Tiles of more than KSG_STASH_NPT nodes per thread: only wave 0 stashes.
+  PatchV* stash = reinterpret_cast<PatchV*>(wcount + 192);
+  const bool stash_all = A.npt <= KSG_STASH_NPT;
+  static_assert(96 * 4 + sizeof(PodLite) + 16 <= 192 * 4, "eval LDS layout");
+  // the next node's row and static record are loaded while this one is evaluated
+  auto fetch = [&](uint32_t kk, RowV& r, StaticRec& sr) {
+    const uint32_t nn = (tile * A.npt + kk) * KSG_TILE + tid;
+    if (nn < C.N) {
+      const int hit = pend_lds((int32_t)(C.goff + nn));
+      if (hit >= 0) r = A.pprev[hit].after;
+      else load_row(C, nn, A.need_eph, r);
+      if (STAT) sr = srec_row(A, q, C.N)[nn];
+    }
+  };
+  RowV rnext;
+  StaticRec snext{KSG_FILTER_PASS, 0};
+  fetch(0, rnext, snext);
+#pragma unroll 1
+  for (uint32_t k = 0; k < A.npt; ++k) {
+  ETIME(t0);
+  if (A.estamps && w == 15) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: load wait
+  ETIME(tl);
+  t_wait += tl - t0;
+  const uint32_t n = (tile * A.npt + k) * KSG_TILE + tid;
+  const RowV r = rnext;
+  const StaticRec sr = snext;
+  if (k + 1 < A.npt) fetch(k + 1, rnext, snext);
   uint64_t key = 0;
   bool feasible = false, achT = false, achA = false;
   if (n < C.N) {
-    RowV r;
-    if (hit >= 0) r = A.pprev[hit].after;
-    else load_row(C, n, A.need_eph, r);
     int32_t fit_s, ba_s;
     int64_t total;
     uint32_t code, raw = 0;
     if (STAT) {
-      const StaticRec sr = srec_row(A, q, C.N)[n];
-      const int64_t MT = A.mpred[2 * (q - A.first)], MA = A.mpred[2 * (q - A.first) + 1];
+      const int64_t MT = mlds[0], MA = mlds[1];
       code = eval_row_s<MODE>(r, F, h, C.R < 4 ? C.R : 4, sr, MT, MA, fit_s, ba_s, total);
       raw = sr.raw;
       achT = F.pos_taint >= 0 && (int64_t)(raw >> 20) == MT;
@@ -1834,23 +1962,37 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     } else {
       code = eval_row<MODE>(r, F, h, C.R < 4 ? C.R : 4, fit_s, ba_s, total);
     }
-    uint32_t* of;
-    int32_t *os, *ot;
-    out_ptrs(A, q, C.N, of, os, ot);
-    write_pair<STAT>(F, of, os, ot, C.N, n, code, fit_s, ba_s, total, raw);
+    if (stash_all || w == 0) {
+      stash[(stash_all ? k * 16 + w : k) * 64 + lane] = PatchV{code, fit_s | (ba_s << 16), (int32_t)total, raw};
+    } else {
+      uint32_t* of;
+      int32_t *os, *ot;
+      out_ptrs(A, q, C.N, of, os, ot);
+      write_pair<STAT>(F, of, os, ot, C.N, n, code, fit_s, ba_s, total, raw);
+    }
     if (code == KSG_FILTER_PASS) {
       feasible = true;
       key = pack_key(total, F.seed, h->queue_idx, C.goff + n);
     }
   }
-  unsigned long long bal = __ballot(feasible);
-  unsigned long long balT = STAT ? __ballot(feasible && achT) : 0ull, balA = STAT ? __ballot(feasible && achA) : 0ull;
+  cF += (uint32_t)__popcll(__ballot(feasible));
+  if (STAT) {
+    cT += (uint32_t)__popcll(__ballot(feasible && achT));
+    cA += (uint32_t)__popcll(__ballot(feasible && achA));
+  }
+  ETIME(t1);
   key = wave_sort_desc(key);
-  L[w * 64 + lane] = key;
+  top = k == 0 ? key : wave_merge_top(top, wave_reverse(key));
+  ETIME(t2);
+  t_eval += t1 - t0;
+  t_sort += t2 - t1;
+  }
+  ETIME(t3);
+  L[w * 64 + lane] = top;
   if (lane == 0) {
-    wcount[w] = (uint32_t)__popcll(bal);
-    wcount[32 + w] = (uint32_t)__popcll(balT);
-    wcount[48 + w] = (uint32_t)__popcll(balA);
+    wcount[w] = cF;
+    wcount[32 + w] = cT;
+    wcount[48 + w] = cA;
   }
   lds_barrier();
 #pragma unroll 1
@@ -1874,9 +2016,39 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     old = __builtin_amdgcn_readfirstlane(old);
     if (lane == 0) wcount[16] = old == A.T - 1 ? 1u : 0u;  // (slots 17..31 unused)
   }
+  auto flush_stash = [&]() {
+    if (!stash_all && w != 0) return;
+    uint32_t* of;
+    int32_t *os, *ot;
+    out_ptrs(A, q, C.N, of, os, ot);
+#pragma unroll 1
+    for (uint32_t k = 0; k < A.npt; ++k) {
+      const uint32_t n = (tile * A.npt + k) * KSG_TILE + tid;
+      if (n >= C.N) break;
+      const PatchV pt = stash[(stash_all ? k * 16 + w : k) * 64 + lane];
+      write_pair<STAT>(F, of, os, ot, C.N, n, pt.code, pt.fitba & 0xFFFF, pt.fitba >> 16, pt.total, pt.raw);
+    }
+  };
   lds_barrier();
-  if (A.estamps && tid == 0) atomicMax((unsigned long long*)&A.estamps[9], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-  if (!wcount[16]) return;
+  ETIME(t4);
+#undef ETIME
+  if (est) {
+    atomicAdd((unsigned long long*)&A.estamps[13], (unsigned long long)t_eval);
+    atomicAdd((unsigned long long*)&A.estamps[14], (unsigned long long)t_sort);
+    atomicAdd((unsigned long long*)&A.estamps[15], (unsigned long long)(t4 - t3));
+    atomicAdd((unsigned long long*)&A.estamps[18], (unsigned long long)t_wait);
+  }
+  if (A.estamps && tid == 0) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    atomicMax((unsigned long long*)&A.estamps[9], (unsigned long long)t);
+    atomicMax((unsigned long long*)&A.estamps[28], (unsigned long long)(t - t_start));
+    atomicAdd((unsigned long long*)&A.estamps[29], (unsigned long long)(t - t_start));
+    atomicAdd((unsigned long long*)&A.estamps[31], 1ull);
+  }
+  if (!wcount[16]) {
+    flush_stash();
+    return;
+  }
   // last tile block of pod b: merge the T tile lists (wave w takes tiles w, w+16, ...)
   {
     const uint64_t* src = A.tile_top + (size_t)b * A.T * KSG_TOPK;
@@ -1898,7 +2070,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     memset(&c, 0, sizeof(c));
     c.key = v;
     int32_t gid = (int32_t)(v & 0xFFFFFull);
-    int hh = pend_index(gid, pn, np);
+    int hh = pend_lds(gid);
     if (v) {
       if (hh >= 0) c.r = A.pprev[hh].after;
       else load_row(C, (uint32_t)gid - C.goff, A.need_eph, c.r);
@@ -1918,6 +2090,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
       if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
   }
+  flush_stash();
 }
 
 // ---- block 0: exact replay of window W as a fixed-point (Jacobi) iteration.
@@ -1937,12 +2110,6 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
 // pods in one wave instruction stream (lanes 0..31: pod w, 32..63: pod w+16,
 // lane&31 = the earlier pick a it re-evaluates); the per-pod reduction then
 // covers 64 candidate lanes + 32 P_{W-1} lanes + its 32 pick lanes.
-struct PatchV {
-  uint32_t code;
-  int32_t fitba;  // raw Fit | raw BalancedAllocation << 16 (both in [0, 100])
-  int32_t total;
-  uint32_t raw;   // static record's raw Taint / NodeAffinity scores
-};
 struct SumLite {
   uint64_t best_key;
   int32_t selected, feasible, status, pad;
@@ -1991,6 +2158,8 @@ struct WinLDS {
 };
 
 static_assert(sizeof(WinLDS) <= 160 * 1024, "window LDS exceeds the CU's 160 KiB");
+static_assert(16 * 64 * 8 + 192 * 4 + (size_t)KSG_STASH_NPT * 16 * 64 * sizeof(PatchV) <= sizeof(WinLDS),
+              "eval blocks' output stash exceeds the window LDS");
 __device__ __forceinline__ uint32_t hslot(int32_t node) { return ((uint32_t)node * 2654435761u) >> 25; }
 __device__ __forceinline__ int prior_of(const WinLDS& L, int32_t x) {
   uint32_t h = hslot(x);
@@ -2805,7 +2974,8 @@ struct Engine::Impl {
   // speculative batch path
   bool batch_ok = false;     // profile of Fit / BA (/ Taint / NodeAffinity) plugins only
   bool batch_static = false;
-  uint32_t stat_chunk_cap = 0;  // diagnostic: cap on the static chunk (pods, multiple of KSG_BATCH)  // ... with Taint / NodeAffinity: static records per pod (k_static)
+  uint32_t stat_chunk_cap = 0;
+  uint32_t n_cus = 256;  // compute units of the device  // diagnostic: cap on the static chunk (pods, multiple of KSG_BATCH)  // ... with Taint / NodeAffinity: static records per pod (k_static)
   DBuf<uint64_t> tile_top;
   DBuf<int32_t> tfeas, pend_n;
   DBuf<uint32_t> arrive;
@@ -2877,6 +3047,11 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   } else {
     HIPCHK(hipStreamCreateWithFlags(&I.stream, hipStreamNonBlocking));
     I.own_stream = true;
+  }
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg.device) == hipSuccess && cus > 0)
+      I.n_cus = (uint32_t)cus;
   }
   HIPCHK(hipEventCreate(&I.ev0));
   HIPCHK(hipEventCreate(&I.ev1));
@@ -3047,7 +3222,11 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   if (I.R > 4) { err = "batch path supports at most 4 resource columns"; return false; }
   hipStream_t s = I.stream;
   DevCluster C = I.cluster();
-  const uint32_t T = std::max<uint32_t>((I.N + KSG_TILE - 1) / KSG_TILE, 1);
+  // nodes per eval thread: enough that one window's eval blocks fit the CUs
+  // beside the replay block in one round (one 1,024-thread block per CU)
+  uint32_t npt = 1;
+  while (npt < 16 && (uint64_t)KSG_BATCH * ((I.N + KSG_TILE * npt - 1) / (KSG_TILE * npt)) + 1 > I.n_cus) ++npt;
+  const uint32_t T = std::max<uint32_t>((I.N + KSG_TILE * npt - 1) / (KSG_TILE * npt), 1);
   const uint32_t nwin = (count + KSG_BATCH - 1) / KSG_BATCH;
   if (I.sample_every) {
     size_t need = 2 * (nwin + 2);
@@ -3076,6 +3255,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   A.kfilter = I.kfilter.p; A.kscore = I.kscore.p; A.ktotal = I.ktotal.p;
   A.sfilter = I.bfilter.p; A.sscore = I.bscore.p; A.stotal = I.btotal.p;
   A.T = T;
+  A.npt = npt;
   A.tile_top = I.tile_top.p;
   A.tile_feas = I.tfeas.p;
   A.arrive = I.arrive.p;
@@ -3122,8 +3302,8 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     if (stat && A.ne && (A.e0 - first) % chunk == 0) {
       const uint32_t q0 = A.e0, cn = std::min(chunk, first + count - q0);
       HIPCHK(hipMemsetAsync(I.mpred.p + 2 * (size_t)(q0 - first), 0xFF, 2 * (size_t)cn * sizeof(int64_t), s));
-      const dim3 sgrid(std::max<uint32_t>((I.N + 256 * KSG_WI_NPT - 1) / (256 * KSG_WI_NPT), 1),
-                       (cn + KSG_WI_PODS - 1) / KSG_WI_PODS);
+      const dim3 sgrid(std::max<uint32_t>((I.N + 256 * KSG_ST_NPT - 1) / (256 * KSG_ST_NPT), 1),
+                       (cn + KSG_ST_PODS - 1) / KSG_ST_PODS);
       hipLaunchKernelGGL(k_static, sgrid, dim3(256), 0, s, C, I.F, I.progs.p, I.prog_off_d.p, q0, cn,
                          I.stat.p + (size_t)((q0 - first) % (2 * chunk)) * I.N, I.mpred.p + 2 * (size_t)(q0 - first));
     }
@@ -3413,8 +3593,8 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
     for (uint32_t c0 = first; c0 < first + count; c0 += chunk) {
       const uint32_t cn = std::min(chunk, first + count - c0);
       HIPCHK(hipMemsetAsync(I.mpred.p, 0xFF, 2 * (size_t)cn * sizeof(int64_t), s));  // -1: no statically feasible node
-      const dim3 grid(std::max<uint32_t>((N + 256 * KSG_WI_NPT - 1) / (256 * KSG_WI_NPT), 1),
-                      (cn + KSG_WI_PODS - 1) / KSG_WI_PODS);
+      const dim3 grid(std::max<uint32_t>((N + 256 * KSG_ST_NPT - 1) / (256 * KSG_ST_NPT), 1),
+                      (cn + KSG_ST_PODS - 1) / KSG_ST_PODS);
       hipLaunchKernelGGL(k_static, grid, dim3(256), 0, s, C, F, I.progs.p, I.prog_off_d.p, c0, cn, I.stat.p, I.mpred.p);
       for (uint32_t j = c0; j < c0 + cn; ++j) {
         const uint8_t* prog = I.progs.p + I.prog_off[j];
@@ -3630,3 +3810,29 @@ float Engine::last_ms() const { return p_->last_ms; }
 std::vector<Engine::KernelStat> Engine::kernel_stats() const { return p_->stats; }
 
 }  // namespace ksg
+
+// Diagnostic: lane-exchange / sort self-test on the device (tests/test_wave_ops_gpu.py).
+extern "C" int ksg_debug_lane_selftest(int32_t* bad) {
+  if (!bad) return -1;
+  const int nb = 64;
+  std::vector<uint64_t> h((size_t)nb * 64);
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  for (size_t i = 0; i < h.size(); ++i) {
+    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+    h[i] = (i % 5 == 0) ? (x & 0xFF) : x;  // duplicates and small values too
+  }
+  uint64_t* d = nullptr;
+  int32_t* db = nullptr;
+  if (hipMalloc((void**)&d, h.size() * 8) != hipSuccess) return -2;
+  if (hipMalloc((void**)&db, 4) != hipSuccess) { (void)hipFree(d); return -2; }
+  int rc = 0;
+  if (hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice) != hipSuccess || hipMemset(db, 0, 4) != hipSuccess)
+    rc = -2;
+  if (!rc) {
+    hipLaunchKernelGGL(ksg::k_selftest_lanes, dim3(nb), dim3(64), 0, 0, d, db);
+    if (hipGetLastError() != hipSuccess || hipMemcpy(bad, db, 4, hipMemcpyDeviceToHost) != hipSuccess) rc = -2;
+  }
+  (void)hipFree(d);
+  (void)hipFree(db);
+  return rc;
+}

@@ -16,7 +16,8 @@ from ksg import Scheduler, generator as g  # noqa: E402
 
 n_nodes = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
 n_pods = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
-doc = g.generate(2, n_nodes=n_nodes, n_pods=n_pods)
+cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+doc = g.generate(cfg, n_nodes=n_nodes, n_pods=n_pods)
 s = Scheduler(doc["profile"])
 s.load_cluster(doc)
 L = s.L
@@ -47,6 +48,14 @@ print("fixup block total median", med([x[5] - x[0] for x in bs[1:]]), "cycles")
 ns = 10.0  # s_memrealtime: 100 MHz
 ev = [((~x[8]) & 0xFFFFFFFFFFFFFFFF) for x in bs]
 print("realtime (us): eval start->last tile eval", med([(bs[j][9] - ev[j]) / 100 for j in range(1, nw)]))
+print("realtime (us): eval block duration max", med([bs[j][28] / 100 for j in range(1, nw)]),
+      "mean", med([bs[j][29] / max(bs[j][31], 1) / 100 for j in range(1, nw)]), "blocks", bs[1][31])
+nb_ = [max(bs[j][31], 1) for j in range(1, nw)]
+print("eval wave-0 cycles per block: eval", med([bs[j][13] / nb_[j - 1] for j in range(1, nw)]),
+      "sort+merge", med([bs[j][14] / nb_[j - 1] for j in range(1, nw)]),
+      "LDS merge+tile store+arrive", med([bs[j][15] / nb_[j - 1] for j in range(1, nw)]),
+      "(of eval: load wait", med([bs[j][18] / nb_[j - 1] for j in range(1, nw)]), ")")
+print("realtime (us): first -> last eval block start", med([(bs[j][30] - ev[j]) / 100 for j in range(1, nw)]))
 print("realtime (us): eval start->last merge", med([(bs[j][10] - ev[j]) / 100 for j in range(1, nw)]))
 # window j's eval runs in the same launch as window j-1's fixup
 print("realtime (us): fixup W-1 start -> eval W start", med([(ev[j] - bs[j - 1][11]) / 100 for j in range(2, nw)]))

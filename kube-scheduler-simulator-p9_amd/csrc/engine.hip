@@ -97,7 +97,7 @@ struct DevProfile {
   uint64_t seed;
   int pos_fit, pos_ba;  // profile positions (-1 absent)
   int pos_taint, pos_na;
-  int64_t w_fit, w_ba;
+  int64_t w_fit, w_ba, w_taint, w_na;  // their weights (0 absent)
   // copies in device memory for run-time indexed loops (kernel-argument arrays
   // indexed at run time would be copied to scratch)
   const int32_t* fit_res_d;
@@ -288,6 +288,13 @@ __device__ __forceinline__ int64_t div_small(int64_t x, int64_t a) {
   if (q * a > x) q--;
   else if ((q + 1) * a <= x) q++;
   return q;
+}
+// floor(x / d) for x < 2^27, 1 <= d, quotient <= 128: one f32 reciprocal
+// estimate (error well below 1) and one exact correction either way.
+__device__ __forceinline__ uint32_t udiv_small(uint32_t x, uint32_t d) {
+  uint32_t q = (uint32_t)((float)x * __builtin_amdgcn_rcpf((float)d));
+  const int32_t r = (int32_t)(x - q * d);
+  return r < 0 ? q - 1 : ((uint32_t)r >= d ? q + 1 : q);
 }
 __device__ __forceinline__ bool lane0() { return (threadIdx.x & 63) == 0; }
 
@@ -1517,7 +1524,7 @@ struct WinArgs {
   uint32_t *kfilter, *sfilter;  // kept outputs / scratch ring of 2*KSG_BATCH pods
   int32_t *kscore, *sscore, *ktotal, *stotal;
   // eval part: window E = queue pods [e0, e0 + ne)
-  uint32_t e0, ne, T, npt;  // T tiles of KSG_TILE * npt nodes per pod
+  uint32_t e0, ne, T, npt, tile_len;  // T tiles of tile_len <= KSG_TILE * npt nodes per pod
   uint64_t* tile_top;    // [KSG_BATCH][T][KSG_TOPK]
   int32_t* tile_feas;    // [KSG_BATCH][T]
   uint32_t* arrive;      // [KSG_BATCH] tile arrivals (reset by the last block)
@@ -1702,10 +1709,16 @@ __device__ __forceinline__ uint32_t eval_row_s(const RowV& r, const DevProfile& 
   if (code != KSG_FILTER_PASS) return code;
   if (F.pos_fit >= 0) fit_s = (int32_t)fit_score_row<MODE>(r, F, h);
   if (F.pos_ba >= 0) ba_s = (int32_t)ba_score_row<MODE>(r, F, h);
-  bool re = false;
-  const bool skip_na = (h->flags & KPF_SKIP_NA_SCORE) != 0;
-  total = static_total(F, skip_na, fit_s, ba_s, s.raw >> 20, (int64_t)(s.raw & KSG_RAW_NA_MASK), MT < 0 ? 0 : MT,
-                       MA < 0 ? 0 : MA, re);
+  // DefaultNormalizeScore (reverse for Taint), weighted; the sum is order-free
+  total = (int64_t)fit_s * F.w_fit + (int64_t)ba_s * F.w_ba;
+  if (F.pos_taint >= 0) {
+    const uint32_t t = s.raw >> 20;
+    total += (int64_t)(MT <= 0 ? 100u : 100u - udiv_small(100u * t, (uint32_t)MT)) * F.w_taint;
+  }
+  if (F.pos_na >= 0 && !(h->flags & KPF_SKIP_NA_SCORE)) {
+    const uint32_t a = s.raw & KSG_RAW_NA_MASK;
+    total += (int64_t)(MA <= 0 ? a : udiv_small(100u * a, (uint32_t)MA)) * F.w_na;
+  }
   return code;
 }
 // raw: the static record's raw Taint/NodeAffinity scores (STAT profiles)
@@ -1807,6 +1820,12 @@ __global__ void k_selftest_lanes(const uint64_t* in, int32_t* bad) {
     c_in += __shfl(v, j, 64) == v;
   }
   e += c_sorted != c_in;
+  for (int i = 0; i < 16; ++i) {  // udiv_small on its domain (quotient <= 100)
+    const uint64_t z = splitmix64(v + (uint64_t)i);
+    const uint32_t d = 1u + (uint32_t)(z % (i < 8 ? 4096u : 1048576u));
+    const uint32_t x = (uint32_t)((z >> 24) % (100ull * d + 1));
+    e += udiv_small(x, d) != x / d;
+  }
   atomicAdd(bad, e);
 }
 
@@ -1926,8 +1945,8 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   static_assert(96 * 4 + sizeof(PodLite) + 16 <= 192 * 4, "eval LDS layout");
   // the next node's row and static record are loaded while this one is evaluated
   auto fetch = [&](uint32_t kk, RowV& r, StaticRec& sr) {
-    const uint32_t nn = (tile * A.npt + kk) * KSG_TILE + tid;
-    if (nn < C.N) {
+    const uint32_t to = kk * KSG_TILE + tid, nn = tile * A.tile_len + to;
+    if (to < A.tile_len && nn < C.N) {
       const int hit = pend_lds((int32_t)(C.goff + nn));
       if (hit >= 0) r = A.pprev[hit].after;
       else load_row(C, nn, A.need_eph, r);
@@ -1943,13 +1962,13 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   if (A.estamps && w == 15) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: load wait
   ETIME(tl);
   t_wait += tl - t0;
-  const uint32_t n = (tile * A.npt + k) * KSG_TILE + tid;
+  const uint32_t to = k * KSG_TILE + tid, n = tile * A.tile_len + to;
   const RowV r = rnext;
   const StaticRec sr = snext;
   if (k + 1 < A.npt) fetch(k + 1, rnext, snext);
   uint64_t key = 0;
   bool feasible = false, achT = false, achA = false;
-  if (n < C.N) {
+  if (to < A.tile_len && n < C.N) {
     int32_t fit_s, ba_s;
     int64_t total;
     uint32_t code, raw = 0;
@@ -2023,8 +2042,8 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     out_ptrs(A, q, C.N, of, os, ot);
 #pragma unroll 1
     for (uint32_t k = 0; k < A.npt; ++k) {
-      const uint32_t n = (tile * A.npt + k) * KSG_TILE + tid;
-      if (n >= C.N) break;
+      const uint32_t to = k * KSG_TILE + tid, n = tile * A.tile_len + to;
+      if (to >= A.tile_len || n >= C.N) break;
       const PatchV pt = stash[(stash_all ? k * 16 + w : k) * 64 + lane];
       write_pair<STAT>(F, of, os, ot, C.N, n, pt.code, pt.fitba & 0xFFFF, pt.fitba >> 16, pt.total, pt.raw);
     }
@@ -2975,7 +2994,10 @@ struct Engine::Impl {
   bool batch_ok = false;     // profile of Fit / BA (/ Taint / NodeAffinity) plugins only
   bool batch_static = false;
   uint32_t stat_chunk_cap = 0;
-  uint32_t n_cus = 256;  // compute units of the device  // diagnostic: cap on the static chunk (pods, multiple of KSG_BATCH)  // ... with Taint / NodeAffinity: static records per pod (k_static)
+  uint32_t n_cus = 256;  // compute units of the device
+  hipStream_t sstream = nullptr;  // low-priority side stream (static records of the window path)
+  bool static_side = false;  // KSG_STATIC_SIDE=1: measured no faster (the windows slow down beside it)
+  hipEvent_t sev_ready[3] = {nullptr, nullptr, nullptr}, sev_free = nullptr;  // diagnostic: cap on the static chunk (pods, multiple of KSG_BATCH)  // ... with Taint / NodeAffinity: static records per pod (k_static)
   DBuf<uint64_t> tile_top;
   DBuf<int32_t> tfeas, pend_n;
   DBuf<uint32_t> arrive;
@@ -3034,6 +3056,9 @@ Engine::~Engine() {
   if (p_->comm) (void)ncclCommDestroy(p_->comm);
   if (p_->ev0) (void)hipEventDestroy(p_->ev0);
   if (p_->ev1) (void)hipEventDestroy(p_->ev1);
+  for (hipEvent_t e : {p_->sev_ready[0], p_->sev_ready[1], p_->sev_ready[2], p_->sev_free})
+    if (e) (void)hipEventDestroy(e);
+  if (p_->sstream) (void)hipStreamDestroy(p_->sstream);
   if (p_->own_stream && p_->stream) (void)hipStreamDestroy(p_->stream);
   delete p_;
 }
@@ -3052,6 +3077,12 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg.device) == hipSuccess && cus > 0)
       I.n_cus = (uint32_t)cus;
+  }
+  {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+    HIPCHK(hipStreamCreateWithPriority(&I.sstream, hipStreamNonBlocking, least));
+    if (const char* e = std::getenv("KSG_STATIC_SIDE")) I.static_side = std::strtol(e, nullptr, 10) != 0;
   }
   HIPCHK(hipEventCreate(&I.ev0));
   HIPCHK(hipEventCreate(&I.ev1));
@@ -3085,10 +3116,10 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   F.ipa_ignore_existing_pref = cfg.ipa_ignore_existing_pref;
   F.seed = cfg.seed;
   F.pos_fit = F.pos_ba = F.pos_taint = F.pos_na = -1;
-  F.w_fit = F.w_ba = 0;
+  F.w_fit = F.w_ba = F.w_taint = F.w_na = 0;
   for (int i = 0; i < F.n; ++i) {
-    if (F.plugins[i] == KP_TAINT) F.pos_taint = i;
-    if (F.plugins[i] == KP_NA) F.pos_na = i;
+    if (F.plugins[i] == KP_TAINT) { F.pos_taint = i; F.w_taint = F.weight[i]; }
+    if (F.plugins[i] == KP_NA) { F.pos_na = i; F.w_na = F.weight[i]; }
     if (F.plugins[i] == KP_FIT) { F.pos_fit = i; F.w_fit = F.weight[i]; }
     if (F.plugins[i] == KP_BA) { F.pos_ba = i; F.w_ba = F.weight[i]; }
   }
@@ -3122,6 +3153,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   return true;
 }
 
+static uint32_t eval_tiles(uint32_t N, uint32_t cus);
 bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, uint32_t term_cap, uint32_t req_cap,
                     uint32_t val_cap, std::string& err) {
   Impl& I = *p_;
@@ -3200,7 +3232,7 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     return false;
   HIPCHK(hipMemsetAsync(I.exist_any.p, 0, 4, s));
   if (I.batch_ok && I.R <= 4) {
-    uint32_t T = std::max<uint32_t>((I.N + KSG_TILE - 1) / KSG_TILE, 1);
+    uint32_t T = eval_tiles(I.N, I.n_cus);
     size_t Nn = std::max<uint32_t>(I.N, 1);
     if (!I.tile_top.alloc((size_t)KSG_BATCH * T * KSG_TOPK, err) || !I.tfeas.alloc((size_t)KSG_BATCH * T * 3, err) ||
         !I.arrive.alloc(KSG_BATCH, err) || !I.pend_n.alloc(2, err) || !I.wrec.alloc(2 * kRecBytes, err) ||
@@ -3215,6 +3247,21 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   return true;
 }
 
+// Eval tiles per pod: the fewest nodes per thread (npt) with which a window's
+// eval blocks (one per CU: 1,024 threads, the window LDS) fit the CUs beside the
+// replay block in one round; at most 16 (then several rounds).  (Tiles balanced
+// to fill every CU were measured slower: the replay block's memory latency
+// grows with the eval blocks around it.)
+static uint32_t eval_npt(uint32_t N, uint32_t cus) {
+  uint32_t npt = 1;
+  while (npt < 16 && (uint64_t)KSG_BATCH * ((N + KSG_TILE * npt - 1) / (KSG_TILE * npt)) + 1 > cus) ++npt;
+  return npt;
+}
+static uint32_t eval_tiles(uint32_t N, uint32_t cus) {
+  const uint32_t npt = eval_npt(N, cus);
+  return std::max<uint32_t>((N + KSG_TILE * npt - 1) / (KSG_TILE * npt), 1);
+}
+
 // Windows of KSG_BATCH pods, one k_window launch each (see the kernel): launch
 // j evaluates window j+1 and replays window j; the sharded path all-gathers
 // each window's candidate records between launches.
@@ -3224,9 +3271,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   DevCluster C = I.cluster();
   // nodes per eval thread: enough that one window's eval blocks fit the CUs
   // beside the replay block in one round (one 1,024-thread block per CU)
-  uint32_t npt = 1;
-  while (npt < 16 && (uint64_t)KSG_BATCH * ((I.N + KSG_TILE * npt - 1) / (KSG_TILE * npt)) + 1 > I.n_cus) ++npt;
-  const uint32_t T = std::max<uint32_t>((I.N + KSG_TILE * npt - 1) / (KSG_TILE * npt), 1);
+  const uint32_t T = eval_tiles(I.N, I.n_cus), npt = eval_npt(I.N, I.n_cus), tile_len = npt * KSG_TILE;
   const uint32_t nwin = (count + KSG_BATCH - 1) / KSG_BATCH;
   if (I.sample_every) {
     size_t need = 2 * (nwin + 2);
@@ -3256,6 +3301,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   A.sfilter = I.bfilter.p; A.sscore = I.bscore.p; A.stotal = I.btotal.p;
   A.T = T;
   A.npt = npt;
+  A.tile_len = tile_len;
   A.tile_top = I.tile_top.p;
   A.tile_feas = I.tfeas.p;
   A.arrive = I.arrive.p;
@@ -3264,18 +3310,49 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   // static records: a ring of two chunks of whole windows (window j+1's eval and
   // window j's replay may sit in consecutive chunks); chunk c computed by k_static
   // just before the launch that evaluates its first window
+  //
+  // Inline: chunk c is computed on the engine stream just before the launch
+  // that evaluates its first window (ring of 2 chunks).  Side stream (default):
+  // k_static runs on a low-priority stream two chunks ahead, on the CUs the
+  // window launches leave idle; ring of 3 chunks, two events per chunk:
+  // ready(c) before the launch evaluating chunk c's first window, and the slot
+  // of chunk c+2 free after the launch replaying chunk c-1's last window.
   const bool stat = I.batch_static;
-  uint32_t chunk = 0;
+  const bool side = stat && I.sstream && I.static_side;
+  const uint32_t nslots = side ? 3 : 2;
+  uint32_t chunk = 0, nchunks = 0;
   if (stat) {
     const size_t Nn = std::max<uint32_t>(I.N, 1);
-    chunk = (uint32_t)std::max<size_t>(KSG_BATCH, (((size_t)64 << 20) / (Nn * sizeof(StaticRec))) / KSG_BATCH * KSG_BATCH);
+    const size_t budget = side ? ((size_t)32 << 20) : ((size_t)64 << 20);
+    chunk = (uint32_t)std::max<size_t>(KSG_BATCH, (budget / (Nn * sizeof(StaticRec))) / KSG_BATCH * KSG_BATCH);
     chunk = std::min<uint32_t>(chunk, (count + KSG_BATCH - 1) / KSG_BATCH * KSG_BATCH);
     if (I.stat_chunk_cap) chunk = std::min<uint32_t>(chunk, I.stat_chunk_cap);  // tests: force ring roll-over
-    if (!I.stat.alloc((size_t)2 * chunk * Nn, err) || !I.mpred.alloc(2 * (size_t)std::max<uint32_t>(count, 1), err))
+    nchunks = (count + chunk - 1) / chunk;
+    if (!I.stat.alloc((size_t)nslots * chunk * Nn, err) || !I.mpred.alloc(2 * (size_t)std::max<uint32_t>(count, 1), err))
       return false;
     A.stat = I.stat.p;
-    A.stat_ring = 2 * chunk;
+    A.stat_ring = nslots * chunk;
     A.mpred = I.mpred.p;
+    if (side && !I.sev_ready[0]) {
+      for (auto* e : {&I.sev_ready[0], &I.sev_ready[1], &I.sev_ready[2], &I.sev_free})
+        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+  }
+  auto issue_static = [&](uint32_t c, hipStream_t st) -> bool {
+    const uint32_t q0 = first + c * chunk, cn = std::min(chunk, first + count - q0);
+    HIPCHK(hipMemsetAsync(I.mpred.p + 2 * (size_t)(q0 - first), 0xFF, 2 * (size_t)cn * sizeof(int64_t), st));
+    const dim3 sgrid(std::max<uint32_t>((I.N + 256 * KSG_ST_NPT - 1) / (256 * KSG_ST_NPT), 1),
+                     (cn + KSG_ST_PODS - 1) / KSG_ST_PODS);
+    hipLaunchKernelGGL(k_static, sgrid, dim3(256), 0, st, C, I.F, I.progs.p, I.prog_off_d.p, q0, cn,
+                       I.stat.p + (size_t)((q0 - first) % (nslots * chunk)) * I.N, I.mpred.p + 2 * (size_t)(q0 - first));
+    if (side) HIPCHK(hipEventRecord(I.sev_ready[c % 3], st));
+    return true;
+  };
+  if (side) {  // the side stream starts after the engine stream's work so far (uploads, previous runs)
+    HIPCHK(hipEventRecord(I.sev_free, s));
+    HIPCHK(hipStreamWaitEvent(I.sstream, I.sev_free, 0));
+    for (uint32_t c = 0; c < std::min<uint32_t>(2, nchunks); ++c)
+      if (!issue_static(c, I.sstream)) return false;
   }
   for (int64_t j = -1; j < (int64_t)nwin; ++j) {
     const int64_t E = j + 1, W = j;
@@ -3299,13 +3376,11 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     const int64_t P = W - 1;  // P_{W-1}: the list the eval part overrides rows from, too
     A.pprev = I.pend.p + (size_t)(P & 1) * KSG_BATCH;
     A.pprev_n = I.pend_n.p + (P & 1);
-    if (stat && A.ne && (A.e0 - first) % chunk == 0) {
-      const uint32_t q0 = A.e0, cn = std::min(chunk, first + count - q0);
-      HIPCHK(hipMemsetAsync(I.mpred.p + 2 * (size_t)(q0 - first), 0xFF, 2 * (size_t)cn * sizeof(int64_t), s));
-      const dim3 sgrid(std::max<uint32_t>((I.N + 256 * KSG_ST_NPT - 1) / (256 * KSG_ST_NPT), 1),
-                       (cn + KSG_ST_PODS - 1) / KSG_ST_PODS);
-      hipLaunchKernelGGL(k_static, sgrid, dim3(256), 0, s, C, I.F, I.progs.p, I.prog_off_d.p, q0, cn,
-                         I.stat.p + (size_t)((q0 - first) % (2 * chunk)) * I.N, I.mpred.p + 2 * (size_t)(q0 - first));
+    const bool chunk_start = stat && A.ne && (A.e0 - first) % chunk == 0;
+    const uint32_t cidx = chunk_start ? (A.e0 - first) / chunk : 0;
+    if (chunk_start) {
+      if (side) HIPCHK(hipStreamWaitEvent(s, I.sev_ready[cidx % 3], 0));
+      else if (!issue_static(cidx, s)) return false;
     }
     bool sampled = I.sample_every && A.ne && A.nw && I.n_samples * 2 + 2 <= I.sev.size();
     if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
@@ -3321,6 +3396,11 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     if (sampled) {
       HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
       I.n_samples++;
+    }
+    if (side && chunk_start && cidx + 2 < nchunks) {  // chunk cidx-1 fully replayed: its slot takes chunk cidx+2
+      HIPCHK(hipEventRecord(I.sev_free, s));
+      HIPCHK(hipStreamWaitEvent(I.sstream, I.sev_free, 0));
+      if (!issue_static(cidx + 2, I.sstream)) return false;
     }
     if (sharded && A.ne) {
       if (I.xmode == 1) {

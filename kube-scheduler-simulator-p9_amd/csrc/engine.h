@@ -51,6 +51,7 @@ struct NodeSoA {
   // topology slots: node label key per slot and value count
   std::vector<int32_t> topo_key;
   std::vector<uint32_t> topo_base, topo_count;
+  std::vector<uint8_t> topo_unique;  // per slot: every value of the key sits on one node (whole cluster)
   uint32_t topo_pairs = 0;
 };
 

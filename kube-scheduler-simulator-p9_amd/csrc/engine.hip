@@ -669,12 +669,15 @@ __global__ void k_pts_prep(DevCluster C, DevScratch S, const uint8_t* prog) {
 }
 
 // minMatchNum / TpKeyToDomainsNum per filter topology key
-__global__ void k_pts_reduce(DevCluster C, DevScratch S, const uint8_t* prog) {
+// slots: topology slots to reduce (sharded chain: the slots whose domains each
+// sit on one node first, from local counts; the shared ones after the exchange)
+__global__ void k_pts_reduce(DevCluster C, DevScratch S, const uint8_t* prog, uint32_t slots) {
   ProgView V = view(prog);
   const ksg_prog* h = V.h;
   uint32_t seen = 0;
   for (int c = 0; c < h->n_tsc_filter; ++c) {
     int slot = h->tsc[c].topo;
+    if (!((slots >> slot) & 1u)) continue;
     if ((seen >> slot) & 1u) continue;
     seen |= 1u << slot;
     uint32_t base = C.tbase[slot], cnt = C.tcount[slot];
@@ -832,7 +835,10 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
 }
 
 // topologyNormalizingWeight per score constraint
-__global__ void k_pts_weights(DevCluster C, DevScratch S, DevOut O, const uint8_t* prog) {
+// regcnt (sharded chain, or null): per score constraint, the global count of
+// registered domains of a slot whose domains each sit on one node (uniq)
+__global__ void k_pts_weights(DevCluster C, DevScratch S, DevOut O, const uint8_t* prog, const int64_t* regcnt,
+                              uint32_t uniq) {
   ProgView V = view(prog);
   const ksg_prog* h = V.h;
   __shared__ int32_t red[kBlock / 64];
@@ -842,6 +848,8 @@ __global__ void k_pts_weights(DevCluster C, DevScratch S, DevOut O, const uint8_
     int64_t size = 0;
     if (t.is_hostname) {
       size = (int64_t)O.sum->feasible - O.sum->ignored;
+    } else if (t.first_of_key && regcnt && ((uniq >> t.topo) & 1u)) {
+      size = regcnt[c - nf];
     } else if (t.first_of_key) {
       uint32_t base = C.tbase[t.topo], cnt = C.tcount[t.topo];
       int32_t x = 0;
@@ -1029,6 +1037,159 @@ __global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* pr
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   ProgView V = view(prog);
   commit_cycle(C, V, O.sum, mode, prow, false);
+}
+
+// ---- sharded per-pod chain: every rank runs the cycle on its
+// nodes and its existing pods (pods live with their node); at the cycle's
+// global reductions the ranks all-gather an int64 vector and merge it:
+//   X1 after the scans: the pair histograms of the topology slots whose
+//      domains span nodes (SUM; presence: any), IPA flags / existing-anti slot
+//      mask (OR), and per slot whose domains each sit on one node the local
+//      (min, #domains) of PodTopologySpread's filter histogram (MIN, SUM);
+//   X2 after Filter+Score: feasible (SUM), ignored (SUM), status (OR), the
+//      normalisers' max / min per position (MAX / MIN), the PTS score
+//      registration of shared pairs (any) and per score constraint on a
+//      one-node-domain slot its registered-domain count (SUM);
+//   X3 after the PTS score: max / min per position again;
+//   X4 after NormalizeScore: the argmax key (MAX) and status (OR).
+// Merging is rank-order independent, so every rank holds the same summary
+// and the owner of the selected node applies the assume.
+struct XLay {
+  uint32_t nsp;          // shared pairs
+  const uint32_t* spair; // [nsp] pair index
+  uint32_t uniq;         // slot bitmask: every value on one node
+};
+__device__ __forceinline__ int64_t xmerge_op(const int64_t* recv, uint32_t ranks, size_t len, size_t i, int op) {
+  int64_t v = recv[i];
+  for (uint32_t r = 1; r < ranks; ++r) {
+    const int64_t x = recv[(size_t)r * len + i];
+    switch (op) {
+      case 0: v += x; break;                      // sum
+      case 1: v = x > v ? x : v; break;           // max
+      case 2: v = x < v ? x : v; break;           // min
+      case 3: v |= x; break;                      // or
+      default: v = (uint64_t)x > (uint64_t)v ? x : v; break;  // unsigned max
+    }
+  }
+  return v;
+}
+__device__ __forceinline__ size_t x1_len(const XLay& L) { return (size_t)7 * L.nsp + 2 + 2 * KSG_MAX_TOPO; }
+__global__ void k_x1_pack(DevScratch S, DevOut O, XLay L, int64_t* out) {
+  for (uint32_t i = threadIdx.x; i < L.nsp; i += blockDim.x) {
+    const uint32_t p = L.spair[i];
+    out[i] = S.hist_f[p];
+    out[L.nsp + i] = S.present_f[p];
+    out[2 * L.nsp + i] = S.hist_s[p];
+    out[3 * L.nsp + i] = S.ipa_aff[p];
+    out[4 * L.nsp + i] = S.ipa_anti[p];
+    out[5 * L.nsp + i] = S.ipa_exist[p];
+    out[6 * L.nsp + i] = S.ipa_score[p];
+  }
+  const size_t b = (size_t)7 * L.nsp;
+  if (threadIdx.x == 0) {
+    out[b] = S.exist_any[0];
+    out[b + 1] = O.sum->ipa_flags;
+  }
+  if (threadIdx.x < KSG_MAX_TOPO) {
+    out[b + 2 + threadIdx.x] = S.pts_min[threadIdx.x];
+    out[b + 2 + KSG_MAX_TOPO + threadIdx.x] = S.pts_dom[threadIdx.x];
+  }
+}
+__global__ void k_x1_merge(DevScratch S, DevOut O, XLay L, const int64_t* recv, uint32_t ranks) {
+  const size_t len = x1_len(L);
+  for (uint32_t i = threadIdx.x; i < L.nsp; i += blockDim.x) {
+    const uint32_t p = L.spair[i];
+    S.hist_f[p] = (int32_t)xmerge_op(recv, ranks, len, i, 0);
+    S.present_f[p] = xmerge_op(recv, ranks, len, L.nsp + i, 0) > 0 ? 1 : 0;
+    S.hist_s[p] = (int32_t)xmerge_op(recv, ranks, len, 2 * L.nsp + i, 0);
+    S.ipa_aff[p] = (int32_t)xmerge_op(recv, ranks, len, 3 * L.nsp + i, 0);
+    S.ipa_anti[p] = (int32_t)xmerge_op(recv, ranks, len, 4 * L.nsp + i, 0);
+    S.ipa_exist[p] = (int32_t)xmerge_op(recv, ranks, len, 5 * L.nsp + i, 0);
+    S.ipa_score[p] = xmerge_op(recv, ranks, len, 6 * L.nsp + i, 0);
+  }
+  const size_t b = (size_t)7 * L.nsp;
+  if (threadIdx.x == 0) {
+    S.exist_any[0] = (uint32_t)xmerge_op(recv, ranks, len, b, 3);
+    O.sum->ipa_flags = (uint32_t)xmerge_op(recv, ranks, len, b + 1, 3);
+  }
+  if (threadIdx.x < KSG_MAX_TOPO && ((L.uniq >> threadIdx.x) & 1u)) {
+    S.pts_min[threadIdx.x] = (int32_t)xmerge_op(recv, ranks, len, b + 2 + threadIdx.x, 2);
+    S.pts_dom[threadIdx.x] = (int32_t)xmerge_op(recv, ranks, len, b + 2 + KSG_MAX_TOPO + threadIdx.x, 0);
+  }
+}
+__device__ __forceinline__ size_t x2_len(const XLay& L) { return 3 + 2 * KSG_MAX_PLUGINS + (size_t)L.nsp + KSG_MAX_TSC; }
+__global__ void k_x2_pack(DevCluster C, DevScratch S, DevOut O, const uint8_t* prog, XLay L, int64_t* out) {
+  __shared__ int32_t red[kBlock / 64];
+  const ksg_prog* h = view(prog).h;
+  if (threadIdx.x == 0) {
+    out[0] = O.sum->feasible;
+    out[1] = O.sum->ignored;
+    out[2] = O.sum->status;
+  }
+  if (threadIdx.x < KSG_MAX_PLUGINS) {
+    out[3 + threadIdx.x] = O.sum->max_score[threadIdx.x];
+    out[3 + KSG_MAX_PLUGINS + threadIdx.x] = O.sum->min_score[threadIdx.x];
+  }
+  const size_t b = 3 + 2 * KSG_MAX_PLUGINS;
+  for (uint32_t i = threadIdx.x; i < L.nsp; i += blockDim.x) out[b + i] = S.reg[L.spair[i]];
+  const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
+  for (int c = 0; c < KSG_MAX_TSC; ++c) {
+    int64_t cnt = 0;
+    if (c < ns) {
+      const ksg_tsc& t = h->tsc[nf + c];
+      if (!t.is_hostname && t.first_of_key && ((L.uniq >> t.topo) & 1u)) {
+        const uint32_t base = C.tbase[t.topo], n = C.tcount[t.topo];
+        int32_t x = 0;
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) x += S.reg[base + i];
+        x = wave_sum(x);
+        if (lane0()) red[threadIdx.x >> 6] = x;
+        __syncthreads();
+        for (int w = 0; w < (int)(blockDim.x / 64); ++w) cnt += red[w];
+        __syncthreads();
+      }
+    }
+    if (threadIdx.x == 0) out[b + L.nsp + c] = cnt;
+  }
+}
+__global__ void k_x2_merge(DevScratch S, DevOut O, XLay L, const int64_t* recv, uint32_t ranks, int64_t* regcnt) {
+  const size_t len = x2_len(L);
+  if (threadIdx.x == 0) {
+    O.sum->feasible = (int32_t)xmerge_op(recv, ranks, len, 0, 0);
+    O.sum->ignored = (int32_t)xmerge_op(recv, ranks, len, 1, 0);
+    O.sum->status = (int32_t)xmerge_op(recv, ranks, len, 2, 3);
+  }
+  if (threadIdx.x < KSG_MAX_PLUGINS) {
+    O.sum->max_score[threadIdx.x] = xmerge_op(recv, ranks, len, 3 + threadIdx.x, 1);
+    O.sum->min_score[threadIdx.x] = xmerge_op(recv, ranks, len, 3 + KSG_MAX_PLUGINS + threadIdx.x, 2);
+  }
+  const size_t b = 3 + 2 * KSG_MAX_PLUGINS;
+  for (uint32_t i = threadIdx.x; i < L.nsp; i += blockDim.x)
+    S.reg[L.spair[i]] = xmerge_op(recv, ranks, len, b + i, 0) > 0 ? 1 : 0;
+  if (threadIdx.x < KSG_MAX_TSC) regcnt[threadIdx.x] = xmerge_op(recv, ranks, len, b + L.nsp + threadIdx.x, 0);
+}
+__global__ void k_x3_pack(DevOut O, int64_t* out) {
+  if (threadIdx.x < KSG_MAX_PLUGINS) {
+    out[threadIdx.x] = O.sum->max_score[threadIdx.x];
+    out[KSG_MAX_PLUGINS + threadIdx.x] = O.sum->min_score[threadIdx.x];
+  }
+}
+__global__ void k_x3_merge(DevOut O, const int64_t* recv, uint32_t ranks) {
+  if (threadIdx.x < KSG_MAX_PLUGINS) {
+    O.sum->max_score[threadIdx.x] = xmerge_op(recv, ranks, 2 * KSG_MAX_PLUGINS, threadIdx.x, 1);
+    O.sum->min_score[threadIdx.x] = xmerge_op(recv, ranks, 2 * KSG_MAX_PLUGINS, KSG_MAX_PLUGINS + threadIdx.x, 2);
+  }
+}
+__global__ void k_x4_pack(DevOut O, int64_t* out) {
+  if (threadIdx.x == 0) {
+    out[0] = (int64_t)O.sum->best_key;
+    out[1] = O.sum->status;
+  }
+}
+__global__ void k_x4_merge(DevOut O, const int64_t* recv, uint32_t ranks) {
+  if (threadIdx.x == 0) {
+    O.sum->best_key = (uint64_t)xmerge_op(recv, ranks, 2, 0, 4);
+    O.sum->status = (int32_t)xmerge_op(recv, ranks, 2, 1, 3);
+  }
 }
 
 // Reserve / Unreserve on an explicit node (the framework's selectHost choice).
@@ -2980,6 +3141,10 @@ struct Engine::Impl {
   DBuf<StaticRec> stat;   // static records of a chunk of pods [chunk][N]
   DBuf<int64_t> mpred;    // [chunk][2] static max of the Taint / NodeAffinity raw scores
   DBuf<int32_t> saux;     // k_fs_static counters
+  // sharded per-pod chain: pairs of topology slots whose domains span nodes, slot mask of one-node domains
+  DBuf<uint32_t> spair;
+  uint32_t nsp = 0, uniq = 0;
+  DBuf<int64_t> xregcnt;  // merged registered-domain counts per score constraint
   size_t prog_bytes = 0;  // used bytes of the program blob
   // kept per-pair outputs
   uint32_t keep_first = 0, keep_n = 0;
@@ -3179,6 +3344,18 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   I.topo.topo_base = ns.topo_base;
   I.topo.topo_count = ns.topo_count;
   I.topo.topo_pairs = ns.topo_pairs;
+  {
+    std::vector<uint32_t> sp;
+    I.uniq = 0;
+    for (size_t t = 0; t < ns.topo_key.size(); ++t) {
+      const bool u = t < ns.topo_unique.size() && ns.topo_unique[t];
+      if (u) I.uniq |= 1u << t;
+      else
+        for (uint32_t v = 0; v < ns.topo_count[t]; ++v) sp.push_back(ns.topo_base[t] + v);
+    }
+    I.nsp = (uint32_t)sp.size();
+    if (!I.spair.upload(sp, s, err) || !I.xregcnt.alloc(KSG_MAX_TSC, err)) return false;
+  }
   if (!I.topo_key_d.upload(ns.topo_key, s, err) || !I.topo_base_d.upload(ns.topo_base, s, err) ||
       !I.topo_count_d.upload(ns.topo_count, s, err))
     return false;
@@ -3511,10 +3688,16 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
 }
 
 // All-gather `bytes` from every rank into I.xrecv (rank order), on the engine stream.
+static bool xgather(Engine::Impl& I, size_t bytes, std::string& err);
 static bool exchange(Engine::Impl& I, const void* src, size_t bytes, std::string& err) {
   hipStream_t s = I.stream;
   if (!I.xsend.grow(bytes, 0, s, err) || !I.xrecv.grow(bytes * I.xranks, 0, s, err)) return false;
   HIPCHK(hipMemcpyAsync(I.xsend.p, src, bytes, hipMemcpyDeviceToDevice, s));
+  return xgather(I, bytes, err);
+}
+// All-gather `bytes` from I.xsend into I.xrecv (rank order).
+static bool xgather(Engine::Impl& I, size_t bytes, std::string& err) {
+  hipStream_t s = I.stream;
   if (I.xmode == 1) {
     ncclResult_t nr = ncclAllGather(I.xsend.p, I.xrecv.p, bytes, ncclUint8, I.comm, s);
     if (nr != ncclSuccess) { err = std::string("ncclAllGather: ") + ncclGetErrorString(nr); return false; }
@@ -3666,7 +3849,8 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   }
   I.n_samples = 0;
   HIPCHK(hipEventRecord(I.ev0, s));
-  if (I.static_ok && I.static_fits) {
+  const bool xchain = I.xranks > 1;  // sharded per-pod chain (exchange points X1..X4)
+  if (I.static_ok && I.static_fits && !xchain) {
     const size_t Nn = std::max<uint32_t>(N, 1);
     const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(count, ((size_t)64 << 20) / (Nn * sizeof(StaticRec))));
     if (!I.stat.alloc((size_t)chunk * Nn, err) || !I.mpred.alloc(2 * (size_t)chunk, err)) return false;
@@ -3700,10 +3884,21 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
     HIPCHK(hipGetLastError());
     return true;
   }
+  const XLay XL{I.nsp, I.spair.p, I.uniq};
+  // one exchange point: pack (device), all-gather, merge (device)
+  auto xrun = [&](size_t len, auto pack, auto merge) -> bool {
+    const size_t bytes = std::max<size_t>(len, 1) * sizeof(int64_t);
+    if (!I.xsend.grow(bytes, 0, s, err) || !I.xrecv.grow(bytes * I.xranks, 0, s, err)) return false;
+    pack(reinterpret_cast<int64_t*>(I.xsend.p));
+    if (!xgather(I, bytes, err)) return false;
+    merge(reinterpret_cast<const int64_t*>(I.xrecv.p));
+    return true;
+  };
+  const uint32_t xr = I.xranks;
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
     const int mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
-    DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j, I.arrive1.p, mode, I.prow.p + j};
+    DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j, xchain ? nullptr : I.arrive1.p, mode, I.prow.p + j};
     bool kept = I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n;
     if (kept) {
       size_t k = j - I.keep_first;
@@ -3721,9 +3916,17 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
       hipLaunchKernelGGL(k_scan_pods, dim3((pc + kBlock - 1) / kBlock), b, 0, s, C, F, S, O, prog);
       if (ipa)
         hipLaunchKernelGGL(k_scan_terms, dim3((I.tcap + kBlock - 1) / kBlock), b, 0, s, C, F, S, O, prog);
+      const dim3 gr(std::max<uint32_t>(std::min<uint32_t>(gN.x, 256), 1));
       if (pts) {
         hipLaunchKernelGGL(k_pts_prep, gN, b, 0, s, C, S, prog);
-        hipLaunchKernelGGL(k_pts_reduce, dim3(std::max<uint32_t>(std::min<uint32_t>(gN.x, 256), 1)), b, 0, s, C, S, prog);
+        hipLaunchKernelGGL(k_pts_reduce, gr, b, 0, s, C, S, prog, xchain ? I.uniq : ~0u);
+      }
+      if (xchain) {  // X1
+        const size_t len = (size_t)7 * I.nsp + 2 + 2 * KSG_MAX_TOPO;
+        if (!xrun(len, [&](int64_t* o) { hipLaunchKernelGGL(k_x1_pack, dim3(1), b, 0, s, S, O, XL, o); },
+                  [&](const int64_t* r) { hipLaunchKernelGGL(k_x1_merge, dim3(1), b, 0, s, S, O, XL, r, xr); }))
+          return false;
+        if (pts) hipLaunchKernelGGL(k_pts_reduce, gr, b, 0, s, C, S, prog, ~I.uniq);
       }
     }
     bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
@@ -3733,14 +3936,32 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
       HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
       I.n_samples++;
     }
+    if (xchain) {  // X2
+      const size_t len = 3 + 2 * KSG_MAX_PLUGINS + (size_t)I.nsp + KSG_MAX_TSC;
+      if (!xrun(len, [&](int64_t* o) { hipLaunchKernelGGL(k_x2_pack, dim3(1), b, 0, s, C, S, O, prog, XL, o); },
+                [&](const int64_t* r) {
+                  hipLaunchKernelGGL(k_x2_merge, dim3(1), b, 0, s, S, O, XL, r, xr, I.xregcnt.p);
+                }))
+        return false;
+    }
     if (F.has_ext) {
       if (pts_pos >= 0 && pts) {
-        hipLaunchKernelGGL(k_pts_weights, dim3(1), b, 0, s, C, S, O, prog);
+        hipLaunchKernelGGL(k_pts_weights, dim3(1), b, 0, s, C, S, O, prog, xchain ? I.xregcnt.p : nullptr, I.uniq);
         hipLaunchKernelGGL(k_pts_score, gN, b, 0, s, C, S, O, prog, pts_pos);
+        if (xchain &&  // X3
+            !xrun(2 * KSG_MAX_PLUGINS, [&](int64_t* o) { hipLaunchKernelGGL(k_x3_pack, dim3(1), b, 0, s, O, o); },
+                  [&](const int64_t* r) { hipLaunchKernelGGL(k_x3_merge, dim3(1), b, 0, s, O, r, xr); }))
+          return false;
       }
       hipLaunchKernelGGL(k_finalize, gN, b, 0, s, C, F, S, O, prog);
     }
-    // selectHost + assume: folded into the last block of the cycle's last kernel
+    if (xchain) {  // X4, then selectHost + assume on the owner of the node
+      if (!xrun(2, [&](int64_t* o) { hipLaunchKernelGGL(k_x4_pack, dim3(1), b, 0, s, O, o); },
+                [&](const int64_t* r) { hipLaunchKernelGGL(k_x4_merge, dim3(1), b, 0, s, O, r, xr); }))
+        return false;
+      hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, s, C, F, O, prog, mode, I.prow.p + j);
+    }
+    // unsharded: selectHost + assume folded into the last block of the cycle's last kernel
   }
   HIPCHK(hipEventRecord(I.ev1, s));
   HIPCHK(hipGetLastError());

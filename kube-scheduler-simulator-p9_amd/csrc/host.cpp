@@ -668,6 +668,20 @@ struct Cluster {
       uint32_t c = k < 0 ? 0 : (uint32_t)nvals[k].names.size();
       S.topo_count.push_back(c);
       pairs += c;
+      // one node per value (e.g. kubernetes.io/hostname): a shard's domains of
+      // this key are its own (no exchange of their histograms)
+      bool uniq = true;
+      if (k >= 0) {
+        std::vector<uint8_t> seen(c, 0);
+        for (auto& nd : nodes) {
+          auto it = nd.labels.find(tk);
+          if (it == nd.labels.end()) continue;
+          int32_t v = nvals[k].get(it->second);
+          if (v < 0) continue;
+          if (seen[(size_t)v]++) { uniq = false; break; }
+        }
+      }
+      S.topo_unique.push_back(uniq ? 1 : 0);
     }
     S.topo_pairs = pairs;
     // bound pods: NodeInfo aggregates + existing-pod table (this shard's nodes)
@@ -1543,10 +1557,8 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   if (!ctx) return KSG_E_INVALID;
   Cluster& c = ctx->c;
   if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
-  if (c.shards != 1) {
-    if (!c.eng->batch_path()) return ctx->fail("sharded contexts support Fit/BalancedAllocation profiles (batch path)", KSG_E_STATE);
-    if (c.eng->exchange_ranks() != c.shards) return ctx->fail("sharded context: call ksg_set_exchange first", KSG_E_STATE);
-  }
+  if (c.shards != 1 && c.eng->exchange_ranks() != c.shards)
+    return ctx->fail("sharded context: call ksg_set_exchange first", KSG_E_STATE);
   if (!c.compile_queue()) return ctx->fail(c.err, KSG_E_INVALID);
   if (!c.eng->run_queue(first, count, true, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
   c.mark_run(first, count);

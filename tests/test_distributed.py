@@ -54,7 +54,7 @@ def test_host_exchange_gloo_world2():
         assert dict(out) == {0: 11, 1: 11}
 
 
-def _sharded_worker(rank, world, port, doc_json, out):
+def _sharded_worker(rank, world, port, doc_json, out, batch=True):
     sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
     dist = _init(rank, world, port)
     import json
@@ -63,7 +63,7 @@ def _sharded_worker(rank, world, port, doc_json, out):
     s = Scheduler(doc["profile"], device=0, shard_rank=rank, shard_count=world)
     s.set_exchange_host(world)
     s.load_cluster(doc)
-    assert s.batch_path
+    assert s.batch_path == batch
     s.schedule()
     out[rank] = [(r.selected, r.feasible, r.status) for r in s.results()]
     dist.barrier()
@@ -87,3 +87,31 @@ def test_sharded_batch_path_matches_oracle(world):
         mp.spawn(_sharded_worker, args=(world, port, json.dumps(doc), out), nprocs=world, join=True)
         for r in range(world):
             assert out[r] == want, f"rank {r} differs"
+
+
+# Sharded per-pod chain (profiles with TaintToleration / NodeAffinity /
+# PodTopologySpread / InterPodAffinity): every rank runs the cycle on its nodes
+# and their existing pods; the cycle's global reductions (domain histograms of
+# keys whose domains span nodes, feasible count, normalisers, PTS registration,
+# argmax) are merged at four exchange points.
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,world", [(3, 2), (4, 2), (4, 3)])
+def test_sharded_per_pod_chain_matches_oracle(cfg, world):
+    import json
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _oracle import Oracle
+    from ksg import generator as g
+    if cfg == 3:
+        doc = g.generate(3, n_nodes=300, n_pods=120)
+    else:
+        doc = g.generate(4, n_nodes=240, n_existing=900, n_pods=120, n_zones=6)
+    o = Oracle(doc)
+    o.schedule(record=0)
+    want = [o.result(q) for q in range(o.n_queue)]
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_sharded_worker, args=(world, port, json.dumps(doc), out, False), nprocs=world, join=True)
+        for r in range(world):
+            bad = [(q, out[r][q], want[q]) for q in range(len(want)) if out[r][q] != want[q]]
+            assert not bad, f"rank {r}: {len(bad)} pods differ, first {bad[:4]}"

@@ -123,10 +123,14 @@ int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples);
 int ksg_set_path(ksg_ctx* ctx, int per_pod);
 int ksg_batch_path(const ksg_ctx* ctx);  /* 1 when the batch path is active */
 
-/* Node sharding across GPUs (ksg_opts.shard_rank / shard_count): per window of
- * 32 pods every rank all-gathers its per-pod top-64 candidates (with their node
+/* Node sharding across GPUs (ksg_opts.shard_rank / shard_count; existing pods
+ * live with their node).  Fit/BalancedAllocation profiles: per window of 32
+ * pods every rank all-gathers its per-pod top-64 candidates (with their node
  * rows) and local feasible counts, merges them, and runs the same deterministic
- * replay, applying only its own nodes' assume deltas.
+ * replay, applying only its own nodes' assume deltas.  Other profiles: the
+ * per-pod chain with four exchanges per cycle (domain histograms, feasible
+ * count and normalisers, PodTopologySpread normaliser, argmax key).  What-if
+ * steps: per-pod summaries merged after each pass.
  *   mode 1: RCCL all-gather on the context stream; nccl_id = 128 bytes from
  *           ksg_nccl_unique_id() on one rank, broadcast by the caller.
  *   mode 2: host callback fn(user, send, recv, bytes_per_rank) that all-gathers

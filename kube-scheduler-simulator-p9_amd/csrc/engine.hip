@@ -443,6 +443,51 @@ __device__ __forceinline__ bool pts_has_keys(const DevCluster& C, const ProgView
 }
 
 // PodTopologySpread Filter
+// Topology-slot value ids of this thread's node, loaded once per kernel into
+// LDS (tv(s) = node_vid(C, C.tkey[s], n)): the cycle's histogram lookups then
+// depend on one LDS read instead of a label load each.
+struct SlotVids {
+  const int32_t* base;  // [KSG_MAX_TOPO][kBlock] in LDS, this thread's column
+  __device__ __forceinline__ int32_t operator()(int s) const { return base[s * kBlock]; }
+};
+__device__ __forceinline__ void load_slot_vids(const DevCluster& C, uint32_t n, bool active, int32_t* lds) {
+  const uint32_t nt = C.n_topo < KSG_MAX_TOPO ? C.n_topo : KSG_MAX_TOPO;
+  int32_t v[KSG_MAX_TOPO];
+#pragma unroll
+  for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = ((uint32_t)s < nt && active) ? node_vid(C, C.tkey[s], n) : -1;
+#pragma unroll
+  for (int s = 0; s < KSG_MAX_TOPO; ++s)
+    if ((uint32_t)s < nt) lds[s * kBlock + threadIdx.x] = v[s];
+}
+// pts_filter with the slot vids preloaded: every histogram load of the pod's
+// constraints is issued before the first check (same verdict and order)
+__device__ __forceinline__ int pts_filter_v(const DevCluster& C, const DevScratch& S, const ProgView& V,
+                                            const SlotVids& tv, bool& error) {
+  const int nf = V.h->n_tsc_filter;
+  int32_t m[KSG_MAX_TSC];
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c) {
+    m[c] = 0;
+    if (c < nf) {
+      const int32_t v = tv(V.h->tsc[c].topo);
+      if (v >= 0) m[c] = S.hist_f[C.tbase[V.h->tsc[c].topo] + v];
+    }
+  }
+  int r = 0;
+  bool done = false;
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c) {
+    if (c < nf && !done) {
+      const ksg_tsc& t = V.h->tsc[c];
+      const int32_t dom = S.pts_dom[t.topo];
+      const int64_t mn = dom < t.min_domains ? 0 : S.pts_min[t.topo];
+      if (tv(t.topo) < 0) { r = 1 + KSG_PTS_MISSING_LABEL; done = true; }
+      else if (dom == 0) { error = true; done = true; }  // minMatchNum: no domains for key -> Error status
+      else if ((int64_t)m[c] + t.self_match - mn > t.max_skew) { r = 1 + KSG_PTS_SKEW; done = true; }
+    }
+  }
+  return r;
+}
 __device__ __forceinline__ int pts_filter(const DevCluster& C, const DevScratch& S, const ProgView& V, uint32_t n,
                                           bool& error) {
   for (int c = 0; c < V.h->n_tsc_filter; ++c) {
@@ -485,6 +530,49 @@ __device__ __forceinline__ int ipa_filter(const DevCluster& C, const DevScratch&
   return 0;
 }
 
+__device__ __forceinline__ int ipa_filter_v(const DevCluster& C, const DevScratch& S, const ProgView& V,
+                                            const SlotVids& tv, uint32_t ipa_flags, uint32_t exist_any) {
+  const ksg_prog* h = V.h;
+  const ksg_aterm* aff = V.at + h->aterm_off;
+  const ksg_aterm* anti = aff + h->n_req_aff;
+  // existing pods' anti-affinity per slot: loaded up front (no early exit in between)
+  int32_t ex[KSG_MAX_TOPO];
+#pragma unroll
+  for (int s = 0; s < KSG_MAX_TOPO; ++s) {
+    ex[s] = 0;
+    if ((exist_any >> s) & 1u) {
+      const int32_t v = tv(s);
+      if (v >= 0) ex[s] = S.ipa_exist[C.tbase[s] + v];
+    }
+  }
+  bool pods_exist = true;
+  for (int i = 0; i < h->n_req_aff; ++i) {
+    int32_t v = tv(aff[i].topo);
+    if (v < 0) return 1 + KSG_IPA_AFFINITY;
+    if (S.ipa_aff[C.tbase[aff[i].topo] + v] <= 0) pods_exist = false;
+  }
+  if (!pods_exist && !(!(ipa_flags & 1u) && h->self_matches_all)) return 1 + KSG_IPA_AFFINITY;
+  if (ipa_flags & 2u)
+    for (int i = 0; i < h->n_req_anti; ++i) {
+      int32_t v = tv(anti[i].topo);
+      if (v >= 0 && S.ipa_anti[C.tbase[anti[i].topo] + v] > 0) return 1 + KSG_IPA_ANTI_AFFINITY;
+    }
+  bool hit = false;
+#pragma unroll
+  for (int s = 0; s < KSG_MAX_TOPO; ++s) hit |= ex[s] > 0;
+  return hit ? 1 + KSG_IPA_EXISTING_ANTI : 0;
+}
+__device__ __forceinline__ int64_t ipa_score_v(const DevCluster& C, const DevScratch& S, const SlotVids& tv) {
+  const uint32_t nt = C.n_topo < KSG_MAX_TOPO ? C.n_topo : KSG_MAX_TOPO;
+  int64_t s = 0;
+#pragma unroll
+  for (int t = 0; t < KSG_MAX_TOPO; ++t) {
+    if ((uint32_t)t >= nt) break;
+    const int32_t v = tv(t);
+    if (v >= 0) s += S.ipa_score[C.tbase[t] + v];
+  }
+  return s;
+}
 __device__ __forceinline__ int64_t ipa_score(const DevCluster& C, const DevScratch& S, uint32_t n) {
   int64_t s = 0;
   for (uint32_t t = 0; t < C.n_topo; ++t) {
@@ -732,6 +820,9 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
   bool err = false;
   uint32_t ipa_flags = O.sum->ipa_flags;
   uint32_t exist_any = S.exist_any ? S.exist_any[0] : 0;
+  __shared__ int32_t tvl[KSG_MAX_TOPO * kBlock];
+  load_slot_vids(C, n, active, tvl);  // (each thread reads back only its own column)
+  const SlotVids tv{tvl + threadIdx.x};
   if (active && !(h->flags & KPF_PREFILTER_REJECT) &&
       !((h->flags & KPF_RESTRICT) && !bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n))) {
     code = KSG_FILTER_PASS;
@@ -755,12 +846,12 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
           break;
         case KP_PTS:
           if (!(h->flags & KPF_SKIP_PTS_FILTER)) {
-            int r = pts_filter(C, S, V, n, err);
+            int r = pts_filter_v(C, S, V, tv, err);
             if (r) { fail = true; detail = (uint32_t)(r - 1); }
           }
           break;
         case KP_IPA: {
-          int r = ipa_filter(C, S, V, n, ipa_flags, exist_any);
+          int r = ipa_filter_v(C, S, V, tv, ipa_flags, exist_any);
           if (r) { fail = true; detail = (uint32_t)(r - 1); }
           break;
         }
@@ -793,7 +884,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
         case KP_BA: sc = ba_score(C, F, V, n); break;
         case KP_TAINT: sc = taint_score(C, V, n); break;
         case KP_NA: sc = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n); break;
-        case KP_IPA: sc = ipa_score(C, S, n); break;
+        case KP_IPA: sc = ipa_score_v(C, S, tv); break;
         default: break;
       }
       O.score[(size_t)pos * C.N + n] = (int32_t)sc;
@@ -813,11 +904,13 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
     // PodTopologySpread PreScore registration (initPreScoreState)
     int nf = h->n_tsc_filter, ns = h->n_tsc_score;
     if (ns > 0 && !(h->flags & KPF_SKIP_PTS_SCORE)) {
-      if (!pts_has_keys(C, V, nf, nf + ns, n)) {
+      bool keys = true;
+      for (int c = nf; c < nf + ns; ++c) keys &= tv(h->tsc[c].topo) >= 0;
+      if (!keys) {
         atomicAdd(&O.sum->ignored, 1);
       } else {
         for (int c = nf; c < nf + ns; ++c)
-          if (!h->tsc[c].is_hostname) S.reg[C.tbase[h->tsc[c].topo] + node_vid(C, h->tsc[c].topo_key, n)] = 1;
+          if (!h->tsc[c].is_hostname) S.reg[C.tbase[h->tsc[c].topo] + tv(h->tsc[c].topo)] = 1;
       }
     }
   }
@@ -908,22 +1001,29 @@ __global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, c
     int nf = h->n_tsc_filter, ns = h->n_tsc_score;
     int64_t tot = 0;
     uint32_t ipa_flags = O.sum->ipa_flags;
-    for (int pos = 0; pos < F.n; ++pos) {
-      int64_t s = O.score[(size_t)pos * C.N + n];
+    // every position's raw score and the PTS key check loaded up front
+    int32_t raw[KSG_MAX_PLUGINS];
+#pragma unroll
+    for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) raw[pos] = pos < F.n ? O.score[(size_t)pos * C.N + n] : 0;
+    const bool pts_keys = ns > 0 && pts_has_keys(C, V, nf, nf + ns, n);
+#pragma unroll
+    for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+      if (pos >= F.n) break;
+      int64_t s = raw[pos];
       int64_t mx = O.sum->max_score[pos], mn = O.sum->min_score[pos];
       switch (F.plugins[pos]) {
-        case KP_TAINT:  // DefaultNormalizeScore(100, reverse)
-          s = mx == 0 ? 100 : 100 - 100 * s / mx;
+        case KP_TAINT:  // DefaultNormalizeScore(100, reverse); 0 <= s <= mx
+          s = mx == 0 ? 100 : 100 - div_small(100 * s, mx);
           break;
         case KP_NA:
           if (h->flags & KPF_SKIP_NA_SCORE) { s = 0; continue; }
-          s = mx == 0 ? s : 100 * s / mx;
+          s = mx == 0 ? s : div_small(100 * s, mx);
           break;
-        case KP_PTS:
+        case KP_PTS:  // 0 <= mn <= s <= mx
           if (h->flags & KPF_SKIP_PTS_SCORE) continue;
-          if (!pts_has_keys(C, V, nf, nf + ns, n)) s = 0;
+          if (!pts_keys) s = 0;
           else if (mx == 0) s = 100;
-          else s = 100 * (mx + mn - s) / mx;
+          else s = div_small(100 * (mx + mn - s), mx);
           break;
         case KP_IPA:
           if (!(ipa_flags & 8u)) continue;  // PreScore Skip (empty topology score map)

@@ -1786,8 +1786,14 @@ struct WinArgs {
   int32_t *kscore, *sscore, *ktotal, *stotal;
   // eval part: window E = queue pods [e0, e0 + ne)
   uint32_t e0, ne, T, npt, tile_len;  // T tiles of tile_len <= KSG_TILE * npt nodes per pod
-  uint64_t* tile_top;    // [KSG_BATCH][T][KSG_TOPK]
-  int32_t* tile_feas;    // [KSG_BATCH][T]
+  uint64_t* tile_top;    // [KSG_BATCH][T][KSG_TOPK] (window E's buffer)
+  int32_t* tile_feas;    // [KSG_BATCH][T][3]
+  // defer: the eval blocks only store their tile lists; block 0 of the next
+  // launch merges them (window W's buffers below) and loads the candidates'
+  // rows from the node rows — the pod's merge leaves the evaluation's chain
+  uint32_t defer;
+  const uint64_t* wtile_top;
+  const int32_t* wtile_feas;
   uint32_t* arrive;      // [KSG_BATCH] tile arrivals (reset by the last block)
   uint8_t* erec;         // candidate record of window E (kRecBytes)
   // fixup part: window W = queue pods [w0, w0 + nw)
@@ -2290,11 +2296,15 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
       __hip_atomic_store(A.tile_feas + ((size_t)b * A.T + tile) * 3 + lane, c, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(A.arrive + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (lane == 0) wcount[16] = old == A.T - 1 ? 1u : 0u;  // (slots 17..31 unused)
+    if (A.defer) {
+      if (lane == 0) wcount[16] = 0u;
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint32_t old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(A.arrive + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (lane == 0) wcount[16] = old == A.T - 1 ? 1u : 0u;  // (slots 17..31 unused)
+    }
   }
   auto flush_stash = [&]() {
     if (!stash_all && w != 0) return;
@@ -2501,6 +2511,7 @@ __device__ __forceinline__ void origin_rows(const DevCluster& C, const WinLDS& L
   } else {
     int p = (o - 64) >> 6, i = (o - 64) & 63;
     if (i < KSG_STAGE) start = L.row[p][i];
+    else if (A.defer) load_row(C, (uint32_t)(L.key[p][i] & 0xFFFFFull) - C.goff, A.need_eph, start);
     else start = reinterpret_cast<const CandRow*>(A.wrec + KSG_XHDR)[p * KSG_CAND + i].r;
     snap = start;
   }
@@ -2676,25 +2687,68 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   // across the prior-node evaluations (vmcnt is in order) and land after them.
   constexpr int kRowW = (int)(sizeof(RowV) / 8), kCandW = (int)(sizeof(CandRow) / 8), kPendW = (int)(sizeof(Pend) / 8);
   const uint64_t* src = reinterpret_cast<const uint64_t*>(A.wrec + KSG_XHDR);
-  const int nk = nb * KSG_CAND, nr = nb * KSG_STAGE * kRowW;
+  const int nk = nb * KSG_CAND, nr = A.defer ? 0 : nb * KSG_STAGE * kRowW;
   uint64_t kv[2], rv[6];
   {
     const uint64_t pv = tid < KSG_BATCH * kPendW ? reinterpret_cast<const uint64_t*>(A.pprev)[tid] : 0;
     constexpr int kPodW = (int)(sizeof(PodLite) / 8);
     const uint64_t qv = tid < nb * kPodW ? reinterpret_cast<const uint64_t*>(A.plite + A.w0)[tid] : 0;
-    const int32_t fv = tid < nb ? reinterpret_cast<const int32_t*>(A.wrec)[tid] : 0;
+    const int32_t fv = tid < nb && !A.defer ? reinterpret_cast<const int32_t*>(A.wrec)[tid] : 0;
     int32_t aT = 0, aA = 0;
     int64_t m0 = -1, m1 = -1;
     if (STAT && tid < nb) {
-      aT = reinterpret_cast<const int32_t*>(A.wrec)[KSG_BATCH + tid];
-      aA = reinterpret_cast<const int32_t*>(A.wrec)[2 * KSG_BATCH + tid];
+      if (!A.defer) {
+        aT = reinterpret_cast<const int32_t*>(A.wrec)[KSG_BATCH + tid];
+        aA = reinterpret_cast<const int32_t*>(A.wrec)[2 * KSG_BATCH + tid];
+      }
       m0 = A.mpred[2 * (A.w0 - A.first + tid)];
       m1 = A.mpred[2 * (A.w0 - A.first + tid) + 1];
     }
+    if (A.defer) {
+      // merge pod b's T tile lists (wave w: pods w and w+16) and sum its tile counts;
+      // the first 8 tiles' loads are issued together
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      int i = tid + k * KSG_WIN_THREADS;
-      kv[k] = i < nk ? src[(size_t)i * kCandW] : 0;
+      for (int k = 0; k < 2; ++k) {
+        const int b = wave + 16 * k;
+        uint64_t v = 0;
+        int32_t c[3] = {0, 0, 0};
+        if (b < nb) {
+          const uint64_t* tsrc = A.wtile_top + (size_t)b * A.T * KSG_TOPK;
+          uint64_t tl[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) tl[t] = (uint32_t)t < A.T ? tsrc[(size_t)t * KSG_TOPK + lane] : 0;
+          for (uint32_t t = lane; t < A.T; t += 64)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) c[j] += A.wtile_feas[((size_t)b * A.T + t) * 3 + j];
+          v = tl[0];
+#pragma unroll
+          for (int t = 1; t < 8; ++t)
+            if ((uint32_t)t < A.T) v = wave_merge_top(v, wave_reverse(tl[t]));
+#pragma unroll 1
+          for (uint32_t t = 8; t < A.T; ++t) v = wave_merge_top(v, wave_reverse(tsrc[(size_t)t * KSG_TOPK + lane]));
+#pragma unroll
+          for (int j = 0; j < 3; ++j) c[j] = wave_sum(c[j]);
+        }
+        kv[k] = v;
+        if (b < nb && lane == 0) {
+          L.feas[b] = c[0];
+          if (STAT) {
+            L.achT[b] = c[1];
+            L.achA[b] = c[2];
+          }
+        }
+        if (b < nb && lane < KSG_STAGE && v) {  // candidate rows of the staged ranks (window-start rows)
+          RowV rr;
+          load_row(C, (uint32_t)(v & 0xFFFFFull) - C.goff, A.need_eph, rr);
+          L.row[b][lane] = rr;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        int i = tid + k * KSG_WIN_THREADS;
+        kv[k] = i < nk ? src[(size_t)i * kCandW] : 0;
+      }
     }
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -2705,10 +2759,12 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     }
     if (tid < np * kPendW) reinterpret_cast<uint64_t*>(L.prior)[tid] = pv;
     if (tid < nb * kPodW) reinterpret_cast<uint64_t*>(L.pod)[tid] = qv;
-    if (tid < nb) L.feas[tid] = fv;
+    if (tid < nb && !A.defer) L.feas[tid] = fv;
     if (STAT && tid < nb) {
-      L.achT[tid] = aT;
-      L.achA[tid] = aA;
+      if (!A.defer) {
+        L.achT[tid] = aT;
+        L.achA[tid] = aA;
+      }
       L.mt[tid] = m0;
       L.ma[tid] = m1;
       L.fbf[tid] = 0;
@@ -3511,7 +3567,7 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   if (I.batch_ok && I.R <= 4) {
     uint32_t T = eval_tiles(I.N, I.n_cus);
     size_t Nn = std::max<uint32_t>(I.N, 1);
-    if (!I.tile_top.alloc((size_t)KSG_BATCH * T * KSG_TOPK, err) || !I.tfeas.alloc((size_t)KSG_BATCH * T * 3, err) ||
+    if (!I.tile_top.alloc((size_t)2 * KSG_BATCH * T * KSG_TOPK, err) || !I.tfeas.alloc((size_t)2 * KSG_BATCH * T * 3, err) ||
         !I.arrive.alloc(KSG_BATCH, err) || !I.pend_n.alloc(2, err) || !I.wrec.alloc(2 * kRecBytes, err) ||
         !I.pend.alloc(2 * KSG_BATCH, err) || !I.bfilter.alloc(Nn * 2 * KSG_BATCH, err) ||
         !I.bscore.alloc(Nn * 2 * KSG_BATCH * KSG_MAX_PLUGINS, err) || !I.btotal.alloc(Nn * 2 * KSG_BATCH, err))
@@ -3579,6 +3635,12 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   A.T = T;
   A.npt = npt;
   A.tile_len = tile_len;
+  // deferred tile merge (KSG_DEFER_MERGE=1, single shard): measured slower on
+  // cfg2 and cfg3 — merging 32 pods' tile lists costs the replay block ~9 us,
+  // more than the evaluation's own merge costs its chain
+  A.defer = 0;
+  if (const char* e = std::getenv("KSG_DEFER_MERGE")) A.defer = (std::strtol(e, nullptr, 10) != 0 && I.xranks <= 1) ? 1u : 0u;
+  const size_t tt_sz = (size_t)KSG_BATCH * T * KSG_TOPK, tf_sz = (size_t)KSG_BATCH * T * 3;
   A.tile_top = I.tile_top.p;
   A.tile_feas = I.tfeas.p;
   A.arrive = I.arrive.p;
@@ -3636,6 +3698,10 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     A.ne = 0;
     A.nw = 0;
     A.stamps = A.estamps = nullptr;
+    A.tile_top = I.tile_top.p + (size_t)(E & 1) * tt_sz;
+    A.tile_feas = I.tfeas.p + (size_t)(E & 1) * tf_sz;
+    A.wtile_top = I.tile_top.p + (size_t)(W & 1) * tt_sz;
+    A.wtile_feas = I.tfeas.p + (size_t)(W & 1) * tf_sz;
     if (E < (int64_t)nwin) {
       A.estamps = I.stamps_on ? I.stamps.p + (size_t)E * 32 : nullptr;
       A.e0 = first + (uint32_t)E * KSG_BATCH;

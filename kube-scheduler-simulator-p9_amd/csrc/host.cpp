@@ -1092,10 +1092,20 @@ struct Cluster {
         nodes.push_back(parse_node(n));
         node_names.add(nodes.back().name);
       }
+    // {"nodes", "pods" (bound), "queue"}; or the simulator's snapshot document
+    // (ResourcesForSnap, simulator/snapshot/snapshot.go:33-42: no "queue") —
+    // then pods without spec.nodeName are the queue, in document order, and
+    // pvs / pvcs / storageClasses / priorityClasses / schedulerConfig /
+    // namespaces are not read (no plugin on the path uses them)
+    const J* qd = d["queue"];
     if (const J* ps = d["pods"])
-      for (auto& p : ps->items) bound.push_back(parse_pod(p));
-    if (const J* q = d["queue"])
-      for (auto& p : q->items) queue.push_back(parse_pod(p));
+      for (auto& p : ps->items) {
+        Pod pod = parse_pod(p);
+        if (!qd && pod.node.empty()) queue.push_back(std::move(pod));
+        else bound.push_back(std::move(pod));
+      }
+    if (qd)
+      for (auto& p : qd->items) queue.push_back(parse_pod(p));
     if (!build_vocab()) return false;
     NodeSoA S;
     PodTableSoA T;

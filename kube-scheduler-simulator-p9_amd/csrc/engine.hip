@@ -1750,7 +1750,9 @@ __global__ __launch_bounds__(kBlock) void k_fs_static(DevCluster C, DevProfile F
 #define KSG_WIN_THREADS 1024
 #define KSG_TILE KSG_WIN_THREADS  // nodes per eval block
 #define KSG_STASH_NPT 8    // eval tiles of up to this many nodes per thread hold their outputs in LDS
-#define KSG_STAGE 16       // candidate ranks whose rows are staged in LDS (deeper ranks: global)
+#ifndef KSG_STAGE
+#define KSG_STAGE 4        // candidate ranks whose rows are staged in LDS (deeper ranks: global; 4 measured +4% over 16 on cfg2)
+#endif
 #define KSG_XHDR 512       // record header: per pod feasible count, static-max achievers (Taint, NodeAffinity): 3 x KSG_BATCH ints
 #define KSG_NOT_PATCHED 0xFFFFFFFDu
 
@@ -1792,6 +1794,7 @@ struct WinArgs {
   // launch merges them (window W's buffers below) and loads the candidates'
   // rows from the node rows — the pod's merge leaves the evaluation's chain
   uint32_t defer;
+  uint32_t stash_npt;  // eval tiles of up to this many nodes per thread hold all outputs in LDS
   const uint64_t* wtile_top;
   const int32_t* wtile_feas;
   uint32_t* arrive;      // [KSG_BATCH] tile arrivals (reset by the last block)
@@ -2208,7 +2211,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   // wave's next-node loads would wait behind its previous node's stores.
   // Tiles of more than KSG_STASH_NPT nodes per thread: only wave 0 stashes.
   PatchV* stash = reinterpret_cast<PatchV*>(wcount + 192);
-  const bool stash_all = A.npt <= KSG_STASH_NPT;
+  const bool stash_all = A.npt <= A.stash_npt;
   static_assert(96 * 4 + sizeof(PodLite) + 16 <= 192 * 4, "eval LDS layout");
   // the next node's row and static record are loaded while this one is evaluated
   auto fetch = [&](uint32_t kk, RowV& r, StaticRec& sr) {
@@ -2448,8 +2451,10 @@ struct WinLDS {
 };
 
 static_assert(sizeof(WinLDS) <= 160 * 1024, "window LDS exceeds the CU's 160 KiB");
-static_assert(16 * 64 * 8 + 192 * 4 + (size_t)KSG_STASH_NPT * 16 * 64 * sizeof(PatchV) <= sizeof(WinLDS),
-              "eval blocks' output stash exceeds the window LDS");
+// eval blocks: keys [16][64] u64 + 192 u32 of counters / pod record, then the stash
+static constexpr uint32_t kStashNpt =
+    (uint32_t)std::min<size_t>(KSG_STASH_NPT, (sizeof(WinLDS) - (16 * 64 * 8 + 192 * 4)) / (16 * 64 * sizeof(PatchV)));
+static_assert(kStashNpt >= 1, "eval blocks' output stash exceeds the window LDS");
 __device__ __forceinline__ uint32_t hslot(int32_t node) { return ((uint32_t)node * 2654435761u) >> 25; }
 __device__ __forceinline__ int prior_of(const WinLDS& L, int32_t x) {
   uint32_t h = hslot(x);
@@ -3639,6 +3644,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   // cfg2 and cfg3 — merging 32 pods' tile lists costs the replay block ~9 us,
   // more than the evaluation's own merge costs its chain
   A.defer = 0;
+  A.stash_npt = kStashNpt;
   if (const char* e = std::getenv("KSG_DEFER_MERGE")) A.defer = (std::strtol(e, nullptr, 10) != 0 && I.xranks <= 1) ? 1u : 0u;
   const size_t tt_sz = (size_t)KSG_BATCH * T * KSG_TOPK, tf_sz = (size_t)KSG_BATCH * T * 3;
   A.tile_top = I.tile_top.p;

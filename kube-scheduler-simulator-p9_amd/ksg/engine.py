@@ -15,7 +15,8 @@ FILTER_NOT_EVALUATED = 0xFFFFFFFE
 
 
 def lib_path() -> str:
-    return os.path.join(_PKG, "libksg.so")
+    # KSG_LIB: diagnostic override (A/B builds of the same sources)
+    return os.environ.get("KSG_LIB") or os.path.join(_PKG, "libksg.so")
 
 
 class _PodResult(ctypes.Structure):

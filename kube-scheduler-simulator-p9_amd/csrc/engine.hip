@@ -1761,15 +1761,24 @@ struct RowV {  // one node row (resource columns 0..3)
   int64_t nzc, nzm;
   int32_t podcnt, allowed;
 };
-struct CandRow {  // candidate key with the row the key was computed on (96 B)
-  uint64_t key;
-  RowV r;
-};
 struct Pend {  // a node modified by a window: row before (base) and after it
   int32_t node, pad;  // global node index
   RowV base, after;
 };
-static constexpr size_t kRecBytes = KSG_XHDR + (size_t)KSG_BATCH * KSG_CAND * sizeof(CandRow);
+// Candidate record of a window: header, then the 32 x 64 candidate keys, then the
+// rows the keys were computed on (structure of arrays: the replay stages every key
+// but only the rows of its shallow ranks).
+static constexpr size_t kRecKeys = (size_t)KSG_BATCH * KSG_CAND;
+static constexpr size_t kRecBytes = KSG_XHDR + kRecKeys * 8 + kRecKeys * sizeof(RowV);
+static_assert(sizeof(RowV) % 8 == 0, "RowV is staged as 64-bit words");
+__device__ __forceinline__ uint64_t* rec_keys(uint8_t* rec) { return reinterpret_cast<uint64_t*>(rec + KSG_XHDR); }
+__device__ __forceinline__ const uint64_t* rec_keys(const uint8_t* rec) {
+  return reinterpret_cast<const uint64_t*>(rec + KSG_XHDR);
+}
+__device__ __forceinline__ RowV* rec_rows(uint8_t* rec) { return reinterpret_cast<RowV*>(rec + KSG_XHDR + kRecKeys * 8); }
+__device__ __forceinline__ const RowV* rec_rows(const uint8_t* rec) {
+  return reinterpret_cast<const RowV*>(rec + KSG_XHDR + kRecKeys * 8);
+}
 
 
 struct PodLite {  // the fields of ksg_prog the Fit/BA evaluation reads (LDS-staged)
@@ -2202,7 +2211,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   uint32_t cF = 0, cT = 0, cA = 0;
   const bool est = A.estamps && tid == 960;  // wave 15: writes its outputs directly
   uint64_t t_eval = 0, t_sort = 0, t_wait = 0;
-#define ETIME(v)                             \
+#define KSG_ETIME(v)                             \
   __builtin_amdgcn_sched_barrier(0);         \
   const uint64_t v = __builtin_amdgcn_s_memtime(); \
   __builtin_amdgcn_sched_barrier(0);
@@ -2228,9 +2237,9 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   fetch(0, rnext, snext);
 #pragma unroll 1
   for (uint32_t k = 0; k < A.npt; ++k) {
-  ETIME(t0);
+  KSG_ETIME(t0);
   if (A.estamps && w == 15) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: load wait
-  ETIME(tl);
+  KSG_ETIME(tl);
   t_wait += tl - t0;
   const uint32_t to = k * KSG_TILE + tid, n = tile * A.tile_len + to;
   const RowV r = rnext;
@@ -2269,14 +2278,14 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     cT += (uint32_t)__popcll(__ballot(feasible && achT));
     cA += (uint32_t)__popcll(__ballot(feasible && achA));
   }
-  ETIME(t1);
+  KSG_ETIME(t1);
   key = wave_sort_desc(key);
   top = k == 0 ? key : wave_merge_top(top, wave_reverse(key));
-  ETIME(t2);
+  KSG_ETIME(t2);
   t_eval += t1 - t0;
   t_sort += t2 - t1;
   }
-  ETIME(t3);
+  KSG_ETIME(t3);
   L[w * 64 + lane] = top;
   if (lane == 0) {
     wcount[w] = cF;
@@ -2323,8 +2332,8 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     }
   };
   lds_barrier();
-  ETIME(t4);
-#undef ETIME
+  KSG_ETIME(t4);
+#undef KSG_ETIME
   if (est) {
     atomicAdd((unsigned long long*)&A.estamps[13], (unsigned long long)t_eval);
     atomicAdd((unsigned long long*)&A.estamps[14], (unsigned long long)t_sort);
@@ -2359,16 +2368,16 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   }
   if (w == 0) {
     uint64_t v = L[lane];
-    CandRow c;
+    RowV c;
     memset(&c, 0, sizeof(c));
-    c.key = v;
     int32_t gid = (int32_t)(v & 0xFFFFFull);
     int hh = pend_lds(gid);
     if (v) {
-      if (hh >= 0) c.r = A.pprev[hh].after;
-      else load_row(C, (uint32_t)gid - C.goff, A.need_eph, c.r);
+      if (hh >= 0) c = A.pprev[hh].after;
+      else load_row(C, (uint32_t)gid - C.goff, A.need_eph, c);
     }
-    reinterpret_cast<CandRow*>(A.erec + KSG_XHDR)[(size_t)b * KSG_CAND + lane] = c;
+    rec_keys(A.erec)[(size_t)b * KSG_CAND + lane] = v;
+    rec_rows(A.erec)[(size_t)b * KSG_CAND + lane] = c;
     int32_t f[3] = {0, 0, 0};
     for (uint32_t t = lane; t < A.T; t += 64)
 #pragma unroll
@@ -2517,7 +2526,7 @@ __device__ __forceinline__ void origin_rows(const DevCluster& C, const WinLDS& L
     int p = (o - 64) >> 6, i = (o - 64) & 63;
     if (i < KSG_STAGE) start = L.row[p][i];
     else if (A.defer) load_row(C, (uint32_t)(L.key[p][i] & 0xFFFFFull) - C.goff, A.need_eph, start);
-    else start = reinterpret_cast<const CandRow*>(A.wrec + KSG_XHDR)[p * KSG_CAND + i].r;
+    else start = rec_rows(A.wrec)[p * KSG_CAND + i];
     snap = start;
   }
 }
@@ -2690,8 +2699,9 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   // ---- stage.  The small inputs (P_{W-1}, pods, counts) are loaded first and
   // stored at once; the candidate keys and rows stay in flight in registers
   // across the prior-node evaluations (vmcnt is in order) and land after them.
-  constexpr int kRowW = (int)(sizeof(RowV) / 8), kCandW = (int)(sizeof(CandRow) / 8), kPendW = (int)(sizeof(Pend) / 8);
-  const uint64_t* src = reinterpret_cast<const uint64_t*>(A.wrec + KSG_XHDR);
+  constexpr int kRowW = (int)(sizeof(RowV) / 8), kPendW = (int)(sizeof(Pend) / 8);
+  const uint64_t* keys = rec_keys(A.wrec);
+  const uint64_t* rows = reinterpret_cast<const uint64_t*>(rec_rows(A.wrec));
   const int nk = nb * KSG_CAND, nr = A.defer ? 0 : nb * KSG_STAGE * kRowW;
   uint64_t kv[2], rv[6];
   {
@@ -2752,7 +2762,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         int i = tid + k * KSG_WIN_THREADS;
-        kv[k] = i < nk ? src[(size_t)i * kCandW] : 0;
+        kv[k] = i < nk ? keys[i] : 0;
       }
     }
 #pragma unroll
@@ -2760,7 +2770,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       int i = tid + k * KSG_WIN_THREADS;
       int row = i / kRowW, wd = i - row * kRowW;
       int p = row / KSG_STAGE, r = row - p * KSG_STAGE;
-      rv[k] = i < nr ? src[(size_t)(p * KSG_CAND + r) * kCandW + 1 + wd] : 0;
+      rv[k] = i < nr ? rows[(size_t)(p * KSG_CAND + r) * kRowW + wd] : 0;
     }
     if (tid < np * kPendW) reinterpret_cast<uint64_t*>(L.prior)[tid] = pv;
     if (tid < nb * kPodW) reinterpret_cast<uint64_t*>(L.pod)[tid] = qv;
@@ -3173,16 +3183,14 @@ __global__ __launch_bounds__(64) void k_window_gmerge(const uint8_t* recv, uint3
   __shared__ uint64_t keys[8 * KSG_CAND];
   const uint32_t b = blockIdx.x;
   const int lane = threadIdx.x;
-  for (uint32_t r = 0; r < ranks; ++r)
-    keys[r * KSG_CAND + lane] =
-        reinterpret_cast<const CandRow*>(recv + r * kRecBytes + KSG_XHDR)[(size_t)b * KSG_CAND + lane].key;
+  for (uint32_t r = 0; r < ranks; ++r) keys[r * KSG_CAND + lane] = rec_keys(recv + r * kRecBytes)[(size_t)b * KSG_CAND + lane];
   __syncthreads();
   uint64_t v = keys[lane];
   for (uint32_t r = 1; r < ranks; ++r) v = wave_merge_top(v, keys[r * KSG_CAND + 63 - lane]);
   int32_t f[3] = {0, 0, 0};
   for (uint32_t r = 0; r < ranks; ++r)
     for (int k = 0; k < 3; ++k) f[k] += reinterpret_cast<const int32_t*>(recv + r * kRecBytes)[k * KSG_BATCH + b];
-  CandRow c;
+  RowV c;
   memset(&c, 0, sizeof(c));
   if (v) {  // find the source entry: each rank's list is sorted descending
     for (uint32_t r = 0; r < ranks; ++r) {
@@ -3195,12 +3203,13 @@ __global__ __launch_bounds__(64) void k_window_gmerge(const uint8_t* recv, uint3
         else hi = mid - 1;
       }
       if (at >= 0) {
-        c = reinterpret_cast<const CandRow*>(recv + r * kRecBytes + KSG_XHDR)[(size_t)b * KSG_CAND + at];
+        c = rec_rows(recv + r * kRecBytes)[(size_t)b * KSG_CAND + at];
         break;
       }
     }
   }
-  reinterpret_cast<CandRow*>(out + KSG_XHDR)[(size_t)b * KSG_CAND + lane] = c;
+  rec_keys(out)[(size_t)b * KSG_CAND + lane] = v;
+  rec_rows(out)[(size_t)b * KSG_CAND + lane] = c;
   if (lane < 3) reinterpret_cast<int32_t*>(out)[lane * KSG_BATCH + b] = f[lane];
 }
 

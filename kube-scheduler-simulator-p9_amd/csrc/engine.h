@@ -44,6 +44,11 @@ struct NodeSoA {
   std::vector<uint32_t> taint_off;        // [n+1]
   std::vector<int32_t> taint_id;
   std::vector<uint8_t> has_labels;        // [n]
+  std::vector<uint8_t> node_flags;        // [n] KSG_NODE_*
+  uint32_t img_words = 0;                 // ImageLocality: node image bitsets [img_words][n] over the image vocabulary
+  std::vector<uint32_t> img_bits;
+  uint32_t n_ports = 0;                   // NodePorts: used host-port triple counts [n_ports][n]
+  std::vector<int32_t> port_count;
   // node-label vocabulary numeric view (Gt/Lt): per key offset into value tables
   std::vector<uint32_t> key_val_off;      // [n_keys+1]
   std::vector<int64_t> val_num;

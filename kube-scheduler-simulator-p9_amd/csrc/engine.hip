@@ -80,6 +80,12 @@ struct DevCluster {
   ksg_req* treq;
   int32_t* tval;
   uint32_t* tcounts;  // [0] pods [1] terms [2] reqs [3] vals [4] overflow flag
+  // rest of the default profile
+  const uint8_t* nflags;   // [N] KSG_NODE_*
+  uint32_t img_words;
+  const uint32_t* img;     // [img_words][N]
+  uint32_t n_ports;
+  int32_t* ports;          // [n_ports][N] used host-port triple counts
 };
 
 struct DevProfile {
@@ -329,6 +335,38 @@ __device__ double go_log(double x) {
 
 // ----------------------------------------------------------------- plugins (per node)
 // NodeResourcesFit Filter (fit.go fitsRequest): reason bits, 0 = fits.
+// NodeUnschedulable Filter (node_unschedulable.go): a cordoned node fails unless the
+// pod tolerates node.kubernetes.io/unschedulable:NoSchedule (decided on the host).
+__device__ __forceinline__ bool unsched_fails(const DevCluster& C, const ProgView& V, uint32_t n) {
+  return (C.nflags[n] & KSG_NODE_UNSCHEDULABLE) && !(V.h->flags & KPF_TOL_UNSCHED);
+}
+// NodeName Filter (node_name.go Fits): empty spec.nodeName or this node's name.
+__device__ __forceinline__ bool nodename_fails(const DevCluster& C, const ProgView& V, uint32_t n) {
+  const int32_t g = V.h->node_name_gid;
+  return g != -1 && (g < 0 || (uint32_t)g != C.goff + n);
+}
+// NodePorts Filter (fitsPorts -> HostPortInfo.CheckConflict): the host folds every
+// wanted (ip, protocol, port) into the used-port triples that conflict with it.
+__device__ __forceinline__ bool ports_fail(const DevCluster& C, const ProgView& V, uint32_t n) {
+  const int32_t k = V.h->n_port_check, o = V.h->port_check_off;
+  for (int i = 0; i < k; ++i)
+    if (C.ports[(size_t)V.i32[o + i] * C.N + n] > 0) return true;
+  return false;
+}
+// ImageLocality Score (image_locality.go): sum of the containers' scaledImageScore
+// over images the node lists, clamped to [minThreshold, maxThreshold], scaled to 0..100.
+__device__ __forceinline__ int64_t image_score(const DevCluster& C, const ProgView& V, uint32_t n) {
+  const ksg_prog* h = V.h;
+  const int64_t kMin = 23ll << 20, kMax = h->img_max_threshold;
+  int64_t sum = 0;
+  for (int i = 0; i < h->n_img; ++i) {
+    const int32_t id = h->img_id[i];
+    if ((C.img[(size_t)(id >> 5) * C.N + n] >> (id & 31)) & 1u) sum += h->img_scaled[i];
+  }
+  sum = sum < kMin ? kMin : (sum > kMax ? kMax : sum);
+  return 100 * (sum - kMin) / (kMax - kMin);
+}
+
 __device__ __forceinline__ uint32_t fit_filter(const DevCluster& C, const ProgView& V, uint32_t n) {
   uint32_t bits = 0;
   if (C.podcnt[n] + 1 > C.allowed[n]) bits |= KSG_FIT_TOO_MANY_PODS;
@@ -855,6 +893,11 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
           if (r) { fail = true; detail = (uint32_t)(r - 1); }
           break;
         }
+        case KP_UNSCHED: fail = unsched_fails(C, V, n); break;
+        case KP_NODENAME: fail = nodename_fails(C, V, n); break;
+        case KP_PORTS:
+          if (!(h->flags & KPF_SKIP_PORTS)) fail = ports_fail(C, V, n);
+          break;
         default: break;
       }
       if (fail) {
@@ -885,6 +928,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
         case KP_TAINT: sc = taint_score(C, V, n); break;
         case KP_NA: sc = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n); break;
         case KP_IPA: sc = ipa_score_v(C, S, tv); break;
+        case KP_IMAGE: sc = image_score(C, V, n); break;
         default: break;
       }
       O.score[(size_t)pos * C.N + n] = (int32_t)sc;
@@ -1008,26 +1052,28 @@ __global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, c
     const bool pts_keys = ns > 0 && pts_has_keys(C, V, nf, nf + ns, n);
 #pragma unroll
     for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
-      if (pos >= F.n) break;
+      if (pos >= F.n) continue;
       int64_t s = raw[pos];
+      bool use = true;  // false: the plugin's PreScore returned Skip (not scored)
       int64_t mx = O.sum->max_score[pos], mn = O.sum->min_score[pos];
       switch (F.plugins[pos]) {
         case KP_TAINT:  // DefaultNormalizeScore(100, reverse); 0 <= s <= mx
           s = mx == 0 ? 100 : 100 - div_small(100 * s, mx);
           break;
         case KP_NA:
-          if (h->flags & KPF_SKIP_NA_SCORE) { s = 0; continue; }
-          s = mx == 0 ? s : div_small(100 * s, mx);
+          if (h->flags & KPF_SKIP_NA_SCORE) use = false;
+          else s = mx == 0 ? s : div_small(100 * s, mx);
           break;
         case KP_PTS:  // 0 <= mn <= s <= mx
-          if (h->flags & KPF_SKIP_PTS_SCORE) continue;
-          if (!pts_keys) s = 0;
+          if (h->flags & KPF_SKIP_PTS_SCORE) use = false;
+          else if (!pts_keys) s = 0;
           else if (mx == 0) s = 100;
           else s = div_small(100 * (mx + mn - s), mx);
           break;
         case KP_IPA:
-          if (!(ipa_flags & 8u)) continue;  // PreScore Skip (empty topology score map)
-          {
+          if (!(ipa_flags & 8u)) {  // PreScore Skip (empty topology score map)
+            use = false;
+          } else {
 #pragma clang fp contract(off)
             int64_t diff = mx - mn;
             double f = 0;
@@ -1035,10 +1081,12 @@ __global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, c
             s = (int64_t)f;
           }
           break;
-        default: break;
+        default: break;  // no ScoreExtensions: the raw score
       }
-      if (s < 0 || s > 100) range_err = true;
-      tot += s * F.weight[pos];
+      if (use) {
+        if (s < 0 || s > 100) range_err = true;
+        tot += s * F.weight[pos];
+      }
     }
     if (O.sum->feasible == 1) tot = 0;  // single feasible node: no scoring
     O.total[n] = (int32_t)tot;
@@ -1059,6 +1107,7 @@ __device__ void assume_pod(DevCluster& C, const ProgView& V, uint32_t n, int sig
   C.nzc[n] += sign * h->nz_cpu;
   C.nzm[n] += sign * h->nz_mem;
   C.podcnt[n] += sign;
+  for (int i = 0; i < h->n_port_own; ++i) C.ports[(size_t)V.i32[h->port_own_off + i] * C.N + n] += sign;
   if (sign < 0) {
     if (prow && *prow >= 0) {
       C.ptflags[*prow] |= KEF_DELETED;
@@ -3285,7 +3334,10 @@ struct Engine::Impl {
   DBuf<int64_t> alloc, req, nzc, nzm, vnum;
   DBuf<int32_t> allowed, podcnt, label, tid;
   DBuf<uint32_t> toff, kvo;
-  DBuf<uint8_t> haslab, vok;
+  DBuf<uint8_t> haslab, vok, nflags;
+  DBuf<uint32_t> img;
+  DBuf<int32_t> ports, ports0;
+  uint32_t img_words = 0, n_ports = 0;
   NodeSoA topo;  // topology tables (host copy)
   DBuf<int32_t> topo_key_d;
   DBuf<uint32_t> topo_base_d, topo_count_d;
@@ -3367,6 +3419,7 @@ struct Engine::Impl {
     C.alloc = alloc.p; C.req = req.p; C.nzc = nzc.p; C.nzm = nzm.p;
     C.allowed = allowed.p; C.podcnt = podcnt.p; C.label = label.p; C.toff = toff.p; C.tid = tid.p;
     C.haslab = haslab.p; C.kvo = kvo.p; C.vnum = vnum.p; C.vok = vok.p;
+    C.nflags = nflags.p; C.img_words = img_words; C.img = img.p; C.n_ports = n_ports; C.ports = ports.p;
     C.n_topo = (uint32_t)topo.topo_key.size();
     C.pairs = topo.topo_pairs;
     C.tkey = topo_key_d.p;
@@ -3509,6 +3562,19 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
       !I.haslab.upload(ns.has_labels, s, err) || !I.kvo.upload(ns.key_val_off, s, err) ||
       !I.vnum.upload(ns.val_num, s, err) || !I.vok.upload(ns.val_num_ok, s, err))
     return false;
+  {
+    std::vector<uint8_t> nf = ns.node_flags;
+    nf.resize(ns.n, 0);
+    I.img_words = ns.img_words;
+    I.n_ports = ns.n_ports;
+    if (ns.img_bits.size() != (size_t)ns.img_words * ns.n || ns.port_count.size() != (size_t)ns.n_ports * ns.n) {
+      err = "node image / host-port columns do not match the node count";
+      return false;
+    }
+    if (!I.nflags.upload(nf, s, err) || !I.img.upload(ns.img_bits, s, err) || !I.ports.upload(ns.port_count, s, err) ||
+        !I.ports0.upload(ns.port_count, s, err))
+      return false;
+  }
   I.topo = NodeSoA();
   I.topo.topo_key = ns.topo_key;
   I.topo.topo_base = ns.topo_base;
@@ -3812,7 +3878,7 @@ static bool exchange(Engine::Impl& I, const void* src, size_t bytes, std::string
 
 bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
   Impl& I = *p_;
-  if (I.has_pts || I.has_ipa) {
+  if (I.has_pts || I.has_ipa || !I.batch_ok) {
     err = "what-if steps support NodeResourcesFit / BalancedAllocation / TaintToleration / NodeAffinity profiles";
     return false;
   }
@@ -4196,6 +4262,8 @@ bool Engine::reset(std::string& err) {
   HIPCHK(hipMemcpyAsync(I.nzc.p, I.nzc0.p, (size_t)I.N * 8, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemcpyAsync(I.nzm.p, I.nzm0.p, (size_t)I.N * 8, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemcpyAsync(I.podcnt.p, I.podcnt0.p, (size_t)I.N * 4, hipMemcpyDeviceToDevice, s));
+  if (I.n_ports)
+    HIPCHK(hipMemcpyAsync(I.ports.p, I.ports0.p, (size_t)I.n_ports * I.N * 4, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemcpyAsync(I.tcounts.p, I.counts0, sizeof(I.counts0), hipMemcpyHostToDevice, s));
   uint32_t cnt = (uint32_t)I.prog_off.size();
   if (cnt) hipLaunchKernelGGL(k_init_summaries, dim3((cnt + 255) / 256), dim3(256), 0, s, I.sums.p, cnt, I.F);

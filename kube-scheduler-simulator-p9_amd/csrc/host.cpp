@@ -241,6 +241,12 @@ struct Pod {
   bool pod_aff = false, pod_anti = false, pref_aff_present = false, pref_anti_present = false;
   vector<ATerm> req_aff, req_anti, pref_aff, pref_anti;
   vector<TSC> tsc;
+  // rest of the default profile
+  vector<string> images;  // init containers then containers (ImageLocality sumImageScores order)
+  int n_containers = 0;   // init + regular
+  struct HostPort { string ip, proto; int32_t port; };
+  vector<HostPort> ports; // Spec.Containers host ports (hostPort > 0), sanitised
+  bool volume_plugins_act = false;  // a volume the volume plugins would not Skip
 };
 
 static RList pod_requests(const J* spec, bool nonzero) {
@@ -301,6 +307,27 @@ static Pod parse_pod(const J& v) {
   p.req_nz = pod_requests(sp, true);
   if (!sp) return p;
   p.node = str_of((*sp)["nodeName"]);
+  for (const char* k : {"initContainers", "containers"})
+    if (auto* cs = (*sp)[k])
+      for (auto& c : cs->items) {
+        p.images.push_back(str_of(c["image"]));
+        p.n_containers++;
+        if (string(k) != "containers") continue;  // v1.30 getContainerPorts / updateUsedPorts: Spec.Containers
+        if (auto* ps = c["ports"])
+          for (auto& x : ps->items) {
+            i64 hp = x["hostPort"] ? (i64)x["hostPort"]->num() : 0;
+            if (hp <= 0) continue;
+            Pod::HostPort h{str_of(x["hostIP"]), str_of(x["protocol"]), (int32_t)hp};
+            if (h.ip.empty()) h.ip = "0.0.0.0";  // HostPortInfo.sanitize
+            if (h.proto.empty()) h.proto = "TCP";
+            p.ports.push_back(h);
+          }
+      }
+  if (auto* vs = (*sp)["volumes"])
+    for (auto& v : vs->items)
+      for (const char* k : {"persistentVolumeClaim", "ephemeral", "gcePersistentDisk", "awsElasticBlockStore", "rbd",
+                            "iscsi", "azureDisk", "cinder", "csi"})
+        if (v[k] && !v[k]->null()) p.volume_plugins_act = true;
   if (auto* ns = (*sp)["nodeSelector"]; ns && !ns->null()) {
     p.has_node_sel = true;
     p.node_sel = smap(ns);
@@ -359,6 +386,8 @@ struct Node {
   map<string, string> labels;
   vector<Taint> taints;
   RList alloc;
+  bool unschedulable = false;
+  vector<std::pair<vector<string>, i64>> images;  // status.images: names, sizeBytes
 };
 static Node parse_node(const J& v) {
   Node n;
@@ -368,8 +397,13 @@ static Node parse_node(const J& v) {
   if (auto* sp = v["spec"])
     if (auto* ts = (*sp)["taints"])
       for (auto& t : ts->items) n.taints.push_back({str_of(t["key"]), str_of(t["value"]), str_of(t["effect"])});
+  if (auto* sp = v["spec"])
+    if (auto* u = (*sp)["unschedulable"]) n.unschedulable = u->b;
   const J* st = v["status"];
   n.alloc = rlist(st ? (*st)["allocatable"] : nullptr);
+  if (st)
+    if (auto* im = (*st)["images"])
+      for (auto& x : im->items) n.images.push_back({slist(x["names"]), x["sizeBytes"] ? (i64)x["sizeBytes"]->num() : 0});
   return n;
 }
 
@@ -390,16 +424,31 @@ struct Dict {
   }
 };
 
-enum { P_FIT = KP_FIT, P_BA = KP_BA, P_TAINT = KP_TAINT, P_NA = KP_NA, P_PTS = KP_PTS, P_IPA = KP_IPA };
-static const char* kPluginNames[] = {"NodeResourcesFit", "NodeResourcesBalancedAllocation", "TaintToleration",
-                                     "NodeAffinity", "PodTopologySpread", "InterPodAffinity"};
+enum { P_FIT = KP_FIT, P_BA = KP_BA, P_TAINT = KP_TAINT, P_NA = KP_NA, P_PTS = KP_PTS, P_IPA = KP_IPA,
+       P_UNSCHED = KP_UNSCHED, P_NODENAME = KP_NODENAME, P_PORTS = KP_PORTS, P_IMAGE = KP_IMAGE,
+       P_VOLUME = KP_VOLUME, P_VOLBIND = KP_VOLBIND, P_NOOP = KP_NOOP };
+// The default profile's plugins (scheduler_test.go:531-557) by original name.
 static int plugin_id(const string& n) {
-  for (int i = 0; i < 6; ++i)
-    if (n == kPluginNames[i]) return i;
+  static const std::pair<const char*, int> tab[] = {
+      {"NodeResourcesFit", P_FIT}, {"NodeResourcesBalancedAllocation", P_BA}, {"TaintToleration", P_TAINT},
+      {"NodeAffinity", P_NA}, {"PodTopologySpread", P_PTS}, {"InterPodAffinity", P_IPA},
+      {"NodeUnschedulable", P_UNSCHED}, {"NodeName", P_NODENAME}, {"NodePorts", P_PORTS}, {"ImageLocality", P_IMAGE},
+      {"VolumeRestrictions", P_VOLUME}, {"EBSLimits", P_VOLUME}, {"GCEPDLimits", P_VOLUME},
+      {"NodeVolumeLimits", P_VOLUME}, {"AzureDiskLimits", P_VOLUME}, {"VolumeZone", P_VOLUME},
+      {"VolumeBinding", P_VOLBIND}, {"SchedulingGates", P_NOOP}, {"PrioritySort", P_NOOP},
+      {"DefaultPreemption", P_NOOP}, {"DefaultBinder", P_NOOP}};
+  for (auto& t : tab)
+    if (n == t.first) return t.second;
   return -1;
 }
-static bool has_prefilter(int p) { return p == P_FIT || p == P_NA || p == P_PTS || p == P_IPA; }
-static bool has_filter(int p) { return p != P_BA; }
+static bool host_only(int p) { return p == P_VOLUME || p == P_VOLBIND || p == P_NOOP; }
+// extension points the original plugin implements (the wrapper records only those)
+static bool has_prefilter(int p) {
+  return p == P_FIT || p == P_NA || p == P_PTS || p == P_IPA || p == P_PORTS || p == P_VOLUME || p == P_VOLBIND;
+}
+static bool has_filter(int p) { return p != P_BA && p != P_IMAGE && p != P_NOOP; }
+static bool has_prescore(int p) { return p <= P_IPA || p == P_VOLBIND; }
+static bool has_score(int p) { return p <= P_IPA || p == P_IMAGE; }  // VolumeBinding: PreScore Skip (no scorer)
 static bool has_ext(int p) { return p == P_TAINT || p == P_NA || p == P_PTS || p == P_IPA; }
 
 // Per-pod host-known facts the renderer needs besides the device outputs.
@@ -417,10 +466,17 @@ struct PodMeta {
 
 struct Cluster {
   // profile
-  int n_plugins = 0;
-  int plugins[KSG_MAX_PLUGINS] = {};
-  string names[KSG_MAX_PLUGINS];
-  i64 fw_w[KSG_MAX_PLUGINS] = {}, store_w[KSG_MAX_PLUGINS] = {};
+  int n_plugins = 0;  // whole profile (host-only plugins included)
+  int plugins[KSG_MAX_PROFILE] = {};
+  string names[KSG_MAX_PROFILE];
+  i64 fw_w[KSG_MAX_PROFILE] = {}, store_w[KSG_MAX_PROFILE] = {};
+  int dpos[KSG_MAX_PROFILE] = {};  // device profile position of each plugin (-1: host-only)
+  int fpos[KSG_MAX_PLUGINS] = {};  // profile position of each device position
+  int n_dev = 0;
+  bool has_volume_plugins = false;
+  Dict images;  // ImageLocality: every image name some node lists
+  vector<std::pair<i64, int32_t>> image_state;  // per image: Size (first node listing it), NumNodes
+  std::map<std::tuple<string, string, int32_t>, int32_t> port_id;  // host-port triples (ip, protocol, port)
   EngineConfig ecfg;
   vector<string> fit_res_names{"cpu", "memory"}, ba_res_names{"cpu", "memory"};
   i64 ipa_hard = 1;
@@ -456,7 +512,7 @@ struct Cluster {
     for (auto& x : pl->items) {
       int id = plugin_id(x.text());
       if (id < 0) { err = "unsupported plugin " + x.text(); return false; }
-      if (n_plugins >= KSG_MAX_PLUGINS) { err = "too many plugins"; return false; }
+      if (n_plugins >= KSG_MAX_PROFILE) { err = "too many plugins"; return false; }
       names[n_plugins] = x.text();
       plugins[n_plugins++] = id;
     }
@@ -502,11 +558,19 @@ struct Cluster {
         if (const J* ig = (*ipa)["ignorePreferredTermsOfExistingPods"]) ipa_ignore = ig->b;
       }
     }
-    ecfg.n_plugins = n_plugins;
+    n_dev = 0;
     for (int i = 0; i < n_plugins; ++i) {
-      ecfg.plugins[i] = plugins[i];
-      ecfg.weight[i] = fw_w[i];
+      has_volume_plugins |= plugins[i] == P_VOLUME || plugins[i] == P_VOLBIND;
+      dpos[i] = -1;
+      if (host_only(plugins[i])) continue;
+      if (n_dev >= KSG_MAX_PLUGINS) { err = "too many plugins with device work"; return false; }
+      dpos[i] = n_dev;
+      fpos[n_dev] = i;
+      ecfg.plugins[n_dev] = plugins[i];
+      ecfg.weight[n_dev] = fw_w[i];
+      n_dev++;
     }
+    ecfg.n_plugins = n_dev;
     ecfg.ba_n = (int)ba_res_names.size();
     ecfg.ipa_hard_weight = ipa_hard;
     ecfg.ipa_ignore_existing_pref = ipa_ignore;
@@ -565,6 +629,25 @@ struct Cluster {
     for (auto* v : {&bound, &queue})
       for (auto& p : *v) intern_pod_labels(p);
     if (nvals.size() < nkeys.names.size()) nvals.resize(nkeys.names.size());
+    // ImageLocality: ImageStateSummary per name (cache addNodeImageStates; NumNodes as in
+    // ImageStateSummary.Snapshot: the nodes listing the name)
+    images = Dict();
+    image_state.clear();
+    for (auto& n : nodes) {
+      set<int32_t> seen;
+      for (auto& im : n.images)
+        for (auto& nm : im.first) {
+          int32_t id = images.add(nm);
+          if ((size_t)id == image_state.size()) image_state.push_back({im.second, 0});
+          if (seen.insert(id).second) image_state[id].second++;
+        }
+    }
+    // NodePorts: every host-port triple a bound or queued pod uses
+    port_id.clear();
+    for (auto* v : {&bound, &queue})
+      for (auto& p : *v)
+        for (auto& h : p.ports) port_id.emplace(std::make_tuple(h.ip, h.proto, h.port), (int32_t)port_id.size());
+    if (port_id.size() > 4096) { err = "too many distinct host ports"; return false; }
     if (topo.names.size() > KSG_MAX_TOPO) { err = "too many topology keys"; return false; }
     if (fit_res_names.size() > KSG_MAX_SCORE_RES || ba_res_names.size() > KSG_MAX_SCORE_RES) {
       err = "too many scoring resources";
@@ -637,6 +720,11 @@ struct Cluster {
     S.pod_count.assign(n, 0);
     S.label_vid.assign((size_t)K * n, -1);
     S.has_labels.assign(n, 0);
+    S.node_flags.assign(n, 0);
+    S.img_words = ((uint32_t)images.names.size() + 31) / 32;
+    S.img_bits.assign((size_t)S.img_words * n, 0);
+    S.n_ports = (uint32_t)port_id.size();
+    S.port_count.assign((size_t)S.n_ports * n, 0);
     S.taint_off.assign(n + 1, 0);
     for (uint32_t i = 0; i < n; ++i) {
       const Node& nd = nodes[lo + i];
@@ -647,6 +735,12 @@ struct Cluster {
       }
       for (auto& kv : nd.labels) S.label_vid[(size_t)nkeys.get(kv.first) * n + i] = nvals[nkeys.get(kv.first)].get(kv.second);
       S.has_labels[i] = !nd.labels.empty();
+      if (nd.unschedulable) S.node_flags[i] |= KSG_NODE_UNSCHEDULABLE;
+      for (auto& im : nd.images)
+        for (auto& nm : im.first) {
+          int32_t id = images.get(nm);
+          S.img_bits[(size_t)(id >> 5) * n + i] |= 1u << (id & 31);
+        }
       for (auto& t : nd.taints) S.taint_id.push_back(taint_id[std::make_tuple(t.key, t.value, t.effect)]);
       S.taint_off[i + 1] = (uint32_t)S.taint_id.size();
     }
@@ -699,6 +793,7 @@ struct Cluster {
       S.nz_cpu[i] += nzc;
       S.nz_mem[i] += nzm;
       S.pod_count[i] += 1;
+      for (auto& h : p.ports) S.port_count[(size_t)port_id[std::make_tuple(h.ip, h.proto, h.port)] * n + i] += 1;
       T.node.push_back((int32_t)i);
       T.ns.push_back(nss.get(p.ns));
       T.flags.push_back(exist_flags(p));
@@ -1042,6 +1137,49 @@ struct Cluster {
     m.ipa_no_req_terms = p.req_aff.empty() && p.req_anti.empty();
     m.ipa_prescore_skip_static = ipa_ignore && !(p.pref_aff_present || p.pref_anti_present);
     if (m.prefilter_error) h.flags |= KPF_PREFILTER_ERROR;
+    // ---- NodeUnschedulable / NodeName / NodePorts / ImageLocality
+    {
+      Taint unsched{"node.kubernetes.io/unschedulable", "", "NoSchedule"};
+      if (tolerated(p.tols, unsched)) h.flags |= KPF_TOL_UNSCHED;
+      h.node_name_gid = p.node.empty() ? -1 : (node_names.get(p.node) < 0 ? -2 : node_names.get(p.node));
+      if (p.ports.empty()) h.flags |= KPF_SKIP_PORTS;
+      set<int32_t> check;  // CheckConflict: 0.0.0.0 wants every ip of (protocol, port); an ip wants itself and 0.0.0.0
+      for (auto& w : p.ports)
+        for (auto& kv : port_id)
+          if (std::get<1>(kv.first) == w.proto && std::get<2>(kv.first) == w.port &&
+              (w.ip == "0.0.0.0" || std::get<0>(kv.first) == "0.0.0.0" || std::get<0>(kv.first) == w.ip))
+            check.insert(kv.second);
+      h.port_check_off = (int32_t)P.i32.size();
+      h.n_port_check = (int32_t)check.size();
+      P.i32.insert(P.i32.end(), check.begin(), check.end());
+      h.port_own_off = (int32_t)P.i32.size();
+      h.n_port_own = 0;
+      for (auto& w : p.ports) {
+        auto it = port_id.find(std::make_tuple(w.ip, w.proto, w.port));
+        if (it == port_id.end()) { err = "pod " + p.name + ": host port outside the vocabulary"; return false; }
+        P.i32.push_back(it->second);
+        h.n_port_own++;
+      }
+      // image_locality.go: normalizedImageName, scaledImageScore (spread = NumNodes / totalNumNodes)
+      std::map<int32_t, i64> sc;
+      for (auto& im : p.images) {
+        string nm = im;
+        size_t c = nm.rfind(':'), sl = nm.rfind('/');
+        if ((c == string::npos ? -1L : (long)c) <= (sl == string::npos ? -1L : (long)sl)) nm += ":latest";
+        int32_t id = images.get(nm);
+        if (id < 0) continue;
+        double spread = (double)image_state[id].second / (double)nodes.size();
+        sc[id] += (i64)((double)image_state[id].first * spread);
+      }
+      if (sc.size() > KSG_MAX_IMG) { err = "pod " + p.name + ": too many node-listed images"; return false; }
+      h.n_img = 0;
+      for (auto& kv : sc) {
+        h.img_id[h.n_img] = kv.first;
+        h.img_scaled[h.n_img++] = kv.second;
+      }
+      h.img_max_threshold = (1000LL << 20) * (i64)p.n_containers;
+      if (h.img_max_threshold <= (23LL << 20)) h.n_img = 0, h.img_max_threshold = (23LL << 20) + 1;  // no containers
+    }
     // ---- as-existing record
     h.exist_flags = exist_flags(p);
     h.exist_terms_off = (int32_t)P.et.size();
@@ -1106,6 +1244,9 @@ struct Cluster {
       }
     if (qd)
       for (auto& p : qd->items) queue.push_back(parse_pod(p));
+    if (has_volume_plugins)
+      for (auto& p : queue)
+        if (p.volume_plugins_act) { err = "pod " + p.name + ": volumes the volume plugins act on are not modelled"; return false; }
     if (!build_vocab()) return false;
     NodeSoA S;
     PodTableSoA T;
@@ -1179,6 +1320,8 @@ struct Cluster {
       if (topo.get(c.key) < 0) return true;
     for (auto& kv : p.req)
       if (scalar_name(kv.first) && res.get(kv.first) < 0) return true;
+    for (auto& h : p.ports)
+      if (!port_id.count(std::make_tuple(h.ip, h.proto, h.port))) return true;
     return false;
   }
   // Re-encode and re-upload the snapshot with every assumed queue pod as a bound
@@ -1238,6 +1381,11 @@ struct Cluster {
     }
     const J& d = *docs.back();
     queue.push_back(parse_pod(d["pod"] ? *d["pod"] : d));
+    if (has_volume_plugins && queue.back().volume_plugins_act) {
+      err = "pod " + queue.back().name + ": volumes the volume plugins act on are not modelled";
+      queue.pop_back();
+      return false;
+    }
     track_queue();
     uint32_t q = (uint32_t)queue.size() - 1;
     qmode[q] = 2;
@@ -1340,8 +1488,11 @@ struct Cluster {
     return o + "}";
   }
 
-  string filter_message(int pos, uint32_t detail) const {
+  string filter_message(int pos, uint32_t detail) const {  // pos: profile position
     switch (plugins[pos]) {
+      case P_UNSCHED: return "node(s) were unschedulable";
+      case P_NODENAME: return "node(s) didn't match the requested node name";
+      case P_PORTS: return "node(s) didn't have free ports for the requested pod ports";
       case P_FIT: {
         string m;
         auto add = [&](const string& s) { m += (m.empty() ? "" : ", ") + s; };
@@ -1367,8 +1518,8 @@ struct Cluster {
   }
 
   // normalized score of one node (host restatement of k_finalize, for finalscore-result)
-  i64 normalize(int pos, i64 s, const ksg_pod_summary& S, bool ignored) const {
-    i64 mx = S.max_score[pos], mn = S.min_score[pos];
+  i64 normalize(int pos, i64 s, const ksg_pod_summary& S, bool ignored) const {  // pos: profile position
+    i64 mx = S.max_score[dpos[pos]], mn = S.min_score[dpos[pos]];
     switch (plugins[pos]) {
       case P_TAINT: return mx == 0 ? 100 : 100 - 100 * s / mx;
       case P_NA: return mx == 0 ? s : 100 * s / mx;
@@ -1401,6 +1552,8 @@ struct Cluster {
     if (m.flags & KPF_SKIP_NA_FILTER) skip_f |= 1u << P_NA;
     if (m.flags & KPF_SKIP_PTS_FILTER) skip_f |= 1u << P_PTS;
     if (m.ipa_no_req_terms && !(S.ipa_flags & 4u)) skip_f |= 1u << P_IPA;
+    if (m.flags & KPF_SKIP_PORTS) skip_f |= 1u << P_PORTS;
+    skip_f |= (1u << P_VOLUME) | (1u << P_VOLBIND);  // pods with volumes they act on are refused at load
     bool aborted = false;
     for (int pos = 0; pos < n_plugins && !aborted; ++pos) {
       int id = plugins[pos];
@@ -1418,7 +1571,7 @@ struct Cluster {
       for (uint32_t i = 0; i < n; ++i) {
         uint32_t code = o.filter[i];
         if (code == KSG_FILTER_NOT_EVALUATED) continue;
-        int fail_pos = code == KSG_FILTER_PASS ? n_plugins : (int)(code >> 24);
+        int fail_pos = code == KSG_FILTER_PASS ? n_plugins : fpos[code >> 24];
         auto& row = filt[nodes[lo + i].name];
         for (int pos = 0; pos < n_plugins; ++pos) {
           int id = plugins[pos];
@@ -1431,7 +1584,9 @@ struct Cluster {
         if (m.flags & KPF_SKIP_NA_SCORE) skip_s |= 1u << P_NA;
         if (m.flags & KPF_SKIP_PTS_SCORE) skip_s |= 1u << P_PTS;
         if (m.ipa_prescore_skip_static || !(S.ipa_flags & 8u)) skip_s |= 1u << P_IPA;
-        for (int pos = 0; pos < n_plugins; ++pos) pre_score[names[pos]] = (skip_s & (1u << plugins[pos])) ? "" : "success";
+        skip_s |= 1u << P_VOLBIND;  // PreScore: no scorer (VolumeCapacityPriority off)
+        for (int pos = 0; pos < n_plugins; ++pos)
+          if (has_prescore(plugins[pos])) pre_score[names[pos]] = (skip_s & (1u << plugins[pos])) ? "" : "success";
         int pts = pos_of(P_PTS);
         for (uint32_t i = 0; i < n; ++i) {
           if (o.filter[i] != KSG_FILTER_PASS) continue;
@@ -1440,8 +1595,8 @@ struct Cluster {
           if (pts >= 0) ignored = pts_ignored(q, i);
           for (int pos = 0; pos < n_plugins; ++pos) {
             int id = plugins[pos];
-            if (skip_s & (1u << id)) continue;
-            i64 raw = o.score[(size_t)pos * n + i];
+            if (!has_score(id) || (skip_s & (1u << id))) continue;
+            i64 raw = o.score[(size_t)dpos[pos] * n + i];
             score[nm][names[pos]] = std::to_string(raw);
             i64 v = has_ext(id) ? normalize(pos, raw, S, ignored) : raw;
             fin[nm][names[pos]] = std::to_string(v * store_w[pos]);
@@ -1450,6 +1605,12 @@ struct Cluster {
       }
     }
     string sel = S.status == 0 && S.selected >= 0 ? nodes[S.selected].name : "";
+    map<string, string> reserve, prebind, bind;  // binding cycle of a scheduled pod (the bind assumed to succeed)
+    if (!sel.empty())
+      for (int pos = 0; pos < n_plugins; ++pos) {
+        if (plugins[pos] == P_VOLBIND) reserve[names[pos]] = prebind[names[pos]] = "success";
+        if (names[pos] == "DefaultBinder") bind[names[pos]] = "success";
+      }
     auto j2 = [&](const map<string, map<string, string>>& mm) {
       string s = "{";
       for (auto it = mm.begin(); it != mm.end(); ++it) {
@@ -1476,9 +1637,9 @@ struct Cluster {
     map<string, string> ann{{P + "prefilter-result", pr},          {P + "prefilter-result-status", jmap(pre_status)},
                             {P + "filter-result", j2(filt)},       {P + "postfilter-result", "{}"},
                             {P + "prescore-result", jmap(pre_score)}, {P + "score-result", j2(score)},
-                            {P + "finalscore-result", j2(fin)},    {P + "reserve-result", "{}"},
+                            {P + "finalscore-result", j2(fin)},    {P + "reserve-result", jmap(reserve)},
                             {P + "permit-result", "{}"},           {P + "permit-result-timeout", "{}"},
-                            {P + "prebind-result", "{}"},          {P + "bind-result", "{}"},
+                            {P + "prebind-result", jmap(prebind)}, {P + "bind-result", jmap(bind)},
                             {P + "selected-node", sel}};
     out = jmap(ann);
     return true;
@@ -1616,7 +1777,10 @@ int ksg_filter_codes(ksg_ctx* ctx, uint32_t q, uint32_t* out, uint32_t n) {
   ksg::PodOutputs o;
   if (!ctx->c.eng->outputs(q, o, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_STATE);
   if (n < o.filter.size()) return KSG_E_NOBUF;
-  std::copy(o.filter.begin(), o.filter.end(), out);
+  for (size_t i = 0; i < o.filter.size(); ++i) {  // device position -> profile position
+    uint32_t c = o.filter[i];
+    out[i] = c >= KSG_FILTER_NOT_EVALUATED ? c : ((uint32_t)ctx->c.fpos[c >> 24] << 24) | (c & 0xFFFFFFu);
+  }
   return KSG_OK;
 }
 
@@ -1625,8 +1789,10 @@ int ksg_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* out, uint32_t n)
   ksg::PodOutputs o;
   if (!ctx->c.eng->outputs(q, o, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_STATE);
   size_t N = o.filter.size();
-  if (n < N || pos >= KSG_MAX_PLUGINS) return KSG_E_NOBUF;
-  std::copy(o.score.begin() + pos * N, o.score.begin() + (pos + 1) * N, out);
+  if (n < N) return KSG_E_NOBUF;
+  if (pos >= (uint32_t)ctx->c.n_plugins || ctx->c.dpos[pos] < 0) return ctx->fail("no device scores at this position", KSG_E_INVALID);
+  const size_t d = (size_t)ctx->c.dpos[pos];
+  std::copy(o.score.begin() + d * N, o.score.begin() + (d + 1) * N, out);
   return KSG_OK;
 }
 

@@ -9,7 +9,9 @@
 #include <stdint.h>
 
 #define KSG_MAX_RES 8        // resource columns: 0 cpu(milli) 1 memory 2 ephemeral-storage 3.. scalar
-#define KSG_MAX_PLUGINS 8    // hot-path plugins in one profile
+#define KSG_MAX_PLUGINS 12   // plugins with device work in one profile (device profile positions)
+#define KSG_MAX_PROFILE 32   // plugins in one profile (host; with the host-only ones)
+#define KSG_MAX_IMG 16       // distinct node-listed images of one pod (ImageLocality)
 #define KSG_MAX_SCORE_RES 8  // resources in a Fit/BA scoring config
 #define KSG_MAX_TSC 8        // topology spread constraints per pod (filter + score)
 #define KSG_MAX_TOPO 16      // distinct topology keys in one cluster
@@ -26,6 +28,18 @@
 #define KP_NA 3
 #define KP_PTS 4
 #define KP_IPA 5
+#define KP_UNSCHED 6    // NodeUnschedulable
+#define KP_NODENAME 7   // NodeName
+#define KP_PORTS 8      // NodePorts
+#define KP_IMAGE 9      // ImageLocality
+// host-only plugin kinds (never in the device profile: nothing to evaluate per node
+// for the pods the build accepts; the host records what the wrapper would)
+#define KP_VOLUME 16    // VolumeRestrictions, EBSLimits, GCEPDLimits, NodeVolumeLimits, AzureDiskLimits, VolumeZone
+#define KP_VOLBIND 17   // VolumeBinding
+#define KP_NOOP 18      // SchedulingGates, PrioritySort, DefaultPreemption, DefaultBinder
+
+// node flags column
+#define KSG_NODE_UNSCHEDULABLE 1u  // node.spec.unschedulable
 
 // filter result code per (pod,node): 0xFFFFFFFF passed every filter plugin,
 // 0xFFFFFFFE not evaluated (outside the NodeAffinity PreFilterResult), else
@@ -146,6 +160,17 @@ typedef struct ksg_prog {
   int32_t aterm_off;        // pool_aterm: req_aff, req_anti, pref_aff, pref_anti
   int32_t self_matches_all; // podMatchesAllAffinityTerms(required affinity, pod)
 
+  // ---- NodeName / NodePorts / ImageLocality
+  int32_t node_name_gid;    // spec.nodeName: -1 empty (fits every node), -2 names no node, else global node index
+  int32_t n_port_check;     // pool_i32[port_check_off ..): host-port triples whose count > 0 on a node conflicts
+  int32_t port_check_off;   //   (HostPortInfo.CheckConflict of every wanted port, folded on the host)
+  int32_t n_port_own;       // pool_i32[port_own_off ..): the pod's own triples (NodeInfo.UsedPorts delta on assume)
+  int32_t port_own_off;
+  int32_t n_img;            // images some node lists, with the summed scaledImageScore of the containers using them
+  int32_t img_id[KSG_MAX_IMG];
+  int64_t img_scaled[KSG_MAX_IMG];
+  int64_t img_max_threshold;  // maxContainerThreshold x (#init + #containers)
+
   // ---- as-existing record (committed on assume)
   uint32_t exist_flags;     // KEF_*
   int32_t n_exist_terms;
@@ -176,6 +201,8 @@ typedef struct ksg_prog {
 #define KPF_HAS_SCALAR_REQ (1u << 10)
 #define KPF_PREFILTER_REJECT (1u << 11)  // PreFilter Unschedulable (host-known): no node evaluated
 #define KPF_PREFILTER_ERROR (1u << 12)   // PreFilter error status: cycle aborts
+#define KPF_TOL_UNSCHED (1u << 13)       // tolerates node.kubernetes.io/unschedulable:NoSchedule
+#define KPF_SKIP_PORTS (1u << 14)        // NodePorts PreFilter Skip (no host ports)
 
 // KEF_* existing-pod flags
 #define KEF_TERMINATING (1u << 0)

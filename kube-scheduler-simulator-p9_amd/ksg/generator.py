@@ -100,8 +100,19 @@ DEFAULT_HOT_PROFILE = [("TaintToleration", 3), ("NodeAffinity", 2), ("NodeResour
                        ("NodeResourcesBalancedAllocation", 1)]
 
 
+# the whole default profile (scheduler_test.go:531-557 configGeneratedFromDefault):
+# MultiPoint order; plugins without an explicit weight get 1 (plugins.go:289-304)
+DEFAULT_PROFILE = [("SchedulingGates", 1), ("PrioritySort", 1), ("NodeUnschedulable", 1), ("NodeName", 1),
+                   ("TaintToleration", 3), ("NodeAffinity", 2), ("NodePorts", 1), ("NodeResourcesFit", 1),
+                   ("VolumeRestrictions", 1), ("EBSLimits", 1), ("GCEPDLimits", 1), ("NodeVolumeLimits", 1),
+                   ("AzureDiskLimits", 1), ("VolumeBinding", 1), ("VolumeZone", 1), ("PodTopologySpread", 2),
+                   ("InterPodAffinity", 2), ("DefaultPreemption", 1), ("NodeResourcesBalancedAllocation", 1),
+                   ("ImageLocality", 1), ("DefaultBinder", 1)]
+
+
 # --------------------------------------------------------------------------- builders
-def node_obj(name, cpu_milli, mem, pods=110, labels=None, taints=None, eph=None, scalars=None):
+def node_obj(name, cpu_milli, mem, pods=110, labels=None, taints=None, eph=None, scalars=None, images=None,
+             unschedulable=False):
     alloc = {"cpu": f"{cpu_milli}m" if cpu_milli % 1000 else str(cpu_milli // 1000),
              "memory": f"{mem // Gi}Gi" if mem % Gi == 0 else str(mem),
              "pods": str(pods)}
@@ -114,8 +125,12 @@ def node_obj(name, cpu_milli, mem, pods=110, labels=None, taints=None, eph=None,
     spec = {}
     if taints:
         spec["taints"] = taints
-    return {"metadata": {"name": name, "labels": lab}, "spec": spec,
-            "status": {"allocatable": alloc, "capacity": dict(alloc)}}
+    if unschedulable:
+        spec["unschedulable"] = True
+    status = {"allocatable": alloc, "capacity": dict(alloc)}
+    if images:
+        status["images"] = [{"names": list(n), "sizeBytes": sz} for n, sz in images]
+    return {"metadata": {"name": name, "labels": lab}, "spec": spec, "status": status}
 
 
 def req(cpu_milli=None, mem=None, extra=None):
@@ -128,9 +143,12 @@ def req(cpu_milli=None, mem=None, extra=None):
     return {"requests": r} if r else {}
 
 
-def pod_obj(name, containers, labels=None, node=None, ns="default", **spec_extra):
-    spec = {"containers": [{"name": f"c{i}", "image": "registry.k8s.io/pause:3.5",
+def pod_obj(name, containers, labels=None, node=None, ns="default", images=None, ports=None, **spec_extra):
+    """images / ports: per container (image name, list of v1.ContainerPort dicts)."""
+    spec = {"containers": [{"name": f"c{i}", "image": (images or {}).get(i, "registry.k8s.io/pause:3.5"),
                             "resources": c} for i, c in enumerate(containers)]}
+    for i, ps in (ports or {}).items():
+        spec["containers"][i]["ports"] = ps
     if node is not None:
         spec["nodeName"] = node
     spec.update(spec_extra)
@@ -144,20 +162,57 @@ def filler_pod(name, node, cpu, mem):
 
 
 # --------------------------------------------------------------------------- config 1
+# image vocabulary of cfg1: (names as listed in node.status.images, sizeBytes)
+CFG1_IMAGES = [((f"registry.k8s.io/app-{k}:1.{k}", f"registry.k8s.io/app-{k}@sha256:{k:064x}"), (40 + 110 * k) * Mi)
+               for k in range(8)] + [(("docker.io/library/busybox:latest",), 4 * Mi),
+                                     (("quay.io/big/model:latest",), 1800 * Mi)]
+CFG1_POD_IMAGES = [f"registry.k8s.io/app-{k}:1.{k}" for k in range(8)] + [
+    "docker.io/library/busybox", "quay.io/big/model", "registry.k8s.io/pause:3.5", "example.com:5000/tool"]
+
+
 def gen_cfg1(n_nodes=100, n_pods=1000, seed=None):
+    """Default KubeSchedulerConfiguration (all 21 MultiPoint plugins).  Besides the
+    hot-path plugins' inputs the cluster carries what the rest of the default
+    profile reads: cordoned nodes (NodeUnschedulable), node images (ImageLocality),
+    host ports on bound and queued pods (NodePorts)."""
     seed = config_seed(1) if seed is None else seed
     r = Rng(seed)
-    nodes = [node_obj(f"node-{i:07d}", 16000, 64 * Gi, labels={ZONE: f"zone-{i % 4}"})
-             for i in range(n_nodes)]
+    nodes = []
+    for i in range(n_nodes):
+        imgs = [CFG1_IMAGES[r.below(len(CFG1_IMAGES))] for _ in range(r.below(5))]
+        imgs = list({n[0]: (n, sz) for n, sz in imgs}.values())
+        nodes.append(node_obj(f"node-{i:07d}", 16000, 64 * Gi, labels={ZONE: f"zone-{i % 4}"}, images=imgs,
+                              unschedulable=r.pct() < 8))
+    bound = []
+    for i in range(0, n_nodes, 5):  # a host-port daemon on every fifth node
+        ports = [{"containerPort": 9100, "hostPort": 9100, "protocol": "TCP"}]
+        if i % 10 == 0:
+            ports.append({"containerPort": 53, "hostPort": 5353, "protocol": "UDP", "hostIP": "10.0.0.1"})
+        bound.append(pod_obj(f"daemon-{i:07d}", [req(100, 128 * Mi)], labels={"app": "daemon"},
+                             node=nodes[i]["metadata"]["name"], ports={0: ports}))
     queue = []
     for j in range(n_pods):
+        nc = 2 if r.pct() < 10 else 1
         if r.pct() < 10:
-            c = [{}]
+            c = [{}] * nc
         else:
-            c = [req(100 * (1 + r.below(10)), 256 * Mi * (1 + r.below(8)))]
-        queue.append(pod_obj(f"pod-{j:07d}", c, labels={"app": f"app-{r.below(10)}"}))
-    return {"profile": make_profile(DEFAULT_HOT_PROFILE, seed), "nodes": nodes, "pods": [],
-            "queue": queue}
+            c = [req(100 * (1 + r.below(10)), 256 * Mi * (1 + r.below(8))) for _ in range(nc)]
+        images = {k: CFG1_POD_IMAGES[r.below(len(CFG1_POD_IMAGES))] for k in range(nc)}
+        ports = None
+        u = r.pct()
+        if u < 4:
+            ports = {0: [{"containerPort": 8080, "hostPort": 8080 + r.below(3)}]}
+        elif u < 6:
+            ports = {0: [{"containerPort": 9100, "hostPort": 9100, "protocol": "TCP", "hostIP": "10.0.0.2"}]}
+        elif u < 7:
+            ports = {0: [{"containerPort": 53, "hostPort": 5353, "protocol": "UDP"}]}
+        extra = {}
+        if r.pct() < 10:
+            extra["tolerations"] = [{"key": "node.kubernetes.io/unschedulable", "operator": "Exists",
+                                     "effect": "NoSchedule"}]
+        queue.append(pod_obj(f"pod-{j:07d}", c, labels={"app": f"app-{r.below(10)}"}, images=images, ports=ports,
+                             **extra))
+    return {"profile": make_profile(DEFAULT_PROFILE, seed), "nodes": nodes, "pods": bound, "queue": queue}
 
 
 # --------------------------------------------------------------------------- config 2

@@ -20,7 +20,16 @@
 //     (balanced_allocation.go), TaintToleration (taint_toleration.go),
 //     NodeAffinity (node_affinity.go + component-helpers nodeaffinity),
 //     PodTopologySpread (filtering.go, scoring.go, common.go), InterPodAffinity
-//     (filtering.go, scoring.go), helper.DefaultNormalizeScore.
+//     (filtering.go, scoring.go), helper.DefaultNormalizeScore; the rest of
+//     the default profile (scheduler_test.go:531-557): NodeUnschedulable
+//     (node_unschedulable.go), NodeName (node_name.go), NodePorts
+//     (node_ports.go + framework HostPortInfo), ImageLocality
+//     (image_locality.go + ImageStateSummary.Snapshot), the volume plugins'
+//     PreFilter/PreScore Skip for pods without volumes they act on
+//     (VolumeRestrictions, EBSLimits, GCEPDLimits, NodeVolumeLimits,
+//     AzureDiskLimits, VolumeBinding, VolumeZone), and the plugins with no
+//     PreFilter/Filter/PreScore/Score extension (PrioritySort, SchedulingGates,
+//     DefaultPreemption, DefaultBinder: the wrapper records nothing for them).
 //   * recording: simulator/scheduler/plugin/wrappedplugin.go:388-548,616-645
 //     (what is recorded per extension point) and resultstore/store.go:133-507
 //     (maps, finalscore = score x weight, GetStoredResult JSON).
@@ -438,9 +447,15 @@ struct TSC {
   vector<string> match_label_keys;
 };
 
+struct HostPort {  // v1.ContainerPort with hostPort > 0, sanitised (HostPortInfo.sanitize)
+  string ip, proto;
+  int32_t port;
+};
 struct Container {
   ResourceList requests;
   bool restart_always = false;
+  string image;
+  vector<HostPort> ports;
 };
 
 struct Pod {
@@ -464,13 +479,20 @@ struct Pod {
   vector<WAffTerm> pref_aff, pref_anti;
   bool pref_aff_present = false, pref_anti_present = false;  // for hasConstraints
   vector<TSC> tsc;
+  bool volume_plugins_act = false;  // a volume the volume plugins would not Skip (unsupported)
 };
 
+struct NodeImage {
+  vector<string> names;
+  i64 size = 0;
+};
 struct Node {
   string name;
   Labels labels;
   vector<Taint> taints;
   Resource alloc;
+  bool unschedulable = false;
+  vector<NodeImage> images;
 };
 
 // ============================================================ parsing
@@ -515,11 +537,28 @@ static bool parse_pod(const ojson::Value& v, Pod& p) {
       auto* res = c.get("resources");
       k.requests = parse_rl(res ? res->get("requests") : nullptr);
       k.restart_always = c.get("restartPolicy") && c.get("restartPolicy")->str() == "Always";
+      k.image = c.get("image") ? c.get("image")->str() : "";
+      if (auto* ps = c.get("ports"))
+        for (auto& x : ps->arr) {
+          i64 hp = x.get("hostPort") ? x.get("hostPort")->i64() : 0;
+          if (hp <= 0) continue;  // node_ports.go getContainerPorts: host ports only
+          HostPort h{x.get("hostIP") ? x.get("hostIP")->str() : "", x.get("protocol") ? x.get("protocol")->str() : "",
+                     (int32_t)hp};
+          if (h.ip.empty()) h.ip = "0.0.0.0";  // HostPortInfo.sanitize
+          if (h.proto.empty()) h.proto = "TCP";
+          k.ports.push_back(h);
+        }
       out.push_back(k);
     }
   };
   conts(sp->get("containers"), p.containers);
   conts(sp->get("initContainers"), p.init_containers);
+  for (auto& c : p.init_containers) c.ports.clear();  // v1.30: Spec.Containers only (getContainerPorts, updateUsedPorts)
+  if (auto* vs = sp->get("volumes"))
+    for (auto& v : vs->arr)
+      for (const char* k : {"persistentVolumeClaim", "ephemeral", "gcePersistentDisk", "awsElasticBlockStore", "rbd",
+                            "iscsi", "azureDisk", "cinder", "csi"})
+        if (v.get(k) && !v.get(k)->is_null()) p.volume_plugins_act = true;
   p.overhead = parse_rl(sp->get("overhead"));
   if (auto* ns = sp->get("nodeSelector"); ns && !ns->is_null()) {
     p.has_node_selector = true;
@@ -594,8 +633,18 @@ static void parse_node(const ojson::Value& v, Node& n) {
       for (auto& t : ts->arr)
         n.taints.push_back({t.get("key") ? t.get("key")->str() : "", t.get("value") ? t.get("value")->str() : "",
                             t.get("effect") ? t.get("effect")->str() : ""});
+  if (auto* sp = v.get("spec"))
+    if (auto* u = sp->get("unschedulable")) n.unschedulable = u->b;
   auto* st = v.get("status");
   resource_add(n.alloc, parse_rl(st ? st->get("allocatable") : nullptr));
+  if (st)
+    if (auto* im = st->get("images"))
+      for (auto& x : im->arr) {
+        NodeImage ni;
+        ni.names = str_list(x.get("names"));
+        ni.size = x.get("sizeBytes") ? x.get("sizeBytes")->i64() : 0;
+        n.images.push_back(ni);
+      }
 }
 
 // ============================================================ resource helpers (PodRequests)
@@ -725,6 +774,7 @@ struct NodeInfo {
   Resource requested;
   i64 nz_cpu = 0, nz_mem = 0;
   vector<int> pods, pods_with_affinity, pods_with_req_anti;
+  map<string, map<std::pair<string, int32_t>, int>> used_ports;  // HostPortInfo: ip -> (protocol, port)
 };
 
 struct ScoreSpec {
@@ -732,7 +782,13 @@ struct ScoreSpec {
   i64 weight;
 };
 
-enum PluginId { P_FIT, P_BA, P_TAINT, P_NA, P_PTS, P_IPA, P_UNKNOWN };
+// P_VOLUME: VolumeRestrictions, EBSLimits, GCEPDLimits, NodeVolumeLimits,
+// AzureDiskLimits, VolumeZone (PreFilter + Filter; PreFilter Skip for pods
+// without volumes they act on).  P_VOLBIND: VolumeBinding (also PreScore, Skip
+// with the default feature gates: no scorer).  P_NOOP: plugins with none of the
+// recorded extension points.
+enum PluginId { P_FIT, P_BA, P_TAINT, P_NA, P_PTS, P_IPA, P_UNSCHED, P_NODENAME, P_PORTS, P_IMAGE,
+                P_VOLUME, P_VOLBIND, P_NOOP, P_UNKNOWN };
 static PluginId plugin_id(const string& n) {
   if (n == "NodeResourcesFit") return P_FIT;
   if (n == "NodeResourcesBalancedAllocation") return P_BA;
@@ -740,12 +796,26 @@ static PluginId plugin_id(const string& n) {
   if (n == "NodeAffinity") return P_NA;
   if (n == "PodTopologySpread") return P_PTS;
   if (n == "InterPodAffinity") return P_IPA;
+  if (n == "NodeUnschedulable") return P_UNSCHED;
+  if (n == "NodeName") return P_NODENAME;
+  if (n == "NodePorts") return P_PORTS;
+  if (n == "ImageLocality") return P_IMAGE;
+  if (n == "VolumeRestrictions" || n == "EBSLimits" || n == "GCEPDLimits" || n == "NodeVolumeLimits" ||
+      n == "AzureDiskLimits" || n == "VolumeZone")
+    return P_VOLUME;
+  if (n == "VolumeBinding") return P_VOLBIND;
+  if (n == "PrioritySort" || n == "SchedulingGates" || n == "DefaultPreemption" || n == "DefaultBinder") return P_NOOP;
   return P_UNKNOWN;
 }
-static bool has_prefilter(PluginId p) { return p == P_FIT || p == P_NA || p == P_PTS || p == P_IPA; }
-static bool has_filter(PluginId p) { return p == P_FIT || p == P_TAINT || p == P_NA || p == P_PTS || p == P_IPA; }
-static bool has_prescore(PluginId p) { return p != P_UNKNOWN; }
-static bool has_score(PluginId p) { return p != P_UNKNOWN; }
+static bool has_prefilter(PluginId p) {
+  return p == P_FIT || p == P_NA || p == P_PTS || p == P_IPA || p == P_PORTS || p == P_VOLUME || p == P_VOLBIND;
+}
+static bool has_filter(PluginId p) {
+  return p == P_FIT || p == P_TAINT || p == P_NA || p == P_PTS || p == P_IPA || p == P_UNSCHED || p == P_NODENAME ||
+         p == P_PORTS || p == P_VOLUME || p == P_VOLBIND;
+}
+static bool has_prescore(PluginId p) { return p <= P_IPA || p == P_VOLBIND; }
+static bool has_score(PluginId p) { return p <= P_IPA || p == P_IMAGE || p == P_VOLBIND; }
 static bool has_score_ext(PluginId p) { return p == P_TAINT || p == P_NA || p == P_PTS || p == P_IPA; }
 
 struct ResSpec {
@@ -767,6 +837,7 @@ struct PodResult {
   int status = 0;  // 0 scheduled, 1 unschedulable, 2 error
   // store maps (resultstore/store.go result)
   map<string, string> pre_filter_status, pre_score;
+  map<string, string> reserve, prebind, bind;  // binding cycle of a scheduled pod (bind assumed to succeed)
   map<string, vector<string>> pre_filter_result;
   std::unordered_map<string, std::unordered_map<string, string>> filter, score, final_score;
 };
@@ -852,11 +923,11 @@ static string render_annotations(const PodResult& r) {
   ann[k("prescore-result")] = json_map(r.pre_score);
   ann[k("score-result")] = json_map2(r.score);
   ann[k("finalscore-result")] = json_map2(r.final_score);
-  ann[k("reserve-result")] = "{}";
+  ann[k("reserve-result")] = json_map(r.reserve);
   ann[k("permit-result")] = "{}";
   ann[k("permit-result-timeout")] = "{}";
-  ann[k("prebind-result")] = "{}";
-  ann[k("bind-result")] = "{}";
+  ann[k("prebind-result")] = json_map(r.prebind);
+  ann[k("bind-result")] = json_map(r.bind);
   ann[k("selected-node")] = r.selected;
   return json_map(ann);
 }
@@ -898,7 +969,19 @@ struct CycleState {
   map<std::pair<string, string>, i64> ipa_existing_anti, ipa_aff_counts, ipa_anti_counts;
   vector<WAffTerm> ipa_pref_aff, ipa_pref_anti;
   map<string, map<string, i64>> ipa_topo_score;
+  // NodePorts preFilterState (getContainerPorts)
+  vector<HostPort> ports_want;
 };
+
+static const i64 kMB = 1024 * 1024;
+static const i64 kImgMinThreshold = 23 * kMB;            // image_locality.go minThreshold
+static const i64 kImgMaxContainerThreshold = 1000 * kMB;  // maxContainerThreshold
+// image_locality.go normalizedImageName
+static string normalized_image_name(const string& n) {
+  size_t c = n.rfind(':'), sl = n.rfind('/');
+  long ci = c == string::npos ? -1 : (long)c, si = sl == string::npos ? -1 : (long)sl;
+  return ci <= si ? n + ":latest" : n;
+}
 
 struct Cluster {
   std::unique_ptr<ojson::Value> doc;
@@ -919,6 +1002,8 @@ struct Cluster {
   i64 ipa_hard_weight = 1;
   bool ipa_ignore_existing_pref = false;
   unsigned long long seed = 0;
+  // ImageStateSummary per image name (size of the first node listing it, node count)
+  std::unordered_map<string, std::pair<i64, int>> image_states;
   // results
   vector<PodResult> results;
   std::mutex store_mu;
@@ -941,6 +1026,8 @@ struct Cluster {
     n.nz_cpu += nz.count("cpu") ? q_milli(nz["cpu"]) : 0;
     n.nz_mem += nz.count("memory") ? q_value(nz["memory"]) : 0;
     n.pods.push_back(pi);
+    for (auto& c : r.pod.containers)  // NodeInfo.updateUsedPorts
+      for (auto& h : c.ports) n.used_ports[h.ip][{h.proto, h.port}]++;
     if (r.with_affinity) n.pods_with_affinity.push_back(pi);
     if (r.has_required_anti) n.pods_with_req_anti.push_back(pi);
   }
@@ -1067,6 +1154,64 @@ struct Cluster {
       std_ = std::sqrt(sum / (double)fr.size());
     }
     return (i64)((1 - std_) * (double)kMaxNodeScore);
+  }
+  // ---------------------------------------------------------------- NodeUnschedulable / NodeName
+  Status unsched_filter(const Pod& p, int ni) {  // node_unschedulable.go Filter
+    if (!nodes[ni].unschedulable) return {};
+    if (tolerations_tolerate(p.tolerations, Taint{"node.kubernetes.io/unschedulable", "", "NoSchedule"})) return {};
+    return {Status::UnschedulableAndUnresolvable, "node(s) were unschedulable"};
+  }
+  Status nodename_filter(const Pod& p, int ni) {  // node_name.go Fits
+    if (p.node_name.empty() || p.node_name == nodes[ni].name) return {};
+    return {Status::UnschedulableAndUnresolvable, "node(s) didn't match the requested node name"};
+  }
+  // ---------------------------------------------------------------- NodePorts
+  Status ports_prefilter(const Pod& p, CycleState& cs) {
+    cs.ports_want.clear();
+    for (auto& c : p.containers) cs.ports_want.insert(cs.ports_want.end(), c.ports.begin(), c.ports.end());
+    if (cs.ports_want.empty()) return Status::skip();
+    return {};
+  }
+  Status ports_filter(CycleState& cs, int ni) {  // fitsPorts -> HostPortInfo.CheckConflict
+    const auto& used = infos[ni].used_ports;
+    for (auto& w : cs.ports_want) {
+      std::pair<string, int32_t> pp{w.proto, w.port};
+      bool conflict = false;
+      if (w.ip == "0.0.0.0") {
+        for (auto& kv : used)
+          if (kv.second.count(pp)) conflict = true;
+      } else {
+        for (const string& k : {string("0.0.0.0"), w.ip}) {
+          auto it = used.find(k);
+          if (it != used.end() && it->second.count(pp)) conflict = true;
+        }
+      }
+      if (conflict) return {Status::Unschedulable, "node(s) didn't have free ports for the requested pod ports"};
+    }
+    return {};
+  }
+  // ---------------------------------------------------------------- ImageLocality
+  i64 image_score(const Pod& p, int ni) {  // image_locality.go Score
+    const Node& n = nodes[ni];
+    i64 sum = 0;
+    auto add = [&](const vector<Container>& cs) {
+      for (auto& c : cs) {
+        string nm = normalized_image_name(c.image);
+        bool has = false;
+        for (auto& im : n.images)
+          for (auto& x : im.names) has |= x == nm;
+        if (!has) continue;
+        auto& st = image_states[nm];
+        double spread = (double)st.second / (double)nodes.size();  // scaledImageScore
+        sum += (i64)((double)st.first * spread);
+      }
+    };
+    add(p.init_containers);
+    add(p.containers);
+    i64 maxT = kImgMaxContainerThreshold * (i64)(p.init_containers.size() + p.containers.size());
+    if (sum < kImgMinThreshold) sum = kImgMinThreshold;
+    else if (sum > maxT) sum = maxT;
+    return kMaxNodeScore * (sum - kImgMinThreshold) / (maxT - kImgMinThreshold);
   }
   // ---------------------------------------------------------------- TaintToleration
   Status taint_filter(const Pod& p, int ni) {
@@ -1550,6 +1695,8 @@ struct Cluster {
       else if (id == P_NA) { auto x = na_prefilter(p, cs, has_res); s = x.first; res = x.second; }
       else if (id == P_PTS) s = pts_prefilter(p, cs, pool);
       else if (id == P_IPA) s = ipa_prefilter(p, cs, pool);
+      else if (id == P_PORTS) s = ports_prefilter(p, cs);
+      else if (id == P_VOLUME || id == P_VOLBIND) s = Status::skip();  // no volumes they act on (checked at load)
       const string& nm = profile_names[k];
       rec([&] {
         r.pre_filter_status[nm] = s.ok() ? "success" : s.msg;
@@ -1581,6 +1728,9 @@ struct Cluster {
         else if (id == P_NA) s = na_filter(cs, ni);
         else if (id == P_PTS) s = pts_filter(p, cs, ni);
         else if (id == P_IPA) s = ipa_filter(p, cs, ni);
+        else if (id == P_UNSCHED) s = unsched_filter(p, ni);
+        else if (id == P_NODENAME) s = nodename_filter(p, ni);
+        else if (id == P_PORTS) s = ports_filter(cs, ni);
         rec([&] { r.filter[nodes[ni].name][profile_names[k]] = s.ok() ? "passed" : s.msg; });
         if (!s.ok()) {
           if (s.code == Status::Error) err = true;
@@ -1611,6 +1761,7 @@ struct Cluster {
         else if (id == P_NA) s = na_prescore(p, cs, (int)feasible.size());
         else if (id == P_PTS) s = pts_prescore(p, cs, feasible, pool);
         else if (id == P_IPA) s = ipa_prescore(p, cs, feasible, pool);
+        else if (id == P_VOLBIND) s = Status::skip();  // PreScore: no scorer (VolumeCapacityPriority off)
         rec([&] { r.pre_score[profile_names[k]] = s.ok() ? "success" : s.msg; });
         if (s.code == Status::Skip) { skip_score.insert(id); continue; }
         if (!s.ok()) { r.status = 2; finish(qidx, pi, r, record); return; }
@@ -1632,6 +1783,7 @@ struct Cluster {
           else if (id == P_NA) s = na_score(cs, ni);
           else if (id == P_PTS) s = pts_score(p, cs, ni);
           else if (id == P_IPA) s = ipa_score(cs, ni);
+          else if (id == P_IMAGE) s = image_score(p, ni);
           scores[j][i] = s;
           const string& nm = profile_names[sp[j]];
           rec([&] {  // Store.AddScoreResult: raw + provisional final = raw x weight
@@ -1672,6 +1824,12 @@ struct Cluster {
     }
     r.selected = nodes[chosen].name;
     r.selected_idx = chosen;
+    rec([&] {  // wrappedplugin.go Reserve/PreBind/Bind: VolumeBinding (allBound), DefaultBinder
+      for (size_t k = 0; k < profile.size(); ++k) {
+        if (profile[k] == P_VOLBIND) r.reserve[profile_names[k]] = r.prebind[profile_names[k]] = "success";
+        if (profile_names[k] == "DefaultBinder") r.bind[profile_names[k]] = "success";
+      }
+    });
     if (defer_assume) deferred.emplace_back(pi, chosen);  // what-if batch: bound after the step
     else add_pod(pi, chosen);  // assume
     finish(qidx, pi, r, record);
@@ -1769,6 +1927,15 @@ static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
       c.nodes.push_back(std::move(x));
     }
   c.infos.assign(c.nodes.size(), NodeInfo());
+  for (auto& n : c.nodes) {  // ImageStateSummary: Size from the first node listing the name, NumNodes
+    set<string> seen;
+    for (auto& im : n.images)
+      for (auto& nm : im.names) {
+        auto it = c.image_states.find(nm);
+        if (it == c.image_states.end()) c.image_states[nm] = {im.size, 0};
+        if (seen.insert(nm).second) c.image_states[nm].second++;
+      }
+  }
   auto add = [&](const ojson::Value& v) {
     PodRecord r;
     r.parse_ok = parse_pod(v, r.pod);
@@ -1786,6 +1953,14 @@ static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
     }
   if (auto* q = d.get("queue"))
     for (auto& p : q->arr) c.queue.push_back(add(p));
+  bool vol = false;
+  for (PluginId id : c.profile) vol |= id == P_VOLUME || id == P_VOLBIND;
+  if (vol)
+    for (int qi : c.queue)
+      if (c.pods[qi].pod.volume_plugins_act) {
+        err = "pod " + c.pods[qi].pod.name + ": volumes the volume plugins act on are not modelled";
+        return false;
+      }
   c.results.assign(c.queue.size(), PodResult());
   c.rendered.assign(c.queue.size(), string());
   c.digests.assign(c.queue.size(), 0);

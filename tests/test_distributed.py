@@ -95,13 +95,15 @@ def test_sharded_batch_path_matches_oracle(world):
 # keys whose domains span nodes, feasible count, normalisers, PTS registration,
 # argmax) are merged at four exchange points.
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,world", [(3, 2), (4, 2), (4, 3)])
+@pytest.mark.parametrize("cfg,world", [(1, 2), (3, 2), (4, 2), (4, 3)])
 def test_sharded_per_pod_chain_matches_oracle(cfg, world):
     import json
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _oracle import Oracle
     from ksg import generator as g
-    if cfg == 3:
+    if cfg == 1:  # whole default profile: NodePorts / ImageLocality / NodeName are node-local
+        doc = g.generate(1, n_nodes=60, n_pods=150)
+    elif cfg == 3:
         doc = g.generate(3, n_nodes=300, n_pods=120)
     else:
         doc = g.generate(4, n_nodes=240, n_existing=900, n_pods=120, n_zones=6)

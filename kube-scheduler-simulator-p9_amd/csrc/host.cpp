@@ -1605,6 +1605,21 @@ struct Cluster {
       }
     }
     string sel = S.status == 0 && S.selected >= 0 ? nodes[S.selected].name : "";
+    string post = "{}";  // DefaultPreemption, equal priorities: every node recorded, none nominated (oracle finish())
+    if (S.status == 1)
+      for (int pos = 0; pos < n_plugins; ++pos)
+        if (names[pos] == "DefaultPreemption") {
+          vector<string> nn;  // encoding/json: map keys sorted
+          for (uint32_t i = 0; i < n; ++i) nn.push_back(nodes[lo + i].name);
+          std::sort(nn.begin(), nn.end());
+          post = "{";
+          for (size_t i = 0; i < nn.size(); ++i) {
+            if (i) post += ',';
+            jstr(post, nn[i]);
+            post += ":{}";
+          }
+          post += "}";
+        }
     map<string, string> reserve, prebind, bind;  // binding cycle of a scheduled pod (the bind assumed to succeed)
     if (!sel.empty())
       for (int pos = 0; pos < n_plugins; ++pos) {
@@ -1635,7 +1650,7 @@ struct Cluster {
     pr += "}";
     const string P = "kube-scheduler-simulator.sigs.k8s.io/";
     map<string, string> ann{{P + "prefilter-result", pr},          {P + "prefilter-result-status", jmap(pre_status)},
-                            {P + "filter-result", j2(filt)},       {P + "postfilter-result", "{}"},
+                            {P + "filter-result", j2(filt)},       {P + "postfilter-result", post},
                             {P + "prescore-result", jmap(pre_score)}, {P + "score-result", j2(score)},
                             {P + "finalscore-result", j2(fin)},    {P + "reserve-result", jmap(reserve)},
                             {P + "permit-result", "{}"},           {P + "permit-result-timeout", "{}"},

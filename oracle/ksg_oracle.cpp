@@ -837,6 +837,7 @@ struct PodResult {
   int status = 0;  // 0 scheduled, 1 unschedulable, 2 error
   // store maps (resultstore/store.go result)
   map<string, string> pre_filter_status, pre_score;
+  vector<string> post_filter_nodes;  // DefaultPreemption: nodes of the NodeToStatusMap (no nomination)
   map<string, string> reserve, prebind, bind;  // binding cycle of a scheduled pod (bind assumed to succeed)
   map<string, vector<string>> pre_filter_result;
   std::unordered_map<string, std::unordered_map<string, string>> filter, score, final_score;
@@ -919,7 +920,17 @@ static string render_annotations(const PodResult& r) {
   ann[k("prefilter-result")] = json_map_list(r.pre_filter_result);
   ann[k("prefilter-result-status")] = json_map(r.pre_filter_status);
   ann[k("filter-result")] = json_map2(r.filter);
-  ann[k("postfilter-result")] = "{}";
+  {  // Store.AddPostFilterResult: every node of the status map gets an (empty) entry
+    map<string, map<string, string>> pf;
+    for (auto& n : r.post_filter_nodes) pf[n];
+    string o = "{";
+    for (auto& kv : pf) {
+      if (o.size() > 1) o += ',';
+      go_json_string(o, kv.first);
+      o += ":{}";
+    }
+    ann[k("postfilter-result")] = o + "}";
+  }
   ann[k("prescore-result")] = json_map(r.pre_score);
   ann[k("score-result")] = json_map2(r.score);
   ann[k("finalscore-result")] = json_map2(r.final_score);
@@ -1856,6 +1867,15 @@ struct Cluster {
   int keep_annotations = 0;
   void finish(int qidx, int pi, PodResult& r, int record) {
     (void)pi;
+    // PostFilter (schedule_one.go: unschedulable pods only).  DefaultPreemption with
+    // every pod at the same priority finds no victims (SelectVictimsOnNode removes
+    // only lower-priority pods), so nothing is nominated; the wrapper still records
+    // every node of the status map, which holds every node (failed Filter, outside
+    // the PreFilterResult, or a rejecting PreFilter).
+    if (record && r.status == 1)
+      for (size_t k = 0; k < profile.size(); ++k)
+        if (profile_names[k] == "DefaultPreemption")
+          for (auto& n : nodes) r.post_filter_nodes.push_back(n.name);
     if (record >= 2) {
       string a = render_annotations(r);
       unsigned long long h = 1469598103934665603ULL;  // FNV-1a 64

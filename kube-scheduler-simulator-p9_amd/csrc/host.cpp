@@ -247,6 +247,7 @@ struct Pod {
   struct HostPort { string ip, proto; int32_t port; };
   vector<HostPort> ports; // Spec.Containers host ports (hostPort > 0), sanitised
   bool volume_plugins_act = false;  // a volume the volume plugins would not Skip
+  i64 priority = 0;                 // spec.priority (DefaultPreemption is modelled for equal priorities)
 };
 
 static RList pod_requests(const J* spec, bool nonzero) {
@@ -307,6 +308,7 @@ static Pod parse_pod(const J& v) {
   p.req_nz = pod_requests(sp, true);
   if (!sp) return p;
   p.node = str_of((*sp)["nodeName"]);
+  if (auto* pr = (*sp)["priority"]; pr && !pr->null()) p.priority = (i64)pr->num();
   for (const char* k : {"initContainers", "containers"})
     if (auto* cs = (*sp)[k])
       for (auto& c : cs->items) {
@@ -1247,6 +1249,7 @@ struct Cluster {
     if (has_volume_plugins)
       for (auto& p : queue)
         if (p.volume_plugins_act) { err = "pod " + p.name + ": volumes the volume plugins act on are not modelled"; return false; }
+    if (!equal_priorities()) return false;
     if (!build_vocab()) return false;
     NodeSoA S;
     PodTableSoA T;
@@ -1275,6 +1278,22 @@ struct Cluster {
     placed.clear();
     assumed_in.clear();
     epoch = 0;
+    return true;
+  }
+
+  // DefaultPreemption's dry run is modelled for queues whose pods all share one
+  // priority (no victims can exist); other clusters are refused, not approximated.
+  bool has_preemption() const {
+    for (int i = 0; i < n_plugins; ++i)
+      if (names[i] == "DefaultPreemption") return true;
+    return false;
+  }
+  bool equal_priorities() {
+    if (!has_preemption()) return true;
+    set<i64> pr;
+    for (auto* v : {&bound, &queue})
+      for (auto& p : *v) pr.insert(p.priority);
+    if (pr.size() > 1) { err = "pods of different priorities: DefaultPreemption victims are not modelled"; return false; }
     return true;
   }
 
@@ -1383,6 +1402,10 @@ struct Cluster {
     queue.push_back(parse_pod(d["pod"] ? *d["pod"] : d));
     if (has_volume_plugins && queue.back().volume_plugins_act) {
       err = "pod " + queue.back().name + ": volumes the volume plugins act on are not modelled";
+      queue.pop_back();
+      return false;
+    }
+    if (!equal_priorities()) {
       queue.pop_back();
       return false;
     }

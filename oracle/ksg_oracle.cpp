@@ -480,6 +480,7 @@ struct Pod {
   bool pref_aff_present = false, pref_anti_present = false;  // for hasConstraints
   vector<TSC> tsc;
   bool volume_plugins_act = false;  // a volume the volume plugins would not Skip (unsupported)
+  i64 priority = 0;
 };
 
 struct NodeImage {
@@ -530,6 +531,7 @@ static bool parse_pod(const ojson::Value& v, Pod& p) {
   p.terminating = md && md->get("deletionTimestamp") && !md->get("deletionTimestamp")->is_null();
   if (!sp) return true;
   p.node_name = sp->get("nodeName") ? sp->get("nodeName")->str() : "";
+  if (auto* pr = sp->get("priority"); pr && !pr->is_null()) p.priority = pr->i64();
   auto conts = [](const ojson::Value* a, vector<Container>& out) {
     if (!a) return;
     for (auto& c : a->arr) {
@@ -1973,8 +1975,17 @@ static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
     }
   if (auto* q = d.get("queue"))
     for (auto& p : q->arr) c.queue.push_back(add(p));
-  bool vol = false;
+  bool vol = false, preempt = false;
   for (PluginId id : c.profile) vol |= id == P_VOLUME || id == P_VOLBIND;
+  for (auto& n : c.profile_names) preempt |= n == "DefaultPreemption";
+  if (preempt) {
+    set<i64> pr;
+    for (auto& r : c.pods) pr.insert(r.pod.priority);
+    if (pr.size() > 1) {
+      err = "pods of different priorities: DefaultPreemption victims are not modelled";
+      return false;
+    }
+  }
   if (vol)
     for (int qi : c.queue)
       if (c.pods[qi].pod.volume_plugins_act) {

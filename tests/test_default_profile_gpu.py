@@ -156,3 +156,12 @@ def test_volume_pods_refused():
     s = Scheduler(doc["profile"])
     with pytest.raises(Exception):
         s.load_cluster(doc)
+
+
+@pytest.mark.gpu
+def test_mixed_priorities_refused():
+    doc = g.generate(1, n_nodes=4, n_pods=2)
+    doc["queue"][1]["spec"]["priority"] = 1000
+    s = Scheduler(doc["profile"])
+    with pytest.raises(Exception):
+        s.load_cluster(doc)

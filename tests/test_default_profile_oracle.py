@@ -96,3 +96,11 @@ def test_unschedulable_nodename_and_skip_records():
     assert fb["n1"]["NodeName"] == "node(s) didn't match the requested node name"
     assert _ann(o, 1, "postfilter-result") == {"n0": {}, "n1": {}}
     assert _ann(o, 1, "bind-result") == {}
+
+
+def test_mixed_priorities_refused():
+    import pytest
+    nodes = [g.node_obj("n0", 4000, 8 * g.Gi)]
+    q = [g.pod_obj("a", [g.req(100, Mi)]), g.pod_obj("b", [g.req(100, Mi)], priority=1000)]
+    with pytest.raises(ValueError):
+        Oracle(_doc(nodes, q))

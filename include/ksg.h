@@ -166,6 +166,22 @@ int ksg_reserve(ksg_ctx* ctx, uint32_t q, int32_t node);
  * pod q (cycle or queue mode): node rows, and its existing-pod table entry. */
 int ksg_unreserve(ksg_ctx* ctx, uint32_t q);
 
+/* Scheduler-cache events between cycles (replaces the informer -> Cache path:
+ * Cache.AddNode/UpdateNode/RemoveNode/AddPod/UpdatePod/RemovePod of upstream
+ * v1.30.4 pkg/scheduler/internal/cache/cache.go, driven by eventhandlers.go;
+ * the simulator raises them from its apiserver).  JSON:
+ *   {"events": [{"op": "addNode"|"updateNode", "node": {v1.Node}},
+ *               {"op": "removeNode", "name": "node-x"},
+ *               {"op": "addPod"|"updatePod", "pod": {v1.Pod with spec.nodeName}},
+ *               {"op": "removePod", "name": "p", "namespace": "ns"}, ...]}
+ * applied in order; the batch is all-or-nothing.  removePod also takes a queue
+ * pod that was scheduled (its placement is released, its result kept);
+ * removeNode requires that no pod is bound or assumed on the node (upstream
+ * deletes the node's pods first).  Placements of scheduled queue pods are kept;
+ * node indices after a removed node shift down by one.  Per-node outputs kept for
+ * pods scheduled before the batch are not re-indexed. */
+int ksg_apply_events(ksg_ctx* ctx, const char* events_json, size_t len);
+
 /* Device node rows (assume parity): requested [n_res][n], pod count [n]. */
 int ksg_node_requested(ksg_ctx* ctx, int64_t* requested, int32_t* pod_count, uint32_t n_res, uint32_t n);
 

@@ -1345,12 +1345,20 @@ struct Cluster {
   }
   // Re-encode and re-upload the snapshot with every assumed queue pod as a bound
   // pod, recompile the queue, and restore the per-pod summaries.
-  bool rebuild() {
+  // remap: old node index -> new index, when nodes were removed (cluster events).
+  bool rebuild(const vector<int32_t>* remap = nullptr) {
     track_queue();
     size_t nq = queue.size();
     const size_t ns = compiled ? progs.size() : 0;  // pods with programs (and summaries) on the device
     vector<ksg_pod_summary> sum(nq);
     if (ns && !eng->summaries(0, (uint32_t)ns, sum.data(), err)) return false;
+    if (remap)
+      for (size_t q = 0; q < ns; ++q)
+        if (sum[q].selected >= 0 && sum[q].selected < (int32_t)remap->size()) {
+          int32_t to = (*remap)[sum[q].selected];
+          sum[q].selected = to;
+          sum[q].best_key = (sum[q].best_key & ~0xFFFFFull) | (uint64_t)(to < 0 ? 0 : to);
+        }
     vector<Pod> saved = bound;
     for (size_t q = 0; q < nq; ++q) {
       int32_t at = placement((uint32_t)q, q < ns ? &sum[q] : nullptr);
@@ -1459,6 +1467,136 @@ struct Cluster {
     placed[q] = -1;
     if (assumed_in[q] == epoch) return eng->assume(q, at, -1, err);
     return rebuild();  // assumed before the last rebuild: it is a bound pod of the snapshot now
+  }
+
+  // ------------------------------------------------------------ cluster events
+  // Scheduler-cache events between cycles: upstream Cache.AddNode / UpdateNode /
+  // RemoveNode / AddPod / UpdatePod / RemovePod (v1.30.4 pkg/scheduler/internal/
+  // cache/cache.go, fed by eventhandlers.go; in the simulator the events come from
+  // its apiserver, e.g. resources applied by simulator/resourceapplier or the
+  // snapshot service).  A batch is applied to the host mirror, then the snapshot
+  // is re-encoded once with every placement kept (queue pods already scheduled
+  // stay bound where they were).  A batch that fails leaves the mirror unchanged.
+  static string obj_name(const J& e, const char* field, string* ns) {
+    const J* o = e[field];
+    const J* md = o ? (*o)["metadata"] : nullptr;
+    if (ns) *ns = md && (*md)["namespace"] ? str_of((*md)["namespace"]) : (e["namespace"] ? str_of(e["namespace"]) : "default");
+    return md ? str_of((*md)["name"]) : str_of(e["name"]);
+  }
+  bool apply_events(const char* js, size_t len) {
+    if (!compile_queue()) return false;
+    try {
+      docs.emplace_back(new J(json::parse(js, len)));
+    } catch (std::exception& e) {
+      err = e.what();
+      return false;
+    }
+    const J& d = *docs.back();
+    const J* ev = d["events"] ? d["events"] : &d;
+    track_queue();
+    const size_t ns = progs.size();
+    vector<ksg_pod_summary> sum(ns);
+    if (ns && !eng->summaries(0, (uint32_t)ns, sum.data(), err)) return false;
+    vector<Node> nn = nodes;
+    vector<Pod> bb = bound;
+    vector<int8_t> qm = qmode;
+    vector<int32_t> pl = placed;
+    vector<int32_t> remap(nodes.size());  // original index -> current index (-1 removed)
+    for (size_t i = 0; i < remap.size(); ++i) remap[i] = (int32_t)i;
+    bool removed = false;
+    auto node_at = [&](const string& name) -> int32_t {
+      for (size_t i = 0; i < nn.size(); ++i)
+        if (nn[i].name == name) return (int32_t)i;
+      return -1;
+    };
+    auto pod_at = [&](const string& name, const string& pns) -> int32_t {
+      for (size_t i = 0; i < bb.size(); ++i)
+        if (bb[i].name == name && bb[i].ns == pns) return (int32_t)i;
+      return -1;
+    };
+    // current node index of queue pod q's placement (-1 none)
+    auto qplace = [&](size_t q) -> int32_t {
+      int32_t at = qm[q] == 2 ? pl[q] : (qm[q] == 1 && q < ns && sum[q].status == 0 ? sum[q].selected : -1);
+      if (at < 0) return -1;
+      return qm[q] == 2 ? at : remap[at];  // summaries hold original indices until the rebuild
+    };
+    auto queue_at = [&](const string& name, const string& pns) -> int32_t {
+      for (size_t q = 0; q < queue.size(); ++q)
+        if (queue[q].name == name && queue[q].ns == pns && qplace(q) >= 0) return (int32_t)q;
+      return -1;
+    };
+    for (auto& e : ev->items) {
+      const string op = str_of(e["op"]);
+      string pns;
+      if (op == "addNode" || op == "updateNode") {
+        if (!e["node"]) { err = op + ": no node object"; return false; }
+        Node x = parse_node(*e["node"]);
+        int32_t at = node_at(x.name);
+        if (op == "addNode") {
+          if (x.name.empty() || at >= 0) { err = "addNode: node '" + x.name + "' exists or has no name"; return false; }
+          nn.push_back(std::move(x));
+        } else {
+          if (at < 0) { err = "updateNode: no node '" + x.name + "'"; return false; }
+          nn[at] = std::move(x);
+        }
+      } else if (op == "removeNode") {
+        string name = obj_name(e, "node", nullptr);
+        int32_t at = node_at(name);
+        if (at < 0) { err = "removeNode: no node '" + name + "'"; return false; }
+        for (auto& p : bb)
+          if (p.node == name) { err = "removeNode: pod " + p.ns + "/" + p.name + " is still bound to " + name; return false; }
+        for (size_t q = 0; q < queue.size(); ++q)
+          if (qplace(q) == at) { err = "removeNode: queue pod " + queue[q].name + " is assumed on " + name; return false; }
+        nn.erase(nn.begin() + at);
+        for (auto& r : remap)
+          if (r == at) r = -1;
+          else if (r > at) --r;
+        for (size_t q = 0; q < queue.size(); ++q)
+          if (qm[q] == 2 && pl[q] > at) --pl[q];
+        removed = true;
+      } else if (op == "addPod" || op == "updatePod") {
+        if (!e["pod"]) { err = op + ": no pod object"; return false; }
+        Pod p = parse_pod(*e["pod"]);
+        if (p.node.empty()) { err = op + ": pod " + p.name + " has no spec.nodeName (pending pods enter through ksg_cycle)"; return false; }
+        if (node_at(p.node) < 0) { err = op + ": pod " + p.name + " is bound to unknown node '" + p.node + "'"; return false; }
+        int32_t at = pod_at(p.name, p.ns);
+        if (op == "addPod") {
+          if (at >= 0 || queue_at(p.name, p.ns) >= 0) { err = "addPod: pod " + p.ns + "/" + p.name + " exists"; return false; }
+          bb.push_back(std::move(p));
+        } else {
+          if (at < 0) { err = "updatePod: no bound pod " + p.ns + "/" + p.name; return false; }
+          bb[at] = std::move(p);
+        }
+      } else if (op == "removePod") {
+        string name = obj_name(e, "pod", &pns);
+        int32_t at = pod_at(name, pns);
+        if (at >= 0) {
+          bb.erase(bb.begin() + at);
+        } else {
+          int32_t q = queue_at(name, pns);
+          if (q < 0) { err = "removePod: no bound or assumed pod " + pns + "/" + name; return false; }
+          qm[q] = 2;  // deleted after it was scheduled: its result stays, its placement goes
+          pl[q] = -1;
+        }
+      } else {
+        err = "unknown event op '" + op + "'";
+        return false;
+      }
+    }
+    std::swap(nodes, nn);
+    std::swap(bound, bb);
+    std::swap(qmode, qm);
+    std::swap(placed, pl);
+    if (!equal_priorities()) {
+      std::swap(nodes, nn);
+      std::swap(bound, bb);
+      std::swap(qmode, qm);
+      std::swap(placed, pl);
+      return false;
+    }
+    node_names = Dict();
+    for (auto& n : nodes) node_names.add(n.name);
+    return rebuild(removed ? &remap : nullptr);
   }
 
   bool compile_queue() {
@@ -1931,6 +2069,16 @@ int ksg_reserve(ksg_ctx* ctx, uint32_t q, int32_t node) {
 int ksg_unreserve(ksg_ctx* ctx, uint32_t q) {
   if (!ctx) return KSG_E_INVALID;
   if (!ctx->c.unreserve(q)) return ctx->fail(ctx->c.err, KSG_E_STATE);
+  return KSG_OK;
+}
+
+int ksg_apply_events(ksg_ctx* ctx, const char* events_json, size_t len) {
+  if (!ctx || !events_json) return KSG_E_INVALID;
+  try {
+    if (!ctx->c.apply_events(events_json, len)) return ctx->fail(ctx->c.err, KSG_E_STATE);
+  } catch (std::exception& e) {
+    return ctx->fail(e.what(), KSG_E_INVALID);
+  }
   return KSG_OK;
 }
 

@@ -73,6 +73,7 @@ def load_library():
     L.ksg_cycle.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_int, ctypes.c_void_p]
     L.ksg_reserve.argtypes = [vp, u32, i32]
     L.ksg_unreserve.argtypes = [vp, u32]
+    L.ksg_apply_events.argtypes = [vp, ctypes.c_char_p, sz]
     _lib = L
     return L
 
@@ -182,6 +183,12 @@ class Scheduler:
 
     def unreserve(self, q):
         self._chk(self.L.ksg_unreserve(self.h, q), "ksg_unreserve")
+
+    def apply_events(self, events):
+        """Scheduler-cache events (addNode/updateNode/removeNode/addPod/updatePod/
+        removePod dicts, see ksg.h) applied as one all-or-nothing batch."""
+        b = json.dumps({"events": list(events)}).encode()
+        self._chk(self.L.ksg_apply_events(self.h, b, len(b)), "ksg_apply_events")
 
     def sample_kernel(self, every):
         self._chk(self.L.ksg_sample_kernel(self.h, every), "ksg_sample_kernel")

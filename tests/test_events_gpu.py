@@ -1,0 +1,153 @@
+"""GPU parity of scheduler-cache events between cycles (ksg_apply_events).
+
+Upstream the scheduler cache follows informer events (v1.30.4
+pkg/scheduler/internal/cache/cache.go AddNode/UpdateNode/RemoveNode/AddPod/
+UpdatePod/RemovePod, via eventhandlers.go).  A queue is scheduled half-way, a
+batch of events mutates the cluster (node resources/labels updated, a node
+added, a drained node removed, bound pods added and removed, a scheduled queue
+pod deleted), and the second half is scheduled.  The oracle sees the equivalent
+fresh cluster: the mutated nodes, the mutated bound pods plus the first half's
+placements as bound pods, and a queue whose first half is replaced by pods
+that fit nowhere (so the second half keeps its queue indices, which the
+tie-break hash uses, and nothing else changes).
+"""
+import copy
+
+import pytest
+
+from _oracle import Oracle
+from ksg import Scheduler, generator as g
+
+CASES = [
+    ("cfg2", 2, dict(n_nodes=200, n_pods=120)),
+    ("cfg3", 3, dict(n_nodes=200, n_pods=80)),
+    ("cfg4", 4, dict(n_nodes=160, n_existing=600, n_pods=60, n_zones=6)),
+]
+
+
+def _nowhere(i):
+    return g.pod_obj(f"zz-dummy-{i:05d}", [g.req(10 ** 9, 1 << 50)])
+
+
+def _events(doc, placed, k):
+    """Event batch + the oracle's equivalent document."""
+    nodes = copy.deepcopy(doc["nodes"])
+    bound = copy.deepcopy(doc.get("pods", []))
+    names = [n["metadata"]["name"] for n in nodes]
+    ev = []
+    # updateNode: more cpu, a relabel (new key = new vocabulary)
+    upd = copy.deepcopy(nodes[3])
+    upd["status"]["allocatable"]["cpu"] = "96"
+    upd["metadata"]["labels"]["evt"] = "updated"
+    ev.append({"op": "updateNode", "node": upd})
+    nodes[3] = upd
+    # addNode: a copy of node 0 under a new name
+    new = copy.deepcopy(nodes[0])
+    new["metadata"]["name"] = "node-9999999"
+    new["metadata"]["labels"]["kubernetes.io/hostname"] = "node-9999999"
+    ev.append({"op": "addNode", "node": new})
+    nodes.append(new)
+    # addPod: a bound pod (copy of an existing one when there is any: labels count for PTS/IPA)
+    src = copy.deepcopy(bound[0]) if bound else g.filler_pod("x", names[5], 500, 1 << 30)
+    src["metadata"]["name"] = "evt-added"
+    src["spec"]["nodeName"] = names[5]
+    ev.append({"op": "addPod", "pod": src})
+    bound.append(src)
+    # removePod: a bound pod of the snapshot
+    if len(bound) > 2:
+        gone = bound[1]["metadata"]
+        ev.append({"op": "removePod", "name": gone["name"], "namespace": gone.get("namespace", "default")})
+        del bound[1]
+    # removePod: a queue pod scheduled in the first half
+    first = [i for i in range(k) if placed[i] >= 0]
+    deleted = first[0] if first else None
+    if deleted is not None:
+        ev.append({"op": "removePod", "name": doc["queue"][deleted]["metadata"]["name"], "namespace": "default"})
+    # removeNode: drain the node with the fewest bound pods and no placement, then remove it
+    on = {}
+    for p in bound:
+        on.setdefault(p["spec"]["nodeName"], []).append(p)
+    taken = {names[placed[i]] for i in range(k) if placed[i] >= 0 and i != deleted}
+    cand = [n for n in names[10:] if n not in taken]
+    victim = min(cand, key=lambda n: len(on.get(n, [])))
+    for p in on.get(victim, []):
+        ev.append({"op": "removePod", "name": p["metadata"]["name"], "namespace": p["metadata"].get("namespace", "default")})
+        bound.remove(p)
+    ev.append({"op": "removeNode", "name": victim})
+    nodes = [n for n in nodes if n["metadata"]["name"] != victim]
+    # the oracle's equivalent document
+    for i in range(k):
+        if placed[i] >= 0 and i != deleted:
+            p = copy.deepcopy(doc["queue"][i])
+            p["spec"]["nodeName"] = names[placed[i]]
+            bound.append(p)
+    eq = dict(doc)
+    eq["nodes"], eq["pods"] = nodes, bound
+    eq["queue"] = [_nowhere(i) for i in range(k)] + doc["queue"][k:]
+    return ev, eq
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
+def test_events_between_cycles(name, c, sizes):
+    doc = g.generate(c, **sizes)
+    n, k = len(doc["queue"]), len(doc["queue"]) // 2
+    s = Scheduler(doc["profile"])
+    s.load_cluster(dict(doc, queue=[]))
+    placed = []
+    for pod in doc["queue"][:k]:
+        _, r = s.cycle(pod, commit=True)
+        placed.append(r.selected if r.status == 0 else -1)
+    ev, eq = _events(doc, placed, k)
+    s.apply_events(ev)
+    assert s.n_nodes == len(eq["nodes"])
+    o = Oracle(eq)
+    o.schedule(record=3)
+    for i in range(k, n):
+        q, r = s.cycle(doc["queue"][i], commit=True)
+        assert q == i
+        assert (r.selected, r.feasible, r.status) == o.result(i), (name, i)
+        if i % 5 == 0:
+            a, b = s.annotations(q), o.annotations(i)
+            for key in b:
+                assert a.get(key) == b[key], (name, i, key)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
+def test_events_between_queue_runs(name, c, sizes):
+    """Queue mode (window path for cfg2/cfg3): schedule [0, k), events, schedule [k, n)."""
+    doc = g.generate(c, **sizes)
+    n, k = len(doc["queue"]), len(doc["queue"]) // 2
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    s.schedule(0, k)
+    placed = [r.selected if r.status == 0 else -1 for r in s.results(0, k)]
+    ev, eq = _events(doc, placed, k)
+    s.apply_events(ev)
+    o = Oracle(eq)
+    o.schedule(record=0)
+    s.schedule(k, n - k)
+    got = s.results(k, n - k)
+    for i in range(k, n):
+        r = got[i - k]
+        assert (r.selected, r.feasible, r.status) == o.result(i), (name, i)
+
+
+@pytest.mark.gpu
+def test_event_batch_is_all_or_nothing():
+    doc = g.generate(2, n_nodes=64, n_pods=40)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(dict(doc, queue=[]))
+    bad = [{"op": "addNode", "node": g.node_obj("node-8888888", 8000, 32 << 30)},
+           {"op": "removeNode", "name": "no-such-node"}]
+    with pytest.raises(Exception, match="removeNode"):
+        s.apply_events(bad)
+    assert s.n_nodes == 64
+    with pytest.raises(Exception, match="unknown node"):
+        s.apply_events([{"op": "addPod", "pod": g.filler_pod("p", "nowhere", 100, 1 << 20)}])
+    o = Oracle(doc)
+    o.schedule(record=0)
+    for i, pod in enumerate(doc["queue"]):
+        _, r = s.cycle(pod, commit=True)
+        assert (r.selected, r.feasible, r.status) == o.result(i)

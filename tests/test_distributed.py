@@ -117,3 +117,51 @@ def test_sharded_per_pod_chain_matches_oracle(cfg, world):
         for r in range(world):
             bad = [(q, out[r][q], want[q]) for q in range(len(want)) if out[r][q] != want[q]]
             assert not bad, f"rank {r}: {len(bad)} pods differ, first {bad[:4]}"
+
+
+def _sharded_events_worker(rank, world, port, doc_json, ev_json, k, out):
+    sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
+    dist = _init(rank, world, port)
+    import json
+    from ksg import Scheduler
+    doc = json.loads(doc_json)
+    s = Scheduler(doc["profile"], device=0, shard_rank=rank, shard_count=world)
+    s.set_exchange_host(world)
+    s.load_cluster(doc)
+    s.schedule(0, k)
+    s.apply_events(json.loads(ev_json))
+    n = s.queue_len
+    s.schedule(k, n - k)
+    out[rank] = [(r.selected, r.feasible, r.status) for r in s.results(k, n - k)]
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+# Cluster events (ksg_apply_events) on a node-sharded context: every rank applies
+# the same batch; adding/removing nodes moves the shard boundaries, so each rank
+# re-encodes a different node range afterwards.
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [2, 4])
+def test_sharded_events_match_oracle(cfg):
+    import json
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _oracle import Oracle
+    from ksg import generator as g
+    from test_events_gpu import _events
+    doc = g.generate(2, n_nodes=400, n_pods=200) if cfg == 2 else \
+        g.generate(4, n_nodes=200, n_existing=700, n_pods=80, n_zones=6)
+    n, k = len(doc["queue"]), len(doc["queue"]) // 2
+    o = Oracle(doc)
+    o.schedule(k, record=0)
+    placed = [o.result(q)[0] if o.result(q)[2] == 0 else -1 for q in range(k)]
+    ev, eq = _events(doc, placed, k)
+    o2 = Oracle(eq)
+    o2.schedule(record=0)
+    want = [o2.result(q) for q in range(k, n)]
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_sharded_events_worker, args=(2, port, json.dumps(doc), json.dumps(ev), k, out), nprocs=2, join=True)
+        for r in range(2):
+            bad = [(k + i, out[r][i], want[i]) for i in range(len(want)) if out[r][i] != want[i]]
+            assert not bad, f"rank {r}: {len(bad)} pods differ, first {bad[:4]}"

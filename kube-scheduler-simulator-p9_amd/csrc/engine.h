@@ -93,6 +93,11 @@ class Engine {
   bool append_program(const std::vector<uint8_t>& prog, std::string& err);
   // Reserve (sign +1) / Unreserve (sign -1) program q on global node gnode.
   bool assume(uint32_t q, int32_t gnode, int sign, std::string& err);
+  // Cluster event applied in place: bound pod `prog` (host-encoded like a queue
+  // program) added on (sign +1) / removed from (sign -1) global node gnode; row is
+  // its existing-pod table row (in: the row to tombstone on removal, out: the row
+  // appended on addition, -1 none).  Nodes outside this shard are ignored.
+  bool bound_delta(const std::vector<uint8_t>& prog, int32_t gnode, int sign, int32_t& row, std::string& err);
   bool set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err);
   // An assume found the existing-pod table full (the pod was not appended).
   bool table_overflow(bool& overflow, std::string& err);

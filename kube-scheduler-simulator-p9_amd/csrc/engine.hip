@@ -3347,6 +3347,8 @@ struct Engine::Impl {
   DBuf<ksg_exist_term> terms;
   DBuf<ksg_req> treq;
   uint32_t pcap = 0, pkeys = 0, tcap = 0, rcap = 0, vcap = 0;
+  DBuf<uint8_t> evprog;  // cluster events applied in place: the bound pod's program
+  DBuf<int32_t> evrow;   // its existing-pod table row
   // scratch
   DBuf<int32_t> cnt, hist_f, hist_s, ipa_aff, ipa_anti, ipa_exist, pts_min, pts_dom;
   DBuf<uint8_t> present_f, reg;
@@ -3994,6 +3996,21 @@ bool Engine::assume(uint32_t q, int32_t gnode, int sign, std::string& err) {
   hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, I.stream, C, I.progs.p + I.prog_off[q], gnode, sign,
                      (I.has_pts || I.has_ipa) ? 1 : 0, I.prow.p + q);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
+bool Engine::bound_delta(const std::vector<uint8_t>& prog, int32_t gnode, int sign, int32_t& row, std::string& err) {
+  Impl& I = *p_;
+  if (prog.size() < sizeof(ksg_prog)) { err = "bound_delta: program too small"; return false; }
+  if (!I.evprog.alloc(prog.size(), err) || !I.evrow.alloc(1, err)) return false;
+  HIPCHK(hipMemcpyAsync(I.evprog.p, prog.data(), prog.size(), hipMemcpyHostToDevice, I.stream));
+  HIPCHK(hipMemcpyAsync(I.evrow.p, &row, sizeof(row), hipMemcpyHostToDevice, I.stream));
+  DevCluster C = I.cluster();
+  hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, I.stream, C, I.evprog.p, gnode, sign,
+                     (I.has_pts || I.has_ipa) ? 1 : 0, I.evrow.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(&row, I.evrow.p, sizeof(row), hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipStreamSynchronize(I.stream));
   return true;
 }

@@ -487,6 +487,8 @@ struct Cluster {
   vector<Node> nodes;
   Dict node_names;
   vector<Pod> bound;
+  vector<int32_t> bound_row;  // per bound pod: its existing-pod table row on this shard's device (-1 none)
+  bool inplace_dirty = false;  // cluster events applied in place since the last encode
   vector<Pod> queue;
   // vocabularies
   Dict res;  // resource columns
@@ -785,7 +787,9 @@ struct Cluster {
     T.n_keys = (uint32_t)pkeys.names.size();
     vector<i64> rq;
     vector<vector<int32_t>> lab;
-    for (auto& p : bound) {
+    bound_row.assign(bound.size(), -1);
+    for (size_t bi = 0; bi < bound.size(); ++bi) {
+      const Pod& p = bound[bi];
       int32_t g = node_names.get(p.node);
       if (g < 0 || (uint32_t)g < lo || (uint32_t)g >= hi) continue;
       uint32_t i = (uint32_t)g - lo;
@@ -796,6 +800,7 @@ struct Cluster {
       S.nz_mem[i] += nzm;
       S.pod_count[i] += 1;
       for (auto& h : p.ports) S.port_count[(size_t)port_id[std::make_tuple(h.ip, h.proto, h.port)] * n + i] += 1;
+      bound_row[bi] = (int32_t)T.n;
       T.node.push_back((int32_t)i);
       T.ns.push_back(nss.get(p.ns));
       T.flags.push_back(exist_flags(p));
@@ -1272,6 +1277,7 @@ struct Cluster {
                      err))
       return false;
     compiled = false;
+    inplace_dirty = false;
     progs.clear();
     meta.clear();
     qmode.clear();
@@ -1389,7 +1395,9 @@ struct Cluster {
                        (uint32_t)(T.reqs.size() + qreqs + 8 * slack), (uint32_t)(T.vals.size() + qvals + 16 * slack), err);
     }
     bound.swap(saved);
+    bound_row.resize(bound.size());  // placements were encoded after the bound pods
     if (!ok) return false;
+    inplace_dirty = false;
     compiled = false;
     if (!compile_queue()) return false;
     if (ns && !eng->set_summaries(0, (uint32_t)ns, sum.data(), err)) return false;
@@ -1483,6 +1491,76 @@ struct Cluster {
     if (ns) *ns = md && (*md)["namespace"] ? str_of((*md)["namespace"]) : (e["namespace"] ? str_of(e["namespace"]) : "default");
     return md ? str_of((*md)["name"]) : str_of(e["name"]);
   }
+  // In-place path for batches of bound-pod additions / removals on known nodes
+  // that bring no new vocabulary: the device applies each as the assume delta
+  // (rows +- requests, host ports; existing-pod table append or tombstone), the
+  // same k_assume Reserve/Unreserve use, instead of a re-encode.  Returns 1
+  // applied, 0 not eligible (nothing changed), -1 error.
+  int inplace_events(const J& ev) {
+    struct Op { bool add; Pod pod; vector<uint8_t> blob; };
+    vector<Op> ops;
+    vector<std::pair<string, string>> names;  // bound pods after the batch, simulated
+    for (auto& p : bound) names.push_back({p.ns, p.name});
+    std::set<i64> prios;
+    if (has_preemption())
+      for (auto* v : {&bound, &queue})
+        for (auto& p : *v) prios.insert(p.priority);
+    for (auto& e : ev.items) {
+      const string op = str_of(e["op"]);
+      if (op == "addPod") {
+        if (!e["pod"]) return 0;
+        Pod p = parse_pod(*e["pod"]);
+        if (p.node.empty() || node_names.get(p.node) < 0 || vocab_grows(p)) return 0;
+        for (auto& x : names)
+          if (x.first == p.ns && x.second == p.name) return 0;
+        for (auto& q : queue)
+          if (q.ns == p.ns && q.name == p.name) return 0;
+        if (has_preemption()) {
+          prios.insert(p.priority);
+          if (prios.size() > 1) return 0;
+        }
+        names.push_back({p.ns, p.name});
+        ops.push_back({true, std::move(p), {}});
+      } else if (op == "removePod") {
+        string pns, name = obj_name(e, "pod", &pns);
+        auto it = std::find(names.begin(), names.end(), std::make_pair(pns, name));
+        if (it == names.end()) return 0;
+        names.erase(it);
+        Pod p;
+        p.ns = pns;
+        p.name = name;
+        ops.push_back({false, std::move(p), {}});
+      } else {
+        return 0;
+      }
+    }
+    for (auto& o : ops) {
+      if (!o.add) continue;
+      PodMeta m;
+      if (!compile(o.pod, 0, o.blob, m)) return -1;
+    }
+    for (auto& o : ops) {
+      if (o.add) {
+        int32_t row = -1;
+        if (!eng->bound_delta(o.blob, node_names.get(o.pod.node), +1, row, err)) return -1;
+        bound.push_back(std::move(o.pod));
+        bound_row.push_back(row);
+      } else {
+        size_t i = 0;
+        while (!(bound[i].ns == o.pod.ns && bound[i].name == o.pod.name)) ++i;
+        vector<uint8_t> blob;
+        PodMeta m;
+        if (!compile(bound[i], 0, blob, m)) return -1;
+        int32_t row = bound_row[i];
+        if (!eng->bound_delta(blob, node_names.get(bound[i].node), -1, row, err)) return -1;
+        bound.erase(bound.begin() + i);
+        bound_row.erase(bound_row.begin() + i);
+      }
+      inplace_dirty = true;
+    }
+    return check_table() ? 1 : -1;  // a full existing-pod table re-encodes from the mirror
+  }
+
   bool apply_events(const char* js, size_t len) {
     if (!compile_queue()) return false;
     try {
@@ -1493,6 +1571,11 @@ struct Cluster {
     }
     const J& d = *docs.back();
     const J* ev = d["events"] ? d["events"] : &d;
+    const J* re = d["reencode"];  // {"reencode": true}: skip the in-place path (A/B tests)
+    if (!(re && re->b)) {
+      int r = inplace_events(*ev);
+      if (r != 0) return r > 0;
+    }
     track_queue();
     const size_t ns = progs.size();
     vector<ksg_pod_summary> sum(ns);
@@ -1985,6 +2068,8 @@ int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len
 
 int ksg_reset(ksg_ctx* ctx) {
   if (!ctx) return KSG_E_INVALID;
+  if (ctx->c.inplace_dirty)
+    return ctx->fail("reset after in-place cluster events: reload the cluster (ksg_load_cluster)", KSG_E_STATE);
   if (!ctx->c.compile_queue()) return ctx->fail(ctx->c.err, KSG_E_INVALID);
   if (!ctx->c.eng->reset(ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
   return KSG_OK;

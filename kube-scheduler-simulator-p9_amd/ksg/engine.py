@@ -184,10 +184,11 @@ class Scheduler:
     def unreserve(self, q):
         self._chk(self.L.ksg_unreserve(self.h, q), "ksg_unreserve")
 
-    def apply_events(self, events):
+    def apply_events(self, events, reencode=False):
         """Scheduler-cache events (addNode/updateNode/removeNode/addPod/updatePod/
-        removePod dicts, see ksg.h) applied as one all-or-nothing batch."""
-        b = json.dumps({"events": list(events)}).encode()
+        removePod dicts, see ksg.h) applied as one all-or-nothing batch;
+        reencode=True skips the in-place path for bound-pod batches."""
+        b = json.dumps({"events": list(events), "reencode": bool(reencode)}).encode()
         self._chk(self.L.ksg_apply_events(self.h, b, len(b)), "ksg_apply_events")
 
     def sample_kernel(self, every):

@@ -151,3 +151,62 @@ def test_event_batch_is_all_or_nothing():
     for i, pod in enumerate(doc["queue"]):
         _, r = s.cycle(pod, commit=True)
         assert (r.selected, r.feasible, r.status) == o.result(i)
+
+
+def _pod_events(doc, placed, k):
+    """Bound-pod additions/removals only (the in-place path) + the oracle's document."""
+    names = [n["metadata"]["name"] for n in doc["nodes"]]
+    bound = copy.deepcopy(doc.get("pods", []))
+    ev = []
+    src = [p for p in bound[:40]] or [g.filler_pod("x", names[0], 300, 1 << 29)]
+    for j in range(12):  # copies of existing pods (labels, terms, ports) on other nodes
+        p = copy.deepcopy(src[j % len(src)])
+        p["metadata"]["name"] = f"evt-add-{j:03d}"
+        p["spec"]["nodeName"] = names[(7 * j + 3) % len(names)]
+        ev.append({"op": "addPod", "pod": p})
+        bound.append(p)
+    for p in list(bound[2:30:3]):  # snapshot pods and some of the pods just added
+        ev.append({"op": "removePod", "name": p["metadata"]["name"], "namespace": p["metadata"].get("namespace", "default")})
+        bound.remove(p)
+    late = next(p for p in bound if p["metadata"]["name"] == "evt-add-010")  # added by this same batch
+    ev.append({"op": "removePod", "name": "evt-add-010", "namespace": late["metadata"].get("namespace", "default")})
+    bound.remove(late)
+    for i in range(k):
+        if placed[i] >= 0:
+            p = copy.deepcopy(doc["queue"][i])
+            p["spec"]["nodeName"] = names[placed[i]]
+            bound.append(p)
+    eq = dict(doc)
+    eq["pods"] = bound
+    eq["queue"] = [_nowhere(i) for i in range(k)] + doc["queue"][k:]
+    return ev, eq
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("reencode", [False, True], ids=["inplace", "reencode"])
+@pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
+def test_bound_pod_events_in_place(name, c, sizes, reencode):
+    """Bound-pod batches go through the device assume delta (no re-encode); both
+    paths must agree with the oracle, in cycle mode and then in queue mode."""
+    doc = g.generate(c, **sizes)
+    n, k = len(doc["queue"]), len(doc["queue"]) // 2
+    s = Scheduler(doc["profile"])
+    s.load_cluster(dict(doc, queue=[]))
+    placed = []
+    for pod in doc["queue"][:k]:
+        _, r = s.cycle(pod, commit=True)
+        placed.append(r.selected if r.status == 0 else -1)
+    ev, eq = _pod_events(doc, placed, k)
+    s.apply_events(ev, reencode=reencode)
+    if not reencode and doc.get("pods"):  # the batch took the in-place path (no re-encode)
+        with pytest.raises(Exception, match="reset after in-place"):
+            s.reset()
+    o = Oracle(eq)
+    o.schedule(record=3)
+    for i in range(k, n):
+        q, r = s.cycle(doc["queue"][i], commit=True)
+        assert (r.selected, r.feasible, r.status) == o.result(i), (name, reencode, i)
+        if i % 5 == 0:
+            a, b = s.annotations(q), o.annotations(i)
+            for key in b:
+                assert a.get(key) == b[key], (name, i, key)

@@ -19,6 +19,7 @@
 #include <set>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/ksg.h"
@@ -489,6 +490,8 @@ struct Cluster {
   vector<Pod> bound;
   vector<int32_t> bound_row;  // per bound pod: its existing-pod table row on this shard's device (-1 none)
   bool inplace_dirty = false;  // cluster events applied in place since the last encode
+  std::unordered_map<string, uint32_t> bound_at;  // "ns\x1fname" -> index in bound (in-place events)
+  bool bound_at_valid = false;
   vector<Pod> queue;
   // vocabularies
   Dict res;  // resource columns
@@ -1278,6 +1281,7 @@ struct Cluster {
       return false;
     compiled = false;
     inplace_dirty = false;
+    bound_at_valid = false;
     progs.clear();
     meta.clear();
     qmode.clear();
@@ -1497,10 +1501,16 @@ struct Cluster {
   // same k_assume Reserve/Unreserve use, instead of a re-encode.  Returns 1
   // applied, 0 not eligible (nothing changed), -1 error.
   int inplace_events(const J& ev) {
-    struct Op { bool add; Pod pod; vector<uint8_t> blob; };
+    struct Op { bool add; Pod pod; vector<uint8_t> blob; string key; };
+    auto pkey = [](const string& ns, const string& name) { return ns + '\x1f' + name; };
+    if (!bound_at_valid) {
+      bound_at.clear();
+      for (size_t i = 0; i < bound.size(); ++i) bound_at[pkey(bound[i].ns, bound[i].name)] = (uint32_t)i;
+      bound_at_valid = true;
+    }
     vector<Op> ops;
-    vector<std::pair<string, string>> names;  // bound pods after the batch, simulated
-    for (auto& p : bound) names.push_back({p.ns, p.name});
+    std::unordered_set<string> added, removed;  // the batch on top of bound_at, simulated
+    auto present = [&](const string& k) { return added.count(k) || (bound_at.count(k) && !removed.count(k)); };
     std::set<i64> prios;
     if (has_preemption())
       for (auto* v : {&bound, &queue})
@@ -1511,25 +1521,23 @@ struct Cluster {
         if (!e["pod"]) return 0;
         Pod p = parse_pod(*e["pod"]);
         if (p.node.empty() || node_names.get(p.node) < 0 || vocab_grows(p)) return 0;
-        for (auto& x : names)
-          if (x.first == p.ns && x.second == p.name) return 0;
+        string k = pkey(p.ns, p.name);
+        if (present(k)) return 0;
         for (auto& q : queue)
           if (q.ns == p.ns && q.name == p.name) return 0;
         if (has_preemption()) {
           prios.insert(p.priority);
           if (prios.size() > 1) return 0;
         }
-        names.push_back({p.ns, p.name});
-        ops.push_back({true, std::move(p), {}});
+        added.insert(k);
+        removed.erase(k);
+        ops.push_back({true, std::move(p), {}, k});
       } else if (op == "removePod") {
         string pns, name = obj_name(e, "pod", &pns);
-        auto it = std::find(names.begin(), names.end(), std::make_pair(pns, name));
-        if (it == names.end()) return 0;
-        names.erase(it);
-        Pod p;
-        p.ns = pns;
-        p.name = name;
-        ops.push_back({false, std::move(p), {}});
+        string k = pkey(pns, name);
+        if (!present(k)) return 0;
+        if (!added.erase(k)) removed.insert(k);
+        ops.push_back({false, Pod(), {}, k});
       } else {
         return 0;
       }
@@ -1543,18 +1551,26 @@ struct Cluster {
       if (o.add) {
         int32_t row = -1;
         if (!eng->bound_delta(o.blob, node_names.get(o.pod.node), +1, row, err)) return -1;
+        bound_at[o.key] = (uint32_t)bound.size();
         bound.push_back(std::move(o.pod));
         bound_row.push_back(row);
       } else {
-        size_t i = 0;
-        while (!(bound[i].ns == o.pod.ns && bound[i].name == o.pod.name)) ++i;
+        const uint32_t i = bound_at.at(o.key);
         vector<uint8_t> blob;
         PodMeta m;
         if (!compile(bound[i], 0, blob, m)) return -1;
         int32_t row = bound_row[i];
         if (!eng->bound_delta(blob, node_names.get(bound[i].node), -1, row, err)) return -1;
-        bound.erase(bound.begin() + i);
-        bound_row.erase(bound_row.begin() + i);
+        // swap with the last pod (bound-pod order does not enter any plugin's result)
+        const uint32_t last = (uint32_t)bound.size() - 1;
+        if (i != last) {
+          std::swap(bound[i], bound[last]);
+          std::swap(bound_row[i], bound_row[last]);
+          bound_at[pkey(bound[i].ns, bound[i].name)] = i;
+        }
+        bound.pop_back();
+        bound_row.pop_back();
+        bound_at.erase(o.key);
       }
       inplace_dirty = true;
     }
@@ -1670,6 +1686,7 @@ struct Cluster {
     std::swap(bound, bb);
     std::swap(qmode, qm);
     std::swap(placed, pl);
+    bound_at_valid = false;
     if (!equal_priorities()) {
       std::swap(nodes, nn);
       std::swap(bound, bb);

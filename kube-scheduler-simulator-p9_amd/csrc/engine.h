@@ -98,6 +98,8 @@ class Engine {
   // its existing-pod table row (in: the row to tombstone on removal, out: the row
   // appended on addition, -1 none).  Nodes outside this shard are ignored.
   bool bound_delta(const std::vector<uint8_t>& prog, int32_t gnode, int sign, int32_t& row, std::string& err);
+  // Cluster event applied in place: node gnode's allocatable [R] and allowed pod count.
+  bool node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_t allowed, std::string& err);
   bool set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err);
   // An assume found the existing-pod table full (the pod was not appended).
   bool table_overflow(bool& overflow, std::string& err);

@@ -4015,6 +4015,18 @@ bool Engine::bound_delta(const std::vector<uint8_t>& prog, int32_t gnode, int si
   return true;
 }
 
+bool Engine::node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_t allowed, std::string& err) {
+  Impl& I = *p_;
+  if (gnode < 0 || (uint32_t)gnode < I.goff || (uint32_t)gnode - I.goff >= I.N) return true;  // another shard's node
+  if (alloc.size() != I.R) { err = "node_alloc: resource count"; return false; }
+  const uint32_t n = (uint32_t)gnode - I.goff;
+  for (uint32_t r = 0; r < I.R; ++r)
+    HIPCHK(hipMemcpyAsync(I.alloc.p + (size_t)r * I.N + n, &alloc[r], sizeof(int64_t), hipMemcpyHostToDevice, I.stream));
+  HIPCHK(hipMemcpyAsync(I.allowed.p + n, &allowed, sizeof(int32_t), hipMemcpyHostToDevice, I.stream));
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
 bool Engine::table_overflow(bool& overflow, std::string& err) {
   Impl& I = *p_;
   uint32_t f = 0;

@@ -1501,7 +1501,7 @@ struct Cluster {
   // same k_assume Reserve/Unreserve use, instead of a re-encode.  Returns 1
   // applied, 0 not eligible (nothing changed), -1 error.
   int inplace_events(const J& ev) {
-    struct Op { bool add; Pod pod; vector<uint8_t> blob; string key; };
+    struct Op { bool add; Pod pod; vector<uint8_t> blob; string key; int32_t node = -1; Node nd; };
     auto pkey = [](const string& ns, const string& name) { return ns + '\x1f' + name; };
     if (!bound_at_valid) {
       bound_at.clear();
@@ -1532,6 +1532,25 @@ struct Cluster {
         added.insert(k);
         removed.erase(k);
         ops.push_back({true, std::move(p), {}, k});
+      } else if (op == "updateNode") {  // allocatable-only updates (same labels, taints, images, flags)
+        if (!e["node"]) return 0;
+        Node x = parse_node(*e["node"]);
+        const int32_t at = node_names.get(x.name);
+        if (at < 0) return 0;
+        const Node& old = nodes[at];
+        if (x.labels != old.labels || x.unschedulable != old.unschedulable || x.images != old.images ||
+            x.taints.size() != old.taints.size())
+          return 0;
+        for (size_t t = 0; t < x.taints.size(); ++t)
+          if (x.taints[t].key != old.taints[t].key || x.taints[t].value != old.taints[t].value ||
+              x.taints[t].effect != old.taints[t].effect)
+            return 0;
+        for (auto& kv : x.alloc)
+          if (kv.first != "pods" && res.get(kv.first) < 0) return 0;
+        Op o{false, Pod(), {}, string()};
+        o.node = at;
+        o.nd = std::move(x);
+        ops.push_back(std::move(o));
       } else if (op == "removePod") {
         string pns, name = obj_name(e, "pod", &pns);
         string k = pkey(pns, name);
@@ -1548,7 +1567,17 @@ struct Cluster {
       if (!compile(o.pod, 0, o.blob, m)) return -1;
     }
     for (auto& o : ops) {
-      if (o.add) {
+      if (o.node >= 0) {
+        vector<int64_t> al(res.names.size(), 0);
+        int32_t allowed = 0;
+        for (auto& kv : o.nd.alloc) {  // as encode_snapshot
+          if (kv.first == "pods") allowed = (int32_t)as_value(kv.second);
+          int32_t r = res.get(kv.first);
+          if (r >= 0) al[r] = r == 0 ? as_milli(kv.second) : as_value(kv.second);
+        }
+        if (!eng->node_alloc(o.node, al, allowed, err)) return -1;
+        nodes[o.node] = std::move(o.nd);
+      } else if (o.add) {
         int32_t row = -1;
         if (!eng->bound_delta(o.blob, node_names.get(o.pod.node), +1, row, err)) return -1;
         bound_at[o.key] = (uint32_t)bound.size();

@@ -154,10 +154,17 @@ def test_event_batch_is_all_or_nothing():
 
 
 def _pod_events(doc, placed, k):
-    """Bound-pod additions/removals only (the in-place path) + the oracle's document."""
+    """Bound-pod additions/removals and allocatable-only node updates (the in-place
+    path) + the oracle's document."""
     names = [n["metadata"]["name"] for n in doc["nodes"]]
+    nodes = copy.deepcopy(doc["nodes"])
     bound = copy.deepcopy(doc.get("pods", []))
     ev = []
+    for j, (cpu, pods) in ((1, ("48", "60")), (4, ("3", "110")), (1, ("40", "50"))):
+        x = copy.deepcopy(nodes[j])
+        x["status"]["allocatable"]["cpu"], x["status"]["allocatable"]["pods"] = cpu, pods
+        ev.append({"op": "updateNode", "node": x})
+        nodes[j] = x
     src = [p for p in bound[:40]] or [g.filler_pod("x", names[0], 300, 1 << 29)]
     for j in range(12):  # copies of existing pods (labels, terms, ports) on other nodes
         p = copy.deepcopy(src[j % len(src)])
@@ -177,7 +184,7 @@ def _pod_events(doc, placed, k):
             p["spec"]["nodeName"] = names[placed[i]]
             bound.append(p)
     eq = dict(doc)
-    eq["pods"] = bound
+    eq["nodes"], eq["pods"] = nodes, bound
     eq["queue"] = [_nowhere(i) for i in range(k)] + doc["queue"][k:]
     return ev, eq
 
@@ -199,6 +206,7 @@ def test_bound_pod_events_in_place(name, c, sizes, reencode):
     ev, eq = _pod_events(doc, placed, k)
     s.apply_events(ev, reencode=reencode)
     if not reencode and doc.get("pods"):  # the batch took the in-place path (no re-encode)
+        assert s.n_nodes == len(doc["nodes"])
         with pytest.raises(Exception, match="reset after in-place"):
             s.reset()
     o = Oracle(eq)

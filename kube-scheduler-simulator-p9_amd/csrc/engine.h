@@ -93,11 +93,15 @@ class Engine {
   bool append_program(const std::vector<uint8_t>& prog, std::string& err);
   // Reserve (sign +1) / Unreserve (sign -1) program q on global node gnode.
   bool assume(uint32_t q, int32_t gnode, int sign, std::string& err);
-  // Cluster event applied in place: bound pod `prog` (host-encoded like a queue
-  // program) added on (sign +1) / removed from (sign -1) global node gnode; row is
-  // its existing-pod table row (in: the row to tombstone on removal, out: the row
-  // appended on addition, -1 none).  Nodes outside this shard are ignored.
-  bool bound_delta(const std::vector<uint8_t>& prog, int32_t gnode, int sign, int32_t& row, std::string& err);
+  // Cluster events applied in place, one k_assume per op in stream order, one sync:
+  // bound pod progs[i] added on (sign +1) / removed from (sign -1) global node
+  // gnode[i] (nodes outside this shard are ignored).  rows[] holds one existing-pod
+  // table row slot per op (in: the row a removal tombstones; out: the row an
+  // addition appended, -1 none); op i reads/writes slot[i] (a removal of a pod
+  // added by the same batch uses that addition's slot).
+  bool bound_deltas(const std::vector<std::vector<uint8_t>>& progs, const std::vector<int32_t>& gnode,
+                    const std::vector<int32_t>& sign, const std::vector<int32_t>& slot, std::vector<int32_t>& rows,
+                    std::string& err);
   // Cluster event applied in place: node gnode's allocatable [R] and allowed pod count.
   bool node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_t allowed, std::string& err);
   bool set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err);

@@ -4000,17 +4000,31 @@ bool Engine::assume(uint32_t q, int32_t gnode, int sign, std::string& err) {
   return true;
 }
 
-bool Engine::bound_delta(const std::vector<uint8_t>& prog, int32_t gnode, int sign, int32_t& row, std::string& err) {
+bool Engine::bound_deltas(const std::vector<std::vector<uint8_t>>& progs, const std::vector<int32_t>& gnode,
+                          const std::vector<int32_t>& sign, const std::vector<int32_t>& slot, std::vector<int32_t>& rows,
+                          std::string& err) {
   Impl& I = *p_;
-  if (prog.size() < sizeof(ksg_prog)) { err = "bound_delta: program too small"; return false; }
-  if (!I.evprog.alloc(prog.size(), err) || !I.evrow.alloc(1, err)) return false;
-  HIPCHK(hipMemcpyAsync(I.evprog.p, prog.data(), prog.size(), hipMemcpyHostToDevice, I.stream));
-  HIPCHK(hipMemcpyAsync(I.evrow.p, &row, sizeof(row), hipMemcpyHostToDevice, I.stream));
+  const size_t n = progs.size();
+  if (gnode.size() != n || sign.size() != n || slot.size() != n || rows.size() != n) { err = "bound_deltas: sizes"; return false; }
+  if (!n) return true;
+  std::vector<size_t> off(n);
+  std::vector<uint8_t> blob;
+  for (size_t i = 0; i < n; ++i) {
+    if (progs[i].size() < sizeof(ksg_prog) || slot[i] < 0 || (size_t)slot[i] >= n) { err = "bound_deltas: program/slot"; return false; }
+    off[i] = (blob.size() + 255) & ~(size_t)255;
+    blob.resize(off[i]);
+    blob.insert(blob.end(), progs[i].begin(), progs[i].end());
+  }
+  if (!I.evprog.alloc(blob.size(), err) || !I.evrow.alloc(n, err)) return false;
+  HIPCHK(hipMemcpyAsync(I.evprog.p, blob.data(), blob.size(), hipMemcpyHostToDevice, I.stream));
+  HIPCHK(hipMemcpyAsync(I.evrow.p, rows.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, I.stream));
   DevCluster C = I.cluster();
-  hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, I.stream, C, I.evprog.p, gnode, sign,
-                     (I.has_pts || I.has_ipa) ? 1 : 0, I.evrow.p);
+  const int table = (I.has_pts || I.has_ipa) ? 1 : 0;
+  for (size_t i = 0; i < n; ++i)  // stream order: a removal sees the row its same-batch addition wrote
+    hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, I.stream, C, I.evprog.p + off[i], gnode[i], sign[i], table,
+                       I.evrow.p + slot[i]);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(&row, I.evrow.p, sizeof(row), hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipMemcpyAsync(rows.data(), I.evrow.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipStreamSynchronize(I.stream));
   return true;
 }

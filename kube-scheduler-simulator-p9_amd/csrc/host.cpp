@@ -1566,6 +1566,10 @@ struct Cluster {
       PodMeta m;
       if (!compile(o.pod, 0, o.blob, m)) return -1;
     }
+    vector<vector<uint8_t>> blobs;
+    vector<int32_t> gn, sg, slot, rows;
+    vector<std::pair<string, size_t>> adds;      // key, op slot of additions
+    std::unordered_map<string, int32_t> add_slot;  // additions of this batch still present
     for (auto& o : ops) {
       if (o.node >= 0) {
         vector<int64_t> al(res.names.size(), 0);
@@ -1578,18 +1582,30 @@ struct Cluster {
         if (!eng->node_alloc(o.node, al, allowed, err)) return -1;
         nodes[o.node] = std::move(o.nd);
       } else if (o.add) {
-        int32_t row = -1;
-        if (!eng->bound_delta(o.blob, node_names.get(o.pod.node), +1, row, err)) return -1;
+        const int32_t k = (int32_t)blobs.size();
+        gn.push_back(node_names.get(o.pod.node));
+        sg.push_back(+1);
+        slot.push_back(k);
+        rows.push_back(-1);
+        blobs.push_back(std::move(o.blob));
+        add_slot[o.key] = k;
+        adds.push_back({o.key, (size_t)k});
         bound_at[o.key] = (uint32_t)bound.size();
         bound.push_back(std::move(o.pod));
-        bound_row.push_back(row);
+        bound_row.push_back(-1);  // known after the launches
       } else {
         const uint32_t i = bound_at.at(o.key);
         vector<uint8_t> blob;
         PodMeta m;
         if (!compile(bound[i], 0, blob, m)) return -1;
-        int32_t row = bound_row[i];
-        if (!eng->bound_delta(blob, node_names.get(bound[i].node), -1, row, err)) return -1;
+        const int32_t k = (int32_t)blobs.size();
+        auto it = add_slot.find(o.key);
+        gn.push_back(node_names.get(bound[i].node));
+        sg.push_back(-1);
+        slot.push_back(it != add_slot.end() ? it->second : k);
+        rows.push_back(bound_row[i]);
+        blobs.push_back(std::move(blob));
+        if (it != add_slot.end()) add_slot.erase(it);
         // swap with the last pod (bound-pod order does not enter any plugin's result)
         const uint32_t last = (uint32_t)bound.size() - 1;
         if (i != last) {
@@ -1603,6 +1619,9 @@ struct Cluster {
       }
       inplace_dirty = true;
     }
+    if (!eng->bound_deltas(blobs, gn, sg, slot, rows, err)) return -1;
+    for (auto& a : adds)
+      if (add_slot.count(a.first)) bound_row[bound_at.at(a.first)] = rows[a.second];
     return check_table() ? 1 : -1;  // a full existing-pod table re-encodes from the mirror
   }
 

@@ -218,3 +218,78 @@ def test_bound_pod_events_in_place(name, c, sizes, reencode):
             a, b = s.annotations(q), o.annotations(i)
             for key in b:
                 assert a.get(key) == b[key], (name, i, key)
+
+
+def _random_batch(rng, nodes, bound, placed_names, tag):
+    """A random mix of events over the python mirror (nodes, bound, placements)."""
+    ev = []
+    for _ in range(rng.randint(1, 6)):
+        kind = rng.choice(["addPod", "removePod", "allocNode", "relabelNode", "addNode"])
+        if kind == "addPod" and bound:
+            p = copy.deepcopy(rng.choice(bound))
+            p["metadata"]["name"] = f"rnd-{tag}-{len(ev)}-{rng.randint(0, 10**6)}"
+            p["spec"]["nodeName"] = rng.choice(nodes)["metadata"]["name"]
+            ev.append({"op": "addPod", "pod": p})
+            bound.append(p)
+        elif kind == "removePod" and len(bound) > 2:
+            p = rng.choice(bound)
+            ev.append({"op": "removePod", "name": p["metadata"]["name"],
+                       "namespace": p["metadata"].get("namespace", "default")})
+            bound.remove(p)
+        elif kind == "allocNode":
+            j = rng.randrange(len(nodes))
+            x = copy.deepcopy(nodes[j])
+            x["status"]["allocatable"]["cpu"] = str(rng.choice([4, 8, 32, 96]))
+            ev.append({"op": "updateNode", "node": x})
+            nodes[j] = x
+        elif kind == "relabelNode":
+            j = rng.randrange(len(nodes))
+            x = copy.deepcopy(nodes[j])
+            x["metadata"]["labels"][f"rnd-{rng.randint(0, 3)}"] = f"v{rng.randint(0, 2)}"
+            ev.append({"op": "updateNode", "node": x})
+            nodes[j] = x
+        elif kind == "addNode":
+            x = copy.deepcopy(rng.choice(nodes))
+            nm = f"node-{9000000 + rng.randint(0, 999999):07d}"
+            if any(n["metadata"]["name"] == nm for n in nodes):
+                continue
+            x["metadata"]["name"] = nm
+            x["metadata"]["labels"]["kubernetes.io/hostname"] = nm
+            ev.append({"op": "addNode", "node": x})
+            nodes.append(x)
+    return ev
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
+def test_random_event_rounds(name, c, sizes):
+    """Eight rounds of (cycles, random event batch: in-place or re-encoded); after
+    every batch the next round's pods match the oracle on the equivalent fresh
+    cluster."""
+    import random
+    rng = random.Random(20250131 + c)
+    doc = g.generate(c, **sizes)
+    n = len(doc["queue"])
+    s = Scheduler(doc["profile"])
+    s.load_cluster(dict(doc, queue=[]))
+    nodes = copy.deepcopy(doc["nodes"])
+    bound = copy.deepcopy(doc.get("pods", [])) or [g.filler_pod("seed-pod", nodes[0]["metadata"]["name"], 100, 1 << 28)]
+    if not doc.get("pods"):
+        s.apply_events([{"op": "addPod", "pod": bound[0]}])
+    R = 8
+    cuts = [n * j // R for j in range(R + 1)]
+    for rnd in range(R):
+        eq = dict(doc)
+        eq["nodes"], eq["pods"] = nodes, list(bound)
+        eq["queue"] = [_nowhere(i) for i in range(cuts[rnd])] + doc["queue"][cuts[rnd]:]
+        o = Oracle(eq)
+        o.schedule(cuts[rnd + 1], record=0)
+        for i in range(cuts[rnd], cuts[rnd + 1]):
+            q, r = s.cycle(doc["queue"][i], commit=True)
+            assert (r.selected, r.feasible, r.status) == o.result(i), (name, rnd, i)
+            if r.status == 0:  # from now on a bound pod of the mirror
+                p = copy.deepcopy(doc["queue"][i])
+                p["spec"]["nodeName"] = nodes[r.selected]["metadata"]["name"]
+                bound.append(p)
+        s.apply_events(_random_batch(rng, nodes, bound, None, rnd))
+        assert s.n_nodes == len(nodes)

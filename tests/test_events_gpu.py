@@ -220,7 +220,7 @@ def test_bound_pod_events_in_place(name, c, sizes, reencode):
                 assert a.get(key) == b[key], (name, i, key)
 
 
-def _random_batch(rng, nodes, bound, placed_names, tag):
+def _random_batch(rng, nodes, bound, tag):
     """A random mix of events over the python mirror (nodes, bound, placements)."""
     ev = []
     for _ in range(rng.randint(1, 6)):
@@ -291,5 +291,5 @@ def test_random_event_rounds(name, c, sizes):
                 p = copy.deepcopy(doc["queue"][i])
                 p["spec"]["nodeName"] = nodes[r.selected]["metadata"]["name"]
                 bound.append(p)
-        s.apply_events(_random_batch(rng, nodes, bound, None, rnd))
+        s.apply_events(_random_batch(rng, nodes, bound, rnd))
         assert s.n_nodes == len(nodes)

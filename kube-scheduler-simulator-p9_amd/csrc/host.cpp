@@ -1529,9 +1529,12 @@ struct Cluster {
           prios.insert(p.priority);
           if (prios.size() > 1) return 0;
         }
+        Op o{true, std::move(p), {}, k};
+        PodMeta m;
+        if (!compile(o.pod, 0, o.blob, m)) return 0;  // the re-encode path takes it
         added.insert(k);
         removed.erase(k);
-        ops.push_back({true, std::move(p), {}, k});
+        ops.push_back(std::move(o));
       } else if (op == "updateNode") {  // allocatable-only updates (same labels, taints, images, flags)
         if (!e["node"]) return 0;
         Node x = parse_node(*e["node"]);
@@ -1555,16 +1558,19 @@ struct Cluster {
         string pns, name = obj_name(e, "pod", &pns);
         string k = pkey(pns, name);
         if (!present(k)) return 0;
+        Op o{false, Pod(), {}, k};
+        if (added.count(k)) {  // added by this batch: the addition's program
+          for (size_t j = ops.size(); j-- > 0;)
+            if (ops[j].add && ops[j].key == k) { o.blob = ops[j].blob; break; }
+        } else {
+          PodMeta m;
+          if (!compile(bound[bound_at.at(k)], 0, o.blob, m)) return 0;  // the re-encode path takes it
+        }
         if (!added.erase(k)) removed.insert(k);
-        ops.push_back({false, Pod(), {}, k});
+        ops.push_back(std::move(o));
       } else {
         return 0;
       }
-    }
-    for (auto& o : ops) {
-      if (!o.add) continue;
-      PodMeta m;
-      if (!compile(o.pod, 0, o.blob, m)) return -1;
     }
     vector<vector<uint8_t>> blobs;
     vector<int32_t> gn, sg, slot, rows;
@@ -1595,16 +1601,13 @@ struct Cluster {
         bound_row.push_back(-1);  // known after the launches
       } else {
         const uint32_t i = bound_at.at(o.key);
-        vector<uint8_t> blob;
-        PodMeta m;
-        if (!compile(bound[i], 0, blob, m)) return -1;
         const int32_t k = (int32_t)blobs.size();
         auto it = add_slot.find(o.key);
         gn.push_back(node_names.get(bound[i].node));
         sg.push_back(-1);
         slot.push_back(it != add_slot.end() ? it->second : k);
         rows.push_back(bound_row[i]);
-        blobs.push_back(std::move(blob));
+        blobs.push_back(std::move(o.blob));
         if (it != add_slot.end()) add_slot.erase(it);
         // swap with the last pod (bound-pod order does not enter any plugin's result)
         const uint32_t last = (uint32_t)bound.size() - 1;

@@ -177,8 +177,9 @@ int ksg_unreserve(ksg_ctx* ctx, uint32_t q);
  * applied in order; the batch is all-or-nothing.  removePod also takes a queue
  * pod that was scheduled (its placement is released, its result kept);
  * removeNode requires that no pod is bound or assumed on the node (upstream
- * deletes the node's pods first).  Batches of bound-pod add/remove events and
- * allocatable-only node updates that bring no new vocabulary are applied in
+ * deletes the node's pods first).  Batches of bound-pod add/remove events,
+ * deletions of queue pods scheduled since the last encode, and allocatable-only
+ * node updates that bring no new vocabulary are applied in
  * place on the device; any other batch re-encodes the snapshot (after an in-place
  * batch ksg_reset is refused: reload).  Placements of scheduled queue pods are kept;
  * node indices after a removed node shift down by one.  Per-node outputs kept for

@@ -1501,8 +1501,9 @@ struct Cluster {
   // same k_assume Reserve/Unreserve use, instead of a re-encode.  Returns 1
   // applied, 0 not eligible (nothing changed), -1 error.
   int inplace_events(const J& ev) {
-    struct Op { bool add; Pod pod; vector<uint8_t> blob; string key; int32_t node = -1; Node nd; };
+    struct Op { bool add; Pod pod; vector<uint8_t> blob; string key; int32_t node = -1; Node nd; int32_t qpod = -1, qat = -1; };
     auto pkey = [](const string& ns, const string& name) { return ns + '\x1f' + name; };
+    track_queue();
     if (!bound_at_valid) {
       bound_at.clear();
       for (size_t i = 0; i < bound.size(); ++i) bound_at[pkey(bound[i].ns, bound[i].name)] = (uint32_t)i;
@@ -1510,6 +1511,7 @@ struct Cluster {
     }
     vector<Op> ops;
     std::unordered_set<string> added, removed;  // the batch on top of bound_at, simulated
+    std::set<int32_t> gone_q;                    // scheduled queue pods the batch deletes
     auto present = [&](const string& k) { return added.count(k) || (bound_at.count(k) && !removed.count(k)); };
     std::set<i64> prios;
     if (has_preemption())
@@ -1557,7 +1559,23 @@ struct Cluster {
       } else if (op == "removePod") {
         string pns, name = obj_name(e, "pod", &pns);
         string k = pkey(pns, name);
-        if (!present(k)) return 0;
+        if (!present(k)) {
+          // a queue pod this context scheduled (assumed since the last encode): Unreserve's delta
+          int32_t q = -1;
+          for (size_t j = 0; j < queue.size() && q < 0; ++j)
+            if (queue[j].ns == pns && queue[j].name == name) q = (int32_t)j;
+          if (q < 0 || gone_q.count(q) || (size_t)q >= qmode.size() || assumed_in[q] != epoch) return 0;
+          ksg_pod_summary sm;
+          if (qmode[q] == 1 && !eng->summaries((uint32_t)q, 1, &sm, err)) return -1;
+          const int32_t at = placement((uint32_t)q, qmode[q] == 1 ? &sm : nullptr);
+          if (at < 0) return 0;
+          gone_q.insert(q);
+          Op o{false, Pod(), {}, k};
+          o.qpod = q;
+          o.qat = at;
+          ops.push_back(std::move(o));
+          continue;
+        }
         Op o{false, Pod(), {}, k};
         if (added.count(k)) {  // added by this batch: the addition's program
           for (size_t j = ops.size(); j-- > 0;)
@@ -1577,7 +1595,11 @@ struct Cluster {
     vector<std::pair<string, size_t>> adds;      // key, op slot of additions
     std::unordered_map<string, int32_t> add_slot;  // additions of this batch still present
     for (auto& o : ops) {
-      if (o.node >= 0) {
+      if (o.qpod >= 0) {  // row deltas commute with the batch's bound-pod deltas launched below
+        if (!eng->assume((uint32_t)o.qpod, o.qat, -1, err)) return -1;
+        qmode[o.qpod] = 2;  // deleted after it was scheduled: its result stays, its placement goes
+        placed[o.qpod] = -1;
+      } else if (o.node >= 0) {
         vector<int64_t> al(res.names.size(), 0);
         int32_t allowed = 0;
         for (auto& kv : o.nd.alloc) {  // as encode_snapshot

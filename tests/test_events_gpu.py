@@ -178,8 +178,12 @@ def _pod_events(doc, placed, k):
     late = next(p for p in bound if p["metadata"]["name"] == "evt-add-010")  # added by this same batch
     ev.append({"op": "removePod", "name": "evt-add-010", "namespace": late["metadata"].get("namespace", "default")})
     bound.remove(late)
+    # a queue pod scheduled in the first half is deleted (Unreserve's delta in place)
+    deleted = next((i for i in range(k) if placed[i] >= 0), None)
+    if deleted is not None:
+        ev.append({"op": "removePod", "name": doc["queue"][deleted]["metadata"]["name"], "namespace": "default"})
     for i in range(k):
-        if placed[i] >= 0:
+        if placed[i] >= 0 and i != deleted:
             p = copy.deepcopy(doc["queue"][i])
             p["spec"]["nodeName"] = names[placed[i]]
             bound.append(p)

@@ -188,6 +188,16 @@ int ksg_apply_events(ksg_ctx* ctx, const char* events_json, size_t len);
 
 /* Device node rows (assume parity): requested [n_res][n], pod count [n]. */
 int ksg_node_requested(ksg_ctx* ctx, int64_t* requested, int32_t* pod_count, uint32_t n_res, uint32_t n);
+/* NonZeroRequested rows (Fit scoring input): cpu in nonzero[0..n), memory in nonzero[n..2n). */
+int ksg_node_nonzero(ksg_ctx* ctx, int64_t* nonzero, uint32_t n);
+
+/* Harness mode (benchmarks, full-size tests; no context): the synthetic cluster
+ * document of BASELINE.json config 2..5 — the document
+ * ksg/generator.py builds, from the same seeded draws.  Sizes < 0: the config's
+ * default; seed 0: the config's seed.  *out is malloc'd: release with ksg_free. */
+int ksg_synth_cluster(int config, int64_t n_nodes, int64_t n_pods, int64_t n_existing, int64_t n_zones, uint64_t seed,
+                      char** out, size_t* len);
+void ksg_free(void* p);
 
 #ifdef __cplusplus
 }

@@ -4,4 +4,4 @@ set -e
 cd "$(dirname "$0")"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 $HIPCC --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \
-  -Wno-unused-result -o libksg.so csrc/engine.hip csrc/host.cpp -L/opt/rocm/lib -lrccl "$@"
+  -Wno-unused-result -o libksg.so csrc/engine.hip csrc/host.cpp csrc/synth.cpp -L/opt/rocm/lib -lrccl "$@"

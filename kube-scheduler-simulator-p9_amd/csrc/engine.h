@@ -107,6 +107,8 @@ class Engine {
   bool set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err);
   // An assume found the existing-pod table full (the pod was not appended).
   bool table_overflow(bool& overflow, std::string& err);
+  // Existing-pod table entries in use and capacity: rows, terms, reqs, vals.
+  bool table_room(uint32_t used[4], uint32_t cap[4], std::string& err);
   // Run pods [first, first+count) of the program list back to back on the device
   // (device-side assume).  keep: store per-pair outputs for pods [keep_first, keep_first+keep_n).
   bool run_queue(uint32_t first, uint32_t count, bool commit, std::string& err);
@@ -140,6 +142,8 @@ class Engine {
   bool kernel_time(float& avg_ms, uint32_t& samples, std::string& err);
   // Read back the node resource rows (parity tests of the assume delta).
   bool read_requested(std::vector<int64_t>& requested, std::vector<int32_t>& pod_count, std::string& err);
+  // NonZeroRequested cpu / memory rows [2][n] (Fit scoring input).
+  bool read_nonzero(std::vector<int64_t>& nz, std::string& err);
   uint32_t n_nodes() const;
   void* stream() const;
   // timing of the last run_queue (device events), ms

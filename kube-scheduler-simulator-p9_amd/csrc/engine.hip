@@ -4052,6 +4052,16 @@ bool Engine::table_overflow(bool& overflow, std::string& err) {
   return true;
 }
 
+bool Engine::table_room(uint32_t used[4], uint32_t cap[4], std::string& err) {
+  Impl& I = *p_;
+  for (int i = 0; i < 4; ++i) used[i] = 0;
+  cap[0] = I.pcap; cap[1] = I.tcap; cap[2] = I.rcap; cap[3] = I.vcap;
+  if (!I.tcounts.p) return true;
+  HIPCHK(hipMemcpyAsync(used, I.tcounts.p, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
 bool Engine::set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err) {
   Impl& I = *p_;
   if (first + count > I.prog_off.size()) { err = "program index out of range"; return false; }
@@ -4294,6 +4304,15 @@ bool Engine::read_requested(std::vector<int64_t>& requested, std::vector<int32_t
   pod_count.resize(I.N);
   HIPCHK(hipMemcpyAsync(requested.data(), I.req.p, requested.size() * 8, hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipMemcpyAsync(pod_count.data(), I.podcnt.p, pod_count.size() * 4, hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
+bool Engine::read_nonzero(std::vector<int64_t>& nz, std::string& err) {
+  Impl& I = *p_;
+  nz.resize((size_t)2 * I.N);
+  HIPCHK(hipMemcpyAsync(nz.data(), I.nzc.p, (size_t)I.N * 8, hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipMemcpyAsync(nz.data() + I.N, I.nzm.p, (size_t)I.N * 8, hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipStreamSynchronize(I.stream));
   return true;
 }

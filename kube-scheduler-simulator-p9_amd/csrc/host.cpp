@@ -11,6 +11,7 @@
 // up to the first failure, score = raw, finalscore = normalized x store weight
 // (raw x weight for plugins without ScoreExtensions), selected node on Reserve.
 #include <algorithm>
+#include <array>
 #include <cctype>
 #include <cstdio>
 #include <cstring>
@@ -511,6 +512,7 @@ struct Cluster {
   bool compiled = false;
   uint32_t keep_first = 0, keep_n = 0;
   string err;
+  bool broken = false;  // a device error left the snapshot half-updated: refuse calls until reload
 
   // ------------------------------------------------------------ profile
   bool load_profile(const J& pr) {
@@ -1254,6 +1256,9 @@ struct Cluster {
       }
     if (qd)
       for (auto& p : qd->items) queue.push_back(parse_pod(p));
+    index_queue();
+    qneed.clear();
+    broken = false;
     if (has_volume_plugins)
       for (auto& p : queue)
         if (p.volume_plugins_act) { err = "pod " + p.name + ": volumes the volume plugins act on are not modelled"; return false; }
@@ -1323,6 +1328,53 @@ struct Cluster {
     placed.resize(queue.size(), -1);
     assumed_in.resize(queue.size(), 0);
   }
+  // (namespace, name) -> queue index, for the events' name lookups
+  std::unordered_map<string, uint32_t> queue_idx;
+  static string pod_key(const string& ns, const string& name) { return ns + '\x1f' + name; }
+  void index_queue() {
+    queue_idx.clear();
+    for (size_t q = 0; q < queue.size(); ++q) queue_idx[pod_key(queue[q].ns, queue[q].name)] = (uint32_t)q;
+  }
+  int32_t queue_find(const string& ns, const string& name) const {
+    auto it = queue_idx.find(pod_key(ns, name));
+    return it == queue_idx.end() ? -1 : (int32_t)it->second;
+  }
+  // Existing-pod table entries one assume of p appends (rows, terms, reqs, vals;
+  // engine assume_pod), cached per queue pod.
+  bool tables_on() const { return pos_of(P_PTS) >= 0 || pos_of(P_IPA) >= 0; }
+  void table_need(const Pod& p, uint64_t need[4]) {
+    vector<ksg_exist_term> et;
+    vector<ksg_req> rq;
+    vector<int32_t> vl, tp;
+    append_terms(p, 0, et, tp, rq, vl);
+    need[0] += 1;
+    need[1] += et.size();
+    need[2] += rq.size();
+    need[3] += vl.size();
+  }
+  vector<std::array<uint32_t, 4>> qneed;
+  void queue_need(uint32_t q, uint64_t need[4]) {
+    if (qneed.size() < queue.size()) {
+      size_t q0 = qneed.size();
+      qneed.resize(queue.size());
+      for (size_t j = q0; j < queue.size(); ++j) {
+        uint64_t n[4] = {0, 0, 0, 0};
+        table_need(queue[j], n);
+        for (int i = 0; i < 4; ++i) qneed[j][i] = (uint32_t)n[i];
+      }
+    }
+    for (int i = 0; i < 4; ++i) need[i] += qneed[q][i];
+  }
+  // Does the device existing-pod table have room for `need` more entries?
+  bool table_fits(const uint64_t need[4], bool& fits) {
+    uint32_t used[4], cap[4];
+    if (!eng->table_room(used, cap, err)) return false;
+    fits = true;
+    for (int i = 0; i < 4; ++i) fits &= (uint64_t)used[i] + need[i] <= cap[i];
+    return true;
+  }
+  // Queue pods that may still be assumed: not run, or cycle pods without a placement.
+  bool may_assume(uint32_t q) const { return qmode[q] == 0 || (qmode[q] == 2 && placed[q] < 0); }
   void mark_run(uint32_t first, uint32_t count) {
     track_queue();
     for (uint32_t q = first; q < first + count; ++q) {
@@ -1431,6 +1483,7 @@ struct Cluster {
     }
     track_queue();
     uint32_t q = (uint32_t)queue.size() - 1;
+    queue_idx[pod_key(queue[q].ns, queue[q].name)] = q;
     qmode[q] = 2;
     if (vocab_grows(queue[q])) {
       if (!rebuild()) return false;
@@ -1525,8 +1578,7 @@ struct Cluster {
         if (p.node.empty() || node_names.get(p.node) < 0 || vocab_grows(p)) return 0;
         string k = pkey(p.ns, p.name);
         if (present(k)) return 0;
-        for (auto& q : queue)
-          if (q.ns == p.ns && q.name == p.name) return 0;
+        if (queue_find(p.ns, p.name) >= 0) return 0;
         if (has_preemption()) {
           prios.insert(p.priority);
           if (prios.size() > 1) return 0;
@@ -1561,9 +1613,7 @@ struct Cluster {
         string k = pkey(pns, name);
         if (!present(k)) {
           // a queue pod this context scheduled (assumed since the last encode): Unreserve's delta
-          int32_t q = -1;
-          for (size_t j = 0; j < queue.size() && q < 0; ++j)
-            if (queue[j].ns == pns && queue[j].name == name) q = (int32_t)j;
+          const int32_t q = queue_find(pns, name);
           if (q < 0 || gone_q.count(q) || (size_t)q >= qmode.size() || assumed_in[q] != epoch) return 0;
           ksg_pod_summary sm;
           if (qmode[q] == 1 && !eng->summaries((uint32_t)q, 1, &sm, err)) return -1;
@@ -1590,13 +1640,31 @@ struct Cluster {
         return 0;
       }
     }
+    // Room in the device existing-pod table (PTS/IPA profiles append every assumed
+    // pod): the batch's additions plus every queue pod that may still be assumed
+    // must fit, else the re-encode path takes the batch (fresh capacity, no tombstones).
+    if (tables_on()) {
+      uint64_t need[4] = {0, 0, 0, 0};
+      for (auto& o : ops)
+        if (o.add) table_need(o.pod, need);
+      for (uint32_t q = 0; q < queue.size(); ++q)
+        if (may_assume(q) && !gone_q.count((int32_t)q)) queue_need(q, need);
+      bool fits = false;
+      if (!table_fits(need, fits)) return -1;
+      if (!fits) return 0;
+    }
+    // Host mirror first; device writes after (bound-pod deltas, then the queue
+    // pods' Unreserve deltas and allocatable updates: row deltas commute).  A
+    // device error part-way leaves the context unusable (broken): reload.
     vector<vector<uint8_t>> blobs;
     vector<int32_t> gn, sg, slot, rows;
     vector<std::pair<string, size_t>> adds;      // key, op slot of additions
     std::unordered_map<string, int32_t> add_slot;  // additions of this batch still present
+    vector<std::pair<int32_t, int32_t>> unres;     // queue pod, node
+    vector<std::tuple<int32_t, vector<int64_t>, int32_t>> allocs;  // node, allocatable, allowed pods
     for (auto& o : ops) {
-      if (o.qpod >= 0) {  // row deltas commute with the batch's bound-pod deltas launched below
-        if (!eng->assume((uint32_t)o.qpod, o.qat, -1, err)) return -1;
+      if (o.qpod >= 0) {
+        unres.push_back({o.qpod, o.qat});
         qmode[o.qpod] = 2;  // deleted after it was scheduled: its result stays, its placement goes
         placed[o.qpod] = -1;
       } else if (o.node >= 0) {
@@ -1607,7 +1675,7 @@ struct Cluster {
           int32_t r = res.get(kv.first);
           if (r >= 0) al[r] = r == 0 ? as_milli(kv.second) : as_value(kv.second);
         }
-        if (!eng->node_alloc(o.node, al, allowed, err)) return -1;
+        allocs.emplace_back(o.node, std::move(al), allowed);
         nodes[o.node] = std::move(o.nd);
       } else if (o.add) {
         const int32_t k = (int32_t)blobs.size();
@@ -1644,7 +1712,14 @@ struct Cluster {
       }
       inplace_dirty = true;
     }
-    if (!eng->bound_deltas(blobs, gn, sg, slot, rows, err)) return -1;
+    bool ok = eng->bound_deltas(blobs, gn, sg, slot, rows, err);
+    for (size_t i = 0; ok && i < unres.size(); ++i) ok = eng->assume((uint32_t)unres[i].first, unres[i].second, -1, err);
+    for (size_t i = 0; ok && i < allocs.size(); ++i)
+      ok = eng->node_alloc(std::get<0>(allocs[i]), std::get<1>(allocs[i]), std::get<2>(allocs[i]), err);
+    if (!ok) {
+      broken = true;
+      return -1;
+    }
     for (auto& a : adds)
       if (add_slot.count(a.first)) bound_row[bound_at.at(a.first)] = rows[a.second];
     return check_table() ? 1 : -1;  // a full existing-pod table re-encodes from the mirror
@@ -2019,6 +2094,14 @@ struct ksg_ctx {
   }
 };
 
+// A context whose device state a failed in-place update left half-applied
+// refuses every call but ksg_load_cluster / ksg_destroy / ksg_last_error.
+#define KSG_GUARD(ctx)                                                                                   \
+  do {                                                                                                   \
+    if (!(ctx)) return KSG_E_INVALID;                                                                    \
+    if ((ctx)->c.broken) return (ctx)->fail("context unusable after a device error: reload", KSG_E_STATE); \
+  } while (0)
+
 extern "C" {
 
 int ksg_abi_version(void) { return KSG_ABI_VERSION; }
@@ -2068,25 +2151,32 @@ int ksg_num_nodes(const ksg_ctx* ctx) { return ctx ? (int)ctx->c.nodes.size() : 
 int ksg_queue_len(const ksg_ctx* ctx) { return ctx ? (int)ctx->c.queue.size() : KSG_E_INVALID; }
 
 int ksg_keep_outputs(ksg_ctx* ctx, uint32_t first, uint32_t count) {
-  if (!ctx) return KSG_E_INVALID;
+  KSG_GUARD(ctx);
   if (!ctx->c.eng->keep_outputs(first, count, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
   return KSG_OK;
 }
 
 int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
-  if (!ctx) return KSG_E_INVALID;
+  KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
   if (c.shards != 1 && c.eng->exchange_ranks() != c.shards)
     return ctx->fail("sharded context: call ksg_set_exchange first", KSG_E_STATE);
   if (!c.compile_queue()) return ctx->fail(c.err, KSG_E_INVALID);
+  if (c.tables_on()) {  // the run appends every scheduled pod to the existing-pod table
+    uint64_t need[4] = {0, 0, 0, 0};
+    for (uint32_t q = first; q < first + count; ++q) c.queue_need(q, need);
+    bool fits = false;
+    if (!c.table_fits(need, fits)) return ctx->fail(c.err, KSG_E_DEVICE);
+    if (!fits && !c.rebuild()) return ctx->fail(c.err, KSG_E_DEVICE);  // fresh capacity, placements kept
+  }
   if (!c.eng->run_queue(first, count, true, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
   c.mark_run(first, count);
   return KSG_OK;
 }
 
 int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count) {
-  if (!ctx) return KSG_E_INVALID;
+  KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
   if (c.shards != 1 && c.eng->exchange_ranks() != c.shards)
@@ -2098,13 +2188,22 @@ int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count) {
 }
 
 int ksg_wait(ksg_ctx* ctx, float* ms) {
-  if (!ctx) return KSG_E_INVALID;
+  KSG_GUARD(ctx);
   if (!ctx->c.eng->sync(ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
   if (ms) *ms = ctx->c.eng->last_ms();
+  if (ctx->c.tables_on()) {  // capacity is checked before every run; an overflow is a bug, not a state
+    bool full = false;
+    if (!ctx->c.eng->table_overflow(full, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
+    if (full) {
+      ctx->c.broken = true;
+      return ctx->fail("existing-pod table overflow: results of this run are not valid; reload", KSG_E_STATE);
+    }
+  }
   return KSG_OK;
 }
 
 int ksg_pod_results(ksg_ctx* ctx, uint32_t first, uint32_t count, ksg_pod_result* out) {
+  KSG_GUARD(ctx);
   if (!ctx || !out) return KSG_E_INVALID;
   Cluster& c = ctx->c;
   if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
@@ -2122,6 +2221,7 @@ int ksg_pod_results(ksg_ctx* ctx, uint32_t first, uint32_t count, ksg_pod_result
 }
 
 int ksg_filter_codes(ksg_ctx* ctx, uint32_t q, uint32_t* out, uint32_t n) {
+  KSG_GUARD(ctx);
   if (!ctx || !out) return KSG_E_INVALID;
   ksg::PodOutputs o;
   if (!ctx->c.eng->outputs(q, o, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_STATE);
@@ -2134,6 +2234,7 @@ int ksg_filter_codes(ksg_ctx* ctx, uint32_t q, uint32_t* out, uint32_t n) {
 }
 
 int ksg_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* out, uint32_t n) {
+  KSG_GUARD(ctx);
   if (!ctx || !out) return KSG_E_INVALID;
   ksg::PodOutputs o;
   if (!ctx->c.eng->outputs(q, o, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_STATE);
@@ -2146,6 +2247,7 @@ int ksg_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* out, uint32_t n)
 }
 
 int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len) {
+  KSG_GUARD(ctx);
   if (!ctx || !len) return KSG_E_INVALID;
   std::string s;
   if (q >= ctx->c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
@@ -2157,7 +2259,7 @@ int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len
 }
 
 int ksg_reset(ksg_ctx* ctx) {
-  if (!ctx) return KSG_E_INVALID;
+  KSG_GUARD(ctx);
   if (ctx->c.inplace_dirty)
     return ctx->fail("reset after in-place cluster events: reload the cluster (ksg_load_cluster)", KSG_E_STATE);
   if (!ctx->c.compile_queue()) return ctx->fail(ctx->c.err, KSG_E_INVALID);
@@ -2202,7 +2304,7 @@ int ksg_nccl_unique_id(uint8_t* out128) {
 }
 
 int ksg_set_exchange(ksg_ctx* ctx, int mode, const uint8_t* nccl_id, ksg_exchange_fn fn, void* user) {
-  if (!ctx) return KSG_E_INVALID;
+  KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (!c.eng->set_exchange(mode, nccl_id, c.rank, c.shards, fn, user, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
   return KSG_OK;
@@ -2217,6 +2319,7 @@ int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples) {
 }
 
 int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_pod_result* out) {
+  KSG_GUARD(ctx);
   if (!ctx || !pod_json) return KSG_E_INVALID;
   ksg_pod_summary s;
   try {
@@ -2236,18 +2339,19 @@ int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_po
 }
 
 int ksg_reserve(ksg_ctx* ctx, uint32_t q, int32_t node) {
-  if (!ctx) return KSG_E_INVALID;
+  KSG_GUARD(ctx);
   if (!ctx->c.reserve(q, node)) return ctx->fail(ctx->c.err, KSG_E_STATE);
   return KSG_OK;
 }
 
 int ksg_unreserve(ksg_ctx* ctx, uint32_t q) {
-  if (!ctx) return KSG_E_INVALID;
+  KSG_GUARD(ctx);
   if (!ctx->c.unreserve(q)) return ctx->fail(ctx->c.err, KSG_E_STATE);
   return KSG_OK;
 }
 
 int ksg_apply_events(ksg_ctx* ctx, const char* events_json, size_t len) {
+  KSG_GUARD(ctx);
   if (!ctx || !events_json) return KSG_E_INVALID;
   try {
     if (!ctx->c.apply_events(events_json, len)) return ctx->fail(ctx->c.err, KSG_E_STATE);
@@ -2258,7 +2362,7 @@ int ksg_apply_events(ksg_ctx* ctx, const char* events_json, size_t len) {
 }
 
 int ksg_node_requested(ksg_ctx* ctx, int64_t* requested, int32_t* pod_count, uint32_t n_res, uint32_t n) {
-  if (!ctx) return KSG_E_INVALID;
+  KSG_GUARD(ctx);
   std::vector<int64_t> r;
   std::vector<int32_t> pc;
   if (!ctx->c.eng->read_requested(r, pc, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
@@ -2267,6 +2371,20 @@ int ksg_node_requested(ksg_ctx* ctx, int64_t* requested, int32_t* pod_count, uin
   for (uint32_t k = 0; k < R; ++k)
     for (uint32_t i = 0; i < N; ++i) requested[(size_t)k * n + i] = r[(size_t)k * N + i];
   for (uint32_t i = 0; i < N; ++i) pod_count[i] = pc[i];
+  return KSG_OK;
+}
+
+int ksg_node_nonzero(ksg_ctx* ctx, int64_t* nonzero, uint32_t n) {
+  KSG_GUARD(ctx);
+  if (!nonzero) return KSG_E_INVALID;
+  std::vector<int64_t> nz;
+  if (!ctx->c.eng->read_nonzero(nz, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
+  const uint32_t N = (uint32_t)(nz.size() / 2);
+  if (n < N) return KSG_E_NOBUF;
+  for (uint32_t i = 0; i < N; ++i) {
+    nonzero[i] = nz[i];
+    nonzero[(size_t)n + i] = nz[(size_t)N + i];
+  }
   return KSG_OK;
 }
 

@@ -74,6 +74,11 @@ def load_library():
     L.ksg_reserve.argtypes = [vp, u32, i32]
     L.ksg_unreserve.argtypes = [vp, u32]
     L.ksg_apply_events.argtypes = [vp, ctypes.c_char_p, sz]
+    i64 = ctypes.c_int64
+    L.ksg_node_nonzero.argtypes = [vp, ctypes.POINTER(i64), u32]
+    L.ksg_synth_cluster.argtypes = [ctypes.c_int, i64, i64, i64, i64, ctypes.c_uint64, ctypes.POINTER(vp),
+                                    ctypes.POINTER(sz)]
+    L.ksg_free.argtypes = [vp]
     _lib = L
     return L
 
@@ -222,3 +227,10 @@ class Scheduler:
         pc = (ctypes.c_int32 * n)()
         self._chk(self.L.ksg_node_requested(self.h, req, pc, n_res, n), "ksg_node_requested")
         return [list(req[r * n:(r + 1) * n]) for r in range(n_res)], list(pc)
+
+    def node_nonzero(self):
+        """NonZeroRequested (cpu milli, memory bytes) rows of every local node."""
+        n = self.n_nodes
+        nz = (ctypes.c_int64 * (2 * n))()
+        self._chk(self.L.ksg_node_nonzero(self.h, nz, n), "ksg_node_nonzero")
+        return list(nz[:n]), list(nz[n:])

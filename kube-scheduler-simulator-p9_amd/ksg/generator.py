@@ -490,3 +490,20 @@ def generate(c: int, **sizes) -> dict:
 
 def dumps(doc) -> str:
     return json.dumps(doc, separators=(",", ":"), sort_keys=False)
+
+
+def generate_native(c: int, n_nodes=-1, n_pods=-1, n_existing=-1, n_zones=-1, seed=0) -> bytes:
+    """The same document as generate(c, ...) as JSON bytes, built by the native twin
+    (libksg.so ksg_synth_cluster, csrc/synth.cpp): configs 2..5 at full size in
+    seconds.  tests/test_synth.py checks the two agree."""
+    import ctypes
+    from .engine import load_library
+    L = load_library()
+    out, n = ctypes.c_void_p(), ctypes.c_size_t()
+    rc = L.ksg_synth_cluster(c, n_nodes, n_pods, n_existing, n_zones, seed, ctypes.byref(out), ctypes.byref(n))
+    if rc != 0:
+        raise ValueError(f"ksg_synth_cluster({c}) failed ({rc})")
+    try:
+        return ctypes.string_at(out, n.value)
+    finally:
+        L.ksg_free(out)

@@ -51,8 +51,22 @@ def empty_maps_example():
             "queue": [g.pod_obj("big", [g.req(4000, 2 * g.Gi)])]}
 
 
+def plugin_extender_example():
+    """simulator/docs/plugin-extender.md:85-107: the same {100m, 16Gi} pod, default
+    profile; node-282x7 already hosts one {100m, 16Gi} pod.  Documented results:
+    node-282x7 Fit 47 / BalancedAllocation 52, node-gp9t4 Fit 73 / BA 76,
+    TaintToleration finalscore 300 on both, selected-node node-gp9t4.  (Its
+    PodTopologySpread "200" and all-"passed" filter map predate v1.27's PreFilter
+    Skip, SURVEY.md §8(c): not asserted.)"""
+    prof = g.make_profile(g.DEFAULT_PROFILE, 1)
+    return {"profile": prof,
+            "nodes": [g.node_obj("node-282x7", 4000, 32 * g.Gi), g.node_obj("node-gp9t4", 4000, 32 * g.Gi)],
+            "pods": [g.pod_obj("pod-running", [g.req(100, 16 * g.Gi)], node="node-282x7")],
+            "queue": [g.pod_obj("pod-8ldq5", [g.req(100, 16 * g.Gi)])]}
+
+
 KNOWN = {"readme_example": readme_example, "store_weight_example": store_weight_example,
-         "empty_maps_example": empty_maps_example}
+         "empty_maps_example": empty_maps_example, "plugin_extender_example": plugin_extender_example}
 FAMILIES = {
     "cfg1_small": (1, dict(n_nodes=12, n_pods=24)),
     "cfg2_small": (2, dict(n_nodes=30, n_pods=30)),

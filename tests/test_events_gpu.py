@@ -297,3 +297,29 @@ def test_random_event_rounds(name, c, sizes):
                 bound.append(p)
         s.apply_events(_random_batch(rng, nodes, bound, rnd))
         assert s.n_nodes == len(nodes)
+
+
+@pytest.mark.gpu
+def test_inplace_adds_beyond_table_slack_then_queue():
+    """bound-pod additions that use up the existing-pod table's
+    slack before the queue runs.  The device table must still hold every queue
+    pod the run assumes (the in-place path checks the room it needs, else the
+    batch is re-encoded), so PTS/IPA results after the batch match the oracle."""
+    doc = g.generate(4, n_nodes=120, n_existing=400, n_pods=80, n_zones=6)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    names = [n["metadata"]["name"] for n in doc["nodes"]]
+    bound = copy.deepcopy(doc["pods"])
+    ev = []
+    for j in range(1400):  # > the 1,024 rows of slack beyond the loaded pods + queue
+        p = copy.deepcopy(doc["pods"][j % len(doc["pods"])])
+        p["metadata"]["name"] = f"slack-{j:05d}"
+        p["spec"]["nodeName"] = names[(11 * j + 5) % len(names)]
+        ev.append({"op": "addPod", "pod": p})
+        bound.append(p)
+    s.apply_events(ev)
+    s.schedule()
+    o = Oracle(dict(doc, pods=bound))
+    o.schedule(record=0)
+    got = [(r.selected, r.feasible, r.status) for r in s.results()]
+    assert got == [o.result(q) for q in range(len(got))]

@@ -40,6 +40,24 @@ def test_readme_known_answer():
     assert a[ANN + "selected-node"] in ("node-282x7", "node-gp9t4")
 
 
+def test_plugin_extender_known_answer():
+    """plugin-extender.md:85-107: node-282x7 (already hosting a {100m, 16Gi} pod) scores
+    Fit 47 / BalancedAllocation 52, node-gp9t4 73 / 76, TaintToleration 300 on both,
+    and node-gp9t4 is selected — Requested / NonZeroRequested after an assume, BA on a
+    loaded node."""
+    o = run(fixture("plugin_extender_example")["cluster"])
+    a = o.annotations(0)
+    fin = json.loads(a[ANN + "finalscore-result"])
+    raw = json.loads(a[ANN + "score-result"])
+    want = {"node-282x7": ("47", "52"), "node-gp9t4": ("73", "76")}
+    for node, (fit, ba) in want.items():
+        assert raw[node]["NodeResourcesFit"] == fin[node]["NodeResourcesFit"] == fit
+        assert raw[node]["NodeResourcesBalancedAllocation"] == fin[node]["NodeResourcesBalancedAllocation"] == ba
+        assert fin[node]["TaintToleration"] == "300"
+    assert a[ANN + "selected-node"] == "node-gp9t4"
+    assert o.result(0)[0] == 1
+
+
 def test_store_weight_semantics():
     """store_test.go:284-446 finalscore = score x weight (10 x 2 = "20"); plugins.go:289-304 weight 0 -> 1."""
     a = run(fixture("store_weight_example")["cluster"]).annotations(0)

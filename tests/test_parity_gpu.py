@@ -55,9 +55,34 @@ def test_assume_delta_matches_oracle_requests():
     doc = g.generate(2, n_nodes=64, n_pods=200)
     o, s = run_both(doc, keep=False)
     req, pc = s.node_requested()
-    # independent recomputation from the oracle's placements: Σ requests per node
-    placed = [o.result(q)[0] for q in range(o.n_queue)]
-    assert sum(pc) == len(doc["pods"]) + sum(1 for p in placed if p >= 0)
+    nzc, nzm = s.node_nonzero()
+    # independent recomputation from the oracle's placements: per node, the bound
+    # pods' and the placed queue pods' Requested and NonZeroRequested (missing
+    # container requests count 100m / 200Mi) and the pod count (NodeInfo.AddPod)
+    names = [n["metadata"]["name"] for n in doc["nodes"]]
+    N = len(names)
+    want = {"cpu": [0] * N, "mem": [0] * N, "nzc": [0] * N, "nzm": [0] * N, "pods": [0] * N}
+
+    def add(pod, i):
+        for c in pod["spec"]["containers"]:
+            r = c.get("resources", {}).get("requests", {})
+            cpu = int(r["cpu"][:-1]) if "cpu" in r else None
+            m = r.get("memory")
+            mem = None if m is None else (int(m[:-2]) * g.Mi if m.endswith("Mi") else int(m))
+            want["cpu"][i] += cpu or 0
+            want["mem"][i] += mem or 0
+            want["nzc"][i] += 100 if cpu is None else cpu
+            want["nzm"][i] += 200 * g.Mi if mem is None else mem
+        want["pods"][i] += 1
+
+    for p in doc["pods"]:
+        add(p, names.index(p["spec"]["nodeName"]))
+    for q in range(o.n_queue):
+        if o.result(q)[0] >= 0:
+            add(doc["queue"][q], o.result(q)[0])
+    assert req[0][:N] == want["cpu"] and req[1][:N] == want["mem"]
+    assert nzc == want["nzc"] and nzm == want["nzm"]
+    assert pc == want["pods"]
 
 
 @pytest.mark.gpu
@@ -77,6 +102,26 @@ def test_known_answer_readme_example():
         assert fin[node]["NodeResourcesFit"] == "73"
         assert fin[node]["NodeResourcesBalancedAllocation"] == "76"
         assert fin[node]["TaintToleration"] == "300"
+
+
+@pytest.mark.gpu
+def test_known_answer_plugin_extender_example():
+    """plugin-extender.md:85-107: Fit 47 / BA 52 on the loaded node-282x7, 73 / 76 on
+    node-gp9t4, TaintToleration 300, node-gp9t4 selected (default profile)."""
+    import json
+    d = _json.load(open(_os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "golden",
+                                      "plugin_extender_example.json")))
+    s = Scheduler(d["cluster"]["profile"])
+    s.load_cluster(d["cluster"])
+    s.keep_outputs(0, 1)
+    s.schedule()
+    a = s.annotations(0)
+    fin = json.loads(a["kube-scheduler-simulator.sigs.k8s.io/finalscore-result"])
+    for node, (fit, ba) in {"node-282x7": ("47", "52"), "node-gp9t4": ("73", "76")}.items():
+        assert (fin[node]["NodeResourcesFit"], fin[node]["NodeResourcesBalancedAllocation"]) == (fit, ba)
+        assert fin[node]["TaintToleration"] == "300"
+    assert a["kube-scheduler-simulator.sigs.k8s.io/selected-node"] == "node-gp9t4"
+    assert s.results()[0].selected == 1
 
 
 def _tight_cluster(n_nodes=24, n_pods=700, seed=7):

@@ -90,6 +90,8 @@ typedef struct ksg_aterm {
   int32_t ns_cnt;    // namespaces (ids) in the program's value pool
   int32_t ns_off;
   int32_t weight;    // preferred terms
+  int32_t cls;       // pod class of the pods the term matches (class tables; -1 matches none)
+  int32_t pad;
 } ksg_aterm;
 
 typedef struct ksg_tsc {
@@ -103,6 +105,9 @@ typedef struct ksg_tsc {
   int32_t self_match;    // selector matches the incoming pod's own labels
   int32_t is_hostname;
   int32_t first_of_key;  // first score constraint with this key (topoSize owner)
+  int32_t cls;           // pod class counted (class tables; -1: the selector counts nothing)
+  int32_t eff_cls;       // filter: class of the LAST filter constraint on this key (its count fills the pair)
+  int32_t sc_n, sc_off;  // score: classes whose counts share this constraint's pair (pool_i32)
   int32_t pad;
 } ksg_tsc;
 
@@ -116,8 +121,29 @@ typedef struct ksg_exist_term {
   int32_t ns_all;
   int32_t ns_cnt;
   int32_t ns_off;    // into the table's value pool
-  int32_t pad;
+  int32_t cls;       // term class (class tables), -1 none
 } ksg_exist_term;
+
+// ---- class tables (PodTopologySpread / InterPodAffinity counts kept by the assume delta)
+// A pod class is a conjunction of (namespaces, label selector) terms, optionally
+// skipping terminating pods (PodTopologySpread's countPodsMatchSelector); per
+// class the device keeps, per node, the matching existing pods, per (topology
+// key, value) of keys whose values span several nodes their sum, and per key the
+// pods on nodes carrying the key.  A term class groups existing pods' affinity
+// terms (kind group, topology key, namespaces, selector): per (key, value) the
+// terms there (anti / required) or their signed weights (preferred).
+#define KSG_TC_HARD 0     // existing pods' required affinity terms (hardPodAffinityWeight)
+#define KSG_TC_ANTI 1     // required anti-affinity (existing anti-affinity filter)
+#define KSG_TC_PREF 2     // preferred affinity (+w) / anti-affinity (-w)
+typedef struct ksg_cterm {
+  ksg_sel sel;       // pod-label space, class pools
+  int32_t ns_all, ns_cnt, ns_off, pad;
+} ksg_cterm;
+typedef struct ksg_pclass {
+  int32_t n_terms, term_off;
+  int32_t excl_term;  // terminating pods never match
+  int32_t pad;
+} ksg_pclass;
 
 // Pod program: everything the kernels need about one incoming pod.  The
 // program is a flat blob: this header followed by pools addressed by offsets
@@ -176,6 +202,12 @@ typedef struct ksg_prog {
   int32_t n_exist_terms;
   int32_t exist_terms_off;  // pool_eterm (sel/ns offsets relative to this program's pools)
 
+  // ---- class tables
+  uint32_t tab;             // KTAB_*: PodTopologySpread / InterPodAffinity read the class tables
+  int32_t aff_cls;          // required pod affinity: class of the pods matching every term (-1 none)
+  int32_t n_pc_match, pc_match_off;  // pool_i32: pod classes this pod belongs to (its assume: +-1)
+  int32_t n_tc_match, tc_match_off;  // pool_i32: term classes whose terms match this pod
+
   // ---- pools (byte offsets from the start of the blob)
   uint32_t off_i32, n_i32;
   uint32_t off_u32, n_u32;
@@ -203,6 +235,12 @@ typedef struct ksg_prog {
 #define KPF_PREFILTER_ERROR (1u << 12)   // PreFilter error status: cycle aborts
 #define KPF_TOL_UNSCHED (1u << 13)       // tolerates node.kubernetes.io/unschedulable:NoSchedule
 #define KPF_SKIP_PORTS (1u << 14)        // NodePorts PreFilter Skip (no host ports)
+
+// KTAB_* (ksg_prog.tab)
+#define KTAB_ON (1u << 0)        // the pod runs the table chain (k_eval / k_final / k_select)
+#define KTAB_PTS_MULTI (1u << 1) // several score constraints: PodTopologySpread raw scores need their own pass
+#define KSG_TAB_MAXV 1024        // table chain: values of a filter key reduced per block (minMatchNum)
+#define KSG_TAB_REGV 64          // table chain: values of a score key registered in a 64-bit mask
 
 // KEF_* existing-pod flags
 #define KEF_TERMINATING (1u << 0)

@@ -14,6 +14,8 @@ Clusters come from the native generator twin (ksg_synth_cluster; tests/test_synt
 pins it to the Python generator).
 """
 import json
+import os
+import time
 
 import pytest
 
@@ -23,17 +25,29 @@ from ksg import Scheduler, generator as g
 WORKERS = 16  # oracle parallelize.Until workers (the box's CPU share)
 
 
+def _progress(msg):
+    """Long steps report to $KSG_PROGRESS (a file the GPU runner watches for liveness)."""
+    p = os.environ.get("KSG_PROGRESS")
+    if p:
+        with open(p, "a") as f:
+            f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
+
+
 @pytest.mark.gpu
+@pytest.mark.timeout(420)
 def test_cfg4_full_size_matches_oracle():
     n_pods, keep0, nkeep = 300, 120, 10
     blob = g.generate_native(4, n_nodes=50000, n_existing=200000, n_pods=n_pods, n_zones=20)
     prof = json.loads(blob[:blob.index(b',"nodes"')] + b"}")["profile"]
     s = Scheduler(prof)
+    _progress("cfg4 generated")
     s.load_cluster(blob)
+    _progress("cfg4 loaded")
     assert s.n_nodes == 50000
     s.keep_outputs(keep0, nkeep)
     s.schedule()
     res = s.results()
+    _progress("cfg4 scheduled on the GPU")
     o = Oracle(blob)
     o.schedule(keep0, workers=WORKERS, record=0)
     o.schedule(nkeep, workers=WORKERS, record=3)
@@ -49,24 +63,30 @@ def test_cfg4_full_size_matches_oracle():
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(420)
 def test_cfg5_full_size_whatif_step_matches_oracle():
     step, sample = 4096, 64
     blob = g.generate_native(5, n_nodes=1_000_000, n_pods=step)
     prof = json.loads(blob[:blob.index(b',"nodes"')] + b"}")["profile"]
     s = Scheduler(prof)
+    _progress("cfg5 generated")
     s.load_cluster(blob)
+    _progress("cfg5 loaded")
     assert s.n_nodes == 1_000_000
     s.keep_outputs(0, 1)
     s.whatif(0, step)
     res = s.results(0, step)
     assert sum(1 for r in res if r.status == 0) > step // 2
+    _progress("cfg5 what-if step done")
     o = Oracle(blob)
+    _progress("cfg5 oracle loaded")
     o.whatif(sample, workers=WORKERS, record=0)
     got = [(r.selected, r.feasible, r.status) for r in res[:sample]]
     assert got == [o.result(q) for q in range(sample)]
     del o
     o1 = Oracle(blob)  # pod 0 rendered: its result in a one-pod step equals its result in the 4,096-pod step
     o1.whatif(1, workers=WORKERS, record=3)
+    _progress("cfg5 oracle pod 0 rendered")
     a, b = s.annotations(0), o1.annotations(0)
     for k in b:
         assert a.get(k) == b[k], k

@@ -58,6 +58,23 @@ struct NodeSoA {
   std::vector<uint32_t> topo_base, topo_count;
   std::vector<uint8_t> topo_unique;  // per slot: every value of the key sits on one node (whole cluster)
   uint32_t topo_pairs = 0;
+  // class tables: per slot the base of its values among the pairs of keys whose
+  // values span nodes (UINT32_MAX for one-node keys) and its values present on
+  // some node of this shard; per pair whether some node of this shard carries it
+  std::vector<uint32_t> nu_base;
+  uint32_t nu_pairs = 0;
+  std::vector<int32_t> slot_dom;
+  std::vector<uint8_t> pair_node;
+};
+
+// Class definitions appended to the device (host.cpp registry; ksg_types.h
+// "class tables").  Offsets are relative to this upload's own pools.
+struct ClassUpload {
+  std::vector<ksg_pclass> pc;    // new pod classes (term_off into ct)
+  std::vector<ksg_cterm> ct;     // their terms (sel.req_off into creq, ns_off into cval)
+  std::vector<ksg_req> creq;     // selector requirements (val_off into cval)
+  std::vector<int32_t> cval;
+  std::vector<int32_t> tc_slot;  // new term classes: their topology slot
 };
 
 // Existing pods (bound) on this shard's nodes, and their (anti)affinity terms.
@@ -109,6 +126,16 @@ class Engine {
   bool table_overflow(bool& overflow, std::string& err);
   // Existing-pod table entries in use and capacity: rows, terms, reqs, vals.
   bool table_room(uint32_t used[4], uint32_t cap[4], std::string& err);
+  // Class tables: append pod / term classes and build their tables from the
+  // existing-pod table; counts of classes with tables; rebuild every table.
+  bool add_classes(const ClassUpload& u, std::string& err);
+  uint32_t pod_classes() const;
+  uint32_t term_classes() const;
+  bool rebuild_class_tables(std::string& err);
+  // Replace program q (its class lists grew); summaries and placements stay.
+  bool replace_program(uint32_t q, const std::vector<uint8_t>& prog, std::string& err);
+  // Normalized scores of a kept pod, [n_plugins][n] (device NormalizeScore).
+  bool normalized(uint32_t prog_idx, std::vector<int32_t>& norm, std::string& err);
   // Run pods [first, first+count) of the program list back to back on the device
   // (device-side assume).  keep: store per-pair outputs for pods [keep_first, keep_first+keep_n).
   bool run_queue(uint32_t first, uint32_t count, bool commit, std::string& err);

@@ -50,6 +50,30 @@ namespace ksg {
 static constexpr int kBlock = 256;
 
 // ----------------------------------------------------------------- kernel args
+// Class tables (ksg_types.h "class tables"): PodTopologySpread / InterPodAffinity
+// counts kept up to date by every assume delta instead of rescanning the
+// existing pods per incoming pod.
+struct DevTables {
+  int on;                    // profile with PodTopologySpread / InterPodAffinity: assumes update the tables
+  uint32_t npc, ntc;         // pod classes / term classes with tables
+  uint32_t NU;               // (key, value) pairs of the keys whose values span several nodes
+  uint32_t uniq;             // topology slots whose every value sits on one node (pair == node)
+  int32_t* pc_cnt;           // [npc][N] matching existing pods per node
+  int32_t* pc_dom;           // [npc][NU] ... per (key, value) of the shared keys
+  int32_t* pc_tot;           // [npc][KSG_MAX_TOPO] ... on nodes carrying the key
+  const uint32_t* nu_base;   // [KSG_MAX_TOPO] slot base in NU space
+  const int32_t* slot_dom;   // [KSG_MAX_TOPO] values of the key on some node
+  const uint8_t* pair_node;  // [pairs] the (key, value) pair is on some node
+  const ksg_pclass* pcls;
+  const ksg_cterm* cterm;
+  const ksg_req* creq;
+  const int32_t* cval;
+  int32_t* tc_val;           // term classes: per (key, value) (per node for one-node keys)
+  const uint32_t* tc_off;    // [ntc]
+  const int32_t* tc_slot;    // [ntc]
+  int32_t* tc_tot;           // [ntc] terms on nodes carrying the key
+};
+
 struct DevCluster {
   uint32_t N, R, K, goff;
   const int64_t* alloc;
@@ -86,6 +110,7 @@ struct DevCluster {
   const uint32_t* img;     // [img_words][N]
   uint32_t n_ports;
   int32_t* ports;          // [n_ports][N] used host-port triple counts
+  DevTables T;
 };
 
 struct DevProfile {
@@ -1033,6 +1058,37 @@ __global__ void k_pts_score(DevCluster C, DevScratch S, DevOut O, const uint8_t*
   }
 }
 
+// NormalizeScore (wrappedplugin.go:400 -> the plugin's ScoreExtensions) of one
+// feasible node's raw score at a profile position, given the pod's normaliser
+// max / min over the feasible nodes: every path that selects (k_finalize, the
+// table chain's k_final) and the normalized-score export (k_norm_out) use this.
+// use = false: the plugin's PreScore returned Skip (no score, no weight).
+__device__ __forceinline__ int64_t normalize_pos(int plugin, const ksg_prog* h, int64_t s, int64_t mx, int64_t mn,
+                                                 uint32_t ipa_flags, bool pts_keys, bool& use) {
+  use = true;
+  switch (plugin) {
+    case KP_TAINT:  // DefaultNormalizeScore(100, reverse); 0 <= s <= mx
+      return mx == 0 ? 100 : 100 - div_small(100 * s, mx);
+    case KP_NA:  // DefaultNormalizeScore(100, false)
+      if (h->flags & KPF_SKIP_NA_SCORE) { use = false; return s; }
+      return mx == 0 ? s : div_small(100 * s, mx);
+    case KP_PTS:  // 0 <= mn <= s <= mx; nodes missing a key (IgnoredNodes) score 0
+      if (h->flags & KPF_SKIP_PTS_SCORE) { use = false; return s; }
+      if (!pts_keys) return 0;
+      if (mx == 0) return 100;
+      return div_small(100 * (mx + mn - s), mx);
+    case KP_IPA: {
+#pragma clang fp contract(off)
+      if (!(ipa_flags & 8u)) { use = false; return s; }  // PreScore Skip (empty topology score map)
+      const int64_t diff = mx - mn;
+      double f = 0;
+      if (diff > 0) f = __dmul_rn(100.0, __ddiv_rn((double)(s - mn), (double)diff));
+      return (int64_t)f;
+    }
+    default: return s;  // no ScoreExtensions: the raw score
+  }
+}
+
 // NormalizeScore + [0,100] check + weights + packed-key argmax
 __global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, const uint8_t* prog) {
   ProgView V = view(prog);
@@ -1053,36 +1109,9 @@ __global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, c
 #pragma unroll
     for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
       if (pos >= F.n) continue;
-      int64_t s = raw[pos];
-      bool use = true;  // false: the plugin's PreScore returned Skip (not scored)
-      int64_t mx = O.sum->max_score[pos], mn = O.sum->min_score[pos];
-      switch (F.plugins[pos]) {
-        case KP_TAINT:  // DefaultNormalizeScore(100, reverse); 0 <= s <= mx
-          s = mx == 0 ? 100 : 100 - div_small(100 * s, mx);
-          break;
-        case KP_NA:
-          if (h->flags & KPF_SKIP_NA_SCORE) use = false;
-          else s = mx == 0 ? s : div_small(100 * s, mx);
-          break;
-        case KP_PTS:  // 0 <= mn <= s <= mx
-          if (h->flags & KPF_SKIP_PTS_SCORE) use = false;
-          else if (!pts_keys) s = 0;
-          else if (mx == 0) s = 100;
-          else s = div_small(100 * (mx + mn - s), mx);
-          break;
-        case KP_IPA:
-          if (!(ipa_flags & 8u)) {  // PreScore Skip (empty topology score map)
-            use = false;
-          } else {
-#pragma clang fp contract(off)
-            int64_t diff = mx - mn;
-            double f = 0;
-            if (diff > 0) f = __dmul_rn(100.0, __ddiv_rn((double)(s - mn), (double)diff));
-            s = (int64_t)f;
-          }
-          break;
-        default: break;  // no ScoreExtensions: the raw score
-      }
+      bool use;  // false: the plugin's PreScore returned Skip (not scored)
+      const int64_t s = normalize_pos(F.plugins[pos], h, raw[pos], O.sum->max_score[pos], O.sum->min_score[pos],
+                                      ipa_flags, pts_keys, use);
       if (use) {
         if (s < 0 || s > 100) range_err = true;
         tot += s * F.weight[pos];
@@ -1098,11 +1127,70 @@ __global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, c
   if (O.arrive) last_block_commit(C, V, O);
 }
 
-// assume (scheduleOne -> assume -> NodeInfo.AddPod, or its reversal for
-// Unreserve) of program V on local node n: resource rows, and for PTS/IPA
-// profiles the existing-pod table (append; reversal marks the row deleted).
-__device__ void assume_pod(DevCluster& C, const ProgView& V, uint32_t n, int sign, bool table, int32_t* prow) {
+// ---- class tables: lookups and the assume delta
+// Pods of class `cls` counted for topology pair (slot, v) of local node n: the
+// node's own count for keys with one node per value, the pair's sum otherwise.
+__device__ __forceinline__ int32_t pc_count(const DevCluster& C, int32_t cls, int slot, uint32_t n, int32_t v) {
+  if (cls < 0 || v < 0) return 0;
+  if ((C.T.uniq >> slot) & 1u) return C.T.pc_cnt[(size_t)cls * C.N + n];
+  return C.T.pc_dom[(size_t)cls * C.T.NU + C.T.nu_base[slot] + v];
+}
+// Term class u's value at local node n (v: n's value of the class's key).
+__device__ __forceinline__ int32_t tc_value(const DevCluster& C, int32_t u, uint32_t n, int32_t v) {
+  if (v < 0) return 0;
+  const int s = C.T.tc_slot[u];
+  return C.T.tc_val[C.T.tc_off[u] + (((C.T.uniq >> s) & 1u) ? n : (uint32_t)v)];
+}
+__device__ void pc_add(DevCluster& C, int32_t cls, uint32_t n, int sign) {
+  const DevTables& T = C.T;
+  if (cls < 0 || (uint32_t)cls >= T.npc) return;
+  atomicAdd(&T.pc_cnt[(size_t)cls * C.N + n], sign);
+  const uint32_t nt = C.n_topo < KSG_MAX_TOPO ? C.n_topo : KSG_MAX_TOPO;
+  for (uint32_t s = 0; s < nt; ++s) {
+    const int32_t v = node_vid(C, C.tkey[s], n);
+    if (v < 0) continue;
+    atomicAdd(&T.pc_tot[(size_t)cls * KSG_MAX_TOPO + s], sign);
+    if (!((T.uniq >> s) & 1u)) atomicAdd(&T.pc_dom[(size_t)cls * T.NU + T.nu_base[s] + v], sign);
+  }
+}
+// an existing pod's term: +1 (required terms) or its signed weight (preferred)
+__device__ __forceinline__ int32_t eterm_inc(const ksg_exist_term& e) {
+  return e.kind == 2 ? e.weight : (e.kind == 3 ? -e.weight : 1);
+}
+__device__ void tc_add(DevCluster& C, int32_t u, uint32_t n, int32_t inc, int sign) {
+  if (u < 0 || (uint32_t)u >= C.T.ntc) return;
+  const int s = C.T.tc_slot[u];
+  const int32_t v = node_vid(C, C.tkey[s], n);
+  if (v < 0) return;
+  atomicAdd(&C.T.tc_val[C.T.tc_off[u] + (((C.T.uniq >> s) & 1u) ? n : (uint32_t)v)], sign * inc);
+  atomicAdd(&C.T.tc_tot[u], sign);
+}
+// Every class-table delta of program V placed on (sign +1) / removed from
+// (sign -1) local node n: its pod classes and its own affinity terms.  Items
+// i = lane, lane + lanes, ... (one thread: lane 0 of 1).
+__device__ void tables_assume(DevCluster& C, const ProgView& V, uint32_t n, int sign, uint32_t lane, uint32_t lanes) {
+  if (!C.T.on) return;
   const ksg_prog* h = V.h;
+  const uint32_t npm = (uint32_t)h->n_pc_match, ne = (uint32_t)h->n_exist_terms;
+  for (uint32_t i = lane; i < npm + ne; i += lanes) {
+    if (i < npm) {
+      pc_add(C, V.i32[h->pc_match_off + i], n, sign);
+    } else {
+      const ksg_exist_term& e = V.et[h->exist_terms_off + (i - npm)];
+      tc_add(C, e.cls, n, eterm_inc(e), sign);
+    }
+  }
+}
+
+// assume (scheduleOne -> assume -> NodeInfo.AddPod, or its reversal for
+// Unreserve) of program V on local node n: resource rows, the class tables, and
+// for PTS/IPA profiles the existing-pod table (append; reversal marks the row
+// deleted).  lanes > 1: the caller's other lanes apply the class-table deltas
+// (tables_assume) themselves.
+__device__ void assume_pod(DevCluster& C, const ProgView& V, uint32_t n, int sign, bool table, int32_t* prow,
+                           uint32_t lanes = 1) {
+  const ksg_prog* h = V.h;
+  if (lanes == 1) tables_assume(C, V, n, sign, 0, 1);
   for (uint32_t r = 0; r < C.R; ++r) C.req[(size_t)r * C.N + n] += sign * h->req[r];
   C.nzc[n] += sign * h->nz_cpu;
   C.nzm[n] += sign * h->nz_mem;
@@ -1349,6 +1437,8 @@ __global__ void k_assume(DevCluster C, const uint8_t* prog, int32_t gnode, int s
   if (gnode < 0 || (uint32_t)gnode < C.goff || n >= C.N) return;
   assume_pod(C, V, n, sign, table != 0, prow);
 }
+
+#include "table_chain.hip"
 
 // ----------------------------------------------------------------- what-if batches (cfg5)
 // A step of `count` queue pods is scheduled against ONE frozen snapshot (no
@@ -3369,6 +3459,23 @@ struct Engine::Impl {
   DBuf<uint32_t> spair;
   uint32_t nsp = 0, uniq = 0;
   DBuf<int64_t> xregcnt;  // merged registered-domain counts per score constraint
+  // class tables (ksg_types.h "class tables")
+  bool tables_on = false;   // profile with PodTopologySpread / InterPodAffinity
+  DBuf<int32_t> pc_cnt, pc_dom, pc_tot, tc_val, tc_tot, tc_slot_d, slot_dom_d, cval_d;
+  DBuf<uint32_t> tc_off_d, nu_base_d;
+  DBuf<uint8_t> pair_node_d;
+  DBuf<ksg_pclass> pcls_d;
+  DBuf<ksg_cterm> cterm_d;
+  DBuf<ksg_req> creq_d;
+  uint32_t npc = 0, ntc = 0, NU = 0, nct = 0, ncreq = 0, ncval = 0, tc_used = 0;
+  std::vector<uint32_t> tc_off_h;
+  // table chain (k_eval / k_ptsraw / k_final / k_select)
+  DBuf<uint32_t> cur;
+  DBuf<int32_t> cpi, cpst;
+  DBuf<int64_t> cpm, cpm2;
+  DBuf<uint64_t> cpr, cpk;
+  uint32_t cnblk = 0;
+  DBuf<int32_t> knorm;    // normalized scores of one kept pod
   size_t prog_bytes = 0;  // used bytes of the program blob
   // kept per-pair outputs
   uint32_t keep_first = 0, keep_n = 0;
@@ -3430,6 +3537,13 @@ struct Engine::Impl {
     C.pcap = pcap; C.pkeys = pkeys; C.tcap = tcap; C.rcap = rcap; C.vcap = vcap;
     C.ptnode = ptnode.p; C.ptns = ptns.p; C.ptflags = ptflags.p; C.ptlab = ptlab.p;
     C.terms = terms.p; C.tpod = tpod.p; C.treq = treq.p; C.tval = tval.p; C.tcounts = tcounts.p;
+    DevTables& T = C.T;
+    T.on = tables_on ? 1 : 0;
+    T.npc = npc; T.ntc = ntc; T.NU = NU; T.uniq = uniq;
+    T.pc_cnt = pc_cnt.p; T.pc_dom = pc_dom.p; T.pc_tot = pc_tot.p;
+    T.nu_base = nu_base_d.p; T.slot_dom = slot_dom_d.p; T.pair_node = pair_node_d.p;
+    T.pcls = pcls_d.p; T.cterm = cterm_d.p; T.creq = creq_d.p; T.cval = cval_d.p;
+    T.tc_val = tc_val.p; T.tc_off = tc_off_d.p; T.tc_slot = tc_slot_d.p; T.tc_tot = tc_tot.p;
     return C;
   }
   DevScratch scratch() const {
@@ -3489,6 +3603,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
     if (p == KP_PTS) I.has_pts = true;
     if (p == KP_IPA) I.has_ipa = true;
   }
+  I.tables_on = I.has_pts || I.has_ipa;
   F.fit_strategy = cfg.fit_strategy;
   F.fit_n = cfg.fit_n;
   F.ba_n = cfg.ba_n;
@@ -3597,6 +3712,24 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   if (!I.topo_key_d.upload(ns.topo_key, s, err) || !I.topo_base_d.upload(ns.topo_base, s, err) ||
       !I.topo_count_d.upload(ns.topo_count, s, err))
     return false;
+  {  // class tables: the definitions come from the host registry after the upload (add_classes)
+    I.npc = I.ntc = I.nct = I.ncreq = I.ncval = I.tc_used = 0;
+    I.tc_off_h.clear();
+    I.NU = ns.nu_pairs;
+    std::vector<uint32_t> nb(KSG_MAX_TOPO, 0xFFFFFFFFu);
+    std::vector<int32_t> sd(KSG_MAX_TOPO, 0);
+    for (size_t t = 0; t < ns.nu_base.size() && t < KSG_MAX_TOPO; ++t) nb[t] = ns.nu_base[t];
+    for (size_t t = 0; t < ns.slot_dom.size() && t < KSG_MAX_TOPO; ++t) sd[t] = ns.slot_dom[t];
+    std::vector<uint8_t> pn = ns.pair_node;
+    pn.resize(std::max<size_t>(ns.topo_pairs, 1), 0);
+    if (!I.nu_base_d.upload(nb, s, err) || !I.slot_dom_d.upload(sd, s, err) || !I.pair_node_d.upload(pn, s, err))
+      return false;
+    I.cnblk = std::max<uint32_t>((ns.n + kBlock - 1) / kBlock, 1);
+    if (!I.cur.alloc(1, err) || !I.cpi.alloc((size_t)KCP_I * I.cnblk, err) || !I.cpst.alloc(I.cnblk, err) ||
+        !I.cpm.alloc((size_t)2 * KCP_X * I.cnblk, err) || !I.cpm2.alloc((size_t)2 * I.cnblk, err) ||
+        !I.cpr.alloc((size_t)KSG_MAX_TSC * I.cnblk, err) || !I.cpk.alloc(I.cnblk, err))
+      return false;
+  }
   // existing-pod table (capacity for device-side appends)
   I.pcap = std::max<uint32_t>(pod_cap, pt.n);
   I.pkeys = pt.n_keys;
@@ -3876,6 +4009,17 @@ static PodLite pod_lite(const std::vector<uint8_t>& prog) {
   return q;
 }
 
+// run_queue's per-pod decisions: bit0 PodTopologySpread constraints, bit1
+// InterPodAffinity (existing pods' terms may apply to any pod), bit2 the table
+// chain, bit3 its PodTopologySpread raw-score pass.
+static uint32_t prog_need_of(const ksg_prog* h) {
+  uint32_t need = 2;
+  if (h->n_tsc_filter + h->n_tsc_score > 0) need |= 1;
+  if (h->tab & KTAB_ON) need |= 4;
+  if (h->tab & KTAB_PTS_MULTI) need |= 8;
+  return need;
+}
+
 static bool exchange(Engine::Impl& I, const void* src, size_t bytes, std::string& err);
 
 bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
@@ -3984,7 +4128,7 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
   I.prog_off.push_back(off);
   if (!na_weights_fit(prog)) I.static_fits = false;
   const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
-  I.prog_need.push_back((h->n_tsc_filter + h->n_tsc_score > 0 ? 1u : 0u) | 2u);
+  I.prog_need.push_back(prog_need_of(h));
   for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
   return true;
 }
@@ -4062,6 +4206,132 @@ bool Engine::table_room(uint32_t used[4], uint32_t cap[4], std::string& err) {
   return true;
 }
 
+uint32_t Engine::pod_classes() const { return p_->npc; }
+uint32_t Engine::term_classes() const { return p_->ntc; }
+
+// Append a device array's new elements (capacity doubling, old contents kept).
+template <class T>
+static bool dev_append(DBuf<T>& b, size_t used, const std::vector<T>& v, hipStream_t s, std::string& err) {
+  if (v.empty()) return true;
+  if (!b.grow(used + v.size(), used, s, err)) return false;
+  HIPCHK(hipMemcpyAsync(b.p + used, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  return true;
+}
+template <class T>
+static bool dev_zero_tail(DBuf<T>& b, size_t used, size_t count, hipStream_t s, std::string& err) {
+  if (!count) return true;
+  if (!b.grow(used + count, used, s, err)) return false;
+  HIPCHK(hipMemsetAsync(b.p + used, 0, count * sizeof(T), s));
+  return true;
+}
+
+bool Engine::add_classes(const ClassUpload& u, std::string& err) {
+  Impl& I = *p_;
+  hipStream_t s = I.stream;
+  const uint32_t pc0 = I.npc, tc0 = I.ntc, npc = (uint32_t)u.pc.size(), ntc = (uint32_t)u.tc_slot.size();
+  if (!npc && !ntc) return true;
+  const size_t Nn = std::max<uint32_t>(I.N, 1), NUn = std::max<uint32_t>(I.NU, 1);
+  if (npc) {  // definitions, rebased onto the device pools
+    std::vector<ksg_pclass> pc = u.pc;
+    std::vector<ksg_cterm> ct = u.ct;
+    std::vector<ksg_req> rq = u.creq;
+    for (auto& x : pc) x.term_off += (int32_t)I.nct;
+    for (auto& x : ct) {
+      x.sel.req_off += (int32_t)I.ncreq;
+      x.ns_off += (int32_t)I.ncval;
+    }
+    for (auto& x : rq) x.val_off += (int32_t)I.ncval;
+    if (!dev_append(I.pcls_d, pc0, pc, s, err) || !dev_append(I.cterm_d, I.nct, ct, s, err) ||
+        !dev_append(I.creq_d, I.ncreq, rq, s, err) || !dev_append(I.cval_d, I.ncval, u.cval, s, err) ||
+        !dev_zero_tail(I.pc_cnt, (size_t)pc0 * Nn, (size_t)npc * Nn, s, err) ||
+        !dev_zero_tail(I.pc_dom, (size_t)pc0 * NUn, (size_t)npc * NUn, s, err) ||
+        !dev_zero_tail(I.pc_tot, (size_t)pc0 * KSG_MAX_TOPO, (size_t)npc * KSG_MAX_TOPO, s, err))
+      return false;
+    I.nct += (uint32_t)ct.size();
+    I.ncreq += (uint32_t)rq.size();
+    I.ncval += (uint32_t)u.cval.size();
+    I.npc += npc;
+  }
+  if (ntc) {  // per term class: one value per (key, value) pair, or per node for one-node keys
+    std::vector<uint32_t> off(ntc);
+    uint32_t add = 0;
+    for (uint32_t i = 0; i < ntc; ++i) {
+      const int32_t sl = u.tc_slot[i];
+      if (sl < 0 || sl >= (int32_t)I.topo.topo_count.size()) { err = "term class without a topology slot"; return false; }
+      off[i] = I.tc_used + add;
+      add += std::max<uint32_t>(((I.uniq >> sl) & 1u) ? I.N : I.topo.topo_count[sl], 1);
+    }
+    if (!dev_zero_tail(I.tc_val, I.tc_used, add, s, err) || !dev_append(I.tc_off_d, tc0, off, s, err) ||
+        !dev_append(I.tc_slot_d, tc0, u.tc_slot, s, err) || !dev_zero_tail(I.tc_tot, tc0, ntc, s, err))
+      return false;
+    I.tc_used += add;
+    I.tc_off_h.insert(I.tc_off_h.end(), off.begin(), off.end());
+    I.ntc += ntc;
+  }
+  DevCluster C = I.cluster();
+  if (npc && I.pcap)
+    hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, pc0, npc);
+  if (ntc && I.tcap) hipLaunchKernelGGL(k_tc_build, dim3((I.tcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, tc0);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  return true;
+}
+
+bool Engine::rebuild_class_tables(std::string& err) {
+  Impl& I = *p_;
+  hipStream_t s = I.stream;
+  if (!I.npc && !I.ntc) return true;
+  const size_t Nn = std::max<uint32_t>(I.N, 1), NUn = std::max<uint32_t>(I.NU, 1);
+  if (I.npc) {
+    HIPCHK(hipMemsetAsync(I.pc_cnt.p, 0, (size_t)I.npc * Nn * 4, s));
+    HIPCHK(hipMemsetAsync(I.pc_dom.p, 0, (size_t)I.npc * NUn * 4, s));
+    HIPCHK(hipMemsetAsync(I.pc_tot.p, 0, (size_t)I.npc * KSG_MAX_TOPO * 4, s));
+  }
+  if (I.ntc) {
+    HIPCHK(hipMemsetAsync(I.tc_val.p, 0, (size_t)I.tc_used * 4, s));
+    HIPCHK(hipMemsetAsync(I.tc_tot.p, 0, (size_t)I.ntc * 4, s));
+  }
+  DevCluster C = I.cluster();
+  if (I.npc && I.pcap)
+    hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, 0u, I.npc);
+  if (I.ntc && I.tcap) hipLaunchKernelGGL(k_tc_build, dim3((I.tcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, 0u);
+  HIPCHK(hipGetLastError());
+  return true;
+}
+
+bool Engine::replace_program(uint32_t q, const std::vector<uint8_t>& prog, std::string& err) {
+  Impl& I = *p_;
+  hipStream_t s = I.stream;
+  if (q >= I.prog_off.size()) { err = "program index out of range"; return false; }
+  const size_t off = (I.prog_bytes + 255) & ~(size_t)255;
+  if (!I.progs.grow(off + prog.size(), I.prog_bytes, s, err)) return false;
+  const uint64_t off64 = off;
+  HIPCHK(hipMemcpyAsync(I.progs.p + off, prog.data(), prog.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.prog_off_d.p + q, &off64, sizeof(off64), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));  // host sources
+  I.prog_bytes = off + prog.size();
+  I.prog_off[q] = off;
+  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
+  I.prog_need[q] = prog_need_of(h);
+  return true;
+}
+
+bool Engine::normalized(uint32_t j, std::vector<int32_t>& norm, std::string& err) {
+  Impl& I = *p_;
+  if (!(I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n)) { err = "outputs not kept for this pod"; return false; }
+  const size_t N = I.N, k = j - I.keep_first;
+  if (!I.knorm.alloc(std::max<size_t>(N, 1) * KSG_MAX_PLUGINS, err)) return false;
+  DevCluster C = I.cluster();
+  hipLaunchKernelGGL(k_norm_out, dim3(std::max<uint32_t>((I.N + kBlock - 1) / kBlock, 1)), dim3(kBlock), 0, I.stream, C,
+                     I.F, I.progs.p + I.prog_off[j], I.sums.p + j, I.kfilter.p + k * N,
+                     I.kscore.p + k * N * KSG_MAX_PLUGINS, I.knorm.p);
+  HIPCHK(hipGetLastError());
+  norm.resize((size_t)I.F.n * N);
+  if (N) HIPCHK(hipMemcpyAsync(norm.data(), I.knorm.p, norm.size() * 4, hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
 bool Engine::set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err) {
   Impl& I = *p_;
   if (first + count > I.prog_off.size()) { err = "program index out of range"; return false; }
@@ -4080,11 +4350,7 @@ bool Engine::set_programs(const std::vector<std::vector<uint8_t>>& progs, std::s
     blob.resize(off);
     I.prog_off.push_back(off);
     blob.insert(blob.end(), p.begin(), p.end());
-    const ksg_prog* h = reinterpret_cast<const ksg_prog*>(p.data());
-    uint32_t need = 0;
-    if (h->n_tsc_filter + h->n_tsc_score > 0) need |= 1;
-    need |= 2;  // IPA: existing pods' terms may apply to any pod
-    I.prog_need.push_back(need);
+    I.prog_need.push_back(prog_need_of(reinterpret_cast<const ksg_prog*>(p.data())));
   }
   if (!I.progs.upload(blob, I.stream, err)) return false;
   I.prog_bytes = blob.size();
@@ -4195,8 +4461,42 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
     return true;
   };
   const uint32_t xr = I.xranks;
+  // table chain (table_chain.hip): pod index on the device, partials per block
+  ChainArgs CA{};
+  CA.progs = I.progs.p;
+  CA.prog_off = I.prog_off_d.p;
+  CA.cur = I.cur.p;
+  CA.end = first + count;
+  CA.sums = I.sums.p;
+  CA.keep_first = I.keep_first;
+  CA.keep_n = I.keep_n;
+  CA.kfilter = I.kfilter.p; CA.kscore = I.kscore.p; CA.ktotal = I.ktotal.p;
+  CA.filter = I.filter.p; CA.score = I.score.p; CA.total = I.total.p;
+  CA.nblk = I.cnblk;
+  CA.pi = I.cpi.p; CA.pm = I.cpm.p; CA.pr = I.cpr.p; CA.pm2 = I.cpm2.p; CA.pk = I.cpk.p; CA.pst = I.cpst.p;
+  CA.mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
+  CA.prow = I.prow.p;
+  uint32_t cur_at = 0xFFFFFFFFu;  // the device pod counter holds this queue index
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
+    if (!xchain && (I.prog_need[j] & 4)) {
+      if (cur_at != j) hipLaunchKernelGGL(k_set_cur, dim3(1), dim3(64), 0, s, I.cur.p, j);
+      const bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
+      if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
+      hipLaunchKernelGGL(k_eval, dim3(I.cnblk), b, 0, s, C, F, CA);
+      if (sampled) {
+        HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
+        I.n_samples++;
+      }
+      if (F.has_ext) {
+        if (I.prog_need[j] & 8) hipLaunchKernelGGL(k_ptsraw, dim3(I.cnblk), b, 0, s, C, F, CA);
+        hipLaunchKernelGGL(k_final, dim3(I.cnblk), b, 0, s, C, F, CA);
+      }
+      hipLaunchKernelGGL(k_select, dim3(1), b, 0, s, C, F, CA);
+      cur_at = j + 1;
+      continue;
+    }
+    cur_at = 0xFFFFFFFFu;
     const int mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
     DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j, xchain ? nullptr : I.arrive1.p, mode, I.prow.p + j};
     bool kept = I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n;
@@ -4327,6 +4627,7 @@ bool Engine::reset(std::string& err) {
   if (I.n_ports)
     HIPCHK(hipMemcpyAsync(I.ports.p, I.ports0.p, (size_t)I.n_ports * I.N * 4, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemcpyAsync(I.tcounts.p, I.counts0, sizeof(I.counts0), hipMemcpyHostToDevice, s));
+  if (!rebuild_class_tables(err)) return false;  // from the restored existing-pod table
   uint32_t cnt = (uint32_t)I.prog_off.size();
   if (cnt) hipLaunchKernelGGL(k_init_summaries, dim3((cnt + 255) / 256), dim3(256), 0, s, I.sums.p, cnt, I.F);
   HIPCHK(hipGetLastError());

@@ -453,7 +453,6 @@ static bool has_prefilter(int p) {
 static bool has_filter(int p) { return p != P_BA && p != P_IMAGE && p != P_NOOP; }
 static bool has_prescore(int p) { return p <= P_IPA || p == P_VOLBIND; }
 static bool has_score(int p) { return p <= P_IPA || p == P_IMAGE; }  // VolumeBinding: PreScore Skip (no scorer)
-static bool has_ext(int p) { return p == P_TAINT || p == P_NA || p == P_PTS || p == P_IPA; }
 
 // Per-pod host-known facts the renderer needs besides the device outputs.
 struct PodMeta {
@@ -592,6 +591,242 @@ struct Cluster {
     return -1;
   }
 
+  // ------------------------------------------------------------ class tables
+  // Registry of the pod classes and term classes the device keeps counts for
+  // (ksg_types.h "class tables"; engine add_classes).  Class ids are stable
+  // until the next encode; a program lists the classes it belongs to / that
+  // apply to it, refreshed when classes are added after it was compiled.
+  struct PClass {
+    bool excl = false;     // terminating pods never match (PodTopologySpread)
+    vector<ATerm> terms;   // conjunction
+  };
+  struct TClass {
+    int group = 0;         // KSG_TC_*
+    string topo;           // topology key
+    ATerm term;
+  };
+  vector<PClass> pcls;
+  vector<TClass> tcls;
+  unordered_map<string, int32_t> pcls_id, tcls_id;
+  // node topology keys (class-table path eligibility), this shard's nodes
+  vector<uint32_t> node_slots;             // per node: bit s = carries topology slot s's key
+  vector<uint32_t> slot_nodes;             // per slot: nodes carrying its key
+  std::unordered_map<uint32_t, uint32_t> keyset_nodes;  // slot mask -> nodes carrying every key of it
+  vector<uint32_t> enc_topo_count;
+  vector<uint8_t> enc_topo_unique;
+
+  static void key_sel(string& k, const LSel& s) {
+    k += s.nothing ? 'N' : (s.err ? 'E' : 'S');
+    for (auto& r : s.reqs) {
+      k += '\x1e';
+      k += r.key;
+      k += '\x1d';
+      k += r.op;
+      for (auto& v : r.vals) {
+        k += '\x1c';
+        k += v;
+      }
+    }
+  }
+  static void key_term(string& k, const ATerm& a) {
+    k += a.ns_all ? 'A' : 'L';
+    for (auto& n : a.namespaces) {
+      k += '\x1f';
+      k += n;
+    }
+    k += '|';
+    key_sel(k, a.sel);
+  }
+  // pod class of the conjunction `terms` (-1: matches no pod)
+  int32_t pclass(bool excl, const vector<ATerm>& terms) {
+    if (terms.empty()) return -1;
+    for (auto& t : terms)
+      if (t.sel.nothing || t.sel.err) return -1;
+    string k(excl ? "X" : "I");
+    for (auto& t : terms) {
+      k += '#';
+      key_term(k, t);
+    }
+    auto it = pcls_id.find(k);
+    if (it != pcls_id.end()) return it->second;
+    const int32_t id = (int32_t)pcls.size();
+    PClass c;
+    c.excl = excl;
+    for (auto& t : terms) {
+      ATerm a;
+      a.sel = t.sel;
+      a.namespaces = t.namespaces;
+      a.ns_all = t.ns_all;
+      c.terms.push_back(std::move(a));
+    }
+    pcls.push_back(std::move(c));
+    pcls_id.emplace(std::move(k), id);
+    return id;
+  }
+  // term class of an existing pod's term of `kind` (0 required affinity, 1 required
+  // anti, 2/3 preferred); -1 matches nothing / no topology slot
+  int32_t tclass(int kind, const ATerm& a) {
+    if (a.sel.nothing || a.sel.err || topo.get(a.topo) < 0) return -1;
+    const int group = kind == 0 ? KSG_TC_HARD : kind == 1 ? KSG_TC_ANTI : KSG_TC_PREF;
+    string k = std::to_string(group) + '@' + a.topo + '@';
+    key_term(k, a);
+    auto it = tcls_id.find(k);
+    if (it != tcls_id.end()) return it->second;
+    const int32_t id = (int32_t)tcls.size();
+    TClass c;
+    c.group = group;
+    c.topo = a.topo;
+    c.term.sel = a.sel;
+    c.term.namespaces = a.namespaces;
+    c.term.ns_all = a.ns_all;
+    tcls.push_back(std::move(c));
+    tcls_id.emplace(std::move(k), id);
+    return id;
+  }
+  static bool term_matches(const ATerm& t, const Pod& p) {
+    return (t.ns_all || t.namespaces.count(p.ns)) && t.sel.matches(p.labels);
+  }
+  static bool pclass_matches(const PClass& c, const Pod& p) {
+    if (c.excl && p.terminating) return false;
+    for (auto& t : c.terms)
+      if (!term_matches(t, p)) return false;
+    return true;
+  }
+  // PodTopologySpread constraint selector with matchLabelKeys merged (v1.30 PreFilter)
+  static LSel tsc_selector(const Pod& p, const TSC& c) {
+    LSel s = lsel(c.sel);
+    if (!c.match_label_keys.empty() && !s.nothing)
+      for (auto& k : c.match_label_keys) {
+        auto it = p.labels.find(k);
+        if (it != p.labels.end()) s.reqs.push_back({k, "In", {it->second}});
+      }
+    return s;
+  }
+  int32_t tsc_class(const Pod& p, const LSel& s) {  // countPodsMatchSelector: Empty() counts nothing
+    if (s.nothing || s.err || s.reqs.empty()) return -1;
+    ATerm a;
+    a.sel = s;
+    a.namespaces.insert(p.ns);
+    return pclass(true, {a});
+  }
+  // Register every class pod p's program refers to (compile_queue's first pass).
+  void register_classes(const Pod& p) {
+    if (!tables_on()) return;
+    for (auto& c : p.tsc) tsc_class(p, tsc_selector(p, c));
+    for (auto* v : {&p.req_aff, &p.req_anti, &p.pref_aff, &p.pref_anti})
+      for (auto& a : *v) pclass(false, {a});
+    if (!p.req_aff.empty()) pclass(false, p.req_aff);
+    for (auto& a : p.req_aff) tclass(0, a);
+    for (auto& a : p.req_anti) tclass(1, a);
+    for (auto& a : p.pref_aff) tclass(2, a);
+    for (auto& a : p.pref_anti) tclass(3, a);
+  }
+  // Upload the classes the device has no tables for yet (and build them).
+  bool sync_classes() {
+    if (!tables_on()) return true;
+    ClassUpload u;
+    for (uint32_t c = eng->pod_classes(); c < pcls.size(); ++c) {
+      ksg_pclass pc{};
+      pc.n_terms = (int32_t)pcls[c].terms.size();
+      pc.term_off = (int32_t)u.ct.size();
+      pc.excl_term = pcls[c].excl ? 1 : 0;
+      for (auto& t : pcls[c].terms) {
+        ksg_cterm ct{};
+        compile_lsel(t.sel, ct.sel, u.creq, u.cval);
+        ct.ns_all = t.ns_all ? 1 : 0;
+        ct.ns_off = (int32_t)u.cval.size();
+        for (auto& ns : t.namespaces) u.cval.push_back(nss.get(ns) < 0 ? -2 : nss.get(ns));
+        ct.ns_cnt = (int32_t)t.namespaces.size();
+        u.ct.push_back(ct);
+      }
+      u.pc.push_back(pc);
+    }
+    for (uint32_t k = eng->term_classes(); k < tcls.size(); ++k) u.tc_slot.push_back(topo.get(tcls[k].topo));
+    return eng->add_classes(u, err);
+  }
+  // nodes carrying every key of slot mask m
+  uint32_t nodes_with_all(uint32_t m) {
+    auto it = keyset_nodes.find(m);
+    if (it != keyset_nodes.end()) return it->second;
+    uint32_t c = 0;
+    for (uint32_t x : node_slots) c += (x & m) == m;
+    keyset_nodes.emplace(m, c);
+    return c;
+  }
+  // every node with one of the keys of mask m carries all of them
+  bool keys_together(uint32_t m) {
+    const uint32_t all = nodes_with_all(m);
+    for (size_t s = 0; s < slot_nodes.size(); ++s)
+      if (((m >> s) & 1u) && slot_nodes[s] != all) return false;
+    return true;
+  }
+  // Class counts each program's lists were computed against (stale-list refresh).
+  vector<std::pair<uint32_t, uint32_t>> prog_cls;
+
+  // Can the pod's PodTopologySpread / InterPodAffinity inputs be read from the
+  // class tables (the table chain)?  Unsharded; for PodTopologySpread, counting
+  // that excludes no node for this pod (no node-inclusion policy narrows it, and
+  // every node carrying one of the constraints' keys carries them all), filter
+  // keys with at most KSG_TAB_MAXV values shared by several nodes (minMatchNum
+  // per block), score keys whose registered values fit a 64-bit mask or sit one
+  // per node.  Every other pod runs the scanning chain (k_scan_pods ...).
+  bool table_path(const ksg_prog& h) {
+    if (shards != 1) return false;
+    if (pos_of(P_PTS) < 0) return true;
+    const bool na_restrict = (h.flags & (KPF_HAS_NODE_SEL | KPF_HAS_REQ_NA)) != 0;
+    const int nf = h.n_tsc_filter, ns = h.n_tsc_score;
+    auto policy_ok = [&](const ksg_tsc& t) { return !(t.honor_affinity && na_restrict) && !t.honor_taints; };
+    if (!(h.flags & KPF_SKIP_PTS_FILTER)) {
+      uint32_t m = 0;
+      for (int c = 0; c < nf; ++c) {
+        const ksg_tsc& t = h.tsc[c];
+        if (!policy_ok(t) || enc_topo_unique[t.topo] || enc_topo_count[t.topo] > KSG_TAB_MAXV) return false;
+        m |= 1u << t.topo;
+      }
+      if (!keys_together(m)) return false;
+    }
+    if (!(h.flags & KPF_SKIP_PTS_SCORE)) {
+      uint32_t m = 0;
+      for (int c = nf; c < nf + ns; ++c) {
+        const ksg_tsc& t = h.tsc[c];
+        if (!policy_ok(t)) return false;
+        if (!t.is_hostname && t.first_of_key && !enc_topo_unique[t.topo] && enc_topo_count[t.topo] > KSG_TAB_REGV)
+          return false;
+        m |= 1u << t.topo;
+      }
+      if (!keys_together(m)) return false;
+    }
+    return true;
+  }
+  // Recompile queue pod q when classes added since its compile apply to it (its
+  // pod-class list must hold every class whose table counts it; its term-class
+  // list every term class that applies to it).
+  bool refresh_program(uint32_t q) {
+    if (!tables_on() || q >= progs.size() || q >= prog_cls.size()) return true;
+    const auto at = prog_cls[q];
+    if (at.first == pcls.size() && at.second == tcls.size()) return true;
+    bool stale = false;
+    for (size_t c = at.first; c < pcls.size() && !stale; ++c) stale = pclass_matches(pcls[c], queue[q]);
+    for (size_t k = at.second; k < tcls.size() && !stale; ++k) stale = term_matches(tcls[k].term, queue[q]);
+    if (!stale) {
+      prog_cls[q] = {(uint32_t)pcls.size(), (uint32_t)tcls.size()};
+      return true;
+    }
+    vector<uint8_t> blob;
+    PodMeta m;
+    if (!compile(queue[q], (int32_t)q, blob, m)) return false;
+    if (!sync_classes()) return false;  // (no new classes: the pod's own were registered)
+    if (!eng->replace_program(q, blob, err)) return false;
+    progs[q] = std::move(blob);
+    meta[q] = std::move(m);
+    return true;
+  }
+  bool refresh_programs(uint32_t first, uint32_t count) {
+    for (uint32_t q = first; q < first + count; ++q)
+      if (!refresh_program(q)) return false;
+    return true;
+  }
+
   // ------------------------------------------------------------ vocabularies
   void intern_pod_labels(const Pod& p) {
     nss.add(p.ns);
@@ -712,6 +947,12 @@ struct Cluster {
   }
 
   bool encode_snapshot(NodeSoA& S, PodTableSoA& T) {
+    // a new snapshot: the class registry restarts (the bound pods' terms register first)
+    pcls.clear();
+    tcls.clear();
+    pcls_id.clear();
+    tcls_id.clear();
+    prog_cls.clear();
     uint32_t G = (uint32_t)nodes.size();
     lo = (uint32_t)((uint64_t)G * rank / shards);
     hi = (uint32_t)((uint64_t)G * (rank + 1) / shards);
@@ -787,6 +1028,35 @@ struct Cluster {
       S.topo_unique.push_back(uniq ? 1 : 0);
     }
     S.topo_pairs = pairs;
+    // class tables: pair index space of the keys whose values span nodes, the
+    // values present on this shard's nodes, and every node's topology keys
+    S.nu_base.assign(topo.names.size(), 0xFFFFFFFFu);
+    S.slot_dom.assign(topo.names.size(), 0);
+    S.pair_node.assign(pairs, 0);
+    S.nu_pairs = 0;
+    for (size_t t = 0; t < topo.names.size(); ++t)
+      if (!S.topo_unique[t]) {
+        S.nu_base[t] = S.nu_pairs;
+        S.nu_pairs += S.topo_count[t];
+      }
+    node_slots.assign(n, 0);
+    slot_nodes.assign(topo.names.size(), 0);
+    keyset_nodes.clear();
+    for (uint32_t i = 0; i < n; ++i)
+      for (size_t t = 0; t < topo.names.size(); ++t) {
+        const int32_t k = S.topo_key[t];
+        if (k < 0) continue;
+        const int32_t v = S.label_vid[(size_t)k * n + i];
+        if (v < 0) continue;
+        node_slots[i] |= 1u << t;
+        slot_nodes[t]++;
+        if (!S.pair_node[S.topo_base[t] + v]) {
+          S.pair_node[S.topo_base[t] + v] = 1;
+          S.slot_dom[t]++;
+        }
+      }
+    enc_topo_count = S.topo_count;
+    enc_topo_unique = S.topo_unique;
     // bound pods: NodeInfo aggregates + existing-pod table (this shard's nodes)
     T = PodTableSoA();
     T.n_keys = (uint32_t)pkeys.names.size();
@@ -843,6 +1113,7 @@ struct Cluster {
       e.ns_off = (int32_t)vals.size();
       for (auto& ns : a.namespaces) vals.push_back(nss.get(ns) < 0 ? -2 : nss.get(ns));
       e.ns_cnt = (int32_t)a.namespaces.size();
+      e.cls = tables_on() ? tclass(kind, a) : -1;
       terms.push_back(e);
       if (term_pod_v) term_pod_v->push_back(row);
     };
@@ -942,6 +1213,7 @@ struct Cluster {
     for (auto& ns : a.namespaces) P.i32.push_back(nss.get(ns) < 0 ? -2 : nss.get(ns));
     t.ns_cnt = (int32_t)a.namespaces.size();
     t.weight = a.weight;
+    t.cls = tables_on() ? pclass(false, {a}) : -1;
   }
 
   bool compile(const Pod& p, int32_t qidx, vector<uint8_t>& blob, PodMeta& m) {
@@ -1094,15 +1366,10 @@ struct Cluster {
         if (idx >= KSG_MAX_TSC) { err = "too many topology spread constraints"; return false; }
         ksg_tsc& t = h.tsc[idx];
         t = ksg_tsc{};
-        LSel s = lsel(c.sel);
-        if (!c.match_label_keys.empty() && !s.nothing) {
-          for (auto& k : c.match_label_keys) {
-            auto it = p.labels.find(k);
-            if (it != p.labels.end()) s.reqs.push_back({k, "In", {it->second}});
-          }
-        }
+        const LSel s = tsc_selector(p, c);
         if (s.err) m.prefilter_error = true;
         compile_lsel(s, t.sel, P.req, P.i32);
+        t.cls = tables_on() ? tsc_class(p, s) : -1;
         t.topo = topo.get(c.key);
         t.topo_key = nkeys.get(c.key);
         t.max_skew = c.max_skew;
@@ -1128,6 +1395,26 @@ struct Cluster {
     }
     if (nf == 0) h.flags |= KPF_SKIP_PTS_FILTER;
     if (ns == 0) h.flags |= KPF_SKIP_PTS_SCORE;
+    // class tables: the filter pair count is the LAST filter constraint's on the key
+    // (calPreFilterState keeps one count per pair); a score pair sums every
+    // non-hostname score constraint on the key (TopologyPairToPodCounts)
+    for (int i = 0; i < nf; ++i) {
+      h.tsc[i].eff_cls = h.tsc[i].cls;
+      for (int j = i + 1; j < nf; ++j)
+        if (h.tsc[j].topo == h.tsc[i].topo) h.tsc[i].eff_cls = h.tsc[j].cls;
+    }
+    for (int i = nf; i < nf + ns; ++i) {
+      ksg_tsc& t = h.tsc[i];
+      t.eff_cls = t.cls;
+      t.sc_off = (int32_t)P.i32.size();
+      t.sc_n = 0;
+      if (t.is_hostname) continue;
+      for (int j = nf; j < nf + ns; ++j)
+        if (h.tsc[j].topo == t.topo && !h.tsc[j].is_hostname && h.tsc[j].cls >= 0) {
+          P.i32.push_back(h.tsc[j].cls);
+          t.sc_n++;
+        }
+    }
     // ---- InterPodAffinity (incoming terms; namespaceSelector merged)
     h.aterm_off = (int32_t)P.at.size();
     for (auto* v : {&p.req_aff, &p.req_anti, &p.pref_aff, &p.pref_anti})
@@ -1145,6 +1432,7 @@ struct Cluster {
     for (auto& a : p.req_aff)
       self_all = self_all && (a.namespaces.count(p.ns) || a.ns_all) && a.sel.matches(p.labels);
     h.self_matches_all = self_all ? 1 : 0;
+    h.aff_cls = tables_on() && !p.req_aff.empty() ? pclass(false, p.req_aff) : -1;
     if (p.pref_aff_present || p.pref_anti_present) h.flags |= KPF_IPA_HAS_CONSTRAINTS;
     m.ipa_no_req_terms = p.req_aff.empty() && p.req_anti.empty();
     m.ipa_prescore_skip_static = ipa_ignore && !(p.pref_aff_present || p.pref_anti_present);
@@ -1198,6 +1486,33 @@ struct Cluster {
     vector<int32_t>* none = nullptr;
     append_terms(p, 0, P.et, none, P.req, P.i32);
     h.n_exist_terms = (int32_t)P.et.size();
+    // ---- class tables: the classes this pod belongs to (its assume's deltas) and
+    // the existing pods' term classes that match it (their groups follow the ids)
+    h.pc_match_off = (int32_t)P.i32.size();
+    h.n_pc_match = 0;
+    h.tc_match_off = h.pc_match_off;
+    h.n_tc_match = 0;
+    if (tables_on()) {
+      for (size_t c = 0; c < pcls.size(); ++c)
+        if (pclass_matches(pcls[c], p)) {
+          P.i32.push_back((int32_t)c);
+          h.n_pc_match++;
+        }
+      h.tc_match_off = (int32_t)P.i32.size();
+      vector<int32_t> grp;
+      for (size_t k = 0; k < tcls.size(); ++k)
+        if (term_matches(tcls[k].term, p)) {
+          P.i32.push_back((int32_t)k);
+          grp.push_back(tcls[k].group);
+          h.n_tc_match++;
+        }
+      P.i32.insert(P.i32.end(), grp.begin(), grp.end());
+      h.tab = table_path(h) ? KTAB_ON : 0;
+      if ((h.tab & KTAB_ON) && pos_of(P_PTS) >= 0 && h.n_tsc_score > 1 && !(h.flags & KPF_SKIP_PTS_SCORE))
+        h.tab |= KTAB_PTS_MULTI;
+    } else {
+      h.tab = shards == 1 ? KTAB_ON : 0;  // profiles without PTS / IPA: the chain needs no tables
+    }
     m.flags = h.flags;
     // ---- lay out the blob
     auto align = [](uint32_t x) { return (x + 15u) & ~15u; };
@@ -1491,9 +1806,10 @@ struct Cluster {
       vector<uint8_t> blob;
       PodMeta m;
       if (!compile(queue[q], (int32_t)q, blob, m)) return false;
-      if (!eng->append_program(blob, err)) return false;
+      if (!sync_classes() || !eng->append_program(blob, err)) return false;  // classes it brought: tables built
       progs.push_back(std::move(blob));
       meta.push_back(std::move(m));
+      prog_cls.resize(progs.size(), {(uint32_t)pcls.size(), (uint32_t)tcls.size()});
     }
     if (!eng->keep_outputs(q, 1, err) || !eng->run_queue(q, 1, commit, err) || !eng->sync(err) ||
         !eng->summaries(q, 1, &out, err))
@@ -1516,7 +1832,7 @@ struct Cluster {
     track_queue();
     if (q >= queue.size() || qmode[q] != 2 || placed[q] >= 0) { err = "reserve: pod not in an uncommitted cycle"; return false; }
     if (node < 0 || node >= (int32_t)nodes.size()) { err = "reserve: node out of range"; return false; }
-    if (!eng->assume(q, node, +1, err)) return false;
+    if (!refresh_program(q) || !eng->assume(q, node, +1, err)) return false;
     placed[q] = node;
     assumed_in[q] = epoch;
     return check_table();
@@ -1530,7 +1846,7 @@ struct Cluster {
     if (at < 0) { err = "unreserve: pod is not assumed"; return false; }
     qmode[q] = 2;
     placed[q] = -1;
-    if (assumed_in[q] == epoch) return eng->assume(q, at, -1, err);
+    if (assumed_in[q] == epoch) return refresh_program(q) && eng->assume(q, at, -1, err);
     return rebuild();  // assumed before the last rebuild: it is a bound pod of the snapshot now
   }
 
@@ -1712,8 +2028,9 @@ struct Cluster {
       }
       inplace_dirty = true;
     }
-    bool ok = eng->bound_deltas(blobs, gn, sg, slot, rows, err);
-    for (size_t i = 0; ok && i < unres.size(); ++i) ok = eng->assume((uint32_t)unres[i].first, unres[i].second, -1, err);
+    bool ok = sync_classes() && eng->bound_deltas(blobs, gn, sg, slot, rows, err);  // (term classes the added pods brought)
+    for (size_t i = 0; ok && i < unres.size(); ++i)
+      ok = refresh_program((uint32_t)unres[i].first) && eng->assume((uint32_t)unres[i].first, unres[i].second, -1, err);
     for (size_t i = 0; ok && i < allocs.size(); ++i)
       ok = eng->node_alloc(std::get<0>(allocs[i]), std::get<1>(allocs[i]), std::get<2>(allocs[i]), err);
     if (!ok) {
@@ -1849,11 +2166,13 @@ struct Cluster {
 
   bool compile_queue() {
     if (compiled) return true;
+    for (auto& p : queue) register_classes(p);  // every class first: complete lists in one pass
     progs.assign(queue.size(), {});
     meta.assign(queue.size(), PodMeta());
     for (size_t q = 0; q < queue.size(); ++q)
       if (!compile(queue[q], (int32_t)q, progs[q], meta[q])) return false;
-    if (!eng->set_programs(progs, err)) return false;
+    prog_cls.assign(queue.size(), {(uint32_t)pcls.size(), (uint32_t)tcls.size()});
+    if (!eng->set_programs(progs, err) || !sync_classes()) return false;
     compiled = true;
     return true;
   }
@@ -1926,27 +2245,6 @@ struct Cluster {
     return "";
   }
 
-  // normalized score of one node (host restatement of k_finalize, for finalscore-result)
-  i64 normalize(int pos, i64 s, const ksg_pod_summary& S, bool ignored) const {  // pos: profile position
-    i64 mx = S.max_score[dpos[pos]], mn = S.min_score[dpos[pos]];
-    switch (plugins[pos]) {
-      case P_TAINT: return mx == 0 ? 100 : 100 - 100 * s / mx;
-      case P_NA: return mx == 0 ? s : 100 * s / mx;
-      case P_PTS:
-        if (ignored) return 0;
-        if (mx == 0) return 100;
-        return 100 * (mx + mn - s) / mx;
-      case P_IPA: {
-        if (!(S.ipa_flags & 8u)) return s;
-        i64 diff = mx - mn;
-        double f = 0;
-        if (diff > 0) f = 100.0 * ((double)(s - mn) / (double)diff);
-        return (i64)f;
-      }
-    }
-    return s;
-  }
-
   bool render(uint32_t q, string& out) {
     PodOutputs o;
     if (!eng->outputs(q, o, err)) return false;
@@ -1996,19 +2294,18 @@ struct Cluster {
         skip_s |= 1u << P_VOLBIND;  // PreScore: no scorer (VolumeCapacityPriority off)
         for (int pos = 0; pos < n_plugins; ++pos)
           if (has_prescore(plugins[pos])) pre_score[names[pos]] = (skip_s & (1u << plugins[pos])) ? "" : "success";
-        int pts = pos_of(P_PTS);
+        vector<int32_t> norm;  // NormalizeScore on the device (k_norm_out: the selection's normalize_pos)
+        if (!eng->normalized(q, norm, err)) return false;
         for (uint32_t i = 0; i < n; ++i) {
           if (o.filter[i] != KSG_FILTER_PASS) continue;
           const string& nm = nodes[lo + i].name;
-          bool ignored = false;
-          if (pts >= 0) ignored = pts_ignored(q, i);
           for (int pos = 0; pos < n_plugins; ++pos) {
             int id = plugins[pos];
             if (!has_score(id) || (skip_s & (1u << id))) continue;
-            i64 raw = o.score[(size_t)dpos[pos] * n + i];
+            const i64 raw = o.score[(size_t)dpos[pos] * n + i];
             score[nm][names[pos]] = std::to_string(raw);
-            i64 v = has_ext(id) ? normalize(pos, raw, S, ignored) : raw;
-            fin[nm][names[pos]] = std::to_string(v * store_w[pos]);
+            // applyWeightOnScore (store.go:504-507): normalized x the store's weight
+            fin[nm][names[pos]] = std::to_string((i64)norm[(size_t)dpos[pos] * n + i] * store_w[pos]);
           }
         }
       }
@@ -2069,14 +2366,6 @@ struct Cluster {
     return true;
   }
 
-  // PodTopologySpread IgnoredNodes: feasible node missing a score-constraint key
-  bool pts_ignored(uint32_t q, uint32_t i) const {
-    const Pod& p = queue[q];
-    const Node& nd = nodes[lo + i];
-    for (auto& c : p.tsc)
-      if (c.when == "ScheduleAnyway" && !nd.labels.count(c.key)) return true;
-    return false;
-  }
 };
 
 }  // namespace host
@@ -2163,6 +2452,7 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   if (c.shards != 1 && c.eng->exchange_ranks() != c.shards)
     return ctx->fail("sharded context: call ksg_set_exchange first", KSG_E_STATE);
   if (!c.compile_queue()) return ctx->fail(c.err, KSG_E_INVALID);
+  if (!c.refresh_programs(first, count)) return ctx->fail(c.err, KSG_E_DEVICE);
   if (c.tables_on()) {  // the run appends every scheduled pod to the existing-pod table
     uint64_t need[4] = {0, 0, 0, 0};
     for (uint32_t q = first; q < first + count; ++q) c.queue_need(q, need);

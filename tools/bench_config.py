@@ -31,8 +31,12 @@ def main():
     if a.existing:
         kw["n_existing"] = a.existing
     t0 = time.time()
-    doc = g.generate(a.config, **kw)
-    blob = json.dumps(doc).encode()
+    if a.config in (2, 3, 4, 5):  # native twin of the generator (tests/test_synth.py)
+        blob = g.generate_native(a.config, **kw)
+        doc = json.loads(blob)
+    else:
+        doc = g.generate(a.config, **kw)
+        blob = json.dumps(doc).encode()
     print(f"generated in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
     import torch
     s = Scheduler(doc["profile"])

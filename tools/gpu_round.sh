@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export KSG_PROGRESS=gpurun_out/progress.log
-timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${TEST_ARGS} > gpurun_out/gputest.log 2>&1
+timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest ${TEST_ARGS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gputest.log 2>&1
 rc=$?
 tail -5 gpurun_out/gputest.log
 [ $rc -ne 0 ] && exit $rc

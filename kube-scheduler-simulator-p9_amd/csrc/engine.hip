@@ -1182,6 +1182,9 @@ __device__ void tables_assume(DevCluster& C, const ProgView& V, uint32_t n, int 
   }
 }
 
+__device__ void table_need(const ProgView& V, uint32_t need[4]);
+__device__ void table_write(DevCluster& C, const ProgView& V, uint32_t n, uint32_t row, uint32_t tb, uint32_t rb,
+                            uint32_t vb);
 // assume (scheduleOne -> assume -> NodeInfo.AddPod, or its reversal for
 // Unreserve) of program V on local node n: resource rows, the class tables, and
 // for PTS/IPA profiles the existing-pod table (append; reversal marks the row
@@ -1204,9 +1207,25 @@ __device__ void assume_pod(DevCluster& C, const ProgView& V, uint32_t n, int sig
     return;
   }
   if (!table) return;
-  uint32_t row = C.tcounts[0];
-  uint32_t tb = C.tcounts[1], rb = C.tcounts[2], vb = C.tcounts[3];
-  int ne = h->n_exist_terms;
+  const uint32_t row = C.tcounts[0], tb = C.tcounts[1], rb = C.tcounts[2], vb = C.tcounts[3];
+  uint32_t need[4];
+  table_need(V, need);
+  if (row + need[0] > C.pcap || tb + need[1] > C.tcap || rb + need[2] > C.rcap || vb + need[3] > C.vcap) {
+    C.tcounts[4] = 1;  // overflow: host re-uploads the table from its mirror
+    return;
+  }
+  table_write(C, V, n, row, tb, rb, vb);
+  C.tcounts[0] = row + 1;
+  C.tcounts[1] = tb + need[1];
+  C.tcounts[2] = rb + need[2];
+  C.tcounts[3] = vb + need[3];
+  if (prow) *prow = (int32_t)row;
+}
+
+// Existing-pod table entries program V's row takes: rows, terms, reqs, vals.
+__device__ void table_need(const ProgView& V, uint32_t need[4]) {
+  const ksg_prog* h = V.h;
+  const int ne = h->n_exist_terms;
   uint32_t need_r = 0, need_v = 0;
   for (int i = 0; i < ne; ++i) {
     const ksg_exist_term& e = V.et[h->exist_terms_off + i];
@@ -1214,10 +1233,16 @@ __device__ void assume_pod(DevCluster& C, const ProgView& V, uint32_t n, int sig
     need_v += e.ns_cnt;
     for (int k = 0; k < e.sel.req_cnt; ++k) need_v += V.req[e.sel.req_off + k].nvals;
   }
-  if (row >= C.pcap || tb + ne > C.tcap || rb + need_r > C.rcap || vb + need_v > C.vcap) {
-    C.tcounts[4] = 1;  // overflow: host re-uploads the table from its mirror
-    return;
-  }
+  need[0] = 1;
+  need[1] = (uint32_t)ne;
+  need[2] = need_r;
+  need[3] = need_v;
+}
+// Write program V's existing-pod row (on local node n) and its terms at the given offsets.
+__device__ void table_write(DevCluster& C, const ProgView& V, uint32_t n, uint32_t row, uint32_t tb, uint32_t rb,
+                            uint32_t vb) {
+  const ksg_prog* h = V.h;
+  const int ne = h->n_exist_terms;
   C.ptnode[row] = (int32_t)n;
   C.ptns[row] = h->ns_id;
   C.ptflags[row] = h->exist_flags;
@@ -1241,11 +1266,6 @@ __device__ void assume_pod(DevCluster& C, const ProgView& V, uint32_t n, int sig
     C.tpod[tb] = (int32_t)row;
     tb++;
   }
-  C.tcounts[0] = row + 1;
-  C.tcounts[1] = tb;
-  C.tcounts[2] = rb;
-  C.tcounts[3] = vb;
-  if (prow) *prow = (int32_t)row;
 }
 
 // selectHost result of the cycle; mode bit 0: assume on the selected node,
@@ -1438,7 +1458,6 @@ __global__ void k_assume(DevCluster C, const uint8_t* prog, int32_t gnode, int s
   assume_pod(C, V, n, sign, table != 0, prow);
 }
 
-#include "table_chain.hip"
 
 // ----------------------------------------------------------------- what-if batches (cfg5)
 // A step of `count` queue pods is scheduled against ONE frozen snapshot (no
@@ -3353,6 +3372,8 @@ __global__ __launch_bounds__(64) void k_window_gmerge(const uint8_t* recv, uint3
 }
 
 // ----------------------------------------------------------------- host side
+#include "table_chain.hip"
+
 template <class T>
 struct DBuf {
   T* p = nullptr;
@@ -3470,7 +3491,8 @@ struct Engine::Impl {
   uint32_t npc = 0, ntc = 0, NU = 0, nct = 0, ncreq = 0, ncval = 0, tc_used = 0;
   std::vector<uint32_t> tc_off_h;
   // table chain (k_eval / k_ptsraw / k_final / k_select)
-  DBuf<uint32_t> cur;
+  DBuf<uint32_t> cur, alog_n;
+  DBuf<int2> alog;        // assumes whose existing-pod table rows k_flush_appends writes
   DBuf<int32_t> cpi, cpst;
   DBuf<int64_t> cpm, cpm2;
   DBuf<uint64_t> cpr, cpk;
@@ -3725,10 +3747,12 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     if (!I.nu_base_d.upload(nb, s, err) || !I.slot_dom_d.upload(sd, s, err) || !I.pair_node_d.upload(pn, s, err))
       return false;
     I.cnblk = std::max<uint32_t>((ns.n + kBlock - 1) / kBlock, 1);
-    if (!I.cur.alloc(1, err) || !I.cpi.alloc((size_t)KCP_I * I.cnblk, err) || !I.cpst.alloc(I.cnblk, err) ||
+    if (!I.cur.alloc(1, err) || !I.alog_n.alloc(1, err) || !I.cpi.alloc((size_t)KCP_I * I.cnblk, err) ||
+        !I.cpst.alloc(I.cnblk, err) ||
         !I.cpm.alloc((size_t)2 * KCP_X * I.cnblk, err) || !I.cpm2.alloc((size_t)2 * I.cnblk, err) ||
         !I.cpr.alloc((size_t)KSG_MAX_TSC * I.cnblk, err) || !I.cpk.alloc(I.cnblk, err))
       return false;
+    HIPCHK(hipMemsetAsync(I.alog_n.p, 0, sizeof(uint32_t), s));
   }
   // existing-pod table (capacity for device-side appends)
   I.pcap = std::max<uint32_t>(pod_cap, pt.n);
@@ -4476,14 +4500,26 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   CA.pi = I.cpi.p; CA.pm = I.cpm.p; CA.pr = I.cpr.p; CA.pm2 = I.cpm2.p; CA.pk = I.cpk.p; CA.pst = I.cpst.p;
   CA.mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
   CA.prow = I.prow.p;
+  CA.need_eph = I.any_eph_req ? 1u : 0u;
+  if (!I.alog.alloc(std::max<uint32_t>(count, 1), err)) return false;
+  CA.alog = I.alog.p;
+  CA.alog_n = I.alog_n.p;
+  const int rowm = I.R > 4 ? 0 : (I.eval_mode == 1 ? 2 : 1);
   uint32_t cur_at = 0xFFFFFFFFu;  // the device pod counter holds this queue index
+  bool pending = false;           // logged assumes whose existing-pod table rows are not written yet
+  auto flush = [&]() {
+    if (pending) hipLaunchKernelGGL(k_flush_appends, dim3(1), b, 0, s, C, CA);
+    pending = false;
+  };
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
     if (!xchain && (I.prog_need[j] & 4)) {
       if (cur_at != j) hipLaunchKernelGGL(k_set_cur, dim3(1), dim3(64), 0, s, I.cur.p, j);
       const bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
       if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
-      hipLaunchKernelGGL(k_eval, dim3(I.cnblk), b, 0, s, C, F, CA);
+      if (rowm == 2) hipLaunchKernelGGL(k_eval<2>, dim3(I.cnblk), b, 0, s, C, F, CA);
+      else if (rowm == 1) hipLaunchKernelGGL(k_eval<1>, dim3(I.cnblk), b, 0, s, C, F, CA);
+      else hipLaunchKernelGGL(k_eval<0>, dim3(I.cnblk), b, 0, s, C, F, CA);
       if (sampled) {
         HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
         I.n_samples++;
@@ -4494,8 +4530,10 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
       }
       hipLaunchKernelGGL(k_select, dim3(1), b, 0, s, C, F, CA);
       cur_at = j + 1;
+      pending |= (CA.mode & 2) != 0;
       continue;
     }
+    flush();  // the scanning chain reads the existing-pod table
     cur_at = 0xFFFFFFFFu;
     const int mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
     DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j, xchain ? nullptr : I.arrive1.p, mode, I.prow.p + j};
@@ -4563,6 +4601,7 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
     }
     // unsharded: selectHost + assume folded into the last block of the cycle's last kernel
   }
+  flush();
   HIPCHK(hipEventRecord(I.ev1, s));
   HIPCHK(hipGetLastError());
   return true;

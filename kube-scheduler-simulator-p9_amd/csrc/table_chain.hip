@@ -9,14 +9,16 @@
 //            PodTopologySpread's registered domains) — no global atomics
 //   k_ptsraw PodTopologySpread raw scores when the pod has several score
 //            constraints (one constraint: max / min follow from the counts)
-//   k_final  every block reduces the partials it needs, then per node:
-//            NormalizeScore, [0,100] check, weights, packed argmax key; per
-//            block the best key
+//   k_final  every block folds the partials, then per node: NormalizeScore,
+//            [0,100] check, weights, packed argmax key; per block the best key
 //   k_select one block: selectHost over the block keys, the summary, and the
-//            assume (node row, class tables, existing-pod table)
+//            assume delta (node row, class tables; the existing-pod table row
+//            is logged and written by k_flush_appends after the run)
 //
-// The pod index lives on the device (A.cur, advanced by k_select), so a run of
-// pods is the same launches repeated (and a HIP graph can replay them).
+// Every node's inputs are loaded up front (the row, the topology values, the
+// class-table counts the pod reads) so their latencies overlap; block
+// reductions take one barrier.  The pod index lives on the device (A.cur,
+// advanced by k_select): a run is the same launches repeated.
 // Upstream: schedule_one.go findNodesThatPassFilters / prioritizeNodes /
 // selectHost, framework.go RunFilterPlugins / RunScorePlugins, the plugins'
 // Filter / Score / NormalizeScore (restated in oracle/ksg_oracle.cpp).
@@ -33,6 +35,7 @@ struct ChainArgs {
   uint32_t* filter;        // outputs of pods not kept
   int32_t *score, *total;
   uint32_t nblk;           // blocks of k_eval / k_ptsraw / k_final
+  uint32_t need_eph;       // some pod requests a resource column beyond cpu / memory
   int32_t* pi;             // [KCP_I][nblk] feasible, ignored, status bits
   int64_t* pm;             // [2 * KCP_X][nblk] normaliser max / min per normalised plugin
   uint64_t* pr;            // [KSG_MAX_TSC][nblk] registered values of small score keys (bit = value)
@@ -41,6 +44,8 @@ struct ChainArgs {
   int32_t* pst;            // [nblk] status bits of k_final
   int mode;                // commit mode (as k_commit)
   int32_t* prow;           // existing-pod table row of each queue pod
+  int2* alog;              // (queue pod, local node) of the assumes whose table rows are pending
+  uint32_t* alog_n;
 };
 
 enum { KCP_FEAS = 0, KCP_IGN = 1, KCP_STAT = 2, KCP_I = 3 };
@@ -64,16 +69,117 @@ __device__ __forceinline__ void chain_outs(const ChainArgs& A, uint32_t q, uint3
   }
 }
 
-// block reductions through LDS (one value per wave, then lane 0 of wave 0)
-template <class T, class Op>
-__device__ __forceinline__ T block_reduce(T v, T* red, Op op) {
-  const int w = threadIdx.x >> 6;
+__device__ __forceinline__ uint64_t wave_or64(uint64_t m) {
+  return (uint64_t)__ockl_wfred_or_u32((uint32_t)m) | ((uint64_t)__ockl_wfred_or_u32((uint32_t)(m >> 32)) << 32);
+}
+__device__ __forceinline__ int32_t wave_or(int32_t m) { return (int32_t)__ockl_wfred_or_u32((uint32_t)m); }
+
+// The per-block / per-pod record the chain reduces.
+struct ChainRec {
+  int32_t feas, ign, st, pad;
+  int64_t mx[KCP_X], mn[KCP_X];
+  uint64_t reg[KSG_MAX_TSC];
+  uint64_t key;
+};
+__device__ __forceinline__ void rec_init(ChainRec& r) {
+  r.feas = r.ign = r.st = r.pad = 0;
+#pragma unroll
+  for (int x = 0; x < KCP_X; ++x) {
+    r.mx[x] = INT64_MIN;
+    r.mn[x] = INT64_MAX;
+  }
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c) r.reg[c] = 0;
+  r.key = 0;
+}
+__device__ __forceinline__ void rec_fold(ChainRec& a, const ChainRec& b) {
+  a.feas += b.feas;
+  a.ign += b.ign;
+  a.st |= b.st;
+#pragma unroll
+  for (int x = 0; x < KCP_X; ++x) {
+    a.mx[x] = b.mx[x] > a.mx[x] ? b.mx[x] : a.mx[x];
+    a.mn[x] = b.mn[x] < a.mn[x] ? b.mn[x] : a.mn[x];
+  }
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c) a.reg[c] |= b.reg[c];
+  a.key = b.key > a.key ? b.key : a.key;
+}
+// run-time slot x of a record's normaliser arrays without dynamic indexing
+// (which would place the record in scratch)
+__device__ __forceinline__ void rec_minmax(ChainRec& r, int x, int64_t v) {
+#pragma unroll
+  for (int i = 0; i < KCP_X; ++i)
+    if (i == x) {
+      r.mx[i] = v > r.mx[i] ? v : r.mx[i];
+      r.mn[i] = v < r.mn[i] ? v : r.mn[i];
+    }
+}
+__device__ __forceinline__ int64_t rec_mx(const ChainRec& r, int x) {
+  int64_t v = INT64_MIN;
+#pragma unroll
+  for (int i = 0; i < KCP_X; ++i) v = i == x ? r.mx[i] : v;
+  return v;
+}
+__device__ __forceinline__ int64_t rec_mn(const ChainRec& r, int x) {
+  int64_t v = INT64_MAX;
+#pragma unroll
+  for (int i = 0; i < KCP_X; ++i) v = i == x ? r.mn[i] : v;
+  return v;
+}
+// field-wise copies (an aggregate copy to / from LDS would put the record in scratch)
+__device__ __forceinline__ void rec_store(ChainRec* d, const ChainRec& r) {
+  d->feas = r.feas;
+  d->ign = r.ign;
+  d->st = r.st;
+#pragma unroll
+  for (int x = 0; x < KCP_X; ++x) {
+    d->mx[x] = r.mx[x];
+    d->mn[x] = r.mn[x];
+  }
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c) d->reg[c] = r.reg[c];
+  d->key = r.key;
+}
+__device__ __forceinline__ void rec_load(ChainRec& r, const ChainRec* d) {
+  r.feas = d->feas;
+  r.ign = d->ign;
+  r.st = d->st;
+#pragma unroll
+  for (int x = 0; x < KCP_X; ++x) {
+    r.mx[x] = d->mx[x];
+    r.mn[x] = d->mn[x];
+  }
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c) r.reg[c] = d->reg[c];
+  r.key = d->key;
+}
+// Block reduction of a record: wave folds on the DPP, one LDS record per wave,
+// one barrier; every thread returns the block's record.  xmask / nreg: the
+// normaliser slots / registration masks in use (the rest stay at their identity).
+__device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t xmask, int nreg) {
+  r.feas = wave_sum(r.feas);
+  r.ign = wave_sum(r.ign);
+  r.st = wave_or(r.st);
+#pragma unroll
+  for (int x = 0; x < KCP_X; ++x)
+    if ((xmask >> x) & 1u) {
+      r.mx[x] = wave_max(r.mx[x]);
+      r.mn[x] = wave_min(r.mn[x]);
+    }
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c)
+    if (c < nreg) r.reg[c] = wave_or64(r.reg[c]);
+  r.key = wave_max(r.key);
+  if (lane0()) rec_store(lds + (threadIdx.x >> 6), r);
   __syncthreads();
-  if (lane0()) red[w] = v;
-  __syncthreads();
-  T r = red[0];
-  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = op(r, red[i]);
-  return r;
+  rec_load(r, lds);
+#pragma unroll
+  for (int i = 1; i < kBlock / 64; ++i) {
+    ChainRec o;
+    rec_load(o, lds + i);
+    rec_fold(r, o);
+  }
 }
 
 // PodTopologySpread score count of constraint c at local node n (its pair's
@@ -91,7 +197,7 @@ __device__ __forceinline__ int64_t pts_count_tab(const DevCluster& C, const Prog
 // required term on a node with a term's key), bit2 an existing pod's required
 // anti-affinity term matches the pod (existingAntiAffinityCounts), bit3 the
 // topology score map is non-empty (PreScore not Skip).
-__device__ uint32_t ipa_table_bits(const DevCluster& C, const DevProfile& F, const ProgView& V) {
+__device__ __forceinline__ uint32_t ipa_table_bits(const DevCluster& C, const DevProfile& F, const ProgView& V) {
   const ksg_prog* h = V.h;
   const ksg_aterm* aff = V.at + h->aterm_off;
   const ksg_aterm* pref = aff + h->n_req_aff + h->n_req_anti;
@@ -117,24 +223,23 @@ __device__ uint32_t ipa_table_bits(const DevCluster& C, const DevProfile& F, con
   return bits;
 }
 
-// Pod-uniform inputs of k_eval, per block: minMatchNum of every filter
-// constraint (the smallest count over the key's values present on nodes) and
-// InterPodAffinity's map-emptiness bits.
 struct EvalShared {
   int32_t tv[KSG_MAX_TOPO * kBlock];
   int32_t minm[KSG_MAX_TSC];
   uint32_t ipa_flags;
-  int64_t red64[kBlock / 64];
-  uint64_t redu[kBlock / 64];
-  int32_t red32[kBlock / 64];
+  ChainRec rec[kBlock / 64];
 };
 
-__device__ void eval_setup(const DevCluster& C, const DevProfile& F, const ProgView& V, EvalShared& L, bool pts_on,
+// Pod-uniform inputs of k_eval, per block: minMatchNum of every filter
+// constraint (the smallest count over the key's values present on nodes) and
+// InterPodAffinity's map-emptiness bits.  LDS-only barriers: the node loads
+// issued before stay in flight.
+__device__ __forceinline__ void eval_setup(const DevCluster& C, const DevProfile& F, const ProgView& V, EvalShared& L, bool pts_on,
                            bool ipa_on) {
   const ksg_prog* h = V.h;
   if (threadIdx.x < KSG_MAX_TSC) L.minm[threadIdx.x] = 0x7FFFFFFF;
   if (threadIdx.x == 0) L.ipa_flags = 0;
-  __syncthreads();
+  lds_barrier();
   if (pts_on && !(h->flags & KPF_SKIP_PTS_FILTER)) {
     for (int c = 0; c < h->n_tsc_filter; ++c) {
       const ksg_tsc& t = h->tsc[c];
@@ -153,9 +258,13 @@ __device__ void eval_setup(const DevCluster& C, const DevProfile& F, const ProgV
     const uint32_t bits = __ockl_wfred_or_u32(ipa_table_bits(C, F, V));
     if (lane0() && bits) atomicOr(&L.ipa_flags, bits);
   }
-  __syncthreads();
+  lds_barrier();
 }
 
+// ROWM: 0 resource columns read by the plugins (more than 4 columns), 1 the
+// node row loaded up front (RowV), 2 the same with the default Fit / BA
+// arguments compiled in.
+template <int ROWM>
 __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, ChainArgs A) {
   const uint32_t q = *A.cur;
   if (q >= A.end) return;
@@ -167,18 +276,70 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
   chain_outs(A, q, C.N, of, os, ot);
   const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
   const bool active = n < C.N;
+  const uint32_t nn = active ? n : 0;  // loads of inactive lanes read node 0 (results unused)
+  RowV row;
+  if (ROWM) load_row(C, nn, A.need_eph, row);
   int pts_pos = -1, ipa_pos = -1;
+  uint32_t xmask = 0;
   for (int p = 0; p < F.n; ++p) {
     if (F.plugins[p] == KP_PTS) pts_pos = p;
     if (F.plugins[p] == KP_IPA) ipa_pos = p;
+    const int x = chain_x(F.plugins[p]);
+    if (x >= 0) xmask |= 1u << x;
   }
-  load_slot_vids(C, n, active, L.tv);
+  load_slot_vids(C, nn, true, L.tv);
   const SlotVids tv{L.tv + threadIdx.x};
-  eval_setup(C, F, V, L, pts_pos >= 0, ipa_pos >= 0);
-  const uint32_t ipa_flags = L.ipa_flags;
   const ksg_aterm* aff = V.at + h->aterm_off;
   const ksg_aterm* anti = aff + h->n_req_aff;
   const ksg_aterm* pref = anti + h->n_req_anti;
+  const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
+  const bool pts_score = pts_pos >= 0 && ns > 0 && !(h->flags & KPF_SKIP_PTS_SCORE);
+  const bool score_on = !(F.ipa_ignore_existing_pref && !(h->flags & KPF_IPA_HAS_CONSTRAINTS));
+  // class-table counts this node's verdicts and scores read, loaded before the
+  // pod-uniform setup so that their latencies overlap it
+  int32_t ptsm[KSG_MAX_TSC];
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c) {
+    ptsm[c] = 0;
+    if (pts_pos >= 0 && c < nf) ptsm[c] = pc_count(C, h->tsc[c].eff_cls, h->tsc[c].topo, nn, tv(h->tsc[c].topo));
+  }
+  bool counted = pts_score;
+  int64_t pts_cnt = 0;
+  if (pts_score) {
+    for (int c = nf; c < nf + ns; ++c) counted &= tv(h->tsc[c].topo) >= 0;
+    if (counted && !(h->tab & KTAB_PTS_MULTI)) pts_cnt = pts_count_tab(C, V, nf, nn, tv(h->tsc[nf].topo));
+  }
+  bool aff_miss = false, aff_zero = false, anti_hit = false, exist_hit = false;
+  int64_t ipa_raw = 0;
+  if (ipa_pos >= 0) {
+    for (int i = 0; i < h->n_req_aff; ++i) {
+      const int32_t v = tv(aff[i].topo);
+      aff_miss |= v < 0;
+      aff_zero |= pc_count(C, h->aff_cls, aff[i].topo, nn, v) <= 0;
+    }
+    for (int i = 0; i < h->n_req_anti; ++i) {
+      const int32_t v = tv(anti[i].topo);
+      anti_hit |= v >= 0 && pc_count(C, anti[i].cls, anti[i].topo, nn, v) > 0;
+    }
+    if (h->flags & KPF_IPA_HAS_CONSTRAINTS)
+      for (int i = 0; i < h->n_pref_aff + h->n_pref_anti; ++i) {
+        const ksg_aterm& t = pref[i];
+        const int64_t k = pc_count(C, t.cls, t.topo, nn, tv(t.topo));
+        ipa_raw += i < h->n_pref_aff ? k * t.weight : -k * t.weight;
+      }
+    for (int i = 0; i < h->n_tc_match; ++i) {
+      const int grp = V.i32[h->tc_match_off + h->n_tc_match + i];
+      const int32_t u = V.i32[h->tc_match_off + i];
+      if (grp == KSG_TC_ANTI) {
+        exist_hit |= tc_value(C, u, nn, tv(C.T.tc_slot[u])) > 0;
+      } else if (score_on && (grp == KSG_TC_PREF || F.ipa_hard_weight > 0)) {
+        const int64_t k = tc_value(C, u, nn, tv(C.T.tc_slot[u]));
+        ipa_raw += grp == KSG_TC_HARD ? k * F.ipa_hard_weight : k;
+      }
+    }
+  }
+  eval_setup(C, F, V, L, pts_pos >= 0, ipa_pos >= 0);
+  const uint32_t ipa_flags = L.ipa_flags;
   uint32_t code = KSG_FILTER_NOT_EVALUATED;
   bool err = false;
   if (active && !(h->flags & KPF_PREFILTER_REJECT) &&
@@ -190,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
       bool fail = false;
       switch (F.plugins[pos]) {
         case KP_FIT: {
-          const uint32_t b = fit_filter(C, V, n);
+          const uint32_t b = ROWM ? fit_filter_row(row, h, C.R) : fit_filter(C, V, n);
           if (b) { fail = true; detail = b; }
           break;
         }
@@ -204,44 +365,29 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
           break;
         case KP_PTS:  // filtering.go: skew = matchNum + selfMatch - minMatchNum > maxSkew
           if (!(h->flags & KPF_SKIP_PTS_FILTER))
-            for (int c = 0; c < h->n_tsc_filter; ++c) {
+#pragma unroll
+            for (int c = 0; c < KSG_MAX_TSC; ++c) {
+              if (c >= nf || fail || err) continue;
               const ksg_tsc& t = h->tsc[c];
-              const int32_t v = tv(t.topo);
               const int32_t dom = C.T.slot_dom[t.topo];
-              if (v < 0) { fail = true; detail = KSG_PTS_MISSING_LABEL; break; }
-              if (dom == 0) { err = true; break; }  // minMatchNum: no domains -> Error
+              if (tv(t.topo) < 0) { fail = true; detail = KSG_PTS_MISSING_LABEL; continue; }
+              if (dom == 0) { err = true; continue; }  // minMatchNum: no domains -> Error
               const int64_t mn = dom < t.min_domains ? 0 : L.minm[c];
-              if ((int64_t)pc_count(C, t.eff_cls, t.topo, n, v) + t.self_match - mn > t.max_skew) {
-                fail = true;
-                detail = KSG_PTS_SKEW;
-                break;
-              }
+              if ((int64_t)ptsm[c] + t.self_match - mn > t.max_skew) { fail = true; detail = KSG_PTS_SKEW; }
             }
           break;
-        case KP_IPA: {  // filtering.go: affinity, anti-affinity, existing pods' anti-affinity
-          bool pods_exist = true, miss = false;
-          for (int i = 0; i < h->n_req_aff; ++i) {
-            const int32_t v = tv(aff[i].topo);
-            if (v < 0) { miss = true; break; }
-            if (pc_count(C, h->aff_cls, aff[i].topo, n, v) <= 0) pods_exist = false;
-          }
-          if (miss || (!pods_exist && !(!(ipa_flags & 1u) && h->self_matches_all))) {
+        case KP_IPA:  // filtering.go: affinity, anti-affinity, existing pods' anti-affinity
+          if (aff_miss || (h->n_req_aff > 0 && aff_zero && !(!(ipa_flags & 1u) && h->self_matches_all))) {
             fail = true;
             detail = KSG_IPA_AFFINITY;
-            break;
+          } else if (anti_hit) {
+            fail = true;
+            detail = KSG_IPA_ANTI_AFFINITY;
+          } else if ((ipa_flags & 4u) && exist_hit) {
+            fail = true;
+            detail = KSG_IPA_EXISTING_ANTI;
           }
-          for (int i = 0; i < h->n_req_anti && !fail; ++i) {
-            const int32_t v = tv(anti[i].topo);
-            if (v >= 0 && pc_count(C, anti[i].cls, anti[i].topo, n, v) > 0) { fail = true; detail = KSG_IPA_ANTI_AFFINITY; }
-          }
-          if (!fail && (ipa_flags & 4u))
-            for (int i = 0; i < h->n_tc_match; ++i) {
-              if (V.i32[h->tc_match_off + h->n_tc_match + i] != KSG_TC_ANTI) continue;
-              const int32_t u = V.i32[h->tc_match_off + i];
-              if (tc_value(C, u, n, tv(C.T.tc_slot[u])) > 0) { fail = true; detail = KSG_IPA_EXISTING_ANTI; break; }
-            }
           break;
-        }
         case KP_UNSCHED: fail = unsched_fails(C, V, n); break;
         case KP_NODENAME: fail = nodename_fails(C, V, n); break;
         case KP_PORTS:
@@ -257,160 +403,117 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
   }
   const bool feasible = active && code == KSG_FILTER_PASS;
   if (active) of[n] = code;
-  // raw scores, the normalisers' inputs, PodTopologySpread registration
-  const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
-  const bool pts_score = pts_pos >= 0 && ns > 0 && !(h->flags & KPF_SKIP_PTS_SCORE);
-  bool counted = false;
-  if (feasible && pts_score) {
-    counted = true;
-    for (int c = nf; c < nf + ns; ++c) counted &= tv(h->tsc[c].topo) >= 0;
-  }
-  int64_t mx[KCP_X], mn[KCP_X];
-#pragma unroll
-  for (int x = 0; x < KCP_X; ++x) {
-    mx[x] = INT64_MIN;
-    mn[x] = INT64_MAX;
-  }
+  counted &= feasible;
+  ChainRec rec;
+  rec_init(rec);
   int64_t tot = 0;
   bool range_err = false;
   if (feasible) {
-    const bool score_on = !(F.ipa_ignore_existing_pref && !(h->flags & KPF_IPA_HAS_CONSTRAINTS));
 #pragma unroll 1
     for (int pos = 0; pos < F.n; ++pos) {
       const int p = F.plugins[pos];
       int64_t sc = 0;
       switch (p) {
-        case KP_FIT: sc = fit_score(C, F, V, n); break;
-        case KP_BA: sc = ba_score(C, F, V, n); break;
+        case KP_FIT:
+          sc = ROWM == 2 ? fit_score_row<1>(row, F, h) : ROWM == 1 ? fit_score_row<0>(row, F, h) : fit_score(C, F, V, n);
+          break;
+        case KP_BA:
+          sc = ROWM == 2 ? ba_score_row<1>(row, F, h) : ROWM == 1 ? ba_score_row<0>(row, F, h) : ba_score(C, F, V, n);
+          break;
         case KP_TAINT: sc = taint_score(C, V, n); break;
         case KP_NA: sc = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n); break;
         case KP_IMAGE: sc = image_score(C, V, n); break;
-        case KP_IPA: {  // scoring.go: the topology score map, read at the node's (key, value) pairs
-          if (h->flags & KPF_IPA_HAS_CONSTRAINTS)
-            for (int i = 0; i < h->n_pref_aff + h->n_pref_anti; ++i) {
-              const ksg_aterm& t = pref[i];
-              const int64_t k = pc_count(C, t.cls, t.topo, n, tv(t.topo));
-              sc += i < h->n_pref_aff ? k * t.weight : -k * t.weight;
-            }
-          if (score_on)
-            for (int i = 0; i < h->n_tc_match; ++i) {
-              const int grp = V.i32[h->tc_match_off + h->n_tc_match + i];
-              if (grp == KSG_TC_ANTI || (grp == KSG_TC_HARD && F.ipa_hard_weight <= 0)) continue;
-              const int32_t u = V.i32[h->tc_match_off + i];
-              const int64_t k = tc_value(C, u, n, tv(C.T.tc_slot[u]));
-              sc += grp == KSG_TC_HARD ? k * F.ipa_hard_weight : k;
-            }
-          break;
-        }
+        case KP_IPA: sc = ipa_raw; break;  // scoring.go: the topology score map at the node's pairs
         case KP_PTS:  // the count of the single score constraint (or a placeholder); -1: ignored node
-          if (!pts_score) sc = 0;
-          else if (!counted) sc = -1;
-          else if (h->tab & KTAB_PTS_MULTI) sc = 0;
-          else sc = pts_count_tab(C, V, nf, n, tv(h->tsc[nf].topo));
+          sc = !pts_score ? 0 : (!counted ? -1 : ((h->tab & KTAB_PTS_MULTI) ? 0 : pts_cnt));
           break;
         default: break;
       }
       os[(size_t)pos * C.N + n] = (int32_t)sc;
       const int x = chain_x(p);
-      if (x >= 0 && (p != KP_PTS || counted)) {
-        mx[x] = sc > mx[x] ? sc : mx[x];
-        mn[x] = sc < mn[x] ? sc : mn[x];
-      }
+      if (x >= 0 && (p != KP_PTS || counted)) rec_minmax(rec, x, sc);
       if (!F.has_ext) {
         if (sc < 0 || sc > 100) range_err = true;
         tot += sc * F.weight[pos];
       }
     }
   }
-  // per block partials
-  const uint32_t b = blockIdx.x, NB = A.nblk;
-  const int32_t feas = block_reduce<int32_t>(wave_sum(feasible ? 1 : 0), L.red32, [](int32_t x, int32_t y) { return x + y; });
-  const int32_t ign = block_reduce<int32_t>(wave_sum(feasible && pts_score && !counted ? 1 : 0), L.red32,
-                                            [](int32_t x, int32_t y) { return x + y; });
-  const int32_t st = block_reduce<int32_t>((int32_t)__ockl_wfred_or_u32((err ? 2u : 0u) | (range_err ? 4u : 0u)), L.red32,
-                                           [](int32_t x, int32_t y) { return x | y; });
-  if (threadIdx.x == 0) {
-    A.pi[KCP_FEAS * NB + b] = feas;
-    A.pi[KCP_IGN * NB + b] = ign;
-    A.pi[KCP_STAT * NB + b] = st;
-  }
+  rec.feas = feasible ? 1 : 0;
+  rec.ign = feasible && pts_score && !counted ? 1 : 0;
+  rec.st = (err ? 2 : 0) | (range_err ? 4 : 0);
+  int nreg = 0;
   if (F.has_ext) {
+    nreg = ns;
 #pragma unroll
-    for (int x = 0; x < KCP_X; ++x) {
-      const int64_t a = block_reduce<int64_t>(wave_max(mx[x]), L.red64, [](int64_t u, int64_t w) { return u > w ? u : w; });
-      const int64_t c = block_reduce<int64_t>(wave_min(mn[x]), L.red64, [](int64_t u, int64_t w) { return u < w ? u : w; });
-      if (threadIdx.x == 0) {
-        A.pm[(2 * x) * NB + b] = a;
-        A.pm[(2 * x + 1) * NB + b] = c;
-      }
+    for (int c = 0; c < KSG_MAX_TSC; ++c) {  // registered values of the score constraints' small keys (initPreScoreState)
+      if (c >= ns) continue;
+      const ksg_tsc& t = h->tsc[nf + c];
+      const int32_t v = tv(t.topo);
+      if (counted && !t.is_hostname && t.first_of_key && !((C.T.uniq >> t.topo) & 1u) && v < KSG_TAB_REGV)
+        rec.reg[c] = 1ull << v;
     }
-    for (int c = nf; c < nf + ns; ++c) {  // registered values of the score constraints' small keys (initPreScoreState)
-        const ksg_tsc& t = h->tsc[c];
-        uint64_t m = 0;
-        const int32_t v = tv(t.topo);
-        if (counted && !t.is_hostname && t.first_of_key && !((C.T.uniq >> t.topo) & 1u) && v < KSG_TAB_REGV)
-          m = 1ull << v;
-        m = (uint64_t)__ockl_wfred_or_u32((uint32_t)m) | ((uint64_t)__ockl_wfred_or_u32((uint32_t)(m >> 32)) << 32);
-        const uint64_t all = block_reduce<uint64_t>(m, L.redu, [](uint64_t u, uint64_t w) { return u | w; });
-        if (threadIdx.x == 0) A.pr[(size_t)(c - nf) * NB + b] = all;
+  } else if (feasible) {
+    ot[n] = (int32_t)tot;
+    rec.key = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
+  }
+  rec_block(rec, L.rec, F.has_ext ? xmask : 0u, nreg);
+  if (threadIdx.x == 0) {
+    const uint32_t b = blockIdx.x, NB = A.nblk;
+    A.pi[KCP_FEAS * NB + b] = rec.feas;
+    A.pi[KCP_IGN * NB + b] = rec.ign;
+    A.pi[KCP_STAT * NB + b] = rec.st;
+    if (F.has_ext) {
+#pragma unroll
+      for (int x = 0; x < KCP_X; ++x) {
+        A.pm[(2 * x) * NB + b] = rec.mx[x];
+        A.pm[(2 * x + 1) * NB + b] = rec.mn[x];
       }
-  } else {
-    const uint64_t key = feasible ? pack_key(tot, F.seed, h->queue_idx, C.goff + n) : 0;
-    if (feasible) ot[n] = (int32_t)tot;
-    const uint64_t best = block_reduce<uint64_t>(wave_max(key), L.redu, [](uint64_t u, uint64_t w) { return u > w ? u : w; });
-    if (threadIdx.x == 0) {
-      A.pk[b] = best;
+#pragma unroll
+      for (int c = 0; c < KSG_MAX_TSC; ++c)
+        if (c < nreg) A.pr[(size_t)c * NB + b] = rec.reg[c];
+    } else {
+      A.pk[b] = rec.key;
       A.pst[b] = 0;
     }
   }
 }
 
-// Reduce k_eval's partials (every block of k_ptsraw / k_final does it for itself).
+// k_eval's partials folded (every block of k_ptsraw / k_final does it for itself)
+// and topologyNormalizingWeight per score constraint.
 struct EvalTotals {
-  int32_t feasible, ignored, status;
-  int64_t mx[KCP_X], mn[KCP_X];
-  uint64_t reg[KSG_MAX_TSC];
+  ChainRec r;
   double w[KSG_MAX_TSC];
 };
-__device__ void reduce_eval(const ChainArgs& A, const ksg_prog* h, uint32_t C_uniq, EvalTotals& E, int64_t* red64,
-                            uint64_t* redu, int32_t* red32) {
+__device__ __forceinline__ void reduce_eval(const DevCluster& C, const ChainArgs& A, const ksg_prog* h, EvalTotals& E, ChainRec* lds) {
   const uint32_t NB = A.nblk;
-  int32_t f = 0, ig = 0, st = 0;
-  int64_t mx[KCP_X], mn[KCP_X];
-  for (int x = 0; x < KCP_X; ++x) { mx[x] = INT64_MIN; mn[x] = INT64_MAX; }
-  uint64_t reg[KSG_MAX_TSC] = {};
   const int ns = h->n_tsc_score;
+  ChainRec& r = E.r;
+  rec_init(r);
   for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) {
-    f += A.pi[KCP_FEAS * NB + b];
-    ig += A.pi[KCP_IGN * NB + b];
-    st |= A.pi[KCP_STAT * NB + b];
+    r.feas += A.pi[KCP_FEAS * NB + b];
+    r.ign += A.pi[KCP_IGN * NB + b];
+    r.st |= A.pi[KCP_STAT * NB + b];
+#pragma unroll
     for (int x = 0; x < KCP_X; ++x) {
       const int64_t a = A.pm[(2 * x) * NB + b], c = A.pm[(2 * x + 1) * NB + b];
-      mx[x] = a > mx[x] ? a : mx[x];
-      mn[x] = c < mn[x] ? c : mn[x];
+      r.mx[x] = a > r.mx[x] ? a : r.mx[x];
+      r.mn[x] = c < r.mn[x] ? c : r.mn[x];
     }
-    for (int c = 0; c < ns; ++c) reg[c] |= A.pr[(size_t)c * NB + b];
+#pragma unroll
+    for (int c = 0; c < KSG_MAX_TSC; ++c)
+      if (c < ns) r.reg[c] |= A.pr[(size_t)c * NB + b];
   }
-  E.feasible = block_reduce<int32_t>(wave_sum(f), red32, [](int32_t x, int32_t y) { return x + y; });
-  E.ignored = block_reduce<int32_t>(wave_sum(ig), red32, [](int32_t x, int32_t y) { return x + y; });
-  E.status = block_reduce<int32_t>((int32_t)__ockl_wfred_or_u32((uint32_t)st), red32, [](int32_t x, int32_t y) { return x | y; });
-  for (int x = 0; x < KCP_X; ++x) {
-    E.mx[x] = block_reduce<int64_t>(wave_max(mx[x]), red64, [](int64_t u, int64_t w) { return u > w ? u : w; });
-    E.mn[x] = block_reduce<int64_t>(wave_min(mn[x]), red64, [](int64_t u, int64_t w) { return u < w ? u : w; });
-  }
-  for (int c = 0; c < ns; ++c) {
-    const uint64_t m = (uint64_t)__ockl_wfred_or_u32((uint32_t)reg[c]) |
-                       ((uint64_t)__ockl_wfred_or_u32((uint32_t)(reg[c] >> 32)) << 32);
-    E.reg[c] = block_reduce<uint64_t>(m, redu, [](uint64_t u, uint64_t w) { return u | w; });
-  }
-  // topologyNormalizingWeight per score constraint (scoring.go initPreScoreState)
+  rec_block(r, lds, (1u << KCP_X) - 1, ns);
   const int nf = h->n_tsc_filter;
-  for (int c = 0; c < ns; ++c) {
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c) {  // scoring.go initPreScoreState topoSize
+    E.w[c] = 0;
+    if (c >= ns) continue;
     const ksg_tsc& t = h->tsc[nf + c];
-    int64_t size = 0;  // topoSize: hostname: filtered - ignored nodes; else the key's registered values
-    if (t.is_hostname) size = (int64_t)E.feasible - E.ignored;
+    int64_t size = 0;  // hostname: filtered - ignored nodes; else the key's registered values
+    if (t.is_hostname) size = (int64_t)r.feas - r.ign;
     else if (t.first_of_key)  // a key with one node per value registers one value per counted node
-      size = ((C_uniq >> t.topo) & 1u) ? (int64_t)E.feasible - E.ignored : (int64_t)__popcll(E.reg[c]);
+      size = ((C.T.uniq >> t.topo) & 1u) ? (int64_t)r.feas - r.ign : (int64_t)__popcll(r.reg[c]);
     E.w[c] = go_log((double)(size + 2));
   }
 }
@@ -423,12 +526,14 @@ __device__ __forceinline__ int64_t pts_raw(const DevCluster& C, const ProgView& 
   const ksg_prog* h = V.h;
   const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
   double score = 0;
-  for (int c = nf; c < nf + ns; ++c) {
-    const ksg_tsc& t = h->tsc[c];
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c) {
+    if (c >= ns) continue;
+    const ksg_tsc& t = h->tsc[nf + c];
     const int32_t v = tv(t.topo);
     if (v < 0) continue;
-    const int64_t cnt = pts_count_tab(C, V, c, n, v);
-    score = __dadd_rn(score, __dadd_rn(__dmul_rn((double)cnt, E.w[c - nf]), (double)(t.max_skew - 1)));
+    const int64_t cnt = pts_count_tab(C, V, nf + c, n, v);
+    score = __dadd_rn(score, __dadd_rn(__dmul_rn((double)cnt, E.w[c]), (double)(t.max_skew - 1)));
   }
   return (int64_t)round(score);
 }
@@ -440,10 +545,8 @@ __device__ __forceinline__ int64_t pts_raw1(const ksg_prog* h, const EvalTotals&
 
 struct FinalShared {
   int32_t tv[KSG_MAX_TOPO * kBlock];
-  EvalTotals E;
-  int64_t red64[kBlock / 64];
-  uint64_t redu[kBlock / 64];
-  int32_t red32[kBlock / 64];
+  ChainRec rec[kBlock / 64];
+  uint32_t ipa_flags;
 };
 
 // PodTopologySpread raw scores of a pod with several score constraints.
@@ -460,27 +563,25 @@ __global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, C
     if (F.plugins[p] == KP_PTS) pts_pos = p;
   const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
   const bool active = n < C.N;
-  load_slot_vids(C, n, active, L.tv);
+  load_slot_vids(C, active ? n : 0, true, L.tv);
   const SlotVids tv{L.tv + threadIdx.x};
   EvalTotals E;
-  reduce_eval(A, V.h, C.T.uniq, E, L.red64, L.redu, L.red32);
-  int64_t s = 0;
-  bool counted = false;
+  reduce_eval(C, A, V.h, E, L.rec);
+  ChainRec r;
+  rec_init(r);
   if (active && of[n] == KSG_FILTER_PASS) {
     int32_t* slot = os + (size_t)pts_pos * C.N + n;
     if (*slot >= 0) {
-      counted = true;
-      s = pts_raw(C, V, E, n, tv);
+      const int64_t s = pts_raw(C, V, E, n, tv);
       *slot = (int32_t)s;
+      r.mx[KCX_PTS] = r.mn[KCX_PTS] = s;
     }
   }
-  const int64_t a = block_reduce<int64_t>(wave_max(counted ? s : INT64_MIN), L.red64,
-                                          [](int64_t u, int64_t w) { return u > w ? u : w; });
-  const int64_t c = block_reduce<int64_t>(wave_min(counted ? s : INT64_MAX), L.red64,
-                                          [](int64_t u, int64_t w) { return u < w ? u : w; });
+  __syncthreads();  // L.rec reused
+  rec_block(r, L.rec, 1u << KCX_PTS, 0);
   if (threadIdx.x == 0) {
-    A.pm2[blockIdx.x] = a;
-    A.pm2[A.nblk + blockIdx.x] = c;
+    A.pm2[blockIdx.x] = r.mx[KCX_PTS];
+    A.pm2[A.nblk + blockIdx.x] = r.mn[KCX_PTS];
   }
 }
 
@@ -493,95 +594,118 @@ __global__ __launch_bounds__(kBlock) void k_final(DevCluster C, DevProfile F, Ch
   uint32_t* of;
   int32_t *os, *ot;
   chain_outs(A, q, C.N, of, os, ot);
+  const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+  const bool mine = n < C.N && of[n] == KSG_FILTER_PASS;
+  int32_t raw[KSG_MAX_PLUGINS];  // this node's raw scores, loaded before the folds
+#pragma unroll
+  for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) raw[pos] = (mine && pos < F.n) ? os[(size_t)pos * C.N + n] : 0;
+  bool ipa = false;
+  for (int p = 0; p < F.n; ++p) ipa |= F.plugins[p] == KP_IPA;
+  if (threadIdx.x == 0) L.ipa_flags = 0;
   EvalTotals E;
-  reduce_eval(A, h, C.T.uniq, E, L.red64, L.redu, L.red32);
+  reduce_eval(C, A, h, E, L.rec);  // (its barrier also publishes L.ipa_flags = 0)
   const bool multi = (h->tab & KTAB_PTS_MULTI) != 0;
   int64_t pmx = INT64_MIN, pmn = INT64_MAX;  // PodTopologySpread raw max / min over counted nodes
   if (multi) {
+    ChainRec r;
+    rec_init(r);
     for (uint32_t b = threadIdx.x; b < A.nblk; b += blockDim.x) {
-      pmx = A.pm2[b] > pmx ? A.pm2[b] : pmx;
-      pmn = A.pm2[A.nblk + b] < pmn ? A.pm2[A.nblk + b] : pmn;
+      r.mx[KCX_PTS] = A.pm2[b] > r.mx[KCX_PTS] ? A.pm2[b] : r.mx[KCX_PTS];
+      r.mn[KCX_PTS] = A.pm2[A.nblk + b] < r.mn[KCX_PTS] ? A.pm2[A.nblk + b] : r.mn[KCX_PTS];
     }
-    pmx = block_reduce<int64_t>(wave_max(pmx), L.red64, [](int64_t u, int64_t w) { return u > w ? u : w; });
-    pmn = block_reduce<int64_t>(wave_min(pmn), L.red64, [](int64_t u, int64_t w) { return u < w ? u : w; });
-  } else if (E.mx[KCX_PTS] != INT64_MIN) {  // one constraint: raw is monotone in the count
-    pmx = pts_raw1(h, E, E.mx[KCX_PTS]);
-    pmn = pts_raw1(h, E, E.mn[KCX_PTS]);
+    __syncthreads();  // L.rec reused
+    rec_block(r, L.rec, 1u << KCX_PTS, 0);
+    pmx = r.mx[KCX_PTS];
+    pmn = r.mn[KCX_PTS];
+  } else if (E.r.mx[KCX_PTS] != INT64_MIN) {  // one constraint: raw is monotone in the count
+    pmx = pts_raw1(h, E, E.r.mx[KCX_PTS]);
+    pmn = pts_raw1(h, E, E.r.mn[KCX_PTS]);
   }
+  if (ipa) {  // InterPodAffinity PreScore Skip: from the tables, as k_eval's blocks did
+    const uint32_t bits = __ockl_wfred_or_u32(ipa_table_bits(C, F, V));
+    if (lane0() && bits) atomicOr(&L.ipa_flags, bits);
+    lds_barrier();
+  }
+  const uint32_t ipa_flags = L.ipa_flags;
   // the summary's normalisers per position (max over feasible nodes; unset as k_init_summaries)
   int64_t smx[KSG_MAX_PLUGINS], smn[KSG_MAX_PLUGINS];
-  for (int pos = 0; pos < F.n; ++pos) {
-    const int p = F.plugins[pos], x = chain_x(p);
-    smx[pos] = p == KP_IPA ? INT64_MIN : 0;
+#pragma unroll
+  for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+    smx[pos] = 0;
     smn[pos] = INT64_MAX;
+    if (pos >= F.n) continue;
+    const int p = F.plugins[pos], x = chain_x(p);
+    if (p == KP_IPA) smx[pos] = INT64_MIN;
     if (x < 0) continue;
     if (p == KP_PTS) {
       if (pmx != INT64_MIN) { smx[pos] = pmx > 0 ? pmx : 0; smn[pos] = pmn; }
-    } else if (E.mx[x] != INT64_MIN) {
-      smx[pos] = p == KP_IPA ? E.mx[x] : (E.mx[x] > 0 ? E.mx[x] : 0);
-      smn[pos] = E.mn[x];
+    } else if (rec_mx(E.r, x) != INT64_MIN) {
+      const int64_t m = rec_mx(E.r, x);
+      smx[pos] = p == KP_IPA ? m : (m > 0 ? m : 0);
+      smn[pos] = rec_mn(E.r, x);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     ksg_pod_summary* S = A.sums + q;
-    S->feasible = E.feasible;
-    S->ignored = E.ignored;
-    S->ipa_flags = 0;
-    for (int pos = 0; pos < F.n; ++pos) {
-      S->max_score[pos] = smx[pos];
-      S->min_score[pos] = smn[pos];
-    }
-    for (int c = 0; c < h->n_tsc_score; ++c) S->pts_weight[c] = E.w[c];
+    S->feasible = E.r.feas;
+    S->ignored = E.r.ign;
+    S->ipa_flags = ipa_flags;
+#pragma unroll
+    for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos)
+      if (pos < F.n) {
+        S->max_score[pos] = smx[pos];
+        S->min_score[pos] = smn[pos];
+      }
+#pragma unroll
+    for (int c = 0; c < KSG_MAX_TSC; ++c)
+      if (c < h->n_tsc_score) S->pts_weight[c] = E.w[c];
   }
-  const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
-  uint64_t key = 0;
-  bool range_err = false;
-  uint32_t ipa_flags = 0;
-  {  // InterPodAffinity PreScore Skip: from the tables, as k_eval's blocks did
-    __shared__ uint32_t fl;
-    if (threadIdx.x == 0) fl = 0;
-    __syncthreads();
-    bool ipa = false;
-    for (int p = 0; p < F.n; ++p) ipa |= F.plugins[p] == KP_IPA;
-    if (ipa) {
-      const uint32_t bits = __ockl_wfred_or_u32(ipa_table_bits(C, F, V));
-      if (lane0() && bits) atomicOr(&fl, bits);
-    }
-    __syncthreads();
-    ipa_flags = fl;
-    if (blockIdx.x == 0 && threadIdx.x == 0) A.sums[q].ipa_flags = ipa_flags;
-  }
-  if (n < C.N && of[n] == KSG_FILTER_PASS) {
+  ChainRec r;
+  rec_init(r);
+  if (mine) {
     int64_t tot = 0;
-    bool pts_keys = false;
-#pragma unroll 1
-    for (int pos = 0; pos < F.n; ++pos) {
+    bool pts_keys = false, range_err = false;
+#pragma unroll
+    for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+      if (pos >= F.n) continue;
       const int p = F.plugins[pos];
-      int64_t raw = os[(size_t)pos * C.N + n];
+      int64_t s = raw[pos];
       if (p == KP_PTS) {
-        pts_keys = raw >= 0 && h->n_tsc_score > 0;
-        if (raw < 0) raw = 0;
-        else if (!multi && h->n_tsc_score > 0 && !(h->flags & KPF_SKIP_PTS_SCORE)) raw = pts_raw1(h, E, raw);
-        os[(size_t)pos * C.N + n] = (int32_t)raw;
+        pts_keys = s >= 0 && h->n_tsc_score > 0;
+        if (s < 0) s = 0;
+        else if (!multi && h->n_tsc_score > 0 && !(h->flags & KPF_SKIP_PTS_SCORE)) s = pts_raw1(h, E, s);
+        os[(size_t)pos * C.N + n] = (int32_t)s;
       }
       bool use;
-      const int64_t s = normalize_pos(p, h, raw, smx[pos], smn[pos], ipa_flags, pts_keys, use);
+      const int64_t v = normalize_pos(p, h, s, smx[pos], smn[pos], ipa_flags, pts_keys, use);
       if (use) {
-        if (s < 0 || s > 100) range_err = true;
-        tot += s * F.weight[pos];
+        if (v < 0 || v > 100) range_err = true;
+        tot += v * F.weight[pos];
       }
     }
-    if (E.feasible == 1) tot = 0;  // single feasible node: no scoring
+    if (E.r.feas == 1) tot = 0;  // single feasible node: no scoring
     ot[n] = (int32_t)tot;
-    key = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
+    r.key = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
+    r.st = (E.r.feas > 1 && range_err) ? 4 : 0;
   }
-  const uint64_t best = block_reduce<uint64_t>(wave_max(key), L.redu, [](uint64_t u, uint64_t w) { return u > w ? u : w; });
-  const int32_t st = block_reduce<int32_t>((E.feasible > 1 && range_err) ? 4 : 0, L.red32,
-                                           [](int32_t x, int32_t y) { return x | y; });
+  __syncthreads();  // L.rec reused
+  rec_block(r, L.rec, 0u, 0);
   if (threadIdx.x == 0) {
-    A.pk[blockIdx.x] = best;
-    A.pst[blockIdx.x] = st;
+    A.pk[blockIdx.x] = r.key;
+    A.pst[blockIdx.x] = r.st;
   }
+}
+
+// The assume delta's node row as fire-and-forget atomics (k_select: no load on
+// the chain's critical path).
+__device__ __forceinline__ void assume_row_atomic(DevCluster& C, const ProgView& V, uint32_t n, int sign) {
+  const ksg_prog* h = V.h;
+  for (uint32_t r = 0; r < C.R; ++r)
+    if (h->req[r]) atomicAdd((unsigned long long*)&C.req[(size_t)r * C.N + n], (unsigned long long)(sign * h->req[r]));
+  atomicAdd((unsigned long long*)&C.nzc[n], (unsigned long long)(sign * h->nz_cpu));
+  atomicAdd((unsigned long long*)&C.nzm[n], (unsigned long long)(sign * h->nz_mem));
+  atomicAdd(&C.podcnt[n], sign);
+  for (int i = 0; i < h->n_port_own; ++i) atomicAdd(&C.ports[(size_t)V.i32[h->port_own_off + i] * C.N + n], sign);
 }
 
 // selectHost + the assume: one block.
@@ -590,44 +714,93 @@ __global__ __launch_bounds__(kBlock) void k_select(DevCluster C, DevProfile F, C
   if (q >= A.end) return;
   const ProgView V = view(A.progs + A.prog_off[q]);
   const ksg_prog* h = V.h;
-  __shared__ uint64_t redu[kBlock / 64];
-  __shared__ int32_t red32[kBlock / 64];
-  __shared__ int32_t s_node;
-  uint64_t best = 0;
-  int32_t f = 0, st = 0;
+  __shared__ ChainRec lds[kBlock / 64];
+  ChainRec r;
+  rec_init(r);
   for (uint32_t b = threadIdx.x; b < A.nblk; b += blockDim.x) {
-    best = A.pk[b] > best ? A.pk[b] : best;
-    f += A.pi[KCP_FEAS * A.nblk + b];
-    st |= A.pi[KCP_STAT * A.nblk + b] | A.pst[b];
+    r.key = A.pk[b] > r.key ? A.pk[b] : r.key;
+    r.feas += A.pi[KCP_FEAS * A.nblk + b];
+    r.st |= A.pi[KCP_STAT * A.nblk + b] | A.pst[b];
   }
-  best = block_reduce<uint64_t>(wave_max(best), redu, [](uint64_t u, uint64_t w) { return u > w ? u : w; });
-  f = block_reduce<int32_t>(wave_sum(f), red32, [](int32_t x, int32_t y) { return x + y; });
-  st = block_reduce<int32_t>((int32_t)__ockl_wfred_or_u32((uint32_t)st), red32, [](int32_t x, int32_t y) { return x | y; });
+  rec_block(r, lds, 0u, 0);
+  const bool error = (r.st & 2) || ((r.st & 4) && r.feas > 1) || (h->flags & KPF_PREFILTER_ERROR);
+  int32_t node = -1;
+  const uint32_t g = (uint32_t)(r.key & 0xFFFFFull);
+  if (!error && r.feas > 0 && (A.mode & 1) && g >= C.goff && g - C.goff < C.N) node = (int32_t)(g - C.goff);
   if (threadIdx.x == 0) {
     ksg_pod_summary* S = A.sums + q;
-    S->feasible = f;
-    S->best_key = best;
-    int32_t node = -1;
-    const bool error = (st & 2) || ((st & 4) && f > 1) || (h->flags & KPF_PREFILTER_ERROR);
+    S->feasible = r.feas;
+    S->best_key = r.key;
     if (error) { S->status = 2; S->selected = -1; }
-    else if (f == 0) { S->status = 1; S->selected = -1; }
-    else {
-      const uint32_t g = (uint32_t)(best & 0xFFFFFull);
-      S->selected = (int32_t)g;
-      S->status = 0;
-      if ((A.mode & 1) && g >= C.goff && g - C.goff < C.N) node = (int32_t)(g - C.goff);
-    }
-    s_node = node;
+    else if (r.feas == 0) { S->status = 1; S->selected = -1; }
+    else { S->status = 0; S->selected = (int32_t)g; }
     A.prow[q] = -1;
+    if (node >= 0) {
+      assume_row_atomic(C, V, (uint32_t)node, +1);
+      if (A.mode & 2) {  // the existing-pod table row: written after the run (k_flush_appends)
+        const uint32_t i = atomicAdd(A.alog_n, 1u);
+        A.alog[i] = make_int2((int)q, node);
+      }
+    }
+    *A.cur = q + 1;
   }
+  if (node >= 0) tables_assume(C, V, (uint32_t)node, +1, threadIdx.x, blockDim.x);
+}
+
+// The existing-pod table rows of the run's logged assumes, in log order (one
+// block): exclusive scans of their entry counts, then every row written at its
+// offsets; the programs' prow entries point at them.
+__global__ __launch_bounds__(kBlock) void k_flush_appends(DevCluster C, ChainArgs A) {
+  const uint32_t cnt = *A.alog_n;
+  __shared__ uint32_t base[4], tot[4];
+  __shared__ uint32_t scan[4][kBlock];
+  __shared__ int32_t over;
+  if (threadIdx.x < 4) base[threadIdx.x] = C.tcounts[threadIdx.x];
+  if (threadIdx.x == 0) over = 0;
   __syncthreads();
-  const int32_t node = s_node;
-  if (node >= 0) {
-    if (threadIdx.x == 0) assume_pod(C, V, (uint32_t)node, +1, (A.mode & 2) != 0, A.prow + q, blockDim.x);
-    tables_assume(C, V, (uint32_t)node, +1, threadIdx.x, blockDim.x);
+  const uint32_t cap[4] = {C.pcap, C.tcap, C.rcap, C.vcap};
+  for (uint32_t c0 = 0; c0 < cnt; c0 += blockDim.x) {
+    const uint32_t i = c0 + threadIdx.x;
+    uint32_t need[4] = {0, 0, 0, 0};
+    int2 e = make_int2(0, 0);
+    if (i < cnt) {
+      e = A.alog[i];
+      table_need(view(A.progs + A.prog_off[e.x]), need);
+    }
+    for (int k = 0; k < 4; ++k) scan[k][threadIdx.x] = need[k];
+    __syncthreads();
+    for (uint32_t d = 1; d < blockDim.x; d <<= 1) {  // inclusive scans
+      uint32_t v[4];
+      for (int k = 0; k < 4; ++k) v[k] = threadIdx.x >= d ? scan[k][threadIdx.x - d] : 0;
+      __syncthreads();
+      for (int k = 0; k < 4; ++k) scan[k][threadIdx.x] += v[k];
+      __syncthreads();
+    }
+    if (threadIdx.x == blockDim.x - 1)
+      for (int k = 0; k < 4; ++k) tot[k] = scan[k][threadIdx.x];
+    if (i < cnt) {
+      uint32_t off[4];
+      bool fits = true;
+      for (int k = 0; k < 4; ++k) {
+        off[k] = base[k] + scan[k][threadIdx.x] - need[k];
+        fits &= off[k] + need[k] <= cap[k];
+      }
+      if (fits) {
+        table_write(C, view(A.progs + A.prog_off[e.x]), (uint32_t)e.y, off[0], off[1], off[2], off[3]);
+        A.prow[e.x] = (int32_t)off[0];
+      } else {
+        over = 1;  // capacity is checked before every run: never, unless the host's count is wrong
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) base[threadIdx.x] += tot[threadIdx.x];
+    __syncthreads();
   }
-  __syncthreads();
-  if (threadIdx.x == 0) *A.cur = q + 1;
+  if (threadIdx.x < 4) C.tcounts[threadIdx.x] = base[threadIdx.x] < cap[threadIdx.x] ? base[threadIdx.x] : cap[threadIdx.x];
+  if (threadIdx.x == 0) {
+    if (over) C.tcounts[4] = 1;
+    *A.alog_n = 0;
+  }
 }
 
 __global__ void k_set_cur(uint32_t* cur, uint32_t q) {

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--cpu-pods", type=int, default=100)
     ap.add_argument("--cpu-workers", type=int, default=16)
     a = ap.parse_args()
+    import torch  # before libksg.so initialises HIP (ksg_synth_cluster loads it)
+    assert torch.cuda.is_available()
     from ksg import Scheduler, generator as g
     kw = {"n_pods": a.pods}
     if a.nodes:
@@ -38,7 +40,6 @@ def main():
         doc = g.generate(a.config, **kw)
         blob = json.dumps(doc).encode()
     print(f"generated in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
-    import torch
     s = Scheduler(doc["profile"])
     s.load_cluster(blob)
     n, q = s.n_nodes, s.queue_len

@@ -166,6 +166,32 @@ int ksg_reserve(ksg_ctx* ctx, uint32_t q, int32_t node);
  * pod q (cycle or queue mode): node rows, and its existing-pod table entry. */
 int ksg_unreserve(ksg_ctx* ctx, uint32_t q);
 
+/* ---- what each wrapped plugin's extension point returns (the Go plugin's calls,
+ * INTEGRATION.md), for queue pod q whose per-node outputs are kept (the pod of the
+ * last ksg_cycle, or a range given to ksg_keep_outputs).  `pos` is the profile
+ * position (ksg_plugin_position); `node` a global node index (ksg_node_index).
+ * Status codes are framework.Code values (v1.30 framework/interface.go):
+ * 0 Success, 1 Error, 2 Unschedulable, 3 UnschedulableAndUnresolvable, 5 Skip;
+ * -1 means the framework does not call this plugin there (an earlier filter
+ * failed on the node, PreFilter Skip, outside the PreFilterResult, no scoring).
+ * Messages are Status.Message() (what the wrapper records, wrappedplugin.go:542). */
+int ksg_plugin_position(const ksg_ctx* ctx, const char* name, size_t len);  /* or KSG_E_RANGE */
+int ksg_node_index(const ksg_ctx* ctx, const char* name, size_t len);       /* or KSG_E_RANGE */
+/* PreFilter (wrappedplugin.go:504, mock framework.go:61): status; and the
+ * PreFilterResult node set as a JSON array of node names, "null" for all nodes. */
+int ksg_prefilter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code, char* msg, size_t cap, size_t* len);
+int ksg_prefilter_result(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len);
+/* Filter (wrappedplugin.go:535, mock framework.go:114) on one node. */
+int ksg_filter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, uint32_t node, int32_t* code, char* msg, size_t cap,
+                      size_t* len);
+/* PreScore (wrappedplugin.go:472, mock framework.go:233). */
+int ksg_prescore_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code);
+/* NormalizeScore (wrappedplugin.go:400, mock framework.go:338): the plugin's
+ * normalized score per local node (raw score for plugins without
+ * ScoreExtensions), computed on the device by the NormalizeScore the selection
+ * used; valid where the node passed every filter. */
+int ksg_normalized_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int64_t* out, uint32_t n);
+
 /* Scheduler-cache events between cycles (replaces the informer -> Cache path:
  * Cache.AddNode/UpdateNode/RemoveNode/AddPod/UpdatePod/RemovePod of upstream
  * v1.30.4 pkg/scheduler/internal/cache/cache.go, driven by eventhandlers.go;

@@ -75,6 +75,7 @@ struct ClassUpload {
   std::vector<ksg_req> creq;     // selector requirements (val_off into cval)
   std::vector<int32_t> cval;
   std::vector<int32_t> tc_slot;  // new term classes: their topology slot
+  std::vector<uint32_t> tc_off;  // ... and the offset of their values in the pool (host-assigned, ascending)
 };
 
 // Existing pods (bound) on this shard's nodes, and their (anti)affinity terms.

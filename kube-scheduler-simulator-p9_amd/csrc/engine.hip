@@ -111,6 +111,10 @@ struct DevCluster {
   uint32_t n_ports;
   int32_t* ports;          // [n_ports][N] used host-port triple counts
   DevTables T;
+  // per topology slot, by value for fully unrolled loops (no load): its node
+  // label key and its base among the shared-key pairs (-1: one node per value)
+  int32_t tkeyv[KSG_MAX_TOPO];
+  int32_t nubv[KSG_MAX_TOPO];
 };
 
 struct DevProfile {
@@ -517,7 +521,7 @@ __device__ __forceinline__ void load_slot_vids(const DevCluster& C, uint32_t n, 
   const uint32_t nt = C.n_topo < KSG_MAX_TOPO ? C.n_topo : KSG_MAX_TOPO;
   int32_t v[KSG_MAX_TOPO];
 #pragma unroll
-  for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = ((uint32_t)s < nt && active) ? node_vid(C, C.tkey[s], n) : -1;
+  for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = ((uint32_t)s < nt && active) ? node_vid(C, C.tkeyv[s], n) : -1;
 #pragma unroll
   for (int s = 0; s < KSG_MAX_TOPO; ++s)
     if ((uint32_t)s < nt) lds[s * kBlock + threadIdx.x] = v[s];
@@ -1130,40 +1134,44 @@ __global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, c
 // ---- class tables: lookups and the assume delta
 // Pods of class `cls` counted for topology pair (slot, v) of local node n: the
 // node's own count for keys with one node per value, the pair's sum otherwise.
-__device__ __forceinline__ int32_t pc_count(const DevCluster& C, int32_t cls, int slot, uint32_t n, int32_t v) {
+// nub: the key's base among the shared-key pairs (ksg_tsc / ksg_aterm .nub),
+// -1 for a key with one node per value.
+__device__ __forceinline__ int32_t pc_count(const DevCluster& C, int32_t cls, int32_t nub, uint32_t n, int32_t v) {
   if (cls < 0 || v < 0) return 0;
-  if ((C.T.uniq >> slot) & 1u) return C.T.pc_cnt[(size_t)cls * C.N + n];
-  return C.T.pc_dom[(size_t)cls * C.T.NU + C.T.nu_base[slot] + v];
+  if (nub < 0) return C.T.pc_cnt[(size_t)cls * C.N + n];
+  return C.T.pc_dom[(size_t)cls * C.T.NU + (uint32_t)nub + v];
 }
-// Term class u's value at local node n (v: n's value of the class's key).
-__device__ __forceinline__ int32_t tc_value(const DevCluster& C, int32_t u, uint32_t n, int32_t v) {
+// A term class's value at local node n: its table at `off`, key in topology
+// slot `slot` (v: n's value of that key).
+__device__ __forceinline__ int32_t tc_value(const DevCluster& C, uint32_t off, int slot, uint32_t n, int32_t v) {
   if (v < 0) return 0;
-  const int s = C.T.tc_slot[u];
-  return C.T.tc_val[C.T.tc_off[u] + (((C.T.uniq >> s) & 1u) ? n : (uint32_t)v)];
+  return C.T.tc_val[off + (((C.T.uniq >> slot) & 1u) ? n : (uint32_t)v)];
 }
 __device__ void pc_add(DevCluster& C, int32_t cls, uint32_t n, int sign) {
   const DevTables& T = C.T;
   if (cls < 0 || (uint32_t)cls >= T.npc) return;
   atomicAdd(&T.pc_cnt[(size_t)cls * C.N + n], sign);
-  const uint32_t nt = C.n_topo < KSG_MAX_TOPO ? C.n_topo : KSG_MAX_TOPO;
-  for (uint32_t s = 0; s < nt; ++s) {
-    const int32_t v = node_vid(C, C.tkey[s], n);
-    if (v < 0) continue;
+  int32_t v[KSG_MAX_TOPO];  // the node's topology values, loaded together
+#pragma unroll
+  for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? node_vid(C, C.tkeyv[s], n) : -1;
+#pragma unroll
+  for (int s = 0; s < KSG_MAX_TOPO; ++s) {
+    if (v[s] < 0) continue;
     atomicAdd(&T.pc_tot[(size_t)cls * KSG_MAX_TOPO + s], sign);
-    if (!((T.uniq >> s) & 1u)) atomicAdd(&T.pc_dom[(size_t)cls * T.NU + T.nu_base[s] + v], sign);
+    if (C.nubv[s] >= 0) atomicAdd(&T.pc_dom[(size_t)cls * T.NU + (uint32_t)C.nubv[s] + v[s]], sign);
   }
 }
 // an existing pod's term: +1 (required terms) or its signed weight (preferred)
 __device__ __forceinline__ int32_t eterm_inc(const ksg_exist_term& e) {
   return e.kind == 2 ? e.weight : (e.kind == 3 ? -e.weight : 1);
 }
-__device__ void tc_add(DevCluster& C, int32_t u, uint32_t n, int32_t inc, int sign) {
-  if (u < 0 || (uint32_t)u >= C.T.ntc) return;
-  const int s = C.T.tc_slot[u];
-  const int32_t v = node_vid(C, C.tkey[s], n);
+// an existing pod's term e (its term class, table offset and topology slot) on node n
+__device__ void tc_add(DevCluster& C, const ksg_exist_term& e, uint32_t n, int sign) {
+  if (e.cls < 0 || (uint32_t)e.cls >= C.T.ntc) return;
+  const int32_t v = node_vid(C, e.topo_key, n);
   if (v < 0) return;
-  atomicAdd(&C.T.tc_val[C.T.tc_off[u] + (((C.T.uniq >> s) & 1u) ? n : (uint32_t)v)], sign * inc);
-  atomicAdd(&C.T.tc_tot[u], sign);
+  atomicAdd(&C.T.tc_val[(uint32_t)e.toff + (((C.T.uniq >> e.topo) & 1u) ? n : (uint32_t)v)], sign * eterm_inc(e));
+  atomicAdd(&C.T.tc_tot[e.cls], sign);
 }
 // Every class-table delta of program V placed on (sign +1) / removed from
 // (sign -1) local node n: its pod classes and its own affinity terms.  Items
@@ -1176,8 +1184,7 @@ __device__ void tables_assume(DevCluster& C, const ProgView& V, uint32_t n, int 
     if (i < npm) {
       pc_add(C, V.i32[h->pc_match_off + i], n, sign);
     } else {
-      const ksg_exist_term& e = V.et[h->exist_terms_off + (i - npm)];
-      tc_add(C, e.cls, n, eterm_inc(e), sign);
+      tc_add(C, V.et[h->exist_terms_off + (i - npm)], n, sign);
     }
   }
 }
@@ -3566,6 +3573,10 @@ struct Engine::Impl {
     T.nu_base = nu_base_d.p; T.slot_dom = slot_dom_d.p; T.pair_node = pair_node_d.p;
     T.pcls = pcls_d.p; T.cterm = cterm_d.p; T.creq = creq_d.p; T.cval = cval_d.p;
     T.tc_val = tc_val.p; T.tc_off = tc_off_d.p; T.tc_slot = tc_slot_d.p; T.tc_tot = tc_tot.p;
+    for (int s = 0; s < KSG_MAX_TOPO; ++s) {
+      C.tkeyv[s] = (size_t)s < topo.topo_key.size() ? topo.topo_key[s] : -1;
+      C.nubv[s] = ((size_t)s < topo.nu_base.size() && topo.nu_base[s] != 0xFFFFFFFFu) ? (int32_t)topo.nu_base[s] : -1;
+    }
     return C;
   }
   DevScratch scratch() const {
@@ -3719,6 +3730,7 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   I.topo.topo_base = ns.topo_base;
   I.topo.topo_count = ns.topo_count;
   I.topo.topo_pairs = ns.topo_pairs;
+  I.topo.nu_base = ns.nu_base;
   {
     std::vector<uint32_t> sp;
     I.uniq = 0;
@@ -4277,14 +4289,17 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
     I.npc += npc;
   }
   if (ntc) {  // per term class: one value per (key, value) pair, or per node for one-node keys
-    std::vector<uint32_t> off(ntc);
-    uint32_t add = 0;
+    const std::vector<uint32_t>& off = u.tc_off;
+    if (off.size() != ntc) { err = "term classes without offsets"; return false; }
+    uint32_t end = I.tc_used;
     for (uint32_t i = 0; i < ntc; ++i) {
       const int32_t sl = u.tc_slot[i];
       if (sl < 0 || sl >= (int32_t)I.topo.topo_count.size()) { err = "term class without a topology slot"; return false; }
-      off[i] = I.tc_used + add;
-      add += std::max<uint32_t>(((I.uniq >> sl) & 1u) ? I.N : I.topo.topo_count[sl], 1);
+      const uint32_t len = std::max<uint32_t>(((I.uniq >> sl) & 1u) ? I.N : I.topo.topo_count[sl], 1);
+      if (off[i] != end) { err = "term class offsets out of sequence"; return false; }
+      end = off[i] + len;
     }
+    const uint32_t add = end - I.tc_used;
     if (!dev_zero_tail(I.tc_val, I.tc_used, add, s, err) || !dev_append(I.tc_off_d, tc0, off, s, err) ||
         !dev_append(I.tc_slot_d, tc0, u.tc_slot, s, err) || !dev_zero_tail(I.tc_tot, tc0, ntc, s, err))
       return false;
@@ -4489,8 +4504,6 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   ChainArgs CA{};
   CA.progs = I.progs.p;
   CA.prog_off = I.prog_off_d.p;
-  CA.cur = I.cur.p;
-  CA.end = first + count;
   CA.sums = I.sums.p;
   CA.keep_first = I.keep_first;
   CA.keep_n = I.keep_n;
@@ -4505,7 +4518,6 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   CA.alog = I.alog.p;
   CA.alog_n = I.alog_n.p;
   const int rowm = I.R > 4 ? 0 : (I.eval_mode == 1 ? 2 : 1);
-  uint32_t cur_at = 0xFFFFFFFFu;  // the device pod counter holds this queue index
   bool pending = false;           // logged assumes whose existing-pod table rows are not written yet
   auto flush = [&]() {
     if (pending) hipLaunchKernelGGL(k_flush_appends, dim3(1), b, 0, s, C, CA);
@@ -4514,7 +4526,8 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
     if (!xchain && (I.prog_need[j] & 4)) {
-      if (cur_at != j) hipLaunchKernelGGL(k_set_cur, dim3(1), dim3(64), 0, s, I.cur.p, j);
+      CA.q = j;
+      CA.prog = prog;
       const bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
       if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
       if (rowm == 2) hipLaunchKernelGGL(k_eval<2>, dim3(I.cnblk), b, 0, s, C, F, CA);
@@ -4529,12 +4542,10 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         hipLaunchKernelGGL(k_final, dim3(I.cnblk), b, 0, s, C, F, CA);
       }
       hipLaunchKernelGGL(k_select, dim3(1), b, 0, s, C, F, CA);
-      cur_at = j + 1;
       pending |= (CA.mode & 2) != 0;
       continue;
     }
     flush();  // the scanning chain reads the existing-pod table
-    cur_at = 0xFFFFFFFFu;
     const int mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
     DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j, xchain ? nullptr : I.arrive1.p, mode, I.prow.p + j};
     bool kept = I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n;

@@ -603,6 +603,8 @@ struct Cluster {
   struct TClass {
     int group = 0;         // KSG_TC_*
     string topo;           // topology key
+    int32_t slot = -1;
+    uint32_t off = 0;      // offset of its values in the device pool (per pair, or per node)
     ATerm term;
   };
   vector<PClass> pcls;
@@ -614,6 +616,16 @@ struct Cluster {
   std::unordered_map<uint32_t, uint32_t> keyset_nodes;  // slot mask -> nodes carrying every key of it
   vector<uint32_t> enc_topo_count;
   vector<uint8_t> enc_topo_unique;
+  vector<uint32_t> enc_nu_base;  // per slot: base among the shared-key pairs (UINT32_MAX: one node per value)
+  vector<uint32_t> enc_topo_base;
+  uint32_t enc_N = 0, enc_NU = 0;
+  uint32_t tc_total = 0;         // term-class value pool entries assigned (offsets follow class order)
+  // a class-table count reference for topology slot `slot`: the key's base among
+  // the shared-key pairs, -1 for a key with one node per value (the node's count)
+  int32_t nub_of(int32_t slot) const {
+    if (slot < 0 || (size_t)slot >= enc_nu_base.size() || enc_nu_base[slot] == 0xFFFFFFFFu) return -1;
+    return (int32_t)enc_nu_base[slot];
+  }
 
   static void key_sel(string& k, const LSel& s) {
     k += s.nothing ? 'N' : (s.err ? 'E' : 'S');
@@ -676,6 +688,10 @@ struct Cluster {
     TClass c;
     c.group = group;
     c.topo = a.topo;
+    c.slot = topo.get(a.topo);
+    c.off = tc_total;
+    const bool one = (size_t)c.slot < enc_topo_unique.size() && enc_topo_unique[c.slot];
+    tc_total += std::max<uint32_t>(one ? enc_N : ((size_t)c.slot < enc_topo_count.size() ? enc_topo_count[c.slot] : 0), 1);
     c.term.sel = a.sel;
     c.term.namespaces = a.namespaces;
     c.term.ns_all = a.ns_all;
@@ -741,7 +757,10 @@ struct Cluster {
       }
       u.pc.push_back(pc);
     }
-    for (uint32_t k = eng->term_classes(); k < tcls.size(); ++k) u.tc_slot.push_back(topo.get(tcls[k].topo));
+    for (uint32_t k = eng->term_classes(); k < tcls.size(); ++k) {
+      u.tc_slot.push_back(tcls[k].slot);
+      u.tc_off.push_back(tcls[k].off);
+    }
     return eng->add_classes(u, err);
   }
   // nodes carrying every key of slot mask m
@@ -1057,6 +1076,11 @@ struct Cluster {
       }
     enc_topo_count = S.topo_count;
     enc_topo_unique = S.topo_unique;
+    enc_nu_base = S.nu_base;
+    enc_topo_base = S.topo_base;
+    enc_N = n;
+    enc_NU = S.nu_pairs;
+    tc_total = 0;
     // bound pods: NodeInfo aggregates + existing-pod table (this shard's nodes)
     T = PodTableSoA();
     T.n_keys = (uint32_t)pkeys.names.size();
@@ -1114,6 +1138,7 @@ struct Cluster {
       for (auto& ns : a.namespaces) vals.push_back(nss.get(ns) < 0 ? -2 : nss.get(ns));
       e.ns_cnt = (int32_t)a.namespaces.size();
       e.cls = tables_on() ? tclass(kind, a) : -1;
+      e.toff = e.cls >= 0 ? (int32_t)tcls[e.cls].off : 0;
       terms.push_back(e);
       if (term_pod_v) term_pod_v->push_back(row);
     };
@@ -1214,6 +1239,7 @@ struct Cluster {
     t.ns_cnt = (int32_t)a.namespaces.size();
     t.weight = a.weight;
     t.cls = tables_on() ? pclass(false, {a}) : -1;
+    t.nub = nub_of(t.topo);
   }
 
   bool compile(const Pod& p, int32_t qidx, vector<uint8_t>& blob, PodMeta& m) {
@@ -1370,6 +1396,8 @@ struct Cluster {
         if (s.err) m.prefilter_error = true;
         compile_lsel(s, t.sel, P.req, P.i32);
         t.cls = tables_on() ? tsc_class(p, s) : -1;
+        t.nub = -1;
+        t.pair_base = t.nvals = 0;
         t.topo = topo.get(c.key);
         t.topo_key = nkeys.get(c.key);
         t.max_skew = c.max_skew;
@@ -1398,6 +1426,13 @@ struct Cluster {
     // class tables: the filter pair count is the LAST filter constraint's on the key
     // (calPreFilterState keeps one count per pair); a score pair sums every
     // non-hostname score constraint on the key (TopologyPairToPodCounts)
+    for (int i = 0; i < nf + ns; ++i) {
+      ksg_tsc& t = h.tsc[i];
+      t.nub = nub_of(t.topo);
+      const bool known = t.topo >= 0 && (size_t)t.topo < enc_topo_base.size();
+      t.pair_base = known ? (int32_t)enc_topo_base[t.topo] : 0;
+      t.nvals = known ? (int32_t)enc_topo_count[t.topo] : 0;
+    }
     for (int i = 0; i < nf; ++i) {
       h.tsc[i].eff_cls = h.tsc[i].cls;
       for (int j = i + 1; j < nf; ++j)
@@ -1499,14 +1534,14 @@ struct Cluster {
           h.n_pc_match++;
         }
       h.tc_match_off = (int32_t)P.i32.size();
-      vector<int32_t> grp;
-      for (size_t k = 0; k < tcls.size(); ++k)
+      for (size_t k = 0; k < tcls.size(); ++k)  // (class, value offset, topology slot, group)
         if (term_matches(tcls[k].term, p)) {
           P.i32.push_back((int32_t)k);
-          grp.push_back(tcls[k].group);
+          P.i32.push_back((int32_t)tcls[k].off);
+          P.i32.push_back(tcls[k].slot);
+          P.i32.push_back(tcls[k].group);
           h.n_tc_match++;
         }
-      P.i32.insert(P.i32.end(), grp.begin(), grp.end());
       h.tab = table_path(h) ? KTAB_ON : 0;
       if ((h.tab & KTAB_ON) && pos_of(P_PTS) >= 0 && h.n_tsc_score > 1 && !(h.flags & KPF_SKIP_PTS_SCORE))
         h.tab |= KTAB_PTS_MULTI;
@@ -2245,6 +2280,122 @@ struct Cluster {
     return "";
   }
 
+  // ------------------------------------------------------------ per-plugin statuses
+  // What each wrapped plugin's extension point returns for the cycle of queue pod
+  // q (the Go plugin API of ksg.h; render() records the same into the store).
+  // framework.Code (v1.30 pkg/scheduler/framework/interface.go)
+  enum { C_SUCCESS = 0, C_ERROR = 1, C_UNSCHED = 2, C_UNRESOLVABLE = 3, C_SKIP = 5 };
+  // PreFilter Skip per plugin id (PreFilter / the NodeAffinity, PTS, IPA, NodePorts Skip rules)
+  uint32_t skip_filter_mask(const PodMeta& m, const ksg_pod_summary& S) const {
+    uint32_t skip_f = 0;
+    if (m.flags & KPF_SKIP_NA_FILTER) skip_f |= 1u << P_NA;
+    if (m.flags & KPF_SKIP_PTS_FILTER) skip_f |= 1u << P_PTS;
+    if (m.ipa_no_req_terms && !(S.ipa_flags & 4u)) skip_f |= 1u << P_IPA;
+    if (m.flags & KPF_SKIP_PORTS) skip_f |= 1u << P_PORTS;
+    skip_f |= (1u << P_VOLUME) | (1u << P_VOLBIND);  // pods with volumes they act on are refused at load
+    return skip_f;
+  }
+  uint32_t skip_score_mask(const PodMeta& m, const ksg_pod_summary& S) const {
+    uint32_t skip_s = 0;
+    if (m.flags & KPF_SKIP_NA_SCORE) skip_s |= 1u << P_NA;
+    if (m.flags & KPF_SKIP_PTS_SCORE) skip_s |= 1u << P_PTS;
+    if (m.ipa_prescore_skip_static || !(S.ipa_flags & 8u)) skip_s |= 1u << P_IPA;
+    skip_s |= 1u << P_VOLBIND;  // PreScore: no scorer (VolumeCapacityPriority off)
+    return skip_s;
+  }
+  // PreFilter of profile position pos: the status code (-1: the plugin has no
+  // PreFilter, or an earlier PreFilter rejected the pod and it never ran).
+  int prefilter_status(uint32_t q, int pos, const ksg_pod_summary& S, string& msg) const {
+    const PodMeta& m = meta[q];
+    const uint32_t skip_f = skip_filter_mask(m, S);
+    for (int p = 0; p < n_plugins; ++p) {
+      if (!has_prefilter(plugins[p])) continue;
+      if (p == pos) {
+        if (p == m.prefilter_fail_pos) { msg = m.prefilter_fail_msg; return C_UNRESOLVABLE; }
+        msg.clear();
+        return (skip_f & (1u << plugins[p])) ? C_SKIP : C_SUCCESS;
+      }
+      if (p == m.prefilter_fail_pos) break;
+    }
+    return -1;
+  }
+  // Filter of profile position pos on local node i: the status code and message
+  // (-1: not called: no Filter, PreFilter Skip / rejection, outside the
+  // PreFilterResult, or an earlier filter failed on the node).
+  int filter_status(uint32_t q, int pos, uint32_t i, const PodOutputs& o, string& msg) const {
+    const PodMeta& m = meta[q];
+    msg.clear();
+    if (pos < 0 || pos >= n_plugins || !has_filter(plugins[pos])) return -1;
+    if (m.prefilter_fail_pos >= 0 || (skip_filter_mask(m, o.summary) & (1u << plugins[pos]))) return -1;
+    const uint32_t code = o.filter[i];
+    if (code == KSG_FILTER_NOT_EVALUATED) return -1;
+    const int fail_pos = code == KSG_FILTER_PASS ? n_plugins : fpos[code >> 24];
+    if (pos < fail_pos) return C_SUCCESS;
+    if (pos > fail_pos) return -1;
+    const uint32_t detail = code & 0xFFFFFFu;
+    msg = filter_message(pos, detail);
+    switch (plugins[pos]) {
+      case P_FIT: {  // fit.go Filter: UnschedulableAndUnresolvable when a request exceeds the allocatable
+        vector<i64> rq;
+        i64 nzc = 0, nzm = 0;
+        add_requests_const(queue[q], rq, nzc, nzm);
+        const Node& nd = nodes[lo + i];
+        for (size_t r = 0; r < res.names.size(); ++r) {
+          if (!(detail & (1u << (1 + r)))) continue;
+          auto it = nd.alloc.find(res.names[r]);
+          const i64 a = it == nd.alloc.end() ? 0 : (r == 0 ? as_milli(it->second) : as_value(it->second));
+          if (rq[r] > a) return C_UNRESOLVABLE;
+        }
+        return C_UNSCHED;
+      }
+      case P_PTS: return detail == KSG_PTS_MISSING_LABEL ? C_UNRESOLVABLE : C_UNSCHED;
+      case P_IPA: return detail == KSG_IPA_AFFINITY ? C_UNRESOLVABLE : C_UNSCHED;
+      case P_PORTS: return C_UNSCHED;
+      default: return C_UNRESOLVABLE;  // TaintToleration, NodeAffinity, NodeUnschedulable, NodeName
+    }
+  }
+  // PreScore of profile position pos (-1: no PreScore, or no scoring: one feasible node / none).
+  int prescore_status(uint32_t q, int pos, const ksg_pod_summary& S) const {
+    if (pos < 0 || pos >= n_plugins || !has_prescore(plugins[pos])) return -1;
+    if (meta[q].prefilter_fail_pos >= 0 || S.feasible <= 1 || S.status == 2) return -1;
+    return (skip_score_mask(meta[q], S) & (1u << plugins[pos])) ? C_SKIP : C_SUCCESS;
+  }
+  void add_requests_const(const Pod& p, vector<i64>& out_req, i64& nzc, i64& nzm) const {
+    out_req.assign(res.names.size(), 0);
+    for (auto& kv : p.req) {
+      const int32_t r = res.get(kv.first);
+      if (r >= 0) out_req[r] += r == 0 ? as_milli(kv.second) : as_value(kv.second);
+    }
+    auto c = p.req_nz.find("cpu");
+    auto mm = p.req_nz.find("memory");
+    nzc = c == p.req_nz.end() ? 0 : as_milli(c->second);
+    nzm = mm == p.req_nz.end() ? 0 : as_value(mm->second);
+  }
+  // Kept outputs of queue pod q, cached until the next run (ABI lookups per node).
+  uint64_t out_gen = 0;
+  int64_t oc_q = -1;
+  uint64_t oc_gen = 0;
+  PodOutputs oc;
+  vector<int32_t> oc_norm;
+  bool oc_norm_ok = false;
+  const PodOutputs* outputs_of(uint32_t q) {
+    if (oc_q != (int64_t)q || oc_gen != out_gen) {
+      if (!eng->outputs(q, oc, err)) { oc_q = -1; return nullptr; }
+      oc_q = q;
+      oc_gen = out_gen;
+      oc_norm_ok = false;
+    }
+    return &oc;
+  }
+  const vector<int32_t>* normalized_of(uint32_t q) {
+    if (!outputs_of(q)) return nullptr;
+    if (!oc_norm_ok) {
+      if (!eng->normalized(q, oc_norm, err)) return nullptr;
+      oc_norm_ok = true;
+    }
+    return &oc_norm;
+  }
+
   bool render(uint32_t q, string& out) {
     PodOutputs o;
     if (!eng->outputs(q, o, err)) return false;
@@ -2255,12 +2406,8 @@ struct Cluster {
     map<string, vector<string>> pre_result;
     map<string, map<string, string>> filt, score, fin;
     // skip sets
-    uint32_t skip_f = 0, skip_s = 0;
-    if (m.flags & KPF_SKIP_NA_FILTER) skip_f |= 1u << P_NA;
-    if (m.flags & KPF_SKIP_PTS_FILTER) skip_f |= 1u << P_PTS;
-    if (m.ipa_no_req_terms && !(S.ipa_flags & 4u)) skip_f |= 1u << P_IPA;
-    if (m.flags & KPF_SKIP_PORTS) skip_f |= 1u << P_PORTS;
-    skip_f |= (1u << P_VOLUME) | (1u << P_VOLBIND);  // pods with volumes they act on are refused at load
+    const uint32_t skip_f = skip_filter_mask(m, S);
+    uint32_t skip_s = 0;
     bool aborted = false;
     for (int pos = 0; pos < n_plugins && !aborted; ++pos) {
       int id = plugins[pos];
@@ -2288,10 +2435,7 @@ struct Cluster {
         }
       }
       if (S.feasible > 1 && S.status != 2) {
-        if (m.flags & KPF_SKIP_NA_SCORE) skip_s |= 1u << P_NA;
-        if (m.flags & KPF_SKIP_PTS_SCORE) skip_s |= 1u << P_PTS;
-        if (m.ipa_prescore_skip_static || !(S.ipa_flags & 8u)) skip_s |= 1u << P_IPA;
-        skip_s |= 1u << P_VOLBIND;  // PreScore: no scorer (VolumeCapacityPriority off)
+        skip_s = skip_score_mask(m, S);
         for (int pos = 0; pos < n_plugins; ++pos)
           if (has_prescore(plugins[pos])) pre_score[names[pos]] = (skip_s & (1u << plugins[pos])) ? "" : "success";
         vector<int32_t> norm;  // NormalizeScore on the device (k_norm_out: the selection's normalize_pos)
@@ -2426,6 +2570,7 @@ const char* ksg_last_error(const ksg_ctx* ctx) { return ctx ? ctx->last_error.c_
 
 int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len) {
   if (!ctx || !json) return KSG_E_INVALID;
+  ctx->c.out_gen++;
   try {
     Cluster& c = ctx->c;
     // fix the engine's global node offset for this shard before upload
@@ -2441,12 +2586,14 @@ int ksg_queue_len(const ksg_ctx* ctx) { return ctx ? (int)ctx->c.queue.size() : 
 
 int ksg_keep_outputs(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   KSG_GUARD(ctx);
+  ctx->c.out_gen++;
   if (!ctx->c.eng->keep_outputs(first, count, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
   return KSG_OK;
 }
 
 int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   KSG_GUARD(ctx);
+  ctx->c.out_gen++;
   Cluster& c = ctx->c;
   if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
   if (c.shards != 1 && c.eng->exchange_ranks() != c.shards)
@@ -2467,6 +2614,7 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
 
 int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   KSG_GUARD(ctx);
+  ctx->c.out_gen++;
   Cluster& c = ctx->c;
   if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
   if (c.shards != 1 && c.eng->exchange_ranks() != c.shards)
@@ -2550,6 +2698,7 @@ int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len
 
 int ksg_reset(ksg_ctx* ctx) {
   KSG_GUARD(ctx);
+  ctx->c.out_gen++;
   if (ctx->c.inplace_dirty)
     return ctx->fail("reset after in-place cluster events: reload the cluster (ksg_load_cluster)", KSG_E_STATE);
   if (!ctx->c.compile_queue()) return ctx->fail(ctx->c.err, KSG_E_INVALID);
@@ -2610,6 +2759,7 @@ int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples) {
 
 int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_pod_result* out) {
   KSG_GUARD(ctx);
+  ctx->c.out_gen++;
   if (!ctx || !pod_json) return KSG_E_INVALID;
   ksg_pod_summary s;
   try {
@@ -2636,12 +2786,14 @@ int ksg_reserve(ksg_ctx* ctx, uint32_t q, int32_t node) {
 
 int ksg_unreserve(ksg_ctx* ctx, uint32_t q) {
   KSG_GUARD(ctx);
+  ctx->c.out_gen++;
   if (!ctx->c.unreserve(q)) return ctx->fail(ctx->c.err, KSG_E_STATE);
   return KSG_OK;
 }
 
 int ksg_apply_events(ksg_ctx* ctx, const char* events_json, size_t len) {
   KSG_GUARD(ctx);
+  ctx->c.out_gen++;
   if (!ctx || !events_json) return KSG_E_INVALID;
   try {
     if (!ctx->c.apply_events(events_json, len)) return ctx->fail(ctx->c.err, KSG_E_STATE);
@@ -2661,6 +2813,94 @@ int ksg_node_requested(ksg_ctx* ctx, int64_t* requested, int32_t* pod_count, uin
   for (uint32_t k = 0; k < R; ++k)
     for (uint32_t i = 0; i < N; ++i) requested[(size_t)k * n + i] = r[(size_t)k * N + i];
   for (uint32_t i = 0; i < N; ++i) pod_count[i] = pc[i];
+  return KSG_OK;
+}
+
+// ---- the Go plugin's per-extension-point calls
+static int put_str(ksg_ctx* ctx, const std::string& s, char* buf, size_t cap, size_t* len) {
+  (void)ctx;
+  if (len) *len = s.size();
+  if (!buf) return cap ? KSG_E_INVALID : KSG_OK;
+  if (cap < s.size()) return KSG_E_NOBUF;
+  std::memcpy(buf, s.data(), s.size());
+  return KSG_OK;
+}
+
+int ksg_plugin_position(const ksg_ctx* ctx, const char* name, size_t len) {
+  if (!ctx || !name) return KSG_E_INVALID;
+  const std::string nm(name, len);
+  for (int i = 0; i < ctx->c.n_plugins; ++i)
+    if (ctx->c.names[i] == nm) return i;
+  return KSG_E_RANGE;
+}
+
+int ksg_node_index(const ksg_ctx* ctx, const char* name, size_t len) {
+  if (!ctx || !name) return KSG_E_INVALID;
+  const int32_t g = ctx->c.node_names.get(std::string(name, len));
+  return g < 0 ? KSG_E_RANGE : g;
+}
+
+int ksg_prefilter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code, char* msg, size_t cap, size_t* len) {
+  KSG_GUARD(ctx);
+  Cluster& c = ctx->c;
+  if (!code || q >= c.meta.size() || (int)pos >= c.n_plugins) return ctx->fail("prefilter_status: range", KSG_E_RANGE);
+  const ksg::PodOutputs* o = c.outputs_of(q);
+  if (!o) return ctx->fail(c.err, KSG_E_STATE);
+  std::string m;
+  *code = c.prefilter_status(q, (int)pos, o->summary, m);
+  return put_str(ctx, m, msg, cap, len);
+}
+
+int ksg_prefilter_result(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len) {
+  KSG_GUARD(ctx);
+  Cluster& c = ctx->c;
+  if (q >= c.meta.size()) return ctx->fail("prefilter_result: range", KSG_E_RANGE);
+  std::string s = "null";  // PreFilterResult nil: every node
+  if (c.meta[q].restricted) {
+    s = "[";
+    for (size_t i = 0; i < c.meta[q].prefilter_names.size(); ++i) {
+      if (i) s += ',';
+      Cluster::jstr(s, c.meta[q].prefilter_names[i]);
+    }
+    s += "]";
+  }
+  return put_str(ctx, s, buf, cap, len);
+}
+
+int ksg_filter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, uint32_t node, int32_t* code, char* msg, size_t cap,
+                      size_t* len) {
+  KSG_GUARD(ctx);
+  Cluster& c = ctx->c;
+  if (!code || q >= c.meta.size() || (int)pos >= c.n_plugins) return ctx->fail("filter_status: range", KSG_E_RANGE);
+  if (node < c.lo || node >= c.hi) return ctx->fail("filter_status: node outside this context's nodes", KSG_E_RANGE);
+  const ksg::PodOutputs* o = c.outputs_of(q);
+  if (!o) return ctx->fail(c.err, KSG_E_STATE);
+  std::string m;
+  *code = c.filter_status(q, (int)pos, node - c.lo, *o, m);
+  return put_str(ctx, m, msg, cap, len);
+}
+
+int ksg_prescore_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code) {
+  KSG_GUARD(ctx);
+  Cluster& c = ctx->c;
+  if (!code || q >= c.meta.size() || (int)pos >= c.n_plugins) return ctx->fail("prescore_status: range", KSG_E_RANGE);
+  const ksg::PodOutputs* o = c.outputs_of(q);
+  if (!o) return ctx->fail(c.err, KSG_E_STATE);
+  *code = c.prescore_status(q, (int)pos, o->summary);
+  return KSG_OK;
+}
+
+int ksg_normalized_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int64_t* out, uint32_t n) {
+  KSG_GUARD(ctx);
+  Cluster& c = ctx->c;
+  if (!out || q >= c.meta.size()) return ctx->fail("normalized_scores: range", KSG_E_RANGE);
+  if ((int)pos >= c.n_plugins || c.dpos[pos] < 0) return ctx->fail("no device scores at this position", KSG_E_INVALID);
+  const std::vector<int32_t>* nm = c.normalized_of(q);
+  if (!nm) return ctx->fail(c.err, KSG_E_STATE);
+  const uint32_t N = c.hi - c.lo;
+  if (n < N) return KSG_E_NOBUF;
+  const size_t d = (size_t)c.dpos[pos];
+  for (uint32_t i = 0; i < N; ++i) out[i] = (*nm)[d * N + i];
   return KSG_OK;
 }
 

@@ -91,7 +91,7 @@ typedef struct ksg_aterm {
   int32_t ns_off;
   int32_t weight;    // preferred terms
   int32_t cls;       // pod class of the pods the term matches (class tables; -1 matches none)
-  int32_t pad;
+  int32_t nub;       // its key's base among the shared-key pairs (pc_dom), -1: one node per value (pc_cnt)
 } ksg_aterm;
 
 typedef struct ksg_tsc {
@@ -107,7 +107,10 @@ typedef struct ksg_tsc {
   int32_t first_of_key;  // first score constraint with this key (topoSize owner)
   int32_t cls;           // pod class counted (class tables; -1: the selector counts nothing)
   int32_t eff_cls;       // filter: class of the LAST filter constraint on this key (its count fills the pair)
-  int32_t sc_n, sc_off;  // score: classes whose counts share this constraint's pair (pool_i32)
+  int32_t nub;           // the key's base among the shared-key pairs (pc_dom), -1: one node per value (pc_cnt)
+  int32_t sc_n, sc_off;  // score: (class, nub) pairs whose counts share this constraint's pair (pool_i32)
+  int32_t pair_base;     // the key's first (key, value) pair, and its values (minMatchNum per block)
+  int32_t nvals;
   int32_t pad;
 } ksg_tsc;
 
@@ -122,6 +125,8 @@ typedef struct ksg_exist_term {
   int32_t ns_cnt;
   int32_t ns_off;    // into the table's value pool
   int32_t cls;       // term class (class tables), -1 none
+  int32_t toff;      // its table's offset in the term-class value pool
+  int32_t pad;
 } ksg_exist_term;
 
 // ---- class tables (PodTopologySpread / InterPodAffinity counts kept by the assume delta)
@@ -206,7 +211,7 @@ typedef struct ksg_prog {
   uint32_t tab;             // KTAB_*: PodTopologySpread / InterPodAffinity read the class tables
   int32_t aff_cls;          // required pod affinity: class of the pods matching every term (-1 none)
   int32_t n_pc_match, pc_match_off;  // pool_i32: pod classes this pod belongs to (its assume: +-1)
-  int32_t n_tc_match, tc_match_off;  // pool_i32: term classes whose terms match this pod
+  int32_t n_tc_match, tc_match_off;  // pool_i32: term classes whose terms match this pod (id, value offset, slot, group)
 
   // ---- pools (byte offsets from the start of the blob)
   uint32_t off_i32, n_i32;

@@ -16,9 +16,8 @@
 //            is logged and written by k_flush_appends after the run)
 //
 // Every node's inputs are loaded up front (the row, the topology values, the
-// class-table counts the pod reads) so their latencies overlap; block
-// reductions take one barrier.  The pod index lives on the device (A.cur,
-// advanced by k_select): a run is the same launches repeated.
+// class-table counts the pod reads, at offsets the program carries) so their
+// latencies overlap; block reductions take one barrier.
 // Upstream: schedule_one.go findNodesThatPassFilters / prioritizeNodes /
 // selectHost, framework.go RunFilterPlugins / RunScorePlugins, the plugins'
 // Filter / Score / NormalizeScore (restated in oracle/ksg_oracle.cpp).
@@ -26,8 +25,8 @@
 struct ChainArgs {
   const uint8_t* progs;
   const uint64_t* prog_off;
-  uint32_t* cur;           // pod index of the running cycle (device)
-  uint32_t end;            // cycles stop at this queue index
+  uint32_t q;              // the cycle's queue pod and its program (per launch)
+  const uint8_t* prog;
   ksg_pod_summary* sums;
   uint32_t keep_first, keep_n;
   uint32_t* kfilter;
@@ -188,7 +187,7 @@ __device__ __forceinline__ int64_t pts_count_tab(const DevCluster& C, const Prog
   const ksg_tsc& t = V.h->tsc[c];
   if (t.is_hostname) return t.cls < 0 ? 0 : C.T.pc_cnt[(size_t)t.cls * C.N + n];
   int64_t s = 0;
-  for (int k = 0; k < t.sc_n; ++k) s += pc_count(C, V.i32[t.sc_off + k], t.topo, n, v);
+  for (int k = 0; k < t.sc_n; ++k) s += pc_count(C, V.i32[t.sc_off + k], t.nub, n, v);
   return s;
 }
 
@@ -212,9 +211,9 @@ __device__ __forceinline__ uint32_t ipa_table_bits(const DevCluster& C, const De
       const ksg_aterm& t = pref[i - h->n_req_aff];
       if (t.cls >= 0 && C.T.pc_tot[(size_t)t.cls * KSG_MAX_TOPO + t.topo] > 0) bits |= 8u;
     } else {
-      const int j = i - h->n_req_aff - npref;
-      if (C.T.tc_tot[V.i32[h->tc_match_off + j]] > 0) {
-        const int grp = V.i32[h->tc_match_off + h->n_tc_match + j];
+      const int32_t* e = V.i32 + h->tc_match_off + 4 * (i - h->n_req_aff - npref);  // (class, offset, slot, group)
+      if (C.T.tc_tot[e[0]] > 0) {
+        const int grp = e[3];
         if (grp == KSG_TC_ANTI) bits |= 4u;
         else if (score_on && (grp == KSG_TC_PREF || F.ipa_hard_weight > 0)) bits |= 8u;
       }
@@ -243,11 +242,11 @@ __device__ __forceinline__ void eval_setup(const DevCluster& C, const DevProfile
   if (pts_on && !(h->flags & KPF_SKIP_PTS_FILTER)) {
     for (int c = 0; c < h->n_tsc_filter; ++c) {
       const ksg_tsc& t = h->tsc[c];
-      const uint32_t base = C.tbase[t.topo], cnt = C.tcount[t.topo];
+      const uint32_t base = (uint32_t)t.pair_base, cnt = (uint32_t)t.nvals;
       int32_t m = 0x7FFFFFFF;
       for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x)
         if (C.T.pair_node[base + i]) {
-          const int32_t x = t.eff_cls < 0 ? 0 : C.T.pc_dom[(size_t)t.eff_cls * C.T.NU + C.T.nu_base[t.topo] + i];
+          const int32_t x = t.eff_cls < 0 ? 0 : C.T.pc_dom[(size_t)t.eff_cls * C.T.NU + (uint32_t)t.nub + i];
           m = x < m ? x : m;
         }
       m = wave_min(m);
@@ -266,9 +265,8 @@ __device__ __forceinline__ void eval_setup(const DevCluster& C, const DevProfile
 // arguments compiled in.
 template <int ROWM>
 __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, ChainArgs A) {
-  const uint32_t q = *A.cur;
-  if (q >= A.end) return;
-  const ProgView V = view(A.progs + A.prog_off[q]);
+  const uint32_t q = A.q;
+  const ProgView V = view(A.prog);
   const ksg_prog* h = V.h;
   __shared__ EvalShared L;
   uint32_t* of;
@@ -301,7 +299,7 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
 #pragma unroll
   for (int c = 0; c < KSG_MAX_TSC; ++c) {
     ptsm[c] = 0;
-    if (pts_pos >= 0 && c < nf) ptsm[c] = pc_count(C, h->tsc[c].eff_cls, h->tsc[c].topo, nn, tv(h->tsc[c].topo));
+    if (pts_pos >= 0 && c < nf) ptsm[c] = pc_count(C, h->tsc[c].eff_cls, h->tsc[c].nub, nn, tv(h->tsc[c].topo));
   }
   bool counted = pts_score;
   int64_t pts_cnt = 0;
@@ -315,25 +313,25 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
     for (int i = 0; i < h->n_req_aff; ++i) {
       const int32_t v = tv(aff[i].topo);
       aff_miss |= v < 0;
-      aff_zero |= pc_count(C, h->aff_cls, aff[i].topo, nn, v) <= 0;
+      aff_zero |= pc_count(C, h->aff_cls, aff[i].nub, nn, v) <= 0;
     }
     for (int i = 0; i < h->n_req_anti; ++i) {
       const int32_t v = tv(anti[i].topo);
-      anti_hit |= v >= 0 && pc_count(C, anti[i].cls, anti[i].topo, nn, v) > 0;
+      anti_hit |= v >= 0 && pc_count(C, anti[i].cls, anti[i].nub, nn, v) > 0;
     }
     if (h->flags & KPF_IPA_HAS_CONSTRAINTS)
       for (int i = 0; i < h->n_pref_aff + h->n_pref_anti; ++i) {
         const ksg_aterm& t = pref[i];
-        const int64_t k = pc_count(C, t.cls, t.topo, nn, tv(t.topo));
+        const int64_t k = pc_count(C, t.cls, t.nub, nn, tv(t.topo));
         ipa_raw += i < h->n_pref_aff ? k * t.weight : -k * t.weight;
       }
     for (int i = 0; i < h->n_tc_match; ++i) {
-      const int grp = V.i32[h->tc_match_off + h->n_tc_match + i];
-      const int32_t u = V.i32[h->tc_match_off + i];
+      const int32_t* e = V.i32 + h->tc_match_off + 4 * i;  // (class, offset, slot, group)
+      const int grp = e[3];
       if (grp == KSG_TC_ANTI) {
-        exist_hit |= tc_value(C, u, nn, tv(C.T.tc_slot[u])) > 0;
+        exist_hit |= tc_value(C, (uint32_t)e[1], e[2], nn, tv(e[2])) > 0;
       } else if (score_on && (grp == KSG_TC_PREF || F.ipa_hard_weight > 0)) {
-        const int64_t k = tc_value(C, u, nn, tv(C.T.tc_slot[u]));
+        const int64_t k = tc_value(C, (uint32_t)e[1], e[2], nn, tv(e[2]));
         ipa_raw += grp == KSG_TC_HARD ? k * F.ipa_hard_weight : k;
       }
     }
@@ -551,9 +549,8 @@ struct FinalShared {
 
 // PodTopologySpread raw scores of a pod with several score constraints.
 __global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, ChainArgs A) {
-  const uint32_t q = *A.cur;
-  if (q >= A.end) return;
-  const ProgView V = view(A.progs + A.prog_off[q]);
+  const uint32_t q = A.q;
+  const ProgView V = view(A.prog);
   __shared__ FinalShared L;
   uint32_t* of;
   int32_t *os, *ot;
@@ -586,9 +583,8 @@ __global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, C
 }
 
 __global__ __launch_bounds__(kBlock) void k_final(DevCluster C, DevProfile F, ChainArgs A) {
-  const uint32_t q = *A.cur;
-  if (q >= A.end) return;
-  const ProgView V = view(A.progs + A.prog_off[q]);
+  const uint32_t q = A.q;
+  const ProgView V = view(A.prog);
   const ksg_prog* h = V.h;
   __shared__ FinalShared L;
   uint32_t* of;
@@ -710,9 +706,8 @@ __device__ __forceinline__ void assume_row_atomic(DevCluster& C, const ProgView&
 
 // selectHost + the assume: one block.
 __global__ __launch_bounds__(kBlock) void k_select(DevCluster C, DevProfile F, ChainArgs A) {
-  const uint32_t q = *A.cur;
-  if (q >= A.end) return;
-  const ProgView V = view(A.progs + A.prog_off[q]);
+  const uint32_t q = A.q;
+  const ProgView V = view(A.prog);
   const ksg_prog* h = V.h;
   __shared__ ChainRec lds[kBlock / 64];
   ChainRec r;
@@ -742,7 +737,6 @@ __global__ __launch_bounds__(kBlock) void k_select(DevCluster C, DevProfile F, C
         A.alog[i] = make_int2((int)q, node);
       }
     }
-    *A.cur = q + 1;
   }
   if (node >= 0) tables_assume(C, V, (uint32_t)node, +1, threadIdx.x, blockDim.x);
 }
@@ -803,10 +797,6 @@ __global__ __launch_bounds__(kBlock) void k_flush_appends(DevCluster C, ChainArg
   }
 }
 
-__global__ void k_set_cur(uint32_t* cur, uint32_t q) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) *cur = q;
-}
-
 // ---- class tables: build from the existing-pod table
 // pod classes [c0, c0 + nc): every live existing pod matching a class adds to its tables
 __global__ void k_pc_build(DevCluster C, uint32_t c0, uint32_t nc) {
@@ -835,7 +825,7 @@ __global__ void k_tc_build(DevCluster C, uint32_t u0) {
   if (C.ptflags[p] & KEF_DELETED) return;
   const ksg_exist_term& e = C.terms[t];
   if (e.cls < 0 || (uint32_t)e.cls < u0) return;
-  tc_add(C, e.cls, (uint32_t)C.ptnode[p], eterm_inc(e), +1);
+  tc_add(C, e, (uint32_t)C.ptnode[p], +1);
 }
 
 // Normalized scores of a kept pod (finalscore-result / ksg_normalized_scores):

@@ -76,6 +76,14 @@ def load_library():
     L.ksg_apply_events.argtypes = [vp, ctypes.c_char_p, sz]
     i64 = ctypes.c_int64
     L.ksg_node_nonzero.argtypes = [vp, ctypes.POINTER(i64), u32]
+    cp = ctypes.c_char_p
+    L.ksg_plugin_position.argtypes = [vp, cp, sz]
+    L.ksg_node_index.argtypes = [vp, cp, sz]
+    L.ksg_prefilter_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
+    L.ksg_prefilter_result.argtypes = [vp, u32, cp, sz, ctypes.POINTER(sz)]
+    L.ksg_filter_status.argtypes = [vp, u32, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
+    L.ksg_prescore_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32)]
+    L.ksg_normalized_scores.argtypes = [vp, u32, u32, ctypes.POINTER(i64), u32]
     L.ksg_synth_cluster.argtypes = [ctypes.c_int, i64, i64, i64, i64, ctypes.c_uint64, ctypes.POINTER(vp),
                                     ctypes.POINTER(sz)]
     L.ksg_free.argtypes = [vp]
@@ -227,6 +235,49 @@ class Scheduler:
         pc = (ctypes.c_int32 * n)()
         self._chk(self.L.ksg_node_requested(self.h, req, pc, n_res, n), "ksg_node_requested")
         return [list(req[r * n:(r + 1) * n]) for r in range(n_res)], list(pc)
+
+    # ---- the Go plugin's per-extension-point calls (ksg.h)
+    def plugin_position(self, name):
+        b = name.encode()
+        r = self.L.ksg_plugin_position(self.h, b, len(b))
+        return None if r < 0 else r
+
+    def node_index(self, name):
+        b = name.encode()
+        r = self.L.ksg_node_index(self.h, b, len(b))
+        return None if r < 0 else r
+
+    def _status(self, fn, *args):
+        code, n = ctypes.c_int32(), ctypes.c_size_t()
+        buf = ctypes.create_string_buffer(4096)
+        self._chk(fn(self.h, *args, ctypes.byref(code), buf, 4096, ctypes.byref(n)), fn.__name__)
+        return code.value, buf.raw[:n.value].decode()
+
+    def prefilter_status(self, q, pos):
+        """(framework.Code, message) of PreFilter at profile position pos; code -1: not run."""
+        return self._status(self.L.ksg_prefilter_status, q, pos)
+
+    def prefilter_result(self, q):
+        n = ctypes.c_size_t()
+        self.L.ksg_prefilter_result(self.h, q, None, 0, ctypes.byref(n))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._chk(self.L.ksg_prefilter_result(self.h, q, buf, n.value + 1, ctypes.byref(n)), "ksg_prefilter_result")
+        return json.loads(buf.raw[:n.value].decode())
+
+    def filter_status(self, q, pos, node):
+        """(framework.Code, Status.Message()) of Filter on a node; code -1: not called."""
+        return self._status(self.L.ksg_filter_status, q, pos, node)
+
+    def prescore_status(self, q, pos):
+        code = ctypes.c_int32()
+        self._chk(self.L.ksg_prescore_status(self.h, q, pos, ctypes.byref(code)), "ksg_prescore_status")
+        return code.value
+
+    def normalized_scores(self, q, pos):
+        n = self.n_nodes
+        arr = (ctypes.c_int64 * n)()
+        self._chk(self.L.ksg_normalized_scores(self.h, q, pos, arr, n), "ksg_normalized_scores")
+        return list(arr)
 
     def node_nonzero(self):
         """NonZeroRequested (cpu milli, memory bytes) rows of every local node."""

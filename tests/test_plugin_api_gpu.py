@@ -1,0 +1,129 @@
+"""The Go-plugin view of the boundary: every scheduling-result annotation the
+simulator's wrapped plugins record, rebuilt from the per-extension-point ABI
+calls alone (ksg_prefilter_status / ksg_prefilter_result / ksg_filter_status /
+ksg_prescore_status / ksg_scores / ksg_normalized_scores), must equal the
+engine's own annotations and the oracle's byte for byte.
+
+This is the recording a wrapped plugin does (simulator/scheduler/plugin/
+wrappedplugin.go: PreFilter :491-518 stores Status.Message() or "success" and
+the PreFilterResult; Filter :535 "passed" or the message; PreScore :472;
+Score :419 the raw score; NormalizeScore :400 the normalized score, which the
+result store multiplies by the plugin's weight, resultstore/store.go:504-507)
+and the serialisation the store does (encoding/json: sorted keys, no spaces).
+"""
+import json
+
+import pytest
+
+from _oracle import Oracle
+from ksg import Scheduler, generator as g
+
+P = "kube-scheduler-simulator.sigs.k8s.io/"
+SCORERS = {"NodeResourcesFit", "NodeResourcesBalancedAllocation", "TaintToleration", "NodeAffinity",
+           "PodTopologySpread", "InterPodAffinity", "ImageLocality"}
+C_SUCCESS, C_SKIP, C_NOT_RUN = 0, 5, -1
+
+CASES = [
+    ("cfg1", 1, dict(n_nodes=60, n_pods=90)),
+    ("cfg2", 2, dict(n_nodes=120, n_pods=60)),
+    ("cfg3", 3, dict(n_nodes=150, n_pods=60)),
+    ("cfg4", 4, dict(n_nodes=120, n_existing=500, n_pods=60, n_zones=5)),
+]
+
+
+def _js(v):
+    return json.dumps(v, separators=(",", ":"), sort_keys=True, ensure_ascii=False)
+
+
+def _store_weight(prof, name):
+    sw = prof.get("storeWeights", {})
+    if name not in sw:
+        return 0
+    return 1 if sw[name] == 0 else sw[name]
+
+
+def rebuild(s, q, prof, names, status):
+    plugins = prof["plugins"]
+    pre_status, pre_result = {}, {}
+    aborted = False
+    for pos, name in enumerate(plugins):
+        code, msg = s.prefilter_status(q, pos)
+        if code == C_NOT_RUN:
+            continue
+        pre_status[name] = "success" if code == C_SUCCESS else msg
+        aborted |= code not in (C_SUCCESS, C_SKIP)
+        if name == "NodeAffinity" and code == C_SUCCESS:
+            r = s.prefilter_result(q)
+            if r is not None:
+                pre_result[name] = r
+    filt, feasible = {}, []
+    for i, nm in enumerate(names):
+        row = {}
+        for pos, name in enumerate(plugins):
+            code, msg = s.filter_status(q, pos, i)
+            if code != C_NOT_RUN:
+                row[name] = "passed" if code == C_SUCCESS else msg
+        if row:
+            filt[nm] = row
+            if all(v == "passed" for v in row.values()):
+                feasible.append(i)
+    pre_score, score, fin = {}, {}, {}
+    if not aborted and len(feasible) > 1 and status != 2:
+        skipped = set()
+        for pos, name in enumerate(plugins):
+            code = s.prescore_status(q, pos)
+            if code == C_NOT_RUN:
+                continue
+            pre_score[name] = "success" if code == C_SUCCESS else ""
+            if code == C_SKIP:
+                skipped.add(name)
+        for pos, name in enumerate(plugins):
+            if name not in SCORERS or name in skipped:
+                continue
+            raw, norm, w = s.scores(q, pos), s.normalized_scores(q, pos), _store_weight(prof, name)
+            for i in feasible:
+                score.setdefault(names[i], {})[name] = str(raw[i])
+                fin.setdefault(names[i], {})[name] = str(norm[i] * w)
+    elif aborted:
+        filt = {}
+    return {P + "prefilter-result-status": _js(pre_status), P + "prefilter-result": _js(pre_result),
+            P + "filter-result": _js(filt), P + "prescore-result": _js(pre_score),
+            P + "score-result": _js(score), P + "finalscore-result": _js(fin)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
+def test_annotations_from_extension_point_calls(name, c, sizes):
+    doc = g.generate(c, **sizes)
+    o = Oracle(doc)
+    o.schedule(record=3)
+    s = Scheduler(doc["profile"])
+    d = dict(doc)
+    d["queue"] = []
+    s.load_cluster(d)
+    names = [n["metadata"]["name"] for n in doc["nodes"]]
+    for i, nm in enumerate(names):
+        assert s.node_index(nm) == i
+    assert s.node_index("no-such-node") is None
+    for pos, pl in enumerate(doc["profile"]["plugins"]):
+        assert s.plugin_position(pl) == pos
+    checked = 0
+    for i, pod in enumerate(doc["queue"]):
+        q, r = s.cycle(pod, commit=True)
+        assert (r.selected, r.feasible, r.status) == o.result(i), (name, i)
+        if i % 3:
+            continue
+        got = rebuild(s, q, doc["profile"], names, r.status)
+        eng, ora = s.annotations(q), o.annotations(i)
+        for k, v in got.items():
+            assert v == eng[k], (name, i, k)
+            assert v == ora[k], (name, i, k)
+        # Σ normalized × framework weight is the total the selection used
+        if r.selected >= 0 and r.feasible > 1:
+            tot = 0
+            for pos, pl in enumerate(doc["profile"]["plugins"]):
+                if pl in SCORERS and s.prescore_status(q, pos) == C_SUCCESS or pl == "ImageLocality":
+                    tot += s.normalized_scores(q, pos)[r.selected] * doc["profile"]["weights"][pl]
+            assert tot == r.total, (name, i)
+        checked += 1
+    assert checked >= 20

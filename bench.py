@@ -33,7 +33,9 @@ def parse():
     ap.add_argument("--nodes", type=int, default=5000)
     ap.add_argument("--pods", type=int, default=10000)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on a bounded sample (rank 0, N=1)")
-    ap.add_argument("--cpu-pods", type=int, default=0, help="pods in the CPU sample (0 = auto, ~15 s)")
+    ap.add_argument("--cpu-seconds", type=float, default=4.0, help="CPU time per oracle variant")
+    ap.add_argument("--extra", default="3,4", help="other BASELINE configs reported beside cfg2 (N=1 only)")
+    ap.add_argument("--extra-steps", type=int, default=2)
     ap.add_argument("--cpu-workers", type=int, default=16, help="parallelize.Until workers (upstream default 16)")
     return ap.parse_args()
 
@@ -65,28 +67,163 @@ def pmc_traffic(kernel):
     tallies 128-B requests at 64 B, MI355X_MICROARCH.md HBM section) + WRITE_SIZE,
     both in KB per dispatch.  None when no pass is committed."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
-    if not files:
-        return None
-    d = json.load(open(files[-1]))
-    k = d.get("kernels", {}).get(kernel)
-    return None if k is None else k["hbm_bytes_per_dispatch"]
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")), reverse=True):
+        k = json.load(open(f)).get("kernels", {}).get(kernel)  # newest pass that holds the kernel
+        if k is not None:
+            return k["hbm_bytes_per_dispatch"]
+    return None
 
 
-def cpu_baseline(doc, n_pods, workers):
-    """Time the oracle (the CPU restatement, test infrastructure) on a bounded sample."""
+def cpu_info():
+    """Host CPU facts for cpu_baseline: nproc, the CPUs this process may run on,
+    the cgroup CPU quota (the box's share), the CPU model."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpus"] = quota
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    info["model"] = model
+    info["all_core_workers"] = min(x for x in (info["affinity"], quota) if x)
+    return info
+
+
+def _timed_oracle(src, n_nodes, workers, record, seconds):
+    """Oracle pairs/s over the first pods of the queue, run until ~`seconds` of wall time."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _oracle import Oracle
-    res, secs = {}, 0.0
-    for w in sorted({1, workers}):
-        o = Oracle(doc)
+    o = Oracle(src)
+    pods, dt, chunk = 0, 0.0, 2
+    while dt < seconds:
         t = time.perf_counter()
-        done = o.schedule(n=n_pods, workers=w, record=0)
-        dt = time.perf_counter() - t
-        secs += dt
-        res[w] = done * len(doc["nodes"]) / dt
-    best_w = max(res, key=res.get)
-    return best_w, res, secs
+        done = o.schedule(n=chunk, workers=workers, record=record)
+        dt += time.perf_counter() - t
+        pods += done
+        if done < chunk:  # queue exhausted
+            break
+        chunk = max(1, min(4096, int(pods / max(dt, 1e-6) * 0.5)))
+    return pods * n_nodes / max(dt, 1e-9), pods, dt
+
+
+def cpu_baseline(src, n_nodes, workers, seconds, label):
+    """The oracle (the CPU restatement, test infrastructure; never the product) timed on
+    this host: plugin-only at 1 worker, at upstream's 16 parallelize.Until workers and at
+    all cores, and the "debuggable" result-store emulation (record=1) at 16 workers
+    (BASELINE.md CPU-baseline plan).  value = plugin-only at all cores."""
+    ci = cpu_info()
+    allw = ci["all_core_workers"]
+    runs = {}
+    for key, w, rec in (("plugins_1_worker", 1, 0), (f"plugins_{workers}_workers", workers, 0),
+                        (f"plugins_all_cores_{allw}_workers", allw, 0), (f"debuggable_{workers}_workers", workers, 1)):
+        if key in runs:
+            continue
+        rate, pods, dt = _timed_oracle(src, n_nodes, w, rec, seconds)
+        runs[key] = {"pairs_per_s": rate, "pods": pods, "s": round(dt, 2)}
+    head = runs[f"plugins_all_cores_{allw}_workers"]
+    return {"value": head["pairs_per_s"], "unit": "pairs/s", "cores": allw, "kind": "port",
+            "sample": f"{label}: the first pods of the same queue, each variant run for ~{seconds:.0f} s "
+                      f"(oracle = CPU restatement of the upstream plugins, parallelize.Until chunking); "
+                      f"value = plugin-only at all cores",
+            "variants": runs, "cpu": ci}
+
+
+def time_queue(s, torch, steps, warmup, dist=None):
+    """K timed steps of the whole queue from the same snapshot (reset inside the step),
+    bracketed by barrier + synchronize; no kernel sampling inside the timed region."""
+    n_pods = s.queue_len
+
+    def step():
+        s.reset()
+        s.schedule(0, n_pods, wait=False)
+        s.wait()
+
+    s.sample_kernel(0)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def sample_dominant(s, every):
+    """One more step, after the timed region, with HIP events on the engine stream
+    around every `every`-th launch of the dominant kernel: average duration (ms), samples."""
+    s.reset()
+    s.sample_kernel(every)
+    s.schedule(0, s.queue_len, wait=False)
+    s.wait()
+    ms, n = s.kernel_time()
+    s.sample_kernel(0)
+    return ms, n
+
+
+# cfg3 / cfg4 (BASELINE.json configs[2], configs[3]) at their full single-GPU size,
+# reported beside the cfg2 headline.  Algorithmic bytes: SURVEY.md §8(d), DESIGN.md.
+CFG3_PAIR_BYTES = 141      # 120 read + 21 written per (pod, node) pair
+CFG4_EVAL_NODE_BYTES = 68  # k_eval: node row 56 + zone id 4 + selector-class count 8; no per-pair writes
+
+
+def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
+    from ksg import Scheduler, generator as g
+    t0 = time.perf_counter()
+    blob = g.generate_native(c)  # native twin of the seeded generator (tests/test_synth.py)
+    doc = json.loads(blob)
+    gen_s = time.perf_counter() - t0
+    s = Scheduler(doc["profile"])
+    s.load_cluster(blob)
+    n_nodes, n_pods = s.n_nodes, s.queue_len
+    elapsed = time_queue(s, torch, steps, warmup)
+    kms, kn = sample_dominant(s, 16)
+    res = s.results()
+    if s.batch_path:
+        kname = "k_window"
+        tiles = (n_nodes + TILE - 1) // TILE
+        bpl = WINDOW * n_nodes * CFG3_PAIR_BYTES + 2 * tiles * WINDOW * 64 * 8 + 2 * REC_BYTES
+    else:
+        kname = "k_eval"
+        bpl = n_nodes * CFG4_EVAL_NODE_BYTES
+    achieved = bpl / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    out = {"metric": "filter+score pod x node pairs/sec", "value": n_nodes * n_pods * steps / elapsed,
+           "unit": "pairs/s", "steps": steps, "warmup": warmup, "ms_per_step": elapsed * 1e3 / steps,
+           "us_per_pod": elapsed * 1e6 / (steps * n_pods),
+           "scheduled_pods_per_s": sum(1 for r in res if r.status == 0) * steps / elapsed,
+           "config": {"workload": f"cfg{c}", "nodes": n_nodes, "existing_pods": len(doc["pods"]), "pods": n_pods,
+                      "profile": doc["profile"]["plugins"], "path": "window" if s.batch_path else "table chain"},
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(f"cfg{c}:{kname}"),
+                        "kernel": kname, "kernel_avg_us": kms * 1e3, "kernel_samples": kn, "bytes_per_launch": bpl},
+           "generate_s": round(gen_s, 1)}
+    del s
+    if cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(blob, n_nodes, cpu_workers, cpu_seconds, f"cfg{c}")
+    return out
 
 
 def main():
@@ -112,40 +249,13 @@ def main():
         s.set_exchange_rccl(rccl_unique_id_broadcast(s.L, rank))
     s.load_cluster(doc)
     n_nodes, n_pods = s.n_nodes, s.queue_len  # n_nodes: whole cluster
-    sample_every = 64
-
-    def step(timed):
-        s.reset()
-        s.sample_kernel(sample_every if timed else 0)
-        s.schedule(0, n_pods, wait=False)
-        s.wait()
-
-    for _ in range(a.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    ksum, kcount = 0.0, 0
-    for _ in range(a.steps):
-        step(True)
-        ms, n = s.kernel_time()
-        ksum += ms * n
-        kcount += n
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = time_queue(s, torch, a.steps, a.warmup, dist)
+    kernel_ms, kcount = sample_dominant(s, 64)
     res = s.results()
     scheduled = sum(1 for r in res if r.status == 0)
     pairs = float(n_nodes) * n_pods * a.steps  # n_nodes already spans all ranks
     value = pairs / elapsed
     ms_per_step = elapsed * 1e3 / a.steps
-    kernel_ms = ksum / max(kcount, 1)
     shard = n_nodes // world
     if s.batch_path:
         kname = "k_window"
@@ -178,13 +288,11 @@ def main():
                      "bytes_per_launch": bytes_per_launch},
     }
     if a.cpu_baseline and world == 1:
-        n_cpu = a.cpu_pods or n_pods
-        w, rates, secs = cpu_baseline(doc, n_cpu, a.cpu_workers)
-        out["cpu_baseline"] = {"value": rates[w], "unit": "pairs/s", "cores": w, "kind": "port",
-                               "sample": f"first {n_cpu} of {n_pods} pods x {n_nodes} nodes (same cfg2 cluster), "
-                                         f"oracle plugin-only path (parallelize.Until chunking), "
-                                         f"{secs:.1f} s of CPU runs; rates by workers: "
-                                         + ", ".join(f"{k}: {v:.3g}" for k, v in sorted(rates.items()))}
+        out["cpu_baseline"] = cpu_baseline(json.dumps(doc).encode(), n_nodes, a.cpu_workers, a.cpu_seconds, "cfg2")
+    if world == 1 and a.extra:
+        for c in (int(x) for x in a.extra.split(",") if x):
+            out[f"cfg{c}"] = extra_config(c, torch, a.extra_steps, 1, a.cpu_seconds if a.cpu_baseline else 0,
+                                          a.cpu_workers)
     print(json.dumps(out))
 
 

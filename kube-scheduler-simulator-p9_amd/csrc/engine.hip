@@ -1723,6 +1723,8 @@ __global__ __launch_bounds__(256) void k_static(DevCluster C, DevProfile F, cons
 
 __device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void st_sc1(int32_t* p, int32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_sc1(uint64_t* p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ int32_t ld_sc1(const int32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
@@ -3498,7 +3500,7 @@ struct Engine::Impl {
   uint32_t npc = 0, ntc = 0, NU = 0, nct = 0, ncreq = 0, ncval = 0, tc_used = 0;
   std::vector<uint32_t> tc_off_h;
   // table chain (k_eval / k_ptsraw / k_final / k_select)
-  DBuf<uint32_t> cur, alog_n;
+  DBuf<uint32_t> carrive;  // table chain: block arrivals of the cycle's last kernel
   DBuf<int2> alog;        // assumes whose existing-pod table rows k_flush_appends writes
   DBuf<int32_t> cpi, cpst;
   DBuf<int64_t> cpm, cpm2;
@@ -3539,6 +3541,8 @@ struct Engine::Impl {
   DBuf<int64_t> fit_w_d;
   bool stamps_on = false;  // diagnostic: s_memtime stamps in the fixup loop
   DBuf<uint64_t> stamps;
+  bool cstamps_on = false;  // diagnostic: table chain stamps
+  DBuf<uint64_t> cstamps;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0;
   // pristine copies for reset()
@@ -3759,12 +3763,12 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     if (!I.nu_base_d.upload(nb, s, err) || !I.slot_dom_d.upload(sd, s, err) || !I.pair_node_d.upload(pn, s, err))
       return false;
     I.cnblk = std::max<uint32_t>((ns.n + kBlock - 1) / kBlock, 1);
-    if (!I.cur.alloc(1, err) || !I.alog_n.alloc(1, err) || !I.cpi.alloc((size_t)KCP_I * I.cnblk, err) ||
+    if (!I.carrive.alloc(1, err) || !I.cpi.alloc((size_t)KCP_I * I.cnblk, err) ||
         !I.cpst.alloc(I.cnblk, err) ||
         !I.cpm.alloc((size_t)2 * KCP_X * I.cnblk, err) || !I.cpm2.alloc((size_t)2 * I.cnblk, err) ||
         !I.cpr.alloc((size_t)KSG_MAX_TSC * I.cnblk, err) || !I.cpk.alloc(I.cnblk, err))
       return false;
-    HIPCHK(hipMemsetAsync(I.alog_n.p, 0, sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(I.carrive.p, 0, sizeof(uint32_t), s));
   }
   // existing-pod table (capacity for device-side appends)
   I.pcap = std::max<uint32_t>(pod_cap, pt.n);
@@ -4516,12 +4520,15 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   CA.need_eph = I.any_eph_req ? 1u : 0u;
   if (!I.alog.alloc(std::max<uint32_t>(count, 1), err)) return false;
   CA.alog = I.alog.p;
-  CA.alog_n = I.alog_n.p;
+  CA.log_base = first;
+  CA.arrive = I.carrive.p;
+  CA.stamps = I.cstamps_on ? I.cstamps.p : nullptr;
   const int rowm = I.R > 4 ? 0 : (I.eval_mode == 1 ? 2 : 1);
   bool pending = false;           // logged assumes whose existing-pod table rows are not written yet
-  auto flush = [&]() {
-    if (pending) hipLaunchKernelGGL(k_flush_appends, dim3(1), b, 0, s, C, CA);
+  auto flush = [&](uint32_t j) {  // rows of the pods [log_base, j), then the log restarts at j
+    if (pending) hipLaunchKernelGGL(k_flush_appends, dim3(1), b, 0, s, C, CA, j - CA.log_base);
     pending = false;
+    CA.log_base = j;
   };
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
@@ -4537,15 +4544,14 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
         I.n_samples++;
       }
-      if (F.has_ext) {
+      if (F.has_ext) {  // (k_final's last block selects; without ScoreExtensions k_eval's)
         if (I.prog_need[j] & 8) hipLaunchKernelGGL(k_ptsraw, dim3(I.cnblk), b, 0, s, C, F, CA);
         hipLaunchKernelGGL(k_final, dim3(I.cnblk), b, 0, s, C, F, CA);
       }
-      hipLaunchKernelGGL(k_select, dim3(1), b, 0, s, C, F, CA);
       pending |= (CA.mode & 2) != 0;
       continue;
     }
-    flush();  // the scanning chain reads the existing-pod table
+    flush(j);  // the scanning chain reads the existing-pod table
     const int mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
     DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j, xchain ? nullptr : I.arrive1.p, mode, I.prow.p + j};
     bool kept = I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n;
@@ -4612,7 +4618,7 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
     }
     // unsharded: selectHost + assume folded into the last block of the cycle's last kernel
   }
-  flush();
+  flush(first + count);
   HIPCHK(hipEventRecord(I.ev1, s));
   HIPCHK(hipGetLastError());
   return true;
@@ -4728,9 +4734,18 @@ bool Engine::nccl_unique_id(void* out128, std::string& err) {
 }
 void Engine::set_path(int per_pod) { p_->force_per_pod = per_pod != 0; }
 bool Engine::eval_stamps(bool on, std::vector<uint64_t>* out, std::string& err) {
-  (void)on;
-  (void)err;
-  if (out) out->clear();  // the window kernel's eval blocks carry no stamps
+  Impl& I = *p_;  // table chain stamps (table_chain.hip CS_*): 64 slots
+  if (!out) {
+    I.cstamps_on = on;
+    if (on) {
+      if (!I.cstamps.alloc(64, err)) return false;
+      HIPCHK(hipMemset(I.cstamps.p, 0, 64 * 8));
+    }
+    return true;
+  }
+  out->assign(64, 0);
+  HIPCHK(hipStreamSynchronize(I.stream));
+  if (I.cstamps_on) HIPCHK(hipMemcpy(out->data(), I.cstamps.p, 64 * 8, hipMemcpyDeviceToHost));
   return true;
 }
 

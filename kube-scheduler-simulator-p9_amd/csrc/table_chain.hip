@@ -10,10 +10,11 @@
 //   k_ptsraw PodTopologySpread raw scores when the pod has several score
 //            constraints (one constraint: max / min follow from the counts)
 //   k_final  every block folds the partials, then per node: NormalizeScore,
-//            [0,100] check, weights, packed argmax key; per block the best key
-//   k_select one block: selectHost over the block keys, the summary, and the
-//            assume delta (node row, class tables; the existing-pod table row
-//            is logged and written by k_flush_appends after the run)
+//            [0,100] check, weights, packed argmax key; per block the best key;
+//            the last-arriving block: selectHost over the block keys, the
+//            summary, and the assume delta (node row, class tables; the
+//            existing-pod table row is logged and written by k_flush_appends)
+//   (a profile without ScoreExtensions: k_eval's last block selects)
 //
 // Every node's inputs are loaded up front (the row, the topology values, the
 // class-table counts the pod reads, at offsets the program carries) so their
@@ -43,11 +44,28 @@ struct ChainArgs {
   int32_t* pst;            // [nblk] status bits of k_final
   int mode;                // commit mode (as k_commit)
   int32_t* prow;           // existing-pod table row of each queue pod
-  int2* alog;              // (queue pod, local node) of the assumes whose table rows are pending
-  uint32_t* alog_n;
+  int2* alog;              // per pod of the run since the last flush: (queue pod, local node or -1)
+  uint32_t log_base;       // the run position alog[0] belongs to
+  uint32_t* arrive;        // block arrivals of the cycle's last kernel (its last block selects)
+  uint64_t* stamps;        // diagnostic (Engine::eval_stamps): block 0's s_memrealtime deltas, or null
 };
 
-enum { KCP_FEAS = 0, KCP_IGN = 1, KCP_STAT = 2, KCP_I = 3 };
+// Diagnostic stamps: block 0 / thread 0 of each chain kernel adds (now - entry)
+// at its points (k_eval slots 0-7, k_ptsraw 8-15, k_final 16-23, its last block's select 24-27),
+// entry-to-entry gaps k_eval->k_final 40, k_final->next k_eval 42 (last
+// entries kept in 48-49), pods in 63.  100 MHz counter.
+#define CS_ON (A.stamps && blockIdx.x == 0 && threadIdx.x == 0)
+#define CS_BEGIN const uint64_t cs_t0 = CS_ON ? __builtin_amdgcn_s_memrealtime() : 0
+#define CS(k) \
+  if (CS_ON) atomicAdd((unsigned long long*)&A.stamps[k], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - cs_t0))
+#define CS_GAP(gap, prev, mine)                                                                  \
+  if (CS_ON) {                                                                                   \
+    const uint64_t pv = A.stamps[prev];                                                          \
+    if (pv) atomicAdd((unsigned long long*)&A.stamps[gap], (unsigned long long)(cs_t0 - pv));    \
+    A.stamps[mine] = cs_t0;                                                                      \
+  }
+
+enum { KCP_FEAS = 0, KCP_IGN = 1, KCP_STAT = 2, KCP_IPAF = 3, KCP_I = 4 };  // KCP_IPAF: block 0 only
 enum { KCX_TAINT = 0, KCX_NA = 1, KCX_PTS = 2, KCX_IPA = 3, KCP_X = 4 };
 __device__ __forceinline__ int chain_x(int plugin) {
   return plugin == KP_TAINT ? KCX_TAINT : plugin == KP_NA ? KCX_NA : plugin == KP_PTS ? KCX_PTS
@@ -91,19 +109,6 @@ __device__ __forceinline__ void rec_init(ChainRec& r) {
   for (int c = 0; c < KSG_MAX_TSC; ++c) r.reg[c] = 0;
   r.key = 0;
 }
-__device__ __forceinline__ void rec_fold(ChainRec& a, const ChainRec& b) {
-  a.feas += b.feas;
-  a.ign += b.ign;
-  a.st |= b.st;
-#pragma unroll
-  for (int x = 0; x < KCP_X; ++x) {
-    a.mx[x] = b.mx[x] > a.mx[x] ? b.mx[x] : a.mx[x];
-    a.mn[x] = b.mn[x] < a.mn[x] ? b.mn[x] : a.mn[x];
-  }
-#pragma unroll
-  for (int c = 0; c < KSG_MAX_TSC; ++c) a.reg[c] |= b.reg[c];
-  a.key = b.key > a.key ? b.key : a.key;
-}
 // run-time slot x of a record's normaliser arrays without dynamic indexing
 // (which would place the record in scratch)
 __device__ __forceinline__ void rec_minmax(ChainRec& r, int x, int64_t v) {
@@ -126,40 +131,21 @@ __device__ __forceinline__ int64_t rec_mn(const ChainRec& r, int x) {
   for (int i = 0; i < KCP_X; ++i) v = i == x ? r.mn[i] : v;
   return v;
 }
-// field-wise copies (an aggregate copy to / from LDS would put the record in scratch)
-__device__ __forceinline__ void rec_store(ChainRec* d, const ChainRec& r) {
-  d->feas = r.feas;
-  d->ign = r.ign;
-  d->st = r.st;
-#pragma unroll
-  for (int x = 0; x < KCP_X; ++x) {
-    d->mx[x] = r.mx[x];
-    d->mn[x] = r.mn[x];
+// Block reduction of the record fields `what` names (RB_*; xmask / nreg: the
+// normaliser slots / registration masks in use): wave folds on the DPP, one LDS
+// record per wave, one barrier; every thread returns the block's record (the
+// other fields keep their values).
+enum { RB_CNT = 1, RB_CNT16 = 2, RB_ST = 4, RB_KEY = 8 };  // RB_CNT16: feas, ign < 2^15 per wave (one sum)
+__device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t xmask, int nreg, uint32_t what) {
+  if (what & RB_CNT16) {
+    const int32_t p = wave_sum(r.feas | (r.ign << 16));
+    r.feas = p & 0xFFFF;
+    r.ign = p >> 16;
+  } else if (what & RB_CNT) {
+    r.feas = wave_sum(r.feas);
+    r.ign = wave_sum(r.ign);
   }
-#pragma unroll
-  for (int c = 0; c < KSG_MAX_TSC; ++c) d->reg[c] = r.reg[c];
-  d->key = r.key;
-}
-__device__ __forceinline__ void rec_load(ChainRec& r, const ChainRec* d) {
-  r.feas = d->feas;
-  r.ign = d->ign;
-  r.st = d->st;
-#pragma unroll
-  for (int x = 0; x < KCP_X; ++x) {
-    r.mx[x] = d->mx[x];
-    r.mn[x] = d->mn[x];
-  }
-#pragma unroll
-  for (int c = 0; c < KSG_MAX_TSC; ++c) r.reg[c] = d->reg[c];
-  r.key = d->key;
-}
-// Block reduction of a record: wave folds on the DPP, one LDS record per wave,
-// one barrier; every thread returns the block's record.  xmask / nreg: the
-// normaliser slots / registration masks in use (the rest stay at their identity).
-__device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t xmask, int nreg) {
-  r.feas = wave_sum(r.feas);
-  r.ign = wave_sum(r.ign);
-  r.st = wave_or(r.st);
+  if (what & RB_ST) r.st = wave_or(r.st);
 #pragma unroll
   for (int x = 0; x < KCP_X; ++x)
     if ((xmask >> x) & 1u) {
@@ -169,15 +155,45 @@ __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t x
 #pragma unroll
   for (int c = 0; c < KSG_MAX_TSC; ++c)
     if (c < nreg) r.reg[c] = wave_or64(r.reg[c]);
-  r.key = wave_max(r.key);
-  if (lane0()) rec_store(lds + (threadIdx.x >> 6), r);
-  __syncthreads();
-  rec_load(r, lds);
+  if (what & RB_KEY) r.key = wave_max(r.key);
+  ChainRec* w = lds + (threadIdx.x >> 6);
+  if (lane0()) {
+    w->feas = r.feas;
+    w->ign = r.ign;
+    w->st = r.st;
 #pragma unroll
-  for (int i = 1; i < kBlock / 64; ++i) {
-    ChainRec o;
-    rec_load(o, lds + i);
-    rec_fold(r, o);
+    for (int x = 0; x < KCP_X; ++x)
+      if ((xmask >> x) & 1u) {
+        w->mx[x] = r.mx[x];
+        w->mn[x] = r.mn[x];
+      }
+#pragma unroll
+    for (int c = 0; c < KSG_MAX_TSC; ++c)
+      if (c < nreg) w->reg[c] = r.reg[c];
+    w->key = r.key;
+  }
+  __syncthreads();
+  const bool cnt = (what & (RB_CNT | RB_CNT16)) != 0;
+  if (cnt) r.feas = r.ign = 0;
+  if (what & RB_ST) r.st = 0;
+#pragma unroll
+  for (int i = 0; i < kBlock / 64; ++i) {
+    const ChainRec* o = lds + i;
+    if (cnt) {
+      r.feas += o->feas;
+      r.ign += o->ign;
+    }
+    if (what & RB_ST) r.st |= o->st;
+#pragma unroll
+    for (int x = 0; x < KCP_X; ++x)
+      if ((xmask >> x) & 1u) {
+        r.mx[x] = o->mx[x] > r.mx[x] ? o->mx[x] : r.mx[x];
+        r.mn[x] = o->mn[x] < r.mn[x] ? o->mn[x] : r.mn[x];
+      }
+#pragma unroll
+    for (int c = 0; c < KSG_MAX_TSC; ++c)
+      if (c < nreg) r.reg[c] |= o->reg[c];
+    if (what & RB_KEY) r.key = o->key > r.key ? o->key : r.key;
   }
 }
 
@@ -260,11 +276,75 @@ __device__ __forceinline__ void eval_setup(const DevCluster& C, const DevProfile
   lds_barrier();
 }
 
+// The assume delta's node row as fire-and-forget atomics (no load on the
+// chain's critical path).
+__device__ __forceinline__ void assume_row_atomic(DevCluster& C, const ProgView& V, uint32_t n, int sign) {
+  const ksg_prog* h = V.h;
+  for (uint32_t r = 0; r < C.R; ++r)
+    if (h->req[r]) atomicAdd((unsigned long long*)&C.req[(size_t)r * C.N + n], (unsigned long long)(sign * h->req[r]));
+  atomicAdd((unsigned long long*)&C.nzc[n], (unsigned long long)(sign * h->nz_cpu));
+  atomicAdd((unsigned long long*)&C.nzm[n], (unsigned long long)(sign * h->nz_mem));
+  atomicAdd(&C.podcnt[n], sign);
+  for (int i = 0; i < h->n_port_own; ++i) atomicAdd(&C.ports[(size_t)V.i32[h->port_own_off + i] * C.N + n], sign);
+}
+
+// selectHost + the assume, by the last-arriving block of the cycle's last
+// kernel: the block keys / statuses were stored sc1 before each block arrived
+// (MI355X_MICROARCH.md hand-off: agent-scope stores, counter, agent-scope loads).
+__device__ __forceinline__ void chain_last_select(DevCluster& C, const DevProfile& F, const ChainArgs& A, ChainRec* lds) {
+  __shared__ uint32_t last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(A.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!last) return;
+  const uint64_t cs_t0 = CS_ON ? __builtin_amdgcn_s_memrealtime() : 0;
+  const uint32_t q = A.q, NB = A.nblk;
+  const ProgView V = view(A.prog);
+  const ksg_prog* h = V.h;
+  ChainRec r;
+  rec_init(r);
+  for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) {
+    const uint64_t k = ld_sc1(A.pk + b);
+    r.key = k > r.key ? k : r.key;
+    r.feas += ld_sc1(A.pi + KCP_FEAS * NB + b);
+    r.st |= ld_sc1(A.pi + KCP_STAT * NB + b) | ld_sc1(A.pst + b);
+  }
+  CS(24);
+  rec_block(r, lds, 0u, 0, RB_CNT | RB_ST | RB_KEY);
+  CS(25);
+  const bool error = (r.st & 2) || ((r.st & 4) && r.feas > 1) || (h->flags & KPF_PREFILTER_ERROR);
+  int32_t node = -1;
+  const uint32_t g = (uint32_t)(r.key & 0xFFFFFull);
+  if (!error && r.feas > 0 && (A.mode & 1) && g >= C.goff && g - C.goff < C.N) node = (int32_t)(g - C.goff);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(A.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ksg_pod_summary* S = A.sums + q;
+    S->feasible = r.feas;
+    S->best_key = r.key;
+    if (error) { S->status = 2; S->selected = -1; }
+    else if (r.feas == 0) { S->status = 1; S->selected = -1; }
+    else { S->status = 0; S->selected = (int32_t)g; }
+    A.prow[q] = -1;
+    // the existing-pod table row: written after the run (k_flush_appends)
+    A.alog[q - A.log_base] = make_int2((int)q, node >= 0 && (A.mode & 2) ? node : -1);
+    if (node >= 0) assume_row_atomic(C, V, (uint32_t)node, +1);
+  }
+  CS(26);
+  if (node >= 0) tables_assume(C, V, (uint32_t)node, +1, threadIdx.x, blockDim.x);
+  CS(27);
+  if (CS_ON) atomicAdd((unsigned long long*)&A.stamps[63], 1ull);
+}
+
 // ROWM: 0 resource columns read by the plugins (more than 4 columns), 1 the
 // node row loaded up front (RowV), 2 the same with the default Fit / BA
 // arguments compiled in.
 template <int ROWM>
 __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, ChainArgs A) {
+  CS_BEGIN;
+  CS_GAP(42, 49, 48);
   const uint32_t q = A.q;
   const ProgView V = view(A.prog);
   const ksg_prog* h = V.h;
@@ -336,7 +416,9 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
       }
     }
   }
+  CS(1);
   eval_setup(C, F, V, L, pts_pos >= 0, ipa_pos >= 0);
+  CS(2);
   const uint32_t ipa_flags = L.ipa_flags;
   uint32_t code = KSG_FILTER_NOT_EVALUATED;
   bool err = false;
@@ -401,6 +483,7 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
   }
   const bool feasible = active && code == KSG_FILTER_PASS;
   if (active) of[n] = code;
+  CS(3);
   counted &= feasible;
   ChainRec rec;
   rec_init(rec);
@@ -454,12 +537,15 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
     ot[n] = (int32_t)tot;
     rec.key = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
   }
-  rec_block(rec, L.rec, F.has_ext ? xmask : 0u, nreg);
+  CS(4);
+  rec_block(rec, L.rec, F.has_ext ? xmask : 0u, nreg, RB_CNT16 | RB_ST | (F.has_ext ? 0u : RB_KEY));
+  CS(5);
   if (threadIdx.x == 0) {
     const uint32_t b = blockIdx.x, NB = A.nblk;
     A.pi[KCP_FEAS * NB + b] = rec.feas;
     A.pi[KCP_IGN * NB + b] = rec.ign;
     A.pi[KCP_STAT * NB + b] = rec.st;
+    if (b == 0) A.pi[KCP_IPAF * NB] = (int32_t)ipa_flags;
     if (F.has_ext) {
 #pragma unroll
       for (int x = 0; x < KCP_X; ++x) {
@@ -469,11 +555,15 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
 #pragma unroll
       for (int c = 0; c < KSG_MAX_TSC; ++c)
         if (c < nreg) A.pr[(size_t)c * NB + b] = rec.reg[c];
-    } else {
-      A.pk[b] = rec.key;
-      A.pst[b] = 0;
+    } else {  // no ScoreExtensions: this is the cycle's last kernel
+      st_sc1(A.pk + b, rec.key);
+      st_sc1(A.pst + b, 0);
+      st_sc1(A.pi + KCP_FEAS * NB + b, rec.feas);
+      st_sc1(A.pi + KCP_STAT * NB + b, rec.st);
     }
   }
+  CS(6);
+  if (!F.has_ext) chain_last_select(C, F, A, L.rec);
 }
 
 // k_eval's partials folded (every block of k_ptsraw / k_final does it for itself)
@@ -482,8 +572,14 @@ struct EvalTotals {
   ChainRec r;
   double w[KSG_MAX_TSC];
 };
-__device__ __forceinline__ void reduce_eval(const DevCluster& C, const ChainArgs& A, const ksg_prog* h, EvalTotals& E, ChainRec* lds) {
+__device__ __forceinline__ void reduce_eval(const DevCluster& C, const DevProfile& F, const ChainArgs& A, const ksg_prog* h,
+                                            EvalTotals& E, ChainRec* lds) {
   const uint32_t NB = A.nblk;
+  uint32_t xmask = 0;
+  for (int p = 0; p < F.n; ++p) {
+    const int x = chain_x(F.plugins[p]);
+    if (x >= 0) xmask |= 1u << x;
+  }
   const int ns = h->n_tsc_score;
   ChainRec& r = E.r;
   rec_init(r);
@@ -493,6 +589,7 @@ __device__ __forceinline__ void reduce_eval(const DevCluster& C, const ChainArgs
     r.st |= A.pi[KCP_STAT * NB + b];
 #pragma unroll
     for (int x = 0; x < KCP_X; ++x) {
+      if (!((xmask >> x) & 1u)) continue;
       const int64_t a = A.pm[(2 * x) * NB + b], c = A.pm[(2 * x + 1) * NB + b];
       r.mx[x] = a > r.mx[x] ? a : r.mx[x];
       r.mn[x] = c < r.mn[x] ? c : r.mn[x];
@@ -501,7 +598,7 @@ __device__ __forceinline__ void reduce_eval(const DevCluster& C, const ChainArgs
     for (int c = 0; c < KSG_MAX_TSC; ++c)
       if (c < ns) r.reg[c] |= A.pr[(size_t)c * NB + b];
   }
-  rec_block(r, lds, (1u << KCP_X) - 1, ns);
+  rec_block(r, lds, xmask, ns, RB_CNT | RB_ST);
   const int nf = h->n_tsc_filter;
 #pragma unroll
   for (int c = 0; c < KSG_MAX_TSC; ++c) {  // scoring.go initPreScoreState topoSize
@@ -563,7 +660,7 @@ __global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, C
   load_slot_vids(C, active ? n : 0, true, L.tv);
   const SlotVids tv{L.tv + threadIdx.x};
   EvalTotals E;
-  reduce_eval(C, A, V.h, E, L.rec);
+  reduce_eval(C, F, A, V.h, E, L.rec);
   ChainRec r;
   rec_init(r);
   if (active && of[n] == KSG_FILTER_PASS) {
@@ -575,7 +672,7 @@ __global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, C
     }
   }
   __syncthreads();  // L.rec reused
-  rec_block(r, L.rec, 1u << KCX_PTS, 0);
+  rec_block(r, L.rec, 1u << KCX_PTS, 0, 0u);
   if (threadIdx.x == 0) {
     A.pm2[blockIdx.x] = r.mx[KCX_PTS];
     A.pm2[A.nblk + blockIdx.x] = r.mn[KCX_PTS];
@@ -583,6 +680,8 @@ __global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, C
 }
 
 __global__ __launch_bounds__(kBlock) void k_final(DevCluster C, DevProfile F, ChainArgs A) {
+  CS_BEGIN;
+  CS_GAP(40, 48, 49);
   const uint32_t q = A.q;
   const ProgView V = view(A.prog);
   const ksg_prog* h = V.h;
@@ -595,11 +694,11 @@ __global__ __launch_bounds__(kBlock) void k_final(DevCluster C, DevProfile F, Ch
   int32_t raw[KSG_MAX_PLUGINS];  // this node's raw scores, loaded before the folds
 #pragma unroll
   for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) raw[pos] = (mine && pos < F.n) ? os[(size_t)pos * C.N + n] : 0;
-  bool ipa = false;
-  for (int p = 0; p < F.n; ++p) ipa |= F.plugins[p] == KP_IPA;
-  if (threadIdx.x == 0) L.ipa_flags = 0;
+  const uint32_t ipa_flags = (uint32_t)A.pi[KCP_IPAF * A.nblk];  // k_eval's block 0
   EvalTotals E;
-  reduce_eval(C, A, h, E, L.rec);  // (its barrier also publishes L.ipa_flags = 0)
+  CS(16);
+  reduce_eval(C, F, A, h, E, L.rec);
+  CS(17);
   const bool multi = (h->tab & KTAB_PTS_MULTI) != 0;
   int64_t pmx = INT64_MIN, pmn = INT64_MAX;  // PodTopologySpread raw max / min over counted nodes
   if (multi) {
@@ -610,19 +709,14 @@ __global__ __launch_bounds__(kBlock) void k_final(DevCluster C, DevProfile F, Ch
       r.mn[KCX_PTS] = A.pm2[A.nblk + b] < r.mn[KCX_PTS] ? A.pm2[A.nblk + b] : r.mn[KCX_PTS];
     }
     __syncthreads();  // L.rec reused
-    rec_block(r, L.rec, 1u << KCX_PTS, 0);
+    rec_block(r, L.rec, 1u << KCX_PTS, 0, 0u);
     pmx = r.mx[KCX_PTS];
     pmn = r.mn[KCX_PTS];
   } else if (E.r.mx[KCX_PTS] != INT64_MIN) {  // one constraint: raw is monotone in the count
     pmx = pts_raw1(h, E, E.r.mx[KCX_PTS]);
     pmn = pts_raw1(h, E, E.r.mn[KCX_PTS]);
   }
-  if (ipa) {  // InterPodAffinity PreScore Skip: from the tables, as k_eval's blocks did
-    const uint32_t bits = __ockl_wfred_or_u32(ipa_table_bits(C, F, V));
-    if (lane0() && bits) atomicOr(&L.ipa_flags, bits);
-    lds_barrier();
-  }
-  const uint32_t ipa_flags = L.ipa_flags;
+  CS(18);
   // the summary's normalisers per position (max over feasible nodes; unset as k_init_summaries)
   int64_t smx[KSG_MAX_PLUGINS], smn[KSG_MAX_PLUGINS];
 #pragma unroll
@@ -684,68 +778,21 @@ __global__ __launch_bounds__(kBlock) void k_final(DevCluster C, DevProfile F, Ch
     r.key = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
     r.st = (E.r.feas > 1 && range_err) ? 4 : 0;
   }
+  CS(19);
   __syncthreads();  // L.rec reused
-  rec_block(r, L.rec, 0u, 0);
+  rec_block(r, L.rec, 0u, 0, RB_ST | RB_KEY);
   if (threadIdx.x == 0) {
-    A.pk[blockIdx.x] = r.key;
-    A.pst[blockIdx.x] = r.st;
+    st_sc1(A.pk + blockIdx.x, r.key);
+    st_sc1(A.pst + blockIdx.x, r.st);
   }
-}
-
-// The assume delta's node row as fire-and-forget atomics (k_select: no load on
-// the chain's critical path).
-__device__ __forceinline__ void assume_row_atomic(DevCluster& C, const ProgView& V, uint32_t n, int sign) {
-  const ksg_prog* h = V.h;
-  for (uint32_t r = 0; r < C.R; ++r)
-    if (h->req[r]) atomicAdd((unsigned long long*)&C.req[(size_t)r * C.N + n], (unsigned long long)(sign * h->req[r]));
-  atomicAdd((unsigned long long*)&C.nzc[n], (unsigned long long)(sign * h->nz_cpu));
-  atomicAdd((unsigned long long*)&C.nzm[n], (unsigned long long)(sign * h->nz_mem));
-  atomicAdd(&C.podcnt[n], sign);
-  for (int i = 0; i < h->n_port_own; ++i) atomicAdd(&C.ports[(size_t)V.i32[h->port_own_off + i] * C.N + n], sign);
-}
-
-// selectHost + the assume: one block.
-__global__ __launch_bounds__(kBlock) void k_select(DevCluster C, DevProfile F, ChainArgs A) {
-  const uint32_t q = A.q;
-  const ProgView V = view(A.prog);
-  const ksg_prog* h = V.h;
-  __shared__ ChainRec lds[kBlock / 64];
-  ChainRec r;
-  rec_init(r);
-  for (uint32_t b = threadIdx.x; b < A.nblk; b += blockDim.x) {
-    r.key = A.pk[b] > r.key ? A.pk[b] : r.key;
-    r.feas += A.pi[KCP_FEAS * A.nblk + b];
-    r.st |= A.pi[KCP_STAT * A.nblk + b] | A.pst[b];
-  }
-  rec_block(r, lds, 0u, 0);
-  const bool error = (r.st & 2) || ((r.st & 4) && r.feas > 1) || (h->flags & KPF_PREFILTER_ERROR);
-  int32_t node = -1;
-  const uint32_t g = (uint32_t)(r.key & 0xFFFFFull);
-  if (!error && r.feas > 0 && (A.mode & 1) && g >= C.goff && g - C.goff < C.N) node = (int32_t)(g - C.goff);
-  if (threadIdx.x == 0) {
-    ksg_pod_summary* S = A.sums + q;
-    S->feasible = r.feas;
-    S->best_key = r.key;
-    if (error) { S->status = 2; S->selected = -1; }
-    else if (r.feas == 0) { S->status = 1; S->selected = -1; }
-    else { S->status = 0; S->selected = (int32_t)g; }
-    A.prow[q] = -1;
-    if (node >= 0) {
-      assume_row_atomic(C, V, (uint32_t)node, +1);
-      if (A.mode & 2) {  // the existing-pod table row: written after the run (k_flush_appends)
-        const uint32_t i = atomicAdd(A.alog_n, 1u);
-        A.alog[i] = make_int2((int)q, node);
-      }
-    }
-  }
-  if (node >= 0) tables_assume(C, V, (uint32_t)node, +1, threadIdx.x, blockDim.x);
+  CS(20);
+  chain_last_select(C, F, A, L.rec);
 }
 
 // The existing-pod table rows of the run's logged assumes, in log order (one
 // block): exclusive scans of their entry counts, then every row written at its
 // offsets; the programs' prow entries point at them.
-__global__ __launch_bounds__(kBlock) void k_flush_appends(DevCluster C, ChainArgs A) {
-  const uint32_t cnt = *A.alog_n;
+__global__ __launch_bounds__(kBlock) void k_flush_appends(DevCluster C, ChainArgs A, uint32_t cnt) {
   __shared__ uint32_t base[4], tot[4];
   __shared__ uint32_t scan[4][kBlock];
   __shared__ int32_t over;
@@ -759,7 +806,7 @@ __global__ __launch_bounds__(kBlock) void k_flush_appends(DevCluster C, ChainArg
     int2 e = make_int2(0, 0);
     if (i < cnt) {
       e = A.alog[i];
-      table_need(view(A.progs + A.prog_off[e.x]), need);
+      if (e.y >= 0) table_need(view(A.progs + A.prog_off[e.x]), need);
     }
     for (int k = 0; k < 4; ++k) scan[k][threadIdx.x] = need[k];
     __syncthreads();
@@ -772,7 +819,7 @@ __global__ __launch_bounds__(kBlock) void k_flush_appends(DevCluster C, ChainArg
     }
     if (threadIdx.x == blockDim.x - 1)
       for (int k = 0; k < 4; ++k) tot[k] = scan[k][threadIdx.x];
-    if (i < cnt) {
+    if (i < cnt && e.y >= 0) {
       uint32_t off[4];
       bool fits = true;
       for (int k = 0; k < 4; ++k) {
@@ -791,10 +838,7 @@ __global__ __launch_bounds__(kBlock) void k_flush_appends(DevCluster C, ChainArg
     __syncthreads();
   }
   if (threadIdx.x < 4) C.tcounts[threadIdx.x] = base[threadIdx.x] < cap[threadIdx.x] ? base[threadIdx.x] : cap[threadIdx.x];
-  if (threadIdx.x == 0) {
-    if (over) C.tcounts[4] = 1;
-    *A.alog_n = 0;
-  }
+  if (threadIdx.x == 0 && over) C.tcounts[4] = 1;
 }
 
 // ---- class tables: build from the existing-pod table

@@ -1,0 +1,50 @@
+"""Where a table-chain cycle spends its time (cfg4): block 0's s_memrealtime
+deltas per kernel point, averaged over the pods of a run (table_chain.hip CS_*).
+
+usage: python tools/chain_stamps.py [--nodes N] [--existing E] [--pods P]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
+
+NAMES = {0: "k_eval: issue loads", 1: "k_eval: loads issued", 2: "k_eval: after eval_setup", 3: "k_eval: filter done",
+         4: "k_eval: scores done", 5: "k_eval: block reduce", 6: "k_eval: partials written",
+         16: "k_final: raw loads issued", 17: "k_final: partials folded", 18: "k_final: ipa bits",
+         19: "k_final: normalized + key", 20: "k_final: block key written",
+         24: "k_select: partials loaded", 25: "k_select: block reduce", 26: "k_select: summary + row atomics",
+         27: "k_select: class tables", 40: "gap k_eval->k_final entry", 41: "gap k_final->k_select entry",
+         42: "gap k_select->next k_eval entry"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=50000)
+    ap.add_argument("--existing", type=int, default=200000)
+    ap.add_argument("--pods", type=int, default=600)
+    a = ap.parse_args()
+    import torch
+    assert torch.cuda.is_available()
+    from ksg import Scheduler, generator as g
+    blob = g.generate_native(4, n_nodes=a.nodes, n_pods=a.pods, n_existing=a.existing)
+    doc = json.loads(blob)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(blob)
+    s.schedule(0, 64)
+    s.L.ksg_debug_eval_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    s.L.ksg_debug_eval_stamps(s.h, 1, None, None)
+    s.schedule(64, s.queue_len - 64)
+    out = (ctypes.c_uint64 * 64)()
+    n = ctypes.c_size_t()
+    s.L.ksg_debug_eval_stamps(s.h, 1, out, ctypes.byref(n))
+    pods = out[63] or 1
+    res = {NAMES.get(k, str(k)): round(out[k] / pods * 0.01, 3) for k in sorted(NAMES) if out[k]}
+    print(json.dumps({"pods": pods, "us_avg_block0": res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -184,8 +184,8 @@ int ksg_prefilter_result(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t
 /* Filter (wrappedplugin.go:535, mock framework.go:114) on one node. */
 int ksg_filter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, uint32_t node, int32_t* code, char* msg, size_t cap,
                       size_t* len);
-/* PreScore (wrappedplugin.go:472, mock framework.go:233). */
-int ksg_prescore_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code);
+/* PreScore (wrappedplugin.go:472, mock framework.go:233): status and message. */
+int ksg_prescore_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code, char* msg, size_t cap, size_t* len);
 /* NormalizeScore (wrappedplugin.go:400, mock framework.go:338): the plugin's
  * normalized score per local node (raw score for plugins without
  * ScoreExtensions), computed on the device by the NormalizeScore the selection

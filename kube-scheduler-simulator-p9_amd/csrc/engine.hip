@@ -187,6 +187,13 @@ __device__ __forceinline__ ProgView view(const uint8_t* p) {
   return v;
 }
 
+// NodeAffinity PreScore error (an invalid preferred term; the host sets the
+// flag only when the profile has NodeAffinity): the cycle ends in Error once
+// PreScore runs, i.e. with more than one feasible node (schedule_one.go).
+__device__ __forceinline__ bool na_prescore_error(uint32_t flags, int32_t feasible) {
+  return (flags & KPF_NA_PREF_ERROR) && feasible > 1;
+}
+
 // ----------------------------------------------------------------- helpers
 __device__ __forceinline__ bool in_list(int32_t v, const int32_t* vals, int cnt) {
   for (int i = 0; i < cnt; ++i)
@@ -1147,13 +1154,19 @@ __device__ __forceinline__ int32_t tc_value(const DevCluster& C, uint32_t off, i
   if (v < 0) return 0;
   return C.T.tc_val[off + (((C.T.uniq >> slot) & 1u) ? n : (uint32_t)v)];
 }
-__device__ void pc_add(DevCluster& C, int32_t cls, uint32_t n, int sign) {
+// v: node n's topology values (node_slot_vids)
+// (the slot keys are read first, all together, so that the value loads issue back to back)
+__device__ __forceinline__ void node_slot_vids(const DevCluster& C, uint32_t n, int32_t v[KSG_MAX_TOPO]) {
+  int32_t key[KSG_MAX_TOPO];
+#pragma unroll
+  for (int s = 0; s < KSG_MAX_TOPO; ++s) key[s] = C.tkeyv[s];
+#pragma unroll
+  for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? node_vid(C, key[s], n) : -1;
+}
+__device__ __forceinline__ void pc_add(DevCluster& C, int32_t cls, uint32_t n, int sign, const int32_t v[KSG_MAX_TOPO]) {
   const DevTables& T = C.T;
   if (cls < 0 || (uint32_t)cls >= T.npc) return;
   atomicAdd(&T.pc_cnt[(size_t)cls * C.N + n], sign);
-  int32_t v[KSG_MAX_TOPO];  // the node's topology values, loaded together
-#pragma unroll
-  for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? node_vid(C, C.tkeyv[s], n) : -1;
 #pragma unroll
   for (int s = 0; s < KSG_MAX_TOPO; ++s) {
     if (v[s] < 0) continue;
@@ -1165,10 +1178,19 @@ __device__ void pc_add(DevCluster& C, int32_t cls, uint32_t n, int sign) {
 __device__ __forceinline__ int32_t eterm_inc(const ksg_exist_term& e) {
   return e.kind == 2 ? e.weight : (e.kind == 3 ? -e.weight : 1);
 }
-// an existing pod's term e (its term class, table offset and topology slot) on node n
-__device__ void tc_add(DevCluster& C, const ksg_exist_term& e, uint32_t n, int sign) {
+// an existing pod's term e (its term class, table offset and topology slot) on
+// node n whose topology values are vs (null: read the term's key)
+__device__ __forceinline__ void tc_add(DevCluster& C, const ksg_exist_term& e, uint32_t n, int sign,
+                                       const int32_t* vs = nullptr) {
   if (e.cls < 0 || (uint32_t)e.cls >= C.T.ntc) return;
-  const int32_t v = node_vid(C, e.topo_key, n);
+  int32_t v = -1;
+  if (vs) {
+#pragma unroll
+    for (int s = 0; s < KSG_MAX_TOPO; ++s)
+      if (s == e.topo) v = vs[s];
+  } else {
+    v = node_vid(C, e.topo_key, n);
+  }
   if (v < 0) return;
   atomicAdd(&C.T.tc_val[(uint32_t)e.toff + (((C.T.uniq >> e.topo) & 1u) ? n : (uint32_t)v)], sign * eterm_inc(e));
   atomicAdd(&C.T.tc_tot[e.cls], sign);
@@ -1180,11 +1202,14 @@ __device__ void tables_assume(DevCluster& C, const ProgView& V, uint32_t n, int 
   if (!C.T.on) return;
   const ksg_prog* h = V.h;
   const uint32_t npm = (uint32_t)h->n_pc_match, ne = (uint32_t)h->n_exist_terms;
+  if (lane >= npm + ne) return;
+  int32_t v[KSG_MAX_TOPO];  // the node's topology values, loaded beside the items
+  node_slot_vids(C, n, v);
   for (uint32_t i = lane; i < npm + ne; i += lanes) {
     if (i < npm) {
-      pc_add(C, V.i32[h->pc_match_off + i], n, sign);
+      pc_add(C, V.i32[h->pc_match_off + i], n, sign, v);
     } else {
-      tc_add(C, V.et[h->exist_terms_off + (i - npm)], n, sign);
+      tc_add(C, V.et[h->exist_terms_off + (i - npm)], n, sign, v);
     }
   }
 }
@@ -1286,7 +1311,7 @@ __device__ void commit_cycle(DevCluster& C, const ProgView& V, ksg_pod_summary* 
   int32_t status = fresh ? (int32_t)atomicOr((uint32_t*)&s->status, 0u) : s->status;
   int32_t feasible = fresh ? atomicAdd(&s->feasible, 0) : s->feasible;
   uint64_t best = fresh ? atomicMax((unsigned long long*)&s->best_key, 0ull) : s->best_key;
-  if (h->flags & KPF_PREFILTER_ERROR) status |= 2;
+  if ((h->flags & KPF_PREFILTER_ERROR) || na_prescore_error(h->flags, feasible)) status |= 2;
   if (status & 2) { s->status = 2; s->selected = -1; return; }
   if (feasible == 0) { s->status = 1; s->selected = -1; return; }
   uint32_t g = (uint32_t)(best & 0xFFFFFull);
@@ -1606,7 +1631,7 @@ __global__ void k_whatif_select(WiArgs A) {
   if (j >= A.count) return;
   const ksg_prog* h = reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[A.q0 + j]);
   ksg_pod_summary* s = A.sums + A.q0 + j;
-  if (h->flags & KPF_PREFILTER_ERROR) s->status |= 2;
+  if ((h->flags & KPF_PREFILTER_ERROR) || na_prescore_error(h->flags, s->feasible)) s->status |= 2;
   if (s->status & 2) { s->status = 2; s->selected = -1; return; }
   if (s->feasible == 0) { s->status = 1; s->selected = -1; return; }
   s->selected = (int32_t)(s->best_key & 0xFFFFFull);
@@ -3200,12 +3225,12 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
         feasible = L.feas[b] + (sum & 1023) - 128;
         const int achT = L.achT[b] + ((sum >> 10) & 1023) - 128, achA = L.achA[b] + ((sum >> 20) & 1023) - 128;
         const bool na_on = F.pos_na >= 0 && !(L.pod[b].flags & KPF_SKIP_NA_SCORE);
-        fb = !(L.pod[b].flags & KPF_PREFILTER_ERROR) && feasible > 0 &&
+        fb = !(L.pod[b].flags & KPF_PREFILTER_ERROR) && !na_prescore_error(L.pod[b].flags, feasible) && feasible > 0 &&
              ((F.pos_taint >= 0 && achT <= 0) || (na_on && achA <= 0));
       } else {
         feasible = L.feas[b] + wave_sum(df);
       }
-      const bool perr = (L.pod[b].flags & KPF_PREFILTER_ERROR) != 0;
+      const bool perr = (L.pod[b].flags & KPF_PREFILTER_ERROR) != 0 || na_prescore_error(L.pod[b].flags, feasible);
       const int32_t sel = (feasible > 0 && best && !perr) ? (int32_t)(best & 0xFFFFFull) : -1;
       const unsigned long long mc = __ballot(best && kc == best), mp = __ballot(best && kp == best),
                                mr = __ballot(best && kr == best);
@@ -4537,16 +4562,16 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
       CA.prog = prog;
       const bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
       if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
-      if (rowm == 2) hipLaunchKernelGGL(k_eval<2>, dim3(I.cnblk), b, 0, s, C, F, CA);
-      else if (rowm == 1) hipLaunchKernelGGL(k_eval<1>, dim3(I.cnblk), b, 0, s, C, F, CA);
-      else hipLaunchKernelGGL(k_eval<0>, dim3(I.cnblk), b, 0, s, C, F, CA);
+      if (rowm == 2) hipLaunchKernelGGL(k_eval<2>, dim3(I.cnblk), b, 0, s, C, F, CA, prog);
+      else if (rowm == 1) hipLaunchKernelGGL(k_eval<1>, dim3(I.cnblk), b, 0, s, C, F, CA, prog);
+      else hipLaunchKernelGGL(k_eval<0>, dim3(I.cnblk), b, 0, s, C, F, CA, prog);
       if (sampled) {
         HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
         I.n_samples++;
       }
       if (F.has_ext) {  // (k_final's last block selects; without ScoreExtensions k_eval's)
-        if (I.prog_need[j] & 8) hipLaunchKernelGGL(k_ptsraw, dim3(I.cnblk), b, 0, s, C, F, CA);
-        hipLaunchKernelGGL(k_final, dim3(I.cnblk), b, 0, s, C, F, CA);
+        if (I.prog_need[j] & 8) hipLaunchKernelGGL(k_ptsraw, dim3(I.cnblk), b, 0, s, C, F, CA, prog);
+        hipLaunchKernelGGL(k_final, dim3(I.cnblk), b, 0, s, C, F, CA, prog);
       }
       pending |= (CA.mode & 2) != 0;
       continue;

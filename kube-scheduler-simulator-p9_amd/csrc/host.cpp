@@ -618,6 +618,7 @@ struct Cluster {
   vector<uint8_t> enc_topo_unique;
   vector<uint32_t> enc_nu_base;  // per slot: base among the shared-key pairs (UINT32_MAX: one node per value)
   vector<uint32_t> enc_topo_base;
+  vector<int32_t> enc_slot_dom;  // per slot: values present on this shard's nodes
   uint32_t enc_N = 0, enc_NU = 0;
   uint32_t tc_total = 0;         // term-class value pool entries assigned (offsets follow class order)
   // a class-table count reference for topology slot `slot`: the key's base among
@@ -816,6 +817,85 @@ struct Cluster {
       if (!keys_together(m)) return false;
     }
     return true;
+  }
+  // The table chain's lookup plan of a compiled program (ksg_look / ksg_ubit):
+  // k_eval's per-node class-table counts and the pod-uniform InterPodAffinity
+  // map totals, in the order k_eval's reads had them.  False: does not fit.
+  template <class Pools>
+  bool lookup_plan(ksg_prog& h, const Pools& P) const {
+    h.n_lk = h.n_ub = 0;
+    bool ok = true;
+    auto look = [&](int kind, uint64_t base, int slot, int use, int64_t weight, int aux) {
+      if (h.n_lk >= KSG_LK_MAX || base > 0x7FFFFFFFull || weight > INT32_MAX || weight < INT32_MIN) { ok = false; return; }
+      ksg_look& e = h.lk[h.n_lk++];
+      e = ksg_look{};
+      e.base = (int32_t)base;
+      e.weight = (int32_t)weight;
+      e.slot = (int16_t)slot;
+      e.kind = (uint8_t)kind;
+      e.use = (uint8_t)use;
+      e.aux = aux;
+    };
+    auto pc_look = [&](int32_t cls, int32_t nub, int slot, int use, int64_t weight, int aux) {
+      if (cls < 0) {
+        if (use == KLU_AFF) look(KLK_NONE, 0, slot, use, 0, aux);  // a missing value still fails
+        return;
+      }
+      if (nub < 0) look(KLK_PC_NODE, (uint64_t)cls * enc_N, slot, use, weight, aux);
+      else look(KLK_PC_DOM, (uint64_t)cls * enc_NU + (uint32_t)nub, slot, use, weight, aux);
+    };
+    auto ub = [&](int kind, uint64_t idx, int bit) {
+      if (!bit) return;
+      if (h.n_ub >= KSG_UB_MAX || idx > 0x7FFFFFFFull) { ok = false; return; }
+      ksg_ubit& u = h.ub[h.n_ub++];
+      u.idx = (int32_t)idx;
+      u.kind = (int16_t)kind;
+      u.bit = (int16_t)bit;
+    };
+    const int nf = h.n_tsc_filter, ns = h.n_tsc_score;
+    if (pos_of(P_PTS) >= 0) {
+      if (!(h.flags & KPF_SKIP_PTS_FILTER))
+        for (int c = 0; c < nf; ++c) pc_look(h.tsc[c].eff_cls, h.tsc[c].nub, h.tsc[c].topo, KLU_PTSF, 0, c);
+      if (ns > 0 && !(h.flags & KPF_SKIP_PTS_SCORE) && !(h.tab & KTAB_PTS_MULTI)) {
+        const ksg_tsc& t = h.tsc[nf];  // pts_count_tab: the constraint's pair count
+        if (t.is_hostname) {
+          if (t.cls >= 0) look(KLK_PC_NODE, (uint64_t)t.cls * enc_N, t.topo, KLU_PTSS, 0, 0);
+        } else {
+          for (int k = 0; k < t.sc_n; ++k) pc_look(P.i32[(size_t)t.sc_off + k], t.nub, t.topo, KLU_PTSS, 0, 0);
+        }
+      }
+    }
+    if (pos_of(P_IPA) >= 0) {
+      const ksg_aterm* aff = P.at.data() + h.aterm_off;
+      const ksg_aterm* anti = aff + h.n_req_aff;
+      const ksg_aterm* pref = anti + h.n_req_anti;
+      const bool has_c = (h.flags & KPF_IPA_HAS_CONSTRAINTS) != 0;
+      const bool score_on = !(ipa_ignore && !has_c);
+      for (int i = 0; i < h.n_req_aff; ++i) {
+        pc_look(h.aff_cls, aff[i].nub, aff[i].topo, KLU_AFF, 0, 0);
+        if (h.aff_cls >= 0) ub(1, (uint64_t)h.aff_cls * KSG_MAX_TOPO + aff[i].topo, 1);
+      }
+      for (int i = 0; i < h.n_req_anti; ++i) pc_look(anti[i].cls, anti[i].nub, anti[i].topo, KLU_ANTI, 0, 0);
+      if (has_c)
+        for (int i = 0; i < h.n_pref_aff + h.n_pref_anti; ++i) {
+          const ksg_aterm& t = pref[i];
+          pc_look(t.cls, t.nub, t.topo, KLU_RAW, i < h.n_pref_aff ? (int64_t)t.weight : -(int64_t)t.weight, 0);
+          if (t.cls >= 0) ub(1, (uint64_t)t.cls * KSG_MAX_TOPO + t.topo, 8);
+        }
+      for (int i = 0; i < h.n_tc_match; ++i) {
+        const int32_t* e = P.i32.data() + h.tc_match_off + 4 * i;  // (class, offset, slot, group)
+        const bool one = (size_t)e[2] < enc_topo_unique.size() && enc_topo_unique[e[2]];
+        const int kind = one ? KLK_TC_NODE : KLK_TC_DOM;
+        if (e[3] == KSG_TC_ANTI) {
+          look(kind, (uint32_t)e[1], e[2], KLU_EXANTI, 0, 0);
+          ub(2, (uint32_t)e[0], 4);
+        } else if (score_on && (e[3] == KSG_TC_PREF || ipa_hard > 0)) {
+          look(kind, (uint32_t)e[1], e[2], KLU_RAW, e[3] == KSG_TC_HARD ? ipa_hard : 1, 0);
+          ub(2, (uint32_t)e[0], 8);
+        }
+      }
+    }
+    return ok;
   }
   // Recompile queue pod q when classes added since its compile apply to it (its
   // pod-class list must hold every class whose table counts it; its term-class
@@ -1078,6 +1158,7 @@ struct Cluster {
     enc_topo_unique = S.topo_unique;
     enc_nu_base = S.nu_base;
     enc_topo_base = S.topo_base;
+    enc_slot_dom = S.slot_dom;
     enc_N = n;
     enc_NU = S.nu_pairs;
     tc_total = 0;
@@ -1378,7 +1459,7 @@ struct Cluster {
         if (!compile_node_term(*pref, P, s)) { bad = true; continue; }
         pts.push_back({s, (int32_t)w});
       }
-      if (bad) { m.na_prescore_error = true; h.flags |= KPF_NA_PREF_ERROR; }
+      if (bad && pos_of(P_NA) >= 0) { m.na_prescore_error = true; h.flags |= KPF_NA_PREF_ERROR; }
       h.n_pref_terms = (int32_t)pts.size();
       h.pref_w_off = (int32_t)P.i32.size();
       for (auto& x : pts) { P.sel.push_back(x.first); P.i32.push_back(x.second); }
@@ -1432,6 +1513,7 @@ struct Cluster {
       const bool known = t.topo >= 0 && (size_t)t.topo < enc_topo_base.size();
       t.pair_base = known ? (int32_t)enc_topo_base[t.topo] : 0;
       t.nvals = known ? (int32_t)enc_topo_count[t.topo] : 0;
+      t.dom = known && (size_t)t.topo < enc_slot_dom.size() ? enc_slot_dom[t.topo] : 0;
     }
     for (int i = 0; i < nf; ++i) {
       h.tsc[i].eff_cls = h.tsc[i].cls;
@@ -1545,6 +1627,7 @@ struct Cluster {
       h.tab = table_path(h) ? KTAB_ON : 0;
       if ((h.tab & KTAB_ON) && pos_of(P_PTS) >= 0 && h.n_tsc_score > 1 && !(h.flags & KPF_SKIP_PTS_SCORE))
         h.tab |= KTAB_PTS_MULTI;
+      if ((h.tab & KTAB_ON) && !lookup_plan(h, P)) h.tab = 0;  // more lookups than the plan holds
     } else {
       h.tab = shards == 1 ? KTAB_ON : 0;  // profiles without PTS / IPA: the chain needs no tables
     }
@@ -2354,11 +2437,23 @@ struct Cluster {
       default: return C_UNRESOLVABLE;  // TaintToleration, NodeAffinity, NodeUnschedulable, NodeName
     }
   }
-  // PreScore of profile position pos (-1: no PreScore, or no scoring: one feasible node / none).
-  int prescore_status(uint32_t q, int pos, const ksg_pod_summary& S) const {
+  // PreScore of profile position pos (-1: no PreScore, or no scoring: one feasible
+  // node / none, or a PreScore before it failed).  NodeAffinity's PreScore fails
+  // on an invalid preferred term (the cycle's Error: a status 2 with more than
+  // one feasible node comes from there; node_affinity.go PreScore).
+  static constexpr const char* kNaPrefErr = "invalid preferred node affinity term";
+  int prescore_status(uint32_t q, int pos, const ksg_pod_summary& S, string& msg) const {
+    msg.clear();
     if (pos < 0 || pos >= n_plugins || !has_prescore(plugins[pos])) return -1;
-    if (meta[q].prefilter_fail_pos >= 0 || S.feasible <= 1 || S.status == 2) return -1;
-    return (skip_score_mask(meta[q], S) & (1u << plugins[pos])) ? C_SKIP : C_SUCCESS;
+    const PodMeta& m = meta[q];
+    if (m.prefilter_fail_pos >= 0 || S.feasible <= 1) return -1;
+    if (S.status == 2) {
+      if (!m.na_prescore_error) return -1;
+      const int na = pos_of(P_NA);
+      if (pos > na) return -1;
+      if (pos == na) { msg = kNaPrefErr; return C_ERROR; }
+    }
+    return (skip_score_mask(m, S) & (1u << plugins[pos])) ? C_SKIP : C_SUCCESS;
   }
   void add_requests_const(const Pod& p, vector<i64>& out_req, i64& nzc, i64& nzm) const {
     out_req.assign(res.names.size(), 0);
@@ -2434,6 +2529,12 @@ struct Cluster {
           else if (pos == fail_pos) { row[names[pos]] = filter_message(pos, code & 0xFFFFFFu); break; }
         }
       }
+      if (S.feasible > 1 && S.status == 2 && m.na_prescore_error)  // PreScore ran up to NodeAffinity's error
+        for (int pos = 0; pos < n_plugins; ++pos) {
+          string msg;
+          const int code = prescore_status(q, pos, S, msg);
+          if (code >= 0) pre_score[names[pos]] = code == C_SUCCESS ? "success" : msg;
+        }
       if (S.feasible > 1 && S.status != 2) {
         skip_s = skip_score_mask(m, S);
         for (int pos = 0; pos < n_plugins; ++pos)
@@ -2880,14 +2981,15 @@ int ksg_filter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, uint32_t node, int
   return put_str(ctx, m, msg, cap, len);
 }
 
-int ksg_prescore_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code) {
+int ksg_prescore_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code, char* msg, size_t cap, size_t* len) {
   KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (!code || q >= c.meta.size() || (int)pos >= c.n_plugins) return ctx->fail("prescore_status: range", KSG_E_RANGE);
   const ksg::PodOutputs* o = c.outputs_of(q);
   if (!o) return ctx->fail(c.err, KSG_E_STATE);
-  *code = c.prescore_status(q, (int)pos, o->summary);
-  return KSG_OK;
+  std::string m;
+  *code = c.prescore_status(q, (int)pos, o->summary, m);
+  return put_str(ctx, m, msg, cap, len);
 }
 
 int ksg_normalized_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int64_t* out, uint32_t n) {

@@ -111,8 +111,39 @@ typedef struct ksg_tsc {
   int32_t sc_n, sc_off;  // score: (class, nub) pairs whose counts share this constraint's pair (pool_i32)
   int32_t pair_base;     // the key's first (key, value) pair, and its values (minMatchNum per block)
   int32_t nvals;
-  int32_t pad;
+  int32_t dom;           // values of the key present on some node of the shard (minMatchNum: none -> Error)
 } ksg_tsc;
+
+// Table-chain lookup plan (host compile, table-path pods): every class-table
+// count k_eval reads per node, issued together once the node's topology values
+// are known, and what the count feeds.
+typedef struct ksg_look {
+  int32_t base;    // the table entry of value 0 / node 0 (kind)
+  int32_t weight;  // KLU_RAW: signed multiplier
+  int16_t slot;    // topology slot whose value selects the entry (no value: count 0)
+  uint8_t kind;    // KLK_*
+  uint8_t use;     // KLU_*
+  int32_t aux;     // KLU_PTSF: the filter constraint
+} ksg_look;
+#define KSG_LK_MAX 24
+#define KLK_NONE 0      // count 0 (class counts nothing)
+#define KLK_PC_NODE 1   // pc_cnt[base + node]
+#define KLK_PC_DOM 2    // pc_dom[base + value]
+#define KLK_TC_NODE 3   // tc_val[base + node]
+#define KLK_TC_DOM 4    // tc_val[base + value]
+#define KLU_PTSF 1      // PodTopologySpread filter count of constraint aux
+#define KLU_PTSS 2      // PodTopologySpread score count (summed)
+#define KLU_AFF 3       // InterPodAffinity required affinity: count <= 0 or no value fails
+#define KLU_ANTI 4      // required anti-affinity: a count > 0 fails
+#define KLU_RAW 5       // InterPodAffinity raw score += count * weight
+#define KLU_EXANTI 6    // existing pods' required anti-affinity: a count > 0 fails (when in force)
+// InterPodAffinity map-emptiness bits (pod-uniform): bit set when the total is > 0
+typedef struct ksg_ubit {
+  int32_t idx;   // pc_tot / tc_tot index
+  int16_t kind;  // 1 pc_tot, 2 tc_tot
+  int16_t bit;
+} ksg_ubit;
+#define KSG_UB_MAX 16
 
 // Existing-pod record appended at assume time (Reserve -> NodeInfo.AddPod).
 typedef struct ksg_exist_term {
@@ -212,6 +243,9 @@ typedef struct ksg_prog {
   int32_t aff_cls;          // required pod affinity: class of the pods matching every term (-1 none)
   int32_t n_pc_match, pc_match_off;  // pool_i32: pod classes this pod belongs to (its assume: +-1)
   int32_t n_tc_match, tc_match_off;  // pool_i32: term classes whose terms match this pod (id, value offset, slot, group)
+  int32_t n_lk, n_ub;       // table chain: lookup plan and InterPodAffinity bits
+  ksg_look lk[KSG_LK_MAX];
+  ksg_ubit ub[KSG_UB_MAX];
 
   // ---- pools (byte offsets from the start of the blob)
   uint32_t off_i32, n_i32;

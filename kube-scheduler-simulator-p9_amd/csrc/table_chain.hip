@@ -207,74 +207,12 @@ __device__ __forceinline__ int64_t pts_count_tab(const DevCluster& C, const Prog
   return s;
 }
 
-// InterPodAffinity's map-emptiness bits from the class tables, this thread's
-// share (OR over the block): bit0 affinityCounts non-empty (a pod matching every
-// required term on a node with a term's key), bit2 an existing pod's required
-// anti-affinity term matches the pod (existingAntiAffinityCounts), bit3 the
-// topology score map is non-empty (PreScore not Skip).
-__device__ __forceinline__ uint32_t ipa_table_bits(const DevCluster& C, const DevProfile& F, const ProgView& V) {
-  const ksg_prog* h = V.h;
-  const ksg_aterm* aff = V.at + h->aterm_off;
-  const ksg_aterm* pref = aff + h->n_req_aff + h->n_req_anti;
-  const int npref = (h->flags & KPF_IPA_HAS_CONSTRAINTS) ? h->n_pref_aff + h->n_pref_anti : 0;
-  const bool score_on = !(F.ipa_ignore_existing_pref && !(h->flags & KPF_IPA_HAS_CONSTRAINTS));
-  const int nt = h->n_req_aff + npref + h->n_tc_match;
-  uint32_t bits = 0;
-  for (int i = threadIdx.x; i < nt; i += blockDim.x) {
-    if (i < h->n_req_aff) {
-      if (h->aff_cls >= 0 && C.T.pc_tot[(size_t)h->aff_cls * KSG_MAX_TOPO + aff[i].topo] > 0) bits |= 1u;
-    } else if (i < h->n_req_aff + npref) {
-      const ksg_aterm& t = pref[i - h->n_req_aff];
-      if (t.cls >= 0 && C.T.pc_tot[(size_t)t.cls * KSG_MAX_TOPO + t.topo] > 0) bits |= 8u;
-    } else {
-      const int32_t* e = V.i32 + h->tc_match_off + 4 * (i - h->n_req_aff - npref);  // (class, offset, slot, group)
-      if (C.T.tc_tot[e[0]] > 0) {
-        const int grp = e[3];
-        if (grp == KSG_TC_ANTI) bits |= 4u;
-        else if (score_on && (grp == KSG_TC_PREF || F.ipa_hard_weight > 0)) bits |= 8u;
-      }
-    }
-  }
-  return bits;
-}
-
 struct EvalShared {
   int32_t tv[KSG_MAX_TOPO * kBlock];
   int32_t minm[KSG_MAX_TSC];
   uint32_t ipa_flags;
   ChainRec rec[kBlock / 64];
 };
-
-// Pod-uniform inputs of k_eval, per block: minMatchNum of every filter
-// constraint (the smallest count over the key's values present on nodes) and
-// InterPodAffinity's map-emptiness bits.  LDS-only barriers: the node loads
-// issued before stay in flight.
-__device__ __forceinline__ void eval_setup(const DevCluster& C, const DevProfile& F, const ProgView& V, EvalShared& L, bool pts_on,
-                           bool ipa_on) {
-  const ksg_prog* h = V.h;
-  if (threadIdx.x < KSG_MAX_TSC) L.minm[threadIdx.x] = 0x7FFFFFFF;
-  if (threadIdx.x == 0) L.ipa_flags = 0;
-  lds_barrier();
-  if (pts_on && !(h->flags & KPF_SKIP_PTS_FILTER)) {
-    for (int c = 0; c < h->n_tsc_filter; ++c) {
-      const ksg_tsc& t = h->tsc[c];
-      const uint32_t base = (uint32_t)t.pair_base, cnt = (uint32_t)t.nvals;
-      int32_t m = 0x7FFFFFFF;
-      for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x)
-        if (C.T.pair_node[base + i]) {
-          const int32_t x = t.eff_cls < 0 ? 0 : C.T.pc_dom[(size_t)t.eff_cls * C.T.NU + (uint32_t)t.nub + i];
-          m = x < m ? x : m;
-        }
-      m = wave_min(m);
-      if (lane0() && m != 0x7FFFFFFF) atomicMin(&L.minm[c], m);
-    }
-  }
-  if (ipa_on) {
-    const uint32_t bits = __ockl_wfred_or_u32(ipa_table_bits(C, F, V));
-    if (lane0() && bits) atomicOr(&L.ipa_flags, bits);
-  }
-  lds_barrier();
-}
 
 // The assume delta's node row as fire-and-forget atomics (no load on the
 // chain's critical path).
@@ -291,7 +229,8 @@ __device__ __forceinline__ void assume_row_atomic(DevCluster& C, const ProgView&
 // selectHost + the assume, by the last-arriving block of the cycle's last
 // kernel: the block keys / statuses were stored sc1 before each block arrived
 // (MI355X_MICROARCH.md hand-off: agent-scope stores, counter, agent-scope loads).
-__device__ __forceinline__ void chain_last_select(DevCluster& C, const DevProfile& F, const ChainArgs& A, ChainRec* lds) {
+__device__ __forceinline__ void chain_last_select(DevCluster& C, const DevProfile& F, const ChainArgs& A, ChainRec* lds,
+                                                  const uint8_t* __restrict__ prog) {
   __shared__ uint32_t last;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -302,7 +241,7 @@ __device__ __forceinline__ void chain_last_select(DevCluster& C, const DevProfil
   if (!last) return;
   const uint64_t cs_t0 = CS_ON ? __builtin_amdgcn_s_memrealtime() : 0;
   const uint32_t q = A.q, NB = A.nblk;
-  const ProgView V = view(A.prog);
+  const ProgView V = view(prog);
   const ksg_prog* h = V.h;
   ChainRec r;
   rec_init(r);
@@ -315,11 +254,12 @@ __device__ __forceinline__ void chain_last_select(DevCluster& C, const DevProfil
   CS(24);
   rec_block(r, lds, 0u, 0, RB_CNT | RB_ST | RB_KEY);
   CS(25);
-  const bool error = (r.st & 2) || ((r.st & 4) && r.feas > 1) || (h->flags & KPF_PREFILTER_ERROR);
+  const bool error = (r.st & 2) || ((r.st & 4) && r.feas > 1) || (h->flags & KPF_PREFILTER_ERROR) ||
+                     na_prescore_error(h->flags, r.feas);
   int32_t node = -1;
   const uint32_t g = (uint32_t)(r.key & 0xFFFFFull);
   if (!error && r.feas > 0 && (A.mode & 1) && g >= C.goff && g - C.goff < C.N) node = (int32_t)(g - C.goff);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == blockDim.x - 64) {  // (the last wave: wave 0 takes the class tables meanwhile)
     __hip_atomic_store(A.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ksg_pod_summary* S = A.sums + q;
     S->feasible = r.feas;
@@ -342,11 +282,12 @@ __device__ __forceinline__ void chain_last_select(DevCluster& C, const DevProfil
 // node row loaded up front (RowV), 2 the same with the default Fit / BA
 // arguments compiled in.
 template <int ROWM>
-__global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, ChainArgs A) {
+__global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
   CS_BEGIN;
   CS_GAP(42, 49, 48);
+  CS(13);
   const uint32_t q = A.q;
-  const ProgView V = view(A.prog);
+  const ProgView V = view(prog);
   const ksg_prog* h = V.h;
   __shared__ EvalShared L;
   uint32_t* of;
@@ -355,8 +296,6 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
   const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
   const bool active = n < C.N;
   const uint32_t nn = active ? n : 0;  // loads of inactive lanes read node 0 (results unused)
-  RowV row;
-  if (ROWM) load_row(C, nn, A.need_eph, row);
   int pts_pos = -1, ipa_pos = -1;
   uint32_t xmask = 0;
   for (int p = 0; p < F.n; ++p) {
@@ -365,60 +304,128 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
     const int x = chain_x(F.plugins[p]);
     if (x >= 0) xmask |= 1u << x;
   }
-  load_slot_vids(C, nn, true, L.tv);
-  const SlotVids tv{L.tv + threadIdx.x};
-  const ksg_aterm* aff = V.at + h->aterm_off;
-  const ksg_aterm* anti = aff + h->n_req_aff;
-  const ksg_aterm* pref = anti + h->n_req_anti;
   const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
+  const bool pts_f = pts_pos >= 0 && !(h->flags & KPF_SKIP_PTS_FILTER);
   const bool pts_score = pts_pos >= 0 && ns > 0 && !(h->flags & KPF_SKIP_PTS_SCORE);
-  const bool score_on = !(F.ipa_ignore_existing_pref && !(h->flags & KPF_IPA_HAS_CONSTRAINTS));
-  // class-table counts this node's verdicts and scores read, loaded before the
-  // pod-uniform setup so that their latencies overlap it
-  int32_t ptsm[KSG_MAX_TSC];
+  // ---- every input in flight together: the node's topology values first (the
+  // class-table reads need them), its row, then the pod-uniform setup inputs
+  // (minMatchNum candidates: value tid of each filter key; InterPodAffinity map
+  // totals: plan entry tid).  Consumed only after the lookups are issued.
+  const uint32_t ntopo = C.n_topo < KSG_MAX_TOPO ? C.n_topo : KSG_MAX_TOPO;
+  int32_t vid[KSG_MAX_TOPO];
+  node_slot_vids(C, nn, vid);
+  RowV row;
+  if (ROWM) load_row(C, nn, A.need_eph, row);
+  uint8_t mpn[KSG_MAX_TSC];
+  int32_t mcnt[KSG_MAX_TSC];
 #pragma unroll
   for (int c = 0; c < KSG_MAX_TSC; ++c) {
-    ptsm[c] = 0;
-    if (pts_pos >= 0 && c < nf) ptsm[c] = pc_count(C, h->tsc[c].eff_cls, h->tsc[c].nub, nn, tv(h->tsc[c].topo));
+    mpn[c] = 0;
+    mcnt[c] = 0;
+    if (pts_f && c < nf && threadIdx.x < (uint32_t)h->tsc[c].nvals) {
+      const ksg_tsc& t = h->tsc[c];
+      mpn[c] = C.T.pair_node[t.pair_base + threadIdx.x];
+      if (t.eff_cls >= 0) mcnt[c] = C.T.pc_dom[(size_t)t.eff_cls * C.T.NU + (uint32_t)t.nub + threadIdx.x];
+    }
+  }
+  int32_t ubv = 0;
+  uint32_t ubbit = 0;
+  if (ipa_pos >= 0 && h->n_ub > 0) {  // entry tid of the plan (uniform reads, then a per-lane pick)
+    int32_t idx = 0, kind = 0;
+#pragma unroll
+    for (int i = 0; i < KSG_UB_MAX; ++i) {
+      const int32_t ei = h->ub[i].idx, ek = h->ub[i].kind, eb = h->ub[i].bit;
+      if (threadIdx.x == (uint32_t)i) {
+        idx = ei;
+        kind = ek;
+        ubbit = (uint32_t)eb;
+      }
+    }
+    if (threadIdx.x < (uint32_t)h->n_ub) ubv = kind == 1 ? C.T.pc_tot[idx] : C.T.tc_tot[idx];
+  }
+  CS(7);
+  CS(11);
+  CS(12);
+#pragma unroll
+  for (int s = 0; s < KSG_MAX_TOPO; ++s)
+    if ((uint32_t)s < ntopo) L.tv[s * kBlock + threadIdx.x] = vid[s];
+  const SlotVids tv{L.tv + threadIdx.x};  // (each thread reads back only its own column)
+  CS(8);
+  // ---- the lookup plan (ksg_look): every class-table count of this node
+  int32_t lkv[KSG_LK_MAX], lks[KSG_LK_MAX];
+#pragma unroll
+  for (int i = 0; i < KSG_LK_MAX; ++i) {
+    lkv[i] = 0;
+    lks[i] = -1;
+    if (i < h->n_lk) {
+      const ksg_look& e = h->lk[i];
+      const int32_t v = tv(e.slot);
+      lks[i] = v;
+      if (e.kind != KLK_NONE) {
+        const uint32_t at = (uint32_t)e.base + ((e.kind == KLK_PC_NODE || e.kind == KLK_TC_NODE) ? nn : (uint32_t)(v < 0 ? 0 : v));
+        lkv[i] = (e.kind == KLK_PC_NODE ? C.T.pc_cnt : e.kind == KLK_PC_DOM ? C.T.pc_dom : C.T.tc_val)[at];
+      }
+    }
+  }
+  CS(9);
+  // ---- pod-uniform setup: minMatchNum per filter constraint, InterPodAffinity bits
+  if (threadIdx.x < KSG_MAX_TSC) L.minm[threadIdx.x] = 0x7FFFFFFF;
+  if (threadIdx.x == 0) L.ipa_flags = 0;
+  lds_barrier();
+  if (pts_f) {
+#pragma unroll
+    for (int c = 0; c < KSG_MAX_TSC; ++c) {
+      if (c >= nf) continue;
+      const ksg_tsc& t = h->tsc[c];
+      int32_t m = (threadIdx.x < (uint32_t)t.nvals && mpn[c]) ? mcnt[c] : 0x7FFFFFFF;
+      for (uint32_t i = threadIdx.x + blockDim.x; i < (uint32_t)t.nvals; i += blockDim.x)  // keys beyond 256 values
+        if (C.T.pair_node[t.pair_base + i]) {
+          const int32_t x = t.eff_cls < 0 ? 0 : C.T.pc_dom[(size_t)t.eff_cls * C.T.NU + (uint32_t)t.nub + i];
+          m = x < m ? x : m;
+        }
+      m = wave_min(m);
+      if (lane0() && m != 0x7FFFFFFF) atomicMin(&L.minm[c], m);
+    }
+  }
+  if (ipa_pos >= 0) {
+    const uint32_t bits = __ockl_wfred_or_u32(ubv > 0 ? ubbit : 0u);
+    if (lane0() && bits) atomicOr(&L.ipa_flags, bits);
+  }
+  lds_barrier();
+  CS(10);
+  // ---- the counts, folded into what the filters and scores read
+  int32_t ptsm[KSG_MAX_TSC];
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c) ptsm[c] = 0;
+  int64_t pts_cnt = 0, ipa_raw = 0;
+  bool aff_miss = false, aff_zero = false, anti_hit = false, exist_hit = false;
+#pragma unroll
+  for (int i = 0; i < KSG_LK_MAX; ++i) {
+    if (i >= h->n_lk) continue;
+    const ksg_look& e = h->lk[i];
+    const int32_t v = lks[i];
+    const int32_t x = v < 0 ? 0 : lkv[i];
+    switch (e.use) {
+      case KLU_PTSF:
+#pragma unroll
+        for (int c = 0; c < KSG_MAX_TSC; ++c)
+          if (c == e.aux) ptsm[c] = x;
+        break;
+      case KLU_PTSS: pts_cnt += x; break;
+      case KLU_AFF:
+        aff_miss |= v < 0;
+        aff_zero |= x <= 0;
+        break;
+      case KLU_ANTI: anti_hit |= x > 0; break;
+      case KLU_RAW: ipa_raw += (int64_t)x * e.weight; break;
+      case KLU_EXANTI: exist_hit |= x > 0; break;
+      default: break;
+    }
   }
   bool counted = pts_score;
-  int64_t pts_cnt = 0;
-  if (pts_score) {
+  if (pts_score)
     for (int c = nf; c < nf + ns; ++c) counted &= tv(h->tsc[c].topo) >= 0;
-    if (counted && !(h->tab & KTAB_PTS_MULTI)) pts_cnt = pts_count_tab(C, V, nf, nn, tv(h->tsc[nf].topo));
-  }
-  bool aff_miss = false, aff_zero = false, anti_hit = false, exist_hit = false;
-  int64_t ipa_raw = 0;
-  if (ipa_pos >= 0) {
-    for (int i = 0; i < h->n_req_aff; ++i) {
-      const int32_t v = tv(aff[i].topo);
-      aff_miss |= v < 0;
-      aff_zero |= pc_count(C, h->aff_cls, aff[i].nub, nn, v) <= 0;
-    }
-    for (int i = 0; i < h->n_req_anti; ++i) {
-      const int32_t v = tv(anti[i].topo);
-      anti_hit |= v >= 0 && pc_count(C, anti[i].cls, anti[i].nub, nn, v) > 0;
-    }
-    if (h->flags & KPF_IPA_HAS_CONSTRAINTS)
-      for (int i = 0; i < h->n_pref_aff + h->n_pref_anti; ++i) {
-        const ksg_aterm& t = pref[i];
-        const int64_t k = pc_count(C, t.cls, t.nub, nn, tv(t.topo));
-        ipa_raw += i < h->n_pref_aff ? k * t.weight : -k * t.weight;
-      }
-    for (int i = 0; i < h->n_tc_match; ++i) {
-      const int32_t* e = V.i32 + h->tc_match_off + 4 * i;  // (class, offset, slot, group)
-      const int grp = e[3];
-      if (grp == KSG_TC_ANTI) {
-        exist_hit |= tc_value(C, (uint32_t)e[1], e[2], nn, tv(e[2])) > 0;
-      } else if (score_on && (grp == KSG_TC_PREF || F.ipa_hard_weight > 0)) {
-        const int64_t k = tc_value(C, (uint32_t)e[1], e[2], nn, tv(e[2]));
-        ipa_raw += grp == KSG_TC_HARD ? k * F.ipa_hard_weight : k;
-      }
-    }
-  }
-  CS(1);
-  eval_setup(C, F, V, L, pts_pos >= 0, ipa_pos >= 0);
-  CS(2);
+  if (h->tab & KTAB_PTS_MULTI) pts_cnt = 0;  // (k_ptsraw computes the raw scores)
   const uint32_t ipa_flags = L.ipa_flags;
   uint32_t code = KSG_FILTER_NOT_EVALUATED;
   bool err = false;
@@ -449,7 +456,7 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
             for (int c = 0; c < KSG_MAX_TSC; ++c) {
               if (c >= nf || fail || err) continue;
               const ksg_tsc& t = h->tsc[c];
-              const int32_t dom = C.T.slot_dom[t.topo];
+              const int32_t dom = t.dom;
               if (tv(t.topo) < 0) { fail = true; detail = KSG_PTS_MISSING_LABEL; continue; }
               if (dom == 0) { err = true; continue; }  // minMatchNum: no domains -> Error
               const int64_t mn = dom < t.min_domains ? 0 : L.minm[c];
@@ -563,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
     }
   }
   CS(6);
-  if (!F.has_ext) chain_last_select(C, F, A, L.rec);
+  if (!F.has_ext) chain_last_select(C, F, A, L.rec, prog);
 }
 
 // k_eval's partials folded (every block of k_ptsraw / k_final does it for itself)
@@ -645,9 +652,9 @@ struct FinalShared {
 };
 
 // PodTopologySpread raw scores of a pod with several score constraints.
-__global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, ChainArgs A) {
+__global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
   const uint32_t q = A.q;
-  const ProgView V = view(A.prog);
+  const ProgView V = view(prog);
   __shared__ FinalShared L;
   uint32_t* of;
   int32_t *os, *ot;
@@ -679,11 +686,11 @@ __global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, C
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_final(DevCluster C, DevProfile F, ChainArgs A) {
+__global__ __launch_bounds__(kBlock) void k_final(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
   CS_BEGIN;
   CS_GAP(40, 48, 49);
   const uint32_t q = A.q;
-  const ProgView V = view(A.prog);
+  const ProgView V = view(prog);
   const ksg_prog* h = V.h;
   __shared__ FinalShared L;
   uint32_t* of;
@@ -786,7 +793,7 @@ __global__ __launch_bounds__(kBlock) void k_final(DevCluster C, DevProfile F, Ch
     st_sc1(A.pst + blockIdx.x, r.st);
   }
   CS(20);
-  chain_last_select(C, F, A, L.rec);
+  chain_last_select(C, F, A, L.rec, prog);
 }
 
 // The existing-pod table rows of the run's logged assumes, in log order (one
@@ -850,6 +857,8 @@ __global__ void k_pc_build(DevCluster C, uint32_t c0, uint32_t nc) {
   if (fl & KEF_DELETED) return;
   const int32_t node = C.ptnode[p], ns = C.ptns[p];
   auto vid = [&](int32_t k) -> int32_t { return (k >= 0 && (uint32_t)k < C.pkeys) ? C.ptlab[(size_t)k * C.pcap + p] : -1; };
+  int32_t nv[KSG_MAX_TOPO];
+  node_slot_vids(C, (uint32_t)node, nv);
   for (uint32_t c = c0; c < c0 + nc; ++c) {
     const ksg_pclass& pc = C.T.pcls[c];
     if (pc.excl_term && (fl & KEF_TERMINATING)) continue;
@@ -858,7 +867,7 @@ __global__ void k_pc_build(DevCluster C, uint32_t c0, uint32_t nc) {
       const ksg_cterm& t = C.T.cterm[pc.term_off + i];
       ok = (t.ns_all || in_list(ns, C.T.cval + t.ns_off, t.ns_cnt)) && sel_eval(t.sel, C.T.creq, C.T.cval, vid);
     }
-    if (ok) pc_add(C, (int32_t)c, (uint32_t)node, +1);
+    if (ok) pc_add(C, (int32_t)c, (uint32_t)node, +1, nv);
   }
 }
 // term classes [u0, ...): every live existing pod's term of such a class

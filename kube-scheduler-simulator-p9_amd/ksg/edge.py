@@ -1,0 +1,363 @@
+"""Edge-case cluster family: the plugin arguments and pod / node shapes the five
+BASELINE configs never produce, so that the device path and the oracle meet on
+them (VERDICT r1 parity holes; SURVEY.md §4 test strategy).
+
+Variants (each a small seeded cluster, same document shape as ``generator``):
+
+* ``fit_most``  NodeResourcesFit MostAllocated over cpu / memory /
+  ephemeral-storage / a scalar resource with unequal weights, BalancedAllocation
+  over four resources; init containers (restartPolicy Always sidecars and plain
+  ones), pod overhead, requests of ephemeral-storage and the scalar, empty
+  requests (the non-zero defaults), pods in several namespaces.
+* ``fit_rtc``   the same cluster shape under RequestedToCapacityRatio (a
+  three-point shape) over cpu / memory / the scalar.
+* ``na``        TaintToleration + NodeAffinity + Fit + BA: nodeSelector,
+  required terms with In / NotIn / Exists / DoesNotExist / Gt / Lt (numeric and
+  non-numeric values), matchFields metadata.name In / NotIn, preferred terms,
+  tolerations with Exists / Equal / empty keys / empty effects, PreferNoSchedule
+  and NoExecute taints, nodes without the labels.
+* ``pts``       Fit + PodTopologySpread + BA: minDomains, nodeAffinityPolicy
+  Honor / Ignore, nodeTaintsPolicy Honor / Ignore, matchLabelKeys, several
+  DoNotSchedule / ScheduleAnyway constraints, nodes without the zone label,
+  terminating bound pods, namespaces.
+* ``ipa``       Fit + InterPodAffinity + BA with hardPodAffinityWeight 3:
+  namespaces lists, namespaceSelector {} (every namespace) and a selector no
+  namespace matches, matchExpressions, required / preferred terms on bound pods
+  in several namespaces.
+* ``ipa_ignore`` the ``ipa`` cluster with ignorePreferredTermsOfExistingPods and
+  hardPodAffinityWeight 0.
+"""
+from __future__ import annotations
+
+import json
+
+from .generator import (HOSTNAME, ZONE, Gi, Mi, Rng, make_profile, node_obj, pod_obj, req)
+
+GPU = "example.com/gpu"
+EPH = "ephemeral-storage"
+NAMESPACES = ["default", "ns-a", "ns-b", "team-x"]
+EDGE_VARIANTS = ("fit_most", "fit_rtc", "na", "pts", "ipa", "ipa_ignore")
+
+
+def edge_seed(variant: str) -> int:
+    return 20250131 * 100 + 50 + EDGE_VARIANTS.index(variant)
+
+
+def _containers(r, scalar=True):
+    cs = []
+    for _ in range(1 + r.below(2)):
+        p = r.pct()
+        if p < 12:
+            cs.append({})  # no requests: the non-zero defaults (scoring) and zero (filter)
+            continue
+        extra = {}
+        if r.pct() < 40:
+            extra[EPH] = f"{1 + r.below(20)}Gi"
+        if scalar and r.pct() < 25:
+            extra[GPU] = str(1 + r.below(2))
+        cs.append(req(100 * (1 + r.below(20)), 128 * Mi * (1 + r.below(24)), extra))
+    return cs
+
+
+def _init_containers(r):
+    out = []
+    for i in range(r.below(3)):
+        c = {"name": f"init{i}", "image": "registry.k8s.io/pause:3.5",
+             "resources": req(100 * (1 + r.below(30)), 64 * Mi * (1 + r.below(40)))}
+        if r.pct() < 50:
+            c["restartPolicy"] = "Always"  # a sidecar: its requests add to the containers'
+        out.append(c)
+    return out
+
+
+def _fit_cluster(r, n_nodes, n_pods):
+    nodes = []
+    for i in range(n_nodes):
+        scal = {GPU: r.pick([0, 0, 2, 4, 8])} if r.pct() < 70 else {}
+        nodes.append(node_obj(f"node-{i:07d}", 1000 * r.pick([4, 8, 16, 32]), Gi * r.pick([16, 32, 64, 128]),
+                              pods=r.pick([8, 16, 110]), eph=Gi * r.pick([50, 100, 400]) if r.pct() < 85 else None,
+                              scalars=scal))
+    queue = []
+    for j in range(n_pods):
+        spec = {}
+        ic = _init_containers(r)
+        if ic:
+            spec["initContainers"] = ic
+        if r.pct() < 30:
+            spec["overhead"] = {"cpu": f"{50 * (1 + r.below(4))}m", "memory": f"{32 * (1 + r.below(4))}Mi"}
+        queue.append(pod_obj(f"pod-{j:07d}", _containers(r), ns=r.pick(NAMESPACES), **spec))
+    return nodes, queue
+
+
+def gen_fit(variant, n_nodes=60, n_pods=160, seed=None):
+    seed = edge_seed(variant) if seed is None else seed
+    r = Rng(seed)
+    nodes, queue = _fit_cluster(r, n_nodes, n_pods)
+    prof = make_profile([("NodeResourcesFit", 1), ("NodeResourcesBalancedAllocation", 1)], seed)
+    pc = prof["pluginConfig"]
+    if variant == "fit_most":
+        pc["NodeResourcesFit"] = {"scoringStrategy": {"type": "MostAllocated", "resources": [
+            {"name": "cpu", "weight": 1}, {"name": "memory", "weight": 2}, {"name": EPH, "weight": 1},
+            {"name": GPU, "weight": 3}]}}
+    else:
+        pc["NodeResourcesFit"] = {"scoringStrategy": {"type": "RequestedToCapacityRatio", "resources": [
+            {"name": "cpu", "weight": 2}, {"name": "memory", "weight": 1}, {"name": GPU, "weight": 1}],
+            "requestedToCapacityRatio": {"shape": [{"utilization": 0, "score": 0}, {"utilization": 40, "score": 8},
+                                                   {"utilization": 100, "score": 3}]}}}
+    pc["NodeResourcesBalancedAllocation"] = {"resources": [
+        {"name": "cpu", "weight": 1}, {"name": "memory", "weight": 1}, {"name": EPH, "weight": 1},
+        {"name": GPU, "weight": 1}]}
+    return {"profile": prof, "nodes": nodes, "pods": [], "queue": queue}
+
+
+NA_TAINTS = [{"key": "dedicated", "value": "infra", "effect": "NoSchedule"},
+             {"key": "dedicated", "value": "gpu", "effect": "NoExecute"},
+             {"key": "spot", "value": "", "effect": "PreferNoSchedule"},
+             {"key": "maint", "value": "soon", "effect": "PreferNoSchedule"},
+             {"key": "flaky", "value": "yes", "effect": "NoSchedule"}]
+
+
+def _na_expr(r, n_nodes):
+    k = r.below(8)
+    if k == 0:
+        return {"key": "disk", "operator": "In", "values": sorted({r.pick(["ssd", "hdd", "nvme"]) for _ in range(2)})}
+    if k == 1:
+        return {"key": "disk", "operator": "NotIn", "values": [r.pick(["ssd", "hdd"])]}
+    if k == 2:
+        return {"key": "gpu-model", "operator": "Exists"}
+    if k == 3:
+        return {"key": "gpu-model", "operator": "DoesNotExist"}
+    if k == 4:
+        return {"key": "gen", "operator": "Gt", "values": [str(r.below(6))]}
+    if k == 5:
+        return {"key": "gen", "operator": "Lt", "values": [str(2 + r.below(7))]}
+    if k == 6:
+        return {"key": ZONE, "operator": "In", "values": [f"zone-{r.below(4)}"]}
+    return {"key": "disk", "operator": "Exists"}
+
+
+def _na_fields(r, n_nodes):
+    names = sorted({f"node-{r.below(n_nodes):07d}" for _ in range(1 + r.below(6))})
+    return {"key": "metadata.name", "operator": r.pick(["In", "In", "NotIn"]), "values": names}
+
+
+def gen_na(n_nodes=80, n_pods=160, seed=None):
+    seed = edge_seed("na") if seed is None else seed
+    r = Rng(seed)
+    nodes = []
+    for i in range(n_nodes):
+        labels = {}
+        if r.pct() < 85:
+            labels[ZONE] = f"zone-{r.below(4)}"
+        if r.pct() < 70:
+            labels["disk"] = r.pick(["ssd", "hdd", "nvme"])
+        if r.pct() < 30:
+            labels["gpu-model"] = r.pick(["a", "b"])
+        if r.pct() < 80:
+            labels["gen"] = r.pick([str(g) for g in range(1, 9)] + ["x9"])  # "x9": not an integer (Gt/Lt fail)
+        taints = []
+        for t in NA_TAINTS:
+            if r.pct() < 15:
+                taints.append(dict(t))
+        nodes.append(node_obj(f"node-{i:07d}", 1000 * r.pick([4, 8, 16]), Gi * r.pick([16, 32, 64]), labels=labels,
+                              taints=taints))
+    queue = []
+    for j in range(n_pods):
+        spec = {}
+        tols = []
+        for _ in range(r.below(4)):
+            t = r.pick(NA_TAINTS)
+            k = r.below(5)
+            if k == 0:
+                tols.append({"operator": "Exists"})  # empty key + Exists: every taint
+            elif k == 1:
+                tols.append({"key": t["key"], "operator": "Exists"})
+            elif k == 2:
+                tols.append({"key": t["key"], "operator": "Equal", "value": t["value"], "effect": t["effect"]})
+            elif k == 3:
+                tols.append({"key": t["key"], "value": t["value"]})  # operator defaults to Equal, any effect
+            else:
+                tols.append({"key": t["key"], "operator": "Exists", "effect": r.pick(["NoSchedule", "NoExecute"])})
+        if tols:
+            spec["tolerations"] = tols
+        if r.pct() < 20:
+            spec["nodeSelector"] = {"disk": r.pick(["ssd", "hdd"])}
+        na = {}
+        if r.pct() < 60:
+            terms = []
+            for _ in range(1 + r.below(3)):
+                t = {}
+                if r.pct() < 75:
+                    t["matchExpressions"] = [_na_expr(r, n_nodes) for _ in range(1 + r.below(3))]
+                if r.pct() < 35:
+                    t["matchFields"] = [_na_fields(r, n_nodes)]
+                terms.append(t)
+            na["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": terms}
+        if r.pct() < 60:
+            pref = []
+            for _ in range(1 + r.below(3)):
+                p = {}
+                if r.pct() < 80:
+                    p["matchExpressions"] = [_na_expr(r, n_nodes)]
+                else:
+                    p["matchFields"] = [_na_fields(r, n_nodes)]
+                pref.append({"weight": 1 + r.below(100), "preference": p})
+            na["preferredDuringSchedulingIgnoredDuringExecution"] = pref
+        if na:
+            spec["affinity"] = {"nodeAffinity": na}
+        queue.append(pod_obj(f"pod-{j:07d}", _containers(r, scalar=False), ns=r.pick(NAMESPACES), **spec))
+    prof = make_profile([("TaintToleration", 3), ("NodeAffinity", 2), ("NodeResourcesFit", 1),
+                         ("NodeResourcesBalancedAllocation", 1)], seed)
+    return {"profile": prof, "nodes": nodes, "pods": [], "queue": queue}
+
+
+APPS = [f"app-{k}" for k in range(6)]
+
+
+def _sel(r, key="app"):
+    if r.pct() < 75:
+        return {"matchLabels": {key: r.pick(APPS)}}
+    return {"matchExpressions": [{"key": key, "operator": r.pick(["In", "NotIn"]),
+                                  "values": sorted({r.pick(APPS) for _ in range(2)})}]}
+
+
+def _labels(r):
+    lab = {"app": r.pick(APPS), "tier": r.pick(["web", "db"])}
+    if r.pct() < 50:
+        lab["pod-template-hash"] = r.pick(["h1", "h2", "h3"])
+    return lab
+
+
+def _topo_nodes(r, n_nodes, taints=True):
+    nodes = []
+    for i in range(n_nodes):
+        labels = {}
+        if r.pct() < 88:
+            labels[ZONE] = f"zone-{r.below(5)}"
+        if r.pct() < 60:
+            labels["disk"] = r.pick(["ssd", "hdd"])
+        tl = [dict(NA_TAINTS[0])] if taints and r.pct() < 15 else []
+        nodes.append(node_obj(f"node-{i:07d}", 1000 * r.pick([8, 16, 32]), Gi * r.pick([32, 64]), labels=labels,
+                              taints=tl))
+    return nodes
+
+
+def _bound(r, nodes, n, terms_fn=None):
+    pods = []
+    for e in range(n):
+        spec = {}
+        if terms_fn:
+            aff = terms_fn(r)
+            if aff:
+                spec["affinity"] = aff
+        p = pod_obj(f"ex-{e:07d}", [req(100 * (1 + r.below(8)), 128 * Mi * (1 + r.below(8)))], labels=_labels(r),
+                    node=nodes[r.below(len(nodes))]["metadata"]["name"], ns=r.pick(NAMESPACES), **spec)
+        if r.pct() < 6:
+            p["metadata"]["deletionTimestamp"] = "2025-01-01T00:00:00Z"  # terminating: PodTopologySpread skips it
+        pods.append(p)
+    return pods
+
+
+def gen_pts(n_nodes=70, n_existing=160, n_pods=140, seed=None):
+    seed = edge_seed("pts") if seed is None else seed
+    r = Rng(seed)
+    nodes = _topo_nodes(r, n_nodes)
+    bound = _bound(r, nodes, n_existing)
+    queue = []
+    for j in range(n_pods):
+        spec = {}
+        tsc = []
+        for _ in range(1 + r.below(3)):
+            c = {"maxSkew": 1 + r.below(3), "topologyKey": r.pick([ZONE, ZONE, HOSTNAME, "disk"]),
+                 "whenUnsatisfiable": r.pick(["DoNotSchedule", "ScheduleAnyway"]), "labelSelector": _sel(r)}
+            if c["whenUnsatisfiable"] == "DoNotSchedule" and r.pct() < 35:
+                c["minDomains"] = 2 + r.below(5)
+            if r.pct() < 30:
+                c["nodeAffinityPolicy"] = r.pick(["Honor", "Ignore"])
+            if r.pct() < 30:
+                c["nodeTaintsPolicy"] = r.pick(["Honor", "Ignore"])
+            if r.pct() < 25:
+                c["matchLabelKeys"] = [r.pick(["pod-template-hash", "tier", "missing-key"])]
+            tsc.append(c)
+        spec["topologySpreadConstraints"] = tsc
+        if r.pct() < 25:
+            spec["nodeSelector"] = {"disk": r.pick(["ssd", "hdd"])}
+        if r.pct() < 20:
+            spec["tolerations"] = [{"key": "dedicated", "operator": "Exists"}]
+        queue.append(pod_obj(f"pod-{j:07d}", [req(100 * (1 + r.below(10)), 128 * Mi * (1 + r.below(10)))],
+                             labels=_labels(r), ns=r.pick(NAMESPACES), **spec))
+    prof = make_profile([("NodeResourcesFit", 1), ("PodTopologySpread", 2), ("NodeResourcesBalancedAllocation", 1)],
+                        seed)
+    return {"profile": prof, "nodes": nodes, "pods": bound, "queue": queue}
+
+
+def _aff_term(r, topo=None):
+    t = {"labelSelector": _sel(r), "topologyKey": topo or r.pick([ZONE, HOSTNAME, ZONE])}
+    k = r.below(5)
+    if k == 1:
+        t["namespaces"] = sorted({r.pick(NAMESPACES) for _ in range(2)})
+    elif k == 2:
+        t["namespaceSelector"] = {}  # every namespace
+    elif k == 3:
+        t["namespaceSelector"] = {"matchLabels": {"team": "x"}}  # namespaces carry no labels: none
+    return t
+
+
+def _ipa_affinity(r, p_req_aff, p_req_anti, p_pref):
+    aff, anti = {}, {}
+    if r.pct() < p_req_aff:
+        aff["requiredDuringSchedulingIgnoredDuringExecution"] = [_aff_term(r) for _ in range(1 + r.below(2))]
+    if r.pct() < p_req_anti:
+        anti["requiredDuringSchedulingIgnoredDuringExecution"] = [_aff_term(r, HOSTNAME)]
+    if r.pct() < p_pref:
+        aff["preferredDuringSchedulingIgnoredDuringExecution"] = [
+            {"weight": 1 + r.below(100), "podAffinityTerm": _aff_term(r)} for _ in range(1 + r.below(2))]
+    if r.pct() < p_pref // 2:
+        anti["preferredDuringSchedulingIgnoredDuringExecution"] = [
+            {"weight": 1 + r.below(100), "podAffinityTerm": _aff_term(r)}]
+    out = {}
+    if aff:
+        out["podAffinity"] = aff
+    if anti:
+        out["podAntiAffinity"] = anti
+    return out
+
+
+def gen_ipa(variant="ipa", n_nodes=60, n_existing=150, n_pods=140, seed=None):
+    seed = edge_seed(variant) if seed is None else seed
+    r = Rng(seed)
+    nodes = _topo_nodes(r, n_nodes, taints=False)
+    bound = _bound(r, nodes, n_existing, lambda rr: _ipa_affinity(rr, 6, 8, 20))
+    queue = []
+    for j in range(n_pods):
+        spec = {}
+        aff = _ipa_affinity(r, 15, 25, 40)
+        if aff:
+            spec["affinity"] = aff
+        queue.append(pod_obj(f"pod-{j:07d}", [req(100 * (1 + r.below(10)), 128 * Mi * (1 + r.below(10)))],
+                             labels=_labels(r), ns=r.pick(NAMESPACES), **spec))
+    prof = make_profile([("NodeResourcesFit", 1), ("InterPodAffinity", 2), ("NodeResourcesBalancedAllocation", 1)],
+                        seed)
+    ipa = prof["pluginConfig"]["InterPodAffinity"]
+    if variant == "ipa_ignore":
+        ipa["hardPodAffinityWeight"] = 0
+        ipa["ignorePreferredTermsOfExistingPods"] = True
+    else:
+        ipa["hardPodAffinityWeight"] = 3
+    return {"profile": prof, "nodes": nodes, "pods": bound, "queue": queue}
+
+
+def generate_edge(variant: str, **sizes) -> dict:
+    if variant in ("fit_most", "fit_rtc"):
+        return gen_fit(variant, **sizes)
+    if variant == "na":
+        return gen_na(**sizes)
+    if variant == "pts":
+        return gen_pts(**sizes)
+    if variant in ("ipa", "ipa_ignore"):
+        return gen_ipa(variant, **sizes)
+    raise ValueError(variant)
+
+
+def dumps(doc) -> str:
+    return json.dumps(doc, separators=(",", ":"), sort_keys=False)

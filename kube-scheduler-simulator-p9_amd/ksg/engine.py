@@ -82,7 +82,7 @@ def load_library():
     L.ksg_prefilter_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_prefilter_result.argtypes = [vp, u32, cp, sz, ctypes.POINTER(sz)]
     L.ksg_filter_status.argtypes = [vp, u32, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
-    L.ksg_prescore_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32)]
+    L.ksg_prescore_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_normalized_scores.argtypes = [vp, u32, u32, ctypes.POINTER(i64), u32]
     L.ksg_synth_cluster.argtypes = [ctypes.c_int, i64, i64, i64, i64, ctypes.c_uint64, ctypes.POINTER(vp),
                                     ctypes.POINTER(sz)]
@@ -269,9 +269,8 @@ class Scheduler:
         return self._status(self.L.ksg_filter_status, q, pos, node)
 
     def prescore_status(self, q, pos):
-        code = ctypes.c_int32()
-        self._chk(self.L.ksg_prescore_status(self.h, q, pos, ctypes.byref(code)), "ksg_prescore_status")
-        return code.value
+        """(framework.Code, message) of PreScore at profile position pos; code -1: not run."""
+        return self._status(self.L.ksg_prescore_status, q, pos)
 
     def normalized_scores(self, q, pos):
         n = self.n_nodes

@@ -20,6 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
 sys.path.insert(0, os.path.dirname(HERE))
 
+from ksg import edge  # noqa: E402
 from ksg import generator as g  # noqa: E402
 from _oracle import Oracle  # noqa: E402
 
@@ -75,6 +76,17 @@ FAMILIES = {
 }
 
 
+# edge-case family (ksg/edge.py): plugin arguments and pod / node shapes the configs never make
+EDGE = {
+    "edge_fit_most_small": ("fit_most", dict(n_nodes=12, n_pods=24)),
+    "edge_fit_rtc_small": ("fit_rtc", dict(n_nodes=12, n_pods=24)),
+    "edge_na_small": ("na", dict(n_nodes=16, n_pods=30)),
+    "edge_pts_small": ("pts", dict(n_nodes=16, n_existing=30, n_pods=24)),
+    "edge_ipa_small": ("ipa", dict(n_nodes=14, n_existing=30, n_pods=24)),
+    "edge_ipa_ignore_small": ("ipa_ignore", dict(n_nodes=14, n_existing=30, n_pods=24)),
+}
+
+
 def expected(doc):
     o = Oracle(doc)
     o.schedule(record=3)
@@ -94,7 +106,11 @@ def main():
         doc = g.generate(c, **kw)
         with open(os.path.join(HERE, name + ".json"), "w") as f:
             json.dump({"config": c, "sizes": kw, "cluster": doc, "expected": expected(doc)}, f, sort_keys=True)
-    print("wrote", len(KNOWN) + len(FAMILIES), "fixtures")
+    for name, (v, kw) in EDGE.items():
+        doc = edge.generate_edge(v, **kw)
+        with open(os.path.join(HERE, name + ".json"), "w") as f:
+            json.dump({"edge": v, "sizes": kw, "cluster": doc, "expected": expected(doc)}, f, sort_keys=True)
+    print("wrote", len(KNOWN) + len(FAMILIES) + len(EDGE), "fixtures")
 
 
 if __name__ == "__main__":

@@ -93,6 +93,11 @@ def test_golden_families_match_generator():
     for name in ("cfg1_small", "cfg2_small", "cfg3_small", "cfg4_small"):
         d = fixture(name)
         assert g.generate(d["config"], **d["sizes"]) == d["cluster"], name
+    from ksg import edge
+    for name in ("edge_fit_most_small", "edge_fit_rtc_small", "edge_na_small", "edge_pts_small", "edge_ipa_small",
+                 "edge_ipa_ignore_small"):
+        d = fixture(name)
+        assert edge.generate_edge(d["edge"], **d["sizes"]) == d["cluster"], name
 
 
 def _py_go_log(x):

@@ -71,7 +71,7 @@ def rebuild(s, q, prof, names, status):
     if not aborted and len(feasible) > 1 and status != 2:
         skipped = set()
         for pos, name in enumerate(plugins):
-            code = s.prescore_status(q, pos)
+            code, _ = s.prescore_status(q, pos)
             if code == C_NOT_RUN:
                 continue
             pre_score[name] = "success" if code == C_SUCCESS else ""
@@ -86,6 +86,11 @@ def rebuild(s, q, prof, names, status):
                 fin.setdefault(names[i], {})[name] = str(norm[i] * w)
     elif aborted:
         filt = {}
+    elif len(feasible) > 1 and status == 2:  # a PreScore failed: the statuses up to it
+        for pos, name in enumerate(plugins):
+            code, msg = s.prescore_status(q, pos)
+            if code != C_NOT_RUN:
+                pre_score[name] = "success" if code == C_SUCCESS else msg
     return {P + "prefilter-result-status": _js(pre_status), P + "prefilter-result": _js(pre_result),
             P + "filter-result": _js(filt), P + "prescore-result": _js(pre_score),
             P + "score-result": _js(score), P + "finalscore-result": _js(fin)}
@@ -122,7 +127,7 @@ def test_annotations_from_extension_point_calls(name, c, sizes):
         if r.selected >= 0 and r.feasible > 1:
             tot = 0
             for pos, pl in enumerate(doc["profile"]["plugins"]):
-                if pl in SCORERS and s.prescore_status(q, pos) == C_SUCCESS or pl == "ImageLocality":
+                if pl in SCORERS and s.prescore_status(q, pos)[0] == C_SUCCESS or pl == "ImageLocality":
                     tot += s.normalized_scores(q, pos)[r.selected] * doc["profile"]["weights"][pl]
             assert tot == r.total, (name, i)
         checked += 1

@@ -12,13 +12,15 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
 
-NAMES = {0: "k_eval: issue loads", 1: "k_eval: loads issued", 2: "k_eval: after eval_setup", 3: "k_eval: filter done",
+NAMES = {13: "k_eval: entry + gap stamp", 7: "k_eval: inputs issued (vids, row, setup)", 11: "k_eval: +1 stamp", 12: "k_eval: +2 stamps", 8: "k_eval: slot vids in LDS", 9: "k_eval: lookups issued",
+         10: "k_eval: setup (minMatchNum, IPA bits)",
+         3: "k_eval: filter done",
          4: "k_eval: scores done", 5: "k_eval: block reduce", 6: "k_eval: partials written",
          16: "k_final: raw loads issued", 17: "k_final: partials folded", 18: "k_final: ipa bits",
          19: "k_final: normalized + key", 20: "k_final: block key written",
-         24: "k_select: partials loaded", 25: "k_select: block reduce", 26: "k_select: summary + row atomics",
-         27: "k_select: class tables", 40: "gap k_eval->k_final entry", 41: "gap k_final->k_select entry",
-         42: "gap k_select->next k_eval entry"}
+         24: "select (last block): partials loaded", 25: "select (last block): block reduce", 26: "select (last block): summary + row atomics",
+         27: "select (last block): class tables", 40: "gap k_eval->k_final entry",
+         42: "gap k_final->next k_eval entry"}
 
 
 def main():
@@ -41,9 +43,11 @@ def main():
     out = (ctypes.c_uint64 * 64)()
     n = ctypes.c_size_t()
     s.L.ksg_debug_eval_stamps(s.h, 1, out, ctypes.byref(n))
-    pods = out[63] or 1
-    res = {NAMES.get(k, str(k)): round(out[k] / pods * 0.01, 3) for k in sorted(NAMES) if out[k]}
-    print(json.dumps({"pods": pods, "us_avg_block0": res}, indent=1))
+    pods = s.queue_len - 64  # every cycle's block 0 stamps; the select's only when block 0 arrives last
+    last = out[63] or 1
+    res = {NAMES.get(k, str(k)): round(out[k] / (last if 24 <= k <= 27 else pods) * 0.01, 3)
+           for k in sorted(NAMES, key=lambda k: (k not in (13, 7, 11, 12, 8, 9, 10), k)) if out[k]}
+    print(json.dumps({"pods": pods, "select_samples": last, "us_avg_block0": res}, indent=1))
 
 
 if __name__ == "__main__":

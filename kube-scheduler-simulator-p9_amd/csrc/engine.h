@@ -105,6 +105,9 @@ class Engine {
   // capacities: pods/terms/reqs/vals of the existing-pod table (device appends on assume)
   bool upload(const NodeSoA& nodes, const PodTableSoA& pods, uint32_t pod_cap, uint32_t term_cap,
               uint32_t req_cap, uint32_t val_cap, std::string& err);
+  // Resource columns of the Fit / BalancedAllocation scoring arguments (after a
+  // vocabulary build: the columns the names resolve to).
+  bool set_score_resources(const int32_t* fit_res, const int32_t* ba_res, std::string& err);
   // Queue programs: blobs laid out by the host encoder (ksg_prog + pools).
   bool set_programs(const std::vector<std::vector<uint8_t>>& progs, std::string& err);
   // Append one program (drop-in cycle API); its index is the previous count.

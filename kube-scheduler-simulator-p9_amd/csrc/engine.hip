@@ -3690,20 +3690,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
     if (F.plugins[i] == KP_FIT) { F.pos_fit = i; F.w_fit = F.weight[i]; }
     if (F.plugins[i] == KP_BA) { F.pos_ba = i; F.w_ba = F.weight[i]; }
   }
-  {
-    std::vector<int32_t> fr(F.fit_res, F.fit_res + KSG_MAX_SCORE_RES), br(F.ba_res, F.ba_res + KSG_MAX_SCORE_RES);
-    std::vector<int64_t> fw(F.fit_w, F.fit_w + KSG_MAX_SCORE_RES);
-    if (!I.fit_res_d.upload(fr, I.stream, err) || !I.ba_res_d.upload(br, I.stream, err) ||
-        !I.fit_w_d.upload(fw, I.stream, err))
-      return false;
-    F.fit_res_d = I.fit_res_d.p;
-    F.fit_w_d = I.fit_w_d.p;
-    F.ba_res_d = I.ba_res_d.p;
-    I.eval_mode = (F.fit_strategy == 0 && F.fit_n == 2 && F.fit_res[0] == 0 && F.fit_res[1] == 1 && F.fit_w[0] == 1 &&
-                   F.fit_w[1] == 1 && F.ba_n == 2 && F.ba_res[0] == 0 && F.ba_res[1] == 1)
-                      ? 1
-                      : 0;
-  }
+  if (!set_score_resources(F.fit_res, F.ba_res, err)) return false;
   I.static_ok = F.n > 0 && (F.pos_taint >= 0 || F.pos_na >= 0);
   for (int i = 0; i < F.n; ++i)
     I.static_ok &= (F.plugins[i] == KP_FIT || F.plugins[i] == KP_BA || F.plugins[i] == KP_TAINT || F.plugins[i] == KP_NA);
@@ -4550,10 +4537,12 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   CA.stamps = I.cstamps_on ? I.cstamps.p : nullptr;
   const int rowm = I.R > 4 ? 0 : (I.eval_mode == 1 ? 2 : 1);
   bool pending = false;           // logged assumes whose existing-pod table rows are not written yet
-  auto flush = [&](uint32_t j) {  // rows of the pods [log_base, j), then the log restarts at j
+  // rows of the logged pods [log_base, j); the log restarts at `next` (a pod of the
+  // scanning chain is not logged: the log restarts after it)
+  auto flush = [&](uint32_t j, uint32_t next) {
     if (pending) hipLaunchKernelGGL(k_flush_appends, dim3(1), b, 0, s, C, CA, j - CA.log_base);
     pending = false;
-    CA.log_base = j;
+    CA.log_base = next;
   };
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
@@ -4576,7 +4565,7 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
       pending |= (CA.mode & 2) != 0;
       continue;
     }
-    flush(j);  // the scanning chain reads the existing-pod table
+    flush(j, j + 1);  // the scanning chain reads the existing-pod table
     const int mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
     DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j, xchain ? nullptr : I.arrive1.p, mode, I.prow.p + j};
     bool kept = I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n;
@@ -4643,7 +4632,7 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
     }
     // unsharded: selectHost + assume folded into the last block of the cycle's last kernel
   }
-  flush(first + count);
+  flush(first + count, first + count);
   HIPCHK(hipEventRecord(I.ev1, s));
   HIPCHK(hipGetLastError());
   return true;
@@ -4758,6 +4747,30 @@ bool Engine::nccl_unique_id(void* out128, std::string& err) {
   return true;
 }
 void Engine::set_path(int per_pod) { p_->force_per_pod = per_pod != 0; }
+// The resource columns of the Fit / BalancedAllocation scoring arguments (known
+// once the snapshot's resource vocabulary is: after every vocabulary build).
+bool Engine::set_score_resources(const int32_t* fit_res, const int32_t* ba_res, std::string& err) {
+  Impl& I = *p_;
+  DevProfile& F = I.F;
+  for (int i = 0; i < KSG_MAX_SCORE_RES; ++i) {
+    F.fit_res[i] = fit_res[i];
+    F.ba_res[i] = ba_res[i];
+  }
+  std::vector<int32_t> fr(F.fit_res, F.fit_res + KSG_MAX_SCORE_RES), br(F.ba_res, F.ba_res + KSG_MAX_SCORE_RES);
+  std::vector<int64_t> fw(F.fit_w, F.fit_w + KSG_MAX_SCORE_RES);
+  if (!I.fit_res_d.upload(fr, I.stream, err) || !I.ba_res_d.upload(br, I.stream, err) ||
+      !I.fit_w_d.upload(fw, I.stream, err))
+    return false;
+  F.fit_res_d = I.fit_res_d.p;
+  F.fit_w_d = I.fit_w_d.p;
+  F.ba_res_d = I.ba_res_d.p;
+  I.eval_mode = (F.fit_strategy == 0 && F.fit_n == 2 && F.fit_res[0] == 0 && F.fit_res[1] == 1 && F.fit_w[0] == 1 &&
+                 F.fit_w[1] == 1 && F.ba_n == 2 && F.ba_res[0] == 0 && F.ba_res[1] == 1)
+                    ? 1
+                    : 0;
+  return true;
+}
+
 bool Engine::eval_stamps(bool on, std::vector<uint64_t>* out, std::string& err) {
   Impl& I = *p_;  // table chain stamps (table_chain.hip CS_*): 64 slots
   if (!out) {

@@ -1696,7 +1696,7 @@ struct Cluster {
       for (auto& p : queue)
         if (p.volume_plugins_act) { err = "pod " + p.name + ": volumes the volume plugins act on are not modelled"; return false; }
     if (!equal_priorities()) return false;
-    if (!build_vocab()) return false;
+    if (!build_vocab() || !eng->set_score_resources(ecfg.fit_res, ecfg.ba_res, err)) return false;
     NodeSoA S;
     PodTableSoA T;
     if (!encode_snapshot(S, T)) return false;
@@ -1864,7 +1864,7 @@ struct Cluster {
     }
     nkeys = Dict(); nvals.clear(); pkeys = Dict(); pvals.clear(); nss = Dict();
     taint_id.clear(); taints.clear(); topo = Dict();
-    bool ok = build_vocab();
+    bool ok = build_vocab() && eng->set_score_resources(ecfg.fit_res, ecfg.ba_res, err);
     NodeSoA S;
     PodTableSoA T;
     ok = ok && encode_snapshot(S, T);

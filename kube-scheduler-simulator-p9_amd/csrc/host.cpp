@@ -78,16 +78,29 @@ static bool parse_i64(const string& s, i64& out) {
 }
 
 // resource.Quantity -> exact nano units; Value()/MilliValue() round up.
+// Quantities beyond 10^30 or with exponents beyond +-40 (no Kubernetes object
+// carries them) are rejected rather than overflowing.
+static bool mul_i128(i128& x, i128 f) {
+  static const i128 kMax = (i128)(((unsigned __int128)1 << 126) - 1);
+  if (x > kMax / f) return false;
+  x *= f;
+  return true;
+}
 static bool quantity(const string& s, i128& nano) {
   size_t i = 0;
   bool neg = false;
   if (i < s.size() && (s[i] == '+' || s[i] == '-')) neg = s[i++] == '-';
   i128 m = 0;
-  int frac = 0;
+  int frac = 0, nd = 0;
   bool digits = false, dot = false;
   for (; i < s.size(); ++i) {
     char c = s[i];
     if (std::isdigit((unsigned char)c)) {
+      if (m == 0 && c == '0' && !dot) {  // leading zeros
+        digits = true;
+        continue;
+      }
+      if (++nd > 30) return false;
       m = m * 10 + (c - '0');
       digits = true;
       if (dot) ++frac;
@@ -100,7 +113,7 @@ static bool quantity(const string& s, i128& nano) {
   if (!digits) return false;
   string suf = s.substr(i);
   i128 num = m * 1000000000, den = 1;
-  for (int k = 0; k < frac; ++k) den *= 10;
+  for (int k = 0; k < frac; ++k) den *= 10;  // <= 10^30
   static const char* dec[] = {"n", "u", "m", "", "k", "M", "G", "T", "P", "E"};
   static const int dexp[] = {-9, -6, -3, 0, 3, 6, 9, 12, 15, 18};
   static const char* bin[] = {"Ki", "Mi", "Gi", "Ti", "Pi", "Ei"};
@@ -108,20 +121,24 @@ static bool quantity(const string& s, i128& nano) {
   for (int k = 0; k < 10 && !ok; ++k)
     if (suf == dec[k]) {
       int e = dexp[k];
-      for (; e > 0; --e) num *= 10;
-      for (; e < 0; ++e) den *= 10;
+      for (; e > 0; --e)
+        if (!mul_i128(num, 10)) return false;
+      for (; e < 0; ++e)
+        if (!mul_i128(den, 10)) return false;
       ok = true;
     }
   for (int k = 0; k < 6 && !ok; ++k)
     if (suf == bin[k]) {
-      num <<= 10 * (k + 1);
+      if (!mul_i128(num, (i128)1 << (10 * (k + 1)))) return false;
       ok = true;
     }
   if (!ok && !suf.empty() && (suf[0] == 'e' || suf[0] == 'E')) {
     i64 e;
-    if (!parse_i64(suf.substr(1), e)) return false;
-    for (; e > 0; --e) num *= 10;
-    for (; e < 0; ++e) den *= 10;
+    if (!parse_i64(suf.substr(1), e) || e > 40 || e < -40) return false;
+    for (; e > 0; --e)
+      if (!mul_i128(num, 10)) return false;
+    for (; e < 0; ++e)
+      if (!mul_i128(den, 10)) return false;
     ok = true;
   }
   if (!ok) return false;
@@ -133,9 +150,13 @@ static bool quantity(const string& s, i128& nano) {
 static i64 up_div(i128 a, i64 b) {
   i128 q = a / b;
   if (q * b != a && a > 0) ++q;
+  if (q > (i128)INT64_MAX) return INT64_MAX;
+  if (q < (i128)INT64_MIN) return INT64_MIN;
   return (i64)q;
 }
 static i64 as_value(i128 nano) { return up_div(nano, 1000000000LL); }
+// int64 addition with Go's wrap-around (NodeInfo sums; the device adds the same way)
+static inline i64 wadd(i64 a, i64 b) { return (i64)((uint64_t)a + (uint64_t)b); }
 static i64 as_milli(i128 nano) { return up_div(nano, 1000000LL); }
 
 typedef map<string, i128> RList;
@@ -545,16 +566,32 @@ struct Cluster {
               if (ecfg.fit_n >= KSG_MAX_SCORE_RES) break;
               fit_res_names.push_back(str_of(r["name"]));
               ecfg.fit_w[ecfg.fit_n++] = r["weight"] ? r["weight"]->num() : 1;
+              if (ecfg.fit_w[ecfg.fit_n - 1] < 1 || ecfg.fit_w[ecfg.fit_n - 1] > 100) {  // validation.go
+                err = "NodeResourcesFit: resource weight out of 1..100";
+                return false;
+              }
             }
           }
           if (const J* rtc = (*ss)["requestedToCapacityRatio"])
             if (const J* sh = (*rtc)["shape"])
-              for (auto& pt : sh->items) {
-                if (ecfg.rtc_n >= KSG_MAX_RTC) break;
-                ecfg.rtc_util[ecfg.rtc_n] = pt["utilization"]->num();
-                ecfg.rtc_score[ecfg.rtc_n++] = pt["score"]->num() * (100 / 10);  // MaxNodeScore / MaxCustomPriorityScore
+              for (auto& pt : sh->items) {  // validation.go: utilization 0..100 increasing, score 0..10
+                if (ecfg.rtc_n >= KSG_MAX_RTC || !pt["utilization"] || !pt["score"]) {
+                  err = "requestedToCapacityRatio: invalid shape";
+                  return false;
+                }
+                const i64 u = pt["utilization"]->num(-1), sc = pt["score"]->num(-1);
+                if (u < 0 || u > 100 || sc < 0 || sc > 10 || (ecfg.rtc_n > 0 && u <= ecfg.rtc_util[ecfg.rtc_n - 1])) {
+                  err = "requestedToCapacityRatio: invalid shape";
+                  return false;
+                }
+                ecfg.rtc_util[ecfg.rtc_n] = u;
+                ecfg.rtc_score[ecfg.rtc_n++] = sc * (100 / 10);  // MaxNodeScore / MaxCustomPriorityScore
               }
         }
+      if (ecfg.fit_strategy == 2 && ecfg.rtc_n == 0) {
+        err = "requestedToCapacityRatio: shape required";
+        return false;
+      }
       if (const J* ba = (*pc)["NodeResourcesBalancedAllocation"])
         if (const J* rs = (*ba)["resources"]) {
           ba_res_names.clear();
@@ -1007,7 +1044,7 @@ struct Cluster {
     for (auto& kv : p.req) {
       int32_t r = res.get(kv.first);
       if (r < 0) continue;
-      out_req[r] += r == 0 ? as_milli(kv.second) : as_value(kv.second);
+      out_req[r] = wadd(out_req[r], r == 0 ? as_milli(kv.second) : as_value(kv.second));
     }
     auto c = p.req_nz.find("cpu");
     auto m = p.req_nz.find("memory");
@@ -1175,9 +1212,9 @@ struct Cluster {
       uint32_t i = (uint32_t)g - lo;
       i64 nzc, nzm;
       add_requests(p, rq, nzc, nzm);
-      for (uint32_t r = 0; r < R; ++r) S.requested[(size_t)r * n + i] += rq[r];
-      S.nz_cpu[i] += nzc;
-      S.nz_mem[i] += nzm;
+      for (uint32_t r = 0; r < R; ++r) S.requested[(size_t)r * n + i] = wadd(S.requested[(size_t)r * n + i], rq[r]);
+      S.nz_cpu[i] = wadd(S.nz_cpu[i], nzc);
+      S.nz_mem[i] = wadd(S.nz_mem[i], nzm);
       S.pod_count[i] += 1;
       for (auto& h : p.ports) S.port_count[(size_t)port_id[std::make_tuple(h.ip, h.proto, h.port)] * n + i] += 1;
       bound_row[bi] = (int32_t)T.n;
@@ -2459,7 +2496,7 @@ struct Cluster {
     out_req.assign(res.names.size(), 0);
     for (auto& kv : p.req) {
       const int32_t r = res.get(kv.first);
-      if (r >= 0) out_req[r] += r == 0 ? as_milli(kv.second) : as_value(kv.second);
+      if (r >= 0) out_req[r] = wadd(out_req[r], r == 0 ? as_milli(kv.second) : as_value(kv.second));
     }
     auto c = p.req_nz.find("cpu");
     auto mm = p.req_nz.find("memory");

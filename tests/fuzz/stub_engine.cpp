@@ -1,0 +1,220 @@
+// Test-only stand-in for the HIP engine (csrc/engine.hip) so that the host
+// layer (csrc/host.cpp: JSON parsing, vocabulary, snapshot encoding, program
+// compilation, class registry, events, rendering, the C ABI) can be built on
+// the CPU with AddressSanitizer / UndefinedBehaviorSanitizer and fuzzed.
+// Nothing here is shipped or linked into libksg.so: every cycle ends
+// "unschedulable" with no node evaluated; the shapes the host hands over are
+// checked so that an encoder bug shows up as a failure here.
+#include <cstring>
+#include <stdexcept>
+
+#include "../../kube-scheduler-simulator-p9_amd/csrc/engine.h"
+
+namespace ksg {
+
+struct Engine::Impl {
+  EngineConfig cfg;
+  uint32_t N = 0, R = 0;
+  std::vector<std::vector<uint8_t>> progs;
+  std::vector<ksg_pod_summary> sums;
+  std::vector<int64_t> req;
+  std::vector<int32_t> podcnt;
+  uint32_t used[4] = {0, 0, 0, 0}, cap[4] = {0, 0, 0, 0};
+  uint32_t npc = 0, ntc = 0;
+  uint32_t keep_first = 0, keep_n = 0;
+};
+
+static bool check_prog(const std::vector<uint8_t>& p, std::string& err) {
+  if (p.size() < sizeof(ksg_prog)) { err = "stub: short program"; return false; }
+  ksg_prog h;
+  std::memcpy(&h, p.data(), sizeof(h));
+  if (h.total_bytes != p.size()) { err = "stub: program size"; return false; }
+  const uint64_t ends[] = {(uint64_t)h.off_i32 + 4ull * h.n_i32, (uint64_t)h.off_u32 + 4ull * h.n_u32,
+                           (uint64_t)h.off_req + sizeof(ksg_req) * (uint64_t)h.n_req,
+                           (uint64_t)h.off_sel + sizeof(ksg_sel) * (uint64_t)h.n_sel,
+                           (uint64_t)h.off_aterm + sizeof(ksg_aterm) * (uint64_t)h.n_aterm,
+                           (uint64_t)h.off_eterm + sizeof(ksg_exist_term) * (uint64_t)h.n_eterm};
+  for (uint64_t e : ends)
+    if (e > p.size()) { err = "stub: pool outside the program"; return false; }
+  if (h.n_lk < 0 || h.n_lk > KSG_LK_MAX || h.n_ub < 0 || h.n_ub > KSG_UB_MAX) { err = "stub: plan"; return false; }
+  if (h.n_tsc_filter < 0 || h.n_tsc_score < 0 || h.n_tsc_filter + h.n_tsc_score > KSG_MAX_TSC) {
+    err = "stub: constraints";
+    return false;
+  }
+  return true;
+}
+
+Engine::Engine() : p_(new Impl) {}
+Engine::~Engine() { delete p_; }
+bool Engine::init(const EngineConfig& cfg, std::string&) {
+  p_->cfg = cfg;
+  return true;
+}
+bool Engine::upload(const NodeSoA& nodes, const PodTableSoA& pods, uint32_t pod_cap, uint32_t term_cap,
+                    uint32_t req_cap, uint32_t val_cap, std::string& err) {
+  Impl& I = *p_;
+  if (nodes.alloc.size() != (size_t)nodes.n_res * nodes.n || nodes.requested.size() != nodes.alloc.size() ||
+      nodes.label_vid.size() != (size_t)nodes.n_keys * nodes.n || nodes.taint_off.size() != (size_t)nodes.n + 1 ||
+      pods.node.size() != pods.n || pods.label_vid.size() != (size_t)pods.n_keys * pods.n) {
+    err = "stub: snapshot shapes";
+    return false;
+  }
+  if (pod_cap < pods.n || term_cap < pods.terms.size()) { err = "stub: capacities"; return false; }
+  I.N = nodes.n;
+  I.R = nodes.n_res;
+  I.req = nodes.requested;
+  I.podcnt = nodes.pod_count;
+  I.used[0] = pods.n;
+  I.used[1] = (uint32_t)pods.terms.size();
+  I.used[2] = (uint32_t)pods.reqs.size();
+  I.used[3] = (uint32_t)pods.vals.size();
+  I.cap[0] = pod_cap;
+  I.cap[1] = term_cap;
+  I.cap[2] = req_cap;
+  I.cap[3] = val_cap;
+  I.npc = I.ntc = 0;
+  return true;
+}
+bool Engine::set_score_resources(const int32_t*, const int32_t*, std::string&) { return true; }
+bool Engine::set_programs(const std::vector<std::vector<uint8_t>>& progs, std::string& err) {
+  for (auto& p : progs)
+    if (!check_prog(p, err)) return false;
+  p_->progs = progs;
+  p_->sums.assign(progs.size(), ksg_pod_summary{});
+  return true;
+}
+bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) {
+  if (!check_prog(prog, err)) return false;
+  p_->progs.push_back(prog);
+  p_->sums.push_back(ksg_pod_summary{});
+  return true;
+}
+bool Engine::assume(uint32_t q, int32_t gnode, int, std::string& err) {
+  if (q >= p_->progs.size() || gnode < 0) { err = "stub: assume range"; return false; }
+  return true;
+}
+bool Engine::bound_deltas(const std::vector<std::vector<uint8_t>>& progs, const std::vector<int32_t>& gnode,
+                          const std::vector<int32_t>& sign, const std::vector<int32_t>& slot, std::vector<int32_t>& rows,
+                          std::string& err) {
+  if (gnode.size() != progs.size() || sign.size() != progs.size() || slot.size() != progs.size()) {
+    err = "stub: deltas";
+    return false;
+  }
+  for (auto& p : progs)
+    if (!check_prog(p, err)) return false;
+  for (size_t i = 0; i < slot.size(); ++i) {
+    if (slot[i] < 0 || (size_t)slot[i] >= rows.size()) { err = "stub: slot"; return false; }
+    if (sign[i] > 0) rows[slot[i]] = -1;
+  }
+  return true;
+}
+bool Engine::node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_t, std::string& err) {
+  if (gnode < 0 || alloc.size() < p_->R) { err = "stub: node_alloc"; return false; }
+  return true;
+}
+bool Engine::set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err) {
+  if ((size_t)first + count > p_->sums.size()) { err = "stub: summaries range"; return false; }
+  std::memcpy(p_->sums.data() + first, in, (size_t)count * sizeof(ksg_pod_summary));
+  return true;
+}
+bool Engine::table_overflow(bool& overflow, std::string&) {
+  overflow = false;
+  return true;
+}
+bool Engine::table_room(uint32_t used[4], uint32_t cap[4], std::string&) {
+  for (int k = 0; k < 4; ++k) {
+    used[k] = p_->used[k];
+    cap[k] = p_->cap[k];
+  }
+  return true;
+}
+bool Engine::add_classes(const ClassUpload& u, std::string& err) {
+  if (u.tc_off.size() != u.tc_slot.size()) { err = "stub: classes"; return false; }
+  p_->npc += (uint32_t)u.pc.size();
+  p_->ntc += (uint32_t)u.tc_slot.size();
+  return true;
+}
+uint32_t Engine::pod_classes() const { return p_->npc; }
+uint32_t Engine::term_classes() const { return p_->ntc; }
+bool Engine::rebuild_class_tables(std::string&) { return true; }
+bool Engine::replace_program(uint32_t q, const std::vector<uint8_t>& prog, std::string& err) {
+  if (q >= p_->progs.size()) { err = "stub: replace range"; return false; }
+  if (!check_prog(prog, err)) return false;
+  p_->progs[q] = prog;
+  return true;
+}
+bool Engine::normalized(uint32_t, std::vector<int32_t>& norm, std::string&) {
+  norm.assign((size_t)p_->cfg.n_plugins * p_->N, 0);
+  return true;
+}
+bool Engine::run_queue(uint32_t first, uint32_t count, bool, std::string& err) {
+  if ((size_t)first + count > p_->progs.size()) { err = "stub: run range"; return false; }
+  for (uint32_t j = first; j < first + count; ++j) {
+    ksg_pod_summary& s = p_->sums[j];
+    s = ksg_pod_summary{};
+    s.selected = -1;
+    s.status = 1;  // unschedulable: no node evaluated
+  }
+  return true;
+}
+bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) { return run_queue(first, count, false, err); }
+bool Engine::keep_outputs(uint32_t keep_first, uint32_t keep_n, std::string&) {
+  p_->keep_first = keep_first;
+  p_->keep_n = keep_n;
+  return true;
+}
+bool Engine::summaries(uint32_t first, uint32_t count, ksg_pod_summary* out, std::string& err) {
+  if ((size_t)first + count > p_->sums.size()) { err = "stub: summaries range"; return false; }
+  std::memcpy(out, p_->sums.data() + first, (size_t)count * sizeof(ksg_pod_summary));
+  return true;
+}
+bool Engine::outputs(uint32_t prog_idx, PodOutputs& out, std::string& err) {
+  if (prog_idx >= p_->sums.size()) { err = "stub: outputs range"; return false; }
+  out.filter.assign(p_->N, KSG_FILTER_NOT_EVALUATED);
+  out.score.assign((size_t)p_->cfg.n_plugins * p_->N, 0);
+  out.total.assign(p_->N, 0);
+  out.summary = p_->sums[prog_idx];
+  return true;
+}
+bool Engine::sync(std::string&) { return true; }
+bool Engine::reset(std::string&) { return true; }
+void Engine::sample_kernel(uint32_t) {}
+void Engine::set_path(int) {}
+bool Engine::batch_path() const { return false; }
+bool Engine::set_exchange(int, const void*, uint32_t, uint32_t, ExchangeFn, void*, std::string& err) {
+  err = "stub: no exchange";
+  return false;
+}
+uint32_t Engine::exchange_ranks() const { return 1; }
+bool Engine::nccl_unique_id(void*, std::string& err) {
+  err = "stub: no RCCL";
+  return false;
+}
+bool Engine::fixup_stamps(uint32_t, std::vector<uint64_t>* out, std::string&) {
+  if (out) out->clear();
+  return true;
+}
+bool Engine::eval_stamps(bool, std::vector<uint64_t>* out, std::string&) {
+  if (out) out->clear();
+  return true;
+}
+bool Engine::kernel_time(float& avg_ms, uint32_t& samples, std::string&) {
+  avg_ms = 0;
+  samples = 0;
+  return true;
+}
+bool Engine::read_requested(std::vector<int64_t>& requested, std::vector<int32_t>& pod_count, std::string&) {
+  requested = p_->req;
+  pod_count = p_->podcnt;
+  return true;
+}
+bool Engine::read_nonzero(std::vector<int64_t>& nz, std::string&) {
+  nz.assign(2 * (size_t)p_->N, 0);
+  return true;
+}
+uint32_t Engine::n_nodes() const { return p_->N; }
+void* Engine::stream() const { return nullptr; }
+float Engine::last_ms() const { return 0; }
+std::vector<Engine::KernelStat> Engine::kernel_stats() const { return {}; }
+
+}  // namespace ksg

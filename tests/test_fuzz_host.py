@@ -1,0 +1,176 @@
+"""Sanitized fuzzing of the host layer's JSON entry points (CPU only).
+
+csrc/host.cpp (JSON parsing, vocabulary, snapshot encoding, program
+compilation, class registry, cluster events, rendering, the C ABI) is built
+with AddressSanitizer and UndefinedBehaviorSanitizer against a test-only
+stand-in for the HIP engine (tests/fuzz/stub_engine.cpp) and driven through
+ksg_create / ksg_load_cluster / ksg_schedule_queue / ksg_annotations /
+ksg_*_status / ksg_cycle / ksg_reserve / ksg_unreserve / ksg_apply_events /
+ksg_whatif with seeded structural and byte-level mutations of the generator's
+clusters.  Every call must return a status; any sanitizer report fails.
+"""
+import copy
+import json
+import os
+import random
+import subprocess
+
+import pytest
+
+from ksg import edge, generator as g
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+BUILD = os.path.join(HERE, "fuzz", "_build")
+SRCS = [os.path.join(HERE, "fuzz", "fuzz_host.cpp"), os.path.join(HERE, "fuzz", "stub_engine.cpp"),
+        os.path.join(ROOT, "kube-scheduler-simulator-p9_amd", "csrc", "host.cpp"),
+        os.path.join(ROOT, "kube-scheduler-simulator-p9_amd", "csrc", "synth.cpp")]
+DEPS = SRCS + [os.path.join(ROOT, "include", "ksg.h")] + [
+    os.path.join(ROOT, "kube-scheduler-simulator-p9_amd", "csrc", f) for f in ("engine.h", "ksg_types.h", "json.hpp")]
+SEP = "\n\x1e\n"
+
+
+def _binary():
+    exe = os.path.join(BUILD, "fuzz_host")
+    newest = max(os.path.getmtime(p) for p in DEPS)
+    if os.path.exists(exe) and os.path.getmtime(exe) >= newest:
+        return exe
+    os.makedirs(BUILD, exist_ok=True)
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+           "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "include"), "-o", exe] + SRCS
+    subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+    return exe
+
+
+WEIRD = [None, -1, 0, 1, 2 ** 63, -(2 ** 63), 1.5, 1e309, "", "x", "-1", "1e3", "0.1m", "1.5Gi", "999999999999Ei",
+         "100000000000000000000000", [], {}, [1, 2], {"a": "b"}, True, False, "Exists", "In", "Gt", "NoSchedule",
+         "kubernetes.io/hostname", "topology.kubernetes.io/zone", "metadata.name", "node-0000000", "default"]
+
+
+def _leaves(o, path=()):
+    if isinstance(o, dict):
+        for k, v in o.items():
+            yield from _leaves(v, path + (k,))
+        yield path, o
+    elif isinstance(o, list):
+        for i, v in enumerate(o):
+            yield from _leaves(v, path + (i,))
+        yield path, o
+    else:
+        yield path, o
+
+
+def _set(o, path, v):
+    for p in path[:-1]:
+        o = o[p]
+    o[path[-1]] = v
+
+
+def _del(o, path):
+    for p in path[:-1]:
+        o = o[p]
+    del o[path[-1]]
+
+
+def _mutate(doc, r):
+    d = copy.deepcopy(doc)
+    for _ in range(1 + r.randrange(4)):
+        paths = [p for p, _ in _leaves(d) if p]
+        if not paths:
+            break
+        p = r.choice(paths)
+        k = r.randrange(3)
+        try:
+            if k == 0:
+                _set(d, p, copy.deepcopy(r.choice(WEIRD)))
+            elif k == 1:
+                _del(d, p)
+            else:  # duplicate a sibling list element / copy a value elsewhere
+                q = r.choice(paths)
+                _set(d, p, copy.deepcopy(_get(d, q)))
+        except (KeyError, IndexError, TypeError):
+            pass
+    return d
+
+
+def _get(o, path):
+    for p in path:
+        o = o[p]
+    return o
+
+
+def _events(doc, r):
+    ev = []
+    pods = doc.get("pods") or []
+    nodes = doc.get("nodes") or []
+    q = doc.get("queue") or []
+    if q and nodes:
+        p = copy.deepcopy(r.choice(q))
+        p["metadata"]["name"] = p["metadata"]["name"] + "-b"
+        p["spec"]["nodeName"] = r.choice(nodes)["metadata"]["name"]
+        ev.append({"op": "addPod", "pod": p})
+    if pods:
+        x = r.choice(pods)
+        ev.append({"op": "removePod", "name": x["metadata"]["name"], "namespace": x["metadata"].get("namespace", "default")})
+    if nodes:
+        n = copy.deepcopy(r.choice(nodes))
+        n["status"]["allocatable"]["cpu"] = "64"
+        ev.append({"op": "updateNode", "node": n})
+        ev.append({"op": r.choice(["removeNode", "addNode"]), "name": "node-x", "node": copy.deepcopy(nodes[0])})
+    return {"events": ev}
+
+
+def _inputs(r, n_structural, n_bytes):
+    seeds = [g.generate(1, n_nodes=6, n_pods=5), g.generate(2, n_nodes=8, n_pods=6),
+             g.generate(3, n_nodes=8, n_pods=6), g.generate(4, n_nodes=8, n_existing=20, n_pods=6, n_zones=3)]
+    seeds += [edge.generate_edge(v, **({"n_nodes": 8, "n_pods": 8} if v.startswith("fit") or v == "na" else
+                                       {"n_nodes": 8, "n_existing": 16, "n_pods": 8})) for v in edge.EDGE_VARIANTS]
+    out = []
+    for d in seeds:  # unmutated
+        out.append(SEP.join([json.dumps(d["profile"]), json.dumps(d), json.dumps(d["queue"][0]),
+                             json.dumps(_events(d, r))]))
+    for _ in range(n_structural):
+        d = r.choice(seeds)
+        prof = _mutate(d["profile"], r) if r.random() < 0.25 else d["profile"]
+        cl = _mutate(d, r)
+        pod = _mutate(d["queue"][0], r) if r.random() < 0.5 else d["queue"][-1]
+        ev = _mutate(_events(d, r), r) if r.random() < 0.5 else _events(d, r)
+        try:
+            out.append(SEP.join([json.dumps(prof), json.dumps(cl), json.dumps(pod), json.dumps(ev)]))
+        except (ValueError, TypeError):
+            continue
+    for _ in range(n_bytes):
+        s = bytearray(r.choice(out[:len(seeds)]).encode())
+        for _k in range(1 + r.randrange(6)):
+            if not s:
+                break
+            i = r.randrange(len(s))
+            op = r.randrange(4)
+            if op == 0:
+                s[i] = r.choice(b'{}[]":,0123456789-.eExyz\\ \x00\xff')
+            elif op == 1:
+                del s[i:i + r.randrange(1, 40)]
+            elif op == 2:
+                s[i:i] = r.choice([b"null", b"-1", b"1e999", b'""', b"[]", b"{}", b"99999999999999999999", b'"\\u0000"'])
+            else:
+                s = s[:i]
+        out.append(s.decode("latin-1"))
+    return out
+
+
+def test_host_entry_points_under_sanitizers(tmp_path):
+    try:
+        exe = _binary()
+    except (OSError, subprocess.CalledProcessError) as e:  # no g++ / libasan
+        pytest.skip(f"sanitizer build unavailable: {e}")
+    r = random.Random(20250131)
+    files = []
+    for i, text in enumerate(_inputs(r, n_structural=260, n_bytes=140)):
+        f = tmp_path / f"in{i:04d}.txt"
+        f.write_bytes(text.encode("latin-1", errors="replace"))
+        files.append(str(f))
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    p = subprocess.run([exe] + files, capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-6000:])
+    assert f"fuzzed {len(files)} inputs" in p.stdout

@@ -3774,7 +3774,7 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     pn.resize(std::max<size_t>(ns.topo_pairs, 1), 0);
     if (!I.nu_base_d.upload(nb, s, err) || !I.slot_dom_d.upload(sd, s, err) || !I.pair_node_d.upload(pn, s, err))
       return false;
-    I.cnblk = std::max<uint32_t>((ns.n + kBlock - 1) / kBlock, 1);
+    I.cnblk = std::max<uint32_t>((ns.n + kChain - 1) / kChain, 1);
     if (!I.carrive.alloc(1, err) || !I.cpi.alloc((size_t)KCP_I * I.cnblk, err) ||
         !I.cpst.alloc(I.cnblk, err) ||
         !I.cpm.alloc((size_t)2 * KCP_X * I.cnblk, err) || !I.cpm2.alloc((size_t)2 * I.cnblk, err) ||
@@ -4551,16 +4551,16 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
       CA.prog = prog;
       const bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
       if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
-      if (rowm == 2) hipLaunchKernelGGL(k_eval<2>, dim3(I.cnblk), b, 0, s, C, F, CA, prog);
-      else if (rowm == 1) hipLaunchKernelGGL(k_eval<1>, dim3(I.cnblk), b, 0, s, C, F, CA, prog);
-      else hipLaunchKernelGGL(k_eval<0>, dim3(I.cnblk), b, 0, s, C, F, CA, prog);
+      if (rowm == 2) hipLaunchKernelGGL(k_eval<2>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+      else if (rowm == 1) hipLaunchKernelGGL(k_eval<1>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+      else hipLaunchKernelGGL(k_eval<0>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
       if (sampled) {
         HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
         I.n_samples++;
       }
       if (F.has_ext) {  // (k_final's last block selects; without ScoreExtensions k_eval's)
-        if (I.prog_need[j] & 8) hipLaunchKernelGGL(k_ptsraw, dim3(I.cnblk), b, 0, s, C, F, CA, prog);
-        hipLaunchKernelGGL(k_final, dim3(I.cnblk), b, 0, s, C, F, CA, prog);
+        if (I.prog_need[j] & 8) hipLaunchKernelGGL(k_ptsraw, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+        hipLaunchKernelGGL(k_final, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
       }
       pending |= (CA.mode & 2) != 0;
       continue;

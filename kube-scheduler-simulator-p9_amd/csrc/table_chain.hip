@@ -23,6 +23,16 @@
 // selectHost, framework.go RunFilterPlugins / RunScorePlugins, the plugins'
 // Filter / Score / NormalizeScore (restated in oracle/ksg_oracle.cpp).
 
+// Threads per block of k_eval / k_ptsraw / k_final.  256 measured faster than
+// 512 on cfg4 (32.4 vs 34.6 us per pod: the 8-wave block barriers cost more
+// than the halved partial folds and block arrivals save).
+constexpr int kChain = 256;
+// A thread's topology values in the block's LDS image [KSG_MAX_TOPO][kChain].
+struct ChainVids {
+  const int32_t* base;
+  __device__ __forceinline__ int32_t operator()(int s) const { return base[s * kChain]; }
+};
+
 struct ChainArgs {
   const uint8_t* progs;
   const uint64_t* prog_off;
@@ -177,7 +187,7 @@ __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t x
   if (cnt) r.feas = r.ign = 0;
   if (what & RB_ST) r.st = 0;
 #pragma unroll
-  for (int i = 0; i < kBlock / 64; ++i) {
+  for (int i = 0; i < kChain / 64; ++i) {
     const ChainRec* o = lds + i;
     if (cnt) {
       r.feas += o->feas;
@@ -208,10 +218,10 @@ __device__ __forceinline__ int64_t pts_count_tab(const DevCluster& C, const Prog
 }
 
 struct EvalShared {
-  int32_t tv[KSG_MAX_TOPO * kBlock];
+  int32_t tv[KSG_MAX_TOPO * kChain];
   int32_t minm[KSG_MAX_TSC];
   uint32_t ipa_flags;
-  ChainRec rec[kBlock / 64];
+  ChainRec rec[kChain / 64];
 };
 
 // The assume delta's node row as fire-and-forget atomics (no load on the
@@ -282,7 +292,7 @@ __device__ __forceinline__ void chain_last_select(DevCluster& C, const DevProfil
 // node row loaded up front (RowV), 2 the same with the default Fit / BA
 // arguments compiled in.
 template <int ROWM>
-__global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
+__global__ __launch_bounds__(kChain) void k_eval(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
   CS_BEGIN;
   CS_GAP(42, 49, 48);
   CS(13);
@@ -293,7 +303,7 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
   uint32_t* of;
   int32_t *os, *ot;
   chain_outs(A, q, C.N, of, os, ot);
-  const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t n = blockIdx.x * kChain + threadIdx.x;
   const bool active = n < C.N;
   const uint32_t nn = active ? n : 0;  // loads of inactive lanes read node 0 (results unused)
   int pts_pos = -1, ipa_pos = -1;
@@ -348,8 +358,8 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevCluster C, DevProfile F, Cha
   CS(12);
 #pragma unroll
   for (int s = 0; s < KSG_MAX_TOPO; ++s)
-    if ((uint32_t)s < ntopo) L.tv[s * kBlock + threadIdx.x] = vid[s];
-  const SlotVids tv{L.tv + threadIdx.x};  // (each thread reads back only its own column)
+    if ((uint32_t)s < ntopo) L.tv[s * kChain + threadIdx.x] = vid[s];
+  const ChainVids tv{L.tv + threadIdx.x};  // (each thread reads back only its own column)
   CS(8);
   // ---- the lookup plan (ksg_look): every class-table count of this node
   int32_t lkv[KSG_LK_MAX], lks[KSG_LK_MAX];
@@ -623,7 +633,7 @@ __device__ __forceinline__ void reduce_eval(const DevCluster& C, const DevProfil
 // PodTopologySpread raw score of a counted node (scoring.go Score): the constraints'
 // cnt * weight + (maxSkew - 1), in constraint order, rounded half away from zero.
 __device__ __forceinline__ int64_t pts_raw(const DevCluster& C, const ProgView& V, const EvalTotals& E, uint32_t n,
-                                           const SlotVids& tv) {
+                                           const ChainVids& tv) {
 #pragma clang fp contract(off)
   const ksg_prog* h = V.h;
   const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
@@ -646,13 +656,13 @@ __device__ __forceinline__ int64_t pts_raw1(const ksg_prog* h, const EvalTotals&
 }
 
 struct FinalShared {
-  int32_t tv[KSG_MAX_TOPO * kBlock];
-  ChainRec rec[kBlock / 64];
+  int32_t tv[KSG_MAX_TOPO * kChain];
+  ChainRec rec[kChain / 64];
   uint32_t ipa_flags;
 };
 
 // PodTopologySpread raw scores of a pod with several score constraints.
-__global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
+__global__ __launch_bounds__(kChain) void k_ptsraw(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
   const uint32_t q = A.q;
   const ProgView V = view(prog);
   __shared__ FinalShared L;
@@ -662,10 +672,16 @@ __global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, C
   int pts_pos = -1;
   for (int p = 0; p < F.n; ++p)
     if (F.plugins[p] == KP_PTS) pts_pos = p;
-  const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t n = blockIdx.x * kChain + threadIdx.x;
   const bool active = n < C.N;
-  load_slot_vids(C, active ? n : 0, true, L.tv);
-  const SlotVids tv{L.tv + threadIdx.x};
+  {
+    int32_t vid[KSG_MAX_TOPO];
+    node_slot_vids(C, active ? n : 0, vid);
+#pragma unroll
+    for (int t = 0; t < KSG_MAX_TOPO; ++t)
+      if ((uint32_t)t < C.n_topo) L.tv[t * kChain + threadIdx.x] = vid[t];
+  }
+  const ChainVids tv{L.tv + threadIdx.x};
   EvalTotals E;
   reduce_eval(C, F, A, V.h, E, L.rec);
   ChainRec r;
@@ -686,7 +702,7 @@ __global__ __launch_bounds__(kBlock) void k_ptsraw(DevCluster C, DevProfile F, C
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_final(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
+__global__ __launch_bounds__(kChain) void k_final(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
   CS_BEGIN;
   CS_GAP(40, 48, 49);
   const uint32_t q = A.q;
@@ -696,7 +712,7 @@ __global__ __launch_bounds__(kBlock) void k_final(DevCluster C, DevProfile F, Ch
   uint32_t* of;
   int32_t *os, *ot;
   chain_outs(A, q, C.N, of, os, ot);
-  const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t n = blockIdx.x * kChain + threadIdx.x;
   const bool mine = n < C.N && of[n] == KSG_FILTER_PASS;
   int32_t raw[KSG_MAX_PLUGINS];  // this node's raw scores, loaded before the folds
 #pragma unroll

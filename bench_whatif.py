@@ -42,17 +42,17 @@ def main():
     from ksg import Scheduler, generator as g
     t0 = time.time()
     n_pods = a.step_pods * (a.warmup + a.steps)
-    doc = g.generate(5, n_nodes=a.nodes, n_pods=n_pods)
+    blob = g.generate_native(5, n_nodes=a.nodes, n_pods=n_pods)  # native twin of the generator (tests/test_synth.py)
+    prof = json.loads(blob[blob.index(b'"profile"') + 10:].split(b',"nodes"', 1)[0]) if blob.startswith(b'{"profile"') \
+        else json.loads(blob)["profile"]
     print(f"[rank {rank}] generated {a.nodes} nodes / {n_pods} pods in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
     stream = torch.cuda.current_stream().cuda_stream if world > 1 else None
-    s = Scheduler(doc["profile"], device=local, stream=stream, shard_rank=rank, shard_count=world)
+    s = Scheduler(prof, device=local, stream=stream, shard_rank=rank, shard_count=world)
     if world > 1:
         from ksg.distributed import rccl_unique_id_broadcast
         s.set_exchange_rccl(rccl_unique_id_broadcast(s.L, rank))
     t0 = time.time()
-    blob = json.dumps(doc).encode()
     s.load_cluster(blob)
-    del doc
     print(f"[rank {rank}] loaded in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
     P = a.step_pods
     for k in range(a.warmup):

@@ -669,7 +669,7 @@ __global__ void k_init_summaries(ksg_pod_summary* sum, uint32_t count, DevProfil
   sum[i] = s;
 }
 
-__global__ void k_begin(DevCluster C, DevScratch S, const uint8_t* prog) {
+__global__ void k_begin(DevCluster C, DevScratch S, const uint8_t* __restrict__ prog) {
   ProgView V = view(prog);
   uint32_t ntsc = (uint32_t)(V.h->n_tsc_filter + V.h->n_tsc_score);
   size_t cnt_n = (size_t)ntsc * C.N;
@@ -689,7 +689,7 @@ __global__ void k_begin(DevCluster C, DevScratch S, const uint8_t* prog) {
 }
 
 // existing pods x (PTS selectors, IPA incoming required terms, IPA incoming preferred terms)
-__global__ void k_scan_pods(DevCluster C, DevProfile F, DevScratch S, DevOut O, const uint8_t* prog) {
+__global__ void k_scan_pods(DevCluster C, DevProfile F, DevScratch S, DevOut O, const uint8_t* __restrict__ prog) {
   ProgView V = view(prog);
   const ksg_prog* h = V.h;
   uint32_t np = C.tcounts[0];
@@ -747,7 +747,7 @@ __global__ void k_scan_pods(DevCluster C, DevProfile F, DevScratch S, DevOut O, 
 }
 
 // existing pods' terms x incoming pod (existing anti-affinity counts, IPA score terms)
-__global__ void k_scan_terms(DevCluster C, DevProfile F, DevScratch S, DevOut O, const uint8_t* prog) {
+__global__ void k_scan_terms(DevCluster C, DevProfile F, DevScratch S, DevOut O, const uint8_t* __restrict__ prog) {
   ProgView V = view(prog);
   const ksg_prog* h = V.h;
   uint32_t nt = C.tcounts[1];
@@ -791,7 +791,7 @@ __global__ void k_scan_terms(DevCluster C, DevProfile F, DevScratch S, DevOut O,
 }
 
 // PodTopologySpread PreFilter / PreScore per-node aggregation
-__global__ void k_pts_prep(DevCluster C, DevScratch S, const uint8_t* prog) {
+__global__ void k_pts_prep(DevCluster C, DevScratch S, const uint8_t* __restrict__ prog) {
   ProgView V = view(prog);
   const ksg_prog* h = V.h;
   uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -833,7 +833,7 @@ __global__ void k_pts_prep(DevCluster C, DevScratch S, const uint8_t* prog) {
 // minMatchNum / TpKeyToDomainsNum per filter topology key
 // slots: topology slots to reduce (sharded chain: the slots whose domains each
 // sit on one node first, from local counts; the shared ones after the exchange)
-__global__ void k_pts_reduce(DevCluster C, DevScratch S, const uint8_t* prog, uint32_t slots) {
+__global__ void k_pts_reduce(DevCluster C, DevScratch S, const uint8_t* __restrict__ prog, uint32_t slots) {
   ProgView V = view(prog);
   const ksg_prog* h = V.h;
   uint32_t seen = 0;
@@ -885,7 +885,7 @@ __device__ __forceinline__ void last_block_commit(DevCluster& C, const ProgView&
 // instruction cache, not the loop overhead, is what limits this kernel); raw
 // scores go straight to global memory, reductions run per position.
 __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfile F, DevScratch S, DevOut O,
-                                                         const uint8_t* prog) {
+                                                         const uint8_t* __restrict__ prog) {
   ProgView V = view(prog);
   const ksg_prog* h = V.h;
   uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1010,7 +1010,7 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
 // topologyNormalizingWeight per score constraint
 // regcnt (sharded chain, or null): per score constraint, the global count of
 // registered domains of a slot whose domains each sit on one node (uniq)
-__global__ void k_pts_weights(DevCluster C, DevScratch S, DevOut O, const uint8_t* prog, const int64_t* regcnt,
+__global__ void k_pts_weights(DevCluster C, DevScratch S, DevOut O, const uint8_t* __restrict__ prog, const int64_t* regcnt,
                               uint32_t uniq) {
   ProgView V = view(prog);
   const ksg_prog* h = V.h;
@@ -1038,7 +1038,7 @@ __global__ void k_pts_weights(DevCluster C, DevScratch S, DevOut O, const uint8_
   }
 }
 
-__global__ void k_pts_score(DevCluster C, DevScratch S, DevOut O, const uint8_t* prog, int pos) {
+__global__ void k_pts_score(DevCluster C, DevScratch S, DevOut O, const uint8_t* __restrict__ prog, int pos) {
   ProgView V = view(prog);
   const ksg_prog* h = V.h;
   uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1101,7 +1101,7 @@ __device__ __forceinline__ int64_t normalize_pos(int plugin, const ksg_prog* h, 
 }
 
 // NormalizeScore + [0,100] check + weights + packed-key argmax
-__global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, const uint8_t* prog) {
+__global__ void k_finalize(DevCluster C, DevProfile F, DevScratch S, DevOut O, const uint8_t* __restrict__ prog) {
   ProgView V = view(prog);
   const ksg_prog* h = V.h;
   uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1322,7 +1322,7 @@ __device__ void commit_cycle(DevCluster& C, const ProgView& V, ksg_pod_summary* 
   assume_pod(C, V, n, +1, (mode & 2) != 0, prow);
 }
 
-__global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* prog, int mode, int32_t* prow) {
+__global__ void k_commit(DevCluster C, DevProfile F, DevOut O, const uint8_t* __restrict__ prog, int mode, int32_t* prow) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   ProgView V = view(prog);
   commit_cycle(C, V, O.sum, mode, prow, false);
@@ -1407,7 +1407,7 @@ __global__ void k_x1_merge(DevScratch S, DevOut O, XLay L, const int64_t* recv, 
   }
 }
 __device__ __forceinline__ size_t x2_len(const XLay& L) { return 3 + 2 * KSG_MAX_PLUGINS + (size_t)L.nsp + KSG_MAX_TSC; }
-__global__ void k_x2_pack(DevCluster C, DevScratch S, DevOut O, const uint8_t* prog, XLay L, int64_t* out) {
+__global__ void k_x2_pack(DevCluster C, DevScratch S, DevOut O, const uint8_t* __restrict__ prog, XLay L, int64_t* out) {
   __shared__ int32_t red[kBlock / 64];
   const ksg_prog* h = view(prog).h;
   if (threadIdx.x == 0) {
@@ -1482,7 +1482,7 @@ __global__ void k_x4_merge(DevOut O, const int64_t* recv, uint32_t ranks) {
 }
 
 // Reserve / Unreserve on an explicit node (the framework's selectHost choice).
-__global__ void k_assume(DevCluster C, const uint8_t* prog, int32_t gnode, int sign, int table, int32_t* prow) {
+__global__ void k_assume(DevCluster C, const uint8_t* __restrict__ prog, int32_t gnode, int sign, int table, int32_t* prow) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   ProgView V = view(prog);
   uint32_t n = (uint32_t)gnode - C.goff;
@@ -1518,15 +1518,18 @@ struct WiArgs {
   int32_t *kscore, *ktotal;
 };
 
+// (programs as restrict parameters: their reads stay scalar loads beside the
+// kernel's summary atomics and kept-output stores)
 template <int PASS>
-__global__ __launch_bounds__(256) void k_whatif(DevCluster C, DevProfile F, WiArgs A) {
+__global__ __launch_bounds__(256) void k_whatif(DevCluster C, DevProfile F, WiArgs A, const uint8_t* __restrict__ progs,
+                                                const uint64_t* __restrict__ prog_off) {
   const uint32_t base = blockIdx.x * (256 * KSG_WI_NPT) + threadIdx.x;
 #pragma unroll 1
   for (uint32_t pi = 0; pi < KSG_WI_PODS; ++pi) {
     const uint32_t j = blockIdx.y * KSG_WI_PODS + pi;
     if (j >= A.count) break;
     const uint32_t q = A.q0 + j;
-    const ProgView V = view(A.progs + A.prog_off[q]);
+    const ProgView V = view(progs + prog_off[q]);
     const ksg_prog* h = V.h;
     ksg_pod_summary* sm = A.sums + q;
     const bool kept = A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n;
@@ -1699,7 +1702,7 @@ struct StaticRec {
 // the label loads' latency behind (the work per pair is a few dependent loads).
 #define KSG_ST_PODS 4
 #define KSG_ST_NPT 1
-__global__ __launch_bounds__(256) void k_static(DevCluster C, DevProfile F, const uint8_t* progs, const uint64_t* prog_off,
+__global__ __launch_bounds__(256) void k_static(DevCluster C, DevProfile F, const uint8_t* __restrict__ progs, const uint64_t* __restrict__ prog_off,
                                                 uint32_t q0, uint32_t count, StaticRec* out, int64_t* mpred) {
   const uint32_t base = blockIdx.x * (256 * KSG_ST_NPT) + threadIdx.x;
 #pragma unroll 1
@@ -1780,7 +1783,7 @@ __device__ __forceinline__ int64_t static_total(const DevProfile& F, bool skip_n
 // weighted total, packed-key argmax; the last block checks the max, falls back
 // to the exact max when no Fit-feasible node reaches it, and commits.
 // Per-pair outputs are stored sc1 (the fallback re-reads them in this kernel).
-__global__ __launch_bounds__(kBlock) void k_fs_static(DevCluster C, DevProfile F, DevOut O, const uint8_t* prog,
+__global__ __launch_bounds__(kBlock) void k_fs_static(DevCluster C, DevProfile F, DevOut O, const uint8_t* __restrict__ prog,
                                                      const StaticRec* st, const int64_t* mp, int32_t* aux) {
   // aux: [0] a feasible node reaches the static Taint max, [1] NodeAffinity, [2] a score out of range, [3] arrivals
   __shared__ uint64_t red64[kBlock / 64];
@@ -4112,8 +4115,8 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
     for (int pass = 1; pass <= 2; ++pass) {
       const bool sampled = I.sample_every != 0;
       if (sampled) HIPCHK(hipEventRecord(I.sev[2 * (pass - 1)], s));
-      if (pass == 1) hipLaunchKernelGGL(k_whatif<1>, grid, dim3(256), 0, s, C, I.F, A);
-      else hipLaunchKernelGGL(k_whatif<2>, grid, dim3(256), 0, s, C, I.F, A);
+      if (pass == 1) hipLaunchKernelGGL(k_whatif<1>, grid, dim3(256), 0, s, C, I.F, A, A.progs, A.prog_off);
+      else hipLaunchKernelGGL(k_whatif<2>, grid, dim3(256), 0, s, C, I.F, A, A.progs, A.prog_off);
       if (sampled) {
         HIPCHK(hipEventRecord(I.sev[2 * (pass - 1) + 1], s));
         I.n_samples++;

@@ -481,6 +481,8 @@ struct Pod {
   vector<TSC> tsc;
   bool volume_plugins_act = false;  // a volume the volume plugins would not Skip (unsupported)
   i64 priority = 0;
+  bool preempt_never = false;       // spec.preemptionPolicy: Never
+  i64 start_time = INT64_MAX;       // status.startTime (epoch s); none: later than any (util.GetPodStartTime: now)
 };
 
 struct NodeImage {
@@ -520,6 +522,18 @@ static AffTerm parse_aff_term(const ojson::Value& t, const string& owner_ns, boo
   return a;
 }
 
+// "YYYY-MM-DDTHH:MM:SSZ" -> seconds since the epoch (days from civil, proleptic Gregorian)
+static i64 parse_rfc3339(const string& s) {
+  int Y, M, D, h, m, sec;
+  if (std::sscanf(s.c_str(), "%d-%d-%dT%d:%d:%d", &Y, &M, &D, &h, &m, &sec) != 6) return INT64_MAX;
+  Y -= M <= 2;
+  const i64 era = (Y >= 0 ? Y : Y - 399) / 400;
+  const i64 yoe = Y - era * 400;
+  const i64 doy = (153 * (M + (M > 2 ? -3 : 9)) + 2) / 5 + D - 1;
+  const i64 doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return (era * 146097 + doe - 719468) * 86400 + h * 3600 + m * 60 + sec;
+}
+
 static bool parse_pod(const ojson::Value& v, Pod& p) {
   bool err = false;
   auto* md = v.get("metadata");
@@ -532,6 +546,9 @@ static bool parse_pod(const ojson::Value& v, Pod& p) {
   if (!sp) return true;
   p.node_name = sp->get("nodeName") ? sp->get("nodeName")->str() : "";
   if (auto* pr = sp->get("priority"); pr && !pr->is_null()) p.priority = pr->i64();
+  if (auto* pp = sp->get("preemptionPolicy"); pp && !pp->is_null()) p.preempt_never = pp->str() == "Never";
+  if (auto* st = v.get("status"))
+    if (auto* t = st->get("startTime"); t && !t->is_null()) p.start_time = parse_rfc3339(t->str());
   auto conts = [](const ojson::Value* a, vector<Container>& out) {
     if (!a) return;
     for (auto& c : a->arr) {
@@ -839,7 +856,10 @@ struct PodResult {
   int status = 0;  // 0 scheduled, 1 unschedulable, 2 error
   // store maps (resultstore/store.go result)
   map<string, string> pre_filter_status, pre_score;
-  vector<string> post_filter_nodes;  // DefaultPreemption: nodes of the NodeToStatusMap (no nomination)
+  vector<string> post_filter_nodes;  // DefaultPreemption: nodes of the NodeToStatusMap
+  string nominated, preempt_plugin;  // DefaultPreemption dry run: the nominated node, and the plugin's name
+  int nominated_idx = -1;
+  vector<string> victims;            // ... and its victims ("namespace/name", most important first)
   map<string, string> reserve, prebind, bind;  // binding cycle of a scheduled pod (bind assumed to succeed)
   map<string, vector<string>> pre_filter_result;
   std::unordered_map<string, std::unordered_map<string, string>> filter, score, final_score;
@@ -925,11 +945,13 @@ static string render_annotations(const PodResult& r) {
   {  // Store.AddPostFilterResult: every node of the status map gets an (empty) entry
     map<string, map<string, string>> pf;
     for (auto& n : r.post_filter_nodes) pf[n];
+    if (!r.nominated.empty()) pf[r.nominated][r.preempt_plugin] = "preemption victim";  // PostFilterNominatedMessage
     string o = "{";
     for (auto& kv : pf) {
       if (o.size() > 1) o += ',';
       go_json_string(o, kv.first);
-      o += ":{}";
+      o += ':';
+      o += json_map(kv.second);
     }
     ann[k("postfilter-result")] = o + "}";
   }
@@ -1043,6 +1065,166 @@ struct Cluster {
       for (auto& h : c.ports) n.used_ports[h.ip][{h.proto, h.port}]++;
     if (r.with_affinity) n.pods_with_affinity.push_back(pi);
     if (r.has_required_anti) n.pods_with_req_anti.push_back(pi);
+  }
+
+  void remove_pod(int pi, int ni) {  // framework.NodeInfo.RemovePod
+    NodeInfo& n = infos[ni];
+    PodRecord& r = pods[pi];
+    Resource res;
+    resource_add(res, pod_requests(r.pod, false));
+    ResourceList nz = pod_requests(r.pod, true);
+    n.requested.milli_cpu -= res.milli_cpu;
+    n.requested.memory -= res.memory;
+    n.requested.eph -= res.eph;
+    for (auto& kv : res.scalar) n.requested.scalar[kv.first] -= kv.second;
+    n.nz_cpu -= nz.count("cpu") ? q_milli(nz["cpu"]) : 0;
+    n.nz_mem -= nz.count("memory") ? q_value(nz["memory"]) : 0;
+    auto drop = [pi](vector<int>& v) {
+      auto it = std::find(v.begin(), v.end(), pi);
+      if (it != v.end()) v.erase(it);
+    };
+    drop(n.pods);
+    drop(n.pods_with_affinity);
+    drop(n.pods_with_req_anti);
+    for (auto& c : r.pod.containers)
+      for (auto& h : c.ports) {
+        auto& m = n.used_ports[h.ip];
+        if (--m[{h.proto, h.port}] <= 0) m.erase({h.proto, h.port});
+        if (m.empty()) n.used_ports.erase(h.ip);
+      }
+  }
+
+  // ---------------------------------------------------------------- DefaultPreemption (dry run)
+  // The PostFilter of an unschedulable pod (default_preemption.go, framework/
+  // preemption/preemption.go; v1.30.4), run without its side effects: victims are
+  // chosen and a node nominated on the current snapshot, nothing is evicted.
+  // Deliberate, documented choices: every potential node is examined
+  // (upstream examines max(10%, 100) of them from a random offset and stops
+  // early), ties of pickOneNodeForPreemption go to the seeded selectHost rule
+  // (upstream: the first of a map iteration), pods without status.startTime
+  // count as started last (upstream: time.Now()).  No PodDisruptionBudgets exist
+  // in this model, so every victim is non-violating.
+  // Does pod p pass every Filter on node ni of the current snapshot
+  // (SelectVictimsOnNode -> RunFilterPluginsWithNominatedPods; the PreFilter
+  // state is recomputed on the snapshot, which is what RemovePod / AddPod keep
+  // it equal to).
+  bool fits_on(const Pod& p, int ni, Pool& pool) {
+    CycleState cs;
+    set<PluginId> skip;
+    for (size_t k = 0; k < profile.size(); ++k) {
+      PluginId id = profile[k];
+      if (!has_prefilter(id)) continue;
+      Status s;
+      bool has_res = false;
+      if (id == P_FIT) s = fit_prefilter(p, cs);
+      else if (id == P_NA) s = na_prefilter(p, cs, has_res).first;
+      else if (id == P_PTS) s = pts_prefilter(p, cs, pool);
+      else if (id == P_IPA) s = ipa_prefilter(p, cs, pool);
+      else if (id == P_PORTS) s = ports_prefilter(p, cs);
+      else if (id == P_VOLUME || id == P_VOLBIND) s = Status::skip();
+      if (s.code == Status::Skip) { skip.insert(id); continue; }
+      if (!s.ok()) return false;
+    }
+    for (size_t k = 0; k < profile.size(); ++k) {
+      PluginId id = profile[k];
+      if (!has_filter(id) || skip.count(id)) continue;
+      Status s;
+      if (id == P_FIT) s = fit_filter(cs, ni);
+      else if (id == P_TAINT) s = taint_filter(p, ni);
+      else if (id == P_NA) s = na_filter(cs, ni);
+      else if (id == P_PTS) s = pts_filter(p, cs, ni);
+      else if (id == P_IPA) s = ipa_filter(p, cs, ni);
+      else if (id == P_UNSCHED) s = unsched_filter(p, ni);
+      else if (id == P_NODENAME) s = nodename_filter(p, ni);
+      else if (id == P_PORTS) s = ports_filter(cs, ni);
+      if (!s.ok()) return false;
+    }
+    return true;
+  }
+  // util.MoreImportantPod: higher priority, then the earlier start
+  bool more_important(int a, int b) const {
+    const Pod& x = pods[a].pod;
+    const Pod& y = pods[b].pod;
+    if (x.priority != y.priority) return x.priority > y.priority;
+    if (x.start_time != y.start_time) return x.start_time < y.start_time;
+    return a < b;
+  }
+  void preempt(int qidx, int pi, const vector<int>& potential, PodResult& r, Pool& pool) {
+    int pk = -1;
+    for (size_t k = 0; k < profile.size(); ++k)
+      if (profile_names[k] == "DefaultPreemption") pk = (int)k;
+    if (pk < 0) return;
+    const Pod& p = pods[pi].pod;
+    if (p.preempt_never) return;  // PodEligibleToPreemptOthers
+    struct Cand { int node; vector<int> victims; };
+    vector<Cand> cands;
+    for (int ni : potential) {  // DryRunPreemption -> SelectVictimsOnNode
+      vector<int> pv;
+      for (int v : infos[ni].pods)
+        if (pods[v].pod.priority < p.priority) pv.push_back(v);
+      if (pv.empty()) continue;  // "No preemption victims found for incoming pod"
+      for (int v : pv) remove_pod(v, ni);
+      if (!fits_on(p, ni, pool)) {
+        for (int v : pv) add_pod(v, ni);
+        continue;
+      }
+      std::sort(pv.begin(), pv.end(), [&](int a, int b) { return more_important(a, b); });
+      vector<int> victims;
+      for (int v : pv) {  // reprieve, most important first
+        add_pod(v, ni);
+        if (!fits_on(p, ni, pool)) {
+          remove_pod(v, ni);
+          victims.push_back(v);
+        }
+      }
+      for (int v : victims) add_pod(v, ni);  // dry run: the snapshot is left as it was
+      if (!victims.empty()) cands.push_back({ni, victims});
+    }
+    if (cands.empty()) return;
+    // pickOneNodeForPreemption: min PDB violations (none), min highest victim
+    // priority, min sum of (priority + 2^31), fewest victims, latest start of the
+    // highest-priority victims; then the seeded tie-break
+    auto key = [&](const Cand& c, int f) -> i64 {
+      const vector<int>& v = c.victims;
+      switch (f) {
+        case 0: return -(i64)pods[v[0]].pod.priority;
+        case 1: {
+          i64 s = 0;
+          for (int x : v) s += pods[x].pod.priority + (i64)2147483648LL;
+          return -s;
+        }
+        case 2: return -(i64)v.size();
+        default: {
+          const i64 hp = pods[v[0]].pod.priority;
+          i64 e = pods[v[0]].pod.start_time;
+          for (int x : v)
+            if (pods[x].pod.priority == hp && pods[x].pod.start_time < e) e = pods[x].pod.start_time;
+          return e;
+        }
+      }
+    };
+    vector<size_t> all(cands.size());
+    for (size_t i = 0; i < all.size(); ++i) all[i] = i;
+    for (int f = 0; f < 4 && all.size() > 1; ++f) {
+      i64 best = INT64_MIN;
+      vector<size_t> sel;
+      for (size_t i : all) {
+        const i64 k = key(cands[i], f);
+        if (k > best) { best = k; sel.clear(); }
+        if (k == best) sel.push_back(i);
+      }
+      all = sel;
+    }
+    size_t pick = all[0];
+    unsigned long long bk = 0;
+    for (size_t i : all) {
+      const unsigned long long k = pack_key(0, qidx, cands[i].node);
+      if (k > bk) { bk = k; pick = i; }
+    }
+    r.nominated = nodes[cands[pick].node].name;
+    r.nominated_idx = cands[pick].node;
+    r.preempt_plugin = profile_names[pk];
+    for (int v : cands[pick].victims) r.victims.push_back(pods[v].pod.ns + "/" + pods[v].pod.name);
   }
 
   // ---------------------------------------------------------------- NodeResourcesFit
@@ -1728,7 +1910,7 @@ struct Cluster {
     vector<int> cand;
     for (int ni = 0; ni < (int)nodes.size(); ++ni)
       if (!have_names || names.count(nodes[ni].name)) cand.push_back(ni);
-    vector<char> pass(cand.size(), 0);
+    vector<char> pass(cand.size(), 0), fcode(cand.size(), 0);  // fcode: 1 Unschedulable, 2 ...AndUnresolvable
     std::atomic<bool> err{false};
     pool.until((int)cand.size(), [&](int i) {
       int ni = cand[i];
@@ -1747,6 +1929,7 @@ struct Cluster {
         rec([&] { r.filter[nodes[ni].name][profile_names[k]] = s.ok() ? "passed" : s.msg; });
         if (!s.ok()) {
           if (s.code == Status::Error) err = true;
+          fcode[i] = s.code == Status::Unschedulable ? 1 : 2;
           return;
         }
       }
@@ -1757,7 +1940,17 @@ struct Cluster {
       if (pass[i]) feasible.push_back(cand[i]);
     r.feasible = (int)feasible.size();
     if (err) { r.status = 2; finish(qidx, pi, r, record); return; }
-    if (feasible.empty()) { r.status = 1; finish(qidx, pi, r, record); return; }
+    if (feasible.empty()) {
+      r.status = 1;
+      if (record) {  // PostFilter: DefaultPreemption dry run
+        vector<int> potential;  // nodesWherePreemptionMightHelp: not UnschedulableAndUnresolvable
+        for (size_t i = 0; i < cand.size(); ++i)
+          if (fcode[i] == 1) potential.push_back(cand[i]);
+        preempt(qidx, pi, potential, r, pool);
+      }
+      finish(qidx, pi, r, record);
+      return;
+    }
     int chosen = -1;
     if (feasible.size() == 1) {
       chosen = feasible[0];
@@ -2064,6 +2257,18 @@ int ksg_oracle_result(ksg_oracle* h, int q, int* selected, int* feasible, int* s
 }
 
 unsigned long long ksg_oracle_digest(ksg_oracle* h, int q) { return h->c.digests[q]; }
+
+// DefaultPreemption dry run of queue pod q (record >= 1): nominated node index or -1;
+// its victims as "namespace/name" lines (most important first) into buf.
+int ksg_oracle_nominated(ksg_oracle* h, int q, char* buf, size_t cap, size_t* len) {
+  if (q < 0 || q >= (int)h->c.results.size()) return -2;
+  const oracle::PodResult& r = h->c.results[q];
+  std::string v;
+  for (auto& x : r.victims) v += x + "\n";
+  if (len) *len = v.size();
+  if (buf && cap >= v.size()) std::memcpy(buf, v.data(), v.size());
+  return r.nominated_idx;
+}
 
 // Rendered GetStoredResult map (JSON object of annotation key -> value); record >= 3.
 const char* ksg_oracle_annotations(ksg_oracle* h, int q, size_t* len) {

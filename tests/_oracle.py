@@ -29,6 +29,9 @@ def lib():
         L.ksg_oracle_result.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.POINTER(ctypes.c_int)] * 3
         L.ksg_oracle_digest.restype = ctypes.c_ulonglong
         L.ksg_oracle_digest.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.ksg_oracle_nominated.restype = ctypes.c_int
+        L.ksg_oracle_nominated.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_size_t)]
         L.ksg_oracle_annotations.restype = ctypes.c_void_p
         L.ksg_oracle_annotations.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
         L.ksg_oracle_go_log.restype = ctypes.c_double
@@ -72,6 +75,14 @@ class Oracle:
 
     def digest(self, q):
         return lib().ksg_oracle_digest(self.h, q)
+
+    def nominated(self, q):
+        """DefaultPreemption dry run of queue pod q: (nominated node index or -1, victims)."""
+        n = ctypes.c_size_t()
+        lib().ksg_oracle_nominated(self.h, q, None, 0, ctypes.byref(n))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        idx = lib().ksg_oracle_nominated(self.h, q, buf, n.value + 1, ctypes.byref(n))
+        return idx, [x for x in buf.raw[:n.value].decode().split("\n") if x]
 
     def annotations(self, q):
         n = ctypes.c_size_t()

@@ -191,6 +191,15 @@ int ksg_prescore_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code, c
  * ScoreExtensions), computed on the device by the NormalizeScore the selection
  * used; valid where the node passed every filter. */
 int ksg_normalized_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int64_t* out, uint32_t n);
+/* PostFilter (wrappedplugin.go:550-577 -> store.go:442 AddPostFilterResult):
+ * DefaultPreemption's dry run for an unschedulable pod q (PodEligibleToPreemptOthers,
+ * nodesWherePreemptionMightHelp, SelectVictimsOnNode, pickOneNodeForPreemption of
+ * upstream v1.30.4 default_preemption.go / preemption.go; nothing is evicted).
+ * *nominated = the nominated global node index, -1 none; buf receives the
+ * victims as "namespace/name\n" lines (most important first).  Unsharded
+ * contexts with DefaultPreemption in the profile; queue runs stop after each
+ * pod that may preempt (ksg_schedule_queue then returns with them done). */
+int ksg_postfilter_result(ksg_ctx* ctx, uint32_t q, int32_t* nominated, char* buf, size_t cap, size_t* len);
 
 /* Scheduler-cache events between cycles (replaces the informer -> Cache path:
  * Cache.AddNode/UpdateNode/RemoveNode/AddPod/UpdatePod/RemovePod of upstream

@@ -123,6 +123,17 @@ class Engine {
   bool bound_deltas(const std::vector<std::vector<uint8_t>>& progs, const std::vector<int32_t>& gnode,
                     const std::vector<int32_t>& sign, const std::vector<int32_t>& slot, std::vector<int32_t>& rows,
                     std::string& err);
+  // DefaultPreemption dry run (host-orchestrated, SelectVictimsOnNode): pods
+  // progs[i] leave (sign -1) / re-enter (sign +1) global node gnode[i]; rows[i]
+  // is the existing-pod table row tombstoned / revived in place (-1 none).
+  bool toggle_pods(const std::vector<const std::vector<uint8_t>*>& progs, const std::vector<int32_t>& gnode,
+                   const std::vector<int32_t>& rows, int sign, std::string& err);
+  // Filter codes of program q against the current device state (its whole cycle
+  // re-run without commit; kept outputs and the pod's summary are left as they
+  // were): global node gnode's code, or every node's when gnode is -1.
+  bool dry_filter(uint32_t q, int32_t gnode, std::vector<uint32_t>& codes, std::string& err);
+  // Existing-pod table row the device appended for queue pod q (-1 none).
+  bool pod_row(uint32_t q, int32_t& row, std::string& err);
   // Cluster event applied in place: node gnode's allocatable [R] and allowed pod count.
   bool node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_t allowed, std::string& err);
   bool set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err);

@@ -187,6 +187,25 @@ __device__ __forceinline__ ProgView view(const uint8_t* p) {
   return v;
 }
 
+// Scalar-cache warm-up: every 64-B line of [p + O, p + END) is requested at
+// once by independent scalar loads, and one wait covers them all.  Without it
+// the kernel's first scalar reads of its (1.5 KB) arguments and of the pod's
+// program header arrive one dependent cache miss at a time.  Loads only (no
+// scalar stores).  The loads land in one compiler-allocated SGPR threaded
+// through every statement as an in/out operand up to the wait (warm_wait), so
+// the register holds nothing else while they are in flight.
+template <int O, int END>
+struct KWarm {
+  static __device__ __forceinline__ void run(const void* p, uint32_t& t) {
+    asm volatile("s_load_dword %0, %1, %2" : "+s"(t) : "s"(p), "i"(O));
+    KWarm<O + 64, END>::run(p, t);
+  }
+};
+template <int END>
+struct KWarm<END, END> {
+  static __device__ __forceinline__ void run(const void*, uint32_t&) {}
+};
+__device__ __forceinline__ void warm_wait(uint32_t& t) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(t)::"memory"); }
 // NodeAffinity PreScore error (an invalid preferred term; the host sets the
 // flag only when the profile has NodeAffinity): the cycle ends in Error once
 // PreScore runs, i.e. with more than one feasible node (schedule_one.go).
@@ -1482,11 +1501,22 @@ __global__ void k_x4_merge(DevOut O, const int64_t* recv, uint32_t ranks) {
 }
 
 // Reserve / Unreserve on an explicit node (the framework's selectHost choice).
+// table 2: a DefaultPreemption dry-run toggle — the pod leaves (sign -1) or
+// re-enters (+1) its node with its existing-pod table row *prow tombstoned or
+// revived in place (the table neither grows nor reorders).
 __global__ void k_assume(DevCluster C, const uint8_t* __restrict__ prog, int32_t gnode, int sign, int table, int32_t* prow) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   ProgView V = view(prog);
   uint32_t n = (uint32_t)gnode - C.goff;
   if (gnode < 0 || (uint32_t)gnode < C.goff || n >= C.N) return;
+  if (table == 2) {
+    assume_pod(C, V, n, sign, false, nullptr);
+    if (prow && *prow >= 0) {
+      if (sign < 0) C.ptflags[*prow] |= KEF_DELETED;
+      else C.ptflags[*prow] &= ~KEF_DELETED;
+    }
+    return;
+  }
   assume_pod(C, V, n, sign, table != 0, prow);
 }
 
@@ -3356,6 +3386,10 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
 template <int MODE, bool STAT>
 __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window(DevCluster C, DevProfile F, WinArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  uint32_t warm = 0;
+  KWarm<0, (int)((sizeof(DevCluster) + sizeof(DevProfile) + sizeof(WinArgs)) / 64 * 64)>::run(
+      (const void*)__builtin_amdgcn_kernarg_segment_ptr(), warm);
+  warm_wait(warm);
   if (blockIdx.x == 0) {
     if (A.nw) win_fixup<MODE, STAT>(C, F, A, *reinterpret_cast<WinLDS*>(lds_raw));
     return;
@@ -3497,6 +3531,7 @@ struct Engine::Impl {
   uint32_t pcap = 0, pkeys = 0, tcap = 0, rcap = 0, vcap = 0;
   DBuf<uint8_t> evprog;  // cluster events applied in place: the bound pod's program
   DBuf<int32_t> evrow;   // its existing-pod table row
+  DBuf<ksg_pod_summary> drysum;  // DefaultPreemption dry run: the preemptor's summary, restored after each probe
   // scratch
   DBuf<int32_t> cnt, hist_f, hist_s, ipa_aff, ipa_anti, ipa_exist, pts_min, pts_dom;
   DBuf<uint8_t> present_f, reg;
@@ -4224,6 +4259,60 @@ bool Engine::bound_deltas(const std::vector<std::vector<uint8_t>>& progs, const 
                        I.evrow.p + slot[i]);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(rows.data(), I.evrow.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
+bool Engine::toggle_pods(const std::vector<const std::vector<uint8_t>*>& progs, const std::vector<int32_t>& gnode,
+                         const std::vector<int32_t>& rows, int sign, std::string& err) {
+  Impl& I = *p_;
+  const size_t n = progs.size();
+  if (gnode.size() != n || rows.size() != n) { err = "toggle_pods: sizes"; return false; }
+  if (!n) return true;
+  std::vector<size_t> off(n);
+  std::vector<uint8_t> blob;
+  for (size_t i = 0; i < n; ++i) {
+    if (!progs[i] || progs[i]->size() < sizeof(ksg_prog)) { err = "toggle_pods: program"; return false; }
+    off[i] = (blob.size() + 255) & ~(size_t)255;
+    blob.resize(off[i]);
+    blob.insert(blob.end(), progs[i]->begin(), progs[i]->end());
+  }
+  if (!I.evprog.alloc(blob.size(), err) || !I.evrow.alloc(n, err)) return false;
+  HIPCHK(hipMemcpyAsync(I.evprog.p, blob.data(), blob.size(), hipMemcpyHostToDevice, I.stream));
+  HIPCHK(hipMemcpyAsync(I.evrow.p, rows.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, I.stream));
+  DevCluster C = I.cluster();
+  for (size_t i = 0; i < n; ++i)
+    hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, I.stream, C, I.evprog.p + off[i], gnode[i], sign, 2,
+                       I.evrow.p + i);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(I.stream));  // (the host buffers are reused by the next toggle)
+  return true;
+}
+
+bool Engine::dry_filter(uint32_t q, int32_t gnode, std::vector<uint32_t>& codes, std::string& err) {
+  Impl& I = *p_;
+  if (q >= I.prog_off.size()) { err = "program index out of range"; return false; }
+  if (gnode >= 0 && ((uint32_t)gnode < I.goff || (uint32_t)gnode - I.goff >= I.N)) { err = "dry_filter: node"; return false; }
+  if (!I.drysum.alloc(1, err)) return false;
+  HIPCHK(hipMemcpyAsync(I.drysum.p, I.sums.p + q, sizeof(ksg_pod_summary), hipMemcpyDeviceToDevice, I.stream));
+  const uint32_t kf = I.keep_first, kn = I.keep_n;
+  I.keep_n = 0;  // outputs to the scratch rows: kept outputs stay as they are
+  const bool ok = run_queue(q, 1, false, err);
+  I.keep_first = kf;
+  I.keep_n = kn;
+  if (!ok) return false;
+  codes.resize(gnode >= 0 ? 1 : I.N);
+  HIPCHK(hipMemcpyAsync(codes.data(), I.filter.p + (gnode >= 0 ? (uint32_t)gnode - I.goff : 0),
+                        codes.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, I.stream));
+  HIPCHK(hipMemcpyAsync(I.sums.p + q, I.drysum.p, sizeof(ksg_pod_summary), hipMemcpyDeviceToDevice, I.stream));
+  HIPCHK(hipStreamSynchronize(I.stream));
+  return true;
+}
+
+bool Engine::pod_row(uint32_t q, int32_t& row, std::string& err) {
+  Impl& I = *p_;
+  if (q >= I.prog_off.size()) { err = "program index out of range"; return false; }
+  HIPCHK(hipMemcpyAsync(&row, I.prow.p + q, sizeof(int32_t), hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipStreamSynchronize(I.stream));
   return true;
 }

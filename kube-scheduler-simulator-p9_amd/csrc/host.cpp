@@ -270,8 +270,36 @@ struct Pod {
   struct HostPort { string ip, proto; int32_t port; };
   vector<HostPort> ports; // Spec.Containers host ports (hostPort > 0), sanitised
   bool volume_plugins_act = false;  // a volume the volume plugins would not Skip
-  i64 priority = 0;                 // spec.priority (DefaultPreemption is modelled for equal priorities)
+  i64 priority = 0;                 // spec.priority (PrioritySort order is the caller's; DefaultPreemption)
+  bool preempt_never = false;       // spec.preemptionPolicy Never (PodEligibleToPreemptOthers)
+  i64 start_time = INT64_MAX;       // status.startTime, epoch seconds; none: started last (GetPodStartTime: now)
 };
+
+// RFC 3339 date-time -> seconds since the epoch (the date and time fields; a
+// fraction and the offset are ignored: the simulator's objects carry "Z").
+// INT64_MAX when the text is not a date-time.
+static i64 rfc3339_seconds(const string& t) {
+  int f[6] = {0, 0, 0, 0, 0, 0};
+  size_t at = 0;
+  const char sep[6] = {'-', '-', 'T', ':', ':', 0};
+  for (int k = 0; k < 6; ++k) {
+    size_t b = at;
+    while (at < t.size() && at - b < 9 && t[at] >= '0' && t[at] <= '9') f[k] = f[k] * 10 + (t[at++] - '0');
+    if (at == b) return INT64_MAX;
+    if (k < 5) {
+      if (at >= t.size() || (t[at] != sep[k] && !(k == 2 && t[at] == 't'))) return INT64_MAX;
+      ++at;
+    }
+  }
+  // days from 1970-01-01 of the proleptic Gregorian date (era arithmetic, March-based years)
+  const i64 y = (i64)f[0] - (f[1] <= 2 ? 1 : 0);
+  const i64 era = (y >= 0 ? y : y - 399) / 400;
+  const i64 yoe = y - era * 400;
+  const i64 mp = (f[1] + 9) % 12;
+  const i64 doy = (153 * mp + 2) / 5 + f[2] - 1;
+  const i64 days = era * 146097 + yoe * 365 + yoe / 4 - yoe / 100 + doy - 719468;
+  return days * 86400 + (i64)f[3] * 3600 + (i64)f[4] * 60 + f[5];
+}
 
 static RList pod_requests(const J* spec, bool nonzero) {
   auto fill = [&](RList r) {
@@ -332,6 +360,9 @@ static Pod parse_pod(const J& v) {
   if (!sp) return p;
   p.node = str_of((*sp)["nodeName"]);
   if (auto* pr = (*sp)["priority"]; pr && !pr->null()) p.priority = (i64)pr->num();
+  p.preempt_never = str_of((*sp)["preemptionPolicy"]) == "Never";
+  if (const J* st = v["status"])
+    if (const J* t = (*st)["startTime"]; t && !t->null()) p.start_time = rfc3339_seconds(str_of(t));
   for (const char* k : {"initContainers", "containers"})
     if (auto* cs = (*sp)[k])
       for (auto& c : cs->items) {
@@ -1766,15 +1797,17 @@ struct Cluster {
     return true;
   }
 
-  // DefaultPreemption's dry run is modelled for queues whose pods all share one
-  // priority (no victims can exist); other clusters are refused, not approximated.
+  // DefaultPreemption's dry run (preempt()) runs on unsharded contexts; a sharded
+  // one takes queues whose pods all share one priority (no victims can exist),
+  // other clusters are refused, not approximated.
   bool has_preemption() const {
     for (int i = 0; i < n_plugins; ++i)
       if (names[i] == "DefaultPreemption") return true;
     return false;
   }
   bool equal_priorities() {
-    if (!has_preemption()) return true;
+    prio_dirty = true;
+    if (!has_preemption() || shards == 1) return true;
     set<i64> pr;
     for (auto* v : {&bound, &queue})
       for (auto& p : *v) pr.insert(p.priority);
@@ -1892,12 +1925,14 @@ struct Cluster {
           sum[q].best_key = (sum[q].best_key & ~0xFFFFFull) | (uint64_t)(to < 0 ? 0 : to);
         }
     vector<Pod> saved = bound;
+    vector<uint32_t> as_bound;  // queue pods encoded as bound pods, in order
     for (size_t q = 0; q < nq; ++q) {
       int32_t at = placement((uint32_t)q, q < ns ? &sum[q] : nullptr);
       if (at < 0 || at >= (int32_t)nodes.size()) continue;
       Pod x = queue[q];
       x.node = nodes[at].name;
       bound.push_back(x);
+      as_bound.push_back((uint32_t)q);
     }
     nkeys = Dict(); nvals.clear(); pkeys = Dict(); pvals.clear(); nss = Dict();
     taint_id.clear(); taints.clear(); topo = Dict();
@@ -1921,6 +1956,9 @@ struct Cluster {
                        (uint32_t)(T.reqs.size() + qreqs + 8 * slack), (uint32_t)(T.vals.size() + qvals + 16 * slack), err);
     }
     bound.swap(saved);
+    qrow.assign(nq, -1);
+    if (ok && bound_row.size() == bound.size() + as_bound.size())
+      for (size_t k = 0; k < as_bound.size(); ++k) qrow[as_bound[k]] = bound_row[bound.size() + k];
     bound_row.resize(bound.size());  // placements were encoded after the bound pods
     if (!ok) return false;
     inplace_dirty = false;
@@ -1969,6 +2007,7 @@ struct Cluster {
     if (!eng->keep_outputs(q, 1, err) || !eng->run_queue(q, 1, commit, err) || !eng->sync(err) ||
         !eng->summaries(q, 1, &out, err))
       return false;
+    if (!preempt(q, out)) return false;  // PostFilter of an unschedulable pod
     if (commit && out.status == 0) {
       placed[q] = out.selected;
       assumed_in[q] = epoch;
@@ -1983,6 +2022,208 @@ struct Cluster {
     if (!eng->table_overflow(full, err)) return false;
     return full ? rebuild() : true;
   }
+  // ------------------------------------------------------------ DefaultPreemption
+  // PostFilter of an unschedulable pod, as a dry run on the device state of the
+  // pod's own cycle (v1.30.4 plugins/defaultpreemption/default_preemption.go,
+  // framework/preemption/preemption.go; the oracle's preempt() restates it):
+  // PodEligibleToPreemptOthers (preemptionPolicy Never), nodesWherePreemptionMightHelp
+  // (nodes whose Filter status is Unschedulable, not UnschedulableAndUnresolvable),
+  // SelectVictimsOnNode per such node (every lower-priority pod taken off, the
+  // pod's cycle re-run on the device, then the victims reprieved most important
+  // first while the pod still fits), pickOneNodeForPreemption.  Nothing is
+  // evicted: the device state is restored exactly (rows revived in place) and the
+  // result is the nominated node and its victims (the store's postfilter-result
+  // entry, store.go:442-458).  Deviations: every potential node is
+  // examined (upstream: a random-offset sample of max(10%, 100)), the seeded
+  // selectHost rule breaks the last tie, no PodDisruptionBudgets exist.
+  struct Nomination {
+    int32_t node = -1;        // global node index
+    vector<string> victims;   // "namespace/name"
+  };
+  vector<Nomination> nom;
+  vector<int32_t> qrow;  // queue pods the last rebuild encoded as bound pods: their table rows
+  bool prio_dirty = true;
+  i64 low_prio = INT64_MAX;
+  // Can queue pod q preempt anything (some pod of a lower priority exists)?
+  bool may_preempt(uint32_t q) {
+    if (!has_preemption() || shards != 1 || queue[q].preempt_never) return false;
+    if (prio_dirty) {
+      low_prio = INT64_MAX;
+      for (auto* v : {&bound, &queue})
+        for (auto& p : *v) low_prio = std::min(low_prio, p.priority);
+      prio_dirty = false;
+    }
+    return queue[q].priority > low_prio;
+  }
+  uint64_t tie_key(uint32_t q, uint32_t g) const {  // engine pack_key with total 0
+    uint64_t z = ecfg.seed ^ ((uint64_t)q * 0x9E3779B97F4A7C15ull) ^ (uint64_t)g;
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return ((0xFFFFFull - (z >> 44)) << 20) | (uint64_t)g;
+  }
+  bool preempt(uint32_t q, const ksg_pod_summary& S) {
+    if (nom.size() < queue.size()) nom.resize(queue.size());
+    nom[q] = Nomination();
+    if (S.status != 1 || q >= meta.size() || meta[q].prefilter_fail_pos >= 0 || !may_preempt(q)) return true;
+    const Pod& p = queue[q];
+    const uint32_t n = hi - lo;
+    PodOutputs o;
+    o.summary = S;
+    if (!refresh_program(q) || !eng->dry_filter(q, -1, o.filter, err)) return false;
+    // victims' candidates per potential node: bound pods, then assumed queue pods
+    struct Vic {
+      int32_t bound = -1, qpod = -1;
+      i64 prio, start;
+      uint64_t order;  // load order (MoreImportantPod's last tie, as the oracle's)
+    };
+    vector<int32_t> potential;
+    vector<char> is_pot(n, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t c = o.filter[i];
+      if (c == KSG_FILTER_PASS || c >= KSG_FILTER_NOT_EVALUATED || (c >> 24) >= (uint32_t)n_dev) continue;
+      string msg;
+      if (filter_status(q, fpos[c >> 24], i, o, msg) == C_UNSCHED) {
+        potential.push_back((int32_t)i);
+        is_pot[i] = 1;
+      }
+    }
+    if (potential.empty()) return true;
+    vector<vector<Vic>> on(n);
+    for (size_t b = 0; b < bound.size(); ++b) {
+      const int32_t g = node_names.get(bound[b].node);
+      if (g < 0 || !is_pot[g] || bound[b].priority >= p.priority) continue;
+      on[g].push_back({(int32_t)b, -1, bound[b].priority, bound[b].start_time, (uint64_t)b});
+    }
+    vector<ksg_pod_summary> sum(progs.size());
+    if (!sum.empty() && !eng->summaries(0, (uint32_t)sum.size(), sum.data(), err)) return false;
+    for (uint32_t j = 0; j < queue.size() && j < progs.size(); ++j) {
+      if (j == q || queue[j].priority >= p.priority) continue;
+      const int32_t g = placement(j, &sum[j]);
+      if (g < 0 || g >= (int32_t)n || !is_pot[g]) continue;
+      on[g].push_back({-1, (int32_t)j, queue[j].priority, queue[j].start_time, (uint64_t)bound.size() + j});
+    }
+    // programs and table rows of every candidate victim (classes they bring: tables built)
+    std::map<int32_t, vector<uint8_t>> bprog;
+    std::map<int32_t, int32_t> qrows;
+    for (int32_t g : potential)
+      for (auto& v : on[g]) {
+        if (v.bound >= 0) {
+          PodMeta m;
+          if (!compile(bound[v.bound], 0, bprog[v.bound], m)) return false;
+        } else {
+          int32_t row = -1;
+          if (tables_on()) {
+            if (assumed_in[v.qpod] == epoch) {
+              if (!eng->pod_row((uint32_t)v.qpod, row, err)) return false;
+            } else if ((size_t)v.qpod < qrow.size()) {
+              row = qrow[v.qpod];
+            }
+          }
+          qrows[v.qpod] = row;
+        }
+      }
+    if (!sync_classes() || !refresh_program(q)) return false;
+    for (auto& kv : qrows)
+      if (!refresh_program((uint32_t)kv.first)) return false;
+    auto toggle = [&](const vector<Vic>& vs, int32_t g, int sign) {
+      vector<const vector<uint8_t>*> pp;
+      vector<int32_t> gn, rows;
+      for (auto& v : vs) {
+        pp.push_back(v.bound >= 0 ? &bprog[v.bound] : &progs[v.qpod]);
+        gn.push_back(g + (int32_t)lo);
+        rows.push_back(v.bound >= 0 ? (tables_on() ? bound_row[v.bound] : -1) : qrows[v.qpod]);
+      }
+      return eng->toggle_pods(pp, gn, rows, sign, err);
+    };
+    vector<uint32_t> code;
+    auto fits = [&](int32_t g, bool& ok) {
+      if (!eng->dry_filter(q, g + (int32_t)lo, code, err)) return false;
+      ok = code[0] == KSG_FILTER_PASS;
+      return true;
+    };
+    struct Cand {
+      int32_t node;
+      vector<Vic> victims;
+    };
+    vector<Cand> cands;
+    for (int32_t g : potential) {
+      vector<Vic>& pv = on[g];
+      if (pv.empty()) continue;  // "No preemption victims found for incoming pod"
+      bool ok = false;
+      if (!toggle(pv, g, -1) || !fits(g, ok)) return false;
+      if (!ok) {
+        if (!toggle(pv, g, +1)) return false;
+        continue;
+      }
+      std::sort(pv.begin(), pv.end(), [](const Vic& a, const Vic& b) {  // util.MoreImportantPod
+        if (a.prio != b.prio) return a.prio > b.prio;
+        if (a.start != b.start) return a.start < b.start;
+        return a.order < b.order;
+      });
+      Cand c{g, {}};
+      for (auto& v : pv) {  // reprieve: most important first
+        if (!toggle({v}, g, +1) || !fits(g, ok)) return false;
+        if (!ok) {
+          if (!toggle({v}, g, -1)) return false;
+          c.victims.push_back(v);
+        }
+      }
+      if (!toggle(c.victims, g, +1)) return false;  // the dry run leaves the state as it was
+      if (!c.victims.empty()) cands.push_back(std::move(c));
+    }
+    if (cands.empty()) return true;
+    // pickOneNodeForPreemption: fewest PDB violations (none here), lowest highest
+    // victim priority, lowest sum of (priority + 2^31), fewest victims, latest
+    // earliest start among the highest-priority victims; then the seeded rule
+    auto crit = [](const Cand& c, int f) -> i64 {
+      const vector<Vic>& v = c.victims;  // most important first
+      if (f == 0) return -v[0].prio;
+      if (f == 1) {
+        i64 t = 0;
+        for (auto& x : v) t += x.prio + ((i64)1 << 31);
+        return -t;
+      }
+      if (f == 2) return -(i64)v.size();
+      i64 e = v[0].start;
+      for (auto& x : v)
+        if (x.prio == v[0].prio) e = std::min(e, x.start);
+      return e;
+    };
+    vector<size_t> keep(cands.size());
+    for (size_t i = 0; i < keep.size(); ++i) keep[i] = i;
+    for (int f = 0; f < 4 && keep.size() > 1; ++f) {
+      i64 best = INT64_MIN;
+      for (size_t i : keep) best = std::max(best, crit(cands[i], f));
+      vector<size_t> next;
+      for (size_t i : keep)
+        if (crit(cands[i], f) == best) next.push_back(i);
+      keep.swap(next);
+    }
+    size_t pick = keep[0];
+    for (size_t i : keep)
+      if (tie_key(q, cands[i].node + lo) > tie_key(q, cands[pick].node + lo)) pick = i;
+    Nomination& r = nom[q];
+    r.node = cands[pick].node + (int32_t)lo;
+    for (auto& v : cands[pick].victims) {
+      const Pod& x = v.bound >= 0 ? bound[v.bound] : queue[v.qpod];
+      r.victims.push_back(x.ns + "/" + x.name);
+    }
+    return true;
+  }
+
+  // The device went back to the last upload (ksg_reset): pods it assumed since
+  // are no longer placed (their results stay).
+  void forget_epoch() {
+    track_queue();
+    for (size_t q = 0; q < queue.size(); ++q)
+      if (assumed_in[q] == epoch && qmode[q] != 0) {
+        if (qmode[q] == 1) qmode[q] = 0;
+        placed[q] = -1;
+      }
+  }
+
   bool reserve(uint32_t q, int32_t node) {
     track_queue();
     if (q >= queue.size() || qmode[q] != 2 || placed[q] >= 0) { err = "reserve: pod not in an uncommitted cycle"; return false; }
@@ -2028,6 +2269,7 @@ struct Cluster {
     struct Op { bool add; Pod pod; vector<uint8_t> blob; string key; int32_t node = -1; Node nd; int32_t qpod = -1, qat = -1; };
     auto pkey = [](const string& ns, const string& name) { return ns + '\x1f' + name; };
     track_queue();
+    prio_dirty = true;
     if (!bound_at_valid) {
       bound_at.clear();
       for (size_t i = 0; i < bound.size(); ++i) bound_at[pkey(bound[i].ns, bound[i].name)] = (uint32_t)i;
@@ -2037,8 +2279,8 @@ struct Cluster {
     std::unordered_set<string> added, removed;  // the batch on top of bound_at, simulated
     std::set<int32_t> gone_q;                    // scheduled queue pods the batch deletes
     auto present = [&](const string& k) { return added.count(k) || (bound_at.count(k) && !removed.count(k)); };
-    std::set<i64> prios;
-    if (has_preemption())
+    std::set<i64> prios;  // a sharded context keeps one priority (equal_priorities)
+    if (has_preemption() && shards != 1)
       for (auto* v : {&bound, &queue})
         for (auto& p : *v) prios.insert(p.priority);
     for (auto& e : ev.items) {
@@ -2050,7 +2292,7 @@ struct Cluster {
         string k = pkey(p.ns, p.name);
         if (present(k)) return 0;
         if (queue_find(p.ns, p.name) >= 0) return 0;
-        if (has_preemption()) {
+        if (has_preemption() && shards != 1) {
           prios.insert(p.priority);
           if (prios.size() > 1) return 0;
         }
@@ -2385,6 +2627,7 @@ struct Cluster {
         return m;
       }
       case P_TAINT: {
+        if (detail >= taints.size()) return "node(s) had untolerated taint";  // (not a device code)
         const Taint& t = taints[detail];
         return "node(s) had untolerated taint {" + t.key + ": " + t.value + "}";
       }
@@ -2593,18 +2836,27 @@ struct Cluster {
       }
     }
     string sel = S.status == 0 && S.selected >= 0 ? nodes[S.selected].name : "";
-    string post = "{}";  // DefaultPreemption, equal priorities: every node recorded, none nominated (oracle finish())
+    // PostFilter: DefaultPreemption records every node of the status map (all of
+    // them), the nominated one with PostFilterNominatedMessage (store.go:442-458)
+    string post = "{}";
     if (S.status == 1)
       for (int pos = 0; pos < n_plugins; ++pos)
         if (names[pos] == "DefaultPreemption") {
-          vector<string> nn;  // encoding/json: map keys sorted
-          for (uint32_t i = 0; i < n; ++i) nn.push_back(nodes[lo + i].name);
+          const int32_t nominated = q < nom.size() ? nom[q].node : -1;
+          vector<std::pair<string, bool>> nn;  // encoding/json: map keys sorted
+          for (uint32_t i = 0; i < n; ++i) nn.push_back({nodes[lo + i].name, (int32_t)(lo + i) == nominated});
           std::sort(nn.begin(), nn.end());
           post = "{";
           for (size_t i = 0; i < nn.size(); ++i) {
             if (i) post += ',';
-            jstr(post, nn[i]);
-            post += ":{}";
+            jstr(post, nn[i].first);
+            if (!nn[i].second) {
+              post += ":{}";
+              continue;
+            }
+            post += ":{";
+            jstr(post, names[pos]);
+            post += ":\"preemption victim\"}";
           }
           post += "}";
         }
@@ -2745,8 +2997,25 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
     if (!c.table_fits(need, fits)) return ctx->fail(c.err, KSG_E_DEVICE);
     if (!fits && !c.rebuild()) return ctx->fail(c.err, KSG_E_DEVICE);  // fresh capacity, placements kept
   }
-  if (!c.eng->run_queue(first, count, true, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
-  c.mark_run(first, count);
+  // Pods that may preempt end a segment: the run stops after each, and an
+  // unschedulable one gets its DefaultPreemption dry run on the state of its own
+  // cycle (Cluster::preempt); the call then returns with those segments done.
+  if (c.nom.size() < c.queue.size()) c.nom.resize(c.queue.size());
+  uint32_t j = first;
+  for (uint32_t q = first; q < first + count; ++q) {
+    c.nom[q] = Cluster::Nomination();
+    if (!c.may_preempt(q)) continue;
+    ksg_pod_summary S;
+    if (!c.eng->run_queue(j, q + 1 - j, true, c.err) || !c.eng->sync(c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
+    c.mark_run(j, q + 1 - j);
+    if (!c.eng->summaries(q, 1, &S, c.err) || !c.preempt(q, S)) return ctx->fail(c.err, KSG_E_DEVICE);
+    if (!c.refresh_programs(q + 1, first + count - q - 1)) return ctx->fail(c.err, KSG_E_DEVICE);
+    j = q + 1;
+  }
+  if (j < first + count) {
+    if (!c.eng->run_queue(j, first + count - j, true, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
+    c.mark_run(j, first + count - j);
+  }
   return KSG_OK;
 }
 
@@ -2841,6 +3110,7 @@ int ksg_reset(ksg_ctx* ctx) {
     return ctx->fail("reset after in-place cluster events: reload the cluster (ksg_load_cluster)", KSG_E_STATE);
   if (!ctx->c.compile_queue()) return ctx->fail(ctx->c.err, KSG_E_INVALID);
   if (!ctx->c.eng->reset(ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
+  ctx->c.forget_epoch();
   return KSG_OK;
 }
 
@@ -3001,6 +3271,19 @@ int ksg_prefilter_result(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t
       Cluster::jstr(s, c.meta[q].prefilter_names[i]);
     }
     s += "]";
+  }
+  return put_str(ctx, s, buf, cap, len);
+}
+
+int ksg_postfilter_result(ksg_ctx* ctx, uint32_t q, int32_t* nominated, char* buf, size_t cap, size_t* len) {
+  KSG_GUARD(ctx);
+  Cluster& c = ctx->c;
+  if (!nominated || q >= c.queue.size()) return ctx->fail("postfilter_result: range", KSG_E_RANGE);
+  *nominated = -1;
+  std::string s;
+  if (q < c.nom.size()) {
+    *nominated = c.nom[q].node;
+    for (auto& v : c.nom[q].victims) s += v + "\n";
   }
   return put_str(ctx, s, buf, cap, len);
 }

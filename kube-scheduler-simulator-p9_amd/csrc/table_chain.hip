@@ -33,22 +33,6 @@ struct ChainVids {
   __device__ __forceinline__ int32_t operator()(int s) const { return base[s * kChain]; }
 };
 
-// Scalar-cache warm-up: every 64-B line of [p + O, p + END) is requested at
-// once by independent scalar loads, and one wait covers them all.  Without it
-// the kernel's first scalar reads of its (1.5 KB) arguments and of the pod's
-// program header arrive one dependent cache miss at a time.  Loads only (no
-// scalar stores); the destination register is clobbered and drained here.
-template <int O, int END>
-struct KWarm {
-  static __device__ __forceinline__ void run(const void* p) {
-    asm volatile("s_load_dword s101, %0, %1" ::"s"(p), "i"(O) : "s101");
-    KWarm<O + 64, END>::run(p);
-  }
-};
-template <int END>
-struct KWarm<END, END> {
-  static __device__ __forceinline__ void run(const void*) {}
-};
 struct ChainArgs {
   const uint8_t* progs;
   const uint64_t* prog_off;
@@ -97,9 +81,10 @@ enum { KCP_FEAS = 0, KCP_IGN = 1, KCP_STAT = 2, KCP_IPAF = 3, KCP_I = 4 };
 constexpr int kArgBytes = (int)((sizeof(DevCluster) + sizeof(DevProfile) + sizeof(ChainArgs)) / 64 * 64);
 constexpr int kHdrBytes = (int)(sizeof(ksg_prog) / 64 * 64);
 __device__ __forceinline__ void chain_warm(const uint8_t* prog) {
-  KWarm<0, kArgBytes>::run((const void*)__builtin_amdgcn_kernarg_segment_ptr());
-  KWarm<0, kHdrBytes>::run(prog);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  uint32_t warm = 0;
+  KWarm<0, kArgBytes>::run((const void*)__builtin_amdgcn_kernarg_segment_ptr(), warm);
+  KWarm<0, kHdrBytes>::run(prog, warm);
+  warm_wait(warm);
 }  // KCP_IPAF: block 0 only
 enum { KCX_TAINT = 0, KCX_NA = 1, KCX_PTS = 2, KCX_IPA = 3, KCP_X = 4 };
 __device__ __forceinline__ int chain_x(int plugin) {

@@ -26,6 +26,13 @@ Variants (each a small seeded cluster, same document shape as ``generator``):
   in several namespaces.
 * ``ipa_ignore`` the ``ipa`` cluster with ignorePreferredTermsOfExistingPods and
   hardPodAffinityWeight 0.
+* ``preempt``   DefaultPreemption: a nearly full cluster of bound pods at mixed
+  priorities (status.startTime set on most of them), queue pods at mixed
+  priorities (some preemptionPolicy Never), host ports, pod-count limits,
+  spread constraints, required anti-affinity, taints and node selectors, so that
+  unschedulable pods meet both Unschedulable nodes (preemption may help) and
+  UnschedulableAndUnresolvable ones.  The queue is in the order given (no
+  PrioritySort): earlier queue pods can be victims of later ones.
 """
 from __future__ import annotations
 
@@ -36,7 +43,7 @@ from .generator import (HOSTNAME, ZONE, Gi, Mi, Rng, make_profile, node_obj, pod
 GPU = "example.com/gpu"
 EPH = "ephemeral-storage"
 NAMESPACES = ["default", "ns-a", "ns-b", "team-x"]
-EDGE_VARIANTS = ("fit_most", "fit_rtc", "na", "pts", "ipa", "ipa_ignore")
+EDGE_VARIANTS = ("fit_most", "fit_rtc", "na", "pts", "ipa", "ipa_ignore", "preempt")
 
 
 def edge_seed(variant: str) -> int:
@@ -347,6 +354,67 @@ def gen_ipa(variant="ipa", n_nodes=60, n_existing=150, n_pods=140, seed=None):
     return {"profile": prof, "nodes": nodes, "pods": bound, "queue": queue}
 
 
+PRIORITIES = [0, 0, 10, 100, 1000]
+PORT = {"containerPort": 8080, "hostPort": 8080, "protocol": "TCP"}
+
+
+def _start(r):
+    if r.pct() < 12:
+        return None  # no status.startTime: started last
+    return f"2025-01-{1 + r.below(28):02d}T{r.below(24):02d}:{r.pick([0, 30]):02d}:00Z"
+
+
+def gen_preempt(n_nodes=24, n_existing=120, n_pods=90, seed=None):
+    seed = edge_seed("preempt") if seed is None else seed
+    r = Rng(seed)
+    nodes = []
+    for i in range(n_nodes):
+        labels = {}
+        if r.pct() < 85:
+            labels[ZONE] = f"zone-{r.below(3)}"
+        if r.pct() < 60:
+            labels["disk"] = r.pick(["ssd", "hdd"])
+        tl = [dict(NA_TAINTS[0])] if r.pct() < 12 else []
+        nodes.append(node_obj(f"node-{i:07d}", 1000 * r.pick([4, 8]), Gi * r.pick([16, 32]),
+                              pods=r.pick([110, 110, 110, 6]), labels=labels, taints=tl))
+    bound = []
+    for e in range(n_existing):
+        spec = {"priority": r.pick(PRIORITIES)}
+        if r.pct() < 8:
+            spec["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": _sel(r), "topologyKey": HOSTNAME}]}}
+        p = pod_obj(f"ex-{e:07d}", [req(250 * (1 + r.below(8)), 512 * Mi * (1 + r.below(6)))], labels=_labels(r),
+                    node=nodes[r.below(n_nodes)]["metadata"]["name"], ns=r.pick(NAMESPACES),
+                    ports={0: [dict(PORT)]} if r.pct() < 10 else None, **spec)
+        st = _start(r)
+        if st:
+            p["status"] = {"startTime": st}
+        bound.append(p)
+    queue = []
+    for j in range(n_pods):
+        spec = {"priority": r.pick(PRIORITIES + [5000, 5000])}
+        if r.pct() < 15:
+            spec["preemptionPolicy"] = "Never"
+        if r.pct() < 20:
+            spec["topologySpreadConstraints"] = [{
+                "maxSkew": 1, "topologyKey": r.pick([ZONE, HOSTNAME, "disk"]), "whenUnsatisfiable": "DoNotSchedule",
+                "labelSelector": _sel(r)}]
+        if r.pct() < 15:
+            spec["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": _sel(r), "topologyKey": HOSTNAME}]}}
+        if r.pct() < 15:
+            spec["tolerations"] = [{"key": "dedicated", "operator": "Exists"}]
+        if r.pct() < 10:
+            spec["nodeSelector"] = {"disk": r.pick(["ssd", "hdd"])}
+        cpu = 500 * (1 + r.below(8)) if r.pct() < 90 else 10000  # 10 cores: above every allocatable
+        queue.append(pod_obj(f"pod-{j:07d}", [req(cpu, 512 * Mi * (1 + r.below(10)))], labels=_labels(r),
+                             ns=r.pick(NAMESPACES), ports={0: [dict(PORT)]} if r.pct() < 12 else None, **spec))
+    prof = make_profile([("TaintToleration", 3), ("NodeAffinity", 2), ("NodePorts", 1), ("NodeResourcesFit", 1),
+                         ("PodTopologySpread", 2), ("InterPodAffinity", 2), ("DefaultPreemption", 1),
+                         ("NodeResourcesBalancedAllocation", 1)], seed)
+    return {"profile": prof, "nodes": nodes, "pods": bound, "queue": queue}
+
+
 def generate_edge(variant: str, **sizes) -> dict:
     if variant in ("fit_most", "fit_rtc"):
         return gen_fit(variant, **sizes)
@@ -356,6 +424,8 @@ def generate_edge(variant: str, **sizes) -> dict:
         return gen_pts(**sizes)
     if variant in ("ipa", "ipa_ignore"):
         return gen_ipa(variant, **sizes)
+    if variant == "preempt":
+        return gen_preempt(**sizes)
     raise ValueError(variant)
 
 

@@ -81,6 +81,7 @@ def load_library():
     L.ksg_node_index.argtypes = [vp, cp, sz]
     L.ksg_prefilter_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_prefilter_result.argtypes = [vp, u32, cp, sz, ctypes.POINTER(sz)]
+    L.ksg_postfilter_result.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_int32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_filter_status.argtypes = [vp, u32, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_prescore_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_normalized_scores.argtypes = [vp, u32, u32, ctypes.POINTER(i64), u32]
@@ -263,6 +264,15 @@ class Scheduler:
         buf = ctypes.create_string_buffer(n.value + 1)
         self._chk(self.L.ksg_prefilter_result(self.h, q, buf, n.value + 1, ctypes.byref(n)), "ksg_prefilter_result")
         return json.loads(buf.raw[:n.value].decode())
+
+    def postfilter_result(self, q):
+        """DefaultPreemption dry run of pod q: (nominated global node index or -1, ["ns/name", ...] victims)."""
+        n, node = ctypes.c_size_t(), ctypes.c_int32()
+        self.L.ksg_postfilter_result(self.h, q, ctypes.byref(node), None, 0, ctypes.byref(n))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._chk(self.L.ksg_postfilter_result(self.h, q, ctypes.byref(node), buf, n.value + 1, ctypes.byref(n)),
+                  "ksg_postfilter_result")
+        return node.value, [x for x in buf.raw[:n.value].decode().split("\n") if x]
 
     def filter_status(self, q, pos, node):
         """(framework.Code, Status.Message()) of Filter on a node; code -1: not called."""

@@ -1239,24 +1239,39 @@ struct Cluster {
     const NodeInfo& n = infos[ni];
     const Resource& a = nodes[ni].alloc;
     vector<string> reasons;
+    bool unres = false;
     if ((i64)n.pods.size() + 1 > a.allowed_pods) reasons.push_back("Too many pods");
     bool any_scalar = false;
     for (auto& kv : pr.scalar) any_scalar = true, (void)kv;
     if (pr.milli_cpu == 0 && pr.memory == 0 && pr.eph == 0 && !any_scalar) goto done;
-    if (pr.milli_cpu > 0 && pr.milli_cpu > a.milli_cpu - n.requested.milli_cpu) reasons.push_back("Insufficient cpu");
-    if (pr.memory > 0 && pr.memory > a.memory - n.requested.memory) reasons.push_back("Insufficient memory");
-    if (pr.eph > 0 && pr.eph > a.eph - n.requested.eph) reasons.push_back("Insufficient ephemeral-storage");
+    // InsufficientResource.Unresolvable: the request exceeds the allocatable itself
+    // (the Filter then returns UnschedulableAndUnresolvable; preemption cannot help)
+    if (pr.milli_cpu > 0 && pr.milli_cpu > a.milli_cpu - n.requested.milli_cpu) {
+      reasons.push_back("Insufficient cpu");
+      unres |= pr.milli_cpu > a.milli_cpu;
+    }
+    if (pr.memory > 0 && pr.memory > a.memory - n.requested.memory) {
+      reasons.push_back("Insufficient memory");
+      unres |= pr.memory > a.memory;
+    }
+    if (pr.eph > 0 && pr.eph > a.eph - n.requested.eph) {
+      reasons.push_back("Insufficient ephemeral-storage");
+      unres |= pr.eph > a.eph;
+    }
     for (auto& kv : pr.scalar) {  // map order upstream; sorted here
       if (kv.second == 0) continue;
       i64 al = a.scalar.count(kv.first) ? a.scalar.at(kv.first) : 0;
       i64 rq = n.requested.scalar.count(kv.first) ? n.requested.scalar.at(kv.first) : 0;
-      if (kv.second > al - rq) reasons.push_back("Insufficient " + kv.first);
+      if (kv.second > al - rq) {
+        reasons.push_back("Insufficient " + kv.first);
+        unres |= kv.second > al;
+      }
     }
   done:
     if (reasons.empty()) return {};
     string m;
     for (size_t i = 0; i < reasons.size(); ++i) m += (i ? ", " : "") + reasons[i];
-    return {Status::Unschedulable, m};
+    return {unres ? Status::UnschedulableAndUnresolvable : Status::Unschedulable, m};
   }
   // resourceAllocationScorer.calculatePodResourceRequest
   static i64 pod_res_request(const Pod& p, const string& name, bool use_requested) {
@@ -2168,17 +2183,8 @@ static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
     }
   if (auto* q = d.get("queue"))
     for (auto& p : q->arr) c.queue.push_back(add(p));
-  bool vol = false, preempt = false;
+  bool vol = false;
   for (PluginId id : c.profile) vol |= id == P_VOLUME || id == P_VOLBIND;
-  for (auto& n : c.profile_names) preempt |= n == "DefaultPreemption";
-  if (preempt) {
-    set<i64> pr;
-    for (auto& r : c.pods) pr.insert(r.pod.priority);
-    if (pr.size() > 1) {
-      err = "pods of different priorities: DefaultPreemption victims are not modelled";
-      return false;
-    }
-  }
   if (vol)
     for (int qi : c.queue)
       if (c.pods[qi].pod.volume_plugins_act) {

@@ -44,6 +44,9 @@ static void exercise(ksg_ctx* c) {
     ksg_annotations(c, (uint32_t)q, buf.data(), buf.size(), &len);
     ksg_annotations(c, (uint32_t)q, nullptr, 0, &len);
     ksg_prefilter_result(c, (uint32_t)q, buf.data(), buf.size(), &len);
+    int32_t nominated = -1;
+    ksg_postfilter_result(c, (uint32_t)q, &nominated, buf.data(), buf.size(), &len);
+    ksg_postfilter_result(c, (uint32_t)q, &nominated, nullptr, 0, &len);
     if (nn > 0) {
       ksg_filter_codes(c, (uint32_t)q, codes.data(), (uint32_t)nn);
       for (uint32_t pos = 0; pos < 24; ++pos) {

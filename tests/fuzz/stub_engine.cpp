@@ -108,6 +108,37 @@ bool Engine::bound_deltas(const std::vector<std::vector<uint8_t>>& progs, const 
   }
   return true;
 }
+bool Engine::toggle_pods(const std::vector<const std::vector<uint8_t>*>& progs, const std::vector<int32_t>& gnode,
+                         const std::vector<int32_t>& rows, int sign, std::string& err) {
+  if (gnode.size() != progs.size() || rows.size() != progs.size() || (sign != 1 && sign != -1)) {
+    err = "stub: toggle";
+    return false;
+  }
+  for (size_t i = 0; i < progs.size(); ++i) {
+    if (!progs[i] || !check_prog(*progs[i], err)) return false;
+    if (gnode[i] < 0 || (uint32_t)gnode[i] >= p_->N) { err = "stub: toggle node"; return false; }
+  }
+  return true;
+}
+// Filter codes that walk the host's preemption paths: every node fails the
+// device position (i mod n) with detail 1; single-node probes pass on odd nodes.
+bool Engine::dry_filter(uint32_t q, int32_t gnode, std::vector<uint32_t>& codes, std::string& err) {
+  if (q >= p_->progs.size()) { err = "stub: dry_filter range"; return false; }
+  if (gnode >= (int32_t)p_->N) { err = "stub: dry_filter node"; return false; }
+  const uint32_t nd = p_->cfg.n_plugins > 0 ? (uint32_t)p_->cfg.n_plugins : 1;
+  if (gnode >= 0) {
+    codes.assign(1, (gnode & 1) ? KSG_FILTER_PASS : ((uint32_t)(gnode % nd) << 24) | 1u);
+    return true;
+  }
+  codes.resize(p_->N);
+  for (uint32_t i = 0; i < p_->N; ++i) codes[i] = ((i % nd) << 24) | 1u;
+  return true;
+}
+bool Engine::pod_row(uint32_t q, int32_t& row, std::string& err) {
+  if (q >= p_->progs.size()) { err = "stub: pod_row range"; return false; }
+  row = -1;
+  return true;
+}
 bool Engine::node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_t, std::string& err) {
   if (gnode < 0 || alloc.size() < p_->R) { err = "stub: node_alloc"; return false; }
   return true;

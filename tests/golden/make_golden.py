@@ -84,6 +84,7 @@ EDGE = {
     "edge_pts_small": ("pts", dict(n_nodes=16, n_existing=30, n_pods=24)),
     "edge_ipa_small": ("ipa", dict(n_nodes=14, n_existing=30, n_pods=24)),
     "edge_ipa_ignore_small": ("ipa_ignore", dict(n_nodes=14, n_existing=30, n_pods=24)),
+    "edge_preempt_small": ("preempt", dict(n_nodes=10, n_existing=40, n_pods=30)),
 }
 
 
@@ -93,7 +94,11 @@ def expected(doc):
     pods = []
     for q in range(o.n_queue):
         sel, feas, st = o.result(q)
-        pods.append({"selected": sel, "feasible": feas, "status": st, "annotations": o.annotations(q)})
+        e = {"selected": sel, "feasible": feas, "status": st, "annotations": o.annotations(q)}
+        node, victims = o.nominated(q)
+        if node >= 0:  # DefaultPreemption dry run (pods of mixed priorities)
+            e["nominated"] = {"node": node, "victims": victims}
+        pods.append(e)
     return pods
 
 

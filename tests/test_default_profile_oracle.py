@@ -98,9 +98,28 @@ def test_unschedulable_nodename_and_skip_records():
     assert _ann(o, 1, "bind-result") == {}
 
 
-def test_mixed_priorities_refused():
-    import pytest
-    nodes = [g.node_obj("n0", 4000, 8 * g.Gi)]
-    q = [g.pod_obj("a", [g.req(100, Mi)]), g.pod_obj("b", [g.req(100, Mi)], priority=1000)]
-    with pytest.raises(ValueError):
-        Oracle(_doc(nodes, q))
+def test_preemption_known_answers():
+    """DefaultPreemption dry run by hand (default_preemption.go / preemption.go v1.30.4):
+    SelectVictimsOnNode removes every lower-priority pod, then reprieves the most
+    important first; pickOneNodeForPreemption prefers the node whose highest
+    victim priority is lowest; preemptionPolicy Never and requests above the
+    allocatable (UnschedulableAndUnresolvable) nominate nothing."""
+    nodes = [g.node_obj("a", 4000, 8 * g.Gi), g.node_obj("b", 4000, 8 * g.Gi)]
+    bound = [g.pod_obj("low", [g.req(3000, Mi)], node="a", priority=0),
+             g.pod_obj("mid", [g.req(500, Mi)], node="a", priority=100),
+             g.pod_obj("b-mid", [g.req(3500, Mi)], node="b", priority=100)]
+    bound[0]["status"] = {"startTime": "2025-01-02T00:00:00Z"}
+    q = [g.pod_obj("hi", [g.req(2000, Mi)], priority=1000),
+         g.pod_obj("never", [g.req(2000, Mi)], priority=1000, preemptionPolicy="Never"),
+         g.pod_obj("huge", [g.req(5000, Mi)], priority=1000)]
+    prof = g.make_profile([("NodeResourcesFit", 1), ("DefaultPreemption", 1)], 7)
+    o = Oracle({"profile": prof, "nodes": nodes, "pods": bound, "queue": q})
+    o.schedule(record=3)
+    assert [o.result(i)[2] for i in range(3)] == [1, 1, 1]
+    # node a: remove low+mid, fits; reprieve mid (2.5 <= 4 cpu), low stays a victim (5.5 > 4)
+    # node b: victim b-mid (priority 100) -> a wins on the lowest highest victim priority
+    assert o.nominated(0) == (0, ["default/low"])
+    assert _ann(o, 0, "postfilter-result") == {"a": {"DefaultPreemption": "preemption victim"}, "b": {}}
+    assert o.nominated(1) == (-1, [])  # preemptionPolicy Never
+    assert o.nominated(2) == (-1, [])  # 5 cpu > allocatable 4: UnschedulableAndUnresolvable everywhere
+    assert _ann(o, 2, "postfilter-result") == {"a": {}, "b": {}}

@@ -86,6 +86,8 @@ def test_oracle_reproduces_golden(path):
     for q, e in enumerate(d["expected"]):
         assert o.result(q) == (e["selected"], e["feasible"], e["status"]), q
         assert o.annotations(q) == e["annotations"], q
+        n = e.get("nominated")
+        assert o.nominated(q) == ((n["node"], n["victims"]) if n else (-1, [])), q
 
 
 def test_golden_families_match_generator():
@@ -95,7 +97,7 @@ def test_golden_families_match_generator():
         assert g.generate(d["config"], **d["sizes"]) == d["cluster"], name
     from ksg import edge
     for name in ("edge_fit_most_small", "edge_fit_rtc_small", "edge_na_small", "edge_pts_small", "edge_ipa_small",
-                 "edge_ipa_ignore_small"):
+                 "edge_ipa_ignore_small", "edge_preempt_small"):
         d = fixture(name)
         assert edge.generate_edge(d["edge"], **d["sizes"]) == d["cluster"], name
 

@@ -91,9 +91,15 @@ def rebuild(s, q, prof, names, status):
             code, msg = s.prescore_status(q, pos)
             if code != C_NOT_RUN:
                 pre_score[name] = "success" if code == C_SUCCESS else msg
+    post = {}  # PostFilter: DefaultPreemption records every node, the nominated one with its message
+    if status == 1 and "DefaultPreemption" in plugins:
+        post = {nm: {} for nm in names}
+        node, _victims = s.postfilter_result(q)
+        if node >= 0:
+            post[names[node]] = {"DefaultPreemption": "preemption victim"}
     return {P + "prefilter-result-status": _js(pre_status), P + "prefilter-result": _js(pre_result),
             P + "filter-result": _js(filt), P + "prescore-result": _js(pre_score),
-            P + "score-result": _js(score), P + "finalscore-result": _js(fin)}
+            P + "score-result": _js(score), P + "finalscore-result": _js(fin), P + "postfilter-result": _js(post)}
 
 
 @pytest.mark.gpu

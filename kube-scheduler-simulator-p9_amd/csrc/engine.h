@@ -139,6 +139,10 @@ class Engine {
   bool set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err);
   // An assume found the existing-pod table full (the pod was not appended).
   bool table_overflow(bool& overflow, std::string& err);
+  // Grow the existing-pod table in place (contents kept): row / term / req / val
+  // capacities and the pod-label key count (new keys' columns read "no label").
+  bool grow_table(uint32_t pod_cap, uint32_t term_cap, uint32_t req_cap, uint32_t val_cap, uint32_t n_keys,
+                  std::string& err);
   // Existing-pod table entries in use and capacity: rows, terms, reqs, vals.
   bool table_room(uint32_t used[4], uint32_t cap[4], std::string& err);
   // Class tables: append pod / term classes and build their tables from the

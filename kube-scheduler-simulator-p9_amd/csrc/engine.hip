@@ -4329,6 +4329,43 @@ bool Engine::node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_
   return true;
 }
 
+bool Engine::grow_table(uint32_t pod_cap, uint32_t term_cap, uint32_t req_cap, uint32_t val_cap, uint32_t n_keys,
+                        std::string& err) {
+  Impl& I = *p_;
+  hipStream_t s = I.stream;
+  pod_cap = std::max(pod_cap, I.pcap);
+  term_cap = std::max(term_cap, I.tcap);
+  req_cap = std::max(req_cap, I.rcap);
+  val_cap = std::max(val_cap, I.vcap);
+  n_keys = std::max(n_keys, I.pkeys);
+  HIPCHK(hipStreamSynchronize(s));
+  if (pod_cap != I.pcap || n_keys != I.pkeys) {
+    if (!I.ptnode.grow(pod_cap, I.pcap, s, err) || !I.ptns.grow(pod_cap, I.pcap, s, err) ||
+        !I.ptflags.grow(pod_cap, I.pcap, s, err))
+      return false;
+    // label columns [key][row]: re-laid at the new row stride; new keys' columns -1 (no label)
+    DBuf<int32_t> lab;
+    if (!lab.alloc((size_t)pod_cap * std::max<uint32_t>(n_keys, 1), err)) return false;
+    HIPCHK(hipMemsetAsync(lab.p, 0xFF, (size_t)pod_cap * std::max<uint32_t>(n_keys, 1) * 4, s));
+    for (uint32_t k = 0; k < I.pkeys; ++k)
+      HIPCHK(hipMemcpyAsync(lab.p + (size_t)k * pod_cap, I.ptlab.p + (size_t)k * I.pcap, (size_t)I.pcap * 4,
+                            hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::swap(lab.p, I.ptlab.p);
+    std::swap(lab.n, I.ptlab.n);
+  }
+  if (!I.terms.grow(term_cap, I.tcap, s, err) || !I.tpod.grow(term_cap, I.tcap, s, err) ||
+      !I.treq.grow(req_cap, I.rcap, s, err) || !I.tval.grow(val_cap, I.vcap, s, err))
+    return false;
+  I.pcap = pod_cap;
+  I.tcap = term_cap;
+  I.rcap = req_cap;
+  I.vcap = val_cap;
+  I.pkeys = n_keys;
+  HIPCHK(hipStreamSynchronize(s));
+  return true;
+}
+
 bool Engine::table_overflow(bool& overflow, std::string& err) {
   Impl& I = *p_;
   uint32_t f = 0;

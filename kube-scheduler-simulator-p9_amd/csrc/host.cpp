@@ -995,17 +995,58 @@ struct Cluster {
   }
 
   // ------------------------------------------------------------ vocabularies
+  // Pod-label space: the pod's namespace, label keys and values, and every key,
+  // value and namespace its selectors name.  Interning what selectors name (not
+  // only what pods carry) keeps every compiled selector exact when a later pod
+  // brings a new label value, key or namespace: the vocabulary then grows in
+  // place (grow_vocab) instead of re-encoding the snapshot.
   void intern_pod_labels(const Pod& p) {
     nss.add(p.ns);
-    for (auto& kv : p.labels) {
-      int32_t k = pkeys.add(kv.first);
+    auto val = [&](const string& key, const string* v) {
+      int32_t k = pkeys.add(key);
       if ((int32_t)pvals.size() <= k) pvals.resize(k + 1);
-      pvals[k].add(kv.second);
-    }
+      if (v) pvals[k].add(*v);
+    };
+    for (auto& kv : p.labels) val(kv.first, &kv.second);
+    auto sel = [&](const LSel& s) {
+      for (auto& r : s.reqs) {
+        val(r.key, nullptr);
+        for (auto& v : r.vals) val(r.key, &v);
+      }
+    };
     auto topo_of = [&](const string& key) { topo.add(key); nkeys.add(key); };
     for (auto* v : {&p.req_aff, &p.req_anti, &p.pref_aff, &p.pref_anti})
-      for (auto& t : *v) topo_of(t.topo);
-    for (auto& c : p.tsc) topo_of(c.key);
+      for (auto& t : *v) {
+        topo_of(t.topo);
+        sel(t.sel);
+        for (auto& ns : t.namespaces) nss.add(ns);
+      }
+    for (auto& c : p.tsc) {
+      topo_of(c.key);
+      sel(tsc_selector(p, c));
+    }
+  }
+  // Could the vocabulary take pod p in place (its topology keys, scalar
+  // resources and host ports are known: only pod-label space grows)?
+  bool vocab_grows_in_place(const Pod& p) const {
+    for (auto* v : {&p.req_aff, &p.req_anti, &p.pref_aff, &p.pref_anti})
+      for (auto& t : *v)
+        if (topo.get(t.topo) < 0) return false;
+    for (auto& c : p.tsc)
+      if (topo.get(c.key) < 0) return false;
+    for (auto& kv : p.req)
+      if (scalar_name(kv.first) && res.get(kv.first) < 0) return false;
+    for (auto& h : p.ports)
+      if (!port_id.count(std::make_tuple(h.ip, h.proto, h.port))) return false;
+    return true;
+  }
+  // Intern pod p's label space in place; new label keys widen the device's
+  // existing-pod label columns (Engine::grow_table).
+  bool grow_vocab(const Pod& p) {
+    const size_t k0 = pkeys.names.size();
+    intern_pod_labels(p);
+    if (pkeys.names.size() == k0) return true;
+    return eng->grow_table(0, 0, 0, 0, (uint32_t)pkeys.names.size(), err);
   }
 
   bool build_vocab() {
@@ -1868,14 +1909,6 @@ struct Cluster {
     }
     for (int i = 0; i < 4; ++i) need[i] += qneed[q][i];
   }
-  // Does the device existing-pod table have room for `need` more entries?
-  bool table_fits(const uint64_t need[4], bool& fits) {
-    uint32_t used[4], cap[4];
-    if (!eng->table_room(used, cap, err)) return false;
-    fits = true;
-    for (int i = 0; i < 4; ++i) fits &= (uint64_t)used[i] + need[i] <= cap[i];
-    return true;
-  }
   // Queue pods that may still be assumed: not run, or cycle pods without a placement.
   bool may_assume(uint32_t q) const { return qmode[q] == 0 || (qmode[q] == 2 && placed[q] < 0); }
   void mark_run(uint32_t first, uint32_t count) {
@@ -1893,15 +1926,28 @@ struct Cluster {
   }
   bool vocab_grows(const Pod& p) const {
     if (nss.get(p.ns) < 0) return true;
-    for (auto& kv : p.labels) {
-      int32_t k = pkeys.get(kv.first);
-      if (k < 0 || k >= (int32_t)pvals.size() || pvals[k].get(kv.second) < 0) return true;
-    }
+    auto known = [&](const string& key, const string* v) {
+      int32_t k = pkeys.get(key);
+      return k >= 0 && k < (int32_t)pvals.size() && (!v || pvals[k].get(*v) >= 0);
+    };
+    auto sel_known = [&](const LSel& s) {
+      for (auto& r : s.reqs) {
+        if (!known(r.key, nullptr)) return false;
+        for (auto& v : r.vals)
+          if (!known(r.key, &v)) return false;
+      }
+      return true;
+    };
+    for (auto& kv : p.labels)
+      if (!known(kv.first, &kv.second)) return true;
     for (auto* v : {&p.req_aff, &p.req_anti, &p.pref_aff, &p.pref_anti})
-      for (auto& t : *v)
-        if (topo.get(t.topo) < 0) return true;
+      for (auto& t : *v) {
+        if (topo.get(t.topo) < 0 || !sel_known(t.sel)) return true;
+        for (auto& ns : t.namespaces)
+          if (nss.get(ns) < 0) return true;
+      }
     for (auto& c : p.tsc)
-      if (topo.get(c.key) < 0) return true;
+      if (topo.get(c.key) < 0 || !sel_known(tsc_selector(p, c))) return true;
     for (auto& kv : p.req)
       if (scalar_name(kv.first) && res.get(kv.first) < 0) return true;
     for (auto& h : p.ports)
@@ -1993,7 +2039,12 @@ struct Cluster {
     uint32_t q = (uint32_t)queue.size() - 1;
     queue_idx[pod_key(queue[q].ns, queue[q].name)] = q;
     qmode[q] = 2;
-    if (vocab_grows(queue[q])) {
+    bool in_place = !vocab_grows(queue[q]);
+    if (!in_place && vocab_grows_in_place(queue[q])) {  // new label values / keys / namespaces only
+      if (!grow_vocab(queue[q])) return false;
+      in_place = true;
+    }
+    if (!in_place) {
       if (!rebuild()) return false;
     } else {
       vector<uint8_t> blob;
@@ -2004,6 +2055,7 @@ struct Cluster {
       meta.push_back(std::move(m));
       prog_cls.resize(progs.size(), {(uint32_t)pcls.size(), (uint32_t)tcls.size()});
     }
+    if (commit && !room_for(q)) return false;
     if (!eng->keep_outputs(q, 1, err) || !eng->run_queue(q, 1, commit, err) || !eng->sync(err) ||
         !eng->summaries(q, 1, &out, err))
       return false;
@@ -2011,16 +2063,28 @@ struct Cluster {
     if (commit && out.status == 0) {
       placed[q] = out.selected;
       assumed_in[q] = epoch;
-      if (!check_table()) return false;
     }
     return true;
   }
-  // The device appends assumed pods to its existing-pod table; when that is full
-  // the snapshot is re-encoded from the mirror (with fresh slack).
-  bool check_table() {
-    bool full = false;
-    if (!eng->table_overflow(full, err)) return false;
-    return full ? rebuild() : true;
+  // The device appends assumed pods to its existing-pod table: before an assume,
+  // make room for queue pod q's row in place (capacities doubled, contents kept).
+  bool room_for(uint32_t q) {
+    if (!tables_on()) return true;
+    uint64_t need[4] = {0, 0, 0, 0};
+    queue_need(q, need);
+    return ensure_room(need);
+  }
+  bool ensure_room(const uint64_t need[4]) {
+    uint32_t used[4], cap[4];
+    if (!eng->table_room(used, cap, err)) return false;
+    bool fits = true;
+    uint32_t nc[4];
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t want = (uint64_t)used[i] + need[i];
+      fits &= want <= cap[i];
+      nc[i] = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * cap[i], want + 1024), UINT32_MAX);
+    }
+    return fits || eng->grow_table(nc[0], nc[1], nc[2], nc[3], 0, err);
   }
   // ------------------------------------------------------------ DefaultPreemption
   // PostFilter of an unschedulable pod, as a dry run on the device state of the
@@ -2228,10 +2292,10 @@ struct Cluster {
     track_queue();
     if (q >= queue.size() || qmode[q] != 2 || placed[q] >= 0) { err = "reserve: pod not in an uncommitted cycle"; return false; }
     if (node < 0 || node >= (int32_t)nodes.size()) { err = "reserve: node out of range"; return false; }
-    if (!refresh_program(q) || !eng->assume(q, node, +1, err)) return false;
+    if (!refresh_program(q) || !room_for(q) || !eng->assume(q, node, +1, err)) return false;
     placed[q] = node;
     assumed_in[q] = epoch;
-    return check_table();
+    return true;
   }
   bool unreserve(uint32_t q) {
     track_queue();
@@ -2288,7 +2352,11 @@ struct Cluster {
       if (op == "addPod") {
         if (!e["pod"]) return 0;
         Pod p = parse_pod(*e["pod"]);
-        if (p.node.empty() || node_names.get(p.node) < 0 || vocab_grows(p)) return 0;
+        if (p.node.empty() || node_names.get(p.node) < 0) return 0;
+        if (vocab_grows(p)) {  // new label values / keys / namespaces grow in place
+          if (!vocab_grows_in_place(p)) return 0;
+          if (!grow_vocab(p)) return -1;
+        }
         string k = pkey(p.ns, p.name);
         if (present(k)) return 0;
         if (queue_find(p.ns, p.name) >= 0) return 0;
@@ -2353,18 +2421,13 @@ struct Cluster {
         return 0;
       }
     }
-    // Room in the device existing-pod table (PTS/IPA profiles append every assumed
-    // pod): the batch's additions plus every queue pod that may still be assumed
-    // must fit, else the re-encode path takes the batch (fresh capacity, no tombstones).
+    // Room in the device existing-pod table (PTS/IPA profiles) for the batch's
+    // additions, grown in place (queue pods get theirs before they are assumed).
     if (tables_on()) {
       uint64_t need[4] = {0, 0, 0, 0};
       for (auto& o : ops)
         if (o.add) table_need(o.pod, need);
-      for (uint32_t q = 0; q < queue.size(); ++q)
-        if (may_assume(q) && !gone_q.count((int32_t)q)) queue_need(q, need);
-      bool fits = false;
-      if (!table_fits(need, fits)) return -1;
-      if (!fits) return 0;
+      if (!ensure_room(need)) return -1;
     }
     // Host mirror first; device writes after (bound-pod deltas, then the queue
     // pods' Unreserve deltas and allocatable updates: row deltas commute).  A
@@ -2436,7 +2499,9 @@ struct Cluster {
     }
     for (auto& a : adds)
       if (add_slot.count(a.first)) bound_row[bound_at.at(a.first)] = rows[a.second];
-    return check_table() ? 1 : -1;  // a full existing-pod table re-encodes from the mirror
+    bool full = false;  // (room was made above: a full table here re-encodes from the mirror)
+    if (!eng->table_overflow(full, err)) return -1;
+    return !full || rebuild() ? 1 : -1;
   }
 
   bool apply_events(const char* js, size_t len) {
@@ -2993,9 +3058,7 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   if (c.tables_on()) {  // the run appends every scheduled pod to the existing-pod table
     uint64_t need[4] = {0, 0, 0, 0};
     for (uint32_t q = first; q < first + count; ++q) c.queue_need(q, need);
-    bool fits = false;
-    if (!c.table_fits(need, fits)) return ctx->fail(c.err, KSG_E_DEVICE);
-    if (!fits && !c.rebuild()) return ctx->fail(c.err, KSG_E_DEVICE);  // fresh capacity, placements kept
+    if (!c.ensure_room(need)) return ctx->fail(c.err, KSG_E_DEVICE);  // grown in place, contents kept
   }
   // Pods that may preempt end a segment: the run stops after each, and an
   // unschedulable one gets its DefaultPreemption dry run on the state of its own

@@ -5,6 +5,7 @@
 // Nothing here is shipped or linked into libksg.so: every cycle ends
 // "unschedulable" with no node evaluated; the shapes the host hands over are
 // checked so that an encoder bug shows up as a failure here.
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 
@@ -137,6 +138,12 @@ bool Engine::dry_filter(uint32_t q, int32_t gnode, std::vector<uint32_t>& codes,
 bool Engine::pod_row(uint32_t q, int32_t& row, std::string& err) {
   if (q >= p_->progs.size()) { err = "stub: pod_row range"; return false; }
   row = -1;
+  return true;
+}
+bool Engine::grow_table(uint32_t pod_cap, uint32_t term_cap, uint32_t req_cap, uint32_t val_cap, uint32_t,
+                        std::string&) {
+  uint32_t c[4] = {pod_cap, term_cap, req_cap, val_cap};
+  for (int i = 0; i < 4; ++i) p_->cap[i] = std::max(p_->cap[i], c[i]);
   return true;
 }
 bool Engine::node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_t, std::string& err) {

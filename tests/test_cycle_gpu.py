@@ -91,15 +91,28 @@ def test_unreserve_restores_state(name, c, sizes):
 
 @pytest.mark.gpu
 def test_cycle_new_vocabulary_rebuilds():
-    """Pods bringing label keys/values and namespaces the snapshot never saw force a
-    re-encode (placements kept): results stay equal to the oracle's.  An Unreserve of
-    a pod assumed before those rebuilds then takes exactly its requests off its node."""
+    """Pods bringing label keys/values and namespaces the snapshot never saw grow the
+    vocabulary in place (new label keys widen the device's label columns); a pod
+    bringing a new topology key re-encodes (placements kept).  Selectors naming
+    values no pod carries yet (an assumed pod's required anti-affinity on a fresh
+    value, carried by a later pod) stay exact.  Results stay equal to the oracle's;
+    an Unreserve of an early pod then takes exactly its requests off its node."""
     doc = g.generate(4, n_nodes=120, n_existing=400, n_pods=40, n_zones=4)
     for i, p in enumerate(doc["queue"]):
         if i % 6 == 3:
             p["metadata"]["labels"] = dict(p["metadata"]["labels"], **{f"fresh-{i}": f"v{i}"})
         if i % 11 == 5:
             p["metadata"]["namespace"] = f"ns-new-{i}"
+        if i % 7 == 2 and i + 3 < len(doc["queue"]):  # anti-affinity on a value only pod i+3 will carry
+            aff = p["spec"].setdefault("affinity", {})
+            aff.setdefault("podAntiAffinity", {}).setdefault("requiredDuringSchedulingIgnoredDuringExecution", []).append(
+                {"labelSelector": {"matchLabels": {"fresh-sel": f"x{i}"}}, "topologyKey": "kubernetes.io/hostname"})
+            q3 = doc["queue"][i + 3]["metadata"]
+            q3["labels"] = dict(q3.get("labels", {}), **{"fresh-sel": f"x{i}"})
+        if i == 30:  # a topology key no node or pod named yet: re-encode
+            p["spec"]["topologySpreadConstraints"] = [{"maxSkew": 1, "topologyKey": "example.com/rack",
+                                                      "whenUnsatisfiable": "ScheduleAnyway",
+                                                      "labelSelector": {"matchLabels": {"app": "x"}}}]
     o = Oracle(doc)
     o.schedule(record=0)
     s = Scheduler(doc["profile"])
@@ -115,3 +128,18 @@ def test_cycle_new_vocabulary_rebuilds():
     assert pc0[sel1] - pc1[sel1] == 1
     assert sum(pc0) - sum(pc1) == 1
     assert req0[0][sel1] - req1[0][sel1] > 0 or req0[1][sel1] - req1[1][sel1] > 0
+
+
+@pytest.mark.gpu
+def test_cycle_table_grows_in_place():
+    """More assumed pods than the existing-pod table's slack (1,024 rows): the table
+    grows in place (rows, terms, reqs, vals re-laid, contents kept) and every
+    cycle still equals the oracle."""
+    doc = g.generate(4, n_nodes=60, n_existing=120, n_pods=1300, n_zones=3)
+    o = Oracle(doc)
+    o.schedule(record=0)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(_empty_queue(doc))
+    for i, pod in enumerate(doc["queue"]):
+        q, r = s.cycle(pod, commit=True)
+        assert (r.selected, r.feasible, r.status) == o.result(i), i

@@ -159,9 +159,13 @@ def test_volume_pods_refused():
 
 
 @pytest.mark.gpu
-def test_mixed_priorities_refused():
+def test_mixed_priorities_sharded_refused():
+    """DefaultPreemption's dry run runs on unsharded contexts (test_preempt_gpu.py);
+    a sharded context refuses a cluster of mixed priorities instead of approximating."""
     doc = g.generate(1, n_nodes=4, n_pods=2)
     doc["queue"][1]["spec"]["priority"] = 1000
     s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    t = Scheduler(doc["profile"], shard_rank=0, shard_count=2)
     with pytest.raises(Exception):
-        s.load_cluster(doc)
+        t.load_cluster(doc)

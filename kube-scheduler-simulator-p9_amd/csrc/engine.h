@@ -37,6 +37,7 @@ struct EngineConfig {
 struct NodeSoA {
   uint32_t n = 0, n_res = 3, n_keys = 0;
   uint32_t global_offset = 0;             // global index of local node 0 (sharding)
+  uint32_t global_n = 0;                  // nodes of the whole cluster (every shard)
   std::vector<int64_t> alloc, requested;  // [n_res][n]
   std::vector<int64_t> nz_cpu, nz_mem;    // [n]
   std::vector<int32_t> allowed_pods, pod_count;

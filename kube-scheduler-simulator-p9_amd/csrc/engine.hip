@@ -1995,6 +1995,10 @@ struct Pend {  // a node modified by a window: row before (base) and after it
 // but only the rows of its shallow ranks).
 static constexpr size_t kRecKeys = (size_t)KSG_BATCH * KSG_CAND;
 static constexpr size_t kRecBytes = KSG_XHDR + kRecKeys * 8 + kRecKeys * sizeof(RowV);
+// Sharded windows exchange the header and the keys only (16.5 KiB per rank):
+// every rank keeps a replica of every node's row (WinArgs::xrows), so the
+// merged candidates' rows come from the local replica, not from the wire.
+static constexpr size_t kXchgBytes = KSG_XHDR + kRecKeys * 8;
 static_assert(sizeof(RowV) % 8 == 0, "RowV is staged as 64-bit words");
 __device__ __forceinline__ uint64_t* rec_keys(uint8_t* rec) { return reinterpret_cast<uint64_t*>(rec + KSG_XHDR); }
 __device__ __forceinline__ const uint64_t* rec_keys(const uint8_t* rec) {
@@ -2048,6 +2052,9 @@ struct WinArgs {
   const StaticRec* stat;
   uint32_t stat_ring;
   const int64_t* mpred;  // [2 * (q - first)]: Taint, NodeAffinity (-1: no statically feasible node)
+  // sharded: replica of every node's row, indexed by global node (kept in step by
+  // every rank's identical replay); null on one shard
+  RowV* xrows;
 };
 __device__ __forceinline__ const StaticRec* srec_row(const WinArgs& A, uint32_t q, uint32_t N) {
   return A.stat + (size_t)((q - A.first) % A.stat_ring) * N;
@@ -2602,7 +2609,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
       else load_row(C, (uint32_t)gid - C.goff, A.need_eph, c);
     }
     rec_keys(A.erec)[(size_t)b * KSG_CAND + lane] = v;
-    rec_rows(A.erec)[(size_t)b * KSG_CAND + lane] = c;
+    if (!A.xrows) rec_rows(A.erec)[(size_t)b * KSG_CAND + lane] = c;  // (sharded: rows from the replica)
     int32_t f[3] = {0, 0, 0};
     for (uint32_t t = lane; t < A.T; t += 64)
 #pragma unroll
@@ -3030,6 +3037,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     const Pend& pe = L.prior[tid];
     uint32_t nl = (uint32_t)pe.node - C.goff;
     if ((uint32_t)pe.node >= C.goff && nl < C.N) store_row(C, nl, pe.after);
+    if (A.xrows) A.xrows[pe.node] = pe.after;  // every rank's replica, every node
   }
   {  // pods on the P_{W-1} nodes as of the window start (independent of the picks)
     const int pb = 2 * wave + (lane >> 5), e = lane & 31;
@@ -3405,41 +3413,43 @@ __global__ void k_apply_pend(DevCluster C, const Pend* p, const int32_t* pn) {
   if ((uint32_t)p[e].node >= C.goff && nl < C.N) store_row(C, nl, p[e].after);
 }
 
-// Sharded windows: every rank's record (feasible counts + its top-KSG_CAND
-// candidates per pod, rows included) is all-gathered; one wave per pod merges
-// the R sorted lists into the global top-KSG_CAND and sums the counts.
-__global__ __launch_bounds__(64) void k_window_gmerge(const uint8_t* recv, uint32_t ranks, uint8_t* out) {
+// Sharded windows: every rank's header and keys (feasible counts + its
+// top-KSG_CAND candidates per pod, kXchgBytes) are all-gathered; one wave per
+// pod merges the R sorted lists into the global top-KSG_CAND, sums the counts and
+// takes each candidate's row from the replica.  Between launches the replica
+// holds the rows as of the end of window E-2 (the replay of E-1 wrote P_{E-2}
+// into it first thing), which is what the owner's eval blocks computed on.
+__global__ __launch_bounds__(64) void k_window_gmerge(const uint8_t* recv, uint32_t ranks, const RowV* xrows,
+                                                      uint8_t* out) {
   __shared__ uint64_t keys[8 * KSG_CAND];
   const uint32_t b = blockIdx.x;
   const int lane = threadIdx.x;
-  for (uint32_t r = 0; r < ranks; ++r) keys[r * KSG_CAND + lane] = rec_keys(recv + r * kRecBytes)[(size_t)b * KSG_CAND + lane];
+  for (uint32_t r = 0; r < ranks; ++r) keys[r * KSG_CAND + lane] = rec_keys(recv + r * kXchgBytes)[(size_t)b * KSG_CAND + lane];
   __syncthreads();
   uint64_t v = keys[lane];
   for (uint32_t r = 1; r < ranks; ++r) v = wave_merge_top(v, keys[r * KSG_CAND + 63 - lane]);
   int32_t f[3] = {0, 0, 0};
   for (uint32_t r = 0; r < ranks; ++r)
-    for (int k = 0; k < 3; ++k) f[k] += reinterpret_cast<const int32_t*>(recv + r * kRecBytes)[k * KSG_BATCH + b];
+    for (int k = 0; k < 3; ++k) f[k] += reinterpret_cast<const int32_t*>(recv + r * kXchgBytes)[k * KSG_BATCH + b];
   RowV c;
   memset(&c, 0, sizeof(c));
-  if (v) {  // find the source entry: each rank's list is sorted descending
-    for (uint32_t r = 0; r < ranks; ++r) {
-      int lo = 0, hi = KSG_CAND - 1, at = -1;
-      while (lo <= hi) {
-        int mid = (lo + hi) >> 1;
-        uint64_t k = keys[r * KSG_CAND + mid];
-        if (k == v) { at = mid; break; }
-        if (k > v) lo = mid + 1;
-        else hi = mid - 1;
-      }
-      if (at >= 0) {
-        c = rec_rows(recv + r * kRecBytes)[(size_t)b * KSG_CAND + at];
-        break;
-      }
-    }
-  }
+  if (v) c = xrows[v & 0xFFFFFull];
   rec_keys(out)[(size_t)b * KSG_CAND + lane] = v;
   rec_rows(out)[(size_t)b * KSG_CAND + lane] = c;
   if (lane < 3) reinterpret_cast<int32_t*>(out)[lane * KSG_BATCH + b] = f[lane];
+}
+// Replica set-up at the start of a sharded run: local rows packed (load_row:
+// what the eval blocks read), all-gathered at a stride of the largest shard,
+// unpacked by global index (shard r holds nodes [G*r/ranks, G*(r+1)/ranks)).
+__global__ void k_rows_pack(DevCluster C, uint32_t need_eph, RowV* out) {
+  const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n < C.N) load_row(C, n, need_eph, out[n]);
+}
+__global__ void k_rows_unpack(const RowV* recv, uint32_t ranks, uint32_t G, uint32_t stride, RowV* xrows) {
+  const uint32_t r = blockIdx.y;
+  const uint32_t lo = (uint32_t)((uint64_t)G * r / ranks), hi = (uint32_t)((uint64_t)G * (r + 1) / ranks);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; lo + i < hi; i += gridDim.x * blockDim.x)
+    xrows[lo + i] = recv[(size_t)r * stride + i];
 }
 
 // ----------------------------------------------------------------- host side
@@ -3507,6 +3517,8 @@ struct Engine::Impl {
   Engine::ExchangeFn xfn = nullptr;
   void* xuser = nullptr;
   DBuf<uint8_t> xsend, xrecv;
+  DBuf<RowV> xrows;  // sharded windows: every node's row (run_batches)
+  uint32_t G = 0;    // nodes of the whole cluster
   std::vector<uint8_t> hsend, hrecv;
   DevProfile F{};
   hipStream_t stream = nullptr;
@@ -3754,6 +3766,7 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   if (ns.n_res > KSG_MAX_RES) { err = "too many resources"; return false; }
   I.N = ns.n;
   I.goff = ns.global_offset;
+  I.G = std::max(ns.global_n, ns.global_offset + ns.n);
   I.static_fits = true;
   for (uint32_t i = 0; i < ns.n; ++i)
     if (ns.taint_off[i + 1] - ns.taint_off[i] >= 4096) I.static_fits = false;
@@ -3903,6 +3916,7 @@ static uint32_t eval_tiles(uint32_t N, uint32_t cus) {
 // Windows of KSG_BATCH pods, one k_window launch each (see the kernel): launch
 // j evaluates window j+1 and replays window j; the sharded path all-gathers
 // each window's candidate records between launches.
+static bool xgather(Engine::Impl& I, size_t bytes, std::string& err);
 static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::string& err) {
   if (I.R > 4) { err = "batch path supports at most 4 resource columns"; return false; }
   hipStream_t s = I.stream;
@@ -3952,6 +3966,19 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   A.arrive = I.arrive.p;
   A.sums = I.sums.p;
   const bool sharded = I.xranks > 1;
+  A.xrows = nullptr;
+  if (sharded) {  // every node's row on every rank (kXchgBytes exchanges: keys only)
+    const uint32_t G = std::max<uint32_t>(I.G, 1), stride = (G + I.xranks - 1) / I.xranks;
+    if (!I.xrows.alloc(G, err)) return false;
+    const size_t bytes = (size_t)stride * sizeof(RowV);
+    if (!I.xsend.grow(std::max(bytes, kRecBytes), 0, s, err) || !I.xrecv.grow(bytes * I.xranks, 0, s, err)) return false;
+    if (I.N) hipLaunchKernelGGL(k_rows_pack, dim3((I.N + 255) / 256), dim3(256), 0, s, C, I.any_eph_req ? 1u : 0u,
+                                reinterpret_cast<RowV*>(I.xsend.p));
+    if (!xgather(I, bytes, err)) return false;
+    hipLaunchKernelGGL(k_rows_unpack, dim3((stride + 255) / 256, I.xranks), dim3(256), 0, s,
+                       reinterpret_cast<const RowV*>(I.xrecv.p), I.xranks, G, stride, I.xrows.p);
+    A.xrows = I.xrows.p;
+  }
   // static records: a ring of two chunks of whole windows (window j+1's eval and
   // window j's replay may sit in consecutive chunks); chunk c computed by k_static
   // just before the launch that evaluates its first window
@@ -4052,16 +4079,8 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
       if (!issue_static(cidx + 2, I.sstream)) return false;
     }
     if (sharded && A.ne) {
-      if (I.xmode == 1) {
-        ncclResult_t nr = ncclAllGather(I.xsend.p, I.xrecv.p, kRecBytes, ncclUint8, I.comm, s);
-        if (nr != ncclSuccess) { err = std::string("ncclAllGather: ") + ncclGetErrorString(nr); return false; }
-      } else {
-        HIPCHK(hipMemcpyAsync(I.hsend.data(), I.xsend.p, kRecBytes, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        if (I.xfn(I.xuser, I.hsend.data(), I.hrecv.data(), kRecBytes) != 0) { err = "exchange callback failed"; return false; }
-        HIPCHK(hipMemcpyAsync(I.xrecv.p, I.hrecv.data(), kRecBytes * I.xranks, hipMemcpyHostToDevice, s));
-      }
-      hipLaunchKernelGGL(k_window_gmerge, dim3(A.ne), dim3(64), 0, s, I.xrecv.p, I.xranks,
+      if (!xgather(I, kXchgBytes, err)) return false;
+      hipLaunchKernelGGL(k_window_gmerge, dim3(A.ne), dim3(64), 0, s, I.xrecv.p, I.xranks, I.xrows.p,
                          I.wrec.p + (size_t)(E & 1) * kRecBytes);
     }
   }

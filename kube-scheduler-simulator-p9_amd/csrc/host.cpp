@@ -1168,6 +1168,7 @@ struct Cluster {
     S = NodeSoA();
     S.n = n;
     S.global_offset = lo;
+    S.global_n = G;
     S.n_res = R;
     S.n_keys = K;
     S.alloc.assign((size_t)R * n, 0);

@@ -175,7 +175,16 @@ int ksg_unreserve(ksg_ctx* ctx, uint32_t q);
  * -1 means the framework does not call this plugin there (an earlier filter
  * failed on the node, PreFilter Skip, outside the PreFilterResult, no scoring).
  * Messages are Status.Message() (what the wrapper records, wrappedplugin.go:542). */
-int ksg_plugin_position(const ksg_ctx* ctx, const char* name, size_t len);  /* or KSG_E_RANGE */
+int ksg_plugin_position(const ksg_ctx* ctx, const char* name, size_t len);  /* or KSG_E_RANGE; "…Wrapped" accepted */
+/* The weights the profile resolved for position `pos`: *weight is the framework's
+ * (upstream framework.go getScoreWeights: an explicit Score weight wins over
+ * MultiPoint's; it scales the total selectHost uses), *store_weight the result
+ * store's (plugins.go:289-304 getScorePluginWeight: MultiPoint overwrites; it
+ * scales finalscore-result, store.go:504-507).  They differ only in the quirk of
+ * scheduler_test.go:344-407.  ksg_create takes the flat profile
+ * {plugins, weights, storeWeights, pluginConfig} or a KubeSchedulerConfiguration /
+ * KubeSchedulerProfile (plugins.multiPoint / plugins.score, pluginConfig list). */
+int ksg_plugin_weights(const ksg_ctx* ctx, uint32_t pos, int64_t* weight, int64_t* store_weight);
 int ksg_node_index(const ksg_ctx* ctx, const char* name, size_t len);       /* or KSG_E_RANGE */
 /* PreFilter (wrappedplugin.go:504, mock framework.go:61): status; and the
  * PreFilterResult node set as a JSON array of node names, "null" for all nodes. */

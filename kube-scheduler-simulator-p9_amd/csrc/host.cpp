@@ -497,6 +497,118 @@ static int plugin_id(const string& n) {
     if (n == t.first) return t.second;
   return -1;
 }
+// ---------------------------------------------------------------- scheduler configuration
+// A KubeSchedulerConfiguration / KubeSchedulerProfile (what the simulator's
+// ConvertForSimulator hands the framework, plugins.go) → the flat profile
+// {plugins, weights, storeWeights, pluginConfig} the engine takes.
+//  * plugin order: multiPoint.enabled (the filter order; scores are order-free);
+//  * framework weights: upstream v1.30.4 framework.go getScoreWeights over
+//    score.enabled ++ multiPoint.enabled — the first entry of a name wins (an
+//    explicit Score weight overrides MultiPoint's), 0 → 1;
+//  * store weights: getScorePluginWeight (plugins.go:289-304) over the same list —
+//    the last entry wins (MultiPoint overwrites), 0 → 1, "Wrapped" suffix stripped.
+// The two differ exactly in the quirk of scheduler_test.go:344-407.  Per-extension-
+// point sets other than score weights of MultiPoint plugins are refused.
+static J jnum(i64 v) {
+  J n;
+  n.t = J::NUM;
+  n.s = std::to_string(v);
+  return n;
+}
+static void jput(J& o, const string& k, J v) {
+  for (size_t i = 0; i < o.keys.size(); ++i)
+    if (o.keys[i] == k) { o.items[i] = std::move(v); return; }
+  o.keys.push_back(k);
+  o.items.push_back(std::move(v));
+}
+static string unwrapped(const string& n) {
+  static const string suf = "Wrapped";
+  return n.size() > suf.size() && n.compare(n.size() - suf.size(), suf.size(), suf) == 0
+             ? n.substr(0, n.size() - suf.size()) : n;
+}
+static bool profile_from_config(const J& in, J& out, string& err) {
+  const J* prof = &in;
+  if (const J* ps = in["profiles"]) {
+    if (ps->t != J::ARR || ps->items.empty()) { err = "profiles: expected a non-empty list"; return false; }
+    prof = &ps->items[0];  // one profile (getScorePluginWeight reads Profiles[0])
+  }
+  const J* pl = (*prof)["plugins"];
+  if (!pl || pl->t != J::OBJ) { err = "profile.plugins: expected an object"; return false; }
+  vector<std::pair<string, i64>> mp, sc;  // (name, weight) in order
+  auto entries = [&](const J* set, const char* what, vector<std::pair<string, i64>>& dst) -> bool {
+    if (!set) return true;
+    if (const J* en = (*set)["enabled"]) {
+      if (en->t != J::ARR) { err = string(what) + ".enabled: expected a list"; return false; }
+      for (auto& e : en->items) {
+        const string nm = unwrapped(str_of(e["name"]));
+        if (nm.empty()) { err = string(what) + ".enabled: plugin without a name"; return false; }
+        const i64 w = e["weight"] ? e["weight"]->num() : 0;
+        if (w < 0 || w > INT32_MAX) { err = string(what) + ": weight of " + nm + " out of range"; return false; }
+        dst.push_back({nm, w});
+      }
+    }
+    return true;
+  };
+  for (size_t i = 0; i < pl->keys.size(); ++i) {
+    const string& ext = pl->keys[i];
+    const J& set = pl->items[i];
+    if (ext == "multiPoint") {
+      if (!entries(&set, "multiPoint", mp)) return false;
+    } else if (ext == "score") {
+      if (!entries(&set, "score", sc)) return false;
+      if (const J* d = set["disabled"])
+        if (!d->items.empty()) { err = "score.disabled: per-extension-point disabling is not supported"; return false; }
+    } else {
+      for (const char* k : {"enabled", "disabled"})
+        if (const J* l = set[k])
+          if (!l->items.empty()) {
+            err = ext + "." + k + ": per-extension-point plugin sets are not supported (use multiPoint)";
+            return false;
+          }
+    }
+  }
+  J names;
+  names.t = J::ARR;
+  set<string> seen;
+  for (auto& e : mp) {
+    if (plugin_id(e.first) < 0) { err = "unsupported plugin " + e.first; return false; }
+    if (!seen.insert(e.first).second) { err = "plugin " + e.first + " already registered"; return false; }
+    J s;
+    s.t = J::STR;
+    s.s = e.first;
+    names.items.push_back(s);
+  }
+  for (auto& e : sc)
+    if (!seen.count(e.first)) { err = "score.enabled: " + e.first + " is not a multiPoint plugin"; return false; }
+  J fw, sw;
+  fw.t = sw.t = J::OBJ;
+  vector<std::pair<string, i64>> all(sc);
+  all.insert(all.end(), mp.begin(), mp.end());
+  for (auto& e : all) {
+    const i64 w = e.second == 0 ? 1 : e.second;
+    if (!fw[e.first.c_str()]) jput(fw, e.first, jnum(w));  // first wins (framework)
+    jput(sw, e.first, jnum(w));                            // last wins (store)
+  }
+  out = J();
+  out.t = J::OBJ;
+  jput(out, "plugins", names);
+  jput(out, "weights", fw);
+  jput(out, "storeWeights", sw);
+  if (const J* pc = (*prof)["pluginConfig"]) {
+    J m;
+    m.t = J::OBJ;
+    if (pc->t == J::ARR) {
+      for (auto& e : pc->items)
+        if (const J* a = e["args"]) jput(m, unwrapped(str_of(e["name"])), *a);
+    } else if (pc->t == J::OBJ) {
+      m = *pc;
+    }
+    jput(out, "pluginConfig", m);
+  }
+  if (const J* s = (*prof)["seed"] ? (*prof)["seed"] : in["seed"]) jput(out, "seed", *s);
+  return true;
+}
+
 static bool host_only(int p) { return p == P_VOLUME || p == P_VOLBIND || p == P_NOOP; }
 // extension points the original plugin implements (the wrapper records only those)
 static bool has_prefilter(int p) {
@@ -567,6 +679,11 @@ struct Cluster {
 
   // ------------------------------------------------------------ profile
   bool load_profile(const J& pr) {
+    if (pr["profiles"] || (pr["plugins"] && pr["plugins"]->t == J::OBJ)) {  // scheduler configuration form
+      J flat;
+      if (!profile_from_config(pr, flat, err)) return false;
+      return load_profile(flat);
+    }
     const J* pl = pr["plugins"];
     if (!pl) { err = "profile.plugins missing"; return false; }
     for (auto& x : pl->items) {
@@ -3300,10 +3417,18 @@ static int put_str(ksg_ctx* ctx, const std::string& s, char* buf, size_t cap, si
 
 int ksg_plugin_position(const ksg_ctx* ctx, const char* name, size_t len) {
   if (!ctx || !name) return KSG_E_INVALID;
-  const std::string nm(name, len);
+  const std::string nm = ksg::host::unwrapped(std::string(name, len));
   for (int i = 0; i < ctx->c.n_plugins; ++i)
     if (ctx->c.names[i] == nm) return i;
   return KSG_E_RANGE;
+}
+
+int ksg_plugin_weights(const ksg_ctx* ctx, uint32_t pos, int64_t* weight, int64_t* store_weight) {
+  if (!ctx) return KSG_E_INVALID;
+  if ((int)pos >= ctx->c.n_plugins) return KSG_E_RANGE;
+  if (weight) *weight = ctx->c.fw_w[pos];
+  if (store_weight) *store_weight = ctx->c.store_w[pos];
+  return KSG_OK;
 }
 
 int ksg_node_index(const ksg_ctx* ctx, const char* name, size_t len) {

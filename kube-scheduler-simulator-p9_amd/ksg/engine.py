@@ -79,6 +79,7 @@ def load_library():
     cp = ctypes.c_char_p
     L.ksg_plugin_position.argtypes = [vp, cp, sz]
     L.ksg_node_index.argtypes = [vp, cp, sz]
+    L.ksg_plugin_weights.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     L.ksg_prefilter_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_prefilter_result.argtypes = [vp, u32, cp, sz, ctypes.POINTER(sz)]
     L.ksg_postfilter_result.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_int32), cp, sz, ctypes.POINTER(sz)]
@@ -242,6 +243,12 @@ class Scheduler:
         b = name.encode()
         r = self.L.ksg_plugin_position(self.h, b, len(b))
         return None if r < 0 else r
+
+    def plugin_weights(self, pos):
+        """(framework weight, store weight) the profile resolved for position pos."""
+        w, sw = ctypes.c_int64(), ctypes.c_int64()
+        self._chk(self.L.ksg_plugin_weights(self.h, pos, ctypes.byref(w), ctypes.byref(sw)), "plugin_weights")
+        return w.value, sw.value
 
     def node_index(self, name):
         b = name.encode()

@@ -94,6 +94,26 @@ def make_profile(plugins, seed):
     }
 
 
+def config_profile(plugins, seed, score=None):
+    """The same profile as a KubeSchedulerConfiguration after the simulator's
+    ConvertForSimulator (scheduler_test.go:344-407 "want"): MultiPoint lists every
+    plugin as "<name>Wrapped" (default MultiPoint disabled "*"), `score` adds
+    Score.Enabled entries [(name, weight)] that re-weight MultiPoint plugins.
+    ksg_create resolves it like the framework (weights) and the store
+    (storeWeights) do; see include/ksg.h ksg_plugin_weights."""
+    def ent(n, w):
+        e = {"name": n + "Wrapped"}
+        if w is not None:
+            e["weight"] = w
+        return e
+    return {"profiles": [{
+        "schedulerName": "default-scheduler",
+        "plugins": {"multiPoint": {"enabled": [ent(p, w) for p, w in plugins], "disabled": [{"name": "*"}]},
+                    "score": {"enabled": [ent(p, w) for p, w in (score or [])]}},
+        "pluginConfig": [{"name": k + "Wrapped", "args": v} for k, v in json.loads(json.dumps(DEFAULT_ARGS)).items()],
+        "seed": seed}]}
+
+
 # default profile order/weights for the hot-path plugins (scheduler_test.go:535-557)
 DEFAULT_HOT_PROFILE = [("TaintToleration", 3), ("NodeAffinity", 2), ("NodeResourcesFit", 1),
                        ("PodTopologySpread", 2), ("InterPodAffinity", 2),

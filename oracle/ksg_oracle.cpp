@@ -2100,6 +2100,115 @@ struct Cluster {
   }
 };
 
+// Scheduler configuration → flat profile.  Restates, for one profile:
+//  * simulator/scheduler/plugin/plugins.go:289-304 getScorePluginWeight — store
+//    weights over Score.Enabled ++ MultiPoint.Enabled, later entries overwrite,
+//    weight 0 → 1, the "Wrapped" suffix trimmed;
+//  * upstream v1.30.4 pkg/scheduler/framework/runtime/framework.go getScoreWeights
+//    — framework weights over the same concatenation, but a name already seen is
+//    skipped ("let the individual Score weight take precedence"), 0 → 1;
+//  * expandMultiPointPlugins — MultiPoint order is the extension-point order when
+//    no extension point lists plugins of its own; a MultiPoint name twice is an error.
+// Pinned by scheduler_test.go:344-407 (Score w3 + MultiPoint w2 → store 2).
+static std::string trim_wrapped(std::string n) {
+  const std::string suffix = "Wrapped";
+  if (n.size() > suffix.size() && n.substr(n.size() - suffix.size()) == suffix) n.resize(n.size() - suffix.size());
+  return n;
+}
+static bool flatten_config(const ojson::Value& cfg, ojson::Value& flat, string& err) {
+  const ojson::Value* prof = &cfg;
+  if (auto* ps = cfg.get("profiles")) {
+    if (ps->kind != ojson::Value::Arr || ps->arr.empty()) {
+      err = "profiles: empty";
+      return false;
+    }
+    prof = &ps->arr[0];
+  }
+  const ojson::Value* plugins = prof->get("plugins");
+  if (!plugins || plugins->kind != ojson::Value::Obj) {
+    err = "plugins: not an object";
+    return false;
+  }
+  struct Entry {
+    std::string name;
+    long long weight;
+  };
+  std::vector<Entry> multi, score;
+  for (auto& ext : plugins->obj) {
+    const ojson::Value* en = ext.second.get("enabled");
+    const ojson::Value* dis = ext.second.get("disabled");
+    std::vector<Entry>* dst = ext.first == "multiPoint" ? &multi : ext.first == "score" ? &score : nullptr;
+    if (!dst) {
+      if ((en && !en->arr.empty()) || (dis && !dis->arr.empty())) {
+        err = ext.first + ": per-extension-point sets unsupported";
+        return false;
+      }
+      continue;
+    }
+    if (ext.first == "score" && dis && !dis->arr.empty()) {
+      err = "score.disabled unsupported";
+      return false;
+    }
+    if (en)
+      for (auto& p : en->arr) {
+        auto* w = p.get("weight");
+        dst->push_back({trim_wrapped(p.get("name") ? p.get("name")->str() : ""), w ? w->i64() : 0});
+      }
+  }
+  ojson::Value list, fw, sw;
+  list.kind = ojson::Value::Arr;
+  fw.kind = sw.kind = ojson::Value::Obj;
+  std::set<std::string> in_multi;
+  for (auto& e : multi) {
+    if (!in_multi.insert(e.name).second) {
+      err = "plugin " + e.name + " already registered";
+      return false;
+    }
+    ojson::Value s;
+    s.kind = ojson::Value::Str;
+    s.raw = e.name;
+    list.arr.push_back(s);
+  }
+  for (auto& e : score)
+    if (!in_multi.count(e.name)) {
+      err = "score plugin " + e.name + " outside multiPoint";
+      return false;
+    }
+  std::vector<Entry> order = score;
+  order.insert(order.end(), multi.begin(), multi.end());
+  std::map<std::string, long long> fwm, swm;
+  for (auto& e : order) {  // getScoreWeights: first one kept
+    if (fwm.count(e.name)) continue;
+    fwm[e.name] = e.weight == 0 ? 1 : e.weight;
+  }
+  for (auto& e : order) swm[e.name] = e.weight != 0 ? e.weight : 1;  // getScorePluginWeight: overwrite
+  auto num = [](long long v) {
+    ojson::Value n;
+    n.kind = ojson::Value::Num;
+    n.raw = std::to_string(v);
+    return n;
+  };
+  for (auto& kv : fwm) fw.obj.push_back({kv.first, num(kv.second)});
+  for (auto& kv : swm) sw.obj.push_back({kv.first, num(kv.second)});
+  flat.kind = ojson::Value::Obj;
+  flat.obj.push_back({"plugins", list});
+  flat.obj.push_back({"weights", fw});
+  flat.obj.push_back({"storeWeights", sw});
+  if (auto* pc = prof->get("pluginConfig")) {
+    ojson::Value m;
+    m.kind = ojson::Value::Obj;
+    if (pc->kind == ojson::Value::Arr) {
+      for (auto& e : pc->arr)
+        if (e.get("args")) m.obj.push_back({trim_wrapped(e.get("name") ? e.get("name")->str() : ""), *e.get("args")});
+    } else {
+      m = *pc;
+    }
+    flat.obj.push_back({"pluginConfig", m});
+  }
+  if (auto* s = prof->get("seed") ? prof->get("seed") : cfg.get("seed")) flat.obj.push_back({"seed", *s});
+  return true;
+}
+
 static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
   ojson::Value doc;
   try {
@@ -2110,7 +2219,13 @@ static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
   }
   c.doc.reset(new ojson::Value(std::move(doc)));  // pods reference JSON nodes (terms)
   const ojson::Value& d = *c.doc;
-  if (auto* pr = d.get("profile")) {
+  ojson::Value flat;
+  const ojson::Value* pr = d.get("profile");
+  if (pr && (pr->get("profiles") || (pr->get("plugins") && pr->get("plugins")->kind == ojson::Value::Obj))) {
+    if (!flatten_config(*pr, flat, err)) return false;
+    pr = &flat;
+  }
+  if (pr) {
     for (auto& n : pr->get("plugins")->arr) {
       PluginId id = plugin_id(n.str());
       if (id == P_UNKNOWN) {

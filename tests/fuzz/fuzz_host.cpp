@@ -94,7 +94,38 @@ static int run_one(const std::string& text) {
   return 0;
 }
 
+// --weights FILE: the profile's resolved plugin order and weights, one
+// "position name weight store_weight" line per plugin (tests/test_fuzz_host.py).
+static int print_weights(const char* path) {
+  std::ifstream f(path, std::ios::binary);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  const std::string prof = ss.str();
+  ksg_ctx* c = nullptr;
+  ksg_opts o{};
+  o.shard_count = 1;
+  if (ksg_create(prof.data(), prof.size(), &o, &c) != KSG_OK) {
+    std::printf("error\n");
+    return 0;
+  }
+  static const char* kNames[] = {"SchedulingGates", "PrioritySort", "NodeUnschedulable", "NodeName",
+                                 "TaintToleration", "NodeAffinity", "NodePorts", "NodeResourcesFit",
+                                 "VolumeRestrictions", "EBSLimits", "GCEPDLimits", "NodeVolumeLimits",
+                                 "AzureDiskLimits", "VolumeBinding", "VolumeZone", "PodTopologySpread",
+                                 "InterPodAffinity", "DefaultPreemption", "NodeResourcesBalancedAllocation",
+                                 "ImageLocality", "DefaultBinder"};
+  for (const char* nm : kNames) {
+    const int pos = ksg_plugin_position(c, nm, std::string(nm).size());
+    int64_t w = 0, sw = 0;
+    if (pos >= 0 && ksg_plugin_weights(c, (uint32_t)pos, &w, &sw) == KSG_OK)
+      std::printf("%d %s %lld %lld\n", pos, nm, (long long)w, (long long)sw);
+  }
+  ksg_destroy(c);
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc == 3 && std::string(argv[1]) == "--weights") return print_weights(argv[2]);
   int n = 0;
   for (int i = 1; i < argc; ++i) {
     std::ifstream f(argv[i], std::ios::binary);

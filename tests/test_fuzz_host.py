@@ -125,6 +125,8 @@ def _inputs(r, n_structural, n_bytes):
              g.generate(3, n_nodes=8, n_pods=6), g.generate(4, n_nodes=8, n_existing=20, n_pods=6, n_zones=3)]
     seeds += [edge.generate_edge(v, **({"n_nodes": 8, "n_pods": 8} if v.startswith("fit") or v == "na" else
                                        {"n_nodes": 8, "n_existing": 16, "n_pods": 8})) for v in edge.EDGE_VARIANTS]
+    cfg = dict(seeds[0], profile=g.config_profile(g.DEFAULT_PROFILE, 1, score=[("NodeResourcesFit", 3)]))
+    seeds.append(cfg)  # scheduler-configuration form of the profile
     out = []
     for d in seeds:  # unmutated
         out.append(SEP.join([json.dumps(d["profile"]), json.dumps(d), json.dumps(d["queue"][0]),
@@ -174,3 +176,46 @@ def test_host_entry_points_under_sanitizers(tmp_path):
     p = subprocess.run([exe] + files, capture_output=True, text=True, timeout=600, env=env)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-6000:])
     assert f"fuzzed {len(files)} inputs" in p.stdout
+
+
+def _weights(tmp_path, prof):
+    exe = _binary()
+    f = tmp_path / "profile.json"
+    f.write_text(json.dumps(prof))
+    out = subprocess.run([exe, "--weights", str(f)], capture_output=True, text=True, timeout=60, check=True).stdout
+    if out.strip() == "error":
+        return None
+    return {ln.split()[1]: (int(ln.split()[0]), int(ln.split()[2]), int(ln.split()[3])) for ln in out.splitlines()}
+
+
+def test_scheduler_configuration_weights(tmp_path):
+    """plugins.go:289-304 getScorePluginWeight vs upstream getScoreWeights, pinned by the
+    quirk case of scheduler_test.go:344-407: Score.Enabled NodeResourcesFit weight 3 and
+    MultiPoint weight 2 -> the framework scores with 3, the store records x2."""
+    try:
+        _binary()
+    except (OSError, subprocess.CalledProcessError) as e:
+        pytest.skip(f"sanitizer build unavailable: {e}")
+    mp = [(n, 2 if n == "NodeResourcesFit" else (None if w == 1 else w)) for n, w in g.DEFAULT_PROFILE]
+    prof = g.config_profile(mp, seed=1, score=[("NodeResourcesFit", 3)])
+    w = _weights(tmp_path, prof)
+    assert w is not None
+    # MultiPoint order is the profile order
+    assert [n for n, _ in sorted(w.items(), key=lambda kv: kv[1][0])] == [n for n, _ in g.DEFAULT_PROFILE]
+    assert w["NodeResourcesFit"][1:] == (3, 2)
+    assert w["TaintToleration"][1:] == (3, 3) and w["NodeAffinity"][1:] == (2, 2)
+    assert w["PodTopologySpread"][1:] == (2, 2) and w["InterPodAffinity"][1:] == (2, 2)
+    assert w["NodeResourcesBalancedAllocation"][1:] == (1, 1) and w["ImageLocality"][1:] == (1, 1)
+    assert w["NodeName"][1:] == (1, 1)  # weight 0 / unset -> 1 (plugins.go:297-300)
+    # flat profile with the same maps resolves identically
+    flat = g.make_profile(g.DEFAULT_PROFILE, 1)
+    flat["weights"]["NodeResourcesFit"], flat["storeWeights"]["NodeResourcesFit"] = 3, 2
+    assert _weights(tmp_path, flat) == w
+    # refused: a plugin twice in MultiPoint, a Score-only plugin, per-extension-point sets
+    dup = g.config_profile([("NodeResourcesFit", 1), ("NodeResourcesFit", 2)], seed=1)
+    assert _weights(tmp_path, dup) is None
+    solo = g.config_profile([("NodeResourcesFit", 1)], seed=1, score=[("ImageLocality", 5)])
+    assert _weights(tmp_path, solo) is None
+    ext = g.config_profile([("NodeResourcesFit", 1)], seed=1)
+    ext["profiles"][0]["plugins"]["filter"] = {"enabled": [{"name": "NodeResourcesFitWrapped"}]}
+    assert _weights(tmp_path, ext) is None

@@ -146,3 +146,21 @@ def test_tiebreak_hash_matches_generator_twin():
         key = lib().ksg_oracle_pack_key(o.h, total, q, n)
         h20 = g.tiebreak_h20(seed, q, n)
         assert key == (total << 40) | ((0xFFFFF - h20) << 20) | n
+
+
+def test_config_profile_store_weight_quirk():
+    """scheduler_test.go:344-407 through the whole recording: a KubeSchedulerConfiguration
+    with Score.Enabled NodeResourcesFit weight 3 and MultiPoint weight 2.  The store's
+    finalscore is raw x 2 (getScorePluginWeight, plugins.go:289-304) while the framework
+    sums raw x 3 (getScoreWeights); same results as the flat profile with those maps."""
+    cl = fixture("plugin_extender_example")["cluster"]
+    flat = cl["profile"]
+    mp = [(n, 2 if n == "NodeResourcesFit" else flat["weights"].get(n, 1)) for n in flat["plugins"]]
+    cfg = dict(cl, profile=g.config_profile(mp, flat["seed"], score=[("NodeResourcesFit", 3)]))
+    a = run(cfg).annotations(0)
+    fin = json.loads(a[ANN + "finalscore-result"])
+    assert fin["node-282x7"]["NodeResourcesFit"] == "94" and fin["node-gp9t4"]["NodeResourcesFit"] == "146"
+    assert a[ANN + "selected-node"] == "node-gp9t4"
+    both = json.loads(json.dumps(cl))
+    both["profile"]["weights"]["NodeResourcesFit"], both["profile"]["storeWeights"]["NodeResourcesFit"] = 3, 2
+    assert run(both).annotations(0) == a

@@ -138,3 +138,38 @@ def test_annotations_from_extension_point_calls(name, c, sizes):
             assert tot == r.total, (name, i)
         checked += 1
     assert checked >= 20
+
+
+@pytest.mark.gpu
+def test_scheduler_configuration_profile():
+    """A KubeSchedulerConfiguration profile (scheduler_test.go:344-407 shape: Score.Enabled
+    re-weights MultiPoint plugins): the engine's selections use the framework weights
+    (Score wins), the recorded finalscore the store weights (MultiPoint wins,
+    plugins.go:289-304) — every pod and every annotation equal to the oracle's, and
+    Σ normalized × framework weight is the selected node's total."""
+    doc = g.generate(1, n_nodes=60, n_pods=80)
+    mp = [(n, 2 if n == "NodeResourcesFit" else (3 if n == "NodeResourcesBalancedAllocation" else w))
+          for n, w in g.DEFAULT_PROFILE]
+    cfg = g.config_profile(mp, doc["profile"]["seed"], score=[("NodeResourcesFit", 5), ("ImageLocality", 4)])
+    doc = dict(doc, profile=cfg)
+    o = Oracle(doc)
+    o.schedule(record=3)
+    s = Scheduler(cfg)
+    s.load_cluster(doc)
+    s.keep_outputs(0, len(doc["queue"]))
+    s.schedule()
+    fw = {}
+    for n, _ in g.DEFAULT_PROFILE:
+        pos = s.plugin_position(n)
+        assert pos == s.plugin_position(n + "Wrapped")
+        fw[n] = s.plugin_weights(pos)
+    assert fw["NodeResourcesFit"] == (5, 2) and fw["ImageLocality"] == (4, 1)
+    assert fw["NodeResourcesBalancedAllocation"] == (3, 3) and fw["TaintToleration"] == (3, 3)
+    for q, r in enumerate(s.results()):
+        assert (r.selected, r.feasible, r.status) == o.result(q), q
+        assert s.annotations(q) == o.annotations(q), q
+        if r.selected >= 0 and r.feasible > 1:
+            tot = sum(s.normalized_scores(q, s.plugin_position(n))[r.selected] * fw[n][0]
+                      for n in SCORERS if s.prescore_status(q, s.plugin_position(n))[0] == C_SUCCESS
+                      or n == "ImageLocality")
+            assert tot == r.total, q

@@ -9,6 +9,12 @@ placements bound (ksg_whatif).  value = pod x node pairs per second over the
 timed steps; W warm-up steps run first on the same queue.  Multi-GPU: one
 process per GPU (torch.distributed.run), nodes sharded, per-pod normalisers and
 argmax keys exchanged over RCCL after each pass.
+
+--variant pts-ipa: the same step shape with PodTopologySpread + InterPodAffinity
+on frozen domain tables (SURVEY §8(d) cfg5 "+PTS/IPA"): 1,000,000 nodes of the
+cfg4 distribution (20 zones, unique hostnames) with existing pods, profile
+Fit + PodTopologySpread + InterPodAffinity + BalancedAllocation; every pod of a
+step runs the table chain without assume, then the step is bound in pod order.
 """
 import argparse
 import json
@@ -29,6 +35,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-pods", type=int, default=48, help="pods in the CPU oracle sample (0: skip)")
     ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--variant", choices=["cfg5", "pts-ipa"], default="cfg5")
+    ap.add_argument("--existing", type=int, default=1_000_000, help="existing pods (pts-ipa variant)")
     a = ap.parse_args()
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -42,7 +50,10 @@ def main():
     from ksg import Scheduler, generator as g
     t0 = time.time()
     n_pods = a.step_pods * (a.warmup + a.steps)
-    blob = g.generate_native(5, n_nodes=a.nodes, n_pods=n_pods)  # native twin of the generator (tests/test_synth.py)
+    if a.variant == "pts-ipa":
+        blob = g.generate_native(4, n_nodes=a.nodes, n_pods=n_pods, n_existing=a.existing, n_zones=20)
+    else:
+        blob = g.generate_native(5, n_nodes=a.nodes, n_pods=n_pods)  # native twin of the generator (tests/test_synth.py)
     prof = json.loads(blob[blob.index(b'"profile"') + 10:].split(b',"nodes"', 1)[0]) if blob.startswith(b'{"profile"') \
         else json.loads(blob)["profile"]
     print(f"[rank {rank}] generated {a.nodes} nodes / {n_pods} pods in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
@@ -60,7 +71,7 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    s.sample_kernel(1)
+    s.sample_kernel(1 if a.variant == "cfg5" else 64)  # (pts-ipa: one k_eval in 64 pods)
     t0 = time.perf_counter()
     pass_ms = [0.0, 0.0]
     for k in range(a.warmup, a.warmup + a.steps):
@@ -85,20 +96,30 @@ def main():
     # columns read by the pod's requirements 16 B) = 80 B x shard x ceil(P/32)
     tiles = (P + 31) // 32
     bytes_per_launch = 80.0 * shard * tiles
+    kernel = "k_whatif (pass avg)"
+    note = ("latency-bound: ~3 B/pair of node-row traffic; PMC (profiles/r02_cfg5_pmc_sq.csv) shows VALU busy "
+            "4-6 % and most wave time waiting on memory")
+    workload = f"cfg5: {a.nodes} nodes, {P} pods/step, TaintToleration+NodeAffinity+Fit+BA"
+    if a.variant == "pts-ipa":  # table chain: k_eval reads 68 B per node (row 56, zone id 4, class count 8)
+        bytes_per_launch = 68.0 * shard
+        kernel = "k_eval (table chain, sampled pods)"
+        note = "per-pod table chain over frozen class tables; sequence of dependent memory round trips per pod"
+        workload = (f"cfg5+PTS/IPA: {a.nodes} nodes (cfg4 distribution, {a.existing} existing pods, 20 zones), "
+                    f"{P} pods/step, Fit+PodTopologySpread+InterPodAffinity+BA on frozen domain tables")
     kernel_ms = pass_ms[0] / a.steps
     out = {
-        "metric": "what-if filter+score pod x node pairs/sec (1M nodes, 4,096 pods/step)",
+        "metric": "what-if filter+score pod x node pairs/sec (1M nodes, 4,096 pods/step)"
+                  + (", PTS/IPA" if a.variant == "pts-ipa" else ""),
         "value": pairs / elapsed, "unit": "pairs/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": elapsed * 1e3 / a.steps, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "int64+f64", "data": "synthetic (seeded generator, SURVEY.md §8(d) cfg5)",
-        "config": {"workload": f"cfg5: {a.nodes} nodes, {P} pods/step, TaintToleration+NodeAffinity+Fit+BA",
+        "config": {"workload": workload,
                    "nodes_total": a.nodes, "nodes_per_gpu": shard, "pods_per_step": P,
                    "parallelism": f"node-shard x{world}" if world > 1 else "1 GPU"},
         "scheduled_per_step": sum(1 for r in res if r.status == 0) / a.steps,
         "roofline": {"bound": "hbm", "achieved": bytes_per_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms else 0.0,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": "k_whatif (pass avg)",
-                     "kernel_avg_ms": kernel_ms, "bytes_per_launch": bytes_per_launch,
-                     "note": "VALU-bound: ~3 B/pair of node-row traffic against ~200-400 integer/f64 ops per pair"},
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": kernel,
+                     "kernel_avg_ms": kernel_ms, "bytes_per_launch": bytes_per_launch, "note": note},
     }
     out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS
     if a.cpu_pods and world == 1:  # the oracle's what-if step on a bounded sample of the same cluster

@@ -1689,6 +1689,26 @@ __global__ void k_whatif_bind(DevCluster C, WiArgs A) {
   atomicAdd(&C.podcnt[n], 1);
 }
 
+// Bind a step's placements one pod after another, in queue order (the order
+// ksg_oracle_whatif applies its deferred AddPods): for profiles with class tables
+// and an existing-pod table, whose appends must stay sequential.  One wave: the
+// lanes apply a pod's class-table deltas, lane 0 its node row and table row.
+__global__ __launch_bounds__(64) void k_whatif_bind_seq(DevCluster C, const uint8_t* __restrict__ progs,
+                                                        const uint64_t* __restrict__ prog_off,
+                                                        const ksg_pod_summary* sums, uint32_t q0, uint32_t count,
+                                                        int table, int32_t* prow) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t j = q0; j < q0 + count; ++j) {
+    const ksg_pod_summary& s = sums[j];
+    const uint32_t g = (uint32_t)s.selected, n = g - C.goff;
+    if (s.status != 0 || g < C.goff || n >= C.N) continue;  // unscheduled, or another shard owns the node
+    const ProgView V = view(progs + prog_off[j]);
+    tables_assume(C, V, n, +1, lane, 64);
+    if (lane == 0) assume_pod(C, V, n, +1, table != 0, prow + j, 64);
+    __syncthreads();
+  }
+}
+
 // Sharded steps: merge the ranks' summaries of the step's pods
 // (phase 1: feasible counts and score max/min; phase 2: argmax key, status bits).
 __global__ void k_whatif_merge(const ksg_pod_summary* recv, uint32_t ranks, uint32_t count, ksg_pod_summary* sums,
@@ -4253,11 +4273,23 @@ static bool exchange(Engine::Impl& I, const void* src, size_t bytes, std::string
 
 bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
   Impl& I = *p_;
-  if (I.has_pts || I.has_ipa || !I.batch_ok) {
-    err = "what-if steps support NodeResourcesFit / BalancedAllocation / TaintToleration / NodeAffinity profiles";
-    return false;
-  }
   if (first + count > I.prog_off.size()) { err = "program index out of range"; return false; }
+  if (I.has_pts || I.has_ipa || !I.batch_ok) {
+    // Profiles with cross-node state (PodTopologySpread / InterPodAffinity domain
+    // counts, or plugins k_whatif does not evaluate): every pod of the step runs
+    // its cycle without assume — the table chain reads the class tables, which
+    // stay frozen for the whole step — then the step's placements are bound in
+    // pod order (rows, host ports, class tables, existing-pod table rows).
+    if (!run_queue(first, count, false, err)) return false;
+    if (count) {
+      const bool tables = I.has_pts || I.has_ipa;
+      hipLaunchKernelGGL(k_whatif_bind_seq, dim3(1), dim3(64), 0, I.stream, I.cluster(), I.progs.p, I.prog_off_d.p,
+                         I.sums.p, first, count, tables ? 1 : 0, I.prow.p);
+      HIPCHK(hipEventRecord(I.ev1, I.stream));
+      HIPCHK(hipGetLastError());
+    }
+    return true;
+  }
   hipStream_t s = I.stream;
   DevCluster C = I.cluster();
   WiArgs A{};

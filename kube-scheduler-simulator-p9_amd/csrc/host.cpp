@@ -3208,6 +3208,12 @@ int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   if (c.shards != 1 && c.eng->exchange_ranks() != c.shards)
     return ctx->fail("sharded context: call ksg_set_exchange first", KSG_E_STATE);
   if (!c.compile_queue()) return ctx->fail(c.err, KSG_E_INVALID);
+  if (!c.refresh_programs(first, count)) return ctx->fail(c.err, KSG_E_DEVICE);
+  if (c.tables_on()) {  // the step's binds append its pods to the existing-pod table
+    uint64_t need[4] = {0, 0, 0, 0};
+    for (uint32_t q = first; q < first + count; ++q) c.queue_need(q, need);
+    if (!c.ensure_room(need)) return ctx->fail(c.err, KSG_E_DEVICE);
+  }
   if (!c.eng->run_whatif(first, count, c.err)) return ctx->fail(c.err, KSG_E_STATE);
   c.mark_run(first, count);
   return KSG_OK;

@@ -1,6 +1,8 @@
 """GPU parity of what-if steps (BASELINE.json cfg5: a step of pods scored against
 one frozen snapshot, placements bound between steps) against the oracle's
-ksg_oracle_whatif, single context and node-sharded (host exchange over gloo)."""
+ksg_oracle_whatif, single context and node-sharded (host exchange over gloo).
+Profiles with PodTopologySpread / InterPodAffinity (cfg4) score every pod of a
+step on frozen domain tables and bind the step in queue order."""
 import json
 import os
 import socket
@@ -24,8 +26,10 @@ def _oracle_steps(doc, steps, record=0, keep=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("c,sizes", [(5, dict(n_nodes=1500, n_pods=3 * STEP)), (2, dict(n_nodes=800, n_pods=2 * STEP))],
-                         ids=["cfg5", "cfg2"])
+@pytest.mark.parametrize("c,sizes", [(5, dict(n_nodes=1500, n_pods=3 * STEP)), (2, dict(n_nodes=800, n_pods=2 * STEP)),
+                                     (4, dict(n_nodes=600, n_existing=2400, n_pods=3 * STEP, n_zones=6)),
+                                     (1, dict(n_nodes=100, n_pods=2 * STEP))],
+                         ids=["cfg5", "cfg2", "cfg4-pts-ipa", "cfg1-default-profile"])
 def test_whatif_steps_match_oracle(c, sizes):
     doc = g.generate(c, **sizes)
     steps = len(doc["queue"]) // STEP
@@ -76,8 +80,10 @@ def _sharded_worker(rank, world, port, doc_json, out):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
-def test_sharded_whatif_matches_oracle(world):
-    doc = g.generate(5, n_nodes=1200, n_pods=2 * STEP)
+@pytest.mark.parametrize("c", [5, 4], ids=["cfg5", "cfg4-pts-ipa"])
+def test_sharded_whatif_matches_oracle(world, c):
+    doc = (g.generate(5, n_nodes=1200, n_pods=2 * STEP) if c == 5 else
+           g.generate(4, n_nodes=300, n_existing=1200, n_pods=2 * STEP, n_zones=4))
     o = _oracle_steps(doc, 2)
     want = [o.result(q) for q in range(o.n_queue)]
     port = _free_port()

@@ -88,7 +88,10 @@ void ksg_destroy(ksg_ctx* ctx);
 const char* ksg_last_error(const ksg_ctx* ctx);
 int ksg_abi_version(void);
 
-/* Snapshot: {"nodes": [v1.Node], "pods": [bound v1.Pod], "queue": [v1.Pod]} .
+/* Snapshot: {"nodes": [v1.Node], "pods": [bound v1.Pod], "queue": [v1.Pod],
+ * "pvs": [v1.PersistentVolume], "pvcs": [v1.PersistentVolumeClaim],
+ * "storageClasses": [storagev1.StorageClass]} (ResourcesForSnap field names; the
+ * storage objects feed the volume plugins).
  * Replaces the device snapshot (UpdateSnapshot) and the queue. */
 int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len);
 int ksg_num_nodes(const ksg_ctx* ctx);     /* global node count */
@@ -102,9 +105,12 @@ int ksg_wait(ksg_ctx* ctx, float* device_ms);
 /* What-if step (BASELINE cfg5): queue pods [first, first+count) are each
  * scheduled against the SAME snapshot (no assume between them: the question
  * "where would each of these pods go now?"), then all their placements are
- * bound together.  Profiles of NodeResourcesFit, BalancedAllocation,
- * TaintToleration and NodeAffinity; sharded contexts reduce the per-pod
- * feasible counts, normaliser max/min and argmax keys across ranks.
+ * bound together, in queue order.  Any profile: NodeResourcesFit /
+ * BalancedAllocation / TaintToleration / NodeAffinity profiles run as two
+ * pod-tile x node-tile passes; others (PodTopologySpread / InterPodAffinity on
+ * frozen class tables, the default profile) run every pod's cycle without
+ * assume.  Sharded contexts reduce the per-pod feasible counts, normaliser
+ * max/min and argmax keys across ranks.
  * Asynchronous like ksg_schedule_queue; results via ksg_pod_results. */
 int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count);
 int ksg_pod_results(ksg_ctx* ctx, uint32_t first, uint32_t count, ksg_pod_result* out);
@@ -143,7 +149,8 @@ int ksg_set_exchange(ksg_ctx* ctx, int mode, const uint8_t* nccl_id, ksg_exchang
  * annotation rendering).  Must precede ksg_schedule_queue. */
 int ksg_keep_outputs(ksg_ctx* ctx, uint32_t first, uint32_t count);
 /* Filter code per local node: KSG_FILTER_PASSED, KSG_FILTER_NOT_EVALUATED or
- * (profile position << 24) | detail. */
+ * (profile position << 24) | detail (volume plugins: KSG_VOL_* reason bits of
+ * ksg_types.h in the low 16 bits). */
 int ksg_filter_codes(ksg_ctx* ctx, uint32_t q, uint32_t* out, uint32_t n);
 /* Raw Score of profile position pos per local node (valid where the filter passed). */
 int ksg_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* out, uint32_t n);
@@ -190,6 +197,12 @@ int ksg_node_index(const ksg_ctx* ctx, const char* name, size_t len);       /* o
  * PreFilterResult node set as a JSON array of node names, "null" for all nodes. */
 int ksg_prefilter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code, char* msg, size_t cap, size_t* len);
 int ksg_prefilter_result(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len);
+/* The PreFilterResult of the plugin at profile position pos (NodeAffinity's, or
+ * VolumeBinding's GetEligibleNodes for claims bound to local PVs): JSON array of
+ * node names, "null" when the plugin returns none.  The framework intersects them;
+ * an empty intersection rejects the pod after the later plugin's PreFilter, whose
+ * own status stays Success (ksg_prefilter_status). */
+int ksg_prefilter_result_pos(ksg_ctx* ctx, uint32_t q, uint32_t pos, char* buf, size_t cap, size_t* len);
 /* Filter (wrappedplugin.go:535, mock framework.go:114) on one node. */
 int ksg_filter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, uint32_t node, int32_t* code, char* msg, size_t cap,
                       size_t* len);

@@ -50,6 +50,7 @@ struct NodeSoA {
   std::vector<uint32_t> img_bits;
   uint32_t n_ports = 0;                   // NodePorts: used host-port triple counts [n_ports][n]
   std::vector<int32_t> port_count;
+  std::vector<int32_t> pvc_use;           // VolumeRestrictions: pods using each PVC id (bound pods of the whole cluster)
   // node-label vocabulary numeric view (Gt/Lt): per key offset into value tables
   std::vector<uint32_t> key_val_off;      // [n_keys+1]
   std::vector<int64_t> val_num;

@@ -112,6 +112,7 @@ struct DevCluster {
   const uint32_t* img;     // [img_words][N]
   uint32_t n_ports;
   int32_t* ports;          // [n_ports][N] used host-port triple counts
+  int32_t* pvcuse;         // [PVC ids] pods (bound + assumed) using the claim: NodeInfo PVCRefCounts summed
   DevTables T;
   // per topology slot, by value for fully unrolled loops (no load): its node
   // label key and its base among the shared-key pairs (-1: one node per value)
@@ -175,6 +176,7 @@ struct ProgView {
   const ksg_sel* sel;
   const ksg_aterm* at;
   const ksg_exist_term* et;
+  const ksg_vchk* vchk;
 };
 
 __device__ __forceinline__ ProgView view(const uint8_t* p) {
@@ -186,6 +188,7 @@ __device__ __forceinline__ ProgView view(const uint8_t* p) {
   v.sel = reinterpret_cast<const ksg_sel*>(p + v.h->off_sel);
   v.at = reinterpret_cast<const ksg_aterm*>(p + v.h->off_aterm);
   v.et = reinterpret_cast<const ksg_exist_term*>(p + v.h->off_eterm);
+  v.vchk = reinterpret_cast<const ksg_vchk*>(v.i32 + v.h->vchk_off);
   return v;
 }
 
@@ -422,6 +425,36 @@ __device__ __forceinline__ int64_t image_score(const DevCluster& C, const ProgVi
   }
   sum = sum < kMin ? kMin : (sum > kMax ? kMax : sum);
   return 100 * (sum - kMin) / (kMax - kMin);
+}
+
+// Volume plugins of the run at device position pos (KP_VOLUMES): the pod's checks
+// for that position, grouped by plugin in profile order (VolumeRestrictions'
+// ReadWriteOncePod conflict, VolumeBinding's PV node affinity / provisioning
+// topology / selected node, VolumeZone's PV zone labels, pod-uniform verdicts;
+// compiled by the host from the PreFilter state, host.cpp compile_volumes).
+// 0: every plugin passes; else (plugin index in the run << 16) | reason bits.
+__device__ uint32_t volume_filter(const DevCluster& C, const ProgView& V, int pos, uint32_t n) {
+  const int nv = V.h->n_vchk;
+  int sub = -1;
+  uint32_t bits = 0;
+  for (int i = 0; i < nv; ++i) {
+    const ksg_vchk c = V.vchk[i];
+    if (c.dpos != pos) continue;
+    if (c.sub != sub) {
+      if (bits) break;
+      sub = c.sub;
+    }
+    if (bits & (uint32_t)c.unless) continue;
+    bool fail = true;
+    if (c.kind == KSG_VCHK_SELS) {
+      for (int t = 0; t < c.cnt && fail; ++t) fail = !node_sel(C, V, V.sel[c.off + t], n);
+    } else if (c.kind == KSG_VCHK_USED) {
+      fail = false;
+      for (int t = 0; t < c.cnt && !fail; ++t) fail = C.pvcuse[V.i32[c.off + t]] > 0;
+    }
+    if (fail) bits |= (uint32_t)c.bits;
+  }
+  return bits ? ((uint32_t)sub << 16) | bits : 0u;
 }
 
 __device__ __forceinline__ uint32_t fit_filter(const DevCluster& C, const ProgView& V, uint32_t n) {
@@ -955,6 +988,10 @@ __global__ __launch_bounds__(kBlock) void k_filter_score(DevCluster C, DevProfil
         case KP_PORTS:
           if (!(h->flags & KPF_SKIP_PORTS)) fail = ports_fail(C, V, n);
           break;
+        case KP_VOLUMES:
+          detail = volume_filter(C, V, pos, n);
+          fail = detail != 0;
+          break;
         default: break;
       }
       if (fail) {
@@ -1252,6 +1289,7 @@ __device__ void assume_pod(DevCluster& C, const ProgView& V, uint32_t n, int sig
   C.nzm[n] += sign * h->nz_mem;
   C.podcnt[n] += sign;
   for (int i = 0; i < h->n_port_own; ++i) C.ports[(size_t)V.i32[h->port_own_off + i] * C.N + n] += sign;
+  for (int i = 0; i < h->n_pvc; ++i) atomicAdd(&C.pvcuse[V.i32[h->pvc_off + i]], sign);
   if (sign < 0) {
     if (prow && *prow >= 0) {
       C.ptflags[*prow] |= KEF_DELETED;
@@ -3570,6 +3608,8 @@ struct Engine::Impl {
   DBuf<uint8_t> haslab, vok, nflags;
   DBuf<uint32_t> img;
   DBuf<int32_t> ports, ports0;
+  DBuf<int32_t> pvcuse, pvcuse0;  // PVC use counts (VolumeRestrictions ReadWriteOncePod)
+  uint32_t n_pvc = 0;
   uint32_t img_words = 0, n_ports = 0;
   NodeSoA topo;  // topology tables (host copy)
   DBuf<int32_t> topo_key_d;
@@ -3678,6 +3718,7 @@ struct Engine::Impl {
     C.allowed = allowed.p; C.podcnt = podcnt.p; C.label = label.p; C.toff = toff.p; C.tid = tid.p;
     C.haslab = haslab.p; C.kvo = kvo.p; C.vnum = vnum.p; C.vok = vok.p;
     C.nflags = nflags.p; C.img_words = img_words; C.img = img.p; C.n_ports = n_ports; C.ports = ports.p;
+    C.pvcuse = pvcuse.p;
     C.n_topo = (uint32_t)topo.topo_key.size();
     C.pairs = topo.topo_pairs;
     C.tkey = topo_key_d.p;
@@ -3839,6 +3880,10 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     if (!I.nflags.upload(nf, s, err) || !I.img.upload(ns.img_bits, s, err) || !I.ports.upload(ns.port_count, s, err) ||
         !I.ports0.upload(ns.port_count, s, err))
       return false;
+    std::vector<int32_t> pu = ns.pvc_use;
+    pu.resize(std::max<size_t>(pu.size(), 1), 0);
+    I.n_pvc = (uint32_t)pu.size();
+    if (!I.pvcuse.upload(pu, s, err) || !I.pvcuse0.upload(pu, s, err)) return false;
   }
   I.topo = NodeSoA();
   I.topo.topo_key = ns.topo_key;
@@ -5014,6 +5059,7 @@ bool Engine::reset(std::string& err) {
   HIPCHK(hipMemcpyAsync(I.podcnt.p, I.podcnt0.p, (size_t)I.N * 4, hipMemcpyDeviceToDevice, s));
   if (I.n_ports)
     HIPCHK(hipMemcpyAsync(I.ports.p, I.ports0.p, (size_t)I.n_ports * I.N * 4, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.pvcuse.p, I.pvcuse0.p, (size_t)I.n_pvc * 4, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemcpyAsync(I.tcounts.p, I.counts0, sizeof(I.counts0), hipMemcpyHostToDevice, s));
   if (!rebuild_class_tables(err)) return false;  // from the restored existing-pod table
   uint32_t cnt = (uint32_t)I.prog_off.size();

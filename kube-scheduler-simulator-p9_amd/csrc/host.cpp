@@ -269,7 +269,8 @@ struct Pod {
   int n_containers = 0;   // init + regular
   struct HostPort { string ip, proto; int32_t port; };
   vector<HostPort> ports; // Spec.Containers host ports (hostPort > 0), sanitised
-  bool volume_plugins_act = false;  // a volume the volume plugins would not Skip
+  bool volume_plugins_act = false;  // a volume other than a PVC the volume plugins act on (not modelled)
+  vector<string> claims;            // spec.volumes[].persistentVolumeClaim.claimName, in volume order
   i64 priority = 0;                 // spec.priority (PrioritySort order is the caller's; DefaultPreemption)
   bool preempt_never = false;       // spec.preemptionPolicy Never (PodEligibleToPreemptOthers)
   i64 start_time = INT64_MAX;       // status.startTime, epoch seconds; none: started last (GetPodStartTime: now)
@@ -380,10 +381,12 @@ static Pod parse_pod(const J& v) {
           }
       }
   if (auto* vs = (*sp)["volumes"])
-    for (auto& v : vs->items)
-      for (const char* k : {"persistentVolumeClaim", "ephemeral", "gcePersistentDisk", "awsElasticBlockStore", "rbd",
-                            "iscsi", "azureDisk", "cinder", "csi"})
+    for (auto& v : vs->items) {
+      if (const J* c = v["persistentVolumeClaim"]; c && !c->null()) p.claims.push_back(str_of((*c)["claimName"]));
+      for (const char* k : {"ephemeral", "gcePersistentDisk", "awsElasticBlockStore", "rbd", "iscsi", "azureDisk",
+                            "cinder", "csi"})
         if (v[k] && !v[k]->null()) p.volume_plugins_act = true;
+    }
   if (auto* ns = (*sp)["nodeSelector"]; ns && !ns->null()) {
     p.has_node_sel = true;
     p.node_sel = smap(ns);
@@ -609,7 +612,19 @@ static bool profile_from_config(const J& in, J& out, string& err) {
   return true;
 }
 
-static bool host_only(int p) { return p == P_VOLUME || p == P_VOLBIND || p == P_NOOP; }
+static bool host_only(int p) { return p == P_NOOP; }
+static bool is_volume(int p) { return p == P_VOLUME || p == P_VOLBIND; }
+// the volume plugins by behaviour (v1.30.4 plugins/volumerestrictions, nodevolumelimits
+// non_csi.go / csi.go, volumebinding, volumezone)
+enum { VK_NONE = 0, VK_RESTRICT, VK_NONCSI, VK_CSI, VK_ZONE, VK_BIND };
+static int volume_kind(const string& n) {
+  if (n == "VolumeRestrictions") return VK_RESTRICT;
+  if (n == "EBSLimits" || n == "GCEPDLimits" || n == "AzureDiskLimits") return VK_NONCSI;
+  if (n == "NodeVolumeLimits") return VK_CSI;
+  if (n == "VolumeZone") return VK_ZONE;
+  if (n == "VolumeBinding") return VK_BIND;
+  return VK_NONE;
+}
 // extension points the original plugin implements (the wrapper records only those)
 static bool has_prefilter(int p) {
   return p == P_FIT || p == P_NA || p == P_PTS || p == P_IPA || p == P_PORTS || p == P_VOLUME || p == P_VOLBIND;
@@ -629,7 +644,100 @@ struct PodMeta {
   bool ipa_no_req_terms = true;
   bool ipa_prescore_skip_static = false;
   bool na_prescore_error = false;
+  // volume plugins
+  uint32_t vol_skip = 0;           // bit = profile position: PreFilter returned Skip
+  bool vb_restricted = false;      // VolumeBinding PreFilterResult (GetEligibleNodes)
+  vector<string> vb_names;
+  bool merge_reject = false;       // the framework's PreFilterResult merge came out empty at prefilter_fail_pos
 };
+
+// ---------------------------------------------------------------- storage objects
+// ResourcesForSnap pvs / pvcs / storageClasses (snapshot.go:33-42), as the volume
+// plugins of v1.30.4 read them.
+struct PVC {
+  string ns, name, volume_name, cls;  // cls: storagehelpers.GetPersistentVolumeClaimClass
+  bool bind_completed = false;        // pv.kubernetes.io/bind-completed present (isPVCFullyBound)
+  bool deleting = false, lost = false, rwop = false;
+  bool has_selected = false;          // volume.kubernetes.io/selected-node
+  string selected;
+};
+struct PV {
+  string name, cls;                   // cls: GetPersistentVolumeClass
+  map<string, string> labels;
+  const J* required = nullptr;        // spec.nodeAffinity.required (NodeSelector)
+  bool claimed = false;               // spec.claimRef
+  string cref_ns, cref_name;
+  bool csi = false, intree = false;   // spec.csi / an in-tree cloud disk source
+};
+struct SClass {
+  string name, provisioner;
+  bool has_mode = false, wffc = false;  // volumeBindingMode set / WaitForFirstConsumer
+  const J* allowed = nullptr;           // allowedTopologies
+};
+static const char* kBetaClassAnn = "volume.beta.kubernetes.io/storage-class";
+static PVC parse_pvc(const J& v) {
+  PVC c;
+  const J* md = v["metadata"];
+  const J* sp = v["spec"];
+  c.name = md ? str_of((*md)["name"]) : "";
+  c.ns = md ? str_of((*md)["namespace"]) : "";
+  if (c.ns.empty()) c.ns = "default";
+  const J* ann = md ? (*md)["annotations"] : nullptr;
+  c.deleting = md && (*md)["deletionTimestamp"] && !(*md)["deletionTimestamp"]->null();
+  if (sp) {
+    c.volume_name = str_of((*sp)["volumeName"]);
+    if (const J* sc = (*sp)["storageClassName"]; sc && !sc->null()) c.cls = sc->text();
+    for (auto& m : slist((*sp)["accessModes"])) c.rwop |= m == "ReadWriteOncePod";
+  }
+  if (ann && (*ann)[kBetaClassAnn]) c.cls = str_of((*ann)[kBetaClassAnn]);
+  c.bind_completed = ann && (*ann)["pv.kubernetes.io/bind-completed"];
+  if (ann && (*ann)["volume.kubernetes.io/selected-node"]) {
+    c.has_selected = true;
+    c.selected = str_of((*ann)["volume.kubernetes.io/selected-node"]);
+  }
+  if (const J* st = v["status"]) c.lost = str_of((*st)["phase"]) == "Lost";
+  return c;
+}
+static PV parse_pv(const J& v) {
+  PV p;
+  const J* md = v["metadata"];
+  const J* sp = v["spec"];
+  p.name = md ? str_of((*md)["name"]) : "";
+  p.labels = smap(md ? (*md)["labels"] : nullptr);
+  const J* ann = md ? (*md)["annotations"] : nullptr;
+  if (sp) {
+    p.cls = str_of((*sp)["storageClassName"]);
+    if (const J* na = (*sp)["nodeAffinity"]; na && !na->null())
+      if (const J* rq = (*na)["required"]; rq && !rq->null()) p.required = rq;
+    if (const J* cr = (*sp)["claimRef"]; cr && !cr->null()) {
+      p.claimed = true;
+      p.cref_ns = str_of((*cr)["namespace"]);
+      p.cref_name = str_of((*cr)["name"]);
+    }
+    p.csi = (*sp)["csi"] && !(*sp)["csi"]->null();
+    for (const char* k : {"awsElasticBlockStore", "gcePersistentDisk", "azureDisk", "cinder"})
+      if ((*sp)[k] && !(*sp)[k]->null()) p.intree = true;
+  }
+  if (ann && (*ann)[kBetaClassAnn]) p.cls = str_of((*ann)[kBetaClassAnn]);
+  return p;
+}
+static SClass parse_sc(const J& v) {
+  SClass c;
+  const J* md = v["metadata"];
+  c.name = md ? str_of((*md)["name"]) : "";
+  c.provisioner = str_of(v["provisioner"]);
+  if (const J* m = v["volumeBindingMode"]; m && !m->null()) {
+    c.has_mode = true;
+    c.wffc = m->text() == "WaitForFirstConsumer";
+  }
+  if (const J* a = v["allowedTopologies"]; a && !a->null()) c.allowed = a;
+  return c;
+}
+// in-tree provisioners the non-CSI limits plugins count (non_csi.go matchProvisioner)
+static bool intree_provisioner(const string& p) {
+  return p == "kubernetes.io/aws-ebs" || p == "kubernetes.io/gce-pd" || p == "kubernetes.io/azure-disk" ||
+         p == "kubernetes.io/cinder";
+}
 
 struct Cluster {
   // profile
@@ -638,7 +746,8 @@ struct Cluster {
   string names[KSG_MAX_PROFILE];
   i64 fw_w[KSG_MAX_PROFILE] = {}, store_w[KSG_MAX_PROFILE] = {};
   int dpos[KSG_MAX_PROFILE] = {};  // device profile position of each plugin (-1: host-only)
-  int fpos[KSG_MAX_PLUGINS] = {};  // profile position of each device position
+  int fpos[KSG_MAX_PLUGINS] = {};  // profile position of each device position (a volume run: its first plugin)
+  int vkind[KSG_MAX_PROFILE] = {};  // VK_* of each profile position
   int n_dev = 0;
   bool has_volume_plugins = false;
   Dict images;  // ImageLocality: every image name some node lists
@@ -657,6 +766,12 @@ struct Cluster {
   std::unordered_map<string, uint32_t> bound_at;  // "ns\x1fname" -> index in bound (in-place events)
   bool bound_at_valid = false;
   vector<Pod> queue;
+  // storage (volume plugins)
+  std::map<string, PVC> pvcs;  // "ns/name"
+  std::map<string, PV> pvs;
+  std::map<string, SClass> classes;
+  bool attach_limits = false;  // some node declares volume attach limits (csiNodes / attachable-volumes-*)
+  Dict pvc_ids;                // PVC keys "ns/name" the pods use (device use counts)
   // vocabularies
   Dict res;  // resource columns
   Dict nkeys;
@@ -753,13 +868,19 @@ struct Cluster {
     }
     n_dev = 0;
     for (int i = 0; i < n_plugins; ++i) {
-      has_volume_plugins |= plugins[i] == P_VOLUME || plugins[i] == P_VOLBIND;
+      const bool vol = is_volume(plugins[i]);
+      has_volume_plugins |= vol;
+      vkind[i] = volume_kind(names[i]);
       dpos[i] = -1;
       if (host_only(plugins[i])) continue;
+      if (vol && i > 0 && is_volume(plugins[i - 1])) {  // consecutive volume plugins share one KP_VOLUMES position
+        dpos[i] = dpos[i - 1];
+        continue;
+      }
       if (n_dev >= KSG_MAX_PLUGINS) { err = "too many plugins with device work"; return false; }
       dpos[i] = n_dev;
       fpos[n_dev] = i;
-      ecfg.plugins[n_dev] = plugins[i];
+      ecfg.plugins[n_dev] = vol ? KP_VOLUMES : plugins[i];
       ecfg.weight[n_dev] = fw_w[i];
       n_dev++;
     }
@@ -1155,6 +1276,8 @@ struct Cluster {
       if (scalar_name(kv.first) && res.get(kv.first) < 0) return false;
     for (auto& h : p.ports)
       if (!port_id.count(std::make_tuple(h.ip, h.proto, h.port))) return false;
+    for (auto& c : p.claims)
+      if (pvc_ids.get(p.ns + "/" + c) < 0) return false;  // the device PVC use counts: re-encode
     return true;
   }
   // Intern pod p's label space in place; new label keys widen the device's
@@ -1167,6 +1290,10 @@ struct Cluster {
   }
 
   bool build_vocab() {
+    pvc_ids = Dict();
+    for (auto* v : {&bound, &queue})
+      for (auto& p : *v)
+        for (auto& c : p.claims) pvc_ids.add(p.ns + "/" + c);
     res = Dict();
     res.add("cpu");
     res.add("memory");
@@ -1301,6 +1428,11 @@ struct Cluster {
     S.img_bits.assign((size_t)S.img_words * n, 0);
     S.n_ports = (uint32_t)port_id.size();
     S.port_count.assign((size_t)S.n_ports * n, 0);
+    // PVCRefCounts of the bound pods, summed over the whole cluster (IsPVCUsedByPods)
+    S.pvc_use.assign(pvc_ids.names.size(), 0);
+    for (auto& p : bound)
+      if (node_names.get(p.node) >= 0)
+        for (auto& c : p.claims) S.pvc_use[pvc_ids.get(p.ns + "/" + c)] += 1;
     S.taint_off.assign(n + 1, 0);
     for (uint32_t i = 0; i < n; ++i) {
       const Node& nd = nodes[lo + i];
@@ -1478,7 +1610,8 @@ struct Cluster {
   }
 
   // node selector term (component-helpers nodeSelectorTerm); false on parse error
-  bool compile_node_term(const J& t, Prog& P, ksg_sel& out) {
+  // labels_only: the node carries only its labels (volume.CheckNodeAffinity): fields read ""
+  bool compile_node_term(const J& t, Prog& P, ksg_sel& out, bool labels_only = false) {
     out = ksg_sel{1, (int32_t)P.req.size(), 0, 0};
     vector<ksg_req> rs;
     if (const J* me = t["matchExpressions"])
@@ -1514,7 +1647,7 @@ struct Cluster {
         if ((op != "In" && op != "NotIn") || vals.size() != 1) return false;
         ksg_req q{};
         q.key = -1;
-        if (key == "metadata.name") {
+        if (key == "metadata.name" && !labels_only) {
           q.op = op == "In" ? KR_NAME_EQ : KR_NAME_NE;
           q.num = node_names.get(vals[0]);  // -1: no such node
         } else {  // other fields read "" on a node
@@ -1548,6 +1681,382 @@ struct Cluster {
     t.weight = a.weight;
     t.cls = tables_on() ? pclass(false, {a}) : -1;
     t.nub = nub_of(t.topo);
+  }
+
+  // ------------------------------------------------------------ volume plugins
+  // Upstream v1.30.4 plugins/volumerestrictions, nodevolumelimits (non_csi.go,
+  // csi.go), volumebinding (volume_binding.go, binder.go FindPodVolumes) and
+  // volumezone: their PreFilter runs here on the storage objects; each Filter
+  // becomes device checks on the node's labels / name (KP_VOLUMES) and, for
+  // ReadWriteOncePod claims, on the device's PVC use counts.
+  bool has_vkind(int k) const {
+    for (int i = 0; i < n_plugins; ++i)
+      if (vkind[i] == k) return true;
+    return false;
+  }
+  const PVC* pvc_of(const string& ns, const string& name) const {
+    auto it = pvcs.find(ns + "/" + name);
+    return it == pvcs.end() ? nullptr : &it->second;
+  }
+  const PV* pv_of(const string& n) const {
+    auto it = pvs.find(n);
+    return it == pvs.end() ? nullptr : &it->second;
+  }
+  const SClass* class_of(const string& n) const {
+    auto it = classes.find(n);
+    return it == classes.end() ? nullptr : &it->second;
+  }
+  static bool fully_bound(const PVC& c) { return !c.volume_name.empty() && c.bind_completed; }  // isPVCFullyBound
+  bool delay_binding(const PVC& c) const {  // volume.IsDelayBindingMode (a class without a mode is refused)
+    if (c.cls.empty()) return false;
+    const SClass* sc = class_of(c.cls);
+    return sc && sc->has_mode && sc->wffc;
+  }
+  // Inputs whose volume-plugin results this build does not model are refused
+  // with an error, never approximated.
+  bool volumes_modelled(const Pod& p) {
+    if (!has_volume_plugins) return true;
+    auto no = [&](const string& why) {
+      err = "pod " + p.name + ": " + why + " (not modelled)";
+      return false;
+    };
+    if (p.volume_plugins_act) return no("volumes other than persistentVolumeClaim");
+    if (p.claims.empty()) return true;
+    if (shards != 1) return no("persistent volume claims on a sharded context");
+    if (attach_limits && has_vkind(VK_CSI)) return no("nodes declaring volume attach limits");
+    const bool rejecting = has_vkind(VK_RESTRICT) || has_vkind(VK_BIND) || has_vkind(VK_ZONE);
+    auto users = [&](const string& ns, const string& cn, bool queue_too) {
+      int u = 0;
+      for (auto* v : {&bound, &queue}) {
+        if (v == &queue && !queue_too) continue;
+        for (auto& o : *v)
+          for (auto& x : o.claims) u += o.ns == ns && x == cn;
+      }
+      return u;
+    };
+    for (auto& cn : p.claims) {
+      const PVC* c = pvc_of(p.ns, cn);
+      if (!c) {
+        if (!rejecting) return no("a missing claim no PreFilter rejects");
+        continue;
+      }
+      if (const PV* v = c->volume_name.empty() ? nullptr : pv_of(c->volume_name); v && v->intree)
+        return no("an in-tree cloud disk persistent volume");
+      if (c->rwop && has_preemption()) {  // RemovePod counts by claim name (volume_restrictions.go)
+        if (users(p.ns, cn, false) > 1) return no("a ReadWriteOncePod claim used by several bound pods");
+        for (auto* v : {&bound, &queue})
+          for (auto& o : *v)
+            for (auto& x : o.claims)
+              if (x == cn && o.ns != p.ns) return no("a ReadWriteOncePod claim name used in several namespaces");
+      }
+      if (fully_bound(*c)) continue;
+      const SClass* sc = c->cls.empty() ? nullptr : class_of(c->cls);
+      if (sc && !sc->has_mode && has_vkind(VK_BIND)) return no("a storage class without volumeBindingMode");
+      if (!delay_binding(*c) || !c->volume_name.empty()) continue;
+      // a WaitForFirstConsumer claim the scheduler provisions for
+      if (intree_provisioner(sc->provisioner) && has_vkind(VK_NONCSI)) return no("an in-tree provisioner");
+      for (auto& kv : pvs)
+        if (kv.second.cls == c->cls && (!kv.second.claimed || (kv.second.cref_ns == c->ns && kv.second.cref_name == c->name)))
+          return no("static persistent volumes a WaitForFirstConsumer claim could bind");
+      if (users(p.ns, cn, true) > 1) return no("a WaitForFirstConsumer claim shared by several pods");
+    }
+    return true;
+  }
+  // volume.GetLocalPersistentVolumeNodeNames
+  static set<string> local_pv_nodes(const PV& v) {
+    set<string> out;
+    if (!v.required) return out;
+    if (const J* ts = (*v.required)["nodeSelectorTerms"])
+      for (auto& t : ts->items) {
+        bool have = false;
+        set<string> nodes;
+        if (const J* me = t["matchExpressions"])
+          for (auto& e : me->items) {
+            if (str_of(e["key"]) != kHostname || str_of(e["operator"]) != "In") continue;
+            vector<string> vs = slist(e["values"]);
+            set<string> x(vs.begin(), vs.end());
+            if (!have) { nodes = x; have = true; }
+            else {
+              set<string> y;
+              for (auto& a : nodes)
+                if (x.count(a)) y.insert(a);
+              nodes = y;
+            }
+          }
+        out.insert(nodes.begin(), nodes.end());
+      }
+    return out;
+  }
+  // A NodeSelector matched against a node carrying only its labels
+  // (volume.CheckNodeAffinity): terms into the sel pool; empty or invalid terms
+  // never match.
+  void pv_affinity_terms(const J& required, Prog& P, int32_t& off, int32_t& cnt) {
+    vector<ksg_sel> terms;
+    if (const J* ts = required["nodeSelectorTerms"])
+      for (auto& t : ts->items) {
+        if (term_empty(t)) continue;
+        ksg_sel s;
+        const size_t r0 = P.req.size(), v0 = P.i32.size();
+        if (compile_node_term(t, P, s, true)) terms.push_back(s);
+        else { P.req.resize(r0); P.i32.resize(v0); }
+      }
+    off = (int32_t)P.sel.size();
+    cnt = (int32_t)terms.size();
+    for (auto& s : terms) P.sel.push_back(s);
+  }
+  // v1helper.MatchTopologySelectorTerms over a class's allowedTopologies: terms
+  // with no expressions or an empty value list select nothing
+  void topology_terms(const J& allowed, Prog& P, int32_t& off, int32_t& cnt) {
+    vector<ksg_sel> terms;
+    for (auto& t : allowed.items) {
+      const J* me = t["matchLabelExpressions"];
+      if (!me || me->size() == 0) continue;
+      ksg_sel s{1, (int32_t)P.req.size(), 0, 0};
+      bool ok = true;
+      vector<ksg_req> rs;
+      for (auto& e : me->items) {
+        vector<string> vals = slist(e["values"]);
+        if (vals.empty()) { ok = false; break; }
+        ksg_req q{};
+        q.key = nkeys.get(str_of(e["key"]));
+        q.op = KR_IN;
+        q.val_off = (int32_t)P.i32.size();
+        for (auto& v : vals) P.i32.push_back(nval(q.key, v));
+        q.nvals = (int32_t)vals.size();
+        rs.push_back(q);
+      }
+      if (!ok) continue;
+      for (auto& q : rs) P.req.push_back(q);
+      s.req_cnt = (int32_t)rs.size();
+      terms.push_back(s);
+    }
+    off = (int32_t)P.sel.size();
+    cnt = (int32_t)terms.size();
+    for (auto& s : terms) P.sel.push_back(s);
+  }
+  static constexpr const char* kZoneKeys[4] = {"failure-domain.beta.kubernetes.io/zone",
+                                               "failure-domain.beta.kubernetes.io/region",
+                                               "topology.kubernetes.io/zone", "topology.kubernetes.io/region"};
+  bool compile_volumes(const Pod& p, Prog& P, PodMeta& m) {
+    ksg_prog& h = P.h;
+    h.pvc_off = (int32_t)P.i32.size();  // NodeInfo.PVCRefCounts delta of the pod's assume
+    for (auto& cn : p.claims) {
+      const int32_t id = pvc_ids.get(p.ns + "/" + cn);
+      if (id < 0) { err = "internal: PVC " + cn + " not interned"; return false; }
+      P.i32.push_back(id);
+    }
+    h.n_pvc = (int32_t)p.claims.size();
+    if (!has_volume_plugins) return true;
+    vector<ksg_vchk> chk;
+    int vb_pos = -1;
+    for (int pos = 0; pos < n_plugins; ++pos) {
+      const int vk = vkind[pos];
+      if (vk == VK_NONE) continue;
+      if (m.prefilter_fail_pos >= 0 && m.prefilter_fail_pos < pos) break;  // an earlier PreFilter rejected the pod
+      const int d = dpos[pos], sub = pos - fpos[d];
+      auto add = [&](int kind, uint32_t bits, uint32_t unless, int32_t off, int32_t cnt) {
+        chk.push_back(ksg_vchk{d, sub, kind, (int32_t)bits, (int32_t)unless, off, cnt, 0});
+      };
+      string fail;  // PreFilter UnschedulableAndUnresolvable message
+      bool skip = p.claims.empty();
+      if (vk == VK_RESTRICT && !skip) {  // readWriteOncePodPVCsForPod + calPreFilterState; Filter satisfyReadWriteOncePod
+        vector<int32_t> rw;
+        for (auto& cn : p.claims) {
+          const PVC* c = pvc_of(p.ns, cn);
+          if (!c) { fail = "persistentvolumeclaim \"" + cn + "\" not found"; break; }
+          if (c->rwop) rw.push_back(pvc_ids.get(p.ns + "/" + cn));
+        }
+        if (fail.empty() && !rw.empty()) {
+          add(KSG_VCHK_USED, KSG_VOL_RWOP, 0, (int32_t)P.i32.size(), (int32_t)rw.size());
+          P.i32.insert(P.i32.end(), rw.begin(), rw.end());
+        }
+      } else if (vk == VK_BIND && !skip) {
+        vb_pos = pos;
+        for (auto& cn : p.claims) {  // podHasPVCs
+          const PVC* c = pvc_of(p.ns, cn);
+          if (!c) fail = "persistentvolumeclaim \"" + cn + "\" not found";
+          else if (c->lost)
+            fail = "persistentvolumeclaim \"" + c->name + "\" bound to non-existent persistentvolume \"" + c->volume_name + "\"";
+          else if (c->deleting) fail = "persistentvolumeclaim \"" + c->name + "\" is being deleted";
+          if (!fail.empty()) break;
+        }
+        vector<const PVC*> bnd, dly;
+        bool immediate = false;
+        if (fail.empty()) {
+          for (auto& cn : p.claims) {  // GetPodVolumeClaims
+            const PVC* c = pvc_of(p.ns, cn);
+            if (fully_bound(*c)) bnd.push_back(c);
+            else if (delay_binding(*c) && c->volume_name.empty()) dly.push_back(c);
+            else immediate = true;
+          }
+          if (immediate) fail = "pod has unbound immediate PersistentVolumeClaims";
+        }
+        if (fail.empty()) {
+          bool have = false, missing = false;  // GetEligibleNodes
+          set<string> elig;
+          for (auto* c : bnd) {
+            const PV* v = pv_of(c->volume_name);
+            if (!v) { missing = true; continue; }
+            set<string> nn = local_pv_nodes(*v);
+            if (nn.empty()) continue;
+            if (!have) { elig = nn; have = true; }
+            else {
+              set<string> y;
+              for (auto& a : elig)
+                if (nn.count(a)) y.insert(a);
+              elig = y;
+            }
+          }
+          if (have && !missing) {
+            m.vb_restricted = true;
+            m.vb_names.assign(elig.begin(), elig.end());
+          }
+          for (auto* c : bnd) {  // checkBoundClaims: stops at a missing PV or a mismatch
+            const PV* v = pv_of(c->volume_name);
+            if (!v) { add(KSG_VCHK_FAIL, KSG_VOL_PV_NOT_EXIST, KSG_VOL_NODE_CONFLICT, 0, 0); break; }
+            if (!v->required) continue;
+            int32_t off, cnt;
+            pv_affinity_terms(*v->required, P, off, cnt);
+            add(KSG_VCHK_SELS, KSG_VOL_NODE_CONFLICT, 0, off, cnt);
+          }
+          vector<const PVC*> prov;  // FindPodVolumes: selected-node claims, then those no static PV matches
+          for (auto* c : dly)
+            if (c->has_selected) {
+              ksg_sel s{1, (int32_t)P.req.size(), 1, 0};
+              ksg_req q{};
+              q.key = -1;
+              const int32_t g = node_names.get(c->selected);
+              q.op = g >= 0 ? KR_NAME_EQ : KR_FALSE;
+              q.num = g;
+              P.req.push_back(q);
+              add(KSG_VCHK_SELS, KSG_VOL_BIND_CONFLICT, 0, (int32_t)P.sel.size(), 1);
+              P.sel.push_back(s);
+              prov.push_back(c);
+            }
+          for (auto* c : dly)
+            if (!c->has_selected) prov.push_back(c);
+          for (auto* c : prov) {  // checkVolumeProvisions (capacity: no CSIDriver objects, sufficient)
+            const SClass* sc = class_of(c->cls);
+            if (sc->provisioner.empty() || sc->provisioner == "kubernetes.io/no-provisioner") {
+              add(KSG_VCHK_FAIL, KSG_VOL_BIND_CONFLICT, 0, 0, 0);
+              break;
+            }
+            if (sc->allowed && sc->allowed->size() > 0) {
+              int32_t off, cnt;
+              topology_terms(*sc->allowed, P, off, cnt);
+              add(KSG_VCHK_SELS, KSG_VOL_BIND_CONFLICT, 0, off, cnt);
+            }
+          }
+        }
+      } else if (vk == VK_ZONE) {  // getPVbyPod; Filter
+        vector<std::pair<int32_t, vector<string>>> topo;  // (node key, zones)
+        for (auto& cn : p.claims) {
+          if (cn.empty()) { fail = "PersistentVolumeClaim had no name"; break; }
+          const PVC* c = pvc_of(p.ns, cn);
+          if (!c) { fail = "persistentvolumeclaim \"" + cn + "\" not found"; break; }
+          if (c->volume_name.empty()) {
+            if (c->cls.empty()) { fail = "PersistentVolumeClaim had no pv name and storageClass name"; break; }
+            const SClass* sc = class_of(c->cls);
+            if (!sc) { fail = "storageclass.storage.k8s.io \"" + c->cls + "\" not found"; break; }
+            if (!sc->has_mode) { fail = "VolumeBindingMode not set for StorageClass \"" + c->cls + "\""; break; }
+            if (sc->wffc) continue;
+            fail = "PersistentVolume had no name";
+            break;
+          }
+          const PV* v = pv_of(c->volume_name);
+          if (!v) { fail = "persistentvolume \"" + c->volume_name + "\" not found"; break; }
+          for (const char* key : kZoneKeys) {  // getPVTopologies, volumehelpers.LabelZonesToSet
+            auto it = v->labels.find(key);
+            if (it == v->labels.end()) continue;
+            vector<string> zs;
+            bool bad = false;
+            size_t at = 0;
+            for (;;) {
+              size_t k = it->second.find("__", at);
+              string z = it->second.substr(at, k == string::npos ? string::npos : k - at);
+              size_t b = z.find_first_not_of(" \t\n\r\v\f"), e = z.find_last_not_of(" \t\n\r\v\f");
+              z = b == string::npos ? "" : z.substr(b, e - b + 1);
+              if (z.empty()) { bad = true; break; }
+              zs.push_back(z);
+              if (k == string::npos) break;
+              at = k + 2;
+            }
+            if (!bad) topo.push_back({nkeys.get(key), zs});
+          }
+        }
+        skip = fail.empty() && topo.empty();
+        if (fail.empty() && !skip) {
+          // node without any zone / region label passes; else every PV topology label must match
+          ksg_sel none{1, (int32_t)P.req.size(), 4, 0};
+          for (const char* key : kZoneKeys) {
+            ksg_req q{};
+            q.key = nkeys.get(key);
+            q.op = KR_NOT_EXISTS;
+            P.req.push_back(q);
+          }
+          ksg_sel all{1, (int32_t)P.req.size(), (int32_t)topo.size(), 0};
+          for (auto& t : topo) {
+            ksg_req q{};
+            q.key = t.first;
+            q.op = KR_IN;
+            q.val_off = (int32_t)P.i32.size();
+            for (auto& z : t.second) P.i32.push_back(nval(q.key, z));
+            q.nvals = (int32_t)t.second.size();
+            P.req.push_back(q);
+          }
+          add(KSG_VCHK_SELS, KSG_VOL_ZONE_CONFLICT, 0, (int32_t)P.sel.size(), 2);
+          P.sel.push_back(none);
+          P.sel.push_back(all);
+        }
+      }
+      // (EBS / GCE / Azure limits, NodeVolumeLimits: the claims bring no volume they
+      // count against a limit, volumes_modelled: every node passes)
+      if (skip) m.vol_skip |= 1u << pos;
+      if (!fail.empty()) {
+        if (m.prefilter_fail_pos < 0 || pos < m.prefilter_fail_pos) {
+          m.prefilter_fail_pos = pos;
+          m.prefilter_fail_msg = fail;
+          h.flags |= KPF_PREFILTER_REJECT;
+        }
+        break;
+      }
+    }
+    // RunPreFilterPlugins merges the PreFilterResults (NodeAffinity's, VolumeBinding's)
+    if (m.vb_restricted && (m.prefilter_fail_pos < 0 || m.prefilter_fail_pos > vb_pos)) {
+      vector<string> names = m.vb_names;
+      if (m.restricted) {
+        vector<string> x;
+        for (auto& a : m.prefilter_names)
+          if (std::binary_search(m.vb_names.begin(), m.vb_names.end(), a)) x.push_back(a);
+        names = x;
+      }
+      const int at = m.restricted ? std::max(vb_pos, pos_of(P_NA)) : vb_pos;
+      if (names.empty()) {  // "node(s) didn't satisfy plugin(s) ..." after the later plugin's PreFilter
+        if (m.prefilter_fail_pos < 0 || at < m.prefilter_fail_pos) {
+          m.prefilter_fail_pos = at;
+          m.prefilter_fail_msg = "success";
+          m.merge_reject = true;
+          h.flags |= KPF_PREFILTER_REJECT;
+        }
+      } else {
+        h.flags |= KPF_RESTRICT;
+        const uint32_t n = hi - lo, w = (n + 31) / 32;
+        h.restrict_words = (int32_t)w;
+        h.restrict_off = (int32_t)P.u32.size();
+        P.u32.resize(P.u32.size() + w, 0);
+        for (auto& nm : names) {
+          int32_t g = node_names.get(nm);
+          if (g >= (int32_t)lo && g < (int32_t)hi) P.u32[h.restrict_off + (g - lo) / 32] |= 1u << ((g - lo) % 32);
+        }
+      }
+    }
+    h.vchk_off = (int32_t)P.i32.size();
+    h.n_vchk = (int32_t)chk.size();
+    for (auto& c : chk) {
+      const int32_t* w = reinterpret_cast<const int32_t*>(&c);
+      P.i32.insert(P.i32.end(), w, w + 8);
+    }
+    return true;
   }
 
   bool compile(const Pod& p, int32_t qidx, vector<uint8_t>& blob, PodMeta& m) {
@@ -1691,6 +2200,8 @@ struct Cluster {
       h.pref_w_off = (int32_t)P.i32.size();
       for (auto& x : pts) { P.sel.push_back(x.first); P.i32.push_back(x.second); }
     }
+    // ---- volume plugins (their PreFilter state on the host, their Filters as device checks)
+    if (!compile_volumes(p, P, m)) return false;
     // ---- PodTopologySpread
     auto build_tsc = [&](const string& when, int& count) -> bool {
       count = 0;
@@ -1916,12 +2427,21 @@ struct Cluster {
       }
     if (qd)
       for (auto& p : qd->items) queue.push_back(parse_pod(p));
+    pvcs.clear(); pvs.clear(); classes.clear();
+    if (const J* a = d["pvcs"])
+      for (auto& x : a->items) { PVC c = parse_pvc(x); pvcs[c.ns + "/" + c.name] = c; }
+    if (const J* a = d["pvs"])
+      for (auto& x : a->items) { PV v = parse_pv(x); pvs[v.name] = v; }
+    if (const J* a = d["storageClasses"])
+      for (auto& x : a->items) { SClass c = parse_sc(x); classes[c.name] = c; }
+    attach_limits = d["csiNodes"] && d["csiNodes"]->size() > 0;
+    for (auto& n : nodes)
+      for (auto& kv : n.alloc) attach_limits |= kv.first.rfind("attachable-volumes-", 0) == 0;
     index_queue();
     qneed.clear();
     broken = false;
-    if (has_volume_plugins)
-      for (auto& p : queue)
-        if (p.volume_plugins_act) { err = "pod " + p.name + ": volumes the volume plugins act on are not modelled"; return false; }
+    for (auto& p : queue)
+      if (!volumes_modelled(p)) return false;
     if (!equal_priorities()) return false;
     if (!build_vocab() || !eng->set_score_resources(ecfg.fit_res, ecfg.ba_res, err)) return false;
     NodeSoA S;
@@ -2044,6 +2564,8 @@ struct Cluster {
   }
   bool vocab_grows(const Pod& p) const {
     if (nss.get(p.ns) < 0) return true;
+    for (auto& c : p.claims)
+      if (pvc_ids.get(p.ns + "/" + c) < 0) return true;  // a PVC the device use counts do not cover
     auto known = [&](const string& key, const string* v) {
       int32_t k = pkeys.get(key);
       return k >= 0 && k < (int32_t)pvals.size() && (!v || pvals[k].get(*v) >= 0);
@@ -2144,8 +2666,7 @@ struct Cluster {
     }
     const J& d = *docs.back();
     queue.push_back(parse_pod(d["pod"] ? *d["pod"] : d));
-    if (has_volume_plugins && queue.back().volume_plugins_act) {
-      err = "pod " + queue.back().name + ": volumes the volume plugins act on are not modelled";
+    if (!volumes_modelled(queue.back())) {
       queue.pop_back();
       return false;
     }
@@ -2266,7 +2787,7 @@ struct Cluster {
       const uint32_t c = o.filter[i];
       if (c == KSG_FILTER_PASS || c >= KSG_FILTER_NOT_EVALUATED || (c >> 24) >= (uint32_t)n_dev) continue;
       string msg;
-      if (filter_status(q, fpos[c >> 24], i, o, msg) == C_UNSCHED) {
+      if (filter_status(q, code_pos(c), i, o, msg) == C_UNSCHED) {
         potential.push_back((int32_t)i);
         is_pot[i] = 1;
       }
@@ -2471,6 +2992,7 @@ struct Cluster {
         if (!e["pod"]) return 0;
         Pod p = parse_pod(*e["pod"]);
         if (p.node.empty() || node_names.get(p.node) < 0) return 0;
+        if (has_volume_plugins && !p.claims.empty()) return 0;  // claim users: the re-encode path re-checks the queue
         if (vocab_grows(p)) {  // new label values / keys / namespaces grow in place
           if (!vocab_grows_in_place(p)) return 0;
           if (!grow_vocab(p)) return -1;
@@ -2732,7 +3254,16 @@ struct Cluster {
     std::swap(qmode, qm);
     std::swap(placed, pl);
     bound_at_valid = false;
-    if (!equal_priorities()) {
+    bool vol_ok = true;  // the batch may change what the volume plugins see (claim users, attach limits)
+    if (has_volume_plugins) {
+      bool limits = attach_limits;
+      for (auto& n : nodes)
+        for (auto& kv : n.alloc) attach_limits |= kv.first.rfind("attachable-volumes-", 0) == 0;
+      for (size_t q = 0; q < queue.size() && vol_ok; ++q)
+        if (qmode.size() <= q || qmode[q] == 0) vol_ok = volumes_modelled(queue[q]);
+      if (!vol_ok) attach_limits = limits;
+    }
+    if (!vol_ok || !equal_priorities()) {
       std::swap(nodes, nn);
       std::swap(bound, bb);
       std::swap(qmode, qm);
@@ -2822,6 +3353,18 @@ struct Cluster {
         return detail == KSG_IPA_AFFINITY ? "node(s) didn't match pod affinity rules"
                : detail == KSG_IPA_ANTI_AFFINITY ? "node(s) didn't match pod anti-affinity rules"
                                                  : "node(s) didn't satisfy existing pods anti-affinity rules";
+      case P_VOLUME:
+      case P_VOLBIND: {  // Status.Message(): the reasons joined (volume_binding.go Filter appends them in this order)
+        if (vkind[pos] == VK_RESTRICT)
+          return "node has pod using PersistentVolumeClaim with the same name and ReadWriteOncePod access mode";
+        if (vkind[pos] == VK_ZONE) return "node(s) had no available volume zone";
+        string m;
+        auto add = [&](const char* r) { m += (m.empty() ? "" : ", ") + string(r); };
+        if (detail & KSG_VOL_NODE_CONFLICT) add("node(s) had volume node affinity conflict");
+        if (detail & KSG_VOL_BIND_CONFLICT) add("node(s) didn't find available persistent volumes to bind");
+        if (detail & KSG_VOL_PV_NOT_EXIST) add("node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)");
+        return m;
+      }
     }
     return "";
   }
@@ -2838,8 +3381,19 @@ struct Cluster {
     if (m.flags & KPF_SKIP_PTS_FILTER) skip_f |= 1u << P_PTS;
     if (m.ipa_no_req_terms && !(S.ipa_flags & 4u)) skip_f |= 1u << P_IPA;
     if (m.flags & KPF_SKIP_PORTS) skip_f |= 1u << P_PORTS;
-    skip_f |= (1u << P_VOLUME) | (1u << P_VOLBIND);  // pods with volumes they act on are refused at load
     return skip_f;
+  }
+  // PreFilter Skip of profile position pos (skip_f: skip_filter_mask; volume plugins per position)
+  bool filter_skipped(const PodMeta& m, uint32_t skip_f, int pos) const {
+    return is_volume(plugins[pos]) ? ((m.vol_skip >> pos) & 1u) != 0 : (skip_f & (1u << plugins[pos])) != 0;
+  }
+  // profile position / detail a device filter code names (a volume run: its failing plugin)
+  int code_pos(uint32_t code) const {
+    const int base = fpos[code >> 24];
+    return is_volume(plugins[base]) ? base + (int)((code >> 16) & 0xFFu) : base;
+  }
+  uint32_t code_detail(uint32_t code) const {
+    return is_volume(plugins[fpos[code >> 24]]) ? code & 0xFFFFu : code & 0xFFFFFFu;
   }
   uint32_t skip_score_mask(const PodMeta& m, const ksg_pod_summary& S) const {
     uint32_t skip_s = 0;
@@ -2857,9 +3411,9 @@ struct Cluster {
     for (int p = 0; p < n_plugins; ++p) {
       if (!has_prefilter(plugins[p])) continue;
       if (p == pos) {
-        if (p == m.prefilter_fail_pos) { msg = m.prefilter_fail_msg; return C_UNRESOLVABLE; }
+        if (p == m.prefilter_fail_pos && !m.merge_reject) { msg = m.prefilter_fail_msg; return C_UNRESOLVABLE; }
         msg.clear();
-        return (skip_f & (1u << plugins[p])) ? C_SKIP : C_SUCCESS;
+        return filter_skipped(m, skip_f, p) ? C_SKIP : C_SUCCESS;
       }
       if (p == m.prefilter_fail_pos) break;
     }
@@ -2872,14 +3426,15 @@ struct Cluster {
     const PodMeta& m = meta[q];
     msg.clear();
     if (pos < 0 || pos >= n_plugins || !has_filter(plugins[pos])) return -1;
-    if (m.prefilter_fail_pos >= 0 || (skip_filter_mask(m, o.summary) & (1u << plugins[pos]))) return -1;
+    if (m.prefilter_fail_pos >= 0 || filter_skipped(m, skip_filter_mask(m, o.summary), pos)) return -1;
     const uint32_t code = o.filter[i];
     if (code == KSG_FILTER_NOT_EVALUATED) return -1;
-    const int fail_pos = code == KSG_FILTER_PASS ? n_plugins : fpos[code >> 24];
+    const int fail_pos = code == KSG_FILTER_PASS ? n_plugins : code_pos(code);
     if (pos < fail_pos) return C_SUCCESS;
     if (pos > fail_pos) return -1;
-    const uint32_t detail = code & 0xFFFFFFu;
+    const uint32_t detail = code_detail(code);
     msg = filter_message(pos, detail);
+    if (is_volume(plugins[pos])) return vkind[pos] == VK_RESTRICT ? C_UNSCHED : C_UNRESOLVABLE;
     switch (plugins[pos]) {
       case P_FIT: {  // fit.go Filter: UnschedulableAndUnresolvable when a request exceeds the allocatable
         vector<i64> rq;
@@ -2971,25 +3526,26 @@ struct Cluster {
       int id = plugins[pos];
       if (!has_prefilter(id)) continue;
       string msg = "success";
-      if (skip_f & (1u << id)) msg = "";
+      if (filter_skipped(m, skip_f, pos)) msg = "";
       if (pos == m.prefilter_fail_pos) {
         msg = m.prefilter_fail_msg;
         aborted = true;
       }
       pre_status[names[pos]] = msg;
       if (id == P_NA && m.restricted) pre_result[names[pos]] = m.prefilter_names;
+      if (vkind[pos] == VK_BIND && m.vb_restricted) pre_result[names[pos]] = m.vb_names;
     }
     if (!aborted) {
       for (uint32_t i = 0; i < n; ++i) {
         uint32_t code = o.filter[i];
         if (code == KSG_FILTER_NOT_EVALUATED) continue;
-        int fail_pos = code == KSG_FILTER_PASS ? n_plugins : fpos[code >> 24];
+        int fail_pos = code == KSG_FILTER_PASS ? n_plugins : code_pos(code);
         auto& row = filt[nodes[lo + i].name];
         for (int pos = 0; pos < n_plugins; ++pos) {
           int id = plugins[pos];
-          if (!has_filter(id) || (skip_f & (1u << id))) continue;
+          if (!has_filter(id) || filter_skipped(m, skip_f, pos)) continue;
           if (pos < fail_pos) row[names[pos]] = "passed";
-          else if (pos == fail_pos) { row[names[pos]] = filter_message(pos, code & 0xFFFFFFu); break; }
+          else if (pos == fail_pos) { row[names[pos]] = filter_message(pos, code_detail(code)); break; }
         }
       }
       if (S.feasible > 1 && S.status == 2 && m.na_prescore_error)  // PreScore ran up to NodeAffinity's error
@@ -3260,7 +3816,7 @@ int ksg_filter_codes(ksg_ctx* ctx, uint32_t q, uint32_t* out, uint32_t n) {
   if (n < o.filter.size()) return KSG_E_NOBUF;
   for (size_t i = 0; i < o.filter.size(); ++i) {  // device position -> profile position
     uint32_t c = o.filter[i];
-    out[i] = c >= KSG_FILTER_NOT_EVALUATED ? c : ((uint32_t)ctx->c.fpos[c >> 24] << 24) | (c & 0xFFFFFFu);
+    out[i] = c >= KSG_FILTER_NOT_EVALUATED ? c : ((uint32_t)ctx->c.code_pos(c) << 24) | ctx->c.code_detail(c);
   }
   return KSG_OK;
 }
@@ -3464,6 +4020,26 @@ int ksg_prefilter_result(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t
     for (size_t i = 0; i < c.meta[q].prefilter_names.size(); ++i) {
       if (i) s += ',';
       Cluster::jstr(s, c.meta[q].prefilter_names[i]);
+    }
+    s += "]";
+  }
+  return put_str(ctx, s, buf, cap, len);
+}
+
+int ksg_prefilter_result_pos(ksg_ctx* ctx, uint32_t q, uint32_t pos, char* buf, size_t cap, size_t* len) {
+  KSG_GUARD(ctx);
+  Cluster& c = ctx->c;
+  if (q >= c.meta.size() || (int)pos >= c.n_plugins) return ctx->fail("prefilter_result_pos: range", KSG_E_RANGE);
+  const ksg::host::PodMeta& m = c.meta[q];
+  const std::vector<std::string>* names = nullptr;  // PreFilterResult nil: every node
+  if (c.plugins[pos] == ksg::host::P_NA && m.restricted) names = &m.prefilter_names;
+  if (c.vkind[pos] == ksg::host::VK_BIND && m.vb_restricted) names = &m.vb_names;
+  std::string s = "null";
+  if (names) {
+    s = "[";
+    for (size_t i = 0; i < names->size(); ++i) {
+      if (i) s += ',';
+      Cluster::jstr(s, (*names)[i]);
     }
     s += "]";
   }

@@ -32,8 +32,10 @@
 #define KP_NODENAME 7   // NodeName
 #define KP_PORTS 8      // NodePorts
 #define KP_IMAGE 9      // ImageLocality
-// host-only plugin kinds (never in the device profile: nothing to evaluate per node
-// for the pods the build accepts; the host records what the wrapper would)
+#define KP_VOLUMES 10   // a run of consecutive volume plugins in the profile (one device position):
+                        // the pod's volume checks (ksg_vchk) of that position, in plugin order
+// host plugin kinds (the host records what the wrapper would; their Filters run on
+// the device as KP_VOLUMES positions)
 #define KP_VOLUME 16    // VolumeRestrictions, EBSLimits, GCEPDLimits, NodeVolumeLimits, AzureDiskLimits, VolumeZone
 #define KP_VOLBIND 17   // VolumeBinding
 #define KP_NOOP 18      // SchedulingGates, PrioritySort, DefaultPreemption, DefaultBinder
@@ -43,7 +45,8 @@
 
 // filter result code per (pod,node): 0xFFFFFFFF passed every filter plugin,
 // 0xFFFFFFFE not evaluated (outside the NodeAffinity PreFilterResult), else
-// (profile position << 24) | detail  (detail: Fit reason bits, taint id, PTS/IPA reason).
+// (profile position << 24) | detail  (detail: Fit reason bits, taint id, PTS/IPA reason;
+// KP_VOLUMES: plugin index within the run << 16 | KSG_VOL_* reason bits).
 #define KSG_FILTER_PASS 0xFFFFFFFFu
 #define KSG_FILTER_NOT_EVALUATED 0xFFFFFFFEu
 #define KSG_FIT_TOO_MANY_PODS 1u   // Fit detail bit 0; bit (1 + r) = insufficient resource column r
@@ -52,6 +55,13 @@
 #define KSG_IPA_AFFINITY 0u
 #define KSG_IPA_ANTI_AFFINITY 1u
 #define KSG_IPA_EXISTING_ANTI 2u
+
+// volume plugin reasons (KP_VOLUMES detail bits; messages rendered by the host)
+#define KSG_VOL_RWOP (1u << 0)            // VolumeRestrictions ErrReasonReadWriteOncePodConflict
+#define KSG_VOL_NODE_CONFLICT (1u << 1)   // VolumeBinding ErrReasonNodeConflict
+#define KSG_VOL_BIND_CONFLICT (1u << 2)   // VolumeBinding ErrReasonBindConflict
+#define KSG_VOL_PV_NOT_EXIST (1u << 3)    // VolumeBinding ErrReasonPVNotExist
+#define KSG_VOL_ZONE_CONFLICT (1u << 4)   // VolumeZone ErrReasonConflict
 
 // requirement operators (labels.Requirement / node selector requirement)
 #define KR_IN 0          // present && value in vals
@@ -113,6 +123,18 @@ typedef struct ksg_tsc {
   int32_t nvals;
   int32_t dom;           // values of the key present on some node of the shard (minMatchNum: none -> Error)
 } ksg_tsc;
+
+// One volume check of an incoming pod (host compile of the volume plugins'
+// PreFilter state; evaluated at device position dpos, KP_VOLUMES).  The checks of
+// one plugin (sub) are consecutive; a failing check ORs `bits` into that plugin's
+// reasons unless one of `unless` is already there; the first plugin of the run
+// with reasons fails the node.
+#define KSG_VCHK_FAIL 0   // always fails (pod-uniform verdict)
+#define KSG_VCHK_SELS 1   // fails unless one of the node selector terms pool_sel[off .. off+cnt) matches
+#define KSG_VCHK_USED 2   // fails if a PVC of pool_i32[off .. off+cnt) is used by a pod (ReadWriteOncePod)
+typedef struct ksg_vchk {
+  int32_t dpos, sub, kind, bits, unless, off, cnt, pad;
+} ksg_vchk;  // 32 B, in pool_i32 (8 words each)
 
 // Table-chain lookup plan (host compile, table-path pods): every class-table
 // count k_eval reads per node, issued together once the node's topology values
@@ -246,6 +268,10 @@ typedef struct ksg_prog {
   int32_t n_lk, n_ub;       // table chain: lookup plan and InterPodAffinity bits
   ksg_look lk[KSG_LK_MAX];
   ksg_ubit ub[KSG_UB_MAX];
+
+  // ---- volume plugins
+  int32_t n_vchk, vchk_off;  // pool_i32: ksg_vchk records (8 words each)
+  int32_t n_pvc, pvc_off;    // pool_i32: PVC ids of the pod's volumes (NodeInfo PVCRefCounts delta on assume)
 
   // ---- pools (byte offsets from the start of the blob)
   uint32_t off_i32, n_i32;

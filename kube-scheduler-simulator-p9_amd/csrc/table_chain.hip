@@ -244,6 +244,7 @@ __device__ __forceinline__ void assume_row_atomic(DevCluster& C, const ProgView&
   atomicAdd((unsigned long long*)&C.nzm[n], (unsigned long long)(sign * h->nz_mem));
   atomicAdd(&C.podcnt[n], sign);
   for (int i = 0; i < h->n_port_own; ++i) atomicAdd(&C.ports[(size_t)V.i32[h->port_own_off + i] * C.N + n], sign);
+  for (int i = 0; i < h->n_pvc; ++i) atomicAdd(&C.pvcuse[V.i32[h->pvc_off + i]], sign);
 }
 
 // selectHost + the assume, by the last-arriving block of the cycle's last
@@ -500,6 +501,10 @@ __global__ __launch_bounds__(kChain) void k_eval(DevCluster C, DevProfile F, Cha
         case KP_NODENAME: fail = nodename_fails(C, V, n); break;
         case KP_PORTS:
           if (!(h->flags & KPF_SKIP_PORTS)) fail = ports_fail(C, V, n);
+          break;
+        case KP_VOLUMES:
+          detail = volume_filter(C, V, pos, n);
+          fail = detail != 0;
           break;
         default: break;
       }

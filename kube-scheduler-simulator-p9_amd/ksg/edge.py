@@ -33,6 +33,16 @@ Variants (each a small seeded cluster, same document shape as ``generator``):
   unschedulable pods meet both Unschedulable nodes (preemption may help) and
   UnschedulableAndUnresolvable ones.  The queue is in the order given (no
   PrioritySort): earlier queue pods can be victims of later ones.
+* ``volumes``   the whole default profile over pods with PersistentVolumeClaims
+  (ResourcesForSnap pvs / pvcs / storageClasses): claims bound to local PVs
+  (hostname node affinity: VolumeBinding's PreFilterResult), to zonal PVs
+  (VolumeZone labels, multi-zone "__" values, a malformed one; node affinity by
+  zone), to a PV with an empty or a matchFields-only affinity, to a missing PV;
+  WaitForFirstConsumer claims to provision (allowedTopologies, a selected-node
+  annotation, a class without a provisioner), immediate and pre-bound unbound
+  claims, deleting / lost / missing claims, ReadWriteOncePod claims used by a
+  bound pod or shared by two queue pods; nodes with and without zone / region
+  labels.
 """
 from __future__ import annotations
 
@@ -43,7 +53,7 @@ from .generator import (HOSTNAME, ZONE, Gi, Mi, Rng, make_profile, node_obj, pod
 GPU = "example.com/gpu"
 EPH = "ephemeral-storage"
 NAMESPACES = ["default", "ns-a", "ns-b", "team-x"]
-EDGE_VARIANTS = ("fit_most", "fit_rtc", "na", "pts", "ipa", "ipa_ignore", "preempt")
+EDGE_VARIANTS = ("fit_most", "fit_rtc", "na", "pts", "ipa", "ipa_ignore", "preempt", "volumes")
 
 
 def edge_seed(variant: str) -> int:
@@ -415,6 +425,174 @@ def gen_preempt(n_nodes=24, n_existing=120, n_pods=90, seed=None):
     return {"profile": prof, "nodes": nodes, "pods": bound, "queue": queue}
 
 
+REGION = "topology.kubernetes.io/region"
+BETA_ZONE = "failure-domain.beta.kubernetes.io/zone"
+CSI = "csi.example.com"
+
+
+def _pvc(name, ns, volume=None, cls=None, bound=False, modes=("ReadWriteOnce",), ann=None, **extra):
+    md = {"name": name, "namespace": ns}
+    a = dict(ann or {})
+    if bound:
+        a["pv.kubernetes.io/bind-completed"] = "yes"
+    if a:
+        md["annotations"] = a
+    md.update(extra.pop("metadata", {}))
+    spec = {"accessModes": list(modes), "resources": {"requests": {"storage": "1Gi"}}}
+    if volume:
+        spec["volumeName"] = volume
+    if cls is not None:
+        spec["storageClassName"] = cls
+    o = {"metadata": md, "spec": spec}
+    o.update(extra)
+    return o
+
+
+def _pv(name, cls, claim=None, labels=None, affinity=None, csi=True):
+    spec = {"capacity": {"storage": "10Gi"}, "accessModes": ["ReadWriteOnce"], "storageClassName": cls}
+    if csi:
+        spec["csi"] = {"driver": CSI, "volumeHandle": name}
+    if claim:
+        spec["claimRef"] = {"namespace": claim[0], "name": claim[1]}
+    if affinity is not None:
+        spec["nodeAffinity"] = {"required": affinity}
+    return {"metadata": {"name": name, "labels": dict(labels or {})}, "spec": spec}
+
+
+def gen_volumes(n_nodes=40, n_existing=60, n_pods=120, seed=None):
+    seed = edge_seed("volumes") if seed is None else seed
+    r = Rng(seed)
+    nodes = []
+    for i in range(n_nodes):
+        labels = {}
+        if r.pct() < 80:
+            z = r.below(3)
+            labels[ZONE] = f"zone-{z}"
+            if r.pct() < 70:
+                labels[REGION] = "region-a" if z < 2 else "region-b"
+        if r.pct() < 15:
+            labels[BETA_ZONE] = f"zone-{r.below(3)}"
+        nodes.append(node_obj(f"node-{i:07d}", 1000 * r.pick([8, 16]), Gi * r.pick([32, 64]), labels=labels))
+    names = [n["metadata"]["name"] for n in nodes]
+    classes = [
+        {"metadata": {"name": "wffc-any"}, "provisioner": CSI, "volumeBindingMode": "WaitForFirstConsumer"},
+        {"metadata": {"name": "wffc-zone"}, "provisioner": CSI, "volumeBindingMode": "WaitForFirstConsumer",
+         "allowedTopologies": [{"matchLabelExpressions": [{"key": ZONE, "values": ["zone-0", "zone-1"]}]},
+                               {"matchLabelExpressions": []}]},
+        {"metadata": {"name": "wffc-region"}, "provisioner": CSI, "volumeBindingMode": "WaitForFirstConsumer",
+         "allowedTopologies": [{"matchLabelExpressions": [{"key": REGION, "values": ["region-b"]},
+                                                          {"key": ZONE, "values": ["zone-2"]}]}]},
+        {"metadata": {"name": "wffc-static"}, "provisioner": "kubernetes.io/no-provisioner",
+         "volumeBindingMode": "WaitForFirstConsumer"},
+        {"metadata": {"name": "immediate"}, "provisioner": CSI, "volumeBindingMode": "Immediate"},
+    ]
+    pvs, pvcs = [], []
+    ns_of = {}
+
+    def claim(name, ns, **kw):
+        pvcs.append(_pvc(name, ns, **kw))
+        ns_of[name] = ns
+        return name
+    # bound claims (a pool several pods may use) and their PVs
+    pool = []
+    for k in range(14):
+        ns = r.pick(NAMESPACES)
+        cn, pn = f"data-{k:03d}", f"pv-{k:03d}"
+        kind = k % 7
+        labels, aff = {}, None
+        if kind == 0:  # local PV: hostname affinity (VolumeBinding PreFilterResult)
+            aff = {"nodeSelectorTerms": [{"matchExpressions": [
+                {"key": HOSTNAME, "operator": "In", "values": [r.pick(names), r.pick(names)]}]}]}
+        elif kind == 1:  # zonal PV by labels (VolumeZone)
+            labels = {ZONE: r.pick(["zone-0", "zone-1", "zone-2", "zone-0__zone-2"])}
+            if r.pct() < 50:
+                labels[REGION] = r.pick(["region-a", "region-b"])
+        elif kind == 2:  # zonal PV by node affinity
+            aff = {"nodeSelectorTerms": [{"matchExpressions": [
+                {"key": ZONE, "operator": "In", "values": [r.pick(["zone-0", "zone-1", "zone-2"])]}]},
+                {"matchExpressions": [{"key": BETA_ZONE, "operator": "Exists"}]}]}
+        elif kind == 3:  # labels + affinity; a malformed zone list is ignored by VolumeZone
+            labels = {BETA_ZONE: "zone-1__", REGION: "region-a"}
+            aff = {"nodeSelectorTerms": [{"matchExpressions": [{"key": REGION, "operator": "NotIn", "values": ["region-b"]}]}]}
+        elif kind == 4:  # an affinity no node matches: empty terms / matchFields against a labels-only node
+            aff = r.pick([{"nodeSelectorTerms": []},
+                          {"nodeSelectorTerms": [{"matchFields": [
+                              {"key": "metadata.name", "operator": "In", "values": [names[0]]}]}]},
+                          {"nodeSelectorTerms": [{}]}])
+        elif kind == 5:  # no constraints
+            pass
+        else:  # local PV on two nodes, several hostname terms (union)
+            aff = {"nodeSelectorTerms": [
+                {"matchExpressions": [{"key": HOSTNAME, "operator": "In", "values": names[k % n_nodes: k % n_nodes + 3]},
+                                      {"key": HOSTNAME, "operator": "In", "values": names[k % n_nodes + 1: k % n_nodes + 2]}]},
+                {"matchExpressions": [{"key": HOSTNAME, "operator": "In", "values": [names[(3 * k) % n_nodes]]}]}]}
+        cls = r.pick(["wffc-any", "immediate", "wffc-zone"])
+        pvs.append(_pv(pn, cls, claim=(ns, cn), labels=labels, affinity=aff))
+        pool.append(claim(cn, ns, volume=pn, cls=cls, bound=True))
+    gone = claim("data-gone", "default", volume="pv-gone", cls="wffc-any", bound=True)  # PV missing
+    rwop_used = claim("rwop-used", "ns-a", volume="pv-rwop-1", cls="wffc-any", bound=True, modes=("ReadWriteOncePod",))
+    pvs.append(_pv("pv-rwop-1", "wffc-any", claim=("ns-a", "rwop-used")))
+    rwop_free = claim("rwop-free", "ns-b", volume="pv-rwop-2", cls="wffc-any", bound=True, modes=("ReadWriteOncePod",))
+    pvs.append(_pv("pv-rwop-2", "wffc-any", claim=("ns-b", "rwop-free"),
+                   affinity={"nodeSelectorTerms": [{"matchExpressions": [
+                       {"key": ZONE, "operator": "In", "values": ["zone-1", "zone-2"]}]}]}))
+    immediate = claim("data-immediate", "default", cls="immediate")
+    prebound = claim("data-prebound", "default", volume="pv-005", cls="wffc-any")  # no bind-completed
+    deleting = claim("data-deleting", "team-x", volume="pv-gone", cls="wffc-any", bound=True,
+                     metadata={"deletionTimestamp": "2025-01-01T00:00:00Z"})
+    lost = claim("data-lost", "ns-a", volume="pv-lost", cls="wffc-any", bound=True, status={"phase": "Lost"})
+    bound = []
+    for e in range(n_existing):
+        ns = r.pick(NAMESPACES)
+        spec = {}
+        mine = [c for c in pool if ns_of[c] == ns]
+        vols = []
+        if mine and r.pct() < 40:
+            vols.append(r.pick(mine))
+        if e == 3:
+            ns, vols = "ns-a", [rwop_used]
+        if vols:
+            spec["volumes"] = [{"name": f"v{i}", "persistentVolumeClaim": {"claimName": c}} for i, c in enumerate(vols)]
+        bound.append(pod_obj(f"ex-{e:07d}", [req(100 * (1 + r.below(6)), 256 * Mi * (1 + r.below(6)))],
+                             node=r.pick(names), ns=ns, **spec))
+    queue = []
+    for j in range(n_pods):
+        ns = r.pick(NAMESPACES)
+        vols = []
+        k = r.pct()
+        if k < 15:
+            pass  # no volumes: every volume plugin Skips
+        elif k < 50:
+            mine = [c for c in pool if ns_of[c] == ns]
+            if mine:
+                vols = [r.pick(mine) for _ in range(1 + r.below(2))]
+        elif k < 72:  # a fresh WaitForFirstConsumer claim of its own
+            cls = r.pick(["wffc-any", "wffc-zone", "wffc-region", "wffc-static"])
+            ann = {"volume.kubernetes.io/selected-node": r.pick(names + ["node-gone"])} if r.pct() < 20 else None
+            vols = [claim(f"new-{j:04d}", ns, cls=cls, ann=ann)]
+            mine = [c for c in pool if ns_of[c] == ns]
+            if mine and r.pct() < 40:
+                vols.append(r.pick(mine))
+        elif k < 80:
+            ns = "default"
+            vols = [r.pick([immediate, prebound, gone, "no-such-claim", ""])]
+        elif k < 86:
+            ns, vols = r.pick([("team-x", [deleting]), ("ns-a", [lost])])
+        else:
+            ns, vols = r.pick([("ns-a", [rwop_used]), ("ns-b", [rwop_free])])
+        spec = {}
+        if vols:
+            spec["volumes"] = [{"name": f"v{i}", "persistentVolumeClaim": {"claimName": c}} for i, c in enumerate(vols)]
+        if r.pct() < 10:
+            spec["nodeSelector"] = {ZONE: r.pick(["zone-0", "zone-1"])}
+        queue.append(pod_obj(f"pod-{j:07d}", [req(100 * (1 + r.below(10)), 256 * Mi * (1 + r.below(8)))],
+                             ns=ns, **spec))
+    from .generator import DEFAULT_PROFILE
+    prof = make_profile(DEFAULT_PROFILE, seed)
+    return {"profile": prof, "nodes": nodes, "pods": bound, "queue": queue, "pvs": pvs, "pvcs": pvcs,
+            "storageClasses": classes}
+
+
 def generate_edge(variant: str, **sizes) -> dict:
     if variant in ("fit_most", "fit_rtc"):
         return gen_fit(variant, **sizes)
@@ -426,6 +604,8 @@ def generate_edge(variant: str, **sizes) -> dict:
         return gen_ipa(variant, **sizes)
     if variant == "preempt":
         return gen_preempt(**sizes)
+    if variant == "volumes":
+        return gen_volumes(**sizes)
     raise ValueError(variant)
 
 

@@ -82,6 +82,7 @@ def load_library():
     L.ksg_plugin_weights.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     L.ksg_prefilter_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_prefilter_result.argtypes = [vp, u32, cp, sz, ctypes.POINTER(sz)]
+    L.ksg_prefilter_result_pos.argtypes = [vp, u32, u32, cp, sz, ctypes.POINTER(sz)]
     L.ksg_postfilter_result.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_int32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_filter_status.argtypes = [vp, u32, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_prescore_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
@@ -270,6 +271,15 @@ class Scheduler:
         self.L.ksg_prefilter_result(self.h, q, None, 0, ctypes.byref(n))
         buf = ctypes.create_string_buffer(n.value + 1)
         self._chk(self.L.ksg_prefilter_result(self.h, q, buf, n.value + 1, ctypes.byref(n)), "ksg_prefilter_result")
+        return json.loads(buf.raw[:n.value].decode())
+
+    def prefilter_result_pos(self, q, pos):
+        """PreFilterResult of the plugin at profile position pos (None: every node)."""
+        n = ctypes.c_size_t()
+        self.L.ksg_prefilter_result_pos(self.h, q, pos, None, 0, ctypes.byref(n))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._chk(self.L.ksg_prefilter_result_pos(self.h, q, pos, buf, n.value + 1, ctypes.byref(n)),
+                  "ksg_prefilter_result_pos")
         return json.loads(buf.raw[:n.value].decode())
 
     def postfilter_result(self, q):

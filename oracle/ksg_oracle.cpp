@@ -479,7 +479,8 @@ struct Pod {
   vector<WAffTerm> pref_aff, pref_anti;
   bool pref_aff_present = false, pref_anti_present = false;  // for hasConstraints
   vector<TSC> tsc;
-  bool volume_plugins_act = false;  // a volume the volume plugins would not Skip (unsupported)
+  bool volume_plugins_act = false;  // a volume other than a PVC the volume plugins act on (unsupported)
+  vector<string> claims;            // persistentVolumeClaim.claimName of spec.volumes, in order
   i64 priority = 0;
   bool preempt_never = false;       // spec.preemptionPolicy: Never
   i64 start_time = INT64_MAX;       // status.startTime (epoch s); none: later than any (util.GetPodStartTime: now)
@@ -494,6 +495,7 @@ struct Node {
   Labels labels;
   vector<Taint> taints;
   Resource alloc;
+  vector<string> alloc_raw;  // allocatable resource names (attach limits: attachable-volumes-*)
   bool unschedulable = false;
   vector<NodeImage> images;
 };
@@ -574,10 +576,13 @@ static bool parse_pod(const ojson::Value& v, Pod& p) {
   conts(sp->get("initContainers"), p.init_containers);
   for (auto& c : p.init_containers) c.ports.clear();  // v1.30: Spec.Containers only (getContainerPorts, updateUsedPorts)
   if (auto* vs = sp->get("volumes"))
-    for (auto& v : vs->arr)
-      for (const char* k : {"persistentVolumeClaim", "ephemeral", "gcePersistentDisk", "awsElasticBlockStore", "rbd",
-                            "iscsi", "azureDisk", "cinder", "csi"})
+    for (auto& v : vs->arr) {
+      auto* pvc = v.get("persistentVolumeClaim");
+      if (pvc && !pvc->is_null()) p.claims.push_back(pvc->get("claimName") ? pvc->get("claimName")->str() : "");
+      for (const char* k : {"ephemeral", "gcePersistentDisk", "awsElasticBlockStore", "rbd", "iscsi", "azureDisk",
+                            "cinder", "csi"})
         if (v.get(k) && !v.get(k)->is_null()) p.volume_plugins_act = true;
+    }
   p.overhead = parse_rl(sp->get("overhead"));
   if (auto* ns = sp->get("nodeSelector"); ns && !ns->is_null()) {
     p.has_node_selector = true;
@@ -656,6 +661,8 @@ static void parse_node(const ojson::Value& v, Node& n) {
     if (auto* u = sp->get("unschedulable")) n.unschedulable = u->b;
   auto* st = v.get("status");
   resource_add(n.alloc, parse_rl(st ? st->get("allocatable") : nullptr));
+  if (auto* al = st ? st->get("allocatable") : nullptr)
+    for (auto& kv : al->obj) n.alloc_raw.push_back(kv.first);
   if (st)
     if (auto* im = st->get("images"))
       for (auto& x : im->arr) {
@@ -801,13 +808,14 @@ struct ScoreSpec {
   i64 weight;
 };
 
-// P_VOLUME: VolumeRestrictions, EBSLimits, GCEPDLimits, NodeVolumeLimits,
-// AzureDiskLimits, VolumeZone (PreFilter + Filter; PreFilter Skip for pods
-// without volumes they act on).  P_VOLBIND: VolumeBinding (also PreScore, Skip
-// with the default feature gates: no scorer).  P_NOOP: plugins with none of the
-// recorded extension points.
+// Volume plugins (PreFilter + Filter): P_VOLRESTRICT VolumeRestrictions,
+// P_NONCSI EBSLimits / GCEPDLimits / AzureDiskLimits, P_CSILIMITS NodeVolumeLimits,
+// P_VOLZONE VolumeZone, P_VOLBIND VolumeBinding (also PreScore, Skip with the
+// default feature gates: no scorer).  P_NOOP: plugins with none of the recorded
+// extension points.
 enum PluginId { P_FIT, P_BA, P_TAINT, P_NA, P_PTS, P_IPA, P_UNSCHED, P_NODENAME, P_PORTS, P_IMAGE,
-                P_VOLUME, P_VOLBIND, P_NOOP, P_UNKNOWN };
+                P_VOLRESTRICT, P_NONCSI, P_CSILIMITS, P_VOLZONE, P_VOLBIND, P_NOOP, P_UNKNOWN };
+static bool is_volume_plugin(PluginId p) { return p >= P_VOLRESTRICT && p <= P_VOLBIND; }
 static PluginId plugin_id(const string& n) {
   if (n == "NodeResourcesFit") return P_FIT;
   if (n == "NodeResourcesBalancedAllocation") return P_BA;
@@ -819,19 +827,20 @@ static PluginId plugin_id(const string& n) {
   if (n == "NodeName") return P_NODENAME;
   if (n == "NodePorts") return P_PORTS;
   if (n == "ImageLocality") return P_IMAGE;
-  if (n == "VolumeRestrictions" || n == "EBSLimits" || n == "GCEPDLimits" || n == "NodeVolumeLimits" ||
-      n == "AzureDiskLimits" || n == "VolumeZone")
-    return P_VOLUME;
+  if (n == "VolumeRestrictions") return P_VOLRESTRICT;
+  if (n == "EBSLimits" || n == "GCEPDLimits" || n == "AzureDiskLimits") return P_NONCSI;
+  if (n == "NodeVolumeLimits") return P_CSILIMITS;
+  if (n == "VolumeZone") return P_VOLZONE;
   if (n == "VolumeBinding") return P_VOLBIND;
   if (n == "PrioritySort" || n == "SchedulingGates" || n == "DefaultPreemption" || n == "DefaultBinder") return P_NOOP;
   return P_UNKNOWN;
 }
 static bool has_prefilter(PluginId p) {
-  return p == P_FIT || p == P_NA || p == P_PTS || p == P_IPA || p == P_PORTS || p == P_VOLUME || p == P_VOLBIND;
+  return p == P_FIT || p == P_NA || p == P_PTS || p == P_IPA || p == P_PORTS || is_volume_plugin(p);
 }
 static bool has_filter(PluginId p) {
   return p == P_FIT || p == P_TAINT || p == P_NA || p == P_PTS || p == P_IPA || p == P_UNSCHED || p == P_NODENAME ||
-         p == P_PORTS || p == P_VOLUME || p == P_VOLBIND;
+         p == P_PORTS || is_volume_plugin(p);
 }
 static bool has_prescore(PluginId p) { return p <= P_IPA || p == P_VOLBIND; }
 static bool has_score(PluginId p) { return p <= P_IPA || p == P_IMAGE || p == P_VOLBIND; }
@@ -967,6 +976,36 @@ static string render_annotations(const PodResult& r) {
   return json_map(ann);
 }
 
+// ============================================================ storage (volume plugins)
+// ResourcesForSnap pvs / pvcs / storageClasses as v1.30.4's volume plugins read
+// them (GetPersistentVolumeClaimClass / GetPersistentVolumeClass: the beta
+// annotation wins over spec.storageClassName).
+struct ClaimObj {
+  string ns, name, volume_name, class_name;
+  bool bind_completed = false, deleting = false, lost = false, rwop = false;
+  bool has_selected_node = false;
+  string selected_node;
+};
+struct VolumeObj {
+  string name, class_name;
+  Labels labels;
+  bool has_required = false;       // spec.nodeAffinity.required
+  vector<NodeSelTerm> required;    // its terms (empty / invalid ones never match)
+  vector<bool> required_empty;
+  bool claim_ref = false;
+  string ref_ns, ref_name;
+  bool intree = false;
+  const ojson::Value* required_json = nullptr;
+};
+struct ClassObj {
+  string name, provisioner;
+  bool mode_set = false, wait_for_consumer = false;
+  vector<vector<std::pair<string, vector<string>>>> topology;  // allowedTopologies terms (label expressions)
+};
+static const char* kVolumeZoneLabels[4] = {"failure-domain.beta.kubernetes.io/zone",
+                                           "failure-domain.beta.kubernetes.io/region",
+                                           "topology.kubernetes.io/zone", "topology.kubernetes.io/region"};
+
 // ============================================================ the simulator
 struct Cluster;
 
@@ -1006,6 +1045,12 @@ struct CycleState {
   map<string, map<string, i64>> ipa_topo_score;
   // NodePorts preFilterState (getContainerPorts)
   vector<HostPort> ports_want;
+  // VolumeRestrictions preFilterState.conflictingPVCRefCount
+  int vr_conflicts = 0;
+  // VolumeBinding stateData.podVolumeClaims
+  vector<const ClaimObj*> vb_bound, vb_delayed;
+  // VolumeZone stateData.podPVTopologies
+  vector<std::pair<string, set<string>>> vz_topologies;
 };
 
 static const i64 kMB = 1024 * 1024;
@@ -1039,6 +1084,12 @@ struct Cluster {
   unsigned long long seed = 0;
   // ImageStateSummary per image name (size of the first node listing it, node count)
   std::unordered_map<string, std::pair<i64, int>> image_states;
+  // storage objects (volume plugins) and NodeInfo.PVCRefCounts summed over the nodes
+  map<string, ClaimObj> claims;  // "namespace/name"
+  map<string, VolumeObj> volumes;
+  map<string, ClassObj> classes;
+  map<string, int> pvc_refs;
+  bool attach_limits = false;
   // results
   vector<PodResult> results;
   std::mutex store_mu;
@@ -1065,6 +1116,7 @@ struct Cluster {
       for (auto& h : c.ports) n.used_ports[h.ip][{h.proto, h.port}]++;
     if (r.with_affinity) n.pods_with_affinity.push_back(pi);
     if (r.has_required_anti) n.pods_with_req_anti.push_back(pi);
+    for (auto& c : r.pod.claims) pvc_refs[r.pod.ns + "/" + c] += 1;  // updatePVCRefCounts
   }
 
   void remove_pod(int pi, int ni) {  // framework.NodeInfo.RemovePod
@@ -1092,6 +1144,224 @@ struct Cluster {
         if (--m[{h.proto, h.port}] <= 0) m.erase({h.proto, h.port});
         if (m.empty()) n.used_ports.erase(h.ip);
       }
+    for (auto& c : r.pod.claims) {
+      const string key = r.pod.ns + "/" + c;
+      if (--pvc_refs[key] <= 0) pvc_refs.erase(key);
+    }
+  }
+
+  // ---------------------------------------------------------------- volume plugins (v1.30.4)
+  const ClaimObj* find_claim(const string& ns, const string& name) const {
+    auto it = claims.find(ns + "/" + name);
+    return it == claims.end() ? nullptr : &it->second;
+  }
+  static Status unresolvable(const string& m) { return {Status::UnschedulableAndUnresolvable, m}; }
+  // volumerestrictions PreFilter: readWriteOncePodPVCsForPod + calPreFilterState
+  // (needsRestrictionsCheck: any PVC volume; inline disks are refused at load)
+  Status vr_prefilter(const Pod& p, CycleState& cs) const {
+    set<string> rwop;
+    for (auto& cn : p.claims) {
+      const ClaimObj* c = find_claim(p.ns, cn);
+      if (!c) return unresolvable("persistentvolumeclaim \"" + cn + "\" not found");
+      if (c->rwop) rwop.insert(c->name);
+    }
+    int conflicts = 0;
+    for (auto& n : rwop)
+      if (pvc_refs.count(p.ns + "/" + n)) conflicts++;  // StorageInfos().IsPVCUsedByPods
+    if (p.claims.empty() && conflicts == 0) return Status::skip();
+    cs.vr_conflicts = conflicts;
+    return {};
+  }
+  Status vr_filter(const CycleState& cs) const {  // satisfyReadWriteOncePod
+    if (cs.vr_conflicts != 0)
+      return {Status::Unschedulable,
+              "node has pod using PersistentVolumeClaim with the same name and ReadWriteOncePod access mode"};
+    return {};
+  }
+  // nodevolumelimits non_csi.go / csi.go PreFilter: Skip without a PVC (the claims
+  // accepted at load bring no volume either counts against a limit: Filter passes)
+  static Status limits_prefilter(const Pod& p) { return p.claims.empty() ? Status::skip() : Status{}; }
+  // volume.GetLocalPersistentVolumeNodeNames
+  static set<string> local_pv_nodes(const VolumeObj& v) {
+    set<string> out;
+    if (!v.has_required || !v.required_json) return out;
+    if (auto* ts = v.required_json->get("nodeSelectorTerms"))
+      for (auto& t : ts->arr) {
+        std::unique_ptr<set<string>> nodes;
+        if (auto* me = t.get("matchExpressions"))
+          for (auto& e : me->arr) {
+            if (!e.get("key") || e.get("key")->str() != "kubernetes.io/hostname") continue;
+            if (!e.get("operator") || e.get("operator")->str() != "In") continue;
+            vector<string> vs = str_list(e.get("values"));
+            set<string> x(vs.begin(), vs.end());
+            if (!nodes) nodes.reset(new set<string>(x));
+            else {
+              set<string> y;
+              std::set_intersection(nodes->begin(), nodes->end(), x.begin(), x.end(), std::inserter(y, y.begin()));
+              *nodes = y;
+            }
+          }
+        if (nodes) out.insert(nodes->begin(), nodes->end());
+      }
+    return out;
+  }
+  // volume.CheckNodeAffinity: the node object carries only its labels
+  static bool pv_affinity_match(const VolumeObj& v, const Labels& node_labels) {
+    if (!v.has_required) return true;
+    for (size_t i = 0; i < v.required.size(); ++i) {
+      if (v.required_empty[i] || v.required[i].err) continue;
+      if (v.required[i].match(node_labels, "")) return true;
+    }
+    return false;
+  }
+  // v1helper.MatchTopologySelectorTerms
+  static bool topology_match(const ClassObj& k, const Labels& ls) {
+    if (k.topology.empty()) return true;
+    for (auto& term : k.topology) {
+      if (term.empty()) continue;
+      bool ok = true;
+      for (auto& e : term) {
+        auto it = ls.find(e.first);
+        if (e.second.empty() || it == ls.end() || std::find(e.second.begin(), e.second.end(), it->second) == e.second.end()) {
+          ok = false;
+          break;
+        }
+      }
+      if (ok) return true;
+    }
+    return false;
+  }
+  // volumebinding PreFilter: podHasPVCs, GetPodVolumeClaims, GetEligibleNodes
+  Status vb_prefilter(const Pod& p, CycleState& cs, bool& has_res, vector<string>& res) const {
+    if (p.claims.empty()) return Status::skip();
+    for (auto& cn : p.claims) {
+      const ClaimObj* c = find_claim(p.ns, cn);
+      if (!c) return unresolvable("persistentvolumeclaim \"" + cn + "\" not found");
+      if (c->lost)
+        return unresolvable("persistentvolumeclaim \"" + c->name + "\" bound to non-existent persistentvolume \"" +
+                            c->volume_name + "\"");
+      if (c->deleting) return unresolvable("persistentvolumeclaim \"" + c->name + "\" is being deleted");
+    }
+    bool immediate = false;
+    for (auto& cn : p.claims) {
+      const ClaimObj* c = find_claim(p.ns, cn);
+      if (!c->volume_name.empty() && c->bind_completed) {
+        cs.vb_bound.push_back(c);
+        continue;
+      }
+      bool delay = false;  // IsDelayBindingMode
+      if (!c->class_name.empty()) {
+        auto k = classes.find(c->class_name);
+        delay = k != classes.end() && k->second.wait_for_consumer;
+      }
+      if (delay && c->volume_name.empty()) cs.vb_delayed.push_back(c);
+      else immediate = true;
+    }
+    if (immediate) return unresolvable("pod has unbound immediate PersistentVolumeClaims");
+    bool any = false, missing = false;
+    set<string> elig;
+    for (auto* c : cs.vb_bound) {
+      auto it = volumes.find(c->volume_name);
+      if (it == volumes.end()) { missing = true; continue; }
+      set<string> nn = local_pv_nodes(it->second);
+      if (nn.empty()) continue;
+      if (!any) { elig = nn; any = true; continue; }
+      set<string> y;
+      std::set_intersection(elig.begin(), elig.end(), nn.begin(), nn.end(), std::inserter(y, y.begin()));
+      elig = y;
+    }
+    if (any && !missing) {
+      has_res = true;
+      res.assign(elig.begin(), elig.end());
+    }
+    return {};
+  }
+  // volumebinding Filter -> binder.FindPodVolumes (static PV matching never applies:
+  // refused at load; provisioning capacity: no CSIDriver objects, sufficient)
+  Status vb_filter(const CycleState& cs, int ni) const {
+    const Node& n = nodes[ni];
+    bool bound_ok = true, found = true, unbound_ok = true;
+    for (auto* c : cs.vb_bound) {  // checkBoundClaims
+      auto it = volumes.find(c->volume_name);
+      if (it == volumes.end()) { found = false; break; }
+      if (!pv_affinity_match(it->second, n.labels)) { bound_ok = false; break; }
+    }
+    if (!cs.vb_delayed.empty()) {
+      vector<const ClaimObj*> provision;
+      for (auto* c : cs.vb_delayed)
+        if (c->has_selected_node) {
+          if (c->selected_node != n.name) { unbound_ok = false; break; }
+          provision.push_back(c);
+        }
+      if (unbound_ok) {
+        for (auto* c : cs.vb_delayed)
+          if (!c->has_selected_node) provision.push_back(c);
+        for (auto* c : provision) {  // checkVolumeProvisions
+          const ClassObj& k = classes.at(c->class_name);
+          if (k.provisioner.empty() || k.provisioner == "kubernetes.io/no-provisioner" || !topology_match(k, n.labels)) {
+            unbound_ok = false;
+            break;
+          }
+        }
+      }
+    }
+    string m;
+    auto reason = [&](const char* r) { m += (m.empty() ? "" : ", ") + string(r); };
+    if (!bound_ok) reason("node(s) had volume node affinity conflict");
+    if (!unbound_ok) reason("node(s) didn't find available persistent volumes to bind");
+    if (!found) reason("node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)");
+    if (m.empty()) return {};
+    return unresolvable(m);
+  }
+  // volumezone PreFilter (getPVbyPod, getPVTopologies / LabelZonesToSet) and Filter
+  Status vz_prefilter(const Pod& p, CycleState& cs) const {
+    for (auto& cn : p.claims) {
+      if (cn.empty()) return unresolvable("PersistentVolumeClaim had no name");
+      const ClaimObj* c = find_claim(p.ns, cn);
+      if (!c) return unresolvable("persistentvolumeclaim \"" + cn + "\" not found");
+      if (c->volume_name.empty()) {
+        if (c->class_name.empty()) return unresolvable("PersistentVolumeClaim had no pv name and storageClass name");
+        auto k = classes.find(c->class_name);
+        if (k == classes.end()) return unresolvable("storageclass.storage.k8s.io \"" + c->class_name + "\" not found");
+        if (!k->second.mode_set) return unresolvable("VolumeBindingMode not set for StorageClass \"" + c->class_name + "\"");
+        if (k->second.wait_for_consumer) continue;
+        return unresolvable("PersistentVolume had no name");
+      }
+      auto v = volumes.find(c->volume_name);
+      if (v == volumes.end()) return unresolvable("persistentvolume \"" + c->volume_name + "\" not found");
+      for (const char* key : kVolumeZoneLabels) {
+        auto it = v->second.labels.find(key);
+        if (it == v->second.labels.end()) continue;
+        set<string> zones;
+        bool bad = false;
+        string rest = it->second;
+        for (;;) {
+          size_t cut = rest.find("__");
+          string z = rest.substr(0, cut);
+          const char* ws = " \t\n\r\v\f";
+          size_t a = z.find_first_not_of(ws);
+          z = a == string::npos ? string() : z.substr(a, z.find_last_not_of(ws) - a + 1);
+          if (z.empty()) { bad = true; break; }
+          zones.insert(z);
+          if (cut == string::npos) break;
+          rest = rest.substr(cut + 2);
+        }
+        if (!bad) cs.vz_topologies.push_back({key, zones});
+      }
+    }
+    if (cs.vz_topologies.empty()) return Status::skip();
+    return {};
+  }
+  Status vz_filter(const CycleState& cs, int ni) const {
+    const Labels& ls = nodes[ni].labels;
+    bool constrained = false;
+    for (const char* key : kVolumeZoneLabels) constrained |= ls.count(key) > 0;
+    if (!constrained) return {};
+    for (auto& t : cs.vz_topologies) {
+      auto it = ls.find(t.first);
+      if (it == ls.end() || !t.second.count(it->second)) return unresolvable("node(s) had no available volume zone");
+    }
+    return {};
   }
 
   // ---------------------------------------------------------------- DefaultPreemption (dry run)
@@ -1121,7 +1391,10 @@ struct Cluster {
       else if (id == P_PTS) s = pts_prefilter(p, cs, pool);
       else if (id == P_IPA) s = ipa_prefilter(p, cs, pool);
       else if (id == P_PORTS) s = ports_prefilter(p, cs);
-      else if (id == P_VOLUME || id == P_VOLBIND) s = Status::skip();
+      else if (id == P_VOLRESTRICT) s = vr_prefilter(p, cs);
+      else if (id == P_NONCSI || id == P_CSILIMITS) s = limits_prefilter(p);
+      else if (id == P_VOLBIND) { vector<string> res; s = vb_prefilter(p, cs, has_res, res); }
+      else if (id == P_VOLZONE) s = vz_prefilter(p, cs);
       if (s.code == Status::Skip) { skip.insert(id); continue; }
       if (!s.ok()) return false;
     }
@@ -1137,6 +1410,9 @@ struct Cluster {
       else if (id == P_UNSCHED) s = unsched_filter(p, ni);
       else if (id == P_NODENAME) s = nodename_filter(p, ni);
       else if (id == P_PORTS) s = ports_filter(cs, ni);
+      else if (id == P_VOLRESTRICT) s = vr_filter(cs);
+      else if (id == P_VOLBIND) s = vb_filter(cs, ni);
+      else if (id == P_VOLZONE) s = vz_filter(cs, ni);
       if (!s.ok()) return false;
     }
     return true;
@@ -1906,7 +2182,10 @@ struct Cluster {
       else if (id == P_PTS) s = pts_prefilter(p, cs, pool);
       else if (id == P_IPA) s = ipa_prefilter(p, cs, pool);
       else if (id == P_PORTS) s = ports_prefilter(p, cs);
-      else if (id == P_VOLUME || id == P_VOLBIND) s = Status::skip();  // no volumes they act on (checked at load)
+      else if (id == P_VOLRESTRICT) s = vr_prefilter(p, cs);
+      else if (id == P_NONCSI || id == P_CSILIMITS) s = limits_prefilter(p);
+      else if (id == P_VOLBIND) s = vb_prefilter(p, cs, has_res, res);
+      else if (id == P_VOLZONE) s = vz_prefilter(p, cs);
       const string& nm = profile_names[k];
       rec([&] {
         r.pre_filter_status[nm] = s.ok() ? "success" : s.msg;
@@ -1941,6 +2220,9 @@ struct Cluster {
         else if (id == P_UNSCHED) s = unsched_filter(p, ni);
         else if (id == P_NODENAME) s = nodename_filter(p, ni);
         else if (id == P_PORTS) s = ports_filter(cs, ni);
+        else if (id == P_VOLRESTRICT) s = vr_filter(cs);
+        else if (id == P_VOLBIND) s = vb_filter(cs, ni);
+        else if (id == P_VOLZONE) s = vz_filter(cs, ni);
         rec([&] { r.filter[nodes[ni].name][profile_names[k]] = s.ok() ? "passed" : s.msg; });
         if (!s.ok()) {
           if (s.code == Status::Error) err = true;
@@ -2298,14 +2580,147 @@ static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
     }
   if (auto* q = d.get("queue"))
     for (auto& p : q->arr) c.queue.push_back(add(p));
-  bool vol = false;
-  for (PluginId id : c.profile) vol |= id == P_VOLUME || id == P_VOLBIND;
-  if (vol)
-    for (int qi : c.queue)
-      if (c.pods[qi].pod.volume_plugins_act) {
-        err = "pod " + c.pods[qi].pod.name + ": volumes the volume plugins act on are not modelled";
-        return false;
+  // storage objects
+  auto beta_class = [](const ojson::Value* md, string& cls) {
+    auto* ann = md ? md->get("annotations") : nullptr;
+    if (auto* b = ann ? ann->get("volume.beta.kubernetes.io/storage-class") : nullptr) cls = b->str();
+  };
+  if (auto* a = d.get("pvcs"))
+    for (auto& v : a->arr) {
+      ClaimObj o;
+      auto* md = v.get("metadata");
+      auto* sp = v.get("spec");
+      o.name = md && md->get("name") ? md->get("name")->str() : "";
+      o.ns = md && md->get("namespace") ? md->get("namespace")->str() : "";
+      if (o.ns.empty()) o.ns = "default";
+      o.deleting = md && md->get("deletionTimestamp") && !md->get("deletionTimestamp")->is_null();
+      if (sp) {
+        o.volume_name = sp->get("volumeName") ? sp->get("volumeName")->str() : "";
+        if (auto* sc = sp->get("storageClassName"); sc && !sc->is_null()) o.class_name = sc->str();
+        for (auto& m : str_list(sp->get("accessModes"))) o.rwop = o.rwop || m == "ReadWriteOncePod";
       }
+      beta_class(md, o.class_name);
+      auto* ann = md ? md->get("annotations") : nullptr;
+      o.bind_completed = ann && ann->get("pv.kubernetes.io/bind-completed");
+      if (auto* sn = ann ? ann->get("volume.kubernetes.io/selected-node") : nullptr) {
+        o.has_selected_node = true;
+        o.selected_node = sn->str();
+      }
+      if (auto* st = v.get("status")) o.lost = st->get("phase") && st->get("phase")->str() == "Lost";
+      c.claims[o.ns + "/" + o.name] = o;
+    }
+  if (auto* a = d.get("pvs"))
+    for (auto& v : a->arr) {
+      VolumeObj o;
+      auto* md = v.get("metadata");
+      auto* sp = v.get("spec");
+      o.name = md && md->get("name") ? md->get("name")->str() : "";
+      o.labels = str_map(md ? md->get("labels") : nullptr);
+      if (sp) {
+        o.class_name = sp->get("storageClassName") ? sp->get("storageClassName")->str() : "";
+        auto* na = sp->get("nodeAffinity");
+        auto* rq = na && !na->is_null() ? na->get("required") : nullptr;
+        if (rq && !rq->is_null()) {
+          o.has_required = true;
+          o.required_json = rq;
+          if (auto* ts = rq->get("nodeSelectorTerms"))
+            for (auto& t : ts->arr) {
+              o.required.push_back(parse_node_term(t));
+              o.required_empty.push_back(term_is_empty(t));
+            }
+        }
+        if (auto* cr = sp->get("claimRef"); cr && !cr->is_null()) {
+          o.claim_ref = true;
+          o.ref_ns = cr->get("namespace") ? cr->get("namespace")->str() : "";
+          o.ref_name = cr->get("name") ? cr->get("name")->str() : "";
+        }
+        for (const char* k : {"awsElasticBlockStore", "gcePersistentDisk", "azureDisk", "cinder"})
+          o.intree = o.intree || (sp->get(k) && !sp->get(k)->is_null());
+      }
+      beta_class(md, o.class_name);
+      c.volumes[o.name] = o;
+    }
+  if (auto* a = d.get("storageClasses"))
+    for (auto& v : a->arr) {
+      ClassObj o;
+      auto* md = v.get("metadata");
+      o.name = md && md->get("name") ? md->get("name")->str() : "";
+      o.provisioner = v.get("provisioner") ? v.get("provisioner")->str() : "";
+      if (auto* m = v.get("volumeBindingMode"); m && !m->is_null()) {
+        o.mode_set = true;
+        o.wait_for_consumer = m->str() == "WaitForFirstConsumer";
+      }
+      if (auto* at = v.get("allowedTopologies"))
+        for (auto& t : at->arr) {
+          vector<std::pair<string, vector<string>>> term;
+          if (auto* me = t.get("matchLabelExpressions"))
+            for (auto& e : me->arr) term.push_back({e.get("key") ? e.get("key")->str() : "", str_list(e.get("values"))});
+          o.topology.push_back(term);
+        }
+      c.classes[o.name] = o;
+    }
+  c.attach_limits = d.get("csiNodes") && !d.get("csiNodes")->arr.empty();
+  for (auto& n : c.nodes)
+    for (auto& kv : n.alloc_raw) c.attach_limits = c.attach_limits || kv.rfind("attachable-volumes-", 0) == 0;
+  // Volume inputs outside the model are refused, never approximated
+  auto in_profile = [&](PluginId id) { return std::find(c.profile.begin(), c.profile.end(), id) != c.profile.end(); };
+  bool vol = false;
+  for (PluginId id : c.profile) vol = vol || is_volume_plugin(id);
+  bool preemption = std::find(c.profile_names.begin(), c.profile_names.end(), "DefaultPreemption") != c.profile_names.end();
+  if (vol)
+    for (int qi : c.queue) {
+      const Pod& p = c.pods[qi].pod;
+      auto refuse = [&](const string& why) {
+        err = "pod " + p.name + ": " + why + " (not modelled)";
+        return false;
+      };
+      if (p.volume_plugins_act) return refuse("volumes other than persistentVolumeClaim");
+      if (p.claims.empty()) continue;
+      if (c.attach_limits && in_profile(P_CSILIMITS)) return refuse("nodes declaring volume attach limits");
+      auto count_users = [&](const string& ns, const string& name, bool with_queue) {
+        int u = 0;
+        for (size_t i = 0; i < c.pods.size(); ++i) {
+          const Pod& o = c.pods[i].pod;
+          const bool queued = std::find(c.queue.begin(), c.queue.end(), (int)i) != c.queue.end();
+          if (queued && !with_queue) continue;
+          u += (int)std::count(o.claims.begin(), o.claims.end(), name) * (o.ns == ns);
+        }
+        return u;
+      };
+      for (auto& cn : p.claims) {
+        const ClaimObj* cl = c.find_claim(p.ns, cn);
+        if (!cl) {
+          if (!in_profile(P_VOLRESTRICT) && !in_profile(P_VOLBIND) && !in_profile(P_VOLZONE))
+            return refuse("a missing claim no PreFilter rejects");
+          continue;
+        }
+        if (!cl->volume_name.empty()) {
+          auto v = c.volumes.find(cl->volume_name);
+          if (v != c.volumes.end() && v->second.intree) return refuse("an in-tree cloud disk persistent volume");
+        }
+        if (cl->rwop && preemption) {
+          if (count_users(p.ns, cn, false) > 1) return refuse("a ReadWriteOncePod claim used by several bound pods");
+          for (auto& pr : c.pods)
+            if (pr.pod.ns != p.ns && std::count(pr.pod.claims.begin(), pr.pod.claims.end(), cn))
+              return refuse("a ReadWriteOncePod claim name used in several namespaces");
+        }
+        if (!cl->volume_name.empty() && cl->bind_completed) continue;
+        auto k = cl->class_name.empty() ? c.classes.end() : c.classes.find(cl->class_name);
+        if (k != c.classes.end() && !k->second.mode_set && in_profile(P_VOLBIND))
+          return refuse("a storage class without volumeBindingMode");
+        if (k == c.classes.end() || !k->second.wait_for_consumer || !cl->volume_name.empty()) continue;
+        const string& prov = k->second.provisioner;
+        if ((prov == "kubernetes.io/aws-ebs" || prov == "kubernetes.io/gce-pd" || prov == "kubernetes.io/azure-disk" ||
+             prov == "kubernetes.io/cinder") && in_profile(P_NONCSI))
+          return refuse("an in-tree provisioner");
+        for (auto& kv : c.volumes) {
+          const VolumeObj& v = kv.second;
+          if (v.class_name == cl->class_name && (!v.claim_ref || (v.ref_ns == cl->ns && v.ref_name == cl->name)))
+            return refuse("static persistent volumes a WaitForFirstConsumer claim could bind");
+        }
+        if (count_users(p.ns, cn, true) > 1) return refuse("a WaitForFirstConsumer claim shared by several pods");
+      }
+    }
   c.results.assign(c.queue.size(), PodResult());
   c.rendered.assign(c.queue.size(), string());
   c.digests.assign(c.queue.size(), 0);

@@ -85,6 +85,7 @@ EDGE = {
     "edge_ipa_small": ("ipa", dict(n_nodes=14, n_existing=30, n_pods=24)),
     "edge_ipa_ignore_small": ("ipa_ignore", dict(n_nodes=14, n_existing=30, n_pods=24)),
     "edge_preempt_small": ("preempt", dict(n_nodes=10, n_existing=40, n_pods=30)),
+    "edge_volumes_small": ("volumes", dict(n_nodes=16, n_existing=30, n_pods=40)),
 }
 
 

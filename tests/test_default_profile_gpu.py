@@ -150,12 +150,17 @@ def test_image_locality_scores_abi():
 
 
 @pytest.mark.gpu
-def test_volume_pods_refused():
+def test_unmodelled_volumes_refused():
+    """PersistentVolumeClaims run on the device (tests/test_volume_gpu.py); inline cloud
+    disks, and claims on a sharded context, are refused instead of approximated."""
     doc = g.generate(1, n_nodes=4, n_pods=2)
-    doc["queue"][1]["spec"]["volumes"] = [{"name": "d", "persistentVolumeClaim": {"claimName": "c"}}]
-    s = Scheduler(doc["profile"])
+    doc["queue"][1]["spec"]["volumes"] = [{"name": "d", "gcePersistentDisk": {"pdName": "disk"}}]
     with pytest.raises(Exception):
-        s.load_cluster(doc)
+        Scheduler(doc["profile"]).load_cluster(doc)
+    doc["queue"][1]["spec"]["volumes"] = [{"name": "d", "persistentVolumeClaim": {"claimName": "c"}}]
+    Scheduler(doc["profile"]).load_cluster(doc)  # a missing claim: VolumeRestrictions' PreFilter rejects the pod
+    with pytest.raises(Exception):
+        Scheduler(doc["profile"], shard_rank=0, shard_count=2).load_cluster(doc)
 
 
 @pytest.mark.gpu

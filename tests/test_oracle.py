@@ -97,7 +97,7 @@ def test_golden_families_match_generator():
         assert g.generate(d["config"], **d["sizes"]) == d["cluster"], name
     from ksg import edge
     for name in ("edge_fit_most_small", "edge_fit_rtc_small", "edge_na_small", "edge_pts_small", "edge_ipa_small",
-                 "edge_ipa_ignore_small", "edge_preempt_small"):
+                 "edge_ipa_ignore_small", "edge_preempt_small", "edge_volumes_small"):
         d = fixture(name)
         assert edge.generate_edge(d["edge"], **d["sizes"]) == d["cluster"], name
 

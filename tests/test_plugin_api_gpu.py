@@ -52,10 +52,12 @@ def rebuild(s, q, prof, names, status):
             continue
         pre_status[name] = "success" if code == C_SUCCESS else msg
         aborted |= code not in (C_SUCCESS, C_SKIP)
-        if name == "NodeAffinity" and code == C_SUCCESS:
-            r = s.prefilter_result(q)
+        if name in ("NodeAffinity", "VolumeBinding") and code == C_SUCCESS:
+            r = s.prefilter_result_pos(q, pos)
             if r is not None:
                 pre_result[name] = r
+            if name == "NodeAffinity":
+                assert r == s.prefilter_result(q)
     filt, feasible = {}, []
     for i, nm in enumerate(names):
         row = {}

@@ -2643,11 +2643,18 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     flush_stash();
     return;
   }
-  // last tile block of pod b: merge the T tile lists (wave w takes tiles w, w+16, ...)
+  // last tile block of pod b: merge the T tile lists (wave w takes tiles w, w+16, ...);
+  // the lists and the tiles' counts are requested together.
+  int32_t f[3] = {0, 0, 0};
   {
     const uint64_t* src = A.tile_top + (size_t)b * A.T * KSG_TOPK;
     uint64_t v = 0;
     if ((uint32_t)w < A.T) v = ld_agent(src + (size_t)w * KSG_TOPK + lane);
+    if (w == 0)
+      for (uint32_t t = lane; t < A.T; t += 64)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          f[k] += __hip_atomic_load(A.tile_feas + ((size_t)b * A.T + t) * 3 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll 1
     for (uint32_t t = w + 16; t < A.T; t += 16) v = wave_merge_top(v, ld_agent(src + (size_t)t * KSG_TOPK + 63 - lane));
     L[w * 64 + lane] = v;
@@ -2670,11 +2677,6 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     }
     rec_keys(A.erec)[(size_t)b * KSG_CAND + lane] = v;
     if (!A.xrows) rec_rows(A.erec)[(size_t)b * KSG_CAND + lane] = c;  // (sharded: rows from the replica)
-    int32_t f[3] = {0, 0, 0};
-    for (uint32_t t = lane; t < A.T; t += 64)
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-        f[k] += __hip_atomic_load(A.tile_feas + ((size_t)b * A.T + t) * 3 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int k = 0; k < 3; ++k) f[k] = wave_sum(f[k]);
     if (lane == 0) {
@@ -3658,6 +3660,10 @@ struct Engine::Impl {
   DBuf<int2> alog;        // assumes whose existing-pod table rows k_flush_appends writes
   DBuf<int32_t> cpi, cpst;
   DBuf<int64_t> cpm, cpm2;
+  DBuf<EvalTotals> cetot;
+  uint32_t fold_blocks = 256;  // table chain: k_fold above this many blocks (KSG_FOLD_BLOCKS; tests force it)
+  uint32_t occ_blocks = 0;     // table chain: occupancy twins above this many blocks (0: 2 per CU; KSG_OCC_BLOCKS)
+  bool occ_force = false;
   DBuf<uint64_t> cpr, cpk;
   uint32_t cnblk = 0;
   DBuf<int32_t> knorm;    // normalized scores of one kept pod
@@ -3771,6 +3777,11 @@ Engine::~Engine() {
 bool Engine::init(const EngineConfig& cfg, std::string& err) {
   Impl& I = *p_;
   I.cfg = cfg;
+  if (const char* e = std::getenv("KSG_FOLD_BLOCKS")) I.fold_blocks = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_OCC_BLOCKS")) {
+    I.occ_blocks = (uint32_t)std::strtoul(e, nullptr, 10);
+    I.occ_force = I.occ_blocks == 0;
+  }
   HIPCHK(hipSetDevice(cfg.device));
   if (cfg.stream) {
     I.stream = (hipStream_t)cfg.stream;
@@ -4896,6 +4907,11 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   CA.log_base = first;
   CA.arrive = I.carrive.p;
   CA.stamps = I.cstamps_on ? I.cstamps.p : nullptr;
+  CA.etot = nullptr;
+  if (I.cnblk > I.fold_blocks) {  // fold k_eval's partials once (k_fold) above this many blocks
+    if (!I.cetot.alloc(1, err)) return false;
+    CA.etot = I.cetot.p;
+  }
   const int rowm = I.R > 4 ? 0 : (I.eval_mode == 1 ? 2 : 1);
   bool pending = false;           // logged assumes whose existing-pod table rows are not written yet
   // rows of the logged pods [log_base, j); the log restarts at `next` (a pod of the
@@ -4912,7 +4928,12 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
       CA.prog = prog;
       const bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
       if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
-      if (rowm == 2) hipLaunchKernelGGL(k_eval<2>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+      const bool occ = I.cnblk > (I.occ_blocks ? I.occ_blocks : 2 * I.n_cus) || I.occ_force;  // many blocks per CU
+      if (occ) {
+        if (rowm == 2) hipLaunchKernelGGL(k_eval_occ<2>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+        else if (rowm == 1) hipLaunchKernelGGL(k_eval_occ<1>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+        else hipLaunchKernelGGL(k_eval_occ<0>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+      } else if (rowm == 2) hipLaunchKernelGGL(k_eval<2>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
       else if (rowm == 1) hipLaunchKernelGGL(k_eval<1>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
       else hipLaunchKernelGGL(k_eval<0>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
       if (sampled) {
@@ -4920,8 +4941,10 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         I.n_samples++;
       }
       if (F.has_ext) {  // (k_final's last block selects; without ScoreExtensions k_eval's)
+        if (CA.etot) hipLaunchKernelGGL(k_fold, dim3(1), dim3(kChain), 0, s, C, F, CA, prog);
         if (I.prog_need[j] & 8) hipLaunchKernelGGL(k_ptsraw, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
-        hipLaunchKernelGGL(k_final, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+        if (occ) hipLaunchKernelGGL(k_final_occ, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+        else hipLaunchKernelGGL(k_final, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
       }
       pending |= (CA.mode & 2) != 0;
       continue;

@@ -33,6 +33,7 @@ struct ChainVids {
   __device__ __forceinline__ int32_t operator()(int s) const { return base[s * kChain]; }
 };
 
+struct EvalTotals;
 struct ChainArgs {
   const uint8_t* progs;
   const uint64_t* prog_off;
@@ -58,6 +59,7 @@ struct ChainArgs {
   uint32_t log_base;       // the run position alog[0] belongs to
   uint32_t* arrive;        // block arrivals of the cycle's last kernel (its last block selects)
   uint64_t* stamps;        // diagnostic (Engine::eval_stamps): block 0's s_memrealtime deltas, or null
+  EvalTotals* etot;        // k_eval's partials folded once by k_fold (large clusters), or null: every block folds
 };
 
 // Diagnostic stamps: block 0 / thread 0 of each chain kernel adds (now - entry)
@@ -303,7 +305,8 @@ __device__ __forceinline__ void chain_last_select(DevCluster& C, const DevProfil
 // node row loaded up front (RowV), 2 the same with the default Fit / BA
 // arguments compiled in.
 template <int ROWM>
-__global__ __launch_bounds__(kChain) void k_eval(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
+__device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, const ChainArgs& A,
+                                          const uint8_t* __restrict__ prog) {
   chain_warm(prog);
   CS_BEGIN;
   CS_GAP(42, 49, 48);
@@ -671,6 +674,20 @@ __device__ __forceinline__ int64_t pts_raw1(const ksg_prog* h, const EvalTotals&
   return (int64_t)round(__dadd_rn(0.0, __dadd_rn(__dmul_rn((double)cnt, E.w[0]), (double)(t.max_skew - 1))));
 }
 
+// Many blocks (large clusters): k_eval's partials folded once, by one block,
+// instead of by every block of k_ptsraw / k_final (O(blocks^2) partial reads).
+__global__ __launch_bounds__(kChain) void k_fold(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
+  __shared__ ChainRec lds[kChain / 64];
+  EvalTotals E;
+  reduce_eval(C, F, A, view(prog).h, E, lds);
+  if (threadIdx.x == 0) *A.etot = E;
+}
+__device__ __forceinline__ void eval_totals(const DevCluster& C, const DevProfile& F, const ChainArgs& A, const ksg_prog* h,
+                                            EvalTotals& E, ChainRec* lds) {
+  if (A.etot) E = *A.etot;
+  else reduce_eval(C, F, A, h, E, lds);
+}
+
 struct FinalShared {
   int32_t tv[KSG_MAX_TOPO * kChain];
   ChainRec rec[kChain / 64];
@@ -699,7 +716,7 @@ __global__ __launch_bounds__(kChain) void k_ptsraw(DevCluster C, DevProfile F, C
   }
   const ChainVids tv{L.tv + threadIdx.x};
   EvalTotals E;
-  reduce_eval(C, F, A, V.h, E, L.rec);
+  eval_totals(C, F, A, V.h, E, L.rec);
   ChainRec r;
   rec_init(r);
   if (active && of[n] == KSG_FILTER_PASS) {
@@ -718,7 +735,8 @@ __global__ __launch_bounds__(kChain) void k_ptsraw(DevCluster C, DevProfile F, C
   }
 }
 
-__global__ __launch_bounds__(kChain) void k_final(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
+__device__ __forceinline__ void final_body(DevCluster& C, const DevProfile& F, const ChainArgs& A,
+                                           const uint8_t* __restrict__ prog) {
   chain_warm(prog);
   CS_BEGIN;
   CS_GAP(40, 48, 49);
@@ -737,7 +755,7 @@ __global__ __launch_bounds__(kChain) void k_final(DevCluster C, DevProfile F, Ch
   const uint32_t ipa_flags = (uint32_t)A.pi[KCP_IPAF * A.nblk];  // k_eval's block 0
   EvalTotals E;
   CS(16);
-  reduce_eval(C, F, A, h, E, L.rec);
+  eval_totals(C, F, A, h, E, L.rec);
   CS(17);
   const bool multi = (h->tab & KTAB_PTS_MULTI) != 0;
   int64_t pmx = INT64_MIN, pmn = INT64_MAX;  // PodTopologySpread raw max / min over counted nodes
@@ -827,6 +845,26 @@ __global__ __launch_bounds__(kChain) void k_final(DevCluster C, DevProfile F, Ch
   }
   CS(20);
   chain_last_select(C, F, A, L.rec, prog);
+}
+
+// Kernels.  The *_occ twins cap registers at 4 waves per SIMD (a few spills)
+// for clusters of many blocks per CU; the plain ones keep every register for
+// the latency of one block per CU (cfg4).
+template <int ROWM>
+__global__ __launch_bounds__(kChain) void k_eval(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
+  eval_body<ROWM>(C, F, A, prog);
+}
+template <int ROWM>
+__global__ __launch_bounds__(kChain) __attribute__((amdgpu_waves_per_eu(4))) void k_eval_occ(
+    DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
+  eval_body<ROWM>(C, F, A, prog);
+}
+__global__ __launch_bounds__(kChain) void k_final(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
+  final_body(C, F, A, prog);
+}
+__global__ __launch_bounds__(kChain) __attribute__((amdgpu_waves_per_eu(4))) void k_final_occ(
+    DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
+  final_body(C, F, A, prog);
 }
 
 // The existing-pod table rows of the run's logged assumes, in log order (one

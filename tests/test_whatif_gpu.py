@@ -92,3 +92,29 @@ def test_sharded_whatif_matches_oracle(world, c):
         mp.spawn(_sharded_worker, args=(world, port, json.dumps(doc), out), nprocs=world, join=True)
         for r in range(world):
             assert out[r] == want, f"rank {r} differs"
+
+
+@pytest.mark.gpu
+def test_folded_partials_match_oracle(monkeypatch):
+    """Large clusters fold the table chain's per-block partials once (k_fold) instead of
+    in every block of k_final, and run the register-capped kernel twins; both forced
+    here on a small cfg4 cluster, queue and what-if."""
+    monkeypatch.setenv("KSG_FOLD_BLOCKS", "0")
+    monkeypatch.setenv("KSG_OCC_BLOCKS", "0")
+    doc = g.generate(4, n_nodes=700, n_existing=2500, n_pods=2 * STEP, n_zones=6)
+    o = Oracle(doc)
+    o.schedule(record=3)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    s.keep_outputs(0, 8)
+    s.schedule()
+    for q, r in enumerate(s.results()):
+        assert (r.selected, r.feasible, r.status) == o.result(q), q
+    for q in range(8):
+        assert s.annotations(q) == o.annotations(q), q
+    w = _oracle_steps(doc, 2)
+    t = Scheduler(doc["profile"])
+    t.load_cluster(doc)
+    for k in range(2):
+        t.whatif(k * STEP, STEP)
+    assert [(r.selected, r.feasible, r.status) for r in t.results()] == [w.result(q) for q in range(w.n_queue)]

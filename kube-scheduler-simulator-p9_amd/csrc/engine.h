@@ -51,6 +51,12 @@ struct NodeSoA {
   uint32_t n_ports = 0;                   // NodePorts: used host-port triple counts [n_ports][n]
   std::vector<int32_t> port_count;
   std::vector<int32_t> pvc_use;           // VolumeRestrictions: pods using each PVC id (bound pods of the whole cluster)
+  // NodeVolumeLimits: per limit key (attachable-volumes-csi-<driver>) the node's limit
+  // (-1 none) and its attached unique volumes; per CSI volume the nodes it is
+  // attached to (KSG_VOL_NODES slots, node -1 empty) and the pods using it there
+  uint32_t n_lkeys = 0, n_vols = 0;
+  std::vector<int32_t> vol_limit, vol_attached;  // [n_lkeys][n]
+  std::vector<int32_t> vol_node, vol_ref;        // [n_vols][KSG_VOL_NODES]
   // node-label vocabulary numeric view (Gt/Lt): per key offset into value tables
   std::vector<uint32_t> key_val_off;      // [n_keys+1]
   std::vector<int64_t> val_num;

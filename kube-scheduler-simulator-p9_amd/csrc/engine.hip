@@ -113,6 +113,10 @@ struct DevCluster {
   uint32_t n_ports;
   int32_t* ports;          // [n_ports][N] used host-port triple counts
   int32_t* pvcuse;         // [PVC ids] pods (bound + assumed) using the claim: NodeInfo PVCRefCounts summed
+  int32_t* vlim;           // [limit keys][N] NodeVolumeLimits limit (-1 none)
+  int32_t* vatt;           // [limit keys][N] attached unique CSI volumes
+  int32_t* vnode;          // [CSI volumes][KSG_VOL_NODES] nodes (local index) the volume is attached to, -1 empty
+  int32_t* vref;           // [CSI volumes][KSG_VOL_NODES] pods using it there
   DevTables T;
   // per topology slot, by value for fully unrolled loops (no load): its node
   // label key and its base among the shared-key pairs (-1: one node per value)
@@ -451,6 +455,25 @@ __device__ uint32_t volume_filter(const DevCluster& C, const ProgView& V, int po
     } else if (c.kind == KSG_VCHK_USED) {
       fail = false;
       for (int t = 0; t < c.cnt && !fail; ++t) fail = C.pvcuse[V.i32[c.off + t]] > 0;
+    } else if (c.kind == KSG_VCHK_LIMIT) {  // csi.go Filter: per limit key, attached + new > limit
+      fail = false;
+      for (int t = 0; t < c.cnt && !fail; ++t) {
+        const int32_t key = V.i32[c.off + 2 * t + 1];
+        bool first = true;  // count each key once, at its first pair
+        for (int u = 0; u < t; ++u) first &= V.i32[c.off + 2 * u + 1] != key;
+        if (!first) continue;
+        const int32_t lim = C.vlim[(size_t)key * C.N + n];
+        if (lim < 0) continue;
+        int32_t fresh = 0;
+        for (int u = t; u < c.cnt; ++u) {
+          if (V.i32[c.off + 2 * u + 1] != key) continue;
+          const int32_t* vn = C.vnode + (size_t)V.i32[c.off + 2 * u] * KSG_VOL_NODES;
+          bool on = false;
+          for (int k = 0; k < KSG_VOL_NODES; ++k) on |= vn[k] == (int32_t)n;
+          fresh += on ? 0 : 1;
+        }
+        fail = fresh > 0 && C.vatt[(size_t)key * C.N + n] + fresh > lim;
+      }
     }
     if (fail) bits |= (uint32_t)c.bits;
   }
@@ -1275,6 +1298,34 @@ __device__ void tables_assume(DevCluster& C, const ProgView& V, uint32_t n, int 
 __device__ void table_need(const ProgView& V, uint32_t need[4]);
 __device__ void table_write(DevCluster& C, const ProgView& V, uint32_t n, uint32_t row, uint32_t tb, uint32_t rb,
                             uint32_t vb);
+// NodeVolumeLimits' attached volumes of node n: the pod's CSI volumes (one thread)
+__device__ __forceinline__ void csi_assume(DevCluster& C, const ProgView& V, uint32_t n, int sign) {
+  const ksg_prog* h = V.h;
+  for (int i = 0; i < h->n_csi; ++i) {
+    const int32_t v = V.i32[h->csi_off + 2 * i], key = V.i32[h->csi_off + 2 * i + 1];
+    int32_t* vn = C.vnode + (size_t)v * KSG_VOL_NODES;
+    int32_t* vr = C.vref + (size_t)v * KSG_VOL_NODES;
+    int at = -1, empty = -1;
+    for (int k = 0; k < KSG_VOL_NODES; ++k) {
+      if (vn[k] == (int32_t)n) at = k;
+      if (vn[k] < 0 && empty < 0) empty = k;
+    }
+    if (sign > 0) {
+      if (at < 0) {
+        if (empty < 0) continue;  // (the host bounds the nodes per volume)
+        at = empty;
+        vn[at] = (int32_t)n;
+        vr[at] = 0;
+        C.vatt[(size_t)key * C.N + n] += 1;
+      }
+      vr[at] += 1;
+    } else if (at >= 0 && --vr[at] <= 0) {
+      vn[at] = -1;
+      C.vatt[(size_t)key * C.N + n] -= 1;
+    }
+  }
+}
+
 // assume (scheduleOne -> assume -> NodeInfo.AddPod, or its reversal for
 // Unreserve) of program V on local node n: resource rows, the class tables, and
 // for PTS/IPA profiles the existing-pod table (append; reversal marks the row
@@ -1290,6 +1341,7 @@ __device__ void assume_pod(DevCluster& C, const ProgView& V, uint32_t n, int sig
   C.podcnt[n] += sign;
   for (int i = 0; i < h->n_port_own; ++i) C.ports[(size_t)V.i32[h->port_own_off + i] * C.N + n] += sign;
   for (int i = 0; i < h->n_pvc; ++i) atomicAdd(&C.pvcuse[V.i32[h->pvc_off + i]], sign);
+  csi_assume(C, V, n, sign);
   if (sign < 0) {
     if (prow && *prow >= 0) {
       C.ptflags[*prow] |= KEF_DELETED;
@@ -3612,6 +3664,8 @@ struct Engine::Impl {
   DBuf<int32_t> ports, ports0;
   DBuf<int32_t> pvcuse, pvcuse0;  // PVC use counts (VolumeRestrictions ReadWriteOncePod)
   uint32_t n_pvc = 0;
+  DBuf<int32_t> vlim, vatt, vatt0, vnode, vnode0, vref, vref0;  // NodeVolumeLimits (CSI)
+  uint32_t n_vatt = 0, n_vnode = 0;
   uint32_t img_words = 0, n_ports = 0;
   NodeSoA topo;  // topology tables (host copy)
   DBuf<int32_t> topo_key_d;
@@ -3725,6 +3779,7 @@ struct Engine::Impl {
     C.haslab = haslab.p; C.kvo = kvo.p; C.vnum = vnum.p; C.vok = vok.p;
     C.nflags = nflags.p; C.img_words = img_words; C.img = img.p; C.n_ports = n_ports; C.ports = ports.p;
     C.pvcuse = pvcuse.p;
+    C.vlim = vlim.p; C.vatt = vatt.p; C.vnode = vnode.p; C.vref = vref.p;
     C.n_topo = (uint32_t)topo.topo_key.size();
     C.pairs = topo.topo_pairs;
     C.tkey = topo_key_d.p;
@@ -3895,6 +3950,17 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     pu.resize(std::max<size_t>(pu.size(), 1), 0);
     I.n_pvc = (uint32_t)pu.size();
     if (!I.pvcuse.upload(pu, s, err) || !I.pvcuse0.upload(pu, s, err)) return false;
+    std::vector<int32_t> vl = ns.vol_limit, va = ns.vol_attached, vn = ns.vol_node, vr = ns.vol_ref;
+    vl.resize(std::max<size_t>(vl.size(), 1), -1);
+    va.resize(std::max<size_t>(va.size(), 1), 0);
+    vn.resize(std::max<size_t>(vn.size(), 1), -1);
+    vr.resize(std::max<size_t>(vr.size(), 1), 0);
+    I.n_vatt = (uint32_t)va.size();
+    I.n_vnode = (uint32_t)vn.size();
+    if (!I.vlim.upload(vl, s, err) || !I.vatt.upload(va, s, err) || !I.vatt0.upload(va, s, err) ||
+        !I.vnode.upload(vn, s, err) || !I.vnode0.upload(vn, s, err) || !I.vref.upload(vr, s, err) ||
+        !I.vref0.upload(vr, s, err))
+      return false;
   }
   I.topo = NodeSoA();
   I.topo.topo_key = ns.topo_key;
@@ -5083,6 +5149,9 @@ bool Engine::reset(std::string& err) {
   if (I.n_ports)
     HIPCHK(hipMemcpyAsync(I.ports.p, I.ports0.p, (size_t)I.n_ports * I.N * 4, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemcpyAsync(I.pvcuse.p, I.pvcuse0.p, (size_t)I.n_pvc * 4, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.vatt.p, I.vatt0.p, (size_t)I.n_vatt * 4, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.vnode.p, I.vnode0.p, (size_t)I.n_vnode * 4, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(I.vref.p, I.vref0.p, (size_t)I.n_vnode * 4, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemcpyAsync(I.tcounts.p, I.counts0, sizeof(I.counts0), hipMemcpyHostToDevice, s));
   if (!rebuild_class_tables(err)) return false;  // from the restored existing-pod table
   uint32_t cnt = (uint32_t)I.prog_off.size();

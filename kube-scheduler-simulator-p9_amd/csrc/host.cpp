@@ -668,6 +668,7 @@ struct PV {
   bool claimed = false;               // spec.claimRef
   string cref_ns, cref_name;
   bool csi = false, intree = false;   // spec.csi / an in-tree cloud disk source
+  string csi_driver, csi_handle;
 };
 struct SClass {
   string name, provisioner;
@@ -715,6 +716,10 @@ static PV parse_pv(const J& v) {
       p.cref_name = str_of((*cr)["name"]);
     }
     p.csi = (*sp)["csi"] && !(*sp)["csi"]->null();
+    if (p.csi) {
+      p.csi_driver = str_of((*(*sp)["csi"])["driver"]);
+      p.csi_handle = str_of((*(*sp)["csi"])["volumeHandle"]);
+    }
     for (const char* k : {"awsElasticBlockStore", "gcePersistentDisk", "azureDisk", "cinder"})
       if ((*sp)[k] && !(*sp)[k]->null()) p.intree = true;
   }
@@ -770,8 +775,10 @@ struct Cluster {
   std::map<string, PVC> pvcs;  // "ns/name"
   std::map<string, PV> pvs;
   std::map<string, SClass> classes;
-  bool attach_limits = false;  // some node declares volume attach limits (csiNodes / attachable-volumes-*)
+  map<string, map<string, i64>> csi_counts;  // CSINode: node -> driver -> allocatable count
   Dict pvc_ids;                // PVC keys "ns/name" the pods use (device use counts)
+  Dict lkeys;                  // NodeVolumeLimits limit keys (attachable-volumes-csi-<driver>)
+  Dict vols;                   // CSI volumes (driver/handle) the pods use
   // vocabularies
   Dict res;  // resource columns
   Dict nkeys;
@@ -1278,6 +1285,12 @@ struct Cluster {
       if (!port_id.count(std::make_tuple(h.ip, h.proto, h.port))) return false;
     for (auto& c : p.claims)
       if (pvc_ids.get(p.ns + "/" + c) < 0) return false;  // the device PVC use counts: re-encode
+    if (has_volume_plugins) {
+      vector<std::pair<string, string>> av;
+      attachable(p, av);
+      for (auto& x : av)
+        if (vols.get(x.first) < 0 || lkeys.get(x.second) < 0) return false;
+    }
     return true;
   }
   // Intern pod p's label space in place; new label keys widen the device's
@@ -1291,9 +1304,27 @@ struct Cluster {
 
   bool build_vocab() {
     pvc_ids = Dict();
+    lkeys = Dict();
+    vols = Dict();
     for (auto* v : {&bound, &queue})
       for (auto& p : *v)
         for (auto& c : p.claims) pvc_ids.add(p.ns + "/" + c);
+    if (has_volume_plugins) {  // NodeVolumeLimits: limit keys and CSI volumes
+      for (auto& n : nodes)
+        for (auto& kv : n.alloc)
+          if (kv.first.rfind("attachable-volumes-", 0) == 0) lkeys.add(kv.first);
+      for (auto& kv : csi_counts)
+        for (auto& d : kv.second) lkeys.add("attachable-volumes-csi-" + d.first);
+      vector<std::pair<string, string>> av;
+      for (auto* v : {&bound, &queue})
+        for (auto& p : *v) {
+          attachable(p, av);
+          for (auto& x : av) {
+            vols.add(x.first);
+            lkeys.add(x.second);
+          }
+        }
+    }
     res = Dict();
     res.add("cpu");
     res.add("memory");
@@ -1433,6 +1464,50 @@ struct Cluster {
     for (auto& p : bound)
       if (node_names.get(p.node) >= 0)
         for (auto& c : p.claims) S.pvc_use[pvc_ids.get(p.ns + "/" + c)] += 1;
+    // NodeVolumeLimits (csi.go getVolumeLimits: attachable-volumes-* allocatable,
+    // CSINode counts over them; attached volumes of the bound pods, each once per node)
+    S.n_lkeys = (uint32_t)lkeys.names.size();
+    S.n_vols = (uint32_t)vols.names.size();
+    S.vol_limit.assign((size_t)S.n_lkeys * n, -1);
+    S.vol_attached.assign((size_t)S.n_lkeys * n, 0);
+    S.vol_node.assign((size_t)S.n_vols * KSG_VOL_NODES, -1);
+    S.vol_ref.assign((size_t)S.n_vols * KSG_VOL_NODES, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+      const Node& nd = nodes[lo + i];
+      for (auto& kv : nd.alloc) {
+        const int32_t k = lkeys.get(kv.first);
+        if (k >= 0) S.vol_limit[(size_t)k * n + i] = (int32_t)as_value(kv.second);
+      }
+      auto it = csi_counts.find(nd.name);
+      if (it != csi_counts.end())
+        for (auto& d : it->second) S.vol_limit[(size_t)lkeys.get("attachable-volumes-csi-" + d.first) * n + i] = (int32_t)d.second;
+    }
+    if (S.n_vols) {
+      vector<std::pair<string, string>> av;
+      for (auto& p : bound) {
+        const int32_t g = node_names.get(p.node);
+        if (g < 0 || (uint32_t)g < lo || (uint32_t)g >= hi) continue;
+        const int32_t i = g - (int32_t)lo;
+        attachable(p, av);
+        for (auto& x : av) {
+          const int32_t v = vols.get(x.first);
+          int32_t* vn = &S.vol_node[(size_t)v * KSG_VOL_NODES];
+          int32_t* vr = &S.vol_ref[(size_t)v * KSG_VOL_NODES];
+          int at = -1, empty = -1;
+          for (int k = 0; k < KSG_VOL_NODES; ++k) {
+            if (vn[k] == i) at = k;
+            if (vn[k] < 0 && empty < 0) empty = k;
+          }
+          if (at < 0) {
+            if (empty < 0) { err = "CSI volume " + x.first + " attached to more than 16 nodes (not modelled)"; return false; }
+            at = empty;
+            vn[at] = i;
+            S.vol_attached[(size_t)lkeys.get(x.second) * n + i] += 1;
+          }
+          vr[at] += 1;
+        }
+      }
+    }
     S.taint_off.assign(n + 1, 0);
     for (uint32_t i = 0; i < n; ++i) {
       const Node& nd = nodes[lo + i];
@@ -1712,6 +1787,31 @@ struct Cluster {
     const SClass* sc = class_of(c.cls);
     return sc && sc->has_mode && sc->wffc;
   }
+  // nodevolumelimits csi.go filterAttachableVolumes: the pod's CSI volumes as
+  // (driver/handle, limit key) — an unbound claim, or one whose PV is missing,
+  // counts by its class's provisioner and the claim (getCSIDriverInfoFromSC)
+  void attachable(const Pod& p, vector<std::pair<string, string>>& out) const {
+    out.clear();
+    set<string> seen;
+    for (auto& cn : p.claims) {
+      const PVC* c = pvc_of(p.ns, cn);
+      if (!c) continue;
+      string driver, handle;
+      const PV* v = c->volume_name.empty() ? nullptr : pv_of(c->volume_name);
+      if (!v) {
+        const SClass* sc = c->cls.empty() ? nullptr : class_of(c->cls);
+        if (sc) {
+          driver = sc->provisioner;
+          handle = "ksg-" + c->ns + "/" + c->name;
+        }
+      } else if (v->csi) {
+        driver = v->csi_driver;
+        handle = v->csi_handle;
+      }
+      if (driver.empty() || handle.empty() || !seen.insert(driver + "/" + handle).second) continue;
+      out.push_back({driver + "/" + handle, "attachable-volumes-csi-" + driver});  // GetCSIAttachLimitKey
+    }
+  }
   // Inputs whose volume-plugin results this build does not model are refused
   // with an error, never approximated.
   bool volumes_modelled(const Pod& p) {
@@ -1723,7 +1823,26 @@ struct Cluster {
     if (p.volume_plugins_act) return no("volumes other than persistentVolumeClaim");
     if (p.claims.empty()) return true;
     if (shards != 1) return no("persistent volume claims on a sharded context");
-    if (attach_limits && has_vkind(VK_CSI)) return no("nodes declaring volume attach limits");
+    if (has_vkind(VK_CSI)) {
+      vector<std::pair<string, string>> mine;
+      attachable(p, mine);
+      for (auto& v : mine) {
+        if (v.second.size() >= 63) return no("a CSI driver name whose attach-limit key is hashed");
+        set<string> at;  // nodes the volume may be attached to: its bound users' nodes + every queue user
+        size_t queued = 0;
+        for (auto* list : {&bound, &queue})
+          for (auto& o : *list) {
+            vector<std::pair<string, string>> theirs;
+            attachable(o, theirs);
+            for (auto& t : theirs)
+              if (t.first == v.first) {
+                if (list == &bound) at.insert(o.node);
+                else queued++;
+              }
+          }
+        if (at.size() + queued > KSG_VOL_NODES) return no("a CSI volume used on more than 16 nodes");
+      }
+    }
     const bool rejecting = has_vkind(VK_RESTRICT) || has_vkind(VK_BIND) || has_vkind(VK_ZONE);
     auto users = [&](const string& ns, const string& cn, bool queue_too) {
       int u = 0;
@@ -1847,6 +1966,16 @@ struct Cluster {
     }
     h.n_pvc = (int32_t)p.claims.size();
     if (!has_volume_plugins) return true;
+    vector<std::pair<string, string>> av;  // NodeVolumeLimits: attached-volume delta of the assume
+    attachable(p, av);
+    h.csi_off = (int32_t)P.i32.size();
+    for (auto& x : av) {
+      const int32_t v = vols.get(x.first), k = lkeys.get(x.second);
+      if (v < 0 || k < 0) { err = "internal: CSI volume " + x.first + " not interned"; return false; }
+      P.i32.push_back(v);
+      P.i32.push_back(k);
+    }
+    h.n_csi = (int32_t)av.size();
     vector<ksg_vchk> chk;
     int vb_pos = -1;
     for (int pos = 0; pos < n_plugins; ++pos) {
@@ -2009,8 +2138,10 @@ struct Cluster {
           P.sel.push_back(all);
         }
       }
-      // (EBS / GCE / Azure limits, NodeVolumeLimits: the claims bring no volume they
-      // count against a limit, volumes_modelled: every node passes)
+      if (vk == VK_CSI && !skip && h.n_csi > 0)  // csi.go Filter: attached + new volumes per limit key
+        add(KSG_VCHK_LIMIT, KSG_VOL_MAX_COUNT, 0, h.csi_off, h.n_csi);
+      // (EBS / GCE / Azure limits: the claims bring no in-tree volume they count,
+      // volumes_modelled: every node passes)
       if (skip) m.vol_skip |= 1u << pos;
       if (!fail.empty()) {
         if (m.prefilter_fail_pos < 0 || pos < m.prefilter_fail_pos) {
@@ -2434,9 +2565,16 @@ struct Cluster {
       for (auto& x : a->items) { PV v = parse_pv(x); pvs[v.name] = v; }
     if (const J* a = d["storageClasses"])
       for (auto& x : a->items) { SClass c = parse_sc(x); classes[c.name] = c; }
-    attach_limits = d["csiNodes"] && d["csiNodes"]->size() > 0;
-    for (auto& n : nodes)
-      for (auto& kv : n.alloc) attach_limits |= kv.first.rfind("attachable-volumes-", 0) == 0;
+    csi_counts.clear();
+    if (const J* a = d["csiNodes"])
+      for (auto& x : a->items) {
+        const string node = (x["metadata"] ? str_of((*x["metadata"])["name"]) : "");
+        if (const J* sp = x["spec"])
+          if (const J* ds = (*sp)["drivers"])
+            for (auto& dr : ds->items)
+              if (const J* al = dr["allocatable"]; al && !al->null())
+                if (const J* c = (*al)["count"]; c && !c->null()) csi_counts[node][str_of(dr["name"])] = c->num();
+      }
     index_queue();
     qneed.clear();
     broken = false;
@@ -2566,6 +2704,12 @@ struct Cluster {
     if (nss.get(p.ns) < 0) return true;
     for (auto& c : p.claims)
       if (pvc_ids.get(p.ns + "/" + c) < 0) return true;  // a PVC the device use counts do not cover
+    if (has_volume_plugins) {
+      vector<std::pair<string, string>> av;
+      attachable(p, av);
+      for (auto& x : av)
+        if (vols.get(x.first) < 0 || lkeys.get(x.second) < 0) return true;  // NodeVolumeLimits tables
+    }
     auto known = [&](const string& key, const string* v) {
       int32_t k = pkeys.get(key);
       return k >= 0 && k < (int32_t)pvals.size() && (!v || pvals[k].get(*v) >= 0);
@@ -3254,15 +3398,10 @@ struct Cluster {
     std::swap(qmode, qm);
     std::swap(placed, pl);
     bound_at_valid = false;
-    bool vol_ok = true;  // the batch may change what the volume plugins see (claim users, attach limits)
-    if (has_volume_plugins) {
-      bool limits = attach_limits;
-      for (auto& n : nodes)
-        for (auto& kv : n.alloc) attach_limits |= kv.first.rfind("attachable-volumes-", 0) == 0;
+    bool vol_ok = true;  // the batch may change what the volume plugins see (claim users)
+    if (has_volume_plugins)
       for (size_t q = 0; q < queue.size() && vol_ok; ++q)
         if (qmode.size() <= q || qmode[q] == 0) vol_ok = volumes_modelled(queue[q]);
-      if (!vol_ok) attach_limits = limits;
-    }
     if (!vol_ok || !equal_priorities()) {
       std::swap(nodes, nn);
       std::swap(bound, bb);
@@ -3358,6 +3497,7 @@ struct Cluster {
         if (vkind[pos] == VK_RESTRICT)
           return "node has pod using PersistentVolumeClaim with the same name and ReadWriteOncePod access mode";
         if (vkind[pos] == VK_ZONE) return "node(s) had no available volume zone";
+        if (vkind[pos] == VK_CSI) return "node(s) exceed max volume count";
         string m;
         auto add = [&](const char* r) { m += (m.empty() ? "" : ", ") + string(r); };
         if (detail & KSG_VOL_NODE_CONFLICT) add("node(s) had volume node affinity conflict");
@@ -3434,7 +3574,7 @@ struct Cluster {
     if (pos > fail_pos) return -1;
     const uint32_t detail = code_detail(code);
     msg = filter_message(pos, detail);
-    if (is_volume(plugins[pos])) return vkind[pos] == VK_RESTRICT ? C_UNSCHED : C_UNRESOLVABLE;
+    if (is_volume(plugins[pos])) return vkind[pos] == VK_RESTRICT || vkind[pos] == VK_CSI ? C_UNSCHED : C_UNRESOLVABLE;
     switch (plugins[pos]) {
       case P_FIT: {  // fit.go Filter: UnschedulableAndUnresolvable when a request exceeds the allocatable
         vector<i64> rq;

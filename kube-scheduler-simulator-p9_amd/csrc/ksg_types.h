@@ -62,6 +62,8 @@
 #define KSG_VOL_BIND_CONFLICT (1u << 2)   // VolumeBinding ErrReasonBindConflict
 #define KSG_VOL_PV_NOT_EXIST (1u << 3)    // VolumeBinding ErrReasonPVNotExist
 #define KSG_VOL_ZONE_CONFLICT (1u << 4)   // VolumeZone ErrReasonConflict
+#define KSG_VOL_MAX_COUNT (1u << 5)       // NodeVolumeLimits ErrReasonMaxVolumeCountExceeded
+#define KSG_VOL_NODES 16                  // nodes one CSI volume may be attached to (host-checked)
 
 // requirement operators (labels.Requirement / node selector requirement)
 #define KR_IN 0          // present && value in vals
@@ -132,6 +134,8 @@ typedef struct ksg_tsc {
 #define KSG_VCHK_FAIL 0   // always fails (pod-uniform verdict)
 #define KSG_VCHK_SELS 1   // fails unless one of the node selector terms pool_sel[off .. off+cnt) matches
 #define KSG_VCHK_USED 2   // fails if a PVC of pool_i32[off .. off+cnt) is used by a pod (ReadWriteOncePod)
+#define KSG_VCHK_LIMIT 3  // NodeVolumeLimits: (volume, limit key) pairs pool_i32[off .. off+2*cnt): attached + new
+                          // volumes of a key above the node's limit for it fails
 typedef struct ksg_vchk {
   int32_t dpos, sub, kind, bits, unless, off, cnt, pad;
 } ksg_vchk;  // 32 B, in pool_i32 (8 words each)
@@ -272,6 +276,7 @@ typedef struct ksg_prog {
   // ---- volume plugins
   int32_t n_vchk, vchk_off;  // pool_i32: ksg_vchk records (8 words each)
   int32_t n_pvc, pvc_off;    // pool_i32: PVC ids of the pod's volumes (NodeInfo PVCRefCounts delta on assume)
+  int32_t n_csi, csi_off;    // pool_i32: (CSI volume, limit key) pairs of the pod (attached-volume delta on assume)
 
   // ---- pools (byte offsets from the start of the blob)
   uint32_t off_i32, n_i32;

@@ -247,6 +247,7 @@ __device__ __forceinline__ void assume_row_atomic(DevCluster& C, const ProgView&
   atomicAdd(&C.podcnt[n], sign);
   for (int i = 0; i < h->n_port_own; ++i) atomicAdd(&C.ports[(size_t)V.i32[h->port_own_off + i] * C.N + n], sign);
   for (int i = 0; i < h->n_pvc; ++i) atomicAdd(&C.pvcuse[V.i32[h->pvc_off + i]], sign);
+  csi_assume(C, V, n, sign);
 }
 
 // selectHost + the assume, by the last-arriving block of the cycle's last

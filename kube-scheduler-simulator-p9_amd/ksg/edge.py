@@ -42,7 +42,7 @@ Variants (each a small seeded cluster, same document shape as ``generator``):
   annotation, a class without a provisioner), immediate and pre-bound unbound
   claims, deleting / lost / missing claims, ReadWriteOncePod claims used by a
   bound pod or shared by two queue pods; nodes with and without zone / region
-  labels.
+  labels; CSI attach limits from CSINode counts or the legacy allocatable key.
 """
 from __future__ import annotations
 
@@ -587,10 +587,23 @@ def gen_volumes(n_nodes=40, n_existing=60, n_pods=120, seed=None):
             spec["nodeSelector"] = {ZONE: r.pick(["zone-0", "zone-1"])}
         queue.append(pod_obj(f"pod-{j:07d}", [req(100 * (1 + r.below(10)), 256 * Mi * (1 + r.below(8)))],
                              ns=ns, **spec))
+    # NodeVolumeLimits: CSINode driver counts on some nodes, the legacy allocatable key on others
+    csi_nodes = []
+    for i, n in enumerate(nodes):
+        k = r.pct()
+        if k < 35:
+            csi_nodes.append({"metadata": {"name": n["metadata"]["name"]},
+                              "spec": {"drivers": [{"name": CSI, "nodeID": n["metadata"]["name"],
+                                                    "allocatable": {"count": 1 + r.below(3)}}]}})
+        elif k < 50:
+            n["status"]["allocatable"]["attachable-volumes-csi-" + CSI] = str(1 + r.below(3))
+        elif k < 55:
+            csi_nodes.append({"metadata": {"name": n["metadata"]["name"]},
+                              "spec": {"drivers": [{"name": CSI, "nodeID": n["metadata"]["name"]}]}})  # no count
     from .generator import DEFAULT_PROFILE
     prof = make_profile(DEFAULT_PROFILE, seed)
     return {"profile": prof, "nodes": nodes, "pods": bound, "queue": queue, "pvs": pvs, "pvcs": pvcs,
-            "storageClasses": classes}
+            "storageClasses": classes, "csiNodes": csi_nodes}
 
 
 def generate_edge(variant: str, **sizes) -> dict:

@@ -495,7 +495,8 @@ struct Node {
   Labels labels;
   vector<Taint> taints;
   Resource alloc;
-  vector<string> alloc_raw;  // allocatable resource names (attach limits: attachable-volumes-*)
+  vector<string> alloc_raw;  // allocatable resource names
+  map<string, i64> attach_alloc;  // attachable-volumes-* allocatable (volume attach limits)
   bool unschedulable = false;
   vector<NodeImage> images;
 };
@@ -662,7 +663,12 @@ static void parse_node(const ojson::Value& v, Node& n) {
   auto* st = v.get("status");
   resource_add(n.alloc, parse_rl(st ? st->get("allocatable") : nullptr));
   if (auto* al = st ? st->get("allocatable") : nullptr)
-    for (auto& kv : al->obj) n.alloc_raw.push_back(kv.first);
+    for (auto& kv : al->obj) {
+      n.alloc_raw.push_back(kv.first);
+      i128 q;
+      if (kv.first.rfind("attachable-volumes-", 0) == 0 && parse_quantity(kv.second.str(), q))
+        n.attach_alloc[kv.first] = (i64)(q / 1000000000);  // (quantity in nano units)
+    }
   if (st)
     if (auto* im = st->get("images"))
       for (auto& x : im->arr) {
@@ -995,6 +1001,8 @@ struct VolumeObj {
   bool claim_ref = false;
   string ref_ns, ref_name;
   bool intree = false;
+  bool csi = false;                // spec.csi
+  string csi_driver, csi_handle;
   const ojson::Value* required_json = nullptr;
 };
 struct ClassObj {
@@ -1089,7 +1097,7 @@ struct Cluster {
   map<string, VolumeObj> volumes;
   map<string, ClassObj> classes;
   map<string, int> pvc_refs;
-  bool attach_limits = false;
+  map<string, map<string, i64>> csi_counts;  // CSINode: node -> driver -> spec.drivers[].allocatable.count
   // results
   vector<PodResult> results;
   std::mutex store_mu;
@@ -1181,6 +1189,62 @@ struct Cluster {
   // nodevolumelimits non_csi.go / csi.go PreFilter: Skip without a PVC (the claims
   // accepted at load bring no volume either counts against a limit: Filter passes)
   static Status limits_prefilter(const Pod& p) { return p.claims.empty() ? Status::skip() : Status{}; }
+  // nodevolumelimits csi.go: volumeutil.GetCSIAttachLimitKey (keys of 63+ characters,
+  // which it hashes, are refused at load)
+  static string csi_limit_key(const string& driver) { return "attachable-volumes-csi-" + driver; }
+  // filterAttachableVolumes: unique volume name (driver/handle) -> limit key of the pod's
+  // CSI volumes; an unbound claim (or one whose PV is missing) counts by its class's
+  // provisioner and the claim's name (getCSIDriverInfoFromSC's handle)
+  void attachable_volumes(const Pod& p, map<string, string>& out) const {
+    for (auto& cn : p.claims) {
+      const ClaimObj* c = find_claim(p.ns, cn);
+      if (!c) continue;
+      string driver, handle;
+      auto from_class = [&] {
+        if (c->class_name.empty()) return;
+        auto k = classes.find(c->class_name);
+        if (k == classes.end()) return;
+        driver = k->second.provisioner;
+        handle = "ksg-" + c->ns + "/" + c->name;
+      };
+      auto v = c->volume_name.empty() ? volumes.end() : volumes.find(c->volume_name);
+      if (c->volume_name.empty() || v == volumes.end()) from_class();
+      else if (v->second.csi) {
+        driver = v->second.csi_driver;
+        handle = v->second.csi_handle;
+      }
+      if (driver.empty() || handle.empty()) continue;
+      out[driver + "/" + handle] = csi_limit_key(driver);
+    }
+  }
+  // getVolumeLimits: attachable-volumes-* of the node's allocatable, CSINode counts over them
+  map<string, i64> volume_limits(int ni) const {
+    map<string, i64> lim = nodes[ni].attach_alloc;
+    auto it = csi_counts.find(nodes[ni].name);
+    if (it != csi_counts.end())
+      for (auto& kv : it->second) lim[csi_limit_key(kv.first)] = kv.second;
+    return lim;
+  }
+  Status csi_filter(const Pod& p, int ni) const {
+    map<string, string> fresh, attached;
+    attachable_volumes(p, fresh);
+    if (fresh.empty()) return {};
+    const map<string, i64> lim = volume_limits(ni);
+    if (lim.empty()) return {};
+    for (int pi : infos[ni].pods) attachable_volumes(pods[pi].pod, attached);
+    map<string, int> have, want;
+    for (auto& kv : attached) {
+      fresh.erase(kv.first);  // a volume already attached is not counted twice
+      have[kv.second]++;
+    }
+    for (auto& kv : fresh) want[kv.second]++;
+    for (auto& kv : want) {
+      auto l = lim.find(kv.first);
+      if (l != lim.end() && have[kv.first] + kv.second > l->second)
+        return {Status::Unschedulable, "node(s) exceed max volume count"};
+    }
+    return {};
+  }
   // volume.GetLocalPersistentVolumeNodeNames
   static set<string> local_pv_nodes(const VolumeObj& v) {
     set<string> out;
@@ -1411,6 +1475,7 @@ struct Cluster {
       else if (id == P_NODENAME) s = nodename_filter(p, ni);
       else if (id == P_PORTS) s = ports_filter(cs, ni);
       else if (id == P_VOLRESTRICT) s = vr_filter(cs);
+      else if (id == P_CSILIMITS) s = csi_filter(p, ni);
       else if (id == P_VOLBIND) s = vb_filter(cs, ni);
       else if (id == P_VOLZONE) s = vz_filter(cs, ni);
       if (!s.ok()) return false;
@@ -2221,6 +2286,7 @@ struct Cluster {
         else if (id == P_NODENAME) s = nodename_filter(p, ni);
         else if (id == P_PORTS) s = ports_filter(cs, ni);
         else if (id == P_VOLRESTRICT) s = vr_filter(cs);
+        else if (id == P_CSILIMITS) s = csi_filter(p, ni);
         else if (id == P_VOLBIND) s = vb_filter(cs, ni);
         else if (id == P_VOLZONE) s = vz_filter(cs, ni);
         rec([&] { r.filter[nodes[ni].name][profile_names[k]] = s.ok() ? "passed" : s.msg; });
@@ -2636,6 +2702,11 @@ static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
         }
         for (const char* k : {"awsElasticBlockStore", "gcePersistentDisk", "azureDisk", "cinder"})
           o.intree = o.intree || (sp->get(k) && !sp->get(k)->is_null());
+        if (auto* cs = sp->get("csi"); cs && !cs->is_null()) {
+          o.csi = true;
+          o.csi_driver = cs->get("driver") ? cs->get("driver")->str() : "";
+          o.csi_handle = cs->get("volumeHandle") ? cs->get("volumeHandle")->str() : "";
+        }
       }
       beta_class(md, o.class_name);
       c.volumes[o.name] = o;
@@ -2659,9 +2730,18 @@ static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
         }
       c.classes[o.name] = o;
     }
-  c.attach_limits = d.get("csiNodes") && !d.get("csiNodes")->arr.empty();
-  for (auto& n : c.nodes)
-    for (auto& kv : n.alloc_raw) c.attach_limits = c.attach_limits || kv.rfind("attachable-volumes-", 0) == 0;
+  if (auto* a = d.get("csiNodes"))
+    for (auto& v : a->arr) {
+      auto* md = v.get("metadata");
+      const string node = md && md->get("name") ? md->get("name")->str() : "";
+      auto* sp = v.get("spec");
+      if (auto* ds = sp ? sp->get("drivers") : nullptr)
+        for (auto& dr : ds->arr) {
+          auto* al = dr.get("allocatable");
+          auto* cnt = al && !al->is_null() ? al->get("count") : nullptr;
+          if (cnt && !cnt->is_null()) c.csi_counts[node][dr.get("name") ? dr.get("name")->str() : ""] = cnt->i64();
+        }
+    }
   // Volume inputs outside the model are refused, never approximated
   auto in_profile = [&](PluginId id) { return std::find(c.profile.begin(), c.profile.end(), id) != c.profile.end(); };
   bool vol = false;
@@ -2676,7 +2756,12 @@ static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
       };
       if (p.volume_plugins_act) return refuse("volumes other than persistentVolumeClaim");
       if (p.claims.empty()) continue;
-      if (c.attach_limits && in_profile(P_CSILIMITS)) return refuse("nodes declaring volume attach limits");
+      if (in_profile(P_CSILIMITS)) {
+        map<string, string> mine;
+        c.attachable_volumes(p, mine);
+        for (auto& kv : mine)
+          if (kv.second.size() >= 63) return refuse("a CSI driver name whose attach-limit key is hashed");
+      }
       auto count_users = [&](const string& ns, const string& name, bool with_queue) {
         int u = 0;
         for (size_t i = 0; i < c.pods.size(); ++i) {

@@ -33,6 +33,15 @@ def _known_clusters():
                    [kv.WFFC])
     d["profile"] = make_profile(kv.PROFILE[:-1], 7)
     docs.append(d)
+    drv = "csi.example.com"  # NodeVolumeLimits (test_csi_attach_limits)
+    pvs = [E._pv("pv-a", "wffc", claim=("default", "a")), E._pv("pv-b", "wffc", claim=("default", "b"))]
+    pvcs = [E._pvc("a", "default", volume="pv-a", cls="wffc", bound=True),
+            E._pvc("b", "default", volume="pv-b", cls="wffc", bound=True)]
+    d = kv.cluster(kv.with_claims("p", "a"), pvcs, pvs, [kv.WFFC], bound=[kv.with_claims("h0", "b", node="n0"),
+                                                                          kv.with_claims("h1", "b", node="n1")])
+    d["csiNodes"] = [{"metadata": {"name": "n0"}, "spec": {"drivers": [{"name": drv, "allocatable": {"count": 1}}]}}]
+    d["nodes"][1]["status"]["allocatable"]["attachable-volumes-csi-" + drv] = "2"
+    docs.append(d)
     return docs
 
 

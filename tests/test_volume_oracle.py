@@ -156,3 +156,27 @@ def test_rwop_conflict_preemption():
     o.schedule(record=3)
     assert o.result(0) == (-1, 0, 1)
     assert o.nominated(0) == (2, ["default/holder"])
+
+
+def test_csi_attach_limits():
+    """NodeVolumeLimits (csi.go): n0 allows 1 volume of the driver (CSINode count) and already
+    holds one of another claim -> "node(s) exceed max volume count" (Unschedulable); n1's
+    limit 2 comes from the legacy allocatable key; a volume already attached on a node is
+    not counted twice; n2 declares no limit."""
+    drv = "csi.example.com"
+    pvs = [edge._pv("pv-a", "wffc", claim=("default", "a")), edge._pv("pv-b", "wffc", claim=("default", "b"))]
+    pvcs = [edge._pvc("a", "default", volume="pv-a", cls="wffc", bound=True),
+            edge._pvc("b", "default", volume="pv-b", cls="wffc", bound=True)]
+    doc = cluster(with_claims("p", "a"), pvcs, pvs, [WFFC], bound=[with_claims("h0", "b", node="n0"),
+                                                                   with_claims("h1", "b", node="n1")])
+    doc["csiNodes"] = [{"metadata": {"name": "n0"}, "spec": {"drivers": [{"name": drv, "allocatable": {"count": 1}}]}}]
+    doc["nodes"][1]["status"]["allocatable"]["attachable-volumes-csi-" + drv] = "2"
+    (sel, feas, st), a = run(doc)
+    f = a["filter-result"]
+    assert f["n0"]["NodeVolumeLimits"] == "node(s) exceed max volume count"
+    assert f["n1"]["NodeVolumeLimits"] == "passed" and f["n2"]["NodeVolumeLimits"] == "passed"
+    assert feas == 2
+    # the pod's volume already attached on n0 (a holder of "a" there): nothing new, n0 passes
+    doc["pods"].append(with_claims("h2", "a", node="n0"))
+    (sel, feas, st), a = run(doc)
+    assert a["filter-result"]["n0"]["NodeVolumeLimits"] == "passed" and feas == 3

@@ -172,6 +172,13 @@ int ksg_reserve(ksg_ctx* ctx, uint32_t q, int32_t node);
 /* ReservePlugin.Unreserve (mock framework.go:611): undo the assume of queue
  * pod q (cycle or queue mode): node rows, and its existing-pod table entry. */
 int ksg_unreserve(ksg_ctx* ctx, uint32_t q);
+/* Bounded memory in plugin mode: queue pods [0, keep_from) leave the queue —
+ * the placed ones become bound pods of the snapshot, the rest are forgotten
+ * (their documents released) — and pod keep_from + i becomes queue pod i, its
+ * results and placement kept.  One snapshot re-encode; call between cycles with
+ * keep_from = the oldest pod whose Reserve / Unreserve / lookups may still come
+ * (ksg_queue_len() when none). */
+int ksg_compact(ksg_ctx* ctx, uint32_t keep_from);
 
 /* ---- what each wrapped plugin's extension point returns (the Go plugin's calls,
  * INTEGRATION.md), for queue pod q whose per-node outputs are kept (the pod of the

@@ -271,6 +271,7 @@ struct Pod {
   vector<HostPort> ports; // Spec.Containers host ports (hostPort > 0), sanitised
   bool volume_plugins_act = false;  // a volume other than a PVC the volume plugins act on (not modelled)
   vector<string> claims;            // spec.volumes[].persistentVolumeClaim.claimName, in volume order
+  int32_t doc = -1;                 // index of a JSON document only this pod references (ksg_cycle), or -1
   i64 priority = 0;                 // spec.priority (PrioritySort order is the caller's; DefaultPreemption)
   bool preempt_never = false;       // spec.preemptionPolicy Never (PodEligibleToPreemptOthers)
   i64 start_time = INT64_MAX;       // status.startTime, epoch seconds; none: started last (GetPodStartTime: now)
@@ -2741,12 +2742,14 @@ struct Cluster {
   // Re-encode and re-upload the snapshot with every assumed queue pod as a bound
   // pod, recompile the queue, and restore the per-pod summaries.
   // remap: old node index -> new index, when nodes were removed (cluster events).
-  bool rebuild(const vector<int32_t>* remap = nullptr) {
+  // given: the queue's summaries (compaction re-indexes the queue), else read from the device
+  bool rebuild(const vector<int32_t>* remap = nullptr, const vector<ksg_pod_summary>* given = nullptr) {
     track_queue();
     size_t nq = queue.size();
-    const size_t ns = compiled ? progs.size() : 0;  // pods with programs (and summaries) on the device
+    const size_t ns = given ? given->size() : compiled ? progs.size() : 0;  // pods with summaries on the device
     vector<ksg_pod_summary> sum(nq);
-    if (ns && !eng->summaries(0, (uint32_t)ns, sum.data(), err)) return false;
+    if (given) std::copy(given->begin(), given->end(), sum.begin());
+    else if (ns && !eng->summaries(0, (uint32_t)ns, sum.data(), err)) return false;
     if (remap)
       for (size_t q = 0; q < ns; ++q)
         if (sum[q].selected >= 0 && sum[q].selected < (int32_t)remap->size()) {
@@ -2798,6 +2801,50 @@ struct Cluster {
     ++epoch;
     return true;
   }
+  // Bounded memory in plugin mode (ksg_compact): queue pods [0, keep_from) leave
+  // the queue — those placed become bound pods of the snapshot, the JSON documents
+  // of the others are released — and the rest are re-indexed from 0 (their
+  // results kept); one re-encode.
+  bool compact(uint32_t keep_from) {
+    if (shards != 1) { err = "compaction needs an unsharded context"; return false; }
+    if (keep_from > queue.size()) { err = "compact: queue range"; return false; }
+    if (!compile_queue()) return false;
+    track_queue();
+    const size_t nq = queue.size(), ns = progs.size();
+    vector<ksg_pod_summary> sum(nq);
+    if (ns && !eng->summaries(0, (uint32_t)ns, sum.data(), err)) return false;
+    for (uint32_t q = 0; q < keep_from; ++q) {
+      const int32_t at = placement(q, q < ns ? &sum[q] : nullptr);
+      if (at >= 0 && at < (int32_t)nodes.size()) {
+        Pod x = queue[q];
+        x.node = nodes[at].name;
+        bound.push_back(std::move(x));
+      } else if (queue[q].doc >= 0 && (size_t)queue[q].doc < docs.size()) {
+        docs[queue[q].doc].reset();  // its own document: nothing else points into it
+      }
+    }
+    auto cut = [&](auto& v) {
+      if (v.size() > keep_from) v.erase(v.begin(), v.begin() + keep_from);
+      else v.clear();
+    };
+    cut(queue);
+    cut(qmode);
+    cut(placed);
+    cut(assumed_in);
+    cut(nom);
+    cut(qneed);
+    cut(sum);
+    if (ns > keep_from) sum.resize(ns - keep_from);
+    else sum.clear();
+    bound_at_valid = false;
+    index_queue();
+    keep_first = keep_n = 0;
+    if (!eng->keep_outputs(0, 0, err)) return false;
+    oc_q = -1;
+    compiled = false;
+    return rebuild(nullptr, &sum);
+  }
+
   // One scheduling cycle of a new pod (appended to the queue).
   bool cycle(const char* js, size_t len, bool commit, ksg_pod_summary& out) {
     if (shards != 1) { err = "the cycle API needs an unsharded context"; return false; }
@@ -2810,6 +2857,7 @@ struct Cluster {
     }
     const J& d = *docs.back();
     queue.push_back(parse_pod(d["pod"] ? *d["pod"] : d));
+    queue.back().doc = (int32_t)docs.size() - 1;
     if (!volumes_modelled(queue.back())) {
       queue.pop_back();
       return false;
@@ -3893,6 +3941,13 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
     if (!c.eng->run_queue(j, first + count - j, true, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
     c.mark_run(j, first + count - j);
   }
+  return KSG_OK;
+}
+
+int ksg_compact(ksg_ctx* ctx, uint32_t keep_from) {
+  KSG_GUARD(ctx);
+  ctx->c.out_gen++;
+  if (!ctx->c.compact(keep_from)) return ctx->fail(ctx->c.err, KSG_E_STATE);
   return KSG_OK;
 }
 

@@ -80,6 +80,7 @@ def load_library():
     L.ksg_plugin_position.argtypes = [vp, cp, sz]
     L.ksg_node_index.argtypes = [vp, cp, sz]
     L.ksg_plugin_weights.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    L.ksg_compact.argtypes = [vp, u32]
     L.ksg_prefilter_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_prefilter_result.argtypes = [vp, u32, cp, sz, ctypes.POINTER(sz)]
     L.ksg_prefilter_result_pos.argtypes = [vp, u32, u32, cp, sz, ctypes.POINTER(sz)]
@@ -244,6 +245,10 @@ class Scheduler:
         b = name.encode()
         r = self.L.ksg_plugin_position(self.h, b, len(b))
         return None if r < 0 else r
+
+    def compact(self, keep_from=None):
+        """Drop queue pods [0, keep_from) (placed ones become bound pods); the rest are re-indexed from 0."""
+        self._chk(self.L.ksg_compact(self.h, self.queue_len if keep_from is None else keep_from), "ksg_compact")
 
     def plugin_weights(self, pos):
         """(framework weight, store weight) the profile resolved for position pos."""

@@ -82,6 +82,8 @@ static int run_one(const std::string& text) {
       ksg_reserve(c, q, r.selected >= 0 ? r.selected : 0);
       ksg_unreserve(c, q);
       ksg_cycle(c, sec[2].data(), sec[2].size(), 1, &r);
+      ksg_compact(c, (uint32_t)ksg_queue_len(c) / 2);
+      ksg_compact(c, 1u << 30);
     }
     if (!sec[3].empty()) ksg_apply_events(c, sec[3].data(), sec[3].size());
     exercise(c);

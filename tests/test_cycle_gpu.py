@@ -143,3 +143,42 @@ def test_cycle_table_grows_in_place():
     for i, pod in enumerate(doc["queue"]):
         q, r = s.cycle(pod, commit=True)
         assert (r.selected, r.feasible, r.status) == o.result(i), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("keep", [0, 2], ids=["keep0", "keep2"])
+def test_compact_bounds_the_queue(name, c, sizes, keep):
+    """ksg_compact (plugin mode's memory bound): after K cycles, all but the last
+    `keep` pods leave the queue (placed ones become bound pods); the kept pods keep
+    their results, and later cycles equal the oracle on the equivalent cluster
+    (every placement bound, the kept pods' queue slots held by pods that fit nowhere)."""
+    from test_events_gpu import _nowhere
+    doc = g.generate(c, **sizes)
+    pods = doc["queue"]
+    k = len(pods) // 2
+    s = Scheduler(doc["profile"])
+    s.load_cluster(_empty_queue(doc))
+    names = [n["metadata"]["name"] for n in doc["nodes"]]
+    first = [s.cycle(p, commit=True)[1] for p in pods[:k]]
+    s.compact(k - keep)
+    assert s.queue_len == keep
+    assert [(r.selected, r.feasible, r.status) for r in s.results()] == \
+        [(r.selected, r.feasible, r.status) for r in first[k - keep:]]
+    eq = copy.deepcopy(doc)
+    for p, r in zip(pods[:k], first):
+        if r.status == 0:
+            b = copy.deepcopy(p)
+            b["spec"]["nodeName"] = names[r.selected]
+            eq["pods"].append(b)
+    eq["queue"] = [_nowhere(i) for i in range(keep)] + pods[k:]
+    o = Oracle(eq)
+    o.schedule(record=3)
+    for j, p in enumerate(pods[k:]):
+        q, r = s.cycle(p, commit=True)
+        assert q == keep + j
+        assert (r.selected, r.feasible, r.status) == o.result(keep + j), (name, j)
+        if j % 5 == 0:
+            assert s.annotations(q) == o.annotations(keep + j), (name, j)
+    s.compact()
+    assert s.queue_len == 0

@@ -2652,9 +2652,17 @@ struct Cluster {
   // (namespace, name) -> queue index, for the events' name lookups
   std::unordered_map<string, uint32_t> queue_idx;
   static string pod_key(const string& ns, const string& name) { return ns + '\x1f' + name; }
+  bool queue_dups = false;  // some (namespace, name) is queued twice
   void index_queue() {
     queue_idx.clear();
-    for (size_t q = 0; q < queue.size(); ++q) queue_idx[pod_key(queue[q].ns, queue[q].name)] = (uint32_t)q;
+    queue_dups = false;
+    for (size_t q = 0; q < queue.size(); ++q) {
+      auto r = queue_idx.emplace(pod_key(queue[q].ns, queue[q].name), (uint32_t)q);
+      if (!r.second) {
+        queue_dups = true;
+        r.first->second = (uint32_t)q;
+      }
+    }
   }
   int32_t queue_find(const string& ns, const string& name) const {
     auto it = queue_idx.find(pod_key(ns, name));
@@ -2868,7 +2876,13 @@ struct Cluster {
     }
     track_queue();
     uint32_t q = (uint32_t)queue.size() - 1;
-    queue_idx[pod_key(queue[q].ns, queue[q].name)] = q;
+    {
+      auto r = queue_idx.emplace(pod_key(queue[q].ns, queue[q].name), q);
+      if (!r.second) {
+        queue_dups = true;
+        r.first->second = q;
+      }
+    }
     qmode[q] = 2;
     bool in_place = !vocab_grows(queue[q]);
     if (!in_place && vocab_grows_in_place(queue[q])) {  // new label values / keys / namespaces only
@@ -3379,6 +3393,10 @@ struct Cluster {
       return qm[q] == 2 ? at : remap[at];  // summaries hold original indices until the rebuild
     };
     auto queue_at = [&](const string& name, const string& pns) -> int32_t {
+      if (!queue_dups) {  // (namespace, name) index; with a name queued twice, the first placed one
+        const int32_t k = queue_find(pns, name);
+        return k >= 0 && qplace((size_t)k) >= 0 ? k : -1;
+      }
       for (size_t q = 0; q < queue.size(); ++q)
         if (queue[q].name == name && queue[q].ns == pns && qplace(q) >= 0) return (int32_t)q;
       return -1;

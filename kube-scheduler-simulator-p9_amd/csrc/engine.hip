@@ -1638,7 +1638,13 @@ struct WiArgs {
   uint32_t keep_first, keep_n;
   uint32_t* kfilter;
   int32_t *kscore, *ktotal;
+  // per-pair record of pass 1 for pass 2 (null: pass 2 recomputes): bit 63 feasible,
+  // 62 Fit/BA score out of range, [32,62) Fit/BA weighted sum, [20,32) raw Taint,
+  // [0,20) raw NodeAffinity; row (q - q0) * N + n
+  uint64_t* rec;
 };
+#define KSG_WREC_FEAS (1ull << 63)
+#define KSG_WREC_RANGE (1ull << 62)
 
 // (programs as restrict parameters: their reads stay scalar loads beside the
 // kernel's summary atomics and kept-output stores)
@@ -1667,6 +1673,7 @@ __global__ __launch_bounds__(256) void k_whatif(DevCluster C, DevProfile F, WiAr
       mx[p] = INT64_MIN;
       mn[p] = INT64_MAX;
     }
+    if (PASS == 2 && A.rec && !kept) continue;  // k_whatif_rec2
 #pragma unroll 1
     for (int k = 0; k < KSG_WI_NPT; ++k) {
       const uint32_t n = base + k * 256;
@@ -1747,6 +1754,162 @@ __global__ __launch_bounds__(256) void k_whatif(DevCluster C, DevProfile F, WiAr
       if (lane0() && b) atomicMax((unsigned long long*)&sm->best_key, (unsigned long long)b);
       if (feas_all > 1 && __any(range_err) && lane0()) atomicOr((uint32_t*)&sm->status, 2u);
     }
+  }
+}
+
+// Record path of a what-if step (run_whatif): pass 1 in the small tiles of
+// k_static (KSG_WI_PODS pods x 256 nodes per block, so a pod's node data stays in
+// L1 for the next), every score of every feasible pair computed once, the
+// step's per-pod feasible count and Taint / NodeAffinity max/min reduced per block
+// (one atomic per block and pod); pass 2 streams the records.
+__global__ __launch_bounds__(256) void k_whatif_rec1(DevCluster C, DevProfile F, WiArgs A,
+                                                     const uint8_t* __restrict__ progs,
+                                                     const uint64_t* __restrict__ prog_off) {
+  __shared__ int64_t red[2][4][5];
+  const uint32_t n = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pt = F.pos_taint, pa = F.pos_na;
+#pragma unroll 1
+  for (uint32_t pi = 0; pi < KSG_WI_PODS; ++pi) {
+    const uint32_t j = blockIdx.y * KSG_WI_PODS + pi;
+    if (j >= A.count) break;
+    const ProgView V = view(progs + prog_off[A.q0 + j]);
+    const ksg_prog* h = V.h;
+    int cnt = 0;
+    int64_t tx = INT64_MIN, tn = INT64_MAX, ax = INT64_MIN, an = INT64_MAX;
+    if (n < C.N) {
+      uint64_t rw = 0;
+      if (!(h->flags & KPF_PREFILTER_REJECT) &&
+          !((h->flags & KPF_RESTRICT) && !bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n))) {
+        bool pass = true;
+#pragma unroll 1
+        for (int pos = 0; pos < F.n && pass; ++pos) {
+          switch (F.plugins[pos]) {
+            case KP_FIT: pass = fit_filter(C, V, n) == 0; break;
+            case KP_TAINT: pass = untolerated_taint(C, V, n) < 0; break;
+            case KP_NA: pass = (h->flags & KPF_SKIP_NA_FILTER) || required_na(C, V, n); break;
+            default: break;
+          }
+        }
+        if (pass) {
+          cnt = 1;
+          rw = KSG_WREC_FEAS;
+          int64_t tot = 0;
+#pragma unroll 1
+          for (int pos = 0; pos < F.n; ++pos) {
+            int64_t s;
+            switch (F.plugins[pos]) {
+              case KP_FIT:
+              case KP_BA:
+                s = F.plugins[pos] == KP_FIT ? fit_score(C, F, V, n) : ba_score(C, F, V, n);
+                if (s < 0 || s > 100) rw |= KSG_WREC_RANGE;
+                else tot += s * F.weight[pos];
+                break;
+              case KP_TAINT:
+                s = taint_score(C, V, n);  // (< 2^12 and NodeAffinity < 2^20: static_fits)
+                tx = tn = s;
+                rw |= (uint64_t)s << 20;
+                break;
+              case KP_NA:
+                s = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n);
+                ax = an = s;
+                rw |= (uint64_t)s;
+                break;
+              default: break;
+            }
+          }
+          if (!(rw & KSG_WREC_RANGE)) rw |= (uint64_t)tot << 32;
+        }
+      }
+      __builtin_nontemporal_store(rw, A.rec + (size_t)j * C.N + n);
+    }
+    int64_t* r = red[pi & 1][w];
+    const int c = wave_sum(cnt);
+    tx = wave_max(tx); tn = wave_min(tn); ax = wave_max(ax); an = wave_min(an);
+    if (lane == 0) { r[0] = c; r[1] = tx; r[2] = tn; r[3] = ax; r[4] = an; }
+    __syncthreads();  // (red double-buffered: one barrier per pod)
+    if (threadIdx.x == 0) {
+      int64_t v[5] = {0, INT64_MIN, INT64_MAX, INT64_MIN, INT64_MAX};
+      for (int k = 0; k < 4; ++k) {
+        const int64_t* x = red[pi & 1][k];
+        v[0] += x[0];
+        v[1] = max(v[1], x[1]); v[2] = min(v[2], x[2]); v[3] = max(v[3], x[3]); v[4] = min(v[4], x[4]);
+      }
+      if (v[0]) {
+        ksg_pod_summary* sm = A.sums + A.q0 + j;
+        atomicAdd(&sm->feasible, (int32_t)v[0]);
+        if (pt >= 0) {
+          atomicMax((long long*)&sm->max_score[pt], (long long)v[1]);
+          atomicMin((long long*)&sm->min_score[pt], (long long)v[2]);
+        }
+        if (pa >= 0) {
+          atomicMax((long long*)&sm->max_score[pa], (long long)v[3]);
+          atomicMin((long long*)&sm->min_score[pa], (long long)v[4]);
+        }
+      }
+    }
+  }
+}
+
+// Pass 2 from the records: NormalizeScore, weights, packed key, per-pod argmax.
+// Each thread keeps the next pod's records in flight while it reduces this one's.
+__global__ __launch_bounds__(256) void k_whatif_rec2(DevCluster C, DevProfile F, WiArgs A,
+                                                     const uint8_t* __restrict__ progs,
+                                                     const uint64_t* __restrict__ prog_off) {
+  const uint32_t base = blockIdx.x * (256 * KSG_WI_NPT) + threadIdx.x;
+  const int pt = F.pos_taint, pa = F.pos_na;
+  const int64_t wt = pt >= 0 ? F.weight[pt] : 0, wa = pa >= 0 ? F.weight[pa] : 0;
+  const uint32_t j0 = blockIdx.y * KSG_WI_PODS, jn = min(A.count - j0, (uint32_t)KSG_WI_PODS);
+  uint64_t nx[KSG_WI_NPT];
+  auto fetch = [&](uint32_t j, uint64_t* r) {
+#pragma unroll
+    for (int k = 0; k < KSG_WI_NPT; ++k) {
+      const uint32_t n = base + k * 256;
+      r[k] = n < C.N ? __builtin_nontemporal_load(A.rec + (size_t)j * C.N + n) : 0;
+    }
+  };
+  fetch(j0, nx);
+#pragma unroll 1
+  for (uint32_t pi = 0; pi < jn; ++pi) {
+    const uint32_t j = j0 + pi, q = A.q0 + j;
+    uint64_t cur[KSG_WI_NPT];
+#pragma unroll
+    for (int k = 0; k < KSG_WI_NPT; ++k) cur[k] = nx[k];
+    if (pi + 1 < jn) fetch(j + 1, nx);
+    const bool kept = A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n;
+    if (kept) continue;  // k_whatif<2> (per-pair outputs)
+    const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[q]);
+    ksg_pod_summary* sm = A.sums + q;
+    const int32_t feas_all = sm->feasible;
+    const int64_t Mt = pt >= 0 ? sm->max_score[pt] : 0, Ma = pa >= 0 ? sm->max_score[pa] : 0;
+    const bool skip_na = (h->flags & KPF_SKIP_NA_SCORE) != 0;
+    bool range_err = false;
+    uint64_t best = 0;
+#pragma unroll
+    for (int k = 0; k < KSG_WI_NPT; ++k) {
+      const uint64_t r = cur[k];
+      if (!(r & KSG_WREC_FEAS)) continue;
+      range_err |= (r & KSG_WREC_RANGE) != 0;
+      int64_t tot = (int64_t)((r >> 32) & 0x3FFFFFFFull);
+      if (pt >= 0) {
+        int64_t s = (int64_t)((r >> 20) & 0xFFFull);
+        s = Mt == 0 ? 100 : 100 - 100 * s / Mt;  // DefaultNormalizeScore(reverse)
+        range_err |= s < 0 || s > 100;
+        tot += s * wt;
+      }
+      if (pa >= 0) {
+        int64_t s = skip_na ? 0 : (int64_t)(r & 0xFFFFFull);
+        s = skip_na ? 0 : (Ma == 0 ? s : 100 * s / Ma);
+        range_err |= s < 0 || s > 100;
+        tot += s * wa;
+      }
+      if (feas_all == 1) tot = 0;  // single feasible node: no scoring
+      const uint64_t key = pack_key(tot, F.seed, h->queue_idx, C.goff + base + k * 256);
+      best = key > best ? key : best;
+    }
+    const uint64_t b = wave_max(best);
+    if (lane0() && b) atomicMax((unsigned long long*)&sm->best_key, (unsigned long long)b);
+    if (feas_all > 1 && __any(range_err) && lane0()) atomicOr((uint32_t*)&sm->status, 2u);
   }
 }
 
@@ -3691,6 +3854,9 @@ struct Engine::Impl {
   DBuf<int32_t> prow;     // existing-pod table row of each assumed queue pod (-1 none)
   DBuf<uint32_t> arrive1; // block arrivals of the per-pod chain's last kernel
   bool static_ok = false; // per-pod cycles of Fit/BA/Taint/NA profiles: k_static + k_fs_static
+  DBuf<uint64_t> wrec_pairs;  // what-if: pass 1's per-pair records (run_whatif)
+  uint32_t wi_chunk = 0;      // ... pods per chunk of the last step, and whether records were used
+  bool wi_rec = false;
   bool static_fits = true; // raw scores fit the record (taints per node < 4096, NodeAffinity weights < 2^20)
   DBuf<StaticRec> stat;   // static records of a chunk of pods [chunk][N]
   DBuf<int64_t> mpred;    // [chunk][2] static max of the Taint / NodeAffinity raw scores
@@ -4435,26 +4601,66 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
   I.n_samples = 0;
   HIPCHK(hipEventRecord(I.ev0, s));
   if (count) {
-    const dim3 grid(std::max<uint32_t>((I.N + 256 * KSG_WI_NPT - 1) / (256 * KSG_WI_NPT), 1),
-                    (count + KSG_WI_PODS - 1) / KSG_WI_PODS);
-    const dim3 pods((count + 255) / 256);
-    const size_t xb = (size_t)count * sizeof(ksg_pod_summary);
-    hipLaunchKernelGGL(k_init_summaries, pods, dim3(256), 0, s, I.sums.p + first, count, I.F);
-    for (int pass = 1; pass <= 2; ++pass) {
-      const bool sampled = I.sample_every != 0;
-      if (sampled) HIPCHK(hipEventRecord(I.sev[2 * (pass - 1)], s));
-      if (pass == 1) hipLaunchKernelGGL(k_whatif<1>, grid, dim3(256), 0, s, C, I.F, A, A.progs, A.prog_off);
-      else hipLaunchKernelGGL(k_whatif<2>, grid, dim3(256), 0, s, C, I.F, A, A.progs, A.prog_off);
-      if (sampled) {
-        HIPCHK(hipEventRecord(I.sev[2 * (pass - 1) + 1], s));
-        I.n_samples++;
+    // Pass 1 leaves an 8-byte record per (pod, node) — feasibility, the Fit/BA
+    // weighted sum, the raw Taint / NodeAffinity scores — so that pass 2 only
+    // normalises and picks (the snapshot is frozen for the step).  Pods go in
+    // chunks whose records fit KSG_WHATIF_REC_MB (default 40 GiB of the 288 GB;
+    // 0: pass 2 recomputes every pair).
+    const uint32_t N = std::max<uint32_t>(I.N, 1);
+    size_t rec_mb = 40960;
+    if (const char* e = std::getenv("KSG_WHATIF_REC_MB")) rec_mb = (size_t)std::strtoull(e, nullptr, 10);
+    int64_t wsum = 0;
+    for (int i = 0; i < I.F.n; ++i)
+      if (I.F.plugins[i] == KP_FIT || I.F.plugins[i] == KP_BA) wsum += I.F.weight[i] > 0 ? I.F.weight[i] : 0;
+    const bool use_rec = rec_mb > 0 && I.static_fits && 100 * wsum < (int64_t)1 << 30;
+    uint32_t chunk = count;
+    if (use_rec) {
+      const size_t per_pod = (size_t)N * sizeof(uint64_t);
+      const size_t fit = (rec_mb << 20) / per_pod / KSG_WI_PODS * KSG_WI_PODS;
+      chunk = (uint32_t)std::min<size_t>(count, std::max<size_t>(fit, KSG_WI_PODS));
+      std::string aerr;  // no room: smaller chunks
+      while (!I.wrec_pairs.alloc((size_t)chunk * N, aerr) && chunk > KSG_WI_PODS) {
+        (void)hipGetLastError();  // (the failed hipMalloc's error is not the run's)
+        chunk = std::max<uint32_t>(chunk / 2 / KSG_WI_PODS * KSG_WI_PODS, KSG_WI_PODS);
       }
-      if (I.xranks > 1) {  // per-pod partials of every shard -> global values on every rank
-        if (!exchange(I, I.sums.p + first, xb, err)) return false;
-        hipLaunchKernelGGL(k_whatif_merge, pods, dim3(256), 0, s, reinterpret_cast<const ksg_pod_summary*>(I.xrecv.p),
-                           I.xranks, count, I.sums.p + first, pass);
+      if ((size_t)chunk * N > I.wrec_pairs.n) { err = aerr; return false; }
+    }
+    const dim3 pods((count + 255) / 256);
+    hipLaunchKernelGGL(k_init_summaries, pods, dim3(256), 0, s, I.sums.p + first, count, I.F);
+    for (uint32_t c0 = 0; c0 < count; c0 += chunk) {
+      WiArgs a = A;
+      a.q0 = first + c0;
+      a.count = std::min(chunk, count - c0);
+      a.rec = use_rec ? I.wrec_pairs.p : nullptr;
+      const dim3 grid(std::max<uint32_t>((I.N + 256 * KSG_WI_NPT - 1) / (256 * KSG_WI_NPT), 1),
+                      (a.count + KSG_WI_PODS - 1) / KSG_WI_PODS);
+      const dim3 grid1(std::max<uint32_t>((I.N + 255) / 256, 1), (a.count + KSG_WI_PODS - 1) / KSG_WI_PODS);
+      const dim3 cpods((a.count + 255) / 256);
+      const size_t xb = (size_t)a.count * sizeof(ksg_pod_summary);
+      for (int pass = 1; pass <= 2; ++pass) {
+        const bool sampled = I.sample_every != 0 && c0 == 0;
+        if (sampled) HIPCHK(hipEventRecord(I.sev[2 * (pass - 1)], s));
+        const bool kept_here = I.keep_n && I.keep_first < a.q0 + a.count && I.keep_first + I.keep_n > a.q0;
+        if (pass == 1 && use_rec) hipLaunchKernelGGL(k_whatif_rec1, grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+        else if (pass == 1) hipLaunchKernelGGL(k_whatif<1>, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+        else if (use_rec) {
+          hipLaunchKernelGGL(k_whatif_rec2, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          if (kept_here) hipLaunchKernelGGL(k_whatif<2>, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+        } else hipLaunchKernelGGL(k_whatif<2>, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+        if (sampled) {
+          HIPCHK(hipEventRecord(I.sev[2 * (pass - 1) + 1], s));
+          I.n_samples++;
+        }
+        if (I.xranks > 1) {  // per-pod partials of every shard -> global values on every rank
+          if (!exchange(I, I.sums.p + a.q0, xb, err)) return false;
+          hipLaunchKernelGGL(k_whatif_merge, cpods, dim3(256), 0, s,
+                             reinterpret_cast<const ksg_pod_summary*>(I.xrecv.p), I.xranks, a.count, I.sums.p + a.q0,
+                             pass);
+        }
       }
     }
+    I.wi_chunk = chunk;
+    I.wi_rec = use_rec;
     hipLaunchKernelGGL(k_whatif_select, pods, dim3(256), 0, s, A);
     hipLaunchKernelGGL(k_whatif_bind, pods, dim3(256), 0, s, C, A);
   }

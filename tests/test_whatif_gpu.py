@@ -118,3 +118,26 @@ def test_folded_partials_match_oracle(monkeypatch):
     for k in range(2):
         t.whatif(k * STEP, STEP)
     assert [(r.selected, r.feasible, r.status) for r in t.results()] == [w.result(q) for q in range(w.n_queue)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rec_mb", ["0", "1"], ids=["recompute", "chunked-records"])
+def test_whatif_pass_records(monkeypatch, rec_mb):
+    """Pass 2 normally reads pass 1's per-pair records; forced here to recompute
+    every pair (0) and to split the step into record chunks (1 MiB: 64 + 32 pods at
+    1,500 nodes), single context and 2-rank sharded."""
+    monkeypatch.setenv("KSG_WHATIF_REC_MB", rec_mb)
+    doc = g.generate(5, n_nodes=1500, n_pods=2 * STEP)
+    o = _oracle_steps(doc, 2)
+    want = [o.result(q) for q in range(o.n_queue)]
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    for k in range(2):
+        s.whatif(k * STEP, STEP)
+    assert [(r.selected, r.feasible, r.status) for r in s.results()] == want
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_sharded_worker, args=(2, port, json.dumps(doc), out), nprocs=2, join=True)
+        for r in range(2):
+            assert out[r] == want, f"rank {r} differs"

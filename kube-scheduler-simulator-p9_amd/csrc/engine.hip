@@ -1762,13 +1762,15 @@ __global__ __launch_bounds__(256) void k_whatif(DevCluster C, DevProfile F, WiAr
 // L1 for the next), every score of every feasible pair computed once, the
 // step's per-pod feasible count and Taint / NodeAffinity max/min reduced per block
 // (one atomic per block and pod); pass 2 streams the records.
-__global__ __launch_bounds__(256) void k_whatif_rec1(DevCluster C, DevProfile F, WiArgs A,
+template <int WAVES>  // occupancy target (VGPR cap): 6 spills nothing; 8 spills a little
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_whatif_rec1(DevCluster C, DevProfile F, WiArgs A,
                                                      const uint8_t* __restrict__ progs,
                                                      const uint64_t* __restrict__ prog_off) {
   __shared__ int64_t red[2][4][5];
   const uint32_t n = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int pt = F.pos_taint, pa = F.pos_na;
+  const bool hf = F.pos_fit >= 0, hb = F.pos_ba >= 0, ht = pt >= 0, ha = pa >= 0;
 #pragma unroll 1
   for (uint32_t pi = 0; pi < KSG_WI_PODS; ++pi) {
     const uint32_t j = blockIdx.y * KSG_WI_PODS + pi;
@@ -1781,42 +1783,33 @@ __global__ __launch_bounds__(256) void k_whatif_rec1(DevCluster C, DevProfile F,
       uint64_t rw = 0;
       if (!(h->flags & KPF_PREFILTER_REJECT) &&
           !((h->flags & KPF_RESTRICT) && !bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n))) {
-        bool pass = true;
-#pragma unroll 1
-        for (int pos = 0; pos < F.n && pass; ++pos) {
-          switch (F.plugins[pos]) {
-            case KP_FIT: pass = fit_filter(C, V, n) == 0; break;
-            case KP_TAINT: pass = untolerated_taint(C, V, n) < 0; break;
-            case KP_NA: pass = (h->flags & KPF_SKIP_NA_FILTER) || required_na(C, V, n); break;
-            default: break;
-          }
-        }
+        // (only pass / fail matters here, and integer sums commute: the profile's
+        // four plugins in a fixed order, no per-pair dispatch on the profile)
+        const bool pass = (!hf || fit_filter(C, V, n) == 0) && (!ht || untolerated_taint(C, V, n) < 0) &&
+                          (!ha || (h->flags & KPF_SKIP_NA_FILTER) || required_na(C, V, n));
         if (pass) {
           cnt = 1;
           rw = KSG_WREC_FEAS;
           int64_t tot = 0;
-#pragma unroll 1
-          for (int pos = 0; pos < F.n; ++pos) {
-            int64_t s;
-            switch (F.plugins[pos]) {
-              case KP_FIT:
-              case KP_BA:
-                s = F.plugins[pos] == KP_FIT ? fit_score(C, F, V, n) : ba_score(C, F, V, n);
-                if (s < 0 || s > 100) rw |= KSG_WREC_RANGE;
-                else tot += s * F.weight[pos];
-                break;
-              case KP_TAINT:
-                s = taint_score(C, V, n);  // (< 2^12 and NodeAffinity < 2^20: static_fits)
-                tx = tn = s;
-                rw |= (uint64_t)s << 20;
-                break;
-              case KP_NA:
-                s = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n);
-                ax = an = s;
-                rw |= (uint64_t)s;
-                break;
-              default: break;
-            }
+          if (hf) {
+            const int64_t s = fit_score(C, F, V, n);
+            if (s < 0 || s > 100) rw |= KSG_WREC_RANGE;
+            else tot += s * F.w_fit;
+          }
+          if (hb) {
+            const int64_t s = ba_score(C, F, V, n);
+            if (s < 0 || s > 100) rw |= KSG_WREC_RANGE;
+            else tot += s * F.w_ba;
+          }
+          if (ht) {
+            const int64_t s = taint_score(C, V, n);  // (< 2^12 and NodeAffinity < 2^20: static_fits)
+            tx = tn = s;
+            rw |= (uint64_t)s << 20;
+          }
+          if (ha) {
+            const int64_t s = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n);
+            ax = an = s;
+            rw |= (uint64_t)s;
           }
           if (!(rw & KSG_WREC_RANGE)) rw |= (uint64_t)tot << 32;
         }
@@ -4612,6 +4605,8 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
     int64_t wsum = 0;
     for (int i = 0; i < I.F.n; ++i)
       if (I.F.plugins[i] == KP_FIT || I.F.plugins[i] == KP_BA) wsum += I.F.weight[i] > 0 ? I.F.weight[i] : 0;
+    int rec1_waves = 6;
+    if (const char* e = std::getenv("KSG_WI_REC1_WAVES")) rec1_waves = (int)std::strtol(e, nullptr, 10);
     const bool use_rec = rec_mb > 0 && I.static_fits && 100 * wsum < (int64_t)1 << 30;
     uint32_t chunk = count;
     if (use_rec) {
@@ -4641,7 +4636,10 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
         const bool sampled = I.sample_every != 0 && c0 == 0;
         if (sampled) HIPCHK(hipEventRecord(I.sev[2 * (pass - 1)], s));
         const bool kept_here = I.keep_n && I.keep_first < a.q0 + a.count && I.keep_first + I.keep_n > a.q0;
-        if (pass == 1 && use_rec) hipLaunchKernelGGL(k_whatif_rec1, grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+        if (pass == 1 && use_rec) {
+          if (rec1_waves == 8) hipLaunchKernelGGL(k_whatif_rec1<8>, grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          else hipLaunchKernelGGL(k_whatif_rec1<6>, grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+        }
         else if (pass == 1) hipLaunchKernelGGL(k_whatif<1>, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
         else if (use_rec) {
           hipLaunchKernelGGL(k_whatif_rec2, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);

@@ -1642,6 +1642,7 @@ struct WiArgs {
   // 62 Fit/BA score out of range, [32,62) Fit/BA weighted sum, [20,32) raw Taint,
   // [0,20) raw NodeAffinity; row (q - q0) * N + n
   uint64_t* rec;
+  uint32_t need_eph;  // resource columns 2..3 requested by some pod (RowV loads)
 };
 #define KSG_WREC_FEAS (1ull << 63)
 #define KSG_WREC_RANGE (1ull << 62)
@@ -1754,155 +1755,6 @@ __global__ __launch_bounds__(256) void k_whatif(DevCluster C, DevProfile F, WiAr
       if (lane0() && b) atomicMax((unsigned long long*)&sm->best_key, (unsigned long long)b);
       if (feas_all > 1 && __any(range_err) && lane0()) atomicOr((uint32_t*)&sm->status, 2u);
     }
-  }
-}
-
-// Record path of a what-if step (run_whatif): pass 1 in the small tiles of
-// k_static (KSG_WI_PODS pods x 256 nodes per block, so a pod's node data stays in
-// L1 for the next), every score of every feasible pair computed once, the
-// step's per-pod feasible count and Taint / NodeAffinity max/min reduced per block
-// (one atomic per block and pod); pass 2 streams the records.
-template <int WAVES>  // occupancy target (VGPR cap): 6 spills nothing; 8 spills a little
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_whatif_rec1(DevCluster C, DevProfile F, WiArgs A,
-                                                     const uint8_t* __restrict__ progs,
-                                                     const uint64_t* __restrict__ prog_off) {
-  __shared__ int64_t red[2][4][5];
-  const uint32_t n = blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int pt = F.pos_taint, pa = F.pos_na;
-  const bool hf = F.pos_fit >= 0, hb = F.pos_ba >= 0, ht = pt >= 0, ha = pa >= 0;
-#pragma unroll 1
-  for (uint32_t pi = 0; pi < KSG_WI_PODS; ++pi) {
-    const uint32_t j = blockIdx.y * KSG_WI_PODS + pi;
-    if (j >= A.count) break;
-    const ProgView V = view(progs + prog_off[A.q0 + j]);
-    const ksg_prog* h = V.h;
-    int cnt = 0;
-    int64_t tx = INT64_MIN, tn = INT64_MAX, ax = INT64_MIN, an = INT64_MAX;
-    if (n < C.N) {
-      uint64_t rw = 0;
-      if (!(h->flags & KPF_PREFILTER_REJECT) &&
-          !((h->flags & KPF_RESTRICT) && !bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n))) {
-        // (only pass / fail matters here, and integer sums commute: the profile's
-        // four plugins in a fixed order, no per-pair dispatch on the profile)
-        const bool pass = (!hf || fit_filter(C, V, n) == 0) && (!ht || untolerated_taint(C, V, n) < 0) &&
-                          (!ha || (h->flags & KPF_SKIP_NA_FILTER) || required_na(C, V, n));
-        if (pass) {
-          cnt = 1;
-          rw = KSG_WREC_FEAS;
-          int64_t tot = 0;
-          if (hf) {
-            const int64_t s = fit_score(C, F, V, n);
-            if (s < 0 || s > 100) rw |= KSG_WREC_RANGE;
-            else tot += s * F.w_fit;
-          }
-          if (hb) {
-            const int64_t s = ba_score(C, F, V, n);
-            if (s < 0 || s > 100) rw |= KSG_WREC_RANGE;
-            else tot += s * F.w_ba;
-          }
-          if (ht) {
-            const int64_t s = taint_score(C, V, n);  // (< 2^12 and NodeAffinity < 2^20: static_fits)
-            tx = tn = s;
-            rw |= (uint64_t)s << 20;
-          }
-          if (ha) {
-            const int64_t s = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n);
-            ax = an = s;
-            rw |= (uint64_t)s;
-          }
-          if (!(rw & KSG_WREC_RANGE)) rw |= (uint64_t)tot << 32;
-        }
-      }
-      __builtin_nontemporal_store(rw, A.rec + (size_t)j * C.N + n);
-    }
-    int64_t* r = red[pi & 1][w];
-    const int c = wave_sum(cnt);
-    tx = wave_max(tx); tn = wave_min(tn); ax = wave_max(ax); an = wave_min(an);
-    if (lane == 0) { r[0] = c; r[1] = tx; r[2] = tn; r[3] = ax; r[4] = an; }
-    __syncthreads();  // (red double-buffered: one barrier per pod)
-    if (threadIdx.x == 0) {
-      int64_t v[5] = {0, INT64_MIN, INT64_MAX, INT64_MIN, INT64_MAX};
-      for (int k = 0; k < 4; ++k) {
-        const int64_t* x = red[pi & 1][k];
-        v[0] += x[0];
-        v[1] = max(v[1], x[1]); v[2] = min(v[2], x[2]); v[3] = max(v[3], x[3]); v[4] = min(v[4], x[4]);
-      }
-      if (v[0]) {
-        ksg_pod_summary* sm = A.sums + A.q0 + j;
-        atomicAdd(&sm->feasible, (int32_t)v[0]);
-        if (pt >= 0) {
-          atomicMax((long long*)&sm->max_score[pt], (long long)v[1]);
-          atomicMin((long long*)&sm->min_score[pt], (long long)v[2]);
-        }
-        if (pa >= 0) {
-          atomicMax((long long*)&sm->max_score[pa], (long long)v[3]);
-          atomicMin((long long*)&sm->min_score[pa], (long long)v[4]);
-        }
-      }
-    }
-  }
-}
-
-// Pass 2 from the records: NormalizeScore, weights, packed key, per-pod argmax.
-// Each thread keeps the next pod's records in flight while it reduces this one's.
-__global__ __launch_bounds__(256) void k_whatif_rec2(DevCluster C, DevProfile F, WiArgs A,
-                                                     const uint8_t* __restrict__ progs,
-                                                     const uint64_t* __restrict__ prog_off) {
-  const uint32_t base = blockIdx.x * (256 * KSG_WI_NPT) + threadIdx.x;
-  const int pt = F.pos_taint, pa = F.pos_na;
-  const int64_t wt = pt >= 0 ? F.weight[pt] : 0, wa = pa >= 0 ? F.weight[pa] : 0;
-  const uint32_t j0 = blockIdx.y * KSG_WI_PODS, jn = min(A.count - j0, (uint32_t)KSG_WI_PODS);
-  uint64_t nx[KSG_WI_NPT];
-  auto fetch = [&](uint32_t j, uint64_t* r) {
-#pragma unroll
-    for (int k = 0; k < KSG_WI_NPT; ++k) {
-      const uint32_t n = base + k * 256;
-      r[k] = n < C.N ? __builtin_nontemporal_load(A.rec + (size_t)j * C.N + n) : 0;
-    }
-  };
-  fetch(j0, nx);
-#pragma unroll 1
-  for (uint32_t pi = 0; pi < jn; ++pi) {
-    const uint32_t j = j0 + pi, q = A.q0 + j;
-    uint64_t cur[KSG_WI_NPT];
-#pragma unroll
-    for (int k = 0; k < KSG_WI_NPT; ++k) cur[k] = nx[k];
-    if (pi + 1 < jn) fetch(j + 1, nx);
-    const bool kept = A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n;
-    if (kept) continue;  // k_whatif<2> (per-pair outputs)
-    const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[q]);
-    ksg_pod_summary* sm = A.sums + q;
-    const int32_t feas_all = sm->feasible;
-    const int64_t Mt = pt >= 0 ? sm->max_score[pt] : 0, Ma = pa >= 0 ? sm->max_score[pa] : 0;
-    const bool skip_na = (h->flags & KPF_SKIP_NA_SCORE) != 0;
-    bool range_err = false;
-    uint64_t best = 0;
-#pragma unroll
-    for (int k = 0; k < KSG_WI_NPT; ++k) {
-      const uint64_t r = cur[k];
-      if (!(r & KSG_WREC_FEAS)) continue;
-      range_err |= (r & KSG_WREC_RANGE) != 0;
-      int64_t tot = (int64_t)((r >> 32) & 0x3FFFFFFFull);
-      if (pt >= 0) {
-        int64_t s = (int64_t)((r >> 20) & 0xFFFull);
-        s = Mt == 0 ? 100 : 100 - 100 * s / Mt;  // DefaultNormalizeScore(reverse)
-        range_err |= s < 0 || s > 100;
-        tot += s * wt;
-      }
-      if (pa >= 0) {
-        int64_t s = skip_na ? 0 : (int64_t)(r & 0xFFFFFull);
-        s = skip_na ? 0 : (Ma == 0 ? s : 100 * s / Ma);
-        range_err |= s < 0 || s > 100;
-        tot += s * wa;
-      }
-      if (feas_all == 1) tot = 0;  // single feasible node: no scoring
-      const uint64_t key = pack_key(tot, F.seed, h->queue_idx, C.goff + base + k * 256);
-      best = key > best ? key : best;
-    }
-    const uint64_t b = wave_max(best);
-    if (lane0() && b) atomicMax((unsigned long long*)&sm->best_key, (unsigned long long)b);
-    if (feas_all > 1 && __any(range_err) && lane0()) atomicOr((uint32_t*)&sm->status, 2u);
   }
 }
 
@@ -2651,6 +2503,182 @@ __device__ __forceinline__ void store_row(const DevCluster& C, uint32_t n, const
   C.nzm[n] = r.nzm;
   C.podcnt[n] = r.podcnt;
 }
+
+// Record path of a what-if step (run_whatif): pass 1 in the small tiles of
+// k_static (KSG_WI_PODS pods x 256 nodes per block), every score of every
+// feasible pair computed once, the step's per-pod feasible count and Taint /
+// NodeAffinity max/min reduced per block (one atomic per block and pod); pass 2
+// streams the records.  The thread's node row and its first four taints are
+// loaded once for the block's pods (RowV evaluation of the window path; the
+// record path needs <= 4 resource columns); the taint list is walked once per
+// pair for both TaintToleration's Filter and its Score.
+template <int WAVES, int MODE>  // occupancy target (VGPR cap); MODE: eval_row specialisation
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_whatif_rec1(
+    DevCluster C, DevProfile F, WiArgs A, const uint8_t* __restrict__ progs, const uint64_t* __restrict__ prog_off) {
+  __shared__ int64_t red[2][4][5];
+  const uint32_t n = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pt = F.pos_taint, pa = F.pos_na;
+  const bool hf = F.pos_fit >= 0, hb = F.pos_ba >= 0, ht = pt >= 0, ha = pa >= 0;
+  const uint32_t R = C.R < 4 ? C.R : 4;
+  const bool live = n < C.N;
+  RowV row{};
+  uint32_t t0 = 0, tc = 0;
+  int32_t tr[4] = {-1, -1, -1, -1};
+  if (live) {
+    load_row(C, n, A.need_eph, row);
+    t0 = C.toff[n];
+    tc = C.toff[n + 1] - t0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if ((uint32_t)i < tc) tr[i] = C.tid[t0 + i];
+  }
+#pragma unroll 1
+  for (uint32_t pi = 0; pi < KSG_WI_PODS; ++pi) {
+    const uint32_t j = blockIdx.y * KSG_WI_PODS + pi;
+    if (j >= A.count) break;
+    const ProgView V = view(progs + prog_off[A.q0 + j]);
+    const ksg_prog* h = V.h;
+    int cnt = 0;
+    int64_t tx = INT64_MIN, tn = INT64_MAX, ax = INT64_MIN, an = INT64_MAX;
+    if (live) {
+      uint64_t rw = 0;
+      if (!(h->flags & KPF_PREFILTER_REJECT) &&
+          !((h->flags & KPF_RESTRICT) && !bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n))) {
+        // (only pass / fail matters here, and integer sums commute: the profile's
+        // four plugins in a fixed order, no per-pair dispatch on the profile)
+        bool pass = !hf || fit_filter_row(row, h, R) == 0;
+        int64_t tpref = 0;
+        if (pass && ht) {
+          const uint32_t* hard = V.u32 + h->taint_hard_off;
+          const uint32_t* pref = V.u32 + h->taint_pref_off;
+          const int tw = h->taint_words;
+#pragma unroll 1
+          for (uint32_t i = 0; i < tc; ++i) {
+            const int32_t t = i == 0 ? tr[0] : i == 1 ? tr[1] : i == 2 ? tr[2] : i == 3 ? tr[3] : C.tid[t0 + i];
+            if (bit(hard, tw, t)) { pass = false; break; }
+            tpref += bit(pref, tw, t) ? 1 : 0;
+          }
+        }
+        pass = pass && (!ha || (h->flags & KPF_SKIP_NA_FILTER) || required_na(C, V, n));
+        if (pass) {
+          cnt = 1;
+          rw = KSG_WREC_FEAS;
+          int64_t tot = 0;
+          if (hf) {
+            const int64_t s = fit_score_row<MODE>(row, F, h);
+            if (s < 0 || s > 100) rw |= KSG_WREC_RANGE;
+            else tot += s * F.w_fit;
+          }
+          if (hb) {
+            const int64_t s = ba_score_row<MODE>(row, F, h);
+            if (s < 0 || s > 100) rw |= KSG_WREC_RANGE;
+            else tot += s * F.w_ba;
+          }
+          if (ht) {  // (< 2^12 and NodeAffinity < 2^20: static_fits)
+            tx = tn = tpref;
+            rw |= (uint64_t)tpref << 20;
+          }
+          if (ha) {
+            const int64_t s = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n);
+            ax = an = s;
+            rw |= (uint64_t)s;
+          }
+          if (!(rw & KSG_WREC_RANGE)) rw |= (uint64_t)tot << 32;
+        }
+      }
+      __builtin_nontemporal_store(rw, A.rec + (size_t)j * C.N + n);
+    }
+    int64_t* r = red[pi & 1][w];
+    const int c = wave_sum(cnt);
+    tx = wave_max(tx); tn = wave_min(tn); ax = wave_max(ax); an = wave_min(an);
+    if (lane == 0) { r[0] = c; r[1] = tx; r[2] = tn; r[3] = ax; r[4] = an; }
+    __syncthreads();  // (red double-buffered: one barrier per pod)
+    if (threadIdx.x == 0) {
+      int64_t v[5] = {0, INT64_MIN, INT64_MAX, INT64_MIN, INT64_MAX};
+      for (int k = 0; k < 4; ++k) {
+        const int64_t* x = red[pi & 1][k];
+        v[0] += x[0];
+        v[1] = max(v[1], x[1]); v[2] = min(v[2], x[2]); v[3] = max(v[3], x[3]); v[4] = min(v[4], x[4]);
+      }
+      if (v[0]) {
+        ksg_pod_summary* sm = A.sums + A.q0 + j;
+        atomicAdd(&sm->feasible, (int32_t)v[0]);
+        if (pt >= 0) {
+          atomicMax((long long*)&sm->max_score[pt], (long long)v[1]);
+          atomicMin((long long*)&sm->min_score[pt], (long long)v[2]);
+        }
+        if (pa >= 0) {
+          atomicMax((long long*)&sm->max_score[pa], (long long)v[3]);
+          atomicMin((long long*)&sm->min_score[pa], (long long)v[4]);
+        }
+      }
+    }
+  }
+}
+
+// Pass 2 from the records: NormalizeScore, weights, packed key, per-pod argmax.
+// Each thread keeps the next pod's records in flight while it reduces this one's.
+__global__ __launch_bounds__(256) void k_whatif_rec2(DevCluster C, DevProfile F, WiArgs A,
+                                                     const uint8_t* __restrict__ progs,
+                                                     const uint64_t* __restrict__ prog_off) {
+  const uint32_t base = blockIdx.x * (256 * KSG_WI_NPT) + threadIdx.x;
+  const int pt = F.pos_taint, pa = F.pos_na;
+  const int64_t wt = pt >= 0 ? F.weight[pt] : 0, wa = pa >= 0 ? F.weight[pa] : 0;
+  const uint32_t j0 = blockIdx.y * KSG_WI_PODS, jn = min(A.count - j0, (uint32_t)KSG_WI_PODS);
+  uint64_t nx[KSG_WI_NPT];
+  auto fetch = [&](uint32_t j, uint64_t* r) {
+#pragma unroll
+    for (int k = 0; k < KSG_WI_NPT; ++k) {
+      const uint32_t n = base + k * 256;
+      r[k] = n < C.N ? __builtin_nontemporal_load(A.rec + (size_t)j * C.N + n) : 0;
+    }
+  };
+  fetch(j0, nx);
+#pragma unroll 1
+  for (uint32_t pi = 0; pi < jn; ++pi) {
+    const uint32_t j = j0 + pi, q = A.q0 + j;
+    uint64_t cur[KSG_WI_NPT];
+#pragma unroll
+    for (int k = 0; k < KSG_WI_NPT; ++k) cur[k] = nx[k];
+    if (pi + 1 < jn) fetch(j + 1, nx);
+    const bool kept = A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n;
+    if (kept) continue;  // k_whatif<2> (per-pair outputs)
+    const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[q]);
+    ksg_pod_summary* sm = A.sums + q;
+    const int32_t feas_all = sm->feasible;
+    const int64_t Mt = pt >= 0 ? sm->max_score[pt] : 0, Ma = pa >= 0 ? sm->max_score[pa] : 0;
+    const bool skip_na = (h->flags & KPF_SKIP_NA_SCORE) != 0;
+    bool range_err = false;
+    uint64_t best = 0;
+#pragma unroll
+    for (int k = 0; k < KSG_WI_NPT; ++k) {
+      const uint64_t r = cur[k];
+      if (!(r & KSG_WREC_FEAS)) continue;
+      range_err |= (r & KSG_WREC_RANGE) != 0;
+      int64_t tot = (int64_t)((r >> 32) & 0x3FFFFFFFull);
+      if (pt >= 0) {
+        int64_t s = (int64_t)((r >> 20) & 0xFFFull);
+        s = Mt == 0 ? 100 : 100 - 100 * s / Mt;  // DefaultNormalizeScore(reverse)
+        range_err |= s < 0 || s > 100;
+        tot += s * wt;
+      }
+      if (pa >= 0) {
+        int64_t s = skip_na ? 0 : (int64_t)(r & 0xFFFFFull);
+        s = skip_na ? 0 : (Ma == 0 ? s : 100 * s / Ma);
+        range_err |= s < 0 || s > 100;
+        tot += s * wa;
+      }
+      if (feas_all == 1) tot = 0;  // single feasible node: no scoring
+      const uint64_t key = pack_key(tot, F.seed, h->queue_idx, C.goff + base + k * 256);
+      best = key > best ? key : best;
+    }
+    const uint64_t b = wave_max(best);
+    if (lane0() && b) atomicMax((unsigned long long*)&sm->best_key, (unsigned long long)b);
+    if (feas_all > 1 && __any(range_err) && lane0()) atomicOr((uint32_t*)&sm->status, 2u);
+  }
+}
+
 // Index of global node gid in P_{W-1} (lane e of pn holds entry e's node), or -1.
 __device__ __forceinline__ int pend_index(int32_t gid, int32_t pn, int np) {
   int hit = -1;
@@ -4607,7 +4635,8 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
       if (I.F.plugins[i] == KP_FIT || I.F.plugins[i] == KP_BA) wsum += I.F.weight[i] > 0 ? I.F.weight[i] : 0;
     int rec1_waves = 6;
     if (const char* e = std::getenv("KSG_WI_REC1_WAVES")) rec1_waves = (int)std::strtol(e, nullptr, 10);
-    const bool use_rec = rec_mb > 0 && I.static_fits && 100 * wsum < (int64_t)1 << 30;
+    A.need_eph = I.any_eph_req ? 1u : 0u;
+    const bool use_rec = rec_mb > 0 && I.R <= 4 && I.static_fits && 100 * wsum < (int64_t)1 << 30;
     uint32_t chunk = count;
     if (use_rec) {
       const size_t per_pod = (size_t)N * sizeof(uint64_t);
@@ -4637,8 +4666,13 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
         if (sampled) HIPCHK(hipEventRecord(I.sev[2 * (pass - 1)], s));
         const bool kept_here = I.keep_n && I.keep_first < a.q0 + a.count && I.keep_first + I.keep_n > a.q0;
         if (pass == 1 && use_rec) {
-          if (rec1_waves == 8) hipLaunchKernelGGL(k_whatif_rec1<8>, grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
-          else hipLaunchKernelGGL(k_whatif_rec1<6>, grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          if (I.eval_mode == 1) {
+            if (rec1_waves == 8) hipLaunchKernelGGL((k_whatif_rec1<8, 1>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+            else hipLaunchKernelGGL((k_whatif_rec1<6, 1>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          } else {
+            if (rec1_waves == 8) hipLaunchKernelGGL((k_whatif_rec1<8, 0>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+            else hipLaunchKernelGGL((k_whatif_rec1<6, 0>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          }
         }
         else if (pass == 1) hipLaunchKernelGGL(k_whatif<1>, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
         else if (use_rec) {

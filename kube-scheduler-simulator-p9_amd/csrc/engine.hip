@@ -1638,14 +1638,14 @@ struct WiArgs {
   uint32_t keep_first, keep_n;
   uint32_t* kfilter;
   int32_t *kscore, *ktotal;
-  // per-pair record of pass 1 for pass 2 (null: pass 2 recomputes): bit 63 feasible,
-  // 62 Fit/BA score out of range, [32,62) Fit/BA weighted sum, [20,32) raw Taint,
-  // [0,20) raw NodeAffinity; row (q - q0) * N + n
-  uint64_t* rec;
+  // per-pair record of pass 1 for pass 2 (null: pass 2 recomputes), 4 or 8 bytes:
+  // top bit feasible, next Fit/BA score out of range, then from bit 0 the raw
+  // NodeAffinity score (bw_a bits), the raw Taint score (bw_t), the Fit/BA weighted
+  // sum (bw_tot); row (q - q0) * N + n
+  void* rec;
+  uint32_t bw_a, bw_t, bw_tot;
   uint32_t need_eph;  // resource columns 2..3 requested by some pod (RowV loads)
 };
-#define KSG_WREC_FEAS (1ull << 63)
-#define KSG_WREC_RANGE (1ull << 62)
 
 // (programs as restrict parameters: their reads stay scalar loads beside the
 // kernel's summary atomics and kept-output stores)
@@ -2512,8 +2512,8 @@ __device__ __forceinline__ void store_row(const DevCluster& C, uint32_t n, const
 // loaded once for the block's pods (RowV evaluation of the window path; the
 // record path needs <= 4 resource columns); the taint list is walked once per
 // pair for both TaintToleration's Filter and its Score.
-template <int WAVES, int MODE>  // occupancy target (VGPR cap); MODE: eval_row specialisation
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) void k_whatif_rec1(
+template <class RT, int MODE>  // record word; MODE: eval_row specialisation
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_whatif_rec1(
     DevCluster C, DevProfile F, WiArgs A, const uint8_t* __restrict__ progs, const uint64_t* __restrict__ prog_off) {
   __shared__ int64_t red[2][4][5];
   const uint32_t n = blockIdx.x * 256 + threadIdx.x;
@@ -2522,6 +2522,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) vo
   const bool hf = F.pos_fit >= 0, hb = F.pos_ba >= 0, ht = pt >= 0, ha = pa >= 0;
   const uint32_t R = C.R < 4 ? C.R : 4;
   const bool live = n < C.N;
+  constexpr RT FEAS = (RT)1 << (8 * sizeof(RT) - 1), RANGE = FEAS >> 1;
+  const uint32_t sh_t = A.bw_a, sh_tot = A.bw_a + A.bw_t;
   RowV row{};
   uint32_t t0 = 0, tc = 0;
   int32_t tr[4] = {-1, -1, -1, -1};
@@ -2542,7 +2544,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) vo
     int cnt = 0;
     int64_t tx = INT64_MIN, tn = INT64_MAX, ax = INT64_MIN, an = INT64_MAX;
     if (live) {
-      uint64_t rw = 0;
+      RT rw = 0;
       if (!(h->flags & KPF_PREFILTER_REJECT) &&
           !((h->flags & KPF_RESTRICT) && !bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n))) {
         // (only pass / fail matters here, and integer sums commute: the profile's
@@ -2553,41 +2555,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) vo
           const uint32_t* hard = V.u32 + h->taint_hard_off;
           const uint32_t* pref = V.u32 + h->taint_pref_off;
           const int tw = h->taint_words;
+          // the pod's first 64 taint bits in scalar registers (one load each per pod)
+          const uint64_t hw = tw > 1 ? ((uint64_t)hard[1] << 32 | hard[0]) : tw > 0 ? hard[0] : 0;
+          const uint64_t pw = tw > 1 ? ((uint64_t)pref[1] << 32 | pref[0]) : tw > 0 ? pref[0] : 0;
 #pragma unroll 1
           for (uint32_t i = 0; i < tc; ++i) {
             const int32_t t = i == 0 ? tr[0] : i == 1 ? tr[1] : i == 2 ? tr[2] : i == 3 ? tr[3] : C.tid[t0 + i];
-            if (bit(hard, tw, t)) { pass = false; break; }
-            tpref += bit(pref, tw, t) ? 1 : 0;
+            const bool lo = (uint32_t)t < 64;
+            if (lo ? ((hw >> t) & 1) : bit(hard, tw, t)) { pass = false; break; }
+            tpref += (lo ? ((pw >> t) & 1) : bit(pref, tw, t)) ? 1 : 0;
           }
         }
         pass = pass && (!ha || (h->flags & KPF_SKIP_NA_FILTER) || required_na(C, V, n));
         if (pass) {
           cnt = 1;
-          rw = KSG_WREC_FEAS;
+          rw = FEAS;
           int64_t tot = 0;
           if (hf) {
             const int64_t s = fit_score_row<MODE>(row, F, h);
-            if (s < 0 || s > 100) rw |= KSG_WREC_RANGE;
+            if (s < 0 || s > 100) rw |= RANGE;
             else tot += s * F.w_fit;
           }
           if (hb) {
             const int64_t s = ba_score_row<MODE>(row, F, h);
-            if (s < 0 || s > 100) rw |= KSG_WREC_RANGE;
+            if (s < 0 || s > 100) rw |= RANGE;
             else tot += s * F.w_ba;
           }
-          if (ht) {  // (< 2^12 and NodeAffinity < 2^20: static_fits)
+          if (ht) {  // (field widths from the cluster's taint counts / the programs' weights)
             tx = tn = tpref;
-            rw |= (uint64_t)tpref << 20;
+            rw |= (RT)tpref << sh_t;
           }
           if (ha) {
             const int64_t s = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n);
             ax = an = s;
-            rw |= (uint64_t)s;
+            rw |= (RT)s;
           }
-          if (!(rw & KSG_WREC_RANGE)) rw |= (uint64_t)tot << 32;
+          if (!(rw & RANGE)) rw |= (RT)tot << sh_tot;
         }
       }
-      __builtin_nontemporal_store(rw, A.rec + (size_t)j * C.N + n);
+      __builtin_nontemporal_store(rw, static_cast<RT*>(A.rec) + (size_t)j * C.N + n);
     }
     int64_t* r = red[pi & 1][w];
     const int c = wave_sum(cnt);
@@ -2618,29 +2624,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) vo
 }
 
 // Pass 2 from the records: NormalizeScore, weights, packed key, per-pod argmax.
-// Each thread keeps the next pod's records in flight while it reduces this one's.
+// Each thread keeps the next pod's records in flight while it reduces this one's;
+// KSG_WI_R2NPT nodes per thread amortise the per-pod reduction and atomics.
+#define KSG_WI_R2NPT 16
+template <class RT>
 __global__ __launch_bounds__(256) void k_whatif_rec2(DevCluster C, DevProfile F, WiArgs A,
                                                      const uint8_t* __restrict__ progs,
                                                      const uint64_t* __restrict__ prog_off) {
-  const uint32_t base = blockIdx.x * (256 * KSG_WI_NPT) + threadIdx.x;
+  const uint32_t base = blockIdx.x * (256 * KSG_WI_R2NPT) + threadIdx.x;
   const int pt = F.pos_taint, pa = F.pos_na;
   const int64_t wt = pt >= 0 ? F.weight[pt] : 0, wa = pa >= 0 ? F.weight[pa] : 0;
   const uint32_t j0 = blockIdx.y * KSG_WI_PODS, jn = min(A.count - j0, (uint32_t)KSG_WI_PODS);
-  uint64_t nx[KSG_WI_NPT];
-  auto fetch = [&](uint32_t j, uint64_t* r) {
+  constexpr RT FEAS = (RT)1 << (8 * sizeof(RT) - 1), RANGE = FEAS >> 1;
+  const uint32_t sh_t = A.bw_a, sh_tot = A.bw_a + A.bw_t;
+  const RT ma_ = (RT)(((uint64_t)1 << A.bw_a) - 1), mt_ = (RT)(((uint64_t)1 << A.bw_t) - 1),
+           mtot = (RT)(((uint64_t)1 << A.bw_tot) - 1);
+  const RT* rec = static_cast<const RT*>(A.rec);
+  RT nx[KSG_WI_R2NPT];
+  auto fetch = [&](uint32_t j, RT* r) {
 #pragma unroll
-    for (int k = 0; k < KSG_WI_NPT; ++k) {
+    for (int k = 0; k < KSG_WI_R2NPT; ++k) {
       const uint32_t n = base + k * 256;
-      r[k] = n < C.N ? __builtin_nontemporal_load(A.rec + (size_t)j * C.N + n) : 0;
+      r[k] = n < C.N ? __builtin_nontemporal_load(rec + (size_t)j * C.N + n) : 0;
     }
   };
   fetch(j0, nx);
 #pragma unroll 1
   for (uint32_t pi = 0; pi < jn; ++pi) {
     const uint32_t j = j0 + pi, q = A.q0 + j;
-    uint64_t cur[KSG_WI_NPT];
+    RT cur[KSG_WI_R2NPT];
 #pragma unroll
-    for (int k = 0; k < KSG_WI_NPT; ++k) cur[k] = nx[k];
+    for (int k = 0; k < KSG_WI_R2NPT; ++k) cur[k] = nx[k];
     if (pi + 1 < jn) fetch(j + 1, nx);
     const bool kept = A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n;
     if (kept) continue;  // k_whatif<2> (per-pair outputs)
@@ -2649,29 +2663,47 @@ __global__ __launch_bounds__(256) void k_whatif_rec2(DevCluster C, DevProfile F,
     const int32_t feas_all = sm->feasible;
     const int64_t Mt = pt >= 0 ? sm->max_score[pt] : 0, Ma = pa >= 0 ? sm->max_score[pa] : 0;
     const bool skip_na = (h->flags & KPF_SKIP_NA_SCORE) != 0;
+    // DefaultNormalizeScore quotients in 32 bits while 100 x max < 2^32 (the raw
+    // fields are unsigned and <= their max); the seeded tie-break hash only for the
+    // nodes at the wave's best total (a lower total cannot win)
+    const bool n32 = Mt < 42949672 && Ma < 42949672;
     bool range_err = false;
-    uint64_t best = 0;
+    int64_t tots[KSG_WI_R2NPT];
+    uint32_t fm = 0;
+    int64_t tmax = INT64_MIN;
 #pragma unroll
-    for (int k = 0; k < KSG_WI_NPT; ++k) {
-      const uint64_t r = cur[k];
-      if (!(r & KSG_WREC_FEAS)) continue;
-      range_err |= (r & KSG_WREC_RANGE) != 0;
-      int64_t tot = (int64_t)((r >> 32) & 0x3FFFFFFFull);
+    for (int k = 0; k < KSG_WI_R2NPT; ++k) {
+      const RT r = cur[k];
+      tots[k] = 0;
+      if (!(r & FEAS)) continue;
+      fm |= 1u << k;
+      range_err |= (r & RANGE) != 0;
+      int64_t tot = (int64_t)((r >> sh_tot) & mtot);
       if (pt >= 0) {
-        int64_t s = (int64_t)((r >> 20) & 0xFFFull);
-        s = Mt == 0 ? 100 : 100 - 100 * s / Mt;  // DefaultNormalizeScore(reverse)
+        const int64_t x = (int64_t)((r >> sh_t) & mt_);
+        const int64_t s = Mt == 0 ? 100
+                          : 100 - (n32 ? (int64_t)((uint32_t)(100 * x) / (uint32_t)Mt) : 100 * x / Mt);  // (reverse)
         range_err |= s < 0 || s > 100;
         tot += s * wt;
       }
-      if (pa >= 0) {
-        int64_t s = skip_na ? 0 : (int64_t)(r & 0xFFFFFull);
-        s = skip_na ? 0 : (Ma == 0 ? s : 100 * s / Ma);
+      if (pa >= 0 && !skip_na) {
+        const int64_t x = (int64_t)(r & ma_);
+        const int64_t s = Ma == 0 ? x : (n32 ? (int64_t)((uint32_t)(100 * x) / (uint32_t)Ma) : 100 * x / Ma);
         range_err |= s < 0 || s > 100;
         tot += s * wa;
       }
       if (feas_all == 1) tot = 0;  // single feasible node: no scoring
-      const uint64_t key = pack_key(tot, F.seed, h->queue_idx, C.goff + base + k * 256);
-      best = key > best ? key : best;
+      tots[k] = tot;
+      tmax = tot > tmax ? tot : tmax;
+    }
+    const int64_t wm = wave_max(tmax);
+    uint64_t best = 0;
+#pragma unroll
+    for (int k = 0; k < KSG_WI_R2NPT; ++k) {
+      if (((fm >> k) & 1u) && tots[k] == wm) {
+        const uint64_t key = pack_key(tots[k], F.seed, h->queue_idx, C.goff + base + k * 256);
+        best = key > best ? key : best;
+      }
     }
     const uint64_t b = wave_max(best);
     if (lane0() && b) atomicMax((unsigned long long*)&sm->best_key, (unsigned long long)b);
@@ -3878,6 +3910,8 @@ struct Engine::Impl {
   DBuf<uint64_t> wrec_pairs;  // what-if: pass 1's per-pair records (run_whatif)
   uint32_t wi_chunk = 0;      // ... pods per chunk of the last step, and whether records were used
   bool wi_rec = false;
+  uint32_t max_taints = 0;  // most taints on one node (what-if record width)
+  int64_t max_na_sum = 0;   // largest preferred NodeAffinity weight sum of a program
   bool static_fits = true; // raw scores fit the record (taints per node < 4096, NodeAffinity weights < 2^20)
   DBuf<StaticRec> stat;   // static records of a chunk of pods [chunk][N]
   DBuf<int64_t> mpred;    // [chunk][2] static max of the Taint / NodeAffinity raw scores
@@ -4110,8 +4144,9 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   I.goff = ns.global_offset;
   I.G = std::max(ns.global_n, ns.global_offset + ns.n);
   I.static_fits = true;
-  for (uint32_t i = 0; i < ns.n; ++i)
-    if (ns.taint_off[i + 1] - ns.taint_off[i] >= 4096) I.static_fits = false;
+  I.max_taints = 0;
+  for (uint32_t i = 0; i < ns.n; ++i) I.max_taints = std::max(I.max_taints, ns.taint_off[i + 1] - ns.taint_off[i]);
+  if (I.max_taints >= 4096) I.static_fits = false;
   I.R = ns.n_res;
   I.K = ns.n_keys;
   if (!I.alloc.upload(ns.alloc, s, err) || !I.req.upload(ns.requested, s, err) || !I.nzc.upload(ns.nz_cpu, s, err) ||
@@ -4544,13 +4579,14 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
 }
 
 // The static record keeps the raw NodeAffinity score in 20 bits.
-static bool na_weights_fit(const std::vector<uint8_t>& prog) {
+static int64_t na_weight_sum(const std::vector<uint8_t>& prog) {
   const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
   const int32_t* i32 = reinterpret_cast<const int32_t*>(prog.data() + h->off_i32);
   int64_t sum = 0;
   for (int t = 0; t < h->n_pref_terms; ++t) sum += i32[h->pref_w_off + t] > 0 ? i32[h->pref_w_off + t] : 0;
-  return sum <= (int64_t)KSG_RAW_NA_MASK;
+  return sum;
 }
+static bool na_weights_fit(const std::vector<uint8_t>& prog) { return na_weight_sum(prog) <= (int64_t)KSG_RAW_NA_MASK; }
 
 static PodLite pod_lite(const std::vector<uint8_t>& prog) {
   const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
@@ -4633,21 +4669,29 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
     int64_t wsum = 0;
     for (int i = 0; i < I.F.n; ++i)
       if (I.F.plugins[i] == KP_FIT || I.F.plugins[i] == KP_BA) wsum += I.F.weight[i] > 0 ? I.F.weight[i] : 0;
-    int rec1_waves = 6;
-    if (const char* e = std::getenv("KSG_WI_REC1_WAVES")) rec1_waves = (int)std::strtol(e, nullptr, 10);
     A.need_eph = I.any_eph_req ? 1u : 0u;
     const bool use_rec = rec_mb > 0 && I.R <= 4 && I.static_fits && 100 * wsum < (int64_t)1 << 30;
+    // record fields as narrow as the cluster allows: 4-byte records when the raw
+    // NodeAffinity (<= the programs' largest weight sum), raw Taint (<= most taints
+    // on a node) and Fit/BA sum (<= 100 x their weights) fit 30 bits
+    auto bits = [](uint64_t v) { uint32_t b = 0; while (v) { ++b; v >>= 1; } return b; };
+    A.bw_a = bits((uint64_t)I.max_na_sum);
+    A.bw_t = bits(I.max_taints);
+    A.bw_tot = bits((uint64_t)(100 * wsum));
+    const bool narrow = A.bw_a + A.bw_t + A.bw_tot <= 30 && !std::getenv("KSG_WHATIF_WIDE");
+    if (!narrow) { A.bw_a = 20; A.bw_t = 12; A.bw_tot = 30; }
+    const size_t rbytes = narrow ? 4 : 8;
     uint32_t chunk = count;
     if (use_rec) {
-      const size_t per_pod = (size_t)N * sizeof(uint64_t);
+      const size_t per_pod = (size_t)N * rbytes;
       const size_t fit = (rec_mb << 20) / per_pod / KSG_WI_PODS * KSG_WI_PODS;
       chunk = (uint32_t)std::min<size_t>(count, std::max<size_t>(fit, KSG_WI_PODS));
       std::string aerr;  // no room: smaller chunks
-      while (!I.wrec_pairs.alloc((size_t)chunk * N, aerr) && chunk > KSG_WI_PODS) {
+      while (!I.wrec_pairs.alloc(((size_t)chunk * N * rbytes + 7) / 8, aerr) && chunk > KSG_WI_PODS) {
         (void)hipGetLastError();  // (the failed hipMalloc's error is not the run's)
         chunk = std::max<uint32_t>(chunk / 2 / KSG_WI_PODS * KSG_WI_PODS, KSG_WI_PODS);
       }
-      if ((size_t)chunk * N > I.wrec_pairs.n) { err = aerr; return false; }
+      if (((size_t)chunk * N * rbytes + 7) / 8 > I.wrec_pairs.n) { err = aerr; return false; }
     }
     const dim3 pods((count + 255) / 256);
     hipLaunchKernelGGL(k_init_summaries, pods, dim3(256), 0, s, I.sums.p + first, count, I.F);
@@ -4655,10 +4699,12 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
       WiArgs a = A;
       a.q0 = first + c0;
       a.count = std::min(chunk, count - c0);
-      a.rec = use_rec ? I.wrec_pairs.p : nullptr;
+      a.rec = use_rec ? (void*)I.wrec_pairs.p : nullptr;
       const dim3 grid(std::max<uint32_t>((I.N + 256 * KSG_WI_NPT - 1) / (256 * KSG_WI_NPT), 1),
                       (a.count + KSG_WI_PODS - 1) / KSG_WI_PODS);
       const dim3 grid1(std::max<uint32_t>((I.N + 255) / 256, 1), (a.count + KSG_WI_PODS - 1) / KSG_WI_PODS);
+      const dim3 grid2(std::max<uint32_t>((I.N + 256 * KSG_WI_R2NPT - 1) / (256 * KSG_WI_R2NPT), 1),
+                       (a.count + KSG_WI_PODS - 1) / KSG_WI_PODS);
       const dim3 cpods((a.count + 255) / 256);
       const size_t xb = (size_t)a.count * sizeof(ksg_pod_summary);
       for (int pass = 1; pass <= 2; ++pass) {
@@ -4667,16 +4713,17 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
         const bool kept_here = I.keep_n && I.keep_first < a.q0 + a.count && I.keep_first + I.keep_n > a.q0;
         if (pass == 1 && use_rec) {
           if (I.eval_mode == 1) {
-            if (rec1_waves == 8) hipLaunchKernelGGL((k_whatif_rec1<8, 1>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
-            else hipLaunchKernelGGL((k_whatif_rec1<6, 1>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+            if (narrow) hipLaunchKernelGGL((k_whatif_rec1<uint32_t, 1>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+            else hipLaunchKernelGGL((k_whatif_rec1<uint64_t, 1>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
           } else {
-            if (rec1_waves == 8) hipLaunchKernelGGL((k_whatif_rec1<8, 0>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
-            else hipLaunchKernelGGL((k_whatif_rec1<6, 0>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+            if (narrow) hipLaunchKernelGGL((k_whatif_rec1<uint32_t, 0>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+            else hipLaunchKernelGGL((k_whatif_rec1<uint64_t, 0>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
           }
         }
         else if (pass == 1) hipLaunchKernelGGL(k_whatif<1>, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
         else if (use_rec) {
-          hipLaunchKernelGGL(k_whatif_rec2, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          if (narrow) hipLaunchKernelGGL(k_whatif_rec2<uint32_t>, grid2, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          else hipLaunchKernelGGL(k_whatif_rec2<uint64_t>, grid2, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
           if (kept_here) hipLaunchKernelGGL(k_whatif<2>, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
         } else hipLaunchKernelGGL(k_whatif<2>, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
         if (sampled) {
@@ -4764,6 +4811,7 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
   I.prog_bytes = off + prog.size();
   I.prog_off.push_back(off);
   if (!na_weights_fit(prog)) I.static_fits = false;
+  I.max_na_sum = std::max(I.max_na_sum, na_weight_sum(prog));
   const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
   I.prog_need.push_back(prog_need_of(h));
   for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
@@ -5044,6 +5092,9 @@ bool Engine::replace_program(uint32_t q, const std::vector<uint8_t>& prog, std::
   I.prog_off[q] = off;
   const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
   I.prog_need[q] = prog_need_of(h);
+  if (!na_weights_fit(prog)) I.static_fits = false;
+  I.max_na_sum = std::max(I.max_na_sum, na_weight_sum(prog));
+  for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
   return true;
 }
 
@@ -5093,10 +5144,12 @@ bool Engine::set_programs(const std::vector<std::vector<uint8_t>>& progs, std::s
   std::vector<uint64_t> offs(I.prog_off.begin(), I.prog_off.end());
   if (!I.prog_off_d.upload(offs, I.stream, err)) return false;
   I.any_eph_req = false;
+  I.max_na_sum = 0;
   for (auto& p : progs) {
     const ksg_prog* h = reinterpret_cast<const ksg_prog*>(p.data());
     for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
     if (!na_weights_fit(p)) I.static_fits = false;
+    I.max_na_sum = std::max(I.max_na_sum, na_weight_sum(p));
   }
   for (int i = 0; i < I.F.fit_n; ++i) I.any_eph_req |= I.F.fit_res[i] >= 2;
   for (int i = 0; i < I.F.ba_n; ++i) I.any_eph_req |= I.F.ba_res[i] >= 2;

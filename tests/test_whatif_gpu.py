@@ -121,12 +121,14 @@ def test_folded_partials_match_oracle(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rec_mb", ["0", "1"], ids=["recompute", "chunked-records"])
-def test_whatif_pass_records(monkeypatch, rec_mb):
-    """Pass 2 normally reads pass 1's per-pair records; forced here to recompute
-    every pair (0) and to split the step into record chunks (1 MiB: 64 + 32 pods at
-    1,500 nodes), single context and 2-rank sharded."""
-    monkeypatch.setenv("KSG_WHATIF_REC_MB", rec_mb)
+@pytest.mark.parametrize("env", [{"KSG_WHATIF_REC_MB": "0"}, {"KSG_WHATIF_REC_MB": "1"}, {"KSG_WHATIF_WIDE": "1"}],
+                         ids=["recompute", "chunked-records", "8-byte-records"])
+def test_whatif_pass_records(monkeypatch, env):
+    """Pass 2 normally reads pass 1's 4-byte per-pair records; forced here to
+    recompute every pair, to split the step into record chunks (1 MiB: 64 + 32 pods
+    at 1,500 nodes) and to the 8-byte layout, single context and 2-rank sharded."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     doc = g.generate(5, n_nodes=1500, n_pods=2 * STEP)
     o = _oracle_steps(doc, 2)
     want = [o.result(q) for q in range(o.n_queue)]

@@ -94,13 +94,14 @@ def main():
     # algorithmic bytes, averaged over the two pass launches: pass 1 reads the node
     # row columns once per 32-pod tile (alloc/requested/nonzero cpu+mem 48 B,
     # pods+allowed 8 B, taint CSR 8 B, ~4 label columns read by the pod's
-    # requirements 16 B = 80 B x shard x ceil(P/32)) and writes an 8-byte record per
-    # pair; pass 2 reads the records (8 B x shard x P)
+    # requirements 16 B = 80 B x shard x ceil(P/32)) and writes a 4-byte record per
+    # pair (cfg5's field widths fit 30 bits); pass 2 reads the records (4 B x shard x P)
     tiles = (P + 31) // 32
-    bytes_per_launch = (80.0 * shard * tiles + 16.0 * shard * P) / 2
-    kernel = "k_whatif (pass avg)"
-    note = ("pass 1 latency-bound on node-row / label reads (PMC profiles/r02_cfg5_pmc_sq.csv: VALU busy 4-6 %); "
-            "pass 2 streams pass 1's 8-byte per-pair records")
+    bytes_per_launch = (80.0 * shard * tiles + 8.0 * shard * P) / 2
+    kernel = "k_whatif_rec1 / k_whatif_rec2 (pass avg)"
+    note = ("pass 1 (k_whatif_rec1) issue- and L1-latency-bound: per 64-node wave and pod ~390 VALU + ~530 SALU "
+            "instructions, 44 % of wave time waiting (profiles/r02e_cfg5_pmc_sq.csv); pass 2 streams pass 1's "
+            "4-byte per-pair records")
     workload = f"cfg5: {a.nodes} nodes, {P} pods/step, TaintToleration+NodeAffinity+Fit+BA"
     if a.variant == "pts-ipa":  # table chain: k_eval reads 68 B per node (row 56, zone id 4, class count 8)
         bytes_per_launch = 68.0 * shard

@@ -12,6 +12,11 @@ value = pairs evaluated by all ranks / max-over-ranks wall time of the K timed
 steps.  Multi-GPU: one process per GPU (torch.distributed.run); each rank owns
 its own shard of nodes of a weak-scaled cluster (5,000 nodes per GPU) —
 see DESIGN.md "Multi-GPU".
+
+At N=1 the same JSON line also carries the other BASELINE configs as extra keys
+(--extra): cfg3 and cfg4 queues at full size, and cfg5 — one what-if step of
+4,096 pods x 1,000,000 nodes per timed step (bench_whatif.py) — each with its own
+roofline and CPU baseline.
 """
 import argparse
 import json
@@ -34,7 +39,8 @@ def parse():
     ap.add_argument("--pods", type=int, default=10000)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on a bounded sample (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="CPU time per oracle variant")
-    ap.add_argument("--extra", default="3,4", help="other BASELINE configs reported beside cfg2 (N=1 only)")
+    ap.add_argument("--extra", default="3,4,5", help="other BASELINE configs reported beside cfg2 (N=1 only; "
+                    "5 = the cfg5 what-if step of bench_whatif.py)")
     ap.add_argument("--extra-steps", type=int, default=2)
     ap.add_argument("--cpu-workers", type=int, default=16, help="parallelize.Until workers (upstream default 16)")
     return ap.parse_args()
@@ -291,6 +297,13 @@ def main():
         out["cpu_baseline"] = cpu_baseline(json.dumps(doc).encode(), n_nodes, a.cpu_workers, a.cpu_seconds, "cfg2")
     if world == 1 and a.extra:
         for c in (int(x) for x in a.extra.split(",") if x):
+            if c == 5:  # what-if steps: 1M nodes x 4,096 pods per step (bench_whatif.py)
+                import bench_whatif
+                wa = bench_whatif.parse(["--steps", str(max(a.extra_steps, 2)), "--warmup", "1",
+                                         "--cpu-pods", "16" if a.cpu_baseline else "0",
+                                         "--cpu-workers", str(a.cpu_workers)])
+                out["cfg5"] = bench_whatif.run(wa, torch)
+                continue
             out[f"cfg{c}"] = extra_config(c, torch, a.extra_steps, 1, a.cpu_seconds if a.cpu_baseline else 0,
                                           a.cpu_workers)
     print(json.dumps(out))

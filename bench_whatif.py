@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
 HBM_PEAK_GBS = 8000.0
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--nodes", type=int, default=1_000_000)
     ap.add_argument("--step-pods", type=int, default=4096)
@@ -37,7 +37,11 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--variant", choices=["cfg5", "pts-ipa"], default="cfg5")
     ap.add_argument("--existing", type=int, default=1_000_000, help="existing pods (pts-ipa variant)")
-    a = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main():
+    a = parse()
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -47,6 +51,14 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    out = run(a, torch, rank, world, local, dist)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+
+
+def run(a, torch, rank=0, world=1, local=0, dist=None):
+    """One what-if benchmark (args as parse()); the result line on rank 0, else None
+    (bench.py reports cfg5 through this at N=1)."""
     from ksg import Scheduler, generator as g
     t0 = time.time()
     n_pods = a.step_pods * (a.warmup + a.steps)
@@ -87,8 +99,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     res = s.results(a.warmup * P, a.steps * P)
+    del s
     if rank != 0:
-        return
+        return None
     pairs = float(a.nodes) * P * a.steps
     shard = a.nodes // world
     # algorithmic bytes, averaged over the two pass launches: pass 1 reads the node
@@ -135,7 +148,7 @@ def main():
         out["cpu_baseline"] = {"value": done * a.nodes / dt, "unit": "pairs/s", "cores": a.cpu_workers, "kind": "port",
                                "sample": f"what-if step of the first {a.cpu_pods} pods x {a.nodes} nodes, oracle "
                                          f"plugin-only path, {a.cpu_workers} parallelize.Until workers, {dt:.1f} s"}
-    print(json.dumps(out), flush=True)
+    return out
 
 
 if __name__ == "__main__":

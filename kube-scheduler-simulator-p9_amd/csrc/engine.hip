@@ -1644,6 +1644,7 @@ struct WiArgs {
   // sum (bw_tot); row (q - q0) * N + n
   void* rec;
   uint32_t bw_a, bw_t, bw_tot;
+  uint32_t small;  // 100 x the profile's weights < 2^31: every total fits 32 bits (k_whatif_rec2)
   uint32_t need_eph;  // resource columns 2..3 requested by some pod (RowV loads)
 };
 
@@ -2623,6 +2624,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
   }
 }
 
+// Unsigned 32-bit division by a pod-uniform divisor (Granlund-Montgomery): one
+// multiply-high, a subtract, an add and two shifts per quotient, exact for every
+// 32-bit dividend.
+struct UDiv {
+  uint32_t m, s1, s2;
+};
+__device__ __forceinline__ UDiv udiv_of(uint32_t d) {
+  const uint32_t l = d <= 1 ? 0u : 32u - (uint32_t)__clz(d - 1);
+  const uint32_t m = (uint32_t)(((((uint64_t)1 << l) - d) << 32) / d + 1);
+  return UDiv{m, l < 1 ? l : 1u, l > 1 ? l - 1 : 0u};
+}
+__device__ __forceinline__ uint32_t udiv(uint32_t n, const UDiv& v) {
+  const uint32_t t = __umulhi(v.m, n);
+  return (t + ((n - t) >> v.s1)) >> v.s2;
+}
+
 // Pass 2 from the records: NormalizeScore, weights, packed key, per-pod argmax.
 // Each thread keeps the next pod's records in flight while it reduces this one's;
 // KSG_WI_R2NPT nodes per thread amortise the per-pod reduction and atomics.
@@ -2648,61 +2665,115 @@ __global__ __launch_bounds__(256) void k_whatif_rec2(DevCluster C, DevProfile F,
       r[k] = n < C.N ? __builtin_nontemporal_load(rec + (size_t)j * C.N + n) : 0;
     }
   };
+  // the next pod's summary fields and program flags are requested with its records
+  struct PodP {
+    int32_t feas, qidx;
+    uint32_t flags;
+    int64_t Mt, Ma;
+  };
+  auto params = [&](uint32_t j) {
+    const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[A.q0 + j]);
+    const ksg_pod_summary* sm = A.sums + A.q0 + j;
+    return PodP{sm->feasible, h->queue_idx, h->flags, pt >= 0 ? sm->max_score[pt] : 0, pa >= 0 ? sm->max_score[pa] : 0};
+  };
   fetch(j0, nx);
+  PodP np = params(j0);
 #pragma unroll 1
   for (uint32_t pi = 0; pi < jn; ++pi) {
     const uint32_t j = j0 + pi, q = A.q0 + j;
     RT cur[KSG_WI_R2NPT];
 #pragma unroll
     for (int k = 0; k < KSG_WI_R2NPT; ++k) cur[k] = nx[k];
-    if (pi + 1 < jn) fetch(j + 1, nx);
+    const PodP P = np;
+    if (pi + 1 < jn) {
+      fetch(j + 1, nx);
+      np = params(j + 1);
+    }
     const bool kept = A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n;
     if (kept) continue;  // k_whatif<2> (per-pair outputs)
-    const ksg_prog* h = reinterpret_cast<const ksg_prog*>(progs + prog_off[q]);
     ksg_pod_summary* sm = A.sums + q;
-    const int32_t feas_all = sm->feasible;
-    const int64_t Mt = pt >= 0 ? sm->max_score[pt] : 0, Ma = pa >= 0 ? sm->max_score[pa] : 0;
-    const bool skip_na = (h->flags & KPF_SKIP_NA_SCORE) != 0;
+    const int32_t feas_all = P.feas;
+    const int64_t Mt = P.Mt, Ma = P.Ma;
+    const bool skip_na = (P.flags & KPF_SKIP_NA_SCORE) != 0;
     // DefaultNormalizeScore quotients in 32 bits while 100 x max < 2^32 (the raw
     // fields are unsigned and <= their max); the seeded tie-break hash only for the
     // nodes at the wave's best total (a lower total cannot win)
     const bool n32 = Mt < 42949672 && Ma < 42949672;
     bool range_err = false;
-    int64_t tots[KSG_WI_R2NPT];
     uint32_t fm = 0;
-    int64_t tmax = INT64_MIN;
-#pragma unroll
-    for (int k = 0; k < KSG_WI_R2NPT; ++k) {
-      const RT r = cur[k];
-      tots[k] = 0;
-      if (!(r & FEAS)) continue;
-      fm |= 1u << k;
-      range_err |= (r & RANGE) != 0;
-      int64_t tot = (int64_t)((r >> sh_tot) & mtot);
-      if (pt >= 0) {
-        const int64_t x = (int64_t)((r >> sh_t) & mt_);
-        const int64_t s = Mt == 0 ? 100
-                          : 100 - (n32 ? (int64_t)((uint32_t)(100 * x) / (uint32_t)Mt) : 100 * x / Mt);  // (reverse)
-        range_err |= s < 0 || s > 100;
-        tot += s * wt;
-      }
-      if (pa >= 0 && !skip_na) {
-        const int64_t x = (int64_t)(r & ma_);
-        const int64_t s = Ma == 0 ? x : (n32 ? (int64_t)((uint32_t)(100 * x) / (uint32_t)Ma) : 100 * x / Ma);
-        range_err |= s < 0 || s > 100;
-        tot += s * wa;
-      }
-      if (feas_all == 1) tot = 0;  // single feasible node: no scoring
-      tots[k] = tot;
-      tmax = tot > tmax ? tot : tmax;
-    }
-    const int64_t wm = wave_max(tmax);
     uint64_t best = 0;
+    if (n32 && A.small) {  // every total < 2^31: 32-bit sums, invariant-divisor quotients
+      const UDiv dt = udiv_of(Mt > 0 ? (uint32_t)Mt : 1u), da = udiv_of(Ma > 0 ? (uint32_t)Ma : 1u);
+      const uint32_t wt32 = (uint32_t)wt, wa32 = (uint32_t)wa;
+      uint32_t tots[KSG_WI_R2NPT];
+      uint32_t tmax = 0;
 #pragma unroll
-    for (int k = 0; k < KSG_WI_R2NPT; ++k) {
-      if (((fm >> k) & 1u) && tots[k] == wm) {
-        const uint64_t key = pack_key(tots[k], F.seed, h->queue_idx, C.goff + base + k * 256);
-        best = key > best ? key : best;
+      for (int k = 0; k < KSG_WI_R2NPT; ++k) {
+        const RT r = cur[k];
+        tots[k] = 0;
+        if (!(r & FEAS)) continue;
+        fm |= 1u << k;
+        range_err |= (r & RANGE) != 0;
+        uint32_t tot = (uint32_t)((r >> sh_tot) & mtot);
+        if (pt >= 0) {
+          const uint32_t x = (uint32_t)((r >> sh_t) & mt_);
+          const uint32_t s = Mt == 0 ? 100u : 100u - udiv(100u * x, dt);  // (reverse)
+          range_err |= s > 100u;
+          tot += s * wt32;
+        }
+        if (pa >= 0 && !skip_na) {
+          const uint32_t x = (uint32_t)(r & ma_);
+          const uint32_t s = Ma == 0 ? x : udiv(100u * x, da);
+          range_err |= s > 100u;
+          tot += s * wa32;
+        }
+        if (feas_all == 1) tot = 0;  // single feasible node: no scoring
+        tots[k] = tot;
+        tmax = tot > tmax ? tot : tmax;
+      }
+      const uint32_t wm = (uint32_t)wave_max((int64_t)(fm ? tmax : 0));
+#pragma unroll
+      for (int k = 0; k < KSG_WI_R2NPT; ++k) {
+        if (((fm >> k) & 1u) && tots[k] == wm) {
+          const uint64_t key = pack_key((int64_t)tots[k], F.seed, P.qidx, C.goff + base + k * 256);
+          best = key > best ? key : best;
+        }
+      }
+    } else {
+      int64_t tots[KSG_WI_R2NPT];
+      int64_t tmax = INT64_MIN;
+#pragma unroll
+      for (int k = 0; k < KSG_WI_R2NPT; ++k) {
+        const RT r = cur[k];
+        tots[k] = 0;
+        if (!(r & FEAS)) continue;
+        fm |= 1u << k;
+        range_err |= (r & RANGE) != 0;
+        int64_t tot = (int64_t)((r >> sh_tot) & mtot);
+        if (pt >= 0) {
+          const int64_t x = (int64_t)((r >> sh_t) & mt_);
+          const int64_t s = Mt == 0 ? 100
+                            : 100 - (n32 ? (int64_t)((uint32_t)(100 * x) / (uint32_t)Mt) : 100 * x / Mt);  // (reverse)
+          range_err |= s < 0 || s > 100;
+          tot += s * wt;
+        }
+        if (pa >= 0 && !skip_na) {
+          const int64_t x = (int64_t)(r & ma_);
+          const int64_t s = Ma == 0 ? x : (n32 ? (int64_t)((uint32_t)(100 * x) / (uint32_t)Ma) : 100 * x / Ma);
+          range_err |= s < 0 || s > 100;
+          tot += s * wa;
+        }
+        if (feas_all == 1) tot = 0;  // single feasible node: no scoring
+        tots[k] = tot;
+        tmax = tot > tmax ? tot : tmax;
+      }
+      const int64_t wm = wave_max(tmax);
+#pragma unroll
+      for (int k = 0; k < KSG_WI_R2NPT; ++k) {
+        if (((fm >> k) & 1u) && tots[k] == wm) {
+          const uint64_t key = pack_key(tots[k], F.seed, P.qidx, C.goff + base + k * 256);
+          best = key > best ? key : best;
+        }
       }
     }
     const uint64_t b = wave_max(best);
@@ -4678,6 +4749,11 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
     A.bw_a = bits((uint64_t)I.max_na_sum);
     A.bw_t = bits(I.max_taints);
     A.bw_tot = bits((uint64_t)(100 * wsum));
+    {
+      int64_t wall = 0;
+      for (int i = 0; i < I.F.n; ++i) wall += I.F.weight[i] > 0 ? I.F.weight[i] : 0;
+      A.small = 100 * wall < ((int64_t)1 << 31) && !std::getenv("KSG_WHATIF_WIDE") ? 1u : 0u;  // (WIDE: 64-bit path too)
+    }
     const bool narrow = A.bw_a + A.bw_t + A.bw_tot <= 30 && !std::getenv("KSG_WHATIF_WIDE");
     if (!narrow) { A.bw_a = 20; A.bw_t = 12; A.bw_tot = 30; }
     const size_t rbytes = narrow ? 4 : 8;

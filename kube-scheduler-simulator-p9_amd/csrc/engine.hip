@@ -343,6 +343,7 @@ __device__ __forceinline__ int64_t wave_max(int64_t v) {  // order-preserving ma
 }
 __device__ __forceinline__ int64_t wave_min(int64_t v) { return ~wave_max((int64_t)~v); }
 __device__ __forceinline__ int32_t wave_min(int32_t v) { return __ockl_wfred_min_i32(v); }
+__device__ __forceinline__ int32_t wave_max(int32_t v) { return __ockl_wfred_max_i32(v); }
 __device__ __forceinline__ int32_t wave_sum(int32_t v) { return __ockl_wfred_add_i32(v); }
 __device__ __noinline__ int64_t div_i64_slow(int64_t x, int64_t a) { return x / a; }
 // floor(x / a) for 0 <= x, a > 0 — exact.  32-bit operands use the hardware
@@ -2543,7 +2544,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     const ProgView V = view(progs + prog_off[A.q0 + j]);
     const ksg_prog* h = V.h;
     int cnt = 0;
-    int64_t tx = INT64_MIN, tn = INT64_MAX, ax = INT64_MIN, an = INT64_MAX;
+    int32_t tx = INT32_MIN, tn = INT32_MAX, ax = INT32_MIN, an = INT32_MAX;  // (raw scores < 2^20: static_fits)
     if (live) {
       RT rw = 0;
       if (!(h->flags & KPF_PREFILTER_REJECT) &&
@@ -2583,12 +2584,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             else tot += s * F.w_ba;
           }
           if (ht) {  // (field widths from the cluster's taint counts / the programs' weights)
-            tx = tn = tpref;
+            tx = tn = (int32_t)tpref;
             rw |= (RT)tpref << sh_t;
           }
           if (ha) {
             const int64_t s = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n);
-            ax = an = s;
+            ax = an = (int32_t)s;
             rw |= (RT)s;
           }
           if (!(rw & RANGE)) rw |= (RT)tot << sh_tot;
@@ -2602,7 +2603,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     if (lane == 0) { r[0] = c; r[1] = tx; r[2] = tn; r[3] = ax; r[4] = an; }
     __syncthreads();  // (red double-buffered: one barrier per pod)
     if (threadIdx.x == 0) {
-      int64_t v[5] = {0, INT64_MIN, INT64_MAX, INT64_MIN, INT64_MAX};
+      int64_t v[5] = {0, INT32_MIN, INT32_MAX, INT32_MIN, INT32_MAX};
       for (int k = 0; k < 4; ++k) {
         const int64_t* x = red[pi & 1][k];
         v[0] += x[0];

@@ -112,8 +112,8 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
     tiles = (P + 31) // 32
     bytes_per_launch = (80.0 * shard * tiles + 8.0 * shard * P) / 2
     kernel = "k_whatif_rec1 / k_whatif_rec2 (pass avg)"
-    note = ("pass 1 (k_whatif_rec1) issue- and L1-latency-bound: per 64-node wave and pod ~390 VALU + ~530 SALU "
-            "instructions, 44 % of wave time waiting (profiles/r02e_cfg5_pmc_sq.csv); pass 2 streams pass 1's "
+    note = ("pass 1 (k_whatif_rec1) issue- and L1-latency-bound: per 64-node wave and pod ~333 VALU + ~525 SALU "
+            "instructions, 45 % of wave time waiting (profiles/r02g_cfg5_pmc_sq.csv); pass 2 streams pass 1's "
             "4-byte per-pair records")
     workload = f"cfg5: {a.nodes} nodes, {P} pods/step, TaintToleration+NodeAffinity+Fit+BA"
     if a.variant == "pts-ipa":  # table chain: k_eval reads 68 B per node (row 56, zone id 4, class count 8)

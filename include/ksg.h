@@ -96,6 +96,17 @@ int ksg_abi_version(void);
 int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len);
 int ksg_num_nodes(const ksg_ctx* ctx);     /* global node count */
 int ksg_queue_len(const ksg_ctx* ctx);
+/* The queue a document loads is the scheduling queue's pop order (upstream
+ * v1.30.4 internal/queue/scheduling_queue.go): with SchedulingGates in the
+ * profile (its PreEnqueue; default MultiPoint, scheduler_test.go:536) pods
+ * carrying spec.schedulingGates never enter it — no cycle, no annotations —
+ * and the rest are ordered as PrioritySort's Less (queuesort/priority_sort.go):
+ * higher spec.priority first, then document order.  Queue index q is that
+ * position; ksg_queue_pod names it ("namespace/name"), ksg_gated_pods lists the
+ * held-back pods ("namespace/name\n" lines).  ksg_cycle pods are appended in
+ * the order the framework runs them. */
+int ksg_queue_pod(const ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len);
+int ksg_gated_pods(const ksg_ctx* ctx, char* buf, size_t cap, size_t* len);
 
 /* Queue mode: schedule queue pods [first, first+count) back to back on the
  * device; every selection is assumed on the device before the next pod

@@ -272,7 +272,8 @@ struct Pod {
   bool volume_plugins_act = false;  // a volume other than a PVC the volume plugins act on (not modelled)
   vector<string> claims;            // spec.volumes[].persistentVolumeClaim.claimName, in volume order
   int32_t doc = -1;                 // index of a JSON document only this pod references (ksg_cycle), or -1
-  i64 priority = 0;                 // spec.priority (PrioritySort order is the caller's; DefaultPreemption)
+  i64 priority = 0;                 // spec.priority (PrioritySort queue order; DefaultPreemption)
+  bool gated = false;               // spec.schedulingGates non-empty (SchedulingGates PreEnqueue)
   bool preempt_never = false;       // spec.preemptionPolicy Never (PodEligibleToPreemptOthers)
   i64 start_time = INT64_MAX;       // status.startTime, epoch seconds; none: started last (GetPodStartTime: now)
 };
@@ -362,6 +363,7 @@ static Pod parse_pod(const J& v) {
   if (!sp) return p;
   p.node = str_of((*sp)["nodeName"]);
   if (auto* pr = (*sp)["priority"]; pr && !pr->null()) p.priority = (i64)pr->num();
+  if (auto* g = (*sp)["schedulingGates"]; g && !g->items.empty()) p.gated = true;
   p.preempt_never = str_of((*sp)["preemptionPolicy"]) == "Never";
   if (const J* st = v["status"])
     if (const J* t = (*st)["startTime"]; t && !t->null()) p.start_time = rfc3339_seconds(str_of(t));
@@ -2559,6 +2561,8 @@ struct Cluster {
       }
     if (qd)
       for (auto& p : qd->items) queue.push_back(parse_pod(p));
+    const J* qs = d["queueSort"];  // false: pods arrive one at a time (arrival order, no PrioritySort reordering)
+    order_queue(!(qs && qs->t == J::BOOL && !qs->b));
     pvcs.clear(); pvs.clear(); classes.clear();
     if (const J* a = d["pvcs"])
       for (auto& x : a->items) { PVC c = parse_pvc(x); pvcs[c.ns + "/" + c.name] = c; }
@@ -2613,6 +2617,34 @@ struct Cluster {
     assumed_in.clear();
     epoch = 0;
     return true;
+  }
+
+  // The pending pods of a loaded document enter the scheduling queue together
+  // (upstream v1.30.4 internal/queue/scheduling_queue.go): PreEnqueue of
+  // SchedulingGates (plugins/schedulinggates, in the default MultiPoint list,
+  // scheduler_test.go:536) keeps a pod with spec.schedulingGates out of activeQ —
+  // it is never scheduled and no plugin records anything for it — and activeQ
+  // pops in PrioritySort order (plugins/queuesort/priority_sort.go Less: higher
+  // spec.priority first, then the earlier queue timestamp = document order).
+  // Queue index q is the position in that order; gated pods are listed apart.
+  // sort == false (document key "queueSort": false): the pods arrive one at a
+  // time at an idle scheduler, each popped before the next arrives (arrival order).
+  vector<Pod> gated;
+  bool has_plugin(const char* n) const {
+    for (int i = 0; i < n_plugins; ++i)
+      if (names[i] == n) return true;
+    return false;
+  }
+  void order_queue(bool sort) {
+    gated.clear();
+    if (has_plugin("SchedulingGates")) {
+      vector<Pod> keep;
+      keep.reserve(queue.size());
+      for (auto& p : queue) (p.gated ? gated : keep).push_back(std::move(p));
+      queue = std::move(keep);
+    }
+    if (sort)
+      std::stable_sort(queue.begin(), queue.end(), [](const Pod& a, const Pod& b) { return a.priority > b.priority; });
   }
 
   // DefaultPreemption's dry run (preempt()) runs on unsharded contexts; a sharded
@@ -4188,6 +4220,19 @@ static int put_str(ksg_ctx* ctx, const std::string& s, char* buf, size_t cap, si
   if (cap < s.size()) return KSG_E_NOBUF;
   std::memcpy(buf, s.data(), s.size());
   return KSG_OK;
+}
+
+int ksg_queue_pod(const ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len) {
+  if (!ctx) return KSG_E_INVALID;
+  if (q >= ctx->c.queue.size()) return KSG_E_RANGE;
+  return put_str(nullptr, ctx->c.queue[q].ns + "/" + ctx->c.queue[q].name, buf, cap, len);
+}
+
+int ksg_gated_pods(const ksg_ctx* ctx, char* buf, size_t cap, size_t* len) {
+  if (!ctx) return KSG_E_INVALID;
+  std::string s;
+  for (auto& p : ctx->c.gated) s += p.ns + "/" + p.name + "\n";
+  return put_str(nullptr, s, buf, cap, len);
 }
 
 int ksg_plugin_position(const ksg_ctx* ctx, const char* name, size_t len) {

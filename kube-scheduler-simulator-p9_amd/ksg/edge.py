@@ -31,8 +31,10 @@ Variants (each a small seeded cluster, same document shape as ``generator``):
   priorities (some preemptionPolicy Never), host ports, pod-count limits,
   spread constraints, required anti-affinity, taints and node selectors, so that
   unschedulable pods meet both Unschedulable nodes (preemption may help) and
-  UnschedulableAndUnresolvable ones.  The queue is in the order given (no
-  PrioritySort): earlier queue pods can be victims of later ones.
+  UnschedulableAndUnresolvable ones.  The queue pops in PrioritySort order;
+  with ``queue_sort=False`` (document key ``"queueSort": false``: pods arriving
+  one at a time) it keeps document order, so earlier queue pods can be victims
+  of later ones.
 * ``volumes``   the whole default profile over pods with PersistentVolumeClaims
   (ResourcesForSnap pvs / pvcs / storageClasses): claims bound to local PVs
   (hostname node affinity: VolumeBinding's PreFilterResult), to zonal PVs
@@ -43,6 +45,12 @@ Variants (each a small seeded cluster, same document shape as ``generator``):
   claims, deleting / lost / missing claims, ReadWriteOncePod claims used by a
   bound pod or shared by two queue pods; nodes with and without zone / region
   labels; CSI attach limits from CSINode counts or the legacy allocatable key.
+* ``queue``     queue entry of the default profile, as a ResourcesForSnap
+  document (pending pods mixed into "pods", no "queue" key): pods carrying
+  spec.schedulingGates (SchedulingGates' PreEnqueue keeps them out: never
+  scheduled, no annotations), pending pods at mixed priorities (PrioritySort:
+  higher priority first, then document order) on a nearly full cluster, so
+  that the order decides placements and DefaultPreemption nominations.
 """
 from __future__ import annotations
 
@@ -53,7 +61,7 @@ from .generator import (HOSTNAME, ZONE, Gi, Mi, Rng, make_profile, node_obj, pod
 GPU = "example.com/gpu"
 EPH = "ephemeral-storage"
 NAMESPACES = ["default", "ns-a", "ns-b", "team-x"]
-EDGE_VARIANTS = ("fit_most", "fit_rtc", "na", "pts", "ipa", "ipa_ignore", "preempt", "volumes")
+EDGE_VARIANTS = ("fit_most", "fit_rtc", "na", "pts", "ipa", "ipa_ignore", "preempt", "volumes", "queue")
 
 
 def edge_seed(variant: str) -> int:
@@ -374,7 +382,7 @@ def _start(r):
     return f"2025-01-{1 + r.below(28):02d}T{r.below(24):02d}:{r.pick([0, 30]):02d}:00Z"
 
 
-def gen_preempt(n_nodes=24, n_existing=120, n_pods=90, seed=None):
+def gen_preempt(n_nodes=24, n_existing=120, n_pods=90, seed=None, queue_sort=True):
     seed = edge_seed("preempt") if seed is None else seed
     r = Rng(seed)
     nodes = []
@@ -422,7 +430,10 @@ def gen_preempt(n_nodes=24, n_existing=120, n_pods=90, seed=None):
     prof = make_profile([("TaintToleration", 3), ("NodeAffinity", 2), ("NodePorts", 1), ("NodeResourcesFit", 1),
                          ("PodTopologySpread", 2), ("InterPodAffinity", 2), ("DefaultPreemption", 1),
                          ("NodeResourcesBalancedAllocation", 1)], seed)
-    return {"profile": prof, "nodes": nodes, "pods": bound, "queue": queue}
+    doc = {"profile": prof, "nodes": nodes, "pods": bound, "queue": queue}
+    if not queue_sort:
+        doc["queueSort"] = False
+    return doc
 
 
 REGION = "topology.kubernetes.io/region"
@@ -606,6 +617,43 @@ def gen_volumes(n_nodes=40, n_existing=60, n_pods=120, seed=None):
             "storageClasses": classes, "csiNodes": csi_nodes}
 
 
+def gen_queue(n_nodes=16, n_existing=60, n_pods=70, seed=None):
+    seed = edge_seed("queue") if seed is None else seed
+    r = Rng(seed)
+    nodes = []
+    for i in range(n_nodes):
+        labels = {ZONE: f"zone-{r.below(3)}"} if r.pct() < 90 else {}
+        nodes.append(node_obj(f"node-{i:07d}", 1000 * r.pick([4, 8]), Gi * r.pick([16, 32]),
+                              pods=r.pick([110, 110, 8]), labels=labels))
+    pods = []
+    for e in range(n_existing):
+        p = pod_obj(f"ex-{e:07d}", [req(250 * (1 + r.below(8)), 512 * Mi * (1 + r.below(6)))], labels=_labels(r),
+                    node=nodes[r.below(n_nodes)]["metadata"]["name"], ns=r.pick(NAMESPACES),
+                    priority=r.pick(PRIORITIES))
+        st = _start(r)
+        if st:
+            p["status"] = {"startTime": st}
+        pods.append(p)
+    for j in range(n_pods):
+        spec = {"priority": r.pick(PRIORITIES + [5000, 20000])}
+        if r.pct() < 18:
+            spec["schedulingGates"] = [{"name": r.pick(["example.com/quota", "example.com/storage"])}]
+        if r.pct() < 10:
+            spec["preemptionPolicy"] = "Never"
+        if r.pct() < 20:
+            spec["topologySpreadConstraints"] = [{
+                "maxSkew": 1, "topologyKey": ZONE, "whenUnsatisfiable": r.pick(["DoNotSchedule", "ScheduleAnyway"]),
+                "labelSelector": _sel(r)}]
+        cpu = 500 * (1 + r.below(8)) if r.pct() < 92 else 10000
+        p = pod_obj(f"pod-{j:07d}", [req(cpu, 512 * Mi * (1 + r.below(10)))], labels=_labels(r),
+                    ns=r.pick(NAMESPACES), **spec)
+        pods.insert(r.below(len(pods) + 1), p)  # pending pods anywhere in the document
+    from .generator import DEFAULT_PROFILE
+    prof = make_profile(DEFAULT_PROFILE, seed)
+    return {"profile": prof, "nodes": nodes, "pods": pods, "pvs": [], "pvcs": [], "storageClasses": [],
+            "priorityClasses": [], "namespaces": []}
+
+
 def generate_edge(variant: str, **sizes) -> dict:
     if variant in ("fit_most", "fit_rtc"):
         return gen_fit(variant, **sizes)
@@ -619,6 +667,8 @@ def generate_edge(variant: str, **sizes) -> dict:
         return gen_preempt(**sizes)
     if variant == "volumes":
         return gen_volumes(**sizes)
+    if variant == "queue":
+        return gen_queue(**sizes)
     raise ValueError(variant)
 
 

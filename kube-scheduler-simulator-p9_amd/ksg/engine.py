@@ -88,6 +88,8 @@ def load_library():
     L.ksg_filter_status.argtypes = [vp, u32, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_prescore_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_normalized_scores.argtypes = [vp, u32, u32, ctypes.POINTER(i64), u32]
+    L.ksg_queue_pod.argtypes = [vp, u32, cp, sz, ctypes.POINTER(sz)]
+    L.ksg_gated_pods.argtypes = [vp, cp, sz, ctypes.POINTER(sz)]
     L.ksg_synth_cluster.argtypes = [ctypes.c_int, i64, i64, i64, i64, ctypes.c_uint64, ctypes.POINTER(vp),
                                     ctypes.POINTER(sz)]
     L.ksg_free.argtypes = [vp]
@@ -138,6 +140,21 @@ class Scheduler:
     @property
     def queue_len(self):
         return self.L.ksg_queue_len(self.h)
+
+    def queue_pod(self, q):
+        """"namespace/name" of queue pod q (the queue is in scheduling order: PrioritySort)."""
+        n = ctypes.c_size_t()
+        buf = ctypes.create_string_buffer(1024)
+        self._chk(self.L.ksg_queue_pod(self.h, q, buf, 1024, ctypes.byref(n)), "ksg_queue_pod")
+        return buf.raw[:n.value].decode()
+
+    def gated_pods(self):
+        """Pods SchedulingGates' PreEnqueue keeps out of the queue ("namespace/name")."""
+        n = ctypes.c_size_t()
+        self.L.ksg_gated_pods(self.h, None, 0, ctypes.byref(n))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._chk(self.L.ksg_gated_pods(self.h, buf, n.value + 1, ctypes.byref(n)), "ksg_gated_pods")
+        return [x for x in buf.raw[:n.value].decode().split("\n") if x]
 
     def keep_outputs(self, first, count):
         self._chk(self.L.ksg_keep_outputs(self.h, first, count), "ksg_keep_outputs")

@@ -482,6 +482,7 @@ struct Pod {
   bool volume_plugins_act = false;  // a volume other than a PVC the volume plugins act on (unsupported)
   vector<string> claims;            // persistentVolumeClaim.claimName of spec.volumes, in order
   i64 priority = 0;
+  bool gated = false;               // spec.schedulingGates non-empty (SchedulingGates PreEnqueue)
   bool preempt_never = false;       // spec.preemptionPolicy: Never
   i64 start_time = INT64_MAX;       // status.startTime (epoch s); none: later than any (util.GetPodStartTime: now)
 };
@@ -549,6 +550,7 @@ static bool parse_pod(const ojson::Value& v, Pod& p) {
   if (!sp) return true;
   p.node_name = sp->get("nodeName") ? sp->get("nodeName")->str() : "";
   if (auto* pr = sp->get("priority"); pr && !pr->is_null()) p.priority = pr->i64();
+  if (auto* g = sp->get("schedulingGates"); g && !g->is_null() && !g->arr.empty()) p.gated = true;
   if (auto* pp = sp->get("preemptionPolicy"); pp && !pp->is_null()) p.preempt_never = pp->str() == "Never";
   if (auto* st = v.get("status"))
     if (auto* t = st->get("startTime"); t && !t->is_null()) p.start_time = parse_rfc3339(t->str());
@@ -1077,7 +1079,8 @@ struct Cluster {
   std::unordered_map<string, int> node_index;
   vector<NodeInfo> infos;
   vector<PodRecord> pods;  // bound + queue
-  vector<int> queue;
+  vector<int> queue;       // scheduling order (PrioritySort)
+  vector<int> gated;       // held back by SchedulingGates' PreEnqueue
   set<string> namespaces;
   // profile
   vector<PluginId> profile;  // MultiPoint order
@@ -2638,14 +2641,35 @@ static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
     c.pods.push_back(std::move(r));
     return (int)c.pods.size() - 1;
   };
+  // {"pods": bound, "queue": pending}, or the simulator's snapshot document
+  // (ResourcesForSnap, simulator/snapshot/snapshot.go:33-42): pending pods (no
+  // spec.nodeName) in "pods" are the queue, in document order
+  const ojson::Value* qdoc = d.get("queue");
   if (auto* ps = d.get("pods"))
     for (auto& p : ps->arr) {
       int pi = add(p);
       auto it = c.node_index.find(c.pods[pi].pod.node_name);
       if (it != c.node_index.end()) c.add_pod(pi, it->second);
+      else if (!qdoc && c.pods[pi].pod.node_name.empty()) c.queue.push_back(pi);
     }
-  if (auto* q = d.get("queue"))
-    for (auto& p : q->arr) c.queue.push_back(add(p));
+  if (qdoc)
+    for (auto& p : qdoc->arr) c.queue.push_back(add(p));
+  // the scheduling queue (upstream v1.30.4 internal/queue/scheduling_queue.go):
+  // SchedulingGates' PreEnqueue (plugins/schedulinggates/scheduling_gates.go)
+  // keeps pods with spec.schedulingGates out of activeQ — never scheduled,
+  // nothing recorded — and activeQ pops in PrioritySort order
+  // (plugins/queuesort/priority_sort.go Less: higher priority first, then the
+  // earlier queue timestamp = document order)
+  if (std::find(c.profile_names.begin(), c.profile_names.end(), "SchedulingGates") != c.profile_names.end()) {
+    vector<int> keep;
+    for (int qi : c.queue) (c.pods[qi].pod.gated ? c.gated : keep).push_back(qi);
+    c.queue = std::move(keep);
+  }
+  // ("queueSort": false — pods arriving one at a time at an idle scheduler — keeps arrival order)
+  auto* qs = d.get("queueSort");
+  if (!(qs && qs->kind == ojson::Value::Bool && !qs->b))
+    std::stable_sort(c.queue.begin(), c.queue.end(),
+                     [&](int a, int b) { return c.pods[a].pod.priority > c.pods[b].pod.priority; });
   // storage objects
   auto beta_class = [](const ojson::Value* md, string& cls) {
     auto* ann = md ? md->get("annotations") : nullptr;
@@ -2767,6 +2791,7 @@ static bool load_cluster(const char* js, size_t len, Cluster& c, string& err) {
         for (size_t i = 0; i < c.pods.size(); ++i) {
           const Pod& o = c.pods[i].pod;
           const bool queued = std::find(c.queue.begin(), c.queue.end(), (int)i) != c.queue.end();
+          if (std::find(c.gated.begin(), c.gated.end(), (int)i) != c.gated.end()) continue;  // never assigned
           if (queued && !with_queue) continue;
           u += (int)std::count(o.claims.begin(), o.claims.end(), name) * (o.ns == ns);
         }
@@ -2839,6 +2864,19 @@ void ksg_oracle_free(ksg_oracle* h) { delete h; }
 
 int ksg_oracle_num_nodes(ksg_oracle* h) { return (int)h->c.nodes.size(); }
 int ksg_oracle_num_queue(ksg_oracle* h) { return (int)h->c.queue.size(); }
+
+// "namespace/name" of queue pod q (scheduling order), or of gated pod -1-q (q < 0)
+int ksg_oracle_queue_pod(ksg_oracle* h, int q, char* buf, size_t cap, size_t* len) {
+  int pi = -1;
+  if (q >= 0 && q < (int)h->c.queue.size()) pi = h->c.queue[q];
+  if (q < 0 && -1 - q < (int)h->c.gated.size()) pi = h->c.gated[-1 - q];
+  if (pi < 0) return -1;
+  const std::string s = h->c.pods[pi].pod.ns + "/" + h->c.pods[pi].pod.name;
+  *len = s.size();
+  if (buf && cap >= s.size()) std::memcpy(buf, s.data(), s.size());
+  return 0;
+}
+int ksg_oracle_num_gated(ksg_oracle* h) { return (int)h->c.gated.size(); }
 
 // Schedule the next n queue pods.  record: 0 = plugins only, 1 = store emulation
 // (global mutex + map insert + FormatInt per (node, plugin), as the debuggable

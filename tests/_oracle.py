@@ -34,6 +34,9 @@ def lib():
                                            ctypes.POINTER(ctypes.c_size_t)]
         L.ksg_oracle_annotations.restype = ctypes.c_void_p
         L.ksg_oracle_annotations.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
+        L.ksg_oracle_queue_pod.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_size_t)]
+        L.ksg_oracle_num_gated.argtypes = [ctypes.c_void_p]
         L.ksg_oracle_go_log.restype = ctypes.c_double
         L.ksg_oracle_go_log.argtypes = [ctypes.c_double]
         L.ksg_oracle_pack_key.restype = ctypes.c_ulonglong
@@ -59,6 +62,28 @@ class Oracle:
     @property
     def n_queue(self):
         return lib().ksg_oracle_num_queue(self.h)
+
+    def _pod_name(self, q):
+        n = ctypes.c_size_t()
+        buf = ctypes.create_string_buffer(1024)
+        if lib().ksg_oracle_queue_pod(self.h, q, buf, 1024, ctypes.byref(n)) != 0:
+            raise IndexError(q)
+        return buf.raw[:n.value].decode()
+
+    def queue_names(self):
+        """"namespace/name" of every queue pod, in scheduling order (PrioritySort)."""
+        return [self._pod_name(q) for q in range(self.n_queue)]
+
+    def gated_names(self):
+        """"namespace/name" of the pods SchedulingGates' PreEnqueue keeps out of the queue."""
+        return [self._pod_name(-1 - i) for i in range(lib().ksg_oracle_num_gated(self.h))]
+
+    def ordered_queue(self, doc):
+        """The document's pending pod objects in the oracle's scheduling order (what the
+        framework would run through the drop-in cycle API one by one)."""
+        pend = doc["queue"] if "queue" in doc else [p for p in doc["pods"] if not p["spec"].get("nodeName")]
+        by = {(p["metadata"].get("namespace") or "default") + "/" + p["metadata"]["name"]: p for p in pend}
+        return [by[n] for n in self.queue_names()]
 
     def schedule(self, n=None, workers=1, record=3):
         n = self.n_queue if n is None else n

@@ -86,6 +86,7 @@ EDGE = {
     "edge_ipa_ignore_small": ("ipa_ignore", dict(n_nodes=14, n_existing=30, n_pods=24)),
     "edge_preempt_small": ("preempt", dict(n_nodes=10, n_existing=40, n_pods=30)),
     "edge_volumes_small": ("volumes", dict(n_nodes=16, n_existing=30, n_pods=40)),
+    "edge_queue_small": ("queue", dict(n_nodes=8, n_existing=24, n_pods=30)),
 }
 
 
@@ -95,7 +96,8 @@ def expected(doc):
     pods = []
     for q in range(o.n_queue):
         sel, feas, st = o.result(q)
-        e = {"selected": sel, "feasible": feas, "status": st, "annotations": o.annotations(q)}
+        e = {"pod": o.queue_names()[q], "selected": sel, "feasible": feas, "status": st,
+             "annotations": o.annotations(q)}
         node, victims = o.nominated(q)
         if node >= 0:  # DefaultPreemption dry run (pods of mixed priorities)
             e["nominated"] = {"node": node, "victims": victims}

@@ -13,6 +13,16 @@ from _oracle import Oracle
 from ksg import Scheduler, edge
 from test_plugin_api_gpu import rebuild
 
+
+def without_queue(doc):
+    """The document with no pending pods (the drop-in cycle API receives them one by one)."""
+    d = dict(doc)
+    if "queue" in d:
+        d["queue"] = []
+    else:
+        d["pods"] = [p for p in d["pods"] if p["spec"].get("nodeName")]
+    return d
+
 VARIANTS = list(edge.EDGE_VARIANTS)
 
 
@@ -27,6 +37,8 @@ def test_edge_queue_matches_oracle(variant):
     s.keep_outputs(0, s.queue_len)
     s.schedule()
     res = s.results()
+    assert [s.queue_pod(q) for q in range(s.queue_len)] == o.queue_names(), variant
+    assert s.gated_pods() == o.gated_names(), variant
     for q, r in enumerate(res):
         assert (r.selected, r.feasible, r.status) == o.result(q), (variant, q)
     for q in range(0, len(res), 3):
@@ -40,11 +52,9 @@ def test_edge_cycle_and_extension_points(variant):
     o = Oracle(doc)
     o.schedule(record=3)
     s = Scheduler(doc["profile"])
-    d = dict(doc)
-    d["queue"] = []
-    s.load_cluster(d)
+    s.load_cluster(without_queue(doc))
     names = [n["metadata"]["name"] for n in doc["nodes"]]
-    for i, pod in enumerate(doc["queue"]):
+    for i, pod in enumerate(o.ordered_queue(doc)):  # the framework runs them in its queue order
         q, r = s.cycle(pod, commit=True)
         assert (r.selected, r.feasible, r.status) == o.result(i), (variant, i)
         if i % 4 == 0:

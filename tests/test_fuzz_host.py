@@ -128,14 +128,17 @@ def _inputs(r, n_structural, n_bytes):
     cfg = dict(seeds[0], profile=g.config_profile(g.DEFAULT_PROFILE, 1, score=[("NodeResourcesFit", 3)]))
     seeds.append(cfg)  # scheduler-configuration form of the profile
     out = []
+
+    def pending(d):  # "queue", or the ResourcesForSnap form's pods without a node
+        return d["queue"] if "queue" in d else [p for p in d["pods"] if not p["spec"].get("nodeName")]
     for d in seeds:  # unmutated
-        out.append(SEP.join([json.dumps(d["profile"]), json.dumps(d), json.dumps(d["queue"][0]),
+        out.append(SEP.join([json.dumps(d["profile"]), json.dumps(d), json.dumps(pending(d)[0]),
                              json.dumps(_events(d, r))]))
     for _ in range(n_structural):
         d = r.choice(seeds)
         prof = _mutate(d["profile"], r) if r.random() < 0.25 else d["profile"]
         cl = _mutate(d, r)
-        pod = _mutate(d["queue"][0], r) if r.random() < 0.5 else d["queue"][-1]
+        pod = _mutate(pending(d)[0], r) if r.random() < 0.5 else pending(d)[-1]
         ev = _mutate(_events(d, r), r) if r.random() < 0.5 else _events(d, r)
         try:
             out.append(SEP.join([json.dumps(prof), json.dumps(cl), json.dumps(pod), json.dumps(ev)]))

@@ -97,9 +97,36 @@ def test_golden_families_match_generator():
         assert g.generate(d["config"], **d["sizes"]) == d["cluster"], name
     from ksg import edge
     for name in ("edge_fit_most_small", "edge_fit_rtc_small", "edge_na_small", "edge_pts_small", "edge_ipa_small",
-                 "edge_ipa_ignore_small", "edge_preempt_small", "edge_volumes_small"):
+                 "edge_ipa_ignore_small", "edge_preempt_small", "edge_volumes_small", "edge_queue_small"):
         d = fixture(name)
         assert edge.generate_edge(d["edge"], **d["sizes"]) == d["cluster"], name
+
+
+def test_queue_entry_semantics():
+    """SchedulingGates' PreEnqueue keeps gated pods out of the queue; activeQ pops in
+    PrioritySort order (higher spec.priority first, then arrival = document order);
+    "queueSort": false models pods arriving one at a time (arrival order).  Hand-worked:
+    A(0) B(100, gated) C(100) D(10) -> [C, D, A], gated [B]."""
+    gates = [{"name": "example.com/hold"}]
+    pods = [g.pod_obj("a", [g.req(100, 64 * g.Mi)], priority=0),
+            g.pod_obj("b", [g.req(100, 64 * g.Mi)], priority=100, schedulingGates=gates),
+            g.pod_obj("c", [g.req(100, 64 * g.Mi)], priority=100),
+            g.pod_obj("d", [g.req(100, 64 * g.Mi)], priority=10)]
+    nodes = [g.node_obj("node-0", 4000, 8 * g.Gi)]
+    full = g.make_profile(g.DEFAULT_PROFILE, 1)
+    o = Oracle({"profile": full, "nodes": nodes, "pods": [], "queue": pods})
+    assert o.queue_names() == ["default/c", "default/d", "default/a"]
+    assert o.gated_names() == ["default/b"]
+    # the ResourcesForSnap form: pending pods among the bound ones
+    snap = {"profile": full, "nodes": nodes, "pods": [pods[0], g.pod_obj("x", [], node="node-0")] + pods[1:]}
+    assert Oracle(snap).queue_names() == ["default/c", "default/d", "default/a"]
+    o = Oracle({"profile": full, "nodes": nodes, "pods": [], "queue": pods, "queueSort": False})
+    assert o.queue_names() == ["default/a", "default/c", "default/d"]
+    hot = g.make_profile(g.DEFAULT_HOT_PROFILE, 1)  # no SchedulingGates: nothing is held back
+    o = Oracle({"profile": hot, "nodes": nodes, "pods": [], "queue": pods})
+    assert o.queue_names() == ["default/b", "default/c", "default/d", "default/a"] and o.gated_names() == []
+    o.schedule(record=3)
+    assert all(o.result(q)[2] == 0 for q in range(4))
 
 
 def _py_go_log(x):

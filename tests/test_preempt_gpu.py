@@ -26,7 +26,8 @@ def _oracle(doc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sizes", [{}, dict(n_nodes=10, n_existing=40, n_pods=30), dict(n_existing=70, n_pods=120)],
+@pytest.mark.parametrize("sizes", [{}, dict(n_nodes=10, n_existing=40, n_pods=30),
+                                   dict(n_existing=70, n_pods=120, queue_sort=False)],
                          ids=["default", "small", "queue-victims"])
 def test_preempt_queue_matches_oracle(sizes):
     doc = _doc(**sizes)
@@ -47,11 +48,13 @@ def test_preempt_queue_matches_oracle(sizes):
 
 @pytest.mark.gpu
 def test_preempt_cycle_api_matches_oracle():
-    doc = _doc(n_pods=50)
+    # pods arriving one at a time (arrival order): earlier queue pods can be victims
+    doc = _doc(n_pods=50, queue_sort=False)
     o = _oracle(doc)
     s = Scheduler(doc["profile"])
     d = dict(doc)
     d["queue"] = []
+    d.pop("queueSort")
     s.load_cluster(d)
     for i, pod in enumerate(doc["queue"]):
         q, r = s.cycle(pod, commit=True)

@@ -73,6 +73,11 @@ struct NodeSoA {
   uint32_t nu_pairs = 0;
   std::vector<int32_t> slot_dom;
   std::vector<uint8_t> pair_node;
+  // node sharding: ranks of the context, and every node's topology values
+  // [slot][global_n] (value id, -1 none) — the pair-level class-table deltas
+  // of an assume on another rank's node (every rank keeps the global tables)
+  uint32_t shards = 1;
+  std::vector<int32_t> gtopo;
 };
 
 // Class definitions appended to the device (host.cpp registry; ksg_types.h
@@ -188,6 +193,8 @@ class Engine {
   bool set_exchange(int mode, const void* nccl_id, uint32_t rank, uint32_t ranks, ExchangeFn fn, void* user,
                     std::string& err);
   uint32_t exchange_ranks() const;
+  // diagnostic: pods the per-pod runs sent down the table chain / the scanning chain
+  void path_counts(uint64_t out[2]) const;
   static bool nccl_unique_id(void* out128, std::string& err);
   // diagnostic: enable (out == nullptr, count pods) / read back s_memtime stamps of the fixup loop
   bool fixup_stamps(uint32_t count, std::vector<uint64_t>* out, std::string& err);

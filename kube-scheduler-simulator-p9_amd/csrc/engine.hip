@@ -74,6 +74,13 @@ struct DevTables {
   const uint32_t* tc_off;    // [ntc]
   const int32_t* tc_slot;    // [ntc]
   int32_t* tc_tot;           // [ntc] terms on nodes carrying the key
+  // node sharding: the node-level entries (pc_cnt, tc_val of one-node keys) are
+  // the owner's, the pair-level ones (pc_dom, pc_tot, tc_val of shared keys,
+  // tc_tot) are global on every rank — an assume on another rank's node applies
+  // them too, with that node's topology values from gtv
+  int sharded;
+  uint32_t G;                // nodes of the whole cluster
+  const int32_t* gtv;        // [n_topo][G] every node's topology values (-1 none), sharded contexts
 };
 
 struct DevCluster {
@@ -1245,16 +1252,26 @@ __device__ __forceinline__ void node_slot_vids(const DevCluster& C, uint32_t n, 
 #pragma unroll
   for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? node_vid(C, key[s], n) : -1;
 }
-__device__ __forceinline__ void pc_add(DevCluster& C, int32_t cls, uint32_t n, int sign, const int32_t v[KSG_MAX_TOPO]) {
+// Class-table deltas come in two parts (DevTables: sharding): TP_NODE the
+// node-level entries of local node n, TP_PAIR the pair-level ones.
+enum { TP_NODE = 1, TP_PAIR = 2, TP_ALL = 3 };
+__device__ __forceinline__ void pc_add(DevCluster& C, int32_t cls, uint32_t n, int sign, const int32_t v[KSG_MAX_TOPO],
+                                       int part = TP_ALL) {
   const DevTables& T = C.T;
   if (cls < 0 || (uint32_t)cls >= T.npc) return;
-  atomicAdd(&T.pc_cnt[(size_t)cls * C.N + n], sign);
+  if (part & TP_NODE) atomicAdd(&T.pc_cnt[(size_t)cls * C.N + n], sign);
+  if (!(part & TP_PAIR)) return;
 #pragma unroll
   for (int s = 0; s < KSG_MAX_TOPO; ++s) {
     if (v[s] < 0) continue;
     atomicAdd(&T.pc_tot[(size_t)cls * KSG_MAX_TOPO + s], sign);
     if (C.nubv[s] >= 0) atomicAdd(&T.pc_dom[(size_t)cls * T.NU + (uint32_t)C.nubv[s] + v[s]], sign);
   }
+}
+// Topology values of global node g from the replicated table (sharded contexts).
+__device__ __forceinline__ void global_slot_vids(const DevCluster& C, uint32_t g, int32_t v[KSG_MAX_TOPO]) {
+#pragma unroll
+  for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? C.T.gtv[(size_t)s * C.T.G + g] : -1;
 }
 // an existing pod's term: +1 (required terms) or its signed weight (preferred)
 __device__ __forceinline__ int32_t eterm_inc(const ksg_exist_term& e) {
@@ -1263,7 +1280,7 @@ __device__ __forceinline__ int32_t eterm_inc(const ksg_exist_term& e) {
 // an existing pod's term e (its term class, table offset and topology slot) on
 // node n whose topology values are vs (null: read the term's key)
 __device__ __forceinline__ void tc_add(DevCluster& C, const ksg_exist_term& e, uint32_t n, int sign,
-                                       const int32_t* vs = nullptr) {
+                                       const int32_t* vs = nullptr, int part = TP_ALL) {
   if (e.cls < 0 || (uint32_t)e.cls >= C.T.ntc) return;
   int32_t v = -1;
   if (vs) {
@@ -1274,26 +1291,43 @@ __device__ __forceinline__ void tc_add(DevCluster& C, const ksg_exist_term& e, u
     v = node_vid(C, e.topo_key, n);
   }
   if (v < 0) return;
-  atomicAdd(&C.T.tc_val[(uint32_t)e.toff + (((C.T.uniq >> e.topo) & 1u) ? n : (uint32_t)v)], sign * eterm_inc(e));
-  atomicAdd(&C.T.tc_tot[e.cls], sign);
+  const bool one = ((C.T.uniq >> e.topo) & 1u) != 0;  // one node per value: a node-level entry
+  if (part & (one ? TP_NODE : TP_PAIR)) atomicAdd(&C.T.tc_val[(uint32_t)e.toff + (one ? n : (uint32_t)v)], sign * eterm_inc(e));
+  if (part & TP_PAIR) atomicAdd(&C.T.tc_tot[e.cls], sign);
 }
 // Every class-table delta of program V placed on (sign +1) / removed from
-// (sign -1) local node n: its pod classes and its own affinity terms.  Items
-// i = lane, lane + lanes, ... (one thread: lane 0 of 1).
+// (sign -1) a node with topology values v: its pod classes and its own affinity
+// terms (part: TP_ALL on local node n; TP_PAIR for another rank's node, n
+// unused).  Items i = lane, lane + lanes, ... (one thread: lane 0 of 1).
+__device__ void tables_assume_v(DevCluster& C, const ProgView& V, uint32_t n, const int32_t v[KSG_MAX_TOPO], int sign,
+                                uint32_t lane, uint32_t lanes, int part) {
+  const ksg_prog* h = V.h;
+  const uint32_t npm = (uint32_t)h->n_pc_match, ne = (uint32_t)h->n_exist_terms;
+  for (uint32_t i = lane; i < npm + ne; i += lanes) {
+    if (i < npm) {
+      pc_add(C, V.i32[h->pc_match_off + i], n, sign, v, part);
+    } else {
+      tc_add(C, V.et[h->exist_terms_off + (i - npm)], n, sign, v, part);
+    }
+  }
+}
 __device__ void tables_assume(DevCluster& C, const ProgView& V, uint32_t n, int sign, uint32_t lane, uint32_t lanes) {
   if (!C.T.on) return;
   const ksg_prog* h = V.h;
-  const uint32_t npm = (uint32_t)h->n_pc_match, ne = (uint32_t)h->n_exist_terms;
-  if (lane >= npm + ne) return;
+  if (lane >= (uint32_t)(h->n_pc_match + h->n_exist_terms)) return;
   int32_t v[KSG_MAX_TOPO];  // the node's topology values, loaded beside the items
   node_slot_vids(C, n, v);
-  for (uint32_t i = lane; i < npm + ne; i += lanes) {
-    if (i < npm) {
-      pc_add(C, V.i32[h->pc_match_off + i], n, sign, v);
-    } else {
-      tc_add(C, V.et[h->exist_terms_off + (i - npm)], n, sign, v);
-    }
-  }
+  tables_assume_v(C, V, n, v, sign, lane, lanes, TP_ALL);
+}
+// A sharded context's assume on global node g another rank owns: the pair-level deltas.
+__device__ void tables_assume_remote(DevCluster& C, const ProgView& V, uint32_t g, int sign, uint32_t lane,
+                                     uint32_t lanes) {
+  if (!C.T.on || !C.T.sharded || g >= C.T.G) return;
+  const ksg_prog* h = V.h;
+  if (lane >= (uint32_t)(h->n_pc_match + h->n_exist_terms)) return;
+  int32_t v[KSG_MAX_TOPO];
+  global_slot_vids(C, g, v);
+  tables_assume_v(C, V, 0, v, sign, lane, lanes, TP_PAIR);
 }
 
 __device__ void table_need(const ProgView& V, uint32_t need[4]);
@@ -1430,7 +1464,11 @@ __device__ void commit_cycle(DevCluster& C, const ProgView& V, ksg_pod_summary* 
   s->selected = (int32_t)g;
   s->status = 0;
   uint32_t n = g - C.goff;
-  if (!(mode & 1) || g < C.goff || n >= C.N) return;  // what-if, or another shard owns the node
+  if (!(mode & 1)) return;  // what-if
+  if (g < C.goff || n >= C.N) {  // another shard owns the node: the global class tables only
+    tables_assume_remote(C, V, g, +1, 0, 1);
+    return;
+  }
   assume_pod(C, V, n, +1, (mode & 2) != 0, prow);
 }
 
@@ -1601,7 +1639,11 @@ __global__ void k_assume(DevCluster C, const uint8_t* __restrict__ prog, int32_t
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   ProgView V = view(prog);
   uint32_t n = (uint32_t)gnode - C.goff;
-  if (gnode < 0 || (uint32_t)gnode < C.goff || n >= C.N) return;
+  if (gnode < 0) return;
+  if ((uint32_t)gnode < C.goff || n >= C.N) {  // another shard's node: the global class tables only
+    if (table != 2) tables_assume_remote(C, V, (uint32_t)gnode, sign, 0, 1);
+    return;
+  }
   if (table == 2) {
     assume_pod(C, V, n, sign, false, nullptr);
     if (prow && *prow >= 0) {
@@ -1801,7 +1843,12 @@ __global__ __launch_bounds__(64) void k_whatif_bind_seq(DevCluster C, const uint
   for (uint32_t j = q0; j < q0 + count; ++j) {
     const ksg_pod_summary& s = sums[j];
     const uint32_t g = (uint32_t)s.selected, n = g - C.goff;
-    if (s.status != 0 || g < C.goff || n >= C.N) continue;  // unscheduled, or another shard owns the node
+    if (s.status != 0) continue;
+    if (g < C.goff || n >= C.N) {  // another shard owns the node: the global class tables only
+      tables_assume_remote(C, view(progs + prog_off[j]), g, +1, lane, 64);
+      __syncthreads();
+      continue;
+    }
     const ProgView V = view(progs + prog_off[j]);
     tables_assume(C, V, n, +1, lane, 64);
     if (lane == 0) assume_pod(C, V, n, +1, table != 0, prow + j, 64);
@@ -4002,6 +4049,14 @@ struct Engine::Impl {
   DBuf<ksg_req> creq_d;
   uint32_t npc = 0, ntc = 0, NU = 0, nct = 0, ncreq = 0, ncval = 0, tc_used = 0;
   std::vector<uint32_t> tc_off_h;
+  // node sharding of the class tables: ranks, every node's topology values, and
+  // the classes built from this rank's existing pods alone since the last
+  // cross-rank sum of their pair-level entries (UINT32_MAX: none pending)
+  uint32_t shards = 1;
+  DBuf<int32_t> gtopo_d;
+  uint32_t red_pc0 = UINT32_MAX, red_tc0 = UINT32_MAX;
+  std::vector<int32_t> tc_slot_h;
+  DBuf<TabSeg> segs_d;
   // table chain (k_eval / k_ptsraw / k_final / k_select)
   DBuf<uint32_t> carrive;  // table chain: block arrivals of the cycle's last kernel
   DBuf<int2> alog;        // assumes whose existing-pod table rows k_flush_appends writes
@@ -4062,6 +4117,7 @@ struct Engine::Impl {
   uint32_t sample_every = 0;
   std::vector<hipEvent_t> sev;
   uint32_t n_samples = 0;
+  uint64_t path_pods[2] = {0, 0};  // diagnostic: pods run by the table chain / the scanning chain
   std::vector<Engine::KernelStat> stats;
 
   DevCluster cluster() const {
@@ -4088,6 +4144,9 @@ struct Engine::Impl {
     T.nu_base = nu_base_d.p; T.slot_dom = slot_dom_d.p; T.pair_node = pair_node_d.p;
     T.pcls = pcls_d.p; T.cterm = cterm_d.p; T.creq = creq_d.p; T.cval = cval_d.p;
     T.tc_val = tc_val.p; T.tc_off = tc_off_d.p; T.tc_slot = tc_slot_d.p; T.tc_tot = tc_tot.p;
+    T.sharded = shards > 1 ? 1 : 0;
+    T.G = G;
+    T.gtv = gtopo_d.p;
     for (int s = 0; s < KSG_MAX_TOPO; ++s) {
       C.tkeyv[s] = (size_t)s < topo.topo_key.size() ? topo.topo_key[s] : -1;
       C.nubv[s] = ((size_t)s < topo.nu_base.size() && topo.nu_base[s] != 0xFFFFFFFFu) ? (int32_t)topo.nu_base[s] : -1;
@@ -4280,6 +4339,7 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   {  // class tables: the definitions come from the host registry after the upload (add_classes)
     I.npc = I.ntc = I.nct = I.ncreq = I.ncval = I.tc_used = 0;
     I.tc_off_h.clear();
+    I.tc_slot_h.clear();
     I.NU = ns.nu_pairs;
     std::vector<uint32_t> nb(KSG_MAX_TOPO, 0xFFFFFFFFu);
     std::vector<int32_t> sd(KSG_MAX_TOPO, 0);
@@ -4289,6 +4349,14 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     pn.resize(std::max<size_t>(ns.topo_pairs, 1), 0);
     if (!I.nu_base_d.upload(nb, s, err) || !I.slot_dom_d.upload(sd, s, err) || !I.pair_node_d.upload(pn, s, err))
       return false;
+    I.shards = std::max<uint32_t>(ns.shards, 1);
+    I.red_pc0 = I.red_tc0 = UINT32_MAX;
+    if (I.shards > 1) {
+      if (ns.gtopo.size() != ns.topo_key.size() * (size_t)I.G) { err = "sharded upload without the topology table"; return false; }
+      std::vector<int32_t> gt = ns.gtopo;
+      gt.resize(std::max<size_t>(gt.size(), 1), -1);
+      if (!I.gtopo_d.upload(gt, s, err)) return false;
+    }
     I.cnblk = std::max<uint32_t>((ns.n + kChain - 1) / kChain, 1);
     if (!I.carrive.alloc(1, err) || !I.cpi.alloc((size_t)KCP_I * I.cnblk, err) ||
         !I.cpst.alloc(I.cnblk, err) ||
@@ -4382,6 +4450,7 @@ static uint32_t eval_tiles(uint32_t N, uint32_t cus) {
 // each window's candidate records between launches.
 static bool xgather(Engine::Impl& I, size_t bytes, std::string& err, const uint8_t* src = nullptr,
                     hipStream_t st = nullptr);
+static bool tables_ready(Engine::Impl& I, std::string& err);
 // Sharded windows, split over three streams so that the exchange leaves the
 // replay's critical path.  Window j's evaluation (eval-only k_window launch,
 // engine stream) needs the rows as of the end of window j-2, i.e. only the
@@ -4897,6 +4966,7 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
 
 bool Engine::assume(uint32_t q, int32_t gnode, int sign, std::string& err) {
   Impl& I = *p_;
+  if (!tables_ready(I, err)) return false;
   if (q >= I.prog_off.size()) { err = "program index out of range"; return false; }
   DevCluster C = I.cluster();
   hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, I.stream, C, I.progs.p + I.prog_off[q], gnode, sign,
@@ -4910,6 +4980,7 @@ bool Engine::bound_deltas(const std::vector<std::vector<uint8_t>>& progs, const 
                           const std::vector<int32_t>& sign, const std::vector<int32_t>& slot, std::vector<int32_t>& rows,
                           std::string& err) {
   Impl& I = *p_;
+  if (!tables_ready(I, err)) return false;
   const size_t n = progs.size();
   if (gnode.size() != n || sign.size() != n || slot.size() != n || rows.size() != n) { err = "bound_deltas: sizes"; return false; }
   if (!n) return true;
@@ -4938,6 +5009,7 @@ bool Engine::bound_deltas(const std::vector<std::vector<uint8_t>>& progs, const 
 bool Engine::toggle_pods(const std::vector<const std::vector<uint8_t>*>& progs, const std::vector<int32_t>& gnode,
                          const std::vector<int32_t>& rows, int sign, std::string& err) {
   Impl& I = *p_;
+  if (!tables_ready(I, err)) return false;
   const size_t n = progs.size();
   if (gnode.size() != n || rows.size() != n) { err = "toggle_pods: sizes"; return false; }
   if (!n) return true;
@@ -5078,6 +5150,54 @@ static bool dev_zero_tail(DBuf<T>& b, size_t used, size_t count, hipStream_t s, 
   return true;
 }
 
+// Node-sharded class tables: sum the pair-level entries of the classes built
+// since the last call across ranks (each rank built them from its own existing
+// pods), in one all-gather on the engine stream.  Without the exchange yet it
+// stays pending: runs and in-place deltas call it first (tables_ready).
+static bool reduce_tables(Engine::Impl& I, std::string& err) {
+  if (I.shards <= 1 || (I.red_pc0 == UINT32_MAX && I.red_tc0 == UINT32_MAX)) return true;
+  if (I.xranks != I.shards) return true;
+  std::vector<TabSeg> sg;
+  uint32_t total = 0;
+  auto seg = [&](int32_t* p, size_t len) {
+    if (!len) return;
+    sg.push_back(TabSeg{p, (uint32_t)len, total});
+    total += (uint32_t)len;
+  };
+  if (I.red_pc0 < I.npc) {
+    const size_t c0 = I.red_pc0, nc = I.npc - c0;
+    if (I.NU) seg(I.pc_dom.p + c0 * I.NU, nc * I.NU);
+    seg(I.pc_tot.p + c0 * KSG_MAX_TOPO, nc * KSG_MAX_TOPO);
+  }
+  if (I.red_tc0 < I.ntc) {
+    seg(I.tc_tot.p + I.red_tc0, I.ntc - I.red_tc0);
+    for (uint32_t u = I.red_tc0; u < I.ntc; ++u) {
+      const int32_t sl = I.tc_slot_h[u];
+      if (!((I.uniq >> sl) & 1u)) seg(I.tc_val.p + I.tc_off_h[u], I.topo.topo_count[sl]);
+    }
+  }
+  I.red_pc0 = I.red_tc0 = UINT32_MAX;
+  if (!total) return true;
+  hipStream_t s = I.stream;
+  if (!I.segs_d.upload(sg, s, err)) return false;
+  const size_t bytes = (size_t)total * 4;
+  if (!I.xsend.grow(bytes, 0, s, err) || !I.xrecv.grow(bytes * I.xranks, 0, s, err)) return false;
+  const uint32_t nseg = (uint32_t)sg.size(), nb = std::min<uint32_t>(nseg, 1024);
+  hipLaunchKernelGGL(k_seg_pack, dim3(nb), dim3(256), 0, s, I.segs_d.p, nseg, reinterpret_cast<int32_t*>(I.xsend.p));
+  if (!xgather(I, bytes, err)) return false;
+  hipLaunchKernelGGL(k_seg_sum, dim3(nb), dim3(256), 0, s, I.segs_d.p, nseg, reinterpret_cast<const int32_t*>(I.xrecv.p),
+                     total, I.xranks);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));  // (segment list uploaded from a host vector)
+  return true;
+}
+// Before anything reads or changes the class tables of a sharded context.
+static bool tables_ready(Engine::Impl& I, std::string& err) {
+  if (I.shards <= 1 || (I.red_pc0 == UINT32_MAX && I.red_tc0 == UINT32_MAX)) return true;
+  if (I.xranks != I.shards) { err = "sharded context: call ksg_set_exchange before scheduling"; return false; }
+  return reduce_tables(I, err);
+}
+
 bool Engine::add_classes(const ClassUpload& u, std::string& err) {
   Impl& I = *p_;
   hipStream_t s = I.stream;
@@ -5122,6 +5242,7 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
       return false;
     I.tc_used += add;
     I.tc_off_h.insert(I.tc_off_h.end(), off.begin(), off.end());
+    I.tc_slot_h.insert(I.tc_slot_h.end(), u.tc_slot.begin(), u.tc_slot.end());
     I.ntc += ntc;
   }
   DevCluster C = I.cluster();
@@ -5129,6 +5250,9 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
     hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, pc0, npc);
   if (ntc && I.tcap) hipLaunchKernelGGL(k_tc_build, dim3((I.tcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, tc0);
   HIPCHK(hipGetLastError());
+  if (npc) I.red_pc0 = std::min(I.red_pc0, pc0);
+  if (ntc) I.red_tc0 = std::min(I.red_tc0, tc0);
+  if (!reduce_tables(I, err)) return false;
   HIPCHK(hipStreamSynchronize(s));
   return true;
 }
@@ -5152,7 +5276,9 @@ bool Engine::rebuild_class_tables(std::string& err) {
     hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, 0u, I.npc);
   if (I.ntc && I.tcap) hipLaunchKernelGGL(k_tc_build, dim3((I.tcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, 0u);
   HIPCHK(hipGetLastError());
-  return true;
+  if (I.npc) I.red_pc0 = 0;
+  if (I.ntc) I.red_tc0 = 0;
+  return reduce_tables(I, err);
 }
 
 bool Engine::replace_program(uint32_t q, const std::vector<uint8_t>& prog, std::string& err) {
@@ -5256,6 +5382,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
 bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string& err) {
   Impl& I = *p_;
   if (first + count > I.prog_off.size()) { err = "program index out of range"; return false; }
+  if (!tables_ready(I, err)) return false;
   if (commit && batch_path()) return run_batches(I, first, count, err);
   hipStream_t s = I.stream;
   DevCluster C = I.cluster();
@@ -5342,10 +5469,17 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   CA.arrive = I.carrive.p;
   CA.stamps = I.cstamps_on ? I.cstamps.p : nullptr;
   CA.etot = nullptr;
-  if (I.cnblk > I.fold_blocks) {  // fold k_eval's partials once (k_fold) above this many blocks
+  CA.xsend = nullptr;
+  if (I.cnblk > I.fold_blocks || xchain) {  // fold k_eval's partials once (k_fold, or the X2 merge) above this many blocks
     if (!I.cetot.alloc(1, err)) return false;
     CA.etot = I.cetot.p;
   }
+  if (xchain) {  // node-sharded table chain: the X2 / X3 / X4 records
+    const size_t xb = (size_t)kX2 * sizeof(int64_t);
+    if (!I.xsend.grow(xb, 0, s, err) || !I.xrecv.grow(xb * I.xranks, 0, s, err)) return false;
+  }
+  int64_t* const xs = reinterpret_cast<int64_t*>(I.xsend.p);
+  const int64_t* const xrv = reinterpret_cast<const int64_t*>(I.xrecv.p);
   const int rowm = I.R > 4 ? 0 : (I.eval_mode == 1 ? 2 : 1);
   bool pending = false;           // logged assumes whose existing-pod table rows are not written yet
   // rows of the logged pods [log_base, j); the log restarts at `next` (a pod of the
@@ -5357,9 +5491,11 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   };
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
-    if (!xchain && (I.prog_need[j] & 4)) {
+    if (I.prog_need[j] & 4) {
+      I.path_pods[0]++;
       CA.q = j;
       CA.prog = prog;
+      CA.xsend = xchain ? xs : nullptr;
       const bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
       if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
       const bool occ = I.cnblk > (I.occ_blocks ? I.occ_blocks : 2 * I.n_cus) || I.occ_force;  // many blocks per CU
@@ -5375,15 +5511,33 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         I.n_samples++;
       }
       if (F.has_ext) {  // (k_final's last block selects; without ScoreExtensions k_eval's)
-        if (CA.etot) hipLaunchKernelGGL(k_fold, dim3(1), dim3(kChain), 0, s, C, F, CA, prog);
-        if (I.prog_need[j] & 8) hipLaunchKernelGGL(k_ptsraw, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+        if (xchain) {  // X2: the cycle's counts and normalisers over every rank
+          hipLaunchKernelGGL(k_tx2_pack, dim3(1), dim3(kChain), 0, s, C, F, CA, prog, xs);
+          if (!xgather(I, (size_t)kX2 * sizeof(int64_t), err)) return false;
+          hipLaunchKernelGGL(k_tx2_merge, dim3(1), dim3(64), 0, s, C, CA, prog, xrv, xr);
+        } else if (CA.etot) {
+          hipLaunchKernelGGL(k_fold, dim3(1), dim3(kChain), 0, s, C, F, CA, prog);
+        }
+        if (I.prog_need[j] & 8) {
+          hipLaunchKernelGGL(k_ptsraw, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+          if (xchain) {  // X3
+            hipLaunchKernelGGL(k_tx3_pack, dim3(1), dim3(kChain), 0, s, CA, xs);
+            if (!xgather(I, 2 * sizeof(int64_t), err)) return false;
+            hipLaunchKernelGGL(k_tx3_merge, dim3(1), dim3(kChain), 0, s, CA, xrv, xr);
+          }
+        }
         if (occ) hipLaunchKernelGGL(k_final_occ, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
         else hipLaunchKernelGGL(k_final, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+      }
+      if (xchain) {  // X4: selectHost over the ranks, the assume split by ownership
+        if (!xgather(I, 3 * sizeof(int64_t), err)) return false;
+        hipLaunchKernelGGL(k_tx4_select, dim3(1), dim3(64), 0, s, C, F, CA, prog, xrv, xr);
       }
       pending |= (CA.mode & 2) != 0;
       continue;
     }
     flush(j, j + 1);  // the scanning chain reads the existing-pod table
+    I.path_pods[1]++;
     const int mode = commit ? (1 | ((I.has_pts || I.has_ipa) ? 2 : 0)) : 0;
     DevOut O{I.filter.p, I.score.p, I.total.p, I.sums.p + j, xchain ? nullptr : I.arrive1.p, mode, I.prow.p + j};
     bool kept = I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n;
@@ -5557,10 +5711,14 @@ bool Engine::set_exchange(int mode, const void* nccl_id, uint32_t rank, uint32_t
     err = "exchange: unknown mode";
     return false;
   }
-  return true;
+  return tables_ready(I, err);  // class tables built before the exchange existed
 }
 
 uint32_t Engine::exchange_ranks() const { return p_->xranks; }
+void Engine::path_counts(uint64_t out[2]) const {
+  out[0] = p_->path_pods[0];
+  out[1] = p_->path_pods[1];
+}
 
 bool Engine::nccl_unique_id(void* out128, std::string& err) {
   ncclUniqueId id;

@@ -1107,7 +1107,6 @@ struct Cluster {
   // per block), score keys whose registered values fit a 64-bit mask or sit one
   // per node.  Every other pod runs the scanning chain (k_scan_pods ...).
   bool table_path(const ksg_prog& h) {
-    if (shards != 1) return false;
     if (pos_of(P_PTS) < 0) return true;
     const bool na_restrict = (h.flags & (KPF_HAS_NODE_SEL | KPF_HAS_REQ_NA)) != 0;
     const int nf = h.n_tsc_filter, ns = h.n_tsc_score;
@@ -1565,7 +1564,10 @@ struct Cluster {
     }
     S.topo_pairs = pairs;
     // class tables: pair index space of the keys whose values span nodes, the
-    // values present on this shard's nodes, and every node's topology keys
+    // values present on some node of the cluster, and every node's topology keys
+    // and values (the whole cluster: a sharded context's class tables are global,
+    // every rank applies the same pair-level deltas, SURVEY §8(e) "Bind delta")
+    S.shards = shards;
     S.nu_base.assign(topo.names.size(), 0xFFFFFFFFu);
     S.slot_dom.assign(topo.names.size(), 0);
     S.pair_node.assign(pairs, 0);
@@ -1575,22 +1577,27 @@ struct Cluster {
         S.nu_base[t] = S.nu_pairs;
         S.nu_pairs += S.topo_count[t];
       }
-    node_slots.assign(n, 0);
+    S.gtopo.assign(topo.names.size() * (size_t)G, -1);
+    node_slots.assign(G, 0);
     slot_nodes.assign(topo.names.size(), 0);
     keyset_nodes.clear();
-    for (uint32_t i = 0; i < n; ++i)
-      for (size_t t = 0; t < topo.names.size(); ++t) {
-        const int32_t k = S.topo_key[t];
-        if (k < 0) continue;
-        const int32_t v = S.label_vid[(size_t)k * n + i];
+    for (size_t t = 0; t < topo.names.size(); ++t) {
+      const int32_t k = S.topo_key[t];
+      if (k < 0) continue;
+      for (uint32_t g = 0; g < G; ++g) {
+        auto it = nodes[g].labels.find(topo.names[t]);
+        if (it == nodes[g].labels.end()) continue;
+        const int32_t v = nvals[k].get(it->second);
         if (v < 0) continue;
-        node_slots[i] |= 1u << t;
+        S.gtopo[t * (size_t)G + g] = v;
+        node_slots[g] |= 1u << t;
         slot_nodes[t]++;
         if (!S.pair_node[S.topo_base[t] + v]) {
           S.pair_node[S.topo_base[t] + v] = 1;
           S.slot_dom[t]++;
         }
       }
+    }
     enc_topo_count = S.topo_count;
     enc_topo_unique = S.topo_unique;
     enc_nu_base = S.nu_base;
@@ -1605,6 +1612,14 @@ struct Cluster {
     vector<i64> rq;
     vector<vector<int32_t>> lab;
     bound_row.assign(bound.size(), -1);
+    if (tables_on())  // term classes in the order of the whole cluster's bound pods: the same ids on every rank
+      for (auto& p : bound)
+        if (node_names.get(p.node) >= 0) {
+          for (auto& t : p.req_aff) tclass(0, t);
+          for (auto& t : p.req_anti) tclass(1, t);
+          for (auto& t : p.pref_aff) tclass(2, t);
+          for (auto& t : p.pref_anti) tclass(3, t);
+        }
     for (size_t bi = 0; bi < bound.size(); ++bi) {
       const Pod& p = bound[bi];
       int32_t g = node_names.get(p.node);
@@ -2501,7 +2516,7 @@ struct Cluster {
         h.tab |= KTAB_PTS_MULTI;
       if ((h.tab & KTAB_ON) && !lookup_plan(h, P)) h.tab = 0;  // more lookups than the plan holds
     } else {
-      h.tab = shards == 1 ? KTAB_ON : 0;  // profiles without PTS / IPA: the chain needs no tables
+      h.tab = KTAB_ON;  // profiles without PTS / IPA: the chain needs no tables
     }
     m.flags = h.flags;
     // ---- lay out the blob
@@ -4129,6 +4144,13 @@ extern "C" int ksg_debug_eval_stamps(ksg_ctx* ctx, int on, uint64_t* out, size_t
   if (!ctx->c.eng->eval_stamps(on != 0, out ? &v : nullptr, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
   if (out) std::copy(v.begin(), v.end(), out);
   if (n) *n = v.size();
+  return KSG_OK;
+}
+
+// diagnostic (not in ksg.h): pods run through the table chain / the scanning chain so far
+extern "C" int ksg_debug_path_counts(ksg_ctx* ctx, uint64_t* out2) {
+  if (!ctx || !out2) return KSG_E_INVALID;
+  ctx->c.eng->path_counts(out2);
   return KSG_OK;
 }
 

@@ -60,6 +60,8 @@ struct ChainArgs {
   uint32_t* arrive;        // block arrivals of the cycle's last kernel (its last block selects)
   uint64_t* stamps;        // diagnostic (Engine::eval_stamps): block 0's s_memrealtime deltas, or null
   EvalTotals* etot;        // k_eval's partials folded once by k_fold (large clusters), or null: every block folds
+  int64_t* xsend;          // node-sharded: the cycle's last block leaves its local (key, feasible, status) here
+                           // for the X4 exchange instead of selecting (k_tx4_select selects), or null
 };
 
 // Diagnostic stamps: block 0 / thread 0 of each chain kernel adds (now - entry)
@@ -278,6 +280,15 @@ __device__ __forceinline__ void chain_last_select(DevCluster& C, const DevProfil
   CS(24);
   rec_block(r, lds, 0u, 0, RB_CNT | RB_ST | RB_KEY);
   CS(25);
+  if (A.xsend) {  // node-sharded: this rank's part of selectHost goes to the X4 exchange
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(A.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      A.xsend[0] = (int64_t)r.key;
+      A.xsend[1] = r.feas;
+      A.xsend[2] = r.st;
+    }
+    return;
+  }
   const bool error = (r.st & 2) || ((r.st & 4) && r.feas > 1) || (h->flags & KPF_PREFILTER_ERROR) ||
                      na_prescore_error(h->flags, r.feas);
   int32_t node = -1;
@@ -609,6 +620,22 @@ struct EvalTotals {
   ChainRec r;
   double w[KSG_MAX_TSC];
 };
+// topologyNormalizingWeight per score constraint from the folded record.
+__device__ __forceinline__ void eval_weights(const DevCluster& C, const ksg_prog* h, EvalTotals& E) {
+  const ChainRec& r = E.r;
+  const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c) {  // scoring.go initPreScoreState topoSize
+    E.w[c] = 0;
+    if (c >= ns) continue;
+    const ksg_tsc& t = h->tsc[nf + c];
+    int64_t size = 0;  // hostname: filtered - ignored nodes; else the key's registered values
+    if (t.is_hostname) size = (int64_t)r.feas - r.ign;
+    else if (t.first_of_key)  // a key with one node per value registers one value per counted node
+      size = ((C.T.uniq >> t.topo) & 1u) ? (int64_t)r.feas - r.ign : (int64_t)__popcll(r.reg[c]);
+    E.w[c] = go_log((double)(size + 2));
+  }
+}
 __device__ __forceinline__ void reduce_eval(const DevCluster& C, const DevProfile& F, const ChainArgs& A, const ksg_prog* h,
                                             EvalTotals& E, ChainRec* lds) {
   const uint32_t NB = A.nblk;
@@ -636,18 +663,7 @@ __device__ __forceinline__ void reduce_eval(const DevCluster& C, const DevProfil
       if (c < ns) r.reg[c] |= A.pr[(size_t)c * NB + b];
   }
   rec_block(r, lds, xmask, ns, RB_CNT | RB_ST);
-  const int nf = h->n_tsc_filter;
-#pragma unroll
-  for (int c = 0; c < KSG_MAX_TSC; ++c) {  // scoring.go initPreScoreState topoSize
-    E.w[c] = 0;
-    if (c >= ns) continue;
-    const ksg_tsc& t = h->tsc[nf + c];
-    int64_t size = 0;  // hostname: filtered - ignored nodes; else the key's registered values
-    if (t.is_hostname) size = (int64_t)r.feas - r.ign;
-    else if (t.first_of_key)  // a key with one node per value registers one value per counted node
-      size = ((C.T.uniq >> t.topo) & 1u) ? (int64_t)r.feas - r.ign : (int64_t)__popcll(r.reg[c]);
-    E.w[c] = go_log((double)(size + 2));
-  }
+  eval_weights(C, h, E);
 }
 
 // PodTopologySpread raw score of a counted node (scoring.go Score): the constraints'
@@ -687,6 +703,116 @@ __device__ __forceinline__ void eval_totals(const DevCluster& C, const DevProfil
                                             EvalTotals& E, ChainRec* lds) {
   if (A.etot) E = *A.etot;
   else reduce_eval(C, F, A, h, E, lds);
+}
+
+// ---- node-sharded table chain: every rank keeps the global
+// class tables (pair-level deltas applied by all ranks), so k_eval is rank-local
+// and a cycle needs two exchange points (three with several PodTopologySpread
+// score constraints):
+//   X2 after k_eval: feasible / ignored (SUM), status (OR), normalisers' max /
+//      min (MAX / MIN), PodTopologySpread score registrations (OR) — then the
+//      normalising weights, identical on every rank;
+//   X3 after k_ptsraw: PodTopologySpread raw max / min;
+//   X4 after NormalizeScore: argmax key (unsigned MAX), feasible (SUM), status
+//      (OR) — selectHost, and the assume: the owner applies the node row and
+//      node-level tables, every rank the pair-level ones.
+constexpr int kX2 = 3 + 2 * KCP_X + KSG_MAX_TSC;  // int64 words
+__global__ __launch_bounds__(kChain) void k_tx2_pack(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog,
+                                                     int64_t* out) {
+  __shared__ ChainRec lds[kChain / 64];
+  EvalTotals E;
+  reduce_eval(C, F, A, view(prog).h, E, lds);
+  if (threadIdx.x == 0) {
+    out[0] = E.r.feas;
+    out[1] = E.r.ign;
+    out[2] = E.r.st;
+#pragma unroll
+    for (int x = 0; x < KCP_X; ++x) {
+      out[3 + x] = E.r.mx[x];
+      out[3 + KCP_X + x] = E.r.mn[x];
+    }
+#pragma unroll
+    for (int c = 0; c < KSG_MAX_TSC; ++c) out[3 + 2 * KCP_X + c] = (int64_t)E.r.reg[c];
+  }
+}
+__global__ void k_tx2_merge(DevCluster C, ChainArgs A, const uint8_t* __restrict__ prog, const int64_t* recv, uint32_t ranks) {
+  if (threadIdx.x != 0) return;
+  EvalTotals E;
+  rec_init(E.r);
+  for (uint32_t k = 0; k < ranks; ++k) {
+    const int64_t* v = recv + (size_t)k * kX2;
+    E.r.feas += (int32_t)v[0];
+    E.r.ign += (int32_t)v[1];
+    E.r.st |= (int32_t)v[2];
+#pragma unroll
+    for (int x = 0; x < KCP_X; ++x) {
+      E.r.mx[x] = v[3 + x] > E.r.mx[x] ? v[3 + x] : E.r.mx[x];
+      E.r.mn[x] = v[3 + KCP_X + x] < E.r.mn[x] ? v[3 + KCP_X + x] : E.r.mn[x];
+    }
+#pragma unroll
+    for (int c = 0; c < KSG_MAX_TSC; ++c) E.r.reg[c] |= (uint64_t)v[3 + 2 * KCP_X + c];
+  }
+  eval_weights(C, view(prog).h, E);
+  *A.etot = E;
+}
+__global__ __launch_bounds__(kChain) void k_tx3_pack(ChainArgs A, int64_t* out) {
+  __shared__ ChainRec lds[kChain / 64];
+  ChainRec r;
+  rec_init(r);
+  for (uint32_t b = threadIdx.x; b < A.nblk; b += blockDim.x) {
+    r.mx[KCX_PTS] = A.pm2[b] > r.mx[KCX_PTS] ? A.pm2[b] : r.mx[KCX_PTS];
+    r.mn[KCX_PTS] = A.pm2[A.nblk + b] < r.mn[KCX_PTS] ? A.pm2[A.nblk + b] : r.mn[KCX_PTS];
+  }
+  rec_block(r, lds, 1u << KCX_PTS, 0, 0u);
+  if (threadIdx.x == 0) {
+    out[0] = r.mx[KCX_PTS];
+    out[1] = r.mn[KCX_PTS];
+  }
+}
+// the merged PodTopologySpread raw max / min as block 0's partial (the others neutral)
+__global__ void k_tx3_merge(ChainArgs A, const int64_t* recv, uint32_t ranks) {
+  int64_t mx = INT64_MIN, mn = INT64_MAX;
+  for (uint32_t k = 0; k < ranks; ++k) {
+    mx = recv[2 * k] > mx ? recv[2 * k] : mx;
+    mn = recv[2 * k + 1] < mn ? recv[2 * k + 1] : mn;
+  }
+  for (uint32_t b = threadIdx.x; b < A.nblk; b += blockDim.x) {
+    A.pm2[b] = b == 0 ? mx : INT64_MIN;
+    A.pm2[A.nblk + b] = b == 0 ? mn : INT64_MAX;
+  }
+}
+// X4: selectHost over the ranks' (key, feasible, status), the summary, and the
+// assume (chain_last_select's, split by ownership).  One wave.
+__global__ __launch_bounds__(64) void k_tx4_select(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog,
+                                                   const int64_t* recv, uint32_t ranks) {
+  const uint32_t q = A.q;
+  const ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  uint64_t key = 0;
+  int32_t feas = 0, st = 0;
+  for (uint32_t k = 0; k < ranks; ++k) {
+    const uint64_t x = (uint64_t)recv[3 * k];
+    key = x > key ? x : key;
+    feas += (int32_t)recv[3 * k + 1];
+    st |= (int32_t)recv[3 * k + 2];
+  }
+  const bool error = (st & 2) || ((st & 4) && feas > 1) || (h->flags & KPF_PREFILTER_ERROR) || na_prescore_error(h->flags, feas);
+  const uint32_t g = (uint32_t)(key & 0xFFFFFull);
+  const bool place = !error && feas > 0 && (A.mode & 1);
+  const bool mine = place && g >= C.goff && g - C.goff < C.N;
+  if (threadIdx.x == 0) {
+    ksg_pod_summary* S = A.sums + q;
+    S->feasible = feas;
+    S->best_key = key;
+    if (error) { S->status = 2; S->selected = -1; }
+    else if (feas == 0) { S->status = 1; S->selected = -1; }
+    else { S->status = 0; S->selected = (int32_t)g; }
+    A.prow[q] = -1;
+    A.alog[q - A.log_base] = make_int2((int)q, mine && (A.mode & 2) ? (int)(g - C.goff) : -1);
+    if (mine) assume_row_atomic(C, V, g - C.goff, +1);
+  }
+  if (mine) tables_assume(C, V, g - C.goff, +1, threadIdx.x, blockDim.x);
+  else if (place) tables_assume_remote(C, V, g, +1, threadIdx.x, blockDim.x);
 }
 
 struct FinalShared {
@@ -951,6 +1077,30 @@ __global__ void k_tc_build(DevCluster C, uint32_t u0) {
   const ksg_exist_term& e = C.terms[t];
   if (e.cls < 0 || (uint32_t)e.cls < u0) return;
   tc_add(C, e, (uint32_t)C.ptnode[p], +1);
+}
+
+// ---- node-sharded class tables: the pair-level entries a rank built from its
+// own existing pods are summed across ranks (segments of int32 entries packed
+// in one canonical order, all-gathered, summed in place).
+struct TabSeg {
+  int32_t* p;
+  uint32_t len, off;  // entries, offset in the packed vector
+};
+__global__ void k_seg_pack(const TabSeg* sg, uint32_t nseg, int32_t* out) {
+  for (uint32_t k = blockIdx.x; k < nseg; k += gridDim.x) {
+    const TabSeg s = sg[k];
+    for (uint32_t i = threadIdx.x; i < s.len; i += blockDim.x) out[s.off + i] = s.p[i];
+  }
+}
+__global__ void k_seg_sum(const TabSeg* sg, uint32_t nseg, const int32_t* recv, uint32_t total, uint32_t ranks) {
+  for (uint32_t k = blockIdx.x; k < nseg; k += gridDim.x) {
+    const TabSeg s = sg[k];
+    for (uint32_t i = threadIdx.x; i < s.len; i += blockDim.x) {
+      int32_t v = 0;
+      for (uint32_t r = 0; r < ranks; ++r) v += recv[(size_t)r * total + s.off + i];
+      s.p[i] = v;
+    }
+  }
 }
 
 // Normalized scores of a kept pod (finalscore-result / ksg_normalized_scores):

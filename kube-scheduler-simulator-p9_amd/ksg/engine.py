@@ -88,6 +88,7 @@ def load_library():
     L.ksg_filter_status.argtypes = [vp, u32, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_prescore_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_normalized_scores.argtypes = [vp, u32, u32, ctypes.POINTER(i64), u32]
+    L.ksg_debug_path_counts.argtypes = [vp, ctypes.c_void_p]
     L.ksg_queue_pod.argtypes = [vp, u32, cp, sz, ctypes.POINTER(sz)]
     L.ksg_gated_pods.argtypes = [vp, cp, sz, ctypes.POINTER(sz)]
     L.ksg_synth_cluster.argtypes = [ctypes.c_int, i64, i64, i64, i64, ctypes.c_uint64, ctypes.POINTER(vp),
@@ -237,6 +238,12 @@ class Scheduler:
         self._xfn = make_host_exchange(world)  # keep alive
         self._chk(self.L.ksg_set_exchange(self.h, 2, None, ctypes.cast(self._xfn, ctypes.c_void_p), None),
                   "ksg_set_exchange")
+
+    def path_counts(self):
+        """Diagnostic: (pods through the table chain, pods through the scanning chain) so far."""
+        out = (ctypes.c_uint64 * 2)()
+        self._chk(self.L.ksg_debug_path_counts(self.h, out), "ksg_debug_path_counts")
+        return out[0], out[1]
 
     def set_path(self, per_pod: bool):
         self._chk(self.L.ksg_set_path(self.h, 1 if per_pod else 0), "ksg_set_path")

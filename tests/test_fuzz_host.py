@@ -38,7 +38,12 @@ def _binary():
     os.makedirs(BUILD, exist_ok=True)
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
            "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "include"), "-o", exe] + SRCS
-    subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    if p.returncode != 0:
+        # a missing toolchain / sanitizer runtime skips; a source that no longer compiles or links fails
+        if "error:" in p.stderr or "undefined reference" in p.stderr:
+            raise AssertionError("sanitizer build of host.cpp failed:\n" + p.stderr[-4000:])
+        raise OSError(p.stderr[-2000:])
     return exe
 
 

@@ -20,9 +20,14 @@
  * Objects cross the boundary as Kubernetes JSON (what json.Marshal of a *v1.Pod /
  * *v1.Node produces); the library interns them into the device SoA snapshot.
  * Conventions: every function returns 0 on success and a negative KSG_E* code on
- * failure (message in ksg_last_error); no exceptions or aborts cross the ABI;
- * output buffers are caller-owned; one context per scheduler profile and GPU;
- * calls on one context must be serialised by the caller.
+ * failure (message in ksg_last_error: the calling thread's last failure on that
+ * context); no exceptions or aborts cross the ABI; output buffers are
+ * caller-owned; one context per scheduler profile and GPU.
+ * Threads: every call that takes a context holds that context's lock for its
+ * duration, so calls from several threads (goroutines) are safe and serialised;
+ * the per-node lookups of the framework's parallel workers should read a
+ * ksg_cycle_view (no call at all) instead of ksg_filter_status & co. per node.
+ * ksg_destroy must not race with other calls on the same context.
  */
 #ifndef KSG_H_
 #define KSG_H_
@@ -148,8 +153,12 @@ int ksg_batch_path(const ksg_ctx* ctx);  /* 1 when the batch path is active */
  * pods every rank all-gathers its per-pod top-64 candidates (with their node
  * rows) and local feasible counts, merges them, and runs the same deterministic
  * replay, applying only its own nodes' assume deltas.  Other profiles: the
- * per-pod chain with four exchanges per cycle (domain histograms, feasible
- * count and normalisers, PodTopologySpread normaliser, argmax key).  What-if
+ * table chain on every rank's nodes against global class tables (each rank sums
+ * its pair-level counts with the others' when a class is built and applies every
+ * assume's pair-level delta), two exchanges per cycle (counts and normalisers;
+ * argmax key), three with several PodTopologySpread score constraints; pods
+ * whose spread constraints the tables cannot answer run the scanning chain
+ * (four exchanges).  Needs ksg_set_exchange before the first run.  What-if
  * steps: per-pod summaries merged after each pass.
  *   mode 1: RCCL all-gather on the context stream; nccl_id = 128 bytes from
  *           ksg_nccl_unique_id() on one rank, broadcast by the caller.
@@ -176,9 +185,10 @@ int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len
  * is ksg_queue_len() - 1), its per-node outputs kept for ksg_filter_codes /
  * ksg_scores / ksg_annotations.  commit != 0 also assumes it on the engine's
  * selectHost choice (harness mode); commit == 0 leaves the assume to
- * ksg_reserve with the framework's own choice (plugin mode).  A pod bringing
- * labels, namespaces, topology keys or scalar resources the snapshot has not
- * seen triggers a re-encode of the snapshot (placements kept). */
+ * ksg_reserve with the framework's own choice (plugin mode).  New label keys,
+ * label values and namespaces are interned in place; a pod bringing a topology
+ * key, a scalar resource or a host port the snapshot has not seen triggers a
+ * re-encode of the snapshot (placements kept). */
 int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_pod_result* out);
 /* ReservePlugin.Reserve (wrappedplugin.go:631 -> scheduler cache assume):
  * assume queue pod q (run with commit == 0) on global node `node`. */
@@ -243,6 +253,40 @@ int ksg_normalized_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int64_t* out, 
  * contexts with DefaultPreemption in the profile; queue runs stop after each
  * pod that may preempt (ksg_schedule_queue then returns with them done). */
 int ksg_postfilter_result(ksg_ctx* ctx, uint32_t q, int32_t* nominated, char* buf, size_t cap, size_t* len);
+
+/* ---- per-node results of one cycle for concurrent readers.  The framework
+ * calls Filter (wrappedplugin.go:523-548) and Score (:420-445) from its 16
+ * parallelize.Until workers and NormalizeScore (:388-415) per plugin; a Go
+ * plugin acquires the cycle's view once (the cycle's first PreFilter, after
+ * ksg_cycle; kept in CycleState) and its per-node calls index these immutable
+ * arrays — no library call, no lock.  Arrays are [pos * n_nodes + i] for
+ * profile position pos and local node i (global index node_offset + i).
+ * Codes are framework.Code values (as ksg_filter_status): -1 = not called.
+ * A view stays valid, unchanged, until ksg_cycle_view_release, whatever the
+ * context does meanwhile (later cycles, Reserve, events); release needs no
+ * context and may run on any thread. */
+typedef struct ksg_cycle_view {
+  uint32_t q;                     /* queue pod */
+  uint32_t n_positions;           /* profile positions */
+  uint32_t node_offset;           /* global index of local node 0 */
+  uint32_t n_nodes;               /* local nodes */
+  ksg_pod_result result;          /* the cycle's outcome (engine selectHost) */
+  const int8_t* filter_code;      /* Filter: Success / Unschedulable / UnschedulableAndUnresolvable / -1 */
+  const uint16_t* filter_msg;     /* Status.Message() of the Filter: index into messages (0: "") */
+  const int64_t* score;           /* Score: raw score (0 where not scored) */
+  const int64_t* normalized;      /* NormalizeScore output (raw for plugins without ScoreExtensions) */
+  const int8_t* prefilter_code;   /* [pos] PreFilter code (ksg_prefilter_status) */
+  const uint16_t* prefilter_msg;  /* [pos] its message index */
+  const int8_t* prescore_code;    /* [pos] PreScore code (ksg_prescore_status) */
+  const uint16_t* prescore_msg;   /* [pos] its message index */
+  const char* const* messages;    /* message table; messages[0] == "" */
+  uint32_t n_messages;
+  const void* owner;              /* library-private */
+} ksg_cycle_view;
+/* Snapshot the kept outputs of queue pod q (the pod of the last ksg_cycle, or a
+ * ksg_keep_outputs range) into a view. */
+int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out);
+void ksg_cycle_view_release(const ksg_cycle_view* view);
 
 /* Scheduler-cache events between cycles (replaces the informer -> Cache path:
  * Cache.AddNode/UpdateNode/RemoveNode/AddPod/UpdatePod/RemovePod of upstream

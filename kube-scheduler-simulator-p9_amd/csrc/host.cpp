@@ -17,6 +17,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <string>
 #include <unordered_map>
@@ -3900,14 +3901,27 @@ struct Cluster {
 // ================================================================== C ABI
 using ksg::host::Cluster;
 
+// Every entry point that takes a context holds its (recursive) mutex for the
+// call, so calls from several threads are serialised by the library; the
+// per-node reads of the framework's parallel Filter / Score workers go through
+// a ksg_cycle_view instead (no call, no lock).  last_error is also kept per
+// thread: ksg_last_error returns the calling thread's last failure on ctx.
+static thread_local const void* t_err_ctx = nullptr;
+static thread_local std::string t_err;
 struct ksg_ctx {
   Cluster c;
   std::string last_error;
+  mutable std::recursive_mutex mu;
   int fail(const std::string& m, int code) {
     last_error = m;
+    t_err_ctx = this;
+    t_err = m;
     return code;
   }
 };
+#define KSG_LOCK(ctx)                                 \
+  std::unique_lock<std::recursive_mutex> ksg_lk_;    \
+  if (ctx) ksg_lk_ = std::unique_lock<std::recursive_mutex>((ctx)->mu)
 
 // A context whose device state a failed in-place update left half-applied
 // refuses every call but ksg_load_cluster / ksg_destroy / ksg_last_error.
@@ -3948,9 +3962,15 @@ int ksg_create(const char* profile_json, size_t len, const ksg_opts* opts, ksg_c
 
 void ksg_destroy(ksg_ctx* ctx) { delete ctx; }
 
-const char* ksg_last_error(const ksg_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+const char* ksg_last_error(const ksg_ctx* ctx) {
+  if (!ctx) return "null context";
+  if (t_err_ctx == ctx) return t_err.c_str();
+  KSG_LOCK(ctx);
+  return ctx->last_error.c_str();
+}
 
 int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len) {
+  KSG_LOCK(ctx);
   if (!ctx || !json) return KSG_E_INVALID;
   ctx->c.out_gen++;
   try {
@@ -3963,10 +3983,17 @@ int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len) {
   return KSG_OK;
 }
 
-int ksg_num_nodes(const ksg_ctx* ctx) { return ctx ? (int)ctx->c.nodes.size() : KSG_E_INVALID; }
-int ksg_queue_len(const ksg_ctx* ctx) { return ctx ? (int)ctx->c.queue.size() : KSG_E_INVALID; }
+int ksg_num_nodes(const ksg_ctx* ctx) {
+  KSG_LOCK(ctx);
+  return ctx ? (int)ctx->c.nodes.size() : KSG_E_INVALID;
+}
+int ksg_queue_len(const ksg_ctx* ctx) {
+  KSG_LOCK(ctx);
+  return ctx ? (int)ctx->c.queue.size() : KSG_E_INVALID;
+}
 
 int ksg_keep_outputs(ksg_ctx* ctx, uint32_t first, uint32_t count) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
   if (!ctx->c.eng->keep_outputs(first, count, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
@@ -3974,6 +4001,7 @@ int ksg_keep_outputs(ksg_ctx* ctx, uint32_t first, uint32_t count) {
 }
 
 int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
   Cluster& c = ctx->c;
@@ -4010,6 +4038,7 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
 }
 
 int ksg_compact(ksg_ctx* ctx, uint32_t keep_from) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
   if (!ctx->c.compact(keep_from)) return ctx->fail(ctx->c.err, KSG_E_STATE);
@@ -4017,6 +4046,7 @@ int ksg_compact(ksg_ctx* ctx, uint32_t keep_from) {
 }
 
 int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
   Cluster& c = ctx->c;
@@ -4036,6 +4066,7 @@ int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count) {
 }
 
 int ksg_wait(ksg_ctx* ctx, float* ms) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   if (!ctx->c.eng->sync(ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
   if (ms) *ms = ctx->c.eng->last_ms();
@@ -4051,6 +4082,7 @@ int ksg_wait(ksg_ctx* ctx, float* ms) {
 }
 
 int ksg_pod_results(ksg_ctx* ctx, uint32_t first, uint32_t count, ksg_pod_result* out) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   if (!ctx || !out) return KSG_E_INVALID;
   Cluster& c = ctx->c;
@@ -4069,6 +4101,7 @@ int ksg_pod_results(ksg_ctx* ctx, uint32_t first, uint32_t count, ksg_pod_result
 }
 
 int ksg_filter_codes(ksg_ctx* ctx, uint32_t q, uint32_t* out, uint32_t n) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   if (!ctx || !out) return KSG_E_INVALID;
   ksg::PodOutputs o;
@@ -4082,6 +4115,7 @@ int ksg_filter_codes(ksg_ctx* ctx, uint32_t q, uint32_t* out, uint32_t n) {
 }
 
 int ksg_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* out, uint32_t n) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   if (!ctx || !out) return KSG_E_INVALID;
   ksg::PodOutputs o;
@@ -4095,6 +4129,7 @@ int ksg_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* out, uint32_t n)
 }
 
 int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   if (!ctx || !len) return KSG_E_INVALID;
   std::string s;
@@ -4107,6 +4142,7 @@ int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len
 }
 
 int ksg_reset(ksg_ctx* ctx) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
   if (ctx->c.inplace_dirty)
@@ -4118,12 +4154,14 @@ int ksg_reset(ksg_ctx* ctx) {
 }
 
 int ksg_sample_kernel(ksg_ctx* ctx, uint32_t every) {
+  KSG_LOCK(ctx);
   if (!ctx) return KSG_E_INVALID;
   ctx->c.eng->sample_kernel(every);
   return KSG_OK;
 }
 
 int ksg_set_path(ksg_ctx* ctx, int per_pod) {
+  KSG_LOCK(ctx);
   if (!ctx) return KSG_E_INVALID;
   ctx->c.eng->set_path(per_pod);
   return KSG_OK;
@@ -4131,6 +4169,7 @@ int ksg_set_path(ksg_ctx* ctx, int per_pod) {
 
 // diagnostic (not in ksg.h): fixup-loop s_memtime stamps, 8 per pod
 extern "C" int ksg_debug_fixup_stamps(ksg_ctx* ctx, uint32_t count, uint64_t* out) {
+  KSG_LOCK(ctx);
   if (!ctx) return KSG_E_INVALID;
   std::vector<uint64_t> v;
   if (!ctx->c.eng->fixup_stamps(count, out ? &v : nullptr, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
@@ -4139,6 +4178,7 @@ extern "C" int ksg_debug_fixup_stamps(ksg_ctx* ctx, uint32_t count, uint64_t* ou
 }
 
 extern "C" int ksg_debug_eval_stamps(ksg_ctx* ctx, int on, uint64_t* out, size_t* n) {
+  KSG_LOCK(ctx);
   if (!ctx) return KSG_E_INVALID;
   std::vector<uint64_t> v;
   if (!ctx->c.eng->eval_stamps(on != 0, out ? &v : nullptr, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
@@ -4149,6 +4189,7 @@ extern "C" int ksg_debug_eval_stamps(ksg_ctx* ctx, int on, uint64_t* out, size_t
 
 // diagnostic (not in ksg.h): pods run through the table chain / the scanning chain so far
 extern "C" int ksg_debug_path_counts(ksg_ctx* ctx, uint64_t* out2) {
+  KSG_LOCK(ctx);
   if (!ctx || !out2) return KSG_E_INVALID;
   ctx->c.eng->path_counts(out2);
   return KSG_OK;
@@ -4161,21 +4202,27 @@ int ksg_nccl_unique_id(uint8_t* out128) {
 }
 
 int ksg_set_exchange(ksg_ctx* ctx, int mode, const uint8_t* nccl_id, ksg_exchange_fn fn, void* user) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (!c.eng->set_exchange(mode, nccl_id, c.rank, c.shards, fn, user, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
   return KSG_OK;
 }
 
-int ksg_batch_path(const ksg_ctx* ctx) { return ctx ? (ctx->c.eng->batch_path() ? 1 : 0) : KSG_E_INVALID; }
+int ksg_batch_path(const ksg_ctx* ctx) {
+  KSG_LOCK(ctx);
+  return ctx ? (ctx->c.eng->batch_path() ? 1 : 0) : KSG_E_INVALID;
+}
 
 int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples) {
+  KSG_LOCK(ctx);
   if (!ctx || !avg_ms || !samples) return KSG_E_INVALID;
   if (!ctx->c.eng->kernel_time(*avg_ms, *samples, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
   return KSG_OK;
 }
 
 int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_pod_result* out) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
   if (!ctx || !pod_json) return KSG_E_INVALID;
@@ -4197,12 +4244,14 @@ int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_po
 }
 
 int ksg_reserve(ksg_ctx* ctx, uint32_t q, int32_t node) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   if (!ctx->c.reserve(q, node)) return ctx->fail(ctx->c.err, KSG_E_STATE);
   return KSG_OK;
 }
 
 int ksg_unreserve(ksg_ctx* ctx, uint32_t q) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
   if (!ctx->c.unreserve(q)) return ctx->fail(ctx->c.err, KSG_E_STATE);
@@ -4210,6 +4259,7 @@ int ksg_unreserve(ksg_ctx* ctx, uint32_t q) {
 }
 
 int ksg_apply_events(ksg_ctx* ctx, const char* events_json, size_t len) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
   if (!ctx || !events_json) return KSG_E_INVALID;
@@ -4222,6 +4272,7 @@ int ksg_apply_events(ksg_ctx* ctx, const char* events_json, size_t len) {
 }
 
 int ksg_node_requested(ksg_ctx* ctx, int64_t* requested, int32_t* pod_count, uint32_t n_res, uint32_t n) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   std::vector<int64_t> r;
   std::vector<int32_t> pc;
@@ -4245,12 +4296,14 @@ static int put_str(ksg_ctx* ctx, const std::string& s, char* buf, size_t cap, si
 }
 
 int ksg_queue_pod(const ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len) {
+  KSG_LOCK(ctx);
   if (!ctx) return KSG_E_INVALID;
   if (q >= ctx->c.queue.size()) return KSG_E_RANGE;
   return put_str(nullptr, ctx->c.queue[q].ns + "/" + ctx->c.queue[q].name, buf, cap, len);
 }
 
 int ksg_gated_pods(const ksg_ctx* ctx, char* buf, size_t cap, size_t* len) {
+  KSG_LOCK(ctx);
   if (!ctx) return KSG_E_INVALID;
   std::string s;
   for (auto& p : ctx->c.gated) s += p.ns + "/" + p.name + "\n";
@@ -4258,6 +4311,7 @@ int ksg_gated_pods(const ksg_ctx* ctx, char* buf, size_t cap, size_t* len) {
 }
 
 int ksg_plugin_position(const ksg_ctx* ctx, const char* name, size_t len) {
+  KSG_LOCK(ctx);
   if (!ctx || !name) return KSG_E_INVALID;
   const std::string nm = ksg::host::unwrapped(std::string(name, len));
   for (int i = 0; i < ctx->c.n_plugins; ++i)
@@ -4266,6 +4320,7 @@ int ksg_plugin_position(const ksg_ctx* ctx, const char* name, size_t len) {
 }
 
 int ksg_plugin_weights(const ksg_ctx* ctx, uint32_t pos, int64_t* weight, int64_t* store_weight) {
+  KSG_LOCK(ctx);
   if (!ctx) return KSG_E_INVALID;
   if ((int)pos >= ctx->c.n_plugins) return KSG_E_RANGE;
   if (weight) *weight = ctx->c.fw_w[pos];
@@ -4274,12 +4329,14 @@ int ksg_plugin_weights(const ksg_ctx* ctx, uint32_t pos, int64_t* weight, int64_
 }
 
 int ksg_node_index(const ksg_ctx* ctx, const char* name, size_t len) {
+  KSG_LOCK(ctx);
   if (!ctx || !name) return KSG_E_INVALID;
   const int32_t g = ctx->c.node_names.get(std::string(name, len));
   return g < 0 ? KSG_E_RANGE : g;
 }
 
 int ksg_prefilter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code, char* msg, size_t cap, size_t* len) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (!code || q >= c.meta.size() || (int)pos >= c.n_plugins) return ctx->fail("prefilter_status: range", KSG_E_RANGE);
@@ -4291,6 +4348,7 @@ int ksg_prefilter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code, 
 }
 
 int ksg_prefilter_result(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (q >= c.meta.size()) return ctx->fail("prefilter_result: range", KSG_E_RANGE);
@@ -4307,6 +4365,7 @@ int ksg_prefilter_result(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t
 }
 
 int ksg_prefilter_result_pos(ksg_ctx* ctx, uint32_t q, uint32_t pos, char* buf, size_t cap, size_t* len) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (q >= c.meta.size() || (int)pos >= c.n_plugins) return ctx->fail("prefilter_result_pos: range", KSG_E_RANGE);
@@ -4327,6 +4386,7 @@ int ksg_prefilter_result_pos(ksg_ctx* ctx, uint32_t q, uint32_t pos, char* buf, 
 }
 
 int ksg_postfilter_result(ksg_ctx* ctx, uint32_t q, int32_t* nominated, char* buf, size_t cap, size_t* len) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (!nominated || q >= c.queue.size()) return ctx->fail("postfilter_result: range", KSG_E_RANGE);
@@ -4341,6 +4401,7 @@ int ksg_postfilter_result(ksg_ctx* ctx, uint32_t q, int32_t* nominated, char* bu
 
 int ksg_filter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, uint32_t node, int32_t* code, char* msg, size_t cap,
                       size_t* len) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (!code || q >= c.meta.size() || (int)pos >= c.n_plugins) return ctx->fail("filter_status: range", KSG_E_RANGE);
@@ -4353,6 +4414,7 @@ int ksg_filter_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, uint32_t node, int
 }
 
 int ksg_prescore_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code, char* msg, size_t cap, size_t* len) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (!code || q >= c.meta.size() || (int)pos >= c.n_plugins) return ctx->fail("prescore_status: range", KSG_E_RANGE);
@@ -4364,6 +4426,7 @@ int ksg_prescore_status(ksg_ctx* ctx, uint32_t q, uint32_t pos, int32_t* code, c
 }
 
 int ksg_normalized_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int64_t* out, uint32_t n) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   Cluster& c = ctx->c;
   if (!out || q >= c.meta.size()) return ctx->fail("normalized_scores: range", KSG_E_RANGE);
@@ -4377,7 +4440,105 @@ int ksg_normalized_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int64_t* out, 
   return KSG_OK;
 }
 
+// ---- ksg_cycle_view: one cycle's per-node results as immutable arrays (the
+// Filter / Score / NormalizeScore calls of the framework's parallel workers read
+// them without calling into the library)
+namespace {
+struct CycleView {
+  ksg_cycle_view pub;  // (first member: the pointer handed out)
+  std::vector<int8_t> fcode, pfcode, pscode;
+  std::vector<uint16_t> fmsg, pfmsg, psmsg;
+  std::vector<int64_t> score, norm;
+  std::vector<std::string> msgs;
+  std::vector<const char*> mptr;
+  std::unordered_map<std::string, uint16_t> mid;
+  uint16_t intern(const std::string& m) {
+    if (m.empty()) return 0;
+    auto it = mid.find(m);
+    if (it != mid.end()) return it->second;
+    if (msgs.size() >= 0xFFFF) return 0;  // (never: a cycle has a few dozen distinct messages)
+    const uint16_t k = (uint16_t)msgs.size();
+    msgs.push_back(m);
+    mid.emplace(m, k);
+    return k;
+  }
+};
+}  // namespace
+
+int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out) {
+  KSG_LOCK(ctx);
+  KSG_GUARD(ctx);
+  Cluster& c = ctx->c;
+  if (!out) return KSG_E_INVALID;
+  *out = nullptr;
+  if (q >= c.meta.size()) return ctx->fail("cycle_view: range", KSG_E_RANGE);
+  const ksg::PodOutputs* o = c.outputs_of(q);
+  if (!o) return ctx->fail(c.err, KSG_E_STATE);
+  const std::vector<int32_t>* nm = c.normalized_of(q);
+  if (!nm) return ctx->fail(c.err, KSG_E_STATE);
+  o = c.outputs_of(q);
+  std::unique_ptr<CycleView> v(new CycleView());
+  const uint32_t P = (uint32_t)c.n_plugins, N = c.hi - c.lo;
+  v->msgs.push_back("");
+  v->fcode.assign((size_t)P * N, -1);
+  v->fmsg.assign((size_t)P * N, 0);
+  v->score.assign((size_t)P * N, 0);
+  v->norm.assign((size_t)P * N, 0);
+  v->pfcode.assign(P, -1);
+  v->pfmsg.assign(P, 0);
+  v->pscode.assign(P, -1);
+  v->psmsg.assign(P, 0);
+  std::string m;
+  for (uint32_t pos = 0; pos < P; ++pos) {
+    v->pfcode[pos] = (int8_t)c.prefilter_status(q, (int)pos, o->summary, m);
+    v->pfmsg[pos] = v->intern(m);
+    v->pscode[pos] = (int8_t)c.prescore_status(q, (int)pos, o->summary, m);
+    v->psmsg[pos] = v->intern(m);
+    for (uint32_t i = 0; i < N; ++i) {
+      const size_t k = (size_t)pos * N + i;
+      v->fcode[k] = (int8_t)c.filter_status(q, (int)pos, i, *o, m);
+      if (!m.empty()) v->fmsg[k] = v->intern(m);
+    }
+    const int d = c.dpos[pos];
+    if (d < 0) continue;
+    for (uint32_t i = 0; i < N; ++i) {
+      v->score[(size_t)pos * N + i] = o->score[(size_t)d * N + i];
+      v->norm[(size_t)pos * N + i] = (*nm)[(size_t)d * N + i];
+    }
+  }
+  for (auto& x : v->msgs) v->mptr.push_back(x.c_str());
+  ksg_cycle_view& p = v->pub;
+  p.q = q;
+  p.n_positions = P;
+  p.node_offset = c.lo;
+  p.n_nodes = N;
+  p.result.selected = o->summary.selected;
+  p.result.feasible = o->summary.feasible;
+  p.result.status = o->summary.status;
+  p.result.skip_filter = o->summary.skip_filter;
+  p.result.skip_score = o->summary.skip_score;
+  p.result.total = (int32_t)(o->summary.best_key >> 40);
+  p.filter_code = v->fcode.data();
+  p.filter_msg = v->fmsg.data();
+  p.score = v->score.data();
+  p.normalized = v->norm.data();
+  p.prefilter_code = v->pfcode.data();
+  p.prefilter_msg = v->pfmsg.data();
+  p.prescore_code = v->pscode.data();
+  p.prescore_msg = v->psmsg.data();
+  p.messages = v->mptr.data();
+  p.n_messages = (uint32_t)v->mptr.size();
+  p.owner = v.get();
+  *out = &v.release()->pub;
+  return KSG_OK;
+}
+
+void ksg_cycle_view_release(const ksg_cycle_view* v) {
+  if (v) delete static_cast<const CycleView*>(v->owner);
+}
+
 int ksg_node_nonzero(ksg_ctx* ctx, int64_t* nonzero, uint32_t n) {
+  KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   if (!nonzero) return KSG_E_INVALID;
   std::vector<int64_t> nz;

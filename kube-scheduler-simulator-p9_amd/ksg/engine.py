@@ -29,6 +29,59 @@ class _Opts(ctypes.Structure):
                 ("shard_count", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
 
 
+class _CycleView(ctypes.Structure):
+    _fields_ = [("q", ctypes.c_uint32), ("n_positions", ctypes.c_uint32), ("node_offset", ctypes.c_uint32),
+                ("n_nodes", ctypes.c_uint32), ("result", _PodResult),
+                ("filter_code", ctypes.POINTER(ctypes.c_int8)), ("filter_msg", ctypes.POINTER(ctypes.c_uint16)),
+                ("score", ctypes.POINTER(ctypes.c_int64)), ("normalized", ctypes.POINTER(ctypes.c_int64)),
+                ("prefilter_code", ctypes.POINTER(ctypes.c_int8)), ("prefilter_msg", ctypes.POINTER(ctypes.c_uint16)),
+                ("prescore_code", ctypes.POINTER(ctypes.c_int8)), ("prescore_msg", ctypes.POINTER(ctypes.c_uint16)),
+                ("messages", ctypes.POINTER(ctypes.c_char_p)), ("n_messages", ctypes.c_uint32),
+                ("owner", ctypes.c_void_p)]
+
+
+class CycleView:
+    """ksg_cycle_view: one cycle's per-node results as immutable arrays, read
+    without calling into the library (what the framework's parallel Filter / Score
+    workers do); released with release() or when garbage-collected."""
+
+    def __init__(self, L, ptr):
+        self._L, self._p = L, ptr
+        v = ptr.contents
+        self.q, self.P, self.N, self.node_offset = v.q, v.n_positions, v.n_nodes, v.node_offset
+        r = v.result
+        self.result = PodResult(r.selected, r.feasible, r.status, r.total)
+        self._v = v
+        self.messages = [v.messages[i].decode() for i in range(v.n_messages)]
+
+    def release(self):
+        if self._p:
+            self._L.ksg_cycle_view_release(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+    def filter_status(self, pos, i):
+        k = pos * self.N + i
+        return self._v.filter_code[k], self.messages[self._v.filter_msg[k]]
+
+    def prefilter_status(self, pos):
+        return self._v.prefilter_code[pos], self.messages[self._v.prefilter_msg[pos]]
+
+    def prescore_status(self, pos):
+        return self._v.prescore_code[pos], self.messages[self._v.prescore_msg[pos]]
+
+    def scores(self, pos):
+        return [self._v.score[pos * self.N + i] for i in range(self.N)]
+
+    def normalized_scores(self, pos):
+        return [self._v.normalized[pos * self.N + i] for i in range(self.N)]
+
+
 @dataclass
 class PodResult:
     selected: int
@@ -88,6 +141,9 @@ def load_library():
     L.ksg_filter_status.argtypes = [vp, u32, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_prescore_status.argtypes = [vp, u32, u32, ctypes.POINTER(i32), cp, sz, ctypes.POINTER(sz)]
     L.ksg_normalized_scores.argtypes = [vp, u32, u32, ctypes.POINTER(i64), u32]
+    L.ksg_cycle_view_acquire.argtypes = [vp, u32, ctypes.POINTER(ctypes.POINTER(_CycleView))]
+    L.ksg_cycle_view_release.argtypes = [ctypes.POINTER(_CycleView)]
+    L.ksg_cycle_view_release.restype = None
     L.ksg_debug_path_counts.argtypes = [vp, ctypes.c_void_p]
     L.ksg_queue_pod.argtypes = [vp, u32, cp, sz, ctypes.POINTER(sz)]
     L.ksg_gated_pods.argtypes = [vp, cp, sz, ctypes.POINTER(sz)]
@@ -238,6 +294,12 @@ class Scheduler:
         self._xfn = make_host_exchange(world)  # keep alive
         self._chk(self.L.ksg_set_exchange(self.h, 2, None, ctypes.cast(self._xfn, ctypes.c_void_p), None),
                   "ksg_set_exchange")
+
+    def cycle_view(self, q) -> CycleView:
+        """ksg_cycle_view_acquire: the kept outputs of queue pod q as a read-only view."""
+        p = ctypes.POINTER(_CycleView)()
+        self._chk(self.L.ksg_cycle_view_acquire(self.h, q, ctypes.byref(p)), "ksg_cycle_view_acquire")
+        return CycleView(self.L, p)
 
     def path_counts(self):
         """Diagnostic: (pods through the table chain, pods through the scanning chain) so far."""

@@ -208,9 +208,17 @@ bool Engine::summaries(uint32_t first, uint32_t count, ksg_pod_summary* out, std
 }
 bool Engine::outputs(uint32_t prog_idx, PodOutputs& out, std::string& err) {
   if (prog_idx >= p_->sums.size()) { err = "stub: outputs range"; return false; }
+  // kept pods: every other node passed, raw scores a function of (pod, node, position)
+  const bool kept = p_->keep_n && prog_idx >= p_->keep_first && prog_idx < p_->keep_first + p_->keep_n;
   out.filter.assign(p_->N, KSG_FILTER_NOT_EVALUATED);
   out.score.assign((size_t)p_->cfg.n_plugins * p_->N, 0);
   out.total.assign(p_->N, 0);
+  if (kept)
+    for (uint32_t i = 0; i < p_->N; ++i) {
+      if ((i + prog_idx) % 2 == 0) out.filter[i] = KSG_FILTER_PASS;
+      for (int d = 0; d < p_->cfg.n_plugins; ++d)
+        out.score[(size_t)d * p_->N + i] = (int32_t)((i * 7 + prog_idx * 3 + (uint32_t)d) % 101);
+    }
   out.summary = p_->sums[prog_idx];
   return true;
 }

@@ -227,3 +227,38 @@ def test_scheduler_configuration_weights(tmp_path):
     ext = g.config_profile([("NodeResourcesFit", 1)], seed=1)
     ext["profiles"][0]["plugins"]["filter"] = {"enabled": [{"name": "NodeResourcesFitWrapped"}]}
     assert _weights(tmp_path, ext) is None
+
+
+TSAN_SRCS = [os.path.join(HERE, "fuzz", "tsan_view.cpp"), os.path.join(HERE, "fuzz", "stub_engine.cpp"),
+             os.path.join(ROOT, "kube-scheduler-simulator-p9_amd", "csrc", "host.cpp"),
+             os.path.join(ROOT, "kube-scheduler-simulator-p9_amd", "csrc", "synth.cpp")]
+
+
+def test_cycle_view_threads_under_tsan(tmp_path):
+    """The boundary's thread model (include/ksg.h "Threads"): 16 threads read one
+    cycle's ksg_cycle_view (the framework's parallel Filter / Score workers), acquire
+    and release views of other pods and call ksg_filter_status / ksg_prefilter_status
+    on the same context while another thread runs new cycles — built with
+    -fsanitize=thread against the stub engine; no race report, and every view equals
+    its single-threaded digest (the shared one also after the new cycles)."""
+    exe = os.path.join(BUILD, "tsan_view")
+    deps = TSAN_SRCS + [os.path.join(ROOT, "include", "ksg.h")]
+    if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(p) for p in deps):
+        os.makedirs(BUILD, exist_ok=True)
+        cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-pthread", "-I", os.path.join(ROOT, "include"),
+               "-o", exe] + TSAN_SRCS
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        if p.returncode != 0:
+            if "error:" in p.stderr or "undefined reference" in p.stderr:
+                raise AssertionError("TSan build failed:\n" + p.stderr[-4000:])
+            pytest.skip("ThreadSanitizer runtime unavailable: " + p.stderr[-500:])
+    doc = g.generate(4, n_nodes=24, n_existing=60, n_pods=10, n_zones=3)
+    files = []
+    for name, obj in (("p.json", doc["profile"]), ("c.json", doc), ("pod.json", doc["queue"][0])):
+        f = tmp_path / name
+        f.write_text(json.dumps(obj))
+        files.append(str(f))
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    p = subprocess.run([exe] + files, capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-6000:])
+    assert "tsan ok" in p.stdout

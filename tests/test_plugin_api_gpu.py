@@ -175,3 +175,73 @@ def test_scheduler_configuration_profile():
                       for n in SCORERS if s.prescore_status(q, s.plugin_position(n))[0] == C_SUCCESS
                       or n == "ImageLocality")
             assert tot == r.total, q
+
+
+class _ViewCalls:
+    """rebuild()'s per-node calls answered from a ksg_cycle_view (no library call);
+    the once-per-cycle PreFilterResult / PostFilter calls go to the context."""
+
+    def __init__(self, s, v):
+        self.s, self.v = s, v
+
+    def prefilter_status(self, q, pos):
+        return self.v.prefilter_status(pos)
+
+    def filter_status(self, q, pos, i):
+        return self.v.filter_status(pos, i)
+
+    def prescore_status(self, q, pos):
+        return self.v.prescore_status(pos)
+
+    def scores(self, q, pos):
+        return self.v.scores(pos)
+
+    def normalized_scores(self, q, pos):
+        return self.v.normalized_scores(pos)
+
+    def prefilter_result(self, q):
+        return self.s.prefilter_result(q)
+
+    def prefilter_result_pos(self, q, pos):
+        return self.s.prefilter_result_pos(q, pos)
+
+    def postfilter_result(self, q):
+        return self.s.postfilter_result(q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
+def test_cycle_view_matches_extension_point_calls(name, c, sizes):
+    """ksg_cycle_view (include/ksg.h): the arrays the framework's 16 parallel
+    Filter / Score workers index instead of calling the library per node.  Every
+    annotation rebuilt from a view equals the oracle's; 16 threads rebuilding from
+    one view agree; a view is unchanged by the cycles that follow it."""
+    from concurrent.futures import ThreadPoolExecutor
+    doc = g.generate(c, **sizes)
+    o = Oracle(doc)
+    o.schedule(record=3)
+    s = Scheduler(doc["profile"])
+    d = dict(doc)
+    d["queue"] = []
+    s.load_cluster(d)
+    names = [n["metadata"]["name"] for n in doc["nodes"]]
+    held = []
+    for i, pod in enumerate(doc["queue"][:30]):
+        q, r = s.cycle(pod, commit=True)
+        v = s.cycle_view(q)
+        assert (v.result.selected, v.result.feasible, v.result.status) == o.result(i), (name, i)
+        for pos in range(len(doc["profile"]["plugins"])):  # the view holds what the per-node calls return
+            for k in (0, len(names) // 2, len(names) - 1):
+                assert v.filter_status(pos, k) == tuple(s.filter_status(q, pos, k)), (name, i, pos, k)
+        vc = _ViewCalls(s, v)
+        with ThreadPoolExecutor(16) as ex:
+            outs = list(ex.map(lambda _: rebuild(vc, q, doc["profile"], names, r.status), range(16)))
+        ora = o.annotations(i)
+        for got in outs:
+            for k, val in got.items():
+                assert val == ora[k], (name, i, k)
+        if i % 10 == 0:
+            held.append((i, q, v, outs[0]))
+    for i, q, v, first in held:  # views stay valid and unchanged after later cycles
+        assert rebuild(_ViewCalls(s, v), q, doc["profile"], names, v.result.status) == first, (name, i)
+        v.release()

@@ -126,7 +126,9 @@ int ksg_wait(ksg_ctx* ctx, float* device_ms);
  * pod-tile x node-tile passes, the first leaving a 4- or 8-byte record per
  * (pod, node) for the second (count x nodes x 4 B: 16 GB at 4,096 pods x 1M
  * nodes; env KSG_WHATIF_REC_MB caps it, default 40960, larger steps run in pod
- * chunks, 0 recomputes every pair in the second pass instead); others (PodTopologySpread / InterPodAffinity on
+ * chunks, 0 recomputes every pair in the second pass instead; the record
+ * buffer stays allocated across steps until the next ksg_load_cluster or
+ * ksg_compact); a what-if step runs no PostFilter (no nomination is reported for its pods); others (PodTopologySpread / InterPodAffinity on
  * frozen class tables, the default profile) run every pod's cycle without
  * assume.  Sharded contexts reduce the per-pod feasible counts, normaliser
  * max/min and argmax keys across ranks.

@@ -174,6 +174,8 @@ class Engine {
   // What-if step: pods [first, first+count) each against the current snapshot,
   // then all their placements bound (Fit/BA/Taint/NodeAffinity profiles).
   bool run_whatif(uint32_t first, uint32_t count, std::string& err);
+  // Free the what-if record buffer (kept across steps: up to KSG_WHATIF_REC_MB).
+  void release_scratch();
   bool keep_outputs(uint32_t keep_first, uint32_t keep_n, std::string& err);
   bool summaries(uint32_t first, uint32_t count, ksg_pod_summary* out, std::string& err);
   bool outputs(uint32_t prog_idx, PodOutputs& out, std::string& err);

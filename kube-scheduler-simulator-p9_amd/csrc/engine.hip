@@ -4894,6 +4894,15 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
   return true;
 }
 
+void Engine::release_scratch() {
+  Impl& I = *p_;
+  if (!I.wrec_pairs.p) return;
+  (void)hipStreamSynchronize(I.stream);
+  (void)hipFree(I.wrec_pairs.p);
+  I.wrec_pairs.p = nullptr;
+  I.wrec_pairs.n = 0;
+}
+
 // All-gather `bytes` from every rank into I.xrecv (rank order), on the engine stream.
 static bool exchange(Engine::Impl& I, const void* src, size_t bytes, std::string& err) {
   hipStream_t s = I.stream;

@@ -1229,7 +1229,7 @@ struct Cluster {
     }
     vector<uint8_t> blob;
     PodMeta m;
-    if (!compile(queue[q], (int32_t)q, blob, m)) return false;
+    if (!compile(queue[q], (int32_t)(seq_base + q), blob, m)) return false;
     if (!sync_classes()) return false;  // (no new classes: the pod's own were registered)
     if (!eng->replace_program(q, blob, err)) return false;
     progs[q] = std::move(blob);
@@ -2603,6 +2603,7 @@ struct Cluster {
       if (!volumes_modelled(p)) return false;
     if (!equal_priorities()) return false;
     if (!build_vocab() || !eng->set_score_resources(ecfg.fit_res, ecfg.ba_res, err)) return false;
+    eng->release_scratch();
     NodeSoA S;
     PodTableSoA T;
     if (!encode_snapshot(S, T)) return false;
@@ -2626,6 +2627,7 @@ struct Cluster {
     compiled = false;
     inplace_dirty = false;
     bound_at_valid = false;
+    seq_base = 0;
     progs.clear();
     meta.clear();
     qmode.clear();
@@ -2697,24 +2699,23 @@ struct Cluster {
     placed.resize(queue.size(), -1);
     assumed_in.resize(queue.size(), 0);
   }
-  // (namespace, name) -> queue index, for the events' name lookups
-  std::unordered_map<string, uint32_t> queue_idx;
+  // (namespace, name) -> every queue index holding that pod, in queue order (a
+  // pod the framework retries is cycled again under the same name), for the
+  // events' name lookups
+  std::unordered_map<string, vector<uint32_t>> queue_idx;
   static string pod_key(const string& ns, const string& name) { return ns + '\x1f' + name; }
-  bool queue_dups = false;  // some (namespace, name) is queued twice
   void index_queue() {
     queue_idx.clear();
-    queue_dups = false;
-    for (size_t q = 0; q < queue.size(); ++q) {
-      auto r = queue_idx.emplace(pod_key(queue[q].ns, queue[q].name), (uint32_t)q);
-      if (!r.second) {
-        queue_dups = true;
-        r.first->second = (uint32_t)q;
-      }
-    }
+    for (size_t q = 0; q < queue.size(); ++q) queue_idx[pod_key(queue[q].ns, queue[q].name)].push_back((uint32_t)q);
   }
+  // the latest queue index of the pod (-1 none)
   int32_t queue_find(const string& ns, const string& name) const {
     auto it = queue_idx.find(pod_key(ns, name));
-    return it == queue_idx.end() ? -1 : (int32_t)it->second;
+    return it == queue_idx.end() || it->second.empty() ? -1 : (int32_t)it->second.back();
+  }
+  const vector<uint32_t>* queue_all(const string& ns, const string& name) const {
+    auto it = queue_idx.find(pod_key(ns, name));
+    return it == queue_idx.end() ? nullptr : &it->second;
   }
   // Existing-pod table entries one assume of p appends (rows, terms, reqs, vals;
   // engine assume_pod), cached per queue pod.
@@ -2861,6 +2862,10 @@ struct Cluster {
   // the queue — those placed become bound pods of the snapshot, the JSON documents
   // of the others are released — and the rest are re-indexed from 0 (their
   // results kept); one re-encode.
+  // Queue position of queue pod 0 in the sequence of every pod this context has
+  // queued since the load: the tie-break hash (pack_key) takes seq_base + q, so a
+  // compaction does not move later pods' ties.
+  uint32_t seq_base = 0;
   bool compact(uint32_t keep_from) {
     if (shards != 1) { err = "compaction needs an unsharded context"; return false; }
     if (keep_from > queue.size()) { err = "compact: queue range"; return false; }
@@ -2898,7 +2903,13 @@ struct Cluster {
     if (!eng->keep_outputs(0, 0, err)) return false;
     oc_q = -1;
     compiled = false;
-    return rebuild(nullptr, &sum);
+    seq_base += keep_from;
+    eng->release_scratch();
+    if (!rebuild(nullptr, &sum)) {  // the host state moved on: the device would hold the old one
+      broken = true;
+      return false;
+    }
+    return true;
   }
 
   // One scheduling cycle of a new pod (appended to the queue).
@@ -2924,13 +2935,7 @@ struct Cluster {
     }
     track_queue();
     uint32_t q = (uint32_t)queue.size() - 1;
-    {
-      auto r = queue_idx.emplace(pod_key(queue[q].ns, queue[q].name), q);
-      if (!r.second) {
-        queue_dups = true;
-        r.first->second = q;
-      }
-    }
+    queue_idx[pod_key(queue[q].ns, queue[q].name)].push_back(q);
     qmode[q] = 2;
     bool in_place = !vocab_grows(queue[q]);
     if (!in_place && vocab_grows_in_place(queue[q])) {  // new label values / keys / namespaces only
@@ -2942,7 +2947,7 @@ struct Cluster {
     } else {
       vector<uint8_t> blob;
       PodMeta m;
-      if (!compile(queue[q], (int32_t)q, blob, m)) return false;
+      if (!compile(queue[q], (int32_t)(seq_base + q), blob, m)) return false;
       if (!sync_classes() || !eng->append_program(blob, err)) return false;  // classes it brought: tables built
       progs.push_back(std::move(blob));
       meta.push_back(std::move(m));
@@ -3013,7 +3018,7 @@ struct Cluster {
     return queue[q].priority > low_prio;
   }
   uint64_t tie_key(uint32_t q, uint32_t g) const {  // engine pack_key with total 0
-    uint64_t z = ecfg.seed ^ ((uint64_t)q * 0x9E3779B97F4A7C15ull) ^ (uint64_t)g;
+    uint64_t z = ecfg.seed ^ ((uint64_t)(seq_base + q) * 0x9E3779B97F4A7C15ull) ^ (uint64_t)g;
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -3440,13 +3445,10 @@ struct Cluster {
       if (at < 0) return -1;
       return qm[q] == 2 ? at : remap[at];  // summaries hold original indices until the rebuild
     };
-    auto queue_at = [&](const string& name, const string& pns) -> int32_t {
-      if (!queue_dups) {  // (namespace, name) index; with a name queued twice, the first placed one
-        const int32_t k = queue_find(pns, name);
-        return k >= 0 && qplace((size_t)k) >= 0 ? k : -1;
-      }
-      for (size_t q = 0; q < queue.size(); ++q)
-        if (queue[q].name == name && queue[q].ns == pns && qplace(q) >= 0) return (int32_t)q;
+    auto queue_at = [&](const string& name, const string& pns) -> int32_t {  // the first placed one
+      if (const vector<uint32_t>* all = queue_all(pns, name))
+        for (uint32_t q : *all)
+          if (q < queue.size() && qplace(q) >= 0) return (int32_t)q;
       return -1;
     };
     for (auto& e : ev->items) {
@@ -3534,7 +3536,7 @@ struct Cluster {
     progs.assign(queue.size(), {});
     meta.assign(queue.size(), PodMeta());
     for (size_t q = 0; q < queue.size(); ++q)
-      if (!compile(queue[q], (int32_t)q, progs[q], meta[q])) return false;
+      if (!compile(queue[q], (int32_t)(seq_base + q), progs[q], meta[q])) return false;
     prog_cls.assign(queue.size(), {(uint32_t)pcls.size(), (uint32_t)tcls.size()});
     if (!eng->set_programs(progs, err) || !sync_classes()) return false;
     compiled = true;
@@ -4060,6 +4062,8 @@ int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count) {
     for (uint32_t q = first; q < first + count; ++q) c.queue_need(q, need);
     if (!c.ensure_room(need)) return ctx->fail(c.err, KSG_E_DEVICE);
   }
+  if (c.nom.size() < c.queue.size()) c.nom.resize(c.queue.size());
+  for (uint32_t q = first; q < first + count; ++q) c.nom[q] = Cluster::Nomination();  // a what-if step runs no PostFilter
   if (!c.eng->run_whatif(first, count, c.err)) return ctx->fail(c.err, KSG_E_STATE);
   c.mark_run(first, count);
   return KSG_OK;

@@ -196,6 +196,7 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool, std::string& err) {
   return true;
 }
 bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) { return run_queue(first, count, false, err); }
+void Engine::release_scratch() {}
 bool Engine::keep_outputs(uint32_t keep_first, uint32_t keep_n, std::string&) {
   p_->keep_first = keep_first;
   p_->keep_n = keep_n;

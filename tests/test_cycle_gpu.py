@@ -151,9 +151,9 @@ def test_cycle_table_grows_in_place():
 def test_compact_bounds_the_queue(name, c, sizes, keep):
     """ksg_compact (plugin mode's memory bound): after K cycles, all but the last
     `keep` pods leave the queue (placed ones become bound pods); the kept pods keep
-    their results, and later cycles equal the oracle on the equivalent cluster
-    (every placement bound, the kept pods' queue slots held by pods that fit nowhere)."""
-    from test_events_gpu import _nowhere
+    their results, and every later cycle equals the oracle's run of the whole
+    queue without any compaction (the tie-break hash keeps each pod's position in
+    the sequence of queued pods: ADVICE r02)."""
     doc = g.generate(c, **sizes)
     pods = doc["queue"]
     k = len(pods) // 2
@@ -165,20 +165,46 @@ def test_compact_bounds_the_queue(name, c, sizes, keep):
     assert s.queue_len == keep
     assert [(r.selected, r.feasible, r.status) for r in s.results()] == \
         [(r.selected, r.feasible, r.status) for r in first[k - keep:]]
-    eq = copy.deepcopy(doc)
-    for p, r in zip(pods[:k], first):
-        if r.status == 0:
-            b = copy.deepcopy(p)
-            b["spec"]["nodeName"] = names[r.selected]
-            eq["pods"].append(b)
-    eq["queue"] = [_nowhere(i) for i in range(keep)] + pods[k:]
-    o = Oracle(eq)
+    o = Oracle(doc)
     o.schedule(record=3)
+    assert [(r.selected, r.feasible, r.status) for r in first] == [o.result(i) for i in range(k)]
     for j, p in enumerate(pods[k:]):
         q, r = s.cycle(p, commit=True)
         assert q == keep + j
-        assert (r.selected, r.feasible, r.status) == o.result(keep + j), (name, j)
+        assert (r.selected, r.feasible, r.status) == o.result(k + j), (name, j)
         if j % 5 == 0:
-            assert s.annotations(q) == o.annotations(keep + j), (name, j)
+            assert s.annotations(q) == o.annotations(k + j), (name, j)
     s.compact()
     assert s.queue_len == 0
+
+
+@pytest.mark.gpu
+def test_retried_pod_then_events():
+    """kube-scheduler retries an unschedulable pod by running a new cycle for the same
+    (namespace, name).  After the retry places it, a removePod event releases that
+    placement (the first placed cycle of the name), and events keep using the name
+    index (a duplicate name no longer switches lookups to a scan)."""
+    doc = g.generate(2, n_nodes=40, n_pods=30)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(_empty_queue(doc))
+    for pod in doc["queue"][:10]:
+        s.cycle(pod, commit=True)
+    big = copy.deepcopy(doc["queue"][10])
+    big["metadata"]["name"] = "retry-me"
+    big["spec"]["containers"][0]["resources"] = {"requests": {"cpu": "200", "memory": "1Gi"}}
+    q1, r1 = s.cycle(big, commit=True)
+    assert r1.status == 1 and r1.selected < 0  # 200 cores fit nowhere
+    before = s.node_requested(3)
+    node = g.node_obj("node-huge", 512000, 2048 * g.Gi)
+    s.apply_events([{"op": "addNode", "node": node}])
+    q2, r2 = s.cycle(big, commit=True)  # the retry
+    assert q2 == q1 + 1 and r2.status == 0
+    assert r2.selected == s.node_index("node-huge")
+    s.apply_events([{"op": "removePod", "name": "retry-me", "namespace": big["metadata"].get("namespace", "default")}])
+    after = s.node_requested(3)
+    n = len(before[1])
+    assert [row[:n] for row in after[0]] == before[0] and after[1][:n] == before[1]
+    assert after[1][n] == 0 and all(row[n] == 0 for row in after[0])  # released from the new node
+    for pod in doc["queue"][11:20]:  # later cycles still run
+        _, r = s.cycle(pod, commit=True)
+        assert r.status in (0, 1)

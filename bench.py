@@ -190,10 +190,43 @@ def sample_dominant(s, every):
     return ms, n
 
 
+def dropin_latency(s, doc, n=100):
+    """The drop-in path a Go plugin takes per pod, after the
+    timed region: ksg_cycle (PreFilter..NormalizeScore on the device, commit=0),
+    ksg_cycle_view_acquire (the per-node results the framework's 16 workers then
+    index without calls), ksg_reserve on the engine's choice, view release.
+    Wall time per call, averaged over n pods (copies of the queue's first pods)."""
+    pods = doc["queue"][:n]
+    t_cycle = t_view = t_res = 0.0
+    done = 0
+    for i, p in enumerate(pods):
+        p = json.loads(json.dumps(p))
+        p["metadata"]["name"] = f"dropin-{i:05d}"
+        t0 = time.perf_counter()
+        q, r = s.cycle(p, commit=False)
+        t1 = time.perf_counter()
+        v = s.cycle_view(q)
+        t2 = time.perf_counter()
+        if r.selected >= 0:
+            s.reserve(q, r.selected)
+        t3 = time.perf_counter()
+        v.release()
+        t_cycle += t1 - t0
+        t_view += t2 - t1
+        t_res += t3 - t2
+        done += 1
+    k = 1e6 / max(done, 1)
+    return {"pods": done, "cycle_us": t_cycle * k, "view_us": t_view * k, "reserve_us": t_res * k,
+            "total_us": (t_cycle + t_view + t_res) * k,
+            "note": "host wall per drop-in cycle (ksg_cycle commit=0 + ksg_cycle_view + ksg_reserve), after the "
+                    "queue's timed steps on the same context"}
+
+
 # cfg3 / cfg4 (BASELINE.json configs[2], configs[3]) at their full single-GPU size,
 # reported beside the cfg2 headline.  Algorithmic bytes: SURVEY.md §8(d), DESIGN.md.
 CFG3_PAIR_BYTES = 141      # 120 read + 21 written per (pod, node) pair
-CFG4_EVAL_NODE_BYTES = 68  # k_eval: node row 56 + zone id 4 + selector-class count 8; no per-pair writes
+CFG4_EVAL_NODE_BYTES = 68 + 20  # k_eval: reads node row 56 + zone id 4 + selector-class count 8, writes the
+                                # per-pair filter code 4 + the four raw scores 16 (k_final re-reads them)
 
 
 def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
@@ -226,6 +259,8 @@ def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(f"cfg{c}:{kname}"),
                         "kernel": kname, "kernel_avg_us": kms * 1e3, "kernel_samples": kn, "bytes_per_launch": bpl},
            "generate_s": round(gen_s, 1)}
+    if c == 4:
+        out["dropin"] = dropin_latency(s, doc)
     del s
     if cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(blob, n_nodes, cpu_workers, cpu_seconds, f"cfg{c}")
@@ -258,6 +293,7 @@ def main():
     elapsed = time_queue(s, torch, a.steps, a.warmup, dist)
     kernel_ms, kcount = sample_dominant(s, 64)
     res = s.results()
+    dropin = dropin_latency(s, doc) if world == 1 else None
     scheduled = sum(1 for r in res if r.status == 0)
     pairs = float(n_nodes) * n_pods * a.steps  # n_nodes already spans all ranks
     value = pairs / elapsed
@@ -293,6 +329,8 @@ def main():
                      "kernel": kname, "kernel_avg_us": kernel_ms * 1e3, "kernel_samples": kcount,
                      "bytes_per_launch": bytes_per_launch},
     }
+    if dropin:
+        out["dropin"] = dropin
     if a.cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(json.dumps(doc).encode(), n_nodes, a.cpu_workers, a.cpu_seconds, "cfg2")
     if world == 1 and a.extra:

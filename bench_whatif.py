@@ -40,6 +40,18 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def pmc_step_traffic(kernels):
+    """HBM bytes of one step from the newest committed PMC pass holding every one of
+    `kernels` (profiles/*cfg5_pmc_traffic.json: FETCH_SIZE x 2 per the gfx950
+    correction + WRITE_SIZE, per dispatch), summed; None when none is committed."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*cfg5_pmc_traffic.json")), reverse=True):
+        ks = json.load(open(f)).get("kernels", {})
+        if all(k in ks for k in kernels):
+            return sum(ks[k]["hbm_bytes_per_dispatch"] for k in kernels)
+    return None
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -61,7 +73,7 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
     (bench.py reports cfg5 through this at N=1)."""
     from ksg import Scheduler, generator as g
     t0 = time.time()
-    n_pods = a.step_pods * (a.warmup + a.steps)
+    n_pods = a.step_pods * (a.warmup + a.steps + 1)  # (+1: one untimed step with kernel sampling)
     if a.variant == "pts-ipa":
         blob = g.generate_native(4, n_nodes=a.nodes, n_pods=n_pods, n_existing=a.existing, n_zones=20)
     else:
@@ -83,13 +95,11 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    s.sample_kernel(1 if a.variant == "cfg5" else 64)  # (pts-ipa: one k_eval in 64 pods)
+    s.sample_kernel(0)  # no events inside the timed steps
     t0 = time.perf_counter()
-    pass_ms = [0.0, 0.0]
     for k in range(a.warmup, a.warmup + a.steps):
-        s.whatif(k * P, P)
-        ms, n = s.kernel_time()  # average of the two sampled passes of this step
-        pass_ms[0] += ms
+        s.whatif(k * P, P, wait=False)
+        s.wait()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -99,30 +109,36 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     res = s.results(a.warmup * P, a.steps * P)
+    # one more (untimed) step with HIP events on the engine stream around the passes
+    s.sample_kernel(1 if a.variant == "cfg5" else 64)  # (pts-ipa: one k_eval in 64 pods)
+    s.whatif((a.warmup + a.steps) * P, P)
+    avg_ms, nsamp = s.kernel_time()  # cfg5: the average of the step's two passes
+    s.sample_kernel(0)
     del s
     if rank != 0:
         return None
     pairs = float(a.nodes) * P * a.steps
     shard = a.nodes // world
-    # algorithmic bytes, averaged over the two pass launches: pass 1 reads the node
-    # row columns once per 32-pod tile (alloc/requested/nonzero cpu+mem 48 B,
-    # pods+allowed 8 B, taint CSR 8 B, ~4 label columns read by the pod's
-    # requirements 16 B = 80 B x shard x ceil(P/32)) and writes a 4-byte record per
-    # pair (cfg5's field widths fit 30 bits); pass 2 reads the records (4 B x shard x P)
-    tiles = (P + 31) // 32
-    bytes_per_launch = (80.0 * shard * tiles + 8.0 * shard * P) / 2
-    kernel = "k_whatif_rec1 / k_whatif_rec2 (pass avg)"
-    note = ("pass 1 (k_whatif_rec1) issue- and L1-latency-bound: per 64-node wave and pod ~333 VALU + ~525 SALU "
-            "instructions, 45 % of wave time waiting (profiles/r02g_cfg5_pmc_sq.csv); pass 2 streams pass 1's "
-            "4-byte per-pair records")
+    # algorithmic bytes per step, SURVEY.md §8(d) basis: cfg5 ~7 B per (pod, node)
+    # pair (the node row amortised over a 64-pod tile ~2 B + filter 1 B + total 4 B);
+    # the kernel time is one step's two passes (k_whatif_rec1 + k_whatif_rec2).
+    # Pass 1's 4-byte per-pair record, written and read back by pass 2, is not
+    # algorithmic: it shows up in roofline.traffic (the PMC pass of both kernels).
+    bytes_per_launch = 7.0 * shard * P
+    kernel_ms = 2 * avg_ms
+    kernel = "k_whatif_rec1 + k_whatif_rec2 (one step)"
+    traffic = pmc_step_traffic(["cfg5:k_whatif_rec1", "cfg5:k_whatif_rec2"])
+    note = ("pass 1 (k_whatif_rec1) program decode per (pod, node tile): SALU issue, "
+            "profiles/*cfg5_pmc_sq.csv; traffic = both passes' HBM bytes (PMC) incl. the record round trip")
     workload = f"cfg5: {a.nodes} nodes, {P} pods/step, TaintToleration+NodeAffinity+Fit+BA"
     if a.variant == "pts-ipa":  # table chain: k_eval reads 68 B per node (row 56, zone id 4, class count 8)
-        bytes_per_launch = 68.0 * shard
+        bytes_per_launch = 88.0 * shard  # + the per-pair filter code and four raw scores it writes
+        kernel_ms = avg_ms
+        traffic = None
         kernel = "k_eval (table chain, sampled pods)"
         note = "per-pod table chain over frozen class tables; sequence of dependent memory round trips per pod"
         workload = (f"cfg5+PTS/IPA: {a.nodes} nodes (cfg4 distribution, {a.existing} existing pods, 20 zones), "
                     f"{P} pods/step, Fit+PodTopologySpread+InterPodAffinity+BA on frozen domain tables")
-    kernel_ms = pass_ms[0] / a.steps
     out = {
         "metric": "what-if filter+score pod x node pairs/sec (1M nodes, 4,096 pods/step)"
                   + (", PTS/IPA" if a.variant == "pts-ipa" else ""),
@@ -135,7 +151,8 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
         "scheduled_per_step": sum(1 for r in res if r.status == 0) / a.steps,
         "roofline": {"bound": "hbm", "achieved": bytes_per_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms else 0.0,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": kernel,
-                     "kernel_avg_ms": kernel_ms, "bytes_per_launch": bytes_per_launch, "note": note},
+                     "kernel_avg_ms": kernel_ms, "kernel_samples": nsamp, "bytes_per_launch": bytes_per_launch,
+                     "traffic": traffic, "note": note},
     }
     out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS
     if a.cpu_pods and world == 1:  # the oracle's what-if step on a bounded sample of the same cluster

@@ -195,8 +195,9 @@ class Engine {
   bool set_exchange(int mode, const void* nccl_id, uint32_t rank, uint32_t ranks, ExchangeFn fn, void* user,
                     std::string& err);
   uint32_t exchange_ranks() const;
-  // diagnostic: pods the per-pod runs sent down the table chain / the scanning chain
-  void path_counts(uint64_t out[2]) const;
+  // diagnostic: pods the per-pod runs sent down the table chain / the scanning chain /
+  // of the table-chain pods, those whose cycle was one launch (k_eval_solo)
+  void path_counts(uint64_t out[3]) const;
   static bool nccl_unique_id(void* out128, std::string& err);
   // diagnostic: enable (out == nullptr, count pods) / read back s_memtime stamps of the fixup loop
   bool fixup_stamps(uint32_t count, std::vector<uint64_t>* out, std::string& err);

@@ -1952,6 +1952,8 @@ __device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) { __hip_atomic_s
 __device__ __forceinline__ void st_sc1(int32_t* p, int32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void st_sc1(uint64_t* p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_sc1(int64_t* p, int64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ int64_t ld_sc1(const int64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ int32_t ld_sc1(const int32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
@@ -4063,6 +4065,8 @@ struct Engine::Impl {
   DBuf<int32_t> cpi, cpst;
   DBuf<int64_t> cpm, cpm2;
   DBuf<EvalTotals> cetot;
+  DBuf<SoloCand> ccand;   // k_eval_solo: classes per block [cnblk][kChain]
+  int solo = -1;          // one-launch cycles: -1 auto (up to 2 blocks per CU), 0 off, 1 forced (KSG_SOLO)
   uint32_t fold_blocks = 256;  // table chain: k_fold above this many blocks (KSG_FOLD_BLOCKS; tests force it)
   uint32_t occ_blocks = 0;     // table chain: occupancy twins above this many blocks (0: 2 per CU; KSG_OCC_BLOCKS)
   bool occ_force = false;
@@ -4117,7 +4121,7 @@ struct Engine::Impl {
   uint32_t sample_every = 0;
   std::vector<hipEvent_t> sev;
   uint32_t n_samples = 0;
-  uint64_t path_pods[2] = {0, 0};  // diagnostic: pods run by the table chain / the scanning chain
+  uint64_t path_pods[3] = {0, 0, 0};  // diagnostic: pods run by the table chain / the scanning chain / of the first, in one launch
   std::vector<Engine::KernelStat> stats;
 
   DevCluster cluster() const {
@@ -4185,6 +4189,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   Impl& I = *p_;
   I.cfg = cfg;
   if (const char* e = std::getenv("KSG_FOLD_BLOCKS")) I.fold_blocks = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_SOLO")) I.solo = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_OCC_BLOCKS")) {
     I.occ_blocks = (uint32_t)std::strtoul(e, nullptr, 10);
     I.occ_force = I.occ_blocks == 0;
@@ -4361,7 +4366,8 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     if (!I.carrive.alloc(1, err) || !I.cpi.alloc((size_t)KCP_I * I.cnblk, err) ||
         !I.cpst.alloc(I.cnblk, err) ||
         !I.cpm.alloc((size_t)2 * KCP_X * I.cnblk, err) || !I.cpm2.alloc((size_t)2 * I.cnblk, err) ||
-        !I.cpr.alloc((size_t)KSG_MAX_TSC * I.cnblk, err) || !I.cpk.alloc(I.cnblk, err))
+        !I.cpr.alloc((size_t)KSG_MAX_TSC * I.cnblk, err) || !I.cpk.alloc(I.cnblk, err) ||
+        !I.ccand.alloc((size_t)kChain * I.cnblk, err))
       return false;
     HIPCHK(hipMemsetAsync(I.carrive.p, 0, sizeof(uint32_t), s));
   }
@@ -5479,6 +5485,10 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   CA.stamps = I.cstamps_on ? I.cstamps.p : nullptr;
   CA.etot = nullptr;
   CA.xsend = nullptr;
+  CA.cand = I.ccand.p;
+  // one-launch cycles (k_eval_solo) for pods of normalising profiles whose outputs
+  // are not kept, unsharded, one PodTopologySpread score constraint at most
+  const bool solo_ok = !xchain && F.has_ext && (I.solo == 1 || (I.solo < 0 && I.cnblk <= 2 * I.n_cus));
   if (I.cnblk > I.fold_blocks || xchain) {  // fold k_eval's partials once (k_fold, or the X2 merge) above this many blocks
     if (!I.cetot.alloc(1, err)) return false;
     CA.etot = I.cetot.p;
@@ -5505,6 +5515,20 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
       CA.q = j;
       CA.prog = prog;
       CA.xsend = xchain ? xs : nullptr;
+      if (solo_ok && !(I.prog_need[j] & 8) && !(I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n)) {
+        const bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
+        if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
+        if (rowm == 2) hipLaunchKernelGGL(k_eval_solo<2>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+        else if (rowm == 1) hipLaunchKernelGGL(k_eval_solo<1>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+        else hipLaunchKernelGGL(k_eval_solo<0>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+        if (sampled) {
+          HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
+          I.n_samples++;
+        }
+        I.path_pods[2]++;
+        pending |= (CA.mode & 2) != 0;
+        continue;
+      }
       const bool sampled = I.sample_every && (j % I.sample_every) == 0 && I.n_samples * 2 + 2 <= I.sev.size();
       if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
       const bool occ = I.cnblk > (I.occ_blocks ? I.occ_blocks : 2 * I.n_cus) || I.occ_force;  // many blocks per CU
@@ -5724,9 +5748,10 @@ bool Engine::set_exchange(int mode, const void* nccl_id, uint32_t rank, uint32_t
 }
 
 uint32_t Engine::exchange_ranks() const { return p_->xranks; }
-void Engine::path_counts(uint64_t out[2]) const {
+void Engine::path_counts(uint64_t out[3]) const {
   out[0] = p_->path_pods[0];
   out[1] = p_->path_pods[1];
+  out[2] = p_->path_pods[2];
 }
 
 bool Engine::nccl_unique_id(void* out128, std::string& err) {

@@ -4191,7 +4191,8 @@ extern "C" int ksg_debug_eval_stamps(ksg_ctx* ctx, int on, uint64_t* out, size_t
   return KSG_OK;
 }
 
-// diagnostic (not in ksg.h): pods run through the table chain / the scanning chain so far
+// diagnostic (not in ksg.h): pods run through the table chain / the scanning chain so far,
+// and of the first those whose cycle was one launch
 extern "C" int ksg_debug_path_counts(ksg_ctx* ctx, uint64_t* out2) {
   KSG_LOCK(ctx);
   if (!ctx || !out2) return KSG_E_INVALID;

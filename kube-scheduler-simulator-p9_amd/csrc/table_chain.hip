@@ -33,7 +33,9 @@ struct ChainVids {
   __device__ __forceinline__ int32_t operator()(int s) const { return base[s * kChain]; }
 };
 
+#define KCP_X_DECL 4
 struct EvalTotals;
+struct SoloCand;
 struct ChainArgs {
   const uint8_t* progs;
   const uint64_t* prog_off;
@@ -62,6 +64,7 @@ struct ChainArgs {
   EvalTotals* etot;        // k_eval's partials folded once by k_fold (large clusters), or null: every block folds
   int64_t* xsend;          // node-sharded: the cycle's last block leaves its local (key, feasible, status) here
                            // for the X4 exchange instead of selecting (k_tx4_select selects), or null
+  SoloCand* cand;          // [nblk][kChain] classes per block (k_eval_solo)
 };
 
 // Diagnostic stamps: block 0 / thread 0 of each chain kernel adds (now - entry)
@@ -79,7 +82,25 @@ struct ChainArgs {
     A.stamps[mine] = cs_t0;                                                                      \
   }
 
-enum { KCP_FEAS = 0, KCP_IGN = 1, KCP_STAT = 2, KCP_IPAF = 3, KCP_I = 4 };
+enum { KCP_FEAS = 0, KCP_IGN = 1, KCP_STAT = 2, KCP_IPAF = 3, KCP_CAND = 4, KCP_I = 5 };
+
+// One-launch cycle (k_eval_solo, pods of normalising profiles whose outputs are
+// not kept).  The total of a node is A + Σ_x w_x · NormalizeScore_x(raw_x), where
+// A sums the plugins without ScoreExtensions and x runs over TaintToleration,
+// NodeAffinity, PodTopologySpread and InterPodAffinity, whose normalisation
+// needs the maxima over every feasible node.  Nodes with the same raw values of
+// those plugins (a class) get the same normalised part, so the argmax of a
+// class is its node with the largest packed key of A alone (pack_key(A) + part
+// << 40 == pack_key(A + part)).  Each block keeps, per class met among its
+// nodes, that best key (an LDS table of kSoloCap classes; a block meeting more
+// dumps every feasible node as a class of its own); the last-arriving block
+// folds the partials into the normalisers and picks the argmax over the
+// classes: selectHost without a second pass over the nodes (k_final).
+constexpr int kSoloCap = 64;  // classes per block before a dump (power of two)
+struct SoloCand {
+  int32_t v[KCP_X_DECL];      // raw scores per normalised slot (KCX_*), PTS -1: ignored node
+  uint64_t key;               // pack_key(A) of the class's best node
+};
 
 // the chain kernels' arguments (DevCluster, DevProfile, ChainArgs, program) and the program header
 constexpr int kArgBytes = (int)((sizeof(DevCluster) + sizeof(DevProfile) + sizeof(ChainArgs)) / 64 * 64);
@@ -91,6 +112,7 @@ __device__ __forceinline__ void chain_warm(const uint8_t* prog) {
   warm_wait(warm);
 }  // KCP_IPAF: block 0 only
 enum { KCX_TAINT = 0, KCX_NA = 1, KCX_PTS = 2, KCX_IPA = 3, KCP_X = 4 };
+static_assert(KCP_X == KCP_X_DECL, "SoloCand slots");
 __device__ __forceinline__ int chain_x(int plugin) {
   return plugin == KP_TAINT ? KCX_TAINT : plugin == KP_NA ? KCX_NA : plugin == KP_PTS ? KCX_PTS
                                                                                       : plugin == KP_IPA ? KCX_IPA : -1;
@@ -252,6 +274,37 @@ __device__ __forceinline__ void assume_row_atomic(DevCluster& C, const ProgView&
   csi_assume(C, V, n, sign);
 }
 
+// selectHost's outcome (the argmax key over every feasible node, the feasible
+// count, status bits) → the summary and the assume delta, by the whole block
+// (the last wave writes the summary and the node row, every lane the class tables).
+__device__ __forceinline__ void chain_commit(DevCluster& C, const ChainArgs& A, const ProgView& V, uint64_t key,
+                                             int32_t feas, int32_t st, uint64_t cs_t0) {
+  const ksg_prog* h = V.h;
+  const uint32_t q = A.q;
+  const bool error = (st & 2) || ((st & 4) && feas > 1) || (h->flags & KPF_PREFILTER_ERROR) ||
+                     na_prescore_error(h->flags, feas);
+  int32_t node = -1;
+  const uint32_t g = (uint32_t)(key & 0xFFFFFull);
+  if (!error && feas > 0 && (A.mode & 1) && g >= C.goff && g - C.goff < C.N) node = (int32_t)(g - C.goff);
+  if (threadIdx.x == blockDim.x - 64) {  // (the last wave: wave 0 takes the class tables meanwhile)
+    __hip_atomic_store(A.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ksg_pod_summary* S = A.sums + q;
+    S->feasible = feas;
+    S->best_key = key;
+    if (error) { S->status = 2; S->selected = -1; }
+    else if (feas == 0) { S->status = 1; S->selected = -1; }
+    else { S->status = 0; S->selected = (int32_t)g; }
+    A.prow[q] = -1;
+    // the existing-pod table row: written after the run (k_flush_appends)
+    A.alog[q - A.log_base] = make_int2((int)q, node >= 0 && (A.mode & 2) ? node : -1);
+    if (node >= 0) assume_row_atomic(C, V, (uint32_t)node, +1);
+  }
+  CS(26);
+  if (node >= 0) tables_assume(C, V, (uint32_t)node, +1, threadIdx.x, blockDim.x);
+  CS(27);
+  if (CS_ON) atomicAdd((unsigned long long*)&A.stamps[63], 1ull);
+}
+
 // selectHost + the assume, by the last-arriving block of the cycle's last
 // kernel: the block keys / statuses were stored sc1 before each block arrived
 // (MI355X_MICROARCH.md hand-off: agent-scope stores, counter, agent-scope loads).
@@ -289,34 +342,67 @@ __device__ __forceinline__ void chain_last_select(DevCluster& C, const DevProfil
     }
     return;
   }
-  const bool error = (r.st & 2) || ((r.st & 4) && r.feas > 1) || (h->flags & KPF_PREFILTER_ERROR) ||
-                     na_prescore_error(h->flags, r.feas);
-  int32_t node = -1;
-  const uint32_t g = (uint32_t)(r.key & 0xFFFFFull);
-  if (!error && r.feas > 0 && (A.mode & 1) && g >= C.goff && g - C.goff < C.N) node = (int32_t)(g - C.goff);
-  if (threadIdx.x == blockDim.x - 64) {  // (the last wave: wave 0 takes the class tables meanwhile)
-    __hip_atomic_store(A.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ksg_pod_summary* S = A.sums + q;
-    S->feasible = r.feas;
-    S->best_key = r.key;
-    if (error) { S->status = 2; S->selected = -1; }
-    else if (r.feas == 0) { S->status = 1; S->selected = -1; }
-    else { S->status = 0; S->selected = (int32_t)g; }
-    A.prow[q] = -1;
-    // the existing-pod table row: written after the run (k_flush_appends)
-    A.alog[q - A.log_base] = make_int2((int)q, node >= 0 && (A.mode & 2) ? node : -1);
-    if (node >= 0) assume_row_atomic(C, V, (uint32_t)node, +1);
-  }
-  CS(26);
-  if (node >= 0) tables_assume(C, V, (uint32_t)node, +1, threadIdx.x, blockDim.x);
-  CS(27);
-  if (CS_ON) atomicAdd((unsigned long long*)&A.stamps[63], 1ull);
+  chain_commit(C, A, V, r.key, r.feas, r.st, cs_t0);
 }
 
 // ROWM: 0 resource columns read by the plugins (more than 4 columns), 1 the
 // node row loaded up front (RowV), 2 the same with the default Fit / BA
 // arguments compiled in.
-template <int ROWM>
+struct SoloShared {
+  uint32_t tag[kSoloCap], ready[kSoloCap];
+  int32_t v[kSoloCap][KCP_X];
+  unsigned long long best[kSoloCap];
+  uint32_t wcnt[kChain / 64];
+  uint32_t dump, count;
+};
+__device__ void solo_last_select(DevCluster& C, const DevProfile& F, const ChainArgs& A, ChainRec* lds,
+                                 const uint8_t* __restrict__ prog, uint32_t ipa_flags, uint64_t cs_t0);
+__device__ __forceinline__ uint32_t solo_hash(int32_t a, int32_t b, int32_t c, int32_t d) {
+  uint32_t h = 0x9E3779B9u;
+  h = (h ^ (uint32_t)a) * 0x85EBCA6Bu;
+  h = (h ^ (uint32_t)b) * 0xC2B2AE35u;
+  h = (h ^ (uint32_t)c) * 0x27D4EB2Fu;
+  h = (h ^ (uint32_t)d) * 0x165667B1u;
+  return (h ^ (h >> 15)) | 1u;
+}
+// One lane of a wave: class (a, b, c, d) with best key `best` into the block's
+// LDS table (claim by CAS on the tag; a wave meeting a claimed tag waits for the
+// claimer's values, then compares them).  A full table sets dump.
+__device__ __forceinline__ void solo_insert(SoloShared& S, int32_t a, int32_t b, int32_t c, int32_t d, uint64_t best) {
+  const uint32_t t = solo_hash(a, b, c, d);
+  for (int k = 0; k < kSoloCap; ++k) {
+    const int i = (int)((t + (uint32_t)k) & (kSoloCap - 1));
+    const uint32_t old = atomicCAS(&S.tag[i], 0u, t);
+    if (old == 0u) {
+      S.v[i][0] = a;
+      S.v[i][1] = b;
+      S.v[i][2] = c;
+      S.v[i][3] = d;
+      __threadfence_block();
+      atomicExch(&S.ready[i], 1u);
+      atomicMax(&S.best[i], (unsigned long long)best);
+      return;
+    }
+    if (old == t) {
+      while (__hip_atomic_load(&S.ready[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+      }
+      __threadfence_block();
+      if (S.v[i][0] == a && S.v[i][1] == b && S.v[i][2] == c && S.v[i][3] == d) {
+        atomicMax(&S.best[i], (unsigned long long)best);
+        return;
+      }
+    }
+  }
+  atomicOr(&S.dump, 1u);
+}
+__device__ __forceinline__ void st_cand(SoloCand* p, const int32_t v[KCP_X], uint64_t key) {
+  uint64_t* w = reinterpret_cast<uint64_t*>(p);
+  st_sc1(w, (uint64_t)(uint32_t)v[0] | ((uint64_t)(uint32_t)v[1] << 32));
+  st_sc1(w + 1, (uint64_t)(uint32_t)v[2] | ((uint64_t)(uint32_t)v[3] << 32));
+  st_sc1(w + 2, key);
+}
+
+template <int ROWM, bool SOLO = false>
 __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, const ChainArgs& A,
                                           const uint8_t* __restrict__ prog) {
   chain_warm(prog);
@@ -530,13 +616,15 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     }
   }
   const bool feasible = active && code == KSG_FILTER_PASS;
-  if (active) of[n] = code;
+  if (!SOLO && active) of[n] = code;
   CS(3);
   counted &= feasible;
   ChainRec rec;
   rec_init(rec);
   int64_t tot = 0;
   bool range_err = false;
+  int64_t sa = 0;                           // SOLO: A, the plugins without ScoreExtensions
+  int64_t cv[KCP_X] = {0, 0, 0, 0};         // SOLO: the node's class (raw scores per normalised slot)
   if (feasible) {
 #pragma unroll 1
     for (int pos = 0; pos < F.n; ++pos) {
@@ -558,9 +646,19 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
           break;
         default: break;
       }
-      os[(size_t)pos * C.N + n] = (int32_t)sc;
+      if (!SOLO) os[(size_t)pos * C.N + n] = (int32_t)sc;
       const int x = chain_x(p);
       if (x >= 0 && (p != KP_PTS || counted)) rec_minmax(rec, x, sc);
+      if (SOLO) {
+        if (x >= 0) {
+#pragma unroll
+          for (int i = 0; i < KCP_X; ++i)
+            if (i == x) cv[i] = sc;
+        } else {  // (no normalisation: the raw score is the score, its [0,100] check is the node's)
+          if (sc < 0 || sc > 100) range_err = true;
+          sa += sc * F.weight[pos];
+        }
+      }
       if (!F.has_ext) {
         if (sc < 0 || sc > 100) range_err = true;
         tot += sc * F.weight[pos];
@@ -586,6 +684,90 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     rec.key = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
   }
   CS(4);
+  if (SOLO) {
+    __shared__ SoloShared S;
+    if (threadIdx.x < kSoloCap) {
+      S.tag[threadIdx.x] = 0u;
+      S.ready[threadIdx.x] = 0u;
+      S.best[threadIdx.x] = 0ull;
+    }
+    if (threadIdx.x == 0) S.dump = 0u;
+    bool fits = true;
+#pragma unroll
+    for (int i = 0; i < KCP_X; ++i) fits &= cv[i] >= INT32_MIN && cv[i] <= INT32_MAX;
+    rec_block(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);  // (its barrier orders the table's reset)
+    CS(5);
+    if (feasible && !fits) atomicOr(&S.dump, 1u);
+    lds_barrier();
+    const uint64_t keya = feasible ? pack_key(sa, F.seed, h->queue_idx, C.goff + n) : 0ull;
+    const int32_t c0 = (int32_t)cv[0], c1 = (int32_t)cv[1], c2 = (int32_t)cv[2], c3 = (int32_t)cv[3];
+    const uint32_t lane = threadIdx.x & 63u;
+    if (!S.dump) {  // each wave: its classes, one leader lane per class, into the block's table
+      bool pend = feasible;
+      for (;;) {
+        const uint64_t m = __ballot(pend);
+        if (!m) break;
+        const int ld = __ffsll((unsigned long long)m) - 1;
+        const int32_t l0 = __builtin_amdgcn_readlane(c0, ld), l1 = __builtin_amdgcn_readlane(c1, ld);
+        const int32_t l2 = __builtin_amdgcn_readlane(c2, ld), l3 = __builtin_amdgcn_readlane(c3, ld);
+        const bool same = pend && c0 == l0 && c1 == l1 && c2 == l2 && c3 == l3;
+        const uint64_t best = wave_max_u64(same ? keya : (uint64_t)0);
+        pend = pend && !same;
+        if (lane == 0) solo_insert(S, l0, l1, l2, l3, best);
+      }
+    }
+    lds_barrier();
+    SoloCand* out = A.cand + (size_t)blockIdx.x * kChain;
+    if (S.dump) {  // every feasible node a class of its own, in node order
+      const uint64_t fb = __ballot(feasible);
+      if (lane == 0) S.wcnt[threadIdx.x >> 6] = (uint32_t)__popcll(fb);
+      lds_barrier();
+      uint32_t at = (uint32_t)__popcll(fb & ((1ull << lane) - 1ull)), cnt = 0;
+#pragma unroll
+      for (int w = 0; w < kChain / 64; ++w) {
+        if (w < (int)(threadIdx.x >> 6)) at += S.wcnt[w];
+        cnt += S.wcnt[w];
+      }
+      if (feasible) {
+        const int32_t cc[KCP_X] = {c0, c1, c2, c3};
+        st_cand(out + at, cc, keya);
+      }
+      if (threadIdx.x == 0) S.count = cnt;
+    } else if (threadIdx.x < 64) {  // the table's classes, compacted
+      const bool has = S.tag[lane] != 0u;
+      const uint64_t hb = __ballot(has);
+      if (has) st_cand(out + __popcll(hb & ((1ull << lane) - 1ull)), S.v[lane], S.best[lane]);
+      if (lane == 0) S.count = (uint32_t)__popcll(hb);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      const uint32_t b = blockIdx.x, NB = A.nblk;
+      st_sc1(A.pi + KCP_FEAS * NB + b, rec.feas);
+      st_sc1(A.pi + KCP_IGN * NB + b, rec.ign);
+      st_sc1(A.pi + KCP_STAT * NB + b, rec.st);
+      st_sc1(A.pi + KCP_CAND * NB + b, (int32_t)S.count);
+#pragma unroll
+      for (int x = 0; x < KCP_X; ++x) {
+        st_sc1(A.pm + (2 * x) * NB + b, rec.mx[x]);
+        st_sc1(A.pm + (2 * x + 1) * NB + b, rec.mn[x]);
+      }
+#pragma unroll
+      for (int c = 0; c < KSG_MAX_TSC; ++c)
+        if (c < nreg) st_sc1(A.pr + (size_t)c * NB + b, rec.reg[c]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    CS(6);
+    __shared__ uint32_t last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(A.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = old == gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (last) solo_last_select(C, F, A, L.rec, prog, ipa_flags, cs_t0);
+    return;
+  }
   rec_block(rec, L.rec, F.has_ext ? xmask : 0u, nreg, RB_CNT16 | RB_ST | (F.has_ext ? 0u : RB_KEY));
   CS(5);
   if (threadIdx.x == 0) {
@@ -815,6 +997,137 @@ __global__ __launch_bounds__(64) void k_tx4_select(DevCluster C, DevProfile F, C
   else if (place) tables_assume_remote(C, V, g, +1, threadIdx.x, blockDim.x);
 }
 
+// The normalisers per profile position from the folded partials (the summary's
+// max / min; PodTopologySpread's from the raw score of its single constraint).
+__device__ __forceinline__ void chain_norms(const DevProfile& F, const ksg_prog* h, const EvalTotals& E,
+                                            int64_t (&smx)[KSG_MAX_PLUGINS], int64_t (&smn)[KSG_MAX_PLUGINS],
+                                            int64_t pmx, int64_t pmn) {
+#pragma unroll
+  for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+    smx[pos] = 0;
+    smn[pos] = INT64_MAX;
+    if (pos >= F.n) continue;
+    const int p = F.plugins[pos], x = chain_x(p);
+    if (p == KP_IPA) smx[pos] = INT64_MIN;
+    if (x < 0) continue;
+    if (p == KP_PTS) {
+      if (pmx != INT64_MIN) { smx[pos] = pmx > 0 ? pmx : 0; smn[pos] = pmn; }
+    } else if (rec_mx(E.r, x) != INT64_MIN) {
+      const int64_t m = rec_mx(E.r, x);
+      smx[pos] = p == KP_IPA ? m : (m > 0 ? m : 0);
+      smn[pos] = rec_mn(E.r, x);
+    }
+  }
+}
+__device__ __forceinline__ void chain_summary(const ChainArgs& A, const DevProfile& F, const ksg_prog* h,
+                                              const EvalTotals& E, const int64_t (&smx)[KSG_MAX_PLUGINS],
+                                              const int64_t (&smn)[KSG_MAX_PLUGINS], uint32_t ipa_flags) {
+  ksg_pod_summary* S = A.sums + A.q;
+  S->feasible = E.r.feas;
+  S->ignored = E.r.ign;
+  S->ipa_flags = ipa_flags;
+#pragma unroll
+  for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos)
+    if (pos < F.n) {
+      S->max_score[pos] = smx[pos];
+      S->min_score[pos] = smn[pos];
+    }
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c)
+    if (c < h->n_tsc_score) S->pts_weight[c] = E.w[c];
+}
+
+// k_eval_solo's last-arriving block: the partials folded (normalisers, the
+// PodTopologySpread weights), the summary, every block's classes normalised and
+// weighted (the [0,100] check per class), the argmax, then the commit.
+__device__ void solo_last_select(DevCluster& C, const DevProfile& F, const ChainArgs& A, ChainRec* lds,
+                                 const uint8_t* __restrict__ prog, uint32_t ipa_flags, uint64_t cs_t0) {
+  const ProgView V = view(prog);
+  const ksg_prog* h = V.h;
+  const uint32_t NB = A.nblk;
+  uint32_t xmask = 0;
+  for (int p = 0; p < F.n; ++p) {
+    const int x = chain_x(F.plugins[p]);
+    if (x >= 0) xmask |= 1u << x;
+  }
+  const int ns = h->n_tsc_score;
+  EvalTotals E;
+  ChainRec& r = E.r;
+  rec_init(r);
+  for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) {
+    r.feas += ld_sc1(A.pi + KCP_FEAS * NB + b);
+    r.ign += ld_sc1(A.pi + KCP_IGN * NB + b);
+    r.st |= ld_sc1(A.pi + KCP_STAT * NB + b);
+#pragma unroll
+    for (int x = 0; x < KCP_X; ++x) {
+      if (!((xmask >> x) & 1u)) continue;
+      const int64_t a = ld_sc1(A.pm + (2 * x) * NB + b), c = ld_sc1(A.pm + (2 * x + 1) * NB + b);
+      r.mx[x] = a > r.mx[x] ? a : r.mx[x];
+      r.mn[x] = c < r.mn[x] ? c : r.mn[x];
+    }
+#pragma unroll
+    for (int c = 0; c < KSG_MAX_TSC; ++c)
+      if (c < ns) r.reg[c] |= ld_sc1(A.pr + (size_t)c * NB + b);
+  }
+  CS(24);
+  rec_block(r, lds, xmask, ns, RB_CNT | RB_ST);
+  eval_weights(C, h, E);
+  int64_t pmx = INT64_MIN, pmn = INT64_MAX;
+  if (E.r.mx[KCX_PTS] != INT64_MIN) {  // one score constraint: raw is monotone in the count
+    pmx = pts_raw1(h, E, E.r.mx[KCX_PTS]);
+    pmn = pts_raw1(h, E, E.r.mn[KCX_PTS]);
+  }
+  int64_t smx[KSG_MAX_PLUGINS], smn[KSG_MAX_PLUGINS];
+  chain_norms(F, h, E, smx, smn, pmx, pmn);
+  if (threadIdx.x == 0) chain_summary(A, F, h, E, smx, smn, ipa_flags);
+  CS(25);
+  // every block's classes
+  const bool pts_skip = (h->flags & KPF_SKIP_PTS_SCORE) != 0;
+  ChainRec k;
+  rec_init(k);
+  for (uint32_t b = threadIdx.x; b < NB; b += blockDim.x) {
+    const uint32_t cnt = (uint32_t)ld_sc1(A.pi + KCP_CAND * NB + b);
+    const uint64_t* base = reinterpret_cast<const uint64_t*>(A.cand + (size_t)b * kChain);
+    for (uint32_t e = 0; e < cnt; ++e) {
+      const uint64_t w0 = ld_sc1(base + 3 * e), w1 = ld_sc1(base + 3 * e + 1), key = ld_sc1(base + 3 * e + 2);
+      const int32_t cvv[KCP_X] = {(int32_t)(uint32_t)w0, (int32_t)(uint32_t)(w0 >> 32), (int32_t)(uint32_t)w1,
+                                  (int32_t)(uint32_t)(w1 >> 32)};
+      int64_t part = 0;
+      bool rerr = false;
+#pragma unroll
+      for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+        if (pos >= F.n) continue;
+        const int p = F.plugins[pos], x = chain_x(p);
+        if (x < 0) continue;
+        int64_t sv = 0;
+#pragma unroll
+        for (int i = 0; i < KCP_X; ++i)
+          if (i == x) sv = cvv[i];
+        bool pts_keys = false;
+        if (p == KP_PTS) {
+          pts_keys = sv >= 0 && ns > 0;
+          if (sv < 0) sv = 0;
+          else if (ns > 0 && !pts_skip) sv = pts_raw1(h, E, sv);
+        }
+        bool use;
+        const int64_t v = normalize_pos(p, h, sv, smx[pos], smn[pos], ipa_flags, pts_keys, use);
+        if (use) {
+          if (v < 0 || v > 100) rerr = true;
+          part += v * F.weight[pos];
+        }
+      }
+      const uint64_t kk = E.r.feas == 1 ? (key & 0xFFFFFFFFFFull) : key + ((uint64_t)part << 40);
+      k.key = kk > k.key ? kk : k.key;
+      if (rerr) k.st |= 4;
+    }
+  }
+  CS(26);
+  __syncthreads();  // (lds reused)
+  rec_block(k, lds, 0u, 0, RB_ST | RB_KEY);
+  const int32_t st = E.r.st | (E.r.feas > 1 ? (k.st & 4) : 0);
+  chain_commit(C, A, V, k.key, E.r.feas, st, cs_t0);
+}
+
 struct FinalShared {
   int32_t tv[KSG_MAX_TOPO * kChain];
   ChainRec rec[kChain / 64];
@@ -985,6 +1298,11 @@ template <int ROWM>
 __global__ __launch_bounds__(kChain) __attribute__((amdgpu_waves_per_eu(4))) void k_eval_occ(
     DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
   eval_body<ROWM>(C, F, A, prog);
+}
+template <int ROWM>
+__global__ __launch_bounds__(kChain) void k_eval_solo(DevCluster C, DevProfile F, ChainArgs A,
+                                                      const uint8_t* __restrict__ prog) {
+  eval_body<ROWM, true>(C, F, A, prog);
 }
 __global__ __launch_bounds__(kChain) void k_final(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
   final_body(C, F, A, prog);

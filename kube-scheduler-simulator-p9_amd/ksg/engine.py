@@ -301,11 +301,12 @@ class Scheduler:
         self._chk(self.L.ksg_cycle_view_acquire(self.h, q, ctypes.byref(p)), "ksg_cycle_view_acquire")
         return CycleView(self.L, p)
 
-    def path_counts(self):
-        """Diagnostic: (pods through the table chain, pods through the scanning chain) so far."""
-        out = (ctypes.c_uint64 * 2)()
+    def path_counts(self, solo=False):
+        """Diagnostic: (pods through the table chain, pods through the scanning chain) so far
+        (+ of the first, the one-launch cycles when solo)."""
+        out = (ctypes.c_uint64 * 3)()
         self._chk(self.L.ksg_debug_path_counts(self.h, out), "ksg_debug_path_counts")
-        return out[0], out[1]
+        return (out[0], out[1], out[2]) if solo else (out[0], out[1])
 
     def set_path(self, per_pod: bool):
         self._chk(self.L.ksg_set_path(self.h, 1 if per_pod else 0), "ksg_set_path")

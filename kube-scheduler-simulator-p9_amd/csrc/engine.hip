@@ -188,6 +188,7 @@ struct ProgView {
   const ksg_aterm* at;
   const ksg_exist_term* et;
   const ksg_vchk* vchk;
+  const ksg_freq* fq;
 };
 
 __device__ __forceinline__ ProgView view(const uint8_t* p) {
@@ -200,6 +201,7 @@ __device__ __forceinline__ ProgView view(const uint8_t* p) {
   v.at = reinterpret_cast<const ksg_aterm*>(p + v.h->off_aterm);
   v.et = reinterpret_cast<const ksg_exist_term*>(p + v.h->off_eterm);
   v.vchk = reinterpret_cast<const ksg_vchk*>(v.i32 + v.h->vchk_off);
+  v.fq = reinterpret_cast<const ksg_freq*>(p + v.h->off_freq);
   return v;
 }
 
@@ -289,8 +291,23 @@ __device__ __forceinline__ bool node_req(const DevCluster& C, const ksg_req& r, 
   return node_req_v(C, r, vals, n, node_vid(C, r.key, n));
 }
 
+// A flattened requirement (ksg_freq) on local node n.
+__device__ __forceinline__ bool freq_match(const DevCluster& C, const ksg_freq& f, uint32_t n) {
+  if (f.mode >= KFR_NAME_EQ) {
+    if (f.mode == KFR_FALSE) return false;
+    return ((uint64_t)(C.goff + n) == f.arg) == (f.mode == KFR_NAME_EQ);
+  }
+  const int32_t v = node_vid(C, f.key, n);
+  const bool b = v >= 0 && ((f.arg >> (uint32_t)v) & 1ull);
+  return f.mode == KFR_ANY ? b : !b;
+}
 __device__ bool node_sel(const DevCluster& C, const ProgView& V, const ksg_sel& s, uint32_t n) {
   if (s.kind == 0) return false;
+  if (V.h->flags & KPF_FLAT_NA) {
+    for (int i = 0; i < s.req_cnt; ++i)
+      if (!freq_match(C, V.fq[s.req_off + i], n)) return false;
+    return true;
+  }
   for (int i = 0; i < s.req_cnt; ++i)
     if (!node_req(C, V.req[s.req_off + i], V.i32, n)) return false;
   return true;
@@ -2567,7 +2584,9 @@ template <class RT, int MODE>  // record word; MODE: eval_row specialisation
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_whatif_rec1(
     DevCluster C, DevProfile F, WiArgs A, const uint8_t* __restrict__ progs, const uint64_t* __restrict__ prog_off) {
   __shared__ int64_t red[2][4][5];
-  const uint32_t n = blockIdx.x * 256 + threadIdx.x;
+  // grid: x = pod group (fastest: the blocks of one node tile run together and
+  // share its rows in L2), y = node tile
+  const uint32_t n = blockIdx.y * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int pt = F.pos_taint, pa = F.pos_na;
   const bool hf = F.pos_fit >= 0, hb = F.pos_ba >= 0, ht = pt >= 0, ha = pa >= 0;
@@ -2588,7 +2607,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
   }
 #pragma unroll 1
   for (uint32_t pi = 0; pi < KSG_WI_PODS; ++pi) {
-    const uint32_t j = blockIdx.y * KSG_WI_PODS + pi;
+    const uint32_t j = blockIdx.x * KSG_WI_PODS + pi;
     if (j >= A.count) break;
     const ProgView V = view(progs + prog_off[A.q0 + j]);
     const ksg_prog* h = V.h;
@@ -4854,7 +4873,7 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
       a.rec = use_rec ? (void*)I.wrec_pairs.p : nullptr;
       const dim3 grid(std::max<uint32_t>((I.N + 256 * KSG_WI_NPT - 1) / (256 * KSG_WI_NPT), 1),
                       (a.count + KSG_WI_PODS - 1) / KSG_WI_PODS);
-      const dim3 grid1(std::max<uint32_t>((I.N + 255) / 256, 1), (a.count + KSG_WI_PODS - 1) / KSG_WI_PODS);
+      const dim3 grid1((a.count + KSG_WI_PODS - 1) / KSG_WI_PODS, std::max<uint32_t>((I.N + 255) / 256, 1));
       const dim3 grid2(std::max<uint32_t>((I.N + 256 * KSG_WI_R2NPT - 1) / (256 * KSG_WI_R2NPT), 1),
                        (a.count + KSG_WI_PODS - 1) / KSG_WI_PODS);
       const dim3 cpods((a.count + 255) / 256);

@@ -1695,7 +1695,50 @@ struct Cluster {
     vector<ksg_sel> sel;
     vector<ksg_aterm> at;
     vector<ksg_exist_term> et;
+    vector<ksg_freq> freq;  // flattened node-label requirements, by req index (KPF_FLAT_NA)
+    bool flat_ok = true;
   };
+  // The flattened form of node-label requirement P.req[idx] (ksg_types.h ksg_freq);
+  // a key with more than 64 values keeps the program on the value-list path.
+  void flatten_req(Prog& P, size_t idx) {
+    if (P.freq.size() <= idx) P.freq.resize(idx + 1, ksg_freq{-1, KFR_FALSE, 0});
+    const ksg_req& q = P.req[idx];
+    ksg_freq& f = P.freq[idx];
+    f = ksg_freq{q.key, KFR_FALSE, 0};
+    if (q.op == KR_NAME_EQ || q.op == KR_NAME_NE) {
+      f.mode = q.op == KR_NAME_EQ ? KFR_NAME_EQ : KFR_NAME_NE;
+      f.arg = (uint64_t)q.num;
+      return;
+    }
+    if (q.op == KR_FALSE) return;
+    const size_t nv = (q.key >= 0 && (size_t)q.key < nvals.size()) ? nvals[q.key].names.size() : 0;
+    if (nv > 64) { P.flat_ok = false; return; }
+    const uint64_t all = nv == 64 ? ~0ull : ((1ull << nv) - 1);
+    uint64_t m = 0;
+    switch (q.op) {
+      case KR_IN:
+      case KR_NOT_IN:
+        for (int i = 0; i < q.nvals; ++i) {
+          const int32_t v = P.i32[(size_t)q.val_off + i];
+          if (v >= 0 && (size_t)v < nv) m |= 1ull << v;
+        }
+        f.mode = q.op == KR_IN ? KFR_ANY : KFR_NONE;
+        break;
+      case KR_EXISTS: m = all; f.mode = KFR_ANY; break;
+      case KR_NOT_EXISTS: m = all; f.mode = KFR_NONE; break;
+      case KR_GT:
+      case KR_LT:
+        for (size_t v = 0; v < nv; ++v) {
+          i64 x = 0;
+          if (!parse_i64(nvals[q.key].names[v], x)) continue;  // (the numeric view: strconv.ParseInt)
+          if (q.op == KR_GT ? x > q.num : x < q.num) m |= 1ull << v;
+        }
+        f.mode = KFR_ANY;
+        break;
+      default: P.flat_ok = false; return;
+    }
+    f.arg = m;
+  }
 
   int32_t nval(int32_t key, const string& v) const {
     if (key < 0 || key >= (int32_t)nvals.size()) return -2;
@@ -1752,7 +1795,10 @@ struct Cluster {
         }
         rs.push_back(q);
       }
-    for (auto& q : rs) P.req.push_back(q);
+    for (auto& q : rs) {
+      P.req.push_back(q);
+      flatten_req(P, P.req.size() - 1);
+    }
     out.req_cnt = (int32_t)rs.size();
     return true;
   }
@@ -2271,6 +2317,7 @@ struct Cluster {
         P.i32.push_back(nval(q.key, kv.second));
         q.nvals = 1;
         P.req.push_back(q);
+        flatten_req(P, P.req.size() - 1);
         h.node_sel.req_cnt++;
       }
     }
@@ -2282,7 +2329,11 @@ struct Cluster {
         ksg_sel s;
         size_t r0 = P.req.size(), v0 = P.i32.size();
         if (compile_node_term(*t, P, s)) terms.push_back(s);
-        else { P.req.resize(r0); P.i32.resize(v0); }  // parse error: term never matches
+        else {  // parse error: term never matches
+          P.req.resize(r0);
+          P.i32.resize(v0);
+          if (P.freq.size() > r0) P.freq.resize(r0);
+        }
       }
       h.req_terms_off = (int32_t)P.sel.size();
       h.n_req_terms = (int32_t)terms.size();
@@ -2519,6 +2570,8 @@ struct Cluster {
     } else {
       h.tab = KTAB_ON;  // profiles without PTS / IPA: the chain needs no tables
     }
+    P.freq.resize(P.req.size(), ksg_freq{-1, KFR_FALSE, 0});
+    if (P.flat_ok) h.flags |= KPF_FLAT_NA;
     m.flags = h.flags;
     // ---- lay out the blob
     auto align = [](uint32_t x) { return (x + 15u) & ~15u; };
@@ -2529,6 +2582,7 @@ struct Cluster {
     h.off_sel = off; h.n_sel = (uint32_t)P.sel.size(); off = align(off + h.n_sel * sizeof(ksg_sel));
     h.off_aterm = off; h.n_aterm = (uint32_t)P.at.size(); off = align(off + h.n_aterm * sizeof(ksg_aterm));
     h.off_eterm = off; h.n_eterm = (uint32_t)P.et.size(); off = align(off + h.n_eterm * sizeof(ksg_exist_term));
+    h.off_freq = off; h.n_freq = (uint32_t)P.freq.size(); off = align(off + h.n_freq * sizeof(ksg_freq));
     h.total_bytes = off;
     blob.assign(off, 0);
     std::memcpy(blob.data(), &h, sizeof(h));
@@ -2538,6 +2592,7 @@ struct Cluster {
     if (h.n_sel) std::memcpy(blob.data() + h.off_sel, P.sel.data(), h.n_sel * sizeof(ksg_sel));
     if (h.n_aterm) std::memcpy(blob.data() + h.off_aterm, P.at.data(), h.n_aterm * sizeof(ksg_aterm));
     if (h.n_eterm) std::memcpy(blob.data() + h.off_eterm, P.et.data(), h.n_eterm * sizeof(ksg_exist_term));
+    if (h.n_freq) std::memcpy(blob.data() + h.off_freq, P.freq.data(), h.n_freq * sizeof(ksg_freq));
     return true;
   }
 

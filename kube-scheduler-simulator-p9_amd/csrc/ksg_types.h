@@ -93,6 +93,23 @@ typedef struct ksg_sel {
   int32_t pad;
 } ksg_sel;
 
+// A node-label requirement flattened by the host (ksg_prog.off_freq, one entry
+// per ksg_req of the program, same index; KPF_FLAT_NA): for keys with at most 64
+// values every operator is a test of the node's value id against a 64-bit mask
+// of the value ids that satisfy it (In: the listed values; Exists: every value;
+// Gt / Lt: the values whose integer view compares true; NotIn / DoesNotExist
+// the complement rule), so the evaluation has no value-list loop.
+#define KFR_ANY 0     // matches when the node has the key and its value's bit is set
+#define KFR_NONE 1    // matches when the node lacks the key or its value's bit is clear
+#define KFR_NAME_EQ 2 // matchFields metadata.name In: global node index == arg
+#define KFR_NAME_NE 3
+#define KFR_FALSE 4
+typedef struct ksg_freq {
+  int32_t key;      // node label key id (-1: not in the vocabulary: no node has it)
+  int32_t mode;     // KFR_*
+  uint64_t arg;     // value-id mask (KFR_ANY / KFR_NONE) or the node index
+} ksg_freq;         // 16 B
+
 // one pod (anti-)affinity term of the incoming pod (framework.AffinityTerm)
 typedef struct ksg_aterm {
   ksg_sel sel;
@@ -285,6 +302,7 @@ typedef struct ksg_prog {
   uint32_t off_sel, n_sel;
   uint32_t off_aterm, n_aterm;
   uint32_t off_eterm, n_eterm;
+  uint32_t off_freq, n_freq;    // ksg_freq per ksg_req (KPF_FLAT_NA)
   uint32_t total_bytes;
   uint32_t pad;
 } ksg_prog;
@@ -305,6 +323,7 @@ typedef struct ksg_prog {
 #define KPF_PREFILTER_ERROR (1u << 12)   // PreFilter error status: cycle aborts
 #define KPF_TOL_UNSCHED (1u << 13)       // tolerates node.kubernetes.io/unschedulable:NoSchedule
 #define KPF_SKIP_PORTS (1u << 14)        // NodePorts PreFilter Skip (no host ports)
+#define KPF_FLAT_NA (1u << 15)           // node selectors evaluate through the ksg_freq pool
 
 // KTAB_* (ksg_prog.tab)
 #define KTAB_ON (1u << 0)        // the pod runs the table chain (k_eval / k_final / k_select)

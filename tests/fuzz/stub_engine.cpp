@@ -34,7 +34,8 @@ static bool check_prog(const std::vector<uint8_t>& p, std::string& err) {
                            (uint64_t)h.off_req + sizeof(ksg_req) * (uint64_t)h.n_req,
                            (uint64_t)h.off_sel + sizeof(ksg_sel) * (uint64_t)h.n_sel,
                            (uint64_t)h.off_aterm + sizeof(ksg_aterm) * (uint64_t)h.n_aterm,
-                           (uint64_t)h.off_eterm + sizeof(ksg_exist_term) * (uint64_t)h.n_eterm};
+                           (uint64_t)h.off_eterm + sizeof(ksg_exist_term) * (uint64_t)h.n_eterm,
+                           (uint64_t)h.off_freq + sizeof(ksg_freq) * (uint64_t)h.n_freq};
   for (uint64_t e : ends)
     if (e > p.size()) { err = "stub: pool outside the program"; return false; }
   if (h.n_lk < 0 || h.n_lk > KSG_LK_MAX || h.n_ub < 0 || h.n_ub > KSG_UB_MAX) { err = "stub: plan"; return false; }

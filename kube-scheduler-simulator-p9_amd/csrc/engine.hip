@@ -291,22 +291,29 @@ __device__ __forceinline__ bool node_req(const DevCluster& C, const ksg_req& r, 
   return node_req_v(C, r, vals, n, node_vid(C, r.key, n));
 }
 
-// A flattened requirement (ksg_freq) on local node n.
-__device__ __forceinline__ bool freq_match(const DevCluster& C, const ksg_freq& f, uint32_t n) {
-  if (f.mode >= KFR_NAME_EQ) {
-    if (f.mode == KFR_FALSE) return false;
-    return ((uint64_t)(C.goff + n) == f.arg) == (f.mode == KFR_NAME_EQ);
-  }
-  const int32_t v = node_vid(C, f.key, n);
-  const bool b = v >= 0 && ((f.arg >> (uint32_t)v) & 1ull);
-  return f.mode == KFR_ANY ? b : !b;
+// A flattened requirement (ksg_freq) on local node n, without branches on the
+// (wave-uniform) mode: one 16-byte scalar load of the entry, the node's value
+// for the key, the mask bit, the name compare, a select.
+__device__ __forceinline__ bool freq_match(const DevCluster& C, const ksg_freq* fp, uint32_t n) {
+  const uint4 w = *reinterpret_cast<const uint4*>(fp);
+  const int32_t key = (int32_t)w.x, mode = (int32_t)w.y;
+  const uint64_t arg = (uint64_t)w.z | ((uint64_t)w.w << 32);
+  const bool kok = key >= 0 && (uint32_t)key < C.K;
+  const int32_t v = C.label[(size_t)(kok ? (uint32_t)key : 0u) * C.N + n];  // (key 0's column when unknown)
+  const bool inset = kok && v >= 0 && ((arg >> ((uint32_t)v & 63u)) & 1ull);
+  const bool name = (uint64_t)(C.goff + n) == arg;
+  const bool r = mode <= KFR_NONE ? inset : name;
+  return mode == KFR_FALSE ? false : (r != (mode == KFR_NONE || mode == KFR_NAME_NE));
 }
 __device__ bool node_sel(const DevCluster& C, const ProgView& V, const ksg_sel& s, uint32_t n) {
   if (s.kind == 0) return false;
-  if (V.h->flags & KPF_FLAT_NA) {
-    for (int i = 0; i < s.req_cnt; ++i)
-      if (!freq_match(C, V.fq[s.req_off + i], n)) return false;
-    return true;
+  if (V.h->flags & KPF_FLAT_NA) {  // (a wave-uniform loop: the entries stay scalar loads)
+    bool ok = true;
+    for (int i = 0; i < s.req_cnt; ++i) {
+      ok &= freq_match(C, V.fq + s.req_off + i, n);
+      if (!__ballot(ok)) break;
+    }
+    return ok;
   }
   for (int i = 0; i < s.req_cnt; ++i)
     if (!node_req(C, V.req[s.req_off + i], V.i32, n)) return false;
@@ -316,6 +323,18 @@ __device__ bool node_sel(const DevCluster& C, const ProgView& V, const ksg_sel& 
 // nodeaffinity.RequiredNodeAffinity.Match
 __device__ bool required_na(const DevCluster& C, const ProgView& V, uint32_t n) {
   uint32_t f = V.h->flags;
+  if (f & KPF_FLAT_NA) {  // wave-uniform loops (no per-lane early exit): scalar program reads
+    bool ok = !(f & KPF_HAS_NODE_SEL) || node_sel(C, V, V.h->node_sel, n);
+    if ((f & KPF_HAS_REQ_NA) && __ballot(ok)) {
+      bool any = false;
+      for (int t = 0; t < V.h->n_req_terms; ++t) {
+        any |= node_sel(C, V, V.sel[V.h->req_terms_off + t], n);
+        if (!__ballot(ok && !any)) break;
+      }
+      ok = ok && any;
+    }
+    return ok;
+  }
   if ((f & KPF_HAS_NODE_SEL) && !node_sel(C, V, V.h->node_sel, n)) return false;
   if (f & KPF_HAS_REQ_NA) {
     for (int t = 0; t < V.h->n_req_terms; ++t)

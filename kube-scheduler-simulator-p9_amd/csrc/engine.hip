@@ -4104,7 +4104,7 @@ struct Engine::Impl {
   DBuf<int64_t> cpm, cpm2;
   DBuf<EvalTotals> cetot;
   DBuf<SoloCand> ccand;   // k_eval_solo: classes per block [cnblk][kChain]
-  int solo = -1;          // one-launch cycles: -1 auto (up to 2 blocks per CU), 0 off, 1 forced (KSG_SOLO)
+  int solo = 0;           // one-launch cycles (k_eval_solo): 0 off, 1 on (KSG_SOLO)
   uint32_t fold_blocks = 256;  // table chain: k_fold above this many blocks (KSG_FOLD_BLOCKS; tests force it)
   uint32_t occ_blocks = 0;     // table chain: occupancy twins above this many blocks (0: 2 per CU; KSG_OCC_BLOCKS)
   bool occ_force = false;
@@ -5525,8 +5525,10 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   CA.xsend = nullptr;
   CA.cand = I.ccand.p;
   // one-launch cycles (k_eval_solo) for pods of normalising profiles whose outputs
-  // are not kept, unsharded, one PodTopologySpread score constraint at most
-  const bool solo_ok = !xchain && F.has_ext && (I.solo == 1 || (I.solo < 0 && I.cnblk <= 2 * I.n_cus));
+  // are not kept, unsharded, committing cycles only (a dry run reads the per-node
+  // filter codes, which k_eval_solo does not write); opt-in (KSG_SOLO=1): measured
+  // slower than the two-launch chain on cfg4 (63.6 vs 35.2 us/pod, r03)
+  const bool solo_ok = commit && !xchain && F.has_ext && I.solo == 1;
   if (I.cnblk > I.fold_blocks || xchain) {  // fold k_eval's partials once (k_fold, or the X2 merge) above this many blocks
     if (!I.cetot.alloc(1, err)) return false;
     CA.etot = I.cetot.p;

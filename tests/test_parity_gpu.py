@@ -194,3 +194,22 @@ def test_engine_matches_golden_fixture(path):
     for q, (r, e) in enumerate(zip(s.results(), d["expected"])):
         assert (r.selected, r.feasible, r.status) == (e["selected"], e["feasible"], e["status"]), q
         assert s.annotations(q) == e["annotations"], q
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,sizes", [(1, dict(n_nodes=40, n_pods=120)),
+                                      (4, dict(n_nodes=600, n_existing=1500, n_pods=150, n_zones=8))],
+                         ids=["cfg1", "cfg4"])
+def test_one_launch_cycles_match_oracle(monkeypatch, c, sizes):
+    """The opt-in one-launch chain (KSG_SOLO=1, k_eval_solo) on pods whose outputs
+    are not kept: placements identical to the oracle's, and the cycles really ran
+    one-launch (path counter)."""
+    monkeypatch.setenv("KSG_SOLO", "1")
+    doc = g.generate(c, **sizes)
+    o, s = run_both(doc, keep=False)
+    res = s.results()
+    bad = [(q, (r.selected, r.feasible, r.status), o.result(q)) for q, r in enumerate(res)
+           if (r.selected, r.feasible, r.status) != o.result(q)]
+    assert not bad, f"{len(bad)} pods differ, first {bad[:5]}"
+    pc = s.path_counts(solo=True)
+    assert pc[2] > 0 or pc[0] == 0, pc  # table-chain pods went one-launch

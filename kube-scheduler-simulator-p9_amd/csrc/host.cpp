@@ -1701,7 +1701,7 @@ struct Cluster {
   // The flattened form of node-label requirement P.req[idx] (ksg_types.h ksg_freq);
   // a key with more than 64 values keeps the program on the value-list path.
   void flatten_req(Prog& P, size_t idx) {
-    if (P.freq.size() <= idx) P.freq.resize(idx + 1, ksg_freq{-1, KFR_FALSE, 0});
+    if (P.freq.size() <= idx) P.freq.resize(idx + 1, ksg_freq{-1, KFR_FALSE, 0});  // (in req order)
     const ksg_req& q = P.req[idx];
     ksg_freq& f = P.freq[idx];
     f = ksg_freq{q.key, KFR_FALSE, 0};
@@ -1795,10 +1795,7 @@ struct Cluster {
         }
         rs.push_back(q);
       }
-    for (auto& q : rs) {
-      P.req.push_back(q);
-      flatten_req(P, P.req.size() - 1);
-    }
+    for (auto& q : rs) P.req.push_back(q);
     out.req_cnt = (int32_t)rs.size();
     return true;
   }
@@ -2317,7 +2314,6 @@ struct Cluster {
         P.i32.push_back(nval(q.key, kv.second));
         q.nvals = 1;
         P.req.push_back(q);
-        flatten_req(P, P.req.size() - 1);
         h.node_sel.req_cnt++;
       }
     }
@@ -2332,7 +2328,6 @@ struct Cluster {
         else {  // parse error: term never matches
           P.req.resize(r0);
           P.i32.resize(v0);
-          if (P.freq.size() > r0) P.freq.resize(r0);
         }
       }
       h.req_terms_off = (int32_t)P.sel.size();
@@ -2570,7 +2565,11 @@ struct Cluster {
     } else {
       h.tab = KTAB_ON;  // profiles without PTS / IPA: the chain needs no tables
     }
-    P.freq.resize(P.req.size(), ksg_freq{-1, KFR_FALSE, 0});
+    // every requirement of the pool (NodeAffinity, node selector, volume and
+    // topology terms alike) in its flattened form
+    P.freq.clear();
+    P.flat_ok = true;
+    for (size_t i = 0; i < P.req.size(); ++i) flatten_req(P, i);
     if (P.flat_ok) h.flags |= KPF_FLAT_NA;
     m.flags = h.flags;
     // ---- lay out the blob

@@ -1725,6 +1725,13 @@ struct WiArgs {
   uint32_t bw_a, bw_t, bw_tot;
   uint32_t small;  // 100 x the profile's weights < 2^31: every total fits 32 bits (k_whatif_rec2)
   uint32_t need_eph;  // resource columns 2..3 requested by some pod (RowV loads)
+  // class path (k_whatif_cls1 / k_whatif_cls2): per (pod, tile) class rows and
+  // feasible counts (bit 31: a Fit/BA score out of range); per pod the folded
+  // class row and flag between the phases of a sharded step
+  uint64_t* wc_part;
+  uint32_t* wc_cnt;
+  uint64_t* wc_cls;
+  uint32_t* wc_flag;
 };
 
 // (programs as restrict parameters: their reads stay scalar loads beside the
@@ -2867,6 +2874,340 @@ __global__ __launch_bounds__(256) void k_whatif_rec2(DevCluster C, DevProfile F,
     const uint64_t b = wave_max(best);
     if (lane0() && b) atomicMax((unsigned long long*)&sm->best_key, (unsigned long long)b);
     if (feas_all > 1 && __any(range_err) && lane0()) atomicOr((uint32_t*)&sm->status, 2u);
+  }
+}
+
+// ---------------------------------------------------------------- what-if class path
+// A what-if step of a Fit / BA (default arguments) + TaintToleration +
+// NodeAffinity profile without the per-pair record round trip.  A (pod, node)
+// total is fb + wt * reverse_norm(xt) + wa * norm(xa): fb is the node's Fit/BA
+// weighted sum, xt the raw Taint score (node taints the pod prefers not to be
+// on), xa the raw NodeAffinity score, the sum of the weights of the matched
+// preferred terms.  Both normalisers are monotone and pod-wide, so for every
+// class c = xt << np | (matched-term mask, np terms) the pair that wins inside
+// c is the one with the largest (fb, tie-break) key — pack_key(fb, ...) — and
+// the pod's winner is the best of its classes' winners once the maxima are
+// known.  Pass 1 (k_whatif_cls1) keeps per block and pod the best key of each
+// class in LDS (ds_max_u64) and writes one row of KSG_WC_CLS keys per (tile,
+// pod); k_whatif_cls2 folds the tiles, derives the feasible count and the raw
+// maxima / minima from the present classes, then normalises and picks.
+// Nothing per pair reaches memory.
+#define KSG_WC_CLS 128
+#define KSG_WC_PODS 32
+#define KSG_WC_NPT 2
+#define KSG_WC_SUB 8
+#define KSG_WC_TILE (256 * KSG_WC_NPT * KSG_WC_SUB)
+
+// Node selector term s on NPT nodes (local, in range) at once: one scalar
+// entry load per requirement for all of them (KPF_FLAT_NA), else node_sel each.
+template <int NPT>
+__device__ __forceinline__ void sel_multi(const DevCluster& C, const ProgView& V, const ksg_sel& s,
+                                          const uint32_t (&n)[NPT], bool (&ok)[NPT]) {
+  if (!(V.h->flags & KPF_FLAT_NA)) {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) ok[k] = node_sel(C, V, s, n[k]);
+    return;
+  }
+  const bool kind = s.kind != 0;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) ok[k] = kind;
+  for (int i = 0; i < s.req_cnt; ++i) {
+    const ksg_freq* fp = V.fq + s.req_off + i;
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      ok[k] &= freq_match(C, fp, n[k]);
+      any |= ok[k];
+    }
+    if (!__ballot(any)) break;
+  }
+}
+// nodeaffinity.RequiredNodeAffinity.Match on NPT nodes (required_na)
+template <int NPT>
+__device__ __forceinline__ void required_na_multi(const DevCluster& C, const ProgView& V, const uint32_t (&n)[NPT],
+                                                  bool (&ok)[NPT]) {
+  const uint32_t f = V.h->flags;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) ok[k] = true;
+  if (f & KPF_HAS_NODE_SEL) sel_multi<NPT>(C, V, V.h->node_sel, n, ok);
+  if (f & KPF_HAS_REQ_NA) {
+    bool any[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) any[k] = false;
+    for (int t = 0; t < V.h->n_req_terms; ++t) {
+      bool m[NPT];
+      sel_multi<NPT>(C, V, V.sel[V.h->req_terms_off + t], n, m);
+      bool pend = false;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        any[k] |= m[k];
+        pend |= ok[k] && !any[k];
+      }
+      if (!__ballot(pend)) break;
+    }
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) ok[k] &= any[k];
+  }
+}
+
+// Pass 1: grid x = group of KSG_WC_PODS pods (fastest: a tile's rows are shared
+// in L2 by its pod groups), y = tile of KSG_WC_TILE nodes; each thread holds the
+// rows of KSG_WC_NPT nodes in registers while the block's pods go by, so a pod's
+// program is decoded once per 256 pairs of a wave.  The filter and the scores
+// are evaluated without branches per node (pass / fail selects the outcome).
+// Host-checked (run_whatif): default Fit / BA arguments, no resource column
+// beyond cpu / memory requested, <= 4 taints per node with ids < 64, every
+// pod's (taints + 1) << preferred terms <= KSG_WC_CLS.
+__global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F, WiArgs A,
+                                                     const uint8_t* __restrict__ progs,
+                                                     const uint64_t* __restrict__ prog_off) {
+  constexpr int NPT = KSG_WC_NPT;
+  __shared__ unsigned long long slot[KSG_WC_PODS][KSG_WC_CLS];
+  __shared__ uint32_t wcnt[KSG_WC_PODS];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t j0 = blockIdx.x * KSG_WC_PODS;
+  const uint32_t np = min(A.count - j0, (uint32_t)KSG_WC_PODS);
+  for (uint32_t i = tid; i < KSG_WC_PODS * KSG_WC_CLS; i += 256) (&slot[0][0])[i] = 0ull;
+  if (tid < KSG_WC_PODS) wcnt[tid] = 0;
+  __syncthreads();
+  const bool hf = F.pos_fit >= 0, hb = F.pos_ba >= 0, ht = F.pos_taint >= 0, ha = F.pos_na >= 0;
+#pragma unroll 1
+  for (uint32_t sub = 0; sub < KSG_WC_SUB; ++sub) {
+    const uint32_t nb = blockIdx.y * KSG_WC_TILE + sub * (256 * NPT);
+    if (nb >= C.N) break;
+    uint32_t n[NPT];
+    bool live[NPT];
+    RowV row[NPT];
+    uint32_t tp[NPT];  // the node's taint ids, one per byte (0xFF: none)
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const uint32_t nn = nb + k * 256 + tid;
+      live[k] = nn < C.N;
+      n[k] = live[k] ? nn : 0u;
+      RowV& r = row[k];
+      r.alloc[0] = C.alloc[n[k]];
+      r.alloc[1] = C.alloc[(size_t)C.N + n[k]];
+      r.req[0] = C.req[n[k]];
+      r.req[1] = C.req[(size_t)C.N + n[k]];
+      r.alloc[2] = r.req[2] = r.alloc[3] = r.req[3] = 0;
+      r.nzc = C.nzc[n[k]];
+      r.nzm = C.nzm[n[k]];
+      r.podcnt = C.podcnt[n[k]];
+      r.allowed = C.allowed[n[k]];
+      const uint32_t t0 = C.toff[n[k]], tc = C.toff[n[k] + 1] - t0;
+      uint32_t w = 0xFFFFFFFFu;
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i)
+        if (i < tc) w = (w & ~(0xFFu << (8 * i))) | ((uint32_t)C.tid[t0 + i] << (8 * i));
+      tp[k] = w;
+    }
+#pragma unroll 1
+    for (uint32_t pi = 0; pi < np; ++pi) {
+      const uint32_t j = j0 + pi;
+      const ProgView V = view(progs + prog_off[A.q0 + j]);
+      const ksg_prog* h = V.h;
+      const uint32_t fl = h->flags;
+      bool pass[NPT];
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) pass[k] = live[k] && !(fl & KPF_PREFILTER_REJECT);
+      if (fl & KPF_RESTRICT) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) pass[k] &= bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n[k]);
+      }
+      if (hf) {
+        const int64_t q0 = h->req[0], q1 = h->req[1];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          const RowV& r = row[k];
+          const bool bad = (r.podcnt + 1 > r.allowed) | ((q0 > 0) & (q0 > r.alloc[0] - r.req[0])) |
+                           ((q1 > 0) & (q1 > r.alloc[1] - r.req[1]));
+          pass[k] &= !bad;
+        }
+      }
+      uint32_t xt[NPT];
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) xt[k] = 0;
+      if (ht) {
+        const uint32_t* hard = V.u32 + h->taint_hard_off;
+        const uint32_t* pref = V.u32 + h->taint_pref_off;
+        const int tw = h->taint_words;
+        const uint64_t hw = tw > 1 ? ((uint64_t)hard[1] << 32 | hard[0]) : tw > 0 ? hard[0] : 0;
+        const uint64_t pw = tw > 1 ? ((uint64_t)pref[1] << 32 | pref[0]) : tw > 0 ? pref[0] : 0;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          bool hit = false;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t t = (tp[k] >> (8 * i)) & 0xFFu;
+            const bool v = t != 0xFFu;
+            hit |= v & (((hw >> (t & 63u)) & 1ull) != 0);
+            xt[k] += (v & (((pw >> (t & 63u)) & 1ull) != 0)) ? 1u : 0u;
+          }
+          pass[k] &= !hit;
+        }
+      }
+      if (ha && !(fl & KPF_SKIP_NA_FILTER)) {
+        bool m[NPT];
+        required_na_multi<NPT>(C, V, n, m);
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) pass[k] &= m[k];
+      }
+      // NodeAffinity's preferred terms: the matched-term mask
+      const int npf = (ha && !(fl & KPF_SKIP_NA_SCORE)) ? h->n_pref_terms : 0;
+      uint32_t mask[NPT];
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) mask[k] = 0;
+      for (int t = 0; t < npf; ++t) {
+        bool m[NPT];
+        sel_multi<NPT>(C, V, V.sel[h->pref_terms_off + t], n, m);
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) mask[k] |= (uint32_t)m[k] << t;
+      }
+      int cnt = 0;
+      bool rng = false;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        int64_t fb = 0;
+        bool bad = false;
+        if (hf) {
+          const int64_t s = fit_score_row<1>(row[k], F, h);
+          bad |= s < 0 || s > 100;
+          fb += s * F.w_fit;
+        }
+        if (hb) {
+          const int64_t s = ba_score_row<1>(row[k], F, h);
+          bad |= s < 0 || s > 100;
+          fb += s * F.w_ba;
+        }
+        const uint32_t c = (xt[k] << npf) | mask[k];
+        const uint64_t key = pack_key(bad ? 0 : fb, F.seed, h->queue_idx, C.goff + n[k]);
+        if (pass[k]) atomicMax(&slot[pi][c], (unsigned long long)key);
+        cnt += pass[k] ? 1 : 0;
+        rng |= pass[k] && bad;
+      }
+      const int c = wave_sum(cnt);
+      const bool anyr = __ballot(rng) != 0;
+      if (lane0() && (c || anyr)) atomicAdd(&wcnt[pi], (uint32_t)c | (anyr ? 0x80000000u : 0u));
+    }
+  }
+  __syncthreads();
+  // this tile's row of every pod of the group
+  const size_t tile = blockIdx.y, tiles = gridDim.y;
+  for (uint32_t i = tid; i < np * KSG_WC_CLS; i += 256) {
+    const uint32_t pi = i / KSG_WC_CLS, c = i % KSG_WC_CLS;
+    A.wc_part[((size_t)(j0 + pi) * tiles + tile) * KSG_WC_CLS + c] = (&slot[0][0])[i];
+  }
+  if (tid < np) A.wc_cnt[(size_t)(j0 + tid) * tiles + tile] = wcnt[tid];
+}
+
+// Pass 2, one block of KSG_WC_CLS threads per pod (thread = class).  phase 0:
+// fold + summary + pick (one shard); 1: fold + summary (the table kept for
+// phase 2, after the shards' summaries are merged); 2: pick from the kept table.
+__global__ __launch_bounds__(KSG_WC_CLS) void k_whatif_cls2(DevProfile F, WiArgs A, uint32_t tiles, int phase) {
+  __shared__ int64_t red[2][6];
+  __shared__ uint32_t rcnt[2];
+  const uint32_t j = blockIdx.x, c = threadIdx.x, lane = c & 63, w = c >> 6;
+  const uint32_t q = A.q0 + j;
+  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[q]);
+  const ProgView V = view(A.progs + A.prog_off[q]);
+  ksg_pod_summary* sm = A.sums + q;
+  const int pt = F.pos_taint, pa = F.pos_na;
+  const int npf = (pa >= 0 && !(h->flags & KPF_SKIP_NA_SCORE)) ? h->n_pref_terms : 0;
+  uint64_t m = 0;
+  uint32_t flag = 0;
+  if (phase != 2) {
+    const uint64_t* p = A.wc_part + (size_t)j * tiles * KSG_WC_CLS + c;
+    uint64_t m0 = 0, m1 = 0;
+    uint32_t t = 0;
+    for (; t + 1 < tiles; t += 2) {
+      const uint64_t a = p[(size_t)t * KSG_WC_CLS], b = p[(size_t)(t + 1) * KSG_WC_CLS];
+      m0 = a > m0 ? a : m0;
+      m1 = b > m1 ? b : m1;
+    }
+    if (t < tiles) m0 = p[(size_t)t * KSG_WC_CLS] > m0 ? p[(size_t)t * KSG_WC_CLS] : m0;
+    m = m0 > m1 ? m0 : m1;
+    // feasible count and Fit/BA range flag over the tiles
+    uint32_t cs = 0, rf = 0;
+    for (uint32_t u = c; u < tiles; u += KSG_WC_CLS) {
+      const uint32_t x = A.wc_cnt[(size_t)j * tiles + u];
+      cs += x & 0x7FFFFFFFu;
+      rf |= x >> 31;
+    }
+    const int32_t cw = wave_sum((int32_t)cs);
+    const bool rw = __ballot(rf != 0) != 0;
+    if (lane == 0) rcnt[w] = (uint32_t)cw | (rw ? 0x80000000u : 0u);
+  } else {
+    m = A.wc_cls[(size_t)j * KSG_WC_CLS + c];
+  }
+  // the class's raw scores
+  const bool present = m != 0;
+  const int64_t xt = (int64_t)(c >> npf);
+  int64_t xa = 0;
+  for (int t = 0; t < npf; ++t)
+    if ((c >> t) & 1u) xa += V.i32[h->pref_w_off + t];
+  if (phase != 2) {
+    int64_t v[4] = {present ? xt : INT64_MIN, present ? xt : INT64_MAX, present ? xa : INT64_MIN,
+                    present ? xa : INT64_MAX};
+    v[0] = wave_max(v[0]); v[1] = wave_min(v[1]); v[2] = wave_max(v[2]); v[3] = wave_min(v[3]);
+    if (lane == 0) for (int i = 0; i < 4; ++i) red[w][i] = v[i];
+    __syncthreads();
+    const int32_t feas = (int32_t)((rcnt[0] & 0x7FFFFFFFu) + (rcnt[1] & 0x7FFFFFFFu));
+    flag = (rcnt[0] | rcnt[1]) >> 31;
+    if (c == 0) {
+      sm->feasible = feas;
+      if (feas) {
+        if (pt >= 0) {
+          sm->max_score[pt] = max(red[0][0], red[1][0]) > sm->max_score[pt] ? max(red[0][0], red[1][0]) : sm->max_score[pt];
+          sm->min_score[pt] = min(red[0][1], red[1][1]) < sm->min_score[pt] ? min(red[0][1], red[1][1]) : sm->min_score[pt];
+        }
+        if (pa >= 0) {
+          sm->max_score[pa] = max(red[0][2], red[1][2]) > sm->max_score[pa] ? max(red[0][2], red[1][2]) : sm->max_score[pa];
+          sm->min_score[pa] = min(red[0][3], red[1][3]) < sm->min_score[pa] ? min(red[0][3], red[1][3]) : sm->min_score[pa];
+        }
+      }
+    }
+    if (phase == 1) {
+      A.wc_cls[(size_t)j * KSG_WC_CLS + c] = m;
+      if (c == 0) A.wc_flag[j] = flag;
+      return;
+    }
+    __syncthreads();  // (the summary above is read back below)
+  } else {
+    flag = A.wc_flag[j];
+  }
+  const bool kept = A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n;
+  if (kept) return;  // k_whatif<2> (per-pair outputs)
+  const int32_t feas_all = sm->feasible;
+  const int64_t Mt = pt >= 0 ? sm->max_score[pt] : 0, Ma = pa >= 0 ? sm->max_score[pa] : 0;
+  const int64_t wt = pt >= 0 ? F.weight[pt] : 0, wa = pa >= 0 ? F.weight[pa] : 0;
+  bool range_err = false;
+  uint64_t best = 0;
+  if (present) {
+    int64_t tot = (int64_t)(m >> 40);
+    if (pt >= 0) {
+      const int64_t s = Mt == 0 ? 100 : 100 - 100 * xt / Mt;  // (reverse)
+      range_err |= s < 0 || s > 100;
+      tot += s * wt;
+    }
+    if (pa >= 0 && !(h->flags & KPF_SKIP_NA_SCORE)) {
+      const int64_t s = Ma == 0 ? xa : 100 * xa / Ma;
+      range_err |= s < 0 || s > 100;
+      tot += s * wa;
+    }
+    if (feas_all == 1) tot = 0;  // single feasible node: no scoring
+    best = ((uint64_t)tot << 40) | (m & 0xFFFFFFFFFFull);
+  }
+  best = wave_max(best);
+  range_err = __ballot(range_err) != 0;
+  if (lane == 0) {
+    red[w][4] = (int64_t)best;
+    red[w][5] = range_err ? 1 : 0;
+  }
+  __syncthreads();
+  if (c == 0) {
+    const uint64_t b = (uint64_t)red[0][4] > (uint64_t)red[1][4] ? (uint64_t)red[0][4] : (uint64_t)red[1][4];
+    if (b) atomicMax((unsigned long long*)&sm->best_key, (unsigned long long)b);
+    if (feas_all > 1 && (flag || red[0][5] || red[1][5])) atomicOr((uint32_t*)&sm->status, 2u);
   }
 }
 
@@ -4069,7 +4410,9 @@ struct Engine::Impl {
   DBuf<uint64_t> wrec_pairs;  // what-if: pass 1's per-pair records (run_whatif)
   uint32_t wi_chunk = 0;      // ... pods per chunk of the last step, and whether records were used
   bool wi_rec = false;
+  bool wi_cls = false;        // ... or the class path
   uint32_t max_taints = 0;  // most taints on one node (what-if record width)
+  int32_t max_tid = -1;     // largest taint id on a node (what-if class path: < 64)
   int64_t max_na_sum = 0;   // largest preferred NodeAffinity weight sum of a program
   bool static_fits = true; // raw scores fit the record (taints per node < 4096, NodeAffinity weights < 2^20)
   DBuf<StaticRec> stat;   // static records of a chunk of pods [chunk][N]
@@ -4159,7 +4502,7 @@ struct Engine::Impl {
   uint32_t sample_every = 0;
   std::vector<hipEvent_t> sev;
   uint32_t n_samples = 0;
-  uint64_t path_pods[3] = {0, 0, 0};  // diagnostic: pods run by the table chain / the scanning chain / of the first, in one launch
+  uint64_t path_pods[4] = {0, 0, 0, 0};  // diagnostic: pods run by the table chain / the scanning chain / of the first, in one launch; what-if pod chunks on the class path
   std::vector<Engine::KernelStat> stats;
 
   DevCluster cluster() const {
@@ -4320,6 +4663,8 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   I.static_fits = true;
   I.max_taints = 0;
   for (uint32_t i = 0; i < ns.n; ++i) I.max_taints = std::max(I.max_taints, ns.taint_off[i + 1] - ns.taint_off[i]);
+  I.max_tid = -1;
+  for (int32_t t : ns.taint_id) I.max_tid = std::max(I.max_tid, t);
   if (I.max_taints >= 4096) I.static_fits = false;
   I.R = ns.n_res;
   I.K = ns.n_keys;
@@ -4796,7 +5141,13 @@ static uint32_t prog_need_of(const ksg_prog* h) {
   if (h->n_tsc_filter + h->n_tsc_score > 0) need |= 1;
   if (h->tab & KTAB_ON) need |= 4;
   if (h->tab & KTAB_PTS_MULTI) need |= 8;
-  return need;
+  // bits 8..15: preferred NodeAffinity terms of the what-if class path (0xFF: a
+  // negative weight or more than 7 terms — the record path)
+  const int32_t* i32 = reinterpret_cast<const int32_t*>(reinterpret_cast<const uint8_t*>(h) + h->off_i32);
+  uint32_t np = h->n_pref_terms > 7 ? 0xFFu : (uint32_t)h->n_pref_terms;
+  for (int t = 0; t < h->n_pref_terms && np != 0xFFu; ++t)
+    if (i32[h->pref_w_off + t] < 0) np = 0xFFu;
+  return need | np << 8;
 }
 
 static bool exchange(Engine::Impl& I, const void* src, size_t bytes, std::string& err);
@@ -4855,7 +5206,15 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
     for (int i = 0; i < I.F.n; ++i)
       if (I.F.plugins[i] == KP_FIT || I.F.plugins[i] == KP_BA) wsum += I.F.weight[i] > 0 ? I.F.weight[i] : 0;
     A.need_eph = I.any_eph_req ? 1u : 0u;
-    const bool use_rec = rec_mb > 0 && I.R <= 4 && I.static_fits && 100 * wsum < (int64_t)1 << 30;
+    // the class path (k_whatif_cls1/2): nothing per pair in memory; KSG_WHATIF_CLASSES=0 off
+    bool use_cls = I.eval_mode == 1 && !I.any_eph_req && I.R <= 4 && I.static_fits && I.max_taints <= 4 &&
+                   I.max_tid < 64 && rec_mb > 0;
+    if (const char* e = std::getenv("KSG_WHATIF_CLASSES")) use_cls &= std::strtol(e, nullptr, 10) != 0;
+    for (uint32_t q = first; use_cls && q < first + count; ++q) {
+      const uint32_t np = (I.prog_need[q] >> 8) & 0xFFu;
+      use_cls = np <= 7 && ((I.max_taints + 1) << np) <= KSG_WC_CLS;
+    }
+    const bool use_rec = !use_cls && rec_mb > 0 && I.R <= 4 && I.static_fits && 100 * wsum < (int64_t)1 << 30;
     // record fields as narrow as the cluster allows: 4-byte records when the raw
     // NodeAffinity (<= the programs' largest weight sum), raw Taint (<= most taints
     // on a node) and Fit/BA sum (<= 100 x their weights) fit 30 bits
@@ -4883,6 +5242,14 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
       }
       if (((size_t)chunk * N * rbytes + 7) / 8 > I.wrec_pairs.n) { err = aerr; return false; }
     }
+    const uint32_t tiles = std::max<uint32_t>((I.N + KSG_WC_TILE - 1) / KSG_WC_TILE, 1);
+    // class path scratch per pod: tiles x (class row + count), folded row + flag
+    const size_t wc_words = (size_t)tiles * KSG_WC_CLS + ((size_t)tiles + 1) / 2 + KSG_WC_CLS + 1;
+    if (use_cls) {
+      const size_t fit = (rec_mb << 20) / (wc_words * 8) / KSG_WC_PODS * KSG_WC_PODS;
+      chunk = (uint32_t)std::min<size_t>(count, std::max<size_t>(fit, KSG_WC_PODS));
+      if (!I.wrec_pairs.alloc((size_t)chunk * wc_words, err)) return false;
+    }
     const dim3 pods((count + 255) / 256);
     hipLaunchKernelGGL(k_init_summaries, pods, dim3(256), 0, s, I.sums.p + first, count, I.F);
     for (uint32_t c0 = 0; c0 < count; c0 += chunk) {
@@ -4897,11 +5264,25 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
                        (a.count + KSG_WI_PODS - 1) / KSG_WI_PODS);
       const dim3 cpods((a.count + 255) / 256);
       const size_t xb = (size_t)a.count * sizeof(ksg_pod_summary);
+      if (use_cls) {
+        a.wc_part = I.wrec_pairs.p;
+        a.wc_cls = a.wc_part + (size_t)a.count * tiles * KSG_WC_CLS;
+        a.wc_cnt = reinterpret_cast<uint32_t*>(a.wc_cls + (size_t)a.count * KSG_WC_CLS);
+        a.wc_flag = a.wc_cnt + (size_t)a.count * tiles;
+      }
+      const dim3 gridc((a.count + KSG_WC_PODS - 1) / KSG_WC_PODS, tiles);
       for (int pass = 1; pass <= 2; ++pass) {
         const bool sampled = I.sample_every != 0 && c0 == 0;
         if (sampled) HIPCHK(hipEventRecord(I.sev[2 * (pass - 1)], s));
         const bool kept_here = I.keep_n && I.keep_first < a.q0 + a.count && I.keep_first + I.keep_n > a.q0;
-        if (pass == 1 && use_rec) {
+        if (pass == 1 && use_cls) {
+          I.path_pods[3]++;
+          hipLaunchKernelGGL(k_whatif_cls1, gridc, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          hipLaunchKernelGGL(k_whatif_cls2, dim3(a.count), dim3(KSG_WC_CLS), 0, s, I.F, a, tiles, I.xranks > 1 ? 1 : 0);
+        } else if (pass == 2 && use_cls) {
+          if (I.xranks > 1) hipLaunchKernelGGL(k_whatif_cls2, dim3(a.count), dim3(KSG_WC_CLS), 0, s, I.F, a, tiles, 2);
+          if (kept_here) hipLaunchKernelGGL(k_whatif<2>, grid, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+        } else if (pass == 1 && use_rec) {
           if (I.eval_mode == 1) {
             if (narrow) hipLaunchKernelGGL((k_whatif_rec1<uint32_t, 1>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
             else hipLaunchKernelGGL((k_whatif_rec1<uint64_t, 1>), grid1, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
@@ -4930,6 +5311,7 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
     }
     I.wi_chunk = chunk;
     I.wi_rec = use_rec;
+    I.wi_cls = use_cls;
     hipLaunchKernelGGL(k_whatif_select, pods, dim3(256), 0, s, A);
     hipLaunchKernelGGL(k_whatif_bind, pods, dim3(256), 0, s, C, A);
   }
@@ -5788,10 +6170,11 @@ bool Engine::set_exchange(int mode, const void* nccl_id, uint32_t rank, uint32_t
 }
 
 uint32_t Engine::exchange_ranks() const { return p_->xranks; }
-void Engine::path_counts(uint64_t out[3]) const {
+void Engine::path_counts(uint64_t out[4]) const {
   out[0] = p_->path_pods[0];
   out[1] = p_->path_pods[1];
   out[2] = p_->path_pods[2];
+  out[3] = p_->path_pods[3];
 }
 
 bool Engine::nccl_unique_id(void* out128, std::string& err) {

@@ -4245,12 +4245,13 @@ extern "C" int ksg_debug_eval_stamps(ksg_ctx* ctx, int on, uint64_t* out, size_t
   return KSG_OK;
 }
 
-// diagnostic (not in ksg.h): pods run through the table chain / the scanning chain so far,
-// and of the first those whose cycle was one launch
-extern "C" int ksg_debug_path_counts(ksg_ctx* ctx, uint64_t* out2) {
+// diagnostic (not in ksg.h): out[4] = pods run through the table chain / the scanning
+// chain so far, of the first those whose cycle was one launch, and what-if pod chunks
+// that ran the class path
+extern "C" int ksg_debug_path_counts(ksg_ctx* ctx, uint64_t* out) {
   KSG_LOCK(ctx);
-  if (!ctx || !out2) return KSG_E_INVALID;
-  ctx->c.eng->path_counts(out2);
+  if (!ctx || !out) return KSG_E_INVALID;
+  ctx->c.eng->path_counts(out);
   return KSG_OK;
 }
 

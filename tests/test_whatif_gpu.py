@@ -121,12 +121,17 @@ def test_folded_partials_match_oracle(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"KSG_WHATIF_REC_MB": "0"}, {"KSG_WHATIF_REC_MB": "1"}, {"KSG_WHATIF_WIDE": "1"}],
-                         ids=["recompute", "chunked-records", "8-byte-records"])
+@pytest.mark.parametrize("env", [{"KSG_WHATIF_REC_MB": "0"}, {"KSG_WHATIF_REC_MB": "1"}, {"KSG_WHATIF_WIDE": "1"},
+                                 {}],
+                         ids=["recompute", "chunked-records", "8-byte-records", "classes"])
 def test_whatif_pass_records(monkeypatch, env):
-    """Pass 2 normally reads pass 1's 4-byte per-pair records; forced here to
-    recompute every pair, to split the step into record chunks (1 MiB: 64 + 32 pods
-    at 1,500 nodes) and to the 8-byte layout, single context and 2-rank sharded."""
+    """The cfg5 profile's steps normally take the class path (no per-pair
+    memory); with it off (KSG_WHATIF_CLASSES=0) pass 2 reads pass 1's 4-byte
+    per-pair records — forced here to recompute every pair, to split the step
+    into record chunks (1 MiB: 64 + 32 pods at 1,500 nodes) and to the 8-byte
+    layout — single context and 2-rank sharded."""
+    if env:
+        monkeypatch.setenv("KSG_WHATIF_CLASSES", "0")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     doc = g.generate(5, n_nodes=1500, n_pods=2 * STEP)
@@ -137,6 +142,7 @@ def test_whatif_pass_records(monkeypatch, env):
     for k in range(2):
         s.whatif(k * STEP, STEP)
     assert [(r.selected, r.feasible, r.status) for r in s.results()] == want
+    assert s.whatif_class_chunks() == (0 if env else 2)
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()

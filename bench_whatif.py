@@ -114,6 +114,7 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
     s.whatif((a.warmup + a.steps) * P, P)
     avg_ms, nsamp = s.kernel_time()  # cfg5: the average of the step's two passes
     s.sample_kernel(0)
+    classes = s.whatif_class_chunks() > 0
     del s
     if rank != 0:
         return None
@@ -121,15 +122,19 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
     shard = a.nodes // world
     # algorithmic bytes per step, SURVEY.md §8(d) basis: cfg5 ~7 B per (pod, node)
     # pair (the node row amortised over a 64-pod tile ~2 B + filter 1 B + total 4 B);
-    # the kernel time is one step's two passes (k_whatif_rec1 + k_whatif_rec2).
-    # Pass 1's 4-byte per-pair record, written and read back by pass 2, is not
-    # algorithmic: it shows up in roofline.traffic (the PMC pass of both kernels).
+    # the kernel time is one step's two passes (HIP events around each, summed).
     bytes_per_launch = 7.0 * shard * P
     kernel_ms = 2 * avg_ms
-    kernel = "k_whatif_rec1 + k_whatif_rec2 (one step)"
-    traffic = pmc_step_traffic(["cfg5:k_whatif_rec1", "cfg5:k_whatif_rec2"])
-    note = ("pass 1 (k_whatif_rec1) program decode per (pod, node tile): SALU issue, "
-            "profiles/*cfg5_pmc_sq.csv; traffic = both passes' HBM bytes (PMC) incl. the record round trip")
+    if classes:  # class path: per-class best keys, nothing per pair in memory
+        kernel = "k_whatif_cls1 + k_whatif_cls2 (one step)"
+        traffic = pmc_step_traffic(["cfg5:k_whatif_cls1", "cfg5:k_whatif_cls2"])
+        note = ("pass 1 (k_whatif_cls1) is VALU / SALU issue bound (profiles/*cfg5_pmc_sq.csv), "
+                "its HBM traffic (PMC) is far below the §8(d) bytes")
+    else:  # record path: pass 1's 4-byte per-pair record, written and read back by pass 2
+        kernel = "k_whatif_rec1 + k_whatif_rec2 (one step)"
+        traffic = pmc_step_traffic(["cfg5:k_whatif_rec1", "cfg5:k_whatif_rec2"])
+        note = ("pass 1 (k_whatif_rec1) program decode per (pod, node tile): SALU issue, "
+                "profiles/*cfg5_pmc_sq.csv; traffic = both passes' HBM bytes (PMC) incl. the record round trip")
     workload = f"cfg5: {a.nodes} nodes, {P} pods/step, TaintToleration+NodeAffinity+Fit+BA"
     if a.variant == "pts-ipa":  # table chain: k_eval reads 68 B per node (row 56, zone id 4, class count 8)
         bytes_per_launch = 88.0 * shard  # + the per-pair filter code and four raw scores it writes

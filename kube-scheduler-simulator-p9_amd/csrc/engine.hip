@@ -2894,9 +2894,8 @@ __global__ __launch_bounds__(256) void k_whatif_rec2(DevCluster C, DevProfile F,
 // Nothing per pair reaches memory.
 #define KSG_WC_CLS 128
 #define KSG_WC_PODS 32
-#define KSG_WC_NPT 2
-#define KSG_WC_SUB 8
-#define KSG_WC_TILE (256 * KSG_WC_NPT * KSG_WC_SUB)
+#define KSG_WC_NPT 2   // default nodes per thread (KSG_WC_NPT=1|2|4)
+#define KSG_WC_TILE 4096  // nodes per block
 
 // Node selector term s on NPT nodes (local, in range) at once: one scalar
 // entry load per requirement for all of them (KPF_FLAT_NA), else node_sel each.
@@ -2958,10 +2957,10 @@ __device__ __forceinline__ void required_na_multi(const DevCluster& C, const Pro
 // Host-checked (run_whatif): default Fit / BA arguments, no resource column
 // beyond cpu / memory requested, <= 4 taints per node with ids < 64, every
 // pod's (taints + 1) << preferred terms <= KSG_WC_CLS.
+template <int NPT>
 __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F, WiArgs A,
                                                      const uint8_t* __restrict__ progs,
                                                      const uint64_t* __restrict__ prog_off) {
-  constexpr int NPT = KSG_WC_NPT;
   __shared__ unsigned long long slot[KSG_WC_PODS][KSG_WC_CLS];
   __shared__ uint32_t wcnt[KSG_WC_PODS];
   const uint32_t tid = threadIdx.x;
@@ -2972,13 +2971,13 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
   __syncthreads();
   const bool hf = F.pos_fit >= 0, hb = F.pos_ba >= 0, ht = F.pos_taint >= 0, ha = F.pos_na >= 0;
 #pragma unroll 1
-  for (uint32_t sub = 0; sub < KSG_WC_SUB; ++sub) {
+  for (uint32_t sub = 0; sub < KSG_WC_TILE / (256 * NPT); ++sub) {
     const uint32_t nb = blockIdx.y * KSG_WC_TILE + sub * (256 * NPT);
     if (nb >= C.N) break;
     uint32_t n[NPT];
     bool live[NPT];
     RowV row[NPT];
-    uint32_t tp[NPT];  // the node's taint ids, one per byte (0xFF: none)
+    uint64_t ts[NPT];  // the node's taints as a set of ids (< 64)
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const uint32_t nn = nb + k * 256 + tid;
@@ -2995,11 +2994,11 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
       r.podcnt = C.podcnt[n[k]];
       r.allowed = C.allowed[n[k]];
       const uint32_t t0 = C.toff[n[k]], tc = C.toff[n[k] + 1] - t0;
-      uint32_t w = 0xFFFFFFFFu;
+      uint64_t w = 0;
 #pragma unroll
       for (uint32_t i = 0; i < 4; ++i)
-        if (i < tc) w = (w & ~(0xFFu << (8 * i))) | ((uint32_t)C.tid[t0 + i] << (8 * i));
-      tp[k] = w;
+        if (i < tc) w |= 1ull << ((uint32_t)C.tid[t0 + i] & 63u);
+      ts[k] = w;
     }
 #pragma unroll 1
     for (uint32_t pi = 0; pi < np; ++pi) {
@@ -3034,16 +3033,9 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
         const uint64_t hw = tw > 1 ? ((uint64_t)hard[1] << 32 | hard[0]) : tw > 0 ? hard[0] : 0;
         const uint64_t pw = tw > 1 ? ((uint64_t)pref[1] << 32 | pref[0]) : tw > 0 ? pref[0] : 0;
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-          bool hit = false;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t t = (tp[k] >> (8 * i)) & 0xFFu;
-            const bool v = t != 0xFFu;
-            hit |= v & (((hw >> (t & 63u)) & 1ull) != 0);
-            xt[k] += (v & (((pw >> (t & 63u)) & 1ull) != 0)) ? 1u : 0u;
-          }
-          pass[k] &= !hit;
+        for (int k = 0; k < NPT; ++k) {  // (a node's taints are distinct: the set counts them)
+          pass[k] &= (ts[k] & hw) == 0;
+          xt[k] = (uint32_t)__popcll(ts[k] & pw);
         }
       }
       if (ha && !(fl & KPF_SKIP_NA_FILTER)) {
@@ -4413,6 +4405,8 @@ struct Engine::Impl {
   bool wi_cls = false;        // ... or the class path
   uint32_t max_taints = 0;  // most taints on one node (what-if record width)
   int32_t max_tid = -1;     // largest taint id on a node (what-if class path: < 64)
+  bool taint_dup = false;   // some node lists a taint twice
+  int wc_npt = KSG_WC_NPT;  // what-if class path: nodes per thread (KSG_WC_NPT)
   int64_t max_na_sum = 0;   // largest preferred NodeAffinity weight sum of a program
   bool static_fits = true; // raw scores fit the record (taints per node < 4096, NodeAffinity weights < 2^20)
   DBuf<StaticRec> stat;   // static records of a chunk of pods [chunk][N]
@@ -4571,6 +4565,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   I.cfg = cfg;
   if (const char* e = std::getenv("KSG_FOLD_BLOCKS")) I.fold_blocks = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_SOLO")) I.solo = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_WC_NPT")) I.wc_npt = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_OCC_BLOCKS")) {
     I.occ_blocks = (uint32_t)std::strtoul(e, nullptr, 10);
     I.occ_force = I.occ_blocks == 0;
@@ -4665,6 +4660,15 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   for (uint32_t i = 0; i < ns.n; ++i) I.max_taints = std::max(I.max_taints, ns.taint_off[i + 1] - ns.taint_off[i]);
   I.max_tid = -1;
   for (int32_t t : ns.taint_id) I.max_tid = std::max(I.max_tid, t);
+  I.taint_dup = false;  // a node listing one taint twice (the class path counts taint sets)
+  for (uint32_t i = 0; i < ns.n && !I.taint_dup && I.max_tid < 64; ++i) {
+    uint64_t seen = 0;
+    for (uint32_t k = ns.taint_off[i]; k < ns.taint_off[i + 1]; ++k) {
+      const uint64_t b = 1ull << (ns.taint_id[k] & 63);
+      I.taint_dup |= (seen & b) != 0;
+      seen |= b;
+    }
+  }
   if (I.max_taints >= 4096) I.static_fits = false;
   I.R = ns.n_res;
   I.K = ns.n_keys;
@@ -5208,7 +5212,7 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
     A.need_eph = I.any_eph_req ? 1u : 0u;
     // the class path (k_whatif_cls1/2): nothing per pair in memory; KSG_WHATIF_CLASSES=0 off
     bool use_cls = I.eval_mode == 1 && !I.any_eph_req && I.R <= 4 && I.static_fits && I.max_taints <= 4 &&
-                   I.max_tid < 64 && rec_mb > 0;
+                   I.max_tid < 64 && !I.taint_dup && rec_mb > 0;
     if (const char* e = std::getenv("KSG_WHATIF_CLASSES")) use_cls &= std::strtol(e, nullptr, 10) != 0;
     for (uint32_t q = first; use_cls && q < first + count; ++q) {
       const uint32_t np = (I.prog_need[q] >> 8) & 0xFFu;
@@ -5277,7 +5281,9 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
         const bool kept_here = I.keep_n && I.keep_first < a.q0 + a.count && I.keep_first + I.keep_n > a.q0;
         if (pass == 1 && use_cls) {
           I.path_pods[3]++;
-          hipLaunchKernelGGL(k_whatif_cls1, gridc, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          if (I.wc_npt == 1) hipLaunchKernelGGL(k_whatif_cls1<1>, gridc, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          else if (I.wc_npt == 4) hipLaunchKernelGGL(k_whatif_cls1<4>, gridc, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          else hipLaunchKernelGGL(k_whatif_cls1<2>, gridc, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
           hipLaunchKernelGGL(k_whatif_cls2, dim3(a.count), dim3(KSG_WC_CLS), 0, s, I.F, a, tiles, I.xranks > 1 ? 1 : 0);
         } else if (pass == 2 && use_cls) {
           if (I.xranks > 1) hipLaunchKernelGGL(k_whatif_cls2, dim3(a.count), dim3(KSG_WC_CLS), 0, s, I.F, a, tiles, 2);

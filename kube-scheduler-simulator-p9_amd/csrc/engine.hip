@@ -2949,18 +2949,43 @@ __device__ __forceinline__ void required_na_multi(const DevCluster& C, const Pro
   }
 }
 
+// A node of the class path's pass 1, held in registers across the block's pods:
+// the columns in doubles (exact: host-checked < 2^45), taints as an id set.
+struct WcNode {
+  double ad0, ad1;  // allocatable cpu / memory
+  double ra0, ra1;  // approximate reciprocals (v_rcp_f64) of ad0 / ad1
+  double fz0, fz1;  // NonZeroRequested cpu / memory (Fit)
+  double rd0, rd1;  // Requested cpu / memory (BalancedAllocation)
+  double fd0, fd1;  // allocatable - requested (Fit's filter)
+  uint64_t ts;      // taint ids (< 64)
+  uint32_t n;       // local node (0 when out of range)
+  bool ok;          // in range and room for one more pod
+};
+// leastRequestedScore floor((a - q) * 100 / a) for integers 0 <= q <= a < 2^45
+// held exactly in doubles: x = (a - q) * 100 < 2^52 is exact, the estimate from
+// the reciprocal is the quotient or one off, the fma remainder is exact.
+__device__ __forceinline__ double least_req_d(double ad, double ra, double qd) {
+  const double x = (ad - qd) * 100.0;
+  const double d = trunc(x * ra);
+  const double rem = __builtin_fma(-d, ad, x);
+  return rem >= ad ? d + 1.0 : (rem < 0.0 ? d - 1.0 : d);
+}
+
 // Pass 1: grid x = group of KSG_WC_PODS pods (fastest: a tile's rows are shared
-// in L2 by its pod groups), y = tile of KSG_WC_TILE nodes; each thread holds the
-// rows of KSG_WC_NPT nodes in registers while the block's pods go by, so a pod's
-// program is decoded once per 256 pairs of a wave.  The filter and the scores
-// are evaluated without branches per node (pass / fail selects the outcome).
+// in L2 by its pod groups), y = tile of KSG_WC_TILE nodes; each thread holds
+// NPT nodes in registers while the block's pods go by, so a pod's program is
+// decoded once per NPT x 64 pairs of a wave.  The filter and the scores are
+// evaluated without branches per node (pass / fail selects the outcome); a pair
+// whose Fit/BA sum is below its class's best so far skips the tie-break hash.
 // Host-checked (run_whatif): default Fit / BA arguments, no resource column
-// beyond cpu / memory requested, <= 4 taints per node with ids < 64, every
-// pod's (taints + 1) << preferred terms <= KSG_WC_CLS.
+// beyond cpu / memory requested, cpu / memory below 2^45 on the nodes and 2^44
+// in the pods, <= 4 distinct taints per node with ids < 64, every pod's
+// (taints + 1) << preferred terms <= KSG_WC_CLS.
 template <int NPT>
 __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F, WiArgs A,
                                                      const uint8_t* __restrict__ progs,
                                                      const uint64_t* __restrict__ prog_off) {
+#pragma clang fp contract(off)
   __shared__ unsigned long long slot[KSG_WC_PODS][KSG_WC_CLS];
   __shared__ uint32_t wcnt[KSG_WC_PODS];
   const uint32_t tid = threadIdx.x;
@@ -2974,31 +2999,34 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
   for (uint32_t sub = 0; sub < KSG_WC_TILE / (256 * NPT); ++sub) {
     const uint32_t nb = blockIdx.y * KSG_WC_TILE + sub * (256 * NPT);
     if (nb >= C.N) break;
+    WcNode x[NPT];
     uint32_t n[NPT];
-    bool live[NPT];
-    RowV row[NPT];
-    uint64_t ts[NPT];  // the node's taints as a set of ids (< 64)
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const uint32_t nn = nb + k * 256 + tid;
-      live[k] = nn < C.N;
-      n[k] = live[k] ? nn : 0u;
-      RowV& r = row[k];
-      r.alloc[0] = C.alloc[n[k]];
-      r.alloc[1] = C.alloc[(size_t)C.N + n[k]];
-      r.req[0] = C.req[n[k]];
-      r.req[1] = C.req[(size_t)C.N + n[k]];
-      r.alloc[2] = r.req[2] = r.alloc[3] = r.req[3] = 0;
-      r.nzc = C.nzc[n[k]];
-      r.nzm = C.nzm[n[k]];
-      r.podcnt = C.podcnt[n[k]];
-      r.allowed = C.allowed[n[k]];
+      const bool live = nn < C.N;
+      n[k] = live ? nn : 0u;
+      WcNode& v = x[k];
+      v.n = n[k];
+      const int64_t a0 = C.alloc[n[k]], a1 = C.alloc[(size_t)C.N + n[k]];
+      const int64_t r0 = C.req[n[k]], r1 = C.req[(size_t)C.N + n[k]];
+      v.ad0 = (double)a0;
+      v.ad1 = (double)a1;
+      v.ra0 = __builtin_amdgcn_rcp(v.ad0);
+      v.ra1 = __builtin_amdgcn_rcp(v.ad1);
+      v.rd0 = (double)r0;
+      v.rd1 = (double)r1;
+      v.fd0 = (double)(a0 - r0);
+      v.fd1 = (double)(a1 - r1);
+      v.fz0 = (double)C.nzc[n[k]];
+      v.fz1 = (double)C.nzm[n[k]];
+      v.ok = live && !(hf && C.podcnt[n[k]] + 1 > C.allowed[n[k]]);
       const uint32_t t0 = C.toff[n[k]], tc = C.toff[n[k] + 1] - t0;
       uint64_t w = 0;
 #pragma unroll
       for (uint32_t i = 0; i < 4; ++i)
         if (i < tc) w |= 1ull << ((uint32_t)C.tid[t0 + i] & 63u);
-      ts[k] = w;
+      v.ts = w;
     }
 #pragma unroll 1
     for (uint32_t pi = 0; pi < np; ++pi) {
@@ -3008,20 +3036,16 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
       const uint32_t fl = h->flags;
       bool pass[NPT];
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) pass[k] = live[k] && !(fl & KPF_PREFILTER_REJECT);
+      for (int k = 0; k < NPT; ++k) pass[k] = x[k].ok && !(fl & KPF_PREFILTER_REJECT);
       if (fl & KPF_RESTRICT) {
 #pragma unroll
         for (int k = 0; k < NPT; ++k) pass[k] &= bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n[k]);
       }
-      if (hf) {
-        const int64_t q0 = h->req[0], q1 = h->req[1];
+      if (hf) {  // (the pod count was checked with the node)
+        const bool c0 = h->req[0] > 0, c1 = h->req[1] > 0;
+        const double q0 = (double)h->req[0], q1 = (double)h->req[1];
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-          const RowV& r = row[k];
-          const bool bad = (r.podcnt + 1 > r.allowed) | ((q0 > 0) & (q0 > r.alloc[0] - r.req[0])) |
-                           ((q1 > 0) & (q1 > r.alloc[1] - r.req[1]));
-          pass[k] &= !bad;
-        }
+        for (int k = 0; k < NPT; ++k) pass[k] &= !(c0 & (q0 > x[k].fd0)) & !(c1 & (q1 > x[k].fd1));
       }
       uint32_t xt[NPT];
 #pragma unroll
@@ -3034,8 +3058,8 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
         const uint64_t pw = tw > 1 ? ((uint64_t)pref[1] << 32 | pref[0]) : tw > 0 ? pref[0] : 0;
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {  // (a node's taints are distinct: the set counts them)
-          pass[k] &= (ts[k] & hw) == 0;
-          xt[k] = (uint32_t)__popcll(ts[k] & pw);
+          pass[k] &= (x[k].ts & hw) == 0;
+          xt[k] = (uint32_t)__popcll(x[k].ts & pw);
         }
       }
       if (ha && !(fl & KPF_SKIP_NA_FILTER)) {
@@ -3055,25 +3079,48 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
 #pragma unroll
         for (int k = 0; k < NPT; ++k) mask[k] |= (uint32_t)m[k] << t;
       }
+      // Fit (LeastAllocated, cpu:1 memory:1) and BalancedAllocation (cpu, memory)
+      const double fs0 = (double)h->fit_score_req[0], fs1 = (double)h->fit_score_req[1];
+      const double bq0 = (double)h->ba_req[0], bq1 = (double)h->ba_req[1];
+      const uint64_t hseed = F.seed ^ ((uint64_t)(uint32_t)h->queue_idx * 0x9E3779B97F4A7C15ull);
       int cnt = 0;
       bool rng = false;
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
+        const WcNode& v = x[k];
+        const bool ok0 = v.ad0 != 0.0, ok1 = v.ad1 != 0.0;
         int64_t fb = 0;
         bool bad = false;
         if (hf) {
-          const int64_t s = fit_score_row<1>(row[k], F, h);
-          bad |= s < 0 || s > 100;
-          fb += s * F.w_fit;
+          const double q0 = v.fz0 + fs0, q1 = v.fz1 + fs1;
+          const double s0 = (ok0 && v.ad0 > 0.0 && !(q0 > v.ad0)) ? least_req_d(v.ad0, v.ra0, q0) : 0.0;
+          const double s1 = (ok1 && v.ad1 > 0.0 && !(q1 > v.ad1)) ? least_req_d(v.ad1, v.ra1, q1) : 0.0;
+          const int64_t ns = (int64_t)s0 + (int64_t)s1;
+          const int64_t sc = ok0 && ok1 ? ns >> 1 : ns;
+          bad |= sc < 0 || sc > 100;
+          fb += sc * F.w_fit;
         }
         if (hb) {
-          const int64_t s = ba_score_row<1>(row[k], F, h);
-          bad |= s < 0 || s > 100;
-          fb += s * F.w_ba;
+          double sd = 0.0;
+          if (ok0 && ok1) {
+            double f0 = (v.rd0 + bq0) / v.ad0;
+            double f1 = (v.rd1 + bq1) / v.ad1;
+            f0 = f0 > 1 ? 1 : f0;
+            f1 = f1 > 1 ? 1 : f1;
+            sd = fabs((f0 - f1) / 2);
+          }
+          const int64_t sc = (int64_t)((1 - sd) * 100.0);
+          bad |= sc < 0 || sc > 100;
+          fb += sc * F.w_ba;
         }
         const uint32_t c = (xt[k] << npf) | mask[k];
-        const uint64_t key = pack_key(bad ? 0 : fb, F.seed, h->queue_idx, C.goff + n[k]);
-        if (pass[k]) atomicMax(&slot[pi][c], (unsigned long long)key);
+        const uint64_t top = (uint64_t)(bad ? 0 : fb) << 40;
+        // (a lower Fit/BA sum than the class's best so far cannot win the class)
+        if (pass[k] && top >= (slot[pi][c] & ~0xFFFFFFFFFFull)) {
+          const uint32_t g = C.goff + v.n;
+          const uint64_t h20 = splitmix64(hseed ^ (uint64_t)g) >> 44;
+          atomicMax(&slot[pi][c], (unsigned long long)(top | ((0xFFFFFull - h20) << 20) | (uint64_t)g));
+        }
         cnt += pass[k] ? 1 : 0;
         rng |= pass[k] && bad;
       }
@@ -4406,6 +4453,7 @@ struct Engine::Impl {
   uint32_t max_taints = 0;  // most taints on one node (what-if record width)
   int32_t max_tid = -1;     // largest taint id on a node (what-if class path: < 64)
   bool taint_dup = false;   // some node lists a taint twice
+  bool cols_small = false;  // cpu / memory columns of every node (alloc, requested, non-zero) in (-2^45, 2^45)
   int wc_npt = KSG_WC_NPT;  // what-if class path: nodes per thread (KSG_WC_NPT)
   int64_t max_na_sum = 0;   // largest preferred NodeAffinity weight sum of a program
   bool static_fits = true; // raw scores fit the record (taints per node < 4096, NodeAffinity weights < 2^20)
@@ -4660,6 +4708,14 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   for (uint32_t i = 0; i < ns.n; ++i) I.max_taints = std::max(I.max_taints, ns.taint_off[i + 1] - ns.taint_off[i]);
   I.max_tid = -1;
   for (int32_t t : ns.taint_id) I.max_tid = std::max(I.max_tid, t);
+  {
+    const int64_t lim = (int64_t)1 << 45;
+    auto in = [&](int64_t v) { return v > -lim && v < lim; };
+    I.cols_small = ns.n_res >= 2;
+    for (uint32_t i = 0; i < ns.n && I.cols_small; ++i)
+      I.cols_small = in(ns.alloc[i]) && in(ns.alloc[(size_t)ns.n + i]) && in(ns.requested[i]) &&
+                     in(ns.requested[(size_t)ns.n + i]) && in(ns.nz_cpu[i]) && in(ns.nz_mem[i]);
+  }
   I.taint_dup = false;  // a node listing one taint twice (the class path counts taint sets)
   for (uint32_t i = 0; i < ns.n && !I.taint_dup && I.max_tid < 64; ++i) {
     uint64_t seen = 0;
@@ -5151,7 +5207,11 @@ static uint32_t prog_need_of(const ksg_prog* h) {
   uint32_t np = h->n_pref_terms > 7 ? 0xFFu : (uint32_t)h->n_pref_terms;
   for (int t = 0; t < h->n_pref_terms && np != 0xFFu; ++t)
     if (i32[h->pref_w_off + t] < 0) np = 0xFFu;
-  return need | np << 8;
+  // bit 16: cpu / memory requests in [0, 2^44) (the class path's doubles stay exact)
+  bool small = true;
+  for (int c = 0; c < 2; ++c)
+    for (int64_t v : {h->req[c], h->fit_score_req[c], h->ba_req[c]}) small &= v >= 0 && v < ((int64_t)1 << 44);
+  return need | np << 8 | (small ? 1u << 16 : 0u);
 }
 
 static bool exchange(Engine::Impl& I, const void* src, size_t bytes, std::string& err);
@@ -5212,11 +5272,11 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
     A.need_eph = I.any_eph_req ? 1u : 0u;
     // the class path (k_whatif_cls1/2): nothing per pair in memory; KSG_WHATIF_CLASSES=0 off
     bool use_cls = I.eval_mode == 1 && !I.any_eph_req && I.R <= 4 && I.static_fits && I.max_taints <= 4 &&
-                   I.max_tid < 64 && !I.taint_dup && rec_mb > 0;
+                   I.max_tid < 64 && !I.taint_dup && I.cols_small && rec_mb > 0;
     if (const char* e = std::getenv("KSG_WHATIF_CLASSES")) use_cls &= std::strtol(e, nullptr, 10) != 0;
     for (uint32_t q = first; use_cls && q < first + count; ++q) {
       const uint32_t np = (I.prog_need[q] >> 8) & 0xFFu;
-      use_cls = np <= 7 && ((I.max_taints + 1) << np) <= KSG_WC_CLS;
+      use_cls = np <= 7 && ((I.max_taints + 1) << np) <= KSG_WC_CLS && (I.prog_need[q] & (1u << 16));
     }
     const bool use_rec = !use_cls && rec_mb > 0 && I.R <= 4 && I.static_fits && 100 * wsum < (int64_t)1 << 30;
     // record fields as narrow as the cluster allows: 4-byte records when the raw

@@ -197,7 +197,7 @@ class Engine {
   uint32_t exchange_ranks() const;
   // diagnostic: pods the per-pod runs sent down the table chain / the scanning chain /
   // of the table-chain pods, those whose cycle was one launch (k_eval_solo)
-  void path_counts(uint64_t out[4]) const;
+  void path_counts(uint64_t out[6]) const;
   static bool nccl_unique_id(void* out128, std::string& err);
   // diagnostic: enable (out == nullptr, count pods) / read back s_memtime stamps of the fixup loop
   bool fixup_stamps(uint32_t count, std::vector<uint64_t>* out, std::string& err);

@@ -1199,13 +1199,19 @@ __global__ void k_pts_score(DevCluster C, DevScratch S, DevOut O, const uint8_t*
 // max / min over the feasible nodes: every path that selects (k_finalize, the
 // table chain's k_final) and the normalized-score export (k_norm_out) use this.
 // use = false: the plugin's PreScore returned Skip (no score, no weight).
+// PM: the plugins compiled in (table_chain.hip eval_body); a plugin outside it
+// is never met at run time
+template <uint32_t PM = ~0u>
 __device__ __forceinline__ int64_t normalize_pos(int plugin, const ksg_prog* h, int64_t s, int64_t mx, int64_t mn,
                                                  uint32_t ipa_flags, bool pts_keys, bool& use) {
   use = true;
+  if (!((PM >> plugin) & 1u)) return s;
   switch (plugin) {
     case KP_TAINT:  // DefaultNormalizeScore(100, reverse); 0 <= s <= mx
+      if constexpr (!((PM >> KP_TAINT) & 1u)) return s;
       return mx == 0 ? 100 : 100 - div_small(100 * s, mx);
     case KP_NA:  // DefaultNormalizeScore(100, false)
+      if constexpr (!((PM >> KP_NA) & 1u)) return s;
       if (h->flags & KPF_SKIP_NA_SCORE) { use = false; return s; }
       return mx == 0 ? s : div_small(100 * s, mx);
     case KP_PTS:  // 0 <= mn <= s <= mx; nodes missing a key (IgnoredNodes) score 0
@@ -1335,8 +1341,8 @@ __device__ __forceinline__ void tc_add(DevCluster& C, const ksg_exist_term& e, u
 // (sign -1) a node with topology values v: its pod classes and its own affinity
 // terms (part: TP_ALL on local node n; TP_PAIR for another rank's node, n
 // unused).  Items i = lane, lane + lanes, ... (one thread: lane 0 of 1).
-__device__ void tables_assume_v(DevCluster& C, const ProgView& V, uint32_t n, const int32_t v[KSG_MAX_TOPO], int sign,
-                                uint32_t lane, uint32_t lanes, int part) {
+__device__ __forceinline__ void tables_assume_items(DevCluster& C, const ProgView& V, uint32_t n, const int32_t v[KSG_MAX_TOPO],
+                                                    int sign, uint32_t lane, uint32_t lanes, int part) {
   const ksg_prog* h = V.h;
   const uint32_t npm = (uint32_t)h->n_pc_match, ne = (uint32_t)h->n_exist_terms;
   for (uint32_t i = lane; i < npm + ne; i += lanes) {
@@ -1346,6 +1352,13 @@ __device__ void tables_assume_v(DevCluster& C, const ProgView& V, uint32_t n, co
       tc_add(C, V.et[h->exist_terms_off + (i - npm)], n, sign, v, part);
     }
   }
+}
+// (an out-of-line copy for the kernels that assume off their critical path; the
+// persistent chain inlines tables_assume_items: a call spills its live registers
+// and the cluster argument to scratch, microseconds on the pod's critical path)
+__device__ void tables_assume_v(DevCluster& C, const ProgView& V, uint32_t n, const int32_t v[KSG_MAX_TOPO], int sign,
+                                uint32_t lane, uint32_t lanes, int part) {
+  tables_assume_items(C, V, n, v, sign, lane, lanes, part);
 }
 __device__ void tables_assume(DevCluster& C, const ProgView& V, uint32_t n, int sign, uint32_t lane, uint32_t lanes) {
   if (!C.T.on) return;
@@ -4490,6 +4503,12 @@ struct Engine::Impl {
   DBuf<EvalTotals> cetot;
   DBuf<SoloCand> ccand;   // k_eval_solo: classes per block [cnblk][kChain]
   int solo = 0;           // one-launch cycles (k_eval_solo): 0 off, 1 on (KSG_SOLO)
+  int run_on = 1;         // persistent segments (k_chain_run): KSG_RUN=0 turns them off
+  uint32_t run_cap = 0;   // blocks every one of which is resident at once (k_chain_run), 0: not queried yet
+  uint32_t run_min = 2;   // shortest segment launched persistently (KSG_RUN_MIN)
+  DBuf<RunSync> rsync;    // k_chain_run's flag and abort word (zeroed per launch)
+  DBuf<uint64_t> rgran;   // k_chain_run's tagged granules: partial records, then keys [2][kChain][kRunGS] (zeroed per launch)
+  bool run_used = false;  // a persistent segment ran since the last sync (its abort word is checked)
   uint32_t fold_blocks = 256;  // table chain: k_fold above this many blocks (KSG_FOLD_BLOCKS; tests force it)
   uint32_t occ_blocks = 0;     // table chain: occupancy twins above this many blocks (0: 2 per CU; KSG_OCC_BLOCKS)
   bool occ_force = false;
@@ -4544,7 +4563,7 @@ struct Engine::Impl {
   uint32_t sample_every = 0;
   std::vector<hipEvent_t> sev;
   uint32_t n_samples = 0;
-  uint64_t path_pods[4] = {0, 0, 0, 0};  // diagnostic: pods run by the table chain / the scanning chain / of the first, in one launch; what-if pod chunks on the class path
+  uint64_t path_pods[6] = {0, 0, 0, 0, 0, 0};  // diagnostic: pods run by the table chain / the scanning chain / of the first, in one launch; what-if pod chunks on the class path; table-chain pods of persistent segments (k_chain_run) / those segments
   std::vector<Engine::KernelStat> stats;
 
   DevCluster cluster() const {
@@ -4613,6 +4632,8 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   I.cfg = cfg;
   if (const char* e = std::getenv("KSG_FOLD_BLOCKS")) I.fold_blocks = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_SOLO")) I.solo = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_RUN")) I.run_on = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_RUN_MIN")) I.run_min = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("KSG_WC_NPT")) I.wc_npt = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_OCC_BLOCKS")) {
     I.occ_blocks = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -5201,6 +5222,9 @@ static uint32_t prog_need_of(const ksg_prog* h) {
   if (h->n_tsc_filter + h->n_tsc_score > 0) need |= 1;
   if (h->tab & KTAB_ON) need |= 4;
   if (h->tab & KTAB_PTS_MULTI) need |= 8;
+  // bit 17: nothing but the node row and the class tables changes on its assume
+  // (no host ports, volume claims or CSI volumes): a persistent segment may hold it
+  if (h->n_port_own == 0 && h->n_pvc == 0 && h->n_csi == 0) need |= 1u << 17;
   // bits 8..15: preferred NodeAffinity terms of the what-if class path (0xFF: a
   // negative weight or more than 7 terms — the record path)
   const int32_t* i32 = reinterpret_cast<const int32_t*>(reinterpret_cast<const uint8_t*>(h) + h->off_i32);
@@ -5996,8 +6020,66 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
     pending = false;
     CA.log_base = next;
   };
+  uint32_t pmask = 0;  // the profile's device plugins (kernel specialisations)
+  for (int i = 0; i < F.n; ++i) pmask |= 1u << F.plugins[i];
+  // persistent segments (k_chain_run): consecutive eligible pods in one launch
+  auto kept_pod = [&](uint32_t j) { return I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n; };
+  bool run_ok = commit && !xchain && F.has_ext && rowm != 0 && I.run_on != 0;
+  if (run_ok && !I.run_cap) {
+    int occ1 = 0, occ2 = 0;
+    int occ3 = 0, occ4 = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_chain_run<1, ~0u>, kChain, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_chain_run<2, ~0u>, kChain, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_chain_run<2, kPmTab>, kChain, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ4, k_chain_run<2, kPmTabTN>, kChain, 0));
+    const int occ = std::min(std::min(occ1, occ2), std::min(occ3, occ4));
+    // (MI355X_MICROARCH.md: the hardware may admit one block per CU fewer than the query)
+    I.run_cap = occ <= 0 ? 1u : I.n_cus * (uint32_t)(occ >= 2 ? occ - 1 : occ);
+    if (occ <= 0) I.run_on = 0;
+  }
+  run_ok = run_ok && I.run_on != 0 && I.cnblk <= I.run_cap && I.cnblk <= (uint32_t)kChain;
+  auto run_elig = [&](uint32_t j) {
+    const uint32_t nd = I.prog_need[j];
+    return (nd & 4) && !(nd & 8) && (nd & (1u << 17)) && !kept_pod(j);
+  };
+  if (run_ok && (!I.rsync.alloc(1, err) || !I.rgran.alloc((size_t)2 * kChain * kRunGS, err))) return false;
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
+    if (run_ok && run_elig(j)) {
+      uint32_t j1 = j + 1;
+      while (j1 < first + count && run_elig(j1)) ++j1;
+      if (j1 - j >= I.run_min) {
+        CA.q = j;
+        CA.prog = prog;
+        CA.xsend = nullptr;
+        ChainArgs RA = CA;  // (stamps: k_chain_run's own slots)
+        HIPCHK(hipMemsetAsync(I.rsync.p, 0, sizeof(RunSync), s));
+        HIPCHK(hipMemsetAsync(I.rgran.p, 0, (size_t)2 * kChain * kRunGS * sizeof(uint64_t), s));
+        const bool sampled = I.sample_every && I.n_samples * 2 + 2 <= I.sev.size();
+        if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
+        uint64_t* const g1 = I.rgran.p;
+        uint64_t* const g2 = I.rgran.p + (size_t)kChain * kRunGS;
+        const dim3 gr(I.cnblk), bk(kChain);
+        if (rowm == 2 && (pmask & ~kPmTab) == 0)
+          hipLaunchKernelGGL((k_chain_run<2, kPmTab>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
+        else if (rowm == 2 && (pmask & ~kPmTabTN) == 0)
+          hipLaunchKernelGGL((k_chain_run<2, kPmTabTN>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
+        else if (rowm == 2) hipLaunchKernelGGL((k_chain_run<2, ~0u>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
+        else hipLaunchKernelGGL((k_chain_run<1, ~0u>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
+        if (sampled) {
+          HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
+          I.n_samples++;
+        }
+        HIPCHK(hipGetLastError());
+        I.run_used = true;
+        I.path_pods[0] += j1 - j;
+        I.path_pods[4] += j1 - j;
+        I.path_pods[5]++;
+        pending |= (CA.mode & 2) != 0;
+        j = j1 - 1;
+        continue;
+      }
+    }
     if (I.prog_need[j] & 4) {
       I.path_pods[0]++;
       CA.q = j;
@@ -6136,6 +6218,12 @@ bool Engine::sync(std::string& err) {
   HIPCHK(hipStreamSynchronize(I.stream));
   I.hcalls.clear();  // every queued host exchange has run
   if (I.xfail.exchange(0)) { err = "exchange callback failed"; return false; }
+  if (I.run_used) {  // a persistent segment whose poll ran out left the launch early
+    I.run_used = false;
+    uint32_t ab = 0;
+    HIPCHK(hipMemcpy(&ab, I.rsync.p->abort, sizeof(ab), hipMemcpyDeviceToHost));
+    if (ab) { err = "persistent table chain: a gate never completed (blocks not co-resident?)"; return false; }
+  }
   HIPCHK(hipEventElapsedTime(&I.last_ms, I.ev0, I.ev1));
   return true;
 }
@@ -6236,11 +6324,8 @@ bool Engine::set_exchange(int mode, const void* nccl_id, uint32_t rank, uint32_t
 }
 
 uint32_t Engine::exchange_ranks() const { return p_->xranks; }
-void Engine::path_counts(uint64_t out[4]) const {
-  out[0] = p_->path_pods[0];
-  out[1] = p_->path_pods[1];
-  out[2] = p_->path_pods[2];
-  out[3] = p_->path_pods[3];
+void Engine::path_counts(uint64_t out[6]) const {
+  for (int i = 0; i < 6; ++i) out[i] = p_->path_pods[i];
 }
 
 bool Engine::nccl_unique_id(void* out128, std::string& err) {

@@ -4245,9 +4245,10 @@ extern "C" int ksg_debug_eval_stamps(ksg_ctx* ctx, int on, uint64_t* out, size_t
   return KSG_OK;
 }
 
-// diagnostic (not in ksg.h): out[4] = pods run through the table chain / the scanning
-// chain so far, of the first those whose cycle was one launch, and what-if pod chunks
-// that ran the class path
+// diagnostic (not in ksg.h): out[6] = pods run through the table chain / the scanning
+// chain so far, of the first those whose cycle was one launch, what-if pod chunks
+// that ran the class path, table-chain pods of persistent segments (k_chain_run)
+// and those segments
 extern "C" int ksg_debug_path_counts(ksg_ctx* ctx, uint64_t* out) {
   KSG_LOCK(ctx);
   if (!ctx || !out) return KSG_E_INVALID;

@@ -277,8 +277,8 @@ __device__ __forceinline__ void assume_row_atomic(DevCluster& C, const ProgView&
 // selectHost's outcome (the argmax key over every feasible node, the feasible
 // count, status bits) → the summary and the assume delta, by the whole block
 // (the last wave writes the summary and the node row, every lane the class tables).
-__device__ __forceinline__ void chain_commit(DevCluster& C, const ChainArgs& A, const ProgView& V, uint64_t key,
-                                             int32_t feas, int32_t st, uint64_t cs_t0) {
+__device__ __forceinline__ int32_t chain_commit(DevCluster& C, const ChainArgs& A, const ProgView& V, uint64_t key,
+                                                int32_t feas, int32_t st, uint64_t cs_t0) {
   const ksg_prog* h = V.h;
   const uint32_t q = A.q;
   const bool error = (st & 2) || ((st & 4) && feas > 1) || (h->flags & KPF_PREFILTER_ERROR) ||
@@ -303,6 +303,7 @@ __device__ __forceinline__ void chain_commit(DevCluster& C, const ChainArgs& A, 
   if (node >= 0) tables_assume(C, V, (uint32_t)node, +1, threadIdx.x, blockDim.x);
   CS(27);
   if (CS_ON) atomicAdd((unsigned long long*)&A.stamps[63], 1ull);
+  return node;
 }
 
 // selectHost + the assume, by the last-arriving block of the cycle's last
@@ -402,17 +403,43 @@ __device__ __forceinline__ void st_cand(SoloCand* p, const int32_t v[KCP_X], uin
   st_sc1(w + 2, key);
 }
 
-template <int ROWM, bool SOLO = false>
+// What one node's evaluation leaves for the persistent chain (MODE kRun): its raw
+// scores per profile position, feasibility, and the block's reduced record.
+struct EvalOut {
+  int32_t raw[KSG_MAX_PLUGINS];  // (as k_final reads them back from the per-pair scores)
+  bool feasible;
+  uint32_t ipa_flags;
+  ChainRec rec;
+};
+enum { kEval = 0, kSolo = 1, kRun = 2 };  // eval_body modes: k_eval, k_eval_solo, k_chain_run
+// Class-table reads: plain loads in a launch of one cycle; in the persistent chain
+// the tables change under the launch (other blocks' assumes), so every read is an
+// agent-scope (sc1) load of what the assuming block wrote by atomics
+// (MI355X_MICROARCH.md hand-off table, row 3).
+template <int MODE>
+__device__ __forceinline__ int32_t ld_tab(const int32_t* p) {
+  if constexpr (MODE == kRun) return ld_sc1(p);
+  else return *p;
+}
+// PM: the plugins the kernel is compiled for (bit KP_*; ~0u every one).  A launch
+// whose profile uses a subset runs a specialisation without the other plugins'
+// code: the generic evaluation is ~75-130 KB of code, beyond the 64 KB
+// instruction cache two CUs share, and misses it on every cycle.
+#define PMH(p) ((PM >> (p)) & 1u)
+template <int ROWM, int MODE = kEval, uint32_t PM = ~0u>
 __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, const ChainArgs& A,
-                                          const uint8_t* __restrict__ prog) {
-  chain_warm(prog);
+                                          const uint8_t* __restrict__ prog, EvalShared* Lrun = nullptr,
+                                          RowV* rowrun = nullptr, EvalOut* eo = nullptr) {
+  constexpr bool SOLO = MODE == kSolo, RUN = MODE == kRun;
+  if constexpr (!RUN) chain_warm(prog);
   CS_BEGIN;
   CS_GAP(42, 49, 48);
   CS(13);
   const uint32_t q = A.q;
   const ProgView V = view(prog);
   const ksg_prog* h = V.h;
-  __shared__ EvalShared L;
+  __shared__ EvalShared Lown;
+  EvalShared& L = RUN ? *Lrun : Lown;
   uint32_t* of;
   int32_t *os, *ot;
   chain_outs(A, q, C.N, of, os, ot);
@@ -422,8 +449,8 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   int pts_pos = -1, ipa_pos = -1;
   uint32_t xmask = 0;
   for (int p = 0; p < F.n; ++p) {
-    if (F.plugins[p] == KP_PTS) pts_pos = p;
-    if (F.plugins[p] == KP_IPA) ipa_pos = p;
+    if (PMH(KP_PTS) && F.plugins[p] == KP_PTS) pts_pos = p;
+    if (PMH(KP_IPA) && F.plugins[p] == KP_IPA) ipa_pos = p;
     const int x = chain_x(F.plugins[p]);
     if (x >= 0) xmask |= 1u << x;
   }
@@ -436,9 +463,10 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   // totals: plan entry tid).  Consumed only after the lookups are issued.
   const uint32_t ntopo = C.n_topo < KSG_MAX_TOPO ? C.n_topo : KSG_MAX_TOPO;
   int32_t vid[KSG_MAX_TOPO];
-  node_slot_vids(C, nn, vid);
-  RowV row;
-  if (ROWM) load_row(C, nn, A.need_eph, row);
+  if constexpr (!RUN) node_slot_vids(C, nn, vid);  // (k_chain_run: in L.tv for the whole run)
+  RowV rowl;
+  RowV& row = RUN ? *rowrun : rowl;
+  if (ROWM && !RUN) load_row(C, nn, A.need_eph, row);
   uint8_t mpn[KSG_MAX_TSC];
   int32_t mcnt[KSG_MAX_TSC];
 #pragma unroll
@@ -448,7 +476,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     if (pts_f && c < nf && threadIdx.x < (uint32_t)h->tsc[c].nvals) {
       const ksg_tsc& t = h->tsc[c];
       mpn[c] = C.T.pair_node[t.pair_base + threadIdx.x];
-      if (t.eff_cls >= 0) mcnt[c] = C.T.pc_dom[(size_t)t.eff_cls * C.T.NU + (uint32_t)t.nub + threadIdx.x];
+      if (t.eff_cls >= 0) mcnt[c] = ld_tab<MODE>(C.T.pc_dom + (size_t)t.eff_cls * C.T.NU + (uint32_t)t.nub + threadIdx.x);
     }
   }
   int32_t ubv = 0;
@@ -464,14 +492,16 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
         ubbit = (uint32_t)eb;
       }
     }
-    if (threadIdx.x < (uint32_t)h->n_ub) ubv = kind == 1 ? C.T.pc_tot[idx] : C.T.tc_tot[idx];
+    if (threadIdx.x < (uint32_t)h->n_ub) ubv = ld_tab<MODE>(kind == 1 ? C.T.pc_tot + idx : C.T.tc_tot + idx);
   }
   CS(7);
   CS(11);
   CS(12);
+  if constexpr (!RUN) {
 #pragma unroll
-  for (int s = 0; s < KSG_MAX_TOPO; ++s)
-    if ((uint32_t)s < ntopo) L.tv[s * kChain + threadIdx.x] = vid[s];
+    for (int s = 0; s < KSG_MAX_TOPO; ++s)
+      if ((uint32_t)s < ntopo) L.tv[s * kChain + threadIdx.x] = vid[s];
+  }
   const ChainVids tv{L.tv + threadIdx.x};  // (each thread reads back only its own column)
   CS(8);
   // ---- the lookup plan (ksg_look): every class-table count of this node
@@ -486,7 +516,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
       lks[i] = v;
       if (e.kind != KLK_NONE) {
         const uint32_t at = (uint32_t)e.base + ((e.kind == KLK_PC_NODE || e.kind == KLK_TC_NODE) ? nn : (uint32_t)(v < 0 ? 0 : v));
-        lkv[i] = (e.kind == KLK_PC_NODE ? C.T.pc_cnt : e.kind == KLK_PC_DOM ? C.T.pc_dom : C.T.tc_val)[at];
+        lkv[i] = ld_tab<MODE>((e.kind == KLK_PC_NODE ? C.T.pc_cnt : e.kind == KLK_PC_DOM ? C.T.pc_dom : C.T.tc_val) + at);
       }
     }
   }
@@ -503,7 +533,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
       int32_t m = (threadIdx.x < (uint32_t)t.nvals && mpn[c]) ? mcnt[c] : 0x7FFFFFFF;
       for (uint32_t i = threadIdx.x + blockDim.x; i < (uint32_t)t.nvals; i += blockDim.x)  // keys beyond 256 values
         if (C.T.pair_node[t.pair_base + i]) {
-          const int32_t x = t.eff_cls < 0 ? 0 : C.T.pc_dom[(size_t)t.eff_cls * C.T.NU + (uint32_t)t.nub + i];
+          const int32_t x = t.eff_cls < 0 ? 0 : ld_tab<MODE>(C.T.pc_dom + (size_t)t.eff_cls * C.T.NU + (uint32_t)t.nub + i);
           m = x < m ? x : m;
         }
       m = wave_min(m);
@@ -559,53 +589,66 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     for (int pos = 0; pos < F.n; ++pos) {
       uint32_t detail = 0;
       bool fail = false;
-      switch (F.plugins[pos]) {
-        case KP_FIT: {
-          const uint32_t b = ROWM ? fit_filter_row(row, h, C.R) : fit_filter(C, V, n);
-          if (b) { fail = true; detail = b; }
-          break;
-        }
-        case KP_TAINT: {
-          const int32_t t = untolerated_taint(C, V, n);
-          if (t >= 0) { fail = true; detail = (uint32_t)t; }
-          break;
-        }
-        case KP_NA:
-          if (!(h->flags & KPF_SKIP_NA_FILTER) && !required_na(C, V, n)) fail = true;
-          break;
-        case KP_PTS:  // filtering.go: skew = matchNum + selfMatch - minMatchNum > maxSkew
-          if (!(h->flags & KPF_SKIP_PTS_FILTER))
-#pragma unroll
-            for (int c = 0; c < KSG_MAX_TSC; ++c) {
-              if (c >= nf || fail || err) continue;
-              const ksg_tsc& t = h->tsc[c];
-              const int32_t dom = t.dom;
-              if (tv(t.topo) < 0) { fail = true; detail = KSG_PTS_MISSING_LABEL; continue; }
-              if (dom == 0) { err = true; continue; }  // minMatchNum: no domains -> Error
-              const int64_t mn = dom < t.min_domains ? 0 : L.minm[c];
-              if ((int64_t)ptsm[c] + t.self_match - mn > t.max_skew) { fail = true; detail = KSG_PTS_SKEW; }
-            }
-          break;
-        case KP_IPA:  // filtering.go: affinity, anti-affinity, existing pods' anti-affinity
-          if (aff_miss || (h->n_req_aff > 0 && aff_zero && !(!(ipa_flags & 1u) && h->self_matches_all))) {
-            fail = true;
-            detail = KSG_IPA_AFFINITY;
-          } else if (anti_hit) {
-            fail = true;
-            detail = KSG_IPA_ANTI_AFFINITY;
-          } else if ((ipa_flags & 4u) && exist_hit) {
-            fail = true;
-            detail = KSG_IPA_EXISTING_ANTI;
+      switch (F.plugins[pos]) {  // (plugins outside PM compile to nothing)
+        case KP_FIT:
+          if constexpr (PMH(KP_FIT)) {
+            const uint32_t b = ROWM ? fit_filter_row(row, h, C.R) : fit_filter(C, V, n);
+            if (b) { fail = true; detail = b; }
           }
           break;
-        case KP_UNSCHED: fail = unsched_fails(C, V, n); break;
-        case KP_NODENAME: fail = nodename_fails(C, V, n); break;
+        case KP_TAINT:
+          if constexpr (PMH(KP_TAINT)) {
+            const int32_t t = untolerated_taint(C, V, n);
+            if (t >= 0) { fail = true; detail = (uint32_t)t; }
+          }
+          break;
+        case KP_NA:
+          if constexpr (PMH(KP_NA))
+            if (!(h->flags & KPF_SKIP_NA_FILTER) && !required_na(C, V, n)) fail = true;
+          break;
+        case KP_PTS:  // filtering.go: skew = matchNum + selfMatch - minMatchNum > maxSkew
+          if constexpr (PMH(KP_PTS))
+            if (!(h->flags & KPF_SKIP_PTS_FILTER))
+#pragma unroll
+              for (int c = 0; c < KSG_MAX_TSC; ++c) {
+                if (c >= nf || fail || err) continue;
+                const ksg_tsc& t = h->tsc[c];
+                const int32_t dom = t.dom;
+                if (tv(t.topo) < 0) { fail = true; detail = KSG_PTS_MISSING_LABEL; continue; }
+                if (dom == 0) { err = true; continue; }  // minMatchNum: no domains -> Error
+                const int64_t mn = dom < t.min_domains ? 0 : L.minm[c];
+                if ((int64_t)ptsm[c] + t.self_match - mn > t.max_skew) { fail = true; detail = KSG_PTS_SKEW; }
+              }
+          break;
+        case KP_IPA:  // filtering.go: affinity, anti-affinity, existing pods' anti-affinity
+          if constexpr (PMH(KP_IPA)) {
+            if (aff_miss || (h->n_req_aff > 0 && aff_zero && !(!(ipa_flags & 1u) && h->self_matches_all))) {
+              fail = true;
+              detail = KSG_IPA_AFFINITY;
+            } else if (anti_hit) {
+              fail = true;
+              detail = KSG_IPA_ANTI_AFFINITY;
+            } else if ((ipa_flags & 4u) && exist_hit) {
+              fail = true;
+              detail = KSG_IPA_EXISTING_ANTI;
+            }
+          }
+          break;
+        case KP_UNSCHED:
+          if constexpr (PMH(KP_UNSCHED)) fail = unsched_fails(C, V, n);
+          break;
+        case KP_NODENAME:
+          if constexpr (PMH(KP_NODENAME)) fail = nodename_fails(C, V, n);
+          break;
         case KP_PORTS:
-          if (!(h->flags & KPF_SKIP_PORTS)) fail = ports_fail(C, V, n);
+          if constexpr (PMH(KP_PORTS))
+            if (!(h->flags & KPF_SKIP_PORTS)) fail = ports_fail(C, V, n);
           break;
         case KP_VOLUMES:
-          detail = volume_filter(C, V, pos, n);
-          fail = detail != 0;
+          if constexpr (PMH(KP_VOLUMES)) {
+            detail = volume_filter(C, V, pos, n);
+            fail = detail != 0;
+          }
           break;
         default: break;
       }
@@ -616,7 +659,8 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     }
   }
   const bool feasible = active && code == KSG_FILTER_PASS;
-  if (!SOLO && active) of[n] = code;
+  const bool kept_run = RUN && A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n;
+  if ((MODE == kEval || kept_run) && active) of[n] = code;
   CS(3);
   counted &= feasible;
   ChainRec rec;
@@ -625,6 +669,10 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   bool range_err = false;
   int64_t sa = 0;                           // SOLO: A, the plugins without ScoreExtensions
   int64_t cv[KCP_X] = {0, 0, 0, 0};         // SOLO: the node's class (raw scores per normalised slot)
+  if constexpr (RUN) {
+#pragma unroll
+    for (int i = 0; i < KSG_MAX_PLUGINS; ++i) eo->raw[i] = 0;
+  }
   if (feasible) {
 #pragma unroll 1
     for (int pos = 0; pos < F.n; ++pos) {
@@ -632,21 +680,34 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
       int64_t sc = 0;
       switch (p) {
         case KP_FIT:
-          sc = ROWM == 2 ? fit_score_row<1>(row, F, h) : ROWM == 1 ? fit_score_row<0>(row, F, h) : fit_score(C, F, V, n);
+          if constexpr (PMH(KP_FIT))
+            sc = ROWM == 2 ? fit_score_row<1>(row, F, h) : ROWM == 1 ? fit_score_row<0>(row, F, h) : fit_score(C, F, V, n);
           break;
         case KP_BA:
-          sc = ROWM == 2 ? ba_score_row<1>(row, F, h) : ROWM == 1 ? ba_score_row<0>(row, F, h) : ba_score(C, F, V, n);
+          if constexpr (PMH(KP_BA))
+            sc = ROWM == 2 ? ba_score_row<1>(row, F, h) : ROWM == 1 ? ba_score_row<0>(row, F, h) : ba_score(C, F, V, n);
           break;
-        case KP_TAINT: sc = taint_score(C, V, n); break;
-        case KP_NA: sc = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n); break;
-        case KP_IMAGE: sc = image_score(C, V, n); break;
+        case KP_TAINT:
+          if constexpr (PMH(KP_TAINT)) sc = taint_score(C, V, n);
+          break;
+        case KP_NA:
+          if constexpr (PMH(KP_NA)) sc = (h->flags & KPF_SKIP_NA_SCORE) ? 0 : na_score(C, V, n);
+          break;
+        case KP_IMAGE:
+          if constexpr (PMH(KP_IMAGE)) sc = image_score(C, V, n);
+          break;
         case KP_IPA: sc = ipa_raw; break;  // scoring.go: the topology score map at the node's pairs
         case KP_PTS:  // the count of the single score constraint (or a placeholder); -1: ignored node
           sc = !pts_score ? 0 : (!counted ? -1 : ((h->tab & KTAB_PTS_MULTI) ? 0 : pts_cnt));
           break;
         default: break;
       }
-      if (!SOLO) os[(size_t)pos * C.N + n] = (int32_t)sc;
+      if (MODE == kEval || kept_run) os[(size_t)pos * C.N + n] = (int32_t)sc;
+      if constexpr (RUN) {
+#pragma unroll
+        for (int i = 0; i < KSG_MAX_PLUGINS; ++i)
+          if (i == pos) eo->raw[i] = (int32_t)sc;
+      }
       const int x = chain_x(p);
       if (x >= 0 && (p != KP_PTS || counted)) rec_minmax(rec, x, sc);
       if (SOLO) {
@@ -684,6 +745,13 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     rec.key = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
   }
   CS(4);
+  if constexpr (RUN) {  // the block's record; the caller publishes it
+    rec_block(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);
+    eo->feasible = feasible;
+    eo->ipa_flags = ipa_flags;
+    eo->rec = rec;
+    return;
+  }
   if (SOLO) {
     __shared__ SoloShared S;
     if (threadIdx.x < kSoloCap) {
@@ -807,15 +875,21 @@ __device__ __forceinline__ void eval_weights(const DevCluster& C, const ksg_prog
   const ChainRec& r = E.r;
   const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
 #pragma unroll
-  for (int c = 0; c < KSG_MAX_TSC; ++c) {  // scoring.go initPreScoreState topoSize
-    E.w[c] = 0;
-    if (c >= ns) continue;
+  for (int c = 0; c < KSG_MAX_TSC; ++c) E.w[c] = 0;
+#pragma unroll 1
+  for (int c = 0; c < ns; ++c) {  // scoring.go initPreScoreState topoSize (one go_log in the code, not eight)
     const ksg_tsc& t = h->tsc[nf + c];
+    uint64_t reg = 0;
+#pragma unroll
+    for (int i = 0; i < KSG_MAX_TSC; ++i) reg = i == c ? r.reg[i] : reg;
     int64_t size = 0;  // hostname: filtered - ignored nodes; else the key's registered values
     if (t.is_hostname) size = (int64_t)r.feas - r.ign;
     else if (t.first_of_key)  // a key with one node per value registers one value per counted node
-      size = ((C.T.uniq >> t.topo) & 1u) ? (int64_t)r.feas - r.ign : (int64_t)__popcll(r.reg[c]);
-    E.w[c] = go_log((double)(size + 2));
+      size = ((C.T.uniq >> t.topo) & 1u) ? (int64_t)r.feas - r.ign : (int64_t)__popcll(reg);
+    const double w = go_log((double)(size + 2));
+#pragma unroll
+    for (int i = 0; i < KSG_MAX_TSC; ++i)
+      if (i == c) E.w[i] = w;
   }
 }
 __device__ __forceinline__ void reduce_eval(const DevCluster& C, const DevProfile& F, const ChainArgs& A, const ksg_prog* h,
@@ -1287,6 +1361,341 @@ __device__ __forceinline__ void final_body(DevCluster& C, const DevProfile& F, c
   chain_last_select(C, F, A, L.rec, prog);
 }
 
+// ---- The persistent chain (k_chain_run): a segment of consecutive table-chain
+// pods in ONE launch, the pod loop on the device.  One block
+// per tile of kChain nodes (at most kChain blocks), every block resident (the host
+// checks the grid against the occupancy query); each block keeps its nodes'
+// topology values in LDS and their rows in registers for the whole segment.  Per
+// pod k, with no grid barrier:
+//   eval    as k_eval (class-table counts read sc1: assumes change them under the
+//           launch); the block's partial record goes out as tagged granules;
+//   fold    every block polls every block's partial granules until their tags
+//           read k + 1, folds them (normalisers, PodTopologySpread weights), then
+//           NormalizeScore / weights / packed key of its own nodes; its best key
+//           goes out as tagged granules;
+//   select  every block polls every block's key granules and takes the same
+//           argmax (selectHost); block 0 writes the summary; the block owning the
+//           selected node applies the assume — the node row (its register copy and
+//           the global row), the class-table deltas with the node's topology values
+//           from its LDS — drains those atomics and raises the pod's flag;
+//   the other blocks wait for that flag only before pod k + 1's class-table reads
+//   (the next program header is pulled into the scalar cache meanwhile).
+// Granule = one 8-byte {data, tag} written by ONE sc1 store and read by sc1
+// loads (MI355X_MICROARCH.md: R2 granules need no ordering; the flag hand-off is
+// table row 1).  Every poll is bounded: a block that waits ~seconds raises
+// `abort`, the others leave at their next poll, the host reports the run failed.
+// Eligible pods (host): table chain, at most one PodTopologySpread score
+// constraint, no host ports / volume claims / CSI volumes (nothing but the rows
+// and the class tables changes during the segment), outputs not kept, committing
+// cycles of an unsharded context whose profile normalises.
+struct RunSync {
+  uint64_t flag[16];   // k + 1: pod k's assume is applied (written by the owning block)
+  uint32_t abort[32];  // a poll ran out: every block leaves
+};
+constexpr uint32_t kRunSpin = 1u << 22;  // polls (~1 us each with the load) before a block gives up
+constexpr int kRunSleep = 8;             // s_sleep between polls (x 64 cycles): every block polls every block
+constexpr int kRunG1 = 2 + 4 * KCP_X + 2 * KSG_MAX_TSC;  // partial-record granules per block (max)
+constexpr int kRunG2 = 3;                                // key granules per block
+constexpr int kRunGS = 64;                               // granule stride per block (uint64)
+__device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t v) { return ((uint64_t)tag << 32) | v; }
+__device__ __forceinline__ bool run_aborted(uint32_t i, const RunSync* Y) {
+  return (i & 63u) == 63u && ld_sc1(&Y->abort[0]) != 0u;
+}
+__device__ __forceinline__ void run_raise(RunSync* Y) {
+  __hip_atomic_store(&Y->abort[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+struct RunShared {
+  EvalShared L;
+  uint32_t go;  // LDS broadcast of a poll's outcome
+};
+// The block record's granule i (wave 0 lanes; every thread holds the record).
+__device__ __forceinline__ uint32_t run_g1_value(const ChainRec& r, int i, uint32_t xmask, int ns) {
+  uint32_t v = 0;
+  if (i == 0) v = (uint32_t)r.feas | ((uint32_t)r.ign << 16);
+  if (i == 1) v = (uint32_t)r.st;
+  int j = 2;
+#pragma unroll
+  for (int x = 0; x < KCP_X; ++x)
+    if ((xmask >> x) & 1u) {
+      if (i == j) v = (uint32_t)(uint64_t)r.mx[x];
+      if (i == j + 1) v = (uint32_t)((uint64_t)r.mx[x] >> 32);
+      if (i == j + 2) v = (uint32_t)(uint64_t)r.mn[x];
+      if (i == j + 3) v = (uint32_t)((uint64_t)r.mn[x] >> 32);
+      j += 4;
+    }
+#pragma unroll
+  for (int c = 0; c < KSG_MAX_TSC; ++c)
+    if (c < ns) {
+      if (i == j) v = (uint32_t)r.reg[c];
+      if (i == j + 1) v = (uint32_t)(r.reg[c] >> 32);
+      j += 2;
+    }
+  return v;
+}
+__device__ __forceinline__ int run_g1_count(uint32_t xmask, int ns) { return 2 + 4 * __popc(xmask) + 2 * ns; }
+__device__ __forceinline__ bool gtag(uint64_t g, uint32_t tag) { return (uint32_t)(g >> 32) == tag; }
+__device__ __forceinline__ int64_t g64(uint64_t lo, uint64_t hi) { return (int64_t)((uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32)); }
+// thread t < NB: block t's partial record, polled until every granule carries tag
+__device__ __forceinline__ bool run_read_g1(const uint64_t* g, uint32_t tag, uint32_t xmask, int ns, ChainRec& r,
+                                            const RunSync* Y) {
+  const int last = run_g1_count(xmask, ns) - 1;
+  for (uint32_t it = 0; it < kRunSpin; ++it) {
+    // one granule per poll until it carries the tag (few loads in flight chip-wide),
+    // then the whole record (whose tags are checked again)
+    if (!gtag(ld_sc1(g + last), tag)) {
+      if (run_aborted(it, Y)) return false;
+      __builtin_amdgcn_s_sleep(kRunSleep);
+      continue;
+    }
+    bool ok = true;
+    const uint64_t w0 = ld_sc1(g), w1 = ld_sc1(g + 1);
+    ok &= gtag(w0, tag) && gtag(w1, tag);
+    int j = 2;
+#pragma unroll
+    for (int x = 0; x < KCP_X; ++x)
+      if ((xmask >> x) & 1u) {
+        const uint64_t a = ld_sc1(g + j), b = ld_sc1(g + j + 1), c = ld_sc1(g + j + 2), d = ld_sc1(g + j + 3);
+        ok &= gtag(a, tag) && gtag(b, tag) && gtag(c, tag) && gtag(d, tag);
+        r.mx[x] = g64(a, b);
+        r.mn[x] = g64(c, d);
+        j += 4;
+      }
+#pragma unroll
+    for (int c = 0; c < KSG_MAX_TSC; ++c)
+      if (c < ns) {
+        const uint64_t a = ld_sc1(g + j), b = ld_sc1(g + j + 1);
+        ok &= gtag(a, tag) && gtag(b, tag);
+        r.reg[c] = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)b << 32);
+        j += 2;
+      }
+    r.feas = (int32_t)((uint32_t)w0 & 0xFFFFu);
+    r.ign = (int32_t)(((uint32_t)w0 >> 16) & 0xFFFFu);
+    r.st = (int32_t)(uint32_t)w1;
+    if (ok) return true;
+    if (run_aborted(it, Y)) return false;
+    __builtin_amdgcn_s_sleep(kRunSleep);
+  }
+  run_raise(const_cast<RunSync*>(Y));
+  return false;
+}
+
+template <int ROWM, uint32_t PM>
+__device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, const ChainArgs& A0, uint32_t count,
+                                         RunSync* Y, uint64_t* G1, uint64_t* G2) {
+  static_assert(ROWM != 0, "the persistent chain keeps the node row in registers");
+  __shared__ RunShared S;
+  EvalShared& L = S.L;
+  const uint32_t NB = A0.nblk, b = blockIdx.x;
+  const uint32_t n = b * kChain + threadIdx.x;
+  const bool active = n < C.N;
+  const uint32_t nn = active ? n : 0;
+  {
+    int32_t vid[KSG_MAX_TOPO];
+    node_slot_vids(C, nn, vid);
+#pragma unroll
+    for (int s = 0; s < KSG_MAX_TOPO; ++s)
+      if ((uint32_t)s < C.n_topo) L.tv[s * kChain + threadIdx.x] = vid[s];
+  }
+  RowV row;
+  load_row(C, nn, A0.need_eph, row);
+  uint32_t xmask = 0;
+  for (int p = 0; p < F.n; ++p) {
+    const int x = chain_x(F.plugins[p]);
+    if (x >= 0) xmask |= 1u << x;
+  }
+  // diagnostic stamps (Engine::eval_stamps): block 0's phase ends since the pod's
+  // start, slots 30..34, pods 35; the owner's commit time 36, commits 37; block
+  // 0's wait for the previous pod's flag 38
+  uint64_t* const rst = A0.stamps;
+  const bool rs_on = rst && b == 0 && threadIdx.x == 0;
+  uint64_t rs_t0 = 0;
+#define RS(k) \
+  if (rs_on) atomicAdd((unsigned long long*)&rst[k], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - rs_t0))
+  __syncthreads();
+  uint32_t wait_for = 0;  // the flag value this block needs before its next class-table read (0: none)
+  for (uint32_t k = 0; k < count; ++k) {
+    ChainArgs A = A0;  // (A.stamps: eval_body's own k_eval slots, block 0)
+    A.q = A0.q + k;
+    const uint8_t* prog = A.progs + A.prog_off[A.q];
+    const uint32_t tag = k + 1u;
+    if (wait_for) {  // the previous pod's assume, applied by the block owning its node
+      if (threadIdx.x == 0) {
+        const uint64_t w0 = rs_on ? __builtin_amdgcn_s_memrealtime() : 0;
+        bool ok = false;
+        for (uint32_t it = 0; it < kRunSpin; ++it) {
+          if (ld_sc1(&Y->flag[0]) >= wait_for) { ok = true; break; }
+          if (run_aborted(it, Y)) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) run_raise(Y);
+        S.go = ok ? 1u : 0u;
+        if (rs_on) atomicAdd((unsigned long long*)&rst[38], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - w0));
+      } else if (threadIdx.x == 64) {  // (another wave: the program header into the scalar cache meanwhile)
+        chain_warm(prog);
+      }
+      __syncthreads();
+      if (!S.go) return;
+      wait_for = 0;
+    }
+    if (rs_on) rs_t0 = __builtin_amdgcn_s_memrealtime();
+    const ProgView V = view(prog);
+    const ksg_prog* h = V.h;
+    // ---- eval: this block's nodes, its partial record
+    EvalOut eo;
+    eval_body<ROWM, kRun, PM>(C, F, A, prog, &L, &row, &eo);
+    const int ns = h->n_tsc_score;
+    const int ng1 = run_g1_count(xmask, ns);
+    if (threadIdx.x < (uint32_t)ng1) st_sc1(G1 + (size_t)b * kRunGS + threadIdx.x, gran(tag, run_g1_value(eo.rec, (int)threadIdx.x, xmask, ns)));
+    RS(30);
+    // ---- fold every block's partials (as reduce_eval)
+    EvalTotals E;
+    {
+      ChainRec& r = E.r;
+      rec_init(r);
+      bool ok = true;
+      if (threadIdx.x < NB) ok = run_read_g1(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y);
+      if (__syncthreads_or(!ok)) return;
+      RS(31);
+      rec_block(r, L.rec, xmask, ns, RB_CNT | RB_ST);
+      eval_weights(C, h, E);
+    }
+    RS(32);
+    int64_t pmx = INT64_MIN, pmn = INT64_MAX;  // single score constraint: raw is monotone in the count
+    if (E.r.mx[KCX_PTS] != INT64_MIN) {
+      pmx = pts_raw1(h, E, E.r.mx[KCX_PTS]);
+      pmn = pts_raw1(h, E, E.r.mn[KCX_PTS]);
+    }
+    int64_t smx[KSG_MAX_PLUGINS], smn[KSG_MAX_PLUGINS];
+    chain_norms(F, h, E, smx, smn, pmx, pmn);
+    if (b == 0 && threadIdx.x == 0) chain_summary(A, F, h, E, smx, smn, eo.ipa_flags);
+    // ---- NormalizeScore, weights, packed key of this block's nodes (final_body)
+    ChainRec r;
+    rec_init(r);
+    if (eo.feasible) {
+      int64_t tot = 0;
+      bool range_err = false;
+#pragma unroll
+      for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+        if (pos >= F.n) continue;
+        const int p = F.plugins[pos];
+        int64_t sv = eo.raw[pos];
+        bool pts_keys = false;
+        if (p == KP_PTS) {
+          pts_keys = sv >= 0 && ns > 0;
+          if (sv < 0) sv = 0;
+          else if (ns > 0 && !(h->flags & KPF_SKIP_PTS_SCORE)) sv = pts_raw1(h, E, sv);
+        }
+        bool use;
+        const int64_t v = normalize_pos<PM>(p, h, sv, smx[pos], smn[pos], eo.ipa_flags, pts_keys, use);
+        if (use) {
+          if (v < 0 || v > 100) range_err = true;
+          tot += v * F.weight[pos];
+        }
+      }
+      if (E.r.feas == 1) tot = 0;  // single feasible node: no scoring
+      r.key = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
+      r.st = (E.r.feas > 1 && range_err) ? 4 : 0;
+    }
+    __syncthreads();  // (L.rec reused)
+    rec_block(r, L.rec, 0u, 0, RB_ST | RB_KEY);
+    if (threadIdx.x < (uint32_t)kRunG2) {
+      const uint32_t v = threadIdx.x == 0 ? (uint32_t)r.key : threadIdx.x == 1 ? (uint32_t)(r.key >> 32) : (uint32_t)r.st;
+      st_sc1(G2 + (size_t)b * kRunGS + threadIdx.x, gran(tag, v));
+    }
+    RS(33);
+    // ---- selectHost: every block takes the argmax of every block's key
+    ChainRec sk;
+    rec_init(sk);
+    {
+      bool ok = true;
+      if (threadIdx.x < NB) {
+        const uint64_t* g = G2 + (size_t)threadIdx.x * kRunGS;
+        ok = false;
+        for (uint32_t it = 0; it < kRunSpin; ++it) {
+          const uint64_t d = ld_sc1(g + 2);
+          const uint64_t a = gtag(d, tag) ? ld_sc1(g) : 0, c = gtag(d, tag) ? ld_sc1(g + 1) : 0;
+          if (gtag(a, tag) && gtag(c, tag) && gtag(d, tag)) {
+            sk.key = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)c << 32);
+            sk.st = (int32_t)(uint32_t)d;
+            ok = true;
+            break;
+          }
+          if (run_aborted(it, Y)) break;
+          __builtin_amdgcn_s_sleep(kRunSleep);
+        }
+        if (!ok && !ld_sc1(&Y->abort[0])) run_raise(Y);
+      }
+      if (__syncthreads_or(!ok)) return;
+    }
+    rec_block(sk, L.rec, 0u, 0, RB_ST | RB_KEY);
+    RS(34);
+    const int32_t feas = E.r.feas, st = E.r.st | sk.st;
+    const bool error = (st & 2) || ((st & 4) && feas > 1) || (h->flags & KPF_PREFILTER_ERROR) || na_prescore_error(h->flags, feas);
+    const uint32_t g = (uint32_t)(sk.key & 0xFFFFFull);
+    int32_t node = -1;
+    if (!error && feas > 0 && (A.mode & 1) && g >= C.goff && g - C.goff < C.N) node = (int32_t)(g - C.goff);
+    if (b == 0 && threadIdx.x == 0) {  // the summary (chain_commit's)
+      ksg_pod_summary* Sm = A.sums + A.q;
+      Sm->feasible = feas;
+      Sm->best_key = sk.key;
+      if (error) { Sm->status = 2; Sm->selected = -1; }
+      else if (feas == 0) { Sm->status = 1; Sm->selected = -1; }
+      else { Sm->status = 0; Sm->selected = (int32_t)g; }
+      A.prow[A.q] = -1;
+      A.alog[A.q - A.log_base] = make_int2((int)A.q, node >= 0 && (A.mode & 2) ? node : -1);
+    }
+    if (node >= 0) {
+      if ((uint32_t)node / kChain == b) {  // ---- the owner applies the assume
+        const uint64_t c0 = rst && threadIdx.x == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
+        const uint32_t ln = (uint32_t)node % kChain;
+        if (threadIdx.x == ln) {  // the register row (assume_row_atomic's delta) and the global row
+#pragma unroll
+          for (uint32_t c = 0; c < 4; ++c)
+            if (c < C.R && (c < 2 || A.need_eph)) row.req[c] += h->req[c];
+          row.nzc += h->nz_cpu;
+          row.nzm += h->nz_mem;
+          row.podcnt += 1;
+          assume_row_atomic(C, V, (uint32_t)node, +1);
+        }
+        if (C.T.on && threadIdx.x < (uint32_t)(h->n_pc_match + h->n_exist_terms)) {
+          int32_t v[KSG_MAX_TOPO];
+#pragma unroll
+          for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? L.tv[s * kChain + ln] : -1;
+          tables_assume_items(C, V, (uint32_t)node, v, +1, threadIdx.x, kChain, TP_ALL);
+        }
+        if (rst && threadIdx.x == 0) {
+          atomicAdd((unsigned long long*)&rst[44], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - c0));
+          atomicAdd((unsigned long long*)&rst[46], (unsigned long long)(h->n_pc_match + h->n_exist_terms));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's assume atomics performed
+        if (rst && threadIdx.x == 0)
+          atomicAdd((unsigned long long*)&rst[45], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - c0));
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          st_sc1(&Y->flag[0], (uint64_t)tag);
+          if (rst) {
+            atomicAdd((unsigned long long*)&rst[36], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - c0));
+            atomicAdd((unsigned long long*)&rst[37], 1ull);
+          }
+        }
+      } else {
+        wait_for = tag;
+      }
+    }
+    if (rs_on) atomicAdd((unsigned long long*)&rst[35], 1ull);
+  }
+#undef RS
+}
+// Plugin sets with a specialisation (PM): the PodTopologySpread / InterPodAffinity
+// profile of cfg4 (with or without TaintToleration / NodeAffinity), every plugin.
+constexpr uint32_t kPmTab = (1u << KP_FIT) | (1u << KP_BA) | (1u << KP_PTS) | (1u << KP_IPA);
+constexpr uint32_t kPmTabTN = kPmTab | (1u << KP_TAINT) | (1u << KP_NA);
+template <int ROWM, uint32_t PM>
+__global__ __launch_bounds__(kChain) void k_chain_run(DevCluster C, DevProfile F, ChainArgs A, uint32_t count, RunSync* Y,
+                                                      uint64_t* G1, uint64_t* G2) {
+  run_body<ROWM, PM>(C, F, A, count, Y, G1, G2);
+}
+
 // Kernels.  The *_occ twins cap registers at 4 waves per SIMD (a few spills)
 // for clusters of many blocks per CU; the plain ones keep every register for
 // the latency of one block per CU (cfg4).
@@ -1302,7 +1711,7 @@ __global__ __launch_bounds__(kChain) __attribute__((amdgpu_waves_per_eu(4))) voi
 template <int ROWM>
 __global__ __launch_bounds__(kChain) void k_eval_solo(DevCluster C, DevProfile F, ChainArgs A,
                                                       const uint8_t* __restrict__ prog) {
-  eval_body<ROWM, true>(C, F, A, prog);
+  eval_body<ROWM, kSolo>(C, F, A, prog);
 }
 __global__ __launch_bounds__(kChain) void k_final(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
   final_body(C, F, A, prog);

@@ -205,6 +205,7 @@ def test_one_launch_cycles_match_oracle(monkeypatch, c, sizes):
     are not kept: placements identical to the oracle's, and the cycles really ran
     one-launch (path counter)."""
     monkeypatch.setenv("KSG_SOLO", "1")
+    monkeypatch.setenv("KSG_RUN", "0")  # (persistent segments take these pods first)
     doc = g.generate(c, **sizes)
     o, s = run_both(doc, keep=False)
     res = s.results()
@@ -213,3 +214,46 @@ def test_one_launch_cycles_match_oracle(monkeypatch, c, sizes):
     assert not bad, f"{len(bad)} pods differ, first {bad[:5]}"
     pc = s.path_counts(solo=True)
     assert pc[2] > 0 or pc[0] == 0, pc  # table-chain pods went one-launch
+
+
+RUN_CASES = [
+    ("cfg4-1block", 4, dict(n_nodes=200, n_existing=600, n_pods=160, n_zones=4), None),
+    ("cfg4-3blocks", 4, dict(n_nodes=600, n_existing=1500, n_pods=300, n_zones=8), None),
+    ("cfg4-20blocks-kept-middle", 4, dict(n_nodes=5000, n_existing=12000, n_pods=240, n_zones=16), (100, 7)),
+    ("cfg4-saturating", 4, dict(n_nodes=64, n_existing=300, n_pods=900, n_zones=4), None),
+    ("cfg1-default-profile", 1, dict(n_nodes=300, n_pods=200), None),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,c,sizes,keep", RUN_CASES, ids=[c[0] for c in RUN_CASES])
+def test_persistent_segments_match_oracle(name, c, sizes, keep):
+    """Persistent segments (k_chain_run: the pod loop inside one launch, gates
+    between blocks) place every pod exactly as the oracle, with 1, 3 and 20
+    blocks (XCD groups of unequal size), around kept pods that split a segment,
+    and on a saturating cluster (unschedulable pods in the middle of a segment)."""
+    doc = g.generate(c, **sizes)
+    o = Oracle(doc)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    if keep:
+        s.keep_outputs(*keep)
+        o.schedule(keep[0], record=0)
+        o.schedule(keep[1], record=3)
+        o.schedule(s.queue_len - keep[0] - keep[1], record=0)
+    else:
+        o.schedule(record=0)
+    s.schedule()
+    res = s.results()
+    bad = [(q, (r.selected, r.feasible, r.status), o.result(q)) for q, r in enumerate(res)
+           if (r.selected, r.feasible, r.status) != o.result(q)]
+    assert not bad, f"{name}: {len(bad)} pods differ, first {bad[:5]}"
+    if keep:
+        for q in range(keep[0], keep[0] + keep[1]):
+            a, b = s.annotations(q), o.annotations(q)
+            for k in b:
+                assert a.get(k) == b[k], f"{name} pod {q} annotation {k}"
+    table, _ = s.path_counts()
+    run_pods, segs = s.run_counts()
+    if table:
+        assert run_pods > 0 and segs > 0, (table, run_pods, segs)

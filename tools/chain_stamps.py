@@ -22,6 +22,9 @@ NAMES = {13: "k_eval: entry + gap stamp", 7: "k_eval: inputs issued (vids, row, 
          27: "select (last block): class tables", 40: "gap k_eval->k_final entry",
          42: "gap k_final->next k_eval entry"}
 
+RUN_NAMES = {30: "eval + partial granules stored", 31: "every partial seen", 32: "partials folded",
+             33: "key granules stored", 34: "every key seen, argmax"}
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -47,7 +50,17 @@ def main():
     last = out[63] or 1
     res = {NAMES.get(k, str(k)): round(out[k] / (last if 24 <= k <= 27 else pods) * 0.01, 3)
            for k in sorted(NAMES, key=lambda k: (k not in (13, 7, 11, 12, 8, 9, 10), k)) if out[k]}
-    print(json.dumps({"pods": pods, "select_samples": last, "us_avg_block0": res}, indent=1))
+    rep = {"pods": pods, "select_samples": last, "us_avg_block0": res}
+    if out[35]:  # persistent segments (k_chain_run)
+        rep["k_chain_run_us_since_pod_start_block0"] = {RUN_NAMES[k]: round(out[k] / out[35] * 0.01, 3) for k in range(30, 35)}
+        rep["k_chain_run_pods_block0"] = out[35]
+        rep["k_chain_run_flag_wait_us_block0"] = round(out[38] / out[35] * 0.01, 3)
+        if out[37]:
+            rep["k_chain_run_owner_commit_us"] = round(out[36] / out[37] * 0.01, 3)
+            rep["k_chain_run_owner_atomics_issued_us"] = round(out[44] / out[37] * 0.01, 3)
+            rep["k_chain_run_owner_atomics_drained_us"] = round(out[45] / out[37] * 0.01, 3)
+            rep["k_chain_run_assume_items_avg"] = round(out[46] / out[37], 2)
+    print(json.dumps(rep, indent=1))
 
 
 if __name__ == "__main__":

@@ -227,6 +227,8 @@ def dropin_latency(s, doc, n=100):
 CFG3_PAIR_BYTES = 141      # 120 read + 21 written per (pod, node) pair
 CFG4_EVAL_NODE_BYTES = 68 + 20  # k_eval: reads node row 56 + zone id 4 + selector-class count 8, writes the
                                 # per-pair filter code 4 + the four raw scores 16 (k_final re-reads them)
+CFG4_RUN_NODE_BYTES = 68        # SURVEY §8(d) cfg4 per node and pod (row 56, zone id 4, class count 8);
+                                # k_chain_run keeps the row and zone id on chip and writes no per-pair outputs
 
 
 def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
@@ -239,12 +241,22 @@ def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
     s.load_cluster(blob)
     n_nodes, n_pods = s.n_nodes, s.queue_len
     elapsed = time_queue(s, torch, steps, warmup)
+    run0 = s.run_counts()
     kms, kn = sample_dominant(s, 16)
+    run1 = s.run_counts()
     res = s.results()
+    per = None
     if s.batch_path:
         kname = "k_window"
         tiles = (n_nodes + TILE - 1) // TILE
         bpl = WINDOW * n_nodes * CFG3_PAIR_BYTES + 2 * tiles * WINDOW * 64 * 8 + 2 * REC_BYTES
+    elif run1[1] > run0[1]:
+        # persistent segments: one k_chain_run launch per segment of pods; the
+        # roofline's "launch" is one pod's cycle inside it (launch time / its pods)
+        kname = "k_chain_run"
+        per = (run1[0] - run0[0]) / (run1[1] - run0[1])
+        kms = kms / per
+        bpl = n_nodes * CFG4_RUN_NODE_BYTES
     else:
         kname = "k_eval"
         bpl = n_nodes * CFG4_EVAL_NODE_BYTES
@@ -257,7 +269,9 @@ def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
                       "profile": doc["profile"]["plugins"], "path": "window" if s.batch_path else "table chain"},
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(f"cfg{c}:{kname}"),
-                        "kernel": kname, "kernel_avg_us": kms * 1e3, "kernel_samples": kn, "bytes_per_launch": bpl},
+                        "kernel": kname, "kernel_avg_us": kms * 1e3, "kernel_samples": kn, "bytes_per_launch": bpl,
+                        **({"pods_per_launch": per, "note": "k_chain_run: kernel_avg_us and bytes_per_launch per pod "
+                            "cycle inside the persistent launch (launch time / its pods)"} if per else {})},
            "generate_s": round(gen_s, 1)}
     if c == 4:
         out["dropin"] = dropin_latency(s, doc)

@@ -5225,6 +5225,8 @@ static uint32_t prog_need_of(const ksg_prog* h) {
   // bit 17: nothing but the node row and the class tables changes on its assume
   // (no host ports, volume claims or CSI volumes): a persistent segment may hold it
   if (h->n_port_own == 0 && h->n_pvc == 0 && h->n_csi == 0) need |= 1u << 17;
+  // bit 18: the persistent chain's small size class (kRunLK lookups, kRunTS constraints)
+  if (h->n_lk <= kRunLK && h->n_tsc_filter + h->n_tsc_score <= kRunTS) need |= 1u << 18;
   // bits 8..15: preferred NodeAffinity terms of the what-if class path (0xFF: a
   // negative weight or more than 7 terms — the record path)
   const int32_t* i32 = reinterpret_cast<const int32_t*>(reinterpret_cast<const uint8_t*>(h) + h->off_i32);
@@ -6032,7 +6034,9 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_chain_run<2, ~0u>, kChain, 0));
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_chain_run<2, kPmTab>, kChain, 0));
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ4, k_chain_run<2, kPmTabTN>, kChain, 0));
-    const int occ = std::min(std::min(occ1, occ2), std::min(occ3, occ4));
+    int occ5 = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ5, (k_chain_run<2, kPmTab, kRunLK, kRunTS>), kChain, 0));
+    const int occ = std::min(std::min(std::min(occ1, occ2), std::min(occ3, occ4)), occ5);
     // (MI355X_MICROARCH.md: the hardware may admit one block per CU fewer than the query)
     I.run_cap = occ <= 0 ? 1u : I.n_cus * (uint32_t)(occ >= 2 ? occ - 1 : occ);
     if (occ <= 0) I.run_on = 0;
@@ -6046,8 +6050,10 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
     if (run_ok && run_elig(j)) {
+      // a segment: consecutive eligible pods of one size class
+      const uint32_t cls = I.prog_need[j] & (1u << 18);
       uint32_t j1 = j + 1;
-      while (j1 < first + count && run_elig(j1)) ++j1;
+      while (j1 < first + count && run_elig(j1) && (I.prog_need[j1] & (1u << 18)) == cls) ++j1;
       if (j1 - j >= I.run_min) {
         CA.q = j;
         CA.prog = prog;
@@ -6060,7 +6066,9 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         uint64_t* const g1 = I.rgran.p;
         uint64_t* const g2 = I.rgran.p + (size_t)kChain * kRunGS;
         const dim3 gr(I.cnblk), bk(kChain);
-        if (rowm == 2 && (pmask & ~kPmTab) == 0)
+        if (rowm == 2 && (pmask & ~kPmTab) == 0 && cls)
+          hipLaunchKernelGGL((k_chain_run<2, kPmTab, kRunLK, kRunTS>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
+        else if (rowm == 2 && (pmask & ~kPmTab) == 0)
           hipLaunchKernelGGL((k_chain_run<2, kPmTab>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
         else if (rowm == 2 && (pmask & ~kPmTabTN) == 0)
           hipLaunchKernelGGL((k_chain_run<2, kPmTabTN>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);

@@ -182,6 +182,7 @@ __device__ __forceinline__ int64_t rec_mn(const ChainRec& r, int x) {
 // record per wave, one barrier; every thread returns the block's record (the
 // other fields keep their values).
 enum { RB_CNT = 1, RB_CNT16 = 2, RB_ST = 4, RB_KEY = 8 };  // RB_CNT16: feas, ign < 2^15 per wave (one sum)
+template <int TS = KSG_MAX_TSC>  // (TS: registration words a caller can have, nreg <= TS)
 __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t xmask, int nreg, uint32_t what) {
   if (what & RB_CNT16) {
     const int32_t p = wave_sum(r.feas | (r.ign << 16));
@@ -199,7 +200,7 @@ __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t x
       r.mn[x] = wave_min(r.mn[x]);
     }
 #pragma unroll
-  for (int c = 0; c < KSG_MAX_TSC; ++c)
+  for (int c = 0; c < TS; ++c)
     if (c < nreg) r.reg[c] = wave_or64(r.reg[c]);
   if (what & RB_KEY) r.key = wave_max(r.key);
   ChainRec* w = lds + (threadIdx.x >> 6);
@@ -214,7 +215,7 @@ __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t x
         w->mn[x] = r.mn[x];
       }
 #pragma unroll
-    for (int c = 0; c < KSG_MAX_TSC; ++c)
+    for (int c = 0; c < TS; ++c)
       if (c < nreg) w->reg[c] = r.reg[c];
     w->key = r.key;
   }
@@ -237,7 +238,7 @@ __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t x
         r.mn[x] = o->mn[x] < r.mn[x] ? o->mn[x] : r.mn[x];
       }
 #pragma unroll
-    for (int c = 0; c < KSG_MAX_TSC; ++c)
+    for (int c = 0; c < TS; ++c)
       if (c < nreg) r.reg[c] |= o->reg[c];
     if (what & RB_KEY) r.key = o->key > r.key ? o->key : r.key;
   }
@@ -406,6 +407,7 @@ __device__ __forceinline__ void st_cand(SoloCand* p, const int32_t v[KCP_X], uin
 // What one node's evaluation leaves for the persistent chain (MODE kRun): its raw
 // scores per profile position, feasibility, and the block's reduced record.
 struct EvalOut {
+  bool abort;                    // a poll ran out (k_chain_run leaves)
   int32_t raw[KSG_MAX_PLUGINS];  // (as k_final reads them back from the per-pair scores)
   bool feasible;
   uint32_t ipa_flags;
@@ -426,10 +428,16 @@ __device__ __forceinline__ int32_t ld_tab(const int32_t* p) {
 // code: the generic evaluation is ~75-130 KB of code, beyond the 64 KB
 // instruction cache two CUs share, and misses it on every cycle.
 #define PMH(p) ((PM >> (p)) & 1u)
-template <int ROWM, int MODE = kEval, uint32_t PM = ~0u>
+// k_chain_run: the flag this block waits for before its class-table reads (the
+// previous pod's assume by the block owning its node; want 0: none)
+struct RunWait;
+__device__ bool run_wait_flag(const RunWait& W);
+// LK / TS: the lookup-plan entries and spread constraints a pod of the launch has
+// at most (k_chain_run size classes; smaller unrolled loops, less code).
+template <int ROWM, int MODE = kEval, uint32_t PM = ~0u, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC>
 __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, const ChainArgs& A,
                                           const uint8_t* __restrict__ prog, EvalShared* Lrun = nullptr,
-                                          RowV* rowrun = nullptr, EvalOut* eo = nullptr) {
+                                          RowV* rowrun = nullptr, EvalOut* eo = nullptr, const RunWait* W = nullptr) {
   constexpr bool SOLO = MODE == kSolo, RUN = MODE == kRun;
   if constexpr (!RUN) chain_warm(prog);
   CS_BEGIN;
@@ -467,10 +475,27 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   RowV rowl;
   RowV& row = RUN ? *rowrun : rowl;
   if (ROWM && !RUN) load_row(C, nn, A.need_eph, row);
+  // the row-only plugins (Fit filter, Fit / BalancedAllocation scores) computed
+  // before the class-table reads: in k_chain_run their compute overlaps the wait
+  // for the previous pod's assume (the rows of this block's nodes are final: only
+  // the owner's changes, in its own registers)
+  uint32_t fit_b = 0;
+  int64_t fit_s = 0, ba_s = 0;
+  if constexpr (RUN && ROWM != 0) {
+    if (PMH(KP_FIT)) {
+      fit_b = fit_filter_row(row, h, C.R);
+      fit_s = ROWM == 2 ? fit_score_row<1>(row, F, h) : fit_score_row<0>(row, F, h);
+    }
+    if (PMH(KP_BA)) ba_s = ROWM == 2 ? ba_score_row<1>(row, F, h) : ba_score_row<0>(row, F, h);
+    if (W && !run_wait_flag(*W)) {
+      eo->abort = true;
+      return;
+    }
+  }
   uint8_t mpn[KSG_MAX_TSC];
   int32_t mcnt[KSG_MAX_TSC];
 #pragma unroll
-  for (int c = 0; c < KSG_MAX_TSC; ++c) {
+  for (int c = 0; c < TS; ++c) {
     mpn[c] = 0;
     mcnt[c] = 0;
     if (pts_f && c < nf && threadIdx.x < (uint32_t)h->tsc[c].nvals) {
@@ -507,7 +532,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   // ---- the lookup plan (ksg_look): every class-table count of this node
   int32_t lkv[KSG_LK_MAX], lks[KSG_LK_MAX];
 #pragma unroll
-  for (int i = 0; i < KSG_LK_MAX; ++i) {
+  for (int i = 0; i < LK; ++i) {
     lkv[i] = 0;
     lks[i] = -1;
     if (i < h->n_lk) {
@@ -527,7 +552,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   lds_barrier();
   if (pts_f) {
 #pragma unroll
-    for (int c = 0; c < KSG_MAX_TSC; ++c) {
+    for (int c = 0; c < TS; ++c) {
       if (c >= nf) continue;
       const ksg_tsc& t = h->tsc[c];
       int32_t m = (threadIdx.x < (uint32_t)t.nvals && mpn[c]) ? mcnt[c] : 0x7FFFFFFF;
@@ -549,11 +574,11 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   // ---- the counts, folded into what the filters and scores read
   int32_t ptsm[KSG_MAX_TSC];
 #pragma unroll
-  for (int c = 0; c < KSG_MAX_TSC; ++c) ptsm[c] = 0;
+  for (int c = 0; c < TS; ++c) ptsm[c] = 0;
   int64_t pts_cnt = 0, ipa_raw = 0;
   bool aff_miss = false, aff_zero = false, anti_hit = false, exist_hit = false;
 #pragma unroll
-  for (int i = 0; i < KSG_LK_MAX; ++i) {
+  for (int i = 0; i < LK; ++i) {
     if (i >= h->n_lk) continue;
     const ksg_look& e = h->lk[i];
     const int32_t v = lks[i];
@@ -561,7 +586,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     switch (e.use) {
       case KLU_PTSF:
 #pragma unroll
-        for (int c = 0; c < KSG_MAX_TSC; ++c)
+        for (int c = 0; c < TS; ++c)
           if (c == e.aux) ptsm[c] = x;
         break;
       case KLU_PTSS: pts_cnt += x; break;
@@ -592,7 +617,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
       switch (F.plugins[pos]) {  // (plugins outside PM compile to nothing)
         case KP_FIT:
           if constexpr (PMH(KP_FIT)) {
-            const uint32_t b = ROWM ? fit_filter_row(row, h, C.R) : fit_filter(C, V, n);
+            const uint32_t b = (RUN && ROWM) ? fit_b : ROWM ? fit_filter_row(row, h, C.R) : fit_filter(C, V, n);
             if (b) { fail = true; detail = b; }
           }
           break;
@@ -610,7 +635,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
           if constexpr (PMH(KP_PTS))
             if (!(h->flags & KPF_SKIP_PTS_FILTER))
 #pragma unroll
-              for (int c = 0; c < KSG_MAX_TSC; ++c) {
+              for (int c = 0; c < TS; ++c) {
                 if (c >= nf || fail || err) continue;
                 const ksg_tsc& t = h->tsc[c];
                 const int32_t dom = t.dom;
@@ -681,11 +706,11 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
       switch (p) {
         case KP_FIT:
           if constexpr (PMH(KP_FIT))
-            sc = ROWM == 2 ? fit_score_row<1>(row, F, h) : ROWM == 1 ? fit_score_row<0>(row, F, h) : fit_score(C, F, V, n);
+            sc = (RUN && ROWM) ? fit_s : ROWM == 2 ? fit_score_row<1>(row, F, h) : ROWM == 1 ? fit_score_row<0>(row, F, h) : fit_score(C, F, V, n);
           break;
         case KP_BA:
           if constexpr (PMH(KP_BA))
-            sc = ROWM == 2 ? ba_score_row<1>(row, F, h) : ROWM == 1 ? ba_score_row<0>(row, F, h) : ba_score(C, F, V, n);
+            sc = (RUN && ROWM) ? ba_s : ROWM == 2 ? ba_score_row<1>(row, F, h) : ROWM == 1 ? ba_score_row<0>(row, F, h) : ba_score(C, F, V, n);
           break;
         case KP_TAINT:
           if constexpr (PMH(KP_TAINT)) sc = taint_score(C, V, n);
@@ -733,7 +758,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   if (F.has_ext) {
     nreg = ns;
 #pragma unroll
-    for (int c = 0; c < KSG_MAX_TSC; ++c) {  // registered values of the score constraints' small keys (initPreScoreState)
+    for (int c = 0; c < TS; ++c) {  // registered values of the score constraints' small keys (initPreScoreState)
       if (c >= ns) continue;
       const ksg_tsc& t = h->tsc[nf + c];
       const int32_t v = tv(t.topo);
@@ -746,7 +771,8 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   }
   CS(4);
   if constexpr (RUN) {  // the block's record; the caller publishes it
-    rec_block(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);
+    rec_block<TS>(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);
+    CS(5);
     eo->feasible = feasible;
     eo->ipa_flags = ipa_flags;
     eo->rec = rec;
@@ -763,7 +789,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     bool fits = true;
 #pragma unroll
     for (int i = 0; i < KCP_X; ++i) fits &= cv[i] >= INT32_MIN && cv[i] <= INT32_MAX;
-    rec_block(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);  // (its barrier orders the table's reset)
+    rec_block<TS>(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);  // (its barrier orders the table's reset)
     CS(5);
     if (feasible && !fits) atomicOr(&S.dump, 1u);
     lds_barrier();
@@ -821,7 +847,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
         st_sc1(A.pm + (2 * x + 1) * NB + b, rec.mn[x]);
       }
 #pragma unroll
-      for (int c = 0; c < KSG_MAX_TSC; ++c)
+      for (int c = 0; c < TS; ++c)
         if (c < nreg) st_sc1(A.pr + (size_t)c * NB + b, rec.reg[c]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -836,7 +862,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     if (last) solo_last_select(C, F, A, L.rec, prog, ipa_flags, cs_t0);
     return;
   }
-  rec_block(rec, L.rec, F.has_ext ? xmask : 0u, nreg, RB_CNT16 | RB_ST | (F.has_ext ? 0u : RB_KEY));
+  rec_block<TS>(rec, L.rec, F.has_ext ? xmask : 0u, nreg, RB_CNT16 | RB_ST | (F.has_ext ? 0u : RB_KEY));
   CS(5);
   if (threadIdx.x == 0) {
     const uint32_t b = blockIdx.x, NB = A.nblk;
@@ -851,7 +877,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
         A.pm[(2 * x + 1) * NB + b] = rec.mn[x];
       }
 #pragma unroll
-      for (int c = 0; c < KSG_MAX_TSC; ++c)
+      for (int c = 0; c < TS; ++c)
         if (c < nreg) A.pr[(size_t)c * NB + b] = rec.reg[c];
     } else {  // no ScoreExtensions: this is the cycle's last kernel
       st_sc1(A.pk + b, rec.key);
@@ -1408,7 +1434,32 @@ struct RunShared {
   EvalShared L;
   uint32_t go;  // LDS broadcast of a poll's outcome
 };
+struct RunWait {
+  RunSync* Y;
+  uint32_t want;  // flag value awaited (0: none)
+  uint32_t* go;   // RunShared::go
+  uint64_t* rst;  // diagnostic stamps (block 0), or null
+};
+// Every thread of the block: thread 0 polls the flag, the block joins it.
+__device__ bool run_wait_flag(const RunWait& W) {
+  if (!W.want) return true;
+  if (threadIdx.x == 0) {
+    const uint64_t w0 = W.rst ? __builtin_amdgcn_s_memrealtime() : 0;
+    bool ok = false;
+    for (uint32_t it = 0; it < kRunSpin; ++it) {
+      if (ld_sc1(&W.Y->flag[0]) >= W.want) { ok = true; break; }
+      if (run_aborted(it, W.Y)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok) run_raise(W.Y);
+    *W.go = ok ? 1u : 0u;
+    if (W.rst) atomicAdd((unsigned long long*)&W.rst[38], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - w0));
+  }
+  __syncthreads();
+  return *W.go != 0u;
+}
 // The block record's granule i (wave 0 lanes; every thread holds the record).
+template <int TS>
 __device__ __forceinline__ uint32_t run_g1_value(const ChainRec& r, int i, uint32_t xmask, int ns) {
   uint32_t v = 0;
   if (i == 0) v = (uint32_t)r.feas | ((uint32_t)r.ign << 16);
@@ -1424,7 +1475,7 @@ __device__ __forceinline__ uint32_t run_g1_value(const ChainRec& r, int i, uint3
       j += 4;
     }
 #pragma unroll
-  for (int c = 0; c < KSG_MAX_TSC; ++c)
+  for (int c = 0; c < TS; ++c)
     if (c < ns) {
       if (i == j) v = (uint32_t)r.reg[c];
       if (i == j + 1) v = (uint32_t)(r.reg[c] >> 32);
@@ -1436,6 +1487,7 @@ __device__ __forceinline__ int run_g1_count(uint32_t xmask, int ns) { return 2 +
 __device__ __forceinline__ bool gtag(uint64_t g, uint32_t tag) { return (uint32_t)(g >> 32) == tag; }
 __device__ __forceinline__ int64_t g64(uint64_t lo, uint64_t hi) { return (int64_t)((uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32)); }
 // thread t < NB: block t's partial record, polled until every granule carries tag
+template <int TS>
 __device__ __forceinline__ bool run_read_g1(const uint64_t* g, uint32_t tag, uint32_t xmask, int ns, ChainRec& r,
                                             const RunSync* Y) {
   const int last = run_g1_count(xmask, ns) - 1;
@@ -1461,7 +1513,7 @@ __device__ __forceinline__ bool run_read_g1(const uint64_t* g, uint32_t tag, uin
         j += 4;
       }
 #pragma unroll
-    for (int c = 0; c < KSG_MAX_TSC; ++c)
+    for (int c = 0; c < TS; ++c)
       if (c < ns) {
         const uint64_t a = ld_sc1(g + j), b = ld_sc1(g + j + 1);
         ok &= gtag(a, tag) && gtag(b, tag);
@@ -1479,7 +1531,7 @@ __device__ __forceinline__ bool run_read_g1(const uint64_t* g, uint32_t tag, uin
   return false;
 }
 
-template <int ROWM, uint32_t PM>
+template <int ROWM, uint32_t PM, int LK, int TS>
 __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, const ChainArgs& A0, uint32_t count,
                                          RunSync* Y, uint64_t* G1, uint64_t* G2) {
   static_assert(ROWM != 0, "the persistent chain keeps the node row in registers");
@@ -1518,34 +1570,20 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     A.q = A0.q + k;
     const uint8_t* prog = A.progs + A.prog_off[A.q];
     const uint32_t tag = k + 1u;
-    if (wait_for) {  // the previous pod's assume, applied by the block owning its node
-      if (threadIdx.x == 0) {
-        const uint64_t w0 = rs_on ? __builtin_amdgcn_s_memrealtime() : 0;
-        bool ok = false;
-        for (uint32_t it = 0; it < kRunSpin; ++it) {
-          if (ld_sc1(&Y->flag[0]) >= wait_for) { ok = true; break; }
-          if (run_aborted(it, Y)) break;
-          __builtin_amdgcn_s_sleep(2);
-        }
-        if (!ok) run_raise(Y);
-        S.go = ok ? 1u : 0u;
-        if (rs_on) atomicAdd((unsigned long long*)&rst[38], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - w0));
-      } else if (threadIdx.x == 64) {  // (another wave: the program header into the scalar cache meanwhile)
-        chain_warm(prog);
-      }
-      __syncthreads();
-      if (!S.go) return;
-      wait_for = 0;
-    }
     if (rs_on) rs_t0 = __builtin_amdgcn_s_memrealtime();
     const ProgView V = view(prog);
     const ksg_prog* h = V.h;
-    // ---- eval: this block's nodes, its partial record
+    // ---- eval: this block's nodes (waiting for the previous pod's assume before
+    // the class-table reads), its partial record
     EvalOut eo;
-    eval_body<ROWM, kRun, PM>(C, F, A, prog, &L, &row, &eo);
+    eo.abort = false;
+    const RunWait W{Y, wait_for, &S.go, rs_on ? rst : nullptr};
+    eval_body<ROWM, kRun, PM, LK, TS>(C, F, A, prog, &L, &row, &eo, &W);
+    if (eo.abort) return;
+    wait_for = 0;
     const int ns = h->n_tsc_score;
     const int ng1 = run_g1_count(xmask, ns);
-    if (threadIdx.x < (uint32_t)ng1) st_sc1(G1 + (size_t)b * kRunGS + threadIdx.x, gran(tag, run_g1_value(eo.rec, (int)threadIdx.x, xmask, ns)));
+    if (threadIdx.x < (uint32_t)ng1) st_sc1(G1 + (size_t)b * kRunGS + threadIdx.x, gran(tag, run_g1_value<TS>(eo.rec, (int)threadIdx.x, xmask, ns)));
     RS(30);
     // ---- fold every block's partials (as reduce_eval)
     EvalTotals E;
@@ -1553,10 +1591,11 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       ChainRec& r = E.r;
       rec_init(r);
       bool ok = true;
-      if (threadIdx.x < NB) ok = run_read_g1(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y);
+      if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y);
       if (__syncthreads_or(!ok)) return;
       RS(31);
-      rec_block(r, L.rec, xmask, ns, RB_CNT | RB_ST);
+      rec_block<TS>(r, L.rec, xmask, ns, RB_CNT | RB_ST);
+      RS(39);
       eval_weights(C, h, E);
     }
     RS(32);
@@ -1596,13 +1635,22 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       r.key = pack_key(tot, F.seed, h->queue_idx, C.goff + n);
       r.st = (E.r.feas > 1 && range_err) ? 4 : 0;
     }
+    RS(47);
     __syncthreads();  // (L.rec reused)
-    rec_block(r, L.rec, 0u, 0, RB_ST | RB_KEY);
+    rec_block<TS>(r, L.rec, 0u, 0, RB_ST | RB_KEY);
     if (threadIdx.x < (uint32_t)kRunG2) {
       const uint32_t v = threadIdx.x == 0 ? (uint32_t)r.key : threadIdx.x == 1 ? (uint32_t)(r.key >> 32) : (uint32_t)r.st;
       st_sc1(G2 + (size_t)b * kRunGS + threadIdx.x, gran(tag, v));
     }
     RS(33);
+    if (threadIdx.x == kChain - 32 && k + 1 < count) {  // the next program header into the scalar cache
+      uint32_t warm = 0;
+      const uint64_t a = (uint64_t)(A.progs + A.prog_off[A.q + 1]);  // (uniform: into scalar registers)
+      const uint64_t su = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32);
+      KWarm<0, kHdrBytes>::run(reinterpret_cast<const void*>(su), warm);
+      warm_wait(warm);  // (the loads land in one scalar register the compiler may reuse: wait here)
+    }
     // ---- selectHost: every block takes the argmax of every block's key
     ChainRec sk;
     rec_init(sk);
@@ -1627,7 +1675,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       }
       if (__syncthreads_or(!ok)) return;
     }
-    rec_block(sk, L.rec, 0u, 0, RB_ST | RB_KEY);
+    rec_block<TS>(sk, L.rec, 0u, 0, RB_ST | RB_KEY);
     RS(34);
     const int32_t feas = E.r.feas, st = E.r.st | sk.st;
     const bool error = (st & 2) || ((st & 4) && feas > 1) || (h->flags & KPF_PREFILTER_ERROR) || na_prescore_error(h->flags, feas);
@@ -1690,10 +1738,13 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
 // profile of cfg4 (with or without TaintToleration / NodeAffinity), every plugin.
 constexpr uint32_t kPmTab = (1u << KP_FIT) | (1u << KP_BA) | (1u << KP_PTS) | (1u << KP_IPA);
 constexpr uint32_t kPmTabTN = kPmTab | (1u << KP_TAINT) | (1u << KP_NA);
-template <int ROWM, uint32_t PM>
+// Size classes: pods with at most kRunLK lookup-plan entries and kRunTS spread
+// constraints (cfg4's) run the small instantiation, the others the generic one.
+constexpr int kRunLK = 8, kRunTS = 4;
+template <int ROWM, uint32_t PM, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC>
 __global__ __launch_bounds__(kChain) void k_chain_run(DevCluster C, DevProfile F, ChainArgs A, uint32_t count, RunSync* Y,
                                                       uint64_t* G1, uint64_t* G2) {
-  run_body<ROWM, PM>(C, F, A, count, Y, G1, G2);
+  run_body<ROWM, PM, LK, TS>(C, F, A, count, Y, G1, G2);
 }
 
 // Kernels.  The *_occ twins cap registers at 4 waves per SIMD (a few spills)

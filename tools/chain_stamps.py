@@ -22,8 +22,8 @@ NAMES = {13: "k_eval: entry + gap stamp", 7: "k_eval: inputs issued (vids, row, 
          27: "select (last block): class tables", 40: "gap k_eval->k_final entry",
          42: "gap k_final->next k_eval entry"}
 
-RUN_NAMES = {30: "eval + partial granules stored", 31: "every partial seen", 32: "partials folded",
-             33: "key granules stored", 34: "every key seen, argmax"}
+RUN_NAMES = {30: "eval + partial granules stored", 31: "every partial seen", 39: "partials block-reduced",
+             32: "partials folded", 47: "normalised + keyed", 33: "key granules stored", 34: "every key seen, argmax"}
 
 
 def main():
@@ -52,7 +52,7 @@ def main():
            for k in sorted(NAMES, key=lambda k: (k not in (13, 7, 11, 12, 8, 9, 10), k)) if out[k]}
     rep = {"pods": pods, "select_samples": last, "us_avg_block0": res}
     if out[35]:  # persistent segments (k_chain_run)
-        rep["k_chain_run_us_since_pod_start_block0"] = {RUN_NAMES[k]: round(out[k] / out[35] * 0.01, 3) for k in range(30, 35)}
+        rep["k_chain_run_us_since_pod_start_block0"] = {RUN_NAMES[k]: round(out[k] / out[35] * 0.01, 3) for k in (30, 31, 39, 32, 47, 33, 34)}
         rep["k_chain_run_pods_block0"] = out[35]
         rep["k_chain_run_flag_wait_us_block0"] = round(out[38] / out[35] * 0.01, 3)
         if out[37]:

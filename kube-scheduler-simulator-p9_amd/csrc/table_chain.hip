@@ -193,12 +193,34 @@ __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t x
     r.ign = wave_sum(r.ign);
   }
   if (what & RB_ST) r.st = wave_or(r.st);
+  if (xmask) {
+    // normalisers whose values (raw scores) all fit 32 bits reduce in one DPP pass
+    // each instead of two (the unset sentinels map to the 32-bit extremes)
+    bool wide = false;
 #pragma unroll
-  for (int x = 0; x < KCP_X; ++x)
-    if ((xmask >> x) & 1u) {
-      r.mx[x] = wave_max(r.mx[x]);
-      r.mn[x] = wave_min(r.mn[x]);
+    for (int x = 0; x < KCP_X; ++x)
+      if ((xmask >> x) & 1u) {
+        wide |= r.mx[x] != INT64_MIN && (r.mx[x] <= INT32_MIN || r.mx[x] >= INT32_MAX);
+        wide |= r.mn[x] != INT64_MAX && (r.mn[x] <= INT32_MIN || r.mn[x] >= INT32_MAX);
+      }
+    if (__ballot(wide) == 0ull) {
+#pragma unroll
+      for (int x = 0; x < KCP_X; ++x)
+        if ((xmask >> x) & 1u) {
+          const int32_t a = wave_max(r.mx[x] == INT64_MIN ? INT32_MIN : (int32_t)r.mx[x]);
+          const int32_t b = wave_min(r.mn[x] == INT64_MAX ? INT32_MAX : (int32_t)r.mn[x]);
+          r.mx[x] = a == INT32_MIN ? INT64_MIN : (int64_t)a;
+          r.mn[x] = b == INT32_MAX ? INT64_MAX : (int64_t)b;
+        }
+    } else {
+#pragma unroll
+      for (int x = 0; x < KCP_X; ++x)
+        if ((xmask >> x) & 1u) {
+          r.mx[x] = wave_max(r.mx[x]);
+          r.mn[x] = wave_min(r.mn[x]);
+        }
     }
+  }
 #pragma unroll
   for (int c = 0; c < TS; ++c)
     if (c < nreg) r.reg[c] = wave_or64(r.reg[c]);
@@ -1651,6 +1673,16 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       KWarm<0, kHdrBytes>::run(reinterpret_cast<const void*>(su), warm);
       warm_wait(warm);  // (the loads land in one scalar register the compiler may reuse: wait here)
     }
+    // the assume's items (class ids, own affinity terms) into registers while the
+    // keys arrive: the owner's commit then issues its atomics without a load
+    const uint32_t npm = (uint32_t)h->n_pc_match, nitems = npm + (uint32_t)h->n_exist_terms;
+    int32_t it_cls = -1;
+    ksg_exist_term it_term;
+    it_term.cls = -1;
+    if (C.T.on && threadIdx.x < nitems) {
+      if (threadIdx.x < npm) it_cls = V.i32[h->pc_match_off + threadIdx.x];
+      else it_term = V.et[h->exist_terms_off + (threadIdx.x - npm)];
+    }
     // ---- selectHost: every block takes the argmax of every block's key
     ChainRec sk;
     rec_init(sk);
@@ -1705,11 +1737,14 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
           row.podcnt += 1;
           assume_row_atomic(C, V, (uint32_t)node, +1);
         }
-        if (C.T.on && threadIdx.x < (uint32_t)(h->n_pc_match + h->n_exist_terms)) {
+        if (C.T.on && threadIdx.x < nitems) {
           int32_t v[KSG_MAX_TOPO];
 #pragma unroll
           for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? L.tv[s * kChain + ln] : -1;
-          tables_assume_items(C, V, (uint32_t)node, v, +1, threadIdx.x, kChain, TP_ALL);
+          if (threadIdx.x < npm) pc_add(C, it_cls, (uint32_t)node, +1, v, TP_ALL);
+          else tc_add(C, it_term, (uint32_t)node, +1, v, TP_ALL);
+          if (nitems > (uint32_t)kChain)  // (items beyond one per thread)
+            tables_assume_items(C, V, (uint32_t)node, v, +1, threadIdx.x + kChain, kChain, TP_ALL);
         }
         if (rst && threadIdx.x == 0) {
           atomicAdd((unsigned long long*)&rst[44], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - c0));

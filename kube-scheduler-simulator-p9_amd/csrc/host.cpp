@@ -4550,15 +4550,37 @@ int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out)
   v->pscode.assign(P, -1);
   v->psmsg.assign(P, 0);
   std::string m;
+  const ksg::host::PodMeta& pm = c.meta[q];
+  const uint32_t skip_f = c.skip_filter_mask(pm, o->summary);
   for (uint32_t pos = 0; pos < P; ++pos) {
     v->pfcode[pos] = (int8_t)c.prefilter_status(q, (int)pos, o->summary, m);
     v->pfmsg[pos] = v->intern(m);
     v->pscode[pos] = (int8_t)c.prescore_status(q, (int)pos, o->summary, m);
     v->psmsg[pos] = v->intern(m);
+    // filter_status per node, its pod-level gates hoisted: a node that passed this
+    // position or failed earlier needs no call; a failure here is memoised by its
+    // code except Fit's (whose status reads the node's allocatable)
+    const bool gated = !ksg::host::has_filter(c.plugins[pos]) || pm.prefilter_fail_pos >= 0 || c.filter_skipped(pm, skip_f, (int)pos);
+    if (gated) continue;  // (-1 everywhere, as filter_status)
+    std::unordered_map<uint32_t, std::pair<int8_t, int32_t>> memo;
     for (uint32_t i = 0; i < N; ++i) {
       const size_t k = (size_t)pos * N + i;
+      const uint32_t code = o->filter[i];
+      if (code == KSG_FILTER_NOT_EVALUATED) continue;
+      const int fail_pos = code == KSG_FILTER_PASS ? c.n_plugins : c.code_pos(code);
+      if ((int)pos < fail_pos) { v->fcode[k] = (int8_t)Cluster::C_SUCCESS; continue; }
+      if ((int)pos > fail_pos) continue;
+      if (c.plugins[pos] != ksg::host::P_FIT) {
+        auto it = memo.find(code);
+        if (it != memo.end()) {
+          v->fcode[k] = it->second.first;
+          v->fmsg[k] = it->second.second;
+          continue;
+        }
+      }
       v->fcode[k] = (int8_t)c.filter_status(q, (int)pos, i, *o, m);
       if (!m.empty()) v->fmsg[k] = v->intern(m);
+      if (c.plugins[pos] != ksg::host::P_FIT) memo.emplace(code, std::make_pair(v->fcode[k], v->fmsg[k]));
     }
     const int d = c.dpos[pos];
     if (d < 0) continue;

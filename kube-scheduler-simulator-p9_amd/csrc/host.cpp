@@ -4561,9 +4561,8 @@ int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out)
     // position or failed earlier needs no call; a failure here is memoised by its
     // code except Fit's (whose status reads the node's allocatable)
     const bool gated = !ksg::host::has_filter(c.plugins[pos]) || pm.prefilter_fail_pos >= 0 || c.filter_skipped(pm, skip_f, (int)pos);
-    if (gated) continue;  // (-1 everywhere, as filter_status)
     std::unordered_map<uint32_t, std::pair<int8_t, int32_t>> memo;
-    for (uint32_t i = 0; i < N; ++i) {
+    for (uint32_t i = 0; i < N && !gated; ++i) {  // (gated: -1 everywhere, as filter_status)
       const size_t k = (size_t)pos * N + i;
       const uint32_t code = o->filter[i];
       if (code == KSG_FILTER_NOT_EVALUATED) continue;

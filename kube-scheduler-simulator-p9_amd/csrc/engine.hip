@@ -3296,6 +3296,13 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   // every one of them waited for all outstanding stores)
   PodLite* h = reinterpret_cast<PodLite*>(wcount + 96);
   int64_t* mlds = reinterpret_cast<int64_t*>(wcount + 96 + sizeof(PodLite) / 4);
+  // the first node's row from memory, issued before the P_{W-1} list it may be
+  // replaced from (one round trip less ahead of the first evaluation)
+  RowV rnext;
+  {
+    const uint32_t nn0 = tile * A.tile_len + tid;
+    if ((uint32_t)tid < A.tile_len && nn0 < C.N) load_row(C, nn0, A.need_eph, rnext);
+  }
   {
     constexpr int kPodW = (int)(sizeof(PodLite) / 8);
     if (tid < kPodW) reinterpret_cast<uint64_t*>(h)[tid] = reinterpret_cast<const uint64_t*>(A.plite + q)[tid];
@@ -3335,18 +3342,17 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   const bool stash_all = A.npt <= A.stash_npt;
   static_assert(96 * 4 + sizeof(PodLite) + 16 <= 192 * 4, "eval LDS layout");
   // the next node's row and static record are loaded while this one is evaluated
-  auto fetch = [&](uint32_t kk, RowV& r, StaticRec& sr) {
+  auto fetch = [&](uint32_t kk, RowV& r, StaticRec& sr, bool loaded) {
     const uint32_t to = kk * KSG_TILE + tid, nn = tile * A.tile_len + to;
     if (to < A.tile_len && nn < C.N) {
       const int hit = pend_lds((int32_t)(C.goff + nn));
       if (hit >= 0) r = A.pprev[hit].after;
-      else load_row(C, nn, A.need_eph, r);
+      else if (!loaded) load_row(C, nn, A.need_eph, r);
       if (STAT) sr = srec_row(A, q, C.N)[nn];
     }
   };
-  RowV rnext;
   StaticRec snext{KSG_FILTER_PASS, 0};
-  fetch(0, rnext, snext);
+  fetch(0, rnext, snext, true);
 #pragma unroll 1
   for (uint32_t k = 0; k < A.npt; ++k) {
   KSG_ETIME(t0);
@@ -3356,7 +3362,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   const uint32_t to = k * KSG_TILE + tid, n = tile * A.tile_len + to;
   const RowV r = rnext;
   const StaticRec sr = snext;
-  if (k + 1 < A.npt) fetch(k + 1, rnext, snext);
+  if (k + 1 < A.npt) fetch(k + 1, rnext, snext, false);
   uint64_t key = 0;
   bool feasible = false, achT = false, achA = false;
   if (to < A.tile_len && n < C.N) {
@@ -3455,9 +3461,8 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   if (A.estamps && tid == 0) {
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
     atomicMax((unsigned long long*)&A.estamps[9], (unsigned long long)t);
-    atomicMax((unsigned long long*)&A.estamps[28], (unsigned long long)(t - t_start));
-    atomicAdd((unsigned long long*)&A.estamps[29], (unsigned long long)(t - t_start));
-    atomicAdd((unsigned long long*)&A.estamps[31], 1ull);
+    (void)t_start;
+    (void)0;
   }
   if (!wcount[16]) {
     flush_stash();
@@ -3465,11 +3470,17 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   }
   // last tile block of pod b: merge the T tile lists (wave w takes tiles w, w+16, ...);
   // the lists and the tiles' counts are requested together.
+  const uint64_t t_merge = A.estamps ? __builtin_amdgcn_s_memrealtime() : 0;
   int32_t f[3] = {0, 0, 0};
   {
     const uint64_t* src = A.tile_top + (size_t)b * A.T * KSG_TOPK;
     uint64_t v = 0;
     if ((uint32_t)w < A.T) v = ld_agent(src + (size_t)w * KSG_TOPK + lane);
+    if (A.estamps && tid == 0) {  // (temp) the first tile list in registers
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint64_t tl = __builtin_amdgcn_s_memrealtime() + (v & 0);
+      atomicMax((unsigned long long*)&A.estamps[31], (unsigned long long)(tl - t_merge));
+    }
     if (w == 0)
       for (uint32_t t = lane; t < A.T; t += 64)
 #pragma unroll
@@ -3480,10 +3491,16 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     L[w * 64 + lane] = v;
   }
   lds_barrier();
+  const uint64_t t_m1 = A.estamps ? __builtin_amdgcn_s_memrealtime() : 0;
 #pragma unroll 1
   for (int s = 8; s >= 1; s >>= 1) {
     if (w < s) L[w * 64 + lane] = wave_merge_top(L[w * 64 + lane], L[(w + s) * 64 + 63 - lane]);
     lds_barrier();
+  }
+  const uint64_t t_m2 = A.estamps ? __builtin_amdgcn_s_memrealtime() : 0;
+  if (A.estamps && tid == 0) {
+    atomicMax((unsigned long long*)&A.estamps[28], (unsigned long long)(t_m1 - t_merge));
+    atomicMax((unsigned long long*)&A.estamps[29], (unsigned long long)(t_m2 - t_m1));
   }
   if (w == 0) {
     uint64_t v = L[lane];
@@ -3503,7 +3520,11 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
 #pragma unroll
       for (int k = 0; k < 3; ++k) reinterpret_cast<int32_t*>(A.erec)[k * KSG_BATCH + b] = f[k];
       A.arrive[b] = 0;
-      if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+      if (A.estamps) {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)t);
+        atomicMax((unsigned long long*)&A.estamps[6], (unsigned long long)(t - t_merge));  // diagnostic: merge duration
+      }
     }
   }
   flush_stash();
@@ -4906,6 +4927,11 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
 // to fill every CU were measured slower: the replay block's memory latency
 // grows with the eval blocks around it.)
 static uint32_t eval_npt(uint32_t N, uint32_t cus) {
+  static const uint32_t forced = [] {  // KSG_WIN_NPT: nodes per thread of the window's eval tiles (A/B)
+    const char* e = std::getenv("KSG_WIN_NPT");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+  }();
+  if (forced) return std::min<uint32_t>(forced, 16);
   uint32_t npt = 1;
   while (npt < 16 && (uint64_t)KSG_BATCH * ((N + KSG_TILE * npt - 1) / (KSG_TILE * npt)) + 1 > cus) ++npt;
   return npt;

@@ -3459,10 +3459,13 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     atomicAdd((unsigned long long*)&A.estamps[18], (unsigned long long)t_wait);
   }
   if (A.estamps && tid == 0) {
+    __builtin_amdgcn_sched_barrier(0);
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_sched_barrier(0);
     atomicMax((unsigned long long*)&A.estamps[9], (unsigned long long)t);
-    (void)t_start;
-    (void)0;
+    atomicMax((unsigned long long*)&A.estamps[28], (unsigned long long)(t - t_start));
+    atomicAdd((unsigned long long*)&A.estamps[29], (unsigned long long)(t - t_start));
+    atomicAdd((unsigned long long*)&A.estamps[31], 1ull);
   }
   if (!wcount[16]) {
     flush_stash();
@@ -3470,17 +3473,11 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   }
   // last tile block of pod b: merge the T tile lists (wave w takes tiles w, w+16, ...);
   // the lists and the tiles' counts are requested together.
-  const uint64_t t_merge = A.estamps ? __builtin_amdgcn_s_memrealtime() : 0;
   int32_t f[3] = {0, 0, 0};
   {
     const uint64_t* src = A.tile_top + (size_t)b * A.T * KSG_TOPK;
     uint64_t v = 0;
     if ((uint32_t)w < A.T) v = ld_agent(src + (size_t)w * KSG_TOPK + lane);
-    if (A.estamps && tid == 0) {  // (temp) the first tile list in registers
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint64_t tl = __builtin_amdgcn_s_memrealtime() + (v & 0);
-      atomicMax((unsigned long long*)&A.estamps[31], (unsigned long long)(tl - t_merge));
-    }
     if (w == 0)
       for (uint32_t t = lane; t < A.T; t += 64)
 #pragma unroll
@@ -3491,16 +3488,10 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     L[w * 64 + lane] = v;
   }
   lds_barrier();
-  const uint64_t t_m1 = A.estamps ? __builtin_amdgcn_s_memrealtime() : 0;
 #pragma unroll 1
   for (int s = 8; s >= 1; s >>= 1) {
     if (w < s) L[w * 64 + lane] = wave_merge_top(L[w * 64 + lane], L[(w + s) * 64 + 63 - lane]);
     lds_barrier();
-  }
-  const uint64_t t_m2 = A.estamps ? __builtin_amdgcn_s_memrealtime() : 0;
-  if (A.estamps && tid == 0) {
-    atomicMax((unsigned long long*)&A.estamps[28], (unsigned long long)(t_m1 - t_merge));
-    atomicMax((unsigned long long*)&A.estamps[29], (unsigned long long)(t_m2 - t_m1));
   }
   if (w == 0) {
     uint64_t v = L[lane];
@@ -3520,11 +3511,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
 #pragma unroll
       for (int k = 0; k < 3; ++k) reinterpret_cast<int32_t*>(A.erec)[k * KSG_BATCH + b] = f[k];
       A.arrive[b] = 0;
-      if (A.estamps) {
-        const uint64_t t = __builtin_amdgcn_s_memrealtime();
-        atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)t);
-        atomicMax((unsigned long long*)&A.estamps[6], (unsigned long long)(t - t_merge));  // diagnostic: merge duration
-      }
+      if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
   }
   flush_stash();
@@ -4736,6 +4723,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
 }
 
 static uint32_t eval_tiles(uint32_t N, uint32_t cus);
+static uint32_t tt_ring();
 bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, uint32_t term_cap, uint32_t req_cap,
                     uint32_t val_cap, std::string& err) {
   Impl& I = *p_;
@@ -4908,7 +4896,7 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
   if (I.batch_ok && I.R <= 4) {
     uint32_t T = eval_tiles(I.N, I.n_cus);
     size_t Nn = std::max<uint32_t>(I.N, 1);
-    if (!I.tile_top.alloc((size_t)2 * KSG_BATCH * T * KSG_TOPK, err) || !I.tfeas.alloc((size_t)2 * KSG_BATCH * T * 3, err) ||
+    if (!I.tile_top.alloc((size_t)tt_ring() * KSG_BATCH * T * KSG_TOPK, err) || !I.tfeas.alloc((size_t)tt_ring() * KSG_BATCH * T * 3, err) ||
         !I.arrive.alloc(KSG_BATCH, err) || !I.pend_n.alloc(2, err) || !I.wrec.alloc(2 * kRecBytes, err) ||
         !I.pend.alloc(2 * KSG_BATCH, err) || !I.bfilter.alloc(Nn * 2 * KSG_BATCH, err) ||
         !I.bscore.alloc(Nn * 2 * KSG_BATCH * KSG_MAX_PLUGINS, err) || !I.btotal.alloc(Nn * 2 * KSG_BATCH, err))
@@ -4926,6 +4914,15 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
 // replay block in one round; at most 16 (then several rounds).  (Tiles balanced
 // to fill every CU were measured slower: the replay block's memory latency
 // grows with the eval blocks around it.)
+// Windows' tile-list slots (KSG_TT_RING, default 2: window parity)
+static uint32_t tt_ring() {
+  static const uint32_t r = [] {
+    const char* e = std::getenv("KSG_TT_RING");
+    const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2u;
+    return v < 2 ? 2u : (v > 64 ? 64u : v);
+  }();
+  return r;
+}
 static uint32_t eval_npt(uint32_t N, uint32_t cus) {
   static const uint32_t forced = [] {  // KSG_WIN_NPT: nodes per thread of the window's eval tiles (A/B)
     const char* e = std::getenv("KSG_WIN_NPT");
@@ -4986,8 +4983,8 @@ static bool run_batches_split(Engine::Impl& I, const WinArgs& A0, uint32_t first
       a.stamps = nullptr;
       a.e0 = first + (uint32_t)E * KSG_BATCH;
       a.ne = std::min<uint32_t>(KSG_BATCH, first + count - a.e0);
-      a.tile_top = I.tile_top.p + (size_t)(E & 1) * tt_sz;
-      a.tile_feas = I.tfeas.p + (size_t)(E & 1) * tf_sz;
+      a.tile_top = I.tile_top.p + (size_t)(E % tt_ring()) * tt_sz;
+      a.tile_feas = I.tfeas.p + (size_t)(E % tt_ring()) * tf_sz;
       a.erec = I.xsend.p + (size_t)(E & 1) * kRecBytes;
       a.estamps = I.stamps_on ? I.stamps.p + (size_t)E * 32 : nullptr;
       a.pprev = I.pend.p + (size_t)(P & 1) * KSG_BATCH;
@@ -5152,10 +5149,10 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     A.ne = 0;
     A.nw = 0;
     A.stamps = A.estamps = nullptr;
-    A.tile_top = I.tile_top.p + (size_t)(E & 1) * tt_sz;
-    A.tile_feas = I.tfeas.p + (size_t)(E & 1) * tf_sz;
-    A.wtile_top = I.tile_top.p + (size_t)(W & 1) * tt_sz;
-    A.wtile_feas = I.tfeas.p + (size_t)(W & 1) * tf_sz;
+    A.tile_top = I.tile_top.p + (size_t)(E % tt_ring()) * tt_sz;
+    A.tile_feas = I.tfeas.p + (size_t)(E % tt_ring()) * tf_sz;
+    A.wtile_top = I.tile_top.p + (size_t)(W % tt_ring()) * tt_sz;
+    A.wtile_feas = I.tfeas.p + (size_t)(W % tt_ring()) * tf_sz;
     if (E < (int64_t)nwin) {
       A.estamps = I.stamps_on ? I.stamps.p + (size_t)E * 32 : nullptr;
       A.e0 = first + (uint32_t)E * KSG_BATCH;

@@ -1213,6 +1213,31 @@ struct Cluster {
     }
     return ok;
   }
+  // The pair-level class-table entries the program's evaluation reads and its
+  // assume writes, as Bloom filters (ksg_prog tab_rd / tab_md).
+  template <class Pools>
+  void tab_blooms(ksg_prog& h, const Pools& P) const {
+    h.tab_rd = h.tab_md = ~0ull;
+    if (!(h.tab & KTAB_ON) || enc_NU == 0) return;
+    uint64_t rd = 0, md = 0;
+    for (int i = 0; i < h.n_lk; ++i) {  // (PC_NODE / TC_NODE entries are node-level)
+      const ksg_look& e = h.lk[i];
+      if (e.kind == KLK_PC_DOM) rd |= ksg_tab_bloom(1, (uint32_t)e.base / (uint32_t)enc_NU);
+      else if (e.kind == KLK_TC_DOM) rd |= ksg_tab_bloom(2, (uint32_t)e.base);
+    }
+    for (int c = 0; c < h.n_tsc_filter; ++c)  // minMatchNum candidates (pc_dom)
+      if (h.tsc[c].eff_cls >= 0) rd |= ksg_tab_bloom(1, (uint32_t)h.tsc[c].eff_cls);
+    for (int i = 0; i < h.n_ub; ++i)
+      rd |= h.ub[i].kind == 1 ? ksg_tab_bloom(1, (uint32_t)h.ub[i].idx / KSG_MAX_TOPO) : ksg_tab_bloom(3, (uint32_t)h.ub[i].idx);
+    for (int i = 0; i < h.n_pc_match; ++i) md |= ksg_tab_bloom(1, (uint32_t)P.i32[(size_t)h.pc_match_off + i]);
+    for (int i = 0; i < h.n_exist_terms; ++i) {
+      const ksg_exist_term& e = P.et[(size_t)h.exist_terms_off + i];
+      if (e.cls < 0) continue;  // (no class: tc_add writes nothing)
+      md |= ksg_tab_bloom(2, (uint32_t)e.toff) | ksg_tab_bloom(3, (uint32_t)e.cls);
+    }
+    h.tab_rd = rd;
+    h.tab_md = md;
+  }
   // Recompile queue pod q when classes added since its compile apply to it (its
   // pod-class list must hold every class whose table counts it; its term-class
   // list every term class that applies to it).
@@ -2562,8 +2587,10 @@ struct Cluster {
       if ((h.tab & KTAB_ON) && pos_of(P_PTS) >= 0 && h.n_tsc_score > 1 && !(h.flags & KPF_SKIP_PTS_SCORE))
         h.tab |= KTAB_PTS_MULTI;
       if ((h.tab & KTAB_ON) && !lookup_plan(h, P)) h.tab = 0;  // more lookups than the plan holds
+      tab_blooms(h, P);
     } else {
       h.tab = KTAB_ON;  // profiles without PTS / IPA: the chain needs no tables
+      h.tab_rd = h.tab_md = 0;
     }
     // every requirement of the pool (NodeAffinity, node selector, volume and
     // topology terms alike) in its flattened form

@@ -187,6 +187,12 @@ typedef struct ksg_ubit {
   int16_t bit;
 } ksg_ubit;
 #define KSG_UB_MAX 16
+// ksg_prog tab_rd / tab_md bit of class-table key (space 1: pod class, 2: term
+// class value offset, 3: term class) — one bit per key
+static inline uint64_t ksg_tab_bloom(uint32_t space, uint32_t id) {
+  const uint64_t x = (((uint64_t)space << 32) | id) * 0x9E3779B97F4A7C15ull;
+  return 1ull << (x >> 58);
+}
 
 // Existing-pod record appended at assume time (Reserve -> NodeInfo.AddPod).
 typedef struct ksg_exist_term {
@@ -289,6 +295,12 @@ typedef struct ksg_prog {
   int32_t n_lk, n_ub;       // table chain: lookup plan and InterPodAffinity bits
   ksg_look lk[KSG_LK_MAX];
   ksg_ubit ub[KSG_UB_MAX];
+  // 64-bit Bloom filters (ksg_tab_bloom) of the pair-level class-table entries —
+  // pod classes' pc_dom / pc_tot, term classes' shared-value tc_val / tc_tot — the
+  // pod's evaluation reads (tab_rd) and its assume writes (tab_md).  k_chain_run:
+  // a pod whose reads miss the previous pod's writes does not wait for that assume
+  // (node-level entries are read only by the block owning the node).  ~0: unknown.
+  uint64_t tab_rd, tab_md;
 
   // ---- volume plugins
   int32_t n_vchk, vchk_off;  // pool_i32: ksg_vchk records (8 words each)

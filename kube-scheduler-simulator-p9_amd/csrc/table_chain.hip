@@ -1456,6 +1456,19 @@ struct RunShared {
   EvalShared L;
   uint32_t go;  // LDS broadcast of a poll's outcome
 };
+// The flag counts the pods of the segment whose assumes are all applied: pod k's
+// owner (block 0 for a pod that places nothing) raises it to k + 1 once it
+// reads k (thread 0; bounded like every poll).
+__device__ __forceinline__ void run_advance(RunSync* Y, uint32_t k) {
+  bool ok = false;
+  for (uint32_t it = 0; it < kRunSpin; ++it) {
+    if (ld_sc1(&Y->flag[0]) >= k) { ok = true; break; }
+    if (run_aborted(it, Y)) return;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (!ok) { run_raise(Y); return; }
+  st_sc1(&Y->flag[0], (uint64_t)(k + 1u));
+}
 struct RunWait {
   RunSync* Y;
   uint32_t want;  // flag value awaited (0: none)
@@ -1724,6 +1737,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       A.prow[A.q] = -1;
       A.alog[A.q - A.log_base] = make_int2((int)A.q, node >= 0 && (A.mode & 2) ? node : -1);
     }
+    bool owned = false;
     if (node >= 0) {
       if ((uint32_t)node / kChain == b) {  // ---- the owner applies the assume
         const uint64_t c0 = rst && threadIdx.x == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1755,15 +1769,23 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
           atomicAdd((unsigned long long*)&rst[45], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - c0));
         __syncthreads();
         if (threadIdx.x == 0) {
-          st_sc1(&Y->flag[0], (uint64_t)tag);
+          run_advance(Y, k);
           if (rst) {
             atomicAdd((unsigned long long*)&rst[36], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - c0));
             atomicAdd((unsigned long long*)&rst[37], 1ull);
           }
         }
-      } else {
-        wait_for = tag;
+        owned = true;  // (the owner's reads need nothing more: run_advance waited for every earlier assume)
       }
+    } else if (b == 0 && threadIdx.x == 0) {
+      run_advance(Y, k);  // no assume: the flag passes the pod
+    }
+    // the flag this block waits for before the next pod's class-table reads: every
+    // assume up to this pod's if the next pod reads an entry this one writes
+    // (tab_rd / tab_md), else every assume before this pod's
+    if (!owned && k + 1 < count) {
+      const ksg_prog* nh = reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[A.q + 1]);
+      wait_for = (node >= 0 && (h->tab_md & nh->tab_rd) != 0) ? tag : k;
     }
     if (rs_on) atomicAdd((unsigned long long*)&rst[35], 1ull);
   }

@@ -57,8 +57,6 @@ print("eval wave-0 cycles per block: eval", med([bs[j][13] / nb_[j - 1] for j in
       "(of eval: load wait", med([bs[j][18] / nb_[j - 1] for j in range(1, nw)]), ")")
 print("realtime (us): first -> last eval block start", med([(bs[j][30] - ev[j]) / 100 for j in range(1, nw)]))
 print("realtime (us): eval start->last merge", med([(bs[j][10] - ev[j]) / 100 for j in range(1, nw)]))
-print("realtime (us): longest tile merge (last tile block)", med([bs[j][6] / 100 for j in range(1, nw)]))
-print("  (temp) merge: tile loads+barrier", med([bs[j][28] / 100 for j in range(1, nw)]), "tree", med([bs[j][29] / 100 for j in range(1, nw)]), "first list in regs", med([bs[j][31] / 100 for j in range(1, nw)]))
 # window j's eval runs in the same launch as window j-1's fixup
 print("realtime (us): fixup W-1 start -> eval W start", med([(ev[j] - bs[j - 1][11]) / 100 for j in range(2, nw)]))
 print("realtime (us): fixup duration", med([(x[12] - x[11]) / 100 for x in bs[1:]]))

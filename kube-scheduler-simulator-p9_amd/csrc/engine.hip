@@ -6064,7 +6064,7 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
     I.run_cap = occ <= 0 ? 1u : I.n_cus * (uint32_t)(occ >= 2 ? occ - 1 : occ);
     if (occ <= 0) I.run_on = 0;
   }
-  run_ok = run_ok && I.run_on != 0 && I.cnblk <= I.run_cap && I.cnblk <= (uint32_t)kChain;
+  run_ok = run_ok && I.run_on != 0 && I.cnblk + 1 <= I.run_cap && I.cnblk <= (uint32_t)kChain;  // (+1: the committer)
   auto run_elig = [&](uint32_t j) {
     const uint32_t nd = I.prog_need[j];
     return (nd & 4) && !(nd & 8) && (nd & (1u << 17)) && !kept_pod(j);
@@ -6088,7 +6088,7 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
         uint64_t* const g1 = I.rgran.p;
         uint64_t* const g2 = I.rgran.p + (size_t)kChain * kRunGS;
-        const dim3 gr(I.cnblk), bk(kChain);
+        const dim3 gr(I.cnblk + 1), bk(kChain);  // node blocks + the committer
         if (rowm == 2 && (pmask & ~kPmTab) == 0 && cls)
           hipLaunchKernelGGL((k_chain_run<2, kPmTab, kRunLK, kRunTS>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
         else if (rowm == 2 && (pmask & ~kPmTab) == 0)

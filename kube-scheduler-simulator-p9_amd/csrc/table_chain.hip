@@ -1477,6 +1477,7 @@ struct RunWait {
 };
 // Every thread of the block: thread 0 polls the flag, the block joins it.
 __device__ bool run_wait_flag(const RunWait& W) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the owner's node-level atomics of the previous pod)
   if (!W.want) return true;
   if (threadIdx.x == 0) {
     const uint64_t w0 = W.rst ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1737,53 +1738,38 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       A.prow[A.q] = -1;
       A.alog[A.q - A.log_base] = make_int2((int)A.q, node >= 0 && (A.mode & 2) ? node : -1);
     }
-    bool owned = false;
-    if (node >= 0) {
-      if ((uint32_t)node / kChain == b) {  // ---- the owner applies the assume
-        const uint64_t c0 = rst && threadIdx.x == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
-        const uint32_t ln = (uint32_t)node % kChain;
-        if (threadIdx.x == ln) {  // the register row (assume_row_atomic's delta) and the global row
+    if (node >= 0 && (uint32_t)node / kChain == b) {
+      // ---- the owner: its register row and the node-level class-table entries
+      // (only this block reads them; drained before its next class-table reads,
+      // run_wait_flag); the committer block applies the rest
+      const uint64_t c0 = rst && threadIdx.x == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
+      const uint32_t ln = (uint32_t)node % kChain;
+      if (threadIdx.x == ln) {  // (assume_row_atomic's delta)
 #pragma unroll
-          for (uint32_t c = 0; c < 4; ++c)
-            if (c < C.R && (c < 2 || A.need_eph)) row.req[c] += h->req[c];
-          row.nzc += h->nz_cpu;
-          row.nzm += h->nz_mem;
-          row.podcnt += 1;
-          assume_row_atomic(C, V, (uint32_t)node, +1);
-        }
-        if (C.T.on && threadIdx.x < nitems) {
-          int32_t v[KSG_MAX_TOPO];
-#pragma unroll
-          for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? L.tv[s * kChain + ln] : -1;
-          if (threadIdx.x < npm) pc_add(C, it_cls, (uint32_t)node, +1, v, TP_ALL);
-          else tc_add(C, it_term, (uint32_t)node, +1, v, TP_ALL);
-          if (nitems > (uint32_t)kChain)  // (items beyond one per thread)
-            tables_assume_items(C, V, (uint32_t)node, v, +1, threadIdx.x + kChain, kChain, TP_ALL);
-        }
-        if (rst && threadIdx.x == 0) {
-          atomicAdd((unsigned long long*)&rst[44], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - c0));
-          atomicAdd((unsigned long long*)&rst[46], (unsigned long long)(h->n_pc_match + h->n_exist_terms));
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's assume atomics performed
-        if (rst && threadIdx.x == 0)
-          atomicAdd((unsigned long long*)&rst[45], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - c0));
-        __syncthreads();
-        if (threadIdx.x == 0) {
-          run_advance(Y, k);
-          if (rst) {
-            atomicAdd((unsigned long long*)&rst[36], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - c0));
-            atomicAdd((unsigned long long*)&rst[37], 1ull);
-          }
-        }
-        owned = true;  // (the owner's reads need nothing more: run_advance waited for every earlier assume)
+        for (uint32_t c = 0; c < 4; ++c)
+          if (c < C.R && (c < 2 || A.need_eph)) row.req[c] += h->req[c];
+        row.nzc += h->nz_cpu;
+        row.nzm += h->nz_mem;
+        row.podcnt += 1;
       }
-    } else if (b == 0 && threadIdx.x == 0) {
-      run_advance(Y, k);  // no assume: the flag passes the pod
+      if (C.T.on && threadIdx.x < nitems) {
+        int32_t v[KSG_MAX_TOPO];
+#pragma unroll
+        for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? L.tv[s * kChain + ln] : -1;
+        if (threadIdx.x < npm) pc_add(C, it_cls, (uint32_t)node, +1, v, TP_NODE);
+        else tc_add(C, it_term, (uint32_t)node, +1, v, TP_NODE);
+        if (nitems > (uint32_t)kChain)  // (items beyond one per thread)
+          tables_assume_items(C, V, (uint32_t)node, v, +1, threadIdx.x + kChain, kChain, TP_NODE);
+      }
+      if (rst && threadIdx.x == 0) {
+        atomicAdd((unsigned long long*)&rst[36], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - c0));
+        atomicAdd((unsigned long long*)&rst[37], 1ull);
+      }
     }
     // the flag this block waits for before the next pod's class-table reads: every
     // assume up to this pod's if the next pod reads an entry this one writes
     // (tab_rd / tab_md), else every assume before this pod's
-    if (!owned && k + 1 < count) {
+    if (k + 1 < count) {
       const ksg_prog* nh = reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[A.q + 1]);
       wait_for = (node >= 0 && (h->tab_md & nh->tab_rd) != 0) ? tag : k;
     }
@@ -1791,6 +1777,83 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
   }
 #undef RS
 }
+// The committer (the launch's last block, no nodes): per pod it folds the
+// feasible count / status from the partial granules and the argmax from the key
+// granules like every block, then applies the assume's pair-level part — node
+// row atomics, pod-class pc_tot / pc_dom and term-class tc_tot / shared tc_val
+// at the node's topology values — drains it and advances the flag.
+template <uint32_t PM, int TS>
+__device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile& F, const ChainArgs& A0, uint32_t count,
+                                                RunSync* Y, const uint64_t* G1, const uint64_t* G2) {
+  __shared__ ChainRec lrec[kChain / 64];
+  const uint32_t NB = A0.nblk;
+  uint32_t xmask = 0;
+  for (int p = 0; p < F.n; ++p) {
+    const int x = chain_x(F.plugins[p]);
+    if (x >= 0) xmask |= 1u << x;
+  }
+  for (uint32_t k = 0; k < count; ++k) {
+    const uint32_t q = A0.q + k, tag = k + 1u;
+    const uint8_t* prog = A0.progs + A0.prog_off[q];
+    const ProgView V = view(prog);
+    const ksg_prog* h = V.h;
+    const int ns = h->n_tsc_score;
+    const uint32_t npm = (uint32_t)h->n_pc_match, nitems = npm + (uint32_t)h->n_exist_terms;
+    int32_t it_cls = -1;
+    ksg_exist_term it_term;
+    it_term.cls = -1;
+    if (C.T.on && threadIdx.x < nitems) {
+      if (threadIdx.x < npm) it_cls = V.i32[h->pc_match_off + threadIdx.x];
+      else it_term = V.et[h->exist_terms_off + (threadIdx.x - npm)];
+    }
+    ChainRec r;
+    rec_init(r);
+    bool ok = true;
+    if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y);
+    if (__syncthreads_or(!ok)) return;
+    rec_block<TS>(r, lrec, 0u, 0, RB_CNT | RB_ST);
+    ChainRec sk;
+    rec_init(sk);
+    ok = true;
+    if (threadIdx.x < NB) {
+      const uint64_t* g = G2 + (size_t)threadIdx.x * kRunGS;
+      ok = false;
+      for (uint32_t it = 0; it < kRunSpin; ++it) {
+        const uint64_t d = ld_sc1(g + 2);
+        const uint64_t a = gtag(d, tag) ? ld_sc1(g) : 0, c = gtag(d, tag) ? ld_sc1(g + 1) : 0;
+        if (gtag(a, tag) && gtag(c, tag) && gtag(d, tag)) {
+          sk.key = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)c << 32);
+          sk.st = (int32_t)(uint32_t)d;
+          ok = true;
+          break;
+        }
+        if (run_aborted(it, Y)) break;
+        __builtin_amdgcn_s_sleep(kRunSleep);
+      }
+      if (!ok && !ld_sc1(&Y->abort[0])) run_raise(Y);
+    }
+    if (__syncthreads_or(!ok)) return;
+    rec_block<TS>(sk, lrec, 0u, 0, RB_ST | RB_KEY);
+    const int32_t feas = r.feas, st = r.st | sk.st;
+    const bool error = (st & 2) || ((st & 4) && feas > 1) || (h->flags & KPF_PREFILTER_ERROR) || na_prescore_error(h->flags, feas);
+    const uint32_t g = (uint32_t)(sk.key & 0xFFFFFull);
+    if (!error && feas > 0 && (A0.mode & 1) && g >= C.goff && g - C.goff < C.N) {
+      const uint32_t node = g - C.goff;
+      if (threadIdx.x == 0) assume_row_atomic(C, V, node, +1);
+      if (C.T.on && threadIdx.x < nitems) {
+        int32_t v[KSG_MAX_TOPO];
+        node_slot_vids(C, node, v);
+        if (threadIdx.x < npm) pc_add(C, it_cls, node, +1, v, TP_PAIR);
+        else tc_add(C, it_term, node, +1, v, TP_PAIR);
+        if (nitems > (uint32_t)kChain) tables_assume_items(C, V, node, v, +1, threadIdx.x + kChain, kChain, TP_PAIR);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's atomics performed
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) run_advance(Y, k);
+  }
+}
+
 // Plugin sets with a specialisation (PM): the PodTopologySpread / InterPodAffinity
 // profile of cfg4 (with or without TaintToleration / NodeAffinity), every plugin.
 constexpr uint32_t kPmTab = (1u << KP_FIT) | (1u << KP_BA) | (1u << KP_PTS) | (1u << KP_IPA);
@@ -1801,7 +1864,8 @@ constexpr int kRunLK = 8, kRunTS = 4;
 template <int ROWM, uint32_t PM, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC>
 __global__ __launch_bounds__(kChain) void k_chain_run(DevCluster C, DevProfile F, ChainArgs A, uint32_t count, RunSync* Y,
                                                       uint64_t* G1, uint64_t* G2) {
-  run_body<ROWM, PM, LK, TS>(C, F, A, count, Y, G1, G2);
+  if (blockIdx.x == A.nblk) run_commit_body<PM, TS>(C, F, A, count, Y, G1, G2);  // (the extra block)
+  else run_body<ROWM, PM, LK, TS>(C, F, A, count, Y, G1, G2);
 }
 
 // Kernels.  The *_occ twins cap registers at 4 waves per SIMD (a few spills)

@@ -115,7 +115,11 @@ int ksg_gated_pods(const ksg_ctx* ctx, char* buf, size_t cap, size_t* len);
 
 /* Queue mode: schedule queue pods [first, first+count) back to back on the
  * device; every selection is assumed on the device before the next pod
- * (no host round trip per pod).  Asynchronous: ksg_wait() completes it. */
+ * (no host round trip per pod).  Runs of consecutive PodTopologySpread /
+ * InterPodAffinity table-chain pods execute as one persistent launch each
+ * (env KSG_RUN=0: one launch pair per pod); a persistent launch whose blocks
+ * cannot all be resident is never started, and one that stalls fails the call
+ * (KSG_E_DEVICE) instead of hanging.  Asynchronous: ksg_wait() completes it. */
 int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count);
 int ksg_wait(ksg_ctx* ctx, float* device_ms);
 /* What-if step (BASELINE cfg5): queue pods [first, first+count) are each

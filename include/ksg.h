@@ -119,7 +119,9 @@ int ksg_gated_pods(const ksg_ctx* ctx, char* buf, size_t cap, size_t* len);
  * InterPodAffinity table-chain pods execute as one persistent launch each
  * (env KSG_RUN=0: one launch pair per pod); a persistent launch whose blocks
  * cannot all be resident is never started, and one that stalls fails the call
- * (KSG_E_DEVICE) instead of hanging.  Asynchronous: ksg_wait() completes it. */
+ * (KSG_E_DEVICE) instead of hanging — e.g. two unsharded contexts running
+ * persistent launches on one GPU at once, each holding part of the CUs (run one
+ * context per GPU, or KSG_RUN=0).  Asynchronous: ksg_wait() completes it. */
 int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count);
 int ksg_wait(ksg_ctx* ctx, float* device_ms);
 /* What-if step (BASELINE cfg5): queue pods [first, first+count) are each

@@ -75,8 +75,8 @@ def pmc_traffic(kernel):
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")), reverse=True):
         k = json.load(open(f)).get("kernels", {}).get(kernel)  # newest pass that holds the kernel
-        if k is not None:
-            return k["hbm_bytes_per_dispatch"]
+        if k is not None:  # (persistent segments: per pod cycle, like the roofline's "launch")
+            return k.get("hbm_bytes_per_pod", k["hbm_bytes_per_dispatch"])
     return None
 
 

@@ -4512,6 +4512,8 @@ struct Engine::Impl {
   DBuf<SoloCand> ccand;   // k_eval_solo: classes per block [cnblk][kChain]
   int solo = 0;           // one-launch cycles (k_eval_solo): 0 off, 1 on (KSG_SOLO)
   int run_on = 1;         // persistent segments (k_chain_run): KSG_RUN=0 turns them off
+  int run_bt = 256;       // k_chain_run threads per block (KSG_RUN_BT=256|512)
+  uint32_t run_cap512 = 0;
   uint32_t run_cap = 0;   // blocks every one of which is resident at once (k_chain_run), 0: not queried yet
   uint32_t run_min = 2;   // shortest segment launched persistently (KSG_RUN_MIN)
   DBuf<RunSync> rsync;    // k_chain_run's flag and abort word (zeroed per launch)
@@ -4641,6 +4643,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (const char* e = std::getenv("KSG_FOLD_BLOCKS")) I.fold_blocks = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_SOLO")) I.solo = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_RUN")) I.run_on = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_RUN_BT")) I.run_bt = std::strtol(e, nullptr, 10) == 512 ? 512 : 256;
   if (const char* e = std::getenv("KSG_RUN_MIN")) I.run_min = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("KSG_WC_NPT")) I.wc_npt = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_OCC_BLOCKS")) {
@@ -6057,13 +6060,18 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_chain_run<2, ~0u>, kChain, 0));
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_chain_run<2, kPmTab>, kChain, 0));
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ4, k_chain_run<2, kPmTabTN>, kChain, 0));
-    int occ5 = 0;
+    int occ5 = 0, occ6 = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ5, (k_chain_run<2, kPmTab, kRunLK, kRunTS>), kChain, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ6, (k_chain_run<2, kPmTab, kRunLK, kRunTS, 512>), 512, 0));
     const int occ = std::min(std::min(std::min(occ1, occ2), std::min(occ3, occ4)), occ5);
+    I.run_cap512 = occ6 <= 0 ? 0u : I.n_cus * (uint32_t)(occ6 >= 2 ? occ6 - 1 : occ6);
     // (MI355X_MICROARCH.md: the hardware may admit one block per CU fewer than the query)
     I.run_cap = occ <= 0 ? 1u : I.n_cus * (uint32_t)(occ >= 2 ? occ - 1 : occ);
     if (occ <= 0) I.run_on = 0;
   }
+  // 512-thread blocks (KSG_RUN_BT=512): half the blocks, for the small size class of the cfg4 plugin set
+  const uint32_t nb512 = (I.N + 511) / 512;
+  const bool bt512 = I.run_bt == 512 && (pmask & ~kPmTab) == 0 && rowm == 2 && nb512 + 1 <= I.run_cap512 && nb512 <= (uint32_t)kChain;
   run_ok = run_ok && I.run_on != 0 && I.cnblk + 1 <= I.run_cap && I.cnblk <= (uint32_t)kChain;  // (+1: the committer)
   auto run_elig = [&](uint32_t j) {
     const uint32_t nd = I.prog_need[j];
@@ -6089,7 +6097,12 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         uint64_t* const g1 = I.rgran.p;
         uint64_t* const g2 = I.rgran.p + (size_t)kChain * kRunGS;
         const dim3 gr(I.cnblk + 1), bk(kChain);  // node blocks + the committer
-        if (rowm == 2 && (pmask & ~kPmTab) == 0 && cls)
+        if (bt512 && cls) {
+          ChainArgs R5 = RA;
+          R5.nblk = nb512;
+          hipLaunchKernelGGL((k_chain_run<2, kPmTab, kRunLK, kRunTS, 512>), dim3(nb512 + 1), dim3(512), 0, s, C, F, R5, j1 - j,
+                             I.rsync.p, g1, g2);
+        } else if (rowm == 2 && (pmask & ~kPmTab) == 0 && cls)
           hipLaunchKernelGGL((k_chain_run<2, kPmTab, kRunLK, kRunTS>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
         else if (rowm == 2 && (pmask & ~kPmTab) == 0)
           hipLaunchKernelGGL((k_chain_run<2, kPmTab>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);

@@ -28,10 +28,12 @@
 // than the halved partial folds and block arrivals save).
 constexpr int kChain = 256;
 // A thread's topology values in the block's LDS image [KSG_MAX_TOPO][kChain].
-struct ChainVids {
+template <int BT>
+struct ChainVidsT {
   const int32_t* base;
-  __device__ __forceinline__ int32_t operator()(int s) const { return base[s * kChain]; }
+  __device__ __forceinline__ int32_t operator()(int s) const { return base[s * BT]; }
 };
+using ChainVids = ChainVidsT<kChain>;
 
 #define KCP_X_DECL 4
 struct EvalTotals;
@@ -182,7 +184,7 @@ __device__ __forceinline__ int64_t rec_mn(const ChainRec& r, int x) {
 // record per wave, one barrier; every thread returns the block's record (the
 // other fields keep their values).
 enum { RB_CNT = 1, RB_CNT16 = 2, RB_ST = 4, RB_KEY = 8 };  // RB_CNT16: feas, ign < 2^15 per wave (one sum)
-template <int TS = KSG_MAX_TSC>  // (TS: registration words a caller can have, nreg <= TS)
+template <int TS = KSG_MAX_TSC, int BT = kChain>  // (TS: registration words a caller can have, nreg <= TS; BT: block threads)
 __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t xmask, int nreg, uint32_t what) {
   if (what & RB_CNT16) {
     const int32_t p = wave_sum(r.feas | (r.ign << 16));
@@ -246,7 +248,7 @@ __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t x
   if (cnt) r.feas = r.ign = 0;
   if (what & RB_ST) r.st = 0;
 #pragma unroll
-  for (int i = 0; i < kChain / 64; ++i) {
+  for (int i = 0; i < BT / 64; ++i) {
     const ChainRec* o = lds + i;
     if (cnt) {
       r.feas += o->feas;
@@ -276,12 +278,14 @@ __device__ __forceinline__ int64_t pts_count_tab(const DevCluster& C, const Prog
   return s;
 }
 
-struct EvalShared {
-  int32_t tv[KSG_MAX_TOPO * kChain];
+template <int BT>
+struct EvalSharedT {
+  int32_t tv[KSG_MAX_TOPO * BT];
   int32_t minm[KSG_MAX_TSC];
   uint32_t ipa_flags;
-  ChainRec rec[kChain / 64];
+  ChainRec rec[BT / 64];
 };
+using EvalShared = EvalSharedT<kChain>;
 
 // The assume delta's node row as fire-and-forget atomics (no load on the
 // chain's critical path).
@@ -456,11 +460,12 @@ struct RunWait;
 __device__ bool run_wait_flag(const RunWait& W);
 // LK / TS: the lookup-plan entries and spread constraints a pod of the launch has
 // at most (k_chain_run size classes; smaller unrolled loops, less code).
-template <int ROWM, int MODE = kEval, uint32_t PM = ~0u, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC>
+template <int ROWM, int MODE = kEval, uint32_t PM = ~0u, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC, int BT = kChain>
 __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, const ChainArgs& A,
-                                          const uint8_t* __restrict__ prog, EvalShared* Lrun = nullptr,
+                                          const uint8_t* __restrict__ prog, EvalSharedT<BT>* Lrun = nullptr,
                                           RowV* rowrun = nullptr, EvalOut* eo = nullptr, const RunWait* W = nullptr) {
   constexpr bool SOLO = MODE == kSolo, RUN = MODE == kRun;
+  static_assert(BT == kChain || RUN, "other block sizes: the persistent chain only");
   if constexpr (!RUN) chain_warm(prog);
   CS_BEGIN;
   CS_GAP(42, 49, 48);
@@ -468,12 +473,18 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   const uint32_t q = A.q;
   const ProgView V = view(prog);
   const ksg_prog* h = V.h;
-  __shared__ EvalShared Lown;
-  EvalShared& L = RUN ? *Lrun : Lown;
+  EvalSharedT<BT>* Lp;  // (k_chain_run: the caller's)
+  if constexpr (RUN) {
+    Lp = Lrun;
+  } else {
+    __shared__ EvalSharedT<BT> Lown;
+    Lp = &Lown;
+  }
+  EvalSharedT<BT>& L = *Lp;
   uint32_t* of;
   int32_t *os, *ot;
   chain_outs(A, q, C.N, of, os, ot);
-  const uint32_t n = blockIdx.x * kChain + threadIdx.x;
+  const uint32_t n = blockIdx.x * BT + threadIdx.x;
   const bool active = n < C.N;
   const uint32_t nn = active ? n : 0;  // loads of inactive lanes read node 0 (results unused)
   int pts_pos = -1, ipa_pos = -1;
@@ -547,9 +558,9 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   if constexpr (!RUN) {
 #pragma unroll
     for (int s = 0; s < KSG_MAX_TOPO; ++s)
-      if ((uint32_t)s < ntopo) L.tv[s * kChain + threadIdx.x] = vid[s];
+      if ((uint32_t)s < ntopo) L.tv[s * BT + threadIdx.x] = vid[s];
   }
-  const ChainVids tv{L.tv + threadIdx.x};  // (each thread reads back only its own column)
+  const ChainVidsT<BT> tv{L.tv + threadIdx.x};  // (each thread reads back only its own column)
   CS(8);
   // ---- the lookup plan (ksg_look): every class-table count of this node
   int32_t lkv[KSG_LK_MAX], lks[KSG_LK_MAX];
@@ -793,7 +804,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   }
   CS(4);
   if constexpr (RUN) {  // the block's record; the caller publishes it
-    rec_block<TS>(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);
+    rec_block<TS, BT>(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);
     CS(5);
     eo->feasible = feasible;
     eo->ipa_flags = ipa_flags;
@@ -811,7 +822,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     bool fits = true;
 #pragma unroll
     for (int i = 0; i < KCP_X; ++i) fits &= cv[i] >= INT32_MIN && cv[i] <= INT32_MAX;
-    rec_block<TS>(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);  // (its barrier orders the table's reset)
+    rec_block<TS, BT>(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);  // (its barrier orders the table's reset)
     CS(5);
     if (feasible && !fits) atomicOr(&S.dump, 1u);
     lds_barrier();
@@ -884,7 +895,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     if (last) solo_last_select(C, F, A, L.rec, prog, ipa_flags, cs_t0);
     return;
   }
-  rec_block<TS>(rec, L.rec, F.has_ext ? xmask : 0u, nreg, RB_CNT16 | RB_ST | (F.has_ext ? 0u : RB_KEY));
+  rec_block<TS, BT>(rec, L.rec, F.has_ext ? xmask : 0u, nreg, RB_CNT16 | RB_ST | (F.has_ext ? 0u : RB_KEY));
   CS(5);
   if (threadIdx.x == 0) {
     const uint32_t b = blockIdx.x, NB = A.nblk;
@@ -1452,8 +1463,9 @@ __device__ __forceinline__ bool run_aborted(uint32_t i, const RunSync* Y) {
 __device__ __forceinline__ void run_raise(RunSync* Y) {
   __hip_atomic_store(&Y->abort[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-struct RunShared {
-  EvalShared L;
+template <int BT>
+struct RunSharedT {
+  EvalSharedT<BT> L;
   uint32_t go;  // LDS broadcast of a poll's outcome
 };
 // The flag counts the pods of the segment whose assumes are all applied: pod k's
@@ -1567,14 +1579,14 @@ __device__ __forceinline__ bool run_read_g1(const uint64_t* g, uint32_t tag, uin
   return false;
 }
 
-template <int ROWM, uint32_t PM, int LK, int TS>
+template <int ROWM, uint32_t PM, int LK, int TS, int BT>
 __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, const ChainArgs& A0, uint32_t count,
                                          RunSync* Y, uint64_t* G1, uint64_t* G2) {
   static_assert(ROWM != 0, "the persistent chain keeps the node row in registers");
-  __shared__ RunShared S;
-  EvalShared& L = S.L;
+  __shared__ RunSharedT<BT> S;
+  EvalSharedT<BT>& L = S.L;
   const uint32_t NB = A0.nblk, b = blockIdx.x;
-  const uint32_t n = b * kChain + threadIdx.x;
+  const uint32_t n = b * BT + threadIdx.x;
   const bool active = n < C.N;
   const uint32_t nn = active ? n : 0;
   {
@@ -1582,7 +1594,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     node_slot_vids(C, nn, vid);
 #pragma unroll
     for (int s = 0; s < KSG_MAX_TOPO; ++s)
-      if ((uint32_t)s < C.n_topo) L.tv[s * kChain + threadIdx.x] = vid[s];
+      if ((uint32_t)s < C.n_topo) L.tv[s * BT + threadIdx.x] = vid[s];
   }
   RowV row;
   load_row(C, nn, A0.need_eph, row);
@@ -1614,7 +1626,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     EvalOut eo;
     eo.abort = false;
     const RunWait W{Y, wait_for, &S.go, rs_on ? rst : nullptr};
-    eval_body<ROWM, kRun, PM, LK, TS>(C, F, A, prog, &L, &row, &eo, &W);
+    eval_body<ROWM, kRun, PM, LK, TS, BT>(C, F, A, prog, &L, &row, &eo, &W);
     if (eo.abort) return;
     wait_for = 0;
     const int ns = h->n_tsc_score;
@@ -1630,7 +1642,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y);
       if (__syncthreads_or(!ok)) return;
       RS(31);
-      rec_block<TS>(r, L.rec, xmask, ns, RB_CNT | RB_ST);
+      rec_block<TS, BT>(r, L.rec, xmask, ns, RB_CNT | RB_ST);
       RS(39);
       eval_weights(C, h, E);
     }
@@ -1673,13 +1685,13 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     }
     RS(47);
     __syncthreads();  // (L.rec reused)
-    rec_block<TS>(r, L.rec, 0u, 0, RB_ST | RB_KEY);
+    rec_block<TS, BT>(r, L.rec, 0u, 0, RB_ST | RB_KEY);
     if (threadIdx.x < (uint32_t)kRunG2) {
       const uint32_t v = threadIdx.x == 0 ? (uint32_t)r.key : threadIdx.x == 1 ? (uint32_t)(r.key >> 32) : (uint32_t)r.st;
       st_sc1(G2 + (size_t)b * kRunGS + threadIdx.x, gran(tag, v));
     }
     RS(33);
-    if (threadIdx.x == kChain - 32 && k + 1 < count) {  // the next program header into the scalar cache
+    if (threadIdx.x == BT - 32 && k + 1 < count) {  // the next program header into the scalar cache
       uint32_t warm = 0;
       const uint64_t a = (uint64_t)(A.progs + A.prog_off[A.q + 1]);  // (uniform: into scalar registers)
       const uint64_t su = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a) |
@@ -1721,7 +1733,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       }
       if (__syncthreads_or(!ok)) return;
     }
-    rec_block<TS>(sk, L.rec, 0u, 0, RB_ST | RB_KEY);
+    rec_block<TS, BT>(sk, L.rec, 0u, 0, RB_ST | RB_KEY);
     RS(34);
     const int32_t feas = E.r.feas, st = E.r.st | sk.st;
     const bool error = (st & 2) || ((st & 4) && feas > 1) || (h->flags & KPF_PREFILTER_ERROR) || na_prescore_error(h->flags, feas);
@@ -1738,12 +1750,12 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       A.prow[A.q] = -1;
       A.alog[A.q - A.log_base] = make_int2((int)A.q, node >= 0 && (A.mode & 2) ? node : -1);
     }
-    if (node >= 0 && (uint32_t)node / kChain == b) {
+    if (node >= 0 && (uint32_t)node / BT == b) {
       // ---- the owner: its register row and the node-level class-table entries
       // (only this block reads them; drained before its next class-table reads,
       // run_wait_flag); the committer block applies the rest
       const uint64_t c0 = rst && threadIdx.x == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
-      const uint32_t ln = (uint32_t)node % kChain;
+      const uint32_t ln = (uint32_t)node % BT;
       if (threadIdx.x == ln) {  // (assume_row_atomic's delta)
 #pragma unroll
         for (uint32_t c = 0; c < 4; ++c)
@@ -1755,11 +1767,11 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       if (C.T.on && threadIdx.x < nitems) {
         int32_t v[KSG_MAX_TOPO];
 #pragma unroll
-        for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? L.tv[s * kChain + ln] : -1;
+        for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? L.tv[s * BT + ln] : -1;
         if (threadIdx.x < npm) pc_add(C, it_cls, (uint32_t)node, +1, v, TP_NODE);
         else tc_add(C, it_term, (uint32_t)node, +1, v, TP_NODE);
-        if (nitems > (uint32_t)kChain)  // (items beyond one per thread)
-          tables_assume_items(C, V, (uint32_t)node, v, +1, threadIdx.x + kChain, kChain, TP_NODE);
+        if (nitems > (uint32_t)BT)  // (items beyond one per thread)
+          tables_assume_items(C, V, (uint32_t)node, v, +1, threadIdx.x + BT, BT, TP_NODE);
       }
       if (rst && threadIdx.x == 0) {
         atomicAdd((unsigned long long*)&rst[36], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - c0));
@@ -1782,10 +1794,10 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
 // granules like every block, then applies the assume's pair-level part — node
 // row atomics, pod-class pc_tot / pc_dom and term-class tc_tot / shared tc_val
 // at the node's topology values — drains it and advances the flag.
-template <uint32_t PM, int TS>
+template <uint32_t PM, int TS, int BT>
 __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile& F, const ChainArgs& A0, uint32_t count,
                                                 RunSync* Y, const uint64_t* G1, const uint64_t* G2) {
-  __shared__ ChainRec lrec[kChain / 64];
+  __shared__ ChainRec lrec[BT / 64];
   const uint32_t NB = A0.nblk;
   uint32_t xmask = 0;
   for (int p = 0; p < F.n; ++p) {
@@ -1811,7 +1823,7 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
     bool ok = true;
     if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y);
     if (__syncthreads_or(!ok)) return;
-    rec_block<TS>(r, lrec, 0u, 0, RB_CNT | RB_ST);
+    rec_block<TS, BT>(r, lrec, 0u, 0, RB_CNT | RB_ST);
     ChainRec sk;
     rec_init(sk);
     ok = true;
@@ -1833,7 +1845,7 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
       if (!ok && !ld_sc1(&Y->abort[0])) run_raise(Y);
     }
     if (__syncthreads_or(!ok)) return;
-    rec_block<TS>(sk, lrec, 0u, 0, RB_ST | RB_KEY);
+    rec_block<TS, BT>(sk, lrec, 0u, 0, RB_ST | RB_KEY);
     const int32_t feas = r.feas, st = r.st | sk.st;
     const bool error = (st & 2) || ((st & 4) && feas > 1) || (h->flags & KPF_PREFILTER_ERROR) || na_prescore_error(h->flags, feas);
     const uint32_t g = (uint32_t)(sk.key & 0xFFFFFull);
@@ -1845,7 +1857,7 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
         node_slot_vids(C, node, v);
         if (threadIdx.x < npm) pc_add(C, it_cls, node, +1, v, TP_PAIR);
         else tc_add(C, it_term, node, +1, v, TP_PAIR);
-        if (nitems > (uint32_t)kChain) tables_assume_items(C, V, node, v, +1, threadIdx.x + kChain, kChain, TP_PAIR);
+        if (nitems > (uint32_t)BT) tables_assume_items(C, V, node, v, +1, threadIdx.x + BT, BT, TP_PAIR);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's atomics performed
     }
@@ -1861,11 +1873,11 @@ constexpr uint32_t kPmTabTN = kPmTab | (1u << KP_TAINT) | (1u << KP_NA);
 // Size classes: pods with at most kRunLK lookup-plan entries and kRunTS spread
 // constraints (cfg4's) run the small instantiation, the others the generic one.
 constexpr int kRunLK = 8, kRunTS = 4;
-template <int ROWM, uint32_t PM, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC>
-__global__ __launch_bounds__(kChain) void k_chain_run(DevCluster C, DevProfile F, ChainArgs A, uint32_t count, RunSync* Y,
-                                                      uint64_t* G1, uint64_t* G2) {
-  if (blockIdx.x == A.nblk) run_commit_body<PM, TS>(C, F, A, count, Y, G1, G2);  // (the extra block)
-  else run_body<ROWM, PM, LK, TS>(C, F, A, count, Y, G1, G2);
+template <int ROWM, uint32_t PM, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC, int BT = kChain>
+__global__ __launch_bounds__(BT) void k_chain_run(DevCluster C, DevProfile F, ChainArgs A, uint32_t count, RunSync* Y,
+                                                  uint64_t* G1, uint64_t* G2) {
+  if (blockIdx.x == A.nblk) run_commit_body<PM, TS, BT>(C, F, A, count, Y, G1, G2);  // (the extra block)
+  else run_body<ROWM, PM, LK, TS, BT>(C, F, A, count, Y, G1, G2);
 }
 
 // Kernels.  The *_occ twins cap registers at 4 waves per SIMD (a few spills)

@@ -42,14 +42,16 @@ print(json.dumps({{"us_per_pod": dt * 1e6 / {pods}, "paths": s.path_counts(True)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--var", default="KSG_RUN")
+    ap.add_argument("--vals", default="0,1", help="the variable's off,on values")
     ap.add_argument("--nodes", type=int, default=50000)
     ap.add_argument("--existing", type=int, default=200000)
     ap.add_argument("--pods", type=int, default=2000)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--check", type=int, default=200, help="pods checked against the oracle")
     a = ap.parse_args()
-    r0 = one(a.var, 0, a.nodes, a.pods, a.existing, a.steps)
-    r1 = one(a.var, 1, a.nodes, a.pods, a.existing, a.steps)
+    v0, v1 = a.vals.split(",")
+    r0 = one(a.var, v0, a.nodes, a.pods, a.existing, a.steps)
+    r1 = one(a.var, v1, a.nodes, a.pods, a.existing, a.steps)
     same = r0["res"] == r1["res"]
     from _oracle import Oracle
     from ksg import generator as g

@@ -6287,7 +6287,8 @@ bool Engine::outputs(uint32_t j, PodOutputs& out, std::string& err) {
   out.score.resize(N * KSG_MAX_PLUGINS);
   out.total.resize(N);
   HIPCHK(hipMemcpyAsync(out.filter.data(), I.kfilter.p + k * N, N * 4, hipMemcpyDeviceToHost, I.stream));
-  HIPCHK(hipMemcpyAsync(out.score.data(), I.kscore.p + k * N * KSG_MAX_PLUGINS, N * KSG_MAX_PLUGINS * 4,
+  // (the profile's device positions only: rows F.n.. are never read)
+  HIPCHK(hipMemcpyAsync(out.score.data(), I.kscore.p + k * N * KSG_MAX_PLUGINS, N * (size_t)I.F.n * 4,
                         hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipMemcpyAsync(out.total.data(), I.ktotal.p + k * N, N * 4, hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipMemcpyAsync(&out.summary, I.sums.p + j, sizeof(ksg_pod_summary), hipMemcpyDeviceToHost, I.stream));

@@ -1718,8 +1718,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
         const uint64_t* g = G2 + (size_t)threadIdx.x * kRunGS;
         ok = false;
         for (uint32_t it = 0; it < kRunSpin; ++it) {
-          const uint64_t d = ld_sc1(g + 2);
-          const uint64_t a = gtag(d, tag) ? ld_sc1(g) : 0, c = gtag(d, tag) ? ld_sc1(g + 1) : 0;
+          const uint64_t d = ld_sc1(g + 2), a = ld_sc1(g), c = ld_sc1(g + 1);  // (3 granules: all per poll)
           if (gtag(a, tag) && gtag(c, tag) && gtag(d, tag)) {
             sk.key = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)c << 32);
             sk.st = (int32_t)(uint32_t)d;
@@ -1831,8 +1830,7 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
       const uint64_t* g = G2 + (size_t)threadIdx.x * kRunGS;
       ok = false;
       for (uint32_t it = 0; it < kRunSpin; ++it) {
-        const uint64_t d = ld_sc1(g + 2);
-        const uint64_t a = gtag(d, tag) ? ld_sc1(g) : 0, c = gtag(d, tag) ? ld_sc1(g + 1) : 0;
+        const uint64_t d = ld_sc1(g + 2), a = ld_sc1(g), c = ld_sc1(g + 1);
         if (gtag(a, tag) && gtag(c, tag) && gtag(d, tag)) {
           sk.key = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)c << 32);
           sk.st = (int32_t)(uint32_t)d;

@@ -226,12 +226,16 @@ RUN_CASES = [
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("env", [{}, {"KSG_RUN_MIN": "1"}, {"KSG_RUN_BT": "512"}], ids=["default", "min1", "bt512"])
 @pytest.mark.parametrize("name,c,sizes,keep", RUN_CASES, ids=[c[0] for c in RUN_CASES])
-def test_persistent_segments_match_oracle(name, c, sizes, keep):
+def test_persistent_segments_match_oracle(monkeypatch, env, name, c, sizes, keep):
     """Persistent segments (k_chain_run: the pod loop inside one launch, gates
     between blocks) place every pod exactly as the oracle, with 1, 3 and 20
     blocks (XCD groups of unequal size), around kept pods that split a segment,
-    and on a saturating cluster (unschedulable pods in the middle of a segment)."""
+    and on a saturating cluster (unschedulable pods in the middle of a segment);
+    also with one-pod segments allowed (KSG_RUN_MIN=1) and 512-thread blocks."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     doc = g.generate(c, **sizes)
     o = Oracle(doc)
     s = Scheduler(doc["profile"])

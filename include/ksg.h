@@ -39,7 +39,13 @@
 extern "C" {
 #endif
 
-#define KSG_ABI_VERSION 1
+/* ABI history.  1: round-1..2 surface.  2: ksg_load_cluster orders the queue by
+ * PrioritySort and holds back pods with schedulingGates (queue index q is no
+ * longer document order: ksg_queue_pod names it); ksg_queue_pod, ksg_gated_pods,
+ * ksg_cycle_view_acquire / _release added; a context whose persistent launch
+ * stalled refuses calls (KSG_E_STATE) until ksg_load_cluster.  Bindings check
+ * ksg_abi_version() >= the version they were written against. */
+#define KSG_ABI_VERSION 2
 
 #define KSG_OK 0
 #define KSG_E_INVALID (-1)   /* bad argument / JSON */
@@ -117,11 +123,21 @@ int ksg_gated_pods(const ksg_ctx* ctx, char* buf, size_t cap, size_t* len);
  * device; every selection is assumed on the device before the next pod
  * (no host round trip per pod).  Runs of consecutive PodTopologySpread /
  * InterPodAffinity table-chain pods execute as one persistent launch each
- * (env KSG_RUN=0: one launch pair per pod); a persistent launch whose blocks
- * cannot all be resident is never started, and one that stalls fails the call
- * (KSG_E_DEVICE) instead of hanging — e.g. two unsharded contexts running
- * persistent launches on one GPU at once, each holding part of the CUs (run one
- * context per GPU, or KSG_RUN=0).  Asynchronous: ksg_wait() completes it. */
+ * (env KSG_RUN=0: one launch pair per pod).  A persistent launch starts with a
+ * handshake: when its blocks are not all resident within a few ms (e.g. another
+ * context's persistent launch holds part of the CUs) every block leaves before
+ * touching any state and the segment's pods run on the two-launch chain; the
+ * call blocks until each segment's handshake has decided.  A launch that stalls
+ * after its handshake (a poll bound of seconds) fails the call (KSG_E_DEVICE
+ * from this call or ksg_wait) instead of hanging, and the context then refuses
+ * every call (KSG_E_STATE) until ksg_load_cluster.  Asynchronous: ksg_wait()
+ * completes it.
+ * Every queue pod gets exactly one scheduling cycle, in queue order: a pod that
+ * is unschedulable stays so (upstream parks it in unschedulablePods and retries
+ * it after cluster events such as AssignedPodAdd; here the caller re-submits it,
+ * e.g. through ksg_cycle, as the framework does in plugin mode).  The oracle
+ * follows the same rule, so long queues on a tight cluster can diverge from a
+ * live scheduler's retry order, not from the per-cycle results. */
 int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count);
 int ksg_wait(ksg_ctx* ctx, float* device_ms);
 /* What-if step (BASELINE cfg5): queue pods [first, first+count) are each

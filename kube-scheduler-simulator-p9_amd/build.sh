@@ -1,7 +1,7 @@
 #!/bin/bash
-# Builds libksg.so (HIP engine + C++ host layer) in-tree for gfx950.
+# Builds libksg.so (HIP engine + C++ host layer) in-tree for gfx950: the three
+# translation units in parallel, each rebuilt only when it or a header changed.
+# Extra compiler flags go in EXTRA="..." (a change of flags needs `make clean`).
 set -e
 cd "$(dirname "$0")"
-HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
-$HIPCC --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \
-  -Wno-unused-result -o libksg.so csrc/engine.hip csrc/host.cpp csrc/synth.cpp -L/opt/rocm/lib -lrccl "$@"
+make -s -j3 libksg.so EXTRA="$*"

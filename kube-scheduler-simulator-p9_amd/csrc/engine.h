@@ -197,7 +197,12 @@ class Engine {
   uint32_t exchange_ranks() const;
   // diagnostic: pods the per-pod runs sent down the table chain / the scanning chain /
   // of the table-chain pods, those whose cycle was one launch (k_eval_solo)
-  void path_counts(uint64_t out[6]) const;
+  // and persistent segments that fell back to the two-launch chain (out[6])
+  void path_counts(uint64_t out[8]) const;
+  // An aborted persistent launch left the device state half-updated: the context
+  // must be reloaded (host.cpp marks it broken); cleared by a reload.
+  bool lost() const;
+  void clear_lost();
   static bool nccl_unique_id(void* out128, std::string& err);
   // diagnostic: enable (out == nullptr, count pods) / read back s_memtime stamps of the fixup loop
   bool fixup_stamps(uint32_t count, std::vector<uint64_t>* out, std::string& err);

@@ -34,6 +34,9 @@
 #include <vector>
 #include <deque>
 #include <atomic>
+#include <chrono>
+#include <cstddef>
+#include <thread>
 
 #include "engine.h"
 #include <rccl/rccl.h>
@@ -4516,9 +4519,16 @@ struct Engine::Impl {
   uint32_t run_cap512 = 0;
   uint32_t run_cap = 0;   // blocks every one of which is resident at once (k_chain_run), 0: not queried yet
   uint32_t run_min = 2;   // shortest segment launched persistently (KSG_RUN_MIN)
-  DBuf<RunSync> rsync;    // k_chain_run's flag and abort word (zeroed per launch)
-  DBuf<uint64_t> rgran;   // k_chain_run's tagged granules: partial records, then keys [2][kChain][kRunGS] (zeroed per launch)
+  DBuf<RunSync> rsync;    // k_chain_run's flag / handshake (zeroed per launch) and sticky abort word
+  DBuf<uint64_t> rgran;   // k_chain_run's tagged granules: partial records [2 parities], then keys [2] (zeroed per launch)
   bool run_used = false;  // a persistent segment ran since the last sync (its abort word is checked)
+  uint32_t* hverdict = nullptr;  // pinned, coherent: the handshake verdict of the last segment (the host polls it)
+  uint32_t run_lag = 0;          // diagnostic (KSG_RUN_LAG): committer delay per pod, s_sleep(127) rounds
+  uint32_t run_need_extra = 0;   // diagnostic (KSG_RUN_NORES=1): a grid that can never be all resident
+  uint32_t run_wait_us = 5000;   // handshake limit (KSG_RUN_WAIT_US)
+  uint32_t run_spin = kRunSpin;  // polls before a persistent block gives up (KSG_RUN_SPIN: tests force an abort)
+  uint64_t run_fallbacks = 0;    // segments that ran on the two-launch chain (not co-resident)
+  bool lost = false;             // an aborted persistent launch left the device state half-updated
   uint32_t fold_blocks = 256;  // table chain: k_fold above this many blocks (KSG_FOLD_BLOCKS; tests force it)
   uint32_t occ_blocks = 0;     // table chain: occupancy twins above this many blocks (0: 2 per CU; KSG_OCC_BLOCKS)
   bool occ_force = false;
@@ -4624,6 +4634,7 @@ Engine::~Engine() {
   if (p_->stream) (void)hipStreamSynchronize(p_->stream);  // (queued host exchanges use the buffers below)
   if (p_->hps) (void)hipHostFree(p_->hps);
   if (p_->hpr) (void)hipHostFree(p_->hpr);
+  if (p_->hverdict) (void)hipHostFree(p_->hverdict);
   if (p_->ev0) (void)hipEventDestroy(p_->ev0);
   if (p_->ev1) (void)hipEventDestroy(p_->ev1);
   for (hipEvent_t e : {p_->sev_ready[0], p_->sev_ready[1], p_->sev_ready[2], p_->sev_free})
@@ -4645,6 +4656,11 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (const char* e = std::getenv("KSG_RUN")) I.run_on = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_RUN_BT")) I.run_bt = std::strtol(e, nullptr, 10) == 512 ? 512 : 256;
   if (const char* e = std::getenv("KSG_RUN_MIN")) I.run_min = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
+  if (const char* e = std::getenv("KSG_RUN_LAG")) I.run_lag = std::min<uint32_t>(4096, (uint32_t)std::strtoul(e, nullptr, 10));
+  if (const char* e = std::getenv("KSG_RUN_NORES")) I.run_need_extra = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
+  if (const char* e = std::getenv("KSG_RUN_SPIN")) I.run_spin = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
+  if (const char* e = std::getenv("KSG_RUN_WAIT_US"))
+    I.run_wait_us = std::max<uint32_t>(10, std::min<uint32_t>(1000000, (uint32_t)std::strtoul(e, nullptr, 10)));
   if (const char* e = std::getenv("KSG_WC_NPT")) I.wc_npt = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_OCC_BLOCKS")) {
     I.occ_blocks = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -6077,7 +6093,13 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
     const uint32_t nd = I.prog_need[j];
     return (nd & 4) && !(nd & 8) && (nd & (1u << 17)) && !kept_pod(j);
   };
-  if (run_ok && (!I.rsync.alloc(1, err) || !I.rgran.alloc((size_t)2 * kChain * kRunGS, err))) return false;
+  if (run_ok) {
+    if (!I.rsync.alloc(1, err) || !I.rgran.alloc(4 * kRunSlot, err)) return false;
+    if (!I.hverdict) {
+      HIPCHK(hipHostMalloc((void**)&I.hverdict, 64, hipHostMallocCoherent | hipHostMallocMapped));
+      HIPCHK(hipMemsetAsync(I.rsync.p, 0, sizeof(RunSync), s));  // (the sticky abort word starts clear)
+    }
+  }
   for (uint32_t j = first; j < first + count; ++j) {
     const uint8_t* prog = I.progs.p + I.prog_off[j];
     if (run_ok && run_elig(j)) {
@@ -6090,38 +6112,76 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         CA.prog = prog;
         CA.xsend = nullptr;
         ChainArgs RA = CA;  // (stamps: k_chain_run's own slots)
-        HIPCHK(hipMemsetAsync(I.rsync.p, 0, sizeof(RunSync), s));
-        HIPCHK(hipMemsetAsync(I.rgran.p, 0, (size_t)2 * kChain * kRunGS * sizeof(uint64_t), s));
+        HIPCHK(hipMemsetAsync(I.rsync.p, 0, kRunSyncReset, s));
+        HIPCHK(hipMemsetAsync(I.rgran.p, 0, 4 * kRunSlot * sizeof(uint64_t), s));
         const bool sampled = I.sample_every && I.n_samples * 2 + 2 <= I.sev.size();
         if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
         uint64_t* const g1 = I.rgran.p;
-        uint64_t* const g2 = I.rgran.p + (size_t)kChain * kRunGS;
-        const dim3 gr(I.cnblk + 1), bk(kChain);  // node blocks + the committer
-        if (bt512 && cls) {
+        uint64_t* const g2 = I.rgran.p + 2 * kRunSlot;
+        const bool l512 = bt512 && cls;
+        const uint32_t grid = (l512 ? nb512 : I.cnblk) + 1;  // node blocks + the committer
+        uint32_t* const hv = I.hverdict;
+        __atomic_store_n(hv, 0u, __ATOMIC_RELEASE);  // (the previous segment's verdict was read)
+        const RunCtl RC{grid + I.run_need_extra, I.run_wait_us * 100u, I.run_lag, hv, I.run_spin};
+        const dim3 gr(grid), bk(kChain);
+        if (l512) {
           ChainArgs R5 = RA;
           R5.nblk = nb512;
-          hipLaunchKernelGGL((k_chain_run<2, kPmTab, kRunLK, kRunTS, 512>), dim3(nb512 + 1), dim3(512), 0, s, C, F, R5, j1 - j,
-                             I.rsync.p, g1, g2);
+          hipLaunchKernelGGL((k_chain_run<2, kPmTab, kRunLK, kRunTS, 512>), gr, dim3(512), 0, s, C, F, R5, j1 - j,
+                             I.rsync.p, g1, g2, RC);
         } else if (rowm == 2 && (pmask & ~kPmTab) == 0 && cls)
-          hipLaunchKernelGGL((k_chain_run<2, kPmTab, kRunLK, kRunTS>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
+          hipLaunchKernelGGL((k_chain_run<2, kPmTab, kRunLK, kRunTS>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC);
         else if (rowm == 2 && (pmask & ~kPmTab) == 0)
-          hipLaunchKernelGGL((k_chain_run<2, kPmTab>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
+          hipLaunchKernelGGL((k_chain_run<2, kPmTab>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC);
         else if (rowm == 2 && (pmask & ~kPmTabTN) == 0)
-          hipLaunchKernelGGL((k_chain_run<2, kPmTabTN>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
-        else if (rowm == 2) hipLaunchKernelGGL((k_chain_run<2, ~0u>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
-        else hipLaunchKernelGGL((k_chain_run<1, ~0u>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2);
+          hipLaunchKernelGGL((k_chain_run<2, kPmTabTN>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC);
+        else if (rowm == 2) hipLaunchKernelGGL((k_chain_run<2, ~0u>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC);
+        else hipLaunchKernelGGL((k_chain_run<1, ~0u>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC);
         if (sampled) {
           HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
           I.n_samples++;
         }
         HIPCHK(hipGetLastError());
         I.run_used = true;
-        I.path_pods[0] += j1 - j;
-        I.path_pods[4] += j1 - j;
-        I.path_pods[5]++;
-        pending |= (CA.mode & 2) != 0;
-        j = j1 - 1;
-        continue;
+        // The handshake: the launch's blocks decide whether all of them are
+        // resident before any state changes.  The host waits for that verdict (the
+        // work queued before the segment runs first), then queues the rest.
+        uint32_t v = 0;
+        {
+          const auto t0 = std::chrono::steady_clock::now();
+          for (uint32_t it = 0; (v = __atomic_load_n(hv, __ATOMIC_ACQUIRE)) == 0u; ++it) {
+            if ((it & 1023u) == 1023u) {
+              if (hipStreamQuery(s) == hipSuccess && (v = __atomic_load_n(hv, __ATOMIC_ACQUIRE)) == 0u) {
+                I.lost = true;
+                err = "persistent table chain: the launch ended without a handshake";
+                return false;
+              }
+              if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+                I.lost = true;
+                err = "persistent table chain: the launch did not start within 60 s";
+                return false;
+              }
+              std::this_thread::yield();
+            }
+          }
+        }
+        if (v == 3u) {  // an earlier segment of this call aborted: the state is not valid
+          I.lost = true;
+          err = "persistent table chain: a gate never completed (blocks not co-resident?)";
+          return false;
+        }
+        if (v == 1u) {
+          I.path_pods[0] += j1 - j;
+          I.path_pods[4] += j1 - j;
+          I.path_pods[5]++;
+          pending |= (CA.mode & 2) != 0;
+          j = j1 - 1;
+          continue;
+        }
+        // v == 2: the blocks were not all resident; they left untouched.  This and
+        // the call's later segments run on the two-launch chain.
+        I.run_fallbacks++;
+        run_ok = false;
       }
     }
     if (I.prog_need[j] & 4) {
@@ -6266,7 +6326,14 @@ bool Engine::sync(std::string& err) {
     I.run_used = false;
     uint32_t ab = 0;
     HIPCHK(hipMemcpy(&ab, I.rsync.p->abort, sizeof(ab), hipMemcpyDeviceToHost));
-    if (ab) { err = "persistent table chain: a gate never completed (blocks not co-resident?)"; return false; }
+    if (ab) {
+      // the segment (and every later one of its call, which left at the handshake)
+      // left summaries unwritten and assumes half applied: the state is lost
+      HIPCHK(hipMemset(I.rsync.p->abort, 0, sizeof(ab)));
+      I.lost = true;
+      err = "persistent table chain: a gate never completed (blocks not co-resident?)";
+      return false;
+    }
   }
   HIPCHK(hipEventElapsedTime(&I.last_ms, I.ev0, I.ev1));
   return true;
@@ -6369,8 +6436,20 @@ bool Engine::set_exchange(int mode, const void* nccl_id, uint32_t rank, uint32_t
 }
 
 uint32_t Engine::exchange_ranks() const { return p_->xranks; }
-void Engine::path_counts(uint64_t out[6]) const {
+void Engine::path_counts(uint64_t out[8]) const {
   for (int i = 0; i < 6; ++i) out[i] = p_->path_pods[i];
+  out[6] = p_->run_fallbacks;
+  out[7] = 0;
+}
+bool Engine::lost() const { return p_->lost; }
+void Engine::clear_lost() {
+  Impl& I = *p_;
+  if (I.rsync.p && (I.lost || I.run_used)) {  // (the sticky abort word: a call that failed before its sync left it set)
+    (void)hipStreamSynchronize(I.stream);
+    (void)hipMemset(I.rsync.p, 0, sizeof(RunSync));
+    I.run_used = false;
+  }
+  I.lost = false;
 }
 
 bool Engine::nccl_unique_id(void* out128, std::string& err) {

@@ -12,6 +12,7 @@
 // (raw x weight for plugins without ScoreExtensions), selected node on Reserve.
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cctype>
 #include <cstdio>
 #include <cstring>
@@ -2680,6 +2681,7 @@ struct Cluster {
     index_queue();
     qneed.clear();
     broken = false;
+    eng->clear_lost();
     for (auto& p : queue)
       if (!volumes_modelled(p)) return false;
     if (!equal_priorities()) return false;
@@ -3989,15 +3991,22 @@ using ksg::host::Cluster;
 // per-node reads of the framework's parallel Filter / Score workers go through
 // a ksg_cycle_view instead (no call, no lock).  last_error is also kept per
 // thread: ksg_last_error returns the calling thread's last failure on ctx.
+// The thread-local copy is tagged with the context's generation id (unique per
+// ksg_create), so a context freed and reallocated at the same address never
+// returns its predecessor's error.
+static std::atomic<uint64_t> g_ctx_gen{0};
 static thread_local const void* t_err_ctx = nullptr;
+static thread_local uint64_t t_err_gen = 0;
 static thread_local std::string t_err;
 struct ksg_ctx {
   Cluster c;
   std::string last_error;
   mutable std::recursive_mutex mu;
+  const uint64_t gen = ++g_ctx_gen;
   int fail(const std::string& m, int code) {
     last_error = m;
     t_err_ctx = this;
+    t_err_gen = gen;
     t_err = m;
     return code;
   }
@@ -4011,6 +4020,7 @@ struct ksg_ctx {
 #define KSG_GUARD(ctx)                                                                                   \
   do {                                                                                                   \
     if (!(ctx)) return KSG_E_INVALID;                                                                    \
+    if ((ctx)->c.eng && (ctx)->c.eng->lost()) (ctx)->c.broken = true;                                    \
     if ((ctx)->c.broken) return (ctx)->fail("context unusable after a device error: reload", KSG_E_STATE); \
   } while (0)
 
@@ -4043,13 +4053,21 @@ int ksg_create(const char* profile_json, size_t len, const ksg_opts* opts, ksg_c
   return KSG_OK;
 }
 
-void ksg_destroy(ksg_ctx* ctx) { delete ctx; }
+void ksg_destroy(ksg_ctx* ctx) {
+  if (ctx && t_err_ctx == ctx) t_err_ctx = nullptr;
+  delete ctx;
+}
 
+// Always the calling thread's own copy: another thread's fail() can reassign
+// ctx->last_error after the lock is released, so it is copied under the lock.
 const char* ksg_last_error(const ksg_ctx* ctx) {
   if (!ctx) return "null context";
-  if (t_err_ctx == ctx) return t_err.c_str();
+  if (t_err_ctx == ctx && t_err_gen == ctx->gen) return t_err.c_str();
   KSG_LOCK(ctx);
-  return ctx->last_error.c_str();
+  t_err = ctx->last_error;
+  t_err_ctx = ctx;
+  t_err_gen = ctx->gen;
+  return t_err.c_str();
 }
 
 int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len) {
@@ -4275,7 +4293,7 @@ extern "C" int ksg_debug_eval_stamps(ksg_ctx* ctx, int on, uint64_t* out, size_t
 // diagnostic (not in ksg.h): out[6] = pods run through the table chain / the scanning
 // chain so far, of the first those whose cycle was one launch, what-if pod chunks
 // that ran the class path, table-chain pods of persistent segments (k_chain_run)
-// and those segments
+// and those segments, segments that fell back to the two-launch chain, 0
 extern "C" int ksg_debug_path_counts(ksg_ctx* ctx, uint64_t* out) {
   KSG_LOCK(ctx);
   if (!ctx || !out) return KSG_E_INVALID;

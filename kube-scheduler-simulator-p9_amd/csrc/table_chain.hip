@@ -1447,21 +1447,70 @@ __device__ __forceinline__ void final_body(DevCluster& C, const DevProfile& F, c
 // constraint, no host ports / volume claims / CSI volumes (nothing but the rows
 // and the class tables changes during the segment), outputs not kept, committing
 // cycles of an unsharded context whose profile normalises.
+// Launch handshake: every block adds to `arrive` on entry and waits (bounded by
+// RunCtl::wait_ticks) until the whole grid has arrived; the first block to decide
+// sets `verdict` by compare-and-swap (1: every block resident, go; 2: not
+// co-resident; 3: an earlier segment of the call aborted) and publishes it to the
+// host's pinned word; a block seeing anything but 1 leaves before touching any
+// state, so the host can run the segment's pods on the two-launch chain instead.
+// Granules are double-buffered by pod parity: pod k's slot is rewritten only by
+// pod k + 2, whose class-table wait needs flag >= k + 1, i.e. the committer done
+// with pod k (it is allowed to lag the node blocks by one pod).
 struct RunSync {
-  uint64_t flag[16];   // k + 1: pod k's assume is applied (written by the owning block)
-  uint32_t abort[32];  // a poll ran out: every block leaves
+  uint64_t flag[16];     // k + 1: pod k's assume is applied (written by the committer)
+  uint32_t arrive[32];   // blocks that entered the launch (handshake)
+  uint32_t verdict[32];  // handshake outcome (0 undecided)
+  uint32_t abort[32];    // a poll ran out: every block leaves; sticky until Engine::sync reads it
+};
+constexpr size_t kRunSyncReset = offsetof(RunSync, abort);  // bytes zeroed per launch (the abort word is kept)
+struct RunCtl {
+  uint32_t need;           // blocks that must be resident (the grid; more forces the fallback: tests)
+  uint32_t wait_ticks;     // handshake limit in s_memrealtime ticks (100 MHz)
+  uint32_t lag;            // diagnostic: the committer's s_sleep(127) rounds before each pod's granule reads
+  uint32_t* host_verdict;  // pinned host word the deciding block writes (the host polls it), or null
+  uint32_t spin;           // polls before a block gives up (kRunSpin; tests force an abort with few)
 };
 constexpr uint32_t kRunSpin = 1u << 22;  // polls (~1 us each with the load) before a block gives up
 constexpr int kRunSleep = 8;             // s_sleep between polls (x 64 cycles): every block polls every block
 constexpr int kRunG1 = 2 + 4 * KCP_X + 2 * KSG_MAX_TSC;  // partial-record granules per block (max)
 constexpr int kRunG2 = 3;                                // key granules per block
 constexpr int kRunGS = 64;                               // granule stride per block (uint64)
+constexpr size_t kRunSlot = (size_t)kChain * kRunGS;     // one parity slot of one granule kind (uint64)
 __device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t v) { return ((uint64_t)tag << 32) | v; }
 __device__ __forceinline__ bool run_aborted(uint32_t i, const RunSync* Y) {
   return (i & 63u) == 63u && ld_sc1(&Y->abort[0]) != 0u;
 }
 __device__ __forceinline__ void run_raise(RunSync* Y) {
   __hip_atomic_store(&Y->abort[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The launch handshake (every thread of the block; thread 0 decides): true = go.
+__device__ bool run_handshake(RunSync* Y, const RunCtl& R, uint32_t* go) {
+  if (threadIdx.x == 0) {
+    uint32_t want = 1;
+    if (ld_sc1(&Y->abort[0]) != 0u) {
+      want = 3;
+    } else {
+      __hip_atomic_fetch_add(&Y->arrive[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      want = 2;
+      for (;;) {
+        if (ld_sc1(&Y->arrive[0]) >= R.need) { want = 1; break; }
+        if (ld_sc1(&Y->verdict[0]) != 0u) break;  // decided by another block
+        if (__builtin_amdgcn_s_memrealtime() - t0 > R.wait_ticks) break;
+        __builtin_amdgcn_s_sleep(4);
+      }
+    }
+    uint32_t old = 0;
+    __hip_atomic_compare_exchange_strong(&Y->verdict[0], &old, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t v = old == 0 ? want : old;
+    if (old == 0 && R.host_verdict) __hip_atomic_store(R.host_verdict, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    *go = v;
+  }
+  __syncthreads();
+  const bool ok = *go == 1u;
+  __syncthreads();  // (go is reused by the body)
+  return ok;
 }
 template <int BT>
 struct RunSharedT {
@@ -1471,9 +1520,9 @@ struct RunSharedT {
 // The flag counts the pods of the segment whose assumes are all applied: pod k's
 // owner (block 0 for a pod that places nothing) raises it to k + 1 once it
 // reads k (thread 0; bounded like every poll).
-__device__ __forceinline__ void run_advance(RunSync* Y, uint32_t k) {
+__device__ __forceinline__ void run_advance(RunSync* Y, uint32_t k, uint32_t spin) {
   bool ok = false;
-  for (uint32_t it = 0; it < kRunSpin; ++it) {
+  for (uint32_t it = 0; it < spin; ++it) {
     if (ld_sc1(&Y->flag[0]) >= k) { ok = true; break; }
     if (run_aborted(it, Y)) return;
     __builtin_amdgcn_s_sleep(2);
@@ -1483,18 +1532,26 @@ __device__ __forceinline__ void run_advance(RunSync* Y, uint32_t k) {
 }
 struct RunWait {
   RunSync* Y;
-  uint32_t want;  // flag value awaited (0: none)
-  uint32_t* go;   // RunShared::go
-  uint64_t* rst;  // diagnostic stamps (block 0), or null
+  uint32_t want;   // flag value awaited (0: none)
+  uint32_t* go;    // RunShared::go
+  uint64_t* rst;   // diagnostic stamps (block 0), or null
+  uint32_t owned;  // this block applied the previous pod's node-level assume
+  uint32_t spin;   // RunCtl::spin
 };
-// Every thread of the block: thread 0 polls the flag, the block joins it.
+// Every thread of the block: thread 0 polls the flag, the block joins it.  The
+// owner's node-level atomics of the previous pod were issued by the item lanes of
+// some waves and are read by lanes of others: every wave drains its own, and a
+// barrier orders them before any wave's class-table reads.
 __device__ bool run_wait_flag(const RunWait& W) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the owner's node-level atomics of the previous pod)
-  if (!W.want) return true;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!W.want) {
+    if (W.owned) __syncthreads();
+    return true;
+  }
   if (threadIdx.x == 0) {
     const uint64_t w0 = W.rst ? __builtin_amdgcn_s_memrealtime() : 0;
     bool ok = false;
-    for (uint32_t it = 0; it < kRunSpin; ++it) {
+    for (uint32_t it = 0; it < W.spin; ++it) {
       if (ld_sc1(&W.Y->flag[0]) >= W.want) { ok = true; break; }
       if (run_aborted(it, W.Y)) break;
       __builtin_amdgcn_s_sleep(2);
@@ -1537,9 +1594,9 @@ __device__ __forceinline__ int64_t g64(uint64_t lo, uint64_t hi) { return (int64
 // thread t < NB: block t's partial record, polled until every granule carries tag
 template <int TS>
 __device__ __forceinline__ bool run_read_g1(const uint64_t* g, uint32_t tag, uint32_t xmask, int ns, ChainRec& r,
-                                            const RunSync* Y) {
+                                            const RunSync* Y, uint32_t spin) {
   const int last = run_g1_count(xmask, ns) - 1;
-  for (uint32_t it = 0; it < kRunSpin; ++it) {
+  for (uint32_t it = 0; it < spin; ++it) {
     // one granule per poll until it carries the tag (few loads in flight chip-wide),
     // then the whole record (whose tags are checked again)
     if (!gtag(ld_sc1(g + last), tag)) {
@@ -1581,10 +1638,11 @@ __device__ __forceinline__ bool run_read_g1(const uint64_t* g, uint32_t tag, uin
 
 template <int ROWM, uint32_t PM, int LK, int TS, int BT>
 __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, const ChainArgs& A0, uint32_t count,
-                                         RunSync* Y, uint64_t* G1, uint64_t* G2) {
+                                         RunSync* Y, uint64_t* G1s, uint64_t* G2s, const RunCtl& R) {
   static_assert(ROWM != 0, "the persistent chain keeps the node row in registers");
   __shared__ RunSharedT<BT> S;
   EvalSharedT<BT>& L = S.L;
+  if (!run_handshake(Y, R, &S.go)) return;
   const uint32_t NB = A0.nblk, b = blockIdx.x;
   const uint32_t n = b * BT + threadIdx.x;
   const bool active = n < C.N;
@@ -1613,11 +1671,14 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
   if (rs_on) atomicAdd((unsigned long long*)&rst[k], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - rs_t0))
   __syncthreads();
   uint32_t wait_for = 0;  // the flag value this block needs before its next class-table read (0: none)
+  uint32_t owned = 0;     // this block applied the previous pod's node-level assume
   for (uint32_t k = 0; k < count; ++k) {
     ChainArgs A = A0;  // (A.stamps: eval_body's own k_eval slots, block 0)
     A.q = A0.q + k;
     const uint8_t* prog = A.progs + A.prog_off[A.q];
     const uint32_t tag = k + 1u;
+    uint64_t* const G1 = G1s + (k & 1u) * kRunSlot;  // (parity slots)
+    uint64_t* const G2 = G2s + (k & 1u) * kRunSlot;
     if (rs_on) rs_t0 = __builtin_amdgcn_s_memrealtime();
     const ProgView V = view(prog);
     const ksg_prog* h = V.h;
@@ -1625,10 +1686,11 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     // the class-table reads), its partial record
     EvalOut eo;
     eo.abort = false;
-    const RunWait W{Y, wait_for, &S.go, rs_on ? rst : nullptr};
+    const RunWait W{Y, wait_for, &S.go, rs_on ? rst : nullptr, owned, R.spin};
     eval_body<ROWM, kRun, PM, LK, TS, BT>(C, F, A, prog, &L, &row, &eo, &W);
     if (eo.abort) return;
     wait_for = 0;
+    owned = 0;
     const int ns = h->n_tsc_score;
     const int ng1 = run_g1_count(xmask, ns);
     if (threadIdx.x < (uint32_t)ng1) st_sc1(G1 + (size_t)b * kRunGS + threadIdx.x, gran(tag, run_g1_value<TS>(eo.rec, (int)threadIdx.x, xmask, ns)));
@@ -1639,7 +1701,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       ChainRec& r = E.r;
       rec_init(r);
       bool ok = true;
-      if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y);
+      if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y, R.spin);
       if (__syncthreads_or(!ok)) return;
       RS(31);
       rec_block<TS, BT>(r, L.rec, xmask, ns, RB_CNT | RB_ST);
@@ -1717,7 +1779,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       if (threadIdx.x < NB) {
         const uint64_t* g = G2 + (size_t)threadIdx.x * kRunGS;
         ok = false;
-        for (uint32_t it = 0; it < kRunSpin; ++it) {
+        for (uint32_t it = 0; it < R.spin; ++it) {
           const uint64_t d = ld_sc1(g + 2), a = ld_sc1(g), c = ld_sc1(g + 1);  // (3 granules: all per poll)
           if (gtag(a, tag) && gtag(c, tag) && gtag(d, tag)) {
             sk.key = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)c << 32);
@@ -1753,6 +1815,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       // ---- the owner: its register row and the node-level class-table entries
       // (only this block reads them; drained before its next class-table reads,
       // run_wait_flag); the committer block applies the rest
+      owned = 1;
       const uint64_t c0 = rst && threadIdx.x == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
       const uint32_t ln = (uint32_t)node % BT;
       if (threadIdx.x == ln) {  // (assume_row_atomic's delta)
@@ -1795,8 +1858,10 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
 // at the node's topology values — drains it and advances the flag.
 template <uint32_t PM, int TS, int BT>
 __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile& F, const ChainArgs& A0, uint32_t count,
-                                                RunSync* Y, const uint64_t* G1, const uint64_t* G2) {
+                                                RunSync* Y, const uint64_t* G1s, const uint64_t* G2s, const RunCtl& R) {
   __shared__ ChainRec lrec[BT / 64];
+  __shared__ uint32_t go;
+  if (!run_handshake(Y, R, &go)) return;
   const uint32_t NB = A0.nblk;
   uint32_t xmask = 0;
   for (int p = 0; p < F.n; ++p) {
@@ -1805,6 +1870,9 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
   }
   for (uint32_t k = 0; k < count; ++k) {
     const uint32_t q = A0.q + k, tag = k + 1u;
+    const uint64_t* const G1 = G1s + (k & 1u) * kRunSlot;  // (parity slots)
+    const uint64_t* const G2 = G2s + (k & 1u) * kRunSlot;
+    for (uint32_t i = 0; i < R.lag; ++i) __builtin_amdgcn_s_sleep(127);  // (diagnostic: a lagging committer)
     const uint8_t* prog = A0.progs + A0.prog_off[q];
     const ProgView V = view(prog);
     const ksg_prog* h = V.h;
@@ -1820,7 +1888,7 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
     ChainRec r;
     rec_init(r);
     bool ok = true;
-    if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y);
+    if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y, R.spin);
     if (__syncthreads_or(!ok)) return;
     rec_block<TS, BT>(r, lrec, 0u, 0, RB_CNT | RB_ST);
     ChainRec sk;
@@ -1829,7 +1897,7 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
     if (threadIdx.x < NB) {
       const uint64_t* g = G2 + (size_t)threadIdx.x * kRunGS;
       ok = false;
-      for (uint32_t it = 0; it < kRunSpin; ++it) {
+      for (uint32_t it = 0; it < R.spin; ++it) {
         const uint64_t d = ld_sc1(g + 2), a = ld_sc1(g), c = ld_sc1(g + 1);
         if (gtag(a, tag) && gtag(c, tag) && gtag(d, tag)) {
           sk.key = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)c << 32);
@@ -1860,7 +1928,7 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's atomics performed
     }
     __syncthreads();
-    if (threadIdx.x == 0) run_advance(Y, k);
+    if (threadIdx.x == 0) run_advance(Y, k, R.spin);
   }
 }
 
@@ -1873,9 +1941,9 @@ constexpr uint32_t kPmTabTN = kPmTab | (1u << KP_TAINT) | (1u << KP_NA);
 constexpr int kRunLK = 8, kRunTS = 4;
 template <int ROWM, uint32_t PM, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC, int BT = kChain>
 __global__ __launch_bounds__(BT) void k_chain_run(DevCluster C, DevProfile F, ChainArgs A, uint32_t count, RunSync* Y,
-                                                  uint64_t* G1, uint64_t* G2) {
-  if (blockIdx.x == A.nblk) run_commit_body<PM, TS, BT>(C, F, A, count, Y, G1, G2);  // (the extra block)
-  else run_body<ROWM, PM, LK, TS, BT>(C, F, A, count, Y, G1, G2);
+                                                  uint64_t* G1, uint64_t* G2, RunCtl R) {
+  if (blockIdx.x == A.nblk) run_commit_body<PM, TS, BT>(C, F, A, count, Y, G1, G2, R);  // (the extra block)
+  else run_body<ROWM, PM, LK, TS, BT>(C, F, A, count, Y, G1, G2, R);
 }
 
 // Kernels.  The *_occ twins cap registers at 4 waves per SIMD (a few spills)

@@ -304,21 +304,28 @@ class Scheduler:
     def path_counts(self, solo=False):
         """Diagnostic: (pods through the table chain, pods through the scanning chain) so far
         (+ of the first, the one-launch cycles when solo)."""
-        out = (ctypes.c_uint64 * 6)()
+        out = (ctypes.c_uint64 * 8)()
         self._chk(self.L.ksg_debug_path_counts(self.h, out), "ksg_debug_path_counts")
         return (out[0], out[1], out[2]) if solo else (out[0], out[1])
 
     def whatif_class_chunks(self):
         """Diagnostic: what-if pod chunks that ran the class path (k_whatif_cls1/2)."""
-        out = (ctypes.c_uint64 * 6)()
+        out = (ctypes.c_uint64 * 8)()
         self._chk(self.L.ksg_debug_path_counts(self.h, out), "ksg_debug_path_counts")
         return out[3]
 
     def run_counts(self):
         """Diagnostic: (table-chain pods of persistent segments, segments) so far (k_chain_run)."""
-        out = (ctypes.c_uint64 * 6)()
+        out = (ctypes.c_uint64 * 8)()
         self._chk(self.L.ksg_debug_path_counts(self.h, out), "ksg_debug_path_counts")
         return out[4], out[5]
+
+    def run_fallbacks(self):
+        """Diagnostic: persistent segments whose blocks were not all resident and ran on
+        the two-launch chain instead."""
+        out = (ctypes.c_uint64 * 8)()
+        self._chk(self.L.ksg_debug_path_counts(self.h, out), "ksg_debug_path_counts")
+        return out[6]
 
     def set_path(self, per_pod: bool):
         self._chk(self.L.ksg_set_path(self.h, 1 if per_pod else 0), "ksg_set_path")

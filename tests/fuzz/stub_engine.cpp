@@ -234,9 +234,11 @@ bool Engine::set_exchange(int, const void*, uint32_t, uint32_t, ExchangeFn, void
   return false;
 }
 uint32_t Engine::exchange_ranks() const { return 1; }
-void Engine::path_counts(uint64_t out[6]) const {
-  for (int i = 0; i < 6; ++i) out[i] = 0;
+void Engine::path_counts(uint64_t out[8]) const {
+  for (int i = 0; i < 8; ++i) out[i] = 0;
 }
+bool Engine::lost() const { return false; }
+void Engine::clear_lost() {}
 bool Engine::nccl_unique_id(void*, std::string& err) {
   err = "stub: no RCCL";
   return false;

@@ -7,7 +7,7 @@ finalscore-result, prefilter/prescore status, selected-node) byte-for-byte.
 import pytest
 
 from _oracle import Oracle
-from ksg import Scheduler, generator as g
+from ksg import KsgError, Scheduler, generator as g
 
 CASES = [
     ("cfg1-default-profile", 1, dict(n_nodes=40, n_pods=120)),
@@ -226,14 +226,18 @@ RUN_CASES = [
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"KSG_RUN_MIN": "1"}, {"KSG_RUN_BT": "512"}], ids=["default", "min1", "bt512"])
+@pytest.mark.parametrize("env", [{}, {"KSG_RUN_MIN": "1"}, {"KSG_RUN_BT": "512"}, {"KSG_RUN_LAG": "4"}],
+                         ids=["default", "min1", "bt512", "lag"])
 @pytest.mark.parametrize("name,c,sizes,keep", RUN_CASES, ids=[c[0] for c in RUN_CASES])
 def test_persistent_segments_match_oracle(monkeypatch, env, name, c, sizes, keep):
     """Persistent segments (k_chain_run: the pod loop inside one launch, gates
     between blocks) place every pod exactly as the oracle, with 1, 3 and 20
     blocks (XCD groups of unequal size), around kept pods that split a segment,
     and on a saturating cluster (unschedulable pods in the middle of a segment);
-    also with one-pod segments allowed (KSG_RUN_MIN=1) and 512-thread blocks."""
+    also with one-pod segments allowed (KSG_RUN_MIN=1), 512-thread blocks, and a
+    committer delayed ~14 us per pod (KSG_RUN_LAG=4: longer than a pod's evaluation,
+    so the node blocks run a pod ahead of it and rewrite the granules of the pod
+    after the one it reads; the parity-slotted granules keep those it reads)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     doc = g.generate(c, **sizes)
@@ -261,3 +265,46 @@ def test_persistent_segments_match_oracle(monkeypatch, env, name, c, sizes, keep
     run_pods, segs = s.run_counts()
     if table:
         assert run_pods > 0 and segs > 0, (table, run_pods, segs)
+
+
+@pytest.mark.gpu
+def test_persistent_not_resident_falls_back(monkeypatch):
+    """A persistent launch whose blocks cannot all be resident (forced: the handshake
+    waits for one block more than the grid, KSG_RUN_NORES) leaves before touching any
+    state, and its pods run on the two-launch chain: placements identical to the
+    oracle's, no pod counted as a persistent-segment pod, the fallback counted."""
+    monkeypatch.setenv("KSG_RUN_NORES", "1")
+    monkeypatch.setenv("KSG_RUN_WAIT_US", "300")
+    doc = g.generate(4, n_nodes=600, n_existing=1500, n_pods=300, n_zones=8)
+    o, s = run_both(doc, keep=False)
+    res = s.results()
+    bad = [(q, (r.selected, r.feasible, r.status), o.result(q)) for q, r in enumerate(res)
+           if (r.selected, r.feasible, r.status) != o.result(q)]
+    assert not bad, f"{len(bad)} pods differ, first {bad[:5]}"
+    assert s.run_fallbacks() >= 1
+    assert s.run_counts() == (0, 0)
+
+
+@pytest.mark.gpu
+def test_persistent_abort_marks_context_unusable(monkeypatch):
+    """A persistent launch whose poll runs out (forced: one poll per wait and a
+    committer delayed ~200 us per pod) raises the sticky abort word: the call fails
+    with a device error (later segments of the call leave at their handshake), every
+    later call is refused until the cluster is reloaded, and a reload runs again."""
+    monkeypatch.setenv("KSG_RUN_SPIN", "1")
+    monkeypatch.setenv("KSG_RUN_LAG", "64")
+    doc = g.generate(4, n_nodes=600, n_existing=1500, n_pods=120, n_zones=8)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    s.keep_outputs(40, 2)  # (two segments: pods 0-39 and 42-119)
+    with pytest.raises(KsgError, match="gate never completed"):
+        s.schedule()
+    with pytest.raises(KsgError, match="unusable"):
+        s.results()
+    s.load_cluster(doc)  # a reload clears the state
+    s.results()
+    monkeypatch.delenv("KSG_RUN_SPIN")
+    monkeypatch.delenv("KSG_RUN_LAG")
+    o, s2 = run_both(doc, keep=False)  # a fresh context on the same device, persistent segments on
+    assert [(r.selected, r.feasible, r.status) for r in s2.results()] == [o.result(q) for q in range(s2.queue_len)]
+    assert s2.run_counts()[0] > 0

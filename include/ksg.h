@@ -44,8 +44,10 @@ extern "C" {
  * longer document order: ksg_queue_pod names it); ksg_queue_pod, ksg_gated_pods,
  * ksg_cycle_view_acquire / _release added; a context whose persistent launch
  * stalled refuses calls (KSG_E_STATE) until ksg_load_cluster.  Bindings check
- * ksg_abi_version() >= the version they were written against. */
-#define KSG_ABI_VERSION 2
+ * ksg_abi_version() >= the version they were written against.  3: ksg_cycle_view
+ * holds the Filter outcome once per node (fail_pos / fail_code / fail_msg) and
+ * 32-bit scores per position, built on the device. */
+#define KSG_ABI_VERSION 3
 
 #define KSG_OK 0
 #define KSG_E_INVALID (-1)   /* bad argument / JSON */
@@ -283,29 +285,39 @@ int ksg_postfilter_result(ksg_ctx* ctx, uint32_t q, int32_t* nominated, char* bu
  * parallelize.Until workers and NormalizeScore (:388-415) per plugin; a Go
  * plugin acquires the cycle's view once (the cycle's first PreFilter, after
  * ksg_cycle; kept in CycleState) and its per-node calls index these immutable
- * arrays — no library call, no lock.  Arrays are [pos * n_nodes + i] for
- * profile position pos and local node i (global index node_offset + i).
- * Codes are framework.Code values (as ksg_filter_status): -1 = not called.
- * A view stays valid, unchanged, until ksg_cycle_view_release, whatever the
- * context does meanwhile (later cycles, Reserve, events); release needs no
- * context and may run on any thread. */
+ * arrays — no library call, no lock.  Local node i is global node
+ * node_offset + i.  The device builds the view (one kernel, one copy into a
+ * pinned host block): the per-node Filter outcome is stored once per node, not
+ * per position.  Filter of profile position pos on node i returns
+ *   -1 (not called)               if !filter_called[pos] or fail_pos[i] < 0 or pos > fail_pos[i]
+ *   Success (0)                    if pos < fail_pos[i]  (fail_pos[i] == n_positions: passed every filter)
+ *   fail_code[i], messages[fail_msg[i]]   if pos == fail_pos[i]
+ * Codes are framework.Code values (as ksg_filter_status).  score[pos] /
+ * normalized[pos] point at n_nodes values (NULL: no device Score at pos), valid
+ * where the node passed every filter; normalized[pos] == score[pos] for plugins
+ * without ScoreExtensions.  A view stays valid, unchanged, until
+ * ksg_cycle_view_release, whatever the context does meanwhile (later cycles,
+ * Reserve, events, ksg_destroy); release needs no context and may run on any
+ * thread. */
 typedef struct ksg_cycle_view {
-  uint32_t q;                     /* queue pod */
-  uint32_t n_positions;           /* profile positions */
-  uint32_t node_offset;           /* global index of local node 0 */
-  uint32_t n_nodes;               /* local nodes */
-  ksg_pod_result result;          /* the cycle's outcome (engine selectHost) */
-  const int8_t* filter_code;      /* Filter: Success / Unschedulable / UnschedulableAndUnresolvable / -1 */
-  const uint16_t* filter_msg;     /* Status.Message() of the Filter: index into messages (0: "") */
-  const int64_t* score;           /* Score: raw score (0 where not scored) */
-  const int64_t* normalized;      /* NormalizeScore output (raw for plugins without ScoreExtensions) */
-  const int8_t* prefilter_code;   /* [pos] PreFilter code (ksg_prefilter_status) */
-  const uint16_t* prefilter_msg;  /* [pos] its message index */
-  const int8_t* prescore_code;    /* [pos] PreScore code (ksg_prescore_status) */
-  const uint16_t* prescore_msg;   /* [pos] its message index */
-  const char* const* messages;    /* message table; messages[0] == "" */
+  uint32_t q;                          /* queue pod */
+  uint32_t n_positions;                /* profile positions */
+  uint32_t node_offset;                /* global index of local node 0 */
+  uint32_t n_nodes;                    /* local nodes */
+  ksg_pod_result result;               /* the cycle's outcome (engine selectHost) */
+  const uint8_t* filter_called;        /* [pos] 1: the framework calls this position's Filter */
+  const int8_t* fail_pos;              /* [node] first failing position; n_positions: passed; -1: not evaluated */
+  const int8_t* fail_code;             /* [node] framework code of that failure */
+  const uint16_t* fail_msg;            /* [node] its Status.Message(): index into messages */
+  const int32_t* const* score;         /* [pos] -> [node] raw Score, or NULL */
+  const int32_t* const* normalized;    /* [pos] -> [node] NormalizeScore output, or NULL */
+  const int8_t* prefilter_code;        /* [pos] PreFilter code (ksg_prefilter_status) */
+  const uint16_t* prefilter_msg;       /* [pos] its message index */
+  const int8_t* prescore_code;         /* [pos] PreScore code (ksg_prescore_status) */
+  const uint16_t* prescore_msg;        /* [pos] its message index */
+  const char* const* messages;         /* message table; messages[0] == "" */
   uint32_t n_messages;
-  const void* owner;              /* library-private */
+  const void* owner;                   /* library-private */
 } ksg_cycle_view;
 /* Snapshot the kept outputs of queue pod q (the pod of the last ksg_cycle, or a
  * ksg_keep_outputs range) into a view. */

@@ -180,6 +180,28 @@ class Engine {
   bool summaries(uint32_t first, uint32_t count, ksg_pod_summary* out, std::string& err);
   bool outputs(uint32_t prog_idx, PodOutputs& out, std::string& err);
   bool sync(std::string& err);
+  // ksg_cycle_view on the device: profile facts the view kernel needs (host.cpp
+  // fills them once per profile), the block layout for the current snapshot, and
+  // the fill of a kept pod's view into a caller's (pinned) host block: one kernel,
+  // one device-to-host copy.  Block: message-slot table (kViewSlots codes, 0xFFFFFFFF
+  // empty, then an overflow word), per node fail_pos / fail_code / fail_msg, raw
+  // scores [device position][node], normalized [normalising row][node].
+  struct ViewCfg {
+    int n_profile = 0;
+    int prof_of_dev[KSG_MAX_PLUGINS] = {};  // device position -> profile position
+    bool dev_vol[KSG_MAX_PLUGINS] = {};     // the device position is a volume run
+    int kind[KSG_MAX_PROFILE] = {};         // Filter failure code: 0 unresolvable, 1 unschedulable, 2 Fit, 3 PTS, 4 IPA
+  };
+  struct ViewLayout {
+    uint32_t N = 0, n_raw = 0, n_norm = 0, n_slots = 0;
+    int norm_row[KSG_MAX_PLUGINS] = {};  // device position -> normalized row (-1: output == raw)
+    size_t off_fail_pos = 0, off_fail_code = 0, off_fail_msg = 0, off_raw = 0, off_norm = 0, bytes = 0;
+  };
+  void view_layout(ViewLayout& lay) const;
+  bool view(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err);
+  // pinned host blocks for views (process-wide pool: a view outlives its context)
+  static uint8_t* pinned_get(size_t bytes, size_t& cap);
+  static void pinned_put(uint8_t* p, size_t cap);
   // Restore the node rows / pod table to the state of the last upload (device copy).
   bool reset(std::string& err);
   // Sample the dominant kernel (k_filter_score) every `every` pods inside run_queue

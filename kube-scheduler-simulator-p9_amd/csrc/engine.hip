@@ -34,6 +34,8 @@
 #include <vector>
 #include <deque>
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <chrono>
 #include <cstddef>
 #include <thread>
@@ -4535,6 +4537,7 @@ struct Engine::Impl {
   DBuf<uint64_t> cpr, cpk;
   uint32_t cnblk = 0;
   DBuf<int32_t> knorm;    // normalized scores of one kept pod
+  DBuf<uint8_t> vblk;     // device cycle view block (Engine::view)
   size_t prog_bytes = 0;  // used bytes of the program blob
   // kept per-pair outputs
   uint32_t keep_first = 0, keep_n = 0;
@@ -5884,6 +5887,92 @@ bool Engine::normalized(uint32_t j, std::vector<int32_t>& norm, std::string& err
   if (N) HIPCHK(hipMemcpyAsync(norm.data(), I.knorm.p, norm.size() * 4, hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipStreamSynchronize(I.stream));
   return true;
+}
+
+// ---- device cycle view (ksg_cycle_view_acquire)
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+void Engine::view_layout(ViewLayout& lay) const {
+  const Impl& I = *p_;
+  lay = ViewLayout{};
+  lay.N = I.N;
+  lay.n_raw = (uint32_t)I.F.n;
+  lay.n_slots = kViewSlots;
+  for (int d = 0; d < KSG_MAX_PLUGINS; ++d) {
+    lay.norm_row[d] = -1;
+    if (d >= I.F.n) continue;
+    const int p = I.F.plugins[d];
+    if (p == KP_TAINT || p == KP_NA || p == KP_PTS || p == KP_IPA) lay.norm_row[d] = (int)lay.n_norm++;
+  }
+  const size_t N = std::max<uint32_t>(I.N, 1);
+  lay.off_fail_pos = al256((kViewSlots + 1) * sizeof(uint32_t));
+  lay.off_fail_code = lay.off_fail_pos + al256(N);
+  lay.off_fail_msg = lay.off_fail_code + al256(N);
+  lay.off_raw = lay.off_fail_msg + al256(2 * N);
+  lay.off_norm = lay.off_raw + al256(4 * N * lay.n_raw);
+  lay.bytes = lay.off_norm + 4 * N * lay.n_norm;
+}
+bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err) {
+  Impl& I = *p_;
+  if (!(I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n)) { err = "outputs not kept for this pod"; return false; }
+  if (lay.N != I.N || lay.n_raw != (uint32_t)I.F.n) { err = "view layout of another snapshot"; return false; }
+  if (!I.vblk.alloc(lay.bytes, err)) return false;
+  ViewDev V{};
+  for (int d = 0; d < KSG_MAX_PLUGINS; ++d) {
+    V.prof_of_dev[d] = (int8_t)cfg.prof_of_dev[d];
+    V.dev_vol[d] = cfg.dev_vol[d] ? 1 : 0;
+    V.norm_row[d] = (int8_t)lay.norm_row[d];
+  }
+  for (int p = 0; p < KSG_MAX_PROFILE; ++p) V.kind[p] = (uint8_t)cfg.kind[p];
+  V.n_profile = cfg.n_profile;
+  V.off_fail_pos = (uint32_t)lay.off_fail_pos;
+  V.off_fail_code = (uint32_t)lay.off_fail_code;
+  V.off_fail_msg = (uint32_t)lay.off_fail_msg;
+  V.off_raw = (uint32_t)lay.off_raw;
+  V.off_norm = (uint32_t)lay.off_norm;
+  const size_t N = I.N, k = j - I.keep_first;
+  hipStream_t s = I.stream;
+  HIPCHK(hipMemsetAsync(I.vblk.p, 0xFF, kViewSlots * sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(I.vblk.p + kViewSlots * sizeof(uint32_t), 0, sizeof(uint32_t), s));
+  if (N)
+    hipLaunchKernelGGL(k_view, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, I.cluster(), I.F, I.progs.p + I.prog_off[j],
+                       I.sums.p + j, I.kfilter.p + k * N, I.kscore.p + k * N * KSG_MAX_PLUGINS, V, I.vblk.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(host, I.vblk.p, lay.bytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return true;
+}
+namespace {
+std::mutex g_pin_mu;
+std::multimap<size_t, uint8_t*> g_pin_free;  // capacity -> block
+}  // namespace
+uint8_t* Engine::pinned_get(size_t bytes, size_t& cap) {
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pin_free.lower_bound(bytes);
+    if (it != g_pin_free.end() && it->first <= 4 * bytes + (1u << 20)) {
+      uint8_t* p = it->second;
+      cap = it->first;
+      g_pin_free.erase(it);
+      return p;
+    }
+  }
+  cap = std::max<size_t>(al256(bytes), 4096);
+  uint8_t* p = nullptr;
+  if (hipHostMalloc((void**)&p, cap, hipHostMallocDefault) != hipSuccess) {
+    p = static_cast<uint8_t*>(std::malloc(cap));  // (pageable: the copy still works, slower)
+    cap |= 1;  // tag: malloc'd
+  }
+  return p;
+}
+void Engine::pinned_put(uint8_t* p, size_t cap) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  if (g_pin_free.size() >= 64) {  // bounded pool: free the block
+    if (cap & 1) std::free(p);
+    else (void)hipHostFree(p);
+    return;
+  }
+  g_pin_free.emplace(cap, p);
 }
 
 bool Engine::set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err) {

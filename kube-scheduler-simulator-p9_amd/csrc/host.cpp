@@ -806,6 +806,7 @@ struct Cluster {
 
   // ------------------------------------------------------------ profile
   bool load_profile(const J& pr) {
+    vcfg_ok_ = false;
     if (pr["profiles"] || (pr["plugins"] && pr["plugins"]->t == J::OBJ)) {  // scheduler configuration form
       J flat;
       if (!profile_from_config(pr, flat, err)) return false;
@@ -3773,6 +3774,10 @@ struct Cluster {
     if (pos > fail_pos) return -1;
     const uint32_t detail = code_detail(code);
     msg = filter_message(pos, detail);
+    return filter_fail_code(q, pos, i, detail);
+  }
+  // framework.Code of a Filter failure of profile position pos on local node i
+  int filter_fail_code(uint32_t q, int pos, uint32_t i, uint32_t detail) const {
     if (is_volume(plugins[pos])) return vkind[pos] == VK_RESTRICT || vkind[pos] == VK_CSI ? C_UNSCHED : C_UNRESOLVABLE;
     switch (plugins[pos]) {
       case P_FIT: {  // fit.go Filter: UnschedulableAndUnresolvable when a request exceeds the allocatable
@@ -3793,6 +3798,31 @@ struct Cluster {
       case P_PORTS: return C_UNSCHED;
       default: return C_UNRESOLVABLE;  // TaintToleration, NodeAffinity, NodeUnschedulable, NodeName
     }
+  }
+  // The same rule per profile position, for the device view (Engine::view)
+  ksg::Engine::ViewCfg vcfg_;
+  bool vcfg_ok_ = false;
+  const ksg::Engine::ViewCfg& view_cfg() {
+    if (!vcfg_ok_) {
+      ksg::Engine::ViewCfg v;
+      v.n_profile = n_plugins;
+      for (int d = 0; d < KSG_MAX_PLUGINS; ++d) {
+        v.prof_of_dev[d] = fpos[d];
+        v.dev_vol[d] = fpos[d] >= 0 && fpos[d] < n_plugins && is_volume(plugins[fpos[d]]);
+      }
+      for (int pos = 0; pos < n_plugins && pos < KSG_MAX_PROFILE; ++pos) {
+        int k = 0;
+        if (is_volume(plugins[pos])) k = vkind[pos] == VK_RESTRICT || vkind[pos] == VK_CSI ? 1 : 0;
+        else if (plugins[pos] == P_FIT) k = 2;
+        else if (plugins[pos] == P_PTS) k = 3;
+        else if (plugins[pos] == P_IPA) k = 4;
+        else if (plugins[pos] == P_PORTS) k = 1;
+        v.kind[pos] = k;
+      }
+      vcfg_ = v;
+      vcfg_ok_ = true;
+    }
+    return vcfg_;
   }
   // PreScore of profile position pos (-1: no PreScore, or no scoring: one feasible
   // node / none, or a PreScore before it failed).  NodeAffinity's PreScore fails
@@ -4548,13 +4578,20 @@ int ksg_normalized_scores(ksg_ctx* ctx, uint32_t q, uint32_t pos, int64_t* out, 
 
 // ---- ksg_cycle_view: one cycle's per-node results as immutable arrays (the
 // Filter / Score / NormalizeScore calls of the framework's parallel workers read
-// them without calling into the library)
+// them without calling into the library).  The device fills the per-node arrays
+// into a pinned block (Engine::view: one kernel, one copy); the host adds the
+// pod-level statuses and renders one message per distinct failing code.
 namespace {
 struct CycleView {
   ksg_cycle_view pub;  // (first member: the pointer handed out)
-  std::vector<int8_t> fcode, pfcode, pscode;
-  std::vector<uint16_t> fmsg, pfmsg, psmsg;
-  std::vector<int64_t> score, norm;
+  uint8_t* block = nullptr;  // pinned (Engine::pinned_get)
+  size_t cap = 0;
+  std::vector<int8_t> fpos_h, fcode_h;  // host-built arrays (slot-table overflow)
+  std::vector<uint16_t> fmsg_h;
+  std::vector<uint8_t> called;
+  std::vector<int8_t> pfcode, pscode;
+  std::vector<uint16_t> pfmsg, psmsg;
+  std::vector<const int32_t*> sptr, nptr;
   std::vector<std::string> msgs;
   std::vector<const char*> mptr;
   std::unordered_map<std::string, uint16_t> mid;
@@ -4568,6 +4605,7 @@ struct CycleView {
     mid.emplace(m, k);
     return k;
   }
+  ~CycleView() { ksg::Engine::pinned_put(block, cap); }
 };
 }  // namespace
 
@@ -4578,60 +4616,69 @@ int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out)
   if (!out) return KSG_E_INVALID;
   *out = nullptr;
   if (q >= c.meta.size()) return ctx->fail("cycle_view: range", KSG_E_RANGE);
-  const ksg::PodOutputs* o = c.outputs_of(q);
-  if (!o) return ctx->fail(c.err, KSG_E_STATE);
-  const std::vector<int32_t>* nm = c.normalized_of(q);
-  if (!nm) return ctx->fail(c.err, KSG_E_STATE);
-  o = c.outputs_of(q);
+  ksg_pod_summary S;
+  if (!c.eng->summaries(q, 1, &S, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
+  ksg::Engine::ViewLayout lay;
+  c.eng->view_layout(lay);
   std::unique_ptr<CycleView> v(new CycleView());
+  v->block = ksg::Engine::pinned_get(lay.bytes, v->cap);
+  if (!v->block) return ctx->fail("cycle_view: no host memory", KSG_E_DEVICE);
+  if (!c.eng->view(q, c.view_cfg(), lay, v->block, c.err)) return ctx->fail(c.err, KSG_E_STATE);
   const uint32_t P = (uint32_t)c.n_plugins, N = c.hi - c.lo;
-  v->msgs.push_back("");
-  v->fcode.assign((size_t)P * N, -1);
-  v->fmsg.assign((size_t)P * N, 0);
-  v->score.assign((size_t)P * N, 0);
-  v->norm.assign((size_t)P * N, 0);
+  v->msgs.resize(lay.n_slots + 1);  // messages[s + 1]: the message of slot s's code
+  const uint32_t* slots = reinterpret_cast<const uint32_t*>(v->block);
+  const bool overflow = slots[lay.n_slots] != 0;
+  const int8_t* fail_pos = reinterpret_cast<const int8_t*>(v->block + lay.off_fail_pos);
+  const int8_t* fail_code = reinterpret_cast<const int8_t*>(v->block + lay.off_fail_code);
+  const uint16_t* fail_msg = reinterpret_cast<const uint16_t*>(v->block + lay.off_fail_msg);
+  if (!overflow) {
+    for (uint32_t k = 0; k < lay.n_slots; ++k)
+      if (slots[k] != 0xFFFFFFFFu) v->msgs[k + 1] = c.filter_message(c.code_pos(slots[k]), c.code_detail(slots[k]));
+  } else {  // more distinct failing codes than slots (never seen): the per-node calls' answers
+    const ksg::PodOutputs* o = c.outputs_of(q);
+    if (!o) return ctx->fail(c.err, KSG_E_STATE);
+    v->fpos_h.assign(N, -1);
+    v->fcode_h.assign(N, 0);
+    v->fmsg_h.assign(N, 0);
+    std::string m;
+    for (uint32_t i = 0; i < N; ++i) {
+      const uint32_t code = o->filter[i];
+      if (code == KSG_FILTER_NOT_EVALUATED) continue;
+      if (code == KSG_FILTER_PASS) { v->fpos_h[i] = (int8_t)P; continue; }
+      const int fp = c.code_pos(code);
+      v->fpos_h[i] = (int8_t)fp;
+      const uint32_t d = c.code_detail(code);
+      m = c.filter_message(fp, d);
+      v->fcode_h[i] = (int8_t)c.filter_fail_code(q, fp, i, d);
+      v->fmsg_h[i] = v->intern(m);
+    }
+    fail_pos = v->fpos_h.data();
+    fail_code = v->fcode_h.data();
+    fail_msg = v->fmsg_h.data();
+  }
+  v->called.assign(P, 0);
   v->pfcode.assign(P, -1);
   v->pfmsg.assign(P, 0);
   v->pscode.assign(P, -1);
   v->psmsg.assign(P, 0);
+  v->sptr.assign(P, nullptr);
+  v->nptr.assign(P, nullptr);
   std::string m;
   const ksg::host::PodMeta& pm = c.meta[q];
-  const uint32_t skip_f = c.skip_filter_mask(pm, o->summary);
+  const uint32_t skip_f = c.skip_filter_mask(pm, S);
+  const int32_t* raw = reinterpret_cast<const int32_t*>(v->block + lay.off_raw);
+  const int32_t* norm = reinterpret_cast<const int32_t*>(v->block + lay.off_norm);
   for (uint32_t pos = 0; pos < P; ++pos) {
-    v->pfcode[pos] = (int8_t)c.prefilter_status(q, (int)pos, o->summary, m);
+    v->pfcode[pos] = (int8_t)c.prefilter_status(q, (int)pos, S, m);
     v->pfmsg[pos] = v->intern(m);
-    v->pscode[pos] = (int8_t)c.prescore_status(q, (int)pos, o->summary, m);
+    v->pscode[pos] = (int8_t)c.prescore_status(q, (int)pos, S, m);
     v->psmsg[pos] = v->intern(m);
-    // filter_status per node, its pod-level gates hoisted: a node that passed this
-    // position or failed earlier needs no call; a failure here is memoised by its
-    // code except Fit's (whose status reads the node's allocatable)
-    const bool gated = !ksg::host::has_filter(c.plugins[pos]) || pm.prefilter_fail_pos >= 0 || c.filter_skipped(pm, skip_f, (int)pos);
-    std::unordered_map<uint32_t, std::pair<int8_t, int32_t>> memo;
-    for (uint32_t i = 0; i < N && !gated; ++i) {  // (gated: -1 everywhere, as filter_status)
-      const size_t k = (size_t)pos * N + i;
-      const uint32_t code = o->filter[i];
-      if (code == KSG_FILTER_NOT_EVALUATED) continue;
-      const int fail_pos = code == KSG_FILTER_PASS ? c.n_plugins : c.code_pos(code);
-      if ((int)pos < fail_pos) { v->fcode[k] = (int8_t)Cluster::C_SUCCESS; continue; }
-      if ((int)pos > fail_pos) continue;
-      if (c.plugins[pos] != ksg::host::P_FIT) {
-        auto it = memo.find(code);
-        if (it != memo.end()) {
-          v->fcode[k] = it->second.first;
-          v->fmsg[k] = it->second.second;
-          continue;
-        }
-      }
-      v->fcode[k] = (int8_t)c.filter_status(q, (int)pos, i, *o, m);
-      if (!m.empty()) v->fmsg[k] = v->intern(m);
-      if (c.plugins[pos] != ksg::host::P_FIT) memo.emplace(code, std::make_pair(v->fcode[k], v->fmsg[k]));
-    }
+    v->called[pos] = ksg::host::has_filter(c.plugins[pos]) && pm.prefilter_fail_pos < 0 &&
+                     !c.filter_skipped(pm, skip_f, (int)pos) ? 1 : 0;
     const int d = c.dpos[pos];
     if (d < 0) continue;
-    for (uint32_t i = 0; i < N; ++i) {
-      v->score[(size_t)pos * N + i] = o->score[(size_t)d * N + i];
-      v->norm[(size_t)pos * N + i] = (*nm)[(size_t)d * N + i];
-    }
+    v->sptr[pos] = raw + (size_t)d * N;
+    v->nptr[pos] = lay.norm_row[d] >= 0 ? norm + (size_t)lay.norm_row[d] * N : v->sptr[pos];
   }
   for (auto& x : v->msgs) v->mptr.push_back(x.c_str());
   ksg_cycle_view& p = v->pub;
@@ -4639,16 +4686,18 @@ int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out)
   p.n_positions = P;
   p.node_offset = c.lo;
   p.n_nodes = N;
-  p.result.selected = o->summary.selected;
-  p.result.feasible = o->summary.feasible;
-  p.result.status = o->summary.status;
-  p.result.skip_filter = o->summary.skip_filter;
-  p.result.skip_score = o->summary.skip_score;
-  p.result.total = (int32_t)(o->summary.best_key >> 40);
-  p.filter_code = v->fcode.data();
-  p.filter_msg = v->fmsg.data();
-  p.score = v->score.data();
-  p.normalized = v->norm.data();
+  p.result.selected = S.selected;
+  p.result.feasible = S.feasible;
+  p.result.status = S.status;
+  p.result.skip_filter = S.skip_filter;
+  p.result.skip_score = S.skip_score;
+  p.result.total = (int32_t)(S.best_key >> 40);
+  p.filter_called = v->called.data();
+  p.fail_pos = fail_pos;
+  p.fail_code = fail_code;
+  p.fail_msg = fail_msg;
+  p.score = v->sptr.data();
+  p.normalized = v->nptr.data();
   p.prefilter_code = v->pfcode.data();
   p.prefilter_msg = v->pfmsg.data();
   p.prescore_code = v->pscode.data();

@@ -2102,3 +2102,105 @@ __global__ void k_norm_out(DevCluster C, DevProfile F, const uint8_t* prog, cons
     norm[(size_t)pos * C.N + n] = (int32_t)s;
   }
 }
+
+// ---- ksg_cycle_view on the device (the drop-in path's per-node lookups).  One
+// thread per node turns the kept filter code into what the framework's Filter
+// call returns there: the first failing profile position, its framework code
+// (Fit: UnschedulableAndUnresolvable when a failing request exceeds the node's
+// allocatable, fit.go) and a message index — the slot of the code in a small
+// open-addressing table of the pod's distinct failing codes (each wave inserts a
+// code once), whose text the host renders per slot.  It also copies the raw
+// scores and writes NormalizeScore's output for the normalising positions, so
+// one device-to-host copy carries the whole view (wrappedplugin.go:523-548
+// Filter, :420-445 Score, :388-415 NormalizeScore).
+constexpr int kViewSlots = 256;
+enum { kVkUnresolvable = 0, kVkUnsched = 1, kVkFit = 2, kVkPts = 3, kVkIpa = 4 };
+struct ViewDev {
+  int8_t prof_of_dev[KSG_MAX_PLUGINS];  // device position -> profile position (a volume run: its first plugin)
+  uint8_t dev_vol[KSG_MAX_PLUGINS];     // the device position is a volume run
+  int8_t norm_row[KSG_MAX_PLUGINS];     // device position -> normalized row, -1: none (output == raw)
+  uint8_t kind[KSG_MAX_PROFILE];        // per profile position: the framework code of its Filter failure
+  int32_t n_profile;
+  uint32_t off_fail_pos, off_fail_code, off_fail_msg, off_raw, off_norm;  // byte offsets in the block
+};
+__device__ __forceinline__ uint32_t view_slot(uint32_t* tab, uint32_t code) {
+  uint32_t h = (code * 2654435761u) >> 24;
+  for (int k = 0; k < kViewSlots; ++k) {
+    const uint32_t old = atomicCAS(&tab[h], 0xFFFFFFFFu, code);
+    if (old == 0xFFFFFFFFu || old == code) return h;
+    h = (h + 1) & (kViewSlots - 1);
+  }
+  atomicOr(&tab[kViewSlots], 1u);  // overflow (the host renders the view itself)
+  return kViewSlots;
+}
+__global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const uint8_t* prog, const ksg_pod_summary* sum,
+                                              const uint32_t* filter, const int32_t* score, ViewDev V, uint8_t* out) {
+  const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = n < C.N;
+  const ProgView PV = view(prog);
+  const ksg_prog* h = PV.h;
+  const uint32_t code = act ? filter[n] : KSG_FILTER_NOT_EVALUATED;
+  int fp = -1, fc = 0;
+  bool need = false;
+  if (code == KSG_FILTER_PASS) {
+    fp = V.n_profile;
+  } else if (code != KSG_FILTER_NOT_EVALUATED) {
+    const uint32_t d = code >> 24;
+    const bool vol = V.dev_vol[d] != 0;
+    fp = V.prof_of_dev[d] + (vol ? (int)((code >> 16) & 0xFFu) : 0);
+    const uint32_t detail = vol ? code & 0xFFFFu : code & 0xFFFFFFu;
+    switch (V.kind[fp]) {
+      case kVkUnsched: fc = 2; break;
+      case kVkFit:
+        fc = 2;
+        for (uint32_t r = 0; r < C.R && r < KSG_MAX_RES; ++r)
+          if ((detail >> (1 + r)) & 1u)
+            if (h->req[r] > C.alloc[(size_t)r * C.N + n]) fc = 3;
+        break;
+      case kVkPts: fc = detail == KSG_PTS_MISSING_LABEL ? 3 : 2; break;
+      case kVkIpa: fc = detail == KSG_IPA_AFFINITY ? 3 : 2; break;
+      default: fc = 3;
+    }
+    need = true;
+  }
+  // message slots: one insert per distinct code of the wave
+  uint32_t* tab = reinterpret_cast<uint32_t*>(out);
+  uint32_t msg = 0;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t m = __ballot(need); m; m = __ballot(need)) {
+    const int leader = __ffsll((long long)m) - 1;
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)code, leader);
+    uint32_t s = 0;
+    if ((int)lane == leader) s = view_slot(tab, c0);
+    s = (uint32_t)__builtin_amdgcn_readlane((int)s, leader);
+    if (need && code == c0) {
+      msg = s < kViewSlots ? s + 1 : 0;
+      need = false;
+    }
+  }
+  if (!act) return;
+  reinterpret_cast<int8_t*>(out + V.off_fail_pos)[n] = (int8_t)fp;
+  reinterpret_cast<int8_t*>(out + V.off_fail_code)[n] = (int8_t)fc;
+  reinterpret_cast<uint16_t*>(out + V.off_fail_msg)[n] = (uint16_t)msg;
+  int32_t* raw = reinterpret_cast<int32_t*>(out + V.off_raw);
+  int32_t* norm = reinterpret_cast<int32_t*>(out + V.off_norm);
+  const bool feasible = code == KSG_FILTER_PASS;
+  const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
+  bool pts_keys = false, pk_done = false;
+  for (int pos = 0; pos < F.n; ++pos) {
+    const int32_t s = score[(size_t)pos * C.N + n];
+    raw[(size_t)pos * C.N + n] = s;
+    const int r = V.norm_row[pos];
+    if (r < 0) continue;
+    int64_t v = 0;
+    if (feasible) {
+      if (F.plugins[pos] == KP_PTS && !pk_done) {
+        pts_keys = ns > 0 && pts_has_keys(C, PV, nf, nf + ns, n);
+        pk_done = true;
+      }
+      bool use;
+      v = normalize_pos(F.plugins[pos], h, s, sum->max_score[pos], sum->min_score[pos], sum->ipa_flags, pts_keys, use);
+    }
+    norm[(size_t)r * C.N + n] = (int32_t)v;
+  }
+}

@@ -32,8 +32,11 @@ class _Opts(ctypes.Structure):
 class _CycleView(ctypes.Structure):
     _fields_ = [("q", ctypes.c_uint32), ("n_positions", ctypes.c_uint32), ("node_offset", ctypes.c_uint32),
                 ("n_nodes", ctypes.c_uint32), ("result", _PodResult),
-                ("filter_code", ctypes.POINTER(ctypes.c_int8)), ("filter_msg", ctypes.POINTER(ctypes.c_uint16)),
-                ("score", ctypes.POINTER(ctypes.c_int64)), ("normalized", ctypes.POINTER(ctypes.c_int64)),
+                ("filter_called", ctypes.POINTER(ctypes.c_uint8)),
+                ("fail_pos", ctypes.POINTER(ctypes.c_int8)), ("fail_code", ctypes.POINTER(ctypes.c_int8)),
+                ("fail_msg", ctypes.POINTER(ctypes.c_uint16)),
+                ("score", ctypes.POINTER(ctypes.POINTER(ctypes.c_int32))),
+                ("normalized", ctypes.POINTER(ctypes.POINTER(ctypes.c_int32))),
                 ("prefilter_code", ctypes.POINTER(ctypes.c_int8)), ("prefilter_msg", ctypes.POINTER(ctypes.c_uint16)),
                 ("prescore_code", ctypes.POINTER(ctypes.c_int8)), ("prescore_msg", ctypes.POINTER(ctypes.c_uint16)),
                 ("messages", ctypes.POINTER(ctypes.c_char_p)), ("n_messages", ctypes.c_uint32),
@@ -66,8 +69,16 @@ class CycleView:
             pass
 
     def filter_status(self, pos, i):
-        k = pos * self.N + i
-        return self._v.filter_code[k], self.messages[self._v.filter_msg[k]]
+        """What Filter of profile position pos returns on local node i (ksg.h rule)."""
+        v = self._v
+        if not v.filter_called[pos]:
+            return -1, ""
+        fp = v.fail_pos[i]
+        if fp < 0 or pos > fp:
+            return -1, ""
+        if pos < fp:
+            return 0, ""
+        return v.fail_code[i], self.messages[v.fail_msg[i]]
 
     def prefilter_status(self, pos):
         return self._v.prefilter_code[pos], self.messages[self._v.prefilter_msg[pos]]
@@ -76,10 +87,12 @@ class CycleView:
         return self._v.prescore_code[pos], self.messages[self._v.prescore_msg[pos]]
 
     def scores(self, pos):
-        return [self._v.score[pos * self.N + i] for i in range(self.N)]
+        p = self._v.score[pos]
+        return [p[i] for i in range(self.N)] if p else [0] * self.N
 
     def normalized_scores(self, pos):
-        return [self._v.normalized[pos * self.N + i] for i in range(self.N)]
+        p = self._v.normalized[pos]
+        return [p[i] for i in range(self.N)] if p else [0] * self.N
 
 
 @dataclass

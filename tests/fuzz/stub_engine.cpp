@@ -271,3 +271,42 @@ float Engine::last_ms() const { return 0; }
 std::vector<Engine::KernelStat> Engine::kernel_stats() const { return {}; }
 
 }  // namespace ksg
+
+// device cycle view, stub: the synthetic outputs laid out as Engine::view does
+namespace ksg {
+static size_t al256s(size_t x) { return (x + 255) & ~(size_t)255; }
+void Engine::view_layout(ViewLayout& lay) const {
+  lay = ViewLayout{};
+  lay.N = p_->N;
+  lay.n_raw = (uint32_t)p_->cfg.n_plugins;
+  lay.n_slots = 256;
+  for (int d = 0; d < KSG_MAX_PLUGINS; ++d) lay.norm_row[d] = -1;
+  const size_t N = p_->N ? p_->N : 1;
+  lay.off_fail_pos = al256s(257 * 4);
+  lay.off_fail_code = lay.off_fail_pos + al256s(N);
+  lay.off_fail_msg = lay.off_fail_code + al256s(N);
+  lay.off_raw = lay.off_fail_msg + al256s(2 * N);
+  lay.off_norm = lay.off_raw + al256s(4 * N * lay.n_raw);
+  lay.bytes = lay.off_norm;
+}
+bool Engine::view(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err) {
+  PodOutputs o;
+  if (!(p_->keep_n && q >= p_->keep_first && q < p_->keep_first + p_->keep_n)) { err = "outputs not kept for this pod"; return false; }
+  if (!outputs(q, o, err)) return false;
+  std::memset(host, 0, lay.bytes);
+  std::memset(host, 0xFF, 256 * 4);
+  for (uint32_t i = 0; i < p_->N; ++i) {
+    const uint32_t c = o.filter[i];
+    reinterpret_cast<int8_t*>(host + lay.off_fail_pos)[i] =
+        (int8_t)(c == KSG_FILTER_PASS ? cfg.n_profile : (c == KSG_FILTER_NOT_EVALUATED ? -1 : 0));
+    for (uint32_t d = 0; d < lay.n_raw; ++d)
+      reinterpret_cast<int32_t*>(host + lay.off_raw)[(size_t)d * p_->N + i] = o.score[(size_t)d * p_->N + i];
+  }
+  return true;
+}
+uint8_t* Engine::pinned_get(size_t bytes, size_t& cap) {
+  cap = bytes ? bytes : 1;
+  return static_cast<uint8_t*>(std::malloc(cap));
+}
+void Engine::pinned_put(uint8_t* p, size_t) { std::free(p); }
+}  // namespace ksg

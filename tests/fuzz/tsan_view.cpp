@@ -27,14 +27,19 @@ static std::string slurp(const char* p) {
 static uint64_t digest(const ksg_cycle_view* v) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
-  const size_t n = (size_t)v->n_positions * v->n_nodes;
-  for (size_t k = 0; k < n; ++k) {
-    mix((uint64_t)(int64_t)v->filter_code[k]);
-    mix(v->filter_msg[k]);
-    mix((uint64_t)v->score[k]);
-    mix((uint64_t)v->normalized[k]);
-    if (v->filter_msg[k] >= v->n_messages) return 0;
-    for (const char* c = v->messages[v->filter_msg[k]]; *c; ++c) mix((uint64_t)*c);
+  for (uint32_t i = 0; i < v->n_nodes; ++i) {
+    mix((uint64_t)(int64_t)v->fail_pos[i]);
+    mix((uint64_t)(int64_t)v->fail_code[i]);
+    mix(v->fail_msg[i]);
+    if (v->fail_msg[i] >= v->n_messages) return 0;
+    for (const char* c = v->messages[v->fail_msg[i]]; *c; ++c) mix((uint64_t)*c);
+  }
+  for (uint32_t p = 0; p < v->n_positions; ++p) {
+    mix(v->filter_called[p]);
+    for (uint32_t i = 0; i < v->n_nodes; ++i) {
+      if (v->score[p]) mix((uint64_t)(int64_t)v->score[p][i]);
+      if (v->normalized[p]) mix((uint64_t)(int64_t)v->normalized[p][i]);
+    }
   }
   for (uint32_t p = 0; p < v->n_positions; ++p) {
     mix((uint64_t)(int64_t)v->prefilter_code[p]);

@@ -230,9 +230,16 @@ def test_cycle_view_matches_extension_point_calls(name, c, sizes):
         q, r = s.cycle(pod, commit=True)
         v = s.cycle_view(q)
         assert (v.result.selected, v.result.feasible, v.result.status) == o.result(i), (name, i)
+        nodes = range(len(names)) if i < 8 else (0, len(names) // 2, len(names) - 1)
         for pos in range(len(doc["profile"]["plugins"])):  # the view holds what the per-node calls return
-            for k in (0, len(names) // 2, len(names) - 1):
+            for k in nodes:
                 assert v.filter_status(pos, k) == tuple(s.filter_status(q, pos, k)), (name, i, pos, k)
+            if i < 8 and r.feasible > 1 and v._v.score[pos]:  # raw / normalized on every feasible node
+                raw, norm = s.scores(q, pos), s.normalized_scores(q, pos)
+                vr, vn = v.scores(pos), v.normalized_scores(pos)
+                for k in range(len(names)):
+                    if v._v.fail_pos[k] == len(doc["profile"]["plugins"]):
+                        assert (vr[k], vn[k]) == (raw[k], norm[k]), (name, i, pos, k)
         vc = _ViewCalls(s, v)
         with ThreadPoolExecutor(16) as ex:
             outs = list(ex.map(lambda _: rebuild(vc, q, doc["profile"], names, r.status), range(16)))

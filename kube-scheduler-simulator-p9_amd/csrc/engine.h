@@ -184,7 +184,8 @@ class Engine {
   // fills them once per profile), the block layout for the current snapshot, and
   // the fill of a kept pod's view into a caller's (pinned) host block: one kernel,
   // one device-to-host copy.  Block: message-slot table (kViewSlots codes, 0xFFFFFFFF
-  // empty, then an overflow word), per node fail_pos / fail_code / fail_msg, raw
+  // empty, then an overflow word; 64-bit entries gen << 32 | code, live when gen is
+  // this view's), the pod's summary, per node fail_pos / fail_code / fail_msg, raw
   // scores [device position][node], normalized [normalising row][node].
   struct ViewCfg {
     int n_profile = 0;
@@ -194,6 +195,8 @@ class Engine {
   };
   struct ViewLayout {
     uint32_t N = 0, n_raw = 0, n_norm = 0, n_slots = 0;
+    mutable uint32_t gen = 0;  // set by view(): live slot entries are gen << 32 | code
+    size_t off_sum = 0;        // the pod's summary
     int norm_row[KSG_MAX_PLUGINS] = {};  // device position -> normalized row (-1: output == raw)
     size_t off_fail_pos = 0, off_fail_code = 0, off_fail_msg = 0, off_raw = 0, off_norm = 0, bytes = 0;
   };

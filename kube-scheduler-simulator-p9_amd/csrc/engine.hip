@@ -2287,6 +2287,20 @@ struct WinArgs {
   // sharded: replica of every node's row, indexed by global node (kept in step by
   // every rank's identical replay); null on one shard
   RowV* xrows;
+  // persistent window loop (k_window_run): the eval blocks count their window's
+  // finished pod records (evd) and written outputs (flushed); the replay waits for
+  // flush_need of them before it patches outputs; abortw / spin bound every wait
+  uint32_t* evd;
+  uint32_t* flushed;
+  uint32_t flush_need;
+  uint32_t* abortw;
+  uint32_t spin;
+  uint32_t* pub;      // the replicated "windows replayed" flag (16 lines of 32 words) and the value
+  uint32_t pub_val;   // replay(W) publishes once P_W is out: W + 1
+  const Pend* pcur;   // eval side: P_{E-1} and its count, published when *pubw >= pub_need
+  const int32_t* pcur_n;
+  const uint32_t* pubw;
+  uint32_t pub_need;
 };
 __device__ __forceinline__ const StaticRec* srec_row(const WinArgs& A, uint32_t q, uint32_t N) {
   return A.stat + (size_t)((q - A.first) % A.stat_ring) * N;
@@ -2465,19 +2479,25 @@ __device__ __forceinline__ uint32_t eval_row_s(const RowV& r, const DevProfile& 
   return code;
 }
 // raw: the static record's raw Taint/NodeAffinity scores (STAT profiles)
-template <bool STAT>
+// P: the persistent window loop's sc1 stores (no dirty line left in this XCD's L2
+// that a later write of the same output from another XCD could be overtaken by)
+template <bool STAT, bool P = false>
 __device__ __forceinline__ void write_pair(const DevProfile& F, uint32_t* of, int32_t* os, int32_t* ot, uint32_t N,
                                            uint32_t n, uint32_t code, int32_t fit_s, int32_t ba_s, int64_t tot,
                                            uint32_t raw) {
-  of[n] = code;
+  auto st = [](auto* p, auto v) {
+    if constexpr (P) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+  };
+  st(of + n, code);
   if (code == KSG_FILTER_PASS) {
-    if (F.pos_fit >= 0) os[(size_t)F.pos_fit * N + n] = fit_s;
-    if (F.pos_ba >= 0) os[(size_t)F.pos_ba * N + n] = ba_s;
+    if (F.pos_fit >= 0) st(os + (size_t)F.pos_fit * N + n, fit_s);
+    if (F.pos_ba >= 0) st(os + (size_t)F.pos_ba * N + n, ba_s);
     if (STAT) {
-      if (F.pos_taint >= 0) os[(size_t)F.pos_taint * N + n] = (int32_t)(raw >> 20);
-      if (F.pos_na >= 0) os[(size_t)F.pos_na * N + n] = (int32_t)(raw & KSG_RAW_NA_MASK);
+      if (F.pos_taint >= 0) st(os + (size_t)F.pos_taint * N + n, (int32_t)(raw >> 20));
+      if (F.pos_na >= 0) st(os + (size_t)F.pos_na * N + n, (int32_t)(raw & KSG_RAW_NA_MASK));
     }
-    ot[n] = (int32_t)tot;
+    st(ot + n, (int32_t)tot);
   }
 }
 
@@ -2574,9 +2594,12 @@ __global__ void k_selftest_lanes(const uint64_t* in, int32_t* bad) {
 
 // Per-pair output rows of queue pod q: the kept window, or a scratch ring of
 // two windows (window j+1 is evaluated while window j is being patched).
+__device__ __forceinline__ bool kept_q(const WinArgs& A, uint32_t q) {
+  return A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n;
+}
 __device__ __forceinline__ void out_ptrs(const WinArgs& A, uint32_t q, uint32_t N, uint32_t*& f, int32_t*& s,
                                          int32_t*& t) {
-  if (A.keep_n && q >= A.keep_first && q < A.keep_first + A.keep_n) {
+  if (kept_q(A, q)) {
     size_t slot = q - A.keep_first;
     f = A.kfilter + slot * N;
     s = A.kscore + slot * N * KSG_MAX_PLUGINS;
@@ -2614,6 +2637,82 @@ __device__ __forceinline__ void store_row(const DevCluster& C, uint32_t n, const
   C.nzc[n] = r.nzc;
   C.nzm[n] = r.nzm;
   C.podcnt[n] = r.podcnt;
+}
+
+// Persistent window loop (k_window_run, PER = true): what one block of the launch
+// hands to another — node rows, the P lists, candidate records, per-pair outputs —
+// moves by agent-scope (sc1) stores and loads (MI355X_MICROARCH.md hand-off table,
+// row 1): an sc1 load never returns a line another CU's L1 or another XCD's L2
+// holds stale, and an sc1 store leaves no dirty line behind in the writer's L2.
+template <bool P, class T>
+__device__ __forceinline__ T ldv(const T* p) {
+  if constexpr (P) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool P, class T>
+__device__ __forceinline__ void stv(T* p, T v) {
+  if constexpr (P) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool P, class T>
+__device__ __forceinline__ T ld_obj(const T* p) {
+  if constexpr (!P) {
+    return *p;
+  } else {
+    static_assert(sizeof(T) % 8 == 0, "8-byte words");
+    T v;
+    uint64_t* d = reinterpret_cast<uint64_t*>(&v);
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+#pragma unroll
+    for (size_t i = 0; i < sizeof(T) / 8; ++i) d[i] = ld_sc1(q + i);
+    return v;
+  }
+}
+template <bool P, class T>
+__device__ __forceinline__ void st_obj(T* p, const T& v) {
+  if constexpr (!P) {
+    *p = v;
+  } else {
+    static_assert(sizeof(T) % 8 == 0, "8-byte words");
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(&v);
+    uint64_t* q = reinterpret_cast<uint64_t*>(p);
+#pragma unroll
+    for (size_t i = 0; i < sizeof(T) / 8; ++i) st_sc1(q + i, s[i]);
+  }
+}
+// load_row / store_row with the columns an assume changes handed over sc1
+template <bool P>
+__device__ __forceinline__ void load_row_p(const DevCluster& C, uint32_t n, uint32_t need_eph, RowV& r) {
+  if constexpr (!P) {
+    load_row(C, n, need_eph, r);
+  } else {
+    r.alloc[0] = C.alloc[n];
+    r.alloc[1] = C.alloc[(size_t)C.N + n];
+    r.req[0] = ldv<true>(C.req + n);
+    r.req[1] = ldv<true>(C.req + (size_t)C.N + n);
+    r.alloc[2] = r.req[2] = r.alloc[3] = r.req[3] = 0;
+    if (need_eph) {
+#pragma unroll
+      for (uint32_t c = 2; c < 4; ++c)
+        if (c < C.R) {
+          r.alloc[c] = C.alloc[(size_t)c * C.N + n];
+          r.req[c] = ldv<true>(C.req + (size_t)c * C.N + n);
+        }
+    }
+    r.nzc = ldv<true>(C.nzc + n);
+    r.nzm = ldv<true>(C.nzm + n);
+    r.podcnt = ldv<true>(C.podcnt + n);
+    r.allowed = C.allowed[n];
+  }
+}
+template <bool P>
+__device__ __forceinline__ void store_row_p(const DevCluster& C, uint32_t n, const RowV& r) {
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k)
+    if (k < C.R) stv<P>(C.req + (size_t)k * C.N + n, r.req[k]);
+  stv<P>(C.nzc + n, r.nzc);
+  stv<P>(C.nzm + n, r.nzm);
+  stv<P>(C.podcnt + n, r.podcnt);
 }
 
 // Record path of a what-if step (run_whatif): pass 1 in the small tiles of
@@ -3288,10 +3387,30 @@ struct PatchV {
   int32_t total;
   uint32_t raw;   // static record's raw Taint / NodeAffinity scores
 };
+// Persistent window loop: what the pod's merging eval block adds to the window's
+// candidate record (in the rows area, which the replay then no longer reads): the
+// pod evaluated on P_{W-1}'s nodes once the previous replay publishes them — the
+// replay's "prior" step, off its critical path — and the rows of its shallow
+// candidate ranks.  Deeper ranks' rows come from the node rows: a candidate that
+// is no P_{W-1} node has the same row at the end of W-1 as at the end of W-2.
+struct PriorRec {
+  uint64_t pkey[KSG_BATCH];  // key on prior node e (0: infeasible)
+  PatchV patch[KSG_BATCH];
+  int32_t pdf[KSG_BATCH];    // feasible-count change vs the snapshot
+  RowV row[KSG_STAGE];       // rows of candidate ranks < KSG_STAGE (window-start rows)
+  uint64_t pmask, pbest;     // candidates that are prior nodes; the best prior key
+  int32_t pbest_e, np;
+};
+__device__ __forceinline__ PriorRec* prior_rec(uint8_t* rec) { return reinterpret_cast<PriorRec*>(rec_rows(rec)); }
+__device__ __forceinline__ const PriorRec* prior_rec(const uint8_t* rec) {
+  return reinterpret_cast<const PriorRec*>(rec_rows(rec));
+}
+static_assert(KSG_BATCH * sizeof(PriorRec) <= kRecKeys * sizeof(RowV), "prior records fit the rows area");
+static_assert(sizeof(PriorRec) % 8 == 0, "8-byte words");
 // Blocks 1.. of k_window: one pod x KSG_TILE nodes per block.  Tile lists are
 // handed to the pod's last-arriving block with sc1 stores/loads and an agent
 // counter (MI355X_MICROARCH.md, hand-off table row 1).
-template <int MODE, bool STAT>
+template <int MODE, bool STAT, bool PER = false>
 __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& F, const WinArgs& A, uint32_t blk, uint64_t* L) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t* wcount = reinterpret_cast<uint32_t*>(L + 16 * 64);
@@ -3306,19 +3425,19 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   RowV rnext;
   {
     const uint32_t nn0 = tile * A.tile_len + tid;
-    if ((uint32_t)tid < A.tile_len && nn0 < C.N) load_row(C, nn0, A.need_eph, rnext);
+    if ((uint32_t)tid < A.tile_len && nn0 < C.N) load_row_p<PER>(C, nn0, A.need_eph, rnext);
   }
   {
     constexpr int kPodW = (int)(sizeof(PodLite) / 8);
     if (tid < kPodW) reinterpret_cast<uint64_t*>(h)[tid] = reinterpret_cast<const uint64_t*>(A.plite + q)[tid];
     if (STAT && tid < 2) mlds[tid] = A.mpred[2 * (q - A.first) + tid];
   }
-  const int np = *A.pprev_n;
+  const int np = ldv<PER>(A.pprev_n);
   // P_{W-1}'s nodes in LDS (a lookup through LDS: a VGPR loaded from memory and
   // read lane by lane in a loop made the compiler wait for every outstanding
   // load and store, vmcnt(0), at each lookup)
   int32_t* pnl = reinterpret_cast<int32_t*>(wcount + 64);
-  if (tid < np) pnl[tid] = A.pprev[tid].node;
+  if (tid < np) pnl[tid] = ldv<PER>(&A.pprev[tid].node);
   lds_barrier();
   auto pend_lds = [&](int32_t gid) {
     int hit = -1;
@@ -3351,8 +3470,8 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     const uint32_t to = kk * KSG_TILE + tid, nn = tile * A.tile_len + to;
     if (to < A.tile_len && nn < C.N) {
       const int hit = pend_lds((int32_t)(C.goff + nn));
-      if (hit >= 0) r = A.pprev[hit].after;
-      else if (!loaded) load_row(C, nn, A.need_eph, r);
+      if (hit >= 0) r = ld_obj<PER>(&A.pprev[hit].after);
+      else if (!loaded) load_row_p<PER>(C, nn, A.need_eph, r);
       if (STAT) sr = srec_row(A, q, C.N)[nn];
     }
   };
@@ -3389,7 +3508,10 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
       uint32_t* of;
       int32_t *os, *ot;
       out_ptrs(A, q, C.N, of, os, ot);
-      write_pair<STAT>(F, of, os, ot, C.N, n, code, fit_s, ba_s, total, raw);
+      // (persistent loop: kept outputs sc1 — the replay may patch them from
+      // another XCD; the scratch ring of the others is never read)
+      if (PER && kept_q(A, q)) write_pair<STAT, true>(F, of, os, ot, C.N, n, code, fit_s, ba_s, total, raw);
+      else write_pair<STAT, false>(F, of, os, ot, C.N, n, code, fit_s, ba_s, total, raw);
     }
     if (code == KSG_FILTER_PASS) {
       feasible = true;
@@ -3451,7 +3573,16 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
       const uint32_t to = k * KSG_TILE + tid, n = tile * A.tile_len + to;
       if (to >= A.tile_len || n >= C.N) break;
       const PatchV pt = stash[(stash_all ? k * 16 + w : k) * 64 + lane];
-      write_pair<STAT>(F, of, os, ot, C.N, n, pt.code, pt.fitba & 0xFFFF, pt.fitba >> 16, pt.total, pt.raw);
+      if (PER && kept_q(A, q)) write_pair<STAT, true>(F, of, os, ot, C.N, n, pt.code, pt.fitba & 0xFFFF, pt.fitba >> 16, pt.total, pt.raw);
+      else write_pair<STAT, false>(F, of, os, ot, C.N, n, pt.code, pt.fitba & 0xFFFF, pt.fitba >> 16, pt.total, pt.raw);
+    }
+  };
+  // (persistent loop) this block's outputs are written: the replay may patch them
+  auto signal_flushed = [&]() {
+    if constexpr (PER) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(A.flushed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   };
   lds_barrier();
@@ -3474,6 +3605,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   }
   if (!wcount[16]) {
     flush_stash();
+    signal_flushed();
     return;
   }
   // last tile block of pod b: merge the T tile lists (wave w takes tiles w, w+16, ...);
@@ -3498,28 +3630,104 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     if (w < s) L[w * 64 + lane] = wave_merge_top(L[w * 64 + lane], L[(w + s) * 64 + 63 - lane]);
     lds_barrier();
   }
-  if (w == 0) {
+  if (PER && w == 0) {  // (persistent loop: keys, counts, shallow rows, then the prior step)
+    const uint64_t v = L[lane];
+    const int32_t gid = (int32_t)(v & 0xFFFFFull);
+    PriorRec* pr = prior_rec(A.erec) + b;
+    stv<true>(rec_keys(A.erec) + (size_t)b * KSG_CAND + lane, v);
+    if (lane < KSG_STAGE) {
+      RowV c;
+      memset(&c, 0, sizeof(c));
+      if (v) {
+        const int hh = pend_lds(gid);
+        if (hh >= 0) c = ld_obj<true>(&A.pprev[hh].after);
+        else load_row_p<true>(C, (uint32_t)gid - C.goff, A.need_eph, c);
+      }
+      st_obj<true>(&pr->row[lane], c);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) f[k] = wave_sum(f[k]);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) stv<true>(reinterpret_cast<int32_t*>(A.erec) + k * KSG_BATCH + b, f[k]);
+      stv<true>(A.arrive + b, 0u);
+    }
+    // the prior step: pod q on P_{E-1}'s nodes (published by the replay of E-1)
+    int np1 = 0;
+    if (A.pubw) {
+      uint32_t ok = 1;
+      if (lane == 0) {
+        ok = 0;
+        for (uint32_t it = 0; it < A.spin; ++it) {
+          if (ld_sc1(A.pubw) >= A.pub_need) { ok = 1; break; }
+          if ((it & 63u) == 63u && ld_sc1(A.abortw) != 0u) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) __hip_atomic_store(A.abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (__builtin_amdgcn_readfirstlane(ok)) np1 = ldv<true>(A.pcur_n);  // (else the run has aborted)
+    }
+    Pend pe;
+    pe.node = -1;
+    uint64_t k = 0;
+    if (lane < np1) {
+      pe = ld_obj<true>(A.pcur + lane);
+      int32_t fs, bs;
+      int64_t tot;
+      const uint32_t R = C.R < 4 ? C.R : 4;
+      const uint32_t code = eval_row<MODE>(pe.after, F, h, R, fs, bs, tot);
+      const bool snap_ok = F.pos_fit < 0 || fit_filter_row(pe.base, h, R) == 0;
+      PatchV pt;
+      pt.code = code;
+      pt.fitba = fs | (bs << 16);
+      pt.total = (int32_t)tot;
+      pt.raw = 0;
+      k = code == KSG_FILTER_PASS ? pack_key(tot, F.seed, h->queue_idx, (uint32_t)pe.node) : 0;
+      stv<true>(&pr->pkey[lane], k);
+      st_obj<true>(&pr->patch[lane], pt);
+      stv<true>(&pr->pdf[lane], (int32_t)((code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0)));
+    }
+    bool isp = false;  // candidate `lane` is a P_{E-1} node
+    for (int e = 0; e < np1; ++e) isp |= v != 0 && __builtin_amdgcn_readlane(pe.node, e) == gid;
+    const unsigned long long pm = __ballot(isp);
+    const uint64_t kb = wave_max(k);
+    const unsigned long long mb = __ballot(kb != 0 && k == kb);
+    if (lane == 0) {
+      stv<true>(&pr->pmask, (uint64_t)pm);
+      stv<true>(&pr->pbest, kb);
+      stv<true>(&pr->pbest_e, (int32_t)(mb ? __ffsll((long long)mb) - 1 : -1));
+      stv<true>(&pr->np, np1);
+      if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pod's record is out (wave 0 stored all of it)
+    if (lane == 0) __hip_atomic_fetch_add(A.evd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (w == 0) {
     uint64_t v = L[lane];
     RowV c;
     memset(&c, 0, sizeof(c));
     int32_t gid = (int32_t)(v & 0xFFFFFull);
     int hh = pend_lds(gid);
     if (v) {
-      if (hh >= 0) c = A.pprev[hh].after;
-      else load_row(C, (uint32_t)gid - C.goff, A.need_eph, c);
+      if (hh >= 0) c = ld_obj<PER>(&A.pprev[hh].after);
+      else load_row_p<PER>(C, (uint32_t)gid - C.goff, A.need_eph, c);
     }
-    rec_keys(A.erec)[(size_t)b * KSG_CAND + lane] = v;
-    if (!A.xrows) rec_rows(A.erec)[(size_t)b * KSG_CAND + lane] = c;  // (sharded: rows from the replica)
+    stv<PER>(rec_keys(A.erec) + (size_t)b * KSG_CAND + lane, v);
+    if (!A.xrows) st_obj<PER>(rec_rows(A.erec) + (size_t)b * KSG_CAND + lane, c);  // (sharded: rows from the replica)
 #pragma unroll
     for (int k = 0; k < 3; ++k) f[k] = wave_sum(f[k]);
     if (lane == 0) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) reinterpret_cast<int32_t*>(A.erec)[k * KSG_BATCH + b] = f[k];
-      A.arrive[b] = 0;
+      for (int k = 0; k < 3; ++k) stv<PER>(reinterpret_cast<int32_t*>(A.erec) + k * KSG_BATCH + b, f[k]);
+      stv<PER>(A.arrive + b, 0u);
       if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+    if constexpr (PER) {  // the pod's record is out (wave 0 stored all of it): the replay may stage it
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(A.evd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   flush_stash();
+  signal_flushed();
 }
 
 // ---- block 0: exact replay of window W as a fixed-point (Jacobi) iteration.
@@ -3641,6 +3849,7 @@ __device__ __forceinline__ int first_pick(const PickTab& T, int32_t x) {
 }
 
 #define KSG_ORG_NODE 0x40000000  // pick origin: node (o & 0xFFFFF) read from the node rows (fallback picks)
+template <bool PER = false>
 __device__ __forceinline__ void origin_rows(const DevCluster& C, const WinLDS& L, const WinArgs& A, int32_t o,
                                             RowV& start, RowV& snap) {
   if (o & KSG_ORG_NODE) {
@@ -3652,7 +3861,7 @@ __device__ __forceinline__ void origin_rows(const DevCluster& C, const WinLDS& L
   } else {
     int p = (o - 64) >> 6, i = (o - 64) & 63;
     if (i < KSG_STAGE) start = L.row[p][i];
-    else if (A.defer) load_row(C, (uint32_t)(L.key[p][i] & 0xFFFFFull) - C.goff, A.need_eph, start);
+    else if (A.defer || PER) load_row_p<PER>(C, (uint32_t)(L.key[p][i] & 0xFFFFFull) - C.goff, A.need_eph, start);
     else start = rec_rows(A.wrec)[p * KSG_CAND + i];
     snap = start;
   }
@@ -3809,7 +4018,7 @@ __device__ __forceinline__ void win_exact_write(const DevCluster& C, const DevPr
   }
 }
 
-template <int MODE, bool STAT>
+template <int MODE, bool STAT, bool PER = false>
 __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile& F, const WinArgs& A, WinLDS& L) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nb = (int)A.nw;
@@ -3822,7 +4031,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   }
   STAMP(0);
   if (A.stamps && tid == 0) A.stamps[11] = __builtin_amdgcn_s_memrealtime();
-  const int np = *A.pprev_n;
+  const int np = ldv<PER>(A.pprev_n);
   // ---- stage.  The small inputs (P_{W-1}, pods, counts) are loaded first and
   // stored at once; the candidate keys and rows stay in flight in registers
   // across the prior-node evaluations (vmcnt is in order) and land after them.
@@ -3831,11 +4040,28 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   const uint64_t* rows = reinterpret_cast<const uint64_t*>(rec_rows(A.wrec));
   const int nk = nb * KSG_CAND, nr = A.defer ? 0 : nb * KSG_STAGE * kRowW;
   uint64_t kv[2], rv[6];
+  // (persistent loop) the prior step the eval blocks did: thread = (pod, prior entry)
+  const int ppb = tid >> 5, ppe = tid & 31;
+  const PriorRec* PR = prior_rec(A.wrec);
+  uint64_t pr_k = 0, pr_p0 = 0, pr_p1 = 0, pr_m = 0;
+  int32_t pr_df = 0;
+  if constexpr (PER) {
+    if (ppb < nb) {
+      pr_k = ldv<true>(&PR[ppb].pkey[ppe]);
+      const uint64_t* pw = reinterpret_cast<const uint64_t*>(&PR[ppb].patch[ppe]);
+      pr_p0 = ldv<true>(pw);
+      pr_p1 = ldv<true>(pw + 1);
+      pr_df = ldv<true>(&PR[ppb].pdf[ppe]);
+      if (ppe == 0) pr_m = ldv<true>(&PR[ppb].pmask);
+      if (ppe == 1) pr_m = ldv<true>(&PR[ppb].pbest);
+      if (ppe == 2) pr_m = (uint64_t)(uint32_t)ldv<true>(&PR[ppb].pbest_e);
+    }
+  }
   {
-    const uint64_t pv = tid < KSG_BATCH * kPendW ? reinterpret_cast<const uint64_t*>(A.pprev)[tid] : 0;
+    const uint64_t pv = tid < KSG_BATCH * kPendW ? ldv<PER>(reinterpret_cast<const uint64_t*>(A.pprev) + tid) : 0;
     constexpr int kPodW = (int)(sizeof(PodLite) / 8);
     const uint64_t qv = tid < nb * kPodW ? reinterpret_cast<const uint64_t*>(A.plite + A.w0)[tid] : 0;
-    const int32_t fv = tid < nb && !A.defer ? reinterpret_cast<const int32_t*>(A.wrec)[tid] : 0;
+    const int32_t fv = tid < nb && !A.defer ? ldv<PER>(reinterpret_cast<const int32_t*>(A.wrec) + tid) : 0;
     int32_t aT = 0, aA = 0;
     int64_t m0 = -1, m1 = -1;
     if (STAT && tid < nb) {
@@ -3889,7 +4115,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         int i = tid + k * KSG_WIN_THREADS;
-        kv[k] = i < nk ? keys[i] : 0;
+        kv[k] = i < nk ? ldv<PER>(keys + i) : 0;
       }
     }
 #pragma unroll
@@ -3897,7 +4123,8 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       int i = tid + k * KSG_WIN_THREADS;
       int row = i / kRowW, wd = i - row * kRowW;
       int p = row / KSG_STAGE, r = row - p * KSG_STAGE;
-      rv[k] = i < nr ? rows[(size_t)(p * KSG_CAND + r) * kRowW + wd] : 0;
+      if constexpr (PER) rv[k] = i < nr ? ldv<true>(reinterpret_cast<const uint64_t*>(&PR[p].row[r]) + wd) : 0;
+      else rv[k] = i < nr ? rows[(size_t)(p * KSG_CAND + r) * kRowW + wd] : 0;
     }
     if (tid < np * kPendW) reinterpret_cast<uint64_t*>(L.prior)[tid] = pv;
     if (tid < nb * kPodW) reinterpret_cast<uint64_t*>(L.pod)[tid] = qv;
@@ -3920,7 +4147,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       for (int t = 0; t < 3; ++t) pick_clear(L.pick[t], tid);
     }
     if (wave == 0) {  // index P_{W-1} (one wave: its LDS operations stay in order)
-      const int32_t pnode = lane < np ? A.pprev[lane].node : -1;
+      const int32_t pnode = lane < np ? ldv<PER>(&A.pprev[lane].node) : -1;
       L.ptn[lane] = -1;
       L.ptn[lane + 64] = -1;
       if (lane < np) L.pte[tab_claim(L.ptn, pnode)] = lane;
@@ -3931,10 +4158,21 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   if (tid < np) {  // write P_{W-1} back (the eval blocks read those rows from the list)
     const Pend& pe = L.prior[tid];
     uint32_t nl = (uint32_t)pe.node - C.goff;
-    if ((uint32_t)pe.node >= C.goff && nl < C.N) store_row(C, nl, pe.after);
+    if ((uint32_t)pe.node >= C.goff && nl < C.N) store_row_p<PER>(C, nl, pe.after);
     if (A.xrows) A.xrows[pe.node] = pe.after;  // every rank's replica, every node
   }
-  {  // pods on the P_{W-1} nodes as of the window start (independent of the picks)
+  if constexpr (PER) {  // the eval blocks' prior step, staged
+    if (ppb < nb) {
+      L.pkey[ppb][ppe] = pr_k;
+      reinterpret_cast<uint64_t*>(&L.patch[ppb][ppe])[0] = pr_p0;
+      reinterpret_cast<uint64_t*>(&L.patch[ppb][ppe])[1] = pr_p1;
+      L.pdf[ppb][ppe] = (int8_t)pr_df;
+      if (ppe == 0) L.pmask[ppb] = pr_m;
+      if (ppe == 1) L.pbest[ppb] = pr_m;
+      if (ppe == 2) L.pbest_e[ppb] = (int32_t)(uint32_t)pr_m;
+    }
+    STAMP(16);
+  } else {  // pods on the P_{W-1} nodes as of the window start (independent of the picks)
     const int pb = 2 * wave + (lane >> 5), e = lane & 31;
     uint64_t k = 0;
     if (pb < nb && e < np) {
@@ -3988,9 +4226,11 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     int i = tid + k * KSG_WIN_THREADS;
     if (i < nk) (&L.key[0][0])[i] = kv[k];
     const int b = wave + 16 * k;
-    bool m = kv[k] != 0 && np > 0 && prior_of(L, (int32_t)(kv[k] & 0xFFFFFull)) >= 0;
-    unsigned long long mask = __ballot(m);
-    if (lane == 0 && b < nb) L.pmask[b] = mask;
+    if constexpr (!PER) {  // (persistent loop: the eval blocks' pmask)
+      bool m = kv[k] != 0 && np > 0 && prior_of(L, (int32_t)(kv[k] & 0xFFFFFull)) >= 0;
+      unsigned long long mask = __ballot(m);
+      if (lane == 0 && b < nb) L.pmask[b] = mask;
+    }
   }
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
@@ -4081,7 +4321,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
             if (iters == 0) STAMP(25);
             if (nx >= b) {  // a is the last pick of the node before b
               RowV cur_r, snap;
-              origin_rows(C, L, A, L.O[cur][a], cur_r, snap);
+              origin_rows<PER>(C, L, A, L.O[cur][a], cur_r, snap);
               apply_delta(cur_r, cum, R);
               const PodLite* h = &L.pod[b];
               int32_t fs, bs;
@@ -4216,8 +4456,37 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   }
   STAMP(4);
   if (A.stamps && tid == 0) A.stamps[7] = iters;
-  // ---- flush: summaries, per-pair patches, P_W
+  // ---- flush: P_W first (the persistent loop publishes it at once: the eval
+  // blocks of window W+2 wait for it), then summaries and per-pair patches
   const PickTab& T = L.pick[cur];
+  if (wave == 0) {  // P_W: each node picked in the window, by its last pick
+    const int a = lane;
+    const int32_t Sv = a < nb ? L.S[cur][a] : -1;
+    int h = Sv >= 0 ? tab_find(T.node, Sv) : -1;
+    const bool last = h >= 0 && T.last[h] == a;
+    unsigned long long m = __ballot(last);
+    if (last) {
+      Delta cum;
+      delta_of(L.pod[a], cum);
+      int nx;
+      if (T.cnt[h] > 1) pick_chain(L, L.S[cur], a, Sv, cum, nx);
+      RowV st, snap;
+      origin_rows<PER>(C, L, A, L.O[cur][a], st, snap);
+      Pend p;
+      p.node = Sv;
+      p.pad = 0;
+      p.base = st;
+      apply_delta(st, cum, R);
+      p.after = st;
+      st_obj<PER>(A.pnext + __popcll(m & ((1ull << a) - 1)), p);
+    }
+    if (lane == 0) stv<PER>(A.pnext_n, (int32_t)__popcll(m));
+  }
+  if constexpr (PER) {  // every wave's stores of rows (P_{W-1}, at the stage) and P_W performed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < 16) st_sc1(A.pub + tid * 32, A.pub_val);
+  }
   if (tid < nb) {
     ksg_pod_summary& d = A.sums[A.w0 + tid];
     d.best_key = L.sum[tid].best_key;
@@ -4228,6 +4497,18 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       if (F.pos_taint >= 0) d.max_score[F.pos_taint] = L.xmt[tid];
       if (F.pos_na >= 0) d.max_score[F.pos_na] = L.xma[tid];
     }
+  }
+  if constexpr (PER) {  // the eval blocks' outputs of this window are written before the patches
+    if (tid == 0) {
+      bool ok = false;
+      for (uint32_t it = 0; it < A.spin; ++it) {
+        if (ld_sc1(A.flushed) >= A.flush_need) { ok = true; break; }
+        if ((it & 63u) == 63u && ld_sc1(A.abortw) != 0u) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (!ok) __hip_atomic_store(A.abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
   }
   {
     const int32_t Sv = L.S[cur][lane & 31];
@@ -4246,7 +4527,10 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
         uint32_t* of;
         int32_t *os, *ot;
         out_ptrs(A, A.w0 + b, C.N, of, os, ot);
-        write_pair<STAT>(F, of, os, ot, C.N, nl, pt.code, pt.fitba & 0xFFFF, pt.fitba >> 16, pt.total, pt.raw);
+        if (PER && kept_q(A, A.w0 + b))
+          write_pair<STAT, true>(F, of, os, ot, C.N, nl, pt.code, pt.fitba & 0xFFFF, pt.fitba >> 16, pt.total, pt.raw);
+        else
+          write_pair<STAT, false>(F, of, os, ot, C.N, nl, pt.code, pt.fitba & 0xFFFF, pt.fitba >> 16, pt.total, pt.raw);
       }
     }
   }
@@ -4257,29 +4541,6 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       fm &= fm - 1;
       win_exact_write<MODE>(C, F, A, L, b, cur, R);
     }
-  }
-  if (wave == 0) {  // P_W: each node picked in the window, by its last pick
-    const int a = lane;
-    const int32_t Sv = a < nb ? L.S[cur][a] : -1;
-    int h = Sv >= 0 ? tab_find(T.node, Sv) : -1;
-    const bool last = h >= 0 && T.last[h] == a;
-    unsigned long long m = __ballot(last);
-    if (last) {
-      Delta cum;
-      delta_of(L.pod[a], cum);
-      int nx;
-      if (T.cnt[h] > 1) pick_chain(L, L.S[cur], a, Sv, cum, nx);
-      RowV st, snap;
-      origin_rows(C, L, A, L.O[cur][a], st, snap);
-      Pend p;
-      p.node = Sv;
-      p.pad = 0;
-      p.base = st;
-      apply_delta(st, cum, R);
-      p.after = st;
-      A.pnext[__popcll(m & ((1ull << a) - 1))] = p;
-    }
-    if (lane == 0) *A.pnext_n = __popcll(m);
   }
   STAMP(5);
   if (A.stamps && tid == 0) A.stamps[12] = __builtin_amdgcn_s_memrealtime();
@@ -4357,6 +4618,120 @@ __global__ void k_rows_unpack(const RowV* recv, uint32_t ranks, uint32_t G, uint
 
 // ----------------------------------------------------------------- host side
 #include "table_chain.hip"
+
+// ---- The persistent window loop: every window of a run in ONE launch (Fit /
+// BalancedAllocation profiles, one shard).  Block 0 replays windows 0, 1, ...;
+// block 1 + b*T + t evaluates tile t of pod b of windows 0, 1, ....  The launch
+// boundaries of k_window become hand-offs (agent-scope counters, sc1 data):
+//   eval(E)   starts once replay(E-2) is published (Z.replayed >= E-1): the rows as of
+//             the end of window E-2 (P_{E-2} from its list) — as k_window's eval part;
+//   replay(W) starts once every pod of window W has its candidate record (Z.evd),
+//             and writes its output patches once every eval block of W wrote its
+//             outputs (Z.flushed);
+// and the buffers of window parity p (tile lists, records, arrivals, P lists,
+// output ring) are reused two windows later, after those waits.  A launch whose
+// blocks are not all resident leaves at the handshake (run_handshake) and the
+// host runs the launch-per-window loop instead.
+struct WinSync {
+  uint32_t replayed[16][32];  // windows replayed and published (block 0), one replica per 128-B line:
+                              // each eval block polls its own (blk % 16), not all one line
+  uint32_t evd[2];        // per window parity: pods whose record is out (cumulative over the launch)
+  uint32_t pad1[30];
+  uint32_t flushed[2];    // per window parity: eval blocks whose outputs are written (cumulative)
+  uint32_t pad2[30];
+};
+struct WinRunArgs {
+  uint32_t nwin, first, count, T;
+  uint32_t tt_sz, tf_sz;   // tile-list / tile-count slot sizes (elements)
+  uint64_t* tile_top;
+  int32_t* tfeas;
+  uint8_t* wrec;           // 2 x kRecBytes
+  Pend* pend;              // [2][KSG_BATCH]
+  int32_t* pend_n;         // [2]
+  uint32_t* arrive;        // [2][KSG_BATCH]
+  uint64_t* stamps;        // diagnostic: 32 slots per window, or null
+};
+__device__ bool win_wait_ge(const uint32_t* w, uint32_t want, uint32_t* abortw, uint32_t spin, uint32_t* go) {
+  if (threadIdx.x == 0) {
+    bool ok = false;
+    for (uint32_t it = 0; it < spin; ++it) {
+      if (ld_sc1(w) >= want) { ok = true; break; }
+      if ((it & 63u) == 63u && ld_sc1(abortw) != 0u) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok) __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *go = ok ? 1u : 0u;
+  }
+  __syncthreads();
+  const bool ok = *go != 0u;
+  __syncthreads();
+  return ok;
+}
+template <int MODE>
+__global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, DevProfile F, WinArgs A0, WinRunArgs R,
+                                                                RunSync* Y, WinSync* Z, RunCtl RC) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  __shared__ uint32_t go;
+  uint32_t warm = 0;
+  KWarm<0, (int)((sizeof(DevCluster) + sizeof(DevProfile) + sizeof(WinArgs)) / 64 * 64)>::run(
+      (const void*)__builtin_amdgcn_kernarg_segment_ptr(), warm);
+  warm_wait(warm);
+  if (!run_handshake(Y, RC, &go)) return;
+  uint32_t* const abortw = &Y->abort[0];
+  WinArgs A = A0;
+  A.abortw = abortw;
+  A.spin = RC.spin;
+  A.defer = 0;
+  if (blockIdx.x == 0) {
+    WinLDS& L = *reinterpret_cast<WinLDS*>(lds_raw);
+    for (uint32_t W = 0; W < R.nwin; ++W) {
+      A.ne = 0;
+      A.w0 = R.first + W * KSG_BATCH;
+      A.nw = min((uint32_t)KSG_BATCH, R.first + R.count - A.w0);
+      A.wrec = R.wrec + (size_t)(W & 1) * kRecBytes;
+      A.pnext = R.pend + (size_t)(W & 1) * KSG_BATCH;
+      A.pnext_n = R.pend_n + (W & 1);
+      A.pprev = R.pend + (size_t)((W + 1) & 1) * KSG_BATCH;  // P_{W-1}
+      A.pprev_n = R.pend_n + ((W + 1) & 1);
+      A.stamps = R.stamps ? R.stamps + (size_t)W * 32 : nullptr;
+      // (the counters of a window parity only grow: every earlier window of that
+      // parity is whole, KSG_BATCH pods)
+      A.flushed = &Z->flushed[W & 1];
+      A.flush_need = ((W >> 1) * KSG_BATCH + A.nw) * R.T;
+      if (!win_wait_ge(&Z->evd[W & 1], (W >> 1) * KSG_BATCH + A.nw, abortw, RC.spin, &go)) return;
+      A.pub = &Z->replayed[0][0];
+      A.pub_val = W + 1;
+      win_fixup<MODE, false, true>(C, F, A, L);  // (publishes P_W before its output patches)
+      __syncthreads();  // (LDS reused by the next window)
+    }
+    return;
+  }
+  const uint32_t blk = blockIdx.x - 1, b = blk / R.T;
+  uint64_t* const L = reinterpret_cast<uint64_t*>(lds_raw);
+  for (uint32_t E = 0; E < R.nwin; ++E) {
+    A.nw = 0;
+    A.e0 = R.first + E * KSG_BATCH;
+    A.ne = min((uint32_t)KSG_BATCH, R.first + R.count - A.e0);
+    if (b >= A.ne) break;  // (only the last window is short)
+    if (E >= 2 && !win_wait_ge(&Z->replayed[blk & 15][0], E - 1, abortw, RC.spin, &go)) return;
+    A.tile_top = R.tile_top + (size_t)(E & 1) * R.tt_sz;
+    A.tile_feas = R.tfeas + (size_t)(E & 1) * R.tf_sz;
+    A.erec = R.wrec + (size_t)(E & 1) * kRecBytes;
+    A.pprev = R.pend + (size_t)(E & 1) * KSG_BATCH;  // P_{E-2}
+    A.pprev_n = R.pend_n + (E & 1);
+    A.arrive = R.arrive + (size_t)(E & 1) * KSG_BATCH;
+    A.estamps = R.stamps ? R.stamps + (size_t)E * 32 : nullptr;
+    A.evd = &Z->evd[E & 1];
+    A.flushed = &Z->flushed[E & 1];
+    A.pcur = R.pend + (size_t)((E + 1) & 1) * KSG_BATCH;  // P_{E-1}
+    A.pcur_n = R.pend_n + ((E + 1) & 1);
+    A.pubw = E >= 1 ? &Z->replayed[blk & 15][0] : nullptr;  // (E = 0: P_{-1} is empty)
+    A.pub_need = E;
+    win_eval<MODE, false, true>(C, F, A, blk, L);
+    __syncthreads();  // (LDS reused by the next window)
+  }
+}
+
 
 template <class T>
 struct DBuf {
@@ -4531,6 +4906,9 @@ struct Engine::Impl {
   uint32_t run_spin = kRunSpin;  // polls before a persistent block gives up (KSG_RUN_SPIN: tests force an abort)
   uint64_t run_fallbacks = 0;    // segments that ran on the two-launch chain (not co-resident)
   bool lost = false;             // an aborted persistent launch left the device state half-updated
+  DBuf<WinSync> wsync;           // k_window_run's counters (zeroed per launch)
+  int win_run_on = 1;            // persistent window loop (k_window_run): KSG_WIN_RUN=0 turns it off
+  uint64_t win_runs = 0, win_fallbacks = 0;  // diagnostic: persistent window launches / not co-resident
   uint32_t fold_blocks = 256;  // table chain: k_fold above this many blocks (KSG_FOLD_BLOCKS; tests force it)
   uint32_t occ_blocks = 0;     // table chain: occupancy twins above this many blocks (0: 2 per CU; KSG_OCC_BLOCKS)
   bool occ_force = false;
@@ -4538,6 +4916,8 @@ struct Engine::Impl {
   uint32_t cnblk = 0;
   DBuf<int32_t> knorm;    // normalized scores of one kept pod
   DBuf<uint8_t> vblk;     // device cycle view block (Engine::view)
+  bool vblk_fresh = true;
+  uint32_t vgen = 0;      // view generation (slot-table entries of older views count as empty)
   size_t prog_bytes = 0;  // used bytes of the program blob
   // kept per-pair outputs
   uint32_t keep_first = 0, keep_n = 0;
@@ -4661,6 +5041,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (const char* e = std::getenv("KSG_RUN_MIN")) I.run_min = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("KSG_RUN_LAG")) I.run_lag = std::min<uint32_t>(4096, (uint32_t)std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("KSG_RUN_NORES")) I.run_need_extra = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
+  if (const char* e = std::getenv("KSG_WIN_RUN")) I.win_run_on = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_RUN_SPIN")) I.run_spin = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("KSG_RUN_WAIT_US"))
     I.run_wait_us = std::max<uint32_t>(10, std::min<uint32_t>(1000000, (uint32_t)std::strtoul(e, nullptr, 10)));
@@ -4919,11 +5300,11 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     uint32_t T = eval_tiles(I.N, I.n_cus);
     size_t Nn = std::max<uint32_t>(I.N, 1);
     if (!I.tile_top.alloc((size_t)tt_ring() * KSG_BATCH * T * KSG_TOPK, err) || !I.tfeas.alloc((size_t)tt_ring() * KSG_BATCH * T * 3, err) ||
-        !I.arrive.alloc(KSG_BATCH, err) || !I.pend_n.alloc(2, err) || !I.wrec.alloc(2 * kRecBytes, err) ||
+        !I.arrive.alloc(2 * KSG_BATCH, err) || !I.pend_n.alloc(2, err) || !I.wrec.alloc(2 * kRecBytes, err) ||
         !I.pend.alloc(2 * KSG_BATCH, err) || !I.bfilter.alloc(Nn * 2 * KSG_BATCH, err) ||
         !I.bscore.alloc(Nn * 2 * KSG_BATCH * KSG_MAX_PLUGINS, err) || !I.btotal.alloc(Nn * 2 * KSG_BATCH, err))
       return false;
-    HIPCHK(hipMemsetAsync(I.arrive.p, 0, KSG_BATCH * 4, s));
+    HIPCHK(hipMemsetAsync(I.arrive.p, 0, 2 * KSG_BATCH * 4, s));
     HIPCHK(hipMemsetAsync(I.pend_n.p, 0, 2 * 4, s));
     HIPCHK(hipMemsetAsync(I.wrec.p, 0, 2 * kRecBytes, s));
   }
@@ -4960,6 +5341,11 @@ static uint32_t eval_tiles(uint32_t N, uint32_t cus) {
   return std::max<uint32_t>((N + KSG_TILE * npt - 1) / (KSG_TILE * npt), 1);
 }
 
+// The handshake verdict of the persistent launch just queued (k_chain_run,
+// k_window_run): the host waits for it (the work queued before runs first).
+// 1 go, 2 not co-resident (its blocks left untouched), 3 an earlier launch of the
+// call aborted; 0 with err set: the launch never decided (state lost).
+static uint32_t wait_verdict(Engine::Impl& I, hipStream_t s, std::string& err);
 // Windows of KSG_BATCH pods, one k_window launch each (see the kernel): launch
 // j evaluates window j+1 and replays window j; the sharded path all-gathers
 // each window's candidate records between launches.
@@ -5166,6 +5552,71 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
       if (!issue_static(c, I.sstream)) return false;
   }
   if (sharded && !stat) return run_batches_split(I, A, first, count, T, err);
+  // the persistent window loop: one launch for every window (its blocks all
+  // resident: one per CU); not co-resident -> the launch-per-window loop below
+  if (!sharded && !stat && I.win_run_on && nwin > 0 && 1 + (uint64_t)KSG_BATCH * T <= I.n_cus) {
+    if (!I.wsync.alloc(1, err) || !I.rsync.alloc(1, err)) return false;
+    if (!I.hverdict) {
+      HIPCHK(hipHostMalloc((void**)&I.hverdict, 64, hipHostMallocCoherent | hipHostMallocMapped));
+      HIPCHK(hipMemsetAsync(I.rsync.p, 0, sizeof(RunSync), s));  // (the sticky abort word starts clear)
+    }
+    static bool wattr = false;
+    if (!wattr) {
+      HIPCHK(hipFuncSetAttribute((const void*)k_window_run<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLDS)));
+      HIPCHK(hipFuncSetAttribute((const void*)k_window_run<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLDS)));
+      wattr = true;
+    }
+    HIPCHK(hipMemsetAsync(I.wsync.p, 0, sizeof(WinSync), s));
+    HIPCHK(hipMemsetAsync(I.rsync.p, 0, kRunSyncReset, s));
+    HIPCHK(hipMemsetAsync(I.arrive.p, 0, 2 * KSG_BATCH * sizeof(uint32_t), s));
+    WinRunArgs R{};
+    R.nwin = nwin;
+    R.first = first;
+    R.count = count;
+    R.T = T;
+    R.tt_sz = (uint32_t)tt_sz;
+    R.tf_sz = (uint32_t)tf_sz;
+    R.tile_top = I.tile_top.p;
+    R.tfeas = I.tfeas.p;
+    R.wrec = I.wrec.p;
+    R.pend = I.pend.p;
+    R.pend_n = I.pend_n.p;
+    R.arrive = I.arrive.p;
+    R.stamps = I.stamps_on ? I.stamps.p : nullptr;
+    const uint32_t grid = 1 + KSG_BATCH * T;
+    __atomic_store_n(I.hverdict, 0u, __ATOMIC_RELEASE);
+    const RunCtl RC{grid + I.run_need_extra, I.run_wait_us * 100u, 0, I.hverdict, I.run_spin};
+    const bool sampled = I.sample_every && I.n_samples * 2 + 2 <= I.sev.size();
+    if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
+    if (I.eval_mode == 1)
+      hipLaunchKernelGGL(k_window_run<1>, dim3(grid), dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, A, R, I.rsync.p, I.wsync.p, RC);
+    else
+      hipLaunchKernelGGL(k_window_run<0>, dim3(grid), dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, A, R, I.rsync.p, I.wsync.p, RC);
+    if (sampled) {
+      HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
+      I.n_samples++;
+    }
+    HIPCHK(hipGetLastError());
+    I.run_used = true;
+    const uint32_t v = wait_verdict(I, s, err);
+    if (v == 0u) return false;
+    if (v == 3u) {
+      I.lost = true;
+      err = "persistent launch: a gate never completed (blocks not co-resident?)";
+      return false;
+    }
+    if (v == 1u) {
+      I.win_runs++;
+      const int64_t L = nwin - 1;
+      hipLaunchKernelGGL(k_apply_pend, dim3(1), dim3(KSG_BATCH), 0, s, C, I.pend.p + (size_t)(L & 1) * KSG_BATCH,
+                         I.pend_n.p + (L & 1));
+      HIPCHK(hipEventRecord(I.ev1, s));
+      HIPCHK(hipGetLastError());
+      return true;
+    }
+    I.win_fallbacks++;  // v == 2: its blocks left untouched; the per-window launches
+    if (sampled) I.n_samples--;
+  }
   for (int64_t j = -1; j < (int64_t)nwin; ++j) {
     const int64_t E = j + 1, W = j;
     A.ne = 0;
@@ -5904,7 +6355,8 @@ void Engine::view_layout(ViewLayout& lay) const {
     if (p == KP_TAINT || p == KP_NA || p == KP_PTS || p == KP_IPA) lay.norm_row[d] = (int)lay.n_norm++;
   }
   const size_t N = std::max<uint32_t>(I.N, 1);
-  lay.off_fail_pos = al256((kViewSlots + 1) * sizeof(uint32_t));
+  lay.off_sum = al256((kViewSlots + 1) * sizeof(uint64_t));
+  lay.off_fail_pos = lay.off_sum + al256(sizeof(ksg_pod_summary));
   lay.off_fail_code = lay.off_fail_pos + al256(N);
   lay.off_fail_msg = lay.off_fail_code + al256(N);
   lay.off_raw = lay.off_fail_msg + al256(2 * N);
@@ -5915,6 +6367,7 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
   Impl& I = *p_;
   if (!(I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n)) { err = "outputs not kept for this pod"; return false; }
   if (lay.N != I.N || lay.n_raw != (uint32_t)I.F.n) { err = "view layout of another snapshot"; return false; }
+  if (lay.bytes > I.vblk.n || !I.vblk.p) I.vblk_fresh = true;
   if (!I.vblk.alloc(lay.bytes, err)) return false;
   ViewDev V{};
   for (int d = 0; d < KSG_MAX_PLUGINS; ++d) {
@@ -5924,6 +6377,10 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
   }
   for (int p = 0; p < KSG_MAX_PROFILE; ++p) V.kind[p] = (uint8_t)cfg.kind[p];
   V.n_profile = cfg.n_profile;
+  if (++I.vgen == 0) ++I.vgen;  // (generation 0: never a live entry)
+  V.gen = I.vgen;
+  lay.gen = I.vgen;
+  V.off_sum = (uint32_t)lay.off_sum;
   V.off_fail_pos = (uint32_t)lay.off_fail_pos;
   V.off_fail_code = (uint32_t)lay.off_fail_code;
   V.off_fail_msg = (uint32_t)lay.off_fail_msg;
@@ -5931,8 +6388,11 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
   V.off_norm = (uint32_t)lay.off_norm;
   const size_t N = I.N, k = j - I.keep_first;
   hipStream_t s = I.stream;
-  HIPCHK(hipMemsetAsync(I.vblk.p, 0xFF, kViewSlots * sizeof(uint32_t), s));
-  HIPCHK(hipMemsetAsync(I.vblk.p + kViewSlots * sizeof(uint32_t), 0, sizeof(uint32_t), s));
+  if (I.vblk_fresh) {  // a new block: generation 0 everywhere
+    HIPCHK(hipMemsetAsync(I.vblk.p, 0, (kViewSlots + 1) * sizeof(uint64_t), s));
+    I.vblk_fresh = false;
+  }
+  if (!N) HIPCHK(hipMemcpyAsync(I.vblk.p + lay.off_sum, I.sums.p + j, sizeof(ksg_pod_summary), hipMemcpyDeviceToDevice, s));
   if (N)
     hipLaunchKernelGGL(k_view, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, I.cluster(), I.F, I.progs.p + I.prog_off[j],
                        I.sums.p + j, I.kfilter.p + k * N, I.kscore.p + k * N * KSG_MAX_PLUGINS, V, I.vblk.p);
@@ -6235,25 +6695,8 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         // The handshake: the launch's blocks decide whether all of them are
         // resident before any state changes.  The host waits for that verdict (the
         // work queued before the segment runs first), then queues the rest.
-        uint32_t v = 0;
-        {
-          const auto t0 = std::chrono::steady_clock::now();
-          for (uint32_t it = 0; (v = __atomic_load_n(hv, __ATOMIC_ACQUIRE)) == 0u; ++it) {
-            if ((it & 1023u) == 1023u) {
-              if (hipStreamQuery(s) == hipSuccess && (v = __atomic_load_n(hv, __ATOMIC_ACQUIRE)) == 0u) {
-                I.lost = true;
-                err = "persistent table chain: the launch ended without a handshake";
-                return false;
-              }
-              if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
-                I.lost = true;
-                err = "persistent table chain: the launch did not start within 60 s";
-                return false;
-              }
-              std::this_thread::yield();
-            }
-          }
-        }
+        const uint32_t v = wait_verdict(I, s, err);
+        if (v == 0u) return false;
         if (v == 3u) {  // an earlier segment of this call aborted: the state is not valid
           I.lost = true;
           err = "persistent table chain: a gate never completed (blocks not co-resident?)";
@@ -6406,6 +6849,28 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   return true;
 }
 
+static uint32_t wait_verdict(Engine::Impl& I, hipStream_t s, std::string& err) {
+  uint32_t* const hv = I.hverdict;
+  uint32_t v = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t it = 0; (v = __atomic_load_n(hv, __ATOMIC_ACQUIRE)) == 0u; ++it) {
+    if ((it & 1023u) == 1023u) {
+      if (hipStreamQuery(s) == hipSuccess && (v = __atomic_load_n(hv, __ATOMIC_ACQUIRE)) == 0u) {
+        I.lost = true;
+        err = "persistent launch ended without a handshake";
+        return 0;
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+        I.lost = true;
+        err = "persistent launch did not start within 60 s";
+        return 0;
+      }
+      std::this_thread::yield();
+    }
+  }
+  return v;
+}
+
 bool Engine::sync(std::string& err) {
   Impl& I = *p_;
   HIPCHK(hipStreamSynchronize(I.stream));
@@ -6527,8 +6992,8 @@ bool Engine::set_exchange(int mode, const void* nccl_id, uint32_t rank, uint32_t
 uint32_t Engine::exchange_ranks() const { return p_->xranks; }
 void Engine::path_counts(uint64_t out[8]) const {
   for (int i = 0; i < 6; ++i) out[i] = p_->path_pods[i];
-  out[6] = p_->run_fallbacks;
-  out[7] = 0;
+  out[6] = p_->run_fallbacks + p_->win_fallbacks;
+  out[7] = p_->win_runs;
 }
 bool Engine::lost() const { return p_->lost; }
 void Engine::clear_lost() {

@@ -4616,8 +4616,6 @@ int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out)
   if (!out) return KSG_E_INVALID;
   *out = nullptr;
   if (q >= c.meta.size()) return ctx->fail("cycle_view: range", KSG_E_RANGE);
-  ksg_pod_summary S;
-  if (!c.eng->summaries(q, 1, &S, c.err)) return ctx->fail(c.err, KSG_E_DEVICE);
   ksg::Engine::ViewLayout lay;
   c.eng->view_layout(lay);
   std::unique_ptr<CycleView> v(new CycleView());
@@ -4626,14 +4624,19 @@ int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out)
   if (!c.eng->view(q, c.view_cfg(), lay, v->block, c.err)) return ctx->fail(c.err, KSG_E_STATE);
   const uint32_t P = (uint32_t)c.n_plugins, N = c.hi - c.lo;
   v->msgs.resize(lay.n_slots + 1);  // messages[s + 1]: the message of slot s's code
-  const uint32_t* slots = reinterpret_cast<const uint32_t*>(v->block);
-  const bool overflow = slots[lay.n_slots] != 0;
+  const uint64_t* slots = reinterpret_cast<const uint64_t*>(v->block);
+  const bool overflow = (uint32_t)(slots[lay.n_slots] >> 32) == lay.gen;
+  ksg_pod_summary S;
+  std::memcpy(&S, v->block + lay.off_sum, sizeof(S));
   const int8_t* fail_pos = reinterpret_cast<const int8_t*>(v->block + lay.off_fail_pos);
   const int8_t* fail_code = reinterpret_cast<const int8_t*>(v->block + lay.off_fail_code);
   const uint16_t* fail_msg = reinterpret_cast<const uint16_t*>(v->block + lay.off_fail_msg);
   if (!overflow) {
     for (uint32_t k = 0; k < lay.n_slots; ++k)
-      if (slots[k] != 0xFFFFFFFFu) v->msgs[k + 1] = c.filter_message(c.code_pos(slots[k]), c.code_detail(slots[k]));
+      if ((uint32_t)(slots[k] >> 32) == lay.gen) {
+        const uint32_t code = (uint32_t)slots[k];
+        v->msgs[k + 1] = c.filter_message(c.code_pos(code), c.code_detail(code));
+      }
   } else {  // more distinct failing codes than slots (never seen): the per-node calls' answers
     const ksg::PodOutputs* o = c.outputs_of(q);
     if (!o) return ctx->fail(c.err, KSG_E_STATE);

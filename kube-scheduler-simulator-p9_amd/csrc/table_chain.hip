@@ -2121,16 +2121,24 @@ struct ViewDev {
   int8_t norm_row[KSG_MAX_PLUGINS];     // device position -> normalized row, -1: none (output == raw)
   uint8_t kind[KSG_MAX_PROFILE];        // per profile position: the framework code of its Filter failure
   int32_t n_profile;
-  uint32_t off_fail_pos, off_fail_code, off_fail_msg, off_raw, off_norm;  // byte offsets in the block
+  uint32_t gen;  // this view's generation: a slot (or the overflow word) holds gen << 32 | code
+  uint32_t off_sum, off_fail_pos, off_fail_code, off_fail_msg, off_raw, off_norm;  // byte offsets in the block
 };
-__device__ __forceinline__ uint32_t view_slot(uint32_t* tab, uint32_t code) {
+// slot of `code` in the table (entries of other generations count as empty: no clearing per view)
+__device__ __forceinline__ uint32_t view_slot(unsigned long long* tab, uint32_t gen, uint32_t code) {
+  const unsigned long long want = ((unsigned long long)gen << 32) | code;
   uint32_t h = (code * 2654435761u) >> 24;
   for (int k = 0; k < kViewSlots; ++k) {
-    const uint32_t old = atomicCAS(&tab[h], 0xFFFFFFFFu, code);
-    if (old == 0xFFFFFFFFu || old == code) return h;
+    unsigned long long cur = __hip_atomic_load(&tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while ((uint32_t)(cur >> 32) != gen) {  // stale: claim it
+      const unsigned long long old = atomicCAS(&tab[h], cur, want);
+      if (old == cur) return h;
+      cur = old;
+    }
+    if (cur == want) return h;
     h = (h + 1) & (kViewSlots - 1);
   }
-  atomicOr(&tab[kViewSlots], 1u);  // overflow (the host renders the view itself)
+  atomicMax(&tab[kViewSlots], (unsigned long long)gen << 32);  // overflow (the host renders the view itself)
   return kViewSlots;
 }
 __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const uint8_t* prog, const ksg_pod_summary* sum,
@@ -2164,14 +2172,15 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
     need = true;
   }
   // message slots: one insert per distinct code of the wave
-  uint32_t* tab = reinterpret_cast<uint32_t*>(out);
+  unsigned long long* tab = reinterpret_cast<unsigned long long*>(out);
+  if (n == 0) *reinterpret_cast<ksg_pod_summary*>(out + V.off_sum) = *sum;
   uint32_t msg = 0;
   const uint32_t lane = threadIdx.x & 63;
   for (uint64_t m = __ballot(need); m; m = __ballot(need)) {
     const int leader = __ffsll((long long)m) - 1;
     const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)code, leader);
     uint32_t s = 0;
-    if ((int)lane == leader) s = view_slot(tab, c0);
+    if ((int)lane == leader) s = view_slot(tab, V.gen, c0);
     s = (uint32_t)__builtin_amdgcn_readlane((int)s, leader);
     if (need && code == c0) {
       msg = s < kViewSlots ? s + 1 : 0;

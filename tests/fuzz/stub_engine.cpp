@@ -282,7 +282,8 @@ void Engine::view_layout(ViewLayout& lay) const {
   lay.n_slots = 256;
   for (int d = 0; d < KSG_MAX_PLUGINS; ++d) lay.norm_row[d] = -1;
   const size_t N = p_->N ? p_->N : 1;
-  lay.off_fail_pos = al256s(257 * 4);
+  lay.off_sum = al256s(257 * 8);
+  lay.off_fail_pos = lay.off_sum + al256s(sizeof(ksg_pod_summary));
   lay.off_fail_code = lay.off_fail_pos + al256s(N);
   lay.off_fail_msg = lay.off_fail_code + al256s(N);
   lay.off_raw = lay.off_fail_msg + al256s(2 * N);
@@ -294,7 +295,8 @@ bool Engine::view(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
   if (!(p_->keep_n && q >= p_->keep_first && q < p_->keep_first + p_->keep_n)) { err = "outputs not kept for this pod"; return false; }
   if (!outputs(q, o, err)) return false;
   std::memset(host, 0, lay.bytes);
-  std::memset(host, 0xFF, 256 * 4);
+  lay.gen = 1;
+  std::memcpy(host + lay.off_sum, &o.summary, sizeof(o.summary));
   for (uint32_t i = 0; i < p_->N; ++i) {
     const uint32_t c = o.filter[i];
     reinterpret_cast<int8_t*>(host + lay.off_fail_pos)[i] =

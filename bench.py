@@ -224,7 +224,10 @@ def dropin_latency(s, doc, n=100):
 
 # cfg3 / cfg4 (BASELINE.json configs[2], configs[3]) at their full single-GPU size,
 # reported beside the cfg2 headline.  Algorithmic bytes: SURVEY.md §8(d), DESIGN.md.
-CFG3_PAIR_BYTES = 141      # 120 read + 21 written per (pod, node) pair
+CFG3_PAIR_BYTES = 141      # 120 read + 21 written per (pod, node) pair (SURVEY §8(d))
+# cfg3 runs two kernels over every pair (DESIGN.md "TaintToleration / NodeAffinity"):
+CFG3_STATIC_PAIR_BYTES = 64 + 8   # k_static: taint masks 16 + label bitsets 40 + numeric label 8 read, record 8 written
+CFG3_WINDOW_PAIR_BYTES = 56 + 8 + 21  # k_window: node row 56 + static record 8 read, filter 1 + 4 raw scores + total written
 CFG4_EVAL_NODE_BYTES = 68 + 20  # k_eval: reads node row 56 + zone id 4 + selector-class count 8, writes the
                                 # per-pair filter code 4 + the four raw scores 16 (k_final re-reads them)
 CFG4_RUN_NODE_BYTES = 68        # SURVEY §8(d) cfg4 per node and pod (row 56, zone id 4, class count 8);
@@ -246,10 +249,26 @@ def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
     run1 = s.run_counts()
     res = s.results()
     per = None
+    extra_kernels = None
     if s.batch_path:
+        # k_window's own bytes; k_static (the Taint / NodeAffinity records it reads)
+        # gets its own line, timed on the same sampled run
         kname = "k_window"
         tiles = (n_nodes + TILE - 1) // TILE
-        bpl = WINDOW * n_nodes * CFG3_PAIR_BYTES + 2 * tiles * WINDOW * 64 * 8 + 2 * REC_BYTES
+        bpl = WINDOW * n_nodes * CFG3_WINDOW_PAIR_BYTES + 2 * tiles * WINDOW * 64 * 8 + 2 * REC_BYTES
+        st_ms, st_n, st_pods = s.static_time()
+        if st_n:
+            sb = st_pods * n_nodes * CFG3_STATIC_PAIR_BYTES
+            win_ms_total = kms * ((n_pods + WINDOW - 1) // WINDOW)
+            extra_kernels = {
+                "k_static": {"launches": st_n, "total_ms": st_ms, "bytes": sb,
+                             "achieved": sb / (st_ms * 1e-3) / 1e9, "frac": sb / (st_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "bytes_per_pair": CFG3_STATIC_PAIR_BYTES, "traffic": pmc_traffic(f"cfg{c}:k_static")},
+                "step": {"note": "both kernels over the whole queue: pairs x (k_static + k_window bytes per pair) / "
+                                 "(k_static time + k_window time); the k_window time is its sampled average x windows",
+                         "bytes_per_pair": CFG3_STATIC_PAIR_BYTES + CFG3_WINDOW_PAIR_BYTES,
+                         "frac": n_pods * n_nodes * (CFG3_STATIC_PAIR_BYTES + CFG3_WINDOW_PAIR_BYTES)
+                         / ((st_ms + win_ms_total) * 1e-3) / 1e9 / HBM_PEAK_GBS}}
     elif run1[1] > run0[1]:
         # persistent segments: one k_chain_run launch per segment of pods; the
         # roofline's "launch" is one pod's cycle inside it (launch time / its pods)
@@ -271,7 +290,8 @@ def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(f"cfg{c}:{kname}"),
                         "kernel": kname, "kernel_avg_us": kms * 1e3, "kernel_samples": kn, "bytes_per_launch": bpl,
                         **({"pods_per_launch": per, "note": "k_chain_run: kernel_avg_us and bytes_per_launch per pod "
-                            "cycle inside the persistent launch (launch time / its pods)"} if per else {})},
+                            "cycle inside the persistent launch (launch time / its pods)"} if per else {}),
+                        **({"bytes_per_pair": CFG3_WINDOW_PAIR_BYTES, "other_kernels": extra_kernels} if extra_kernels else {})},
            "generate_s": round(gen_s, 1)}
     if c == 4:
         out["dropin"] = dropin_latency(s, doc)
@@ -305,7 +325,12 @@ def main():
     s.load_cluster(doc)
     n_nodes, n_pods = s.n_nodes, s.queue_len  # n_nodes: whole cluster
     elapsed = time_queue(s, torch, a.steps, a.warmup, dist)
+    wr0 = s.window_runs()
     kernel_ms, kcount = sample_dominant(s, 64)
+    persistent = s.window_runs() > wr0  # one k_window_run launch for the whole queue
+    nwin = (n_pods + WINDOW - 1) // WINDOW
+    if persistent:
+        kernel_ms /= nwin  # per window inside the persistent launch
     res = s.results()
     dropin = dropin_latency(s, doc) if world == 1 else None
     scheduled = sum(1 for r in res if r.status == 0)
@@ -314,7 +339,7 @@ def main():
     ms_per_step = elapsed * 1e3 / a.steps
     shard = n_nodes // world
     if s.batch_path:
-        kname = "k_window"
+        kname = "k_window_run" if persistent else "k_window"
         bytes_per_launch = window_bytes_per_launch(shard)
     else:
         kname = "k_filter_score"
@@ -341,7 +366,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(kname),
                      "kernel": kname, "kernel_avg_us": kernel_ms * 1e3, "kernel_samples": kcount,
-                     "bytes_per_launch": bytes_per_launch},
+                     "bytes_per_launch": bytes_per_launch,
+                     **({"note": "k_window_run: the whole queue in one persistent launch; kernel_avg_us and "
+                                 "bytes_per_launch per 32-pod window inside it (launch time / windows)",
+                         "windows_per_launch": nwin} if persistent else {})},
     }
     if dropin:
         out["dropin"] = dropin

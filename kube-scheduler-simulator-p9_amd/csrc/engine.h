@@ -234,6 +234,9 @@ class Engine {
   bool eval_stamps(bool on, std::vector<uint64_t>* out, std::string& err);
   // Average duration (ms) and count of the sampled launches of the last run.
   bool kernel_time(float& avg_ms, uint32_t& samples, std::string& err);
+  // The static-record launches (k_static) of the same sampled window run: their
+  // total time, launches and pods.
+  bool static_time(float& total_ms, uint32_t& launches, uint64_t& pods, std::string& err);
   // Read back the node resource rows (parity tests of the assume delta).
   bool read_requested(std::vector<int64_t>& requested, std::vector<int32_t>& pod_count, std::string& err);
   // NonZeroRequested cpu / memory rows [2][n] (Fit scoring input).

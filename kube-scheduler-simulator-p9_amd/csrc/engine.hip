@@ -2301,6 +2301,8 @@ struct WinArgs {
   const int32_t* pcur_n;
   const uint32_t* pubw;
   uint32_t pub_need;
+  uint32_t mblocks;   // persistent loop: dedicated merge blocks (one per pod) merge the tile lists
+  uint32_t astride;   // arrival counter stride (u32): 1, or 32 in the persistent loop (a line per pod)
 };
 __device__ __forceinline__ const StaticRec* srec_row(const WinArgs& A, uint32_t q, uint32_t N) {
   return A.stat + (size_t)((q - A.first) % A.stat_ring) * N;
@@ -3407,6 +3409,170 @@ __device__ __forceinline__ const PriorRec* prior_rec(const uint8_t* rec) {
 }
 static_assert(KSG_BATCH * sizeof(PriorRec) <= kRecKeys * sizeof(RowV), "prior records fit the rows area");
 static_assert(sizeof(PriorRec) % 8 == 0, "8-byte words");
+// The merge of pod b's T tile lists into its candidate record (the pod's
+// last-arriving tile block, or in the persistent loop its merge block): LDS L as
+// win_eval's, h its pod record, pnl / np P_{E-2}'s nodes.
+template <int MODE, bool STAT, bool PER>
+__device__ __forceinline__ void win_merge(const DevCluster& C, const DevProfile& F, const WinArgs& A, uint32_t b, uint64_t* L,
+                                          const PodLite* h, const int32_t* pnl, int np) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  (void)tid;
+  auto pend_lds = [&](int32_t gid) {
+    int hit = -1;
+    for (int e = 0; e < np; ++e) hit = pnl[e] == gid ? e : hit;
+    return hit;
+  };
+  // last tile block of pod b: merge the T tile lists (wave w takes tiles w, w+16, ...);
+  // the lists and the tiles' counts are requested together.
+  int32_t f[3] = {0, 0, 0};
+  {
+    const uint64_t* src = A.tile_top + (size_t)b * A.T * KSG_TOPK;
+    uint64_t v = 0;
+    if ((uint32_t)w < A.T) v = ld_agent(src + (size_t)w * KSG_TOPK + lane);
+    if (w == 0)
+      for (uint32_t t = lane; t < A.T; t += 64)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          f[k] += __hip_atomic_load(A.tile_feas + ((size_t)b * A.T + t) * 3 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll 1
+    for (uint32_t t = w + 16; t < A.T; t += 16) v = wave_merge_top(v, ld_agent(src + (size_t)t * KSG_TOPK + 63 - lane));
+    L[w * 64 + lane] = v;
+  }
+  lds_barrier();
+  int s0 = 1;  // (waves >= T hold no list: the tree starts at the level that covers T)
+  while (s0 < (int)A.T && s0 < 16) s0 <<= 1;
+#pragma unroll 1
+  for (int s = s0 >> 1; s >= 1; s >>= 1) {
+    if (w < s) L[w * 64 + lane] = wave_merge_top(L[w * 64 + lane], L[(w + s) * 64 + 63 - lane]);
+    lds_barrier();
+  }
+  if (PER && w == 0) {  // (persistent loop: keys, counts, shallow rows, then the prior step)
+    const uint64_t v = L[lane];
+    const int32_t gid = (int32_t)(v & 0xFFFFFull);
+    PriorRec* pr = prior_rec(A.erec) + b;
+    stv<true>(rec_keys(A.erec) + (size_t)b * KSG_CAND + lane, v);
+    if (lane < KSG_STAGE) {
+      RowV c;
+      memset(&c, 0, sizeof(c));
+      if (v) {
+        const int hh = pend_lds(gid);
+        if (hh >= 0) c = ld_obj<true>(&A.pprev[hh].after);
+        else load_row_p<true>(C, (uint32_t)gid - C.goff, A.need_eph, c);
+      }
+      st_obj<true>(&pr->row[lane], c);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) f[k] = wave_sum(f[k]);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) stv<true>(reinterpret_cast<int32_t*>(A.erec) + k * KSG_BATCH + b, f[k]);
+      stv<true>(A.arrive + b * A.astride, 0u);
+    }
+    // the prior step: pod q on P_{E-1}'s nodes (published by the replay of E-1)
+    int np1 = 0;
+    if (A.pubw) {
+      uint32_t ok = 1;
+      if (lane == 0) {
+        ok = 0;
+        for (uint32_t it = 0; it < A.spin; ++it) {
+          if (ld_sc1(A.pubw) >= A.pub_need) { ok = 1; break; }
+          if ((it & 63u) == 63u && ld_sc1(A.abortw) != 0u) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) __hip_atomic_store(A.abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (__builtin_amdgcn_readfirstlane(ok)) np1 = ldv<true>(A.pcur_n);  // (else the run has aborted)
+    }
+    Pend pe;
+    pe.node = -1;
+    uint64_t k = 0;
+    if (lane < np1) {
+      pe = ld_obj<true>(A.pcur + lane);
+      int32_t fs, bs;
+      int64_t tot;
+      const uint32_t R = C.R < 4 ? C.R : 4;
+      const uint32_t code = eval_row<MODE>(pe.after, F, h, R, fs, bs, tot);
+      const bool snap_ok = F.pos_fit < 0 || fit_filter_row(pe.base, h, R) == 0;
+      PatchV pt;
+      pt.code = code;
+      pt.fitba = fs | (bs << 16);
+      pt.total = (int32_t)tot;
+      pt.raw = 0;
+      k = code == KSG_FILTER_PASS ? pack_key(tot, F.seed, h->queue_idx, (uint32_t)pe.node) : 0;
+      stv<true>(&pr->pkey[lane], k);
+      st_obj<true>(&pr->patch[lane], pt);
+      stv<true>(&pr->pdf[lane], (int32_t)((code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0)));
+    }
+    bool isp = false;  // candidate `lane` is a P_{E-1} node
+    for (int e = 0; e < np1; ++e) isp |= v != 0 && __builtin_amdgcn_readlane(pe.node, e) == gid;
+    const unsigned long long pm = __ballot(isp);
+    const uint64_t kb = wave_max(k);
+    const unsigned long long mb = __ballot(kb != 0 && k == kb);
+    if (lane == 0) {
+      stv<true>(&pr->pmask, (uint64_t)pm);
+      stv<true>(&pr->pbest, kb);
+      stv<true>(&pr->pbest_e, (int32_t)(mb ? __ffsll((long long)mb) - 1 : -1));
+      stv<true>(&pr->np, np1);
+      if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pod's record is out (wave 0 stored all of it)
+    if (lane == 0) __hip_atomic_fetch_add(A.evd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (w == 0) {
+    uint64_t v = L[lane];
+    RowV c;
+    memset(&c, 0, sizeof(c));
+    int32_t gid = (int32_t)(v & 0xFFFFFull);
+    int hh = pend_lds(gid);
+    if (v) {
+      if (hh >= 0) c = ld_obj<PER>(&A.pprev[hh].after);
+      else load_row_p<PER>(C, (uint32_t)gid - C.goff, A.need_eph, c);
+    }
+    stv<PER>(rec_keys(A.erec) + (size_t)b * KSG_CAND + lane, v);
+    if (!A.xrows) st_obj<PER>(rec_rows(A.erec) + (size_t)b * KSG_CAND + lane, c);  // (sharded: rows from the replica)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) f[k] = wave_sum(f[k]);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) stv<PER>(reinterpret_cast<int32_t*>(A.erec) + k * KSG_BATCH + b, f[k]);
+      stv<PER>(A.arrive + b * A.astride, 0u);
+      if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+    if constexpr (PER) {  // the pod's record is out (wave 0 stored all of it): the replay may stage it
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(A.evd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+// Persistent loop, dedicated merge block of pod b: waits for the pod's T tile
+// lists (the arrival counter), then merges them (win_merge) while the tile blocks
+// go on to the next window.
+template <int MODE>
+__device__ __forceinline__ bool win_merge_block(const DevCluster& C, const DevProfile& F, const WinArgs& A, uint32_t b,
+                                                uint64_t* L) {
+  const int tid = threadIdx.x;
+  uint32_t* wcount = reinterpret_cast<uint32_t*>(L + 16 * 64);
+  PodLite* h = reinterpret_cast<PodLite*>(wcount + 96);
+  int32_t* pnl = reinterpret_cast<int32_t*>(wcount + 64);
+  const uint32_t q = A.e0 + b;
+  constexpr int kPodW = (int)(sizeof(PodLite) / 8);
+  if (tid < kPodW) reinterpret_cast<uint64_t*>(h)[tid] = reinterpret_cast<const uint64_t*>(A.plite + q)[tid];
+  const int np = ldv<true>(A.pprev_n);
+  if (tid < np) pnl[tid] = ldv<true>(&A.pprev[tid].node);
+  if (tid == 0) {
+    bool ok = false;
+    for (uint32_t it = 0; it < A.spin; ++it) {
+      if (ld_sc1(A.arrive + b * A.astride) >= A.T) { ok = true; break; }
+      if ((it & 63u) == 63u && ld_sc1(A.abortw) != 0u) break;
+      __builtin_amdgcn_s_sleep(4);
+    }
+    if (!ok) __hip_atomic_store(A.abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    wcount[17] = ok ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!wcount[17]) return false;
+  win_merge<MODE, false, true>(C, F, A, b, L, h, pnl, np);
+  return true;
+}
 // Blocks 1.. of k_window: one pod x KSG_TILE nodes per block.  Tile lists are
 // handed to the pod's last-arriving block with sc1 stores/loads and an agent
 // counter (MI355X_MICROARCH.md, hand-off table row 1).
@@ -3558,9 +3724,9 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       uint32_t old = 0;
-      if (lane == 0) old = __hip_atomic_fetch_add(A.arrive + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) old = __hip_atomic_fetch_add(A.arrive + b * A.astride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       old = __builtin_amdgcn_readfirstlane(old);
-      if (lane == 0) wcount[16] = old == A.T - 1 ? 1u : 0u;  // (slots 17..31 unused)
+      if (lane == 0) wcount[16] = (!A.mblocks && old == A.T - 1) ? 1u : 0u;  // (slots 17..31 unused)
     }
   }
   auto flush_stash = [&]() {
@@ -3608,124 +3774,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
     signal_flushed();
     return;
   }
-  // last tile block of pod b: merge the T tile lists (wave w takes tiles w, w+16, ...);
-  // the lists and the tiles' counts are requested together.
-  int32_t f[3] = {0, 0, 0};
-  {
-    const uint64_t* src = A.tile_top + (size_t)b * A.T * KSG_TOPK;
-    uint64_t v = 0;
-    if ((uint32_t)w < A.T) v = ld_agent(src + (size_t)w * KSG_TOPK + lane);
-    if (w == 0)
-      for (uint32_t t = lane; t < A.T; t += 64)
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-          f[k] += __hip_atomic_load(A.tile_feas + ((size_t)b * A.T + t) * 3 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll 1
-    for (uint32_t t = w + 16; t < A.T; t += 16) v = wave_merge_top(v, ld_agent(src + (size_t)t * KSG_TOPK + 63 - lane));
-    L[w * 64 + lane] = v;
-  }
-  lds_barrier();
-#pragma unroll 1
-  for (int s = 8; s >= 1; s >>= 1) {
-    if (w < s) L[w * 64 + lane] = wave_merge_top(L[w * 64 + lane], L[(w + s) * 64 + 63 - lane]);
-    lds_barrier();
-  }
-  if (PER && w == 0) {  // (persistent loop: keys, counts, shallow rows, then the prior step)
-    const uint64_t v = L[lane];
-    const int32_t gid = (int32_t)(v & 0xFFFFFull);
-    PriorRec* pr = prior_rec(A.erec) + b;
-    stv<true>(rec_keys(A.erec) + (size_t)b * KSG_CAND + lane, v);
-    if (lane < KSG_STAGE) {
-      RowV c;
-      memset(&c, 0, sizeof(c));
-      if (v) {
-        const int hh = pend_lds(gid);
-        if (hh >= 0) c = ld_obj<true>(&A.pprev[hh].after);
-        else load_row_p<true>(C, (uint32_t)gid - C.goff, A.need_eph, c);
-      }
-      st_obj<true>(&pr->row[lane], c);
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) f[k] = wave_sum(f[k]);
-    if (lane == 0) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) stv<true>(reinterpret_cast<int32_t*>(A.erec) + k * KSG_BATCH + b, f[k]);
-      stv<true>(A.arrive + b, 0u);
-    }
-    // the prior step: pod q on P_{E-1}'s nodes (published by the replay of E-1)
-    int np1 = 0;
-    if (A.pubw) {
-      uint32_t ok = 1;
-      if (lane == 0) {
-        ok = 0;
-        for (uint32_t it = 0; it < A.spin; ++it) {
-          if (ld_sc1(A.pubw) >= A.pub_need) { ok = 1; break; }
-          if ((it & 63u) == 63u && ld_sc1(A.abortw) != 0u) break;
-          __builtin_amdgcn_s_sleep(2);
-        }
-        if (!ok) __hip_atomic_store(A.abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (__builtin_amdgcn_readfirstlane(ok)) np1 = ldv<true>(A.pcur_n);  // (else the run has aborted)
-    }
-    Pend pe;
-    pe.node = -1;
-    uint64_t k = 0;
-    if (lane < np1) {
-      pe = ld_obj<true>(A.pcur + lane);
-      int32_t fs, bs;
-      int64_t tot;
-      const uint32_t R = C.R < 4 ? C.R : 4;
-      const uint32_t code = eval_row<MODE>(pe.after, F, h, R, fs, bs, tot);
-      const bool snap_ok = F.pos_fit < 0 || fit_filter_row(pe.base, h, R) == 0;
-      PatchV pt;
-      pt.code = code;
-      pt.fitba = fs | (bs << 16);
-      pt.total = (int32_t)tot;
-      pt.raw = 0;
-      k = code == KSG_FILTER_PASS ? pack_key(tot, F.seed, h->queue_idx, (uint32_t)pe.node) : 0;
-      stv<true>(&pr->pkey[lane], k);
-      st_obj<true>(&pr->patch[lane], pt);
-      stv<true>(&pr->pdf[lane], (int32_t)((code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0)));
-    }
-    bool isp = false;  // candidate `lane` is a P_{E-1} node
-    for (int e = 0; e < np1; ++e) isp |= v != 0 && __builtin_amdgcn_readlane(pe.node, e) == gid;
-    const unsigned long long pm = __ballot(isp);
-    const uint64_t kb = wave_max(k);
-    const unsigned long long mb = __ballot(kb != 0 && k == kb);
-    if (lane == 0) {
-      stv<true>(&pr->pmask, (uint64_t)pm);
-      stv<true>(&pr->pbest, kb);
-      stv<true>(&pr->pbest_e, (int32_t)(mb ? __ffsll((long long)mb) - 1 : -1));
-      stv<true>(&pr->np, np1);
-      if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pod's record is out (wave 0 stored all of it)
-    if (lane == 0) __hip_atomic_fetch_add(A.evd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if (w == 0) {
-    uint64_t v = L[lane];
-    RowV c;
-    memset(&c, 0, sizeof(c));
-    int32_t gid = (int32_t)(v & 0xFFFFFull);
-    int hh = pend_lds(gid);
-    if (v) {
-      if (hh >= 0) c = ld_obj<PER>(&A.pprev[hh].after);
-      else load_row_p<PER>(C, (uint32_t)gid - C.goff, A.need_eph, c);
-    }
-    stv<PER>(rec_keys(A.erec) + (size_t)b * KSG_CAND + lane, v);
-    if (!A.xrows) st_obj<PER>(rec_rows(A.erec) + (size_t)b * KSG_CAND + lane, c);  // (sharded: rows from the replica)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) f[k] = wave_sum(f[k]);
-    if (lane == 0) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) stv<PER>(reinterpret_cast<int32_t*>(A.erec) + k * KSG_BATCH + b, f[k]);
-      stv<PER>(A.arrive + b, 0u);
-      if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    }
-    if constexpr (PER) {  // the pod's record is out (wave 0 stored all of it): the replay may stage it
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(A.evd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  win_merge<MODE, STAT, PER>(C, F, A, b, L, h, pnl, np);
   flush_stash();
   signal_flushed();
 }
@@ -4648,7 +4697,7 @@ struct WinRunArgs {
   uint8_t* wrec;           // 2 x kRecBytes
   Pend* pend;              // [2][KSG_BATCH]
   int32_t* pend_n;         // [2]
-  uint32_t* arrive;        // [2][KSG_BATCH]
+  uint32_t* arrive;        // [2][KSG_BATCH] counters, one 128-B line each
   uint64_t* stamps;        // diagnostic: 32 slots per window, or null
 };
 __device__ bool win_wait_ge(const uint32_t* w, uint32_t want, uint32_t* abortw, uint32_t spin, uint32_t* go) {
@@ -4706,8 +4755,32 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
     }
     return;
   }
-  const uint32_t blk = blockIdx.x - 1, b = blk / R.T;
   uint64_t* const L = reinterpret_cast<uint64_t*>(lds_raw);
+  if (A0.mblocks && blockIdx.x >= 1 + KSG_BATCH * R.T) {  // the merge block of pod b
+    const uint32_t b = blockIdx.x - 1 - KSG_BATCH * R.T;
+    for (uint32_t E = 0; E < R.nwin; ++E) {
+      A.nw = 0;
+      A.e0 = R.first + E * KSG_BATCH;
+      A.ne = min((uint32_t)KSG_BATCH, R.first + R.count - A.e0);
+      if (b >= A.ne) break;
+      A.tile_top = R.tile_top + (size_t)(E & 1) * R.tt_sz;
+      A.tile_feas = R.tfeas + (size_t)(E & 1) * R.tf_sz;
+      A.erec = R.wrec + (size_t)(E & 1) * kRecBytes;
+      A.pprev = R.pend + (size_t)(E & 1) * KSG_BATCH;  // P_{E-2}
+      A.pprev_n = R.pend_n + (E & 1);
+      A.arrive = R.arrive + (size_t)(E & 1) * KSG_BATCH * 32;
+      A.estamps = R.stamps ? R.stamps + (size_t)E * 32 : nullptr;
+      A.evd = &Z->evd[E & 1];
+      A.pcur = R.pend + (size_t)((E + 1) & 1) * KSG_BATCH;  // P_{E-1}
+      A.pcur_n = R.pend_n + ((E + 1) & 1);
+      A.pubw = E >= 1 ? &Z->replayed[b & 15][0] : nullptr;
+      A.pub_need = E;
+      if (!win_merge_block<MODE>(C, F, A, b, L)) return;
+      __syncthreads();  // (LDS reused by the next window)
+    }
+    return;
+  }
+  const uint32_t blk = blockIdx.x - 1, b = blk / R.T;
   for (uint32_t E = 0; E < R.nwin; ++E) {
     A.nw = 0;
     A.e0 = R.first + E * KSG_BATCH;
@@ -4719,7 +4792,7 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
     A.erec = R.wrec + (size_t)(E & 1) * kRecBytes;
     A.pprev = R.pend + (size_t)(E & 1) * KSG_BATCH;  // P_{E-2}
     A.pprev_n = R.pend_n + (E & 1);
-    A.arrive = R.arrive + (size_t)(E & 1) * KSG_BATCH;
+    A.arrive = R.arrive + (size_t)(E & 1) * KSG_BATCH * 32;
     A.estamps = R.stamps ? R.stamps + (size_t)E * 32 : nullptr;
     A.evd = &Z->evd[E & 1];
     A.flushed = &Z->flushed[E & 1];
@@ -4908,6 +4981,7 @@ struct Engine::Impl {
   bool lost = false;             // an aborted persistent launch left the device state half-updated
   DBuf<WinSync> wsync;           // k_window_run's counters (zeroed per launch)
   int win_run_on = 1;            // persistent window loop (k_window_run): KSG_WIN_RUN=0 turns it off
+  int win_mblocks = 1;           // ... with dedicated merge blocks (KSG_WIN_MB=0: the last tile block merges)
   uint64_t win_runs = 0, win_fallbacks = 0;  // diagnostic: persistent window launches / not co-resident
   uint32_t fold_blocks = 256;  // table chain: k_fold above this many blocks (KSG_FOLD_BLOCKS; tests force it)
   uint32_t occ_blocks = 0;     // table chain: occupancy twins above this many blocks (0: 2 per CU; KSG_OCC_BLOCKS)
@@ -4966,6 +5040,9 @@ struct Engine::Impl {
   uint32_t sample_every = 0;
   std::vector<hipEvent_t> sev;
   uint32_t n_samples = 0;
+  std::vector<hipEvent_t> sev_st;  // ... and around the static-record launches (k_static) of the same run
+  uint32_t n_st = 0;
+  uint64_t stat_pods_sampled = 0;
   uint64_t path_pods[6] = {0, 0, 0, 0, 0, 0};  // diagnostic: pods run by the table chain / the scanning chain / of the first, in one launch; what-if pod chunks on the class path; table-chain pods of persistent segments (k_chain_run) / those segments
   std::vector<Engine::KernelStat> stats;
 
@@ -5042,6 +5119,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (const char* e = std::getenv("KSG_RUN_LAG")) I.run_lag = std::min<uint32_t>(4096, (uint32_t)std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("KSG_RUN_NORES")) I.run_need_extra = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
   if (const char* e = std::getenv("KSG_WIN_RUN")) I.win_run_on = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_WIN_MB")) I.win_mblocks = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_RUN_SPIN")) I.run_spin = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("KSG_RUN_WAIT_US"))
     I.run_wait_us = std::max<uint32_t>(10, std::min<uint32_t>(1000000, (uint32_t)std::strtoul(e, nullptr, 10)));
@@ -5300,11 +5378,11 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     uint32_t T = eval_tiles(I.N, I.n_cus);
     size_t Nn = std::max<uint32_t>(I.N, 1);
     if (!I.tile_top.alloc((size_t)tt_ring() * KSG_BATCH * T * KSG_TOPK, err) || !I.tfeas.alloc((size_t)tt_ring() * KSG_BATCH * T * 3, err) ||
-        !I.arrive.alloc(2 * KSG_BATCH, err) || !I.pend_n.alloc(2, err) || !I.wrec.alloc(2 * kRecBytes, err) ||
+        !I.arrive.alloc(2 * KSG_BATCH * 32, err) || !I.pend_n.alloc(2, err) || !I.wrec.alloc(2 * kRecBytes, err) ||
         !I.pend.alloc(2 * KSG_BATCH, err) || !I.bfilter.alloc(Nn * 2 * KSG_BATCH, err) ||
         !I.bscore.alloc(Nn * 2 * KSG_BATCH * KSG_MAX_PLUGINS, err) || !I.btotal.alloc(Nn * 2 * KSG_BATCH, err))
       return false;
-    HIPCHK(hipMemsetAsync(I.arrive.p, 0, 2 * KSG_BATCH * 4, s));
+    HIPCHK(hipMemsetAsync(I.arrive.p, 0, 2 * KSG_BATCH * 32 * 4, s));
     HIPCHK(hipMemsetAsync(I.pend_n.p, 0, 2 * 4, s));
     HIPCHK(hipMemsetAsync(I.wrec.p, 0, 2 * kRecBytes, s));
   }
@@ -5458,6 +5536,8 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     }
   }
   I.n_samples = 0;
+  I.n_st = 0;
+  I.stat_pods_sampled = 0;
   static bool attr = false;
   if (!attr) {
     const void* fns[4] = {(const void*)k_window<0, false>, (const void*)k_window<1, false>,
@@ -5488,6 +5568,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   A.tile_top = I.tile_top.p;
   A.tile_feas = I.tfeas.p;
   A.arrive = I.arrive.p;
+  A.astride = 1;
   A.sums = I.sums.p;
   const bool sharded = I.xranks > 1;
   A.xrows = nullptr;
@@ -5540,8 +5621,22 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     HIPCHK(hipMemsetAsync(I.mpred.p + 2 * (size_t)(q0 - first), 0xFF, 2 * (size_t)cn * sizeof(int64_t), st));
     const dim3 sgrid(std::max<uint32_t>((I.N + 256 * KSG_ST_NPT - 1) / (256 * KSG_ST_NPT), 1),
                      (cn + KSG_ST_PODS - 1) / KSG_ST_PODS);
+    const bool ssamp = I.sample_every && st == s;
+    if (ssamp) {
+      while (I.sev_st.size() < 2 * (size_t)(I.n_st + 1)) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        I.sev_st.push_back(e);
+      }
+      HIPCHK(hipEventRecord(I.sev_st[2 * I.n_st], st));
+    }
     hipLaunchKernelGGL(k_static, sgrid, dim3(256), 0, st, C, I.F, I.progs.p, I.prog_off_d.p, q0, cn,
                        I.stat.p + (size_t)((q0 - first) % (nslots * chunk)) * I.N, I.mpred.p + 2 * (size_t)(q0 - first));
+    if (ssamp) {
+      HIPCHK(hipEventRecord(I.sev_st[2 * I.n_st + 1], st));
+      I.stat_pods_sampled += cn;
+      I.n_st++;
+    }
     if (side) HIPCHK(hipEventRecord(I.sev_ready[c % 3], st));
     return true;
   };
@@ -5555,6 +5650,8 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   // the persistent window loop: one launch for every window (its blocks all
   // resident: one per CU); not co-resident -> the launch-per-window loop below
   if (!sharded && !stat && I.win_run_on && nwin > 0 && 1 + (uint64_t)KSG_BATCH * T <= I.n_cus) {
+    // dedicated merge blocks (one per pod) when they fit beside the tile blocks
+    const bool mb = I.win_mblocks && 1 + (uint64_t)KSG_BATCH * (T + 1) <= I.n_cus;
     if (!I.wsync.alloc(1, err) || !I.rsync.alloc(1, err)) return false;
     if (!I.hverdict) {
       HIPCHK(hipHostMalloc((void**)&I.hverdict, 64, hipHostMallocCoherent | hipHostMallocMapped));
@@ -5568,7 +5665,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     }
     HIPCHK(hipMemsetAsync(I.wsync.p, 0, sizeof(WinSync), s));
     HIPCHK(hipMemsetAsync(I.rsync.p, 0, kRunSyncReset, s));
-    HIPCHK(hipMemsetAsync(I.arrive.p, 0, 2 * KSG_BATCH * sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(I.arrive.p, 0, 2 * KSG_BATCH * 32 * sizeof(uint32_t), s));
     WinRunArgs R{};
     R.nwin = nwin;
     R.first = first;
@@ -5583,15 +5680,18 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     R.pend_n = I.pend_n.p;
     R.arrive = I.arrive.p;
     R.stamps = I.stamps_on ? I.stamps.p : nullptr;
-    const uint32_t grid = 1 + KSG_BATCH * T;
+    const uint32_t grid = 1 + KSG_BATCH * T + (mb ? KSG_BATCH : 0);
+    WinArgs AP = A;
+    AP.mblocks = mb ? 1u : 0u;
+    AP.astride = 32;
     __atomic_store_n(I.hverdict, 0u, __ATOMIC_RELEASE);
     const RunCtl RC{grid + I.run_need_extra, I.run_wait_us * 100u, 0, I.hverdict, I.run_spin};
     const bool sampled = I.sample_every && I.n_samples * 2 + 2 <= I.sev.size();
     if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
     if (I.eval_mode == 1)
-      hipLaunchKernelGGL(k_window_run<1>, dim3(grid), dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, A, R, I.rsync.p, I.wsync.p, RC);
+      hipLaunchKernelGGL(k_window_run<1>, dim3(grid), dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, AP, R, I.rsync.p, I.wsync.p, RC);
     else
-      hipLaunchKernelGGL(k_window_run<0>, dim3(grid), dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, A, R, I.rsync.p, I.wsync.p, RC);
+      hipLaunchKernelGGL(k_window_run<0>, dim3(grid), dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, AP, R, I.rsync.p, I.wsync.p, RC);
     if (sampled) {
       HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
       I.n_samples++;
@@ -7087,6 +7187,19 @@ bool Engine::kernel_time(float& avg_ms, uint32_t& samples, std::string& err) {
   return true;
 }
 
+bool Engine::static_time(float& total_ms, uint32_t& launches, uint64_t& pods, std::string& err) {
+  Impl& I = *p_;
+  double tot = 0;
+  for (uint32_t i = 0; i < I.n_st; ++i) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, I.sev_st[2 * i], I.sev_st[2 * i + 1]));
+    tot += ms;
+  }
+  total_ms = (float)tot;
+  launches = I.n_st;
+  pods = I.stat_pods_sampled;
+  return true;
+}
 uint32_t Engine::n_nodes() const { return p_->N; }
 void* Engine::stream() const { return p_->stream; }
 float Engine::last_ms() const { return p_->last_ms; }

@@ -3109,6 +3109,19 @@ struct Cluster {
     z ^= z >> 31;
     return ((0xFFFFFull - (z >> 44)) << 20) | (uint64_t)g;
   }
+  // The batched victim search applies (see preempt): removing pods changes
+  // nothing the pod's filters read but the node they are removed from.
+  uint64_t preempt_batched_runs = 0;  // diagnostic: pods whose dry run took the batched search
+  bool preempt_no_batch = std::getenv("KSG_PREEMPT_BATCH") && std::strtol(std::getenv("KSG_PREEMPT_BATCH"), nullptr, 10) == 0;
+  bool preempt_batched(const Pod& p, const ksg_pod_summary& S) const {
+    if (preempt_no_batch) return false;
+    if (!p.tsc.empty() || !p.req_aff.empty() || !p.req_anti.empty() || (S.ipa_flags & 4u)) return false;
+    for (auto& cn : p.claims) {
+      const PVC* c = pvc_of(p.ns, cn);
+      if (c && c->rwop) return false;
+    }
+    return true;
+  }
   bool preempt(uint32_t q, const ksg_pod_summary& S) {
     if (nom.size() < queue.size()) nom.resize(queue.size());
     nom[q] = Nomination();
@@ -3194,30 +3207,100 @@ struct Cluster {
       vector<Vic> victims;
     };
     vector<Cand> cands;
-    for (int32_t g : potential) {
-      vector<Vic>& pv = on[g];
-      if (pv.empty()) continue;  // "No preemption victims found for incoming pod"
-      bool ok = false;
-      if (!toggle(pv, g, -1) || !fits(g, ok)) return false;
-      if (!ok) {
-        if (!toggle(pv, g, +1)) return false;
-        continue;
-      }
-      std::sort(pv.begin(), pv.end(), [](const Vic& a, const Vic& b) {  // util.MoreImportantPod
-        if (a.prio != b.prio) return a.prio > b.prio;
-        if (a.start != b.start) return a.start < b.start;
-        return a.order < b.order;
-      });
-      Cand c{g, {}};
-      for (auto& v : pv) {  // reprieve: most important first
-        if (!toggle({v}, g, +1) || !fits(g, ok)) return false;
-        if (!ok) {
-          if (!toggle({v}, g, -1)) return false;
-          c.victims.push_back(v);
+    auto more_important = [](const Vic& a, const Vic& b) {  // util.MoreImportantPod
+      if (a.prio != b.prio) return a.prio > b.prio;
+      if (a.start != b.start) return a.start < b.start;
+      return a.order < b.order;
+    };
+    if (preempt_batched(p, S)) {
+      // Batched search (every potential node at once).  Removing a node's victims
+      // changes only that node (its row, host ports, attached volumes): the pod
+      // has no spread constraint, no (anti)affinity term, no existing pod's
+      // anti-affinity applies to it and it holds no ReadWriteOncePod claim, so its
+      // PreFilter state is the same whatever is removed, and the victim sets of
+      // different nodes are disjoint.  One dry run with every potential node's
+      // victims removed answers SelectVictimsOnNode's first question for all of
+      // them; the reprieve then runs in lockstep over the candidates, one dry run
+      // per round (its i-th most important victim re-added on every candidate).
+      auto toggle_many = [&](const vector<std::pair<int32_t, Vic>>& vs, int sign) {
+        if (vs.empty()) return true;
+        vector<const vector<uint8_t>*> pp;
+        vector<int32_t> gn, rows;
+        for (auto& gv : vs) {
+          const Vic& v = gv.second;
+          pp.push_back(v.bound >= 0 ? &bprog[v.bound] : &progs[v.qpod]);
+          gn.push_back(gv.first + (int32_t)lo);
+          rows.push_back(v.bound >= 0 ? (tables_on() ? bound_row[v.bound] : -1) : qrows[v.qpod]);
         }
+        return eng->toggle_pods(pp, gn, rows, sign, err);
+      };
+      vector<std::pair<int32_t, Vic>> all;
+      for (int32_t g : potential)
+        for (auto& v : on[g]) all.push_back({g, v});
+      if (all.empty()) return true;
+      vector<uint32_t> codes;
+      if (!toggle_many(all, -1) || !eng->dry_filter(q, -1, codes, err) || !toggle_many(all, +1)) return false;
+      vector<vector<Vic>> pv;  // per candidate: its victims, most important first
+      for (int32_t g : potential) {
+        if (on[g].empty() || codes[g] != KSG_FILTER_PASS) continue;
+        cands.push_back(Cand{g, {}});
+        pv.push_back(on[g]);
+        std::sort(pv.back().begin(), pv.back().end(), more_important);
       }
-      if (!toggle(c.victims, g, +1)) return false;  // the dry run leaves the state as it was
-      if (!c.victims.empty()) cands.push_back(std::move(c));
+      vector<std::pair<int32_t, Vic>> off;  // every candidate's victims off, then reprieve round by round
+      size_t rounds = 0;
+      for (size_t c = 0; c < cands.size(); ++c) {
+        for (auto& v : pv[c]) off.push_back({cands[c].node, v});
+        rounds = std::max(rounds, pv[c].size());
+      }
+      if (!toggle_many(off, -1)) return false;
+      ++preempt_batched_runs;
+      for (size_t r = 0; r < rounds; ++r) {
+        vector<std::pair<int32_t, Vic>> back, keep_off;
+        vector<size_t> who;
+        for (size_t c = 0; c < cands.size(); ++c)
+          if (r < pv[c].size()) {
+            back.push_back({cands[c].node, pv[c][r]});
+            who.push_back(c);
+          }
+        if (!toggle_many(back, +1) || !eng->dry_filter(q, -1, codes, err)) return false;
+        for (size_t i = 0; i < who.size(); ++i)
+          if (codes[cands[who[i]].node] != KSG_FILTER_PASS) {  // it must go: a victim
+            keep_off.push_back(back[i]);
+            cands[who[i]].victims.push_back(back[i].second);
+          }
+        if (!toggle_many(keep_off, -1)) return false;
+      }
+      vector<std::pair<int32_t, Vic>> restore;  // the dry run leaves the state as it was
+      for (auto& c : cands)
+        for (auto& v : c.victims) restore.push_back({c.node, v});
+      if (!toggle_many(restore, +1)) return false;
+      vector<Cand> kept;
+      for (auto& c : cands)
+        if (!c.victims.empty()) kept.push_back(std::move(c));
+      cands.swap(kept);
+    } else {
+      for (int32_t g : potential) {
+        vector<Vic>& pvg = on[g];
+        if (pvg.empty()) continue;  // "No preemption victims found for incoming pod"
+        bool ok = false;
+        if (!toggle(pvg, g, -1) || !fits(g, ok)) return false;
+        if (!ok) {
+          if (!toggle(pvg, g, +1)) return false;
+          continue;
+        }
+        std::sort(pvg.begin(), pvg.end(), more_important);
+        Cand c{g, {}};
+        for (auto& v : pvg) {  // reprieve: most important first
+          if (!toggle({v}, g, +1) || !fits(g, ok)) return false;
+          if (!ok) {
+            if (!toggle({v}, g, -1)) return false;
+            c.victims.push_back(v);
+          }
+        }
+        if (!toggle(c.victims, g, +1)) return false;  // the dry run leaves the state as it was
+        if (!c.victims.empty()) cands.push_back(std::move(c));
+      }
     }
     if (cands.empty()) return true;
     // pickOneNodeForPreemption: fewest PDB violations (none here), lowest highest
@@ -4331,6 +4414,14 @@ extern "C" int ksg_debug_path_counts(ksg_ctx* ctx, uint64_t* out) {
   return KSG_OK;
 }
 
+// diagnostic (not in ksg.h): DefaultPreemption dry runs that took the batched search
+extern "C" int ksg_debug_preempt_batched(ksg_ctx* ctx, uint64_t* out) {
+  KSG_LOCK(ctx);
+  if (!ctx || !out) return KSG_E_INVALID;
+  *out = ctx->c.preempt_batched_runs;
+  return KSG_OK;
+}
+
 int ksg_nccl_unique_id(uint8_t* out128) {
   std::string err;
   if (!out128) return KSG_E_INVALID;
@@ -4348,6 +4439,14 @@ int ksg_set_exchange(ksg_ctx* ctx, int mode, const uint8_t* nccl_id, ksg_exchang
 int ksg_batch_path(const ksg_ctx* ctx) {
   KSG_LOCK(ctx);
   return ctx ? (ctx->c.eng->batch_path() ? 1 : 0) : KSG_E_INVALID;
+}
+
+// diagnostic (not in ksg.h): the sampled run's k_static launches (cfg3 roofline)
+extern "C" int ksg_debug_static_time(ksg_ctx* ctx, float* total_ms, uint32_t* launches, uint64_t* pods) {
+  KSG_LOCK(ctx);
+  if (!ctx || !total_ms || !launches || !pods) return KSG_E_INVALID;
+  if (!ctx->c.eng->static_time(*total_ms, *launches, *pods, ctx->c.err)) return ctx->fail(ctx->c.err, KSG_E_DEVICE);
+  return KSG_OK;
 }
 
 int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples) {

@@ -347,6 +347,27 @@ class Scheduler:
     def batch_path(self) -> bool:
         return self.L.ksg_batch_path(self.h) == 1
 
+    def static_time(self):
+        """Diagnostic: (total ms, launches, pods) of the sampled run's k_static launches."""
+        ms, n, pods = ctypes.c_float(), ctypes.c_uint32(), ctypes.c_uint64()
+        self.L.ksg_debug_static_time.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        self._chk(self.L.ksg_debug_static_time(self.h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(pods)),
+                  "ksg_debug_static_time")
+        return ms.value, n.value, pods.value
+
+    def preempt_batched(self):
+        """Diagnostic: DefaultPreemption dry runs that took the batched victim search."""
+        out = ctypes.c_uint64()
+        self.L.ksg_debug_preempt_batched.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self._chk(self.L.ksg_debug_preempt_batched(self.h, ctypes.byref(out)), "ksg_debug_preempt_batched")
+        return out.value
+
+    def window_runs(self):
+        """Diagnostic: persistent window launches (k_window_run) so far."""
+        out = (ctypes.c_uint64 * 8)()
+        self._chk(self.L.ksg_debug_path_counts(self.h, out), "ksg_debug_path_counts")
+        return out[7]
+
     def kernel_time(self):
         ms, n = ctypes.c_float(), ctypes.c_uint32()
         self._chk(self.L.ksg_kernel_time(self.h, ctypes.byref(ms), ctypes.byref(n)), "ksg_kernel_time")

@@ -225,6 +225,12 @@ bool Engine::outputs(uint32_t prog_idx, PodOutputs& out, std::string& err) {
   return true;
 }
 bool Engine::sync(std::string&) { return true; }
+bool Engine::static_time(float& total_ms, uint32_t& launches, uint64_t& pods, std::string&) {
+  total_ms = 0;
+  launches = 0;
+  pods = 0;
+  return true;
+}
 bool Engine::reset(std::string&) { return true; }
 void Engine::sample_kernel(uint32_t) {}
 void Engine::set_path(int) {}

@@ -1,0 +1,79 @@
+"""DefaultPreemption dry-run latency at scale: pods that fit nowhere without
+preempting, on a cluster of N nodes full of lower-priority bound pods
+(ksg/edge.py's preempt family, queue pods made large and high-priority).  Each
+queue run stops after every pod that may preempt and runs its dry run on the
+device state of its own cycle (host.cpp Cluster::preempt), so the wall time per
+pod is the cycle plus the victim search.  The batched search (every potential
+node in one dry run, the reprieve in lockstep) and the per-node probes run in
+separate processes (KSG_PREEMPT_BATCH); their nominations must agree.
+
+usage: python tools/bench_preempt.py [--nodes 50000] [--pods 8] [--per-node-pods 1]"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
+
+
+def make_doc(nodes, pods):
+    from ksg import edge
+    doc = edge.gen_preempt(n_nodes=nodes, n_existing=4 * nodes, n_pods=pods)
+    for p in doc["queue"]:
+        sp = p["spec"]
+        sp["priority"] = 5000
+        for k in ("preemptionPolicy", "topologySpreadConstraints", "affinity", "nodeSelector", "tolerations"):
+            sp.pop(k, None)
+        for c in sp["containers"]:
+            c["resources"] = {"requests": {"cpu": "3500m", "memory": "2Gi"}}
+            c.pop("ports", None)
+    return doc
+
+
+def one(batch, nodes, pods):
+    env = dict(os.environ, KSG_PREEMPT_BATCH=str(batch))
+    code = f"""
+import json, sys, time
+sys.path.insert(0, {os.path.join(ROOT, 'tools')!r})
+sys.path.insert(0, {os.path.join(ROOT, 'kube-scheduler-simulator-p9_amd')!r})
+import torch
+from bench_preempt import make_doc
+from ksg import Scheduler
+doc = make_doc({nodes}, {pods})
+s = Scheduler(doc["profile"])
+s.load_cluster(doc)
+t = time.perf_counter()
+s.schedule()
+dt = time.perf_counter() - t
+noms = [s.postfilter_result(q) for q in range(s.queue_len)]
+print(json.dumps({{"ms_per_pod": dt * 1e3 / s.queue_len, "nominated": sum(1 for n in noms if n[0] >= 0),
+                  "batched": s.preempt_batched(), "noms": noms,
+                  "res": [(r.selected, r.feasible, r.status) for r in s.results()]}}))
+"""
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=900)
+    if out.returncode != 0:
+        raise RuntimeError(out.stderr[-3000:])
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=50000)
+    ap.add_argument("--pods", type=int, default=8)
+    ap.add_argument("--per-node-pods", type=int, default=1)
+    a = ap.parse_args()
+    b = one(1, a.nodes, a.pods)
+    p = one(0, a.nodes, a.per_node_pods)
+    k = a.per_node_pods
+    print(json.dumps({"nodes": a.nodes, "bound_pods": 4 * a.nodes,
+                      "batched": {"pods": a.pods, "ms_per_pod": b["ms_per_pod"], "nominated": b["nominated"],
+                                  "batched_searches": b["batched"]},
+                      "per_node": {"pods": k, "ms_per_pod": p["ms_per_pod"], "nominated": p["nominated"]},
+                      "same_nominations": b["noms"][:k] == p["noms"][:k] and b["res"][:k] == p["res"][:k]}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -77,6 +77,11 @@ struct NodeSoA {
   // [slot][global_n] (value id, -1 none) — the pair-level class-table deltas
   // of an assume on another rank's node (every rank keeps the global tables)
   uint32_t shards = 1;
+  // node-sharded Taint / NodeAffinity windows: every node's static data (labels,
+  // taints) on every rank, so that each rank holds every (pod, node) static record
+  std::vector<int32_t> g_label_vid;   // [n_keys][global_n], empty when not needed
+  std::vector<uint32_t> g_taint_off;  // [global_n + 1]
+  std::vector<int32_t> g_taint_id;
   std::vector<int32_t> gtopo;
 };
 

@@ -1962,8 +1962,10 @@ struct StaticRec {
 // the label loads' latency behind (the work per pair is a few dependent loads).
 #define KSG_ST_PODS 4
 #define KSG_ST_NPT 1
+// glob: C covers every node of a node-sharded cluster (the PreFilterResult's
+// global bitmap applies)
 __global__ __launch_bounds__(256) void k_static(DevCluster C, DevProfile F, const uint8_t* __restrict__ progs, const uint64_t* __restrict__ prog_off,
-                                                uint32_t q0, uint32_t count, StaticRec* out, int64_t* mpred) {
+                                                uint32_t q0, uint32_t count, StaticRec* out, int64_t* mpred, int glob) {
   const uint32_t base = blockIdx.x * (256 * KSG_ST_NPT) + threadIdx.x;
 #pragma unroll 1
   for (uint32_t pi = 0; pi < KSG_ST_PODS; ++pi) {
@@ -1979,7 +1981,8 @@ __global__ __launch_bounds__(256) void k_static(DevCluster C, DevProfile F, cons
       if (n >= C.N) continue;
       uint32_t code = KSG_FILTER_PASS, raw = 0;
       if ((h->flags & KPF_PREFILTER_REJECT) ||
-          ((h->flags & KPF_RESTRICT) && !bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n))) {
+          ((h->flags & KPF_RESTRICT) && !(glob ? bit(V.u32 + h->restrict_g_off, h->restrict_g_words, (int32_t)n)
+                                               : bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n)))) {
         code = KSG_FILTER_NOT_EVALUATED;
       } else {
 #pragma unroll 1
@@ -2283,6 +2286,8 @@ struct WinArgs {
   // stat_ring queue pods (pod q at slot (q - first) % stat_ring) and their static maxima
   const StaticRec* stat;
   uint32_t stat_ring;
+  uint32_t stat_n, stat_base;  // a record row holds stat_n nodes from global node stat_base (node-sharded: every node)
+  uint32_t G;                  // nodes of the whole cluster
   const int64_t* mpred;  // [2 * (q - first)]: Taint, NodeAffinity (-1: no statically feasible node)
   // sharded: replica of every node's row, indexed by global node (kept in step by
   // every rank's identical replay); null on one shard
@@ -2304,8 +2309,9 @@ struct WinArgs {
   uint32_t mblocks;   // persistent loop: dedicated merge blocks (one per pod) merge the tile lists
   uint32_t astride;   // arrival counter stride (u32): 1, or 32 in the persistent loop (a line per pod)
 };
-__device__ __forceinline__ const StaticRec* srec_row(const WinArgs& A, uint32_t q, uint32_t N) {
-  return A.stat + (size_t)((q - A.first) % A.stat_ring) * N;
+// the static record of (queue pod q, global node g)
+__device__ __forceinline__ StaticRec srec_at(const WinArgs& A, uint32_t q, uint32_t g) {
+  return A.stat[(size_t)((q - A.first) % A.stat_ring) * A.stat_n + (g - A.stat_base)];
 }
 __device__ __forceinline__ int64_t sel4(const int64_t (&v)[4], int i) {
   return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3];
@@ -3638,7 +3644,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
       const int hit = pend_lds((int32_t)(C.goff + nn));
       if (hit >= 0) r = ld_obj<PER>(&A.pprev[hit].after);
       else if (!loaded) load_row_p<PER>(C, nn, A.need_eph, r);
-      if (STAT) sr = srec_row(A, q, C.N)[nn];
+      if (STAT) sr = srec_at(A, q, C.goff + nn);
     }
   };
   StaticRec snext{KSG_FILTER_PASS, 0};
@@ -3902,7 +3908,8 @@ template <bool PER = false>
 __device__ __forceinline__ void origin_rows(const DevCluster& C, const WinLDS& L, const WinArgs& A, int32_t o,
                                             RowV& start, RowV& snap) {
   if (o & KSG_ORG_NODE) {
-    load_row(C, (uint32_t)(o & 0xFFFFF) - C.goff, A.need_eph, start);
+    if (A.xrows) start = A.xrows[o & 0xFFFFF];  // (node-sharded: the replica holds every node)
+    else load_row(C, (uint32_t)(o & 0xFFFFF) - C.goff, A.need_eph, start);
     snap = start;
   } else if (o < KSG_BATCH) {
     start = L.prior[o].after;
@@ -3952,13 +3959,15 @@ __device__ __forceinline__ uint64_t max3u(uint64_t a, uint64_t b, uint64_t c) {
   return m > c ? m : c;
 }
 
-// Pod b's row of local node i under the picks S of the pods < b.
+// Pod b's row of global node g under the picks S of the pods < b (a local node's
+// row from the node rows, another shard's from the replica).
 __device__ __forceinline__ void row_under(const DevCluster& C, const WinLDS& L, const WinArgs& A, const int32_t* S,
-                                          const PickTab& T, int b, uint32_t i, uint32_t R, RowV& r) {
-  const int32_t g = (int32_t)(C.goff + i);
+                                          const PickTab& T, int b, uint32_t gu, uint32_t R, RowV& r) {
+  const int32_t g = (int32_t)gu;
   const int e = prior_of(L, g);
   if (e >= 0) r = L.prior[e].after;
-  else load_row(C, i, A.need_eph, r);
+  else if (A.xrows) r = A.xrows[g];
+  else load_row(C, gu - C.goff, A.need_eph, r);
   const int hs = tab_find(T.node, g);
   if (hs >= 0 && T.first[hs] < b) {
     Delta cum{};
@@ -3975,16 +3984,17 @@ __device__ __forceinline__ void win_exact_select(const DevCluster& C, const DevP
                                               int b, int cur, int nxt, uint32_t R) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const PodLite* h = &L.pod[b];
-  const StaticRec* st = srec_row(A, A.w0 + b, C.N);
   const int32_t* S = L.S[cur];
   const PickTab& T = L.pick[cur];
+  // every node of the cluster: node-sharded, from the replica and the global records
+  const uint32_t g0 = A.xrows ? 0u : C.goff, gn = A.xrows ? A.G : C.N;
   int32_t feas = 0;
   int64_t lt = 0, la = 0;
 #pragma unroll 1
-  for (uint32_t i = tid; i < C.N; i += KSG_WIN_THREADS) {
+  for (uint32_t i = tid; i < gn; i += KSG_WIN_THREADS) {
     RowV r;
-    row_under(C, L, A, S, T, b, i, R, r);
-    const StaticRec sr = st[i];
+    row_under(C, L, A, S, T, b, g0 + i, R, r);
+    const StaticRec sr = srec_at(A, A.w0 + b, g0 + i);
     int32_t fs, bs;
     int64_t tot;
     if (eval_row_s<MODE>(r, F, h, R, sr, 0, 0, fs, bs, tot) == KSG_FILTER_PASS) {
@@ -4011,13 +4021,13 @@ __device__ __forceinline__ void win_exact_select(const DevCluster& C, const DevP
   }
   uint64_t best = 0;
 #pragma unroll 1
-  for (uint32_t i = tid; i < C.N; i += KSG_WIN_THREADS) {
+  for (uint32_t i = tid; i < gn; i += KSG_WIN_THREADS) {
     RowV r;
-    row_under(C, L, A, S, T, b, i, R, r);
+    row_under(C, L, A, S, T, b, g0 + i, R, r);
     int32_t fs, bs;
     int64_t tot;
-    if (eval_row_s<MODE>(r, F, h, R, st[i], mt, ma, fs, bs, tot) == KSG_FILTER_PASS) {
-      const uint64_t k = pack_key(tot, F.seed, h->queue_idx, C.goff + i);
+    if (eval_row_s<MODE>(r, F, h, R, srec_at(A, A.w0 + b, g0 + i), mt, ma, fs, bs, tot) == KSG_FILTER_PASS) {
+      const uint64_t k = pack_key(tot, F.seed, h->queue_idx, g0 + i);
       best = k > best ? k : best;
     }
   }
@@ -4050,16 +4060,15 @@ template <int MODE>
 __device__ __forceinline__ void win_exact_write(const DevCluster& C, const DevProfile& F, const WinArgs& A, WinLDS& L,
                                              int b, int cur, uint32_t R) {
   const PodLite* h = &L.pod[b];
-  const StaticRec* st = srec_row(A, A.w0 + b, C.N);
   uint32_t* of;
   int32_t *os, *ot;
   out_ptrs(A, A.w0 + b, C.N, of, os, ot);
   const int64_t mt = L.xmt[b], ma = L.xma[b];
 #pragma unroll 1
-  for (uint32_t i = threadIdx.x; i < C.N; i += KSG_WIN_THREADS) {
+  for (uint32_t i = threadIdx.x; i < C.N; i += KSG_WIN_THREADS) {  // (this shard's outputs)
     RowV r;
-    row_under(C, L, A, L.S[cur], L.pick[cur], b, i, R, r);
-    const StaticRec sr = st[i];
+    row_under(C, L, A, L.S[cur], L.pick[cur], b, C.goff + i, R, r);
+    const StaticRec sr = srec_at(A, A.w0 + b, C.goff + i);
     int32_t fs, bs;
     int64_t tot;
     const uint32_t code = eval_row_s<MODE>(r, F, h, R, sr, mt, ma, fs, bs, tot);
@@ -4232,7 +4241,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       StaticRec sr{KSG_FILTER_PASS, 0};
       uint32_t code;
       if (STAT) {
-        sr = srec_row(A, A.w0 + pb, C.N)[(uint32_t)pe.node - C.goff];
+        sr = srec_at(A, A.w0 + pb, (uint32_t)pe.node);
         code = eval_row_s<MODE>(pe.after, F, h, R, sr, L.mt[pb], L.ma[pb], fs, bs, tot);
       } else {
         code = eval_row<MODE>(pe.after, F, h, R, fs, bs, tot);
@@ -4379,7 +4388,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
               StaticRec sr{KSG_FILTER_PASS, 0};
               uint32_t code;
               if (STAT) {
-                sr = srec_row(A, A.w0 + b, C.N)[(uint32_t)Sv - C.goff];
+                sr = srec_at(A, A.w0 + b, (uint32_t)Sv);
                 code = eval_row_s<MODE>(cur_r, F, h, R, sr, L.mt[b], L.ma[b], fs, bs, tot);
               } else {
                 code = eval_row<MODE>(cur_r, F, h, R, fs, bs, tot);
@@ -4953,6 +4962,9 @@ struct Engine::Impl {
   // cross-rank sum of their pair-level entries (UINT32_MAX: none pending)
   uint32_t shards = 1;
   DBuf<int32_t> gtopo_d;
+  DBuf<int32_t> glabel, gtid;  // node-sharded static records: every node's labels [K][G] and taints (CSR)
+  DBuf<uint32_t> gtoff;
+  bool gstat = false;
   uint32_t red_pc0 = UINT32_MAX, red_tc0 = UINT32_MAX;
   std::vector<int32_t> tc_slot_h;
   DBuf<TabSeg> segs_d;
@@ -5076,6 +5088,18 @@ struct Engine::Impl {
     for (int s = 0; s < KSG_MAX_TOPO; ++s) {
       C.tkeyv[s] = (size_t)s < topo.topo_key.size() ? topo.topo_key[s] : -1;
       C.nubv[s] = ((size_t)s < topo.nu_base.size() && topo.nu_base[s] != 0xFFFFFFFFu) ? (int32_t)topo.nu_base[s] : -1;
+    }
+    return C;
+  }
+  // k_static over every node of a node-sharded cluster (the replicated static columns)
+  DevCluster cluster_static() const {
+    DevCluster C = cluster();
+    if (gstat) {
+      C.N = G;
+      C.goff = 0;
+      C.label = glabel.p;
+      C.toff = gtoff.p;
+      C.tid = gtid.p;
     }
     return C;
   }
@@ -5235,6 +5259,18 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
       I.taint_dup |= (seen & b) != 0;
       seen |= b;
     }
+  }
+  I.gstat = !ns.g_label_vid.empty();
+  if (I.gstat) {
+    if (ns.g_label_vid.size() != (size_t)ns.n_keys * I.G || ns.g_taint_off.size() != (size_t)I.G + 1) {
+      err = "sharded upload: global static columns do not match the cluster";
+      return false;
+    }
+    for (uint32_t g = 0; g < I.G; ++g) I.max_taints = std::max(I.max_taints, ns.g_taint_off[g + 1] - ns.g_taint_off[g]);
+    std::vector<int32_t> gl = ns.g_label_vid, gt = ns.g_taint_id;
+    gl.resize(std::max<size_t>(gl.size(), 1), -1);
+    gt.resize(std::max<size_t>(gt.size(), 1), 0);
+    if (!I.glabel.upload(gl, s, err) || !I.gtoff.upload(ns.g_taint_off, s, err) || !I.gtid.upload(gt, s, err)) return false;
   }
   if (I.max_taints >= 4096) I.static_fits = false;
   I.R = ns.n_res;
@@ -5599,8 +5635,14 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   const bool side = stat && I.sstream && I.static_side;
   const uint32_t nslots = side ? 3 : 2;
   uint32_t chunk = 0, nchunks = 0;
+  const bool gstat = stat && I.gstat && sharded;  // node-sharded: records over every node
+  const DevCluster CS = gstat ? I.cluster_static() : C;
+  const uint32_t SN = gstat ? I.G : I.N;
+  A.stat_n = std::max<uint32_t>(SN, 1);
+  A.stat_base = gstat ? 0 : I.goff;
+  A.G = I.G;
   if (stat) {
-    const size_t Nn = std::max<uint32_t>(I.N, 1);
+    const size_t Nn = std::max<uint32_t>(SN, 1);
     const size_t budget = side ? ((size_t)32 << 20) : ((size_t)64 << 20);
     chunk = (uint32_t)std::max<size_t>(KSG_BATCH, (budget / (Nn * sizeof(StaticRec))) / KSG_BATCH * KSG_BATCH);
     chunk = std::min<uint32_t>(chunk, (count + KSG_BATCH - 1) / KSG_BATCH * KSG_BATCH);
@@ -5619,7 +5661,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   auto issue_static = [&](uint32_t c, hipStream_t st) -> bool {
     const uint32_t q0 = first + c * chunk, cn = std::min(chunk, first + count - q0);
     HIPCHK(hipMemsetAsync(I.mpred.p + 2 * (size_t)(q0 - first), 0xFF, 2 * (size_t)cn * sizeof(int64_t), st));
-    const dim3 sgrid(std::max<uint32_t>((I.N + 256 * KSG_ST_NPT - 1) / (256 * KSG_ST_NPT), 1),
+    const dim3 sgrid(std::max<uint32_t>((SN + 256 * KSG_ST_NPT - 1) / (256 * KSG_ST_NPT), 1),
                      (cn + KSG_ST_PODS - 1) / KSG_ST_PODS);
     const bool ssamp = I.sample_every && st == s;
     if (ssamp) {
@@ -5630,8 +5672,9 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
       }
       HIPCHK(hipEventRecord(I.sev_st[2 * I.n_st], st));
     }
-    hipLaunchKernelGGL(k_static, sgrid, dim3(256), 0, st, C, I.F, I.progs.p, I.prog_off_d.p, q0, cn,
-                       I.stat.p + (size_t)((q0 - first) % (nslots * chunk)) * I.N, I.mpred.p + 2 * (size_t)(q0 - first));
+    hipLaunchKernelGGL(k_static, sgrid, dim3(256), 0, st, CS, I.F, I.progs.p, I.prog_off_d.p, q0, cn,
+                       I.stat.p + (size_t)((q0 - first) % (nslots * chunk)) * A.stat_n, I.mpred.p + 2 * (size_t)(q0 - first),
+                       gstat ? 1 : 0);
     if (ssamp) {
       HIPCHK(hipEventRecord(I.sev_st[2 * I.n_st + 1], st));
       I.stat_pods_sampled += cn;
@@ -6631,7 +6674,7 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
       HIPCHK(hipMemsetAsync(I.mpred.p, 0xFF, 2 * (size_t)cn * sizeof(int64_t), s));  // -1: no statically feasible node
       const dim3 grid(std::max<uint32_t>((N + 256 * KSG_ST_NPT - 1) / (256 * KSG_ST_NPT), 1),
                       (cn + KSG_ST_PODS - 1) / KSG_ST_PODS);
-      hipLaunchKernelGGL(k_static, grid, dim3(256), 0, s, C, F, I.progs.p, I.prog_off_d.p, c0, cn, I.stat.p, I.mpred.p);
+      hipLaunchKernelGGL(k_static, grid, dim3(256), 0, s, C, F, I.progs.p, I.prog_off_d.p, c0, cn, I.stat.p, I.mpred.p, 0);
       for (uint32_t j = c0; j < c0 + cn; ++j) {
         const uint8_t* prog = I.progs.p + I.prog_off[j];
         const int mode = commit ? 1 : 0;
@@ -7171,7 +7214,8 @@ bool Engine::fixup_stamps(uint32_t count, std::vector<uint64_t>* out, std::strin
 bool Engine::batch_path() const {
   const Impl& I = *p_;
   if (!I.batch_ok || I.force_per_pod || I.R > 4) return false;
-  return !I.batch_static || (I.static_fits && I.xranks <= 1);  // static maxima: single shard for now
+  // node-sharded Taint / NodeAffinity windows: every rank holds every node's static data
+  return !I.batch_static || (I.static_fits && (I.xranks <= 1 || I.gstat));
 }
 
 bool Engine::kernel_time(float& avg_ms, uint32_t& samples, std::string& err) {

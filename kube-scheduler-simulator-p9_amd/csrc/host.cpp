@@ -1538,6 +1538,18 @@ struct Cluster {
         }
       }
     }
+    if (shards > 1 && (has_plugin("TaintToleration") || has_plugin("NodeAffinity"))) {
+      // every node's labels and taints (the sharded Taint / NodeAffinity window's
+      // static records cover the whole cluster on every rank)
+      S.g_label_vid.assign((size_t)K * G, -1);
+      S.g_taint_off.assign(G + 1, 0);
+      for (uint32_t g = 0; g < G; ++g) {
+        const Node& nd = nodes[g];
+        for (auto& kv : nd.labels) S.g_label_vid[(size_t)nkeys.get(kv.first) * G + g] = nvals[nkeys.get(kv.first)].get(kv.second);
+        for (auto& t : nd.taints) S.g_taint_id.push_back(taint_id[std::make_tuple(t.key, t.value, t.effect)]);
+        S.g_taint_off[g + 1] = (uint32_t)S.g_taint_id.size();
+      }
+    }
     S.taint_off.assign(n + 1, 0);
     for (uint32_t i = 0; i < n; ++i) {
       const Node& nd = nodes[lo + i];
@@ -2400,6 +2412,16 @@ struct Cluster {
             for (auto& nm : names) {
               int32_t g = node_names.get(nm);
               if (g >= (int32_t)lo && g < (int32_t)hi) P.u32[h.restrict_off + (g - lo) / 32] |= 1u << ((g - lo) % 32);
+            }
+            if (shards > 1) {  // (the sharded static records cover every node)
+              const uint32_t G = (uint32_t)nodes.size(), wg = (G + 31) / 32;
+              h.restrict_g_words = (int32_t)wg;
+              h.restrict_g_off = (int32_t)P.u32.size();
+              P.u32.resize(P.u32.size() + wg, 0);
+              for (auto& nm : names) {
+                const int32_t g = node_names.get(nm);
+                if (g >= 0) P.u32[h.restrict_g_off + g / 32] |= 1u << (g % 32);
+              }
             }
           }
         }

@@ -261,6 +261,8 @@ typedef struct ksg_prog {
   int32_t pref_w_off;
   int32_t restrict_words;   // PreFilterResult node bitmask (local nodes) in pool_u32
   int32_t restrict_off;
+  int32_t restrict_g_words; // ... over every node of the cluster (node-sharded static records), or 0
+  int32_t restrict_g_off;
 
   // ---- PodTopologySpread
   int32_t n_tsc_filter, n_tsc_score;

@@ -54,8 +54,9 @@ def test_host_exchange_gloo_world2():
         assert dict(out) == {0: 11, 1: 11}
 
 
-def _sharded_worker(rank, world, port, doc_json, out, batch=True):
+def _sharded_worker(rank, world, port, doc_json, out, batch=True, per_pod=False, env=None):
     sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
+    os.environ.update(env or {})
     dist = _init(rank, world, port)
     import json
     from ksg import Scheduler
@@ -63,6 +64,8 @@ def _sharded_worker(rank, world, port, doc_json, out, batch=True):
     s = Scheduler(doc["profile"], device=0, shard_rank=rank, shard_count=world)
     s.set_exchange_host(world)
     s.load_cluster(doc)
+    if per_pod:
+        s.set_path(True)
     assert s.batch_path == batch
     s.schedule()
     out[rank] = [(r.selected, r.feasible, r.status) for r in s.results()]
@@ -116,10 +119,46 @@ def test_sharded_per_pod_chain_matches_oracle(cfg, world):
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_sharded_worker, args=(world, port, json.dumps(doc), out, False), nprocs=world, join=True)
+        mp.spawn(_sharded_worker, args=(world, port, json.dumps(doc), out, False, cfg == 3), nprocs=world, join=True)
         for r in range(world):
             bad = [(q, out[r][q], want[q]) for q in range(len(want)) if out[r][q] != want[q]]
             assert not bad, f"rank {r}: {len(bad)} pods differ, first {bad[:4]}"
+
+
+# Sharded Taint / NodeAffinity windows: every rank holds every node's static data
+# (labels, taints) and computes every (pod, node) static record, so the static
+# maxima are global and the replay's exact re-evaluation (a pod left without a
+# feasible node at its static max) runs over every node from the row replica.
+def _static_docs():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from ksg import generator as g
+    from test_static_window_gpu import _fallback_doc, _tight_cfg3
+    return {"cfg3": lambda: g.generate(3, n_nodes=300, n_pods=250),
+            "tight": lambda: _tight_cfg3(),
+            "fallback-taint": lambda: _fallback_doc("taint"),
+            "fallback-na": lambda: _fallback_doc("na"),
+            "cfg3-15k": lambda: g.generate(3, n_nodes=15000, n_pods=400)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,world", [("cfg3", 2), ("cfg3", 3), ("tight", 2), ("tight", 3), ("fallback-taint", 2),
+                                        ("fallback-na", 3), ("cfg3-15k", 2)])
+def test_sharded_static_window_matches_oracle(case, world):
+    import json
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _oracle import Oracle
+    doc = _static_docs()[case]()
+    o = Oracle(doc)
+    o.schedule(record=0, workers=8)
+    want = [o.result(q) for q in range(o.n_queue)]
+    port = _free_port()
+    env = {"KSG_STATIC_CHUNK": "64"} if case == "cfg3" else {}  # (windows straddle static chunks)
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_sharded_worker, args=(world, port, json.dumps(doc), out, True, False, env), nprocs=world, join=True)
+        for r in range(world):
+            bad = [(q, out[r][q], want[q]) for q in range(len(want)) if out[r][q] != want[q]]
+            assert not bad, f"{case} rank {r}: {len(bad)} pods differ, first {bad[:4]}"
 
 
 def _sharded_events_worker(rank, world, port, doc_json, ev_json, k, out):

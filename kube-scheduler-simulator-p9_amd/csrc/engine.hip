@@ -3022,56 +3022,122 @@ __global__ __launch_bounds__(256) void k_whatif_rec2(DevCluster C, DevProfile F,
 #define KSG_WC_NPT 2   // default nodes per thread (KSG_WC_NPT=1|2|4)
 #define KSG_WC_TILE 4096  // nodes per block
 
-// Node selector term s on NPT nodes (local, in range) at once: one scalar
-// entry load per requirement for all of them (KPF_FLAT_NA), else node_sel each.
-template <int NPT>
-__device__ __forceinline__ void sel_multi(const DevCluster& C, const ProgView& V, const ksg_sel& s,
-                                          const uint32_t (&n)[NPT], bool (&ok)[NPT]) {
-  if (!(V.h->flags & KPF_FLAT_NA)) {
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) ok[k] = node_sel(C, V, s, n[k]);
-    return;
-  }
-  const bool kind = s.kind != 0;
-#pragma unroll
-  for (int k = 0; k < NPT; ++k) ok[k] = kind;
-  for (int i = 0; i < s.req_cnt; ++i) {
-    const ksg_freq* fp = V.fq + s.req_off + i;
-    bool any = false;
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      ok[k] &= freq_match(C, fp, n[k]);
-      any |= ok[k];
-    }
-    if (!__ballot(any)) break;
-  }
+// A pod of the class path, decoded once per step (k_wc_decode) into a fixed
+// layout that pass 1 reads with a few wide scalar loads per (pod, sub-tile):
+// the program's header fields it needs as ready operands, and its node
+// selector / required terms / preferred terms as ONE flat list of requirements,
+// each tagged with the bit of the term it belongs to.  Pass 1 then evaluates
+// every requirement on every node of the thread (no per-term loops, no ballots,
+// no pointer chasing through the program) and folds the outcomes into a
+// failed-term mask: bit 0 the node selector, bits 1..15 the required terms,
+// bits 16..22 the preferred terms.  Host-checked per pod (prog_need bit 19):
+// flattened requirements, <= 15 required terms, <= KSG_WC_MAXREQ requirements.
+#define KSG_WC_MAXREQ 24
+#define KSG_WC_PREF_BIT 16
+struct WcReq {          // 32 B
+  uint64_t col;         // the key's label column: element offset key * N into C.label
+  uint64_t arg;         // value-id mask (modes 0 / 1) or the global node index (2 / 3)
+  uint32_t gbit;        // the term's bit in the failed-term mask
+  uint32_t mode;        // 0 value in mask, 1 not in mask (or no value), 2 name ==, 3 name !=, 4 false
+  uint64_t pad;
+};
+struct WcPod {
+  uint32_t flags;       // bit 0: no node passes; bit 1: PreFilterResult bitmap
+  uint32_t nreq;        // requirements in req[]
+  uint32_t npf;         // scored preferred terms (the class's mask bits)
+  uint32_t reqmask;     // bits of the required terms (0: no required-terms filter)
+  uint64_t hw, pw;      // taint ids: untolerated NoSchedule/NoExecute, untolerated PreferNoSchedule
+  uint64_t hseed;       // tie-break hash seed of the pod
+  uint64_t roff;        // PreFilterResult bitmap (local nodes, rwords words): byte offset into A.progs
+  uint32_t rwords, pad0;
+  double q0, q1;        // Fit filter requests (-inf: not requested)
+  double fs0, fs1;      // Fit score requests
+  double bq0, bq1;      // BalancedAllocation requests
+  uint64_t pad1[3];     // (128-byte header)
+  WcReq req[KSG_WC_MAXREQ];
+};
+static_assert(sizeof(WcReq) == 32 && sizeof(WcPod) == 128 + 32 * KSG_WC_MAXREQ, "WcPod layout");
+
+// Is program h a class-path pod the decoder can flatten (prog_need bit 19)?
+__host__ __device__ inline bool wc_decodable(const ksg_prog* h) {
+  if (!(h->flags & KPF_FLAT_NA) || h->n_req_terms > 15 || h->n_pref_terms > 7) return false;
+  const ksg_sel* sel = reinterpret_cast<const ksg_sel*>(reinterpret_cast<const uint8_t*>(h) + h->off_sel);
+  auto cnt = [](const ksg_sel& x) { return x.kind == 0 ? 1 : x.req_cnt; };
+  int n = (h->flags & KPF_HAS_NODE_SEL) ? cnt(h->node_sel) : 0;
+  if (h->flags & KPF_HAS_REQ_NA)
+    for (int t = 0; t < h->n_req_terms; ++t) n += cnt(sel[h->req_terms_off + t]);
+  for (int t = 0; t < h->n_pref_terms; ++t) n += cnt(sel[h->pref_terms_off + t]);
+  return n <= KSG_WC_MAXREQ;
 }
-// nodeaffinity.RequiredNodeAffinity.Match on NPT nodes (required_na)
-template <int NPT>
-__device__ __forceinline__ void required_na_multi(const DevCluster& C, const ProgView& V, const uint32_t (&n)[NPT],
-                                                  bool (&ok)[NPT]) {
-  const uint32_t f = V.h->flags;
-#pragma unroll
-  for (int k = 0; k < NPT; ++k) ok[k] = true;
-  if (f & KPF_HAS_NODE_SEL) sel_multi<NPT>(C, V, V.h->node_sel, n, ok);
-  if (f & KPF_HAS_REQ_NA) {
-    bool any[NPT];
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) any[k] = false;
-    for (int t = 0; t < V.h->n_req_terms; ++t) {
-      bool m[NPT];
-      sel_multi<NPT>(C, V, V.sel[V.h->req_terms_off + t], n, m);
-      bool pend = false;
-#pragma unroll
-      for (int k = 0; k < NPT; ++k) {
-        any[k] |= m[k];
-        pend |= ok[k] && !any[k];
-      }
-      if (!__ballot(pend)) break;
-    }
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) ok[k] &= any[k];
+
+// One thread per pod of the chunk: WcPod of pod q0 + j (run_whatif checked
+// wc_decodable for every one).  The same outcome rules as freq_match / node_sel /
+// required_na: a term of kind 0 matches no node, a key outside the vocabulary is
+// absent from every node.
+__global__ __launch_bounds__(64) void k_wc_decode(DevCluster C, DevProfile F, WiArgs A, WcPod* __restrict__ out) {
+  const uint32_t j = blockIdx.x * 64 + threadIdx.x;
+  if (j >= A.count) return;
+  const ProgView V = view(A.progs + A.prog_off[A.q0 + j]);
+  const ksg_prog* h = V.h;
+  const uint32_t fl = h->flags;
+  const bool ht = F.pos_taint >= 0, ha = F.pos_na >= 0;
+  WcPod P{};
+  P.flags = (fl & KPF_PREFILTER_REJECT) ? 1u : 0u;
+  if (fl & KPF_RESTRICT) {
+    P.flags |= 2u;
+    P.roff = A.prog_off[A.q0 + j] + h->off_u32 + 4ull * (uint32_t)h->restrict_off;
+    P.rwords = (uint32_t)h->restrict_words;
   }
+  P.q0 = h->req[0] > 0 ? (double)h->req[0] : -INFINITY;
+  P.q1 = h->req[1] > 0 ? (double)h->req[1] : -INFINITY;
+  P.fs0 = (double)h->fit_score_req[0];
+  P.fs1 = (double)h->fit_score_req[1];
+  P.bq0 = (double)h->ba_req[0];
+  P.bq1 = (double)h->ba_req[1];
+  P.hseed = F.seed ^ ((uint64_t)(uint32_t)h->queue_idx * 0x9E3779B97F4A7C15ull);
+  if (ht) {
+    const uint32_t* hard = V.u32 + h->taint_hard_off;
+    const uint32_t* pref = V.u32 + h->taint_pref_off;
+    const int tw = h->taint_words;
+    P.hw = tw > 1 ? ((uint64_t)hard[1] << 32 | hard[0]) : tw > 0 ? hard[0] : 0;
+    P.pw = tw > 1 ? ((uint64_t)pref[1] << 32 | pref[0]) : tw > 0 ? pref[0] : 0;
+  }
+  uint32_t nr = 0;
+  auto emit = [&](const ksg_sel& s, uint32_t gbit) {
+    if (s.kind == 0) {
+      P.req[nr++] = WcReq{0, 0, gbit, 4u, 0};
+      return;
+    }
+    for (int i = 0; i < s.req_cnt; ++i) {
+      const ksg_freq f = V.fq[s.req_off + i];
+      WcReq r{0, f.arg, gbit, 4u, 0};
+      if (f.mode == KFR_NAME_EQ || f.mode == KFR_NAME_NE) {
+        r.mode = f.mode == KFR_NAME_EQ ? 2u : 3u;
+      } else if (f.mode == KFR_ANY || f.mode == KFR_NONE) {
+        if (f.key >= 0 && (uint32_t)f.key < C.K) {
+          r.col = (uint64_t)(uint32_t)f.key * C.N;
+          r.mode = f.mode == KFR_ANY ? 0u : 1u;
+        } else if (f.mode == KFR_NONE) {
+          continue;  // (no node has the key: the requirement holds everywhere)
+        }
+      }
+      P.req[nr++] = r;
+    }
+  };
+  if (ha && !(fl & KPF_SKIP_NA_FILTER)) {
+    if (fl & KPF_HAS_NODE_SEL) emit(h->node_sel, 1u);
+    if (fl & KPF_HAS_REQ_NA) {
+      if (h->n_req_terms == 0) P.flags |= 1u;  // (no term to match: no node passes)
+      for (int t = 0; t < h->n_req_terms; ++t) {
+        emit(V.sel[h->req_terms_off + t], 1u << (1 + t));
+        P.reqmask |= 1u << (1 + t);
+      }
+    }
+  }
+  P.npf = (ha && !(fl & KPF_SKIP_NA_SCORE)) ? (uint32_t)h->n_pref_terms : 0u;
+  for (uint32_t t = 0; t < P.npf; ++t) emit(V.sel[h->pref_terms_off + t], 1u << (KSG_WC_PREF_BIT + t));
+  P.nreq = nr;
+  out[j] = P;
 }
 
 // A node of the class path's pass 1, held in registers across the block's pods:
@@ -3108,8 +3174,7 @@ __device__ __forceinline__ double least_req_d(double ad, double ra, double qd) {
 // (taints + 1) << preferred terms <= KSG_WC_CLS.
 template <int NPT>
 __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F, WiArgs A,
-                                                     const uint8_t* __restrict__ progs,
-                                                     const uint64_t* __restrict__ prog_off) {
+                                                     const WcPod* __restrict__ pods) {
 #pragma clang fp contract(off)
   __shared__ unsigned long long slot[KSG_WC_PODS][KSG_WC_CLS];
   __shared__ uint32_t wcnt[KSG_WC_PODS];
@@ -3119,7 +3184,7 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
   for (uint32_t i = tid; i < KSG_WC_PODS * KSG_WC_CLS; i += 256) (&slot[0][0])[i] = 0ull;
   if (tid < KSG_WC_PODS) wcnt[tid] = 0;
   __syncthreads();
-  const bool hf = F.pos_fit >= 0, hb = F.pos_ba >= 0, ht = F.pos_taint >= 0, ha = F.pos_na >= 0;
+  const bool hf = F.pos_fit >= 0, hb = F.pos_ba >= 0;
 #pragma unroll 1
   for (uint32_t sub = 0; sub < KSG_WC_TILE / (256 * NPT); ++sub) {
     const uint32_t nb = blockIdx.y * KSG_WC_TILE + sub * (256 * NPT);
@@ -3155,59 +3220,71 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
     }
 #pragma unroll 1
     for (uint32_t pi = 0; pi < np; ++pi) {
-      const uint32_t j = j0 + pi;
-      const ProgView V = view(progs + prog_off[A.q0 + j]);
-      const ksg_prog* h = V.h;
-      const uint32_t fl = h->flags;
+      const WcPod& P = pods[j0 + pi];
+      const uint32_t fl = P.flags;
       bool pass[NPT];
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) pass[k] = x[k].ok && !(fl & KPF_PREFILTER_REJECT);
-      if (fl & KPF_RESTRICT) {
+      for (int k = 0; k < NPT; ++k) pass[k] = x[k].ok && !(fl & 1u);
+      if (fl & 2u) {
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) pass[k] &= bit(V.u32 + h->restrict_off, h->restrict_words, (int32_t)n[k]);
+        for (int k = 0; k < NPT; ++k)
+          pass[k] &= bit(reinterpret_cast<const uint32_t*>(A.progs + P.roff), (int)P.rwords, (int32_t)n[k]);
       }
-      if (hf) {  // (the pod count was checked with the node)
-        const bool c0 = h->req[0] > 0, c1 = h->req[1] > 0;
-        const double q0 = (double)h->req[0], q1 = (double)h->req[1];
+      if (hf) {  // (the pod count was checked with the node; q = -inf when not requested)
+        const double q0 = P.q0, q1 = P.q1;
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) pass[k] &= !(c0 & (q0 > x[k].fd0)) & !(c1 & (q1 > x[k].fd1));
+        for (int k = 0; k < NPT; ++k) pass[k] &= !(q0 > x[k].fd0) & !(q1 > x[k].fd1);
       }
       uint32_t xt[NPT];
+      {  // TaintToleration (a node's taints are distinct: the set counts them; zero sets without the plugin)
+        const uint64_t hw = P.hw, pw = P.pw;
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) xt[k] = 0;
-      if (ht) {
-        const uint32_t* hard = V.u32 + h->taint_hard_off;
-        const uint32_t* pref = V.u32 + h->taint_pref_off;
-        const int tw = h->taint_words;
-        const uint64_t hw = tw > 1 ? ((uint64_t)hard[1] << 32 | hard[0]) : tw > 0 ? hard[0] : 0;
-        const uint64_t pw = tw > 1 ? ((uint64_t)pref[1] << 32 | pref[0]) : tw > 0 ? pref[0] : 0;
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {  // (a node's taints are distinct: the set counts them)
+        for (int k = 0; k < NPT; ++k) {
           pass[k] &= (x[k].ts & hw) == 0;
           xt[k] = (uint32_t)__popcll(x[k].ts & pw);
         }
       }
-      if (ha && !(fl & KPF_SKIP_NA_FILTER)) {
-        bool m[NPT];
-        required_na_multi<NPT>(C, V, n, m);
+      // NodeAffinity: every flattened requirement on every node -> failed-term masks
+      uint32_t failm[NPT];
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) pass[k] &= m[k];
+      for (int k = 0; k < NPT; ++k) failm[k] = 0;
+      const uint32_t nreq = P.nreq;
+#pragma unroll 1
+      for (uint32_t r = 0; r < nreq; ++r) {
+        const WcReq& R = P.req[r];
+        const uint32_t mode = R.mode, gb = R.gbit;
+        const uint64_t arg = R.arg;
+        if (mode <= 1u) {
+          const int32_t* col = C.label + R.col;
+          int32_t v[NPT];
+#pragma unroll
+          for (int k = 0; k < NPT; ++k) v[k] = col[n[k]];
+#pragma unroll
+          for (int k = 0; k < NPT; ++k) {
+            const bool inset = v[k] >= 0 && ((arg >> ((uint32_t)v[k] & 63u)) & 1ull);
+            failm[k] |= (inset != (mode == 0u)) ? gb : 0u;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < NPT; ++k) {
+            const bool eq = (uint64_t)(C.goff + n[k]) == arg;
+            const bool m = mode == 4u ? false : (eq != (mode == 3u));
+            failm[k] |= m ? 0u : gb;
+          }
+        }
       }
-      // NodeAffinity's preferred terms: the matched-term mask
-      const int npf = (ha && !(fl & KPF_SKIP_NA_SCORE)) ? h->n_pref_terms : 0;
+      const uint32_t reqm = P.reqmask;
+      const int npf = (int)P.npf;
       uint32_t mask[NPT];
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) mask[k] = 0;
-      for (int t = 0; t < npf; ++t) {
-        bool m[NPT];
-        sel_multi<NPT>(C, V, V.sel[h->pref_terms_off + t], n, m);
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) mask[k] |= (uint32_t)m[k] << t;
+      for (int k = 0; k < NPT; ++k) {
+        pass[k] &= !(failm[k] & 1u) & (reqm == 0u || (~failm[k] & reqm) != 0u);
+        mask[k] = (~failm[k] >> KSG_WC_PREF_BIT) & ((1u << npf) - 1u);
       }
       // Fit (LeastAllocated, cpu:1 memory:1) and BalancedAllocation (cpu, memory)
-      const double fs0 = (double)h->fit_score_req[0], fs1 = (double)h->fit_score_req[1];
-      const double bq0 = (double)h->ba_req[0], bq1 = (double)h->ba_req[1];
-      const uint64_t hseed = F.seed ^ ((uint64_t)(uint32_t)h->queue_idx * 0x9E3779B97F4A7C15ull);
+      const double fs0 = P.fs0, fs1 = P.fs1;
+      const double bq0 = P.bq0, bq1 = P.bq1;
+      const uint64_t hseed = P.hseed;
       int cnt = 0;
       bool rng = false;
 #pragma unroll
@@ -4930,6 +5007,7 @@ struct Engine::Impl {
   DBuf<uint32_t> arrive1; // block arrivals of the per-pod chain's last kernel
   bool static_ok = false; // per-pod cycles of Fit/BA/Taint/NA profiles: k_static + k_fs_static
   DBuf<uint64_t> wrec_pairs;  // what-if: pass 1's per-pair records (run_whatif)
+  DBuf<uint64_t> wc_pods;     // what-if class path: the chunk's decoded pods (WcPod)
   uint32_t wi_chunk = 0;      // ... pods per chunk of the last step, and whether records were used
   bool wi_rec = false;
   bool wi_cls = false;        // ... or the class path
@@ -5876,6 +5954,8 @@ static uint32_t prog_need_of(const ksg_prog* h) {
   bool small = true;
   for (int c = 0; c < 2; ++c)
     for (int64_t v : {h->req[c], h->fit_score_req[c], h->ba_req[c]}) small &= v >= 0 && v < ((int64_t)1 << 44);
+  // bit 19: the class path's decoder flattens its NodeAffinity (wc_decodable)
+  if (wc_decodable(h)) need |= 1u << 19;
   return need | np << 8 | (small ? 1u << 16 : 0u);
 }
 
@@ -5941,7 +6021,8 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
     if (const char* e = std::getenv("KSG_WHATIF_CLASSES")) use_cls &= std::strtol(e, nullptr, 10) != 0;
     for (uint32_t q = first; use_cls && q < first + count; ++q) {
       const uint32_t np = (I.prog_need[q] >> 8) & 0xFFu;
-      use_cls = np <= 7 && ((I.max_taints + 1) << np) <= KSG_WC_CLS && (I.prog_need[q] & (1u << 16));
+      use_cls = np <= 7 && ((I.max_taints + 1) << np) <= KSG_WC_CLS && (I.prog_need[q] & (1u << 16)) &&
+                (I.prog_need[q] & (1u << 19));
     }
     const bool use_rec = !use_cls && rec_mb > 0 && I.R <= 4 && I.static_fits && 100 * wsum < (int64_t)1 << 30;
     // record fields as narrow as the cluster allows: 4-byte records when the raw
@@ -5977,7 +6058,9 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
     if (use_cls) {
       const size_t fit = (rec_mb << 20) / (wc_words * 8) / KSG_WC_PODS * KSG_WC_PODS;
       chunk = (uint32_t)std::min<size_t>(count, std::max<size_t>(fit, KSG_WC_PODS));
-      if (!I.wrec_pairs.alloc((size_t)chunk * wc_words, err)) return false;
+      if (!I.wrec_pairs.alloc((size_t)chunk * wc_words, err) ||
+          !I.wc_pods.alloc((size_t)chunk * (sizeof(WcPod) / 8), err))
+        return false;
     }
     const dim3 pods((count + 255) / 256);
     hipLaunchKernelGGL(k_init_summaries, pods, dim3(256), 0, s, I.sums.p + first, count, I.F);
@@ -6006,9 +6089,11 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
         const bool kept_here = I.keep_n && I.keep_first < a.q0 + a.count && I.keep_first + I.keep_n > a.q0;
         if (pass == 1 && use_cls) {
           I.path_pods[3]++;
-          if (I.wc_npt == 1) hipLaunchKernelGGL(k_whatif_cls1<1>, gridc, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
-          else if (I.wc_npt == 4) hipLaunchKernelGGL(k_whatif_cls1<4>, gridc, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
-          else hipLaunchKernelGGL(k_whatif_cls1<2>, gridc, dim3(256), 0, s, C, I.F, a, a.progs, a.prog_off);
+          WcPod* wp = reinterpret_cast<WcPod*>(I.wc_pods.p);
+          hipLaunchKernelGGL(k_wc_decode, dim3((a.count + 63) / 64), dim3(64), 0, s, C, I.F, a, wp);
+          if (I.wc_npt == 1) hipLaunchKernelGGL(k_whatif_cls1<1>, gridc, dim3(256), 0, s, C, I.F, a, wp);
+          else if (I.wc_npt == 4) hipLaunchKernelGGL(k_whatif_cls1<4>, gridc, dim3(256), 0, s, C, I.F, a, wp);
+          else hipLaunchKernelGGL(k_whatif_cls1<2>, gridc, dim3(256), 0, s, C, I.F, a, wp);
           hipLaunchKernelGGL(k_whatif_cls2, dim3(a.count), dim3(KSG_WC_CLS), 0, s, I.F, a, tiles, I.xranks > 1 ? 1 : 0);
         } else if (pass == 2 && use_cls) {
           if (I.xranks > 1) hipLaunchKernelGGL(k_whatif_cls2, dim3(a.count), dim3(KSG_WC_CLS), 0, s, I.F, a, tiles, 2);

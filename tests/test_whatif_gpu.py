@@ -149,3 +149,44 @@ def test_whatif_pass_records(monkeypatch, env):
         mp.spawn(_sharded_worker, args=(2, port, json.dumps(doc), out), nprocs=2, join=True)
         for r in range(2):
             assert out[r] == want, f"rank {r} differs"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("npt", ["1", "2", "4"])
+def test_whatif_class_path_edge_selectors(monkeypatch, npt):
+    """The class path's decoded pods (k_wc_decode: one flat requirement list per
+    pod, failed-term masks in pass 1) on the NodeAffinity edge family: matchFields
+    In / NotIn (PreFilterResult bitmaps and name requirements), field-only and
+    empty terms, DoesNotExist / NotIn, Gt / Lt on non-numeric values, tolerations
+    of every form, plus keys and values no node has and an empty nodeSelectorTerms
+    list; every nodes-per-thread variant of pass 1."""
+    from ksg import edge
+    monkeypatch.setenv("KSG_WC_NPT", npt)
+    doc = edge.generate_edge("na", n_pods=2 * STEP - 4)
+    for p in doc["queue"]:  # (ephemeral-storage requests keep a step off the class path)
+        for c in p["spec"]["containers"]:
+            c.get("resources", {}).get("requests", {}).pop(edge.EPH, None)
+    extra = [
+        {"nodeSelector": {"no-such-key": "x"}},
+        {"affinity": {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
+            {"matchExpressions": [{"key": "no-such-key", "operator": "DoesNotExist"},
+                                  {"key": "disk", "operator": "NotIn", "values": ["no-such-value"]}]}]}}}},
+        {"affinity": {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": []}}}},
+        {"affinity": {"nodeAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+            {"weight": 7, "preference": {"matchExpressions": [{"key": "no-such-key", "operator": "NotIn",
+                                                               "values": ["a"]}]}},
+            {"weight": 5, "preference": {"matchExpressions": [{"key": "no-such-key", "operator": "Exists"}]}},
+            {"weight": 3, "preference": {}}]}}},
+    ]
+    for i, spec in enumerate(extra):
+        doc["queue"].append(g.pod_obj(f"pod-extra-{i}", [g.req(200, 256 * 1024 * 1024)], **spec))
+    o = _oracle_steps(doc, 2)
+    want = [o.result(q) for q in range(o.n_queue)]
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    for k in range(2):
+        s.whatif(k * STEP, STEP)
+    got = [(r.selected, r.feasible, r.status) for r in s.results()]
+    bad = [(q, got[q], want[q]) for q in range(len(want)) if got[q] != want[q]]
+    assert not bad, bad[:5]
+    assert s.whatif_class_chunks() == 2

@@ -25,6 +25,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
 HBM_PEAK_GBS = 8000.0
+CUS = 256  # MI355X compute units (MI355X_MICROARCH.md)
 
 
 def parse(argv=None):
@@ -49,6 +50,28 @@ def pmc_step_traffic(kernels):
         ks = json.load(open(f)).get("kernels", {})
         if all(k in ks for k in kernels):
             return sum(ks[k]["hbm_bytes_per_dispatch"] for k in kernels)
+    return None
+
+
+def pmc_issue(kernel, kernel_ms):
+    """Issue utilisation of `kernel` from the newest committed SQ pass holding it
+    (profiles/*cfg5_pmc_sq.csv, per-dispatch means): SALU instructions over one
+    scalar issue slot per CU per cycle, VALU wave-instructions over one per SIMD
+    per 2 cycles (wave64 on SIMD-32), cycles = GRBM_GUI_ACTIVE / 8 XCDs when the
+    pass has it, else the kernel time at the 2.4 GHz peak clock."""
+    import csv
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*cfg5_pmc_sq.csv")), reverse=True):
+        for row in csv.DictReader(open(f)):
+            if row["kernel"].split("::")[-1] != kernel:
+                continue
+            salu = float(row["SQ_INSTS_SALU_per_dispatch"])
+            valu = float(row["SQ_INSTS_VALU_per_dispatch"])
+            gui = float(row.get("GRBM_GUI_ACTIVE_per_dispatch") or 0.0)
+            cyc = gui / 8 if gui else kernel_ms * 1e-3 * 2.4e9
+            return {"kernel": kernel, "source": os.path.basename(f), "salu_per_dispatch": salu,
+                    "valu_per_dispatch": valu, "cycles": cyc, "cycles_from": "GRBM_GUI_ACTIVE/8" if gui else "2.4 GHz",
+                    "salu_util": salu / (CUS * cyc), "valu_util": 2 * valu / (4 * CUS * cyc)}
     return None
 
 
@@ -125,11 +148,14 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
     # the kernel time is one step's two passes (HIP events around each, summed).
     bytes_per_launch = 7.0 * shard * P
     kernel_ms = 2 * avg_ms
+    issue = None
     if classes:  # class path: per-class best keys, nothing per pair in memory
         kernel = "k_whatif_cls1 + k_whatif_cls2 (one step)"
         traffic = pmc_step_traffic(["cfg5:k_whatif_cls1", "cfg5:k_whatif_cls2"])
-        note = ("pass 1 (k_whatif_cls1) is VALU / SALU issue bound (profiles/*cfg5_pmc_sq.csv), "
-                "its HBM traffic (PMC) is far below the §8(d) bytes")
+        note = ("issue-bound: pass 1 (k_whatif_cls1) is limited by VALU / SALU issue (`issue`, from "
+                "profiles/*cfg5_pmc_sq.csv), not HBM: its measured traffic is far below the §8(d) bytes, "
+                "so `frac` prices the step against bytes it never moves")
+        issue = pmc_issue("k_whatif_cls1", kernel_ms)
     else:  # record path: pass 1's 4-byte per-pair record, written and read back by pass 2
         kernel = "k_whatif_rec1 + k_whatif_rec2 (one step)"
         traffic = pmc_step_traffic(["cfg5:k_whatif_rec1", "cfg5:k_whatif_rec2"])
@@ -154,11 +180,13 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
                    "nodes_total": a.nodes, "nodes_per_gpu": shard, "pods_per_step": P,
                    "parallelism": f"node-shard x{world}" if world > 1 else "1 GPU"},
         "scheduled_per_step": sum(1 for r in res if r.status == 0) / a.steps,
-        "roofline": {"bound": "hbm", "achieved": bytes_per_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms else 0.0,
+        "roofline": {"bound": "issue" if issue else "hbm", "achieved": bytes_per_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms else 0.0,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": kernel,
                      "kernel_avg_ms": kernel_ms, "kernel_samples": nsamp, "bytes_per_launch": bytes_per_launch,
                      "traffic": traffic, "note": note},
     }
+    if issue:
+        out["roofline"]["issue"] = issue
     out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS
     if a.cpu_pods and world == 1:  # the oracle's what-if step on a bounded sample of the same cluster
         sys.path.insert(0, os.path.join(ROOT, "tests"))

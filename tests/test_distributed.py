@@ -224,7 +224,7 @@ def _sharded_edge_worker(rank, world, port, doc_json, out):
     s.set_exchange_host(world)
     s.load_cluster(doc)
     s.schedule()
-    out[rank] = ([(r.selected, r.feasible, r.status) for r in s.results()], s.path_counts())
+    out[rank] = ([(r.selected, r.feasible, r.status) for r in s.results()], s.path_counts(), s.batch_path)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -250,10 +250,13 @@ def test_sharded_table_chain_edge_matches_oracle(variant, world):
         out = m.dict()
         mp.spawn(_sharded_edge_worker, args=(world, port, json.dumps(doc), out), nprocs=world, join=True)
         for r in range(world):
-            got, paths = out[r]
+            got, paths, batch = out[r]
             bad = [(q, got[q], want[q]) for q in range(len(want)) if got[q] != want[q]]
             assert not bad, f"{variant} rank {r}: {len(bad)} pods differ, first {bad[:4]} (paths {paths})"
-            assert paths[0] > 0, paths  # the sharded table chain ran
+            if variant == "na":  # (Taint / NodeAffinity / Fit / BA: the node-sharded static window)
+                assert batch, paths
+            else:
+                assert paths[0] > 0, paths  # the sharded table chain ran
 
 
 def _sharded_full_worker(rank, world, port, n_pods, out):

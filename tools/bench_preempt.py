@@ -20,15 +20,25 @@ sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
 
 
 def make_doc(nodes, pods):
+    """The preempt family at `nodes` nodes, 4 random bound pods per node plus one
+    lowest-priority 4-core filler on every node (no node has 6 free cores), and
+    `pods` queue pods of priority 5000 asking 6 cores: every node is a potential
+    node (Unschedulable: insufficient cpu), the 8-core ones fit once their
+    lower-priority pods are gone, so every pod runs a full victim search."""
     from ksg import edge
+    from ksg.generator import pod_obj, req
     doc = edge.gen_preempt(n_nodes=nodes, n_existing=4 * nodes, n_pods=pods)
+    low = min(edge.PRIORITIES)
+    for i, n in enumerate(doc["nodes"]):
+        doc["pods"].append(pod_obj(f"fill-{i:07d}", [req(4000, 1024 * 1024 * 1024)], node=n["metadata"]["name"],
+                                   priority=low))
     for p in doc["queue"]:
         sp = p["spec"]
         sp["priority"] = 5000
         for k in ("preemptionPolicy", "topologySpreadConstraints", "affinity", "nodeSelector", "tolerations"):
             sp.pop(k, None)
         for c in sp["containers"]:
-            c["resources"] = {"requests": {"cpu": "3500m", "memory": "2Gi"}}
+            c["resources"] = {"requests": {"cpu": "6000m", "memory": "2Gi"}}
             c.pop("ports", None)
     return doc
 
@@ -68,7 +78,7 @@ def main():
     b = one(1, a.nodes, a.pods)
     p = one(0, a.nodes, a.per_node_pods)
     k = a.per_node_pods
-    print(json.dumps({"nodes": a.nodes, "bound_pods": 4 * a.nodes,
+    print(json.dumps({"nodes": a.nodes, "bound_pods": 5 * a.nodes,
                       "batched": {"pods": a.pods, "ms_per_pod": b["ms_per_pod"], "nominated": b["nominated"],
                                   "batched_searches": b["batched"]},
                       "per_node": {"pods": k, "ms_per_pod": p["ms_per_pod"], "nominated": p["nominated"]},

@@ -11,7 +11,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/wi_f -o run -- python3 bench_whatif.py $A > gpurun_out/wi_f.log 2>&1 || exit 1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/wi_w -o run -- python3 bench_whatif.py $A > gpurun_out/wi_w.log 2>&1 || exit 1
 python3 tools/pmc_traffic.py gpurun_out/wi_f gpurun_out/wi_w "cfg5:" > gpurun_out/${TAG}_cfg5_pmc_traffic.json || exit 1
-timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d gpurun_out/wi_s -o run -- python3 bench_whatif.py $A > gpurun_out/wi_s.log 2>&1 || exit 1
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/wi_s -o run -- python3 bench_whatif.py $A > gpurun_out/wi_s.log 2>&1 || exit 1
 python3 tools/pmc_summary.py "$(find gpurun_out/wi_s -name "*counter_collection.csv" -print -quit)" > gpurun_out/${TAG}_cfg5_pmc_sq.csv || exit 1
 timeout -s KILL 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA --output-format csv -d gpurun_out/wi_l -o run -- python3 bench_whatif.py $A > gpurun_out/wi_l.log 2>&1 || exit 1
 python3 tools/pmc_summary.py "$(find gpurun_out/wi_l -name "*counter_collection.csv" -print -quit)" > gpurun_out/${TAG}_cfg5_pmc_lds.csv || exit 1

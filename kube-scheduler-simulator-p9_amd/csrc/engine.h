@@ -146,6 +146,13 @@ class Engine {
   // is the existing-pod table row tombstoned / revived in place (-1 none).
   bool toggle_pods(const std::vector<const std::vector<uint8_t>*>& progs, const std::vector<int32_t>& gnode,
                    const std::vector<int32_t>& rows, int sign, std::string& err);
+  // The batched victim search's form: the candidate victims are uploaded once
+  // (entries 0..n-1: program, global node, table row), then subsets of them
+  // toggled by index, one launch per subset (one thread per node: a node's
+  // victims in sequence, different nodes in parallel).
+  bool toggle_stage(const std::vector<const std::vector<uint8_t>*>& progs, const std::vector<int32_t>& gnode,
+                    const std::vector<int32_t>& rows, std::string& err);
+  bool toggle_staged(const std::vector<uint32_t>& idx, int sign, std::string& err);
   // Filter codes of program q against the current device state (its whole cycle
   // re-run without commit; kept outputs and the pod's summary are left as they
   // were): global node gnode's code, or every node's when gnode is -1.

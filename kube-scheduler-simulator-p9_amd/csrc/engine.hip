@@ -1708,6 +1708,30 @@ __global__ void k_assume(DevCluster C, const uint8_t* __restrict__ prog, int32_t
   }
   assume_pod(C, V, n, sign, table != 0, prow);
 }
+// toggle_staged: thread g toggles group g's entries (sorted idx[gs[g] .. gs[g+1]),
+// all on one node) in sequence: a node's row, ports and existing-pod flags are
+// touched by one thread only; the class tables and claim counts take atomics.
+// (Entries with CSI volumes, whose per-volume node lists are shared across
+// nodes, never come here: the host toggles those one launch per pod.)
+__global__ __launch_bounds__(256) void k_toggle_groups(DevCluster C, const uint8_t* __restrict__ blob,
+                                                       const uint64_t* __restrict__ off, const int32_t* __restrict__ gnode,
+                                                       int32_t* rows, const uint32_t* __restrict__ idx,
+                                                       const uint32_t* __restrict__ gs, uint32_t ngroups, int sign) {
+  const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= ngroups) return;
+  for (uint32_t j = gs[g]; j < gs[g + 1]; ++j) {
+    const uint32_t e = idx[j];
+    const ProgView V = view(blob + off[e]);
+    const uint32_t n = (uint32_t)gnode[e] - C.goff;
+    if (gnode[e] < 0 || (uint32_t)gnode[e] < C.goff || n >= C.N) continue;
+    assume_pod(C, V, n, sign, false, nullptr);
+    const int32_t r = rows[e];
+    if (r >= 0) {
+      if (sign < 0) C.ptflags[r] |= KEF_DELETED;
+      else C.ptflags[r] &= ~KEF_DELETED;
+    }
+  }
+}
 
 
 // ----------------------------------------------------------------- what-if batches (cfg5)
@@ -2308,6 +2332,10 @@ struct WinArgs {
   uint32_t pub_need;
   uint32_t mblocks;   // persistent loop: dedicated merge blocks (one per pod) merge the tile lists
   uint32_t astride;   // arrival counter stride (u32): 1, or 32 in the persistent loop (a line per pod)
+  // persistent loop: 1 = the replay evaluates its window's pods on P_{W-1} itself
+  // (the merges hand over keys and rows without waiting for P_{W-1}); 0 = the
+  // merges do it once P_{W-1} is published (PriorRec)
+  uint32_t prior_fix;
 };
 // the static record of (queue pod q, global node g)
 __device__ __forceinline__ StaticRec srec_at(const WinArgs& A, uint32_t q, uint32_t g) {
@@ -3551,9 +3579,12 @@ __device__ __forceinline__ void win_merge(const DevCluster& C, const DevProfile&
       for (int k = 0; k < 3; ++k) stv<true>(reinterpret_cast<int32_t*>(A.erec) + k * KSG_BATCH + b, f[k]);
       stv<true>(A.arrive + b * A.astride, 0u);
     }
-    // the prior step: pod q on P_{E-1}'s nodes (published by the replay of E-1)
+    // the prior step: pod q on P_{E-1}'s nodes (published by the replay of E-1);
+    // prior_fix: the replay evaluates it itself
     int np1 = 0;
-    if (A.pubw) {
+    Pend pe;
+    pe.node = -1;
+    if (A.pubw && !A.prior_fix) {
       uint32_t ok = 1;
       if (lane == 0) {
         ok = 0;
@@ -3564,13 +3595,15 @@ __device__ __forceinline__ void win_merge(const DevCluster& C, const DevProfile&
         }
         if (!ok) __hip_atomic_store(A.abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (__builtin_amdgcn_readfirstlane(ok)) np1 = ldv<true>(A.pcur_n);  // (else the run has aborted)
+      if (__builtin_amdgcn_readfirstlane(ok)) {  // (else the run has aborted)
+        // the count and every entry requested together (one round trip, not two)
+        np1 = ldv<true>(A.pcur_n);
+        if (lane < KSG_BATCH) pe = ld_obj<true>(A.pcur + lane);
+      }
     }
-    Pend pe;
-    pe.node = -1;
+    if (lane >= np1) pe.node = -1;
     uint64_t k = 0;
     if (lane < np1) {
-      pe = ld_obj<true>(A.pcur + lane);
       int32_t fs, bs;
       int64_t tot;
       const uint32_t R = C.R < 4 ? C.R : 4;
@@ -3592,10 +3625,12 @@ __device__ __forceinline__ void win_merge(const DevCluster& C, const DevProfile&
     const uint64_t kb = wave_max(k);
     const unsigned long long mb = __ballot(kb != 0 && k == kb);
     if (lane == 0) {
-      stv<true>(&pr->pmask, (uint64_t)pm);
-      stv<true>(&pr->pbest, kb);
-      stv<true>(&pr->pbest_e, (int32_t)(mb ? __ffsll((long long)mb) - 1 : -1));
-      stv<true>(&pr->np, np1);
+      if (!A.prior_fix) {
+        stv<true>(&pr->pmask, (uint64_t)pm);
+        stv<true>(&pr->pbest, kb);
+        stv<true>(&pr->pbest_e, (int32_t)(mb ? __ffsll((long long)mb) - 1 : -1));
+        stv<true>(&pr->np, np1);
+      }
       if (A.estamps) atomicMax((unsigned long long*)&A.estamps[10], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pod's record is out (wave 0 stored all of it)
@@ -3639,8 +3674,6 @@ __device__ __forceinline__ bool win_merge_block(const DevCluster& C, const DevPr
   const uint32_t q = A.e0 + b;
   constexpr int kPodW = (int)(sizeof(PodLite) / 8);
   if (tid < kPodW) reinterpret_cast<uint64_t*>(h)[tid] = reinterpret_cast<const uint64_t*>(A.plite + q)[tid];
-  const int np = ldv<true>(A.pprev_n);
-  if (tid < np) pnl[tid] = ldv<true>(&A.pprev[tid].node);
   if (tid == 0) {
     bool ok = false;
     for (uint32_t it = 0; it < A.spin; ++it) {
@@ -3653,6 +3686,11 @@ __device__ __forceinline__ bool win_merge_block(const DevCluster& C, const DevPr
   }
   __syncthreads();
   if (!wcount[17]) return false;
+  // P_{E-2} only now: the tiles arrived, so their blocks saw it published (a merge
+  // block may otherwise run a window ahead of the replay that writes it)
+  const int np = ldv<true>(A.pprev_n);
+  if (tid < np) pnl[tid] = ldv<true>(&A.pprev[tid].node);
+  __syncthreads();
   win_merge<MODE, false, true>(C, F, A, b, L, h, pnl, np);
   return true;
 }
@@ -4180,7 +4218,8 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   const PriorRec* PR = prior_rec(A.wrec);
   uint64_t pr_k = 0, pr_p0 = 0, pr_p1 = 0, pr_m = 0;
   int32_t pr_df = 0;
-  if constexpr (PER) {
+  const bool prior_rec_in = PER && !A.prior_fix;  // (else the prior step is evaluated below)
+  if (prior_rec_in) {
     if (ppb < nb) {
       pr_k = ldv<true>(&PR[ppb].pkey[ppe]);
       const uint64_t* pw = reinterpret_cast<const uint64_t*>(&PR[ppb].patch[ppe]);
@@ -4296,7 +4335,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     if ((uint32_t)pe.node >= C.goff && nl < C.N) store_row_p<PER>(C, nl, pe.after);
     if (A.xrows) A.xrows[pe.node] = pe.after;  // every rank's replica, every node
   }
-  if constexpr (PER) {  // the eval blocks' prior step, staged
+  if (prior_rec_in) {  // the eval blocks' prior step, staged
     if (ppb < nb) {
       L.pkey[ppb][ppe] = pr_k;
       reinterpret_cast<uint64_t*>(&L.patch[ppb][ppe])[0] = pr_p0;
@@ -4361,7 +4400,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     int i = tid + k * KSG_WIN_THREADS;
     if (i < nk) (&L.key[0][0])[i] = kv[k];
     const int b = wave + 16 * k;
-    if constexpr (!PER) {  // (persistent loop: the eval blocks' pmask)
+    if (!prior_rec_in) {  // (PriorRec: the eval blocks' pmask)
       bool m = kv[k] != 0 && np > 0 && prior_of(L, (int32_t)(kv[k] & 0xFFFFFull)) >= 0;
       unsigned long long mask = __ballot(m);
       if (lane == 0 && b < nb) L.pmask[b] = mask;
@@ -4622,6 +4661,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     __syncthreads();
     if (tid < 16) st_sc1(A.pub + tid * 32, A.pub_val);
   }
+  STAMP(6);
   if (tid < nb) {
     ksg_pod_summary& d = A.sums[A.w0 + tid];
     d.best_key = L.sum[tid].best_key;
@@ -4993,6 +5033,15 @@ struct Engine::Impl {
   uint32_t pcap = 0, pkeys = 0, tcap = 0, rcap = 0, vcap = 0;
   DBuf<uint8_t> evprog;  // cluster events applied in place: the bound pod's program
   DBuf<int32_t> evrow;   // its existing-pod table row
+  // toggle_stage / toggle_staged: the staged candidate victims
+  DBuf<uint8_t> tgprog;
+  DBuf<uint64_t> tgoff;
+  DBuf<int32_t> tgnode, tgrow;
+  DBuf<uint32_t> tgidx;
+  std::vector<int32_t> tg_gnode;  // host copies: grouping, CSI entries
+  std::vector<char> tg_csi;
+  std::vector<uint64_t> tg_off;
+  uint32_t tg_n = 0;
   DBuf<ksg_pod_summary> drysum;  // DefaultPreemption dry run: the preemptor's summary, restored after each probe
   // scratch
   DBuf<int32_t> cnt, hist_f, hist_s, ipa_aff, ipa_anti, ipa_exist, pts_min, pts_dom;
@@ -5071,7 +5120,8 @@ struct Engine::Impl {
   bool lost = false;             // an aborted persistent launch left the device state half-updated
   DBuf<WinSync> wsync;           // k_window_run's counters (zeroed per launch)
   int win_run_on = 1;            // persistent window loop (k_window_run): KSG_WIN_RUN=0 turns it off
-  int win_mblocks = 1;           // ... with dedicated merge blocks (KSG_WIN_MB=0: the last tile block merges)
+  int win_mblocks = 0;           // ... with dedicated merge blocks (KSG_WIN_MB=1; the last tile block merges: measured faster)
+  int win_pfix = 0;              // ... the replay evaluates the prior step itself (KSG_WIN_PFIX=1; measured slower)
   uint64_t win_runs = 0, win_fallbacks = 0;  // diagnostic: persistent window launches / not co-resident
   uint32_t fold_blocks = 256;  // table chain: k_fold above this many blocks (KSG_FOLD_BLOCKS; tests force it)
   uint32_t occ_blocks = 0;     // table chain: occupancy twins above this many blocks (0: 2 per CU; KSG_OCC_BLOCKS)
@@ -5222,6 +5272,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (const char* e = std::getenv("KSG_RUN_NORES")) I.run_need_extra = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
   if (const char* e = std::getenv("KSG_WIN_RUN")) I.win_run_on = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_MB")) I.win_mblocks = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_WIN_PFIX")) I.win_pfix = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_RUN_SPIN")) I.run_spin = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("KSG_RUN_WAIT_US"))
     I.run_wait_us = std::max<uint32_t>(10, std::min<uint32_t>(1000000, (uint32_t)std::strtoul(e, nullptr, 10)));
@@ -5805,6 +5856,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     WinArgs AP = A;
     AP.mblocks = mb ? 1u : 0u;
     AP.astride = 32;
+    AP.prior_fix = I.win_pfix ? 1u : 0u;
     __atomic_store_n(I.hverdict, 0u, __ATOMIC_RELEASE);
     const RunCtl RC{grid + I.run_need_extra, I.run_wait_us * 100u, 0, I.hverdict, I.run_spin};
     const bool sampled = I.sample_every && I.n_samples * 2 + 2 <= I.sev.size();
@@ -6281,6 +6333,72 @@ bool Engine::toggle_pods(const std::vector<const std::vector<uint8_t>*>& progs, 
                        I.evrow.p + i);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(I.stream));  // (the host buffers are reused by the next toggle)
+  return true;
+}
+
+bool Engine::toggle_stage(const std::vector<const std::vector<uint8_t>*>& progs, const std::vector<int32_t>& gnode,
+                          const std::vector<int32_t>& rows, std::string& err) {
+  Impl& I = *p_;
+  if (!tables_ready(I, err)) return false;
+  const size_t n = progs.size();
+  if (gnode.size() != n || rows.size() != n) { err = "toggle_stage: sizes"; return false; }
+  I.tg_off.assign(n, 0);
+  I.tg_csi.assign(n, 0);
+  size_t bytes = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (!progs[i] || progs[i]->size() < sizeof(ksg_prog)) { err = "toggle_stage: program"; return false; }
+    I.tg_off[i] = bytes;
+    bytes = (bytes + progs[i]->size() + 255) & ~(size_t)255;
+    I.tg_csi[i] = reinterpret_cast<const ksg_prog*>(progs[i]->data())->n_csi > 0 ? 1 : 0;
+  }
+  std::vector<uint8_t> blob(std::max<size_t>(bytes, 1));
+  for (size_t i = 0; i < n; ++i) std::memcpy(blob.data() + I.tg_off[i], progs[i]->data(), progs[i]->size());
+  if (!I.tgprog.alloc(blob.size(), err) || !I.tgoff.alloc(n, err) || !I.tgnode.alloc(n, err) || !I.tgrow.alloc(n, err))
+    return false;
+  hipStream_t s = I.stream;
+  HIPCHK(hipMemcpyAsync(I.tgprog.p, blob.data(), blob.size(), hipMemcpyHostToDevice, s));
+  if (n) {
+    HIPCHK(hipMemcpyAsync(I.tgoff.p, I.tg_off.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(I.tgnode.p, gnode.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(I.tgrow.p, rows.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));  // (the host blob goes out of scope)
+  I.tg_gnode = gnode;
+  I.tg_n = (uint32_t)n;
+  return true;
+}
+bool Engine::toggle_staged(const std::vector<uint32_t>& idx, int sign, std::string& err) {
+  Impl& I = *p_;
+  if (sign != 1 && sign != -1) { err = "toggle_staged: sign"; return false; }
+  if (idx.empty()) return true;
+  std::vector<uint32_t> sorted;  // grouped by node (stable: a node's entries keep their order)
+  sorted.reserve(idx.size());
+  std::vector<uint32_t> serial;  // entries with CSI volumes: one launch each
+  for (uint32_t e : idx) {
+    if (e >= I.tg_n) { err = "toggle_staged: index"; return false; }
+    (I.tg_csi[e] ? serial : sorted).push_back(e);
+  }
+  std::stable_sort(sorted.begin(), sorted.end(),
+                   [&](uint32_t a, uint32_t b) { return I.tg_gnode[a] < I.tg_gnode[b]; });
+  std::vector<uint32_t> gs;
+  for (size_t j = 0; j < sorted.size(); ++j)
+    if (j == 0 || I.tg_gnode[sorted[j]] != I.tg_gnode[sorted[j - 1]]) gs.push_back((uint32_t)j);
+  gs.push_back((uint32_t)sorted.size());
+  const uint32_t ng = (uint32_t)gs.size() - 1;
+  std::vector<uint32_t> up(sorted);
+  up.insert(up.end(), gs.begin(), gs.end());
+  if (!I.tgidx.alloc(up.size(), err)) return false;
+  hipStream_t s = I.stream;
+  HIPCHK(hipMemcpyAsync(I.tgidx.p, up.data(), up.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  DevCluster C = I.cluster();
+  if (ng)
+    hipLaunchKernelGGL(k_toggle_groups, dim3((ng + 255) / 256), dim3(256), 0, s, C, I.tgprog.p, I.tgoff.p, I.tgnode.p,
+                       I.tgrow.p, I.tgidx.p, I.tgidx.p + sorted.size(), ng, sign);
+  for (uint32_t e : serial)
+    hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, s, C, I.tgprog.p + I.tg_off[e], I.tg_gnode[e], sign, 2,
+                       I.tgrow.p + e);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));  // (the host index list goes out of scope)
   return true;
 }
 

@@ -3244,59 +3244,74 @@ struct Cluster {
       // victims removed answers SelectVictimsOnNode's first question for all of
       // them; the reprieve then runs in lockstep over the candidates, one dry run
       // per round (its i-th most important victim re-added on every candidate).
-      auto toggle_many = [&](const vector<std::pair<int32_t, Vic>>& vs, int sign) {
-        if (vs.empty()) return true;
+      // every candidate victim staged on the device once (entry i = all[i]); the
+      // toggles below name entries (one launch each, a thread per node)
+      vector<std::pair<int32_t, Vic>> all;
+      for (int32_t g : potential)
+        for (auto& v : on[g]) all.push_back({g, v});
+      if (all.empty()) return true;
+      {
         vector<const vector<uint8_t>*> pp;
         vector<int32_t> gn, rows;
-        for (auto& gv : vs) {
+        for (auto& gv : all) {
           const Vic& v = gv.second;
           pp.push_back(v.bound >= 0 ? &bprog[v.bound] : &progs[v.qpod]);
           gn.push_back(gv.first + (int32_t)lo);
           rows.push_back(v.bound >= 0 ? (tables_on() ? bound_row[v.bound] : -1) : qrows[v.qpod]);
         }
-        return eng->toggle_pods(pp, gn, rows, sign, err);
-      };
-      vector<std::pair<int32_t, Vic>> all;
-      for (int32_t g : potential)
-        for (auto& v : on[g]) all.push_back({g, v});
-      if (all.empty()) return true;
-      vector<uint32_t> codes;
-      if (!toggle_many(all, -1) || !eng->dry_filter(q, -1, codes, err) || !toggle_many(all, +1)) return false;
-      vector<vector<Vic>> pv;  // per candidate: its victims, most important first
-      for (int32_t g : potential) {
-        if (on[g].empty() || codes[g] != KSG_FILTER_PASS) continue;
-        cands.push_back(Cand{g, {}});
-        pv.push_back(on[g]);
-        std::sort(pv.back().begin(), pv.back().end(), more_important);
+        if (!eng->toggle_stage(pp, gn, rows, err)) return false;
       }
-      vector<std::pair<int32_t, Vic>> off;  // every candidate's victims off, then reprieve round by round
+      vector<uint32_t> every(all.size());
+      for (size_t i = 0; i < all.size(); ++i) every[i] = (uint32_t)i;
+      vector<uint32_t> codes;
+      if (!eng->toggle_staged(every, -1, err) || !eng->dry_filter(q, -1, codes, err) ||
+          !eng->toggle_staged(every, +1, err))
+        return false;
+      vector<vector<uint32_t>> pv;  // per candidate: its victims (entries), most important first
+      {
+        size_t i = 0;
+        for (int32_t g : potential) {
+          const size_t i0 = i;
+          i += on[g].size();
+          if (on[g].empty() || codes[g] != KSG_FILTER_PASS) continue;
+          cands.push_back(Cand{g, {}});
+          pv.emplace_back();
+          for (size_t k = i0; k < i; ++k) pv.back().push_back((uint32_t)k);
+          std::sort(pv.back().begin(), pv.back().end(),
+                    [&](uint32_t a, uint32_t b) { return more_important(all[a].second, all[b].second); });
+        }
+      }
+      vector<uint32_t> off;  // every candidate's victims off, then reprieve round by round
       size_t rounds = 0;
       for (size_t c = 0; c < cands.size(); ++c) {
-        for (auto& v : pv[c]) off.push_back({cands[c].node, v});
+        off.insert(off.end(), pv[c].begin(), pv[c].end());
         rounds = std::max(rounds, pv[c].size());
       }
-      if (!toggle_many(off, -1)) return false;
+      if (!eng->toggle_staged(off, -1, err)) return false;
       ++preempt_batched_runs;
+      vector<vector<uint32_t>> vict(cands.size());
       for (size_t r = 0; r < rounds; ++r) {
-        vector<std::pair<int32_t, Vic>> back, keep_off;
+        vector<uint32_t> back, keep_off;
         vector<size_t> who;
         for (size_t c = 0; c < cands.size(); ++c)
           if (r < pv[c].size()) {
-            back.push_back({cands[c].node, pv[c][r]});
+            back.push_back(pv[c][r]);
             who.push_back(c);
           }
-        if (!toggle_many(back, +1) || !eng->dry_filter(q, -1, codes, err)) return false;
+        if (!eng->toggle_staged(back, +1, err) || !eng->dry_filter(q, -1, codes, err)) return false;
         for (size_t i = 0; i < who.size(); ++i)
           if (codes[cands[who[i]].node] != KSG_FILTER_PASS) {  // it must go: a victim
             keep_off.push_back(back[i]);
-            cands[who[i]].victims.push_back(back[i].second);
+            vict[who[i]].push_back(back[i]);
           }
-        if (!toggle_many(keep_off, -1)) return false;
+        if (!eng->toggle_staged(keep_off, -1, err)) return false;
       }
-      vector<std::pair<int32_t, Vic>> restore;  // the dry run leaves the state as it was
-      for (auto& c : cands)
-        for (auto& v : c.victims) restore.push_back({c.node, v});
-      if (!toggle_many(restore, +1)) return false;
+      vector<uint32_t> restore;  // the dry run leaves the state as it was
+      for (size_t c = 0; c < cands.size(); ++c) {
+        restore.insert(restore.end(), vict[c].begin(), vict[c].end());
+        for (uint32_t e : vict[c]) cands[c].victims.push_back(all[e].second);
+      }
+      if (!eng->toggle_staged(restore, +1, err)) return false;
       vector<Cand> kept;
       for (auto& c : cands)
         if (!c.victims.empty()) kept.push_back(std::move(c));

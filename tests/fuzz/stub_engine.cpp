@@ -23,6 +23,7 @@ struct Engine::Impl {
   uint32_t used[4] = {0, 0, 0, 0}, cap[4] = {0, 0, 0, 0};
   uint32_t npc = 0, ntc = 0;
   uint32_t keep_first = 0, keep_n = 0;
+  size_t staged = 0;
 };
 
 static bool check_prog(const std::vector<uint8_t>& p, std::string& err) {
@@ -120,6 +121,22 @@ bool Engine::toggle_pods(const std::vector<const std::vector<uint8_t>*>& progs, 
     if (!progs[i] || !check_prog(*progs[i], err)) return false;
     if (gnode[i] < 0 || (uint32_t)gnode[i] >= p_->N) { err = "stub: toggle node"; return false; }
   }
+  return true;
+}
+bool Engine::toggle_stage(const std::vector<const std::vector<uint8_t>*>& progs, const std::vector<int32_t>& gnode,
+                          const std::vector<int32_t>& rows, std::string& err) {
+  if (gnode.size() != progs.size() || rows.size() != progs.size()) { err = "stub: toggle_stage"; return false; }
+  for (size_t i = 0; i < progs.size(); ++i) {
+    if (!progs[i] || !check_prog(*progs[i], err)) return false;
+    if (gnode[i] < 0 || (uint32_t)gnode[i] >= p_->N) { err = "stub: toggle node"; return false; }
+  }
+  p_->staged = progs.size();
+  return true;
+}
+bool Engine::toggle_staged(const std::vector<uint32_t>& idx, int sign, std::string& err) {
+  if (sign != 1 && sign != -1) { err = "stub: toggle sign"; return false; }
+  for (uint32_t i : idx)
+    if (i >= p_->staged) { err = "stub: toggle index"; return false; }
   return true;
 }
 // Filter codes that walk the host's preemption paths: every node fails the

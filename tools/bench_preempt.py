@@ -7,7 +7,7 @@ pod is the cycle plus the victim search.  The batched search (every potential
 node in one dry run, the reprieve in lockstep) and the per-node probes run in
 separate processes (KSG_PREEMPT_BATCH); their nominations must agree.
 
-usage: python tools/bench_preempt.py [--nodes 50000] [--pods 8] [--per-node-pods 1]"""
+usage: python tools/bench_preempt.py [--nodes 50000] [--pods 8] [--per-node-pods 2] [--per-node-nodes 2000]"""
 import argparse
 import json
 import os
@@ -24,11 +24,15 @@ def make_doc(nodes, pods):
     lowest-priority 4-core filler on every node (no node has 6 free cores), and
     `pods` queue pods of priority 5000 asking 6 cores: every node is a potential
     node (Unschedulable: insufficient cpu), the 8-core ones fit once their
-    lower-priority pods are gone, so every pod runs a full victim search."""
+    lower-priority pods are gone, so every pod runs a full victim search.  The bound
+    pods carry no anti-affinity terms (one applying to the incoming pod takes the
+    per-node search: ksg's preempt_batched)."""
     from ksg import edge
     from ksg.generator import pod_obj, req
     doc = edge.gen_preempt(n_nodes=nodes, n_existing=4 * nodes, n_pods=pods)
     low = min(edge.PRIORITIES)
+    for b in doc["pods"]:  # (an existing pod's anti-affinity term would apply to the incoming pods: per-node search)
+        b["spec"].pop("affinity", None)
     for i, n in enumerate(doc["nodes"]):
         doc["pods"].append(pod_obj(f"fill-{i:07d}", [req(4000, 1024 * 1024 * 1024)], node=n["metadata"]["name"],
                                    priority=low))
@@ -53,8 +57,10 @@ import torch
 from bench_preempt import make_doc
 from ksg import Scheduler
 doc = make_doc({nodes}, {pods})
+print("[child] document built", file=sys.stderr, flush=True)
 s = Scheduler(doc["profile"])
 s.load_cluster(doc)
+print("[child] cluster loaded", file=sys.stderr, flush=True)
 t = time.perf_counter()
 s.schedule()
 dt = time.perf_counter() - t
@@ -63,9 +69,10 @@ print(json.dumps({{"ms_per_pod": dt * 1e3 / s.queue_len, "nominated": sum(1 for 
                   "batched": s.preempt_batched(), "noms": noms,
                   "res": [(r.selected, r.feasible, r.status) for r in s.results()]}}))
 """
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=900)
+    print(f"[bench_preempt] batch={batch} nodes={nodes} pods={pods}", file=sys.stderr, flush=True)
+    out = subprocess.run([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE, text=True, timeout=900)
     if out.returncode != 0:
-        raise RuntimeError(out.stderr[-3000:])
+        raise RuntimeError(f"exit {out.returncode}")
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
@@ -73,16 +80,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nodes", type=int, default=50000)
     ap.add_argument("--pods", type=int, default=8)
-    ap.add_argument("--per-node-pods", type=int, default=1)
+    ap.add_argument("--per-node-pods", type=int, default=2)
+    ap.add_argument("--per-node-nodes", type=int, default=2000,
+                    help="cluster size of the batched vs per-node comparison (a per-node search is one dry run per node)")
     a = ap.parse_args()
     b = one(1, a.nodes, a.pods)
-    p = one(0, a.nodes, a.per_node_pods)
     k = a.per_node_pods
+    bs = one(1, a.per_node_nodes, k)
+    p = one(0, a.per_node_nodes, k)
     print(json.dumps({"nodes": a.nodes, "bound_pods": 5 * a.nodes,
                       "batched": {"pods": a.pods, "ms_per_pod": b["ms_per_pod"], "nominated": b["nominated"],
                                   "batched_searches": b["batched"]},
-                      "per_node": {"pods": k, "ms_per_pod": p["ms_per_pod"], "nominated": p["nominated"]},
-                      "same_nominations": b["noms"][:k] == p["noms"][:k] and b["res"][:k] == p["res"][:k]}, indent=1))
+                      "compare": {"nodes": a.per_node_nodes, "pods": k,
+                                  "batched_ms_per_pod": bs["ms_per_pod"], "per_node_ms_per_pod": p["ms_per_pod"],
+                                  "nominated": p["nominated"], "batched_searches": bs["batched"],
+                                  "same_nominations": bs["noms"] == p["noms"] and bs["res"] == p["res"]}}, indent=1))
 
 
 if __name__ == "__main__":

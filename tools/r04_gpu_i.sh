@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 T=${TAG:-r04i}
 timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py tests/test_plugin_api_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/${T}_tests.log; [ $rc -ne 0 ] && exit $rc
-for v in "1 0" "1 1" "0 0"; do
+for v in "0 0" "0 1"; do
   set -- $v
   export KSG_WIN_PFIX=$1 KSG_WIN_MB=$2
   timeout -k 10 200 python bench.py --extra "" --cpu-baseline 0 --steps 10 --warmup 2 > gpurun_out/${T}_cfg2_pf$1mb$2.json 2>&1 || exit 1
@@ -16,5 +16,10 @@ for v in "1 0" "1 1" "0 0"; do
   sed -n 7,17p gpurun_out/${T}_probe_pf$1mb$2.txt
 done
 unset KSG_WIN_PFIX KSG_WIN_MB
-timeout -k 10 500 python tools/bench_preempt.py --nodes 50000 --pods 8 --per-node-pods 1 > gpurun_out/${T}_preempt_bench.json 2> gpurun_out/${T}_preempt_bench.err || { tail -5 gpurun_out/${T}_preempt_bench.err; exit 1; }
+timeout -k 10 500 python tools/bench_preempt.py --nodes 50000 --pods 8 > gpurun_out/${T}_preempt_bench.json 2> gpurun_out/${T}_preempt_bench.err || { tail -5 gpurun_out/${T}_preempt_bench.err; exit 1; }
 cat gpurun_out/${T}_preempt_bench.json
+timeout -k 10 300 python tools/dropin_probe.py > gpurun_out/${T}_dropin.json 2> gpurun_out/${T}_dropin.err || { tail -5 gpurun_out/${T}_dropin.err; exit 1; }
+cat gpurun_out/${T}_dropin.json
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d gpurun_out/${T}_dropin_prof -o run -- python3 tools/dropin_probe.py > gpurun_out/${T}_dropin_prof.log 2>&1 || { tail -5 gpurun_out/${T}_dropin_prof.log; exit 1; }
+find gpurun_out/${T}_dropin_prof -name "*stats.csv" | while read f; do echo "== $f"; head -12 "$f"; done

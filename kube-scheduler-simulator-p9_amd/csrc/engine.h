@@ -131,7 +131,9 @@ class Engine {
   // Append one program (drop-in cycle API); its index is the previous count.
   bool append_program(const std::vector<uint8_t>& prog, std::string& err);
   // Reserve (sign +1) / Unreserve (sign -1) program q on global node gnode.
-  bool assume(uint32_t q, int32_t gnode, int sign, std::string& err);
+  // (wait = false: the launch is queued and the call returns; a later sync
+  // reports any device error)
+  bool assume(uint32_t q, int32_t gnode, int sign, std::string& err, bool wait = true);
   // Cluster events applied in place, one k_assume per op in stream order, one sync:
   // bound pod progs[i] added on (sign +1) / removed from (sign -1) global node
   // gnode[i] (nodes outside this shard are ignored).  rows[] holds one existing-pod

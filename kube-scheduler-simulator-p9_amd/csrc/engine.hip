@@ -795,6 +795,11 @@ __global__ void k_init_summaries(ksg_pod_summary* sum, uint32_t count, DevProfil
   sum[i] = s;
 }
 
+// append_program's placement of one staged [PodLite | program] block.
+__global__ void k_place_program(const uint8_t* __restrict__ src, uint32_t bytes, uint8_t* dst, uint64_t* off_slot,
+                                uint64_t off, void* plite_slot, int32_t* prow_slot, int32_t row, ksg_pod_summary* sum,
+                                DevProfile F);
+
 __global__ void k_begin(DevCluster C, DevScratch S, const uint8_t* __restrict__ prog) {
   ProgView V = view(prog);
   uint32_t ntsc = (uint32_t)(V.h->n_tsc_filter + V.h->n_tsc_score);
@@ -2277,6 +2282,26 @@ struct PodLite {  // the fields of ksg_prog the Fit/BA evaluation reads (LDS-sta
   int32_t queue_idx;
   uint32_t flags;
 };
+
+__global__ void k_place_program(const uint8_t* __restrict__ src, uint32_t bytes, uint8_t* dst, uint64_t* off_slot,
+                                uint64_t off, void* plite_slot, int32_t* prow_slot, int32_t row, ksg_pod_summary* sum,
+                                DevProfile F) {
+  const uint32_t t = threadIdx.x;
+  const uint8_t* prog = src + sizeof(PodLite);
+  for (uint32_t i = t; i < bytes; i += blockDim.x) dst[i] = prog[i];
+  for (uint32_t i = t; i < (uint32_t)sizeof(PodLite); i += blockDim.x) reinterpret_cast<uint8_t*>(plite_slot)[i] = src[i];
+  if (t == 0) {
+    *off_slot = off;
+    *prow_slot = row;
+    ksg_pod_summary z = {};
+    z.selected = -1;
+    for (int p = 0; p < KSG_MAX_PLUGINS; ++p) {
+      z.max_score[p] = (p < F.n && F.plugins[p] == KP_IPA) ? INT64_MIN : 0;
+      z.min_score[p] = INT64_MAX;
+    }
+    *sum = z;
+  }
+}
 
 struct WinArgs {
   const PodLite* plite;  // Fit/BA fields of every queue pod (flat copy of the programs)
@@ -5033,6 +5058,10 @@ struct Engine::Impl {
   uint32_t pcap = 0, pkeys = 0, tcap = 0, rcap = 0, vcap = 0;
   DBuf<uint8_t> evprog;  // cluster events applied in place: the bound pod's program
   DBuf<int32_t> evrow;   // its existing-pod table row
+  uint8_t* apstage = nullptr;  // append_program: pinned staging block (apstage_ev: its last copy)
+  size_t apstage_cap = 0;
+  hipEvent_t apstage_ev = nullptr;
+  DBuf<uint8_t> apdev;
   // toggle_stage / toggle_staged: the staged candidate victims
   DBuf<uint8_t> tgprog;
   DBuf<uint64_t> tgoff;
@@ -5247,6 +5276,8 @@ Engine::~Engine() {
   if (p_->hps) (void)hipHostFree(p_->hps);
   if (p_->hpr) (void)hipHostFree(p_->hpr);
   if (p_->hverdict) (void)hipHostFree(p_->hverdict);
+  if (p_->apstage) (void)hipHostFree(p_->apstage);
+  if (p_->apstage_ev) (void)hipEventDestroy(p_->apstage_ev);
   if (p_->ev0) (void)hipEventDestroy(p_->ev0);
   if (p_->ev1) (void)hipEventDestroy(p_->ev1);
   for (hipEvent_t e : {p_->sev_ready[0], p_->sev_ready[1], p_->sev_ready[2], p_->sev_free})
@@ -6249,14 +6280,35 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
     return false;
   const uint64_t off64 = off;
   const PodLite pl = pod_lite(prog);
-  const int32_t none = -1;
-  HIPCHK(hipMemcpyAsync(I.progs.p + off, prog.data(), prog.size(), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(I.prog_off_d.p + q, &off64, sizeof(off64), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(I.plite.p + q, &pl, sizeof(pl), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(I.prow.p + q, &none, sizeof(none), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_init_summaries, dim3(1), dim3(256), 0, s, I.sums.p + q, 1u, I.F);
+  // One pinned staging block [PodLite | program] -> one copy, and one kernel that
+  // places it (program, offset, PodLite, table row, fresh summary): no wait here.
+  // The block is reused once its previous copy has completed (an event).
+  const size_t sbytes = sizeof(PodLite) + prog.size();
+  if (!I.apstage || I.apstage_cap < sbytes) {
+    if (I.apstage) {
+      HIPCHK(hipEventSynchronize(I.apstage_ev));
+      (void)hipHostFree(I.apstage);
+      I.apstage = nullptr;
+    }
+    I.apstage_cap = std::max<size_t>(sbytes, 64 << 10);
+    if (hipHostMalloc((void**)&I.apstage, I.apstage_cap, hipHostMallocDefault) != hipSuccess) {
+      I.apstage = nullptr;
+      I.apstage_cap = 0;
+      err = "hipHostMalloc: program staging";
+      return false;
+    }
+    if (!I.apstage_ev) HIPCHK(hipEventCreateWithFlags(&I.apstage_ev, hipEventDisableTiming));
+  } else {
+    HIPCHK(hipEventSynchronize(I.apstage_ev));  // (the previous append's copy: long done)
+  }
+  if (!I.apdev.grow(sbytes, 0, s, err)) return false;
+  std::memcpy(I.apstage, &pl, sizeof(pl));
+  std::memcpy(I.apstage + sizeof(PodLite), prog.data(), prog.size());
+  HIPCHK(hipMemcpyAsync(I.apdev.p, I.apstage, sbytes, hipMemcpyHostToDevice, s));
+  HIPCHK(hipEventRecord(I.apstage_ev, s));
+  hipLaunchKernelGGL(k_place_program, dim3(1), dim3(256), 0, s, I.apdev.p, (uint32_t)prog.size(), I.progs.p + off,
+                     I.prog_off_d.p + q, off64, (void*)(I.plite.p + q), I.prow.p + q, (int32_t)-1, I.sums.p + q, I.F);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s));  // the host sources above are stack / caller buffers
   I.prog_bytes = off + prog.size();
   I.prog_off.push_back(off);
   if (!na_weights_fit(prog)) I.static_fits = false;
@@ -6267,7 +6319,7 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
   return true;
 }
 
-bool Engine::assume(uint32_t q, int32_t gnode, int sign, std::string& err) {
+bool Engine::assume(uint32_t q, int32_t gnode, int sign, std::string& err, bool wait) {
   Impl& I = *p_;
   if (!tables_ready(I, err)) return false;
   if (q >= I.prog_off.size()) { err = "program index out of range"; return false; }
@@ -6275,7 +6327,7 @@ bool Engine::assume(uint32_t q, int32_t gnode, int sign, std::string& err) {
   hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, I.stream, C, I.progs.p + I.prog_off[q], gnode, sign,
                      (I.has_pts || I.has_ipa) ? 1 : 0, I.prow.p + q);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (wait) HIPCHK(hipStreamSynchronize(I.stream));
   return true;
 }
 

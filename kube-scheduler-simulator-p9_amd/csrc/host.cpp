@@ -2907,6 +2907,7 @@ struct Cluster {
   // remap: old node index -> new index, when nodes were removed (cluster events).
   // given: the queue's summaries (compaction re-indexes the queue), else read from the device
   bool rebuild(const vector<int32_t>* remap = nullptr, const vector<ksg_pod_summary>* given = nullptr) {
+    room_ok = false;
     track_queue();
     size_t nq = queue.size();
     const size_t ns = given ? given->size() : compiled ? progs.size() : 0;  // pods with summaries on the device
@@ -3059,9 +3060,11 @@ struct Cluster {
       meta.push_back(std::move(m));
       prog_cls.resize(progs.size(), {(uint32_t)pcls.size(), (uint32_t)tcls.size()});
     }
+    if (commit) room_ok = false;
     if (commit && !room_for(q)) return false;
-    if (!eng->keep_outputs(q, 1, err) || !eng->run_queue(q, 1, commit, err) || !eng->sync(err) ||
-        !eng->summaries(q, 1, &out, err))
+    // (the summary's copy waits for the run; sync then only checks the run's state)
+    if (!eng->keep_outputs(q, 1, err) || !eng->run_queue(q, 1, commit, err) || !eng->summaries(q, 1, &out, err) ||
+        !eng->sync(err))
       return false;
     if (!preempt(q, out)) return false;  // PostFilter of an unschedulable pod
     if (commit && out.status == 0) {
@@ -3072,13 +3075,28 @@ struct Cluster {
   }
   // The device appends assumed pods to its existing-pod table: before an assume,
   // make room for queue pod q's row in place (capacities doubled, contents kept).
-  bool room_for(uint32_t q) {
+  // room_ok: the device's table use is known on the host (room_used, an upper
+  // bound) — set by a query from the drop-in Reserve path, whose own appends it
+  // counts, and cleared by every other entry point that may append or re-upload
+  // (the C API calls and rebuild()), so back-to-back Reserves skip the read-back.
+  bool room_ok = false;
+  uint64_t room_used[4] = {0, 0, 0, 0}, room_cap[4] = {0, 0, 0, 0};
+  bool room_for(uint32_t q, bool cached = false) {
     if (!tables_on()) return true;
     uint64_t need[4] = {0, 0, 0, 0};
     queue_need(q, need);
-    return ensure_room(need);
+    return ensure_room(need, cached);
   }
-  bool ensure_room(const uint64_t need[4]) {
+  bool ensure_room(const uint64_t need[4], bool cached = false) {
+    if (cached && room_ok) {
+      bool fits = true;
+      for (int i = 0; i < 4; ++i) fits &= room_used[i] + need[i] <= room_cap[i];
+      if (fits) {
+        for (int i = 0; i < 4; ++i) room_used[i] += need[i];
+        return true;
+      }
+    }
+    room_ok = false;
     uint32_t used[4], cap[4];
     if (!eng->table_room(used, cap, err)) return false;
     bool fits = true;
@@ -3088,7 +3106,15 @@ struct Cluster {
       fits &= want <= cap[i];
       nc[i] = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * cap[i], want + 1024), UINT32_MAX);
     }
-    return fits || eng->grow_table(nc[0], nc[1], nc[2], nc[3], 0, err);
+    if (!fits) return eng->grow_table(nc[0], nc[1], nc[2], nc[3], 0, err);
+    if (cached) {
+      for (int i = 0; i < 4; ++i) {
+        room_used[i] = (uint64_t)used[i] + need[i];
+        room_cap[i] = cap[i];
+      }
+      room_ok = true;
+    }
+    return true;
   }
   // ------------------------------------------------------------ DefaultPreemption
   // PostFilter of an unschedulable pod, as a dry run on the device state of the
@@ -3394,7 +3420,8 @@ struct Cluster {
     track_queue();
     if (q >= queue.size() || qmode[q] != 2 || placed[q] >= 0) { err = "reserve: pod not in an uncommitted cycle"; return false; }
     if (node < 0 || node >= (int32_t)nodes.size()) { err = "reserve: node out of range"; return false; }
-    if (!refresh_program(q) || !room_for(q) || !eng->assume(q, node, +1, err)) return false;
+    // (no wait for the assume: every later call is ordered behind it on the stream)
+    if (!refresh_program(q) || !room_for(q, true) || !eng->assume(q, node, +1, err, false)) return false;
     placed[q] = node;
     assumed_in[q] = epoch;
     return true;
@@ -4224,6 +4251,7 @@ int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len) {
   KSG_LOCK(ctx);
   if (!ctx || !json) return KSG_E_INVALID;
   ctx->c.out_gen++;
+  ctx->c.room_ok = false;  // (room_ok: see Cluster::ensure_room)
   try {
     Cluster& c = ctx->c;
     // fix the engine's global node offset for this shard before upload
@@ -4255,6 +4283,7 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
+  ctx->c.room_ok = false;  // (room_ok: see Cluster::ensure_room)
   Cluster& c = ctx->c;
   if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
   if (c.shards != 1 && c.eng->exchange_ranks() != c.shards)
@@ -4292,6 +4321,7 @@ int ksg_compact(ksg_ctx* ctx, uint32_t keep_from) {
   KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
+  ctx->c.room_ok = false;  // (room_ok: see Cluster::ensure_room)
   if (!ctx->c.compact(keep_from)) return ctx->fail(ctx->c.err, KSG_E_STATE);
   return KSG_OK;
 }
@@ -4300,6 +4330,7 @@ int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
+  ctx->c.room_ok = false;  // (room_ok: see Cluster::ensure_room)
   Cluster& c = ctx->c;
   if (first + count > c.queue.size()) return ctx->fail("queue range", KSG_E_RANGE);
   if (c.shards != 1 && c.eng->exchange_ranks() != c.shards)
@@ -4398,6 +4429,7 @@ int ksg_reset(ksg_ctx* ctx) {
   KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
+  ctx->c.room_ok = false;  // (room_ok: see Cluster::ensure_room)
   if (ctx->c.inplace_dirty)
     return ctx->fail("reset after in-place cluster events: reload the cluster (ksg_load_cluster)", KSG_E_STATE);
   if (!ctx->c.compile_queue()) return ctx->fail(ctx->c.err, KSG_E_INVALID);
@@ -4526,6 +4558,7 @@ int ksg_unreserve(ksg_ctx* ctx, uint32_t q) {
   KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
+  ctx->c.room_ok = false;  // (room_ok: see Cluster::ensure_room)
   if (!ctx->c.unreserve(q)) return ctx->fail(ctx->c.err, KSG_E_STATE);
   return KSG_OK;
 }
@@ -4534,6 +4567,7 @@ int ksg_apply_events(ksg_ctx* ctx, const char* events_json, size_t len) {
   KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
+  ctx->c.room_ok = false;  // (room_ok: see Cluster::ensure_room)
   if (!ctx || !events_json) return KSG_E_INVALID;
   try {
     if (!ctx->c.apply_events(events_json, len)) return ctx->fail(ctx->c.err, KSG_E_STATE);

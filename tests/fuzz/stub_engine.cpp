@@ -92,7 +92,7 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
   p_->sums.push_back(ksg_pod_summary{});
   return true;
 }
-bool Engine::assume(uint32_t q, int32_t gnode, int, std::string& err) {
+bool Engine::assume(uint32_t q, int32_t gnode, int, std::string& err, bool) {
   if (q >= p_->progs.size() || gnode < 0) { err = "stub: assume range"; return false; }
   return true;
 }

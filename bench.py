@@ -345,6 +345,9 @@ def main():
         kname = "k_filter_score"
         bytes_per_launch = shard * algorithmic_bytes_per_node_fit_ba()
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    traffic = pmc_traffic(kname)
+    if persistent and traffic is not None:
+        traffic /= nwin  # (the PMC pass counts the whole-queue launch: per window, like bytes_per_launch)
     if rank != 0:
         return
     out = {
@@ -364,7 +367,7 @@ def main():
                    "nodes_per_gpu": shard, "nodes_total": n_nodes, "pods": n_pods, "parallelism": f"node-shard x{world} (RCCL all-gather per 32-pod batch)" if world > 1 else "1 GPU"},
         "scheduled_pods_per_s": scheduled * a.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(kname),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kname, "kernel_avg_us": kernel_ms * 1e3, "kernel_samples": kcount,
                      "bytes_per_launch": bytes_per_launch,
                      **({"note": "k_window_run: the whole queue in one persistent launch; kernel_avg_us and "

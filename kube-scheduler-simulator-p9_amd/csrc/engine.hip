@@ -5150,6 +5150,7 @@ struct Engine::Impl {
   DBuf<WinSync> wsync;           // k_window_run's counters (zeroed per launch)
   int win_run_on = 1;            // persistent window loop (k_window_run): KSG_WIN_RUN=0 turns it off
   int win_mblocks = 0;           // ... with dedicated merge blocks (KSG_WIN_MB=1; the last tile block merges: measured faster)
+  int view_copy = 0;             // cycle view: 1 = the per-node arrays by a copy (KSG_VIEW_COPY), 0 = written by k_view
   int win_pfix = 0;              // ... the replay evaluates the prior step itself (KSG_WIN_PFIX=1; measured slower)
   uint64_t win_runs = 0, win_fallbacks = 0;  // diagnostic: persistent window launches / not co-resident
   uint32_t fold_blocks = 256;  // table chain: k_fold above this many blocks (KSG_FOLD_BLOCKS; tests force it)
@@ -5304,6 +5305,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (const char* e = std::getenv("KSG_WIN_RUN")) I.win_run_on = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_MB")) I.win_mblocks = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_PFIX")) I.win_pfix = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_VIEW_COPY")) I.view_copy = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_RUN_SPIN")) I.run_spin = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("KSG_RUN_WAIT_US"))
     I.run_wait_us = std::max<uint32_t>(10, std::min<uint32_t>(1000000, (uint32_t)std::strtoul(e, nullptr, 10)));
@@ -6791,11 +6793,19 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
     I.vblk_fresh = false;
   }
   if (!N) HIPCHK(hipMemcpyAsync(I.vblk.p + lay.off_sum, I.sums.p + j, sizeof(ksg_pod_summary), hipMemcpyDeviceToDevice, s));
+  // the per-node arrays straight into the caller's pinned block when the device
+  // can address it (one kernel, then only the slot table and summary are copied)
+  uint8_t* hdev = nullptr;
+  if (N && !I.view_copy && hipHostGetDevicePointer((void**)&hdev, host, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    hdev = nullptr;
+  }
   if (N)
     hipLaunchKernelGGL(k_view, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, I.cluster(), I.F, I.progs.p + I.prog_off[j],
-                       I.sums.p + j, I.kfilter.p + k * N, I.kscore.p + k * N * KSG_MAX_PLUGINS, V, I.vblk.p);
+                       I.sums.p + j, I.kfilter.p + k * N, I.kscore.p + k * N * KSG_MAX_PLUGINS, V, I.vblk.p,
+                       hdev ? hdev : I.vblk.p);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(host, I.vblk.p, lay.bytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(host, I.vblk.p, hdev ? lay.off_fail_pos : lay.bytes, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   return true;
 }

@@ -2141,8 +2141,12 @@ __device__ __forceinline__ uint32_t view_slot(unsigned long long* tab, uint32_t 
   atomicMax(&tab[kViewSlots], (unsigned long long)gen << 32);  // overflow (the host renders the view itself)
   return kViewSlots;
 }
+// out: the device block (slot table, summary); hout: where the per-node arrays go —
+// the host's pinned block itself (written over the link by this kernel, no copy
+// launch after it) or out.
 __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const uint8_t* prog, const ksg_pod_summary* sum,
-                                              const uint32_t* filter, const int32_t* score, ViewDev V, uint8_t* out) {
+                                              const uint32_t* filter, const int32_t* score, ViewDev V, uint8_t* out,
+                                              uint8_t* hout) {
   const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = n < C.N;
   const ProgView PV = view(prog);
@@ -2188,11 +2192,11 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
     }
   }
   if (!act) return;
-  reinterpret_cast<int8_t*>(out + V.off_fail_pos)[n] = (int8_t)fp;
-  reinterpret_cast<int8_t*>(out + V.off_fail_code)[n] = (int8_t)fc;
-  reinterpret_cast<uint16_t*>(out + V.off_fail_msg)[n] = (uint16_t)msg;
-  int32_t* raw = reinterpret_cast<int32_t*>(out + V.off_raw);
-  int32_t* norm = reinterpret_cast<int32_t*>(out + V.off_norm);
+  reinterpret_cast<int8_t*>(hout + V.off_fail_pos)[n] = (int8_t)fp;
+  reinterpret_cast<int8_t*>(hout + V.off_fail_code)[n] = (int8_t)fc;
+  reinterpret_cast<uint16_t*>(hout + V.off_fail_msg)[n] = (uint16_t)msg;
+  int32_t* raw = reinterpret_cast<int32_t*>(hout + V.off_raw);
+  int32_t* norm = reinterpret_cast<int32_t*>(hout + V.off_norm);
   const bool feasible = code == KSG_FILTER_PASS;
   const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
   bool pts_keys = false, pk_done = false;

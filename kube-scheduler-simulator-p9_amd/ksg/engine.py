@@ -55,7 +55,17 @@ class CycleView:
         r = v.result
         self.result = PodResult(r.selected, r.feasible, r.status, r.total)
         self._v = v
-        self.messages = [v.messages[i].decode() for i in range(v.n_messages)]
+        self._msgs = None  # (decoded on first use: most of the slots are empty)
+
+    @property
+    def messages(self):
+        if self._msgs is None:
+            v = self._v
+            self._msgs = [v.messages[i].decode() for i in range(v.n_messages)]
+        return self._msgs
+
+    def message(self, k):
+        return self._v.messages[k].decode() if self._msgs is None else self._msgs[k]
 
     def release(self):
         if self._p:
@@ -78,13 +88,13 @@ class CycleView:
             return -1, ""
         if pos < fp:
             return 0, ""
-        return v.fail_code[i], self.messages[v.fail_msg[i]]
+        return v.fail_code[i], self.message(v.fail_msg[i])
 
     def prefilter_status(self, pos):
-        return self._v.prefilter_code[pos], self.messages[self._v.prefilter_msg[pos]]
+        return self._v.prefilter_code[pos], self.message(self._v.prefilter_msg[pos])
 
     def prescore_status(self, pos):
-        return self._v.prescore_code[pos], self.messages[self._v.prescore_msg[pos]]
+        return self._v.prescore_code[pos], self.message(self._v.prescore_msg[pos])
 
     def scores(self, pos):
         p = self._v.score[pos]

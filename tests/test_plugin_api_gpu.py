@@ -210,13 +210,17 @@ class _ViewCalls:
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("copy", ["0", "1"], ids=["direct", "copy"])
 @pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
-def test_cycle_view_matches_extension_point_calls(name, c, sizes):
+def test_cycle_view_matches_extension_point_calls(monkeypatch, name, c, sizes, copy):
     """ksg_cycle_view (include/ksg.h): the arrays the framework's 16 parallel
     Filter / Score workers index instead of calling the library per node.  Every
     annotation rebuilt from a view equals the oracle's; 16 threads rebuilding from
-    one view agree; a view is unchanged by the cycles that follow it."""
+    one view agree; a view is unchanged by the cycles that follow it.  Per-node
+    arrays written by the view kernel into the pinned block, or copied after it
+    (KSG_VIEW_COPY=1)."""
     from concurrent.futures import ThreadPoolExecutor
+    monkeypatch.setenv("KSG_VIEW_COPY", copy)
     doc = g.generate(c, **sizes)
     o = Oracle(doc)
     o.schedule(record=3)

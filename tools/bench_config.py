@@ -60,7 +60,8 @@ def main():
     out = {"config": a.config, "nodes": n, "pods_timed": q - warm, "existing_pods": len(doc["pods"]),
            "profile": doc["profile"]["plugins"], "path": "window" if s.batch_path else "per-pod chain",
            "pairs_per_s": n * (q - warm) / dt, "pods_per_s": (q - warm) / dt, "us_per_pod": dt * 1e6 / (q - warm),
-           "scheduled": sum(1 for r in res if r.status == 0), "sampled_kernel_us": kms * 1e3, "samples": ks}
+           "scheduled": sum(1 for r in res if r.status == 0), "sampled_kernel_us": kms * 1e3, "samples": ks,
+           "run_counts": list(s.run_counts())}  # (persistent-segment pods, segments) over both passes
     if a.cpu_pods:
         from _oracle import Oracle
         o = Oracle(blob)

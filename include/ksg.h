@@ -46,8 +46,9 @@ extern "C" {
  * stalled refuses calls (KSG_E_STATE) until ksg_load_cluster.  Bindings check
  * ksg_abi_version() >= the version they were written against.  3: ksg_cycle_view
  * holds the Filter outcome once per node (fail_pos / fail_code / fail_msg) and
- * 32-bit scores per position, built on the device. */
-#define KSG_ABI_VERSION 3
+ * 32-bit scores per position, built on the device.  4: its score rows are as
+ * narrow as their values allow (score_bytes / normalized_bytes; ksg_view_score). */
+#define KSG_ABI_VERSION 4
 
 #define KSG_OK 0
 #define KSG_E_INVALID (-1)   /* bad argument / JSON */
@@ -293,8 +294,11 @@ int ksg_postfilter_result(ksg_ctx* ctx, uint32_t q, int32_t* nominated, char* bu
  *   Success (0)                    if pos < fail_pos[i]  (fail_pos[i] == n_positions: passed every filter)
  *   fail_code[i], messages[fail_msg[i]]   if pos == fail_pos[i]
  * Codes are framework.Code values (as ksg_filter_status).  score[pos] /
- * normalized[pos] point at n_nodes values (NULL: no device Score at pos), valid
- * where the node passed every filter; normalized[pos] == score[pos] for plugins
+ * normalized[pos] point at n_nodes signed little-endian integers of
+ * score_bytes[pos] / normalized_bytes[pos] bytes each (1, 2 or 4: the narrowest
+ * width the cycle's values need, so fewer bytes cross the host link; read them
+ * with ksg_view_score), NULL when there is no device Score at pos; valid where
+ * the node passed every filter; normalized[pos] == score[pos] for plugins
  * without ScoreExtensions.  A view stays valid, unchanged, until
  * ksg_cycle_view_release, whatever the context does meanwhile (later cycles,
  * Reserve, events, ksg_destroy); release needs no context and may run on any
@@ -309,8 +313,10 @@ typedef struct ksg_cycle_view {
   const int8_t* fail_pos;              /* [node] first failing position; n_positions: passed; -1: not evaluated */
   const int8_t* fail_code;             /* [node] framework code of that failure */
   const uint16_t* fail_msg;            /* [node] its Status.Message(): index into messages */
-  const int32_t* const* score;         /* [pos] -> [node] raw Score, or NULL */
-  const int32_t* const* normalized;    /* [pos] -> [node] NormalizeScore output, or NULL */
+  const void* const* score;            /* [pos] -> [node] raw Score (score_bytes[pos] each), or NULL */
+  const void* const* normalized;       /* [pos] -> [node] NormalizeScore output, or NULL */
+  const uint8_t* score_bytes;          /* [pos] width of score[pos]'s values: 1, 2 or 4 */
+  const uint8_t* normalized_bytes;     /* [pos] width of normalized[pos]'s values */
   const int8_t* prefilter_code;        /* [pos] PreFilter code (ksg_prefilter_status) */
   const uint16_t* prefilter_msg;       /* [pos] its message index */
   const int8_t* prescore_code;         /* [pos] PreScore code (ksg_prescore_status) */
@@ -319,6 +325,15 @@ typedef struct ksg_cycle_view {
   uint32_t n_messages;
   const void* owner;                   /* library-private */
 } ksg_cycle_view;
+/* The raw (normalized == 0) or normalized score of position pos on local node i. */
+static inline int64_t ksg_view_score(const ksg_cycle_view* v, uint32_t pos, uint32_t i, int normalized) {
+  const void* row = normalized ? v->normalized[pos] : v->score[pos];
+  const uint8_t w = normalized ? v->normalized_bytes[pos] : v->score_bytes[pos];
+  if (!row) return 0;
+  if (w == 1) return ((const int8_t*)row)[i];
+  if (w == 2) return ((const int16_t*)row)[i];
+  return ((const int32_t*)row)[i];
+}
 /* Snapshot the kept outputs of queue pod q (the pod of the last ksg_cycle, or a
  * ksg_keep_outputs range) into a view. */
 int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out);

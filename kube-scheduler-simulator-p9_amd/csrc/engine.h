@@ -207,11 +207,19 @@ class Engine {
     bool dev_vol[KSG_MAX_PLUGINS] = {};     // the device position is a volume run
     int kind[KSG_MAX_PROFILE] = {};         // Filter failure code: 0 unresolvable, 1 unschedulable, 2 Fit, 3 PTS, 4 IPA
   };
+  // the view block's score-row table (written by the view: offsets in the block,
+  // value widths; index d: raw row of device position d, KSG_MAX_PLUGINS + r:
+  // normalized row r)
+  struct ViewRows {
+    uint32_t off[2 * KSG_MAX_PLUGINS];
+    uint8_t bytes[2 * KSG_MAX_PLUGINS];
+  };
   struct ViewLayout {
     uint32_t N = 0, n_raw = 0, n_norm = 0, n_slots = 0;
     mutable uint32_t gen = 0;  // set by view(): live slot entries are gen << 32 | code
     size_t off_sum = 0;        // the pod's summary
     int norm_row[KSG_MAX_PLUGINS] = {};  // device position -> normalized row (-1: output == raw)
+    size_t off_rows = 0;       // its ViewRows (score rows start at off_raw, packed, 256-B aligned)
     size_t off_fail_pos = 0, off_fail_code = 0, off_fail_msg = 0, off_raw = 0, off_norm = 0, bytes = 0;
   };
   void view_layout(ViewLayout& lay) const;

@@ -6756,12 +6756,13 @@ void Engine::view_layout(ViewLayout& lay) const {
   }
   const size_t N = std::max<uint32_t>(I.N, 1);
   lay.off_sum = al256((kViewSlots + 1) * sizeof(uint64_t));
-  lay.off_fail_pos = lay.off_sum + al256(sizeof(ksg_pod_summary));
+  lay.off_rows = lay.off_sum + al256(sizeof(ksg_pod_summary));
+  lay.off_fail_pos = lay.off_rows + al256(sizeof(ViewRows));
   lay.off_fail_code = lay.off_fail_pos + al256(N);
   lay.off_fail_msg = lay.off_fail_code + al256(N);
   lay.off_raw = lay.off_fail_msg + al256(2 * N);
-  lay.off_norm = lay.off_raw + al256(4 * N * lay.n_raw);
-  lay.bytes = lay.off_norm + 4 * N * lay.n_norm;
+  lay.off_norm = lay.off_raw + al256(4 * N) * lay.n_raw;  // (the widest layout: every row 4 bytes)
+  lay.bytes = lay.off_norm + al256(4 * N) * lay.n_norm;
 }
 bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err) {
   Impl& I = *p_;
@@ -6786,13 +6787,18 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
   V.off_fail_msg = (uint32_t)lay.off_fail_msg;
   V.off_raw = (uint32_t)lay.off_raw;
   V.off_norm = (uint32_t)lay.off_norm;
+  V.off_rows = (uint32_t)lay.off_rows;
+  V.n_norm = lay.n_norm;
   const size_t N = I.N, k = j - I.keep_first;
   hipStream_t s = I.stream;
   if (I.vblk_fresh) {  // a new block: generation 0 everywhere
     HIPCHK(hipMemsetAsync(I.vblk.p, 0, (kViewSlots + 1) * sizeof(uint64_t), s));
     I.vblk_fresh = false;
   }
-  if (!N) HIPCHK(hipMemcpyAsync(I.vblk.p + lay.off_sum, I.sums.p + j, sizeof(ksg_pod_summary), hipMemcpyDeviceToDevice, s));
+  if (!N) {
+    HIPCHK(hipMemcpyAsync(I.vblk.p + lay.off_sum, I.sums.p + j, sizeof(ksg_pod_summary), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemsetAsync(I.vblk.p + lay.off_rows, 0, sizeof(ViewRows), s));
+  }
   // the per-node arrays straight into the caller's pinned block when the device
   // can address it (one kernel, then only the slot table and summary are copied)
   uint8_t* hdev = nullptr;

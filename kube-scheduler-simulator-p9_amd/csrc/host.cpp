@@ -4761,7 +4761,8 @@ struct CycleView {
   std::vector<uint8_t> called;
   std::vector<int8_t> pfcode, pscode;
   std::vector<uint16_t> pfmsg, psmsg;
-  std::vector<const int32_t*> sptr, nptr;
+  std::vector<const void*> sptr, nptr;
+  std::vector<uint8_t> sbytes, nbytes;
   std::vector<std::string> msgs;
   std::vector<const char*> mptr;
   std::unordered_map<std::string, uint16_t> mid;
@@ -4836,11 +4837,13 @@ int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out)
   v->psmsg.assign(P, 0);
   v->sptr.assign(P, nullptr);
   v->nptr.assign(P, nullptr);
+  v->sbytes.assign(P, 4);
+  v->nbytes.assign(P, 4);
+  ksg::Engine::ViewRows rows;
+  std::memcpy(&rows, v->block + lay.off_rows, sizeof(rows));
   std::string m;
   const ksg::host::PodMeta& pm = c.meta[q];
   const uint32_t skip_f = c.skip_filter_mask(pm, S);
-  const int32_t* raw = reinterpret_cast<const int32_t*>(v->block + lay.off_raw);
-  const int32_t* norm = reinterpret_cast<const int32_t*>(v->block + lay.off_norm);
   for (uint32_t pos = 0; pos < P; ++pos) {
     v->pfcode[pos] = (int8_t)c.prefilter_status(q, (int)pos, S, m);
     v->pfmsg[pos] = v->intern(m);
@@ -4849,9 +4852,12 @@ int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out)
     v->called[pos] = ksg::host::has_filter(c.plugins[pos]) && pm.prefilter_fail_pos < 0 &&
                      !c.filter_skipped(pm, skip_f, (int)pos) ? 1 : 0;
     const int d = c.dpos[pos];
-    if (d < 0) continue;
-    v->sptr[pos] = raw + (size_t)d * N;
-    v->nptr[pos] = lay.norm_row[d] >= 0 ? norm + (size_t)lay.norm_row[d] * N : v->sptr[pos];
+    if (d < 0 || !rows.bytes[d]) continue;
+    v->sptr[pos] = v->block + rows.off[d];
+    v->sbytes[pos] = rows.bytes[d];
+    const int r = lay.norm_row[d];
+    v->nptr[pos] = r >= 0 ? (const void*)(v->block + rows.off[KSG_MAX_PLUGINS + r]) : v->sptr[pos];
+    v->nbytes[pos] = r >= 0 ? rows.bytes[KSG_MAX_PLUGINS + r] : v->sbytes[pos];
   }
   for (auto& x : v->msgs) v->mptr.push_back(x.c_str());
   ksg_cycle_view& p = v->pub;
@@ -4871,6 +4877,8 @@ int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out)
   p.fail_msg = fail_msg;
   p.score = v->sptr.data();
   p.normalized = v->nptr.data();
+  p.score_bytes = v->sbytes.data();
+  p.normalized_bytes = v->nbytes.data();
   p.prefilter_code = v->pfcode.data();
   p.prefilter_msg = v->pfmsg.data();
   p.prescore_code = v->pscode.data();

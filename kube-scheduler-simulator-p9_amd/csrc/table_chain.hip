@@ -2123,7 +2123,38 @@ struct ViewDev {
   int32_t n_profile;
   uint32_t gen;  // this view's generation: a slot (or the overflow word) holds gen << 32 | code
   uint32_t off_sum, off_fail_pos, off_fail_code, off_fail_msg, off_raw, off_norm;  // byte offsets in the block
+  uint32_t off_rows, n_norm;  // the score-row table (Engine::ViewRows); normalized rows
 };
+// Score-row widths of a view, the same in every thread: 1 byte for the rows whose
+// values are within [0, 100] by construction when the cycle has no Score error
+// (Fit and BalancedAllocation raw, every normalized row), else 4; rows packed
+// from off_raw, each 256-B aligned.  (Values of nodes that failed a filter are
+// unspecified in the view: clamped.)
+__device__ __forceinline__ void view_rows(const DevProfile& F, const ViewDev& V, const ksg_pod_summary* sum, uint32_t N,
+                                          Engine::ViewRows& R) {
+  const bool err = sum->status == 2;
+  uint32_t off = V.off_raw;
+  auto al = [](uint32_t x) { return (x + 255u) & ~255u; };
+  for (int d = 0; d < 2 * KSG_MAX_PLUGINS; ++d) {
+    R.off[d] = 0;
+    R.bytes[d] = 0;
+  }
+  for (int d = 0; d < F.n; ++d) {
+    const bool narrow = !err && (F.plugins[d] == KP_FIT || F.plugins[d] == KP_BA);
+    R.bytes[d] = narrow ? 1 : 4;
+    R.off[d] = off;
+    off += al(N * R.bytes[d]);
+  }
+  for (uint32_t r = 0; r < V.n_norm; ++r) {
+    R.bytes[KSG_MAX_PLUGINS + r] = err ? 4 : 1;
+    R.off[KSG_MAX_PLUGINS + r] = off;
+    off += al(N * R.bytes[KSG_MAX_PLUGINS + r]);
+  }
+}
+__device__ __forceinline__ void view_put(uint8_t* base, uint32_t off, uint8_t w, uint32_t n, int64_t v) {
+  if (w == 1) reinterpret_cast<int8_t*>(base + off)[n] = (int8_t)(v < -128 ? -128 : v > 127 ? 127 : v);
+  else reinterpret_cast<int32_t*>(base + off)[n] = (int32_t)v;
+}
 // slot of `code` in the table (entries of other generations count as empty: no clearing per view)
 __device__ __forceinline__ uint32_t view_slot(unsigned long long* tab, uint32_t gen, uint32_t code) {
   const unsigned long long want = ((unsigned long long)gen << 32) | code;
@@ -2191,18 +2222,19 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
       need = false;
     }
   }
+  Engine::ViewRows RW;
+  view_rows(F, V, sum, C.N, RW);
+  if (n == 0) *reinterpret_cast<Engine::ViewRows*>(out + V.off_rows) = RW;
   if (!act) return;
   reinterpret_cast<int8_t*>(hout + V.off_fail_pos)[n] = (int8_t)fp;
   reinterpret_cast<int8_t*>(hout + V.off_fail_code)[n] = (int8_t)fc;
   reinterpret_cast<uint16_t*>(hout + V.off_fail_msg)[n] = (uint16_t)msg;
-  int32_t* raw = reinterpret_cast<int32_t*>(hout + V.off_raw);
-  int32_t* norm = reinterpret_cast<int32_t*>(hout + V.off_norm);
   const bool feasible = code == KSG_FILTER_PASS;
   const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
   bool pts_keys = false, pk_done = false;
   for (int pos = 0; pos < F.n; ++pos) {
     const int32_t s = score[(size_t)pos * C.N + n];
-    raw[(size_t)pos * C.N + n] = s;
+    view_put(hout, RW.off[pos], RW.bytes[pos], n, s);
     const int r = V.norm_row[pos];
     if (r < 0) continue;
     int64_t v = 0;
@@ -2214,6 +2246,6 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
       bool use;
       v = normalize_pos(F.plugins[pos], h, s, sum->max_score[pos], sum->min_score[pos], sum->ipa_flags, pts_keys, use);
     }
-    norm[(size_t)r * C.N + n] = (int32_t)v;
+    view_put(hout, RW.off[KSG_MAX_PLUGINS + r], RW.bytes[KSG_MAX_PLUGINS + r], n, v);
   }
 }

@@ -35,8 +35,8 @@ class _CycleView(ctypes.Structure):
                 ("filter_called", ctypes.POINTER(ctypes.c_uint8)),
                 ("fail_pos", ctypes.POINTER(ctypes.c_int8)), ("fail_code", ctypes.POINTER(ctypes.c_int8)),
                 ("fail_msg", ctypes.POINTER(ctypes.c_uint16)),
-                ("score", ctypes.POINTER(ctypes.POINTER(ctypes.c_int32))),
-                ("normalized", ctypes.POINTER(ctypes.POINTER(ctypes.c_int32))),
+                ("score", ctypes.POINTER(ctypes.c_void_p)), ("normalized", ctypes.POINTER(ctypes.c_void_p)),
+                ("score_bytes", ctypes.POINTER(ctypes.c_uint8)), ("normalized_bytes", ctypes.POINTER(ctypes.c_uint8)),
                 ("prefilter_code", ctypes.POINTER(ctypes.c_int8)), ("prefilter_msg", ctypes.POINTER(ctypes.c_uint16)),
                 ("prescore_code", ctypes.POINTER(ctypes.c_int8)), ("prescore_msg", ctypes.POINTER(ctypes.c_uint16)),
                 ("messages", ctypes.POINTER(ctypes.c_char_p)), ("n_messages", ctypes.c_uint32),
@@ -96,13 +96,19 @@ class CycleView:
     def prescore_status(self, pos):
         return self._v.prescore_code[pos], self.message(self._v.prescore_msg[pos])
 
+    _WIDTH = {1: ctypes.c_int8, 2: ctypes.c_int16, 4: ctypes.c_int32}
+
+    def _row(self, p, w):
+        if not p:
+            return [0] * self.N
+        return list(ctypes.cast(p, ctypes.POINTER(self._WIDTH[w] * self.N)).contents)
+
     def scores(self, pos):
-        p = self._v.score[pos]
-        return [p[i] for i in range(self.N)] if p else [0] * self.N
+        """Raw scores of position pos (ksg_view_score: rows as narrow as their values)."""
+        return self._row(self._v.score[pos], self._v.score_bytes[pos])
 
     def normalized_scores(self, pos):
-        p = self._v.normalized[pos]
-        return [p[i] for i in range(self.N)] if p else [0] * self.N
+        return self._row(self._v.normalized[pos], self._v.normalized_bytes[pos])
 
 
 @dataclass

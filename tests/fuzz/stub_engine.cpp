@@ -306,11 +306,12 @@ void Engine::view_layout(ViewLayout& lay) const {
   for (int d = 0; d < KSG_MAX_PLUGINS; ++d) lay.norm_row[d] = -1;
   const size_t N = p_->N ? p_->N : 1;
   lay.off_sum = al256s(257 * 8);
-  lay.off_fail_pos = lay.off_sum + al256s(sizeof(ksg_pod_summary));
+  lay.off_rows = lay.off_sum + al256s(sizeof(ksg_pod_summary));
+  lay.off_fail_pos = lay.off_rows + al256s(sizeof(ViewRows));
   lay.off_fail_code = lay.off_fail_pos + al256s(N);
   lay.off_fail_msg = lay.off_fail_code + al256s(N);
   lay.off_raw = lay.off_fail_msg + al256s(2 * N);
-  lay.off_norm = lay.off_raw + al256s(4 * N * lay.n_raw);
+  lay.off_norm = lay.off_raw + al256s(4 * N) * lay.n_raw;
   lay.bytes = lay.off_norm;
 }
 bool Engine::view(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err) {
@@ -320,12 +321,18 @@ bool Engine::view(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
   std::memset(host, 0, lay.bytes);
   lay.gen = 1;
   std::memcpy(host + lay.off_sum, &o.summary, sizeof(o.summary));
+  ViewRows rows{};
+  for (uint32_t d = 0; d < lay.n_raw; ++d) {
+    rows.off[d] = (uint32_t)(lay.off_raw + al256s(4 * (size_t)(p_->N ? p_->N : 1)) * d);
+    rows.bytes[d] = 4;
+  }
+  std::memcpy(host + lay.off_rows, &rows, sizeof(rows));
   for (uint32_t i = 0; i < p_->N; ++i) {
     const uint32_t c = o.filter[i];
     reinterpret_cast<int8_t*>(host + lay.off_fail_pos)[i] =
         (int8_t)(c == KSG_FILTER_PASS ? cfg.n_profile : (c == KSG_FILTER_NOT_EVALUATED ? -1 : 0));
     for (uint32_t d = 0; d < lay.n_raw; ++d)
-      reinterpret_cast<int32_t*>(host + lay.off_raw)[(size_t)d * p_->N + i] = o.score[(size_t)d * p_->N + i];
+      reinterpret_cast<int32_t*>(host + rows.off[d])[i] = o.score[(size_t)d * p_->N + i];
   }
   return true;
 }

@@ -37,8 +37,8 @@ static uint64_t digest(const ksg_cycle_view* v) {
   for (uint32_t p = 0; p < v->n_positions; ++p) {
     mix(v->filter_called[p]);
     for (uint32_t i = 0; i < v->n_nodes; ++i) {
-      if (v->score[p]) mix((uint64_t)(int64_t)v->score[p][i]);
-      if (v->normalized[p]) mix((uint64_t)(int64_t)v->normalized[p][i]);
+      if (v->score[p]) mix((uint64_t)ksg_view_score(v, p, i, 0));
+      if (v->normalized[p]) mix((uint64_t)ksg_view_score(v, p, i, 1));
     }
   }
   for (uint32_t p = 0; p < v->n_positions; ++p) {

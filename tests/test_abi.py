@@ -32,4 +32,4 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version():
     from ksg import load_library
     L = load_library()
-    assert L.ksg_abi_version() == 3
+    assert L.ksg_abi_version() == 4

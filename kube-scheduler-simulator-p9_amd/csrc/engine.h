@@ -227,6 +227,7 @@ class Engine {
   // pinned host blocks for views (process-wide pool: a view outlives its context)
   static uint8_t* pinned_get(size_t bytes, size_t& cap);
   static void pinned_put(uint8_t* p, size_t cap);
+  static uint8_t* pinned_dev(const uint8_t* host);  // its device address (null: none / not pinned)
   // Restore the node rows / pod table to the state of the last upload (device copy).
   bool reset(std::string& err);
   // Sample the dominant kernel (k_filter_score) every `every` pods inside run_queue

@@ -2361,6 +2361,8 @@ struct WinArgs {
   // (the merges hand over keys and rows without waiting for P_{W-1}); 0 = the
   // merges do it once P_{W-1} is published (PriorRec)
   uint32_t prior_fix;
+  const uint32_t* nxt_evd;  // persistent loop: the next window's record counter and its target (null: last)
+  uint32_t nxt_need;
 };
 // the static record of (queue pod q, global node g)
 __device__ __forceinline__ StaticRec srec_at(const WinArgs& A, uint32_t q, uint32_t g) {
@@ -3965,6 +3967,7 @@ struct WinLDS {
   uint64_t pkey[KSG_BATCH][KSG_BATCH];  // key of pod b on prior node e as of the window start
   int8_t pdf[KSG_BATCH][KSG_BATCH];     // its feasible-count change vs the snapshot
   uint64_t pmask[KSG_BATCH];            // bit i: candidate i of pod b is a prior node
+  uint32_t nxt_ok;                      // (persistent loop) the next window's records were complete at the flush
   uint64_t pbest[KSG_BATCH];
   int32_t pbest_e[KSG_BATCH];
   int32_t S[3][KSG_BATCH];              // picks (global node, -1 none), rotating buffers
@@ -4655,6 +4658,13 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   }
   STAMP(4);
   if (A.stamps && tid == 0) A.stamps[7] = iters;
+  // (persistent loop) the two counters the flush and the next window wait on,
+  // requested now: their round trips overlap the flush instead of following it
+  uint32_t pre_fl = 0, pre_ev = 0;
+  if (PER && tid == 0) {
+    pre_fl = ld_sc1(A.flushed);
+    pre_ev = A.nxt_evd ? ld_sc1(A.nxt_evd) : 0u;
+  }
   // ---- flush: P_W first (the persistent loop publishes it at once: the eval
   // blocks of window W+2 wait for it), then summaries and per-pair patches
   const PickTab& T = L.pick[cur];
@@ -4700,8 +4710,9 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   }
   if constexpr (PER) {  // the eval blocks' outputs of this window are written before the patches
     if (tid == 0) {
-      bool ok = false;
-      for (uint32_t it = 0; it < A.spin; ++it) {
+      L.nxt_ok = A.nxt_evd && pre_ev >= A.nxt_need ? 1u : 0u;  // (read after the block's next barrier)
+      bool ok = pre_fl >= A.flush_need;
+      for (uint32_t it = 0; !ok && it < A.spin; ++it) {
         if (ld_sc1(A.flushed) >= A.flush_need) { ok = true; break; }
         if ((it & 63u) == 63u && ld_sc1(A.abortw) != 0u) break;
         __builtin_amdgcn_s_sleep(2);
@@ -4884,7 +4895,10 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
   A.defer = 0;
   if (blockIdx.x == 0) {
     WinLDS& L = *reinterpret_cast<WinLDS*>(lds_raw);
+    L.nxt_ok = 0;
+    __syncthreads();
     for (uint32_t W = 0; W < R.nwin; ++W) {
+      const bool ready = L.nxt_ok != 0;  // (the previous replay saw this window's records complete)
       A.ne = 0;
       A.w0 = R.first + W * KSG_BATCH;
       A.nw = min((uint32_t)KSG_BATCH, R.first + R.count - A.w0);
@@ -4898,9 +4912,16 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
       // parity is whole, KSG_BATCH pods)
       A.flushed = &Z->flushed[W & 1];
       A.flush_need = ((W >> 1) * KSG_BATCH + A.nw) * R.T;
-      if (!win_wait_ge(&Z->evd[W & 1], (W >> 1) * KSG_BATCH + A.nw, abortw, RC.spin, &go)) return;
+      if (!ready && !win_wait_ge(&Z->evd[W & 1], (W >> 1) * KSG_BATCH + A.nw, abortw, RC.spin, &go)) return;
       A.pub = &Z->replayed[0][0];
       A.pub_val = W + 1;
+      if (W + 1 < R.nwin) {
+        const uint32_t w1 = W + 1, nw1 = min((uint32_t)KSG_BATCH, R.first + R.count - (R.first + w1 * KSG_BATCH));
+        A.nxt_evd = &Z->evd[w1 & 1];
+        A.nxt_need = (w1 >> 1) * KSG_BATCH + nw1;
+      } else {
+        A.nxt_evd = nullptr;
+      }
       win_fixup<MODE, false, true>(C, F, A, L);  // (publishes P_W before its output patches)
       __syncthreads();  // (LDS reused by the next window)
     }
@@ -5160,6 +5181,7 @@ struct Engine::Impl {
   uint32_t cnblk = 0;
   DBuf<int32_t> knorm;    // normalized scores of one kept pod
   DBuf<uint8_t> vblk;     // device cycle view block (Engine::view)
+  DBuf<uint32_t> vdone;   // k_view's finished-block count (direct views)
   bool vblk_fresh = true;
   uint32_t vgen = 0;      // view generation (slot-table entries of older views count as empty)
   size_t prog_bytes = 0;  // used bytes of the program blob
@@ -6801,24 +6823,30 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
   }
   // the per-node arrays straight into the caller's pinned block when the device
   // can address it (one kernel, then only the slot table and summary are copied)
-  uint8_t* hdev = nullptr;
-  if (N && !I.view_copy && hipHostGetDevicePointer((void**)&hdev, host, 0) != hipSuccess) {
-    (void)hipGetLastError();
-    hdev = nullptr;
+  uint8_t* hdev = N && !I.view_copy ? pinned_dev(host) : nullptr;
+  if (hdev && !I.vdone.p) {
+    if (!I.vdone.alloc(1, err)) return false;
+    HIPCHK(hipMemsetAsync(I.vdone.p, 0, sizeof(uint32_t), s));
   }
   if (N)
     hipLaunchKernelGGL(k_view, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, I.cluster(), I.F, I.progs.p + I.prog_off[j],
                        I.sums.p + j, I.kfilter.p + k * N, I.kscore.p + k * N * KSG_MAX_PLUGINS, V, I.vblk.p,
-                       hdev ? hdev : I.vblk.p);
+                       hdev ? hdev : I.vblk.p, I.vdone.p);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(host, I.vblk.p, hdev ? lay.off_fail_pos : lay.bytes, hipMemcpyDeviceToHost, s));
+  if (!hdev) HIPCHK(hipMemcpyAsync(host, I.vblk.p, lay.bytes, hipMemcpyDeviceToHost, s));  // (direct: k_view wrote it all)
   HIPCHK(hipStreamSynchronize(s));
   return true;
 }
 namespace {
 std::mutex g_pin_mu;
 std::multimap<size_t, uint8_t*> g_pin_free;  // capacity -> block
+std::unordered_map<const uint8_t*, uint8_t*> g_pin_dev;  // pinned block -> its device address
 }  // namespace
+uint8_t* Engine::pinned_dev(const uint8_t* host) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pin_dev.find(host);
+  return it == g_pin_dev.end() ? nullptr : it->second;
+}
 uint8_t* Engine::pinned_get(size_t bytes, size_t& cap) {
   {
     std::lock_guard<std::mutex> lk(g_pin_mu);
@@ -6835,6 +6863,14 @@ uint8_t* Engine::pinned_get(size_t bytes, size_t& cap) {
   if (hipHostMalloc((void**)&p, cap, hipHostMallocDefault) != hipSuccess) {
     p = static_cast<uint8_t*>(std::malloc(cap));  // (pageable: the copy still works, slower)
     cap |= 1;  // tag: malloc'd
+  } else {
+    uint8_t* d = nullptr;  // (the view kernel writes the block directly when the device can address it)
+    if (hipHostGetDevicePointer((void**)&d, p, 0) == hipSuccess && d) {
+      std::lock_guard<std::mutex> lk(g_pin_mu);
+      g_pin_dev[p] = d;
+    } else {
+      (void)hipGetLastError();
+    }
   }
   return p;
 }
@@ -6842,6 +6878,7 @@ void Engine::pinned_put(uint8_t* p, size_t cap) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(g_pin_mu);
   if (g_pin_free.size() >= 64) {  // bounded pool: free the block
+    g_pin_dev.erase(p);
     if (cap & 1) std::free(p);
     else (void)hipHostFree(p);
     return;

@@ -2177,7 +2177,7 @@ __device__ __forceinline__ uint32_t view_slot(unsigned long long* tab, uint32_t 
 // launch after it) or out.
 __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const uint8_t* prog, const ksg_pod_summary* sum,
                                               const uint32_t* filter, const int32_t* score, ViewDev V, uint8_t* out,
-                                              uint8_t* hout) {
+                                              uint8_t* hout, uint32_t* done) {
   const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = n < C.N;
   const ProgView PV = view(prog);
@@ -2208,7 +2208,7 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
   }
   // message slots: one insert per distinct code of the wave
   unsigned long long* tab = reinterpret_cast<unsigned long long*>(out);
-  if (n == 0) *reinterpret_cast<ksg_pod_summary*>(out + V.off_sum) = *sum;
+  if (n == 0 && hout == out) *reinterpret_cast<ksg_pod_summary*>(out + V.off_sum) = *sum;
   uint32_t msg = 0;
   const uint32_t lane = threadIdx.x & 63;
   for (uint64_t m = __ballot(need); m; m = __ballot(need)) {
@@ -2224,8 +2224,11 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
   }
   Engine::ViewRows RW;
   view_rows(F, V, sum, C.N, RW);
-  if (n == 0) *reinterpret_cast<Engine::ViewRows*>(out + V.off_rows) = RW;
-  if (!act) return;
+  if (n == 0) {  // (direct: straight into the host block, like the per-node arrays)
+    *reinterpret_cast<Engine::ViewRows*>(hout + V.off_rows) = RW;
+    *reinterpret_cast<ksg_pod_summary*>(hout + V.off_sum) = *sum;
+  }
+  if (act) {
   reinterpret_cast<int8_t*>(hout + V.off_fail_pos)[n] = (int8_t)fp;
   reinterpret_cast<int8_t*>(hout + V.off_fail_code)[n] = (int8_t)fc;
   reinterpret_cast<uint16_t*>(hout + V.off_fail_msg)[n] = (uint16_t)msg;
@@ -2247,5 +2250,24 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
       v = normalize_pos(F.plugins[pos], h, s, sum->max_score[pos], sum->min_score[pos], sum->ipa_flags, pts_keys, use);
     }
     view_put(hout, RW.off[KSG_MAX_PLUGINS + r], RW.bytes[KSG_MAX_PLUGINS + r], n, v);
+  }
+  }
+  // direct: the last block to finish copies the message-slot table (every
+  // block's inserts done) into the host block, so no copy launch follows
+  if (hout != out && done) {
+    __shared__ uint32_t last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      last = atomicAdd(done, 1u) == gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (last) {
+      __threadfence();
+      unsigned long long* htab = reinterpret_cast<unsigned long long*>(hout);
+      for (uint32_t i = threadIdx.x; i <= (uint32_t)kViewSlots; i += blockDim.x)
+        htab[i] = __hip_atomic_load(&tab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0) *done = 0;  // (the next view's count)
+    }
   }
 }

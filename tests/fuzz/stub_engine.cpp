@@ -341,4 +341,5 @@ uint8_t* Engine::pinned_get(size_t bytes, size_t& cap) {
   return static_cast<uint8_t*>(std::malloc(cap));
 }
 void Engine::pinned_put(uint8_t* p, size_t) { std::free(p); }
+uint8_t* Engine::pinned_dev(const uint8_t*) { return nullptr; }
 }  // namespace ksg

@@ -4233,6 +4233,8 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   STAMP(0);
   if (A.stamps && tid == 0) A.stamps[11] = __builtin_amdgcn_s_memrealtime();
   const int np = ldv<PER>(A.pprev_n);
+  // (P_{W-1}'s nodes for wave 0's index, requested with the count, not after it)
+  const int32_t pn_all = wave == 0 && lane < KSG_BATCH ? ldv<PER>(&A.pprev[lane].node) : -1;
   // ---- stage.  The small inputs (P_{W-1}, pods, counts) are loaded first and
   // stored at once; the candidate keys and rows stay in flight in registers
   // across the prior-node evaluations (vmcnt is in order) and land after them.
@@ -4349,7 +4351,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       for (int t = 0; t < 3; ++t) pick_clear(L.pick[t], tid);
     }
     if (wave == 0) {  // index P_{W-1} (one wave: its LDS operations stay in order)
-      const int32_t pnode = lane < np ? ldv<PER>(&A.pprev[lane].node) : -1;
+      const int32_t pnode = lane < np ? pn_all : -1;
       L.ptn[lane] = -1;
       L.ptn[lane + 64] = -1;
       if (lane < np) L.pte[tab_claim(L.ptn, pnode)] = lane;
@@ -4528,7 +4530,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
               const PodLite* h = &L.pod[b];
               int32_t fs, bs;
               int64_t tot;
-              if (iters == 0) STAMP(26);
+
               StaticRec sr{KSG_FILTER_PASS, 0};
               uint32_t code;
               if (STAT) {
@@ -4537,7 +4539,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
               } else {
                 code = eval_row<MODE>(cur_r, F, h, R, fs, bs, tot);
               }
-              if (iters == 0) STAMP(27);
+
               bool snap_ok = sr.code == KSG_FILTER_PASS && (F.pos_fit < 0 || fit_filter_row(snap, h, R) == 0);
               df = (code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0);
               if (STAT) {
@@ -4691,8 +4693,10 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     }
     if (lane == 0) stv<PER>(A.pnext_n, (int32_t)__popcll(m));
   }
+  STAMP(26);
   if constexpr (PER) {  // every wave's stores of rows (P_{W-1}, at the stage) and P_W performed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(27);
     __syncthreads();
     if (tid < 16) st_sc1(A.pub + tid * 32, A.pub_val);
   }

@@ -66,8 +66,9 @@ print("realtime (us): window period", med([(bs[j][11] - bs[j - 1][11]) / 100 for
 for lab, i0, i1 in [("prior eval", 1, 16), ("keys->LDS+sync", 16, 17), ("pmask+sync", 17, 2),
                      ("iteration 1", 3, 19), ("it1 phase A", 3, 21), ("it1 barrier A", 21, 22), ("it1 phase B", 22, 23),
                      ("it1 barrier B", 23, 19), ("A: start->find", 3, 24), ("A: find/chain", 24, 25),
-                     ("A: origin rows", 25, 26), ("A: eval_row", 26, 27), ("A: rest", 27, 21),
-                     ("flush: P_W+publish", 4, 6), ("flush: patches", 6, 5)]:
+                     ("A: find/chain->phase A end", 25, 21),
+                     ("flush: P_W+publish", 4, 6), ("flush: patches", 6, 5),
+                     ("flush: P_W built (wave 0)", 4, 26), ("flush: P_W acks", 26, 27), ("flush: barrier+publish", 27, 6)]:
     print(f"fixup {lab:14s} median {med([x[i1] - x[i0] for x in bs[1:]]):6d}")
 two = [x for x in bs[1:] if x[7] >= 2]
 if two:

@@ -1220,25 +1220,35 @@ struct Cluster {
   template <class Pools>
   void tab_blooms(ksg_prog& h, const Pools& P) const {
     h.tab_rd = h.tab_md = ~0ull;
-    if (!(h.tab & KTAB_ON) || enc_NU == 0) return;
-    uint64_t rd = 0, md = 0;
-    for (int i = 0; i < h.n_lk; ++i) {  // (PC_NODE / TC_NODE entries are node-level)
+    h.nd_rd = h.nd_md = ~0ull;
+    if (!(h.tab & KTAB_ON) || enc_NU == 0 || enc_N == 0) return;
+    uint64_t rd = 0, md = 0, nrd = 0, nmd = 0;
+    for (int i = 0; i < h.n_lk; ++i) {  // (PC_NODE / TC_NODE entries are node-level: nd_rd)
       const ksg_look& e = h.lk[i];
       if (e.kind == KLK_PC_DOM) rd |= ksg_tab_bloom(1, (uint32_t)e.base / (uint32_t)enc_NU);
       else if (e.kind == KLK_TC_DOM) rd |= ksg_tab_bloom(2, (uint32_t)e.base);
+      else if (e.kind == KLK_PC_NODE) nrd |= ksg_tab_bloom(4, (uint32_t)(e.base / (uint64_t)enc_N));
+      else if (e.kind == KLK_TC_NODE) nrd |= ksg_tab_bloom(5, (uint32_t)e.base);
     }
     for (int c = 0; c < h.n_tsc_filter; ++c)  // minMatchNum candidates (pc_dom)
       if (h.tsc[c].eff_cls >= 0) rd |= ksg_tab_bloom(1, (uint32_t)h.tsc[c].eff_cls);
     for (int i = 0; i < h.n_ub; ++i)
       rd |= h.ub[i].kind == 1 ? ksg_tab_bloom(1, (uint32_t)h.ub[i].idx / KSG_MAX_TOPO) : ksg_tab_bloom(3, (uint32_t)h.ub[i].idx);
-    for (int i = 0; i < h.n_pc_match; ++i) md |= ksg_tab_bloom(1, (uint32_t)P.i32[(size_t)h.pc_match_off + i]);
+    for (int i = 0; i < h.n_pc_match; ++i) {
+      const uint32_t c = (uint32_t)P.i32[(size_t)h.pc_match_off + i];
+      md |= ksg_tab_bloom(1, c);
+      nmd |= ksg_tab_bloom(4, c);  // (its pc_cnt entry at the node)
+    }
     for (int i = 0; i < h.n_exist_terms; ++i) {
       const ksg_exist_term& e = P.et[(size_t)h.exist_terms_off + i];
       if (e.cls < 0) continue;  // (no class: tc_add writes nothing)
       md |= ksg_tab_bloom(2, (uint32_t)e.toff) | ksg_tab_bloom(3, (uint32_t)e.cls);
+      nmd |= ksg_tab_bloom(5, (uint32_t)e.toff);  // (a one-node-per-value key's entry at the node)
     }
     h.tab_rd = rd;
     h.tab_md = md;
+    h.nd_rd = nrd;
+    h.nd_md = nmd;
   }
   // Recompile queue pod q when classes added since its compile apply to it (its
   // pod-class list must hold every class whose table counts it; its term-class
@@ -2615,6 +2625,7 @@ struct Cluster {
     } else {
       h.tab = KTAB_ON;  // profiles without PTS / IPA: the chain needs no tables
       h.tab_rd = h.tab_md = 0;
+      h.nd_rd = h.nd_md = 0;
     }
     // every requirement of the pool (NodeAffinity, node selector, volume and
     // topology terms alike) in its flattened form

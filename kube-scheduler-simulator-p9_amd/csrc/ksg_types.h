@@ -303,6 +303,10 @@ typedef struct ksg_prog {
   // a pod whose reads miss the previous pod's writes does not wait for that assume
   // (node-level entries are read only by the block owning the node).  ~0: unknown.
   uint64_t tab_rd, tab_md;
+  // the same for the node-level entries (pc_cnt of the pod's classes, one-node-per-value
+  // tc_val): k_chain_run evaluates pod k+1 before pod k's assume only when pod k+1
+  // reads none of the entries pod k writes at either level.  ~0: unknown.
+  uint64_t nd_rd, nd_md;
 
   // ---- volume plugins
   int32_t n_vchk, vchk_off;  // pool_i32: ksg_vchk records (8 words each)

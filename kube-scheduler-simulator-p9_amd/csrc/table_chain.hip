@@ -440,6 +440,18 @@ struct EvalOut {
   ChainRec rec;
 };
 enum { kEval = 0, kSolo = 1, kRun = 2 };  // eval_body modes: k_eval, k_eval_solo, k_chain_run
+// k_chain_run's evaluation in two stages (eval_body STG): 1 issues every
+// class-table read of the node (the lookup plan, minMatchNum candidates,
+// InterPodAffinity map totals) and leaves the values in flight in an EvalPre;
+// 2 finishes from it (row-only plugins on the row as of then, filters, scores,
+// the block's record).  0: both at once.
+struct EvalPre {
+  int32_t lkv[KSG_LK_MAX], lks[KSG_LK_MAX];
+  uint8_t mpn[KSG_MAX_TSC];
+  int32_t mcnt[KSG_MAX_TSC];
+  int32_t ubv;
+  uint32_t ubbit;
+};
 // Class-table reads: plain loads in a launch of one cycle; in the persistent chain
 // the tables change under the launch (other blocks' assumes), so every read is an
 // agent-scope (sc1) load of what the assuming block wrote by atomics
@@ -460,11 +472,14 @@ struct RunWait;
 __device__ bool run_wait_flag(const RunWait& W);
 // LK / TS: the lookup-plan entries and spread constraints a pod of the launch has
 // at most (k_chain_run size classes; smaller unrolled loops, less code).
-template <int ROWM, int MODE = kEval, uint32_t PM = ~0u, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC, int BT = kChain>
+template <int ROWM, int MODE = kEval, uint32_t PM = ~0u, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC, int BT = kChain,
+          int STG = 0>
 __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, const ChainArgs& A,
                                           const uint8_t* __restrict__ prog, EvalSharedT<BT>* Lrun = nullptr,
-                                          RowV* rowrun = nullptr, EvalOut* eo = nullptr, const RunWait* W = nullptr) {
+                                          RowV* rowrun = nullptr, EvalOut* eo = nullptr, const RunWait* W = nullptr,
+                                          EvalPre* pre = nullptr) {
   constexpr bool SOLO = MODE == kSolo, RUN = MODE == kRun;
+  static_assert(STG == 0 || RUN, "staged evaluation: the persistent chain only");
   static_assert(BT == kChain || RUN, "other block sizes: the persistent chain only");
   if constexpr (!RUN) chain_warm(prog);
   CS_BEGIN;
@@ -515,12 +530,14 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   uint32_t fit_b = 0;
   int64_t fit_s = 0, ba_s = 0;
   if constexpr (RUN && ROWM != 0) {
-    if (PMH(KP_FIT)) {
-      fit_b = fit_filter_row(row, h, C.R);
-      fit_s = ROWM == 2 ? fit_score_row<1>(row, F, h) : fit_score_row<0>(row, F, h);
+    if (STG != 1) {  // (staged: on the row as of the finish)
+      if (PMH(KP_FIT)) {
+        fit_b = fit_filter_row(row, h, C.R);
+        fit_s = ROWM == 2 ? fit_score_row<1>(row, F, h) : fit_score_row<0>(row, F, h);
+      }
+      if (PMH(KP_BA)) ba_s = ROWM == 2 ? ba_score_row<1>(row, F, h) : ba_score_row<0>(row, F, h);
     }
-    if (PMH(KP_BA)) ba_s = ROWM == 2 ? ba_score_row<1>(row, F, h) : ba_score_row<0>(row, F, h);
-    if (W && !run_wait_flag(*W)) {
+    if (STG != 2 && W && !run_wait_flag(*W)) {
       eo->abort = true;
       return;
     }
@@ -531,7 +548,10 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   for (int c = 0; c < TS; ++c) {
     mpn[c] = 0;
     mcnt[c] = 0;
-    if (pts_f && c < nf && threadIdx.x < (uint32_t)h->tsc[c].nvals) {
+    if constexpr (STG == 2) {
+      mpn[c] = pre->mpn[c];
+      mcnt[c] = pre->mcnt[c];
+    } else if (pts_f && c < nf && threadIdx.x < (uint32_t)h->tsc[c].nvals) {
       const ksg_tsc& t = h->tsc[c];
       mpn[c] = C.T.pair_node[t.pair_base + threadIdx.x];
       if (t.eff_cls >= 0) mcnt[c] = ld_tab<MODE>(C.T.pc_dom + (size_t)t.eff_cls * C.T.NU + (uint32_t)t.nub + threadIdx.x);
@@ -539,7 +559,10 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   }
   int32_t ubv = 0;
   uint32_t ubbit = 0;
-  if (ipa_pos >= 0 && h->n_ub > 0) {  // entry tid of the plan (uniform reads, then a per-lane pick)
+  if constexpr (STG == 2) {
+    ubv = pre->ubv;
+    ubbit = pre->ubbit;
+  } else if (ipa_pos >= 0 && h->n_ub > 0) {  // entry tid of the plan (uniform reads, then a per-lane pick)
     int32_t idx = 0, kind = 0;
 #pragma unroll
     for (int i = 0; i < KSG_UB_MAX; ++i) {
@@ -568,7 +591,10 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   for (int i = 0; i < LK; ++i) {
     lkv[i] = 0;
     lks[i] = -1;
-    if (i < h->n_lk) {
+    if constexpr (STG == 2) {
+      lkv[i] = pre->lkv[i];
+      lks[i] = pre->lks[i];
+    } else if (i < h->n_lk) {
       const ksg_look& e = h->lk[i];
       const int32_t v = tv(e.slot);
       lks[i] = v;
@@ -579,6 +605,21 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     }
   }
   CS(9);
+  if constexpr (STG == 1) {  // the reads are in flight: the caller finishes later (STG 2)
+#pragma unroll
+    for (int i = 0; i < LK; ++i) {
+      pre->lkv[i] = lkv[i];
+      pre->lks[i] = lks[i];
+    }
+#pragma unroll
+    for (int c = 0; c < TS; ++c) {
+      pre->mpn[c] = mpn[c];
+      pre->mcnt[c] = mcnt[c];
+    }
+    pre->ubv = ubv;
+    pre->ubbit = ubbit;
+    return;
+  }
   // ---- pod-uniform setup: minMatchNum per filter constraint, InterPodAffinity bits
   if (threadIdx.x < KSG_MAX_TSC) L.minm[threadIdx.x] = 0x7FFFFFFF;
   if (threadIdx.x == 0) L.ipa_flags = 0;
@@ -1469,7 +1510,14 @@ struct RunCtl {
   uint32_t lag;            // diagnostic: the committer's s_sleep(127) rounds before each pod's granule reads
   uint32_t* host_verdict;  // pinned host word the deciding block writes (the host polls it), or null
   uint32_t spin;           // polls before a block gives up (kRunSpin; tests force an abort with few)
+  uint32_t overlap;        // issue pod k+1's class-table reads during pod k's hand-offs (KSG_RUN_OVERLAP)
 };
+// Pod j+1 (header n) may read the class tables before pod j's (header h) assume:
+// it reads none of the pair-level nor node-level entries pod j writes (its row,
+// the only other change, is read only at the finish, after the assume).
+__device__ __forceinline__ bool run_indep(const ksg_prog* h, const ksg_prog* n) {
+  return (h->tab_md & n->tab_rd) == 0 && (h->nd_md & n->nd_rd) == 0;
+}
 constexpr uint32_t kRunSpin = 1u << 22;  // polls (~1 us each with the load) before a block gives up
 constexpr int kRunSleep = 8;             // s_sleep between polls (x 64 cycles): every block polls every block
 constexpr int kRunG1 = 2 + 4 * KCP_X + 2 * KSG_MAX_TSC;  // partial-record granules per block (max)
@@ -1671,7 +1719,14 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
   if (rs_on) atomicAdd((unsigned long long*)&rst[k], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - rs_t0))
   __syncthreads();
   uint32_t wait_for = 0;  // the flag value this block needs before its next class-table read (0: none)
-  uint32_t owned = 0;     // this block applied the previous pod's node-level assume
+  uint32_t owned = 0;     // this block applied a node-level assume not yet drained before a class-table read
+  // Overlap (KSG_RUN_OVERLAP): when pod k+1 is independent of pod k (run_indep),
+  // its class-table reads are issued right after pod k's partial record goes out
+  // and stay in flight across pod k's fold, selection and assume; pod k+1 then
+  // finishes from them (eval_body stages 1 / 2) on its row as of then.
+  bool have = false;       // pre holds pod k's reads (issued during pod k-1)
+  EvalPre pre;
+  const ksg_prog* ph = nullptr;  // pod k-1's header
   for (uint32_t k = 0; k < count; ++k) {
     ChainArgs A = A0;  // (A.stamps: eval_body's own k_eval slots, block 0)
     A.q = A0.q + k;
@@ -1686,15 +1741,34 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     // the class-table reads), its partial record
     EvalOut eo;
     eo.abort = false;
-    const RunWait W{Y, wait_for, &S.go, rs_on ? rst : nullptr, owned, R.spin};
-    eval_body<ROWM, kRun, PM, LK, TS, BT>(C, F, A, prog, &L, &row, &eo, &W);
+    if (have) {
+      eval_body<ROWM, kRun, PM, LK, TS, BT, 2>(C, F, A, prog, &L, &row, &eo, nullptr, &pre);
+    } else {
+      const RunWait W{Y, wait_for, &S.go, rs_on ? rst : nullptr, owned, R.spin};
+      eval_body<ROWM, kRun, PM, LK, TS, BT>(C, F, A, prog, &L, &row, &eo, &W);
+      owned = 0;
+    }
     if (eo.abort) return;
     wait_for = 0;
-    owned = 0;
     const int ns = h->n_tsc_score;
     const int ng1 = run_g1_count(xmask, ns);
     if (threadIdx.x < (uint32_t)ng1) st_sc1(G1 + (size_t)b * kRunGS + threadIdx.x, gran(tag, run_g1_value<TS>(eo.rec, (int)threadIdx.x, xmask, ns)));
     RS(30);
+    // ---- pod k+1's class-table reads, in flight across this pod's hand-offs
+    const ksg_prog* nh = k + 1 < count ? reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[A.q + 1]) : nullptr;
+    const bool tnext = R.overlap && nh && run_indep(h, nh);
+    if (tnext) {
+      ChainArgs A1 = A0;
+      A1.q = A.q + 1;
+      // the assumes before pod k (before pod k-1 when pod k+1 is independent of it too)
+      const RunWait W1{Y, (ph && run_indep(ph, nh)) ? (k ? k - 1 : 0u) : k, &S.go, nullptr, owned, R.spin};
+      EvalOut ea;
+      ea.abort = false;
+      eval_body<ROWM, kRun, PM, LK, TS, BT, 1>(C, F, A1, A1.progs + A1.prog_off[A1.q], &L, &row, &ea, &W1, &pre);
+      if (ea.abort) return;
+      owned = 0;
+      if (rs_on) atomicAdd((unsigned long long*)&rst[40], 1ull);  // (pods whose reads went ahead)
+    }
     // ---- fold every block's partials (as reduce_eval)
     EvalTotals E;
     {
@@ -1843,10 +1917,9 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     // the flag this block waits for before the next pod's class-table reads: every
     // assume up to this pod's if the next pod reads an entry this one writes
     // (tab_rd / tab_md), else every assume before this pod's
-    if (k + 1 < count) {
-      const ksg_prog* nh = reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[A.q + 1]);
-      wait_for = (node >= 0 && (h->tab_md & nh->tab_rd) != 0) ? tag : k;
-    }
+    have = tnext;
+    if (nh && !tnext) wait_for = (node >= 0 && (h->tab_md & nh->tab_rd) != 0) ? tag : k;
+    ph = h;
     if (rs_on) atomicAdd((unsigned long long*)&rst[35], 1ull);
   }
 #undef RS

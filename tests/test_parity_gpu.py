@@ -233,8 +233,9 @@ RUN_CASES = [
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"KSG_RUN_MIN": "1"}, {"KSG_RUN_BT": "512"}, {"KSG_RUN_LAG": "4"}],
-                         ids=["default", "min1", "bt512", "lag"])
+@pytest.mark.parametrize("env", [{}, {"KSG_RUN_MIN": "1"}, {"KSG_RUN_BT": "512"}, {"KSG_RUN_LAG": "4"},
+                                 {"KSG_RUN_OVERLAP": "1"}],
+                         ids=["default", "min1", "bt512", "lag", "overlap"])
 @pytest.mark.parametrize("name,c,sizes,keep", RUN_CASES, ids=[c[0] for c in RUN_CASES])
 def test_persistent_segments_match_oracle(monkeypatch, env, name, c, sizes, keep):
     """Persistent segments (k_chain_run: the pod loop inside one launch, gates

@@ -54,6 +54,7 @@ def main():
     if out[35]:  # persistent segments (k_chain_run)
         rep["k_chain_run_us_since_pod_start_block0"] = {RUN_NAMES[k]: round(out[k] / out[35] * 0.01, 3) for k in (30, 31, 39, 32, 47, 33, 34)}
         rep["k_chain_run_pods_block0"] = out[35]
+        rep["k_chain_run_pods_read_ahead_block0"] = out[40]
         rep["k_chain_run_flag_wait_us_block0"] = round(out[38] / out[35] * 0.01, 3)
         if out[37]:
             rep["k_chain_run_owner_commit_us"] = round(out[36] / out[37] * 0.01, 3)

@@ -163,6 +163,16 @@ class Engine {
   bool pod_row(uint32_t q, int32_t& row, std::string& err);
   // Cluster event applied in place: node gnode's allocatable [R] and allowed pod count.
   bool node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_t allowed, std::string& err);
+  // Cluster event applied in place: node gnode's label value per node-label key
+  // ([K], -1 none; vocabulary and topology values unchanged), has-labels byte and
+  // KSG_NODE_* flags — into its columns when it is on this shard, and into the
+  // every-node static columns when the context keeps them.
+  bool node_static(int32_t gnode, const std::vector<int32_t>& label_vid, uint8_t has_labels, uint8_t flags,
+                   std::string& err);
+  // The node taint lists replaced (CSR over this shard's nodes; gofs/gids over
+  // every node, used when the context keeps the every-node static columns).
+  bool node_taints(const std::vector<uint32_t>& offs, const std::vector<int32_t>& ids,
+                   const std::vector<uint32_t>& gofs, const std::vector<int32_t>& gids, std::string& err);
   bool set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err);
   // An assume found the existing-pod table full (the pod was not appended).
   bool table_overflow(bool& overflow, std::string& err);

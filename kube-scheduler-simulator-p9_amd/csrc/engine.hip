@@ -6524,6 +6524,65 @@ bool Engine::node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_
   return true;
 }
 
+bool Engine::node_static(int32_t gnode, const std::vector<int32_t>& label_vid, uint8_t has_labels, uint8_t flags,
+                         std::string& err) {
+  Impl& I = *p_;
+  if (gnode < 0 || (uint32_t)gnode >= I.G) { err = "node_static: node index"; return false; }
+  if (label_vid.size() != I.K) { err = "node_static: label key count"; return false; }
+  hipStream_t s = I.stream;
+  // one column entry per key: a strided copy down the [K][N] (and [K][G]) columns
+  if (I.K && I.gstat)
+    HIPCHK(hipMemcpy2DAsync(I.glabel.p + gnode, (size_t)I.G * 4, label_vid.data(), 4, 4, I.K, hipMemcpyHostToDevice, s));
+  if ((uint32_t)gnode >= I.goff && (uint32_t)gnode - I.goff < I.N) {
+    const uint32_t n = (uint32_t)gnode - I.goff;
+    if (I.K)
+      HIPCHK(hipMemcpy2DAsync(I.label.p + n, (size_t)I.N * 4, label_vid.data(), 4, 4, I.K, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(I.haslab.p + n, &has_labels, 1, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(I.nflags.p + n, &flags, 1, hipMemcpyHostToDevice, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  return true;
+}
+
+bool Engine::node_taints(const std::vector<uint32_t>& offs, const std::vector<int32_t>& ids,
+                         const std::vector<uint32_t>& gofs, const std::vector<int32_t>& gids, std::string& err) {
+  Impl& I = *p_;
+  hipStream_t s = I.stream;
+  if (offs.size() != (size_t)I.N + 1 || offs.back() != ids.size() ||
+      (I.gstat && (gofs.size() != (size_t)I.G + 1 || gofs.back() != gids.size()))) {
+    err = "node_taints: taint lists do not match the node count";
+    return false;
+  }
+  HIPCHK(hipStreamSynchronize(s));  // (a re-allocation frees what a queued launch may read)
+  // what upload() derives from the lists: widest list, largest id, a taint listed twice
+  uint32_t mt = 0;
+  int32_t mx = -1;
+  bool dup = false;
+  for (uint32_t i = 0; i < I.N; ++i) mt = std::max(mt, offs[i + 1] - offs[i]);
+  for (int32_t t : ids) mx = std::max(mx, t);
+  for (uint32_t i = 0; i < I.N && !dup && mx < 64; ++i) {
+    uint64_t seen = 0;
+    for (uint32_t k = offs[i]; k < offs[i + 1]; ++k) {
+      const uint64_t b = 1ull << (ids[k] & 63);
+      dup |= (seen & b) != 0;
+      seen |= b;
+    }
+  }
+  if (I.gstat) {
+    for (uint32_t g = 0; g < I.G; ++g) mt = std::max(mt, gofs[g + 1] - gofs[g]);
+    std::vector<int32_t> gt = gids;
+    gt.resize(std::max<size_t>(gt.size(), 1), 0);
+    if (!I.gtoff.upload(gofs, s, err) || !I.gtid.upload(gt, s, err)) return false;
+  }
+  if (!I.toff.upload(offs, s, err) || !I.tid.upload(ids, s, err)) return false;
+  I.max_taints = mt;
+  I.max_tid = mx;
+  I.taint_dup = dup;
+  if (mt >= 4096) I.static_fits = false;  // (other causes may hold it false: never raised here)
+  HIPCHK(hipStreamSynchronize(s));
+  return true;
+}
+
 bool Engine::grow_table(uint32_t pod_cap, uint32_t term_cap, uint32_t req_cap, uint32_t val_cap, uint32_t n_keys,
                         std::string& err) {
   Impl& I = *p_;

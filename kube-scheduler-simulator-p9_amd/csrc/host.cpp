@@ -1469,6 +1469,38 @@ struct Cluster {
     }
   }
 
+  // The sharded Taint / NodeAffinity window keeps every node's labels and taints
+  // on every rank.
+  bool global_statics() const { return shards > 1 && (has_plugin("TaintToleration") || has_plugin("NodeAffinity")); }
+  // Taint lists of nodes [a, b) as CSR over the taint vocabulary (node order kept:
+  // the first untolerated taint names the Filter failure).
+  void taint_lists(uint32_t a, uint32_t b, vector<uint32_t>& off, vector<int32_t>& ids) const {
+    off.assign(b - a + 1, 0);
+    ids.clear();
+    for (uint32_t i = a; i < b; ++i) {
+      for (auto& t : nodes[i].taints) ids.push_back(taint_id.at(std::make_tuple(t.key, t.value, t.effect)));
+      off[i - a + 1] = (uint32_t)ids.size();
+    }
+  }
+  // Can node labels `from` become `to` by rewriting label columns alone?  Every
+  // key and value is in the node-label vocabulary (selectors were compiled
+  // against it) and no topology key changes value (topology slots, class
+  // tables and spread domains stay valid).
+  bool labels_in_place(const map<string, string>& from, const map<string, string>& to) const {
+    auto ok = [&](const string& key, const string* v) {
+      const int32_t k = nkeys.get(key);
+      if (k < 0 || topo.get(key) >= 0) return false;
+      return !v || nvals[k].get(*v) >= 0;
+    };
+    for (auto& kv : to) {
+      auto it = from.find(kv.first);
+      if ((it == from.end() || it->second != kv.second) && !ok(kv.first, &kv.second)) return false;
+    }
+    for (auto& kv : from)
+      if (!to.count(kv.first) && !ok(kv.first, nullptr)) return false;
+    return true;
+  }
+
   bool encode_snapshot(NodeSoA& S, PodTableSoA& T) {
     // a new snapshot: the class registry restarts (the bound pods' terms register first)
     pcls.clear();
@@ -1548,19 +1580,16 @@ struct Cluster {
         }
       }
     }
-    if (shards > 1 && (has_plugin("TaintToleration") || has_plugin("NodeAffinity"))) {
+    if (global_statics()) {
       // every node's labels and taints (the sharded Taint / NodeAffinity window's
       // static records cover the whole cluster on every rank)
       S.g_label_vid.assign((size_t)K * G, -1);
-      S.g_taint_off.assign(G + 1, 0);
-      for (uint32_t g = 0; g < G; ++g) {
-        const Node& nd = nodes[g];
-        for (auto& kv : nd.labels) S.g_label_vid[(size_t)nkeys.get(kv.first) * G + g] = nvals[nkeys.get(kv.first)].get(kv.second);
-        for (auto& t : nd.taints) S.g_taint_id.push_back(taint_id[std::make_tuple(t.key, t.value, t.effect)]);
-        S.g_taint_off[g + 1] = (uint32_t)S.g_taint_id.size();
-      }
+      for (uint32_t g = 0; g < G; ++g)
+        for (auto& kv : nodes[g].labels)
+          S.g_label_vid[(size_t)nkeys.get(kv.first) * G + g] = nvals[nkeys.get(kv.first)].get(kv.second);
+      taint_lists(0, G, S.g_taint_off, S.g_taint_id);
     }
-    S.taint_off.assign(n + 1, 0);
+    taint_lists(lo, hi, S.taint_off, S.taint_id);
     for (uint32_t i = 0; i < n; ++i) {
       const Node& nd = nodes[lo + i];
       for (auto& kv : nd.alloc) {
@@ -1576,8 +1605,6 @@ struct Cluster {
           int32_t id = images.get(nm);
           S.img_bits[(size_t)(id >> 5) * n + i] |= 1u << (id & 31);
         }
-      for (auto& t : nd.taints) S.taint_id.push_back(taint_id[std::make_tuple(t.key, t.value, t.effect)]);
-      S.taint_off[i + 1] = (uint32_t)S.taint_id.size();
     }
     S.key_val_off.assign(K + 1, 0);
     for (uint32_t k = 0; k < K; ++k) {
@@ -3470,7 +3497,16 @@ struct Cluster {
   // same k_assume Reserve/Unreserve use, instead of a re-encode.  Returns 1
   // applied, 0 not eligible (nothing changed), -1 error.
   int inplace_events(const J& ev) {
-    struct Op { bool add; Pod pod; vector<uint8_t> blob; string key; int32_t node = -1; Node nd; int32_t qpod = -1, qat = -1; };
+    struct Op {
+      bool add;
+      Pod pod;
+      vector<uint8_t> blob;
+      string key;
+      int32_t node = -1;
+      Node nd;
+      int32_t qpod = -1, qat = -1;
+      bool statics = false, taints = false;  // node update: label / flag columns, taint lists rewritten
+    };
     auto pkey = [](const string& ns, const string& name) { return ns + '\x1f' + name; };
     track_queue();
     prio_dirty = true;
@@ -3511,23 +3547,32 @@ struct Cluster {
         added.insert(k);
         removed.erase(k);
         ops.push_back(std::move(o));
-      } else if (op == "updateNode") {  // allocatable-only updates (same labels, taints, images, flags)
+      } else if (op == "updateNode") {
+        // allocatable, unschedulable, label and taint updates whose values the
+        // vocabularies already hold (no topology key changes value: the class
+        // tables and topology slots stay as they are); images unchanged
         if (!e["node"]) return 0;
         Node x = parse_node(*e["node"]);
         const int32_t at = node_names.get(x.name);
         if (at < 0) return 0;
         const Node& old = nodes[at];
-        if (x.labels != old.labels || x.unschedulable != old.unschedulable || x.images != old.images ||
-            x.taints.size() != old.taints.size())
-          return 0;
-        for (size_t t = 0; t < x.taints.size(); ++t)
-          if (x.taints[t].key != old.taints[t].key || x.taints[t].value != old.taints[t].value ||
-              x.taints[t].effect != old.taints[t].effect)
-            return 0;
+        if (x.images != old.images) return 0;
+        bool retaint = x.taints.size() != old.taints.size();
+        for (size_t t = 0; t < x.taints.size() && !retaint; ++t)
+          retaint = x.taints[t].key != old.taints[t].key || x.taints[t].value != old.taints[t].value ||
+                    x.taints[t].effect != old.taints[t].effect;
+        const bool relabel = x.labels != old.labels;
+        if ((relabel || retaint) && has_volume_plugins) return 0;  // (volume topology is read from labels at encode)
+        if (relabel && !labels_in_place(old.labels, x.labels)) return 0;
+        if (retaint)
+          for (auto& t : x.taints)
+            if (!taint_id.count(std::make_tuple(t.key, t.value, t.effect))) return 0;
         for (auto& kv : x.alloc)
           if (kv.first != "pods" && res.get(kv.first) < 0) return 0;
         Op o{false, Pod(), {}, string()};
         o.node = at;
+        o.statics = relabel || x.unschedulable != old.unschedulable;
+        o.taints = retaint;
         o.nd = std::move(x);
         ops.push_back(std::move(o));
       } else if (op == "removePod") {
@@ -3579,6 +3624,8 @@ struct Cluster {
     std::unordered_map<string, int32_t> add_slot;  // additions of this batch still present
     vector<std::pair<int32_t, int32_t>> unres;     // queue pod, node
     vector<std::tuple<int32_t, vector<int64_t>, int32_t>> allocs;  // node, allocatable, allowed pods
+    vector<int32_t> restat;  // nodes whose label / flag columns are rewritten
+    bool retaint = false;    // some node's taint list changed: the lists are re-uploaded
     for (auto& o : ops) {
       if (o.qpod >= 0) {
         unres.push_back({o.qpod, o.qat});
@@ -3593,6 +3640,8 @@ struct Cluster {
           if (r >= 0) al[r] = r == 0 ? as_milli(kv.second) : as_value(kv.second);
         }
         allocs.emplace_back(o.node, std::move(al), allowed);
+        if (o.statics) restat.push_back(o.node);
+        retaint |= o.taints;
         nodes[o.node] = std::move(o.nd);
       } else if (o.add) {
         const int32_t k = (int32_t)blobs.size();
@@ -3634,6 +3683,19 @@ struct Cluster {
       ok = refresh_program((uint32_t)unres[i].first) && eng->assume((uint32_t)unres[i].first, unres[i].second, -1, err);
     for (size_t i = 0; ok && i < allocs.size(); ++i)
       ok = eng->node_alloc(std::get<0>(allocs[i]), std::get<1>(allocs[i]), std::get<2>(allocs[i]), err);
+    for (size_t i = 0; ok && i < restat.size(); ++i) {
+      const Node& nd = nodes[restat[i]];
+      vector<int32_t> lv(nkeys.names.size(), -1);  // as encode_snapshot
+      for (auto& kv : nd.labels) lv[nkeys.get(kv.first)] = nvals[nkeys.get(kv.first)].get(kv.second);
+      ok = eng->node_static(restat[i], lv, nd.labels.empty() ? 0 : 1, nd.unschedulable ? KSG_NODE_UNSCHEDULABLE : 0, err);
+    }
+    if (ok && retaint) {
+      vector<uint32_t> off, goff;
+      vector<int32_t> ids, gids;
+      taint_lists(lo, hi, off, ids);
+      if (global_statics()) taint_lists(0, (uint32_t)nodes.size(), goff, gids);
+      ok = eng->node_taints(off, ids, goff, gids, err);
+    }
     if (!ok) {
       broken = true;
       return -1;

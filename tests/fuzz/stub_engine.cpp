@@ -168,6 +168,15 @@ bool Engine::node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_
   if (gnode < 0 || alloc.size() < p_->R) { err = "stub: node_alloc"; return false; }
   return true;
 }
+bool Engine::node_static(int32_t gnode, const std::vector<int32_t>&, uint8_t, uint8_t, std::string& err) {
+  if (gnode < 0) { err = "stub: node_static"; return false; }
+  return true;
+}
+bool Engine::node_taints(const std::vector<uint32_t>& offs, const std::vector<int32_t>& ids,
+                         const std::vector<uint32_t>&, const std::vector<int32_t>&, std::string& err) {
+  if (offs.empty() || offs.back() != ids.size()) { err = "stub: node_taints"; return false; }
+  return true;
+}
 bool Engine::set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary* in, std::string& err) {
   if ((size_t)first + count > p_->sums.size()) { err = "stub: summaries range"; return false; }
   std::memcpy(p_->sums.data() + first, in, (size_t)count * sizeof(ksg_pod_summary));

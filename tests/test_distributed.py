@@ -183,21 +183,34 @@ def _sharded_events_worker(rank, world, port, doc_json, ev_json, k, out):
 # the same batch; adding/removing nodes moves the shard boundaries, so each rank
 # re-encodes a different node range afterwards.
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["mixed", "bound_pods"])
-@pytest.mark.parametrize("cfg", [2, 4])
+@pytest.mark.parametrize("cfg,kind", [(2, "mixed"), (2, "bound_pods"), (4, "mixed"), (4, "bound_pods"),
+                                      (3, "statics")])
 def test_sharded_events_match_oracle(cfg, kind):
+    """statics: node label / taint rewrites in place on a sharded Taint /
+    NodeAffinity window context (every rank's every-node static columns)."""
     import json
+    import random
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _oracle import Oracle
     from ksg import generator as g
-    from test_events_gpu import _events, _pod_events
+    from test_events_gpu import _events, _nowhere, _pod_events, _static_events
     doc = g.generate(2, n_nodes=400, n_pods=200) if cfg == 2 else \
+        g.generate(3, n_nodes=300, n_pods=160) if cfg == 3 else \
         g.generate(4, n_nodes=200, n_existing=700, n_pods=80, n_zones=6)
     n, k = len(doc["queue"]), len(doc["queue"]) // 2
     o = Oracle(doc)
     o.schedule(k, record=0)
     placed = [o.result(q)[0] if o.result(q)[2] == 0 else -1 for q in range(k)]
-    ev, eq = (_events if kind == "mixed" else _pod_events)(doc, placed, k)  # bound_pods: in-place path
+    if kind == "statics":
+        ev, nodes = _static_events(doc, random.Random(7300))
+        names = [x["metadata"]["name"] for x in doc["nodes"]]
+        bound = list(doc.get("pods", []))
+        for i in range(k):
+            if placed[i] >= 0:
+                bound.append(dict(doc["queue"][i], spec=dict(doc["queue"][i]["spec"], nodeName=names[placed[i]])))
+        eq = dict(doc, nodes=nodes, pods=bound, queue=[_nowhere(i) for i in range(k)] + doc["queue"][k:])
+    else:
+        ev, eq = (_events if kind == "mixed" else _pod_events)(doc, placed, k)  # bound_pods: in-place path
     o2 = Oracle(eq)
     o2.schedule(record=0)
     want = [o2.result(q) for q in range(k, n)]

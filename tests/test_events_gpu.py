@@ -323,3 +323,121 @@ def test_inplace_adds_beyond_table_slack_then_queue():
     o.schedule(record=0)
     got = [(r.selected, r.feasible, r.status) for r in s.results()]
     assert got == [o.result(q) for q in range(len(got))]
+
+
+def _static_events(doc, rng, fresh=False):
+    """updateNode events that rewrite labels (non-topology keys, values some node
+    already carries), taint lists (taints some node already carries: added,
+    removed, replaced, reordered) and spec.unschedulable — the in-place path.
+    fresh=True also brings a label value no node carries (the re-encode path)."""
+    nodes = copy.deepcopy(doc["nodes"])
+    topo = {"kubernetes.io/hostname", "topology.kubernetes.io/zone"}
+    vals = {}
+    taints = []
+    for n in nodes:
+        for k, v in n["metadata"].get("labels", {}).items():
+            if k not in topo:
+                vals.setdefault(k, set()).add(v)
+        for t in (n.get("spec") or {}).get("taints") or []:
+            if t not in taints:
+                taints.append(t)
+    vals = {k: sorted(v) for k, v in sorted(vals.items())}
+    ev = []
+    for j in rng.sample(range(len(nodes)), min(40, len(nodes))):
+        x = copy.deepcopy(nodes[j])
+        lab = x["metadata"].setdefault("labels", {})
+        spec = x.setdefault("spec", {})
+        for _ in range(rng.randint(1, 3)):
+            kind = rng.choice(["set", "drop", "taint+", "taint-", "taint~", "unsched"] if taints else ["set", "drop", "unsched"])
+            keys = list(vals)
+            if kind == "set" and keys:
+                k = rng.choice(keys)
+                lab[k] = rng.choice(vals[k])
+            elif kind == "drop":
+                droppable = [k for k in lab if k not in topo]
+                if droppable:
+                    del lab[rng.choice(droppable)]
+            elif kind == "taint+":
+                t = rng.choice(taints)
+                spec.setdefault("taints", []).insert(rng.randint(0, len(spec.get("taints") or [])), copy.deepcopy(t))
+            elif kind == "taint-" and spec.get("taints"):
+                spec["taints"].pop(rng.randrange(len(spec["taints"])))
+            elif kind == "taint~" and spec.get("taints"):
+                spec["taints"][rng.randrange(len(spec["taints"]))] = copy.deepcopy(rng.choice(taints))
+                rng.shuffle(spec["taints"])
+            elif kind == "unsched":
+                spec["unschedulable"] = not spec.get("unschedulable", False)
+        ev.append({"op": "updateNode", "node": x})
+        nodes[j] = x
+    if fresh:
+        x = copy.deepcopy(nodes[0])
+        x["metadata"].setdefault("labels", {})["tier"] = "never-seen-before"
+        ev.append({"op": "updateNode", "node": x})
+        nodes[0] = x
+    return ev, nodes
+
+
+STATIC_CASES = [
+    ("cfg3", 3, dict(n_nodes=200, n_pods=80)),
+    ("cfg2", 2, dict(n_nodes=200, n_pods=120)),
+    ("cfg4", 4, dict(n_nodes=160, n_existing=600, n_pods=60, n_zones=6)),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["inplace", "reencode", "fresh"])
+@pytest.mark.parametrize("name,c,sizes", STATIC_CASES, ids=[c[0] for c in STATIC_CASES])
+def test_node_label_taint_events_in_place(name, c, sizes, path):
+    """Node label / taint / unschedulable rewrites between cycles go to the device
+    columns in place (no re-encode) when the vocabularies hold their values and no
+    topology key changes; a batch with a value no node carried is re-encoded.
+    Cycle mode for the first half, events, then queue mode for the second half —
+    every result matches the oracle on the equivalent fresh cluster."""
+    import random
+    rng = random.Random(7100 + c)
+    doc = g.generate(c, **sizes)
+    n, k = len(doc["queue"]), len(doc["queue"]) // 2
+    s = Scheduler(doc["profile"])
+    s.load_cluster(dict(doc, queue=[]))
+    placed = []
+    for pod in doc["queue"][:k]:
+        _, r = s.cycle(pod, commit=True)
+        placed.append(r.selected if r.status == 0 else -1)
+    ev, nodes = _static_events(doc, rng, fresh=path == "fresh")
+    s.apply_events(ev, reencode=path == "reencode")
+    if path == "inplace":
+        with pytest.raises(Exception, match="reset after in-place"):
+            s.reset()
+    bound = copy.deepcopy(doc.get("pods", []))
+    names = [x["metadata"]["name"] for x in doc["nodes"]]
+    for i in range(k):
+        if placed[i] >= 0:
+            p = copy.deepcopy(doc["queue"][i])
+            p["spec"]["nodeName"] = names[placed[i]]
+            bound.append(p)
+    eq = dict(doc, nodes=nodes, pods=bound, queue=[_nowhere(i) for i in range(k)] + doc["queue"][k:])
+    o = Oracle(eq)
+    o.schedule(record=3)
+    h = (n - k) // 2
+    for i in range(k, k + h):  # cycle mode
+        q, r = s.cycle(doc["queue"][i], commit=True)
+        assert (r.selected, r.feasible, r.status) == o.result(i), (name, path, i)
+        if i % 7 == 0:
+            a, b = s.annotations(q), o.annotations(i)
+            for key in b:
+                assert a.get(key) == b[key], (name, path, i, key)
+    # the rest through a second batch (queue mode): the context's own queue
+    s2 = Scheduler(doc["profile"])
+    s2.load_cluster(dict(doc, pods=copy.deepcopy(bound), queue=[_nowhere(i) for i in range(k)] + doc["queue"][k:]))
+    s2.schedule(0, k)
+    ev2, nodes2 = _static_events(doc, random.Random(7200 + c), fresh=path == "fresh")
+    s2.apply_events(ev2, reencode=path == "reencode")
+    if path == "inplace":
+        with pytest.raises(Exception, match="reset after in-place"):
+            s2.reset()
+    o2 = Oracle(dict(eq, nodes=nodes2))
+    o2.schedule(record=0)
+    s2.schedule(k, n - k)
+    got = s2.results(k, n - k)
+    for i in range(k, n):
+        assert (got[i - k].selected, got[i - k].feasible, got[i - k].status) == o2.result(i), (name, path, "queue", i)

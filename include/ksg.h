@@ -351,8 +351,10 @@ void ksg_cycle_view_release(const ksg_cycle_view* view);
  * pod that was scheduled (its placement is released, its result kept);
  * removeNode requires that no pod is bound or assumed on the node (upstream
  * deletes the node's pods first).  Batches of bound-pod add/remove events,
- * deletions of queue pods scheduled since the last encode, and allocatable-only
- * node updates that bring no new vocabulary are applied in
+ * deletions of queue pods scheduled since the last encode, and node updates of
+ * allocatable, spec.unschedulable, labels (keys and values some node already
+ * carried, no topology key changing value) and taints (taints some node already
+ * carried) with the same images, all bringing no new vocabulary, are applied in
  * place on the device; any other batch re-encodes the snapshot (after an in-place
  * batch ksg_reset is refused: reload).  Placements of scheduled queue pods are kept;
  * node indices after a removed node shift down by one.  Per-node outputs kept for

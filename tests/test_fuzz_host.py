@@ -121,6 +121,18 @@ def _events(doc, r):
         n = copy.deepcopy(r.choice(nodes))
         n["status"]["allocatable"]["cpu"] = "64"
         ev.append({"op": "updateNode", "node": n})
+        # label / taint / unschedulable rewrites with values other nodes carry (in place)
+        m = copy.deepcopy(r.choice(nodes))
+        other = r.choice(nodes)
+        lab = m["metadata"].setdefault("labels", {})
+        for k, v in list((other["metadata"].get("labels") or {}).items())[:3]:
+            lab[k] = v
+        if lab and r.random() < 0.5:
+            del lab[r.choice(sorted(lab))]
+        spec = m.setdefault("spec", {})
+        spec["taints"] = copy.deepcopy((other.get("spec") or {}).get("taints") or [])[::-1]
+        spec["unschedulable"] = r.random() < 0.5
+        ev.append({"op": "updateNode", "node": m})
         ev.append({"op": r.choice(["removeNode", "addNode"]), "name": "node-x", "node": copy.deepcopy(nodes[0])})
     return {"events": ev}
 

@@ -63,7 +63,7 @@ def pmc_issue(kernel, kernel_ms):
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*cfg5_pmc_sq.csv")), reverse=True):
         for row in csv.DictReader(open(f)):
-            if row["kernel"].split("::")[-1] != kernel:
+            if row["kernel"].split("::")[-1].split("<")[0] != kernel:  # (template arguments dropped)
                 continue
             salu = float(row["SQ_INSTS_SALU_per_dispatch"])
             valu = float(row["SQ_INSTS_VALU_per_dispatch"])
@@ -152,7 +152,8 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
     if classes:  # class path: per-class best keys, nothing per pair in memory
         kernel = "k_whatif_cls1 + k_whatif_cls2 (one step)"
         traffic = pmc_step_traffic(["cfg5:k_whatif_cls1", "cfg5:k_whatif_cls2"])
-        note = ("issue-bound: pass 1 (k_whatif_cls1) is limited by VALU / SALU issue (`issue`, from "
+        note = ("issue-bound: pass 1 (k_whatif_cls1) runs at its occupancy limit (4 waves/SIMD, LDS) with "
+                "VALU / SALU / SMEM issue and their latencies as the limit (`issue`: utilisation from "
                 "profiles/*cfg5_pmc_sq.csv), not HBM: its measured traffic is far below the §8(d) bytes, "
                 "so `frac` prices the step against bytes it never moves")
         issue = pmc_issue("k_whatif_cls1", kernel_ms)

@@ -2361,6 +2361,14 @@ struct WinArgs {
   // (the merges hand over keys and rows without waiting for P_{W-1}); 0 = the
   // merges do it once P_{W-1} is published (PriorRec)
   uint32_t prior_fix;
+  // persistent loop, split hand-over (KSG_WIN_SPLIT=1): a merge counts its keys and
+  // shallow rows out (evk) before its prior step, so the replay stages them while the
+  // prior steps run and waits for the records (evd_wait >= evd_need; null: not split)
+  // only before it reads the PriorRecs
+  uint32_t split;
+  uint32_t* evk;
+  const uint32_t* evd_wait;
+  uint32_t evd_need;
   const uint32_t* nxt_evd;  // persistent loop: the next window's record counter and its target (null: last)
   uint32_t nxt_need;
 };
@@ -3606,6 +3614,10 @@ __device__ __forceinline__ void win_merge(const DevCluster& C, const DevProfile&
       for (int k = 0; k < 3; ++k) stv<true>(reinterpret_cast<int32_t*>(A.erec) + k * KSG_BATCH + b, f[k]);
       stv<true>(A.arrive + b * A.astride, 0u);
     }
+    if (A.evk) {  // (split hand-over) keys, shallow rows and counts are out: the replay may stage them
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(A.evk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // the prior step: pod q on P_{E-1}'s nodes (published by the replay of E-1);
     // prior_fix: the replay evaluates it itself
     int np1 = 0;
@@ -4249,7 +4261,8 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
   uint64_t pr_k = 0, pr_p0 = 0, pr_p1 = 0, pr_m = 0;
   int32_t pr_df = 0;
   const bool prior_rec_in = PER && !A.prior_fix;  // (else the prior step is evaluated below)
-  if (prior_rec_in) {
+  const bool pr_late = prior_rec_in && A.evd_wait != nullptr;  // (split: after the keys and rows are requested)
+  auto prior_loads = [&]() {
     if (ppb < nb) {
       pr_k = ldv<true>(&PR[ppb].pkey[ppe]);
       const uint64_t* pw = reinterpret_cast<const uint64_t*>(&PR[ppb].patch[ppe]);
@@ -4260,7 +4273,8 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       if (ppe == 1) pr_m = ldv<true>(&PR[ppb].pbest);
       if (ppe == 2) pr_m = (uint64_t)(uint32_t)ldv<true>(&PR[ppb].pbest_e);
     }
-  }
+  };
+  if (prior_rec_in && !pr_late) prior_loads();
   {
     const uint64_t pv = tid < KSG_BATCH * kPendW ? ldv<PER>(reinterpret_cast<const uint64_t*>(A.pprev) + tid) : 0;
     constexpr int kPodW = (int)(sizeof(PodLite) / 8);
@@ -4329,6 +4343,19 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       int p = row / KSG_STAGE, r = row - p * KSG_STAGE;
       if constexpr (PER) rv[k] = i < nr ? ldv<true>(reinterpret_cast<const uint64_t*>(&PR[p].row[r]) + wd) : 0;
       else rv[k] = i < nr ? rows[(size_t)(p * KSG_CAND + r) * kRowW + wd] : 0;
+    }
+    if (pr_late) {  // the keys and rows are in flight: wait for the window's prior steps, then their records
+      if (tid == 0) {
+        bool ok = false;
+        for (uint32_t it = 0; it < A.spin; ++it) {
+          if (ld_sc1(A.evd_wait) >= A.evd_need) { ok = true; break; }
+          if ((it & 63u) == 63u && ld_sc1(A.abortw) != 0u) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (!ok) __hip_atomic_store(A.abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      prior_loads();
     }
     if (tid < np * kPendW) reinterpret_cast<uint64_t*>(L.prior)[tid] = pv;
     if (tid < nb * kPodW) reinterpret_cast<uint64_t*>(L.pod)[tid] = qv;
@@ -4854,6 +4881,8 @@ struct WinSync {
   uint32_t pad1[30];
   uint32_t flushed[2];    // per window parity: eval blocks whose outputs are written (cumulative)
   uint32_t pad2[30];
+  uint32_t evk[2];        // per window parity: pods whose keys and shallow rows are out (split hand-over)
+  uint32_t pad3[30];
 };
 struct WinRunArgs {
   uint32_t nwin, first, count, T;
@@ -4916,12 +4945,18 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
       // parity is whole, KSG_BATCH pods)
       A.flushed = &Z->flushed[W & 1];
       A.flush_need = ((W >> 1) * KSG_BATCH + A.nw) * R.T;
-      if (!ready && !win_wait_ge(&Z->evd[W & 1], (W >> 1) * KSG_BATCH + A.nw, abortw, RC.spin, &go)) return;
+      // (split: the keys counter gates the stage, the records counter the PriorRec reads;
+      // `ready` then refers to the keys counter)
+      const uint32_t need = (W >> 1) * KSG_BATCH + A.nw;
+      const bool split = A0.split && !A0.prior_fix;
+      if (!ready && !win_wait_ge(split ? &Z->evk[W & 1] : &Z->evd[W & 1], need, abortw, RC.spin, &go)) return;
+      A.evd_wait = split ? &Z->evd[W & 1] : nullptr;
+      A.evd_need = need;
       A.pub = &Z->replayed[0][0];
       A.pub_val = W + 1;
       if (W + 1 < R.nwin) {
         const uint32_t w1 = W + 1, nw1 = min((uint32_t)KSG_BATCH, R.first + R.count - (R.first + w1 * KSG_BATCH));
-        A.nxt_evd = &Z->evd[w1 & 1];
+        A.nxt_evd = split ? &Z->evk[w1 & 1] : &Z->evd[w1 & 1];
         A.nxt_need = (w1 >> 1) * KSG_BATCH + nw1;
       } else {
         A.nxt_evd = nullptr;
@@ -4947,6 +4982,7 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
       A.arrive = R.arrive + (size_t)(E & 1) * KSG_BATCH * 32;
       A.estamps = R.stamps ? R.stamps + (size_t)E * 32 : nullptr;
       A.evd = &Z->evd[E & 1];
+      A.evk = A0.split && !A0.prior_fix ? &Z->evk[E & 1] : nullptr;
       A.pcur = R.pend + (size_t)((E + 1) & 1) * KSG_BATCH;  // P_{E-1}
       A.pcur_n = R.pend_n + ((E + 1) & 1);
       A.pubw = E >= 1 ? &Z->replayed[b & 15][0] : nullptr;
@@ -4971,6 +5007,7 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
     A.arrive = R.arrive + (size_t)(E & 1) * KSG_BATCH * 32;
     A.estamps = R.stamps ? R.stamps + (size_t)E * 32 : nullptr;
     A.evd = &Z->evd[E & 1];
+    A.evk = A0.split && !A0.prior_fix ? &Z->evk[E & 1] : nullptr;
     A.flushed = &Z->flushed[E & 1];
     A.pcur = R.pend + (size_t)((E + 1) & 1) * KSG_BATCH;  // P_{E-1}
     A.pcur_n = R.pend_n + ((E + 1) & 1);
@@ -5177,6 +5214,7 @@ struct Engine::Impl {
   int win_mblocks = 0;           // ... with dedicated merge blocks (KSG_WIN_MB=1; the last tile block merges: measured faster)
   int view_copy = 0;             // cycle view: 1 = the per-node arrays by a copy (KSG_VIEW_COPY), 0 = written by k_view
   int run_overlap = 0;           // k_chain_run: pod k+1's class-table reads during pod k's hand-offs (KSG_RUN_OVERLAP=1; measured no faster)
+  int win_split = 0;             // ... split hand-over: keys staged while the prior steps run (KSG_WIN_SPLIT=1)
   int win_pfix = 0;              // ... the replay evaluates the prior step itself (KSG_WIN_PFIX=1; measured slower)
   uint64_t win_runs = 0, win_fallbacks = 0;  // diagnostic: persistent window launches / not co-resident
   uint32_t fold_blocks = 256;  // table chain: k_fold above this many blocks (KSG_FOLD_BLOCKS; tests force it)
@@ -5332,6 +5370,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (const char* e = std::getenv("KSG_WIN_RUN")) I.win_run_on = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_MB")) I.win_mblocks = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_PFIX")) I.win_pfix = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_WIN_SPLIT")) I.win_split = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_RUN_OVERLAP")) I.run_overlap = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_VIEW_COPY")) I.view_copy = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_RUN_SPIN")) I.run_spin = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
@@ -5918,6 +5957,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     AP.mblocks = mb ? 1u : 0u;
     AP.astride = 32;
     AP.prior_fix = I.win_pfix ? 1u : 0u;
+    AP.split = I.win_split ? 1u : 0u;
     __atomic_store_n(I.hverdict, 0u, __ATOMIC_RELEASE);
     const RunCtl RC{grid + I.run_need_extra, I.run_wait_us * 100u, 0, I.hverdict, I.run_spin};
     const bool sampled = I.sample_every && I.n_samples * 2 + 2 <= I.sev.size();

@@ -5214,7 +5214,7 @@ struct Engine::Impl {
   int win_mblocks = 0;           // ... with dedicated merge blocks (KSG_WIN_MB=1; the last tile block merges: measured faster)
   int view_copy = 0;             // cycle view: 1 = the per-node arrays by a copy (KSG_VIEW_COPY), 0 = written by k_view
   int run_overlap = 0;           // k_chain_run: pod k+1's class-table reads during pod k's hand-offs (KSG_RUN_OVERLAP=1; measured no faster)
-  int win_split = 0;             // ... split hand-over: keys staged while the prior steps run (KSG_WIN_SPLIT=1)
+  int win_split = 1;             // ... split hand-over: keys staged while the prior steps run (KSG_WIN_SPLIT=0: one counter)
   int win_pfix = 0;              // ... the replay evaluates the prior step itself (KSG_WIN_PFIX=1; measured slower)
   uint64_t win_runs = 0, win_fallbacks = 0;  // diagnostic: persistent window launches / not co-resident
   uint32_t fold_blocks = 256;  // table chain: k_fold above this many blocks (KSG_FOLD_BLOCKS; tests force it)

@@ -163,14 +163,14 @@ def test_tight_cluster_both_paths(per_pod):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"KSG_WIN_MB": "1"}, {"KSG_WIN_PFIX": "1"}, {"KSG_WIN_MB": "1", "KSG_WIN_PFIX": "1"},
-                                 {"KSG_WIN_RUN": "0"}, {"KSG_WIN_SPLIT": "1"}, {"KSG_WIN_SPLIT": "1", "KSG_WIN_MB": "1"}],
-                         ids=["default", "merge-blocks", "prior-in-replay", "both", "launch-per-window", "split",
-                              "split-merge-blocks"])
+                                 {"KSG_WIN_RUN": "0"}, {"KSG_WIN_SPLIT": "0"}, {"KSG_WIN_SPLIT": "0", "KSG_WIN_MB": "1"}],
+                         ids=["default", "merge-blocks", "prior-in-replay", "both", "launch-per-window", "one-counter",
+                              "one-counter-merge-blocks"])
 def test_cfg2_large_batch_path_selected_nodes(monkeypatch, env):
     """Full-width cfg2 node count, a queue of 1,000 pods: every selection equals the
     oracle's, for each variant of the window loop (dedicated merge blocks, the
-    prior step evaluated by the replay, one launch per window, the hand-over split
-    into a keys counter and a records counter)."""
+    prior step evaluated by the replay, one launch per window, the hand-over on one
+    counter instead of the default split keys / records counters)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     doc = g.generate(2, n_nodes=5000, n_pods=1000)

@@ -2240,7 +2240,9 @@ __global__ __launch_bounds__(kBlock) void k_fs_static(DevCluster C, DevProfile F
 #define KSG_TILE KSG_WIN_THREADS  // nodes per eval block
 #define KSG_STASH_NPT 8    // eval tiles of up to this many nodes per thread hold their outputs in LDS
 #ifndef KSG_STAGE
+#ifndef KSG_STAGE
 #define KSG_STAGE 4        // candidate ranks whose rows are staged in LDS (deeper ranks: global; 4 measured +4% over 16 on cfg2)
+#endif
 #endif
 #define KSG_XHDR 512       // record header: per pod feasible count, static-max achievers (Taint, NodeAffinity): 3 x KSG_BATCH ints
 #define KSG_NOT_PATCHED 0xFFFFFFFDu

@@ -13,10 +13,14 @@ steps.  Multi-GPU: one process per GPU (torch.distributed.run); each rank owns
 its own shard of nodes of a weak-scaled cluster (5,000 nodes per GPU) —
 see DESIGN.md "Multi-GPU".
 
-At N=1 the same JSON line also carries the other BASELINE configs as extra keys
+The same JSON line also carries the other BASELINE configs as extra keys
 (--extra): cfg3 and cfg4 queues at full size, and cfg5 — one what-if step of
 4,096 pods x 1,000,000 nodes per timed step (bench_whatif.py) — each with its own
-roofline and CPU baseline.
+roofline (and, at N=1, its CPU baseline).  At N>1 they run node-sharded over the
+N ranks at their BASELINE sizes (strong scaling: the cluster is fixed, every rank
+holds 1/N of its nodes; RCCL all-gathers on the engine stream, "transport"),
+which is what BASELINE.json quotes for cfg3 ("1 and 8 MI355X"), cfg4 ("8x
+sharded") and cfg5 ("node-sharded over 8x with RCCL argmax").
 """
 import argparse
 import json
@@ -39,8 +43,10 @@ def parse():
     ap.add_argument("--pods", type=int, default=10000)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on a bounded sample (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="CPU time per oracle variant")
-    ap.add_argument("--extra", default="3,4,5", help="other BASELINE configs reported beside cfg2 (N=1 only; "
-                    "5 = the cfg5 what-if step of bench_whatif.py)")
+    ap.add_argument("--extra", default="3,4,5", help="other BASELINE configs reported beside cfg2 (node-sharded "
+                    "at N>1; 5 = the cfg5 what-if step of bench_whatif.py)")
+    ap.add_argument("--extra-sizes", default="", help="tests only: c:nodes:pods[:existing],... overriding the "
+                    "BASELINE sizes of the extra configs (e.g. 3:300:64,4:400:64:800,5:2000:64)")
     ap.add_argument("--extra-steps", type=int, default=2)
     ap.add_argument("--cpu-workers", type=int, default=16, help="parallelize.Until workers (upstream default 16)")
     return ap.parse_args()
@@ -171,11 +177,18 @@ def time_queue(s, torch, steps, warmup, dist=None):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return elapsed
+    return max_over_ranks(torch, dist, elapsed)
+
+
+def max_over_ranks(torch, dist, x):
+    """The slowest rank's value (the contract's max-over-ranks timing); the
+    tensor lives where the process group's backend reduces (RCCL: the GPU)."""
+    if not dist:
+        return x
+    dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def sample_dominant(s, every):
@@ -234,16 +247,23 @@ CFG4_RUN_NODE_BYTES = 68        # SURVEY §8(d) cfg4 per node and pod (row 56, z
                                 # k_chain_run keeps the row and zone id on chip and writes no per-pair outputs
 
 
-def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
-    from ksg import Scheduler, generator as g
+def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers, rank=0, world=1, local=0, dist=None, size=None):
+    """cfg3 / cfg4 at their BASELINE size, on one GPU or node-sharded over `world`
+    ranks (strong scaling); the line on rank 0, else None."""
+    from ksg import generator as g
     t0 = time.perf_counter()
-    blob = g.generate_native(c)  # native twin of the seeded generator (tests/test_synth.py)
+    kw = {}
+    if size:
+        kw = dict(n_nodes=size[0], n_pods=size[1], **({"n_existing": size[2]} if len(size) > 2 else {}))
+    blob = g.generate_native(c, **kw)  # native twin of the seeded generator (tests/test_synth.py)
     doc = json.loads(blob)
     gen_s = time.perf_counter() - t0
-    s = Scheduler(doc["profile"])
+    from ksg.distributed import sharded_scheduler
+    s = sharded_scheduler(doc["profile"], torch, rank, world, local)
     s.load_cluster(blob)
-    n_nodes, n_pods = s.n_nodes, s.queue_len
-    elapsed = time_queue(s, torch, steps, warmup)
+    n_nodes, n_pods = s.n_nodes, s.queue_len  # n_nodes: the whole cluster
+    shard = n_nodes // world
+    elapsed = time_queue(s, torch, steps, warmup, dist)
     run0 = s.run_counts()
     kms, kn = sample_dominant(s, 16)
     run1 = s.run_counts()
@@ -254,10 +274,10 @@ def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
         # k_window's own bytes; k_static (the Taint / NodeAffinity records it reads)
         # gets its own line, timed on the same sampled run
         kname = "k_window"
-        tiles = (n_nodes + TILE - 1) // TILE
-        bpl = WINDOW * n_nodes * CFG3_WINDOW_PAIR_BYTES + 2 * tiles * WINDOW * 64 * 8 + 2 * REC_BYTES
+        tiles = (shard + TILE - 1) // TILE
+        bpl = WINDOW * shard * CFG3_WINDOW_PAIR_BYTES + 2 * tiles * WINDOW * 64 * 8 + 2 * REC_BYTES
         st_ms, st_n, st_pods = s.static_time()
-        if st_n:
+        if st_n:  # (sharded: k_static covers every node of the cluster on every rank)
             sb = st_pods * n_nodes * CFG3_STATIC_PAIR_BYTES
             win_ms_total = kms * ((n_pods + WINDOW - 1) // WINDOW)
             extra_kernels = {
@@ -267,7 +287,7 @@ def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
                 "step": {"note": "both kernels over the whole queue: pairs x (k_static + k_window bytes per pair) / "
                                  "(k_static time + k_window time); the k_window time is its sampled average x windows",
                          "bytes_per_pair": CFG3_STATIC_PAIR_BYTES + CFG3_WINDOW_PAIR_BYTES,
-                         "frac": n_pods * n_nodes * (CFG3_STATIC_PAIR_BYTES + CFG3_WINDOW_PAIR_BYTES)
+                         "frac": n_pods * (n_nodes * CFG3_STATIC_PAIR_BYTES + shard * CFG3_WINDOW_PAIR_BYTES)
                          / ((st_ms + win_ms_total) * 1e-3) / 1e9 / HBM_PEAK_GBS}}
     elif run1[1] > run0[1]:
         # persistent segments: one k_chain_run launch per segment of pods; the
@@ -275,29 +295,45 @@ def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers):
         kname = "k_chain_run"
         per = (run1[0] - run0[0]) / (run1[1] - run0[1])
         kms = kms / per
-        bpl = n_nodes * CFG4_RUN_NODE_BYTES
-    else:
+        bpl = shard * CFG4_RUN_NODE_BYTES
+    else:  # (sharded: the two-launch chain on the rank's shard, two all-gathers per pod)
         kname = "k_eval"
-        bpl = n_nodes * CFG4_EVAL_NODE_BYTES
+        bpl = shard * CFG4_EVAL_NODE_BYTES
     achieved = bpl / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    if rank != 0:
+        del s
+        return None
     out = {"metric": "filter+score pod x node pairs/sec", "value": n_nodes * n_pods * steps / elapsed,
-           "unit": "pairs/s", "steps": steps, "warmup": warmup, "ms_per_step": elapsed * 1e3 / steps,
+           "unit": "pairs/s", "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": elapsed * 1e3 / steps,
            "us_per_pod": elapsed * 1e6 / (steps * n_pods),
            "scheduled_pods_per_s": sum(1 for r in res if r.status == 0) * steps / elapsed,
-           "config": {"workload": f"cfg{c}", "nodes": n_nodes, "existing_pods": len(doc["pods"]), "pods": n_pods,
-                      "profile": doc["profile"]["plugins"], "path": "window" if s.batch_path else "table chain"},
+           "scaling": "strong",
+           "config": {"workload": f"cfg{c}", "nodes": n_nodes, "nodes_per_gpu": shard, "existing_pods": len(doc["pods"]),
+                      "pods": n_pods, "profile": doc["profile"]["plugins"],
+                      "path": "window" if s.batch_path else "table chain",
+                      "parallelism": f"node-shard x{world}" if world > 1 else "1 GPU",
+                      **({"transport": "rccl"} if world > 1 else {})},
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(f"cfg{c}:{kname}"),
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(f"cfg{c}:{kname}") if world == 1 else None,
                         "kernel": kname, "kernel_avg_us": kms * 1e3, "kernel_samples": kn, "bytes_per_launch": bpl,
                         **({"pods_per_launch": per, "note": "k_chain_run: kernel_avg_us and bytes_per_launch per pod "
                             "cycle inside the persistent launch (launch time / its pods)"} if per else {}),
                         **({"bytes_per_pair": CFG3_WINDOW_PAIR_BYTES, "other_kernels": extra_kernels} if extra_kernels else {})},
            "generate_s": round(gen_s, 1)}
-    if c == 4:
+    if c == 4 and world == 1:
         out["dropin"] = dropin_latency(s, doc)
     del s
-    if cpu_seconds > 0:
+    if cpu_seconds > 0 and world == 1:
         out["cpu_baseline"] = cpu_baseline(blob, n_nodes, cpu_workers, cpu_seconds, f"cfg{c}")
+    return out
+
+
+def parse_sizes(spec):
+    """--extra-sizes "c:nodes:pods[:existing],..." -> {c: (nodes, pods[, existing])}."""
+    out = {}
+    for part in (x for x in spec.split(",") if x):
+        f = [int(v) for v in part.split(":")]
+        out[f[0]] = tuple(f[1:])
     return out
 
 
@@ -312,16 +348,20 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from ksg import Scheduler, generator as g
+    out = run(a, torch, rank, world, local, dist)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+
+
+def run(a, torch, rank=0, world=1, local=0, dist=None):
+    """The whole bench line (rank 0; None on the other ranks)."""
+    from ksg import generator as g
+    from ksg.distributed import sharded_scheduler
 
     # weak scaling: a cluster of nodes x world nodes, node-sharded (each rank owns
     # `nodes`); every pod is scheduled over the whole cluster (RCCL exchange per batch)
     doc = g.generate(2, n_nodes=a.nodes * world, n_pods=a.pods)
-    stream = torch.cuda.current_stream().cuda_stream if world > 1 else None
-    s = Scheduler(doc["profile"], device=local, stream=stream, shard_rank=rank, shard_count=world)
-    if world > 1:
-        from ksg.distributed import rccl_unique_id_broadcast
-        s.set_exchange_rccl(rccl_unique_id_broadcast(s.L, rank))
+    s = sharded_scheduler(doc["profile"], torch, rank, world, local)
     s.load_cluster(doc)
     n_nodes, n_pods = s.n_nodes, s.queue_len  # n_nodes: whole cluster
     elapsed = time_queue(s, torch, a.steps, a.warmup, dist)
@@ -345,51 +385,61 @@ def main():
         kname = "k_filter_score"
         bytes_per_launch = shard * algorithmic_bytes_per_node_fit_ba()
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
-    traffic = pmc_traffic(kname)
+    traffic = pmc_traffic(kname) if world == 1 else None
     if persistent and traffic is not None:
         traffic /= nwin  # (the PMC pass counts the whole-queue launch: per window, like bytes_per_launch)
-    if rank != 0:
-        return
-    out = {
-        "metric": "filter+score pod x node pairs/sec (5k nodes, Fit+BalancedAllocation)",
-        "value": value,
-        "unit": "pairs/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": ms_per_step,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "int64+f64",
-        "data": "synthetic (seeded generator, SURVEY.md §8(d) cfg2)",
-        "config": {"workload": "cfg2: 5,000 nodes x 10,000 pods, NodeResourcesFit+NodeResourcesBalancedAllocation",
-                   "nodes_per_gpu": shard, "nodes_total": n_nodes, "pods": n_pods, "parallelism": f"node-shard x{world} (RCCL all-gather per 32-pod batch)" if world > 1 else "1 GPU"},
-        "scheduled_pods_per_s": scheduled * a.steps / elapsed,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": kname, "kernel_avg_us": kernel_ms * 1e3, "kernel_samples": kcount,
-                     "bytes_per_launch": bytes_per_launch,
-                     **({"note": "k_window_run: the whole queue in one persistent launch; kernel_avg_us and "
-                                 "bytes_per_launch per 32-pod window inside it (launch time / windows)",
-                         "windows_per_launch": nwin} if persistent else {})},
-    }
-    if dropin:
-        out["dropin"] = dropin
-    if a.cpu_baseline and world == 1:
-        out["cpu_baseline"] = cpu_baseline(json.dumps(doc).encode(), n_nodes, a.cpu_workers, a.cpu_seconds, "cfg2")
-    if world == 1 and a.extra:
-        for c in (int(x) for x in a.extra.split(",") if x):
-            if c == 5:  # what-if steps: 1M nodes x 4,096 pods per step (bench_whatif.py)
-                import bench_whatif
-                wa = bench_whatif.parse(["--steps", str(max(a.extra_steps, 2)), "--warmup", "1",
-                                         "--cpu-pods", "16" if a.cpu_baseline else "0",
-                                         "--cpu-workers", str(a.cpu_workers)])
-                out["cfg5"] = bench_whatif.run(wa, torch)
-                continue
-            out[f"cfg{c}"] = extra_config(c, torch, a.extra_steps, 1, a.cpu_seconds if a.cpu_baseline else 0,
-                                          a.cpu_workers)
-    print(json.dumps(out))
+    del s
+    out = None
+    if rank == 0:
+        out = {
+            "metric": "filter+score pod x node pairs/sec (5k nodes, Fit+BalancedAllocation)",
+            "value": value,
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64+f64",
+            "data": "synthetic (seeded generator, SURVEY.md §8(d) cfg2)",
+            "config": {"workload": "cfg2: 5,000 nodes x 10,000 pods, NodeResourcesFit+NodeResourcesBalancedAllocation",
+                       "nodes_per_gpu": shard, "nodes_total": n_nodes, "pods": n_pods,
+                       "parallelism": f"node-shard x{world} (RCCL all-gather per 32-pod batch)" if world > 1 else "1 GPU",
+                       **({"transport": "rccl"} if world > 1 else {})},
+            "scheduled_pods_per_s": scheduled * a.steps / elapsed,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": kname, "kernel_avg_us": kernel_ms * 1e3, "kernel_samples": kcount,
+                         "bytes_per_launch": bytes_per_launch,
+                         **({"note": "k_window_run: the whole queue in one persistent launch; kernel_avg_us and "
+                                     "bytes_per_launch per 32-pod window inside it (launch time / windows)",
+                             "windows_per_launch": nwin} if persistent else {})},
+        }
+        if dropin:
+            out["dropin"] = dropin
+        if a.cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(json.dumps(doc).encode(), n_nodes, a.cpu_workers, a.cpu_seconds, "cfg2")
+    # the other BASELINE configs: one GPU, or node-sharded over every rank (each
+    # rank runs every leg: the exchanges are collective)
+    sizes = parse_sizes(a.extra_sizes)
+    for c in (int(x) for x in a.extra.split(",") if x):
+        if c == 5:  # what-if steps: 1M nodes x 4,096 pods per step (bench_whatif.py)
+            import bench_whatif
+            wargs = ["--steps", str(max(a.extra_steps, 2)), "--warmup", "1",
+                     "--cpu-pods", "16" if (a.cpu_baseline and world == 1) else "0", "--cpu-workers", str(a.cpu_workers)]
+            if c in sizes:
+                wargs += ["--nodes", str(sizes[c][0]), "--step-pods", str(sizes[c][1])]
+            r = bench_whatif.run(bench_whatif.parse(wargs), torch, rank, world, local, dist)
+            if r is not None and world > 1:
+                r["config"]["transport"] = "rccl"
+        else:
+            r = extra_config(c, torch, a.extra_steps, 1, a.cpu_seconds if (a.cpu_baseline and world == 1) else 0,
+                             a.cpu_workers, rank, world, local, dist, sizes.get(c))
+        if out is not None:
+            out[f"cfg{c}"] = r
+    return out
 
 
 if __name__ == "__main__":

@@ -94,7 +94,8 @@ def main():
 def run(a, torch, rank=0, world=1, local=0, dist=None):
     """One what-if benchmark (args as parse()); the result line on rank 0, else None
     (bench.py reports cfg5 through this at N=1)."""
-    from ksg import Scheduler, generator as g
+    from ksg import generator as g
+    from ksg.distributed import sharded_scheduler
     t0 = time.time()
     n_pods = a.step_pods * (a.warmup + a.steps + 1)  # (+1: one untimed step with kernel sampling)
     if a.variant == "pts-ipa":
@@ -104,11 +105,7 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
     prof = json.loads(blob[blob.index(b'"profile"') + 10:].split(b',"nodes"', 1)[0]) if blob.startswith(b'{"profile"') \
         else json.loads(blob)["profile"]
     print(f"[rank {rank}] generated {a.nodes} nodes / {n_pods} pods in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
-    stream = torch.cuda.current_stream().cuda_stream if world > 1 else None
-    s = Scheduler(prof, device=local, stream=stream, shard_rank=rank, shard_count=world)
-    if world > 1:
-        from ksg.distributed import rccl_unique_id_broadcast
-        s.set_exchange_rccl(rccl_unique_id_broadcast(s.L, rank))
+    s = sharded_scheduler(prof, torch, rank, world, local)
     t0 = time.time()
     s.load_cluster(blob)
     print(f"[rank {rank}] loaded in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
@@ -127,8 +124,8 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device="cuda")
+    if dist:  # the slowest rank's time (gloo in the CPU test of the multi-rank path)
+        t = torch.tensor([elapsed], device="cpu" if dist.get_backend() == "gloo" else "cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     res = s.results(a.warmup * P, a.steps * P)

@@ -218,7 +218,11 @@ int ksg_annotations(ksg_ctx* ctx, uint32_t q, char* buf, size_t cap, size_t* len
  * re-encode of the snapshot (placements kept). */
 int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_pod_result* out);
 /* ReservePlugin.Reserve (wrappedplugin.go:631 -> scheduler cache assume):
- * assume queue pod q (run with commit == 0) on global node `node`. */
+ * assume queue pod q (run with commit == 0) on global node `node`.  The device
+ * delta is queued without a wait: a device failure of it is reported late, by the
+ * next call that synchronises (a cycle, a view, Unreserve ...), which then returns
+ * KSG_E_DEVICE and leaves the context refusing calls (KSG_E_STATE) until
+ * ksg_load_cluster, since the host already counts the pod as placed. */
 int ksg_reserve(ksg_ctx* ctx, uint32_t q, int32_t node);
 /* ReservePlugin.Unreserve (mock framework.go:611): undo the assume of queue
  * pod q (cycle or queue mode): node rows, and its existing-pod table entry. */

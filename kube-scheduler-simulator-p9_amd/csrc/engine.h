@@ -163,12 +163,13 @@ class Engine {
   bool pod_row(uint32_t q, int32_t& row, std::string& err);
   // Cluster event applied in place: node gnode's allocatable [R] and allowed pod count.
   bool node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_t allowed, std::string& err);
-  // Cluster event applied in place: node gnode's label value per node-label key
-  // ([K], -1 none; vocabulary and topology values unchanged), has-labels byte and
-  // KSG_NODE_* flags — into its columns when it is on this shard, and into the
-  // every-node static columns when the context keeps them.
-  bool node_static(int32_t gnode, const std::vector<int32_t>& label_vid, uint8_t has_labels, uint8_t flags,
-                   std::string& err);
+  // Cluster events applied in place, one batch: node gnodes[i]'s label value per
+  // node-label key (label_vid[i*K .. i*K+K), -1 none; vocabulary and topology
+  // values unchanged), has-labels byte and KSG_NODE_* flags — into its columns when
+  // it is on this shard, and into the every-node static columns when the context
+  // keeps them.  One stream synchronisation for the whole batch.
+  bool node_static(const std::vector<int32_t>& gnodes, const std::vector<int32_t>& label_vid,
+                   const std::vector<uint8_t>& has_labels, const std::vector<uint8_t>& flags, std::string& err);
   // The node taint lists replaced (CSR over this shard's nodes; gofs/gids over
   // every node, used when the context keeps the every-node static columns).
   bool node_taints(const std::vector<uint32_t>& offs, const std::vector<int32_t>& ids,

@@ -2240,9 +2240,7 @@ __global__ __launch_bounds__(kBlock) void k_fs_static(DevCluster C, DevProfile F
 #define KSG_TILE KSG_WIN_THREADS  // nodes per eval block
 #define KSG_STASH_NPT 8    // eval tiles of up to this many nodes per thread hold their outputs in LDS
 #ifndef KSG_STAGE
-#ifndef KSG_STAGE
 #define KSG_STAGE 4        // candidate ranks whose rows are staged in LDS (deeper ranks: global; 4 measured +4% over 16 on cfg2)
-#endif
 #endif
 #define KSG_XHDR 512       // record header: per pod feasible count, static-max achievers (Taint, NodeAffinity): 3 x KSG_BATCH ints
 #define KSG_NOT_PATCHED 0xFFFFFFFDu
@@ -5211,6 +5209,8 @@ struct Engine::Impl {
   uint32_t run_spin = kRunSpin;  // polls before a persistent block gives up (KSG_RUN_SPIN: tests force an abort)
   uint64_t run_fallbacks = 0;    // segments that ran on the two-launch chain (not co-resident)
   bool lost = false;             // an aborted persistent launch left the device state half-updated
+  bool unwaited = false;         // a state-changing launch was queued without a wait (Reserve's k_assume):
+                                 // a failing synchronisation then leaves host mirror and device apart (lost)
   DBuf<WinSync> wsync;           // k_window_run's counters (zeroed per launch)
   int win_run_on = 1;            // persistent window loop (k_window_run): KSG_WIN_RUN=0 turns it off
   int win_mblocks = 0;           // ... with dedicated merge blocks (KSG_WIN_MB=1; the last tile block merges: measured faster)
@@ -5336,6 +5336,19 @@ struct Engine::Impl {
     return S;
   }
 };
+// Every synchronisation of the engine stream: a failure after a state-changing
+// launch nobody waited for (ksg_reserve) means the host mirror counts a delta the
+// device may not hold, so the context is marked lost (ksg.h: errors reported late).
+static bool stream_sync(Engine::Impl& I, hipStream_t s, std::string& err) {
+  const hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    err = std::string("hipStreamSynchronize: ") + hipGetErrorString(e);
+    if (I.unwaited) I.lost = true;
+    return false;
+  }
+  if (s == I.stream) I.unwaited = false;
+  return true;
+}
 
 Engine::Engine() : p_(new Impl()) {}
 Engine::~Engine() {
@@ -5653,7 +5666,7 @@ bool Engine::upload(const NodeSoA& ns, const PodTableSoA& pt, uint32_t pod_cap, 
     HIPCHK(hipMemsetAsync(I.pend_n.p, 0, 2 * 4, s));
     HIPCHK(hipMemsetAsync(I.wrec.p, 0, 2 * kRecBytes, s));
   }
-  HIPCHK(hipStreamSynchronize(s));
+  if (!stream_sync(I, s, err)) return false;
   return true;
 }
 
@@ -6399,7 +6412,11 @@ bool Engine::assume(uint32_t q, int32_t gnode, int sign, std::string& err, bool 
   hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, I.stream, C, I.progs.p + I.prog_off[q], gnode, sign,
                      (I.has_pts || I.has_ipa) ? 1 : 0, I.prow.p + q);
   HIPCHK(hipGetLastError());
-  if (wait) HIPCHK(hipStreamSynchronize(I.stream));
+  if (wait) {
+    if (!stream_sync(I, I.stream, err)) return false;
+  } else {
+    I.unwaited = true;
+  }
   return true;
 }
 
@@ -6429,7 +6446,7 @@ bool Engine::bound_deltas(const std::vector<std::vector<uint8_t>>& progs, const 
                        I.evrow.p + slot[i]);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(rows.data(), I.evrow.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   return true;
 }
 
@@ -6456,7 +6473,7 @@ bool Engine::toggle_pods(const std::vector<const std::vector<uint8_t>*>& progs, 
     hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, I.stream, C, I.evprog.p + off[i], gnode[i], sign, 2,
                        I.evrow.p + i);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(I.stream));  // (the host buffers are reused by the next toggle)
+  if (!stream_sync(I, I.stream, err)) return false;  // (the host buffers are reused by the next toggle)
   return true;
 }
 
@@ -6486,7 +6503,7 @@ bool Engine::toggle_stage(const std::vector<const std::vector<uint8_t>*>& progs,
     HIPCHK(hipMemcpyAsync(I.tgnode.p, gnode.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(I.tgrow.p, rows.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
   }
-  HIPCHK(hipStreamSynchronize(s));  // (the host blob goes out of scope)
+  if (!stream_sync(I, s, err)) return false;  // (the host blob goes out of scope)
   I.tg_gnode = gnode;
   I.tg_n = (uint32_t)n;
   return true;
@@ -6522,7 +6539,7 @@ bool Engine::toggle_staged(const std::vector<uint32_t>& idx, int sign, std::stri
     hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, s, C, I.tgprog.p + I.tg_off[e], I.tg_gnode[e], sign, 2,
                        I.tgrow.p + e);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s));  // (the host index list goes out of scope)
+  if (!stream_sync(I, s, err)) return false;  // (the host index list goes out of scope)
   return true;
 }
 
@@ -6542,7 +6559,7 @@ bool Engine::dry_filter(uint32_t q, int32_t gnode, std::vector<uint32_t>& codes,
   HIPCHK(hipMemcpyAsync(codes.data(), I.filter.p + (gnode >= 0 ? (uint32_t)gnode - I.goff : 0),
                         codes.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipMemcpyAsync(I.sums.p + q, I.drysum.p, sizeof(ksg_pod_summary), hipMemcpyDeviceToDevice, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   return true;
 }
 
@@ -6550,7 +6567,7 @@ bool Engine::pod_row(uint32_t q, int32_t& row, std::string& err) {
   Impl& I = *p_;
   if (q >= I.prog_off.size()) { err = "program index out of range"; return false; }
   HIPCHK(hipMemcpyAsync(&row, I.prow.p + q, sizeof(int32_t), hipMemcpyDeviceToHost, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   return true;
 }
 
@@ -6562,28 +6579,34 @@ bool Engine::node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_
   for (uint32_t r = 0; r < I.R; ++r)
     HIPCHK(hipMemcpyAsync(I.alloc.p + (size_t)r * I.N + n, &alloc[r], sizeof(int64_t), hipMemcpyHostToDevice, I.stream));
   HIPCHK(hipMemcpyAsync(I.allowed.p + n, &allowed, sizeof(int32_t), hipMemcpyHostToDevice, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   return true;
 }
 
-bool Engine::node_static(int32_t gnode, const std::vector<int32_t>& label_vid, uint8_t has_labels, uint8_t flags,
-                         std::string& err) {
+bool Engine::node_static(const std::vector<int32_t>& gnodes, const std::vector<int32_t>& label_vid,
+                         const std::vector<uint8_t>& has_labels, const std::vector<uint8_t>& flags, std::string& err) {
   Impl& I = *p_;
-  if (gnode < 0 || (uint32_t)gnode >= I.G) { err = "node_static: node index"; return false; }
-  if (label_vid.size() != I.K) { err = "node_static: label key count"; return false; }
+  const size_t m = gnodes.size();
+  if (label_vid.size() != m * I.K || has_labels.size() != m || flags.size() != m) { err = "node_static: sizes"; return false; }
+  for (int32_t g : gnodes)
+    if (g < 0 || (uint32_t)g >= I.G) { err = "node_static: node index"; return false; }
   hipStream_t s = I.stream;
-  // one column entry per key: a strided copy down the [K][N] (and [K][G]) columns
-  if (I.K && I.gstat)
-    HIPCHK(hipMemcpy2DAsync(I.glabel.p + gnode, (size_t)I.G * 4, label_vid.data(), 4, 4, I.K, hipMemcpyHostToDevice, s));
-  if ((uint32_t)gnode >= I.goff && (uint32_t)gnode - I.goff < I.N) {
-    const uint32_t n = (uint32_t)gnode - I.goff;
-    if (I.K)
-      HIPCHK(hipMemcpy2DAsync(I.label.p + n, (size_t)I.N * 4, label_vid.data(), 4, 4, I.K, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(I.haslab.p + n, &has_labels, 1, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(I.nflags.p + n, &flags, 1, hipMemcpyHostToDevice, s));
+  // per node, one column entry per key: a strided copy down the [K][N] (and [K][G])
+  // columns; every copy of the batch queued, one synchronisation (the host
+  // vectors stay alive until it)
+  for (size_t i = 0; i < m; ++i) {
+    const uint32_t g = (uint32_t)gnodes[i];
+    const int32_t* lv = label_vid.data() + i * I.K;
+    if (I.K && I.gstat)
+      HIPCHK(hipMemcpy2DAsync(I.glabel.p + g, (size_t)I.G * 4, lv, 4, 4, I.K, hipMemcpyHostToDevice, s));
+    if (g >= I.goff && g - I.goff < I.N) {
+      const uint32_t n = g - I.goff;
+      if (I.K) HIPCHK(hipMemcpy2DAsync(I.label.p + n, (size_t)I.N * 4, lv, 4, 4, I.K, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(I.haslab.p + n, &has_labels[i], 1, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(I.nflags.p + n, &flags[i], 1, hipMemcpyHostToDevice, s));
+    }
   }
-  HIPCHK(hipStreamSynchronize(s));
-  return true;
+  return stream_sync(I, s, err);
 }
 
 bool Engine::node_taints(const std::vector<uint32_t>& offs, const std::vector<int32_t>& ids,
@@ -6595,7 +6618,7 @@ bool Engine::node_taints(const std::vector<uint32_t>& offs, const std::vector<in
     err = "node_taints: taint lists do not match the node count";
     return false;
   }
-  HIPCHK(hipStreamSynchronize(s));  // (a re-allocation frees what a queued launch may read)
+  if (!stream_sync(I, s, err)) return false;  // (a re-allocation frees what a queued launch may read)
   // what upload() derives from the lists: widest list, largest id, a taint listed twice
   uint32_t mt = 0;
   int32_t mx = -1;
@@ -6621,7 +6644,7 @@ bool Engine::node_taints(const std::vector<uint32_t>& offs, const std::vector<in
   I.max_tid = mx;
   I.taint_dup = dup;
   if (mt >= 4096) I.static_fits = false;  // (other causes may hold it false: never raised here)
-  HIPCHK(hipStreamSynchronize(s));
+  if (!stream_sync(I, s, err)) return false;
   return true;
 }
 
@@ -6634,7 +6657,7 @@ bool Engine::grow_table(uint32_t pod_cap, uint32_t term_cap, uint32_t req_cap, u
   req_cap = std::max(req_cap, I.rcap);
   val_cap = std::max(val_cap, I.vcap);
   n_keys = std::max(n_keys, I.pkeys);
-  HIPCHK(hipStreamSynchronize(s));
+  if (!stream_sync(I, s, err)) return false;
   if (pod_cap != I.pcap || n_keys != I.pkeys) {
     if (!I.ptnode.grow(pod_cap, I.pcap, s, err) || !I.ptns.grow(pod_cap, I.pcap, s, err) ||
         !I.ptflags.grow(pod_cap, I.pcap, s, err))
@@ -6646,7 +6669,7 @@ bool Engine::grow_table(uint32_t pod_cap, uint32_t term_cap, uint32_t req_cap, u
     for (uint32_t k = 0; k < I.pkeys; ++k)
       HIPCHK(hipMemcpyAsync(lab.p + (size_t)k * pod_cap, I.ptlab.p + (size_t)k * I.pcap, (size_t)I.pcap * 4,
                             hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));
+    if (!stream_sync(I, s, err)) return false;
     std::swap(lab.p, I.ptlab.p);
     std::swap(lab.n, I.ptlab.n);
   }
@@ -6658,7 +6681,7 @@ bool Engine::grow_table(uint32_t pod_cap, uint32_t term_cap, uint32_t req_cap, u
   I.rcap = req_cap;
   I.vcap = val_cap;
   I.pkeys = n_keys;
-  HIPCHK(hipStreamSynchronize(s));
+  if (!stream_sync(I, s, err)) return false;
   return true;
 }
 
@@ -6668,7 +6691,7 @@ bool Engine::table_overflow(bool& overflow, std::string& err) {
   overflow = false;
   if (!I.tcounts.p) return true;
   HIPCHK(hipMemcpyAsync(&f, I.tcounts.p + 4, sizeof(f), hipMemcpyDeviceToHost, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   overflow = f != 0;
   return true;
 }
@@ -6679,7 +6702,7 @@ bool Engine::table_room(uint32_t used[4], uint32_t cap[4], std::string& err) {
   cap[0] = I.pcap; cap[1] = I.tcap; cap[2] = I.rcap; cap[3] = I.vcap;
   if (!I.tcounts.p) return true;
   HIPCHK(hipMemcpyAsync(used, I.tcounts.p, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   return true;
 }
 
@@ -6740,7 +6763,7 @@ static bool reduce_tables(Engine::Impl& I, std::string& err) {
   hipLaunchKernelGGL(k_seg_sum, dim3(nb), dim3(256), 0, s, I.segs_d.p, nseg, reinterpret_cast<const int32_t*>(I.xrecv.p),
                      total, I.xranks);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s));  // (segment list uploaded from a host vector)
+  if (!stream_sync(I, s, err)) return false;  // (segment list uploaded from a host vector)
   return true;
 }
 // Before anything reads or changes the class tables of a sharded context.
@@ -6805,7 +6828,7 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
   if (npc) I.red_pc0 = std::min(I.red_pc0, pc0);
   if (ntc) I.red_tc0 = std::min(I.red_tc0, tc0);
   if (!reduce_tables(I, err)) return false;
-  HIPCHK(hipStreamSynchronize(s));
+  if (!stream_sync(I, s, err)) return false;
   return true;
 }
 
@@ -6842,7 +6865,7 @@ bool Engine::replace_program(uint32_t q, const std::vector<uint8_t>& prog, std::
   const uint64_t off64 = off;
   HIPCHK(hipMemcpyAsync(I.progs.p + off, prog.data(), prog.size(), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(I.prog_off_d.p + q, &off64, sizeof(off64), hipMemcpyHostToDevice, s));
-  HIPCHK(hipStreamSynchronize(s));  // host sources
+  if (!stream_sync(I, s, err)) return false;  // host sources
   I.prog_bytes = off + prog.size();
   I.prog_off[q] = off;
   const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
@@ -6865,7 +6888,7 @@ bool Engine::normalized(uint32_t j, std::vector<int32_t>& norm, std::string& err
   HIPCHK(hipGetLastError());
   norm.resize((size_t)I.F.n * N);
   if (N) HIPCHK(hipMemcpyAsync(norm.data(), I.knorm.p, norm.size() * 4, hipMemcpyDeviceToHost, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   return true;
 }
 
@@ -6941,7 +6964,7 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
                        hdev ? hdev : I.vblk.p, I.vdone.p);
   HIPCHK(hipGetLastError());
   if (!hdev) HIPCHK(hipMemcpyAsync(host, I.vblk.p, lay.bytes, hipMemcpyDeviceToHost, s));  // (direct: k_view wrote it all)
-  HIPCHK(hipStreamSynchronize(s));
+  if (!stream_sync(I, s, err)) return false;
   return true;
 }
 namespace {
@@ -6997,7 +7020,7 @@ bool Engine::set_summaries(uint32_t first, uint32_t count, const ksg_pod_summary
   Impl& I = *p_;
   if (first + count > I.prog_off.size()) { err = "program index out of range"; return false; }
   HIPCHK(hipMemcpyAsync(I.sums.p + first, in, count * sizeof(ksg_pod_summary), hipMemcpyHostToDevice, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   return true;
 }
 
@@ -7431,7 +7454,7 @@ static uint32_t wait_verdict(Engine::Impl& I, hipStream_t s, std::string& err) {
 
 bool Engine::sync(std::string& err) {
   Impl& I = *p_;
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   I.hcalls.clear();  // every queued host exchange has run
   if (I.xfail.exchange(0)) { err = "exchange callback failed"; return false; }
   if (I.run_used) {  // a persistent segment whose poll ran out left the launch early
@@ -7454,7 +7477,7 @@ bool Engine::sync(std::string& err) {
 bool Engine::summaries(uint32_t first, uint32_t count, ksg_pod_summary* out, std::string& err) {
   Impl& I = *p_;
   HIPCHK(hipMemcpyAsync(out, I.sums.p + first, count * sizeof(ksg_pod_summary), hipMemcpyDeviceToHost, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   return true;
 }
 
@@ -7471,7 +7494,7 @@ bool Engine::outputs(uint32_t j, PodOutputs& out, std::string& err) {
                         hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipMemcpyAsync(out.total.data(), I.ktotal.p + k * N, N * 4, hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipMemcpyAsync(&out.summary, I.sums.p + j, sizeof(ksg_pod_summary), hipMemcpyDeviceToHost, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   return true;
 }
 
@@ -7481,7 +7504,7 @@ bool Engine::read_requested(std::vector<int64_t>& requested, std::vector<int32_t
   pod_count.resize(I.N);
   HIPCHK(hipMemcpyAsync(requested.data(), I.req.p, requested.size() * 8, hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipMemcpyAsync(pod_count.data(), I.podcnt.p, pod_count.size() * 4, hipMemcpyDeviceToHost, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   return true;
 }
 
@@ -7490,7 +7513,7 @@ bool Engine::read_nonzero(std::vector<int64_t>& nz, std::string& err) {
   nz.resize((size_t)2 * I.N);
   HIPCHK(hipMemcpyAsync(nz.data(), I.nzc.p, (size_t)I.N * 8, hipMemcpyDeviceToHost, I.stream));
   HIPCHK(hipMemcpyAsync(nz.data() + I.N, I.nzm.p, (size_t)I.N * 8, hipMemcpyDeviceToHost, I.stream));
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   return true;
 }
 
@@ -7571,6 +7594,48 @@ bool Engine::nccl_unique_id(void* out128, std::string& err) {
   std::memcpy(out128, &id, sizeof(id));
   return true;
 }
+// Diagnostic (ksg_debug_rccl_selftest): the RCCL exchange's calls on this device
+// with a ONE-rank communicator — unique id, ncclCommInitRank, ncclAllGather on a
+// created stream, a byte-exact check of the gathered buffer, ncclCommDestroy.  A
+// one-GPU box cannot hold two RCCL ranks (RCCL refuses a duplicate device), so
+// this is the only RCCL call a single-GPU run can make; the sharded paths
+// themselves are tested over the host exchange.
+bool rccl_selftest(int device, size_t bytes, std::string& err) {
+  HIPCHK(hipSetDevice(device));
+  ncclUniqueId id;
+  ncclResult_t nr = ncclGetUniqueId(&id);
+  if (nr != ncclSuccess) { err = std::string("ncclGetUniqueId: ") + ncclGetErrorString(nr); return false; }
+  ncclComm_t comm = nullptr;
+  nr = ncclCommInitRank(&comm, 1, id, 0);
+  if (nr != ncclSuccess) { err = std::string("ncclCommInitRank: ") + ncclGetErrorString(nr); return false; }
+  hipStream_t s = nullptr;
+  uint8_t *a = nullptr, *b = nullptr;
+  std::vector<uint8_t> h(bytes), back(bytes);
+  for (size_t i = 0; i < bytes; ++i) h[i] = (uint8_t)(i * 131 + 7);
+  bool ok = hipStreamCreate(&s) == hipSuccess && hipMalloc(&a, bytes) == hipSuccess && hipMalloc(&b, bytes) == hipSuccess &&
+            hipMemcpyAsync(a, h.data(), bytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipMemsetAsync(b, 0, bytes, s) == hipSuccess;
+  if (!ok) err = "rccl selftest: buffers";
+  if (ok && (nr = ncclAllGather(a, b, bytes, ncclUint8, comm, s)) != ncclSuccess) {
+    err = std::string("ncclAllGather: ") + ncclGetErrorString(nr);
+    ok = false;
+  }
+  if (ok && (hipMemcpyAsync(back.data(), b, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+             hipStreamSynchronize(s) != hipSuccess)) {
+    err = "rccl selftest: copy back";
+    ok = false;
+  }
+  if (ok && back != h) {
+    err = "rccl selftest: gathered bytes differ";
+    ok = false;
+  }
+  if (s) (void)hipStreamSynchronize(s);
+  (void)ncclCommDestroy(comm);
+  if (a) (void)hipFree(a);
+  if (b) (void)hipFree(b);
+  if (s) (void)hipStreamDestroy(s);
+  return ok;
+}
 void Engine::set_path(int per_pod) { p_->force_per_pod = per_pod != 0; }
 // The resource columns of the Fit / BalancedAllocation scoring arguments (known
 // once the snapshot's resource vocabulary is: after every vocabulary build).
@@ -7607,7 +7672,7 @@ bool Engine::eval_stamps(bool on, std::vector<uint64_t>* out, std::string& err) 
     return true;
   }
   out->assign(64, 0);
-  HIPCHK(hipStreamSynchronize(I.stream));
+  if (!stream_sync(I, I.stream, err)) return false;
   if (I.cstamps_on) HIPCHK(hipMemcpy(out->data(), I.cstamps.p, 64 * 8, hipMemcpyDeviceToHost));
   return true;
 }

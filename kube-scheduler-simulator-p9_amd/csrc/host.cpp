@@ -3683,11 +3683,18 @@ struct Cluster {
       ok = refresh_program((uint32_t)unres[i].first) && eng->assume((uint32_t)unres[i].first, unres[i].second, -1, err);
     for (size_t i = 0; ok && i < allocs.size(); ++i)
       ok = eng->node_alloc(std::get<0>(allocs[i]), std::get<1>(allocs[i]), std::get<2>(allocs[i]), err);
-    for (size_t i = 0; ok && i < restat.size(); ++i) {
-      const Node& nd = nodes[restat[i]];
-      vector<int32_t> lv(nkeys.names.size(), -1);  // as encode_snapshot
-      for (auto& kv : nd.labels) lv[nkeys.get(kv.first)] = nvals[nkeys.get(kv.first)].get(kv.second);
-      ok = eng->node_static(restat[i], lv, nd.labels.empty() ? 0 : 1, nd.unschedulable ? KSG_NODE_UNSCHEDULABLE : 0, err);
+    if (ok && !restat.empty()) {  // one batch, one synchronisation
+      const size_t K = nkeys.names.size();
+      vector<int32_t> gs, lv(restat.size() * K, -1);  // as encode_snapshot
+      vector<uint8_t> hl, fl;
+      for (size_t i = 0; i < restat.size(); ++i) {
+        const Node& nd = nodes[restat[i]];
+        gs.push_back((int32_t)restat[i]);
+        for (auto& kv : nd.labels) lv[i * K + nkeys.get(kv.first)] = nvals[nkeys.get(kv.first)].get(kv.second);
+        hl.push_back(nd.labels.empty() ? 0 : 1);
+        fl.push_back(nd.unschedulable ? KSG_NODE_UNSCHEDULABLE : 0);
+      }
+      ok = eng->node_static(gs, lv, hl, fl, err);
     }
     if (ok && retaint) {
       vector<uint32_t> off, goff;
@@ -4248,6 +4255,7 @@ static std::atomic<uint64_t> g_ctx_gen{0};
 static thread_local const void* t_err_ctx = nullptr;
 static thread_local uint64_t t_err_gen = 0;
 static thread_local std::string t_err;
+static thread_local bool t_err_own = false;  // t_err was set by this thread's own failing call
 struct ksg_ctx {
   Cluster c;
   std::string last_error;
@@ -4258,9 +4266,13 @@ struct ksg_ctx {
     t_err_ctx = this;
     t_err_gen = gen;
     t_err = m;
+    t_err_own = true;
     return code;
   }
 };
+namespace ksg {
+bool rccl_selftest(int device, size_t bytes, std::string& err);  // engine.hip (diagnostic)
+}
 #define KSG_LOCK(ctx)                                 \
   std::unique_lock<std::recursive_mutex> ksg_lk_;    \
   if (ctx) ksg_lk_ = std::unique_lock<std::recursive_mutex>((ctx)->mu)
@@ -4312,11 +4324,14 @@ void ksg_destroy(ksg_ctx* ctx) {
 // ctx->last_error after the lock is released, so it is copied under the lock.
 const char* ksg_last_error(const ksg_ctx* ctx) {
   if (!ctx) return "null context";
-  if (t_err_ctx == ctx && t_err_gen == ctx->gen) return t_err.c_str();
+  // this thread's own failure on ctx; otherwise the context's current error,
+  // copied under the lock on every call (a newer failure of another thread shows)
+  if (t_err_own && t_err_ctx == ctx && t_err_gen == ctx->gen) return t_err.c_str();
   KSG_LOCK(ctx);
   t_err = ctx->last_error;
   t_err_ctx = ctx;
   t_err_gen = ctx->gen;
+  t_err_own = false;
   return t_err.c_str();
 }
 
@@ -4581,6 +4596,17 @@ int ksg_set_exchange(ksg_ctx* ctx, int mode, const uint8_t* nccl_id, ksg_exchang
 int ksg_batch_path(const ksg_ctx* ctx) {
   KSG_LOCK(ctx);
   return ctx ? (ctx->c.eng->batch_path() ? 1 : 0) : KSG_E_INVALID;
+}
+
+// diagnostic (not in ksg.h): a one-rank RCCL communicator's all-gather on `device`
+// (the calls the exchange's mode 1 makes; error text into err_buf)
+extern "C" int ksg_debug_rccl_selftest(int device, size_t bytes, char* err_buf, size_t cap) {
+  std::string err;
+  const bool ok = ksg::rccl_selftest(device, bytes, err);
+  if (err_buf && cap) {
+    std::snprintf(err_buf, cap, "%s", err.c_str());
+  }
+  return ok ? KSG_OK : KSG_E_DEVICE;
 }
 
 // diagnostic (not in ksg.h): the sampled run's k_static launches (cfg3 roofline)

@@ -537,10 +537,12 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
       }
       if (PMH(KP_BA)) ba_s = ROWM == 2 ? ba_score_row<1>(row, F, h) : ba_score_row<0>(row, F, h);
     }
+    CS(14);
     if (STG != 2 && W && !run_wait_flag(*W)) {
       eo->abort = true;
       return;
     }
+    CS(15);
   }
   uint8_t mpn[KSG_MAX_TSC];
   int32_t mcnt[KSG_MAX_TSC];
@@ -1710,7 +1712,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     if (x >= 0) xmask |= 1u << x;
   }
   // diagnostic stamps (Engine::eval_stamps): block 0's phase ends since the pod's
-  // start, slots 30..34, pods 35; the owner's commit time 36, commits 37; block
+  // start, slots 30..34, 39, 47, the pod's end 50, pods 35; the owner's commit time 36, commits 37; block
   // 0's wait for the previous pod's flag 38
   uint64_t* const rst = A0.stamps;
   const bool rs_on = rst && b == 0 && threadIdx.x == 0;
@@ -1920,6 +1922,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     have = tnext;
     if (nh && !tnext) wait_for = (node >= 0 && (h->tab_md & nh->tab_rd) != 0) ? tag : k;
     ph = h;
+    RS(50);
     if (rs_on) atomicAdd((unsigned long long*)&rst[35], 1ull);
   }
 #undef RS

@@ -52,3 +52,15 @@ def rccl_unique_id_broadcast(lib, rank: int) -> bytes:
         obj = [bytes(buf)]
     dist.broadcast_object_list(obj, src=0)
     return obj[0]
+
+
+def sharded_scheduler(profile, torch, rank: int, world: int, local: int):
+    """An engine context for this rank's node shard (bench.py, bench_whatif.py);
+    at world > 1 on torch's current stream with an RCCL exchange (mode 1:
+    ncclAllGather on the engine stream, the unique id broadcast from rank 0)."""
+    from .engine import Scheduler
+    stream = torch.cuda.current_stream().cuda_stream if world > 1 else None
+    s = Scheduler(profile, device=local, stream=stream, shard_rank=rank, shard_count=world)
+    if world > 1:
+        s.set_exchange_rccl(rccl_unique_id_broadcast(s.L, rank))
+    return s

@@ -168,8 +168,11 @@ bool Engine::node_alloc(int32_t gnode, const std::vector<int64_t>& alloc, int32_
   if (gnode < 0 || alloc.size() < p_->R) { err = "stub: node_alloc"; return false; }
   return true;
 }
-bool Engine::node_static(int32_t gnode, const std::vector<int32_t>&, uint8_t, uint8_t, std::string& err) {
-  if (gnode < 0) { err = "stub: node_static"; return false; }
+bool Engine::node_static(const std::vector<int32_t>& gnodes, const std::vector<int32_t>&, const std::vector<uint8_t>& hl,
+                         const std::vector<uint8_t>& fl, std::string& err) {
+  if (hl.size() != gnodes.size() || fl.size() != gnodes.size()) { err = "stub: node_static sizes"; return false; }
+  for (int32_t g : gnodes)
+    if (g < 0) { err = "stub: node_static"; return false; }
   return true;
 }
 bool Engine::node_taints(const std::vector<uint32_t>& offs, const std::vector<int32_t>& ids,
@@ -351,4 +354,8 @@ uint8_t* Engine::pinned_get(size_t bytes, size_t& cap) {
 }
 void Engine::pinned_put(uint8_t* p, size_t) { std::free(p); }
 uint8_t* Engine::pinned_dev(const uint8_t*) { return nullptr; }
+bool rccl_selftest(int, size_t, std::string& err) {
+  err = "stub: no RCCL";
+  return false;
+}
 }  // namespace ksg

@@ -46,6 +46,23 @@ def _exchange_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbytes", [16896, 1 << 20])
+def test_rccl_one_rank_allgather_selftest(nbytes):
+    """The RCCL exchange (mode 1) on the MI355X with a one-rank communicator:
+    unique id, ncclCommInitRank, ncclAllGather of the keys-only window record's
+    size (16,896 B) and of 1 MiB, gathered bytes checked.  Two ranks cannot share
+    one GPU under RCCL, so this is the RCCL call a one-GPU box can test; the
+    driver's multi-GPU bench is the first multi-rank RCCL run."""
+    sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
+    from ksg import load_library
+    L = load_library()
+    L.ksg_debug_rccl_selftest.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+    buf = ctypes.create_string_buffer(512)
+    rc = L.ksg_debug_rccl_selftest(0, nbytes, buf, 512)
+    assert rc == 0, buf.value.decode()
+
+
 def test_host_exchange_gloo_world2():
     port = _free_port()
     with mp.Manager() as m:

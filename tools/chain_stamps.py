@@ -12,7 +12,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
 
-NAMES = {13: "k_eval: entry + gap stamp", 7: "k_eval: inputs issued (vids, row, setup)", 11: "k_eval: +1 stamp", 12: "k_eval: +2 stamps", 8: "k_eval: slot vids in LDS", 9: "k_eval: lookups issued",
+NAMES = {13: "k_eval: entry + gap stamp", 14: "k_eval (run): row-only Fit/BA done", 15: "k_eval (run): flag wait done", 7: "k_eval: inputs issued (vids, row, setup)", 11: "k_eval: +1 stamp", 12: "k_eval: +2 stamps", 8: "k_eval: slot vids in LDS", 9: "k_eval: lookups issued",
          10: "k_eval: setup (minMatchNum, IPA bits)",
          3: "k_eval: filter done",
          4: "k_eval: scores done", 5: "k_eval: block reduce", 6: "k_eval: partials written",
@@ -23,7 +23,8 @@ NAMES = {13: "k_eval: entry + gap stamp", 7: "k_eval: inputs issued (vids, row, 
          42: "gap k_final->next k_eval entry"}
 
 RUN_NAMES = {30: "eval + partial granules stored", 31: "every partial seen", 39: "partials block-reduced",
-             32: "partials folded", 47: "normalised + keyed", 33: "key granules stored", 34: "every key seen, argmax"}
+             32: "partials folded", 47: "normalised + keyed", 33: "key granules stored", 34: "every key seen, argmax",
+             50: "pod done (owner commit, next wait set)"}
 
 
 def main():
@@ -49,10 +50,10 @@ def main():
     pods = s.queue_len - 64  # every cycle's block 0 stamps; the select's only when block 0 arrives last
     last = out[63] or 1
     res = {NAMES.get(k, str(k)): round(out[k] / (last if 24 <= k <= 27 else pods) * 0.01, 3)
-           for k in sorted(NAMES, key=lambda k: (k not in (13, 7, 11, 12, 8, 9, 10), k)) if out[k]}
+           for k in sorted(NAMES, key=lambda k: (k not in (13, 14, 15, 7, 11, 12, 8, 9, 10), k)) if out[k]}
     rep = {"pods": pods, "select_samples": last, "us_avg_block0": res}
     if out[35]:  # persistent segments (k_chain_run)
-        rep["k_chain_run_us_since_pod_start_block0"] = {RUN_NAMES[k]: round(out[k] / out[35] * 0.01, 3) for k in (30, 31, 39, 32, 47, 33, 34)}
+        rep["k_chain_run_us_since_pod_start_block0"] = {RUN_NAMES[k]: round(out[k] / out[35] * 0.01, 3) for k in (30, 31, 39, 32, 47, 33, 34, 50)}
         rep["k_chain_run_pods_block0"] = out[35]
         rep["k_chain_run_pods_read_ahead_block0"] = out[40]
         rep["k_chain_run_flag_wait_us_block0"] = round(out[38] / out[35] * 0.01, 3)

@@ -184,29 +184,47 @@ struct DevOut {
   int32_t* prow;     // existing-pod table row of the assumed pod
 };
 
+// Programs are read through the constant address space: they never change
+// during a launch (uploads and k_place_program run between launches), so every
+// wave-uniform read of a header field is a scalar load (s_load, scalar cache),
+// whatever stores, atomics, fences or asm memory clobbers the kernel holds.
+// Through a generic pointer the compiler could prove that only for __restrict__
+// kernel arguments with no clobber on the path: the persistent kernels read
+// their programs with vector loads, each one waited for (round 5).
+// (the host pass of this single-source file parses these device functions but
+// never emits them: there the qualifier is left out, which its semantic checks need)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define KSG_CONST __attribute__((address_space(4)))
+#else
+#define KSG_CONST
+#endif
+template <class T>
+using cptr = const KSG_CONST T*;
+using PH = cptr<ksg_prog>;
 struct ProgView {
-  const ksg_prog* h;
-  const int32_t* i32;
-  const uint32_t* u32;
-  const ksg_req* req;
-  const ksg_sel* sel;
-  const ksg_aterm* at;
-  const ksg_exist_term* et;
-  const ksg_vchk* vchk;
-  const ksg_freq* fq;
+  PH h;
+  cptr<int32_t> i32;
+  cptr<uint32_t> u32;
+  cptr<ksg_req> req;
+  cptr<ksg_sel> sel;
+  cptr<ksg_aterm> at;
+  cptr<ksg_exist_term> et;
+  cptr<ksg_vchk> vchk;
+  cptr<ksg_freq> fq;
 };
 
-__device__ __forceinline__ ProgView view(const uint8_t* p) {
+__device__ __forceinline__ ProgView view(const uint8_t* pg) {
   ProgView v;
-  v.h = reinterpret_cast<const ksg_prog*>(p);
-  v.i32 = reinterpret_cast<const int32_t*>(p + v.h->off_i32);
-  v.u32 = reinterpret_cast<const uint32_t*>(p + v.h->off_u32);
-  v.req = reinterpret_cast<const ksg_req*>(p + v.h->off_req);
-  v.sel = reinterpret_cast<const ksg_sel*>(p + v.h->off_sel);
-  v.at = reinterpret_cast<const ksg_aterm*>(p + v.h->off_aterm);
-  v.et = reinterpret_cast<const ksg_exist_term*>(p + v.h->off_eterm);
-  v.vchk = reinterpret_cast<const ksg_vchk*>(v.i32 + v.h->vchk_off);
-  v.fq = reinterpret_cast<const ksg_freq*>(p + v.h->off_freq);
+  const KSG_CONST uint8_t* p = (const KSG_CONST uint8_t*)pg;
+  v.h = (PH)p;
+  v.i32 = (cptr<int32_t>)(p + v.h->off_i32);
+  v.u32 = (cptr<uint32_t>)(p + v.h->off_u32);
+  v.req = (cptr<ksg_req>)(p + v.h->off_req);
+  v.sel = (cptr<ksg_sel>)(p + v.h->off_sel);
+  v.at = (cptr<ksg_aterm>)(p + v.h->off_aterm);
+  v.et = (cptr<ksg_exist_term>)(p + v.h->off_eterm);
+  v.vchk = (cptr<ksg_vchk>)(v.i32 + v.h->vchk_off);
+  v.fq = (cptr<ksg_freq>)(p + v.h->off_freq);
   return v;
 }
 
@@ -7258,15 +7276,15 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
           ChainArgs R5 = RA;
           R5.nblk = nb512;
           hipLaunchKernelGGL((k_chain_run<2, kPmTab, kRunLK, kRunTS, 512>), gr, dim3(512), 0, s, C, F, R5, j1 - j,
-                             I.rsync.p, g1, g2, RC);
+                             I.rsync.p, g1, g2, RC, RA.progs, RA.prog_off);
         } else if (rowm == 2 && (pmask & ~kPmTab) == 0 && cls)
-          hipLaunchKernelGGL((k_chain_run<2, kPmTab, kRunLK, kRunTS>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC);
+          hipLaunchKernelGGL((k_chain_run<2, kPmTab, kRunLK, kRunTS>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC, RA.progs, RA.prog_off);
         else if (rowm == 2 && (pmask & ~kPmTab) == 0)
-          hipLaunchKernelGGL((k_chain_run<2, kPmTab>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC);
+          hipLaunchKernelGGL((k_chain_run<2, kPmTab>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC, RA.progs, RA.prog_off);
         else if (rowm == 2 && (pmask & ~kPmTabTN) == 0)
-          hipLaunchKernelGGL((k_chain_run<2, kPmTabTN>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC);
-        else if (rowm == 2) hipLaunchKernelGGL((k_chain_run<2, ~0u>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC);
-        else hipLaunchKernelGGL((k_chain_run<1, ~0u>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC);
+          hipLaunchKernelGGL((k_chain_run<2, kPmTabTN>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC, RA.progs, RA.prog_off);
+        else if (rowm == 2) hipLaunchKernelGGL((k_chain_run<2, ~0u>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC, RA.progs, RA.prog_off);
+        else hipLaunchKernelGGL((k_chain_run<1, ~0u>), gr, bk, 0, s, C, F, RA, j1 - j, I.rsync.p, g1, g2, RC, RA.progs, RA.prog_off);
         if (sampled) {
           HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
           I.n_samples++;

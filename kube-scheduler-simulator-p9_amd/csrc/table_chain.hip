@@ -1686,9 +1686,14 @@ __device__ __forceinline__ bool run_read_g1(const uint64_t* g, uint32_t tag, uin
   return false;
 }
 
+// P / PO: the programs and their offsets as __restrict__ kernel arguments, so the
+// wave-uniform header reads stay scalar loads (s_load) despite the launch's own
+// stores: through ChainArgs' plain pointers they were vector loads, each waited
+// for with vmcnt(0) (round 5).
 template <int ROWM, uint32_t PM, int LK, int TS, int BT>
 __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, const ChainArgs& A0, uint32_t count,
-                                         RunSync* Y, uint64_t* G1s, uint64_t* G2s, const RunCtl& R) {
+                                         RunSync* Y, uint64_t* G1s, uint64_t* G2s, const RunCtl& R,
+                                         const uint8_t* __restrict__ P, const uint64_t* __restrict__ PO) {
   static_assert(ROWM != 0, "the persistent chain keeps the node row in registers");
   __shared__ RunSharedT<BT> S;
   EvalSharedT<BT>& L = S.L;
@@ -1732,7 +1737,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
   for (uint32_t k = 0; k < count; ++k) {
     ChainArgs A = A0;  // (A.stamps: eval_body's own k_eval slots, block 0)
     A.q = A0.q + k;
-    const uint8_t* prog = A.progs + A.prog_off[A.q];
+    const uint8_t* prog = P + PO[A.q];
     const uint32_t tag = k + 1u;
     uint64_t* const G1 = G1s + (k & 1u) * kRunSlot;  // (parity slots)
     uint64_t* const G2 = G2s + (k & 1u) * kRunSlot;
@@ -1757,7 +1762,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     if (threadIdx.x < (uint32_t)ng1) st_sc1(G1 + (size_t)b * kRunGS + threadIdx.x, gran(tag, run_g1_value<TS>(eo.rec, (int)threadIdx.x, xmask, ns)));
     RS(30);
     // ---- pod k+1's class-table reads, in flight across this pod's hand-offs
-    const ksg_prog* nh = k + 1 < count ? reinterpret_cast<const ksg_prog*>(A.progs + A.prog_off[A.q + 1]) : nullptr;
+    const ksg_prog* nh = k + 1 < count ? reinterpret_cast<const ksg_prog*>(P + PO[A.q + 1]) : nullptr;
     const bool tnext = R.overlap && nh && run_indep(h, nh);
     if (tnext) {
       ChainArgs A1 = A0;
@@ -1766,7 +1771,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       const RunWait W1{Y, (ph && run_indep(ph, nh)) ? (k ? k - 1 : 0u) : k, &S.go, nullptr, owned, R.spin};
       EvalOut ea;
       ea.abort = false;
-      eval_body<ROWM, kRun, PM, LK, TS, BT, 1>(C, F, A1, A1.progs + A1.prog_off[A1.q], &L, &row, &ea, &W1, &pre);
+      eval_body<ROWM, kRun, PM, LK, TS, BT, 1>(C, F, A1, P + PO[A1.q], &L, &row, &ea, &W1, &pre);
       if (ea.abort) return;
       owned = 0;
       if (rs_on) atomicAdd((unsigned long long*)&rst[40], 1ull);  // (pods whose reads went ahead)
@@ -1831,7 +1836,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     RS(33);
     if (threadIdx.x == BT - 32 && k + 1 < count) {  // the next program header into the scalar cache
       uint32_t warm = 0;
-      const uint64_t a = (uint64_t)(A.progs + A.prog_off[A.q + 1]);  // (uniform: into scalar registers)
+      const uint64_t a = (uint64_t)(P + PO[A.q + 1]);  // (uniform: into scalar registers)
       const uint64_t su = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a) |
                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32);
       KWarm<0, kHdrBytes>::run(reinterpret_cast<const void*>(su), warm);
@@ -1934,7 +1939,8 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
 // at the node's topology values — drains it and advances the flag.
 template <uint32_t PM, int TS, int BT>
 __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile& F, const ChainArgs& A0, uint32_t count,
-                                                RunSync* Y, const uint64_t* G1s, const uint64_t* G2s, const RunCtl& R) {
+                                                RunSync* Y, const uint64_t* G1s, const uint64_t* G2s, const RunCtl& R,
+                                                const uint8_t* __restrict__ P, const uint64_t* __restrict__ PO) {
   __shared__ ChainRec lrec[BT / 64];
   __shared__ uint32_t go;
   if (!run_handshake(Y, R, &go)) return;
@@ -1949,7 +1955,7 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
     const uint64_t* const G1 = G1s + (k & 1u) * kRunSlot;  // (parity slots)
     const uint64_t* const G2 = G2s + (k & 1u) * kRunSlot;
     for (uint32_t i = 0; i < R.lag; ++i) __builtin_amdgcn_s_sleep(127);  // (diagnostic: a lagging committer)
-    const uint8_t* prog = A0.progs + A0.prog_off[q];
+    const uint8_t* prog = P + PO[q];
     const ProgView V = view(prog);
     const ksg_prog* h = V.h;
     const int ns = h->n_tsc_score;
@@ -2017,9 +2023,10 @@ constexpr uint32_t kPmTabTN = kPmTab | (1u << KP_TAINT) | (1u << KP_NA);
 constexpr int kRunLK = 8, kRunTS = 4;
 template <int ROWM, uint32_t PM, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC, int BT = kChain>
 __global__ __launch_bounds__(BT) void k_chain_run(DevCluster C, DevProfile F, ChainArgs A, uint32_t count, RunSync* Y,
-                                                  uint64_t* G1, uint64_t* G2, RunCtl R) {
-  if (blockIdx.x == A.nblk) run_commit_body<PM, TS, BT>(C, F, A, count, Y, G1, G2, R);  // (the extra block)
-  else run_body<ROWM, PM, LK, TS, BT>(C, F, A, count, Y, G1, G2, R);
+                                                  uint64_t* G1, uint64_t* G2, RunCtl R, const uint8_t* __restrict__ P,
+                                                  const uint64_t* __restrict__ PO) {
+  if (blockIdx.x == A.nblk) run_commit_body<PM, TS, BT>(C, F, A, count, Y, G1, G2, R, P, PO);  // (the extra block)
+  else run_body<ROWM, PM, LK, TS, BT>(C, F, A, count, Y, G1, G2, R, P, PO);
 }
 
 // Kernels.  The *_occ twins cap registers at 4 waves per SIMD (a few spills)

@@ -261,6 +261,7 @@ class Engine {
   // An aborted persistent launch left the device state half-updated: the context
   // must be reloaded (host.cpp marks it broken); cleared by a reload.
   bool lost() const;
+  uint64_t static_dec_chunks() const;  // diagnostic: static-record chunks computed from decoded pods
   void clear_lost();
   static bool nccl_unique_id(void* out128, std::string& err);
   // diagnostic: enable (out == nullptr, count pods) / read back s_memtime stamps of the fixup loop

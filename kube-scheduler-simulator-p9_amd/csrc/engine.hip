@@ -3123,21 +3123,23 @@ struct WcReq {          // 32 B
   uint64_t pad;
 };
 struct WcPod {
-  uint32_t flags;       // bit 0: no node passes; bit 1: PreFilterResult bitmap
+  uint32_t flags;       // bit 0: no node passes; bit 1: PreFilterResult bitmap; bit 2: PreFilter rejected the
+                        // pod (static records: not evaluated); bit 3: an empty required-terms list (NodeAffinity fails)
   uint32_t nreq;        // requirements in req[]
   uint32_t npf;         // scored preferred terms (the class's mask bits)
   uint32_t reqmask;     // bits of the required terms (0: no required-terms filter)
   uint64_t hw, pw;      // taint ids: untolerated NoSchedule/NoExecute, untolerated PreferNoSchedule
   uint64_t hseed;       // tie-break hash seed of the pod
-  uint64_t roff;        // PreFilterResult bitmap (local nodes, rwords words): byte offset into A.progs
+  uint64_t roff;        // PreFilterResult bitmap (rwords words): byte offset into A.progs
   uint32_t rwords, pad0;
   double q0, q1;        // Fit filter requests (-inf: not requested)
   double fs0, fs1;      // Fit score requests
   double bq0, bq1;      // BalancedAllocation requests
   uint64_t pad1[3];     // (128-byte header)
+  int32_t pwt[8];       // weights of the scored preferred terms (static records' raw NodeAffinity score)
   WcReq req[KSG_WC_MAXREQ];
 };
-static_assert(sizeof(WcReq) == 32 && sizeof(WcPod) == 128 + 32 * KSG_WC_MAXREQ, "WcPod layout");
+static_assert(sizeof(WcReq) == 32 && sizeof(WcPod) == 160 + 32 * KSG_WC_MAXREQ, "WcPod layout");
 
 // Is program h a class-path pod the decoder can flatten (prog_need bit 19)?
 __host__ __device__ inline bool wc_decodable(const ksg_prog* h) {
@@ -3155,19 +3157,19 @@ __host__ __device__ inline bool wc_decodable(const ksg_prog* h) {
 // wc_decodable for every one).  The same outcome rules as freq_match / node_sel /
 // required_na: a term of kind 0 matches no node, a key outside the vocabulary is
 // absent from every node.
-__global__ __launch_bounds__(64) void k_wc_decode(DevCluster C, DevProfile F, WiArgs A, WcPod* __restrict__ out) {
-  const uint32_t j = blockIdx.x * 64 + threadIdx.x;
-  if (j >= A.count) return;
-  const ProgView V = view(A.progs + A.prog_off[A.q0 + j]);
+// glob: the PreFilterResult bitmap over every node (node-sharded static records)
+__device__ __forceinline__ void wc_decode_one(const DevCluster& C, const DevProfile& F, const uint8_t* progs,
+                                              uint64_t off, WcPod* __restrict__ outp, bool glob) {
+  const ProgView V = view(progs + off);
   const ksg_prog* h = V.h;
   const uint32_t fl = h->flags;
   const bool ht = F.pos_taint >= 0, ha = F.pos_na >= 0;
   WcPod P{};
-  P.flags = (fl & KPF_PREFILTER_REJECT) ? 1u : 0u;
+  P.flags = (fl & KPF_PREFILTER_REJECT) ? 5u : 0u;
   if (fl & KPF_RESTRICT) {
     P.flags |= 2u;
-    P.roff = A.prog_off[A.q0 + j] + h->off_u32 + 4ull * (uint32_t)h->restrict_off;
-    P.rwords = (uint32_t)h->restrict_words;
+    P.roff = off + h->off_u32 + 4ull * (uint32_t)(glob ? h->restrict_g_off : h->restrict_off);
+    P.rwords = (uint32_t)(glob ? h->restrict_g_words : h->restrict_words);
   }
   P.q0 = h->req[0] > 0 ? (double)h->req[0] : -INFINITY;
   P.q1 = h->req[1] > 0 ? (double)h->req[1] : -INFINITY;
@@ -3208,7 +3210,7 @@ __global__ __launch_bounds__(64) void k_wc_decode(DevCluster C, DevProfile F, Wi
   if (ha && !(fl & KPF_SKIP_NA_FILTER)) {
     if (fl & KPF_HAS_NODE_SEL) emit(h->node_sel, 1u);
     if (fl & KPF_HAS_REQ_NA) {
-      if (h->n_req_terms == 0) P.flags |= 1u;  // (no term to match: no node passes)
+      if (h->n_req_terms == 0) P.flags |= 9u;  // (no term to match: no node passes)
       for (int t = 0; t < h->n_req_terms; ++t) {
         emit(V.sel[h->req_terms_off + t], 1u << (1 + t));
         P.reqmask |= 1u << (1 + t);
@@ -3216,9 +3218,145 @@ __global__ __launch_bounds__(64) void k_wc_decode(DevCluster C, DevProfile F, Wi
     }
   }
   P.npf = (ha && !(fl & KPF_SKIP_NA_SCORE)) ? (uint32_t)h->n_pref_terms : 0u;
-  for (uint32_t t = 0; t < P.npf; ++t) emit(V.sel[h->pref_terms_off + t], 1u << (KSG_WC_PREF_BIT + t));
+  for (uint32_t t = 0; t < P.npf; ++t) {
+    emit(V.sel[h->pref_terms_off + t], 1u << (KSG_WC_PREF_BIT + t));
+    P.pwt[t] = V.i32[h->pref_w_off + t];
+  }
   P.nreq = nr;
-  out[j] = P;
+  *outp = P;
+}
+__global__ __launch_bounds__(64) void k_wc_decode(DevCluster C, DevProfile F, WiArgs A, WcPod* __restrict__ out) {
+  const uint32_t j = blockIdx.x * 64 + threadIdx.x;
+  if (j >= A.count) return;
+  wc_decode_one(C, F, A.progs, A.prog_off[A.q0 + j], out + j, false);
+}
+// The chunk's pods of a static-record launch (k_static_dec), one thread each.
+__global__ __launch_bounds__(64) void k_st_decode(DevCluster C, DevProfile F, const uint8_t* __restrict__ progs,
+                                                  const uint64_t* __restrict__ prog_off, uint32_t q0, uint32_t count,
+                                                  WcPod* __restrict__ out, int glob) {
+  const uint32_t j = blockIdx.x * 64 + threadIdx.x;
+  if (j >= count) return;
+  wc_decode_one(C, F, progs, prog_off[q0 + j], out + j, glob != 0);
+}
+
+// k_static on decoded pods (the cfg5 class path's WcPod): the same records, no
+// program walking per (pod, node).  A thread holds KSG_SD_NPT nodes — their
+// taint ids in node order (<= 4, ids < 64: host-checked) — while the block's
+// KSG_SD_PODS pods go by; each pod's flattened requirements are evaluated into a
+// failed-term mask as in k_whatif_cls1.  Record: the first failing static
+// filter in profile order (TaintToleration: its first untolerated taint in
+// node.spec.taints order; NodeAffinity), else the raw scores; the static maxima
+// over the statically feasible nodes per pod.
+#define KSG_SD_PODS 8
+#define KSG_SD_NPT 2
+__global__ __launch_bounds__(256) void k_static_dec(DevCluster C, DevProfile F, const WcPod* __restrict__ pods,
+                                                    const uint8_t* __restrict__ progs, uint32_t count, StaticRec* out,
+                                                    int64_t* mpred) {
+  const bool ht = F.pos_taint >= 0, ha = F.pos_na >= 0;
+  const bool taint_first = ht && (!ha || F.pos_taint < F.pos_na);
+  uint32_t n[KSG_SD_NPT], tcnt[KSG_SD_NPT];
+  uint32_t tids[KSG_SD_NPT];  // four 8-bit ids in node order
+  uint64_t ts[KSG_SD_NPT];
+  bool live[KSG_SD_NPT];
+#pragma unroll
+  for (int k = 0; k < KSG_SD_NPT; ++k) {
+    const uint32_t nn = blockIdx.x * (256 * KSG_SD_NPT) + k * 256 + threadIdx.x;
+    live[k] = nn < C.N;
+    n[k] = live[k] ? nn : 0u;
+    const uint32_t t0 = C.toff[n[k]], tc = C.toff[n[k] + 1] - t0;
+    uint32_t ids = 0;
+    uint64_t w = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i)
+      if (i < tc) {
+        const uint32_t t = (uint32_t)C.tid[t0 + i] & 63u;
+        ids |= t << (8 * i);
+        w |= 1ull << t;
+      }
+    tcnt[k] = tc < 4 ? tc : 4;
+    tids[k] = ids;
+    ts[k] = w;
+  }
+#pragma unroll 1
+  for (uint32_t pi = 0; pi < KSG_SD_PODS; ++pi) {
+    const uint32_t j = blockIdx.y * KSG_SD_PODS + pi;
+    if (j >= count) break;
+    const WcPod& P = pods[j];
+    const uint32_t fl = P.flags;
+    uint32_t failm[KSG_SD_NPT];
+#pragma unroll
+    for (int k = 0; k < KSG_SD_NPT; ++k) failm[k] = 0;
+    const uint32_t nreq = P.nreq;
+#pragma unroll 1
+    for (uint32_t r = 0; r < nreq; ++r) {
+      const WcReq& R = P.req[r];
+      const uint32_t mode = R.mode, gb = R.gbit;
+      const uint64_t arg = R.arg;
+      if (mode <= 1u) {
+        const int32_t* col = C.label + R.col;
+        int32_t v[KSG_SD_NPT];
+#pragma unroll
+        for (int k = 0; k < KSG_SD_NPT; ++k) v[k] = col[n[k]];
+#pragma unroll
+        for (int k = 0; k < KSG_SD_NPT; ++k) {
+          const bool inset = v[k] >= 0 && ((arg >> ((uint32_t)v[k] & 63u)) & 1ull);
+          failm[k] |= (inset != (mode == 0u)) ? gb : 0u;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < KSG_SD_NPT; ++k) {
+          const bool eq = (uint64_t)(C.goff + n[k]) == arg;
+          const bool m = mode == 4u ? false : (eq != (mode == 3u));
+          failm[k] |= m ? 0u : gb;
+        }
+      }
+    }
+    const uint64_t hw = P.hw, pw = P.pw;
+    const uint32_t reqm = P.reqmask, npf = P.npf;
+    int64_t mt = -1, ma = -1;
+#pragma unroll
+    for (int k = 0; k < KSG_SD_NPT; ++k) {
+      uint32_t code = KSG_FILTER_PASS, raw = 0;
+      bool evaluated = !(fl & 4u);
+      if (evaluated && (fl & 2u))
+        evaluated = bit(reinterpret_cast<const uint32_t*>(progs + P.roff), (int)P.rwords, (int32_t)n[k]);
+      if (!evaluated) {
+        code = KSG_FILTER_NOT_EVALUATED;
+      } else {
+        // TaintToleration Filter: the node's first untolerated NoSchedule / NoExecute taint
+        uint32_t tfail = 0xFFFFFFFFu;
+#pragma unroll
+        for (int i = 3; i >= 0; --i) {
+          const uint32_t t = (tids[k] >> (8 * i)) & 0xFFu;
+          if ((uint32_t)i < tcnt[k] && ((hw >> t) & 1ull)) tfail = t;
+        }
+        const bool nfail = (fl & 8u) || (failm[k] & 1u) || (reqm != 0u && (~failm[k] & reqm) == 0u);
+        if (taint_first) {
+          if (tfail != 0xFFFFFFFFu) code = ((uint32_t)F.pos_taint << 24) | tfail;
+          else if (ha && nfail) code = (uint32_t)F.pos_na << 24;
+        } else {
+          if (ha && nfail) code = (uint32_t)F.pos_na << 24;
+          else if (ht && tfail != 0xFFFFFFFFu) code = ((uint32_t)F.pos_taint << 24) | tfail;
+        }
+        if (code == KSG_FILTER_PASS) {
+          const int64_t t = ht ? (int64_t)__popcll(ts[k] & pw) : 0;
+          int64_t a = 0;
+#pragma unroll
+          for (uint32_t u = 0; u < 8; ++u)
+            if (u < npf && !((failm[k] >> (KSG_WC_PREF_BIT + u)) & 1u)) a += P.pwt[u];
+          raw = ((uint32_t)t << 20) | ((uint32_t)a & KSG_RAW_NA_MASK);
+          mt = t > mt ? t : mt;
+          ma = a > ma ? a : ma;
+        }
+      }
+      if (live[k]) out[(size_t)j * C.N + n[k]] = StaticRec{code, raw};
+    }
+    const int64_t a0 = wave_max(mt), a1 = wave_max(ma);
+    if (lane0()) {
+      if (a0 >= 0) atomicMax((long long*)&mpred[2 * j], (long long)a0);
+      if (a1 >= 0) atomicMax((long long*)&mpred[2 * j + 1], (long long)a1);
+    }
+  }
 }
 
 // A node of the class path's pass 1, held in registers across the block's pods:
@@ -5166,6 +5304,9 @@ struct Engine::Impl {
   bool static_ok = false; // per-pod cycles of Fit/BA/Taint/NA profiles: k_static + k_fs_static
   DBuf<uint64_t> wrec_pairs;  // what-if: pass 1's per-pair records (run_whatif)
   DBuf<uint64_t> wc_pods;     // what-if class path: the chunk's decoded pods (WcPod)
+  DBuf<uint64_t> sd_pods;     // static records: the chunk's decoded pods (WcPod, k_static_dec)
+  int static_dec = 1;         // k_static_dec where the chunk's pods decode (KSG_STATIC_DEC=0: k_static)
+  uint64_t static_dec_chunks = 0;  // diagnostic: static chunks computed from decoded pods
   uint32_t wi_chunk = 0;      // ... pods per chunk of the last step, and whether records were used
   bool wi_rec = false;
   bool wi_cls = false;        // ... or the class path
@@ -5431,6 +5572,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
     HIPCHK(hipStreamCreateWithPriority(&I.sstream, hipStreamNonBlocking, least));
     if (const char* e = std::getenv("KSG_STATIC_SIDE")) I.static_side = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("KSG_STATIC_DEC")) I.static_dec = (int)std::strtol(e, nullptr, 10);
   }
   HIPCHK(hipEventCreate(&I.ev0));
   HIPCHK(hipEventCreate(&I.ev1));
@@ -5934,9 +6076,25 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
       }
       HIPCHK(hipEventRecord(I.sev_st[2 * I.n_st], st));
     }
-    hipLaunchKernelGGL(k_static, sgrid, dim3(256), 0, st, CS, I.F, I.progs.p, I.prog_off_d.p, q0, cn,
-                       I.stat.p + (size_t)((q0 - first) % (nslots * chunk)) * A.stat_n, I.mpred.p + 2 * (size_t)(q0 - first),
-                       gstat ? 1 : 0);
+    StaticRec* const sout = I.stat.p + (size_t)((q0 - first) % (nslots * chunk)) * A.stat_n;
+    // decoded pods (k_static_dec) when every pod of the chunk flattens and the
+    // nodes' taints fit the id set (KSG_STATIC_DEC=0: the program-walking k_static)
+    bool dec = I.static_dec && I.max_taints <= 4 && I.max_tid < 64 && !I.taint_dup;
+    for (uint32_t q = q0; dec && q < q0 + cn; ++q) dec = (I.prog_need[q] & (1u << 19)) != 0;
+    if (dec) {
+      if (!I.sd_pods.alloc((size_t)chunk * (sizeof(WcPod) / 8), err)) return false;
+      WcPod* wp = reinterpret_cast<WcPod*>(I.sd_pods.p);
+      hipLaunchKernelGGL(k_st_decode, dim3((cn + 63) / 64), dim3(64), 0, st, CS, I.F, I.progs.p, I.prog_off_d.p, q0, cn,
+                         wp, gstat ? 1 : 0);
+      const dim3 dgrid(std::max<uint32_t>((SN + 256 * KSG_SD_NPT - 1) / (256 * KSG_SD_NPT), 1),
+                       (cn + KSG_SD_PODS - 1) / KSG_SD_PODS);
+      hipLaunchKernelGGL(k_static_dec, dgrid, dim3(256), 0, st, CS, I.F, wp, I.progs.p, cn, sout,
+                         I.mpred.p + 2 * (size_t)(q0 - first));
+      I.static_dec_chunks++;
+    } else {
+      hipLaunchKernelGGL(k_static, sgrid, dim3(256), 0, st, CS, I.F, I.progs.p, I.prog_off_d.p, q0, cn, sout,
+                         I.mpred.p + 2 * (size_t)(q0 - first), gstat ? 1 : 0);
+    }
     if (ssamp) {
       HIPCHK(hipEventRecord(I.sev_st[2 * I.n_st + 1], st));
       I.stat_pods_sampled += cn;
@@ -7595,6 +7753,7 @@ void Engine::path_counts(uint64_t out[8]) const {
   out[7] = p_->win_runs;
 }
 bool Engine::lost() const { return p_->lost; }
+uint64_t Engine::static_dec_chunks() const { return p_->static_dec_chunks; }
 void Engine::clear_lost() {
   Impl& I = *p_;
   if (I.rsync.p && (I.lost || I.run_used)) {  // (the sticky abort word: a call that failed before its sync left it set)

@@ -1149,9 +1149,9 @@ struct Cluster {
       e = ksg_look{};
       e.base = (int32_t)base;
       e.weight = (int32_t)weight;
-      e.slot = (int16_t)slot;
-      e.kind = (uint8_t)kind;
-      e.use = (uint8_t)use;
+      e.slot = (int32_t)slot;
+      e.kind = (int32_t)kind;
+      e.use = (int32_t)use;
       e.aux = aux;
     };
     auto pc_look = [&](int32_t cls, int32_t nub, int slot, int use, int64_t weight, int aux) {
@@ -1167,8 +1167,8 @@ struct Cluster {
       if (h.n_ub >= KSG_UB_MAX || idx > 0x7FFFFFFFull) { ok = false; return; }
       ksg_ubit& u = h.ub[h.n_ub++];
       u.idx = (int32_t)idx;
-      u.kind = (int16_t)kind;
-      u.bit = (int16_t)bit;
+      u.kind = (int32_t)kind;
+      u.bit = (int32_t)bit;
     };
     const int nf = h.n_tsc_filter, ns = h.n_tsc_score;
     if (pos_of(P_PTS) >= 0) {
@@ -4607,6 +4607,14 @@ extern "C" int ksg_debug_rccl_selftest(int device, size_t bytes, char* err_buf, 
     std::snprintf(err_buf, cap, "%s", err.c_str());
   }
   return ok ? KSG_OK : KSG_E_DEVICE;
+}
+
+// diagnostic (not in ksg.h): static-record chunks computed from decoded pods (k_static_dec)
+extern "C" int ksg_debug_static_dec_chunks(ksg_ctx* ctx, uint64_t* out) {
+  KSG_LOCK(ctx);
+  if (!ctx || !out) return KSG_E_INVALID;
+  *out = ctx->c.eng->static_dec_chunks();
+  return KSG_OK;
 }
 
 // diagnostic (not in ksg.h): the sampled run's k_static launches (cfg3 roofline)

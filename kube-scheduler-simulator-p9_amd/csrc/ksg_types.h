@@ -163,9 +163,12 @@ typedef struct ksg_vchk {
 typedef struct ksg_look {
   int32_t base;    // the table entry of value 0 / node 0 (kind)
   int32_t weight;  // KLU_RAW: signed multiplier
-  int16_t slot;    // topology slot whose value selects the entry (no value: count 0)
-  uint8_t kind;    // KLK_*
-  uint8_t use;     // KLU_*
+  // (every field a 32-bit word: the device reads the plan with scalar loads, which
+  // cannot fetch a byte at an unaligned offset — a byte field became a vector load
+  // whose vmcnt(0) wait serialised every class-table read before it)
+  int32_t slot;    // topology slot whose value selects the entry (no value: count 0)
+  int32_t kind;    // KLK_*
+  int32_t use;     // KLU_*
   int32_t aux;     // KLU_PTSF: the filter constraint
 } ksg_look;
 #define KSG_LK_MAX 24
@@ -183,8 +186,8 @@ typedef struct ksg_look {
 // InterPodAffinity map-emptiness bits (pod-uniform): bit set when the total is > 0
 typedef struct ksg_ubit {
   int32_t idx;   // pc_tot / tc_tot index
-  int16_t kind;  // 1 pc_tot, 2 tc_tot
-  int16_t bit;
+  int32_t kind;  // 1 pc_tot, 2 tc_tot (32-bit fields: scalar loads, see ksg_look)
+  int32_t bit;
 } ksg_ubit;
 #define KSG_UB_MAX 16
 // ksg_prog tab_rd / tab_md bit of class-table key (space 1: pod class, 2: term

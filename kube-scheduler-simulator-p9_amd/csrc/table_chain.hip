@@ -847,6 +847,12 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   }
   CS(4);
   if constexpr (RUN) {  // the block's record; the caller publishes it
+    // diagnostic: each wave of block 0 adds its own arrival (absolute clock) here
+    // (slots 56..59), thread 0 its entry (slot 60)
+    if (A.stamps && blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < 4) {
+      atomicAdd((unsigned long long*)&A.stamps[56 + (threadIdx.x >> 6)], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+      if (threadIdx.x == 0) atomicAdd((unsigned long long*)&A.stamps[60], (unsigned long long)cs_t0);
+    }
     rec_block<TS, BT>(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);
     CS(5);
     eo->feasible = feasible;
@@ -1565,7 +1571,8 @@ __device__ bool run_handshake(RunSync* Y, const RunCtl& R, uint32_t* go) {
 template <int BT>
 struct RunSharedT {
   EvalSharedT<BT> L;
-  uint32_t go;  // LDS broadcast of a poll's outcome
+  uint32_t go;    // LDS broadcast of a poll's outcome
+  uint32_t seen;  // the highest flag value this block has read (a wait it already covers polls nothing)
 };
 // The flag counts the pods of the segment whose assumes are all applied: pod k's
 // owner (block 0 for a pod that places nothing) raises it to k + 1 once it
@@ -1584,6 +1591,7 @@ struct RunWait {
   RunSync* Y;
   uint32_t want;   // flag value awaited (0: none)
   uint32_t* go;    // RunShared::go
+  uint32_t* seen;  // RunShared::seen
   uint64_t* rst;   // diagnostic stamps (block 0), or null
   uint32_t owned;  // this block applied the previous pod's node-level assume
   uint32_t spin;   // RunCtl::spin
@@ -1593,8 +1601,10 @@ struct RunWait {
 // some waves and are read by lanes of others: every wave drains its own, and a
 // barrier orders them before any wave's class-table reads.
 __device__ bool run_wait_flag(const RunWait& W) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (!W.want) {
+  if (W.owned) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the owner's node-level atomics)
+  // a flag value already read (during the previous pod's key poll) covers the
+  // wait of a pod independent of its predecessor: no poll round trip
+  if (!W.want || *W.seen >= W.want) {
     if (W.owned) __syncthreads();
     return true;
   }
@@ -1602,6 +1612,8 @@ __device__ bool run_wait_flag(const RunWait& W) {
     const uint64_t w0 = W.rst ? __builtin_amdgcn_s_memrealtime() : 0;
     bool ok = false;
     for (uint32_t it = 0; it < W.spin; ++it) {
+      // (seen is not updated here: the other waves read it at the top of this call
+      // with no barrier in between; it changes only in the key poll, between barriers)
       if (ld_sc1(&W.Y->flag[0]) >= W.want) { ok = true; break; }
       if (run_aborted(it, W.Y)) break;
       __builtin_amdgcn_s_sleep(2);
@@ -1711,6 +1723,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
   }
   RowV row;
   load_row(C, nn, A0.need_eph, row);
+  if (threadIdx.x == 0) S.seen = 0;
   uint32_t xmask = 0;
   for (int p = 0; p < F.n; ++p) {
     const int x = chain_x(F.plugins[p]);
@@ -1751,7 +1764,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     if (have) {
       eval_body<ROWM, kRun, PM, LK, TS, BT, 2>(C, F, A, prog, &L, &row, &eo, nullptr, &pre);
     } else {
-      const RunWait W{Y, wait_for, &S.go, rs_on ? rst : nullptr, owned, R.spin};
+      const RunWait W{Y, wait_for, &S.go, &S.seen, rs_on ? rst : nullptr, owned, R.spin};
       eval_body<ROWM, kRun, PM, LK, TS, BT>(C, F, A, prog, &L, &row, &eo, &W);
       owned = 0;
     }
@@ -1761,6 +1774,8 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     const int ng1 = run_g1_count(xmask, ns);
     if (threadIdx.x < (uint32_t)ng1) st_sc1(G1 + (size_t)b * kRunGS + threadIdx.x, gran(tag, run_g1_value<TS>(eo.rec, (int)threadIdx.x, xmask, ns)));
     RS(30);
+    // diagnostic: the latest block's partial store (absolute clock, per pod parity)
+    if (rst && threadIdx.x == 0) atomicMax((unsigned long long*)&rst[52 + (k & 1)], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     // ---- pod k+1's class-table reads, in flight across this pod's hand-offs
     const ksg_prog* nh = k + 1 < count ? reinterpret_cast<const ksg_prog*>(P + PO[A.q + 1]) : nullptr;
     const bool tnext = R.overlap && nh && run_indep(h, nh);
@@ -1768,7 +1783,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       ChainArgs A1 = A0;
       A1.q = A.q + 1;
       // the assumes before pod k (before pod k-1 when pod k+1 is independent of it too)
-      const RunWait W1{Y, (ph && run_indep(ph, nh)) ? (k ? k - 1 : 0u) : k, &S.go, nullptr, owned, R.spin};
+      const RunWait W1{Y, (ph && run_indep(ph, nh)) ? (k ? k - 1 : 0u) : k, &S.go, &S.seen, nullptr, owned, R.spin};
       EvalOut ea;
       ea.abort = false;
       eval_body<ROWM, kRun, PM, LK, TS, BT, 1>(C, F, A1, P + PO[A1.q], &L, &row, &ea, &W1, &pre);
@@ -1785,6 +1800,11 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y, R.spin);
       if (__syncthreads_or(!ok)) return;
       RS(31);
+      if (rs_on) {  // the latest block's partial vs this pod's start in block 0 (slot 51)
+        const uint64_t lt = __hip_atomic_load(&rst[52 + (k & 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lt > rs_t0) atomicAdd((unsigned long long*)&rst[51], (unsigned long long)(lt - rs_t0));
+        __hip_atomic_store(&rst[52 + (k & 1)], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       rec_block<TS, BT>(r, L.rec, xmask, ns, RB_CNT | RB_ST);
       RS(39);
       eval_weights(C, h, E);
@@ -1834,6 +1854,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       st_sc1(G2 + (size_t)b * kRunGS + threadIdx.x, gran(tag, v));
     }
     RS(33);
+    if (rst && threadIdx.x == 0) atomicMax((unsigned long long*)&rst[54 + (k & 1)], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     if (threadIdx.x == BT - 32 && k + 1 < count) {  // the next program header into the scalar cache
       uint32_t warm = 0;
       const uint64_t a = (uint64_t)(P + PO[A.q + 1]);  // (uniform: into scalar registers)
@@ -1860,6 +1881,9 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       if (threadIdx.x < NB) {
         const uint64_t* g = G2 + (size_t)threadIdx.x * kRunGS;
         ok = false;
+        // (thread 0 also reads the assume flag: the next pod's wait then needs no poll
+        // when this value covers it — every assume before this pod's, normally)
+        const uint64_t fseen = threadIdx.x == 0 ? ld_sc1(&Y->flag[0]) : 0;
         for (uint32_t it = 0; it < R.spin; ++it) {
           const uint64_t d = ld_sc1(g + 2), a = ld_sc1(g), c = ld_sc1(g + 1);  // (3 granules: all per poll)
           if (gtag(a, tag) && gtag(c, tag) && gtag(d, tag)) {
@@ -1872,11 +1896,17 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
           __builtin_amdgcn_s_sleep(kRunSleep);
         }
         if (!ok && !ld_sc1(&Y->abort[0])) run_raise(Y);
+        if (threadIdx.x == 0 && (uint32_t)fseen > S.seen) S.seen = (uint32_t)fseen;
       }
       if (__syncthreads_or(!ok)) return;
     }
     rec_block<TS, BT>(sk, L.rec, 0u, 0, RB_ST | RB_KEY);
     RS(34);
+    if (rs_on) {  // the latest block's key vs this pod's start in block 0 (slot 53)
+      const uint64_t lt = __hip_atomic_load(&rst[54 + (k & 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lt > rs_t0) atomicAdd((unsigned long long*)&rst[53], (unsigned long long)(lt - rs_t0));
+      __hip_atomic_store(&rst[54 + (k & 1)], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const int32_t feas = E.r.feas, st = E.r.st | sk.st;
     const bool error = (st & 2) || ((st & 4) && feas > 1) || (h->flags & KPF_PREFILTER_ERROR) || na_prescore_error(h->flags, feas);
     const uint32_t g = (uint32_t)(sk.key & 0xFFFFFull);

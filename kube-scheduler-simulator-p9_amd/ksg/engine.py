@@ -363,6 +363,13 @@ class Scheduler:
     def batch_path(self) -> bool:
         return self.L.ksg_batch_path(self.h) == 1
 
+    def static_dec_chunks(self):
+        """Diagnostic: static-record chunks computed from decoded pods (k_static_dec)."""
+        out = ctypes.c_uint64()
+        self.L.ksg_debug_static_dec_chunks.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self._chk(self.L.ksg_debug_static_dec_chunks(self.h, ctypes.byref(out)), "ksg_debug_static_dec_chunks")
+        return out.value
+
     def static_time(self):
         """Diagnostic: (total ms, launches, pods) of the sampled run's k_static launches."""
         ms, n, pods = ctypes.c_float(), ctypes.c_uint32(), ctypes.c_uint64()

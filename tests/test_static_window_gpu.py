@@ -116,3 +116,17 @@ def test_cfg3_full_width_selected_nodes():
     """cfg3's 15,000 nodes, 600 queue pods: every selection equals the oracle's."""
     doc = g.generate(3, n_nodes=15000, n_pods=600)
     _compare(doc, workers=8, record=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dec", ["1", "0"], ids=["decoded", "program-walk"])
+def test_static_records_decoded_and_walked(monkeypatch, dec):
+    """The static records come from decoded pods (k_static_dec: flattened
+    requirements, taint-id sets) wherever a chunk's pods decode, else from the
+    program-walking k_static; both against the oracle on a cfg3 cluster and on
+    the saturating one, and on the NodeAffinity / TaintToleration fallback cases."""
+    monkeypatch.setenv("KSG_STATIC_DEC", dec)
+    for doc in (g.generate(3, n_nodes=700, n_pods=300), _tight_cfg3(n_pods=400), _fallback_doc("taint"),
+                _fallback_doc("na")):
+        _, s = _compare(doc, every=11)
+        assert (s.static_dec_chunks() > 0) == (dec == "1")

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cctype>
 #include <cstdio>
 #include <cstring>
@@ -3058,9 +3059,23 @@ struct Cluster {
   }
 
   // One scheduling cycle of a new pod (appended to the queue).
+  // Host wall time per phase of the drop-in cycle (diagnostic: ksg_debug_cycle_times):
+  // [0] JSON parse + pod decode, [1] queue checks + vocabulary, [2] compile,
+  // [3] program append (+ classes), [4] launch, [5] summary wait, [6] PostFilter,
+  // [7] cycles; microseconds summed.
+  double ctimes[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
   bool cycle(const char* js, size_t len, bool commit, ksg_pod_summary& out) {
     if (shards != 1) { err = "the cycle API needs an unsharded context"; return false; }
     if (!compile_queue()) return false;
+    double t = now_us();
+    auto lap = [&](int k) {
+      const double u = now_us();
+      ctimes[k] += u - t;
+      t = u;
+    };
     try {
       docs.emplace_back(new J(json::parse(js, len)));
     } catch (std::exception& e) {
@@ -3069,6 +3084,7 @@ struct Cluster {
     }
     const J& d = *docs.back();
     queue.push_back(parse_pod(d["pod"] ? *d["pod"] : d));
+    lap(0);
     queue.back().doc = (int32_t)docs.size() - 1;
     if (!volumes_modelled(queue.back())) {
       queue.pop_back();
@@ -3087,24 +3103,30 @@ struct Cluster {
       if (!grow_vocab(queue[q])) return false;
       in_place = true;
     }
+    lap(1);
     if (!in_place) {
       if (!rebuild()) return false;
     } else {
       vector<uint8_t> blob;
       PodMeta m;
       if (!compile(queue[q], (int32_t)(seq_base + q), blob, m)) return false;
+      lap(2);
       if (!sync_classes() || !eng->append_program(blob, err)) return false;  // classes it brought: tables built
       progs.push_back(std::move(blob));
       meta.push_back(std::move(m));
       prog_cls.resize(progs.size(), {(uint32_t)pcls.size(), (uint32_t)tcls.size()});
     }
+    lap(3);
     if (commit) room_ok = false;
     if (commit && !room_for(q)) return false;
     // (the summary's copy waits for the run; sync then only checks the run's state)
-    if (!eng->keep_outputs(q, 1, err) || !eng->run_queue(q, 1, commit, err) || !eng->summaries(q, 1, &out, err) ||
-        !eng->sync(err))
-      return false;
+    if (!eng->keep_outputs(q, 1, err) || !eng->run_queue(q, 1, commit, err)) return false;
+    lap(4);
+    if (!eng->summaries(q, 1, &out, err) || !eng->sync(err)) return false;
+    lap(5);
     if (!preempt(q, out)) return false;  // PostFilter of an unschedulable pod
+    lap(6);
+    ctimes[7] += 1;
     if (commit && out.status == 0) {
       placed[q] = out.selected;
       assumed_in[q] = epoch;
@@ -4607,6 +4629,16 @@ extern "C" int ksg_debug_rccl_selftest(int device, size_t bytes, char* err_buf, 
     std::snprintf(err_buf, cap, "%s", err.c_str());
   }
   return ok ? KSG_OK : KSG_E_DEVICE;
+}
+
+// diagnostic (not in ksg.h): the drop-in cycle's host phases (Cluster::ctimes), 8
+// doubles; reset = 1 clears them after the read
+extern "C" int ksg_debug_cycle_times(ksg_ctx* ctx, double* out, int reset) {
+  KSG_LOCK(ctx);
+  if (!ctx) return KSG_E_INVALID;
+  if (out) std::memcpy(out, ctx->c.ctimes, sizeof(ctx->c.ctimes));
+  if (reset) std::memset(ctx->c.ctimes, 0, sizeof(ctx->c.ctimes));
+  return KSG_OK;
 }
 
 // diagnostic (not in ksg.h): static-record chunks computed from decoded pods (k_static_dec)

@@ -185,7 +185,13 @@ __device__ __forceinline__ int64_t rec_mn(const ChainRec& r, int x) {
 // other fields keep their values).
 enum { RB_CNT = 1, RB_CNT16 = 2, RB_ST = 4, RB_KEY = 8 };  // RB_CNT16: feas, ign < 2^15 per wave (one sum)
 template <int TS = KSG_MAX_TSC, int BT = kChain>  // (TS: registration words a caller can have, nreg <= TS; BT: block threads)
-__device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t xmask, int nreg, uint32_t what) {
+__device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t xmask, int nreg, uint32_t what,
+                                          uint64_t* dbg = nullptr) {
+  // dbg (diagnostic, one thread): time to the wave folds [0], the LDS record [1],
+  // past the barrier [2], the end [61] (the eval-stamp slots that are free)
+  const uint64_t rb0 = dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+#define RBS(i) \
+  if (dbg) atomicAdd((unsigned long long*)&dbg[i], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - rb0))
   if (what & RB_CNT16) {
     const int32_t p = wave_sum(r.feas | (r.ign << 16));
     r.feas = p & 0xFFFF;
@@ -227,6 +233,7 @@ __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t x
   for (int c = 0; c < TS; ++c)
     if (c < nreg) r.reg[c] = wave_or64(r.reg[c]);
   if (what & RB_KEY) r.key = wave_max(r.key);
+  RBS(0);
   ChainRec* w = lds + (threadIdx.x >> 6);
   if (lane0()) {
     w->feas = r.feas;
@@ -243,7 +250,9 @@ __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t x
       if (c < nreg) w->reg[c] = r.reg[c];
     w->key = r.key;
   }
+  RBS(1);
   __syncthreads();
+  RBS(2);
   const bool cnt = (what & (RB_CNT | RB_CNT16)) != 0;
   if (cnt) r.feas = r.ign = 0;
   if (what & RB_ST) r.st = 0;
@@ -266,6 +275,8 @@ __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t x
       if (c < nreg) r.reg[c] |= o->reg[c];
     if (what & RB_KEY) r.key = o->key > r.key ? o->key : r.key;
   }
+  RBS(61);
+#undef RBS
 }
 
 // PodTopologySpread score count of constraint c at local node n (its pair's
@@ -853,7 +864,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
       atomicAdd((unsigned long long*)&A.stamps[56 + (threadIdx.x >> 6)], (unsigned long long)__builtin_amdgcn_s_memrealtime());
       if (threadIdx.x == 0) atomicAdd((unsigned long long*)&A.stamps[60], (unsigned long long)cs_t0);
     }
-    rec_block<TS, BT>(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST);
+    rec_block<TS, BT>(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST, CS_ON ? A.stamps : nullptr);
     CS(5);
     eo->feasible = feasible;
     eo->ipa_flags = ipa_flags;

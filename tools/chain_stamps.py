@@ -59,6 +59,7 @@ def main():
         rep["k_chain_run_flag_wait_us_block0"] = round(out[38] / out[35] * 0.01, 3)
         rep["k_chain_run_latest_block_partial_us"] = round(out[51] / out[35] * 0.01, 3)
         rep["k_chain_run_latest_block_key_us"] = round(out[53] / out[35] * 0.01, 3)
+        rep["rec_block_eval_us: folds, lds record, barrier, end"] = [round(out[i] / out[35] * 0.01, 3) for i in (0, 1, 2, 61)]
         rep["k_eval_block0_wave_scores_done_us"] = [round((out[56 + w] - out[60]) / out[35] * 0.01, 3) for w in range(4)]
         if out[37]:
             rep["k_chain_run_owner_commit_us"] = round(out[36] / out[37] * 0.01, 3)

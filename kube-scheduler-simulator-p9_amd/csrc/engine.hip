@@ -32,6 +32,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <utility>
 #include <deque>
 #include <atomic>
 #include <map>
@@ -7927,6 +7928,7 @@ extern "C" int ksg_debug_lane_selftest(int32_t* bad) {
     rc = -2;
   if (!rc) {
     hipLaunchKernelGGL(ksg::k_selftest_lanes, dim3(nb), dim3(64), 0, 0, d, db);
+    hipLaunchKernelGGL(ksg::k_selftest_fold, dim3(nb / 4), dim3(256), 0, 0, d, db);  // (the same words, 256 a block)
     if (hipGetLastError() != hipSuccess || hipMemcpy(bad, db, 4, hipMemcpyDeviceToHost) != hipSuccess) rc = -2;
   }
   (void)hipFree(d);

@@ -279,6 +279,180 @@ __device__ __forceinline__ void rec_block(ChainRec& r, ChainRec* lds, uint32_t x
 #undef RBS
 }
 
+// ---- Interleaved wave folds (round 5).  rec_block folds each field with its own
+// wave reduction (ockl wfred: DPP steps, each waiting for the previous one, plus
+// the hazard nops), one field after the other: at one wave per SIMD the eight
+// folds of a cfg4 record took ~0.8 us and reading the four wave records back
+// ~0.7 us (stamps, profiles/r05_*).  fold_block runs the DPP steps of ALL fields
+// together (one step's latency paid once for every field: the other fields'
+// instructions fill the hazard slots), then one LDS row of words per wave, one
+// barrier and one read sweep.  Fields are 32-bit words; every lane of the block
+// takes part (no divergent caller).
+enum { FO_ADD = 0, FO_MAXI = 1, FO_MINI = 2, FO_OR = 3, FO_MAXU = 4 };
+template <int OP>
+__device__ __forceinline__ uint32_t fo(uint32_t a, uint32_t b) {
+  if constexpr (OP == FO_ADD) return a + b;
+  else if constexpr (OP == FO_MAXI) return (uint32_t)((int32_t)a > (int32_t)b ? (int32_t)a : (int32_t)b);
+  else if constexpr (OP == FO_MINI) return (uint32_t)((int32_t)a < (int32_t)b ? (int32_t)a : (int32_t)b);
+  else if constexpr (OP == FO_OR) return a | b;
+  else return a > b ? a : b;
+}
+template <int OP>
+__device__ __forceinline__ constexpr uint32_t fo_id() {
+  return OP == FO_MAXI ? 0x80000000u : OP == FO_MINI ? 0x7FFFFFFFu : 0u;
+}
+// one DPP step of a fold: lanes without a source in the pattern (bound_ctrl off, or
+// rows the row mask leaves out) see the identity
+template <int OP, int CTRL, int RM>
+__device__ __forceinline__ uint32_t fo_step(uint32_t v) {
+  return fo<OP>(v, (uint32_t)__builtin_amdgcn_update_dpp((int)fo_id<OP>(), (int)v, CTRL, RM, 0xF, false));
+}
+template <int... OPS>
+struct WFold {
+  static constexpr int K = sizeof...(OPS);
+  template <int CTRL, int RM, size_t... I>
+  static __device__ __forceinline__ void step_(uint32_t (&v)[K], std::index_sequence<I...>) {
+    ((v[I] = fo_step<OPS, CTRL, RM>(v[I])), ...);
+  }
+  template <int CTRL, int RM>
+  static __device__ __forceinline__ void step(uint32_t (&v)[K]) {
+    step_<CTRL, RM>(v, std::make_index_sequence<K>{});
+  }
+  template <size_t... I>
+  static __device__ __forceinline__ void cross_(uint32_t (&v)[K], const uint32_t* row, std::index_sequence<I...>) {
+    ((v[I] = fo<OPS>(v[I], row[I])), ...);
+  }
+  // the wave's fold: row_shr 1, 2, 4, 8 (a row's total in its lane 15), then
+  // row_bcast 15 / 31 (the wave's total in lane 63), read back as uniform values
+  static __device__ __forceinline__ void wave(uint32_t (&v)[K]) {
+    step<0x111, 0xF>(v);
+    step<0x112, 0xF>(v);
+    step<0x114, 0xF>(v);
+    step<0x118, 0xF>(v);
+    step<0x142, 0xA>(v);
+    step<0x143, 0xC>(v);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = (uint32_t)__builtin_amdgcn_readlane((int)v[k], 63);
+  }
+  // the block's fold: wave folds, one row of K words per wave in LDS (stride 16
+  // words), one barrier, every thread folds the rows.  lds: NW * 16 words.
+  template <int NW>
+  static __device__ __forceinline__ void block(uint32_t (&v)[K], uint32_t* lds) {
+    static_assert(K <= 16, "fold row");
+    wave(v);
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) lds[(threadIdx.x >> 6) * 16 + k] = v[k];
+    }
+    __syncthreads();
+    uint32_t row[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = lds[k];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) row[k] = lds[w * 16 + k];
+      cross_(v, row, std::make_index_sequence<K>{});
+    }
+  }
+};
+// int64 normaliser fields as 32-bit words (callers checked the values fit): the
+// unset sentinels map to the 32-bit extremes and back
+__device__ __forceinline__ uint32_t mx32(int64_t v) { return v == INT64_MIN ? 0x80000000u : (uint32_t)(int32_t)v; }
+__device__ __forceinline__ uint32_t mn32(int64_t v) { return v == INT64_MAX ? 0x7FFFFFFFu : (uint32_t)(int32_t)v; }
+__device__ __forceinline__ int64_t mx64(uint32_t v) { return v == 0x80000000u ? INT64_MIN : (int64_t)(int32_t)v; }
+__device__ __forceinline__ int64_t mn64(uint32_t v) { return v == 0x7FFFFFFFu ? INT64_MAX : (int64_t)(int32_t)v; }
+__device__ __forceinline__ bool fits32(const ChainRec& r, int x) {
+  return (r.mx[x] == INT64_MIN || (r.mx[x] > INT32_MIN && r.mx[x] < INT32_MAX)) &&
+         (r.mn[x] == INT64_MAX || (r.mn[x] > INT32_MIN && r.mn[x] < INT32_MAX));
+}
+// The persistent chain's record folds (rec_block's results, fast): a partial
+// record with the counts, status, the normalisers of slots XA / XB (KCX_*) and one
+// registration word — what a table-chain pod of k_chain_run's size class reduces
+// (<= 1 PodTopologySpread score constraint; cfg4's PodTopologySpread +
+// InterPodAffinity); the generic rec_block when a normaliser needs 64 bits.
+template <int XA, int XB, int BT>
+__device__ __forceinline__ void fold_partial(ChainRec& r, ChainRec* lds, uint32_t xmask, int nreg, bool cnt16) {
+  bool wide = false;
+  if ((xmask >> XA) & 1u) wide |= !fits32(r, XA);
+  if ((xmask >> XB) & 1u) wide |= !fits32(r, XB);
+  // (the choice is the block's: a barrier-OR, which also orders the rows' reuse)
+  if (__syncthreads_or(wide) || nreg > 1 || (xmask & ~((1u << XA) | (1u << XB)))) {
+    rec_block<KSG_MAX_TSC, BT>(r, lds, xmask, nreg, (cnt16 ? RB_CNT16 : RB_CNT) | RB_ST);
+    return;
+  }
+  uint32_t v[9] = {(uint32_t)r.feas, (uint32_t)r.ign, (uint32_t)r.st, mx32(r.mx[XA]), mn32(r.mn[XA]), mx32(r.mx[XB]),
+                   mn32(r.mn[XB]), nreg ? (uint32_t)r.reg[0] : 0u, nreg ? (uint32_t)(r.reg[0] >> 32) : 0u};
+  WFold<FO_ADD, FO_ADD, FO_OR, FO_MAXI, FO_MINI, FO_MAXI, FO_MINI, FO_OR, FO_OR>::block<BT / 64>(
+      v, reinterpret_cast<uint32_t*>(lds));
+  r.feas = (int32_t)v[0];
+  r.ign = (int32_t)v[1];
+  r.st = (int32_t)v[2];
+  if ((xmask >> XA) & 1u) { r.mx[XA] = mx64(v[3]); r.mn[XA] = mn64(v[4]); }
+  if ((xmask >> XB) & 1u) { r.mx[XB] = mx64(v[5]); r.mn[XB] = mn64(v[6]); }
+  if (nreg) r.reg[0] = (uint64_t)v[7] | ((uint64_t)v[8] << 32);
+}
+// The key folds: status (or) and the 64-bit best key (its high word, then the low
+// word among the lanes holding the winning high word).
+template <int BT>
+__device__ __forceinline__ void fold_key(ChainRec& r, ChainRec* lds) {
+  __syncthreads();  // (lds reused)
+  uint32_t* w = reinterpret_cast<uint32_t*>(lds);
+  uint32_t v[2] = {(uint32_t)r.st, (uint32_t)(r.key >> 32)};
+  WFold<FO_OR, FO_MAXU>::wave(v);
+  uint32_t lo[1] = {(uint32_t)(r.key >> 32) == v[1] ? (uint32_t)r.key : 0u};
+  WFold<FO_MAXU>::wave(lo);
+  if ((threadIdx.x & 63) == 0) {
+    w[(threadIdx.x >> 6) * 16 + 0] = v[0];
+    w[(threadIdx.x >> 6) * 16 + 1] = v[1];
+    w[(threadIdx.x >> 6) * 16 + 2] = lo[0];
+  }
+  __syncthreads();
+  uint32_t st = 0, hi = 0, l = 0;
+#pragma unroll
+  for (int i = 0; i < BT / 64; ++i) {
+    const uint32_t s0 = w[i * 16], h0 = w[i * 16 + 1], l0 = w[i * 16 + 2];
+    st |= s0;
+    if (h0 > hi || (h0 == hi && l0 > l)) { hi = h0; l = l0; }
+  }
+  r.st = (int32_t)st;
+  r.key = ((uint64_t)hi << 32) | l;
+}
+
+// Self-test of the interleaved folds (ksg_debug_lane_selftest): a block fold of
+// every operation against LDS atomics, and the key fold against a plain scan.
+__global__ __launch_bounds__(256) void k_selftest_fold(const uint64_t* in, int32_t* bad) {
+  __shared__ uint32_t rows[4 * 16];
+  __shared__ uint32_t ref[5];
+  __shared__ ChainRec lrec[4];
+  __shared__ unsigned long long kref;
+  const uint64_t x = in[blockIdx.x * 256 + threadIdx.x];
+  const uint32_t a = (uint32_t)x, b = (uint32_t)(x >> 32);
+  if (threadIdx.x == 0) {
+    ref[0] = 0; ref[1] = 0x80000000u; ref[2] = 0x7FFFFFFFu; ref[3] = 0; ref[4] = 0;
+    kref = 0;
+  }
+  __syncthreads();
+  atomicAdd(&ref[0], a & 0xFFFu);
+  atomicMax((int*)&ref[1], (int)a);
+  atomicMin((int*)&ref[2], (int)b);
+  atomicOr(&ref[3], a & 0xF0F0u);
+  atomicMax(&ref[4], b);
+  atomicMax(&kref, (unsigned long long)(x & ~0xFull));
+  __syncthreads();
+  uint32_t v[5] = {a & 0xFFFu, a, b, a & 0xF0F0u, b};
+  WFold<FO_ADD, FO_MAXI, FO_MINI, FO_OR, FO_MAXU>::block<4>(v, rows);
+  int e = 0;
+  for (int k = 0; k < 5; ++k) e += v[k] != ref[k];
+  ChainRec r;
+  rec_init(r);
+  r.key = x & ~0xFull;
+  r.st = (int32_t)(a & 3u);
+  fold_key<256>(r, lrec);
+  e += r.key != kref;
+  atomicAdd(bad, e);
+}
+
 // PodTopologySpread score count of constraint c at local node n (its pair's
 // TopologyPairToPodCounts, or the node's own count for the hostname key).
 __device__ __forceinline__ int64_t pts_count_tab(const DevCluster& C, const ProgView& V, int c, uint32_t n, int32_t v) {
@@ -864,7 +1038,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
       atomicAdd((unsigned long long*)&A.stamps[56 + (threadIdx.x >> 6)], (unsigned long long)__builtin_amdgcn_s_memrealtime());
       if (threadIdx.x == 0) atomicAdd((unsigned long long*)&A.stamps[60], (unsigned long long)cs_t0);
     }
-    rec_block<TS, BT>(rec, L.rec, xmask, nreg, RB_CNT16 | RB_ST, CS_ON ? A.stamps : nullptr);
+    fold_partial<KCX_PTS, KCX_IPA, BT>(rec, L.rec, xmask, nreg, true);
     CS(5);
     eo->feasible = feasible;
     eo->ipa_flags = ipa_flags;
@@ -1816,7 +1990,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
         if (lt > rs_t0) atomicAdd((unsigned long long*)&rst[51], (unsigned long long)(lt - rs_t0));
         __hip_atomic_store(&rst[52 + (k & 1)], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      rec_block<TS, BT>(r, L.rec, xmask, ns, RB_CNT | RB_ST);
+      fold_partial<KCX_PTS, KCX_IPA, BT>(r, L.rec, xmask, ns, false);
       RS(39);
       eval_weights(C, h, E);
     }
@@ -1858,8 +2032,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       r.st = (E.r.feas > 1 && range_err) ? 4 : 0;
     }
     RS(47);
-    __syncthreads();  // (L.rec reused)
-    rec_block<TS, BT>(r, L.rec, 0u, 0, RB_ST | RB_KEY);
+    fold_key<BT>(r, L.rec);
     if (threadIdx.x < (uint32_t)kRunG2) {
       const uint32_t v = threadIdx.x == 0 ? (uint32_t)r.key : threadIdx.x == 1 ? (uint32_t)(r.key >> 32) : (uint32_t)r.st;
       st_sc1(G2 + (size_t)b * kRunGS + threadIdx.x, gran(tag, v));
@@ -1911,7 +2084,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       }
       if (__syncthreads_or(!ok)) return;
     }
-    rec_block<TS, BT>(sk, L.rec, 0u, 0, RB_ST | RB_KEY);
+    fold_key<BT>(sk, L.rec);
     RS(34);
     if (rs_on) {  // the latest block's key vs this pod's start in block 0 (slot 53)
       const uint64_t lt = __hip_atomic_load(&rst[54 + (k & 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2013,7 +2186,7 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
     bool ok = true;
     if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y, R.spin);
     if (__syncthreads_or(!ok)) return;
-    rec_block<TS, BT>(r, lrec, 0u, 0, RB_CNT | RB_ST);
+    fold_partial<KCX_PTS, KCX_IPA, BT>(r, lrec, 0u, 0, false);
     ChainRec sk;
     rec_init(sk);
     ok = true;
@@ -2034,7 +2207,7 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
       if (!ok && !ld_sc1(&Y->abort[0])) run_raise(Y);
     }
     if (__syncthreads_or(!ok)) return;
-    rec_block<TS, BT>(sk, lrec, 0u, 0, RB_ST | RB_KEY);
+    fold_key<BT>(sk, lrec);
     const int32_t feas = r.feas, st = r.st | sk.st;
     const bool error = (st & 2) || ((st & 4) && feas > 1) || (h->flags & KPF_PREFILTER_ERROR) || na_prescore_error(h->flags, feas);
     const uint32_t g = (uint32_t)(sk.key & 0xFFFFFull);

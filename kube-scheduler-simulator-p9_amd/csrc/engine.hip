@@ -1223,6 +1223,14 @@ __global__ void k_pts_score(DevCluster C, DevScratch S, DevOut O, const uint8_t*
   }
 }
 
+// floor(x / mx) for NormalizeScore's 0 <= x <= 100 * mx: the f32-reciprocal
+// divide (udiv_small: x < 2^27, quotient <= 128) for every normaliser below 2^20
+// (pod-uniform branch), else div_small — not the 32-bit integer divide's
+// ~40-instruction sequence per node
+__device__ __forceinline__ int64_t norm_div(int64_t x, int64_t mx) {
+  return mx < ((int64_t)1 << 20) && x >= 0 && x <= 100 * mx ? (int64_t)udiv_small((uint32_t)x, (uint32_t)mx)
+                                                              : div_small(x, mx);
+}
 // NormalizeScore (wrappedplugin.go:400 -> the plugin's ScoreExtensions) of one
 // feasible node's raw score at a profile position, given the pod's normaliser
 // max / min over the feasible nodes: every path that selects (k_finalize, the
@@ -1238,16 +1246,16 @@ __device__ __forceinline__ int64_t normalize_pos(int plugin, const ksg_prog* h, 
   switch (plugin) {
     case KP_TAINT:  // DefaultNormalizeScore(100, reverse); 0 <= s <= mx
       if constexpr (!((PM >> KP_TAINT) & 1u)) return s;
-      return mx == 0 ? 100 : 100 - div_small(100 * s, mx);
+      return mx == 0 ? 100 : 100 - norm_div(100 * s, mx);
     case KP_NA:  // DefaultNormalizeScore(100, false)
       if constexpr (!((PM >> KP_NA) & 1u)) return s;
       if (h->flags & KPF_SKIP_NA_SCORE) { use = false; return s; }
-      return mx == 0 ? s : div_small(100 * s, mx);
+      return mx == 0 ? s : norm_div(100 * s, mx);
     case KP_PTS:  // 0 <= mn <= s <= mx; nodes missing a key (IgnoredNodes) score 0
       if (h->flags & KPF_SKIP_PTS_SCORE) { use = false; return s; }
       if (!pts_keys) return 0;
       if (mx == 0) return 100;
-      return div_small(100 * (mx + mn - s), mx);
+      return norm_div(100 * (mx + mn - s), mx);
     case KP_IPA: {
 #pragma clang fp contract(off)
       if (!(ipa_flags & 8u)) { use = false; return s; }  // PreScore Skip (empty topology score map)

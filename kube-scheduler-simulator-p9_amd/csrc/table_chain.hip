@@ -657,12 +657,30 @@ struct RunWait;
 __device__ bool run_wait_flag(const RunWait& W);
 // LK / TS: the lookup-plan entries and spread constraints a pod of the launch has
 // at most (k_chain_run size classes; smaller unrolled loops, less code).
+// The row-only plugins of a persistent-chain pod computed ahead, during the
+// previous pod's key hand-off (k_chain_run): Fit's filter bits, Fit's and
+// BalancedAllocation's raw scores on the row as of then (the owner of the
+// previous pod's node recomputes that node's after its assume).
+struct RowPre {
+  uint32_t fb;
+  int64_t fs, bs;
+};
+template <int ROWM, uint32_t PM, class P>
+__device__ __forceinline__ void row_pre(const RowV& row, const DevProfile& F, const P* h, uint32_t R, RowPre& o) {
+  o.fb = 0;
+  o.fs = o.bs = 0;
+  if (PMH(KP_FIT)) {
+    o.fb = fit_filter_row(row, h, R);
+    o.fs = ROWM == 2 ? fit_score_row<1>(row, F, h) : fit_score_row<0>(row, F, h);
+  }
+  if (PMH(KP_BA)) o.bs = ROWM == 2 ? ba_score_row<1>(row, F, h) : ba_score_row<0>(row, F, h);
+}
 template <int ROWM, int MODE = kEval, uint32_t PM = ~0u, int LK = KSG_LK_MAX, int TS = KSG_MAX_TSC, int BT = kChain,
           int STG = 0>
 __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, const ChainArgs& A,
                                           const uint8_t* __restrict__ prog, EvalSharedT<BT>* Lrun = nullptr,
                                           RowV* rowrun = nullptr, EvalOut* eo = nullptr, const RunWait* W = nullptr,
-                                          EvalPre* pre = nullptr) {
+                                          EvalPre* pre = nullptr, const RowPre* rp = nullptr) {
   constexpr bool SOLO = MODE == kSolo, RUN = MODE == kRun;
   static_assert(STG == 0 || RUN, "staged evaluation: the persistent chain only");
   static_assert(BT == kChain || RUN, "other block sizes: the persistent chain only");
@@ -715,7 +733,11 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   uint32_t fit_b = 0;
   int64_t fit_s = 0, ba_s = 0;
   if constexpr (RUN && ROWM != 0) {
-    if (STG != 1) {  // (staged: on the row as of the finish)
+    if (rp) {  // (computed during the previous pod's key hand-off)
+      fit_b = rp->fb;
+      fit_s = rp->fs;
+      ba_s = rp->bs;
+    } else if (STG != 1) {  // (staged: on the row as of the finish)
       if (PMH(KP_FIT)) {
         fit_b = fit_filter_row(row, h, C.R);
         fit_s = ROWM == 2 ? fit_score_row<1>(row, F, h) : fit_score_row<0>(row, F, h);
@@ -1931,6 +1953,8 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
   // finishes from them (eval_body stages 1 / 2) on its row as of then.
   bool have = false;       // pre holds pod k's reads (issued during pod k-1)
   EvalPre pre;
+  RowPre rpre;             // pod k's row-only plugins, computed during pod k-1's key hand-off
+  bool rpre_ok = false;
   const ksg_prog* ph = nullptr;  // pod k-1's header
   for (uint32_t k = 0; k < count; ++k) {
     ChainArgs A = A0;  // (A.stamps: eval_body's own k_eval slots, block 0)
@@ -1950,7 +1974,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       eval_body<ROWM, kRun, PM, LK, TS, BT, 2>(C, F, A, prog, &L, &row, &eo, nullptr, &pre);
     } else {
       const RunWait W{Y, wait_for, &S.go, &S.seen, rs_on ? rst : nullptr, owned, R.spin};
-      eval_body<ROWM, kRun, PM, LK, TS, BT>(C, F, A, prog, &L, &row, &eo, &W);
+      eval_body<ROWM, kRun, PM, LK, TS, BT>(C, F, A, prog, &L, &row, &eo, &W, nullptr, rpre_ok ? &rpre : nullptr);
       owned = 0;
     }
     if (eo.abort) return;
@@ -2047,6 +2071,13 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       KWarm<0, kHdrBytes>::run(reinterpret_cast<const void*>(su), warm);
       warm_wait(warm);  // (the loads land in one scalar register the compiler may reuse: wait here)
     }
+    // the next pod's row-only plugins while the keys arrive (not when its reads go
+    // ahead: the staged evaluation computes them itself)
+    rpre_ok = false;
+    if (nh && !tnext) {
+      row_pre<ROWM, PM>(row, F, view(P + PO[A.q + 1]).h, C.R, rpre);
+      rpre_ok = true;
+    }
     // the assume's items (class ids, own affinity terms) into registers while the
     // keys arrive: the owner's commit then issues its atomics without a load
     const uint32_t npm = (uint32_t)h->n_pc_match, nitems = npm + (uint32_t)h->n_exist_terms;
@@ -2120,6 +2151,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
         row.nzc += h->nz_cpu;
         row.nzm += h->nz_mem;
         row.podcnt += 1;
+        if (rpre_ok) row_pre<ROWM, PM>(row, F, view(P + PO[A.q + 1]).h, C.R, rpre);  // (its row changed)
       }
       if (C.T.on && threadIdx.x < nitems) {
         int32_t v[KSG_MAX_TOPO];

@@ -3709,7 +3709,8 @@ struct PatchV {
 struct PriorRec {
   uint64_t pkey[KSG_BATCH];  // key on prior node e (0: infeasible)
   PatchV patch[KSG_BATCH];
-  int32_t pdf[KSG_BATCH];    // feasible-count change vs the snapshot
+  int32_t pdf[KSG_BATCH];    // feasible-count change vs the snapshot (byte 0); Taint / NodeAffinity profiles:
+                             // the static-max achievers' changes in bytes 1 / 2 (each an int8)
   RowV row[KSG_STAGE];       // rows of candidate ranks < KSG_STAGE (window-start rows)
   uint64_t pmask, pbest;     // candidates that are prior nodes; the best prior key
   int32_t pbest_e, np;
@@ -3811,17 +3812,35 @@ __device__ __forceinline__ void win_merge(const DevCluster& C, const DevProfile&
       int32_t fs, bs;
       int64_t tot;
       const uint32_t R = C.R < 4 ? C.R : 4;
-      const uint32_t code = eval_row<MODE>(pe.after, F, h, R, fs, bs, tot);
-      const bool snap_ok = F.pos_fit < 0 || fit_filter_row(pe.base, h, R) == 0;
+      StaticRec sr{KSG_FILTER_PASS, 0};
+      uint32_t code;
+      int64_t mt = 0, ma = 0;
+      if (STAT) {  // (the static maxima and records were computed before the launch)
+        const uint32_t q = A.e0 + b;
+        mt = A.mpred[2 * (q - A.first)];
+        ma = A.mpred[2 * (q - A.first) + 1];
+        sr = srec_at(A, q, (uint32_t)pe.node);
+        code = eval_row_s<MODE>(pe.after, F, h, R, sr, mt, ma, fs, bs, tot);
+      } else {
+        code = eval_row<MODE>(pe.after, F, h, R, fs, bs, tot);
+      }
+      const bool snap_ok = sr.code == KSG_FILTER_PASS && (F.pos_fit < 0 || fit_filter_row(pe.base, h, R) == 0);
       PatchV pt;
       pt.code = code;
       pt.fitba = fs | (bs << 16);
       pt.total = (int32_t)tot;
-      pt.raw = 0;
+      pt.raw = sr.raw;
       k = code == KSG_FILTER_PASS ? pack_key(tot, F.seed, h->queue_idx, (uint32_t)pe.node) : 0;
       stv<true>(&pr->pkey[lane], k);
       st_obj<true>(&pr->patch[lane], pt);
-      stv<true>(&pr->pdf[lane], (int32_t)((code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0)));
+      const int df = (code == KSG_FILTER_PASS ? 1 : 0) - (snap_ok ? 1 : 0);
+      int dT = 0, dA = 0;
+      if (STAT) {
+        const bool na_on = F.pos_na >= 0 && !(h->flags & KPF_SKIP_NA_SCORE);
+        dT = F.pos_taint >= 0 && (int64_t)(sr.raw >> 20) == mt ? df : 0;
+        dA = na_on && (int64_t)(sr.raw & KSG_RAW_NA_MASK) == ma ? df : 0;
+      }
+      stv<true>(&pr->pdf[lane], (int32_t)(((uint32_t)df & 0xFFu) | (((uint32_t)dT & 0xFFu) << 8) | (((uint32_t)dA & 0xFFu) << 16)));
     }
     bool isp = false;  // candidate `lane` is a P_{E-1} node
     for (int e = 0; e < np1; ++e) isp |= v != 0 && __builtin_amdgcn_readlane(pe.node, e) == gid;
@@ -3868,7 +3887,7 @@ __device__ __forceinline__ void win_merge(const DevCluster& C, const DevProfile&
 // Persistent loop, dedicated merge block of pod b: waits for the pod's T tile
 // lists (the arrival counter), then merges them (win_merge) while the tile blocks
 // go on to the next window.
-template <int MODE>
+template <int MODE, bool STAT = false>
 __device__ __forceinline__ bool win_merge_block(const DevCluster& C, const DevProfile& F, const WinArgs& A, uint32_t b,
                                                 uint64_t* L) {
   const int tid = threadIdx.x;
@@ -3895,7 +3914,7 @@ __device__ __forceinline__ bool win_merge_block(const DevCluster& C, const DevPr
   const int np = ldv<true>(A.pprev_n);
   if (tid < np) pnl[tid] = ldv<true>(&A.pprev[tid].node);
   __syncthreads();
-  win_merge<MODE, false, true>(C, F, A, b, L, h, pnl, np);
+  win_merge<MODE, STAT, true>(C, F, A, b, L, h, pnl, np);
   return true;
 }
 // Blocks 1.. of k_window: one pod x KSG_TILE nodes per block.  Tile lists are
@@ -4281,13 +4300,14 @@ __device__ __forceinline__ uint64_t max3u(uint64_t a, uint64_t b, uint64_t c) {
 
 // Pod b's row of global node g under the picks S of the pods < b (a local node's
 // row from the node rows, another shard's from the replica).
+template <bool PER = false>
 __device__ __forceinline__ void row_under(const DevCluster& C, const WinLDS& L, const WinArgs& A, const int32_t* S,
                                           const PickTab& T, int b, uint32_t gu, uint32_t R, RowV& r) {
   const int32_t g = (int32_t)gu;
   const int e = prior_of(L, g);
   if (e >= 0) r = L.prior[e].after;
   else if (A.xrows) r = A.xrows[g];
-  else load_row(C, gu - C.goff, A.need_eph, r);
+  else load_row_p<PER>(C, gu - C.goff, A.need_eph, r);  // (persistent loop: rows this block rewrites)
   const int hs = tab_find(T.node, g);
   if (hs >= 0 && T.first[hs] < b) {
     Delta cum{};
@@ -4299,7 +4319,7 @@ __device__ __forceinline__ void row_under(const DevCluster& C, const WinLDS& L, 
 // STAT profiles, no feasible node of pod b left at the static max (rare): its
 // exact result under S = L.S[cur] from two block-wide passes over all nodes —
 // the normaliser over the feasible nodes, then the argmax — into L.S[nxt][b].
-template <int MODE>
+template <int MODE, bool PER = false>
 __device__ __forceinline__ void win_exact_select(const DevCluster& C, const DevProfile& F, const WinArgs& A, WinLDS& L,
                                               int b, int cur, int nxt, uint32_t R) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -4313,7 +4333,7 @@ __device__ __forceinline__ void win_exact_select(const DevCluster& C, const DevP
 #pragma unroll 1
   for (uint32_t i = tid; i < gn; i += KSG_WIN_THREADS) {
     RowV r;
-    row_under(C, L, A, S, T, b, g0 + i, R, r);
+    row_under<PER>(C, L, A, S, T, b, g0 + i, R, r);
     const StaticRec sr = srec_at(A, A.w0 + b, g0 + i);
     int32_t fs, bs;
     int64_t tot;
@@ -4343,7 +4363,7 @@ __device__ __forceinline__ void win_exact_select(const DevCluster& C, const DevP
 #pragma unroll 1
   for (uint32_t i = tid; i < gn; i += KSG_WIN_THREADS) {
     RowV r;
-    row_under(C, L, A, S, T, b, g0 + i, R, r);
+    row_under<PER>(C, L, A, S, T, b, g0 + i, R, r);
     int32_t fs, bs;
     int64_t tot;
     if (eval_row_s<MODE>(r, F, h, R, srec_at(A, A.w0 + b, g0 + i), mt, ma, fs, bs, tot) == KSG_FILTER_PASS) {
@@ -4376,7 +4396,7 @@ __device__ __forceinline__ void win_exact_select(const DevCluster& C, const DevP
   }
 }
 // ... and, once S is final, every per-pair output of such a pod.
-template <int MODE>
+template <int MODE, bool PER = false>
 __device__ __forceinline__ void win_exact_write(const DevCluster& C, const DevProfile& F, const WinArgs& A, WinLDS& L,
                                              int b, int cur, uint32_t R) {
   const PodLite* h = &L.pod[b];
@@ -4387,12 +4407,13 @@ __device__ __forceinline__ void win_exact_write(const DevCluster& C, const DevPr
 #pragma unroll 1
   for (uint32_t i = threadIdx.x; i < C.N; i += KSG_WIN_THREADS) {  // (this shard's outputs)
     RowV r;
-    row_under(C, L, A, L.S[cur], L.pick[cur], b, C.goff + i, R, r);
+    row_under<PER>(C, L, A, L.S[cur], L.pick[cur], b, C.goff + i, R, r);
     const StaticRec sr = srec_at(A, A.w0 + b, C.goff + i);
     int32_t fs, bs;
     int64_t tot;
     const uint32_t code = eval_row_s<MODE>(r, F, h, R, sr, mt, ma, fs, bs, tot);
-    write_pair<true>(F, of, os, ot, C.N, i, code, fs, bs, tot, sr.raw);
+    if (PER && kept_q(A, A.w0 + b)) write_pair<true, true>(F, of, os, ot, C.N, i, code, fs, bs, tot, sr.raw);
+    else write_pair<true>(F, of, os, ot, C.N, i, code, fs, bs, tot, sr.raw);
   }
 }
 
@@ -4449,8 +4470,8 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     int64_t m0 = -1, m1 = -1;
     if (STAT && tid < nb) {
       if (!A.defer) {
-        aT = reinterpret_cast<const int32_t*>(A.wrec)[KSG_BATCH + tid];
-        aA = reinterpret_cast<const int32_t*>(A.wrec)[2 * KSG_BATCH + tid];
+        aT = ldv<PER>(reinterpret_cast<const int32_t*>(A.wrec) + KSG_BATCH + tid);
+        aA = ldv<PER>(reinterpret_cast<const int32_t*>(A.wrec) + 2 * KSG_BATCH + tid);
       }
       m0 = A.mpred[2 * (A.w0 - A.first + tid)];
       m1 = A.mpred[2 * (A.w0 - A.first + tid) + 1];
@@ -4562,7 +4583,11 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       L.pkey[ppb][ppe] = pr_k;
       reinterpret_cast<uint64_t*>(&L.patch[ppb][ppe])[0] = pr_p0;
       reinterpret_cast<uint64_t*>(&L.patch[ppb][ppe])[1] = pr_p1;
-      L.pdf[ppb][ppe] = (int8_t)pr_df;
+      L.pdf[ppb][ppe] = (int8_t)(pr_df & 0xFF);
+      if (STAT) {
+        L.pdfT[ppb][ppe] = (int8_t)((pr_df >> 8) & 0xFF);
+        L.pdfA[ppb][ppe] = (int8_t)((pr_df >> 16) & 0xFF);
+      }
       if (ppe == 0) L.pmask[ppb] = pr_m;
       if (ppe == 1) L.pbest[ppb] = pr_m;
       if (ppe == 2) L.pbest_e[ppb] = (int32_t)(uint32_t)pr_m;
@@ -4835,7 +4860,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
         while (fm) {
           const int b = __ffsll((long long)fm) - 1;
           fm &= fm - 1;
-          win_exact_select<MODE>(C, F, A, L, b, cur, nxt, R);
+          win_exact_select<MODE, PER>(C, F, A, L, b, cur, nxt, R);
         }
         lds_barrier();
       }
@@ -4946,7 +4971,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
     while (fm) {
       const int b = __ffsll((long long)fm) - 1;
       fm &= fm - 1;
-      win_exact_write<MODE>(C, F, A, L, b, cur, R);
+      win_exact_write<MODE, PER>(C, F, A, L, b, cur, R);
     }
   }
   STAMP(5);
@@ -5076,7 +5101,9 @@ __device__ bool win_wait_ge(const uint32_t* w, uint32_t want, uint32_t* abortw, 
   __syncthreads();
   return ok;
 }
-template <int MODE>
+// STAT: Taint / NodeAffinity profiles, on static records computed for the whole
+// run before the launch (round 5; the launch-per-window loop rolls a ring of chunks)
+template <int MODE, bool STAT = false>
 __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, DevProfile F, WinArgs A0, WinRunArgs R,
                                                                 RunSync* Y, WinSync* Z, RunCtl RC) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -5126,7 +5153,7 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
       } else {
         A.nxt_evd = nullptr;
       }
-      win_fixup<MODE, false, true>(C, F, A, L);  // (publishes P_W before its output patches)
+      win_fixup<MODE, STAT, true>(C, F, A, L);  // (publishes P_W before its output patches)
       __syncthreads();  // (LDS reused by the next window)
     }
     return;
@@ -5152,7 +5179,7 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
       A.pcur_n = R.pend_n + ((E + 1) & 1);
       A.pubw = E >= 1 ? &Z->replayed[b & 15][0] : nullptr;
       A.pub_need = E;
-      if (!win_merge_block<MODE>(C, F, A, b, L)) return;
+      if (!win_merge_block<MODE, STAT>(C, F, A, b, L)) return;
       __syncthreads();  // (LDS reused by the next window)
     }
     return;
@@ -5178,7 +5205,7 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
     A.pcur_n = R.pend_n + ((E + 1) & 1);
     A.pubw = E >= 1 ? &Z->replayed[blk & 15][0] : nullptr;  // (E = 0: P_{-1} is empty)
     A.pub_need = E;
-    win_eval<MODE, false, true>(C, F, A, blk, L);
+    win_eval<MODE, STAT, true>(C, F, A, blk, L);
     __syncthreads();  // (LDS reused by the next window)
   }
 }
@@ -5315,6 +5342,7 @@ struct Engine::Impl {
   DBuf<uint64_t> wc_pods;     // what-if class path: the chunk's decoded pods (WcPod)
   DBuf<uint64_t> sd_pods;     // static records: the chunk's decoded pods (WcPod, k_static_dec)
   int static_dec = 1;         // k_static_dec where the chunk's pods decode (KSG_STATIC_DEC=0: k_static)
+  uint32_t static_run_mb = 16384;  // static records of a whole run in the persistent window loop (KSG_STATIC_RUN_MB; 0: off)
   uint64_t static_dec_chunks = 0;  // diagnostic: static chunks computed from decoded pods
   uint32_t wi_chunk = 0;      // ... pods per chunk of the last step, and whether records were used
   bool wi_rec = false;
@@ -5582,6 +5610,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
     HIPCHK(hipStreamCreateWithPriority(&I.sstream, hipStreamNonBlocking, least));
     if (const char* e = std::getenv("KSG_STATIC_SIDE")) I.static_side = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("KSG_STATIC_DEC")) I.static_dec = (int)std::strtol(e, nullptr, 10);
+    if (const char* e = std::getenv("KSG_STATIC_RUN_MB")) I.static_run_mb = (uint32_t)std::strtoul(e, nullptr, 10);
   }
   HIPCHK(hipEventCreate(&I.ev0));
   HIPCHK(hipEventCreate(&I.ev1));
@@ -6046,7 +6075,14 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   // of chunk c+2 free after the launch replaying chunk c-1's last window.
   const bool stat = I.batch_static;
   const bool side = stat && I.sstream && I.static_side;
-  const uint32_t nslots = side ? 3 : 2;
+  // the persistent window loop over static records: every record of the run
+  // computed before the launch (one chunk; the loop has no ring to roll), when
+  // they fit KSG_STATIC_RUN_MB (default 16 GiB of the 288 GB)
+  const bool persist_ok = !sharded && I.win_run_on && nwin > 0 && 1 + (uint64_t)KSG_BATCH * T <= I.n_cus;
+  const uint32_t count32 = (count + KSG_BATCH - 1) / KSG_BATCH * KSG_BATCH;
+  const bool stat_run = stat && !side && persist_ok && I.static_run_mb > 0 && !I.stat_chunk_cap &&
+                        (uint64_t)count32 * std::max<uint32_t>(I.N, 1) * sizeof(StaticRec) <= ((uint64_t)I.static_run_mb << 20);
+  const uint32_t nslots = stat_run ? 1 : side ? 3 : 2;
   uint32_t chunk = 0, nchunks = 0;
   const bool gstat = stat && I.gstat && sharded;  // node-sharded: records over every node
   const DevCluster CS = gstat ? I.cluster_static() : C;
@@ -6058,8 +6094,9 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     const size_t Nn = std::max<uint32_t>(SN, 1);
     const size_t budget = side ? ((size_t)32 << 20) : ((size_t)64 << 20);
     chunk = (uint32_t)std::max<size_t>(KSG_BATCH, (budget / (Nn * sizeof(StaticRec))) / KSG_BATCH * KSG_BATCH);
-    chunk = std::min<uint32_t>(chunk, (count + KSG_BATCH - 1) / KSG_BATCH * KSG_BATCH);
+    chunk = std::min<uint32_t>(chunk, count32);
     if (I.stat_chunk_cap) chunk = std::min<uint32_t>(chunk, I.stat_chunk_cap);  // tests: force ring roll-over
+    if (stat_run) chunk = count32;
     nchunks = (count + chunk - 1) / chunk;
     if (!I.stat.alloc((size_t)nslots * chunk * Nn, err) || !I.mpred.alloc(2 * (size_t)std::max<uint32_t>(count, 1), err))
       return false;
@@ -6121,7 +6158,8 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   if (sharded && !stat) return run_batches_split(I, A, first, count, T, err);
   // the persistent window loop: one launch for every window (its blocks all
   // resident: one per CU); not co-resident -> the launch-per-window loop below
-  if (!sharded && !stat && I.win_run_on && nwin > 0 && 1 + (uint64_t)KSG_BATCH * T <= I.n_cus) {
+  if (persist_ok && (!stat || stat_run)) {
+    if (stat_run && !issue_static(0, s)) return false;  // (every record of the run)
     // dedicated merge blocks (one per pod) when they fit beside the tile blocks
     const bool mb = I.win_mblocks && 1 + (uint64_t)KSG_BATCH * (T + 1) <= I.n_cus;
     if (!I.wsync.alloc(1, err) || !I.rsync.alloc(1, err)) return false;
@@ -6133,6 +6171,8 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     if (!wattr) {
       HIPCHK(hipFuncSetAttribute((const void*)k_window_run<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLDS)));
       HIPCHK(hipFuncSetAttribute((const void*)k_window_run<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLDS)));
+      HIPCHK(hipFuncSetAttribute((const void*)k_window_run<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLDS)));
+      HIPCHK(hipFuncSetAttribute((const void*)k_window_run<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLDS)));
       wattr = true;
     }
     HIPCHK(hipMemsetAsync(I.wsync.p, 0, sizeof(WinSync), s));
@@ -6162,10 +6202,16 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     const RunCtl RC{grid + I.run_need_extra, I.run_wait_us * 100u, 0, I.hverdict, I.run_spin};
     const bool sampled = I.sample_every && I.n_samples * 2 + 2 <= I.sev.size();
     if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
-    if (I.eval_mode == 1)
+    if (stat_run) {
+      if (I.eval_mode == 1)
+        hipLaunchKernelGGL((k_window_run<1, true>), dim3(grid), dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, AP, R, I.rsync.p, I.wsync.p, RC);
+      else
+        hipLaunchKernelGGL((k_window_run<0, true>), dim3(grid), dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, AP, R, I.rsync.p, I.wsync.p, RC);
+    } else if (I.eval_mode == 1) {
       hipLaunchKernelGGL(k_window_run<1>, dim3(grid), dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, AP, R, I.rsync.p, I.wsync.p, RC);
-    else
+    } else {
       hipLaunchKernelGGL(k_window_run<0>, dim3(grid), dim3(KSG_WIN_THREADS), sizeof(WinLDS), s, C, I.F, AP, R, I.rsync.p, I.wsync.p, RC);
+    }
     if (sampled) {
       HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
       I.n_samples++;

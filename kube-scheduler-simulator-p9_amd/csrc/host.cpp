@@ -17,6 +17,7 @@
 #include <cctype>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -1337,6 +1338,7 @@ struct Cluster {
   // Intern pod p's label space in place; new label keys widen the device's
   // existing-pod label columns (Engine::grow_table).
   bool grow_vocab(const Pod& p) {
+    ++bprog_gen;
     const size_t k0 = pkeys.names.size();
     intern_pod_labels(p);
     if (pkeys.names.size() == k0) return true;
@@ -1502,7 +1504,60 @@ struct Cluster {
     return true;
   }
 
+  // Compiled programs of bound pods for the preemption search (DefaultPreemption
+  // toggles candidate victims with them), cached by bound index: valid while
+  // bprog_gen holds (bumped by every encode, vocabulary growth, node change and
+  // event batch: bound indices, vocabulary ids and node columns are then stable)
+  // and refreshed like refresh_program when classes were added since.
+  struct BProg {
+    vector<uint8_t> blob;
+    uint32_t npc = 0, ntc = 0;
+    uint64_t gen = 0;  // bprog_gen + 1 when valid
+  };
+  vector<BProg> bprog_cache;
+  uint64_t bprog_gen = 0;
+  uint64_t node_gen = 0;  // node list / allocatable changes (alloc_cache)
+  const vector<uint8_t>* bound_prog(int32_t b) {
+    if (bprog_cache.size() < bound.size()) bprog_cache.resize(bound.size());
+    BProg& e = bprog_cache[(size_t)b];
+    if (e.gen == bprog_gen + 1) {
+      if (e.npc == pcls.size() && e.ntc == tcls.size()) return &e.blob;
+      bool stale = false;
+      for (size_t c = e.npc; c < pcls.size() && !stale; ++c) stale = pclass_matches(pcls[c], bound[b]);
+      for (size_t k = e.ntc; k < tcls.size() && !stale; ++k) stale = term_matches(tcls[k].term, bound[b]);
+      if (!stale) {
+        e.npc = (uint32_t)pcls.size();
+        e.ntc = (uint32_t)tcls.size();
+        return &e.blob;
+      }
+    }
+    PodMeta m;
+    e.blob.clear();
+    if (!compile(bound[b], 0, e.blob, m)) return nullptr;
+    e.npc = (uint32_t)pcls.size();
+    e.ntc = (uint32_t)tcls.size();
+    e.gen = bprog_gen + 1;
+    return &e.blob;
+  }
+  // allocatable per resource column and local node (Fit's Filter code rule),
+  // rebuilt when node_gen moves
+  vector<i64> alloc_cache;
+  uint64_t alloc_cache_gen = ~0ull;
+  const vector<i64>& node_allocs() {
+    if (alloc_cache_gen == node_gen && alloc_cache.size() == res.names.size() * (size_t)(hi - lo)) return alloc_cache;
+    const size_t R = res.names.size(), n = hi - lo;
+    alloc_cache.assign(R * n, 0);
+    for (size_t i = 0; i < n; ++i)
+      for (auto& kv : nodes[lo + i].alloc) {
+        const int32_t r = res.get(kv.first);
+        if (r >= 0) alloc_cache[(size_t)r * n + i] = r == 0 ? as_milli(kv.second) : as_value(kv.second);
+      }
+    alloc_cache_gen = node_gen;
+    return alloc_cache;
+  }
   bool encode_snapshot(NodeSoA& S, PodTableSoA& T) {
+    ++bprog_gen;
+    ++node_gen;
     // a new snapshot: the class registry restarts (the bound pods' terms register first)
     pcls.clear();
     tcls.clear();
@@ -2697,6 +2752,8 @@ struct Cluster {
     docs.emplace_back(new J(std::move(doc)));
     const J& d = *docs.back();
     nodes.clear();
+    ++node_gen;
+    ++bprog_gen;
     node_names = Dict();
     bound.clear();
     queue.clear();
@@ -3230,10 +3287,24 @@ struct Cluster {
     }
     return true;
   }
+  // Host wall time per phase of the DefaultPreemption dry runs (diagnostic:
+  // ksg_debug_preempt_times): [0] the pod's dry run + potential nodes, [1] candidate
+  // victims and their programs, [2] the victim search (toggles, dry runs), [3] searches.
+  double ptimes[4] = {0, 0, 0, 0};
   bool preempt(uint32_t q, const ksg_pod_summary& S) {
     if (nom.size() < queue.size()) nom.resize(queue.size());
     nom[q] = Nomination();
     if (S.status != 1 || q >= meta.size() || meta[q].prefilter_fail_pos >= 0 || !may_preempt(q)) return true;
+    double pt = now_us();
+    auto plap = [&](int k) {
+      const double u = now_us();
+      ptimes[k] += u - pt;
+      pt = u;
+    };
+    struct PCount {
+      double* c;
+      ~PCount() { *c += 1; }
+    } pcount{&ptimes[3]};
     const Pod& p = queue[q];
     const uint32_t n = hi - lo;
     PodOutputs o;
@@ -3247,15 +3318,34 @@ struct Cluster {
     };
     vector<int32_t> potential;
     vector<char> is_pot(n, 0);
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint32_t c = o.filter[i];
-      if (c == KSG_FILTER_PASS || c >= KSG_FILTER_NOT_EVALUATED || (c >> 24) >= (uint32_t)n_dev) continue;
-      string msg;
-      if (filter_status(q, code_pos(c), i, o, msg) == C_UNSCHED) {
-        potential.push_back((int32_t)i);
-        is_pot[i] = 1;
+    {  // nodesWherePreemptionMightHelp: the framework code of each node's failure
+      // (filter_status without its message; Fit's rule on the cached allocatable)
+      vector<i64> rq;
+      i64 nzc = 0, nzm = 0;
+      add_requests_const(p, rq, nzc, nzm);
+      const vector<i64>& al = node_allocs();
+      const uint32_t skip = skip_filter_mask(meta[q], o.summary);
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t c = o.filter[i];
+        if (c == KSG_FILTER_PASS || c >= KSG_FILTER_NOT_EVALUATED || (c >> 24) >= (uint32_t)n_dev) continue;
+        const int pos = code_pos(c);
+        if (pos < 0 || pos >= n_plugins || !has_filter(plugins[pos]) || filter_skipped(meta[q], skip, pos)) continue;
+        int fc;
+        if (plugins[pos] == P_FIT) {
+          fc = C_UNSCHED;
+          const uint32_t detail = code_detail(c);
+          for (size_t r = 0; r < res.names.size(); ++r)
+            if ((detail & (1u << (1 + r))) && rq[r] > al[r * n + i]) fc = C_UNRESOLVABLE;
+        } else {
+          fc = filter_fail_code(q, pos, i, code_detail(c));
+        }
+        if (fc == C_UNSCHED) {
+          potential.push_back((int32_t)i);
+          is_pot[i] = 1;
+        }
       }
     }
+    plap(0);
     if (potential.empty()) return true;
     vector<vector<Vic>> on(n);
     for (size_t b = 0; b < bound.size(); ++b) {
@@ -3271,14 +3361,16 @@ struct Cluster {
       if (g < 0 || g >= (int32_t)n || !is_pot[g]) continue;
       on[g].push_back({-1, (int32_t)j, queue[j].priority, queue[j].start_time, (uint64_t)bound.size() + j});
     }
-    // programs and table rows of every candidate victim (classes they bring: tables built)
-    std::map<int32_t, vector<uint8_t>> bprog;
+    // programs and table rows of every candidate victim (bound pods' programs from
+    // the context's cache: compiled once, not once per search)
+    std::unordered_map<int32_t, const vector<uint8_t>*> bprog;
     std::map<int32_t, int32_t> qrows;
     for (int32_t g : potential)
       for (auto& v : on[g]) {
         if (v.bound >= 0) {
-          PodMeta m;
-          if (!compile(bound[v.bound], 0, bprog[v.bound], m)) return false;
+          const vector<uint8_t>* bp = bound_prog(v.bound);
+          if (!bp) return false;
+          bprog[v.bound] = bp;
         } else {
           int32_t row = -1;
           if (tables_on()) {
@@ -3294,11 +3386,16 @@ struct Cluster {
     if (!sync_classes() || !refresh_program(q)) return false;
     for (auto& kv : qrows)
       if (!refresh_program((uint32_t)kv.first)) return false;
+    plap(1);
+    struct PLap {  // the search's time, whichever way it returns
+      std::function<void()> f;
+      ~PLap() { f(); }
+    } psearch{[&]() { plap(2); }};
     auto toggle = [&](const vector<Vic>& vs, int32_t g, int sign) {
       vector<const vector<uint8_t>*> pp;
       vector<int32_t> gn, rows;
       for (auto& v : vs) {
-        pp.push_back(v.bound >= 0 ? &bprog[v.bound] : &progs[v.qpod]);
+        pp.push_back(v.bound >= 0 ? bprog[v.bound] : &progs[v.qpod]);
         gn.push_back(g + (int32_t)lo);
         rows.push_back(v.bound >= 0 ? (tables_on() ? bound_row[v.bound] : -1) : qrows[v.qpod]);
       }
@@ -3341,7 +3438,7 @@ struct Cluster {
         vector<int32_t> gn, rows;
         for (auto& gv : all) {
           const Vic& v = gv.second;
-          pp.push_back(v.bound >= 0 ? &bprog[v.bound] : &progs[v.qpod]);
+          pp.push_back(v.bound >= 0 ? bprog[v.bound] : &progs[v.qpod]);
           gn.push_back(gv.first + (int32_t)lo);
           rows.push_back(v.bound >= 0 ? (tables_on() ? bound_row[v.bound] : -1) : qrows[v.qpod]);
         }
@@ -3737,6 +3834,8 @@ struct Cluster {
   }
 
   bool apply_events(const char* js, size_t len) {
+    ++bprog_gen;
+    ++node_gen;
     if (!compile_queue()) return false;
     try {
       docs.emplace_back(new J(json::parse(js, len)));
@@ -4638,6 +4737,16 @@ extern "C" int ksg_debug_cycle_times(ksg_ctx* ctx, double* out, int reset) {
   if (!ctx) return KSG_E_INVALID;
   if (out) std::memcpy(out, ctx->c.ctimes, sizeof(ctx->c.ctimes));
   if (reset) std::memset(ctx->c.ctimes, 0, sizeof(ctx->c.ctimes));
+  return KSG_OK;
+}
+
+// diagnostic (not in ksg.h): the preemption dry runs' host phases (Cluster::ptimes), 4
+// doubles; reset = 1 clears them after the read
+extern "C" int ksg_debug_preempt_times(ksg_ctx* ctx, double* out, int reset) {
+  KSG_LOCK(ctx);
+  if (!ctx) return KSG_E_INVALID;
+  if (out) std::memcpy(out, ctx->c.ptimes, sizeof(ctx->c.ptimes));
+  if (reset) std::memset(ctx->c.ptimes, 0, sizeof(ctx->c.ptimes));
   return KSG_OK;
 }
 

@@ -1734,7 +1734,10 @@ __device__ __forceinline__ bool run_indep(const ksg_prog* h, const ksg_prog* n) 
   return (h->tab_md & n->tab_rd) == 0 && (h->nd_md & n->nd_rd) == 0;
 }
 constexpr uint32_t kRunSpin = 1u << 22;  // polls (~1 us each with the load) before a block gives up
-constexpr int kRunSleep = 8;             // s_sleep between polls (x 64 cycles): every block polls every block
+#ifndef KSG_RUN_SLEEP
+#define KSG_RUN_SLEEP 8
+#endif
+constexpr int kRunSleep = KSG_RUN_SLEEP;  // s_sleep between polls (x 64 cycles): every block polls every block
 constexpr int kRunG1 = 2 + 4 * KCP_X + 2 * KSG_MAX_TSC;  // partial-record granules per block (max)
 constexpr int kRunG2 = 3;                                // key granules per block
 constexpr int kRunGS = 64;                               // granule stride per block (uint64)
@@ -1831,31 +1834,6 @@ __device__ bool run_wait_flag(const RunWait& W) {
   }
   __syncthreads();
   return *W.go != 0u;
-}
-// The block record's granule i (wave 0 lanes; every thread holds the record).
-template <int TS>
-__device__ __forceinline__ uint32_t run_g1_value(const ChainRec& r, int i, uint32_t xmask, int ns) {
-  uint32_t v = 0;
-  if (i == 0) v = (uint32_t)r.feas | ((uint32_t)r.ign << 16);
-  if (i == 1) v = (uint32_t)r.st;
-  int j = 2;
-#pragma unroll
-  for (int x = 0; x < KCP_X; ++x)
-    if ((xmask >> x) & 1u) {
-      if (i == j) v = (uint32_t)(uint64_t)r.mx[x];
-      if (i == j + 1) v = (uint32_t)((uint64_t)r.mx[x] >> 32);
-      if (i == j + 2) v = (uint32_t)(uint64_t)r.mn[x];
-      if (i == j + 3) v = (uint32_t)((uint64_t)r.mn[x] >> 32);
-      j += 4;
-    }
-#pragma unroll
-  for (int c = 0; c < TS; ++c)
-    if (c < ns) {
-      if (i == j) v = (uint32_t)r.reg[c];
-      if (i == j + 1) v = (uint32_t)(r.reg[c] >> 32);
-      j += 2;
-    }
-  return v;
 }
 __device__ __forceinline__ int run_g1_count(uint32_t xmask, int ns) { return 2 + 4 * __popc(xmask) + 2 * ns; }
 __device__ __forceinline__ bool gtag(uint64_t g, uint32_t tag) { return (uint32_t)(g >> 32) == tag; }
@@ -1980,8 +1958,31 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     if (eo.abort) return;
     wait_for = 0;
     const int ns = h->n_tsc_score;
-    const int ng1 = run_g1_count(xmask, ns);
-    if (threadIdx.x < (uint32_t)ng1) st_sc1(G1 + (size_t)b * kRunGS + threadIdx.x, gran(tag, run_g1_value<TS>(eo.rec, (int)threadIdx.x, xmask, ns)));
+    // the partial record's granules, stored by one lane field after field (a
+    // per-lane pick of its granule was a long select chain on every lane)
+    if (threadIdx.x == 0) {
+      uint64_t* g = G1 + (size_t)b * kRunGS;
+      const ChainRec& rr = eo.rec;
+      st_sc1(g, gran(tag, (uint32_t)rr.feas | ((uint32_t)rr.ign << 16)));
+      st_sc1(g + 1, gran(tag, (uint32_t)rr.st));
+      int j = 2;
+#pragma unroll
+      for (int x = 0; x < KCP_X; ++x)
+        if ((xmask >> x) & 1u) {
+          st_sc1(g + j, gran(tag, (uint32_t)(uint64_t)rr.mx[x]));
+          st_sc1(g + j + 1, gran(tag, (uint32_t)((uint64_t)rr.mx[x] >> 32)));
+          st_sc1(g + j + 2, gran(tag, (uint32_t)(uint64_t)rr.mn[x]));
+          st_sc1(g + j + 3, gran(tag, (uint32_t)((uint64_t)rr.mn[x] >> 32)));
+          j += 4;
+        }
+#pragma unroll
+      for (int c = 0; c < TS; ++c)
+        if (c < ns) {
+          st_sc1(g + j, gran(tag, (uint32_t)rr.reg[c]));
+          st_sc1(g + j + 1, gran(tag, (uint32_t)(rr.reg[c] >> 32)));
+          j += 2;
+        }
+    }
     RS(30);
     // diagnostic: the latest block's partial store (absolute clock, per pod parity)
     if (rst && threadIdx.x == 0) atomicMax((unsigned long long*)&rst[52 + (k & 1)], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -2057,9 +2058,11 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     }
     RS(47);
     fold_key<BT>(r, L.rec);
-    if (threadIdx.x < (uint32_t)kRunG2) {
-      const uint32_t v = threadIdx.x == 0 ? (uint32_t)r.key : threadIdx.x == 1 ? (uint32_t)(r.key >> 32) : (uint32_t)r.st;
-      st_sc1(G2 + (size_t)b * kRunGS + threadIdx.x, gran(tag, v));
+    if (threadIdx.x == 0) {
+      uint64_t* g = G2 + (size_t)b * kRunGS;
+      st_sc1(g, gran(tag, (uint32_t)r.key));
+      st_sc1(g + 1, gran(tag, (uint32_t)(r.key >> 32)));
+      st_sc1(g + 2, gran(tag, (uint32_t)r.st));
     }
     RS(33);
     if (rst && threadIdx.x == 0) atomicMax((unsigned long long*)&rst[54 + (k & 1)], (unsigned long long)__builtin_amdgcn_s_memrealtime());

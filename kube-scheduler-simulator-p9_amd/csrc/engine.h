@@ -155,6 +155,14 @@ class Engine {
   bool toggle_stage(const std::vector<const std::vector<uint8_t>*>& progs, const std::vector<int32_t>& gnode,
                     const std::vector<int32_t>& rows, std::string& err);
   bool toggle_staged(const std::vector<uint32_t>& idx, int sign, std::string& err);
+  // The same staging by reference, without a program upload per search: the bound
+  // pods' programs live on the device in the victim store (entry b = bound pod b,
+  // uploaded by victim_store when the host's cache moves); entry i of the staging
+  // is bound pod ref[i] (>= 0) or queue pod -1 - ref[i] (its program in the
+  // queue's buffer; queue_csi[q]: it has CSI volumes).
+  bool victim_store(const std::vector<const std::vector<uint8_t>*>& progs, std::string& err);
+  bool toggle_stage_refs(const std::vector<int64_t>& ref, const std::vector<int32_t>& gnode,
+                         const std::vector<int32_t>& rows, const std::vector<uint8_t>& queue_csi, std::string& err);
   // Filter codes of program q against the current device state (its whole cycle
   // re-run without commit; kept outputs and the pod's summary are left as they
   // were): global node gnode's code, or every node's when gnode is -1.
@@ -234,7 +242,8 @@ class Engine {
     size_t off_fail_pos = 0, off_fail_code = 0, off_fail_msg = 0, off_raw = 0, off_norm = 0, bytes = 0;
   };
   void view_layout(ViewLayout& lay) const;
-  bool view(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err);
+  // wait = false: only queued on the engine stream (the block is complete after the next sync)
+  bool view(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err, bool wait = true);
   // pinned host blocks for views (process-wide pool: a view outlives its context)
   static uint8_t* pinned_get(size_t bytes, size_t& cap);
   static void pinned_put(uint8_t* p, size_t cap);

@@ -30,6 +30,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 #include <utility>
@@ -1745,15 +1746,15 @@ __global__ void k_assume(DevCluster C, const uint8_t* __restrict__ prog, int32_t
 // touched by one thread only; the class tables and claim counts take atomics.
 // (Entries with CSI volumes, whose per-volume node lists are shared across
 // nodes, never come here: the host toggles those one launch per pod.)
-__global__ __launch_bounds__(256) void k_toggle_groups(DevCluster C, const uint8_t* __restrict__ blob,
-                                                       const uint64_t* __restrict__ off, const int32_t* __restrict__ gnode,
+__global__ __launch_bounds__(256) void k_toggle_groups(DevCluster C, const uint64_t* __restrict__ addr,
+                                                       const int32_t* __restrict__ gnode,
                                                        int32_t* rows, const uint32_t* __restrict__ idx,
                                                        const uint32_t* __restrict__ gs, uint32_t ngroups, int sign) {
   const uint32_t g = blockIdx.x * 256 + threadIdx.x;
   if (g >= ngroups) return;
   for (uint32_t j = gs[g]; j < gs[g + 1]; ++j) {
     const uint32_t e = idx[j];
-    const ProgView V = view(blob + off[e]);
+    const ProgView V = view(reinterpret_cast<const uint8_t*>(addr[e]));
     const uint32_t n = (uint32_t)gnode[e] - C.goff;
     if (gnode[e] < 0 || (uint32_t)gnode[e] < C.goff || n >= C.N) continue;
     assume_pod(C, V, n, sign, false, nullptr);
@@ -2263,7 +2264,9 @@ __global__ __launch_bounds__(kBlock) void k_fs_static(DevCluster C, DevProfile F
 #define KSG_BATCH 32
 #define KSG_CAND 64        // candidates per pod: >= 2*KSG_BATCH (see above)
 #define KSG_TOPK 64
-#define KSG_WIN_THREADS 1024
+#ifndef KSG_WIN_THREADS
+#define KSG_WIN_THREADS 1024  // (a build-time knob for A/B builds: 512 lifts the 128-VGPR cap)
+#endif
 #define KSG_TILE KSG_WIN_THREADS  // nodes per eval block
 #define KSG_STASH_NPT 8    // eval tiles of up to this many nodes per thread hold their outputs in LDS
 #ifndef KSG_STAGE
@@ -5316,15 +5319,20 @@ struct Engine::Impl {
   size_t apstage_cap = 0;
   hipEvent_t apstage_ev = nullptr;
   DBuf<uint8_t> apdev;
-  // toggle_stage / toggle_staged: the staged candidate victims
+  // toggle_stage / toggle_staged: the staged candidate victims (tg_addr: each
+  // entry's program, a device address in tgprog, the victim store or the queue's
+  // program buffer)
   DBuf<uint8_t> tgprog;
-  DBuf<uint64_t> tgoff;
+  DBuf<uint64_t> tgaddr;
   DBuf<int32_t> tgnode, tgrow;
   DBuf<uint32_t> tgidx;
   std::vector<int32_t> tg_gnode;  // host copies: grouping, CSI entries
   std::vector<char> tg_csi;
-  std::vector<uint64_t> tg_off;
+  std::vector<uint64_t> tg_addr;
   uint32_t tg_n = 0;
+  DBuf<uint8_t> vstore;  // victim_store: bound pods' programs (entry b at vstore_off[b])
+  std::vector<uint64_t> vstore_off;
+  std::vector<char> vstore_csi;
   DBuf<ksg_pod_summary> drysum;  // DefaultPreemption dry run: the preemptor's summary, restored after each probe
   // scratch
   DBuf<int32_t> cnt, hist_f, hist_s, ipa_aff, ipa_anti, ipa_exist, pts_min, pts_dom;
@@ -5405,6 +5413,7 @@ struct Engine::Impl {
   uint32_t run_spin = kRunSpin;  // polls before a persistent block gives up (KSG_RUN_SPIN: tests force an abort)
   uint64_t run_fallbacks = 0;    // segments that ran on the two-launch chain (not co-resident)
   bool lost = false;             // an aborted persistent launch left the device state half-updated
+  std::vector<std::shared_ptr<const void>> hold;  // host sources of queued uploads (add_classes), until the next sync
   bool unwaited = false;         // a state-changing launch was queued without a wait (Reserve's k_assume):
                                  // a failing synchronisation then leaves host mirror and device apart (lost)
   DBuf<WinSync> wsync;           // k_window_run's counters (zeroed per launch)
@@ -5542,7 +5551,10 @@ static bool stream_sync(Engine::Impl& I, hipStream_t s, std::string& err) {
     if (I.unwaited) I.lost = true;
     return false;
   }
-  if (s == I.stream) I.unwaited = false;
+  if (s == I.stream) {
+    I.unwaited = false;
+    I.hold.clear();  // (every queued copy from them has completed)
+  }
   return true;
 }
 
@@ -6708,36 +6720,88 @@ bool Engine::toggle_pods(const std::vector<const std::vector<uint8_t>*>& progs, 
   return true;
 }
 
+static bool stage_entries(Engine::Impl& I, const std::vector<int32_t>& gnode, const std::vector<int32_t>& rows,
+                          std::string& err);
 bool Engine::toggle_stage(const std::vector<const std::vector<uint8_t>*>& progs, const std::vector<int32_t>& gnode,
                           const std::vector<int32_t>& rows, std::string& err) {
   Impl& I = *p_;
   if (!tables_ready(I, err)) return false;
   const size_t n = progs.size();
   if (gnode.size() != n || rows.size() != n) { err = "toggle_stage: sizes"; return false; }
-  I.tg_off.assign(n, 0);
+  std::vector<uint64_t> off(n);
   I.tg_csi.assign(n, 0);
   size_t bytes = 0;
   for (size_t i = 0; i < n; ++i) {
     if (!progs[i] || progs[i]->size() < sizeof(ksg_prog)) { err = "toggle_stage: program"; return false; }
-    I.tg_off[i] = bytes;
+    off[i] = bytes;
     bytes = (bytes + progs[i]->size() + 255) & ~(size_t)255;
     I.tg_csi[i] = reinterpret_cast<const ksg_prog*>(progs[i]->data())->n_csi > 0 ? 1 : 0;
   }
   std::vector<uint8_t> blob(std::max<size_t>(bytes, 1));
-  for (size_t i = 0; i < n; ++i) std::memcpy(blob.data() + I.tg_off[i], progs[i]->data(), progs[i]->size());
-  if (!I.tgprog.alloc(blob.size(), err) || !I.tgoff.alloc(n, err) || !I.tgnode.alloc(n, err) || !I.tgrow.alloc(n, err))
-    return false;
+  for (size_t i = 0; i < n; ++i) std::memcpy(blob.data() + off[i], progs[i]->data(), progs[i]->size());
+  if (!I.tgprog.alloc(blob.size(), err)) return false;
+  I.tg_addr.resize(n);
+  for (size_t i = 0; i < n; ++i) I.tg_addr[i] = reinterpret_cast<uint64_t>(I.tgprog.p) + off[i];
+  HIPCHK(hipMemcpyAsync(I.tgprog.p, blob.data(), blob.size(), hipMemcpyHostToDevice, I.stream));
+  return stage_entries(I, gnode, rows, err);  // (syncs: the host blob goes out of scope)
+}
+// the staged entries' addresses, nodes and rows (I.tg_addr / tg_csi set by the caller)
+static bool stage_entries(Engine::Impl& I, const std::vector<int32_t>& gnode, const std::vector<int32_t>& rows,
+                          std::string& err) {
+  const size_t n = gnode.size();
+  if (!I.tgaddr.alloc(n, err) || !I.tgnode.alloc(n, err) || !I.tgrow.alloc(n, err)) return false;
   hipStream_t s = I.stream;
-  HIPCHK(hipMemcpyAsync(I.tgprog.p, blob.data(), blob.size(), hipMemcpyHostToDevice, s));
   if (n) {
-    HIPCHK(hipMemcpyAsync(I.tgoff.p, I.tg_off.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(I.tgaddr.p, I.tg_addr.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(I.tgnode.p, gnode.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(I.tgrow.p, rows.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
   }
-  if (!stream_sync(I, s, err)) return false;  // (the host blob goes out of scope)
+  if (!stream_sync(I, s, err)) return false;
   I.tg_gnode = gnode;
   I.tg_n = (uint32_t)n;
   return true;
+}
+bool Engine::victim_store(const std::vector<const std::vector<uint8_t>*>& progs, std::string& err) {
+  Impl& I = *p_;
+  if (!tables_ready(I, err)) return false;
+  const size_t n = progs.size();
+  I.vstore_off.assign(n, 0);
+  I.vstore_csi.assign(n, 0);
+  size_t bytes = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (!progs[i] || progs[i]->size() < sizeof(ksg_prog)) { err = "victim_store: program"; return false; }
+    I.vstore_off[i] = bytes;
+    bytes = (bytes + progs[i]->size() + 15) & ~(size_t)15;
+    I.vstore_csi[i] = reinterpret_cast<const ksg_prog*>(progs[i]->data())->n_csi > 0 ? 1 : 0;
+  }
+  std::vector<uint8_t> blob(std::max<size_t>(bytes, 1));
+  for (size_t i = 0; i < n; ++i) std::memcpy(blob.data() + I.vstore_off[i], progs[i]->data(), progs[i]->size());
+  if (!I.vstore.alloc(blob.size(), err)) return false;
+  HIPCHK(hipMemcpyAsync(I.vstore.p, blob.data(), blob.size(), hipMemcpyHostToDevice, I.stream));
+  return stream_sync(I, I.stream, err);
+}
+bool Engine::toggle_stage_refs(const std::vector<int64_t>& ref, const std::vector<int32_t>& gnode,
+                               const std::vector<int32_t>& rows, const std::vector<uint8_t>& queue_csi, std::string& err) {
+  Impl& I = *p_;
+  if (!tables_ready(I, err)) return false;
+  const size_t n = ref.size();
+  if (gnode.size() != n || rows.size() != n) { err = "toggle_stage_refs: sizes"; return false; }
+  I.tg_addr.resize(n);
+  I.tg_csi.assign(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t r = ref[i];
+    if (r >= 0) {
+      if ((size_t)r >= I.vstore_off.size()) { err = "toggle_stage_refs: bound pod outside the victim store"; return false; }
+      I.tg_addr[i] = reinterpret_cast<uint64_t>(I.vstore.p) + I.vstore_off[(size_t)r];
+      I.tg_csi[i] = I.vstore_csi[(size_t)r];
+    } else {
+      const size_t q = (size_t)(-1 - r);
+      if (q >= I.prog_off.size() || q >= queue_csi.size()) { err = "toggle_stage_refs: queue pod"; return false; }
+      I.tg_addr[i] = reinterpret_cast<uint64_t>(I.progs.p) + I.prog_off[q];
+      I.tg_csi[i] = queue_csi[q];
+    }
+  }
+  return stage_entries(I, gnode, rows, err);
 }
 bool Engine::toggle_staged(const std::vector<uint32_t>& idx, int sign, std::string& err) {
   Impl& I = *p_;
@@ -6746,12 +6810,19 @@ bool Engine::toggle_staged(const std::vector<uint32_t>& idx, int sign, std::stri
   std::vector<uint32_t> sorted;  // grouped by node (stable: a node's entries keep their order)
   sorted.reserve(idx.size());
   std::vector<uint32_t> serial;  // entries with CSI volumes: one launch each
+  bool in_order = true;  // (the search's lists come node by node: no sort)
   for (uint32_t e : idx) {
     if (e >= I.tg_n) { err = "toggle_staged: index"; return false; }
-    (I.tg_csi[e] ? serial : sorted).push_back(e);
+    if (I.tg_csi[e]) {
+      serial.push_back(e);
+      continue;
+    }
+    in_order &= sorted.empty() || I.tg_gnode[sorted.back()] <= I.tg_gnode[e];
+    sorted.push_back(e);
   }
-  std::stable_sort(sorted.begin(), sorted.end(),
-                   [&](uint32_t a, uint32_t b) { return I.tg_gnode[a] < I.tg_gnode[b]; });
+  if (!in_order)
+    std::stable_sort(sorted.begin(), sorted.end(),
+                     [&](uint32_t a, uint32_t b) { return I.tg_gnode[a] < I.tg_gnode[b]; });
   std::vector<uint32_t> gs;
   for (size_t j = 0; j < sorted.size(); ++j)
     if (j == 0 || I.tg_gnode[sorted[j]] != I.tg_gnode[sorted[j - 1]]) gs.push_back((uint32_t)j);
@@ -6764,11 +6835,11 @@ bool Engine::toggle_staged(const std::vector<uint32_t>& idx, int sign, std::stri
   HIPCHK(hipMemcpyAsync(I.tgidx.p, up.data(), up.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s));
   DevCluster C = I.cluster();
   if (ng)
-    hipLaunchKernelGGL(k_toggle_groups, dim3((ng + 255) / 256), dim3(256), 0, s, C, I.tgprog.p, I.tgoff.p, I.tgnode.p,
-                       I.tgrow.p, I.tgidx.p, I.tgidx.p + sorted.size(), ng, sign);
+    hipLaunchKernelGGL(k_toggle_groups, dim3((ng + 255) / 256), dim3(256), 0, s, C, I.tgaddr.p, I.tgnode.p, I.tgrow.p,
+                       I.tgidx.p, I.tgidx.p + sorted.size(), ng, sign);
   for (uint32_t e : serial)
-    hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, s, C, I.tgprog.p + I.tg_off[e], I.tg_gnode[e], sign, 2,
-                       I.tgrow.p + e);
+    hipLaunchKernelGGL(k_assume, dim3(1), dim3(64), 0, s, C, reinterpret_cast<const uint8_t*>(I.tg_addr[e]), I.tg_gnode[e],
+                       sign, 2, I.tgrow.p + e);
   HIPCHK(hipGetLastError());
   if (!stream_sync(I, s, err)) return false;  // (the host index list goes out of scope)
   return true;
@@ -7010,29 +7081,38 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
   const uint32_t pc0 = I.npc, tc0 = I.ntc, npc = (uint32_t)u.pc.size(), ntc = (uint32_t)u.tc_slot.size();
   if (!npc && !ntc) return true;
   const size_t Nn = std::max<uint32_t>(I.N, 1), NUn = std::max<uint32_t>(I.NU, 1);
+  // (unsharded, the upload is not waited for: its host sources are held until the
+  // engine stream's next sync, and a late failure marks the context lost)
+  auto held = [&](auto v) {
+    auto p = std::make_shared<decltype(v)>(std::move(v));
+    I.hold.push_back(p);
+    return p;
+  };
   if (npc) {  // definitions, rebased onto the device pools
-    std::vector<ksg_pclass> pc = u.pc;
-    std::vector<ksg_cterm> ct = u.ct;
-    std::vector<ksg_req> rq = u.creq;
-    for (auto& x : pc) x.term_off += (int32_t)I.nct;
-    for (auto& x : ct) {
+    auto pc = held(u.pc);
+    auto ct = held(u.ct);
+    auto rq = held(u.creq);
+    auto cv = held(u.cval);
+    for (auto& x : *pc) x.term_off += (int32_t)I.nct;
+    for (auto& x : *ct) {
       x.sel.req_off += (int32_t)I.ncreq;
       x.ns_off += (int32_t)I.ncval;
     }
-    for (auto& x : rq) x.val_off += (int32_t)I.ncval;
-    if (!dev_append(I.pcls_d, pc0, pc, s, err) || !dev_append(I.cterm_d, I.nct, ct, s, err) ||
-        !dev_append(I.creq_d, I.ncreq, rq, s, err) || !dev_append(I.cval_d, I.ncval, u.cval, s, err) ||
+    for (auto& x : *rq) x.val_off += (int32_t)I.ncval;
+    if (!dev_append(I.pcls_d, pc0, *pc, s, err) || !dev_append(I.cterm_d, I.nct, *ct, s, err) ||
+        !dev_append(I.creq_d, I.ncreq, *rq, s, err) || !dev_append(I.cval_d, I.ncval, *cv, s, err) ||
         !dev_zero_tail(I.pc_cnt, (size_t)pc0 * Nn, (size_t)npc * Nn, s, err) ||
         !dev_zero_tail(I.pc_dom, (size_t)pc0 * NUn, (size_t)npc * NUn, s, err) ||
         !dev_zero_tail(I.pc_tot, (size_t)pc0 * KSG_MAX_TOPO, (size_t)npc * KSG_MAX_TOPO, s, err))
       return false;
-    I.nct += (uint32_t)ct.size();
-    I.ncreq += (uint32_t)rq.size();
-    I.ncval += (uint32_t)u.cval.size();
+    I.nct += (uint32_t)ct->size();
+    I.ncreq += (uint32_t)rq->size();
+    I.ncval += (uint32_t)cv->size();
     I.npc += npc;
   }
   if (ntc) {  // per term class: one value per (key, value) pair, or per node for one-node keys
-    const std::vector<uint32_t>& off = u.tc_off;
+    const std::vector<uint32_t>& off = *held(u.tc_off);
+    const std::vector<int32_t>& tslot = *held(u.tc_slot);
     if (off.size() != ntc) { err = "term classes without offsets"; return false; }
     uint32_t end = I.tc_used;
     for (uint32_t i = 0; i < ntc; ++i) {
@@ -7044,7 +7124,7 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
     }
     const uint32_t add = end - I.tc_used;
     if (!dev_zero_tail(I.tc_val, I.tc_used, add, s, err) || !dev_append(I.tc_off_d, tc0, off, s, err) ||
-        !dev_append(I.tc_slot_d, tc0, u.tc_slot, s, err) || !dev_zero_tail(I.tc_tot, tc0, ntc, s, err))
+        !dev_append(I.tc_slot_d, tc0, tslot, s, err) || !dev_zero_tail(I.tc_tot, tc0, ntc, s, err))
       return false;
     I.tc_used += add;
     I.tc_off_h.insert(I.tc_off_h.end(), off.begin(), off.end());
@@ -7059,7 +7139,8 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
   if (npc) I.red_pc0 = std::min(I.red_pc0, pc0);
   if (ntc) I.red_tc0 = std::min(I.red_tc0, tc0);
   if (!reduce_tables(I, err)) return false;
-  if (!stream_sync(I, s, err)) return false;
+  if (I.shards > 1) return stream_sync(I, s, err);
+  I.unwaited = true;
   return true;
 }
 
@@ -7147,7 +7228,7 @@ void Engine::view_layout(ViewLayout& lay) const {
   lay.off_norm = lay.off_raw + al256(4 * N) * lay.n_raw;  // (the widest layout: every row 4 bytes)
   lay.bytes = lay.off_norm + al256(4 * N) * lay.n_norm;
 }
-bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err) {
+bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err, bool wait) {
   Impl& I = *p_;
   if (!(I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n)) { err = "outputs not kept for this pod"; return false; }
   if (lay.N != I.N || lay.n_raw != (uint32_t)I.F.n) { err = "view layout of another snapshot"; return false; }
@@ -7195,6 +7276,7 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
                        hdev ? hdev : I.vblk.p, I.vdone.p);
   HIPCHK(hipGetLastError());
   if (!hdev) HIPCHK(hipMemcpyAsync(host, I.vblk.p, lay.bytes, hipMemcpyDeviceToHost, s));  // (direct: k_view wrote it all)
+  if (!wait) return true;  // (queued behind the cycle's run: the caller's next sync completes it)
   if (!stream_sync(I, s, err)) return false;
   return true;
 }

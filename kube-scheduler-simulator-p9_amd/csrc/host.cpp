@@ -1555,6 +1555,54 @@ struct Cluster {
     alloc_cache_gen = node_gen;
     return alloc_cache;
   }
+  // bound pods grouped by local node (bcsr_idx[boff[i] .. boff[i + 1]), load order),
+  // rebuilt when bprog_gen moves
+  vector<uint32_t> bcsr_off;
+  vector<int32_t> bcsr_idx;
+  uint64_t bcsr_gen = ~0ull;
+  const vector<uint32_t>& bound_by_node() {
+    const uint32_t n = hi - lo;
+    if (bcsr_gen == bprog_gen && bcsr_off.size() == (size_t)n + 1 && bcsr_idx.size() <= bound.size()) return bcsr_off;
+    vector<int32_t> at(bound.size(), -1);
+    bcsr_off.assign((size_t)n + 1, 0);
+    for (size_t b = 0; b < bound.size(); ++b) {
+      const int32_t g = node_names.get(bound[b].node);
+      if (g < (int32_t)lo || g >= (int32_t)hi) continue;
+      at[b] = g - (int32_t)lo;
+      ++bcsr_off[at[b] + 1];
+    }
+    for (uint32_t i = 0; i < n; ++i) bcsr_off[i + 1] += bcsr_off[i];
+    bcsr_idx.assign(bcsr_off[n], 0);
+    vector<uint32_t> fill(bcsr_off.begin(), bcsr_off.end() - 1);
+    for (size_t b = 0; b < bound.size(); ++b)
+      if (at[b] >= 0) bcsr_idx[fill[at[b]]++] = (int32_t)b;
+    bcsr_gen = bprog_gen;
+    return bcsr_off;
+  }
+  // The device-resident victim store (Engine::victim_store): every bound pod's
+  // program, current while bprog_gen and the class registry hold.
+  // bound victims that make a search upload the store (KSG_VICTIM_STORE_MIN: tests force it)
+  size_t victim_store_min = std::getenv("KSG_VICTIM_STORE_MIN") ? std::strtoull(std::getenv("KSG_VICTIM_STORE_MIN"), nullptr, 10) : 2048;
+  uint64_t vstore_gen = ~0ull;
+  size_t vstore_n = 0, vstore_npc = 0, vstore_ntc = 0;
+  const void* vstore_eng = nullptr;
+  bool victim_store_current() const {
+    return vstore_eng == eng.get() && vstore_gen == bprog_gen && vstore_n == bound.size() && vstore_npc == pcls.size() &&
+           vstore_ntc == tcls.size();
+  }
+  bool ensure_victim_store() {
+    if (victim_store_current()) return true;
+    vector<const vector<uint8_t>*> pp(bound.size());
+    for (size_t b = 0; b < bound.size(); ++b)
+      if (!(pp[b] = bound_prog((int32_t)b))) return false;
+    if (!eng->victim_store(pp, err)) return false;
+    vstore_eng = eng.get();
+    vstore_gen = bprog_gen;
+    vstore_n = bound.size();
+    vstore_npc = pcls.size();
+    vstore_ntc = tcls.size();
+    return true;
+  }
   bool encode_snapshot(NodeSoA& S, PodTableSoA& T) {
     ++bprog_gen;
     ++node_gen;
@@ -3121,6 +3169,35 @@ struct Cluster {
   // [3] program append (+ classes), [4] launch, [5] summary wait, [6] PostFilter,
   // [7] cycles; microseconds summed.
   double ctimes[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // The cycle view of the last ksg_cycle(commit = 0), filled by a k_view queued
+  // behind the cycle's own run (the cycle's one sync completes it), so that the
+  // plugin's ksg_cycle_view_acquire for that pod needs no launch and no sync.
+  // Valid while out_gen is unchanged (any later state-changing call drops it).
+  struct PreView {
+    uint8_t* block = nullptr;
+    size_t cap = 0;
+    int64_t q = -1;
+    uint64_t gen = 0;
+    ksg::Engine::ViewLayout lay;
+    void drop() {
+      if (block) ksg::Engine::pinned_put(block, cap);
+      block = nullptr;
+      cap = 0;
+      q = -1;
+    }
+    ~PreView() { drop(); }
+  } pview;
+  bool view_prefetch = !(std::getenv("KSG_VIEW_PREFETCH") && std::strtol(std::getenv("KSG_VIEW_PREFETCH"), nullptr, 10) == 0);
+  bool prefetch_view(uint32_t q) {
+    pview.drop();
+    eng->view_layout(pview.lay);
+    pview.block = ksg::Engine::pinned_get(pview.lay.bytes, pview.cap);
+    if (!pview.block) return true;  // (no pinned memory: acquire builds it)
+    if (!eng->view(q, view_cfg(), pview.lay, pview.block, err, false)) return false;
+    pview.q = q;
+    pview.gen = out_gen;
+    return true;
+  }
   static double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
   }
@@ -3178,6 +3255,7 @@ struct Cluster {
     if (commit && !room_for(q)) return false;
     // (the summary's copy waits for the run; sync then only checks the run's state)
     if (!eng->keep_outputs(q, 1, err) || !eng->run_queue(q, 1, commit, err)) return false;
+    if (!commit && view_prefetch && !prefetch_view(q)) return false;
     lap(4);
     if (!eng->summaries(q, 1, &out, err) || !eng->sync(err)) return false;
     lap(5);
@@ -3347,45 +3425,65 @@ struct Cluster {
     }
     plap(0);
     if (potential.empty()) return true;
-    vector<vector<Vic>> on(n);
-    for (size_t b = 0; b < bound.size(); ++b) {
-      const int32_t g = node_names.get(bound[b].node);
-      if (g < 0 || !is_pot[g] || bound[b].priority >= p.priority) continue;
-      on[g].push_back({(int32_t)b, -1, bound[b].priority, bound[b].start_time, (uint64_t)b});
-    }
+    // candidate victims per potential node k (flat: vic[voff[k] .. voff[k + 1])):
+    // its lower-priority bound pods in load order, then its assumed queue pods
+    const vector<uint32_t>& boff = bound_by_node();
+    vector<std::pair<int32_t, Vic>> qvic;  // queue pods placed on potential nodes, by node
     vector<ksg_pod_summary> sum(progs.size());
     if (!sum.empty() && !eng->summaries(0, (uint32_t)sum.size(), sum.data(), err)) return false;
     for (uint32_t j = 0; j < queue.size() && j < progs.size(); ++j) {
       if (j == q || queue[j].priority >= p.priority) continue;
       const int32_t g = placement(j, &sum[j]);
       if (g < 0 || g >= (int32_t)n || !is_pot[g]) continue;
-      on[g].push_back({-1, (int32_t)j, queue[j].priority, queue[j].start_time, (uint64_t)bound.size() + j});
+      qvic.push_back({g, Vic{-1, (int32_t)j, queue[j].priority, queue[j].start_time, (uint64_t)bound.size() + j}});
     }
-    // programs and table rows of every candidate victim (bound pods' programs from
-    // the context's cache: compiled once, not once per search)
+    std::stable_sort(qvic.begin(), qvic.end(), [](const std::pair<int32_t, Vic>& a, const std::pair<int32_t, Vic>& b) {
+      return a.first < b.first;
+    });
+    vector<Vic> vic;
+    vector<uint32_t> voff(potential.size() + 1, 0);
+    size_t n_bound_vic = 0;
+    for (size_t k = 0, qi = 0; k < potential.size(); ++k) {
+      const int32_t g = potential[k];
+      voff[k] = (uint32_t)vic.size();
+      for (uint32_t e = boff[g]; e < boff[g + 1]; ++e) {
+        const int32_t b = bcsr_idx[e];
+        if (bound[b].priority >= p.priority) continue;
+        vic.push_back({b, -1, bound[b].priority, bound[b].start_time, (uint64_t)b});
+      }
+      n_bound_vic += vic.size() - voff[k];
+      while (qi < qvic.size() && qvic[qi].first < g) ++qi;
+      for (; qi < qvic.size() && qvic[qi].first == g; ++qi) vic.push_back(qvic[qi].second);
+    }
+    voff[potential.size()] = (uint32_t)vic.size();
+    // bound victims' programs: the device-resident victim store (every bound pod,
+    // uploaded once per cache generation) once the search is large or the store is
+    // current; small searches stage copies of the victims' programs
+    const bool by_ref = preempt_batched(p, S) && (victim_store_current() || n_bound_vic >= victim_store_min);
     std::unordered_map<int32_t, const vector<uint8_t>*> bprog;
     std::map<int32_t, int32_t> qrows;
-    for (int32_t g : potential)
-      for (auto& v : on[g]) {
-        if (v.bound >= 0) {
-          const vector<uint8_t>* bp = bound_prog(v.bound);
-          if (!bp) return false;
-          bprog[v.bound] = bp;
-        } else {
-          int32_t row = -1;
-          if (tables_on()) {
-            if (assumed_in[v.qpod] == epoch) {
-              if (!eng->pod_row((uint32_t)v.qpod, row, err)) return false;
-            } else if ((size_t)v.qpod < qrow.size()) {
-              row = qrow[v.qpod];
-            }
+    for (const Vic& v : vic) {
+      if (v.bound >= 0) {
+        if (by_ref) continue;
+        const vector<uint8_t>* bp = bound_prog(v.bound);
+        if (!bp) return false;
+        bprog[v.bound] = bp;
+      } else {
+        int32_t row = -1;
+        if (tables_on()) {
+          if (assumed_in[v.qpod] == epoch) {
+            if (!eng->pod_row((uint32_t)v.qpod, row, err)) return false;
+          } else if ((size_t)v.qpod < qrow.size()) {
+            row = qrow[v.qpod];
           }
-          qrows[v.qpod] = row;
         }
+        qrows[v.qpod] = row;
       }
+    }
     if (!sync_classes() || !refresh_program(q)) return false;
     for (auto& kv : qrows)
       if (!refresh_program((uint32_t)kv.first)) return false;
+    if (by_ref && !ensure_victim_store()) return false;
     plap(1);
     struct PLap {  // the search's time, whichever way it returns
       std::function<void()> f;
@@ -3427,41 +3525,54 @@ struct Cluster {
       // victims removed answers SelectVictimsOnNode's first question for all of
       // them; the reprieve then runs in lockstep over the candidates, one dry run
       // per round (its i-th most important victim re-added on every candidate).
-      // every candidate victim staged on the device once (entry i = all[i]); the
+      // every candidate victim staged on the device once (entry i = vic[i]); the
       // toggles below name entries (one launch each, a thread per node)
-      vector<std::pair<int32_t, Vic>> all;
-      for (int32_t g : potential)
-        for (auto& v : on[g]) all.push_back({g, v});
-      if (all.empty()) return true;
+      // (entry i = vic[i]: node by node, so every list below comes grouped by node)
+      if (vic.empty()) return true;
       {
-        vector<const vector<uint8_t>*> pp;
-        vector<int32_t> gn, rows;
-        for (auto& gv : all) {
-          const Vic& v = gv.second;
-          pp.push_back(v.bound >= 0 ? bprog[v.bound] : &progs[v.qpod]);
-          gn.push_back(gv.first + (int32_t)lo);
-          rows.push_back(v.bound >= 0 ? (tables_on() ? bound_row[v.bound] : -1) : qrows[v.qpod]);
+        vector<int32_t> gn(vic.size()), rows(vic.size());
+        for (size_t k = 0; k < potential.size(); ++k)
+          for (uint32_t i = voff[k]; i < voff[k + 1]; ++i) {
+            const Vic& v = vic[i];
+            gn[i] = potential[k] + (int32_t)lo;
+            rows[i] = v.bound >= 0 ? (tables_on() ? bound_row[v.bound] : -1) : qrows[v.qpod];
+          }
+        if (by_ref) {
+          vector<int64_t> ref(vic.size());
+          vector<uint8_t> qcsi(progs.size(), 0);
+          for (size_t i = 0; i < vic.size(); ++i) {
+            const Vic& v = vic[i];
+            if (v.bound >= 0) {
+              ref[i] = v.bound;
+            } else {
+              ref[i] = -1 - (int64_t)v.qpod;
+              qcsi[v.qpod] = reinterpret_cast<const ksg_prog*>(progs[v.qpod].data())->n_csi > 0 ? 1 : 0;
+            }
+          }
+          if (!eng->toggle_stage_refs(ref, gn, rows, qcsi, err)) return false;
+        } else {
+          vector<const vector<uint8_t>*> pp(vic.size());
+          for (size_t i = 0; i < vic.size(); ++i) pp[i] = vic[i].bound >= 0 ? bprog[vic[i].bound] : &progs[vic[i].qpod];
+          if (!eng->toggle_stage(pp, gn, rows, err)) return false;
         }
-        if (!eng->toggle_stage(pp, gn, rows, err)) return false;
       }
-      vector<uint32_t> every(all.size());
-      for (size_t i = 0; i < all.size(); ++i) every[i] = (uint32_t)i;
+      auto all_vic = [&](uint32_t e) -> const Vic& { return vic[e]; };
+      vector<uint32_t> every(vic.size());
+      for (size_t i = 0; i < vic.size(); ++i) every[i] = (uint32_t)i;
       vector<uint32_t> codes;
       if (!eng->toggle_staged(every, -1, err) || !eng->dry_filter(q, -1, codes, err) ||
           !eng->toggle_staged(every, +1, err))
         return false;
       vector<vector<uint32_t>> pv;  // per candidate: its victims (entries), most important first
       {
-        size_t i = 0;
-        for (int32_t g : potential) {
-          const size_t i0 = i;
-          i += on[g].size();
-          if (on[g].empty() || codes[g] != KSG_FILTER_PASS) continue;
+        for (size_t k = 0; k < potential.size(); ++k) {
+          const int32_t g = potential[k];
+          if (voff[k] == voff[k + 1] || codes[g] != KSG_FILTER_PASS) continue;
           cands.push_back(Cand{g, {}});
           pv.emplace_back();
-          for (size_t k = i0; k < i; ++k) pv.back().push_back((uint32_t)k);
+          for (uint32_t i = voff[k]; i < voff[k + 1]; ++i) pv.back().push_back(i);
           std::sort(pv.back().begin(), pv.back().end(),
-                    [&](uint32_t a, uint32_t b) { return more_important(all[a].second, all[b].second); });
+                    [&](uint32_t a, uint32_t b) { return more_important(all_vic(a), all_vic(b)); });
         }
       }
       vector<uint32_t> off;  // every candidate's victims off, then reprieve round by round
@@ -3492,7 +3603,7 @@ struct Cluster {
       vector<uint32_t> restore;  // the dry run leaves the state as it was
       for (size_t c = 0; c < cands.size(); ++c) {
         restore.insert(restore.end(), vict[c].begin(), vict[c].end());
-        for (uint32_t e : vict[c]) cands[c].victims.push_back(all[e].second);
+        for (uint32_t e : vict[c]) cands[c].victims.push_back(all_vic(e));
       }
       if (!eng->toggle_staged(restore, +1, err)) return false;
       vector<Cand> kept;
@@ -3500,8 +3611,9 @@ struct Cluster {
         if (!c.victims.empty()) kept.push_back(std::move(c));
       cands.swap(kept);
     } else {
-      for (int32_t g : potential) {
-        vector<Vic>& pvg = on[g];
+      for (size_t k = 0; k < potential.size(); ++k) {
+        const int32_t g = potential[k];
+        vector<Vic> pvg(vic.begin() + voff[k], vic.begin() + voff[k + 1]);
         if (pvg.empty()) continue;  // "No preemption victims found for incoming pod"
         bool ok = false;
         if (!toggle(pvg, g, -1) || !fits(g, ok)) return false;
@@ -5038,9 +5150,19 @@ int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out)
   ksg::Engine::ViewLayout lay;
   c.eng->view_layout(lay);
   std::unique_ptr<CycleView> v(new CycleView());
-  v->block = ksg::Engine::pinned_get(lay.bytes, v->cap);
-  if (!v->block) return ctx->fail("cycle_view: no host memory", KSG_E_DEVICE);
-  if (!c.eng->view(q, c.view_cfg(), lay, v->block, c.err)) return ctx->fail(c.err, KSG_E_STATE);
+  auto& pv = c.pview;
+  if (pv.block && pv.q == (int64_t)q && pv.gen == c.out_gen && pv.lay.bytes == lay.bytes && pv.lay.N == lay.N &&
+      pv.lay.n_raw == lay.n_raw) {  // filled by q's own cycle
+    lay = pv.lay;
+    v->block = pv.block;
+    v->cap = pv.cap;
+    pv.block = nullptr;
+    pv.drop();
+  } else {
+    v->block = ksg::Engine::pinned_get(lay.bytes, v->cap);
+    if (!v->block) return ctx->fail("cycle_view: no host memory", KSG_E_DEVICE);
+    if (!c.eng->view(q, c.view_cfg(), lay, v->block, c.err)) return ctx->fail(c.err, KSG_E_STATE);
+  }
   const uint32_t P = (uint32_t)c.n_plugins, N = c.hi - c.lo;
   v->msgs.resize(lay.n_slots + 1);  // messages[s + 1]: the message of slot s's code
   const uint64_t* slots = reinterpret_cast<const uint64_t*>(v->block);

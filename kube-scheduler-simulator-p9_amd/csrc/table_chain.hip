@@ -356,6 +356,13 @@ struct WFold {
     }
   }
 };
+// N signed minima then one OR (eval_body's pod-uniform setup)
+template <int N, int... OPS>
+struct MinsThenOr : MinsThenOr<N - 1, FO_MINI, OPS...> {};
+template <int... OPS>
+struct MinsThenOr<0, OPS...> {
+  using W = WFold<OPS..., FO_OR>;
+};
 // int64 normaliser fields as 32-bit words (callers checked the values fit): the
 // unset sentinels map to the 32-bit extremes and back
 __device__ __forceinline__ uint32_t mx32(int64_t v) { return v == INT64_MIN ? 0x80000000u : (uint32_t)(int32_t)v; }
@@ -466,8 +473,7 @@ __device__ __forceinline__ int64_t pts_count_tab(const DevCluster& C, const Prog
 template <int BT>
 struct EvalSharedT {
   int32_t tv[KSG_MAX_TOPO * BT];
-  int32_t minm[KSG_MAX_TSC];
-  uint32_t ipa_flags;
+  uint32_t setup[BT / 64 * 16];  // eval_body's setup fold (rows of its own: rec's may still be read)
   ChainRec rec[BT / 64];
 };
 using EvalShared = EvalSharedT<kChain>;
@@ -829,30 +835,25 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
     pre->ubbit = ubbit;
     return;
   }
-  // ---- pod-uniform setup: minMatchNum per filter constraint, InterPodAffinity bits
-  if (threadIdx.x < KSG_MAX_TSC) L.minm[threadIdx.x] = 0x7FFFFFFF;
-  if (threadIdx.x == 0) L.ipa_flags = 0;
-  lds_barrier();
-  if (pts_f) {
+  // ---- pod-uniform setup: minMatchNum per filter constraint, InterPodAffinity
+  // bits — one interleaved block fold (one barrier; the results uniform in registers)
+  uint32_t su[TS + 1];
 #pragma unroll
-    for (int c = 0; c < TS; ++c) {
-      if (c >= nf) continue;
+  for (int c = 0; c < TS; ++c) {
+    int32_t m = 0x7FFFFFFF;
+    if (pts_f && c < nf) {
       const ksg_tsc& t = h->tsc[c];
-      int32_t m = (threadIdx.x < (uint32_t)t.nvals && mpn[c]) ? mcnt[c] : 0x7FFFFFFF;
-      for (uint32_t i = threadIdx.x + blockDim.x; i < (uint32_t)t.nvals; i += blockDim.x)  // keys beyond 256 values
+      if (threadIdx.x < (uint32_t)t.nvals && mpn[c]) m = mcnt[c];
+      for (uint32_t i = threadIdx.x + BT; i < (uint32_t)t.nvals; i += BT)  // keys beyond one value per thread
         if (C.T.pair_node[t.pair_base + i]) {
           const int32_t x = t.eff_cls < 0 ? 0 : ld_tab<MODE>(C.T.pc_dom + (size_t)t.eff_cls * C.T.NU + (uint32_t)t.nub + i);
           m = x < m ? x : m;
         }
-      m = wave_min(m);
-      if (lane0() && m != 0x7FFFFFFF) atomicMin(&L.minm[c], m);
     }
+    su[c] = (uint32_t)m;
   }
-  if (ipa_pos >= 0) {
-    const uint32_t bits = __ockl_wfred_or_u32(ubv > 0 ? ubbit : 0u);
-    if (lane0() && bits) atomicOr(&L.ipa_flags, bits);
-  }
-  lds_barrier();
+  su[TS] = ipa_pos >= 0 && ubv > 0 ? ubbit : 0u;
+  MinsThenOr<TS>::W::template block<BT / 64>(su, L.setup);
   CS(10);
   // ---- the counts, folded into what the filters and scores read
   int32_t ptsm[KSG_MAX_TSC];
@@ -887,7 +888,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   if (pts_score)
     for (int c = nf; c < nf + ns; ++c) counted &= tv(h->tsc[c].topo) >= 0;
   if (h->tab & KTAB_PTS_MULTI) pts_cnt = 0;  // (k_ptsraw computes the raw scores)
-  const uint32_t ipa_flags = L.ipa_flags;
+  const uint32_t ipa_flags = su[TS];
   uint32_t code = KSG_FILTER_NOT_EVALUATED;
   bool err = false;
   if (active && !(h->flags & KPF_PREFILTER_REJECT) &&
@@ -924,7 +925,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
                 const int32_t dom = t.dom;
                 if (tv(t.topo) < 0) { fail = true; detail = KSG_PTS_MISSING_LABEL; continue; }
                 if (dom == 0) { err = true; continue; }  // minMatchNum: no domains -> Error
-                const int64_t mn = dom < t.min_domains ? 0 : L.minm[c];
+                const int64_t mn = dom < t.min_domains ? 0 : (int64_t)(int32_t)su[c];
                 if ((int64_t)ptsm[c] + t.self_match - mn > t.max_skew) { fail = true; detail = KSG_PTS_SKEW; }
               }
           break;

@@ -23,7 +23,7 @@ struct Engine::Impl {
   uint32_t used[4] = {0, 0, 0, 0}, cap[4] = {0, 0, 0, 0};
   uint32_t npc = 0, ntc = 0;
   uint32_t keep_first = 0, keep_n = 0;
-  size_t staged = 0;
+  size_t staged = 0, vstore = 0;
 };
 
 static bool check_prog(const std::vector<uint8_t>& p, std::string& err) {
@@ -131,6 +131,25 @@ bool Engine::toggle_stage(const std::vector<const std::vector<uint8_t>*>& progs,
     if (gnode[i] < 0 || (uint32_t)gnode[i] >= p_->N) { err = "stub: toggle node"; return false; }
   }
   p_->staged = progs.size();
+  return true;
+}
+bool Engine::victim_store(const std::vector<const std::vector<uint8_t>*>& progs, std::string& err) {
+  for (auto* pr : progs)
+    if (!pr || !check_prog(*pr, err)) return false;
+  p_->vstore = progs.size();
+  return true;
+}
+bool Engine::toggle_stage_refs(const std::vector<int64_t>& ref, const std::vector<int32_t>& gnode,
+                               const std::vector<int32_t>& rows, const std::vector<uint8_t>& queue_csi, std::string& err) {
+  if (gnode.size() != ref.size() || rows.size() != ref.size()) { err = "stub: toggle_stage_refs"; return false; }
+  for (size_t i = 0; i < ref.size(); ++i) {
+    if (ref[i] >= 0 ? (size_t)ref[i] >= p_->vstore : (size_t)(-1 - ref[i]) >= std::min(p_->progs.size(), queue_csi.size())) {
+      err = "stub: toggle ref";
+      return false;
+    }
+    if (gnode[i] < 0 || (uint32_t)gnode[i] >= p_->N) { err = "stub: toggle node"; return false; }
+  }
+  p_->staged = ref.size();
   return true;
 }
 bool Engine::toggle_staged(const std::vector<uint32_t>& idx, int sign, std::string& err) {
@@ -326,7 +345,7 @@ void Engine::view_layout(ViewLayout& lay) const {
   lay.off_norm = lay.off_raw + al256s(4 * N) * lay.n_raw;
   lay.bytes = lay.off_norm;
 }
-bool Engine::view(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err) {
+bool Engine::view(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err, bool) {
   PodOutputs o;
   if (!(p_->keep_n && q >= p_->keep_first && q < p_->keep_first + p_->keep_n)) { err = "outputs not kept for this pod"; return false; }
   if (!outputs(q, o, err)) return false;

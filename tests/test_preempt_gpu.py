@@ -26,15 +26,19 @@ def _oracle(doc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("batch", ["1", "0"], ids=["batched", "per-node"])
+@pytest.mark.parametrize("batch", ["1", "store", "0"], ids=["batched", "victim-store", "per-node"])
 @pytest.mark.parametrize("sizes", [{}, dict(n_nodes=10, n_existing=40, n_pods=30),
                                    dict(n_existing=70, n_pods=120, queue_sort=False)],
                          ids=["default", "small", "queue-victims"])
 def test_preempt_queue_matches_oracle(monkeypatch, sizes, batch):
     """Both victim searches — batched over every potential node (pods whose
     PreFilter state no removal changes) and the per-node probes — nominate the
-    oracle's node and victims."""
-    monkeypatch.setenv("KSG_PREEMPT_BATCH", batch)
+    oracle's node and victims; "victim-store": the batched search staging its
+    candidates by reference into the device-resident store of every bound pod's
+    program (what searches with thousands of victims use) from the first search."""
+    monkeypatch.setenv("KSG_PREEMPT_BATCH", "0" if batch == "0" else "1")
+    if batch == "store":
+        monkeypatch.setenv("KSG_VICTIM_STORE_MIN", "0")
     doc = _doc(**sizes)
     o = _oracle(doc)
     s = Scheduler(doc["profile"])
@@ -49,7 +53,7 @@ def test_preempt_queue_matches_oracle(monkeypatch, sizes, batch):
         nominated += s.postfilter_result(q)[0] >= 0
         assert s.annotations(q) == o.annotations(q), q
     assert nominated >= 5  # the family exercises the dry run
-    if batch == "1":
+    if batch != "0":
         assert s.preempt_batched() > 0
     else:
         assert s.preempt_batched() == 0

@@ -271,6 +271,7 @@ class Engine {
   // must be reloaded (host.cpp marks it broken); cleared by a reload.
   bool lost() const;
   uint64_t static_dec_chunks() const;  // diagnostic: static-record chunks computed from decoded pods
+  uint64_t static_overlaps() const;     // diagnostic: persistent runs whose static records were computed beside the loop
   void clear_lost();
   static bool nccl_unique_id(void* out128, std::string& err);
   // diagnostic: enable (out == nullptr, count pods) / read back s_memtime stamps of the fixup loop

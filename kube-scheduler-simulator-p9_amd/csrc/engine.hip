@@ -2402,9 +2402,17 @@ struct WinArgs {
   const uint32_t* nxt_evd;  // persistent loop: the next window's record counter and its target (null: last)
   uint32_t nxt_need;
 };
-// the static record of (queue pod q, global node g)
+// the static record of (queue pod q, global node g); PER (the persistent loop,
+// whose records k_static_dec may still be writing beside it): an sc1 load
+template <bool PER = false>
 __device__ __forceinline__ StaticRec srec_at(const WinArgs& A, uint32_t q, uint32_t g) {
-  return A.stat[(size_t)((q - A.first) % A.stat_ring) * A.stat_n + (g - A.stat_base)];
+  const StaticRec* p = A.stat + (size_t)((q - A.first) % A.stat_ring) * A.stat_n + (g - A.stat_base);
+  if constexpr (!PER) {
+    return *p;
+  } else {
+    const uint64_t v = ld_sc1(reinterpret_cast<const uint64_t*>(p));
+    return StaticRec{(uint32_t)v, (uint32_t)(v >> 32)};
+  }
 }
 __device__ __forceinline__ int64_t sel4(const int64_t (&v)[4], int i) {
   return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3];
@@ -3261,9 +3269,14 @@ __global__ __launch_bounds__(64) void k_st_decode(DevCluster C, DevProfile F, co
 // over the statically feasible nodes per pod.
 #define KSG_SD_PODS 8
 #define KSG_SD_NPT 2
+// ready (non-null: the persistent window loop reads the records while this runs
+// beside it): records stored sc1, then — after every wave's stores and maxima
+// have drained and a block barrier — one agent-scope add per block to its pod
+// group's counter (MI355X_MICROARCH.md hand-off table, row 1); a group's records
+// and maxima are complete once its counter reaches gridDim.x.
 __global__ __launch_bounds__(256) void k_static_dec(DevCluster C, DevProfile F, const WcPod* __restrict__ pods,
                                                     const uint8_t* __restrict__ progs, uint32_t count, StaticRec* out,
-                                                    int64_t* mpred) {
+                                                    int64_t* mpred, uint32_t* ready) {
   const bool ht = F.pos_taint >= 0, ha = F.pos_na >= 0;
   const bool taint_first = ht && (!ha || F.pos_taint < F.pos_na);
   uint32_t n[KSG_SD_NPT], tcnt[KSG_SD_NPT];
@@ -3361,13 +3374,22 @@ __global__ __launch_bounds__(256) void k_static_dec(DevCluster C, DevProfile F, 
           ma = a > ma ? a : ma;
         }
       }
-      if (live[k]) out[(size_t)j * C.N + n[k]] = StaticRec{code, raw};
+      if (live[k]) {
+        StaticRec* o = out + (size_t)j * C.N + n[k];
+        if (ready) st_sc1(reinterpret_cast<uint64_t*>(o), (uint64_t)code | ((uint64_t)raw << 32));
+        else *o = StaticRec{code, raw};
+      }
     }
     const int64_t a0 = wave_max(mt), a1 = wave_max(ma);
     if (lane0()) {
       if (a0 >= 0) atomicMax((long long*)&mpred[2 * j], (long long)a0);
       if (a1 >= 0) atomicMax((long long*)&mpred[2 * j + 1], (long long)a1);
     }
+  }
+  if (ready) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ready + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -3820,9 +3842,9 @@ __device__ __forceinline__ void win_merge(const DevCluster& C, const DevProfile&
       int64_t mt = 0, ma = 0;
       if (STAT) {  // (the static maxima and records were computed before the launch)
         const uint32_t q = A.e0 + b;
-        mt = A.mpred[2 * (q - A.first)];
-        ma = A.mpred[2 * (q - A.first) + 1];
-        sr = srec_at(A, q, (uint32_t)pe.node);
+        mt = ldv<PER>(A.mpred + 2 * (q - A.first));
+        ma = ldv<PER>(A.mpred + 2 * (q - A.first) + 1);
+        sr = srec_at<PER>(A, q, (uint32_t)pe.node);
         code = eval_row_s<MODE>(pe.after, F, h, R, sr, mt, ma, fs, bs, tot);
       } else {
         code = eval_row<MODE>(pe.after, F, h, R, fs, bs, tot);
@@ -3943,7 +3965,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
   {
     constexpr int kPodW = (int)(sizeof(PodLite) / 8);
     if (tid < kPodW) reinterpret_cast<uint64_t*>(h)[tid] = reinterpret_cast<const uint64_t*>(A.plite + q)[tid];
-    if (STAT && tid < 2) mlds[tid] = A.mpred[2 * (q - A.first) + tid];
+    if (STAT && tid < 2) mlds[tid] = ldv<PER>(A.mpred + 2 * (q - A.first) + tid);
   }
   const int np = ldv<PER>(A.pprev_n);
   // P_{W-1}'s nodes in LDS (a lookup through LDS: a VGPR loaded from memory and
@@ -3985,7 +4007,7 @@ __device__ __forceinline__ void win_eval(const DevCluster& C, const DevProfile& 
       const int hit = pend_lds((int32_t)(C.goff + nn));
       if (hit >= 0) r = ld_obj<PER>(&A.pprev[hit].after);
       else if (!loaded) load_row_p<PER>(C, nn, A.need_eph, r);
-      if (STAT) sr = srec_at(A, q, C.goff + nn);
+      if (STAT) sr = srec_at<PER>(A, q, C.goff + nn);
     }
   };
   StaticRec snext{KSG_FILTER_PASS, 0};
@@ -4337,7 +4359,7 @@ __device__ __forceinline__ void win_exact_select(const DevCluster& C, const DevP
   for (uint32_t i = tid; i < gn; i += KSG_WIN_THREADS) {
     RowV r;
     row_under<PER>(C, L, A, S, T, b, g0 + i, R, r);
-    const StaticRec sr = srec_at(A, A.w0 + b, g0 + i);
+    const StaticRec sr = srec_at<PER>(A, A.w0 + b, g0 + i);
     int32_t fs, bs;
     int64_t tot;
     if (eval_row_s<MODE>(r, F, h, R, sr, 0, 0, fs, bs, tot) == KSG_FILTER_PASS) {
@@ -4369,7 +4391,7 @@ __device__ __forceinline__ void win_exact_select(const DevCluster& C, const DevP
     row_under<PER>(C, L, A, S, T, b, g0 + i, R, r);
     int32_t fs, bs;
     int64_t tot;
-    if (eval_row_s<MODE>(r, F, h, R, srec_at(A, A.w0 + b, g0 + i), mt, ma, fs, bs, tot) == KSG_FILTER_PASS) {
+    if (eval_row_s<MODE>(r, F, h, R, srec_at<PER>(A, A.w0 + b, g0 + i), mt, ma, fs, bs, tot) == KSG_FILTER_PASS) {
       const uint64_t k = pack_key(tot, F.seed, h->queue_idx, g0 + i);
       best = k > best ? k : best;
     }
@@ -4411,7 +4433,7 @@ __device__ __forceinline__ void win_exact_write(const DevCluster& C, const DevPr
   for (uint32_t i = threadIdx.x; i < C.N; i += KSG_WIN_THREADS) {  // (this shard's outputs)
     RowV r;
     row_under<PER>(C, L, A, L.S[cur], L.pick[cur], b, C.goff + i, R, r);
-    const StaticRec sr = srec_at(A, A.w0 + b, C.goff + i);
+    const StaticRec sr = srec_at<PER>(A, A.w0 + b, C.goff + i);
     int32_t fs, bs;
     int64_t tot;
     const uint32_t code = eval_row_s<MODE>(r, F, h, R, sr, mt, ma, fs, bs, tot);
@@ -4476,8 +4498,8 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
         aT = ldv<PER>(reinterpret_cast<const int32_t*>(A.wrec) + KSG_BATCH + tid);
         aA = ldv<PER>(reinterpret_cast<const int32_t*>(A.wrec) + 2 * KSG_BATCH + tid);
       }
-      m0 = A.mpred[2 * (A.w0 - A.first + tid)];
-      m1 = A.mpred[2 * (A.w0 - A.first + tid) + 1];
+      m0 = ldv<PER>(A.mpred + 2 * (A.w0 - A.first + tid));
+      m1 = ldv<PER>(A.mpred + 2 * (A.w0 - A.first + tid) + 1);
     }
     if (A.defer) {
       // merge pod b's T tile lists (wave w: pods w and w+16) and sum its tile counts;
@@ -4607,7 +4629,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       StaticRec sr{KSG_FILTER_PASS, 0};
       uint32_t code;
       if (STAT) {
-        sr = srec_at(A, A.w0 + pb, (uint32_t)pe.node);
+        sr = srec_at<PER>(A, A.w0 + pb, (uint32_t)pe.node);
         code = eval_row_s<MODE>(pe.after, F, h, R, sr, L.mt[pb], L.ma[pb], fs, bs, tot);
       } else {
         code = eval_row<MODE>(pe.after, F, h, R, fs, bs, tot);
@@ -4754,7 +4776,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
               StaticRec sr{KSG_FILTER_PASS, 0};
               uint32_t code;
               if (STAT) {
-                sr = srec_at(A, A.w0 + b, (uint32_t)Sv);
+                sr = srec_at<PER>(A, A.w0 + b, (uint32_t)Sv);
                 code = eval_row_s<MODE>(cur_r, F, h, R, sr, L.mt[b], L.ma[b], fs, bs, tot);
               } else {
                 code = eval_row<MODE>(cur_r, F, h, R, fs, bs, tot);
@@ -5087,7 +5109,33 @@ struct WinRunArgs {
   int32_t* pend_n;         // [2]
   uint32_t* arrive;        // [2][KSG_BATCH] counters, one 128-B line each
   uint64_t* stamps;        // diagnostic: 32 slots per window, or null
+  const uint32_t* sready;  // STAT beside k_static_dec: per group of KSG_SD_PODS pods, its finished node tiles (null: before)
+  uint32_t sready_need;    // ... the node tiles of k_static_dec's grid
 };
+// The eval blocks' gate on the static records of window pods [r0, r0 + n) (run
+// offsets) when k_static_dec runs beside the loop: thread 0 polls the groups'
+// counters (sc1), the block waits at a barrier.  Every other reader of a window's
+// records (merges, the replay) reads them after this window's evaluation.
+__device__ bool win_stat_gate(const WinRunArgs& R, uint32_t r0, uint32_t n, uint32_t* abortw, uint32_t spin,
+                              uint32_t* go) {
+  if (threadIdx.x == 0) {
+    const uint32_t g0 = r0 / KSG_SD_PODS, g1 = (r0 + n - 1) / KSG_SD_PODS;
+    bool ok = false;
+    for (uint32_t it = 0; it < spin; ++it) {
+      bool all = true;
+      for (uint32_t g = g0; g <= g1; ++g) all &= ld_sc1(R.sready + g) >= R.sready_need;
+      if (all) { ok = true; break; }
+      if ((it & 63u) == 63u && ld_sc1(abortw) != 0u) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok) __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *go = ok ? 1u : 0u;
+  }
+  __syncthreads();
+  const bool ok = *go != 0u;
+  __syncthreads();
+  return ok;
+}
 __device__ bool win_wait_ge(const uint32_t* w, uint32_t want, uint32_t* abortw, uint32_t spin, uint32_t* go) {
   if (threadIdx.x == 0) {
     bool ok = false;
@@ -5208,6 +5256,7 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
     A.pcur_n = R.pend_n + ((E + 1) & 1);
     A.pubw = E >= 1 ? &Z->replayed[blk & 15][0] : nullptr;  // (E = 0: P_{-1} is empty)
     A.pub_need = E;
+    if (STAT && R.sready && !win_stat_gate(R, A.e0 - R.first, A.ne, abortw, RC.spin, &go)) return;
     win_eval<MODE, STAT, true>(C, F, A, blk, L);
     __syncthreads();  // (LDS reused by the next window)
   }
@@ -5352,6 +5401,9 @@ struct Engine::Impl {
   int static_dec = 1;         // k_static_dec where the chunk's pods decode (KSG_STATIC_DEC=0: k_static)
   uint32_t static_run_mb = 16384;  // static records of a whole run in the persistent window loop (KSG_STATIC_RUN_MB; 0: off)
   uint64_t static_dec_chunks = 0;  // diagnostic: static chunks computed from decoded pods
+  int static_overlap = 1;          // KSG_STATIC_OVERLAP=0: a persistent run's records all before its launch
+  uint64_t static_overlaps = 0;    // diagnostic: persistent runs whose records were computed beside the loop
+  DBuf<uint32_t> sready;           // ... per group of KSG_SD_PODS pods, the node tiles done
   uint32_t wi_chunk = 0;      // ... pods per chunk of the last step, and whether records were used
   bool wi_rec = false;
   bool wi_cls = false;        // ... or the class path
@@ -5623,6 +5675,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
     if (const char* e = std::getenv("KSG_STATIC_SIDE")) I.static_side = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("KSG_STATIC_DEC")) I.static_dec = (int)std::strtol(e, nullptr, 10);
     if (const char* e = std::getenv("KSG_STATIC_RUN_MB")) I.static_run_mb = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("KSG_STATIC_OVERLAP")) I.static_overlap = (int)std::strtol(e, nullptr, 10);
   }
   HIPCHK(hipEventCreate(&I.ev0));
   HIPCHK(hipEventCreate(&I.ev1));
@@ -6120,12 +6173,22 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
         HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
   }
-  auto issue_static = [&](uint32_t c, hipStream_t st) -> bool {
+  // decoded pods (k_static_dec) when every pod of the chunk flattens and the
+  // nodes' taints fit the id set (KSG_STATIC_DEC=0: the program-walking k_static)
+  auto static_dec_ok = [&](uint32_t q0, uint32_t cn) {
+    bool dec = I.static_dec && I.max_taints <= 4 && I.max_tid < 64 && !I.taint_dup;
+    for (uint32_t q = q0; dec && q < q0 + cn; ++q) dec = (I.prog_need[q] & (1u << 19)) != 0;
+    return dec;
+  };
+  // ready: k_static_dec beside the persistent loop, counting its pod groups there
+  // (the maxima already reset on the engine stream)
+  auto issue_static = [&](uint32_t c, hipStream_t st, uint32_t* ready = nullptr) -> bool {
     const uint32_t q0 = first + c * chunk, cn = std::min(chunk, first + count - q0);
-    HIPCHK(hipMemsetAsync(I.mpred.p + 2 * (size_t)(q0 - first), 0xFF, 2 * (size_t)cn * sizeof(int64_t), st));
+    if (!ready)
+      HIPCHK(hipMemsetAsync(I.mpred.p + 2 * (size_t)(q0 - first), 0xFF, 2 * (size_t)cn * sizeof(int64_t), st));
     const dim3 sgrid(std::max<uint32_t>((SN + 256 * KSG_ST_NPT - 1) / (256 * KSG_ST_NPT), 1),
                      (cn + KSG_ST_PODS - 1) / KSG_ST_PODS);
-    const bool ssamp = I.sample_every && st == s;
+    const bool ssamp = I.sample_every && (st == s || ready);
     if (ssamp) {
       while (I.sev_st.size() < 2 * (size_t)(I.n_st + 1)) {
         hipEvent_t e;
@@ -6135,10 +6198,8 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
       HIPCHK(hipEventRecord(I.sev_st[2 * I.n_st], st));
     }
     StaticRec* const sout = I.stat.p + (size_t)((q0 - first) % (nslots * chunk)) * A.stat_n;
-    // decoded pods (k_static_dec) when every pod of the chunk flattens and the
-    // nodes' taints fit the id set (KSG_STATIC_DEC=0: the program-walking k_static)
-    bool dec = I.static_dec && I.max_taints <= 4 && I.max_tid < 64 && !I.taint_dup;
-    for (uint32_t q = q0; dec && q < q0 + cn; ++q) dec = (I.prog_need[q] & (1u << 19)) != 0;
+    const bool dec = static_dec_ok(q0, cn);
+    if (ready && !dec) { err = "static records beside the loop: pods that do not decode"; return false; }
     if (dec) {
       if (!I.sd_pods.alloc((size_t)chunk * (sizeof(WcPod) / 8), err)) return false;
       WcPod* wp = reinterpret_cast<WcPod*>(I.sd_pods.p);
@@ -6147,7 +6208,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
       const dim3 dgrid(std::max<uint32_t>((SN + 256 * KSG_SD_NPT - 1) / (256 * KSG_SD_NPT), 1),
                        (cn + KSG_SD_PODS - 1) / KSG_SD_PODS);
       hipLaunchKernelGGL(k_static_dec, dgrid, dim3(256), 0, st, CS, I.F, wp, I.progs.p, cn, sout,
-                         I.mpred.p + 2 * (size_t)(q0 - first));
+                         I.mpred.p + 2 * (size_t)(q0 - first), ready);
       I.static_dec_chunks++;
     } else {
       hipLaunchKernelGGL(k_static, sgrid, dim3(256), 0, st, CS, I.F, I.progs.p, I.prog_off_d.p, q0, cn, sout,
@@ -6171,7 +6232,23 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   // the persistent window loop: one launch for every window (its blocks all
   // resident: one per CU); not co-resident -> the launch-per-window loop below
   if (persist_ok && (!stat || stat_run)) {
-    if (stat_run && !issue_static(0, s)) return false;  // (every record of the run)
+    // the run's records: before the launch, or (KSG_STATIC_OVERLAP, default) by
+    // k_static_dec on the side stream once the loop's blocks are all resident,
+    // on the CUs it leaves idle; its eval blocks wait per window for their pods'
+    // groups (win_stat_gate)
+    const bool overlap = stat_run && I.static_overlap && I.sstream && static_dec_ok(first, count);
+    const uint32_t sgroups = (count + KSG_SD_PODS - 1) / KSG_SD_PODS;
+    if (overlap) {  // (every buffer k_static_dec needs allocated now: a free beside the loop would wait for it)
+      if (!I.sready.alloc(sgroups, err) || !I.sd_pods.alloc((size_t)chunk * (sizeof(WcPod) / 8), err)) return false;
+      HIPCHK(hipMemsetAsync(I.sready.p, 0, sgroups * sizeof(uint32_t), s));
+      HIPCHK(hipMemsetAsync(I.mpred.p, 0xFF, 2 * (size_t)count * sizeof(int64_t), s));
+      if (!I.sev_ready[0])
+        for (auto* e : {&I.sev_ready[0], &I.sev_ready[1], &I.sev_ready[2], &I.sev_free})
+          HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+      HIPCHK(hipEventRecord(I.sev_free, s));
+    } else if (stat_run && !issue_static(0, s)) {  // (every record of the run)
+      return false;
+    }
     // dedicated merge blocks (one per pod) when they fit beside the tile blocks
     const bool mb = I.win_mblocks && 1 + (uint64_t)KSG_BATCH * (T + 1) <= I.n_cus;
     if (!I.wsync.alloc(1, err) || !I.rsync.alloc(1, err)) return false;
@@ -6204,6 +6281,8 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     R.pend_n = I.pend_n.p;
     R.arrive = I.arrive.p;
     R.stamps = I.stamps_on ? I.stamps.p : nullptr;
+    R.sready = overlap ? I.sready.p : nullptr;
+    R.sready_need = std::max<uint32_t>((SN + 256 * KSG_SD_NPT - 1) / (256 * KSG_SD_NPT), 1);  // (k_static_dec's grid.x)
     const uint32_t grid = 1 + KSG_BATCH * T + (mb ? KSG_BATCH : 0);
     WinArgs AP = A;
     AP.mblocks = mb ? 1u : 0u;
@@ -6239,6 +6318,13 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     }
     if (v == 1u) {
       I.win_runs++;
+      if (overlap) {  // the loop holds its CUs: the records beside it, then the stream waits for them
+        HIPCHK(hipStreamWaitEvent(I.sstream, I.sev_free, 0));
+        if (!issue_static(0, I.sstream, I.sready.p)) return false;
+        HIPCHK(hipEventRecord(I.sev_ready[0], I.sstream));
+        HIPCHK(hipStreamWaitEvent(s, I.sev_ready[0], 0));
+        I.static_overlaps++;
+      }
       const int64_t L = nwin - 1;
       hipLaunchKernelGGL(k_apply_pend, dim3(1), dim3(KSG_BATCH), 0, s, C, I.pend.p + (size_t)(L & 1) * KSG_BATCH,
                          I.pend_n.p + (L & 1));
@@ -7891,6 +7977,7 @@ void Engine::path_counts(uint64_t out[8]) const {
 }
 bool Engine::lost() const { return p_->lost; }
 uint64_t Engine::static_dec_chunks() const { return p_->static_dec_chunks; }
+uint64_t Engine::static_overlaps() const { return p_->static_overlaps; }
 void Engine::clear_lost() {
   Impl& I = *p_;
   if (I.rsync.p && (I.lost || I.run_used)) {  // (the sticky abort word: a call that failed before its sync left it set)

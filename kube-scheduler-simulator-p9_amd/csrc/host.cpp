@@ -4869,6 +4869,12 @@ extern "C" int ksg_debug_static_dec_chunks(ksg_ctx* ctx, uint64_t* out) {
   *out = ctx->c.eng->static_dec_chunks();
   return KSG_OK;
 }
+extern "C" int ksg_debug_static_overlaps(ksg_ctx* ctx, uint64_t* out) {
+  KSG_LOCK(ctx);
+  if (!ctx || !out) return KSG_E_INVALID;
+  *out = ctx->c.eng->static_overlaps();
+  return KSG_OK;
+}
 
 // diagnostic (not in ksg.h): the sampled run's k_static launches (cfg3 roofline)
 extern "C" int ksg_debug_static_time(ksg_ctx* ctx, float* total_ms, uint32_t* launches, uint64_t* pods) {

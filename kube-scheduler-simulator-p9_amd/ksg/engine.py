@@ -370,6 +370,14 @@ class Scheduler:
         self._chk(self.L.ksg_debug_static_dec_chunks(self.h, ctypes.byref(out)), "ksg_debug_static_dec_chunks")
         return out.value
 
+    def static_overlaps(self):
+        """Diagnostic: persistent window runs whose static records k_static_dec
+        computed beside the loop (KSG_STATIC_OVERLAP)."""
+        out = ctypes.c_uint64()
+        self.L.ksg_debug_static_overlaps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self._chk(self.L.ksg_debug_static_overlaps(self.h, ctypes.byref(out)), "ksg_debug_static_overlaps")
+        return out.value
+
     def static_time(self):
         """Diagnostic: (total ms, launches, pods) of the sampled run's k_static launches."""
         ms, n, pods = ctypes.c_float(), ctypes.c_uint32(), ctypes.c_uint64()

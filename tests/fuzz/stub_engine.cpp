@@ -374,6 +374,7 @@ uint8_t* Engine::pinned_get(size_t bytes, size_t& cap) {
 void Engine::pinned_put(uint8_t* p, size_t) { std::free(p); }
 uint8_t* Engine::pinned_dev(const uint8_t*) { return nullptr; }
 uint64_t Engine::static_dec_chunks() const { return 0; }
+uint64_t Engine::static_overlaps() const { return 0; }
 bool rccl_selftest(int, size_t, std::string& err) {
   err = "stub: no RCCL";
   return false;

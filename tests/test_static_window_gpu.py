@@ -133,17 +133,23 @@ def test_static_records_decoded_and_walked(monkeypatch, dec):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"KSG_STATIC_RUN_MB": "0"}, {"KSG_WIN_MB": "1"}, {"KSG_WIN_PFIX": "1"},
-                                 {"KSG_WIN_SPLIT": "0"}],
-                         ids=["persistent", "per-window", "merge-blocks", "prior-in-replay", "one-counter"])
+@pytest.mark.parametrize("env", [{}, {"KSG_STATIC_OVERLAP": "0"}, {"KSG_STATIC_RUN_MB": "0"}, {"KSG_WIN_MB": "1"},
+                                 {"KSG_WIN_PFIX": "1"}, {"KSG_WIN_SPLIT": "0"}],
+                         ids=["persistent", "records-before", "per-window", "merge-blocks", "prior-in-replay",
+                              "one-counter"])
 def test_static_profiles_persistent_window_loop(monkeypatch, env):
-    """Taint / NodeAffinity profiles in the persistent window loop (k_window_run
-    with static records computed for the whole run before the launch), its
-    variants, and the launch-per-window loop it replaces: a cfg3 queue, the
-    saturating cluster and both normaliser-fallback cases against the oracle."""
+    """Taint / NodeAffinity profiles in the persistent window loop (k_window_run;
+    its static records computed by k_static_dec beside the loop, each window's
+    evaluation gated on its pods' groups — or, "records-before", all before the
+    launch), its variants, and the launch-per-window loop it replaces: a cfg3
+    queue, the saturating cluster and both normaliser-fallback cases against the
+    oracle."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    for doc in (g.generate(3, n_nodes=900, n_pods=500), _tight_cfg3(n_pods=500), _fallback_doc("taint"),
-                _fallback_doc("na")):
+    for i, doc in enumerate((g.generate(3, n_nodes=900, n_pods=500), _tight_cfg3(n_pods=500), _fallback_doc("taint"),
+                             _fallback_doc("na"))):
         _, s = _compare(doc, every=13)
         assert (s.window_runs() > 0) == (env.get("KSG_STATIC_RUN_MB") != "0")
+        if i == 0:  # (decodable pods: the records beside the loop unless switched off)
+            assert (s.static_overlaps() > 0) == (env.get("KSG_STATIC_OVERLAP") != "0" and
+                                                 env.get("KSG_STATIC_RUN_MB") != "0")

@@ -1741,8 +1741,17 @@ constexpr uint32_t kRunSpin = 1u << 22;  // polls (~1 us each with the load) bef
 constexpr int kRunSleep = KSG_RUN_SLEEP;  // s_sleep between polls (x 64 cycles): every block polls every block
 constexpr int kRunG1 = 2 + 4 * KCP_X + 2 * KSG_MAX_TSC;  // partial-record granules per block (max)
 constexpr int kRunG2 = 3;                                // key granules per block
-constexpr int kRunGS = 64;                               // granule stride per block (uint64)
+constexpr int kRunGS = 64;                               // granules per block (uint64)
 constexpr size_t kRunSlot = (size_t)kChain * kRunGS;     // one parity slot of one granule kind (uint64)
+// Granule j of block b sits at j * kGF + b * kGB of its slot.  Field-major (the
+// default, round 5): the readers' lanes are the blocks, so one poll or record load
+// of a wave reads 64 consecutive granules (8 lines) instead of one line per lane
+// (64); KSG_RUN_GT=0 restores the block-major layout.
+#ifndef KSG_RUN_GT
+#define KSG_RUN_GT 1
+#endif
+constexpr size_t kGB = KSG_RUN_GT ? 1 : kRunGS;
+constexpr size_t kGF = KSG_RUN_GT ? kChain : 1;
 __device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t v) { return ((uint64_t)tag << 32) | v; }
 __device__ __forceinline__ bool run_aborted(uint32_t i, const RunSync* Y) {
   return (i & 63u) == 63u && ld_sc1(&Y->abort[0]) != 0u;
@@ -1847,19 +1856,20 @@ __device__ __forceinline__ bool run_read_g1(const uint64_t* g, uint32_t tag, uin
   for (uint32_t it = 0; it < spin; ++it) {
     // one granule per poll until it carries the tag (few loads in flight chip-wide),
     // then the whole record (whose tags are checked again)
-    if (!gtag(ld_sc1(g + last), tag)) {
+    if (!gtag(ld_sc1(g + last * kGF), tag)) {
       if (run_aborted(it, Y)) return false;
       __builtin_amdgcn_s_sleep(kRunSleep);
       continue;
     }
     bool ok = true;
-    const uint64_t w0 = ld_sc1(g), w1 = ld_sc1(g + 1);
+    const uint64_t w0 = ld_sc1(g), w1 = ld_sc1(g + kGF);
     ok &= gtag(w0, tag) && gtag(w1, tag);
     int j = 2;
 #pragma unroll
     for (int x = 0; x < KCP_X; ++x)
       if ((xmask >> x) & 1u) {
-        const uint64_t a = ld_sc1(g + j), b = ld_sc1(g + j + 1), c = ld_sc1(g + j + 2), d = ld_sc1(g + j + 3);
+        const uint64_t a = ld_sc1(g + j * kGF), b = ld_sc1(g + (j + 1) * kGF), c = ld_sc1(g + (j + 2) * kGF),
+                       d = ld_sc1(g + (j + 3) * kGF);
         ok &= gtag(a, tag) && gtag(b, tag) && gtag(c, tag) && gtag(d, tag);
         r.mx[x] = g64(a, b);
         r.mn[x] = g64(c, d);
@@ -1868,7 +1878,7 @@ __device__ __forceinline__ bool run_read_g1(const uint64_t* g, uint32_t tag, uin
 #pragma unroll
     for (int c = 0; c < TS; ++c)
       if (c < ns) {
-        const uint64_t a = ld_sc1(g + j), b = ld_sc1(g + j + 1);
+        const uint64_t a = ld_sc1(g + j * kGF), b = ld_sc1(g + (j + 1) * kGF);
         ok &= gtag(a, tag) && gtag(b, tag);
         r.reg[c] = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)b << 32);
         j += 2;
@@ -1962,25 +1972,25 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     // the partial record's granules, stored by one lane field after field (a
     // per-lane pick of its granule was a long select chain on every lane)
     if (threadIdx.x == 0) {
-      uint64_t* g = G1 + (size_t)b * kRunGS;
+      uint64_t* g = G1 + (size_t)b * kGB;
       const ChainRec& rr = eo.rec;
       st_sc1(g, gran(tag, (uint32_t)rr.feas | ((uint32_t)rr.ign << 16)));
-      st_sc1(g + 1, gran(tag, (uint32_t)rr.st));
+      st_sc1(g + kGF, gran(tag, (uint32_t)rr.st));
       int j = 2;
 #pragma unroll
       for (int x = 0; x < KCP_X; ++x)
         if ((xmask >> x) & 1u) {
-          st_sc1(g + j, gran(tag, (uint32_t)(uint64_t)rr.mx[x]));
-          st_sc1(g + j + 1, gran(tag, (uint32_t)((uint64_t)rr.mx[x] >> 32)));
-          st_sc1(g + j + 2, gran(tag, (uint32_t)(uint64_t)rr.mn[x]));
-          st_sc1(g + j + 3, gran(tag, (uint32_t)((uint64_t)rr.mn[x] >> 32)));
+          st_sc1(g + j * kGF, gran(tag, (uint32_t)(uint64_t)rr.mx[x]));
+          st_sc1(g + (j + 1) * kGF, gran(tag, (uint32_t)((uint64_t)rr.mx[x] >> 32)));
+          st_sc1(g + (j + 2) * kGF, gran(tag, (uint32_t)(uint64_t)rr.mn[x]));
+          st_sc1(g + (j + 3) * kGF, gran(tag, (uint32_t)((uint64_t)rr.mn[x] >> 32)));
           j += 4;
         }
 #pragma unroll
       for (int c = 0; c < TS; ++c)
         if (c < ns) {
-          st_sc1(g + j, gran(tag, (uint32_t)rr.reg[c]));
-          st_sc1(g + j + 1, gran(tag, (uint32_t)(rr.reg[c] >> 32)));
+          st_sc1(g + j * kGF, gran(tag, (uint32_t)rr.reg[c]));
+          st_sc1(g + (j + 1) * kGF, gran(tag, (uint32_t)(rr.reg[c] >> 32)));
           j += 2;
         }
     }
@@ -2008,7 +2018,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       ChainRec& r = E.r;
       rec_init(r);
       bool ok = true;
-      if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y, R.spin);
+      if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kGB, tag, xmask, ns, r, Y, R.spin);
       if (__syncthreads_or(!ok)) return;
       RS(31);
       if (rs_on) {  // the latest block's partial vs this pod's start in block 0 (slot 51)
@@ -2060,10 +2070,10 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     RS(47);
     fold_key<BT>(r, L.rec);
     if (threadIdx.x == 0) {
-      uint64_t* g = G2 + (size_t)b * kRunGS;
+      uint64_t* g = G2 + (size_t)b * kGB;
       st_sc1(g, gran(tag, (uint32_t)r.key));
-      st_sc1(g + 1, gran(tag, (uint32_t)(r.key >> 32)));
-      st_sc1(g + 2, gran(tag, (uint32_t)r.st));
+      st_sc1(g + kGF, gran(tag, (uint32_t)(r.key >> 32)));
+      st_sc1(g + 2 * kGF, gran(tag, (uint32_t)r.st));
     }
     RS(33);
     if (rst && threadIdx.x == 0) atomicMax((unsigned long long*)&rst[54 + (k & 1)], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -2098,13 +2108,13 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
     {
       bool ok = true;
       if (threadIdx.x < NB) {
-        const uint64_t* g = G2 + (size_t)threadIdx.x * kRunGS;
+        const uint64_t* g = G2 + (size_t)threadIdx.x * kGB;
         ok = false;
         // (thread 0 also reads the assume flag: the next pod's wait then needs no poll
         // when this value covers it — every assume before this pod's, normally)
         const uint64_t fseen = threadIdx.x == 0 ? ld_sc1(&Y->flag[0]) : 0;
         for (uint32_t it = 0; it < R.spin; ++it) {
-          const uint64_t d = ld_sc1(g + 2), a = ld_sc1(g), c = ld_sc1(g + 1);  // (3 granules: all per poll)
+          const uint64_t d = ld_sc1(g + 2 * kGF), a = ld_sc1(g), c = ld_sc1(g + kGF);  // (3 granules: all per poll)
           if (gtag(a, tag) && gtag(c, tag) && gtag(d, tag)) {
             sk.key = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)c << 32);
             sk.st = (int32_t)(uint32_t)d;
@@ -2220,17 +2230,17 @@ __device__ __forceinline__ void run_commit_body(DevCluster& C, const DevProfile&
     ChainRec r;
     rec_init(r);
     bool ok = true;
-    if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kRunGS, tag, xmask, ns, r, Y, R.spin);
+    if (threadIdx.x < NB) ok = run_read_g1<TS>(G1 + (size_t)threadIdx.x * kGB, tag, xmask, ns, r, Y, R.spin);
     if (__syncthreads_or(!ok)) return;
     fold_partial<KCX_PTS, KCX_IPA, BT>(r, lrec, 0u, 0, false);
     ChainRec sk;
     rec_init(sk);
     ok = true;
     if (threadIdx.x < NB) {
-      const uint64_t* g = G2 + (size_t)threadIdx.x * kRunGS;
+      const uint64_t* g = G2 + (size_t)threadIdx.x * kGB;
       ok = false;
       for (uint32_t it = 0; it < R.spin; ++it) {
-        const uint64_t d = ld_sc1(g + 2), a = ld_sc1(g), c = ld_sc1(g + 1);
+        const uint64_t d = ld_sc1(g + 2 * kGF), a = ld_sc1(g), c = ld_sc1(g + kGF);
         if (gtag(a, tag) && gtag(c, tag) && gtag(d, tag)) {
           sk.key = (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)c << 32);
           sk.st = (int32_t)(uint32_t)d;

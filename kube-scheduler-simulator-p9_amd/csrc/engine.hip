@@ -6698,6 +6698,32 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
   // places it (program, offset, PodLite, table row, fresh summary): no wait here.
   // The block is reused once its previous copy has completed (an event).
   const size_t sbytes = sizeof(PodLite) + prog.size();
+  {  // (round 5) zero-copy: k_place_program reads a mapped pinned block, held until the next sync
+    size_t cap = 0;
+    uint8_t* blk = pinned_get(sbytes, cap);
+    uint8_t* dv = blk ? pinned_dev(blk) : nullptr;
+    if (dv) {
+      std::memcpy(blk, &pl, sizeof(pl));
+      std::memcpy(blk + sizeof(PodLite), prog.data(), prog.size());
+      I.hold.push_back(std::shared_ptr<const void>(blk, [cap](const void* b) {
+        Engine::pinned_put(const_cast<uint8_t*>(static_cast<const uint8_t*>(b)), cap);
+      }));
+      I.unwaited = true;
+      hipLaunchKernelGGL(k_place_program, dim3(1), dim3(256), 0, s, dv, (uint32_t)prog.size(), I.progs.p + off,
+                         I.prog_off_d.p + q, off64, (void*)(I.plite.p + q), I.prow.p + q, (int32_t)-1, I.sums.p + q,
+                         I.F);
+      HIPCHK(hipGetLastError());
+      I.prog_bytes = off + prog.size();
+      I.prog_off.push_back(off);
+      if (!na_weights_fit(prog)) I.static_fits = false;
+      I.max_na_sum = std::max(I.max_na_sum, na_weight_sum(prog));
+      const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
+      I.prog_need.push_back(prog_need_of(h));
+      for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
+      return true;
+    }
+    if (blk) pinned_put(blk, cap);
+  }
   if (!I.apstage || I.apstage_cap < sbytes) {
     if (I.apstage) {
       HIPCHK(hipEventSynchronize(I.apstage_ev));
@@ -7113,6 +7139,21 @@ static bool dev_zero_tail(DBuf<T>& b, size_t used, size_t count, hipStream_t s, 
   return true;
 }
 
+// add_classes' uploads in one launch (unsharded drop-in cycles): segment b of
+// the list copies `words` 32-bit words from mapped pinned host memory (src), or
+// zeroes them (src 0), into device memory; the list itself sits in the same
+// pinned block.  One launch instead of a copy or fill per array.
+struct UpSeg {
+  uint64_t dst, src;
+  uint32_t words, pad;
+};
+__global__ __launch_bounds__(256) void k_upload(const UpSeg* __restrict__ segs) {
+  const UpSeg g = segs[blockIdx.x];
+  uint32_t* d = reinterpret_cast<uint32_t*>(g.dst);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(g.src);
+  for (uint32_t i = blockIdx.y * 256 + threadIdx.x; i < g.words; i += gridDim.y * 256) d[i] = src ? src[i] : 0u;
+}
+
 // Node-sharded class tables: sum the pair-level entries of the classes built
 // since the last call across ranks (each rank built them from its own existing
 // pods), in one all-gather on the engine stream.  Without the exchange yet it
@@ -7168,12 +7209,34 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
   if (!npc && !ntc) return true;
   const size_t Nn = std::max<uint32_t>(I.N, 1), NUn = std::max<uint32_t>(I.NU, 1);
   // (unsharded, the upload is not waited for: its host sources are held until the
-  // engine stream's next sync, and a late failure marks the context lost)
+  // engine stream's next sync, and a late failure marks the context lost; the
+  // copies and zero tails go out as ONE k_upload from a mapped pinned block)
+  std::vector<UpSeg> segs;
+  std::vector<uint8_t> pay;  // payloads, 16-byte aligned (offsets into the block after the list)
+  const bool fused = I.shards <= 1;
+  auto up = [&](auto& buf, size_t used, const auto& v) -> bool {  // dev_append
+    if (v.empty()) return true;
+    if (!fused) return dev_append(buf, used, v, s, err);
+    if (!buf.grow(used + v.size(), used, s, err)) return false;
+    const size_t o = (pay.size() + 15) & ~(size_t)15, b = v.size() * sizeof(v[0]);
+    pay.resize(o + b);
+    std::memcpy(pay.data() + o, v.data(), b);
+    segs.push_back(UpSeg{reinterpret_cast<uint64_t>(buf.p + used), o + 1, (uint32_t)(b / 4), 0});  // (src: offset + 1)
+    return true;
+  };
+  auto zero = [&](auto& buf, size_t used, size_t count) -> bool {  // dev_zero_tail
+    if (!count) return true;
+    if (!fused) return dev_zero_tail(buf, used, count, s, err);
+    if (!buf.grow(used + count, used, s, err)) return false;
+    segs.push_back(UpSeg{reinterpret_cast<uint64_t>(buf.p + used), 0, (uint32_t)(count * sizeof(buf.p[0]) / 4), 0});
+    return true;
+  };
   auto held = [&](auto v) {
     auto p = std::make_shared<decltype(v)>(std::move(v));
     I.hold.push_back(p);
     return p;
   };
+  PcStage pst{I.nct, 0, I.ncreq, 0, I.ncval, 0};  // (k_pc_build: the new classes' pool ranges)
   if (npc) {  // definitions, rebased onto the device pools
     auto pc = held(u.pc);
     auto ct = held(u.ct);
@@ -7185,15 +7248,17 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
       x.ns_off += (int32_t)I.ncval;
     }
     for (auto& x : *rq) x.val_off += (int32_t)I.ncval;
-    if (!dev_append(I.pcls_d, pc0, *pc, s, err) || !dev_append(I.cterm_d, I.nct, *ct, s, err) ||
-        !dev_append(I.creq_d, I.ncreq, *rq, s, err) || !dev_append(I.cval_d, I.ncval, *cv, s, err) ||
-        !dev_zero_tail(I.pc_cnt, (size_t)pc0 * Nn, (size_t)npc * Nn, s, err) ||
-        !dev_zero_tail(I.pc_dom, (size_t)pc0 * NUn, (size_t)npc * NUn, s, err) ||
-        !dev_zero_tail(I.pc_tot, (size_t)pc0 * KSG_MAX_TOPO, (size_t)npc * KSG_MAX_TOPO, s, err))
+    if (!up(I.pcls_d, pc0, *pc) || !up(I.cterm_d, I.nct, *ct) || !up(I.creq_d, I.ncreq, *rq) ||
+        !up(I.cval_d, I.ncval, *cv) || !zero(I.pc_cnt, (size_t)pc0 * Nn, (size_t)npc * Nn) ||
+        !zero(I.pc_dom, (size_t)pc0 * NUn, (size_t)npc * NUn) ||
+        !zero(I.pc_tot, (size_t)pc0 * KSG_MAX_TOPO, (size_t)npc * KSG_MAX_TOPO))
       return false;
     I.nct += (uint32_t)ct->size();
     I.ncreq += (uint32_t)rq->size();
     I.ncval += (uint32_t)cv->size();
+    pst.nt = (uint32_t)ct->size();
+    pst.nr = (uint32_t)rq->size();
+    pst.nv = (uint32_t)cv->size();
     I.npc += npc;
   }
   if (ntc) {  // per term class: one value per (key, value) pair, or per node for one-node keys
@@ -7209,17 +7274,40 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
       end = off[i] + len;
     }
     const uint32_t add = end - I.tc_used;
-    if (!dev_zero_tail(I.tc_val, I.tc_used, add, s, err) || !dev_append(I.tc_off_d, tc0, off, s, err) ||
-        !dev_append(I.tc_slot_d, tc0, tslot, s, err) || !dev_zero_tail(I.tc_tot, tc0, ntc, s, err))
+    if (!zero(I.tc_val, I.tc_used, add) || !up(I.tc_off_d, tc0, off) || !up(I.tc_slot_d, tc0, tslot) ||
+        !zero(I.tc_tot, tc0, ntc))
       return false;
     I.tc_used += add;
     I.tc_off_h.insert(I.tc_off_h.end(), off.begin(), off.end());
     I.tc_slot_h.insert(I.tc_slot_h.end(), u.tc_slot.begin(), u.tc_slot.end());
     I.ntc += ntc;
   }
+  if (!segs.empty()) {  // the fused upload: [list | payloads] in one mapped pinned block
+    const size_t lb = (segs.size() * sizeof(UpSeg) + 15) & ~(size_t)15, total = lb + pay.size();
+    size_t cap = 0;
+    uint8_t* blk = pinned_get(total, cap);
+    uint8_t* dv = blk ? pinned_dev(blk) : nullptr;
+    if (!dv) {
+      if (blk) pinned_put(blk, cap);
+      err = "add_classes: no mapped pinned memory";
+      return false;
+    }
+    uint32_t most = 0;
+    for (auto& g : segs) {
+      if (g.src) g.src = reinterpret_cast<uint64_t>(dv + lb + (g.src - 1));
+      most = std::max(most, g.words);
+    }
+    std::memcpy(blk, segs.data(), segs.size() * sizeof(UpSeg));
+    if (!pay.empty()) std::memcpy(blk + lb, pay.data(), pay.size());
+    I.hold.push_back(std::shared_ptr<const void>(blk, [cap](const void* q) {
+      Engine::pinned_put(const_cast<uint8_t*>(static_cast<const uint8_t*>(q)), cap);
+    }));
+    const dim3 ug((uint32_t)segs.size(), std::max<uint32_t>(std::min<uint32_t>((most + 4095) / 4096, 64), 1));
+    hipLaunchKernelGGL(k_upload, ug, dim3(256), 0, s, reinterpret_cast<const UpSeg*>(dv));
+  }
   DevCluster C = I.cluster();
   if (npc && I.pcap)
-    hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, pc0, npc);
+    hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, pc0, npc, pst);
   if (ntc && I.tcap) hipLaunchKernelGGL(k_tc_build, dim3((I.tcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, tc0);
   HIPCHK(hipGetLastError());
   if (npc) I.red_pc0 = std::min(I.red_pc0, pc0);
@@ -7246,7 +7334,8 @@ bool Engine::rebuild_class_tables(std::string& err) {
   }
   DevCluster C = I.cluster();
   if (I.npc && I.pcap)
-    hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, 0u, I.npc);
+    hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, 0u, I.npc,
+                       PcStage{0, 0xFFFFFFFFu, 0, 0, 0, 0});
   if (I.ntc && I.tcap) hipLaunchKernelGGL(k_tc_build, dim3((I.tcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, 0u);
   HIPCHK(hipGetLastError());
   if (I.npc) I.red_pc0 = 0;

@@ -1146,15 +1146,16 @@ struct Cluster {
     h.n_lk = h.n_ub = 0;
     bool ok = true;
     auto look = [&](int kind, uint64_t base, int slot, int use, int64_t weight, int aux) {
-      if (h.n_lk >= KSG_LK_MAX || base > 0x7FFFFFFFull || weight > INT32_MAX || weight < INT32_MIN) { ok = false; return; }
+      if (h.n_lk >= KSG_LK_MAX || base > 0x7FFFFFFFull || weight > INT32_MAX || weight < INT32_MIN || slot < -1 ||
+          slot > 254 || kind < 0 || kind > 255 || use < 0 || use > 255 || aux < 0 || aux > 255) {
+        ok = false;
+        return;
+      }
       ksg_look& e = h.lk[h.n_lk++];
       e = ksg_look{};
       e.base = (int32_t)base;
       e.weight = (int32_t)weight;
-      e.slot = (int32_t)slot;
-      e.kind = (int32_t)kind;
-      e.use = (int32_t)use;
-      e.aux = aux;
+      e.sku = (uint32_t)(slot + 1) | (uint32_t)kind << 8 | (uint32_t)use << 16 | (uint32_t)aux << 24;
     };
     auto pc_look = [&](int32_t cls, int32_t nub, int slot, int use, int64_t weight, int aux) {
       if (cls < 0) {
@@ -1227,10 +1228,11 @@ struct Cluster {
     uint64_t rd = 0, md = 0, nrd = 0, nmd = 0;
     for (int i = 0; i < h.n_lk; ++i) {  // (PC_NODE / TC_NODE entries are node-level: nd_rd)
       const ksg_look& e = h.lk[i];
-      if (e.kind == KLK_PC_DOM) rd |= ksg_tab_bloom(1, (uint32_t)e.base / (uint32_t)enc_NU);
-      else if (e.kind == KLK_TC_DOM) rd |= ksg_tab_bloom(2, (uint32_t)e.base);
-      else if (e.kind == KLK_PC_NODE) nrd |= ksg_tab_bloom(4, (uint32_t)(e.base / (uint64_t)enc_N));
-      else if (e.kind == KLK_TC_NODE) nrd |= ksg_tab_bloom(5, (uint32_t)e.base);
+      const int32_t kind = ksg_lk_kind(e.sku);
+      if (kind == KLK_PC_DOM) rd |= ksg_tab_bloom(1, (uint32_t)e.base / (uint32_t)enc_NU);
+      else if (kind == KLK_TC_DOM) rd |= ksg_tab_bloom(2, (uint32_t)e.base);
+      else if (kind == KLK_PC_NODE) nrd |= ksg_tab_bloom(4, (uint32_t)(e.base / (uint64_t)enc_N));
+      else if (kind == KLK_TC_NODE) nrd |= ksg_tab_bloom(5, (uint32_t)e.base);
     }
     for (int c = 0; c < h.n_tsc_filter; ++c)  // minMatchNum candidates (pc_dom)
       if (h.tsc[c].eff_cls >= 0) rd |= ksg_tab_bloom(1, (uint32_t)h.tsc[c].eff_cls);
@@ -3257,7 +3259,12 @@ struct Cluster {
     if (!eng->keep_outputs(q, 1, err) || !eng->run_queue(q, 1, commit, err)) return false;
     if (!commit && view_prefetch && !prefetch_view(q)) return false;
     lap(4);
-    if (!eng->summaries(q, 1, &out, err) || !eng->sync(err)) return false;
+    if (!commit && pview.block && pview.q == (int64_t)q) {  // (the prefetched view carries the summary)
+      if (!eng->sync(err)) return false;
+      std::memcpy(&out, pview.block + pview.lay.off_sum, sizeof(out));
+    } else if (!eng->summaries(q, 1, &out, err) || !eng->sync(err)) {
+      return false;
+    }
     lap(5);
     if (!preempt(q, out)) return false;  // PostFilter of an unschedulable pod
     lap(6);

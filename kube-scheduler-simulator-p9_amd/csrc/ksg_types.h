@@ -163,15 +163,22 @@ typedef struct ksg_vchk {
 typedef struct ksg_look {
   int32_t base;    // the table entry of value 0 / node 0 (kind)
   int32_t weight;  // KLU_RAW: signed multiplier
-  // (every field a 32-bit word: the device reads the plan with scalar loads, which
-  // cannot fetch a byte at an unaligned offset — a byte field became a vector load
-  // whose vmcnt(0) wait serialised every class-table read before it)
-  int32_t slot;    // topology slot whose value selects the entry (no value: count 0)
-  int32_t kind;    // KLK_*
-  int32_t use;     // KLU_*
-  int32_t aux;     // KLU_PTSF: the filter constraint
+  // slot + 1 | kind << 8 | use << 16 | aux << 24 in ONE 32-bit word (ksg_lk_*):
+  // the device reads the plan with scalar loads (which cannot fetch a byte at an
+  // unaligned offset), and the unrolled plan's fields are live in SGPRs across
+  // the evaluation — four words per entry there spilled to VGPR lanes.
+  //   slot: topology slot whose value selects the entry (no value: count 0)
+  //   kind: KLK_*; use: KLU_*; aux: KLU_PTSF's filter constraint
+  uint32_t sku;
+  int32_t pad;
 } ksg_look;
 #define KSG_LK_MAX 24
+#ifdef __cplusplus  // (constexpr: host and device functions alike under hipcc)
+constexpr int32_t ksg_lk_slot(uint32_t sku) { return (int32_t)(sku & 0xFFu) - 1; }
+constexpr int32_t ksg_lk_kind(uint32_t sku) { return (int32_t)((sku >> 8) & 0xFFu); }
+constexpr int32_t ksg_lk_use(uint32_t sku) { return (int32_t)((sku >> 16) & 0xFFu); }
+constexpr int32_t ksg_lk_aux(uint32_t sku) { return (int32_t)(sku >> 24); }
+#endif
 #define KLK_NONE 0      // count 0 (class counts nothing)
 #define KLK_PC_NODE 1   // pc_cnt[base + node]
 #define KLK_PC_DOM 2    // pc_dom[base + value]

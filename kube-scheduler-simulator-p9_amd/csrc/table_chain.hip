@@ -811,11 +811,13 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
       lks[i] = pre->lks[i];
     } else if (i < h->n_lk) {
       const ksg_look& e = h->lk[i];
-      const int32_t v = tv(e.slot);
+      const uint32_t sku = e.sku;
+      const int32_t kind = ksg_lk_kind(sku);
+      const int32_t v = tv(ksg_lk_slot(sku));
       lks[i] = v;
-      if (e.kind != KLK_NONE) {
-        const uint32_t at = (uint32_t)e.base + ((e.kind == KLK_PC_NODE || e.kind == KLK_TC_NODE) ? nn : (uint32_t)(v < 0 ? 0 : v));
-        lkv[i] = ld_tab<MODE>((e.kind == KLK_PC_NODE ? C.T.pc_cnt : e.kind == KLK_PC_DOM ? C.T.pc_dom : C.T.tc_val) + at);
+      if (kind != KLK_NONE) {
+        const uint32_t at = (uint32_t)e.base + ((kind == KLK_PC_NODE || kind == KLK_TC_NODE) ? nn : (uint32_t)(v < 0 ? 0 : v));
+        lkv[i] = ld_tab<MODE>((kind == KLK_PC_NODE ? C.T.pc_cnt : kind == KLK_PC_DOM ? C.T.pc_dom : C.T.tc_val) + at);
       }
     }
   }
@@ -865,13 +867,14 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   for (int i = 0; i < LK; ++i) {
     if (i >= h->n_lk) continue;
     const ksg_look& e = h->lk[i];
+    const uint32_t sku = e.sku;
     const int32_t v = lks[i];
     const int32_t x = v < 0 ? 0 : lkv[i];
-    switch (e.use) {
+    switch (ksg_lk_use(sku)) {
       case KLU_PTSF:
 #pragma unroll
         for (int c = 0; c < TS; ++c)
-          if (c == e.aux) ptsm[c] = x;
+          if (c == ksg_lk_aux(sku)) ptsm[c] = x;
         break;
       case KLU_PTSS: pts_cnt += x; break;
       case KLU_AFF:
@@ -2368,24 +2371,85 @@ __global__ __launch_bounds__(kBlock) void k_flush_appends(DevCluster C, ChainArg
 
 // ---- class tables: build from the existing-pod table
 // pod classes [c0, c0 + nc): every live existing pod matching a class adds to its tables
-__global__ void k_pc_build(DevCluster C, uint32_t c0, uint32_t nc) {
+// One thread per existing-pod row; pc_add's counts, aggregated per wave before
+// the atomics (round 5): pc_tot is ONE address per (class, slot) and a zone-like
+// slot has a few domains, so per-row atomics serialised on a handful of L2
+// addresses (≈ 30 µs per new class at 200,000 rows in the drop-in cycle).  A
+// slot whose every value sits on one node keeps per-row atomics.
+// The new classes' definitions (their pool ranges, appended together by
+// add_classes) are staged in LDS first when they fit: the per-row selector walk
+// then reads LDS instead of a chain of dependent global loads (class -> term ->
+// requirement -> values) per row.  st.nt == UINT32_MAX: read the pools in place.
+struct PcStage {
+  uint32_t t0, nt, r0, nr, v0, nv;
+};
+#define KSG_PCB_C 16
+#define KSG_PCB_T 64
+#define KSG_PCB_R 128
+#define KSG_PCB_V 512
+__global__ __launch_bounds__(256) void k_pc_build(DevCluster C, uint32_t c0, uint32_t nc, PcStage st) {
+  __shared__ ksg_pclass s_pc[KSG_PCB_C];
+  __shared__ ksg_cterm s_ct[KSG_PCB_T];
+  __shared__ ksg_req s_rq[KSG_PCB_R];
+  __shared__ int32_t s_cv[KSG_PCB_V];
+  const bool staged = st.nt != 0xFFFFFFFFu && nc <= KSG_PCB_C && st.nt <= KSG_PCB_T && st.nr <= KSG_PCB_R &&
+                      st.nv <= KSG_PCB_V;
+  const ksg_pclass* PCs = C.T.pcls;
+  const ksg_cterm* CTs = C.T.cterm;
+  const ksg_req* RQs = C.T.creq;
+  const int32_t* CVs = C.T.cval;
+  if (staged) {
+    for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) s_pc[i] = C.T.pcls[c0 + i];
+    for (uint32_t i = threadIdx.x; i < st.nt; i += blockDim.x) s_ct[i] = C.T.cterm[st.t0 + i];
+    for (uint32_t i = threadIdx.x; i < st.nr; i += blockDim.x) s_rq[i] = C.T.creq[st.r0 + i];
+    for (uint32_t i = threadIdx.x; i < st.nv; i += blockDim.x) s_cv[i] = C.T.cval[st.v0 + i];
+    __syncthreads();
+    PCs = s_pc - c0;  // (indexed with the pools' absolute offsets, which lie in the staged ranges)
+    CTs = s_ct - st.t0;
+    RQs = s_rq - st.r0;
+    CVs = s_cv - st.v0;
+  }
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= C.tcounts[0]) return;
-  const uint32_t fl = C.ptflags[p];
-  if (fl & KEF_DELETED) return;
-  const int32_t node = C.ptnode[p], ns = C.ptns[p];
-  auto vid = [&](int32_t k) -> int32_t { return (k >= 0 && (uint32_t)k < C.pkeys) ? C.ptlab[(size_t)k * C.pcap + p] : -1; };
+  bool live = p < C.tcounts[0];
+  const uint32_t pp = live ? p : 0u;
+  const uint32_t fl = C.ptflags[pp];
+  live = live && !(fl & KEF_DELETED);
+  const int32_t node = C.ptnode[pp], ns = C.ptns[pp];
+  auto vid = [&](int32_t k) -> int32_t { return (k >= 0 && (uint32_t)k < C.pkeys) ? C.ptlab[(size_t)k * C.pcap + pp] : -1; };
   int32_t nv[KSG_MAX_TOPO];
-  node_slot_vids(C, (uint32_t)node, nv);
+  node_slot_vids(C, live ? (uint32_t)node : 0u, nv);
+  const DevTables& T = C.T;
   for (uint32_t c = c0; c < c0 + nc; ++c) {
-    const ksg_pclass& pc = C.T.pcls[c];
-    if (pc.excl_term && (fl & KEF_TERMINATING)) continue;
-    bool ok = pc.n_terms > 0;
+    const ksg_pclass pc = PCs[c];
+    bool ok = live && pc.n_terms > 0 && !(pc.excl_term && (fl & KEF_TERMINATING));
     for (int i = 0; i < pc.n_terms && ok; ++i) {
-      const ksg_cterm& t = C.T.cterm[pc.term_off + i];
-      ok = (t.ns_all || in_list(ns, C.T.cval + t.ns_off, t.ns_cnt)) && sel_eval(t.sel, C.T.creq, C.T.cval, vid);
+      const ksg_cterm& t = CTs[pc.term_off + i];
+      ok = (t.ns_all || in_list(ns, CVs + t.ns_off, t.ns_cnt)) && sel_eval(t.sel, RQs, CVs, vid);
     }
-    if (ok) pc_add(C, (int32_t)c, (uint32_t)node, +1, nv);
+    if (c >= T.npc) continue;  // (pc_add's guard)
+    if (ok) atomicAdd(&T.pc_cnt[(size_t)c * C.N + (uint32_t)node], 1);
+#pragma unroll
+    for (int sl = 0; sl < KSG_MAX_TOPO; ++sl) {
+      const bool m = ok && nv[sl] >= 0;
+      const uint64_t b = __ballot(m);
+      if (!b) continue;
+      if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((unsigned long long)b) - 1))
+        atomicAdd(&T.pc_tot[(size_t)c * KSG_MAX_TOPO + sl], (int)__popcll(b));
+      if (C.nubv[sl] < 0) continue;
+      int32_t* dom = T.pc_dom + (size_t)c * T.NU + (uint32_t)C.nubv[sl];
+      if ((T.uniq >> sl) & 1u) {
+        if (m) atomicAdd(dom + nv[sl], 1);
+        continue;
+      }
+      uint64_t left = b;  // one atomic per distinct domain of the wave
+      while (left) {
+        const int ld = __ffsll((unsigned long long)left) - 1;
+        const int32_t lv = __builtin_amdgcn_readlane(nv[sl], ld);
+        const uint64_t same = __ballot(m && nv[sl] == lv);
+        if ((threadIdx.x & 63u) == (uint32_t)ld) atomicAdd(dom + lv, (int)__popcll(same));
+        left &= ~same;
+      }
+    }
   }
 }
 // term classes [u0, ...): every live existing pod's term of such a class

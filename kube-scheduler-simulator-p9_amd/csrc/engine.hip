@@ -2313,13 +2313,22 @@ struct PodLite {  // the fields of ksg_prog the Fit/BA evaluation reads (LDS-sta
   uint32_t flags;
 };
 
+// staging block [PodLite | pad | program]: the program 16-byte aligned
+constexpr size_t kPlOff = (sizeof(PodLite) + 15) & ~(size_t)15;
+static_assert(sizeof(PodLite) % 4 == 0, "PodLite words");
 __global__ void k_place_program(const uint8_t* __restrict__ src, uint32_t bytes, uint8_t* dst, uint64_t* off_slot,
                                 uint64_t off, void* plite_slot, int32_t* prow_slot, int32_t row, ksg_pod_summary* sum,
                                 DevProfile F) {
   const uint32_t t = threadIdx.x;
-  const uint8_t* prog = src + sizeof(PodLite);
-  for (uint32_t i = t; i < bytes; i += blockDim.x) dst[i] = prog[i];
-  for (uint32_t i = t; i < (uint32_t)sizeof(PodLite); i += blockDim.x) reinterpret_cast<uint8_t*>(plite_slot)[i] = src[i];
+  const uint8_t* prog = src + kPlOff;
+  // 16-byte pieces, all issued before any is stored (src may be pinned host
+  // memory: one PCIe round trip, not one per byte-loop iteration)
+  const uint32_t n16 = bytes / 16;
+  for (uint32_t i = t; i < n16; i += blockDim.x)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(prog)[i];
+  for (uint32_t i = n16 * 16 + t; i < bytes; i += blockDim.x) dst[i] = prog[i];
+  for (uint32_t i = t; i < (uint32_t)(sizeof(PodLite) / 4); i += blockDim.x)
+    reinterpret_cast<uint32_t*>(plite_slot)[i] = reinterpret_cast<const uint32_t*>(src)[i];
   if (t == 0) {
     *off_slot = off;
     *prow_slot = row;
@@ -6697,14 +6706,14 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
   // One pinned staging block [PodLite | program] -> one copy, and one kernel that
   // places it (program, offset, PodLite, table row, fresh summary): no wait here.
   // The block is reused once its previous copy has completed (an event).
-  const size_t sbytes = sizeof(PodLite) + prog.size();
+  const size_t sbytes = kPlOff + prog.size();
   {  // (round 5) zero-copy: k_place_program reads a mapped pinned block, held until the next sync
     size_t cap = 0;
     uint8_t* blk = pinned_get(sbytes, cap);
     uint8_t* dv = blk ? pinned_dev(blk) : nullptr;
     if (dv) {
       std::memcpy(blk, &pl, sizeof(pl));
-      std::memcpy(blk + sizeof(PodLite), prog.data(), prog.size());
+      std::memcpy(blk + kPlOff, prog.data(), prog.size());
       I.hold.push_back(std::shared_ptr<const void>(blk, [cap](const void* b) {
         Engine::pinned_put(const_cast<uint8_t*>(static_cast<const uint8_t*>(b)), cap);
       }));
@@ -6743,7 +6752,7 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
   }
   if (!I.apdev.grow(sbytes, 0, s, err)) return false;
   std::memcpy(I.apstage, &pl, sizeof(pl));
-  std::memcpy(I.apstage + sizeof(PodLite), prog.data(), prog.size());
+  std::memcpy(I.apstage + kPlOff, prog.data(), prog.size());
   HIPCHK(hipMemcpyAsync(I.apdev.p, I.apstage, sbytes, hipMemcpyHostToDevice, s));
   HIPCHK(hipEventRecord(I.apstage_ev, s));
   hipLaunchKernelGGL(k_place_program, dim3(1), dim3(256), 0, s, I.apdev.p, (uint32_t)prog.size(), I.progs.p + off,

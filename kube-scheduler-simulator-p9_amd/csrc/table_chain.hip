@@ -2398,16 +2398,31 @@ __global__ __launch_bounds__(256) void k_pc_build(DevCluster C, uint32_t c0, uin
   const ksg_cterm* CTs = C.T.cterm;
   const ksg_req* RQs = C.T.creq;
   const int32_t* CVs = C.T.cval;
-  if (staged) {
-    for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) s_pc[i] = C.T.pcls[c0 + i];
-    for (uint32_t i = threadIdx.x; i < st.nt; i += blockDim.x) s_ct[i] = C.T.cterm[st.t0 + i];
-    for (uint32_t i = threadIdx.x; i < st.nr; i += blockDim.x) s_rq[i] = C.T.creq[st.r0 + i];
+  uint32_t cbase = 0;
+  if (staged) {  // (copies rebased onto the staged ranges: every offset indexes the LDS arrays from 0)
+    for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
+      ksg_pclass x = C.T.pcls[c0 + i];
+      x.term_off -= (int32_t)st.t0;
+      s_pc[i] = x;
+    }
+    for (uint32_t i = threadIdx.x; i < st.nt; i += blockDim.x) {
+      ksg_cterm x = C.T.cterm[st.t0 + i];
+      x.sel.req_off -= (int32_t)st.r0;
+      x.ns_off -= (int32_t)st.v0;
+      s_ct[i] = x;
+    }
+    for (uint32_t i = threadIdx.x; i < st.nr; i += blockDim.x) {
+      ksg_req x = C.T.creq[st.r0 + i];
+      x.val_off -= (int32_t)st.v0;
+      s_rq[i] = x;
+    }
     for (uint32_t i = threadIdx.x; i < st.nv; i += blockDim.x) s_cv[i] = C.T.cval[st.v0 + i];
     __syncthreads();
-    PCs = s_pc - c0;  // (indexed with the pools' absolute offsets, which lie in the staged ranges)
-    CTs = s_ct - st.t0;
-    RQs = s_rq - st.r0;
-    CVs = s_cv - st.v0;
+    PCs = s_pc;
+    CTs = s_ct;
+    RQs = s_rq;
+    CVs = s_cv;
+    cbase = c0;
   }
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   bool live = p < C.tcounts[0];
@@ -2420,7 +2435,7 @@ __global__ __launch_bounds__(256) void k_pc_build(DevCluster C, uint32_t c0, uin
   node_slot_vids(C, live ? (uint32_t)node : 0u, nv);
   const DevTables& T = C.T;
   for (uint32_t c = c0; c < c0 + nc; ++c) {
-    const ksg_pclass pc = PCs[c];
+    const ksg_pclass pc = PCs[c - cbase];
     bool ok = live && pc.n_terms > 0 && !(pc.excl_term && (fl & KEF_TERMINATING));
     for (int i = 0; i < pc.n_terms && ok; ++i) {
       const ksg_cterm& t = CTs[pc.term_off + i];

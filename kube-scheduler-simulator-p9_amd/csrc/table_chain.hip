@@ -2371,11 +2371,8 @@ __global__ __launch_bounds__(kBlock) void k_flush_appends(DevCluster C, ChainArg
 
 // ---- class tables: build from the existing-pod table
 // pod classes [c0, c0 + nc): every live existing pod matching a class adds to its tables
-// One thread per existing-pod row; pc_add's counts, aggregated per wave before
-// the atomics (round 5): pc_tot is ONE address per (class, slot) and a zone-like
-// slot has a few domains, so per-row atomics serialised on a handful of L2
-// addresses (≈ 30 µs per new class at 200,000 rows in the drop-in cycle).  A
-// slot whose every value sits on one node keeps per-row atomics.
+// One thread per existing-pod row; pc_add's counts, with pc_tot (ONE address per
+// (class, slot)) counted per wave before its atomic.
 // The new classes' definitions (their pool ranges, appended together by
 // add_classes) are staged in LDS first when they fit: the per-row selector walk
 // then reads LDS instead of a chain of dependent global loads (class -> term ->
@@ -2450,20 +2447,9 @@ __global__ __launch_bounds__(256) void k_pc_build(DevCluster C, uint32_t c0, uin
       if (!b) continue;
       if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((unsigned long long)b) - 1))
         atomicAdd(&T.pc_tot[(size_t)c * KSG_MAX_TOPO + sl], (int)__popcll(b));
-      if (C.nubv[sl] < 0) continue;
-      int32_t* dom = T.pc_dom + (size_t)c * T.NU + (uint32_t)C.nubv[sl];
-      if ((T.uniq >> sl) & 1u) {
-        if (m) atomicAdd(dom + nv[sl], 1);
-        continue;
-      }
-      uint64_t left = b;  // one atomic per distinct domain of the wave
-      while (left) {
-        const int ld = __ffsll((unsigned long long)left) - 1;
-        const int32_t lv = __builtin_amdgcn_readlane(nv[sl], ld);
-        const uint64_t same = __ballot(m && nv[sl] == lv);
-        if ((threadIdx.x & 63u) == (uint32_t)ld) atomicAdd(dom + lv, (int)__popcll(same));
-        left &= ~same;
-      }
+      // (per-row domain atomics: a per-wave loop over the distinct domains measured
+      // slower — 38 vs 32 µs per build, up to 170 on many-valued slots)
+      if (m && C.nubv[sl] >= 0) atomicAdd(T.pc_dom + (size_t)c * T.NU + (uint32_t)C.nubv[sl] + nv[sl], 1);
     }
   }
 }

@@ -5,6 +5,8 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_cycle_gpu.py tests/test_events_gpu.py tests/test_plugin_api_gpu.py -m gpu > gpurun_out/r05_final_b_gputest.log 2>&1 || { tail -30 gpurun_out/r05_final_b_gputest.log; exit 1; }
+tail -1 gpurun_out/r05_final_b_gputest.log
 bash tools/pmc_config.sh 3 r05 > gpurun_out/r05_pmc3.log 2>&1 || { tail -20 gpurun_out/r05_pmc3.log; exit 1; }
 bash tools/pmc_config.sh 4 r05 > gpurun_out/r05_pmc4.log 2>&1 || { tail -20 gpurun_out/r05_pmc4.log; exit 1; }
 bash tools/prof_config.sh 3 > gpurun_out/r05_cfg3_kernel_stats.csv 2> gpurun_out/r05_kt3.err || { tail -20 gpurun_out/r05_kt3.err; exit 1; }

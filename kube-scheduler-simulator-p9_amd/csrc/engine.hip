@@ -5482,6 +5482,7 @@ struct Engine::Impl {
   int win_mblocks = 0;           // ... with dedicated merge blocks (KSG_WIN_MB=1; the last tile block merges: measured faster)
   int view_copy = 0;             // cycle view: 1 = the per-node arrays by a copy (KSG_VIEW_COPY), 0 = written by k_view
   int run_overlap = 0;           // k_chain_run: pod k+1's class-table reads during pod k's hand-offs (KSG_RUN_OVERLAP=1; measured no faster)
+  int run_defer = 1;             // k_chain_run: the owner's independent node-level assume deferred (KSG_RUN_DEFER=0: off)
   int win_split = 1;             // ... split hand-over: keys staged while the prior steps run (KSG_WIN_SPLIT=0: one counter)
   int win_pfix = 0;              // ... the replay evaluates the prior step itself (KSG_WIN_PFIX=1; measured slower)
   uint64_t win_runs = 0, win_fallbacks = 0;  // diagnostic: persistent window launches / not co-resident
@@ -5656,6 +5657,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (const char* e = std::getenv("KSG_WIN_PFIX")) I.win_pfix = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_SPLIT")) I.win_split = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_RUN_OVERLAP")) I.run_overlap = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_RUN_DEFER")) I.run_defer = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_VIEW_COPY")) I.view_copy = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_RUN_SPIN")) I.run_spin = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("KSG_RUN_WAIT_US"))
@@ -7749,7 +7751,8 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         const uint32_t grid = (l512 ? nb512 : I.cnblk) + 1;  // node blocks + the committer
         uint32_t* const hv = I.hverdict;
         __atomic_store_n(hv, 0u, __ATOMIC_RELEASE);  // (the previous segment's verdict was read)
-        const RunCtl RC{grid + I.run_need_extra, I.run_wait_us * 100u, I.run_lag, hv, I.run_spin, I.run_overlap ? 1u : 0u};
+        const RunCtl RC{grid + I.run_need_extra, I.run_wait_us * 100u, I.run_lag, hv, I.run_spin, I.run_overlap ? 1u : 0u,
+                        I.run_defer ? 1u : 0u};
         const dim3 gr(grid), bk(kChain);
         if (l512) {
           ChainArgs R5 = RA;

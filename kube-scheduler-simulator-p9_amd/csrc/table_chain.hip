@@ -1730,6 +1730,7 @@ struct RunCtl {
   uint32_t* host_verdict;  // pinned host word the deciding block writes (the host polls it), or null
   uint32_t spin;           // polls before a block gives up (kRunSpin; tests force an abort with few)
   uint32_t overlap;        // issue pod k+1's class-table reads during pod k's hand-offs (KSG_RUN_OVERLAP)
+  uint32_t defer;          // the owner's node-level assume after the next partial record when independent (KSG_RUN_DEFER)
 };
 // Pod j+1 (header n) may read the class tables before pod j's (header h) assume:
 // it reads none of the pair-level nor node-level entries pod j writes (its row,
@@ -1939,6 +1940,18 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
   __syncthreads();
   uint32_t wait_for = 0;  // the flag value this block needs before its next class-table read (0: none)
   uint32_t owned = 0;     // this block applied a node-level assume not yet drained before a class-table read
+  // The owner's node-level assume deferred past the next pod's evaluation when
+  // that pod reads none of the entries it writes (node-level Bloom filters): its
+  // atomics then go out after the next partial record (their acknowledgement
+  // overlaps the partials' hand-off) instead of being drained at the start of
+  // the next evaluation, which made the owner block the last one of the pod
+  // (KSG_RUN_DEFER=0: drained as before).
+  uint32_t dfr_node = 0xFFFFFFFFu;  // (per item lane: its deferred item, this node)
+  int32_t dfr_cls = -1;
+  ksg_exist_term dfr_term;
+  dfr_term.cls = -1;
+  bool dfr_is_cls = false;
+  bool dfr_any = false;  // (block-uniform: some lane holds a deferred item)
   // Overlap (KSG_RUN_OVERLAP): when pod k+1 is independent of pod k (run_indep),
   // its class-table reads are issued right after pod k's partial record goes out
   // and stay in flight across pod k's fold, selection and assume; pod k+1 then
@@ -1996,6 +2009,19 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
           st_sc1(g + (j + 1) * kGF, gran(tag, (uint32_t)(rr.reg[c] >> 32)));
           j += 2;
         }
+    }
+    if (dfr_node != 0xFFFFFFFFu) {  // (the previous pod's deferred node-level items)
+      int32_t v[KSG_MAX_TOPO];
+      const uint32_t ln = dfr_node % BT;
+#pragma unroll
+      for (int s2 = 0; s2 < KSG_MAX_TOPO; ++s2) v[s2] = (uint32_t)s2 < C.n_topo ? L.tv[s2 * BT + ln] : -1;
+      if (dfr_is_cls) pc_add(C, dfr_cls, dfr_node, +1, v, TP_NODE);
+      else tc_add(C, dfr_term, dfr_node, +1, v, TP_NODE);
+      dfr_node = 0xFFFFFFFFu;
+    }
+    if (dfr_any) {  // (drained before the next class-table read that may see them)
+      owned = 1;
+      dfr_any = false;
     }
     RS(30);
     // diagnostic: the latest block's partial store (absolute clock, per pod parity)
@@ -2170,7 +2196,17 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
         row.podcnt += 1;
         if (rpre_ok) row_pre<ROWM, PM>(row, F, view(P + PO[A.q + 1]).h, C.R, rpre);  // (its row changed)
       }
-      if (C.T.on && threadIdx.x < nitems) {
+      const bool defer = R.defer && nh && !tnext && nitems <= (uint32_t)BT && (h->nd_md & nh->nd_rd) == 0;
+      if (defer) {
+        if (C.T.on && threadIdx.x < nitems) {
+          dfr_node = (uint32_t)node;
+          dfr_is_cls = threadIdx.x < npm;
+          dfr_cls = it_cls;
+          dfr_term = it_term;
+        }
+        dfr_any = C.T.on && nitems > 0;
+        owned = 0;
+      } else if (C.T.on && threadIdx.x < nitems) {
         int32_t v[KSG_MAX_TOPO];
 #pragma unroll
         for (int s = 0; s < KSG_MAX_TOPO; ++s) v[s] = (uint32_t)s < C.n_topo ? L.tv[s * BT + ln] : -1;
@@ -2636,29 +2672,65 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
     *reinterpret_cast<Engine::ViewRows*>(hout + V.off_rows) = RW;
     *reinterpret_cast<ksg_pod_summary*>(hout + V.off_sum) = *sum;
   }
-  if (act) {
-  reinterpret_cast<int8_t*>(hout + V.off_fail_pos)[n] = (int8_t)fp;
-  reinterpret_cast<int8_t*>(hout + V.off_fail_code)[n] = (int8_t)fc;
-  reinterpret_cast<uint16_t*>(hout + V.off_fail_msg)[n] = (uint16_t)msg;
-  const bool feasible = code == KSG_FILTER_PASS;
-  const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
-  bool pts_keys = false, pk_done = false;
-  for (int pos = 0; pos < F.n; ++pos) {
-    const int32_t s = score[(size_t)pos * C.N + n];
-    view_put(hout, RW.off[pos], RW.bytes[pos], n, s);
-    const int r = V.norm_row[pos];
-    if (r < 0) continue;
-    int64_t v = 0;
-    if (feasible) {
-      if (F.plugins[pos] == KP_PTS && !pk_done) {
-        pts_keys = ns > 0 && pts_has_keys(C, PV, nf, nf + ns, n);
-        pk_done = true;
-      }
-      bool use;
-      v = normalize_pos(F.plugins[pos], h, s, sum->max_score[pos], sum->min_score[pos], sum->ipa_flags, pts_keys, use);
-    }
-    view_put(hout, RW.off[KSG_MAX_PLUGINS + r], RW.bytes[KSG_MAX_PLUGINS + r], n, v);
+  // The block's per-node arrays are staged in LDS (one segment of 256 entries
+  // per array, in the block layout's order) and written out in 16-byte pieces:
+  // wide writes over the host link instead of one 1-4 byte write per lane (round 5).
+  __shared__ __attribute__((aligned(16))) uint8_t vst[256 * (4 + 8 * KSG_MAX_PLUGINS)];
+  const uint32_t tid = threadIdx.x;
+  auto lput = [&](uint32_t loff, uint8_t w, int64_t v) {
+    if (w == 1) reinterpret_cast<int8_t*>(vst + loff)[tid] = (int8_t)(v < -128 ? -128 : v > 127 ? 127 : v);
+    else reinterpret_cast<int32_t*>(vst + loff)[tid] = (int32_t)v;
+  };
+  uint32_t lraw[KSG_MAX_PLUGINS], lnorm[KSG_MAX_PLUGINS];  // LDS segment offsets (uniform)
+  uint32_t lo = 1024;
+  for (int d = 0; d < KSG_MAX_PLUGINS; ++d) {
+    lraw[d] = lo;
+    if (d < F.n) lo += 256u * RW.bytes[d];
   }
+  for (int r = 0; r < KSG_MAX_PLUGINS; ++r) {
+    lnorm[r] = lo;
+    if ((uint32_t)r < V.n_norm) lo += 256u * RW.bytes[KSG_MAX_PLUGINS + r];
+  }
+  if (act) {
+    reinterpret_cast<int8_t*>(vst)[tid] = (int8_t)fp;
+    reinterpret_cast<int8_t*>(vst + 256)[tid] = (int8_t)fc;
+    reinterpret_cast<uint16_t*>(vst + 512)[tid] = (uint16_t)msg;
+    const bool feasible = code == KSG_FILTER_PASS;
+    const int nf = h->n_tsc_filter, ns = h->n_tsc_score;
+    bool pts_keys = false, pk_done = false;
+    for (int pos = 0; pos < F.n; ++pos) {
+      const int32_t s = score[(size_t)pos * C.N + n];
+      lput(lraw[pos], RW.bytes[pos], s);
+      const int r = V.norm_row[pos];
+      if (r < 0) continue;
+      int64_t v = 0;
+      if (feasible) {
+        if (F.plugins[pos] == KP_PTS && !pk_done) {
+          pts_keys = ns > 0 && pts_has_keys(C, PV, nf, nf + ns, n);
+          pk_done = true;
+        }
+        bool use;
+        v = normalize_pos(F.plugins[pos], h, s, sum->max_score[pos], sum->min_score[pos], sum->ipa_flags, pts_keys, use);
+      }
+      lput(lnorm[r], RW.bytes[KSG_MAX_PLUGINS + r], v);
+    }
+  }
+  __syncthreads();
+  {
+    const uint32_t n0 = blockIdx.x * blockDim.x, cnt = C.N - n0 < blockDim.x ? C.N - n0 : blockDim.x;
+    auto flush = [&](uint32_t loff, uint32_t dst, uint32_t w) {  // entries [n0, n0 + cnt) of one array
+      uint8_t* d = hout + dst + (size_t)n0 * w;
+      const uint8_t* src = vst + loff;
+      const uint32_t bytes = cnt * w, n16 = bytes / 16;
+      for (uint32_t i = tid; i < n16; i += blockDim.x)
+        reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(src)[i];
+      for (uint32_t i = n16 * 16 + tid; i < bytes; i += blockDim.x) d[i] = src[i];
+    };
+    flush(0, V.off_fail_pos, 1);
+    flush(256, V.off_fail_code, 1);
+    flush(512, V.off_fail_msg, 2);
+    for (int d = 0; d < F.n; ++d) flush(lraw[d], RW.off[d], RW.bytes[d]);
+    for (uint32_t r = 0; r < V.n_norm; ++r) flush(lnorm[r], RW.off[KSG_MAX_PLUGINS + r], RW.bytes[KSG_MAX_PLUGINS + r]);
   }
   // direct: the last block to finish copies the message-slot table (every
   // block's inserts done) into the host block, so no copy launch follows

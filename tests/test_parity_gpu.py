@@ -236,8 +236,8 @@ RUN_CASES = [
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{}, {"KSG_RUN_MIN": "1"}, {"KSG_RUN_BT": "512"}, {"KSG_RUN_LAG": "4"},
-                                 {"KSG_RUN_OVERLAP": "1"}],
-                         ids=["default", "min1", "bt512", "lag", "overlap"])
+                                 {"KSG_RUN_OVERLAP": "1"}, {"KSG_RUN_DEFER": "0"}],
+                         ids=["default", "min1", "bt512", "lag", "overlap", "no-defer"])
 @pytest.mark.parametrize("name,c,sizes,keep", RUN_CASES, ids=[c[0] for c in RUN_CASES])
 def test_persistent_segments_match_oracle(monkeypatch, env, name, c, sizes, keep):
     """Persistent segments (k_chain_run: the pod loop inside one launch, gates
@@ -247,7 +247,9 @@ def test_persistent_segments_match_oracle(monkeypatch, env, name, c, sizes, keep
     also with one-pod segments allowed (KSG_RUN_MIN=1), 512-thread blocks, and a
     committer delayed ~14 us per pod (KSG_RUN_LAG=4: longer than a pod's evaluation,
     so the node blocks run a pod ahead of it and rewrite the granules of the pod
-    after the one it reads; the parity-slotted granules keep those it reads)."""
+    after the one it reads; the parity-slotted granules keep those it reads), and
+    with the owner's node-level assume drained at once (KSG_RUN_DEFER=0) instead of
+    deferred past an independent next pod's evaluation (the default)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     doc = g.generate(c, **sizes)

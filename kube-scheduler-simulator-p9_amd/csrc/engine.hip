@@ -3278,14 +3278,17 @@ __global__ __launch_bounds__(64) void k_st_decode(DevCluster C, DevProfile F, co
 // over the statically feasible nodes per pod.
 #define KSG_SD_PODS 8
 #define KSG_SD_NPT 2
-// ready (non-null: the persistent window loop reads the records while this runs
-// beside it): records stored sc1, then — after every wave's stores and maxima
-// have drained and a block barrier — one agent-scope add per block to its pod
-// group's counter (MI355X_MICROARCH.md hand-off table, row 1); a group's records
-// and maxima are complete once its counter reaches gridDim.x.
-__global__ __launch_bounds__(256) void k_static_dec(DevCluster C, DevProfile F, const WcPod* __restrict__ pods,
-                                                    const uint8_t* __restrict__ progs, uint32_t count, StaticRec* out,
-                                                    int64_t* mpred, uint32_t* ready) {
+// One item of the static records: node tile bx (BT * KSG_SD_NPT nodes), pod group
+// by (KSG_SD_PODS pods).  ready (non-null: the persistent window loop reads the
+// records while they are computed beside it): records stored sc1, then — after
+// every wave's stores and maxima have drained and a block barrier — one
+// agent-scope add to the group's counter (MI355X_MICROARCH.md hand-off table,
+// row 1); a group's records and maxima are complete once its counter reaches the
+// number of node tiles.
+template <int BT>
+__device__ __forceinline__ void static_dec_item(const DevCluster& C, const DevProfile& F, const WcPod* __restrict__ pods,
+                                                const uint8_t* __restrict__ progs, uint32_t count, StaticRec* out,
+                                                int64_t* mpred, uint32_t* ready, uint32_t bx, uint32_t by) {
   const bool ht = F.pos_taint >= 0, ha = F.pos_na >= 0;
   const bool taint_first = ht && (!ha || F.pos_taint < F.pos_na);
   uint32_t n[KSG_SD_NPT], tcnt[KSG_SD_NPT];
@@ -3294,7 +3297,7 @@ __global__ __launch_bounds__(256) void k_static_dec(DevCluster C, DevProfile F, 
   bool live[KSG_SD_NPT];
 #pragma unroll
   for (int k = 0; k < KSG_SD_NPT; ++k) {
-    const uint32_t nn = blockIdx.x * (256 * KSG_SD_NPT) + k * 256 + threadIdx.x;
+    const uint32_t nn = bx * (BT * KSG_SD_NPT) + k * BT + threadIdx.x;
     live[k] = nn < C.N;
     n[k] = live[k] ? nn : 0u;
     const uint32_t t0 = C.toff[n[k]], tc = C.toff[n[k] + 1] - t0;
@@ -3313,7 +3316,7 @@ __global__ __launch_bounds__(256) void k_static_dec(DevCluster C, DevProfile F, 
   }
 #pragma unroll 1
   for (uint32_t pi = 0; pi < KSG_SD_PODS; ++pi) {
-    const uint32_t j = blockIdx.y * KSG_SD_PODS + pi;
+    const uint32_t j = by * KSG_SD_PODS + pi;
     if (j >= count) break;
     const WcPod& P = pods[j];
     const uint32_t fl = P.flags;
@@ -3398,7 +3401,25 @@ __global__ __launch_bounds__(256) void k_static_dec(DevCluster C, DevProfile F, 
   if (ready) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(ready + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ready + by, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__global__ __launch_bounds__(256) void k_static_dec(DevCluster C, DevProfile F, const WcPod* __restrict__ pods,
+                                                    const uint8_t* __restrict__ progs, uint32_t count, StaticRec* out,
+                                                    int64_t* mpred, uint32_t* ready) {
+  static_dec_item<256>(C, F, pods, progs, count, out, mpred, ready, blockIdx.x, blockIdx.y);
+}
+// Beside the persistent window loop: a few 1,024-thread blocks (one per CU the
+// loop leaves idle, launched BEFORE the loop so that the loop's blocks take the
+// other CUs) walk the items group by group; when kernels run one at a time (a
+// PMC profiling pass) it simply completes before the loop starts.
+__global__ __launch_bounds__(1024) void k_static_dec_run(DevCluster C, DevProfile F, const WcPod* __restrict__ pods,
+                                                         const uint8_t* __restrict__ progs, uint32_t count,
+                                                         StaticRec* out, int64_t* mpred, uint32_t* ready, uint32_t ntx,
+                                                         uint32_t items) {
+  for (uint32_t i = blockIdx.x; i < items; i += gridDim.x) {
+    static_dec_item<1024>(C, F, pods, progs, count, out, mpred, ready, i % ntx, i / ntx);
+    __syncthreads();  // (the item's registers and the next item's loads)
   }
 }
 
@@ -6193,7 +6214,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   };
   // ready: k_static_dec beside the persistent loop, counting its pod groups there
   // (the maxima already reset on the engine stream)
-  auto issue_static = [&](uint32_t c, hipStream_t st, uint32_t* ready = nullptr) -> bool {
+  auto issue_static = [&](uint32_t c, hipStream_t st, uint32_t* ready = nullptr, uint32_t run_grid = 0) -> bool {
     const uint32_t q0 = first + c * chunk, cn = std::min(chunk, first + count - q0);
     if (!ready)
       HIPCHK(hipMemsetAsync(I.mpred.p + 2 * (size_t)(q0 - first), 0xFF, 2 * (size_t)cn * sizeof(int64_t), st));
@@ -6218,8 +6239,15 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
                          wp, gstat ? 1 : 0);
       const dim3 dgrid(std::max<uint32_t>((SN + 256 * KSG_SD_NPT - 1) / (256 * KSG_SD_NPT), 1),
                        (cn + KSG_SD_PODS - 1) / KSG_SD_PODS);
-      hipLaunchKernelGGL(k_static_dec, dgrid, dim3(256), 0, st, CS, I.F, wp, I.progs.p, cn, sout,
-                         I.mpred.p + 2 * (size_t)(q0 - first), ready);
+      if (run_grid) {  // (beside the persistent loop: a few 1,024-thread blocks walking the items)
+        const uint32_t ntx = std::max<uint32_t>((SN + 1024 * KSG_SD_NPT - 1) / (1024 * KSG_SD_NPT), 1);
+        const uint32_t items = ntx * ((cn + KSG_SD_PODS - 1) / KSG_SD_PODS);
+        hipLaunchKernelGGL(k_static_dec_run, dim3(std::min(run_grid, items)), dim3(1024), 0, st, CS, I.F, wp, I.progs.p, cn,
+                           sout, I.mpred.p + 2 * (size_t)(q0 - first), ready, ntx, items);
+      } else {
+        hipLaunchKernelGGL(k_static_dec, dgrid, dim3(256), 0, st, CS, I.F, wp, I.progs.p, cn, sout,
+                           I.mpred.p + 2 * (size_t)(q0 - first), ready);
+      }
       I.static_dec_chunks++;
     } else {
       hipLaunchKernelGGL(k_static, sgrid, dim3(256), 0, st, CS, I.F, I.progs.p, I.prog_off_d.p, q0, cn, sout,
@@ -6243,13 +6271,19 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   // the persistent window loop: one launch for every window (its blocks all
   // resident: one per CU); not co-resident -> the launch-per-window loop below
   if (persist_ok && (!stat || stat_run)) {
-    // the run's records: before the launch, or (KSG_STATIC_OVERLAP, default) by
-    // k_static_dec on the side stream once the loop's blocks are all resident,
-    // on the CUs it leaves idle; its eval blocks wait per window for their pods'
-    // groups (win_stat_gate)
-    const bool overlap = stat_run && I.static_overlap && I.sstream && static_dec_ok(first, count);
+    // dedicated merge blocks (one per pod) when they fit beside the tile blocks
+    const bool mb = I.win_mblocks && 1 + (uint64_t)KSG_BATCH * (T + 1) <= I.n_cus;
+    const uint32_t grid = 1 + KSG_BATCH * T + (mb ? KSG_BATCH : 0);
+    // the run's records: before the launch, or (KSG_STATIC_OVERLAP, default)
+    // beside it — k_static_dec_run, one 1,024-thread block per CU the loop leaves
+    // idle, launched on the side stream BEFORE the loop (its blocks then hold
+    // those CUs and the loop's take the rest; kernels run one at a time, as under
+    // a PMC pass, it simply completes first); the eval blocks wait per window for
+    // their pods' groups (win_stat_gate)
+    const uint32_t side_grid = I.n_cus > grid ? I.n_cus - grid : 0;
+    const bool overlap = stat_run && I.static_overlap && I.sstream && side_grid > 0 && static_dec_ok(first, count);
     const uint32_t sgroups = (count + KSG_SD_PODS - 1) / KSG_SD_PODS;
-    if (overlap) {  // (every buffer k_static_dec needs allocated now: a free beside the loop would wait for it)
+    if (overlap) {
       if (!I.sready.alloc(sgroups, err) || !I.sd_pods.alloc((size_t)chunk * (sizeof(WcPod) / 8), err)) return false;
       HIPCHK(hipMemsetAsync(I.sready.p, 0, sgroups * sizeof(uint32_t), s));
       HIPCHK(hipMemsetAsync(I.mpred.p, 0xFF, 2 * (size_t)count * sizeof(int64_t), s));
@@ -6257,11 +6291,12 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
         for (auto* e : {&I.sev_ready[0], &I.sev_ready[1], &I.sev_ready[2], &I.sev_free})
           HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
       HIPCHK(hipEventRecord(I.sev_free, s));
+      HIPCHK(hipStreamWaitEvent(I.sstream, I.sev_free, 0));
+      if (!issue_static(0, I.sstream, I.sready.p, side_grid)) return false;
+      HIPCHK(hipEventRecord(I.sev_ready[0], I.sstream));
     } else if (stat_run && !issue_static(0, s)) {  // (every record of the run)
       return false;
     }
-    // dedicated merge blocks (one per pod) when they fit beside the tile blocks
-    const bool mb = I.win_mblocks && 1 + (uint64_t)KSG_BATCH * (T + 1) <= I.n_cus;
     if (!I.wsync.alloc(1, err) || !I.rsync.alloc(1, err)) return false;
     if (!I.hverdict) {
       HIPCHK(hipHostMalloc((void**)&I.hverdict, 64, hipHostMallocCoherent | hipHostMallocMapped));
@@ -6293,8 +6328,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     R.arrive = I.arrive.p;
     R.stamps = I.stamps_on ? I.stamps.p : nullptr;
     R.sready = overlap ? I.sready.p : nullptr;
-    R.sready_need = std::max<uint32_t>((SN + 256 * KSG_SD_NPT - 1) / (256 * KSG_SD_NPT), 1);  // (k_static_dec's grid.x)
-    const uint32_t grid = 1 + KSG_BATCH * T + (mb ? KSG_BATCH : 0);
+    R.sready_need = std::max<uint32_t>((SN + 1024 * KSG_SD_NPT - 1) / (1024 * KSG_SD_NPT), 1);  // (k_static_dec_run's node tiles)
     WinArgs AP = A;
     AP.mblocks = mb ? 1u : 0u;
     AP.astride = 32;
@@ -6329,10 +6363,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     }
     if (v == 1u) {
       I.win_runs++;
-      if (overlap) {  // the loop holds its CUs: the records beside it, then the stream waits for them
-        HIPCHK(hipStreamWaitEvent(I.sstream, I.sev_free, 0));
-        if (!issue_static(0, I.sstream, I.sready.p)) return false;
-        HIPCHK(hipEventRecord(I.sev_ready[0], I.sstream));
+      if (overlap) {  // (the run's last kernel after the side stream's records)
         HIPCHK(hipStreamWaitEvent(s, I.sev_ready[0], 0));
         I.static_overlaps++;
       }
@@ -6345,6 +6376,9 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     }
     I.win_fallbacks++;  // v == 2: its blocks left untouched; the per-window launches
     if (sampled) I.n_samples--;
+    // (the side kernel's records and maxima are rewritten by the per-window loop's
+    // k_static: it waits for the side kernel first)
+    if (overlap) HIPCHK(hipStreamWaitEvent(s, I.sev_ready[0], 0));
   }
   for (int64_t j = -1; j < (int64_t)nwin; ++j) {
     const int64_t E = j + 1, W = j;

@@ -292,7 +292,9 @@ def extra_config(c, torch, steps, warmup, cpu_seconds, cpu_workers, rank=0, worl
             extra_kernels = {
                 "k_static": {"launches": st_n, "total_ms": st_ms, "bytes": sb,
                              "achieved": sb / (st_ms * 1e-3) / 1e9, "frac": sb / (st_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                             "bytes_per_pair": CFG3_STATIC_PAIR_BYTES, "traffic": pmc_traffic(f"cfg{c}:k_static"),
+                             "bytes_per_pair": CFG3_STATIC_PAIR_BYTES,
+                             "kernel": "k_static_dec_run" if beside else "k_static_dec",
+                             "traffic": pmc_traffic(f"cfg{c}:" + ("k_static_dec_run" if beside else "k_static_dec")),
                              "beside_loop": beside},
                 "step": {"note": "both kernels over the whole queue: pairs x (k_static + k_window bytes per pair) / "
                                  "the step's kernel time (k_static + k_window, or the longer of the two when k_static "

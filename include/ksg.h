@@ -339,7 +339,9 @@ static inline int64_t ksg_view_score(const ksg_cycle_view* v, uint32_t pos, uint
   return ((const int32_t*)row)[i];
 }
 /* Snapshot the kept outputs of queue pod q (the pod of the last ksg_cycle, or a
- * ksg_keep_outputs range) into a view. */
+ * ksg_keep_outputs range) into a view.  For the pod of the last ksg_cycle with
+ * commit = 0, acquired before any other state-changing call, the view was filled
+ * behind that cycle's own kernels and is returned without a device launch. */
 int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out);
 void ksg_cycle_view_release(const ksg_cycle_view* view);
 

@@ -7729,6 +7729,7 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
   };
   uint32_t pmask = 0;  // the profile's device plugins (kernel specialisations)
   for (int i = 0; i < F.n; ++i) pmask |= 1u << F.plugins[i];
+  if (__builtin_popcount(pmask) != F.n) pmask = ~0u;  // (a plugin at two positions: the generic kernels, kNPos)
   // persistent segments (k_chain_run): consecutive eligible pods in one launch
   auto kept_pod = [&](uint32_t j) { return I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n; };
   bool run_ok = commit && !xchain && F.has_ext && rowm != 0 && I.run_on != 0;

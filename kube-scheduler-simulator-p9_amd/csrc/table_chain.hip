@@ -657,6 +657,12 @@ __device__ __forceinline__ int32_t ld_tab(const int32_t* p) {
 // code: the generic evaluation is ~75-130 KB of code, beyond the 64 KB
 // instruction cache two CUs share, and misses it on every cycle.
 #define PMH(p) ((PM >> (p)) & 1u)
+// Device positions a kernel specialised on plugin set PM can see (the host picks
+// such a kernel only when the profile's positions are PM's plugins, each once):
+// the per-position loops unroll that many times instead of KSG_MAX_PLUGINS.
+template <uint32_t PM>
+constexpr int kNPos = PM == ~0u ? KSG_MAX_PLUGINS
+                                : (__builtin_popcount(PM) < KSG_MAX_PLUGINS ? __builtin_popcount(PM) : KSG_MAX_PLUGINS);
 // k_chain_run: the flag this block waits for before its class-table reads (the
 // previous pod's assume by the block owning its node; want 0: none)
 struct RunWait;
@@ -983,7 +989,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
   int64_t cv[KCP_X] = {0, 0, 0, 0};         // SOLO: the node's class (raw scores per normalised slot)
   if constexpr (RUN) {
 #pragma unroll
-    for (int i = 0; i < KSG_MAX_PLUGINS; ++i) eo->raw[i] = 0;
+    for (int i = 0; i < kNPos<PM>; ++i) eo->raw[i] = 0;
   }
   if (feasible) {
 #pragma unroll 1
@@ -1017,7 +1023,7 @@ __device__ __forceinline__ void eval_body(DevCluster& C, const DevProfile& F, co
       if (MODE == kEval || kept_run) os[(size_t)pos * C.N + n] = (int32_t)sc;
       if constexpr (RUN) {
 #pragma unroll
-        for (int i = 0; i < KSG_MAX_PLUGINS; ++i)
+        for (int i = 0; i < kNPos<PM>; ++i)
           if (i == pos) eo->raw[i] = (int32_t)sc;
       }
       const int x = chain_x(p);
@@ -1392,11 +1398,12 @@ __global__ __launch_bounds__(64) void k_tx4_select(DevCluster C, DevProfile F, C
 
 // The normalisers per profile position from the folded partials (the summary's
 // max / min; PodTopologySpread's from the raw score of its single constraint).
+template <uint32_t PM = ~0u>
 __device__ __forceinline__ void chain_norms(const DevProfile& F, const ksg_prog* h, const EvalTotals& E,
                                             int64_t (&smx)[KSG_MAX_PLUGINS], int64_t (&smn)[KSG_MAX_PLUGINS],
                                             int64_t pmx, int64_t pmn) {
 #pragma unroll
-  for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+  for (int pos = 0; pos < kNPos<PM>; ++pos) {
     smx[pos] = 0;
     smn[pos] = INT64_MAX;
     if (pos >= F.n) continue;
@@ -2066,7 +2073,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       pmn = pts_raw1(h, E, E.r.mn[KCX_PTS]);
     }
     int64_t smx[KSG_MAX_PLUGINS], smn[KSG_MAX_PLUGINS];
-    chain_norms(F, h, E, smx, smn, pmx, pmn);
+    chain_norms<PM>(F, h, E, smx, smn, pmx, pmn);
     if (b == 0 && threadIdx.x == 0) chain_summary(A, F, h, E, smx, smn, eo.ipa_flags);
     // ---- NormalizeScore, weights, packed key of this block's nodes (final_body)
     ChainRec r;
@@ -2075,7 +2082,7 @@ __device__ __forceinline__ void run_body(DevCluster& C, const DevProfile& F, con
       int64_t tot = 0;
       bool range_err = false;
 #pragma unroll
-      for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+      for (int pos = 0; pos < kNPos<PM>; ++pos) {
         if (pos >= F.n) continue;
         const int p = F.plugins[pos];
         int64_t sv = eo.raw[pos];

@@ -193,7 +193,11 @@ class Engine {
   bool table_room(uint32_t used[4], uint32_t cap[4], std::string& err);
   // Class tables: append pod / term classes and build their tables from the
   // existing-pod table; counts of classes with tables; rebuild every table.
-  bool add_classes(const ClassUpload& u, std::string& err);
+  // prog: the cycle's pod program, appended (as append_program) in the same
+  // upload when the classes go out as one (*placed: it was; otherwise the caller
+  // appends it).
+  bool add_classes(const ClassUpload& u, std::string& err, const std::vector<uint8_t>* prog = nullptr,
+                   bool* placed = nullptr);
   uint32_t pod_classes() const;
   uint32_t term_classes() const;
   bool rebuild_class_tables(std::string& err);

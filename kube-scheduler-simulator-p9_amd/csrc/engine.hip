@@ -5499,6 +5499,10 @@ struct Engine::Impl {
   bool unwaited = false;         // a state-changing launch was queued without a wait (Reserve's k_assume):
                                  // a failing synchronisation then leaves host mirror and device apart (lost)
   DBuf<WinSync> wsync;           // k_window_run's counters (zeroed per launch)
+  int view_narrow = 1;           // k_view: PTS / IPA raw rows by the summary's range (KSG_VIEW_NARROW=0: 4 bytes)
+  int place_fused = 1;           // add_classes places the cycle's program in its upload (KSG_PLACE_FUSED=0: off)
+  int pc_agg = 1;                // k_pc_build counts few-domain slots per block (KSG_PC_AGG=0: per row)
+  int pc_prefetch = 1;           // k_pc_build reads the requirement keys' label columns up front (KSG_PC_PREFETCH=0: off)
   int win_run_on = 1;            // persistent window loop (k_window_run): KSG_WIN_RUN=0 turns it off
   int win_mblocks = 0;           // ... with dedicated merge blocks (KSG_WIN_MB=1; the last tile block merges: measured faster)
   int view_copy = 0;             // cycle view: 1 = the per-node arrays by a copy (KSG_VIEW_COPY), 0 = written by k_view
@@ -5674,6 +5678,10 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (const char* e = std::getenv("KSG_RUN_LAG")) I.run_lag = std::min<uint32_t>(4096, (uint32_t)std::strtoul(e, nullptr, 10));
   if (const char* e = std::getenv("KSG_RUN_NORES")) I.run_need_extra = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
   if (const char* e = std::getenv("KSG_WIN_RUN")) I.win_run_on = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_PC_PREFETCH")) I.pc_prefetch = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_PC_AGG")) I.pc_agg = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_PLACE_FUSED")) I.place_fused = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_VIEW_NARROW")) I.view_narrow = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_MB")) I.win_mblocks = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_PFIX")) I.win_pfix = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_SPLIT")) I.win_split = (int)std::strtol(e, nullptr, 10);
@@ -6729,6 +6737,17 @@ static void host_exchange(void* p) {
   if (I.xfn(I.xuser, I.hps, I.hpr, c->bytes) != 0) I.xfail.store(1);
 }
 
+// The host-side record of a program placed at byte offset off (append_program,
+// add_classes' fused placement).
+static void note_program(Engine::Impl& I, const std::vector<uint8_t>& prog, size_t off) {
+  I.prog_bytes = off + prog.size();
+  I.prog_off.push_back(off);
+  if (!na_weights_fit(prog)) I.static_fits = false;
+  I.max_na_sum = std::max(I.max_na_sum, na_weight_sum(prog));
+  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
+  I.prog_need.push_back(prog_need_of(h));
+  for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
+}
 bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) {
   Impl& I = *p_;
   hipStream_t s = I.stream;
@@ -6758,13 +6777,7 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
                          I.prog_off_d.p + q, off64, (void*)(I.plite.p + q), I.prow.p + q, (int32_t)-1, I.sums.p + q,
                          I.F);
       HIPCHK(hipGetLastError());
-      I.prog_bytes = off + prog.size();
-      I.prog_off.push_back(off);
-      if (!na_weights_fit(prog)) I.static_fits = false;
-      I.max_na_sum = std::max(I.max_na_sum, na_weight_sum(prog));
-      const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
-      I.prog_need.push_back(prog_need_of(h));
-      for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
+      note_program(I, prog, off);
       return true;
     }
     if (blk) pinned_put(blk, cap);
@@ -6794,13 +6807,7 @@ bool Engine::append_program(const std::vector<uint8_t>& prog, std::string& err) 
   hipLaunchKernelGGL(k_place_program, dim3(1), dim3(256), 0, s, I.apdev.p, (uint32_t)prog.size(), I.progs.p + off,
                      I.prog_off_d.p + q, off64, (void*)(I.plite.p + q), I.prow.p + q, (int32_t)-1, I.sums.p + q, I.F);
   HIPCHK(hipGetLastError());
-  I.prog_bytes = off + prog.size();
-  I.prog_off.push_back(off);
-  if (!na_weights_fit(prog)) I.static_fits = false;
-  I.max_na_sum = std::max(I.max_na_sum, na_weight_sum(prog));
-  const ksg_prog* h = reinterpret_cast<const ksg_prog*>(prog.data());
-  I.prog_need.push_back(prog_need_of(h));
-  for (int c = 2; c < KSG_MAX_RES; ++c) I.any_eph_req |= h->req[c] != 0;
+  note_program(I, prog, off);
   return true;
 }
 
@@ -7196,7 +7203,15 @@ __global__ __launch_bounds__(256) void k_upload(const UpSeg* __restrict__ segs) 
   const UpSeg g = segs[blockIdx.x];
   uint32_t* d = reinterpret_cast<uint32_t*>(g.dst);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(g.src);
-  for (uint32_t i = blockIdx.y * 256 + threadIdx.x; i < g.words; i += gridDim.y * 256) d[i] = src ? src[i] : 0u;
+  uint32_t w0 = 0;
+  if (((g.dst | g.src) & 15) == 0) {  // 16-byte pieces (a source in host memory: fewer link reads)
+    w0 = g.words & ~3u;
+    uint4* d4 = reinterpret_cast<uint4*>(d);
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    for (uint32_t i = blockIdx.y * 256 + threadIdx.x; i < w0 / 4; i += gridDim.y * 256)
+      d4[i] = src ? s4[i] : make_uint4(0, 0, 0, 0);
+  }
+  for (uint32_t i = w0 + blockIdx.y * 256 + threadIdx.x; i < g.words; i += gridDim.y * 256) d[i] = src ? src[i] : 0u;
 }
 
 // Node-sharded class tables: sum the pair-level entries of the classes built
@@ -7247,8 +7262,9 @@ static bool tables_ready(Engine::Impl& I, std::string& err) {
   return reduce_tables(I, err);
 }
 
-bool Engine::add_classes(const ClassUpload& u, std::string& err) {
+bool Engine::add_classes(const ClassUpload& u, std::string& err, const std::vector<uint8_t>* prog, bool* placed) {
   Impl& I = *p_;
+  if (placed) *placed = false;
   hipStream_t s = I.stream;
   const uint32_t pc0 = I.npc, tc0 = I.ntc, npc = (uint32_t)u.pc.size(), ntc = (uint32_t)u.tc_slot.size();
   if (!npc && !ntc) return true;
@@ -7281,7 +7297,15 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
     I.hold.push_back(p);
     return p;
   };
-  PcStage pst{I.nct, 0, I.ncreq, 0, I.ncval, 0};  // (k_pc_build: the new classes' pool ranges)
+  PcStage pst{I.nct, 0, I.ncreq, 0, I.ncval, 0, 0xFFFFFFFFu, {}, 0, {}, {}};  // (k_pc_build: the new classes' pool ranges)
+  if (I.pc_agg)  // slots with at most 256 domains: pc_dom counted per block
+    for (uint32_t sl = 0; sl < KSG_MAX_TOPO && sl < I.topo.topo_count.size() && sl < I.topo.nu_base.size(); ++sl) {
+      const uint32_t cnt = ((I.uniq >> sl) & 1u) ? I.N : I.topo.topo_count[sl];
+      if (I.topo.nu_base[sl] == 0xFFFFFFFFu || cnt == 0 || cnt > 256) continue;
+      pst.hbase[sl] = (uint16_t)pst.hsum;
+      pst.hcnt[sl] = (uint16_t)cnt;
+      pst.hsum += cnt;
+    }
   if (npc) {  // definitions, rebased onto the device pools
     auto pc = held(u.pc);
     auto ct = held(u.ct);
@@ -7292,7 +7316,17 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
       x.sel.req_off += (int32_t)I.ncreq;
       x.ns_off += (int32_t)I.ncval;
     }
-    for (auto& x : *rq) x.val_off += (int32_t)I.ncval;
+    pst.nk = 0;  // (k_pc_build: the distinct requirement keys, read per row up front)
+    for (auto& x : *rq) {
+      x.val_off += (int32_t)I.ncval;
+      uint32_t j = 0;
+      while (j < pst.nk && j < KSG_PCB_K && pst.key[j] != x.key) ++j;
+      if (j == pst.nk) {
+        if (pst.nk < KSG_PCB_K) pst.key[j] = x.key;
+        ++pst.nk;
+      }
+    }
+    if (!I.pc_prefetch) pst.nk = 0xFFFFFFFFu;
     if (!up(I.pcls_d, pc0, *pc) || !up(I.cterm_d, I.nct, *ct) || !up(I.creq_d, I.ncreq, *rq) ||
         !up(I.cval_d, I.ncval, *cv) || !zero(I.pc_cnt, (size_t)pc0 * Nn, (size_t)npc * Nn) ||
         !zero(I.pc_dom, (size_t)pc0 * NUn, (size_t)npc * NUn) ||
@@ -7327,6 +7361,38 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
     I.tc_slot_h.insert(I.tc_slot_h.end(), u.tc_slot.begin(), u.tc_slot.end());
     I.ntc += ntc;
   }
+  // the cycle's program in the same upload (what k_place_program writes: program,
+  // offset, PodLite, table row, fresh summary), so a pod that brings classes costs
+  // one copy kernel, not two
+  if (prog && placed && fused && I.place_fused && !segs.empty() && prog->size() % 4 == 0) {
+    const size_t q = I.prog_off.size();
+    const size_t off = (I.prog_bytes + 255) & ~(size_t)255;
+    if (!I.progs.grow(off + prog->size(), I.prog_bytes, s, err) || !I.prog_off_d.grow(q + 1, q, s, err) ||
+        !I.plite.grow(q + 1, q, s, err) || !I.sums.grow(q + 1, q, s, err) || !I.prow.grow(q + 1, q, s, err))
+      return false;
+    auto put = [&](void* dst, const void* src, size_t b) {
+      const size_t o = (pay.size() + 15) & ~(size_t)15;
+      pay.resize(o + b);
+      std::memcpy(pay.data() + o, src, b);
+      segs.push_back(UpSeg{reinterpret_cast<uint64_t>(dst), o + 1, (uint32_t)(b / 4), 0});
+    };
+    const PodLite pl = pod_lite(*prog);
+    const uint64_t off64 = off;
+    const int32_t row = -1;
+    ksg_pod_summary z = {};
+    z.selected = -1;
+    for (int p = 0; p < KSG_MAX_PLUGINS; ++p) {
+      z.max_score[p] = (p < I.F.n && I.F.plugins[p] == KP_IPA) ? INT64_MIN : 0;
+      z.min_score[p] = INT64_MAX;
+    }
+    put(I.progs.p + off, prog->data(), prog->size());
+    put(I.prog_off_d.p + q, &off64, sizeof(off64));
+    put(I.plite.p + q, &pl, sizeof(pl));
+    put(I.prow.p + q, &row, sizeof(row));
+    put(I.sums.p + q, &z, sizeof(z));
+    note_program(I, *prog, off);
+    *placed = true;
+  }
   if (!segs.empty()) {  // the fused upload: [list | payloads] in one mapped pinned block
     const size_t lb = (segs.size() * sizeof(UpSeg) + 15) & ~(size_t)15, total = lb + pay.size();
     size_t cap = 0;
@@ -7352,7 +7418,7 @@ bool Engine::add_classes(const ClassUpload& u, std::string& err) {
   }
   DevCluster C = I.cluster();
   if (npc && I.pcap)
-    hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, pc0, npc, pst);
+    hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kPcBlock - 1) / kPcBlock), dim3(kPcBlock), 0, s, C, pc0, npc, pst);
   if (ntc && I.tcap) hipLaunchKernelGGL(k_tc_build, dim3((I.tcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, tc0);
   HIPCHK(hipGetLastError());
   if (npc) I.red_pc0 = std::min(I.red_pc0, pc0);
@@ -7379,8 +7445,8 @@ bool Engine::rebuild_class_tables(std::string& err) {
   }
   DevCluster C = I.cluster();
   if (I.npc && I.pcap)
-    hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, 0u, I.npc,
-                       PcStage{0, 0xFFFFFFFFu, 0, 0, 0, 0});
+    hipLaunchKernelGGL(k_pc_build, dim3((I.pcap + kPcBlock - 1) / kPcBlock), dim3(kPcBlock), 0, s, C, 0u, I.npc,
+                       PcStage{0, 0xFFFFFFFFu, 0, 0, 0, 0, 0xFFFFFFFFu, {}, 0, {}, {}});
   if (I.ntc && I.tcap) hipLaunchKernelGGL(k_tc_build, dim3((I.tcap + kBlock - 1) / kBlock), dim3(kBlock), 0, s, C, 0u);
   HIPCHK(hipGetLastError());
   if (I.npc) I.red_pc0 = 0;
@@ -7473,6 +7539,7 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
   V.off_norm = (uint32_t)lay.off_norm;
   V.off_rows = (uint32_t)lay.off_rows;
   V.n_norm = lay.n_norm;
+  V.narrow = I.view_narrow ? 1u : 0u;
   const size_t N = I.N, k = j - I.keep_first;
   hipStream_t s = I.stream;
   if (I.vblk_fresh) {  // a new block: generation 0 everywhere

@@ -1059,8 +1059,10 @@ struct Cluster {
     for (auto& a : p.pref_aff) tclass(2, a);
     for (auto& a : p.pref_anti) tclass(3, a);
   }
-  // Upload the classes the device has no tables for yet (and build them).
-  bool sync_classes() {
+  // Upload the classes the device has no tables for yet (and build them); prog:
+  // the cycle's program, placed in the same upload when *placed comes back true.
+  bool sync_classes(const vector<uint8_t>* prog = nullptr, bool* placed = nullptr) {
+    if (placed) *placed = false;
     if (!tables_on()) return true;
     ClassUpload u;
     for (uint32_t c = eng->pod_classes(); c < pcls.size(); ++c) {
@@ -1083,7 +1085,7 @@ struct Cluster {
       u.tc_slot.push_back(tcls[k].slot);
       u.tc_off.push_back(tcls[k].off);
     }
-    return eng->add_classes(u, err);
+    return eng->add_classes(u, err, prog, placed);
   }
   // nodes carrying every key of slot mask m
   uint32_t nodes_with_all(uint32_t m) {
@@ -3247,7 +3249,8 @@ struct Cluster {
       PodMeta m;
       if (!compile(queue[q], (int32_t)(seq_base + q), blob, m)) return false;
       lap(2);
-      if (!sync_classes() || !eng->append_program(blob, err)) return false;  // classes it brought: tables built
+      bool placed = false;  // (with the classes it brought, in one upload)
+      if (!sync_classes(&blob, &placed) || (!placed && !eng->append_program(blob, err))) return false;
       progs.push_back(std::move(blob));
       meta.push_back(std::move(m));
       prog_cls.resize(progs.size(), {(uint32_t)pcls.size(), (uint32_t)tcls.size()});

@@ -2420,20 +2420,53 @@ __global__ __launch_bounds__(kBlock) void k_flush_appends(DevCluster C, ChainArg
 // add_classes) are staged in LDS first when they fit: the per-row selector walk
 // then reads LDS instead of a chain of dependent global loads (class -> term ->
 // requirement -> values) per row.  st.nt == UINT32_MAX: read the pools in place.
+#define KSG_PCB_K 4
 struct PcStage {
   uint32_t t0, nt, r0, nr, v0, nv;
+  // the distinct label keys the staged requirements name (host-collected; nk >
+  // KSG_PCB_K: none): their label columns are read for every row up front, in
+  // parallel with the row's own loads, instead of one dependent load per
+  // requirement after the class walk reached it
+  uint32_t nk;
+  int32_t key[KSG_PCB_K];
+  // the slots with few domains (hcnt > 0: a zone, not a hostname): their pc_dom
+  // entries, like pc_tot, are counted per block in LDS and added once per block.
+  // Every matching row of a class adds to one entry of such a slot — with 20
+  // zones, 20 addresses in one cache line — so row-level atomics serialise at one
+  // L2 channel (class c's entries at LDS c_local * hsum + hbase[slot] + value).
+  uint32_t hsum;
+  uint16_t hbase[KSG_MAX_TOPO], hcnt[KSG_MAX_TOPO];
 };
 #define KSG_PCB_C 16
 #define KSG_PCB_T 64
 #define KSG_PCB_R 128
 #define KSG_PCB_V 512
-__global__ __launch_bounds__(256) void k_pc_build(DevCluster C, uint32_t c0, uint32_t nc, PcStage st) {
+#define KSG_PCB_H 4096
+constexpr uint32_t kPcBlock = 1024;  // rows per block (fewer blocks: fewer per-block adds to the hot lines)
+__global__ __launch_bounds__(kPcBlock) void k_pc_build(DevCluster C, uint32_t c0, uint32_t nc, PcStage st) {
   __shared__ ksg_pclass s_pc[KSG_PCB_C];
   __shared__ ksg_cterm s_ct[KSG_PCB_T];
   __shared__ ksg_req s_rq[KSG_PCB_R];
   __shared__ int32_t s_cv[KSG_PCB_V];
+  __shared__ int32_t s_tot[KSG_PCB_C * KSG_MAX_TOPO];
+  __shared__ int32_t s_dom[KSG_PCB_H];
   const bool staged = st.nt != 0xFFFFFFFFu && nc <= KSG_PCB_C && st.nt <= KSG_PCB_T && st.nr <= KSG_PCB_R &&
                       st.nv <= KSG_PCB_V;
+  const bool agg = staged && st.hsum > 0 && nc * st.hsum <= KSG_PCB_H;
+  const bool pre = staged && st.nk <= KSG_PCB_K;  // requirement keys as indices into kv below
+  // the row's loads first, independent of the table use and of the class
+  // definitions (rows past the use are read but never counted: p < pcap)
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t pp = p < C.pcap ? p : C.pcap - 1;
+  const uint32_t fl = C.ptflags[pp];
+  const int32_t node = C.ptnode[pp], ns = C.ptns[pp];
+  int32_t kv[KSG_PCB_K];
+#pragma unroll
+  for (int j = 0; j < KSG_PCB_K; ++j) {
+    const int32_t k = st.key[j];
+    kv[j] = (pre && (uint32_t)j < st.nk && k >= 0 && (uint32_t)k < C.pkeys) ? C.ptlab[(size_t)k * C.pcap + pp] : -1;
+  }
+  const bool live = p < C.tcounts[0] && !(fl & KEF_DELETED);
   const ksg_pclass* PCs = C.T.pcls;
   const ksg_cterm* CTs = C.T.cterm;
   const ksg_req* RQs = C.T.creq;
@@ -2454,9 +2487,18 @@ __global__ __launch_bounds__(256) void k_pc_build(DevCluster C, uint32_t c0, uin
     for (uint32_t i = threadIdx.x; i < st.nr; i += blockDim.x) {
       ksg_req x = C.T.creq[st.r0 + i];
       x.val_off -= (int32_t)st.v0;
+      if (pre) {  // key -> its index in st.key (-1: a key the rows never carry)
+        int32_t j = -1;
+        for (uint32_t t = 0; t < st.nk; ++t)
+          if (st.key[t] == x.key) j = (int32_t)t;
+        x.key = j;
+      }
       s_rq[i] = x;
     }
     for (uint32_t i = threadIdx.x; i < st.nv; i += blockDim.x) s_cv[i] = C.T.cval[st.v0 + i];
+    for (uint32_t i = threadIdx.x; i < nc * KSG_MAX_TOPO; i += blockDim.x) s_tot[i] = 0;
+    if (agg)
+      for (uint32_t i = threadIdx.x; i < nc * st.hsum; i += blockDim.x) s_dom[i] = 0;
     __syncthreads();
     PCs = s_pc;
     CTs = s_ct;
@@ -2464,13 +2506,16 @@ __global__ __launch_bounds__(256) void k_pc_build(DevCluster C, uint32_t c0, uin
     CVs = s_cv;
     cbase = c0;
   }
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  bool live = p < C.tcounts[0];
-  const uint32_t pp = live ? p : 0u;
-  const uint32_t fl = C.ptflags[pp];
-  live = live && !(fl & KEF_DELETED);
-  const int32_t node = C.ptnode[pp], ns = C.ptns[pp];
-  auto vid = [&](int32_t k) -> int32_t { return (k >= 0 && (uint32_t)k < C.pkeys) ? C.ptlab[(size_t)k * C.pcap + pp] : -1; };
+  auto vid = [&](int32_t k) -> int32_t {
+    if (pre) {
+      int32_t v = -1;
+#pragma unroll
+      for (int j = 0; j < KSG_PCB_K; ++j)
+        if (k == j) v = kv[j];
+      return v;
+    }
+    return (k >= 0 && (uint32_t)k < C.pkeys) ? C.ptlab[(size_t)k * C.pcap + pp] : -1;
+  };
   int32_t nv[KSG_MAX_TOPO];
   node_slot_vids(C, live ? (uint32_t)node : 0u, nv);
   const DevTables& T = C.T;
@@ -2488,13 +2533,33 @@ __global__ __launch_bounds__(256) void k_pc_build(DevCluster C, uint32_t c0, uin
       const bool m = ok && nv[sl] >= 0;
       const uint64_t b = __ballot(m);
       if (!b) continue;
-      if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((unsigned long long)b) - 1))
-        atomicAdd(&T.pc_tot[(size_t)c * KSG_MAX_TOPO + sl], (int)__popcll(b));
+      if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((unsigned long long)b) - 1)) {
+        if (staged) atomicAdd(&s_tot[(c - c0) * KSG_MAX_TOPO + sl], (int)__popcll(b));
+        else atomicAdd(&T.pc_tot[(size_t)c * KSG_MAX_TOPO + sl], (int)__popcll(b));
+      }
       // (per-row domain atomics: a per-wave loop over the distinct domains measured
       // slower — 38 vs 32 µs per build, up to 170 on many-valued slots)
-      if (m && C.nubv[sl] >= 0) atomicAdd(T.pc_dom + (size_t)c * T.NU + (uint32_t)C.nubv[sl] + nv[sl], 1);
+      if (m && C.nubv[sl] >= 0) {
+        if (agg && (uint32_t)nv[sl] < st.hcnt[sl]) atomicAdd(&s_dom[(c - c0) * st.hsum + st.hbase[sl] + nv[sl]], 1);
+        else atomicAdd(T.pc_dom + (size_t)c * T.NU + (uint32_t)C.nubv[sl] + nv[sl], 1);
+      }
     }
   }
+  if (!staged) return;
+  __syncthreads();  // the block's counts, added once
+  for (uint32_t i = threadIdx.x; i < nc * KSG_MAX_TOPO; i += blockDim.x) {
+    const uint32_t c = c0 + i / KSG_MAX_TOPO;
+    if (s_tot[i] && c < T.npc) atomicAdd(&T.pc_tot[(size_t)c * KSG_MAX_TOPO + i % KSG_MAX_TOPO], s_tot[i]);
+  }
+  if (agg)
+    for (uint32_t i = threadIdx.x; i < nc * st.hsum; i += blockDim.x) {
+      const int32_t x = s_dom[i];
+      const uint32_t c = c0 + i / st.hsum, r = i % st.hsum;
+      if (!x || c >= T.npc) continue;
+      for (int sl = 0; sl < KSG_MAX_TOPO; ++sl)
+        if (st.hcnt[sl] && r >= st.hbase[sl] && r < (uint32_t)st.hbase[sl] + st.hcnt[sl] && C.nubv[sl] >= 0)
+          atomicAdd(T.pc_dom + (size_t)c * T.NU + (uint32_t)C.nubv[sl] + (r - st.hbase[sl]), x);
+    }
 }
 // term classes [u0, ...): every live existing pod's term of such a class
 __global__ void k_tc_build(DevCluster C, uint32_t u0) {
@@ -2575,12 +2640,15 @@ struct ViewDev {
   uint32_t gen;  // this view's generation: a slot (or the overflow word) holds gen << 32 | code
   uint32_t off_sum, off_fail_pos, off_fail_code, off_fail_msg, off_raw, off_norm;  // byte offsets in the block
   uint32_t off_rows, n_norm;  // the score-row table (Engine::ViewRows); normalized rows
+  uint32_t narrow;            // PodTopologySpread / InterPodAffinity raw rows sized by the summary's range
 };
 // Score-row widths of a view, the same in every thread: 1 byte for the rows whose
 // values are within [0, 100] by construction when the cycle has no Score error
-// (Fit and BalancedAllocation raw, every normalized row), else 4; rows packed
-// from off_raw, each 256-B aligned.  (Values of nodes that failed a filter are
-// unspecified in the view: clamped.)
+// (Fit and BalancedAllocation raw, every normalized row); PodTopologySpread's and
+// InterPodAffinity's raw rows as narrow as the summary's range over the feasible
+// nodes allows (1, 2 or 4 bytes; the range widened by PodTopologySpread's -1 of
+// an ignored node and 0), else 4; rows packed from off_raw, each 256-B aligned.
+// (Values of nodes that failed a filter are unspecified in the view: clamped.)
 __device__ __forceinline__ void view_rows(const DevProfile& F, const ViewDev& V, const ksg_pod_summary* sum, uint32_t N,
                                           Engine::ViewRows& R) {
   const bool err = sum->status == 2;
@@ -2591,8 +2659,18 @@ __device__ __forceinline__ void view_rows(const DevProfile& F, const ViewDev& V,
     R.bytes[d] = 0;
   }
   for (int d = 0; d < F.n; ++d) {
-    const bool narrow = !err && (F.plugins[d] == KP_FIT || F.plugins[d] == KP_BA);
-    R.bytes[d] = narrow ? 1 : 4;
+    const int p = F.plugins[d];
+    uint8_t w = 4;
+    if (!err && (p == KP_FIT || p == KP_BA)) {
+      w = 1;
+    } else if (!err && V.narrow && (p == KP_PTS || p == KP_IPA)) {
+      int64_t lo = sum->min_score[d], hi = sum->max_score[d];
+      if (lo == INT64_MAX || hi == INT64_MIN) lo = hi = 0;  // (no feasible / counted node)
+      lo = lo < -1 ? lo : -1;
+      hi = hi > 0 ? hi : 0;
+      w = (lo >= -128 && hi <= 127) ? 1 : (lo >= -32768 && hi <= 32767) ? 2 : 4;
+    }
+    R.bytes[d] = w;
     R.off[d] = off;
     off += al(N * R.bytes[d]);
   }
@@ -2604,6 +2682,7 @@ __device__ __forceinline__ void view_rows(const DevProfile& F, const ViewDev& V,
 }
 __device__ __forceinline__ void view_put(uint8_t* base, uint32_t off, uint8_t w, uint32_t n, int64_t v) {
   if (w == 1) reinterpret_cast<int8_t*>(base + off)[n] = (int8_t)(v < -128 ? -128 : v > 127 ? 127 : v);
+  else if (w == 2) reinterpret_cast<int16_t*>(base + off)[n] = (int16_t)(v < -32768 ? -32768 : v > 32767 ? 32767 : v);
   else reinterpret_cast<int32_t*>(base + off)[n] = (int32_t)v;
 }
 // slot of `code` in the table (entries of other generations count as empty: no clearing per view)
@@ -2686,6 +2765,7 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
   const uint32_t tid = threadIdx.x;
   auto lput = [&](uint32_t loff, uint8_t w, int64_t v) {
     if (w == 1) reinterpret_cast<int8_t*>(vst + loff)[tid] = (int8_t)(v < -128 ? -128 : v > 127 ? 127 : v);
+    else if (w == 2) reinterpret_cast<int16_t*>(vst + loff)[tid] = (int16_t)(v < -32768 ? -32768 : v > 32767 ? 32767 : v);
     else reinterpret_cast<int32_t*>(vst + loff)[tid] = (int32_t)v;
   };
   uint32_t lraw[KSG_MAX_PLUGINS], lnorm[KSG_MAX_PLUGINS];  // LDS segment offsets (uniform)

@@ -215,7 +215,8 @@ bool Engine::table_room(uint32_t used[4], uint32_t cap[4], std::string&) {
   }
   return true;
 }
-bool Engine::add_classes(const ClassUpload& u, std::string& err) {
+bool Engine::add_classes(const ClassUpload& u, std::string& err, const std::vector<uint8_t>*, bool* placed) {
+  if (placed) *placed = false;
   if (u.tc_off.size() != u.tc_slot.size()) { err = "stub: classes"; return false; }
   p_->npc += (uint32_t)u.pc.size();
   p_->ntc += (uint32_t)u.tc_slot.size();

@@ -230,9 +230,14 @@ def test_cycle_view_matches_extension_point_calls(monkeypatch, name, c, sizes, c
     s.load_cluster(d)
     names = [n["metadata"]["name"] for n in doc["nodes"]]
     held = []
+    widths = set()  # PodTopologySpread / InterPodAffinity raw rows: as narrow as the cycle's range
+    plugins = doc["profile"]["plugins"]
     for i, pod in enumerate(doc["queue"][:30]):
         q, r = s.cycle(pod, commit=True)
         v = s.cycle_view(q)
+        for pos, pl in enumerate(plugins):
+            if pl in ("PodTopologySpread", "InterPodAffinity") and v._v.score[pos] and r.status == 0:
+                widths.add(v._v.score_bytes[pos])
         assert (v.result.selected, v.result.feasible, v.result.status) == o.result(i), (name, i)
         nodes = range(len(names)) if i < 8 else (0, len(names) // 2, len(names) - 1)
         for pos in range(len(doc["profile"]["plugins"])):  # the view holds what the per-node calls return
@@ -253,6 +258,9 @@ def test_cycle_view_matches_extension_point_calls(monkeypatch, name, c, sizes, c
                 assert val == ora[k], (name, i, k)
         if i % 10 == 0:
             held.append((i, q, v, outs[0]))
+    assert widths <= {1, 2, 4}, widths
+    if name == "cfg4":
+        assert widths and min(widths) < 4, widths
     for i, q, v, first in held:  # views stay valid and unchanged after later cycles
         assert rebuild(_ViewCalls(s, v), q, doc["profile"], names, v.result.status) == first, (name, i)
         v.release()

@@ -5499,6 +5499,7 @@ struct Engine::Impl {
   bool unwaited = false;         // a state-changing launch was queued without a wait (Reserve's k_assume):
                                  // a failing synchronisation then leaves host mirror and device apart (lost)
   DBuf<WinSync> wsync;           // k_window_run's counters (zeroed per launch)
+  int view_slots_direct = 1;     // k_view: message slots into the host block as claimed (KSG_VIEW_SLOTS_DIRECT=0: last block copies)
   int view_narrow = 1;           // k_view: PTS / IPA raw rows by the summary's range (KSG_VIEW_NARROW=0: 4 bytes)
   int place_fused = 1;           // add_classes places the cycle's program in its upload (KSG_PLACE_FUSED=0: off)
   int pc_agg = 1;                // k_pc_build counts few-domain slots per block (KSG_PC_AGG=0: per row)
@@ -5682,6 +5683,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (const char* e = std::getenv("KSG_PC_AGG")) I.pc_agg = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_PLACE_FUSED")) I.place_fused = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_VIEW_NARROW")) I.view_narrow = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_VIEW_SLOTS_DIRECT")) I.view_slots_direct = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_MB")) I.win_mblocks = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_PFIX")) I.win_pfix = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_SPLIT")) I.win_split = (int)std::strtol(e, nullptr, 10);
@@ -7540,6 +7542,7 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
   V.off_rows = (uint32_t)lay.off_rows;
   V.n_norm = lay.n_norm;
   V.narrow = I.view_narrow ? 1u : 0u;
+  V.slots_direct = I.view_slots_direct ? 1u : 0u;
   const size_t N = I.N, k = j - I.keep_first;
   hipStream_t s = I.stream;
   if (I.vblk_fresh) {  // a new block: generation 0 everywhere
@@ -7553,6 +7556,8 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
   // the per-node arrays straight into the caller's pinned block when the device
   // can address it (one kernel, then only the slot table and summary are copied)
   uint8_t* hdev = N && !I.view_copy ? pinned_dev(host) : nullptr;
+  if (hdev && I.view_slots_direct)  // (k_view writes each slot as it claims it: the rest reads empty)
+    std::memset(host, 0, (kViewSlots + 1) * sizeof(uint64_t));
   if (hdev && !I.vdone.p) {
     if (!I.vdone.alloc(1, err)) return false;
     HIPCHK(hipMemsetAsync(I.vdone.p, 0, sizeof(uint32_t), s));

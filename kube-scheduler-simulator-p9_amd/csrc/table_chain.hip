@@ -2641,6 +2641,7 @@ struct ViewDev {
   uint32_t off_sum, off_fail_pos, off_fail_code, off_fail_msg, off_raw, off_norm;  // byte offsets in the block
   uint32_t off_rows, n_norm;  // the score-row table (Engine::ViewRows); normalized rows
   uint32_t narrow;            // PodTopologySpread / InterPodAffinity raw rows sized by the summary's range
+  uint32_t slots_direct;      // direct: slots written to the host block as claimed (no last-block copy)
 };
 // Score-row widths of a view, the same in every thread: 1 byte for the rows whose
 // values are within [0, 100] by construction when the cycle has no Score error
@@ -2685,21 +2686,29 @@ __device__ __forceinline__ void view_put(uint8_t* base, uint32_t off, uint8_t w,
   else if (w == 2) reinterpret_cast<int16_t*>(base + off)[n] = (int16_t)(v < -32768 ? -32768 : v > 32767 ? 32767 : v);
   else reinterpret_cast<int32_t*>(base + off)[n] = (int32_t)v;
 }
-// slot of `code` in the table (entries of other generations count as empty: no clearing per view)
-__device__ __forceinline__ uint32_t view_slot(unsigned long long* tab, uint32_t gen, uint32_t code) {
+// slot of `code` in the table (entries of other generations count as empty: no
+// clearing per view).  htab (or null): the host block's copy of the table, zeroed
+// by the host before the launch — a claimed slot never changes within a
+// generation, so the claiming lane writes it there too.
+__device__ __forceinline__ uint32_t view_slot(unsigned long long* tab, uint32_t gen, uint32_t code,
+                                              unsigned long long* htab) {
   const unsigned long long want = ((unsigned long long)gen << 32) | code;
   uint32_t h = (code * 2654435761u) >> 24;
   for (int k = 0; k < kViewSlots; ++k) {
     unsigned long long cur = __hip_atomic_load(&tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while ((uint32_t)(cur >> 32) != gen) {  // stale: claim it
       const unsigned long long old = atomicCAS(&tab[h], cur, want);
-      if (old == cur) return h;
+      if (old == cur) {
+        if (htab) htab[h] = want;
+        return h;
+      }
       cur = old;
     }
     if (cur == want) return h;
     h = (h + 1) & (kViewSlots - 1);
   }
   atomicMax(&tab[kViewSlots], (unsigned long long)gen << 32);  // overflow (the host renders the view itself)
+  if (htab) htab[kViewSlots] = (unsigned long long)gen << 32;
   return kViewSlots;
 }
 // out: the device block (slot table, summary); hout: where the per-node arrays go —
@@ -2745,7 +2754,9 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
     const int leader = __ffsll((long long)m) - 1;
     const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)code, leader);
     uint32_t s = 0;
-    if ((int)lane == leader) s = view_slot(tab, V.gen, c0);
+    if ((int)lane == leader)
+      s = view_slot(tab, V.gen, c0,
+                    (hout != out && V.slots_direct) ? reinterpret_cast<unsigned long long*>(hout) : nullptr);
     s = (uint32_t)__builtin_amdgcn_readlane((int)s, leader);
     if (need && code == c0) {
       msg = s < kViewSlots ? s + 1 : 0;
@@ -2821,7 +2832,7 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
   }
   // direct: the last block to finish copies the message-slot table (every
   // block's inserts done) into the host block, so no copy launch follows
-  if (hout != out && done) {
+  if (hout != out && done && !V.slots_direct) {
     __shared__ uint32_t last;
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -27,9 +27,60 @@
 #include <unordered_set>
 #include <vector>
 
+#include <dlfcn.h>
+
 #include "../../include/ksg.h"
 #include "engine.h"
 #include "json.hpp"
+
+// ROCTx ranges (KSG_ROCTX=1): the C entry points and ksg_cycle's host phases as
+// named ranges for `rocprofv3 --marker-trace`, beside the kernels they launch.
+// The ROCTx library is opened at run time, so nothing links against it and a
+// run without the variable (or without the library) pays one branch per range.
+namespace rtx {
+struct Api {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+};
+inline const Api& api() {
+  static const Api a = [] {
+    Api x;
+    const char* e = std::getenv("KSG_ROCTX");
+    if (!e || std::strtol(e, nullptr, 10) == 0) return x;
+    void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return x;
+    x.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+    x.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+    if (!x.push || !x.pop) x = Api{};
+    return x;
+  }();
+  return a;
+}
+struct Range {  // one range for the scope
+  bool on;
+  explicit Range(const char* name) : on(api().push != nullptr) {
+    if (on) api().push(name);
+  }
+  ~Range() {
+    if (on) api().pop();
+  }
+  Range(const Range&) = delete;
+  Range& operator=(const Range&) = delete;
+};
+struct Phases {  // consecutive ranges within a scope: next() ends one and starts the next
+  bool on, open = false;
+  Phases() : on(api().push != nullptr) {}
+  void next(const char* name) {
+    if (!on) return;
+    if (open) api().pop();
+    api().push(name);
+    open = true;
+  }
+  ~Phases() {
+    if (on && open) api().pop();
+  }
+};
+}  // namespace rtx
 
 namespace ksg {
 namespace host {
@@ -3191,6 +3242,7 @@ struct Cluster {
     }
     ~PreView() { drop(); }
   } pview;
+  bool classes_early = std::getenv("KSG_CLASSES_EARLY") && std::strtol(std::getenv("KSG_CLASSES_EARLY"), nullptr, 10) != 0;
   bool view_prefetch = !(std::getenv("KSG_VIEW_PREFETCH") && std::strtol(std::getenv("KSG_VIEW_PREFETCH"), nullptr, 10) == 0);
   bool prefetch_view(uint32_t q) {
     pview.drop();
@@ -3208,11 +3260,15 @@ struct Cluster {
   bool cycle(const char* js, size_t len, bool commit, ksg_pod_summary& out) {
     if (shards != 1) { err = "the cycle API needs an unsharded context"; return false; }
     if (!compile_queue()) return false;
+    static const char* const kPhase[8] = {"parse", "checks_vocab", "compile", "append", "launch", "wait", "postfilter", ""};
+    rtx::Phases ph;
+    ph.next(kPhase[0]);
     double t = now_us();
     auto lap = [&](int k) {
       const double u = now_us();
       ctimes[k] += u - t;
       t = u;
+      if (k < 6) ph.next(kPhase[k + 1]);
     };
     try {
       docs.emplace_back(new J(json::parse(js, len)));
@@ -3247,6 +3303,15 @@ struct Cluster {
     } else {
       vector<uint8_t> blob;
       PodMeta m;
+      // classes_early: the pod's new classes registered and their tables built
+      // (one upload + k_pc_build on the engine stream) before its program is
+      // compiled, so the device builds them while the host compiles; the program
+      // then goes out on its own (k_place_program).  Otherwise the program rides
+      // in the class upload after the compile.
+      if (classes_early) {
+        register_classes(queue[q]);
+        if (!sync_classes()) return false;
+      }
       if (!compile(queue[q], (int32_t)(seq_base + q), blob, m)) return false;
       lap(2);
       bool placed = false;  // (with the classes it brought, in one upload)
@@ -4611,6 +4676,7 @@ int ksg_keep_outputs(ksg_ctx* ctx, uint32_t first, uint32_t count) {
 }
 
 int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
+  rtx::Range rr("ksg_schedule_queue");
   KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
@@ -4658,6 +4724,7 @@ int ksg_compact(ksg_ctx* ctx, uint32_t keep_from) {
 }
 
 int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count) {
+  rtx::Range rr("ksg_whatif");
   KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
@@ -4902,6 +4969,7 @@ int ksg_kernel_time(ksg_ctx* ctx, float* avg_ms, uint32_t* samples) {
 }
 
 int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_pod_result* out) {
+  rtx::Range rr("ksg_cycle");
   KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   ctx->c.out_gen++;
@@ -4924,6 +4992,7 @@ int ksg_cycle(ksg_ctx* ctx, const char* pod_json, size_t len, int commit, ksg_po
 }
 
 int ksg_reserve(ksg_ctx* ctx, uint32_t q, int32_t node) {
+  rtx::Range rr("ksg_reserve");
   KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   if (!ctx->c.reserve(q, node)) return ctx->fail(ctx->c.err, KSG_E_STATE);
@@ -5157,6 +5226,7 @@ struct CycleView {
 }  // namespace
 
 int ksg_cycle_view_acquire(ksg_ctx* ctx, uint32_t q, const ksg_cycle_view** out) {
+  rtx::Range rr("ksg_cycle_view_acquire");
   KSG_LOCK(ctx);
   KSG_GUARD(ctx);
   Cluster& c = ctx->c;

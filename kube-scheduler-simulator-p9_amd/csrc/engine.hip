@@ -5505,6 +5505,7 @@ struct Engine::Impl {
   bool unwaited = false;         // a state-changing launch was queued without a wait (Reserve's k_assume):
                                  // a failing synchronisation then leaves host mirror and device apart (lost)
   DBuf<WinSync> wsync;           // k_window_run's counters (zeroed per launch)
+  int final_pm = 1;              // k_final specialised for the Fit/BA/PTS/IPA plugin set (KSG_FINAL_PM=0: generic)
   int view_slots_direct = 1;     // k_view: message slots into the host block as claimed (KSG_VIEW_SLOTS_DIRECT=0: last block copies)
   int view_narrow = 1;           // k_view: PTS / IPA raw rows by the summary's range (KSG_VIEW_NARROW=0: 4 bytes)
   int place_fused = 1;           // add_classes places the cycle's program in its upload (KSG_PLACE_FUSED=0: off)
@@ -5689,6 +5690,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
   if (const char* e = std::getenv("KSG_PC_AGG")) I.pc_agg = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_PLACE_FUSED")) I.place_fused = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_VIEW_NARROW")) I.view_narrow = (int)std::strtol(e, nullptr, 10);
+  if (const char* e = std::getenv("KSG_FINAL_PM")) I.final_pm = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_VIEW_SLOTS_DIRECT")) I.view_slots_direct = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_MB")) I.win_mblocks = (int)std::strtol(e, nullptr, 10);
   if (const char* e = std::getenv("KSG_WIN_PFIX")) I.win_pfix = (int)std::strtol(e, nullptr, 10);
@@ -7960,7 +7962,9 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
           }
         }
         if (occ) hipLaunchKernelGGL(k_final_occ, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
-        else hipLaunchKernelGGL(k_final, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+        else if ((pmask & ~kPmTab) == 0 && I.final_pm)  // (the plugin-set specialisation: kNPos)
+          hipLaunchKernelGGL(k_final<kPmTab>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+        else hipLaunchKernelGGL(k_final<>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
       }
       if (xchain) {  // X4: selectHost over the ranks, the assume split by ownership
         if (!xgather(I, 3 * sizeof(int64_t), err)) return false;

@@ -1575,6 +1575,7 @@ __global__ __launch_bounds__(kChain) void k_ptsraw(DevCluster C, DevProfile F, C
   }
 }
 
+template <uint32_t PM = ~0u>
 __device__ __forceinline__ void final_body(DevCluster& C, const DevProfile& F, const ChainArgs& A,
                                            const uint8_t* __restrict__ prog) {
   chain_warm(prog);
@@ -1591,7 +1592,7 @@ __device__ __forceinline__ void final_body(DevCluster& C, const DevProfile& F, c
   const bool mine = n < C.N && of[n] == KSG_FILTER_PASS;
   int32_t raw[KSG_MAX_PLUGINS];  // this node's raw scores, loaded before the folds
 #pragma unroll
-  for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) raw[pos] = (mine && pos < F.n) ? os[(size_t)pos * C.N + n] : 0;
+  for (int pos = 0; pos < kNPos<PM>; ++pos) raw[pos] = (mine && pos < F.n) ? os[(size_t)pos * C.N + n] : 0;
   const uint32_t ipa_flags = (uint32_t)A.pi[KCP_IPAF * A.nblk];  // k_eval's block 0
   EvalTotals E;
   CS(16);
@@ -1618,7 +1619,7 @@ __device__ __forceinline__ void final_body(DevCluster& C, const DevProfile& F, c
   // the summary's normalisers per position (max over feasible nodes; unset as k_init_summaries)
   int64_t smx[KSG_MAX_PLUGINS], smn[KSG_MAX_PLUGINS];
 #pragma unroll
-  for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+  for (int pos = 0; pos < kNPos<PM>; ++pos) {
     smx[pos] = 0;
     smn[pos] = INT64_MAX;
     if (pos >= F.n) continue;
@@ -1639,7 +1640,7 @@ __device__ __forceinline__ void final_body(DevCluster& C, const DevProfile& F, c
     S->ignored = E.r.ign;
     S->ipa_flags = ipa_flags;
 #pragma unroll
-    for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos)
+    for (int pos = 0; pos < kNPos<PM>; ++pos)
       if (pos < F.n) {
         S->max_score[pos] = smx[pos];
         S->min_score[pos] = smn[pos];
@@ -1654,7 +1655,7 @@ __device__ __forceinline__ void final_body(DevCluster& C, const DevProfile& F, c
     int64_t tot = 0;
     bool pts_keys = false, range_err = false;
 #pragma unroll
-    for (int pos = 0; pos < KSG_MAX_PLUGINS; ++pos) {
+    for (int pos = 0; pos < kNPos<PM>; ++pos) {
       if (pos >= F.n) continue;
       const int p = F.plugins[pos];
       int64_t s = raw[pos];
@@ -2352,8 +2353,9 @@ __global__ __launch_bounds__(kChain) void k_eval_solo(DevCluster C, DevProfile F
                                                       const uint8_t* __restrict__ prog) {
   eval_body<ROWM, kSolo>(C, F, A, prog);
 }
+template <uint32_t PM = ~0u>
 __global__ __launch_bounds__(kChain) void k_final(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
-  final_body(C, F, A, prog);
+  final_body<PM>(C, F, A, prog);
 }
 __global__ __launch_bounds__(kChain) __attribute__((amdgpu_waves_per_eu(4))) void k_final_occ(
     DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {

@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--extra-sizes", default="", help="tests only: c:nodes:pods[:existing],... overriding the "
                     "BASELINE sizes of the extra configs (e.g. 3:300:64,4:400:64:800,5:2000:64)")
     ap.add_argument("--extra-steps", type=int, default=2)
+    ap.add_argument("--whatif-steps", type=int, default=16, help="cfg5 timed what-if steps (SURVEY.md §8(d): 16, "
+                    "binds between them)")
     ap.add_argument("--cpu-workers", type=int, default=16, help="parallelize.Until workers (upstream default 16)")
     return ap.parse_args()
 
@@ -445,7 +447,7 @@ def run(a, torch, rank=0, world=1, local=0, dist=None):
     for c in (int(x) for x in a.extra.split(",") if x):
         if c == 5:  # what-if steps: 1M nodes x 4,096 pods per step (bench_whatif.py)
             import bench_whatif
-            wargs = ["--steps", str(max(a.extra_steps, 2)), "--warmup", "1",
+            wargs = ["--steps", str(max(a.whatif_steps, 1)), "--warmup", "1",
                      "--cpu-pods", "16" if (a.cpu_baseline and world == 1) else "0", "--cpu-workers", str(a.cpu_workers)]
             if c in sizes:
                 wargs += ["--nodes", str(sizes[c][0]), "--step-pods", str(sizes[c][1])]

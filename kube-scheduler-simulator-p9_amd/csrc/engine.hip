@@ -3416,7 +3416,10 @@ __global__ __launch_bounds__(256) void k_static_dec(DevCluster C, DevProfile F, 
 __global__ __launch_bounds__(1024) void k_static_dec_run(DevCluster C, DevProfile F, const WcPod* __restrict__ pods,
                                                          const uint8_t* __restrict__ progs, uint32_t count,
                                                          StaticRec* out, int64_t* mpred, uint32_t* ready, uint32_t ntx,
-                                                         uint32_t items) {
+                                                         uint32_t items, uint32_t* arrive) {
+  // (the loop's handshake goes only once every block of this grid has started: a
+  // started block runs to its end, so the loop's gates on these records complete)
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (uint32_t i = blockIdx.x; i < items; i += gridDim.x) {
     static_dec_item<1024>(C, F, pods, progs, count, out, mpred, ready, i % ntx, i / ntx);
     __syncthreads();  // (the item's registers and the next item's loads)
@@ -5435,9 +5438,12 @@ struct Engine::Impl {
   DBuf<uint64_t> wc_pods;     // what-if class path: the chunk's decoded pods (WcPod)
   DBuf<uint64_t> sd_pods;     // static records: the chunk's decoded pods (WcPod, k_static_dec)
   int static_dec = 1;         // k_static_dec where the chunk's pods decode (KSG_STATIC_DEC=0: k_static)
-  uint32_t static_run_mb = 16384;  // static records of a whole run in the persistent window loop (KSG_STATIC_RUN_MB; 0: off)
+  uint32_t static_run_mb = 4096;   // static records of a whole run in the persistent window loop (KSG_STATIC_RUN_MB; 0: off;
+                                   // also at most half the device's free memory, else the ring of chunks)
   uint64_t static_dec_chunks = 0;  // diagnostic: static chunks computed from decoded pods
   int static_overlap = 1;          // KSG_STATIC_OVERLAP=0: a persistent run's records all before its launch
+  int static_beside_test = 0;      // tests (KSG_STATIC_BESIDE_TEST): 1 = the side kernel launched after the loop,
+                                   // 2 = only after the loop's verdict (never resident beside it: the fallback)
   uint64_t static_overlaps = 0;    // diagnostic: persistent runs whose records were computed beside the loop
   DBuf<uint32_t> sready;           // ... per group of KSG_SD_PODS pods, the node tiles done
   uint32_t wi_chunk = 0;      // ... pods per chunk of the last step, and whether records were used
@@ -5726,6 +5732,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
     if (const char* e = std::getenv("KSG_STATIC_DEC")) I.static_dec = (int)std::strtol(e, nullptr, 10);
     if (const char* e = std::getenv("KSG_STATIC_RUN_MB")) I.static_run_mb = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("KSG_STATIC_OVERLAP")) I.static_overlap = (int)std::strtol(e, nullptr, 10);
+    if (const char* e = std::getenv("KSG_STATIC_BESIDE_TEST")) I.static_beside_test = (int)std::strtol(e, nullptr, 10);
   }
   HIPCHK(hipEventCreate(&I.ev0));
   HIPCHK(hipEventCreate(&I.ev1));
@@ -6195,10 +6202,19 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   // they fit KSG_STATIC_RUN_MB (default 16 GiB of the 288 GB)
   const bool persist_ok = !sharded && I.win_run_on && nwin > 0 && 1 + (uint64_t)KSG_BATCH * T <= I.n_cus;
   const uint32_t count32 = (count + KSG_BATCH - 1) / KSG_BATCH * KSG_BATCH;
-  const bool stat_run = stat && !side && persist_ok && I.static_run_mb > 0 && !I.stat_chunk_cap &&
-                        (uint64_t)count32 * std::max<uint32_t>(I.N, 1) * sizeof(StaticRec) <= ((uint64_t)I.static_run_mb << 20);
-  const uint32_t nslots = stat_run ? 1 : side ? 3 : 2;
-  uint32_t chunk = 0, nchunks = 0;
+  const uint64_t run_bytes = (uint64_t)count32 * std::max<uint32_t>(I.N, 1) * sizeof(StaticRec);
+  bool stat_run = stat && !side && persist_ok && I.static_run_mb > 0 && !I.stat_chunk_cap &&
+                  run_bytes <= ((uint64_t)I.static_run_mb << 20);
+  if (stat_run && run_bytes > I.stat.n * sizeof(StaticRec)) {
+    // (a run-sized buffer only while it leaves most of the device free: another
+    // context or process may hold memory; otherwise the ring of chunks)
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || run_bytes > fr / 2) {
+      (void)hipGetLastError();
+      stat_run = false;
+    }
+  }
+  uint32_t chunk = 0, nchunks = 0, nslots = 2;
   const bool gstat = stat && I.gstat && sharded;  // node-sharded: records over every node
   const DevCluster CS = gstat ? I.cluster_static() : C;
   const uint32_t SN = gstat ? I.G : I.N;
@@ -6207,14 +6223,24 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   A.G = I.G;
   if (stat) {
     const size_t Nn = std::max<uint32_t>(SN, 1);
-    const size_t budget = side ? ((size_t)32 << 20) : ((size_t)64 << 20);
-    chunk = (uint32_t)std::max<size_t>(KSG_BATCH, (budget / (Nn * sizeof(StaticRec))) / KSG_BATCH * KSG_BATCH);
-    chunk = std::min<uint32_t>(chunk, count32);
-    if (I.stat_chunk_cap) chunk = std::min<uint32_t>(chunk, I.stat_chunk_cap);  // tests: force ring roll-over
-    if (stat_run) chunk = count32;
-    nchunks = (count + chunk - 1) / chunk;
-    if (!I.stat.alloc((size_t)nslots * chunk * Nn, err) || !I.mpred.alloc(2 * (size_t)std::max<uint32_t>(count, 1), err))
-      return false;
+    auto size_ring = [&]() {
+      nslots = stat_run ? 1 : side ? 3 : 2;
+      const size_t budget = side ? ((size_t)32 << 20) : ((size_t)64 << 20);
+      chunk = (uint32_t)std::max<size_t>(KSG_BATCH, (budget / (Nn * sizeof(StaticRec))) / KSG_BATCH * KSG_BATCH);
+      chunk = std::min<uint32_t>(chunk, count32);
+      if (I.stat_chunk_cap) chunk = std::min<uint32_t>(chunk, I.stat_chunk_cap);  // tests: force ring roll-over
+      if (stat_run) chunk = count32;
+      nchunks = (count + chunk - 1) / chunk;
+    };
+    size_ring();
+    if (!I.stat.alloc((size_t)nslots * chunk * Nn, err)) {
+      if (!stat_run) return false;
+      (void)hipGetLastError();  // (the run-sized buffer did not fit after all: the ring)
+      stat_run = false;
+      size_ring();
+      if (!I.stat.alloc((size_t)nslots * chunk * Nn, err)) return false;
+    }
+    if (!I.mpred.alloc(2 * (size_t)std::max<uint32_t>(count, 1), err)) return false;
     A.stat = I.stat.p;
     A.stat_ring = nslots * chunk;
     A.mpred = I.mpred.p;
@@ -6232,7 +6258,8 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
   };
   // ready: k_static_dec beside the persistent loop, counting its pod groups there
   // (the maxima already reset on the engine stream)
-  auto issue_static = [&](uint32_t c, hipStream_t st, uint32_t* ready = nullptr, uint32_t run_grid = 0) -> bool {
+  auto issue_static = [&](uint32_t c, hipStream_t st, uint32_t* ready = nullptr, uint32_t run_grid = 0,
+                          uint32_t* arrive = nullptr) -> bool {
     const uint32_t q0 = first + c * chunk, cn = std::min(chunk, first + count - q0);
     if (!ready)
       HIPCHK(hipMemsetAsync(I.mpred.p + 2 * (size_t)(q0 - first), 0xFF, 2 * (size_t)cn * sizeof(int64_t), st));
@@ -6261,7 +6288,7 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
         const uint32_t ntx = std::max<uint32_t>((SN + 1024 * KSG_SD_NPT - 1) / (1024 * KSG_SD_NPT), 1);
         const uint32_t items = ntx * ((cn + KSG_SD_PODS - 1) / KSG_SD_PODS);
         hipLaunchKernelGGL(k_static_dec_run, dim3(std::min(run_grid, items)), dim3(1024), 0, st, CS, I.F, wp, I.progs.p, cn,
-                           sout, I.mpred.p + 2 * (size_t)(q0 - first), ready, ntx, items);
+                           sout, I.mpred.p + 2 * (size_t)(q0 - first), ready, ntx, items, arrive);
       } else {
         hipLaunchKernelGGL(k_static_dec, dgrid, dim3(256), 0, st, CS, I.F, wp, I.progs.p, cn, sout,
                            I.mpred.p + 2 * (size_t)(q0 - first), ready);
@@ -6297,21 +6324,32 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     // idle, launched on the side stream BEFORE the loop (its blocks then hold
     // those CUs and the loop's take the rest; kernels run one at a time, as under
     // a PMC pass, it simply completes first); the eval blocks wait per window for
-    // their pods' groups (win_stat_gate)
+    // their pods' groups (win_stat_gate).  The side blocks count themselves in
+    // (one word after the groups' counters) and the loop's handshake goes only
+    // once all of them have started: side blocks that never become resident
+    // beside the loop send it to the per-window fallback before any state changes,
+    // instead of a gate running out mid-run.
     const uint32_t side_grid = I.n_cus > grid ? I.n_cus - grid : 0;
     const bool overlap = stat_run && I.static_overlap && I.sstream && side_grid > 0 && static_dec_ok(first, count);
     const uint32_t sgroups = (count + KSG_SD_PODS - 1) / KSG_SD_PODS;
+    uint32_t side_blocks = 0;
+    auto issue_side = [&]() -> bool {
+      if (!issue_static(0, I.sstream, I.sready.p, side_grid, I.sready.p + sgroups)) return false;
+      HIPCHK(hipEventRecord(I.sev_ready[0], I.sstream));
+      return true;
+    };
     if (overlap) {
-      if (!I.sready.alloc(sgroups, err) || !I.sd_pods.alloc((size_t)chunk * (sizeof(WcPod) / 8), err)) return false;
-      HIPCHK(hipMemsetAsync(I.sready.p, 0, sgroups * sizeof(uint32_t), s));
+      const uint32_t ntx = std::max<uint32_t>((SN + 1024 * KSG_SD_NPT - 1) / (1024 * KSG_SD_NPT), 1);
+      side_blocks = std::min<uint32_t>(side_grid, ntx * sgroups);
+      if (!I.sready.alloc(sgroups + 1, err) || !I.sd_pods.alloc((size_t)chunk * (sizeof(WcPod) / 8), err)) return false;
+      HIPCHK(hipMemsetAsync(I.sready.p, 0, (sgroups + 1) * sizeof(uint32_t), s));
       HIPCHK(hipMemsetAsync(I.mpred.p, 0xFF, 2 * (size_t)count * sizeof(int64_t), s));
       if (!I.sev_ready[0])
         for (auto* e : {&I.sev_ready[0], &I.sev_ready[1], &I.sev_ready[2], &I.sev_free})
           HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
       HIPCHK(hipEventRecord(I.sev_free, s));
       HIPCHK(hipStreamWaitEvent(I.sstream, I.sev_free, 0));
-      if (!issue_static(0, I.sstream, I.sready.p, side_grid)) return false;
-      HIPCHK(hipEventRecord(I.sev_ready[0], I.sstream));
+      if (I.static_beside_test == 0 && !issue_side()) return false;
     } else if (stat_run && !issue_static(0, s)) {  // (every record of the run)
       return false;
     }
@@ -6353,7 +6391,11 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
     AP.prior_fix = I.win_pfix ? 1u : 0u;
     AP.split = I.win_split ? 1u : 0u;
     __atomic_store_n(I.hverdict, 0u, __ATOMIC_RELEASE);
-    const RunCtl RC{grid + I.run_need_extra, I.run_wait_us * 100u, 0, I.hverdict, I.run_spin};
+    RunCtl RC{grid + I.run_need_extra, I.run_wait_us * 100u, 0, I.hverdict, I.run_spin};
+    if (overlap) {
+      RC.side_arrive = I.sready.p + sgroups;
+      RC.side_need = side_blocks;
+    }
     const bool sampled = I.sample_every && I.n_samples * 2 + 2 <= I.sev.size();
     if (sampled) HIPCHK(hipEventRecord(I.sev[I.n_samples * 2], s));
     if (stat_run) {
@@ -6371,8 +6413,10 @@ static bool run_batches(Engine::Impl& I, uint32_t first, uint32_t count, std::st
       I.n_samples++;
     }
     HIPCHK(hipGetLastError());
+    if (overlap && I.static_beside_test == 1 && !issue_side()) return false;  // (tests: launched after the loop)
     I.run_used = true;
     const uint32_t v = wait_verdict(I, s, err);
+    if (overlap && I.static_beside_test == 2 && !issue_side()) return false;  // (tests: after the verdict)
     if (v == 0u) return false;
     if (v == 3u) {
       I.lost = true;

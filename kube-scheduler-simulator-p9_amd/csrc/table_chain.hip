@@ -1739,6 +1739,11 @@ struct RunCtl {
   uint32_t spin;           // polls before a block gives up (kRunSpin; tests force an abort with few)
   uint32_t overlap;        // issue pod k+1's class-table reads during pod k's hand-offs (KSG_RUN_OVERLAP)
   uint32_t defer;          // the owner's node-level assume after the next partial record when independent (KSG_RUN_DEFER)
+  // blocks of another kernel this launch waits on (k_static_dec_run beside the window
+  // loop: its blocks count themselves in here as they start); go only once side_need
+  // of them have started, so every later wait on their output is on running blocks
+  const uint32_t* side_arrive;
+  uint32_t side_need;
 };
 // Pod j+1 (header n) may read the class tables before pod j's (header h) assume:
 // it reads none of the pair-level nor node-level entries pod j writes (its row,
@@ -1782,7 +1787,10 @@ __device__ bool run_handshake(RunSync* Y, const RunCtl& R, uint32_t* go) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       want = 2;
       for (;;) {
-        if (ld_sc1(&Y->arrive[0]) >= R.need) { want = 1; break; }
+        if (ld_sc1(&Y->arrive[0]) >= R.need && (!R.side_arrive || ld_sc1(R.side_arrive) >= R.side_need)) {
+          want = 1;
+          break;
+        }
         if (ld_sc1(&Y->verdict[0]) != 0u) break;  // decided by another block
         if (__builtin_amdgcn_s_memrealtime() - t0 > R.wait_ticks) break;
         __builtin_amdgcn_s_sleep(4);

@@ -153,3 +153,24 @@ def test_static_profiles_persistent_window_loop(monkeypatch, env):
         if i == 0:  # (decodable pods: the records beside the loop unless switched off)
             assert (s.static_overlaps() > 0) == (env.get("KSG_STATIC_OVERLAP") != "0" and
                                                  env.get("KSG_STATIC_RUN_MB") != "0")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["1", "2"], ids=["side-late", "side-absent"])
+def test_static_side_kernel_late_or_absent(monkeypatch, mode):
+    """The static records beside the loop come from a kernel on another stream, and
+    HIP only orders launches, not residency.  The
+    loop's handshake counts that kernel's blocks in: launched after the loop
+    ("side-late") it either becomes resident beside it or the run falls back; never
+    resident beside it ("side-absent": launched only after the loop's verdict) the
+    loop must take the per-window fallback before any state changes.  Either way
+    every pod equals the oracle's and the context stays usable (a second pass)."""
+    monkeypatch.setenv("KSG_STATIC_BESIDE_TEST", mode)
+    doc = g.generate(3, n_nodes=900, n_pods=500)
+    o, s = _compare(doc, every=13)
+    if mode == "2":
+        assert s.window_runs() == 0, "a loop whose side blocks never started must not go"
+    s.reset()
+    s.schedule()
+    got = [(r.selected, r.feasible, r.status) for r in s.results()]
+    assert got == [o.result(q) for q in range(len(got))]

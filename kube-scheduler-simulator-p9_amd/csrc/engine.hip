@@ -4483,7 +4483,15 @@ __device__ __forceinline__ void win_exact_write(const DevCluster& C, const DevPr
 
 template <int MODE, bool STAT, bool PER = false>
 __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile& F, const WinArgs& A, WinLDS& L) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // (the thread index through an empty asm: every window recomputes the per-lane
+  // LDS / record addresses derived from it instead of the compiler hoisting them
+  // out of the persistent loop, where at the 128-VGPR cap they were spilled to
+  // scratch and reloaded on the replay's critical path each window)
+  int tid_ = (int)threadIdx.x;
+#ifndef KSG_FIXUP_HOIST
+  asm volatile("" : "+v"(tid_));
+#endif
+  const int tid = tid_, lane = tid & 63, wave = tid >> 6;
   const int nb = (int)A.nw;
   const uint32_t R = C.R < 4 ? C.R : 4;
 #define STAMP(k)                                        \

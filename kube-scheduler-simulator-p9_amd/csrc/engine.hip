@@ -4612,7 +4612,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
         }
         if (!ok) __hip_atomic_store(A.abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      __syncthreads();
+      lds_barrier();  // (no fence: the previous window's patch stores stay in flight)
       prior_loads();
     }
     if (tid < np * kPendW) reinterpret_cast<uint64_t*>(L.prior)[tid] = pv;
@@ -5012,7 +5012,7 @@ __device__ __forceinline__ void win_fixup(const DevCluster& C, const DevProfile&
       }
       if (!ok) __hip_atomic_store(A.abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __syncthreads();
+    lds_barrier();  // (thread 0 acquired the count; the summaries' stores need no ack here)
   }
   {
     const int32_t Sv = L.S[cur][lane & 31];
@@ -5183,6 +5183,10 @@ __device__ bool win_stat_gate(const WinRunArgs& R, uint32_t r0, uint32_t n, uint
   __syncthreads();
   return ok;
 }
+// FENCE = false (the replay): a plain LDS barrier — __syncthreads' release fence
+// would first wait for every store of the block still in flight (the previous
+// window's output patches), about 2.5 us per window (round 6)
+template <bool FENCE = true>
 __device__ bool win_wait_ge(const uint32_t* w, uint32_t want, uint32_t* abortw, uint32_t spin, uint32_t* go) {
   if (threadIdx.x == 0) {
     bool ok = false;
@@ -5194,9 +5198,9 @@ __device__ bool win_wait_ge(const uint32_t* w, uint32_t want, uint32_t* abortw, 
     if (!ok) __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *go = ok ? 1u : 0u;
   }
-  __syncthreads();
+  if constexpr (FENCE) __syncthreads(); else lds_barrier();
   const bool ok = *go != 0u;
-  __syncthreads();
+  if constexpr (FENCE) __syncthreads(); else lds_barrier();
   return ok;
 }
 // STAT: Taint / NodeAffinity profiles, on static records computed for the whole
@@ -5239,7 +5243,7 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
       // `ready` then refers to the keys counter)
       const uint32_t need = (W >> 1) * KSG_BATCH + A.nw;
       const bool split = A0.split && !A0.prior_fix;
-      if (!ready && !win_wait_ge(split ? &Z->evk[W & 1] : &Z->evd[W & 1], need, abortw, RC.spin, &go)) return;
+      if (!ready && !win_wait_ge<false>(split ? &Z->evk[W & 1] : &Z->evd[W & 1], need, abortw, RC.spin, &go)) return;
       A.evd_wait = split ? &Z->evd[W & 1] : nullptr;
       A.evd_need = need;
       A.pub = &Z->replayed[0][0];
@@ -5252,7 +5256,7 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
         A.nxt_evd = nullptr;
       }
       win_fixup<MODE, STAT, true>(C, F, A, L);  // (publishes P_W before its output patches)
-      __syncthreads();  // (LDS reused by the next window)
+      lds_barrier();  // (LDS reused by the next window; no fence: the patches need no ack before it)
     }
     return;
   }

@@ -5243,7 +5243,14 @@ __global__ __launch_bounds__(KSG_WIN_THREADS) void k_window_run(DevCluster C, De
       // `ready` then refers to the keys counter)
       const uint32_t need = (W >> 1) * KSG_BATCH + A.nw;
       const bool split = A0.split && !A0.prior_fix;
+      // (diagnostic stamps past the windows' slots: loop top, ready, after the wait)
+      uint64_t* const lt = R.stamps ? R.stamps + (size_t)R.nwin * 32 + (size_t)W * 4 : nullptr;
+      if (lt && threadIdx.x == 0) {
+        lt[0] = __builtin_amdgcn_s_memrealtime();
+        lt[1] = ready ? 1u : 0u;
+      }
       if (!ready && !win_wait_ge<false>(split ? &Z->evk[W & 1] : &Z->evd[W & 1], need, abortw, RC.spin, &go)) return;
+      if (lt && threadIdx.x == 0) lt[2] = __builtin_amdgcn_s_memrealtime();
       A.evd_wait = split ? &Z->evd[W & 1] : nullptr;
       A.evd_need = need;
       A.pub = &Z->replayed[0][0];

@@ -981,6 +981,59 @@ struct Cluster {
   };
   vector<PClass> pcls;
   vector<TClass> tcls;
+  // Candidate index over the registry's selector conjunctions: every class is
+  // filed under one necessary condition of its selectors -- an In requirement's
+  // (key, value) pairs, else an Exists key -- or, with neither, checked for every
+  // pod.  A pod's candidates are the classes filed under its labels plus the
+  // unfiled ones, in id order; pclass_matches / term_matches then decide exactly.
+  // compile() lists a pod's class memberships through it: O(matching classes)
+  // instead of a scan of the registry per pod (250,000 bound pods' victim
+  // programs, the drop-in cycle's compile).
+  struct SelIndex {
+    size_t n = 0;  // classes filed
+    std::unordered_map<string, vector<int32_t>> kv, key;
+    vector<int32_t> always;
+    void add(const vector<const LSel*>& sels, int32_t id) {
+      const SelReq* best = nullptr;
+      for (auto* sl : sels)
+        for (auto& r : sl->reqs) {
+          if (r.op == "In" && !r.vals.empty() &&
+              (!best || best->op != "In" || r.vals.size() < best->vals.size()))
+            best = &r;
+          else if (r.op == "Exists" && !best)
+            best = &r;
+        }
+      if (!best) {
+        always.push_back(id);
+      } else if (best->op == "In") {
+        vector<string> v(best->vals);
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        for (auto& x : v) kv[best->key + '\x1f' + x].push_back(id);
+      } else {
+        key[best->key].push_back(id);
+      }
+    }
+    void candidates(const map<string, string>& labels, vector<int32_t>& out) const {
+      out = always;
+      for (auto& l : labels) {
+        auto it = kv.find(l.first + '\x1f' + l.second);
+        if (it != kv.end()) out.insert(out.end(), it->second.begin(), it->second.end());
+        auto jt = key.find(l.first);
+        if (jt != key.end()) out.insert(out.end(), jt->second.begin(), jt->second.end());
+      }
+      std::sort(out.begin(), out.end());
+    }
+  };
+  SelIndex pidx, tidx;
+  void sync_index() {
+    for (; pidx.n < pcls.size(); ++pidx.n) {
+      vector<const LSel*> v;
+      for (auto& t : pcls[pidx.n].terms) v.push_back(&t.sel);
+      pidx.add(v, (int32_t)pidx.n);
+    }
+    for (; tidx.n < tcls.size(); ++tidx.n) tidx.add({&tcls[tidx.n].term.sel}, (int32_t)tidx.n);
+  }
   unordered_map<string, int32_t> pcls_id, tcls_id;
   // node topology keys (class-table path eligibility), this shard's nodes
   vector<uint32_t> node_slots;             // per node: bit s = carries topology slot s's key
@@ -1648,9 +1701,14 @@ struct Cluster {
   bool ensure_victim_store() {
     if (victim_store_current()) return true;
     vector<const vector<uint8_t>*> pp(bound.size());
+    const double t0 = now_us();
     for (size_t b = 0; b < bound.size(); ++b)
       if (!(pp[b] = bound_prog((int32_t)b))) return false;
+    const double t1 = now_us();
     if (!eng->victim_store(pp, err)) return false;
+    if (std::getenv("KSG_PREEMPT_TRACE"))
+      std::fprintf(stderr, "victim store: %zu programs compiled in %.1f ms, uploaded in %.1f ms\n", pp.size(),
+                   (t1 - t0) / 1e3, (now_us() - t1) / 1e3);
     vstore_eng = eng.get();
     vstore_gen = bprog_gen;
     vstore_n = bound.size();
@@ -1664,6 +1722,8 @@ struct Cluster {
     // a new snapshot: the class registry restarts (the bound pods' terms register first)
     pcls.clear();
     tcls.clear();
+    pidx = SelIndex();
+    tidx = SelIndex();
     pcls_id.clear();
     tcls_id.clear();
     prog_cls.clear();
@@ -2789,13 +2849,17 @@ struct Cluster {
     h.tc_match_off = h.pc_match_off;
     h.n_tc_match = 0;
     if (tables_on()) {
-      for (size_t c = 0; c < pcls.size(); ++c)
+      sync_index();
+      vector<int32_t> cand;
+      pidx.candidates(p.labels, cand);  // (ascending ids: the order of a scan of the registry)
+      for (const int32_t c : cand)
         if (pclass_matches(pcls[c], p)) {
-          P.i32.push_back((int32_t)c);
+          P.i32.push_back(c);
           h.n_pc_match++;
         }
       h.tc_match_off = (int32_t)P.i32.size();
-      for (size_t k = 0; k < tcls.size(); ++k)  // (class, value offset, topology slot, group)
+      tidx.candidates(p.labels, cand);
+      for (const int32_t k : cand)  // (class, value offset, topology slot, group)
         if (term_matches(tcls[k].term, p)) {
           P.i32.push_back((int32_t)k);
           P.i32.push_back((int32_t)tcls[k].off);
@@ -3483,15 +3547,9 @@ struct Cluster {
         if (c == KSG_FILTER_PASS || c >= KSG_FILTER_NOT_EVALUATED || (c >> 24) >= (uint32_t)n_dev) continue;
         const int pos = code_pos(c);
         if (pos < 0 || pos >= n_plugins || !has_filter(plugins[pos]) || filter_skipped(meta[q], skip, pos)) continue;
-        int fc;
-        if (plugins[pos] == P_FIT) {
-          fc = C_UNSCHED;
-          const uint32_t detail = code_detail(c);
-          for (size_t r = 0; r < res.names.size(); ++r)
-            if ((detail & (1u << (1 + r))) && rq[r] > al[r * n + i]) fc = C_UNRESOLVABLE;
-        } else {
-          fc = filter_fail_code(q, pos, i, code_detail(c));
-        }
+        const int fc = plugins[pos] == P_FIT
+                           ? fit_fail_code(rq, code_detail(c), res.names.size(), [&](size_t r) { return al[r * n + i]; })
+                           : filter_fail_code(q, pos, i, code_detail(c));
         if (fc == C_UNSCHED) {
           potential.push_back((int32_t)i);
           is_pot[i] = 1;
@@ -4311,22 +4369,29 @@ struct Cluster {
     msg = filter_message(pos, detail);
     return filter_fail_code(q, pos, i, detail);
   }
+  // fit.go Filter's code: UnschedulableAndUnresolvable when a failing request
+  // exceeds the node's allocatable, else Unschedulable -- the one rule behind the
+  // status calls, the cycle view and DefaultPreemption's potential nodes
+  // (alloc_of(r): the node's allocatable of resource column r)
+  template <class AllocOf>
+  static int fit_fail_code(const vector<i64>& rq, uint32_t detail, size_t R, AllocOf alloc_of) {
+    for (size_t r = 0; r < R; ++r)
+      if ((detail & (1u << (1 + r))) && rq[r] > alloc_of(r)) return C_UNRESOLVABLE;
+    return C_UNSCHED;
+  }
   // framework.Code of a Filter failure of profile position pos on local node i
   int filter_fail_code(uint32_t q, int pos, uint32_t i, uint32_t detail) const {
     if (is_volume(plugins[pos])) return vkind[pos] == VK_RESTRICT || vkind[pos] == VK_CSI ? C_UNSCHED : C_UNRESOLVABLE;
     switch (plugins[pos]) {
-      case P_FIT: {  // fit.go Filter: UnschedulableAndUnresolvable when a request exceeds the allocatable
+      case P_FIT: {
         vector<i64> rq;
         i64 nzc = 0, nzm = 0;
         add_requests_const(queue[q], rq, nzc, nzm);
         const Node& nd = nodes[lo + i];
-        for (size_t r = 0; r < res.names.size(); ++r) {
-          if (!(detail & (1u << (1 + r)))) continue;
+        return fit_fail_code(rq, detail, res.names.size(), [&](size_t r) -> i64 {
           auto it = nd.alloc.find(res.names[r]);
-          const i64 a = it == nd.alloc.end() ? 0 : (r == 0 ? as_milli(it->second) : as_value(it->second));
-          if (rq[r] > a) return C_UNRESOLVABLE;
-        }
-        return C_UNSCHED;
+          return it == nd.alloc.end() ? 0 : (r == 0 ? as_milli(it->second) : as_value(it->second));
+        });
       }
       case P_PTS: return detail == KSG_PTS_MISSING_LABEL ? C_UNRESOLVABLE : C_UNSCHED;
       case P_IPA: return detail == KSG_IPA_AFFINITY ? C_UNRESOLVABLE : C_UNSCHED;

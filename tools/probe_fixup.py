@@ -31,6 +31,7 @@ s.schedule()
 buf = (ctypes.c_uint64 * (8 * n))()
 L.ksg_debug_fixup_stamps(s.h, n, buf)
 bs = [buf[j * 32:(j + 1) * 32] for j in range(nw)]
+lt = [buf[nw * 32 + j * 4:nw * 32 + (j + 1) * 4] for j in range(nw)]  # persistent loop: loop top, ready, after wait
 
 
 def med(v):
@@ -70,6 +71,12 @@ for lab, i0, i1 in [("prior eval", 1, 16), ("keys->LDS+sync", 16, 17), ("pmask+s
                      ("flush: P_W+publish", 4, 6), ("flush: patches", 6, 5),
                      ("flush: P_W built (wave 0)", 4, 26), ("flush: P_W acks", 26, 27), ("flush: barrier+publish", 27, 6)]:
     print(f"fixup {lab:14s} median {med([x[i1] - x[i0] for x in bs[1:]]):6d}")
+if any(x[0] for x in lt):
+    print("loop top: windows ready at the flush", sum(1 for x in lt[1:] if x[1]), "of", nw - 1)
+    print("realtime (us): fixup W-1 end -> loop top", med([(lt[j][0] - bs[j - 1][12]) / 100 for j in range(2, nw)]))
+    print("realtime (us): loop-top wait", med([(lt[j][2] - lt[j][0]) / 100 for j in range(2, nw)]),
+          "(not ready only:", med([(lt[j][2] - lt[j][0]) / 100 for j in range(2, nw) if not lt[j][1]] or [0]), ")")
+    print("realtime (us): after wait -> fixup start", med([(bs[j][11] - lt[j][2]) / 100 for j in range(2, nw)]))
 two = [x for x in bs[1:] if x[7] >= 2]
 if two:
     print("iteration 2 median", med([x[20] - x[19] for x in two]), "windows", len(two))

@@ -99,3 +99,61 @@ def test_preempt_dry_run_leaves_state():
     s.schedule()
     assert [(r.selected, r.feasible, r.status) for r in s.results()] == res
     assert [s.postfilter_result(q) for q in range(s.queue_len)] == noms
+
+
+@pytest.mark.gpu
+def test_victim_store_refreshed_after_events_and_compaction(monkeypatch):
+    """The device-resident victim store (every bound pod's program, KSG_VICTIM_STORE_MIN=0:
+    from the first search) stays valid only while the bound pods do not change
+    (ADVICE r05).  Drop-in cycles run searches, then an event batch removes a bound
+    pod and adds another and a compaction turns the placed queue pods into bound
+    pods; every later search must see the new set.  The oracle schedules the
+    equivalent cluster: the mutated bound pods, the first half's placements as bound
+    pods, and pods that fit nowhere in the first half's queue slots (the tie-break
+    hash keeps each later pod's queue index)."""
+    import copy
+    from ksg import generator as g
+    monkeypatch.setenv("KSG_PREEMPT_BATCH", "1")
+    monkeypatch.setenv("KSG_VICTIM_STORE_MIN", "0")
+    doc = _doc(n_pods=80, queue_sort=False)
+    queue = doc["queue"]
+    s = Scheduler(doc["profile"])
+    d = dict(doc)
+    d["queue"] = []
+    d.pop("queueSort")
+    s.load_cluster(d)
+    placed = []
+    for pod in queue:  # (until a batched search has built the store)
+        _, r = s.cycle(pod, commit=True)
+        placed.append(r.selected)
+        if s.preempt_batched() > 0 and len(placed) >= 8:
+            break
+    k = len(placed)
+    assert s.preempt_batched() > 0 and k + 16 <= len(queue), "no search ran before the events"
+    bound = copy.deepcopy(doc["pods"])
+    gone = bound[0]["metadata"]
+    added = copy.deepcopy(bound[1])
+    added["metadata"]["name"] = "evt-added"
+    s.apply_events([{"op": "removePod", "name": gone["name"], "namespace": gone.get("namespace", "default")},
+                    {"op": "addPod", "pod": added}])
+    del bound[0]
+    bound.append(added)
+    s.compact()
+    names = [n["metadata"]["name"] for n in doc["nodes"]]
+    for i in range(k):
+        if placed[i] >= 0:
+            p = copy.deepcopy(queue[i])
+            p["spec"]["nodeName"] = names[placed[i]]
+            bound.append(p)
+    eq = dict(doc)  # (arrival order, like the cycles: queueSort kept off)
+    eq["pods"] = bound
+    eq["queue"] = [g.pod_obj(f"zz-dummy-{i:05d}", [g.req(10 ** 9, 1 << 50)]) for i in range(k)] + queue[k:]
+    o = _oracle(eq)
+    b0 = s.preempt_batched()
+    nominated = 0
+    for i in range(k, len(queue)):
+        q, r = s.cycle(queue[i], commit=True)
+        assert (r.selected, r.feasible, r.status) == o.result(i), i
+        assert s.postfilter_result(q) == o.nominated(i), i
+        nominated += s.postfilter_result(q)[0] >= 0
+    assert s.preempt_batched() > b0 and nominated > 0, "no search ran after the events"

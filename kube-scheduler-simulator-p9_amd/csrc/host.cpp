@@ -25,6 +25,7 @@
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
+#include <thread>
 #include <vector>
 
 #include <dlfcn.h>
@@ -1697,6 +1698,38 @@ struct Cluster {
   bool victim_store_current() const {
     return vstore_eng == eng.get() && vstore_gen == bprog_gen && vstore_n == bound.size() && vstore_npc == pcls.size() &&
            vstore_ntc == tcls.size();
+  }
+  // Background warm-up of the victim store after a load (round 6): a thread of the
+  // context (ksg_ctx::warm) compiles the bound pods' programs in slices under the
+  // context lock and uploads the store, so the first DefaultPreemption search of a
+  // snapshot finds it current instead of compiling 250,000 programs itself.  A
+  // slice stops the warm-up when the state moved (events, vocabulary growth,
+  // another load): the search then builds what it needs, as before.
+  size_t warm_next = 0;
+  uint64_t warm_gen = 0;
+  bool warm_started = false, warm_done = false, warm_running = false;
+  double warm_t0 = 0, warm_ms = -1;  // diagnostic: wall time from the load to the store being current
+  bool warm_wanted() const {
+    const char* e = std::getenv("KSG_VICTIM_WARM");
+    if (e && std::strtol(e, nullptr, 10) == 0) return false;
+    return has_preemption() && shards == 1 && tables_on() && bound.size() >= std::max<size_t>(victim_store_min, 1);
+  }
+  // one slice of up to n programs; true when the warm-up is over
+  bool warm_step(size_t n) {
+    if (!warm_started) {
+      if (!compile_queue()) return true;  // (the queue's classes first: the store is built against them)
+      warm_started = true;
+      warm_gen = bprog_gen;
+      warm_next = 0;
+    }
+    if (warm_gen != bprog_gen || broken) return true;
+    const size_t end = std::min(bound.size(), warm_next + n);
+    for (; warm_next < end; ++warm_next)
+      if (!bound_prog((int32_t)warm_next)) return true;
+    if (warm_next < bound.size()) return false;
+    warm_done = ensure_victim_store();
+    if (warm_done) warm_ms = (now_us() - warm_t0) / 1e3;
+    return true;
   }
   bool ensure_victim_store() {
     if (victim_store_current()) return true;
@@ -4634,6 +4667,17 @@ struct ksg_ctx {
   std::string last_error;
   mutable std::recursive_mutex mu;
   const uint64_t gen = ++g_ctx_gen;
+  // the victim-store warm-up after a load (Cluster::warm_step), stopped and joined
+  // before the next load and at destruction (never while holding mu: a slice takes it)
+  std::thread warm;
+  std::atomic<bool> warm_stop{false};
+  void stop_warm() {
+    warm_stop = true;
+    if (warm.joinable()) warm.join();
+    warm_stop = false;
+  }
+  void start_warm();
+  ~ksg_ctx();
   int fail(const std::string& m, int code) {
     last_error = m;
     t_err_ctx = this;
@@ -4658,6 +4702,45 @@ bool rccl_selftest(int device, size_t bytes, std::string& err);  // engine.hip (
     if ((ctx)->c.eng && (ctx)->c.eng->lost()) (ctx)->c.broken = true;                                    \
     if ((ctx)->c.broken) return (ctx)->fail("context unusable after a device error: reload", KSG_E_STATE); \
   } while (0)
+
+// Contexts with a running warm-up: joined at library teardown, before the HIP
+// runtime's own (a thread still inside a HIP call at process exit would race it).
+static std::mutex g_warm_mu;
+static std::set<ksg_ctx*> g_warm_ctx;
+static struct WarmTeardown {
+  ~WarmTeardown() {
+    std::lock_guard<std::mutex> g(g_warm_mu);
+    for (ksg_ctx* c : g_warm_ctx) {
+      c->warm_stop = true;
+      if (c->warm.joinable()) c->warm.join();
+    }
+    g_warm_ctx.clear();
+  }
+} g_warm_teardown;
+void ksg_ctx::start_warm() {
+  {
+    std::lock_guard<std::mutex> g(g_warm_mu);
+    g_warm_ctx.insert(this);
+  }
+  c.warm_running = true;  // (under the load's lock)
+  warm = std::thread([this] {
+    for (;;) {
+      {
+        std::lock_guard<std::recursive_mutex> g(mu);
+        if (warm_stop || c.warm_step(4096)) {
+          c.warm_running = false;
+          return;
+        }
+      }
+      std::this_thread::yield();  // (a foreground call may take the lock between slices)
+    }
+  });
+}
+ksg_ctx::~ksg_ctx() {
+  stop_warm();
+  std::lock_guard<std::mutex> g(g_warm_mu);
+  g_warm_ctx.erase(this);
+}
 
 extern "C" {
 
@@ -4709,6 +4792,7 @@ const char* ksg_last_error(const ksg_ctx* ctx) {
 }
 
 int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len) {
+  if (ctx) ctx->stop_warm();  // (before the lock: a warm-up slice holds it)
   KSG_LOCK(ctx);
   if (!ctx || !json) return KSG_E_INVALID;
   ctx->c.out_gen++;
@@ -4717,6 +4801,10 @@ int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len) {
     Cluster& c = ctx->c;
     // fix the engine's global node offset for this shard before upload
     if (!c.load(json, len)) return ctx->fail(c.err, KSG_E_INVALID);
+    c.warm_started = c.warm_done = false;
+    c.warm_ms = -1;
+    c.warm_t0 = Cluster::now_us();
+    if (c.warm_wanted()) ctx->start_warm();  // (it waits for this call's lock)
   } catch (std::exception& e) {
     return ctx->fail(e.what(), KSG_E_INVALID);
   }
@@ -4996,6 +5084,14 @@ extern "C" int ksg_debug_cycle_times(ksg_ctx* ctx, double* out, int reset) {
 
 // diagnostic (not in ksg.h): the preemption dry runs' host phases (Cluster::ptimes), 4
 // doubles; reset = 1 clears them after the read
+// Diagnostic: the victim-store warm-up after the last load: 1 done (*ms: load to
+// current store), 0 running, -1 none (not wanted, stopped, or failed).
+extern "C" int ksg_debug_victim_warm(ksg_ctx* ctx, double* ms) {
+  if (!ctx) return KSG_E_INVALID;
+  KSG_LOCK(ctx);
+  if (ms) *ms = ctx->c.warm_ms;
+  return ctx->c.warm_done ? 1 : ctx->c.warm_running ? 0 : -1;
+}
 extern "C" int ksg_debug_preempt_times(ksg_ctx* ctx, double* out, int reset) {
   KSG_LOCK(ctx);
   if (!ctx) return KSG_E_INVALID;

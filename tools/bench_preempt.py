@@ -47,7 +47,7 @@ def make_doc(nodes, pods):
     return doc
 
 
-def one(batch, nodes, pods):
+def one(batch, nodes, pods, warm=0):
     env = dict(os.environ, KSG_PREEMPT_BATCH=str(batch))
     code = f"""
 import json, sys, time
@@ -62,6 +62,13 @@ s = Scheduler(doc["profile"])
 s.load_cluster(doc)
 print("[child] cluster loaded", file=sys.stderr, flush=True)
 import ctypes
+# the victim store's warm-up after the load (host.cpp Cluster::warm_step, a thread of
+# the context): WARM=1 waits for it before the first pod, 0 starts right after the load
+s.L.ksg_debug_victim_warm.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+wms = ctypes.c_double(-1)
+if {warm}:
+    while s.L.ksg_debug_victim_warm(s.h, ctypes.byref(wms)) == 0:
+        time.sleep(0.005)
 s.L.ksg_debug_preempt_times.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 def split():
     pt = (ctypes.c_double * 4)()
@@ -78,7 +85,9 @@ if s.queue_len > 1:
 dt = time.perf_counter() - t
 rest = split() if s.queue_len > 1 else None
 noms = [s.postfilter_result(q) for q in range(s.queue_len)]
+warm = s.L.ksg_debug_victim_warm(s.h, ctypes.byref(wms))
 print(json.dumps({{"ms_per_pod": dt * 1e3 / s.queue_len, "nominated": sum(1 for n in noms if n[0] >= 0),
+                  "victim_store_warm": {{"waited": bool({warm}), "state": warm, "load_to_store_ms": wms.value}},
                   "first_pod_ms": (t1 - t) * 1e3,
                   "ms_per_pod_after_first": (dt - (t1 - t)) * 1e3 / max(s.queue_len - 1, 1),
                   "host_split_ms_per_search": {{"first": first, "after_first": rest}},
@@ -101,13 +110,21 @@ def main():
                     help="cluster size of the batched vs per-node comparison (a per-node search is one dry run per node)")
     a = ap.parse_args()
     b = one(1, a.nodes, a.pods)
+    bw = one(1, a.nodes, a.pods, warm=1)
     k = a.per_node_pods
     bs = one(1, a.per_node_nodes, k)
     p = one(0, a.per_node_nodes, k)
     print(json.dumps({"nodes": a.nodes, "bound_pods": 5 * a.nodes,
                       "batched": {"pods": a.pods, "ms_per_pod": b["ms_per_pod"], "nominated": b["nominated"],
                                   "first_pod_ms": b["first_pod_ms"], "ms_per_pod_after_first": b["ms_per_pod_after_first"],
-                                  "batched_searches": b["batched"], "split": b["host_split_ms_per_search"]},
+                                  "batched_searches": b["batched"], "split": b["host_split_ms_per_search"],
+                                  "victim_store_warm": b["victim_store_warm"]},
+                      "batched_after_warmup": {"pods": a.pods, "ms_per_pod": bw["ms_per_pod"], "nominated": bw["nominated"],
+                                               "first_pod_ms": bw["first_pod_ms"],
+                                               "ms_per_pod_after_first": bw["ms_per_pod_after_first"],
+                                               "split": bw["host_split_ms_per_search"],
+                                               "victim_store_warm": bw["victim_store_warm"],
+                                               "same_nominations": bw["noms"] == b["noms"] and bw["res"] == b["res"]},
                       "compare": {"nodes": a.per_node_nodes, "pods": k,
                                   "batched_ms_per_pod": bs["ms_per_pod"], "per_node_ms_per_pod": p["ms_per_pod"],
                                   "nominated": p["nominated"], "batched_searches": bs["batched"],

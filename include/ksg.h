@@ -106,7 +106,12 @@ int ksg_abi_version(void);
  * "pvs": [v1.PersistentVolume], "pvcs": [v1.PersistentVolumeClaim],
  * "storageClasses": [storagev1.StorageClass]} (ResourcesForSnap field names; the
  * storage objects feed the volume plugins).
- * Replaces the device snapshot (UpdateSnapshot) and the queue. */
+ * Replaces the device snapshot (UpdateSnapshot) and the queue.
+ * With DefaultPreemption in the profile and >= 2,048 bound pods, the call starts a
+ * thread of the context that compiles the bound pods' programs and uploads the
+ * victim store DefaultPreemption's search reads (slices under the context's lock;
+ * KSG_VICTIM_WARM=0: off); it is joined by the next ksg_load_cluster and by
+ * ksg_destroy.  No entry point waits for it. */
 int ksg_load_cluster(ksg_ctx* ctx, const char* json, size_t len);
 int ksg_num_nodes(const ksg_ctx* ctx);     /* global node count */
 int ksg_queue_len(const ksg_ctx* ctx);

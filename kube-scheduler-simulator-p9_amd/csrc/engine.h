@@ -248,6 +248,15 @@ class Engine {
   void view_layout(ViewLayout& lay) const;
   // wait = false: only queued on the engine stream (the block is complete after the next sync)
   bool view(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err, bool wait = true);
+  // The fused view (round 6): view_arm prepares pod q's view like view() but launches
+  // nothing; the next run_queue writes it from k_eval itself when the pod's cycle
+  // is one k_eval (a profile without ScoreExtensions), and view_arm_finish launches
+  // k_view otherwise.  view_fused(): the last armed view was written by k_eval (its
+  // rows assume no Score error: a summary with status 2 needs a view() rebuild).
+  bool view_arm(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err);
+  bool view_arm_finish(std::string& err);
+  bool view_fused() const;
+  uint64_t views_fused() const;  // diagnostic: views written by k_eval so far
   // pinned host blocks for views (process-wide pool: a view outlives its context)
   static uint8_t* pinned_get(size_t bytes, size_t& cap);
   static void pinned_put(uint8_t* p, size_t cap);
@@ -306,6 +315,8 @@ class Engine {
   Impl* impl() { return p_; }
 
  private:
+  bool view_impl(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err, bool wait,
+                 bool arm);
   Impl* p_;
 };
 

@@ -5541,6 +5541,13 @@ struct Engine::Impl {
   int win_run_on = 1;            // persistent window loop (k_window_run): KSG_WIN_RUN=0 turns it off
   int win_mblocks = 0;           // ... with dedicated merge blocks (KSG_WIN_MB=1; the last tile block merges: measured faster)
   int view_copy = 0;             // cycle view: 1 = the per-node arrays by a copy (KSG_VIEW_COPY), 0 = written by k_view
+  int view_fuse = 1;             // fused views (Engine::view_arm; KSG_VIEW_FUSE=0: k_view always)
+  bool vp_armed = false, vp_fused = false, vp_last_fused = false;  // the armed view and its launch parameters
+  uint64_t views_fused = 0;      // diagnostic: views k_eval wrote (ksg_debug_views_fused)
+  uint32_t vp_q = 0;
+  size_t vp_k = 0;
+  ViewDev vp_V{};
+  uint8_t* vp_hout = nullptr;
   int run_overlap = 0;           // k_chain_run: pod k+1's class-table reads during pod k's hand-offs (KSG_RUN_OVERLAP=1; measured no faster)
   int run_defer = 1;             // k_chain_run: the owner's independent node-level assume deferred (KSG_RUN_DEFER=0: off)
   int win_split = 1;             // ... split hand-over: keys staged while the prior steps run (KSG_WIN_SPLIT=0: one counter)
@@ -5755,6 +5762,7 @@ bool Engine::init(const EngineConfig& cfg, std::string& err) {
     if (const char* e = std::getenv("KSG_STATIC_RUN_MB")) I.static_run_mb = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("KSG_STATIC_OVERLAP")) I.static_overlap = (int)std::strtol(e, nullptr, 10);
     if (const char* e = std::getenv("KSG_STATIC_BESIDE_TEST")) I.static_beside_test = (int)std::strtol(e, nullptr, 10);
+    if (const char* e = std::getenv("KSG_VIEW_FUSE")) I.view_fuse = (int)std::strtol(e, nullptr, 10);
   }
   HIPCHK(hipEventCreate(&I.ev0));
   HIPCHK(hipEventCreate(&I.ev1));
@@ -7599,7 +7607,34 @@ void Engine::view_layout(ViewLayout& lay) const {
   lay.off_norm = lay.off_raw + al256(4 * N) * lay.n_raw;  // (the widest layout: every row 4 bytes)
   lay.bytes = lay.off_norm + al256(4 * N) * lay.n_norm;
 }
+bool Engine::view_arm(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err) {
+  return view_impl(j, cfg, lay, host, err, false, true);
+}
+bool Engine::view_arm_finish(std::string& err) {
+  Impl& I = *p_;
+  if (!I.vp_armed) return true;
+  I.vp_armed = false;
+  I.vp_last_fused = I.vp_fused;
+  if (I.vp_fused) {  // (k_eval wrote it)
+    I.views_fused++;
+    return true;
+  }
+  const size_t N = I.N, k = I.vp_k;
+  hipLaunchKernelGGL(k_view, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, I.stream, I.cluster(), I.F,
+                     I.progs.p + I.prog_off[I.vp_q], I.sums.p + I.vp_q, I.kfilter.p + k * N,
+                     I.kscore.p + k * N * KSG_MAX_PLUGINS, I.vp_V, I.vblk.p, I.vp_hout, I.vdone.p);
+  HIPCHK(hipGetLastError());
+  return true;
+}
+bool Engine::view_fused() const { return p_->vp_last_fused; }
+uint64_t Engine::views_fused() const { return p_->views_fused; }
 bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err, bool wait) {
+  p_->vp_armed = false;
+  p_->vp_last_fused = false;
+  return view_impl(j, cfg, lay, host, err, wait, false);
+}
+bool Engine::view_impl(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err, bool wait,
+                       bool arm) {
   Impl& I = *p_;
   if (!(I.keep_n && j >= I.keep_first && j < I.keep_first + I.keep_n)) { err = "outputs not kept for this pod"; return false; }
   if (lay.N != I.N || lay.n_raw != (uint32_t)I.F.n) { err = "view layout of another snapshot"; return false; }
@@ -7644,6 +7679,16 @@ bool Engine::view(uint32_t j, const ViewCfg& cfg, const ViewLayout& lay, uint8_t
   if (hdev && !I.vdone.p) {
     if (!I.vdone.alloc(1, err)) return false;
     HIPCHK(hipMemsetAsync(I.vdone.p, 0, sizeof(uint32_t), s));
+  }
+  if (arm) {  // (launched by the next run_queue's k_eval, or by view_arm_finish)
+    if (!N || !hdev) { err = "view_arm: a direct view of a non-empty snapshot only"; return false; }
+    I.vp_armed = true;
+    I.vp_fused = false;
+    I.vp_q = j;
+    I.vp_k = k;
+    I.vp_V = V;
+    I.vp_hout = hdev;
+    return true;
   }
   if (N)
     hipLaunchKernelGGL(k_view, dim3((uint32_t)((N + 255) / 256)), dim3(256), 0, s, I.cluster(), I.F, I.progs.p + I.prog_off[j],
@@ -8013,9 +8058,19 @@ bool Engine::run_queue(uint32_t first, uint32_t count, bool commit, std::string&
         if (rowm == 2) hipLaunchKernelGGL(k_eval_occ<2>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
         else if (rowm == 1) hipLaunchKernelGGL(k_eval_occ<1>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
         else hipLaunchKernelGGL(k_eval_occ<0>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
-      } else if (rowm == 2) hipLaunchKernelGGL(k_eval<2>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
-      else if (rowm == 1) hipLaunchKernelGGL(k_eval<1>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
-      else hipLaunchKernelGGL(k_eval<0>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CA, prog);
+      } else {
+        // (a fused view: the armed view of this pod when its cycle is this one launch)
+        ChainArgs CE = CA;
+        if (I.vp_armed && I.vp_q == j && !I.vp_fused && I.view_fuse && !F.has_ext && !xchain && I.vblk.p) {
+          CE.vf = I.vp_V;
+          CE.vf_out = I.vblk.p;
+          CE.vf_hout = I.vp_hout;
+          I.vp_fused = true;
+        }
+        if (rowm == 2) hipLaunchKernelGGL(k_eval<2>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CE, prog);
+        else if (rowm == 1) hipLaunchKernelGGL(k_eval<1>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CE, prog);
+        else hipLaunchKernelGGL(k_eval<0>, dim3(I.cnblk), dim3(kChain), 0, s, C, F, CE, prog);
+      }
       if (sampled) {
         HIPCHK(hipEventRecord(I.sev[I.n_samples * 2 + 1], s));
         I.n_samples++;

@@ -3341,12 +3341,19 @@ struct Cluster {
   } pview;
   bool classes_early = std::getenv("KSG_CLASSES_EARLY") && std::strtol(std::getenv("KSG_CLASSES_EARLY"), nullptr, 10) != 0;
   bool view_prefetch = !(std::getenv("KSG_VIEW_PREFETCH") && std::strtol(std::getenv("KSG_VIEW_PREFETCH"), nullptr, 10) == 0);
-  bool prefetch_view(uint32_t q) {
+  // arm: prepared before the cycle's run (Engine::view_arm), so that the run's k_eval
+  // can write it itself (a profile without ScoreExtensions); the run's caller then
+  // calls Engine::view_arm_finish
+  bool prefetch_view(uint32_t q, bool arm = false) {
     pview.drop();
     eng->view_layout(pview.lay);
     pview.block = ksg::Engine::pinned_get(pview.lay.bytes, pview.cap);
     if (!pview.block) return true;  // (no pinned memory: acquire builds it)
-    if (!eng->view(q, view_cfg(), pview.lay, pview.block, err, false)) return false;
+    if (arm && pview.lay.N && ksg::Engine::pinned_dev(pview.block)) {
+      if (!eng->view_arm(q, view_cfg(), pview.lay, pview.block, err)) return false;
+    } else if (!eng->view(q, view_cfg(), pview.lay, pview.block, err, false)) {
+      return false;
+    }
     pview.q = q;
     pview.gen = out_gen;
     return true;
@@ -3421,12 +3428,17 @@ struct Cluster {
     if (commit) room_ok = false;
     if (commit && !room_for(q)) return false;
     // (the summary's copy waits for the run; sync then only checks the run's state)
-    if (!eng->keep_outputs(q, 1, err) || !eng->run_queue(q, 1, commit, err)) return false;
-    if (!commit && view_prefetch && !prefetch_view(q)) return false;
+    if (!eng->keep_outputs(q, 1, err)) return false;
+    if (!commit && view_prefetch && !prefetch_view(q, true)) return false;  // (armed: the run may write it)
+    if (!eng->run_queue(q, 1, commit, err) || !eng->view_arm_finish(err)) return false;
     lap(4);
     if (!commit && pview.block && pview.q == (int64_t)q) {  // (the prefetched view carries the summary)
       if (!eng->sync(err)) return false;
       std::memcpy(&out, pview.block + pview.lay.off_sum, sizeof(out));
+      if (out.status == 2 && eng->view_fused()) {  // (a Score error: its rows at 4 bytes, rebuilt)
+        if (!eng->view(q, view_cfg(), pview.lay, pview.block, err, true)) return false;
+        std::memcpy(&out, pview.block + pview.lay.off_sum, sizeof(out));
+      }
     } else if (!eng->summaries(q, 1, &out, err) || !eng->sync(err)) {
       return false;
     }
@@ -5101,6 +5113,13 @@ extern "C" int ksg_debug_preempt_times(ksg_ctx* ctx, double* out, int reset) {
 }
 
 // diagnostic (not in ksg.h): static-record chunks computed from decoded pods (k_static_dec)
+// diagnostic (not in ksg.h): cycle views k_eval wrote itself (the fused view, Engine::view_arm)
+extern "C" int ksg_debug_views_fused(ksg_ctx* ctx, uint64_t* out) {
+  KSG_LOCK(ctx);
+  if (!ctx || !out) return KSG_E_INVALID;
+  *out = ctx->c.eng->views_fused();
+  return KSG_OK;
+}
 extern "C" int ksg_debug_static_dec_chunks(ksg_ctx* ctx, uint64_t* out) {
   KSG_LOCK(ctx);
   if (!ctx || !out) return KSG_E_INVALID;

@@ -36,6 +36,19 @@ struct ChainVidsT {
 using ChainVids = ChainVidsT<kChain>;
 
 #define KCP_X_DECL 4
+// The cycle view's device description (k_view; a fused view rides in ChainArgs)
+struct ViewDev {
+  int8_t prof_of_dev[KSG_MAX_PLUGINS];  // device position -> profile position (a volume run: its first plugin)
+  uint8_t dev_vol[KSG_MAX_PLUGINS];     // the device position is a volume run
+  int8_t norm_row[KSG_MAX_PLUGINS];     // device position -> normalized row, -1: none (output == raw)
+  uint8_t kind[KSG_MAX_PROFILE];        // per profile position: the framework code of its Filter failure
+  int32_t n_profile;
+  uint32_t gen;  // this view's generation: a slot (or the overflow word) holds gen << 32 | code
+  uint32_t off_sum, off_fail_pos, off_fail_code, off_fail_msg, off_raw, off_norm;  // byte offsets in the block
+  uint32_t off_rows, n_norm;  // the score-row table (Engine::ViewRows); normalized rows
+  uint32_t narrow;            // PodTopologySpread / InterPodAffinity raw rows sized by the summary's range
+  uint32_t slots_direct;      // direct: slots written to the host block as claimed (no last-block copy)
+};
 struct EvalTotals;
 struct SoloCand;
 struct ChainArgs {
@@ -67,7 +80,14 @@ struct ChainArgs {
   int64_t* xsend;          // node-sharded: the cycle's last block leaves its local (key, feasible, status) here
                            // for the X4 exchange instead of selecting (k_tx4_select selects), or null
   SoloCand* cand;          // [nblk][kChain] classes per block (k_eval_solo)
+  // fused view (round 6): a kept pod of a profile without ScoreExtensions has its
+  // cycle view written by k_eval itself -- every block its nodes' rows, the last
+  // block the summary -- instead of by a k_view launch after it (vf_hout null: none)
+  ViewDev vf;
+  uint8_t* vf_out;         // the view's device block (message-slot table)
+  uint8_t* vf_hout;        // the caller's pinned block, device address
 };
+__device__ __forceinline__ void view_fused_tail(const DevCluster& C, const DevProfile& F, const ChainArgs& A);
 
 // Diagnostic stamps: block 0 / thread 0 of each chain kernel adds (now - entry)
 // at its points (k_eval slots 0-7, k_ptsraw 8-15, k_final 16-23, its last block's select 24-27),
@@ -562,6 +582,10 @@ __device__ __forceinline__ void chain_last_select(DevCluster& C, const DevProfil
     return;
   }
   chain_commit(C, A, V, r.key, r.feas, r.st, cs_t0);
+  if (A.vf_hout) {  // (a fused view: the summary is out, its copy and the row table follow)
+    __syncthreads();
+    view_fused_tail(C, F, A);
+  }
 }
 
 // ROWM: 0 resource columns read by the plugins (more than 4 columns), 1 the
@@ -2347,9 +2371,19 @@ __global__ __launch_bounds__(BT) void k_chain_run(DevCluster C, DevProfile F, Ch
 // Kernels.  The *_occ twins cap registers at 4 waves per SIMD (a few spills)
 // for clusters of many blocks per CU; the plain ones keep every register for
 // the latency of one block per CU (cfg4).
+__device__ __forceinline__ void view_body(const DevCluster& C, const DevProfile& F, const uint8_t* prog,
+                                          const ksg_pod_summary* sum, const uint32_t* filter, const int32_t* score,
+                                          const ViewDev& V, uint8_t* out, uint8_t* hout, uint32_t* done);
 template <int ROWM>
 __global__ __launch_bounds__(kChain) void k_eval(DevCluster C, DevProfile F, ChainArgs A, const uint8_t* __restrict__ prog) {
   eval_body<ROWM>(C, F, A, prog);
+  if (A.vf_hout) {  // fused view: this block's nodes, from the kept outputs it just wrote
+    uint32_t* of;
+    int32_t *os, *ot;
+    chain_outs(A, A.q, C.N, of, os, ot);
+    __syncthreads();
+    view_body(C, F, prog, nullptr, of, os, A.vf, A.vf_out, A.vf_hout, nullptr);
+  }
 }
 template <int ROWM>
 __global__ __launch_bounds__(kChain) __attribute__((amdgpu_waves_per_eu(4))) void k_eval_occ(
@@ -2641,18 +2675,6 @@ __global__ void k_norm_out(DevCluster C, DevProfile F, const uint8_t* prog, cons
 // Filter, :420-445 Score, :388-415 NormalizeScore).
 constexpr int kViewSlots = 256;
 enum { kVkUnresolvable = 0, kVkUnsched = 1, kVkFit = 2, kVkPts = 3, kVkIpa = 4 };
-struct ViewDev {
-  int8_t prof_of_dev[KSG_MAX_PLUGINS];  // device position -> profile position (a volume run: its first plugin)
-  uint8_t dev_vol[KSG_MAX_PLUGINS];     // the device position is a volume run
-  int8_t norm_row[KSG_MAX_PLUGINS];     // device position -> normalized row, -1: none (output == raw)
-  uint8_t kind[KSG_MAX_PROFILE];        // per profile position: the framework code of its Filter failure
-  int32_t n_profile;
-  uint32_t gen;  // this view's generation: a slot (or the overflow word) holds gen << 32 | code
-  uint32_t off_sum, off_fail_pos, off_fail_code, off_fail_msg, off_raw, off_norm;  // byte offsets in the block
-  uint32_t off_rows, n_norm;  // the score-row table (Engine::ViewRows); normalized rows
-  uint32_t narrow;            // PodTopologySpread / InterPodAffinity raw rows sized by the summary's range
-  uint32_t slots_direct;      // direct: slots written to the host block as claimed (no last-block copy)
-};
 // Score-row widths of a view, the same in every thread: 1 byte for the rows whose
 // values are within [0, 100] by construction when the cycle has no Score error
 // (Fit and BalancedAllocation raw, every normalized row); PodTopologySpread's and
@@ -2660,9 +2682,13 @@ struct ViewDev {
 // nodes allows (1, 2 or 4 bytes; the range widened by PodTopologySpread's -1 of
 // an ignored node and 0), else 4; rows packed from off_raw, each 256-B aligned.
 // (Values of nodes that failed a filter are unspecified in the view: clamped.)
+// (sum null: a fused view, written before the summary exists -- no Score error
+// assumed, PodTopologySpread / InterPodAffinity rows, which need ScoreExtensions
+// and so never fuse, at 4 bytes; the host rebuilds the view when the summary
+// reports an error)
 __device__ __forceinline__ void view_rows(const DevProfile& F, const ViewDev& V, const ksg_pod_summary* sum, uint32_t N,
                                           Engine::ViewRows& R) {
-  const bool err = sum->status == 2;
+  const bool err = sum != nullptr && sum->status == 2;
   uint32_t off = V.off_raw;
   auto al = [](uint32_t x) { return (x + 255u) & ~255u; };
   for (int d = 0; d < 2 * KSG_MAX_PLUGINS; ++d) {
@@ -2674,7 +2700,7 @@ __device__ __forceinline__ void view_rows(const DevProfile& F, const ViewDev& V,
     uint8_t w = 4;
     if (!err && (p == KP_FIT || p == KP_BA)) {
       w = 1;
-    } else if (!err && V.narrow && (p == KP_PTS || p == KP_IPA)) {
+    } else if (!err && V.narrow && sum != nullptr && (p == KP_PTS || p == KP_IPA)) {
       int64_t lo = sum->min_score[d], hi = sum->max_score[d];
       if (lo == INT64_MAX || hi == INT64_MIN) lo = hi = 0;  // (no feasible / counted node)
       lo = lo < -1 ? lo : -1;
@@ -2724,9 +2750,11 @@ __device__ __forceinline__ uint32_t view_slot(unsigned long long* tab, uint32_t 
 // out: the device block (slot table, summary); hout: where the per-node arrays go —
 // the host's pinned block itself (written over the link by this kernel, no copy
 // launch after it) or out.
-__global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const uint8_t* prog, const ksg_pod_summary* sum,
-                                              const uint32_t* filter, const int32_t* score, ViewDev V, uint8_t* out,
-                                              uint8_t* hout, uint32_t* done) {
+// (sum null: a fused view inside k_eval -- the per-node part only; its last block
+// writes the summary and the row table, view_fused_tail)
+__device__ __forceinline__ void view_body(const DevCluster& C, const DevProfile& F, const uint8_t* prog,
+                                          const ksg_pod_summary* sum, const uint32_t* filter, const int32_t* score,
+                                          const ViewDev& V, uint8_t* out, uint8_t* hout, uint32_t* done) {
   const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = n < C.N;
   const ProgView PV = view(prog);
@@ -2757,7 +2785,7 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
   }
   // message slots: one insert per distinct code of the wave
   unsigned long long* tab = reinterpret_cast<unsigned long long*>(out);
-  if (n == 0 && hout == out) *reinterpret_cast<ksg_pod_summary*>(out + V.off_sum) = *sum;
+  if (n == 0 && hout == out && sum) *reinterpret_cast<ksg_pod_summary*>(out + V.off_sum) = *sum;
   uint32_t msg = 0;
   const uint32_t lane = threadIdx.x & 63;
   for (uint64_t m = __ballot(need); m; m = __ballot(need)) {
@@ -2775,7 +2803,7 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
   }
   Engine::ViewRows RW;
   view_rows(F, V, sum, C.N, RW);
-  if (n == 0) {  // (direct: straight into the host block, like the per-node arrays)
+  if (n == 0 && sum) {  // (direct: straight into the host block, like the per-node arrays)
     *reinterpret_cast<Engine::ViewRows*>(hout + V.off_rows) = RW;
     *reinterpret_cast<ksg_pod_summary*>(hout + V.off_sum) = *sum;
   }
@@ -2810,7 +2838,7 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
       const int32_t s = score[(size_t)pos * C.N + n];
       lput(lraw[pos], RW.bytes[pos], s);
       const int r = V.norm_row[pos];
-      if (r < 0) continue;
+      if (r < 0 || !sum) continue;
       int64_t v = 0;
       if (feasible) {
         if (F.plugins[pos] == KP_PTS && !pk_done) {
@@ -2858,4 +2886,19 @@ __global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const 
       if (threadIdx.x == 0) *done = 0;  // (the next view's count)
     }
   }
+}
+__global__ __launch_bounds__(256) void k_view(DevCluster C, DevProfile F, const uint8_t* prog, const ksg_pod_summary* sum,
+                                              const uint32_t* filter, const int32_t* score, ViewDev V, uint8_t* out,
+                                              uint8_t* hout, uint32_t* done) {
+  view_body(C, F, prog, sum, filter, score, V, out, hout, done);
+}
+// A fused view's last part, by the cycle's last block once its summary is out:
+// the summary and the row table into the caller's block (thread 0)
+__device__ __forceinline__ void view_fused_tail(const DevCluster& C, const DevProfile& F, const ChainArgs& A) {
+  if (threadIdx.x != 0) return;
+  const ksg_pod_summary* sum = A.sums + A.q;
+  Engine::ViewRows RW;
+  view_rows(F, A.vf, nullptr, C.N, RW);
+  *reinterpret_cast<Engine::ViewRows*>(A.vf_hout + A.vf.off_rows) = RW;
+  *reinterpret_cast<ksg_pod_summary*>(A.vf_hout + A.vf.off_sum) = *sum;
 }

@@ -349,6 +349,13 @@ class Scheduler:
         self._chk(self.L.ksg_debug_path_counts(self.h, out), "ksg_debug_path_counts")
         return out[4], out[5]
 
+    def views_fused(self):
+        """Diagnostic: cycle views written by the cycle's k_eval itself (no k_view launch)."""
+        out = ctypes.c_uint64()
+        self.L.ksg_debug_views_fused.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self._chk(self.L.ksg_debug_views_fused(self.h, ctypes.byref(out)), "ksg_debug_views_fused")
+        return out.value
+
     def run_fallbacks(self):
         """Diagnostic: persistent segments whose blocks were not all resident and ran on
         the two-launch chain instead."""

@@ -346,6 +346,12 @@ void Engine::view_layout(ViewLayout& lay) const {
   lay.off_norm = lay.off_raw + al256s(4 * N) * lay.n_raw;
   lay.bytes = lay.off_norm;
 }
+bool Engine::view_arm(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err) {
+  return view(q, cfg, lay, host, err, false);
+}
+bool Engine::view_arm_finish(std::string&) { return true; }
+bool Engine::view_fused() const { return false; }
+uint64_t Engine::views_fused() const { return 0; }
 bool Engine::view(uint32_t q, const ViewCfg& cfg, const ViewLayout& lay, uint8_t* host, std::string& err, bool) {
   PodOutputs o;
   if (!(p_->keep_n && q >= p_->keep_first && q < p_->keep_first + p_->keep_n)) { err = "outputs not kept for this pod"; return false; }

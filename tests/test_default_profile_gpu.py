@@ -78,7 +78,9 @@ def edge_cluster():
 
 @pytest.mark.gpu
 def test_default_profile_cfg1_matches_oracle():
-    _compare(g.generate(1, n_nodes=100, n_pods=400))
+    """BASELINE configs[0] at its full size: 100 nodes, all 1,000 queue pods of the
+    default profile, every selection and every annotation byte for byte."""
+    _compare(g.generate(1, n_nodes=100, n_pods=1000))
 
 
 @pytest.mark.gpu

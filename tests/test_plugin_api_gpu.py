@@ -210,7 +210,7 @@ class _ViewCalls:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("copy", ["0", "1"], ids=["direct", "copy"])
+@pytest.mark.parametrize("copy", ["0", "1", "r"], ids=["direct", "copy", "reserve"])
 @pytest.mark.parametrize("name,c,sizes", CASES, ids=[c[0] for c in CASES])
 def test_cycle_view_matches_extension_point_calls(monkeypatch, name, c, sizes, copy):
     """ksg_cycle_view (include/ksg.h): the arrays the framework's 16 parallel
@@ -218,9 +218,12 @@ def test_cycle_view_matches_extension_point_calls(monkeypatch, name, c, sizes, c
     annotation rebuilt from a view equals the oracle's; 16 threads rebuilding from
     one view agree; a view is unchanged by the cycles that follow it.  Per-node
     arrays written by the view kernel into the pinned block, or copied after it
-    (KSG_VIEW_COPY=1)."""
+    (KSG_VIEW_COPY=1).  "reserve": the drop-in's own order -- a cycle without the
+    assume, its view, then Reserve on the node the framework picked -- where a
+    profile without ScoreExtensions (cfg2) has the cycle's k_eval write the view
+    itself (the fused view, no k_view launch)."""
     from concurrent.futures import ThreadPoolExecutor
-    monkeypatch.setenv("KSG_VIEW_COPY", copy)
+    monkeypatch.setenv("KSG_VIEW_COPY", "1" if copy == "1" else "0")
     doc = g.generate(c, **sizes)
     o = Oracle(doc)
     o.schedule(record=3)
@@ -233,7 +236,7 @@ def test_cycle_view_matches_extension_point_calls(monkeypatch, name, c, sizes, c
     widths = set()  # PodTopologySpread / InterPodAffinity raw rows: as narrow as the cycle's range
     plugins = doc["profile"]["plugins"]
     for i, pod in enumerate(doc["queue"][:30]):
-        q, r = s.cycle(pod, commit=True)
+        q, r = s.cycle(pod, commit=copy != "r")
         v = s.cycle_view(q)
         for pos, pl in enumerate(plugins):
             if pl in ("PodTopologySpread", "InterPodAffinity") and v._v.score[pos] and r.status == 0:
@@ -258,9 +261,13 @@ def test_cycle_view_matches_extension_point_calls(monkeypatch, name, c, sizes, c
                 assert val == ora[k], (name, i, k)
         if i % 10 == 0:
             held.append((i, q, v, outs[0]))
+        if copy == "r" and r.selected >= 0:
+            s.reserve(q, r.selected)
     assert widths <= {1, 2, 4}, widths
     if name == "cfg4":
         assert widths and min(widths) < 4, widths
+    if copy == "r" and name == "cfg2":  # no ScoreExtensions: the cycle's k_eval wrote the view
+        assert s.views_fused() > 0
     for i, q, v, first in held:  # views stay valid and unchanged after later cycles
         assert rebuild(_ViewCalls(s, v), q, doc["profile"], names, v.result.status) == first, (name, i)
         v.release()

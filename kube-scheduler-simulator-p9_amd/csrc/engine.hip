@@ -3431,7 +3431,7 @@ __global__ __launch_bounds__(1024) void k_static_dec_run(DevCluster C, DevProfil
 struct WcNode {
   double ad0, ad1;  // allocatable cpu / memory
   double ra0, ra1;  // reciprocals of ad0 / ad1, correctly rounded (1.0 / ad: one division per node)
-  double fz0, fz1;  // NonZeroRequested cpu / memory (Fit)
+  double fx0, fx1;  // (allocatable - NonZeroRequested) x 100, cpu / memory (Fit; exact: < 2^53)
   double rd0, rd1;  // Requested cpu / memory (BalancedAllocation)
   double fd0, fd1;  // allocatable - requested (Fit's filter)
   uint64_t ts;      // taint ids (< 64)
@@ -3441,11 +3441,14 @@ struct WcNode {
 // leastRequestedScore floor((a - q) * 100 / a) for integers 0 <= q <= a < 2^45
 // held exactly in doubles: x = (a - q) * 100 < 2^52 is exact, the estimate from
 // the reciprocal is the quotient or one off, the fma remainder is exact.
-__device__ __forceinline__ double least_req_d(double ad, double ra, double qd) {
-  const double x = (ad - qd) * 100.0;
+// The quotient lies in [0, 100]: the correction is done on the int32 estimate
+// (one conversion instead of double selects and a 64-bit conversion).  x is
+// (a - q) * 100, formed by the caller (pass 1: the node's (a - nonzero) * 100
+// less the pod's request x 100, both exact integers, |x| < 2^53).
+__device__ __forceinline__ int32_t least_req_d(double ad, double ra, double x) {
   const double d = trunc(x * ra);
   const double rem = __builtin_fma(-d, ad, x);
-  return rem >= ad ? d + 1.0 : (rem < 0.0 ? d - 1.0 : d);
+  return (int32_t)d + (rem >= ad ? 1 : 0) - (rem < 0.0 ? 1 : 0);
 }
 
 // Pass 1: grid x = group of KSG_WC_PODS pods (fastest: a tile's rows are shared
@@ -3471,6 +3474,7 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
   if (tid < KSG_WC_PODS) wcnt[tid] = 0;
   __syncthreads();
   const bool hf = F.pos_fit >= 0, hb = F.pos_ba >= 0;
+  const uint32_t wfit = (uint32_t)F.w_fit, wba = (uint32_t)F.w_ba;
 #pragma unroll 1
   for (uint32_t sub = 0; sub < KSG_WC_TILE / (256 * NPT); ++sub) {
     const uint32_t nb = blockIdx.y * KSG_WC_TILE + sub * (256 * NPT);
@@ -3494,8 +3498,8 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
       v.rd1 = (double)r1;
       v.fd0 = (double)(a0 - r0);
       v.fd1 = (double)(a1 - r1);
-      v.fz0 = (double)C.nzc[n[k]];
-      v.fz1 = (double)C.nzm[n[k]];
+      v.fx0 = (v.ad0 - (double)C.nzc[n[k]]) * 100.0;
+      v.fx1 = (v.ad1 - (double)C.nzm[n[k]]) * 100.0;
       v.ok = live && !(hf && C.podcnt[n[k]] + 1 > C.allowed[n[k]]);
       const uint32_t t0 = C.toff[n[k]], tc = C.toff[n[k] + 1] - t0;
       uint64_t w = 0;
@@ -3531,7 +3535,9 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
         }
       }
       // NodeAffinity: every flattened requirement on every node -> failed-term masks
-      uint32_t failm[NPT];
+      uint32_t failm[NPT], n4[NPT];
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) n4[k] = n[k] * 4u;
 #pragma unroll
       for (int k = 0; k < NPT; ++k) failm[k] = 0;
       const uint32_t nreq = P.nreq;
@@ -3540,7 +3546,17 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
         const WcReq& R = P.req[r];
         const uint32_t mode = R.mode, gb = R.gbit;
         const uint64_t arg = R.arg;
-        if (mode <= 1u) {
+        if (mode <= 1u && !(arg >> 63)) {
+          // (value id 63 not in the mask: a node without the key (-1, bit 63) tests
+          // clear with no sign test; the outcome bit shifted straight into place)
+          const uint8_t* col = reinterpret_cast<const uint8_t*>(C.label + R.col);
+          const uint32_t sh = (uint32_t)__builtin_ctz(gb), m0 = mode == 0u ? 1u : 0u;
+          uint32_t v[NPT];
+#pragma unroll
+          for (int k = 0; k < NPT; ++k) v[k] = *reinterpret_cast<const uint32_t*>(col + (uint64_t)n4[k]);
+#pragma unroll
+          for (int k = 0; k < NPT; ++k) failm[k] |= ((((uint32_t)(arg >> (v[k] & 63u))) & 1u) ^ m0) << sh;
+        } else if (mode <= 1u) {
           const int32_t* col = C.label + R.col;
           int32_t v[NPT];
 #pragma unroll
@@ -3568,25 +3584,27 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
         mask[k] = (~failm[k] >> KSG_WC_PREF_BIT) & ((1u << npf) - 1u);
       }
       // Fit (LeastAllocated, cpu:1 memory:1) and BalancedAllocation (cpu, memory)
-      const double fs0 = P.fs0, fs1 = P.fs1;
+      const double fs0 = P.fs0 * 100.0, fs1 = P.fs1 * 100.0;  // (exact: < 2^51)
       const double bq0 = P.bq0, bq1 = P.bq1;
       const uint64_t hseed = P.hseed;
-      int cnt = 0;
+      uint32_t nfeas = 0;  // (feasible nodes of the wave: ballots, on the scalar unit)
       bool rng = false;
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
         const WcNode& v = x[k];
         const bool ok0 = v.ad0 != 0.0, ok1 = v.ad1 != 0.0;
-        int64_t fb = 0;
+        // (32-bit: the scores are in [0, 100] or flagged bad, 100 x the weights < 2^24: host-checked)
+        uint32_t fb = 0;
         bool bad = false;
         if (hf) {
-          const double q0 = v.fz0 + fs0, q1 = v.fz1 + fs1;
-          const double s0 = (ok0 && v.ad0 > 0.0 && !(q0 > v.ad0)) ? least_req_d(v.ad0, v.ra0, q0) : 0.0;
-          const double s1 = (ok1 && v.ad1 > 0.0 && !(q1 > v.ad1)) ? least_req_d(v.ad1, v.ra1, q1) : 0.0;
-          const int64_t ns = (int64_t)s0 + (int64_t)s1;
-          const int64_t sc = ok0 && ok1 ? ns >> 1 : ns;
+          // (q <= a  <=>  x = (a - q) x 100 >= 0)
+          const double x0 = v.fx0 - fs0, x1 = v.fx1 - fs1;
+          const int32_t s0 = (ok0 && v.ad0 > 0.0 && x0 >= 0.0) ? least_req_d(v.ad0, v.ra0, x0) : 0;
+          const int32_t s1 = (ok1 && v.ad1 > 0.0 && x1 >= 0.0) ? least_req_d(v.ad1, v.ra1, x1) : 0;
+          const int32_t ns = s0 + s1;
+          const int32_t sc = ok0 && ok1 ? ns >> 1 : ns;
           bad |= sc < 0 || sc > 100;
-          fb += sc * F.w_fit;
+          fb += (uint32_t)sc * wfit;
         }
         if (hb) {
           double sd = 0.0;
@@ -3603,24 +3621,24 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
             f1 = f1 > 1 ? 1 : f1;
             sd = fabs((f0 - f1) / 2);
           }
-          const int64_t sc = (int64_t)((1 - sd) * 100.0);
+          // (a value outside int32 saturates: still < 0 or > 100, i.e. bad)
+          const int32_t sc = __double2int_rz((1 - sd) * 100.0);
           bad |= sc < 0 || sc > 100;
-          fb += sc * F.w_ba;
+          fb += (uint32_t)sc * wba;
         }
         const uint32_t c = (xt[k] << npf) | mask[k];
-        const uint64_t top = (uint64_t)(bad ? 0 : fb) << 40;
+        const uint64_t top = (uint64_t)(bad ? 0u : fb) << 40;
         // (a lower Fit/BA sum than the class's best so far cannot win the class)
         if (pass[k] && top >= (slot[pi][c] & ~0xFFFFFFFFFFull)) {
           const uint32_t g = C.goff + v.n;
           const uint64_t h20 = splitmix64(hseed ^ (uint64_t)g) >> 44;
           atomicMax(&slot[pi][c], (unsigned long long)(top | ((0xFFFFFull - h20) << 20) | (uint64_t)g));
         }
-        cnt += pass[k] ? 1 : 0;
+        nfeas += (uint32_t)__popcll(__ballot(pass[k]));
         rng |= pass[k] && bad;
       }
-      const int c = wave_sum(cnt);
       const bool anyr = __ballot(rng) != 0;
-      if (lane0() && (c || anyr)) atomicAdd(&wcnt[pi], (uint32_t)c | (anyr ? 0x80000000u : 0u));
+      if (lane0() && (nfeas || anyr)) atomicAdd(&wcnt[pi], nfeas | (anyr ? 0x80000000u : 0u));
     }
   }
   __syncthreads();
@@ -6650,8 +6668,13 @@ bool Engine::run_whatif(uint32_t first, uint32_t count, std::string& err) {
       if (I.F.plugins[i] == KP_FIT || I.F.plugins[i] == KP_BA) wsum += I.F.weight[i] > 0 ? I.F.weight[i] : 0;
     A.need_eph = I.any_eph_req ? 1u : 0u;
     // the class path (k_whatif_cls1/2): nothing per pair in memory; KSG_WHATIF_CLASSES=0 off
+    // (the class key holds the Fit/BA sum in 24 bits: 100 x the weights below 2^24, none negative)
+    bool wts_ok = true;
+    for (int i = 0; i < I.F.n; ++i)
+      if (I.F.plugins[i] == KP_FIT || I.F.plugins[i] == KP_BA) wts_ok &= I.F.weight[i] >= 0;
     bool use_cls = I.eval_mode == 1 && !I.any_eph_req && I.R <= 4 && I.static_fits && I.max_taints <= 4 &&
-                   I.max_tid < 64 && !I.taint_dup && I.cols_small && rec_mb > 0;
+                   I.max_tid < 64 && !I.taint_dup && I.cols_small && rec_mb > 0 && wts_ok &&
+                   100 * wsum < ((int64_t)1 << 24);
     if (const char* e = std::getenv("KSG_WHATIF_CLASSES")) use_cls &= std::strtol(e, nullptr, 10) != 0;
     for (uint32_t q = first; use_cls && q < first + count; ++q) {
       const uint32_t np = (I.prog_need[q] >> 8) & 0xFFu;

@@ -3528,10 +3528,19 @@ __global__ __launch_bounds__(256) void k_whatif_cls1(DevCluster C, DevProfile F,
       uint32_t xt[NPT];
       {  // TaintToleration (a node's taints are distinct: the set counts them; zero sets without the plugin)
         const uint64_t hw = P.hw, pw = P.pw;
+        if (((hw | pw) >> 32) == 0) {  // (the pod's sets name only ids < 32: 32-bit tests)
+          const uint32_t hl = (uint32_t)hw, pl = (uint32_t)pw;
 #pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-          pass[k] &= (x[k].ts & hw) == 0;
-          xt[k] = (uint32_t)__popcll(x[k].ts & pw);
+          for (int k = 0; k < NPT; ++k) {
+            pass[k] &= ((uint32_t)x[k].ts & hl) == 0u;
+            xt[k] = (uint32_t)__popc((uint32_t)x[k].ts & pl);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < NPT; ++k) {
+            pass[k] &= (x[k].ts & hw) == 0;
+            xt[k] = (uint32_t)__popcll(x[k].ts & pw);
+          }
         }
       }
       // NodeAffinity: every flattened requirement on every node -> failed-term masks

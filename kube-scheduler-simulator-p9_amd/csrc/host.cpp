@@ -883,6 +883,18 @@ struct Cluster {
       fw_w[i] = w == 0 ? 1 : w;
       store_w[i] = sw.count(names[i]) ? (s == 0 ? 1 : s) : 0;
     }
+    {  // the selection key (pack_key) holds the weighted total in 24 bits: a node's total is at
+       // most 100 (MaxNodeScore) x the sum of the weights, so that sum is bounded here, loudly
+      i64 wsum = 0;
+      for (int i = 0; i < n_plugins; ++i) {
+        if (fw_w[i] < 0) { err = "profile: negative weight of " + names[i]; return false; }
+        wsum += fw_w[i] < ((i64)1 << 24) ? fw_w[i] : ((i64)1 << 24);
+      }
+      if (100 * wsum >= ((i64)1 << 24)) {
+        err = "profile: 100 x the sum of the plugin weights must be below 2^24 (the selection key's score field)";
+        return false;
+      }
+    }
     if (const J* s = pr["seed"]) ecfg.seed = std::strtoull(s->text().c_str(), nullptr, 10);
     if (const J* pc = pr["pluginConfig"]) {
       if (const J* fit = (*pc)["NodeResourcesFit"])

@@ -241,6 +241,23 @@ def test_scheduler_configuration_weights(tmp_path):
     assert _weights(tmp_path, ext) is None
 
 
+def test_weight_sum_bound_refused(tmp_path):
+    """The selection key (pack_key, SURVEY.md §8 tie-break) holds a node's weighted
+    total in 24 bits, and a total is at most 100 x the sum of the weights: a
+    profile whose 100 x sum reaches 2^24 is refused at ksg_create, as is a negative
+    weight, instead of selecting on a truncated total."""
+    try:
+        _binary()
+    except (OSError, subprocess.CalledProcessError) as e:
+        pytest.skip(f"sanitizer build unavailable: {e}")
+    ok = g.make_profile([("NodeResourcesFit", 100000), ("NodeResourcesBalancedAllocation", 67771)], 1)
+    assert _weights(tmp_path, ok)["NodeResourcesFit"][1] == 100000  # 100 x 167771 = 2^24 - 100
+    big = g.make_profile([("NodeResourcesFit", 100000), ("NodeResourcesBalancedAllocation", 67773)], 1)
+    assert _weights(tmp_path, big) is None  # 100 x 167773 > 2^24
+    neg = g.make_profile([("NodeResourcesFit", 1), ("NodeResourcesBalancedAllocation", -1)], 1)
+    assert _weights(tmp_path, neg) is None
+
+
 TSAN_SRCS = [os.path.join(HERE, "fuzz", "tsan_view.cpp"), os.path.join(HERE, "fuzz", "stub_engine.cpp"),
              os.path.join(ROOT, "kube-scheduler-simulator-p9_amd", "csrc", "host.cpp"),
              os.path.join(ROOT, "kube-scheduler-simulator-p9_amd", "csrc", "synth.cpp")]

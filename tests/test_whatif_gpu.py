@@ -190,3 +190,24 @@ def test_whatif_class_path_edge_selectors(monkeypatch, npt):
     bad = [(q, got[q], want[q]) for q in range(len(want)) if got[q] != want[q]]
     assert not bad, bad[:5]
     assert s.whatif_class_chunks() == 2
+
+
+@pytest.mark.gpu
+def test_whatif_class_path_weight_bound():
+    """The class key holds the weighted Fit + BalancedAllocation sum in 24 bits:
+    with 100 x the profile's weights just below 2^24 a step runs the class path and
+    equals the oracle's (framework.go RunScorePlugins: score x weight)."""
+    doc = g.generate(5, n_nodes=1200, n_pods=2 * STEP)
+    for k in ("weights", "storeWeights"):
+        doc["profile"][k]["NodeResourcesFit"] = 100000
+        doc["profile"][k]["NodeResourcesBalancedAllocation"] = 67000
+    o = _oracle_steps(doc, 2)
+    want = [o.result(q) for q in range(o.n_queue)]
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    for k in range(2):
+        s.whatif(k * STEP, STEP)
+    got = [(r.selected, r.feasible, r.status) for r in s.results()]
+    bad = [(q, got[q], want[q]) for q in range(len(want)) if got[q] != want[q]]
+    assert not bad, bad[:5]
+    assert s.whatif_class_chunks() > 0

@@ -3554,7 +3554,11 @@ struct Cluster {
   bool preempt_no_batch = std::getenv("KSG_PREEMPT_BATCH") && std::strtol(std::getenv("KSG_PREEMPT_BATCH"), nullptr, 10) == 0;
   bool preempt_batched(const Pod& p, const ksg_pod_summary& S) const {
     if (preempt_no_batch) return false;
-    if (!p.tsc.empty() || !p.req_aff.empty() || !p.req_anti.empty() || (S.ipa_flags & 4u)) return false;
+    if (!p.req_aff.empty() || !p.req_anti.empty() || (S.ipa_flags & 4u)) return false;
+    // (ScheduleAnyway constraints only score: PodTopologySpread's PreFilter state
+    // holds the DoNotSchedule ones, so a pod with no other reads no spread counts)
+    for (auto& t : p.tsc)
+      if (t.when != "ScheduleAnyway") return false;
     for (auto& cn : p.claims) {
       const PVC* c = pvc_of(p.ns, cn);
       if (c && c->rwop) return false;
@@ -3708,7 +3712,7 @@ struct Cluster {
     if (preempt_batched(p, S)) {
       // Batched search (every potential node at once).  Removing a node's victims
       // changes only that node (its row, host ports, attached volumes): the pod
-      // has no spread constraint, no (anti)affinity term, no existing pod's
+      // has no DoNotSchedule spread constraint, no required (anti)affinity term, no existing pod's
       // anti-affinity applies to it and it holds no ReadWriteOncePod claim, so its
       // PreFilter state is the same whatever is removed, and the victim sets of
       // different nodes are disjoint.  One dry run with every potential node's

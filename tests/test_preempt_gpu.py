@@ -157,3 +157,32 @@ def test_victim_store_refreshed_after_events_and_compaction(monkeypatch):
         assert s.postfilter_result(q) == o.nominated(i), i
         nominated += s.postfilter_result(q)[0] >= 0
     assert s.preempt_batched() > b0 and nominated > 0, "no search ran after the events"
+
+
+@pytest.mark.gpu
+def test_preempt_batched_with_schedule_anyway_constraints(monkeypatch):
+    """A preemptor whose spread constraints are all ScheduleAnyway takes the batched
+    search (upstream podtopologyspread's PreFilter state holds only DoNotSchedule
+    constraints, so no removal changes what its filters read): every queue pod of the
+    preempt family gets a ScheduleAnyway zone constraint instead of its DoNotSchedule
+    one and loses its required anti-affinity; nominations and victims equal the
+    oracle's and the batched search ran."""
+    monkeypatch.setenv("KSG_PREEMPT_BATCH", "1")
+    doc = _doc()
+    for p in doc["queue"]:
+        p["spec"]["topologySpreadConstraints"] = [{
+            "maxSkew": 1, "topologyKey": "topology.kubernetes.io/zone", "whenUnsatisfiable": "ScheduleAnyway",
+            "labelSelector": {"matchLabels": dict(list(p["metadata"].get("labels", {}).items())[:1])}}]
+        p["spec"].pop("affinity", None)
+    o = _oracle(doc)
+    s = Scheduler(doc["profile"])
+    s.load_cluster(doc)
+    s.keep_outputs(0, s.queue_len)
+    s.schedule()
+    nominated = 0
+    for q, r in enumerate(s.results()):
+        assert (r.selected, r.feasible, r.status) == o.result(q), q
+        assert s.postfilter_result(q) == o.nominated(q), q
+        nominated += s.postfilter_result(q)[0] >= 0
+    assert nominated >= 5
+    assert s.preempt_batched() >= nominated // 2

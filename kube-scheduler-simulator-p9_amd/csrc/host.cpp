@@ -3552,9 +3552,29 @@ struct Cluster {
   // nothing the pod's filters read but the node they are removed from.
   uint64_t preempt_batched_runs = 0;  // diagnostic: pods whose dry run took the batched search
   bool preempt_no_batch = std::getenv("KSG_PREEMPT_BATCH") && std::strtol(std::getenv("KSG_PREEMPT_BATCH"), nullptr, 10) == 0;
+  // Is every node's value of label key `key` its own (no two nodes share one)?  A
+  // required anti-affinity term over such a key reads only the pods of the node it
+  // filters (upstream satisfyPodAntiAffinity: counts per (key, value) domain).
+  mutable std::unordered_map<string, std::pair<uint64_t, bool>> topo_uniq_cache;
+  bool topo_unique_now(const string& key) const {
+    auto it = topo_uniq_cache.find(key);
+    if (it != topo_uniq_cache.end() && it->second.first == node_gen) return it->second.second;
+    std::unordered_set<string> seen;
+    bool u = !key.empty();
+    for (size_t i = 0; u && i < nodes.size(); ++i) {
+      auto l = nodes[i].labels.find(key);
+      if (l != nodes[i].labels.end() && !seen.insert(l->second).second) u = false;
+    }
+    topo_uniq_cache[key] = {node_gen, u};
+    return u;
+  }
   bool preempt_batched(const Pod& p, const ksg_pod_summary& S) const {
     if (preempt_no_batch) return false;
-    if (!p.req_aff.empty() || !p.req_anti.empty() || (S.ipa_flags & 4u)) return false;
+    if (!p.req_aff.empty() || (S.ipa_flags & 4u)) return false;
+    // (required anti-affinity over one-node-per-value keys, e.g. kubernetes.io/hostname:
+    // a node's removals change only its own domain)
+    for (auto& t : p.req_anti)
+      if (!topo_unique_now(t.topo)) return false;
     // (ScheduleAnyway constraints only score: PodTopologySpread's PreFilter state
     // holds the DoNotSchedule ones, so a pod with no other reads no spread counts)
     for (auto& t : p.tsc)
@@ -3712,7 +3732,8 @@ struct Cluster {
     if (preempt_batched(p, S)) {
       // Batched search (every potential node at once).  Removing a node's victims
       // changes only that node (its row, host ports, attached volumes): the pod
-      // has no DoNotSchedule spread constraint, no required (anti)affinity term, no existing pod's
+      // has no DoNotSchedule spread constraint, no required affinity term, required
+      // anti-affinity only over one-node-per-value keys, no existing pod's
       // anti-affinity applies to it and it holds no ReadWriteOncePod claim, so its
       // PreFilter state is the same whatever is removed, and the victim sets of
       // different nodes are disjoint.  One dry run with every potential node's

@@ -19,14 +19,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator-p9_amd"))
 
 
-def make_doc(nodes, pods):
+def make_doc(nodes, pods, spread=0):
     """The preempt family at `nodes` nodes, 4 random bound pods per node plus one
     lowest-priority 4-core filler on every node (no node has 6 free cores), and
     `pods` queue pods of priority 5000 asking 6 cores: every node is a potential
     node (Unschedulable: insufficient cpu), the 8-core ones fit once their
     lower-priority pods are gone, so every pod runs a full victim search.  The bound
     pods carry no anti-affinity terms (one applying to the incoming pod takes the
-    per-node search: ksg's preempt_batched)."""
+    per-node search: ksg's preempt_batched).  spread=1: every queue pod also carries a
+    ScheduleAnyway zone spread constraint and a required hostname anti-affinity term
+    on its own first label (both batched since round 6)."""
     from ksg import edge
     from ksg.generator import pod_obj, req
     doc = edge.gen_preempt(n_nodes=nodes, n_existing=4 * nodes, n_pods=pods)
@@ -44,10 +46,16 @@ def make_doc(nodes, pods):
         for c in sp["containers"]:
             c["resources"] = {"requests": {"cpu": "6000m", "memory": "2Gi"}}
             c.pop("ports", None)
+        if spread:
+            sel = {"matchLabels": dict(list(p["metadata"].get("labels", {}).items())[:1])}
+            sp["topologySpreadConstraints"] = [{"maxSkew": 1, "topologyKey": edge.ZONE,
+                                                "whenUnsatisfiable": "ScheduleAnyway", "labelSelector": sel}]
+            sp["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": sel, "topologyKey": edge.HOSTNAME}]}}
     return doc
 
 
-def one(batch, nodes, pods, warm=0):
+def one(batch, nodes, pods, warm=0, spread=0):
     env = dict(os.environ, KSG_PREEMPT_BATCH=str(batch))
     code = f"""
 import json, sys, time
@@ -56,7 +64,7 @@ sys.path.insert(0, {os.path.join(ROOT, 'kube-scheduler-simulator-p9_amd')!r})
 import torch
 from bench_preempt import make_doc
 from ksg import Scheduler
-doc = make_doc({nodes}, {pods})
+doc = make_doc({nodes}, {pods}, {spread})
 print("[child] document built", file=sys.stderr, flush=True)
 s = Scheduler(doc["profile"])
 s.load_cluster(doc)
@@ -106,15 +114,17 @@ def main():
     ap.add_argument("--nodes", type=int, default=50000)
     ap.add_argument("--pods", type=int, default=8)
     ap.add_argument("--per-node-pods", type=int, default=2)
+    ap.add_argument("--spread", type=int, default=0, help="1: preemptors with a ScheduleAnyway spread constraint "
+                    "and hostname anti-affinity (make_doc)")
     ap.add_argument("--per-node-nodes", type=int, default=2000,
                     help="cluster size of the batched vs per-node comparison (a per-node search is one dry run per node)")
     a = ap.parse_args()
-    b = one(1, a.nodes, a.pods)
-    bw = one(1, a.nodes, a.pods, warm=1)
+    b = one(1, a.nodes, a.pods, spread=a.spread)
+    bw = one(1, a.nodes, a.pods, warm=1, spread=a.spread)
     k = a.per_node_pods
-    bs = one(1, a.per_node_nodes, k)
-    p = one(0, a.per_node_nodes, k)
-    print(json.dumps({"nodes": a.nodes, "bound_pods": 5 * a.nodes,
+    bs = one(1, a.per_node_nodes, k, spread=a.spread)
+    p = one(0, a.per_node_nodes, k, spread=a.spread)
+    print(json.dumps({"nodes": a.nodes, "bound_pods": 5 * a.nodes, "spread": a.spread,
                       "batched": {"pods": a.pods, "ms_per_pod": b["ms_per_pod"], "nominated": b["nominated"],
                                   "first_pod_ms": b["first_pod_ms"], "ms_per_pod_after_first": b["ms_per_pod_after_first"],
                                   "batched_searches": b["batched"], "split": b["host_split_ms_per_search"],

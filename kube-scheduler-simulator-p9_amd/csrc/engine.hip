@@ -7324,8 +7324,7 @@ struct UpSeg {
   uint64_t dst, src;
   uint32_t words, pad;
 };
-__global__ __launch_bounds__(256) void k_upload(const UpSeg* __restrict__ segs) {
-  const UpSeg g = segs[blockIdx.x];
+__device__ __forceinline__ void copy_seg(const UpSeg g) {
   uint32_t* d = reinterpret_cast<uint32_t*>(g.dst);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(g.src);
   uint32_t w0 = 0;
@@ -7338,6 +7337,14 @@ __global__ __launch_bounds__(256) void k_upload(const UpSeg* __restrict__ segs) 
   }
   for (uint32_t i = w0 + blockIdx.y * 256 + threadIdx.x; i < g.words; i += gridDim.y * 256) d[i] = src ? src[i] : 0u;
 }
+__global__ __launch_bounds__(256) void k_upload(const UpSeg* __restrict__ segs) { copy_seg(segs[blockIdx.x]); }
+// Engine::reset's restores of the snapshot's node columns in one launch (the
+// segments travel as kernel arguments: one block row per segment)
+constexpr int kRestoreSegs = 12;
+struct RestoreSegs {
+  UpSeg seg[kRestoreSegs];
+};
+__global__ __launch_bounds__(256) void k_restore(const RestoreSegs S) { copy_seg(S.seg[blockIdx.x]); }
 
 // Node-sharded class tables: sum the pair-level entries of the classes built
 // since the last call across ranks (each rank built them from its own existing
@@ -8299,16 +8306,26 @@ bool Engine::read_nonzero(std::vector<int64_t>& nz, std::string& err) {
 bool Engine::reset(std::string& err) {
   Impl& I = *p_;
   hipStream_t s = I.stream;
-  HIPCHK(hipMemcpyAsync(I.req.p, I.req0.p, (size_t)I.R * I.N * 8, hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipMemcpyAsync(I.nzc.p, I.nzc0.p, (size_t)I.N * 8, hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipMemcpyAsync(I.nzm.p, I.nzm0.p, (size_t)I.N * 8, hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipMemcpyAsync(I.podcnt.p, I.podcnt0.p, (size_t)I.N * 4, hipMemcpyDeviceToDevice, s));
-  if (I.n_ports)
-    HIPCHK(hipMemcpyAsync(I.ports.p, I.ports0.p, (size_t)I.n_ports * I.N * 4, hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipMemcpyAsync(I.pvcuse.p, I.pvcuse0.p, (size_t)I.n_pvc * 4, hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipMemcpyAsync(I.vatt.p, I.vatt0.p, (size_t)I.n_vatt * 4, hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipMemcpyAsync(I.vnode.p, I.vnode0.p, (size_t)I.n_vnode * 4, hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipMemcpyAsync(I.vref.p, I.vref0.p, (size_t)I.n_vnode * 4, hipMemcpyDeviceToDevice, s));
+  {  // the node columns from their snapshot copies: one launch (was nine device copies)
+    RestoreSegs R{};
+    uint32_t n = 0, ny = 1;
+    auto add = [&](const void* dst, const void* src, size_t bytes) {
+      if (!bytes || !dst || !src) return;
+      R.seg[n++] = UpSeg{(uint64_t)(uintptr_t)dst, (uint64_t)(uintptr_t)src, (uint32_t)(bytes / 4), 0};
+      ny = std::max<uint32_t>(ny, std::min<uint32_t>(64, (uint32_t)((bytes / 4 + 4095) / 4096)));
+    };
+    add(I.req.p, I.req0.p, (size_t)I.R * I.N * 8);
+    add(I.nzc.p, I.nzc0.p, (size_t)I.N * 8);
+    add(I.nzm.p, I.nzm0.p, (size_t)I.N * 8);
+    add(I.podcnt.p, I.podcnt0.p, (size_t)I.N * 4);
+    if (I.n_ports) add(I.ports.p, I.ports0.p, (size_t)I.n_ports * I.N * 4);
+    add(I.pvcuse.p, I.pvcuse0.p, (size_t)I.n_pvc * 4);
+    add(I.vatt.p, I.vatt0.p, (size_t)I.n_vatt * 4);
+    add(I.vnode.p, I.vnode0.p, (size_t)I.n_vnode * 4);
+    add(I.vref.p, I.vref0.p, (size_t)I.n_vnode * 4);
+    static_assert(kRestoreSegs >= 9, "restore segments");
+    if (n) hipLaunchKernelGGL(k_restore, dim3(n, ny), dim3(256), 0, s, R);
+  }
   HIPCHK(hipMemcpyAsync(I.tcounts.p, I.counts0, sizeof(I.counts0), hipMemcpyHostToDevice, s));
   if (!rebuild_class_tables(err)) return false;  // from the restored existing-pod table
   uint32_t cnt = (uint32_t)I.prog_off.size();

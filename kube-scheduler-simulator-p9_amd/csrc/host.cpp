@@ -1397,6 +1397,7 @@ struct Cluster {
     return true;
   }
   bool refresh_programs(uint32_t first, uint32_t count) {
+    if (!tables_on()) return true;  // (no class tables: no program to refresh)
     for (uint32_t q = first; q < first + count; ++q)
       if (!refresh_program(q)) return false;
     return true;
@@ -4899,7 +4900,9 @@ int ksg_schedule_queue(ksg_ctx* ctx, uint32_t first, uint32_t count) {
   // cycle (Cluster::preempt); the call then returns with those segments done.
   if (c.nom.size() < c.queue.size()) c.nom.resize(c.queue.size());
   uint32_t j = first;
-  for (uint32_t q = first; q < first + count; ++q) {
+  // (without DefaultPreemption no pod is ever nominated: nothing to clear or stop for)
+  const bool may_nominate = c.has_preemption();
+  for (uint32_t q = first; may_nominate && q < first + count; ++q) {
     c.nom[q] = Cluster::Nomination();
     if (!c.may_preempt(q)) continue;
     ksg_pod_summary S;
@@ -4943,7 +4946,8 @@ int ksg_whatif(ksg_ctx* ctx, uint32_t first, uint32_t count) {
     if (!c.ensure_room(need)) return ctx->fail(c.err, KSG_E_DEVICE);
   }
   if (c.nom.size() < c.queue.size()) c.nom.resize(c.queue.size());
-  for (uint32_t q = first; q < first + count; ++q) c.nom[q] = Cluster::Nomination();  // a what-if step runs no PostFilter
+  if (c.has_preemption())  // (a what-if step runs no PostFilter; without DefaultPreemption none ever ran)
+    for (uint32_t q = first; q < first + count; ++q) c.nom[q] = Cluster::Nomination();
   if (!c.eng->run_whatif(first, count, c.err)) return ctx->fail(c.err, KSG_E_STATE);
   c.mark_run(first, count);
   return KSG_OK;

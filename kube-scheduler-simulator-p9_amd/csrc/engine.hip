@@ -8240,13 +8240,21 @@ static uint32_t wait_verdict(Engine::Impl& I, hipStream_t s, std::string& err) {
 
 bool Engine::sync(std::string& err) {
   Impl& I = *p_;
+  // (the sticky abort word read behind the run on the stream, into a spare word of
+  // the pinned verdict block: no second blocking round trip after the sync)
+  const bool abort_async = I.run_used && I.hverdict;
+  if (abort_async) {
+    __atomic_store_n(&I.hverdict[8], 0u, __ATOMIC_RELAXED);
+    HIPCHK(hipMemcpyAsync(&I.hverdict[8], I.rsync.p->abort, sizeof(uint32_t), hipMemcpyDeviceToHost, I.stream));
+  }
   if (!stream_sync(I, I.stream, err)) return false;
   I.hcalls.clear();  // every queued host exchange has run
   if (I.xfail.exchange(0)) { err = "exchange callback failed"; return false; }
   if (I.run_used) {  // a persistent segment whose poll ran out left the launch early
     I.run_used = false;
     uint32_t ab = 0;
-    HIPCHK(hipMemcpy(&ab, I.rsync.p->abort, sizeof(ab), hipMemcpyDeviceToHost));
+    if (abort_async) ab = __atomic_load_n(&I.hverdict[8], __ATOMIC_ACQUIRE);
+    else HIPCHK(hipMemcpy(&ab, I.rsync.p->abort, sizeof(ab), hipMemcpyDeviceToHost));
     if (ab) {
       // the segment (and every later one of its call, which left at the handshake)
       // left summaries unwritten and assumes half applied: the state is lost
